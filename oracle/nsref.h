@@ -1,0 +1,121 @@
+/*
+ * nsref.h — CPU ORACLE for the nsgpu hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This is a plain-C++ restatement of the ns-3 (ybaddi/ns-3-dev-dnemu, ns-3.13-dev)
+ * algorithms on the hot path.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it, and only as the checker / CPU baseline — never as
+ * the thing measured or shipped.  The product path (libnsgpu.so) never links it.
+ *
+ * Parity pin: the reference tree cannot be built here
+ * (its int64x64/Time headers include the waf-generated ns3/core-config.h and its
+ * mpi module needs <mpi.h>), so there is no oracle/_ref.  This
+ * restatement is pinned against every known-answer vector the reference's own
+ * test suites hold for this path (the JSON files under tests/golden, each entry citing its
+ * reference file:line), and against the survey-time reference run facts.
+ *
+ * Every function cites the reference file:line it restates.
+ */
+#ifndef NSREF_H
+#define NSREF_H
+
+#include <stdint.h>
+#include "../include/nsgpu_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- int64x64_t (src/core/model/int64x64-128.{h,cc}) ----------------
+ * A 64.64 fixed-point value is passed as two little-endian 64-bit words of the
+ * two's-complement int128: w[0] = low word, w[1] = high word. */
+void     nsref_i64x64_from_double(double v, uint64_t out[2]);        /* int64x64-128.h:26-36 */
+void     nsref_i64x64_from_int(int64_t v, uint64_t out[2]);          /* int64x64-128.h:37-66 */
+void     nsref_i64x64_from_parts(int64_t hi, uint64_t lo, uint64_t out[2]); /* int64x64-128.h:67-74 */
+void     nsref_i64x64_mul(const uint64_t a[2], const uint64_t b[2], uint64_t out[2]);  /* int64x64-128.cc:20-57 */
+void     nsref_i64x64_div(const uint64_t a[2], const uint64_t b[2], uint64_t out[2]);  /* int64x64-128.cc:58-92 */
+void     nsref_i64x64_invert(uint64_t v, uint64_t out[2]);                             /* int64x64-128.cc:119-134 */
+void     nsref_i64x64_mul_by_invert(const uint64_t a[2], const uint64_t b[2], uint64_t out[2]); /* :94-118 */
+int64_t  nsref_i64x64_get_high(const uint64_t a[2]);                 /* int64x64-128.h:98-105 */
+uint64_t nsref_i64x64_get_low(const uint64_t a[2]);                  /* int64x64-128.h:106-113 */
+double   nsref_i64x64_get_double(const uint64_t a[2]);               /* int64x64-128.h:85-97 */
+
+/* ---------------- Time at NS resolution (src/core/model/nstime.h, time.cc) ---------------- */
+int64_t  nsref_seconds(double s);                          /* Seconds(double).GetTimeStep(): nstime.h:388-391,403-418,586-589 */
+void     nsref_seconds_batch(const double *s, int64_t *out, int64_t n);
+double   nsref_get_seconds(int64_t ts);                    /* Time::GetSeconds(): nstime.h:398-401,419-431 */
+int64_t  nsref_from_integer(int64_t v, int unit);          /* Time::FromInteger: nstime.h:344-361 (unit: 0=S..5=FS) */
+
+/* ---------------- Mobility + propagation (src/propagation, src/mobility) ---------------- */
+double nsref_distance(double ax, double ay, double az, double bx, double by, double bz);  /* vector.cc:63-70 */
+double nsref_calc_rx_power(double tx_dbm, double distance, const nsgpu_loss_chain *chain); /* propagation-loss-model.cc:64-74 */
+int64_t nsref_const_speed_delay(double distance, double speed);                           /* propagation-delay-model.cc:90-96 */
+
+/* YansWifiChannel::Send (src/wifi/model/yans-wifi-channel.cc:77-115).
+ * phys are in m_phyList order; returns the number of records written (= receivers scheduled). */
+int64_t nsref_fanout_yans(const double *x, const double *y, const double *z,
+                          const uint32_t *chan, const uint32_t *node, int64_t nphy,
+                          int64_t sender, double tx_dbm, const nsgpu_loss_chain *loss, double speed,
+                          uint64_t now_ts, uint32_t uid_base, nsgpu_rx_record *out);
+
+/* SingleModelSpectrumChannel::StartTx (src/spectrum/model/single-model-spectrum-channel.cc:106-183):
+ * loss computed with tx = 0 dBm, receivers with -gain > max_loss_db are skipped (no uid),
+ * survivors get psd_out[k*nbands + b] = psd_tx[b] * 10^(gain/10). */
+int64_t nsref_fanout_spectrum(const double *x, const double *y, const double *z,
+                              const uint32_t *node, int64_t nphy, int64_t sender,
+                              const nsgpu_loss_chain *loss, double speed, double max_loss_db,
+                              const double *psd_tx, int32_t nbands,
+                              uint64_t now_ts, uint32_t uid_base,
+                              nsgpu_rx_record *out, double *psd_out);
+
+/* ---------------- Sequential engine: DefaultSimulatorImpl + Map/Heap scheduler ----------------
+ * (src/core/model/default-simulator-impl.cc:49-353, map-scheduler.cc:51-100, heap-scheduler.cc:44-217) */
+enum { NSREF_SCHED_MAP = 0, NSREF_SCHED_HEAP = 1, NSREF_SCHED_LIST = 2 };
+
+typedef void (*nsref_fn)(void *user, uint64_t arg);
+typedef struct nsref_sim nsref_sim;
+
+nsref_sim *nsref_sim_new(int scheduler);
+void       nsref_sim_free(nsref_sim *s);
+nsgpu_event_id nsref_sim_schedule(nsref_sim *s, int64_t delay, nsref_fn fn, void *user, uint64_t arg);
+void       nsref_sim_schedule_with_context(nsref_sim *s, uint32_t ctx, int64_t delay, nsref_fn fn, void *user, uint64_t arg);
+nsgpu_event_id nsref_sim_schedule_now(nsref_sim *s, nsref_fn fn, void *user, uint64_t arg);
+nsgpu_event_id nsref_sim_schedule_destroy(nsref_sim *s, nsref_fn fn, void *user, uint64_t arg);
+void       nsref_sim_remove(nsref_sim *s, const nsgpu_event_id *id);
+void       nsref_sim_cancel(nsref_sim *s, const nsgpu_event_id *id);
+int        nsref_sim_is_expired(nsref_sim *s, const nsgpu_event_id *id);
+void       nsref_sim_run(nsref_sim *s);
+void       nsref_sim_stop(nsref_sim *s);
+void       nsref_sim_stop_at(nsref_sim *s, int64_t delay);
+void       nsref_sim_destroy(nsref_sim *s);
+uint64_t   nsref_sim_now(nsref_sim *s);
+uint32_t   nsref_sim_context(nsref_sim *s);
+uint64_t   nsref_sim_delay_left(nsref_sim *s, const nsgpu_event_id *id);
+uint64_t   nsref_sim_dispatched(nsref_sim *s);   /* RemoveNext count (cancelled included) */
+uint32_t   nsref_sim_next_uid(nsref_sim *s);
+/* Optional pop-order log of every dispatch: (ts, uid, ctx). */
+void       nsref_sim_set_log(nsref_sim *s, uint64_t *ts, uint32_t *uid, uint32_t *ctx, uint64_t cap);
+
+/* ---------------- utils/bench-simulator.cc (config 1) ----------------
+ * Bench::RunBench/Cb (bench-simulator.cc:79-127) on the restated engine.
+ * dist_ns: the distribution already converted by ReadDistribution (:59-76). */
+typedef struct nsref_churn_result {
+  uint64_t dispatched;   /* RemoveNext calls */
+  uint64_t holds;        /* Bench::m_n */
+  uint64_t final_ts;     /* ts of the last dispatched event */
+  uint64_t digest;       /* sum_k nsgpu_dispatch_digest_term(k, ts_k, uid_k) */
+  uint32_t next_uid;
+  uint32_t pad_;
+  double   run_seconds;  /* wall time of Simulator::Run only (bench-simulator.cc:94-97) */
+  double   init_seconds; /* wall time of the initial inserts (:83-90) */
+} nsref_churn_result;
+
+int nsref_churn_run(const uint64_t *dist_ns, uint32_t n, uint32_t total, int scheduler,
+                    uint64_t *log_ts, uint32_t *log_uid, uint64_t log_cap, nsref_churn_result *out);
+
+/* bench-simulator ReadDistribution: (uint64_t)(data * 1000000000)  (bench-simulator.cc:66) */
+uint64_t nsref_distribution_ns(double seconds);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,339 @@
+"""ctypes binding of the CPU ORACLE (oracle/build/libnsref.so).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker / CPU baseline.  The product path never does.
+See oracle/nsref.h for what is restated and where the reference code lives.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libnsref.so")
+
+
+class EventId(C.Structure):  # nsgpu_event_id (include/nsgpu_types.h)
+    _fields_ = [("impl", C.c_uint64), ("ts", C.c_uint64), ("context", C.c_uint32), ("uid", C.c_uint32)]
+
+
+class LossModel(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p0", C.c_double), ("p1", C.c_double), ("p2", C.c_double)]
+
+
+class LossChain(C.Structure):
+    _fields_ = [("n", C.c_int32), ("pad_", C.c_int32), ("m", LossModel * 4)]
+
+
+RX_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("context", "<u4"), ("phy", "<u4"),
+                            ("pad_", "<u4"), ("rx_dbm", "<f8")])
+
+
+class ChurnResult(C.Structure):
+    _fields_ = [("dispatched", C.c_uint64), ("holds", C.c_uint64), ("final_ts", C.c_uint64),
+                ("digest", C.c_uint64), ("next_uid", C.c_uint32), ("pad_", C.c_uint32),
+                ("run_seconds", C.c_double), ("init_seconds", C.c_double)]
+
+
+LOSS_NONE, LOSS_LOG_DISTANCE, LOSS_FRIIS, LOSS_FIXED_RSS, LOSS_RANGE = 0, 1, 2, 3, 4
+SCHED_MAP, SCHED_HEAP, SCHED_LIST = 0, 1, 2
+
+EVENT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)
+
+
+def loss_chain(*models):
+    """models: (kind, p0, p1, p2) tuples in m_next order."""
+    ch = LossChain()
+    ch.n = len(models)
+    for i, (k, a, b, c) in enumerate(models):
+        ch.m[i].kind, ch.m[i].p0, ch.m[i].p1, ch.m[i].p2 = k, a, b, c
+    return ch
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        u64p = C.POINTER(C.c_uint64)
+        L.nsref_i64x64_from_double.argtypes = [C.c_double, u64p]
+        L.nsref_i64x64_from_int.argtypes = [C.c_int64, u64p]
+        L.nsref_i64x64_from_parts.argtypes = [C.c_int64, C.c_uint64, u64p]
+        for f in ("nsref_i64x64_mul", "nsref_i64x64_div", "nsref_i64x64_mul_by_invert"):
+            getattr(L, f).argtypes = [u64p, u64p, u64p]
+        L.nsref_i64x64_invert.argtypes = [C.c_uint64, u64p]
+        L.nsref_i64x64_get_high.argtypes = [u64p]
+        L.nsref_i64x64_get_high.restype = C.c_int64
+        L.nsref_i64x64_get_low.argtypes = [u64p]
+        L.nsref_i64x64_get_low.restype = C.c_uint64
+        L.nsref_i64x64_get_double.argtypes = [u64p]
+        L.nsref_i64x64_get_double.restype = C.c_double
+        L.nsref_seconds.argtypes = [C.c_double]
+        L.nsref_seconds.restype = C.c_int64
+        L.nsref_seconds_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.nsref_get_seconds.argtypes = [C.c_int64]
+        L.nsref_get_seconds.restype = C.c_double
+        L.nsref_from_integer.argtypes = [C.c_int64, C.c_int]
+        L.nsref_from_integer.restype = C.c_int64
+        L.nsref_distance.argtypes = [C.c_double] * 6
+        L.nsref_distance.restype = C.c_double
+        L.nsref_calc_rx_power.argtypes = [C.c_double, C.c_double, C.POINTER(LossChain)]
+        L.nsref_calc_rx_power.restype = C.c_double
+        L.nsref_const_speed_delay.argtypes = [C.c_double, C.c_double]
+        L.nsref_const_speed_delay.restype = C.c_int64
+        L.nsref_fanout_yans.argtypes = [C.c_void_p] * 5 + [C.c_int64, C.c_int64, C.c_double, C.POINTER(LossChain),
+                                                           C.c_double, C.c_uint64, C.c_uint32, C.c_void_p]
+        L.nsref_fanout_yans.restype = C.c_int64
+        L.nsref_fanout_spectrum.argtypes = [C.c_void_p] * 4 + [C.c_int64, C.c_int64, C.POINTER(LossChain), C.c_double,
+                                                               C.c_double, C.c_void_p, C.c_int32, C.c_uint64,
+                                                               C.c_uint32, C.c_void_p, C.c_void_p]
+        L.nsref_fanout_spectrum.restype = C.c_int64
+        L.nsref_sim_new.argtypes = [C.c_int]
+        L.nsref_sim_new.restype = C.c_void_p
+        L.nsref_sim_free.argtypes = [C.c_void_p]
+        L.nsref_sim_schedule.argtypes = [C.c_void_p, C.c_int64, EVENT_FN, C.c_void_p, C.c_uint64]
+        L.nsref_sim_schedule.restype = EventId
+        L.nsref_sim_schedule_with_context.argtypes = [C.c_void_p, C.c_uint32, C.c_int64, EVENT_FN, C.c_void_p,
+                                                      C.c_uint64]
+        L.nsref_sim_schedule_now.argtypes = [C.c_void_p, EVENT_FN, C.c_void_p, C.c_uint64]
+        L.nsref_sim_schedule_now.restype = EventId
+        L.nsref_sim_schedule_destroy.argtypes = [C.c_void_p, EVENT_FN, C.c_void_p, C.c_uint64]
+        L.nsref_sim_schedule_destroy.restype = EventId
+        for f in ("nsref_sim_remove", "nsref_sim_cancel"):
+            getattr(L, f).argtypes = [C.c_void_p, C.POINTER(EventId)]
+        L.nsref_sim_is_expired.argtypes = [C.c_void_p, C.POINTER(EventId)]
+        L.nsref_sim_is_expired.restype = C.c_int
+        for f in ("nsref_sim_run", "nsref_sim_stop", "nsref_sim_destroy"):
+            getattr(L, f).argtypes = [C.c_void_p]
+        L.nsref_sim_stop_at.argtypes = [C.c_void_p, C.c_int64]
+        L.nsref_sim_now.argtypes = [C.c_void_p]
+        L.nsref_sim_now.restype = C.c_uint64
+        L.nsref_sim_context.argtypes = [C.c_void_p]
+        L.nsref_sim_context.restype = C.c_uint32
+        L.nsref_sim_delay_left.argtypes = [C.c_void_p, C.POINTER(EventId)]
+        L.nsref_sim_delay_left.restype = C.c_uint64
+        L.nsref_sim_dispatched.argtypes = [C.c_void_p]
+        L.nsref_sim_dispatched.restype = C.c_uint64
+        L.nsref_sim_next_uid.argtypes = [C.c_void_p]
+        L.nsref_sim_next_uid.restype = C.c_uint32
+        L.nsref_sim_set_log.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.nsref_churn_run.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_void_p,
+                                      C.c_uint64, C.POINTER(ChurnResult)]
+        L.nsref_churn_run.restype = C.c_int
+        L.nsref_distribution_ns.argtypes = [C.c_double]
+        L.nsref_distribution_ns.restype = C.c_uint64
+        _lib = L
+    return _lib
+
+
+# ---------------- convenience wrappers ----------------
+def _w(x):
+    return (C.c_uint64 * 2)(*x) if x is not None else (C.c_uint64 * 2)()
+
+
+class I64x64:
+    """int64x64_t restated (oracle)."""
+
+    def __init__(self, words):
+        self.w = (C.c_uint64 * 2)(*words)
+
+    @classmethod
+    def from_double(cls, v):
+        o = _w(None)
+        lib().nsref_i64x64_from_double(v, o)
+        return cls(o)
+
+    @classmethod
+    def from_int(cls, v):
+        o = _w(None)
+        lib().nsref_i64x64_from_int(v, o)
+        return cls(o)
+
+    @classmethod
+    def from_parts(cls, hi, lo):
+        o = _w(None)
+        lib().nsref_i64x64_from_parts(hi, lo, o)
+        return cls(o)
+
+    @classmethod
+    def invert(cls, v):
+        o = _w(None)
+        lib().nsref_i64x64_invert(v, o)
+        return cls(o)
+
+    def _bin(self, f, other):
+        o = _w(None)
+        getattr(lib(), f)(self.w, other.w, o)
+        return I64x64(o)
+
+    def __mul__(self, o):
+        return self._bin("nsref_i64x64_mul", o)
+
+    def __truediv__(self, o):
+        return self._bin("nsref_i64x64_div", o)
+
+    def mul_by_invert(self, o):
+        return self._bin("nsref_i64x64_mul_by_invert", o)
+
+    def _int(self):
+        v = self.w[0] | (self.w[1] << 64)
+        return v - (1 << 128) if v >> 127 else v
+
+    def __add__(self, o):
+        v = (self._int() + o._int()) & ((1 << 128) - 1)
+        return I64x64((v & ((1 << 64) - 1), v >> 64))
+
+    def __sub__(self, o):
+        v = (self._int() - o._int()) & ((1 << 128) - 1)
+        return I64x64((v & ((1 << 64) - 1), v >> 64))
+
+    def high(self):
+        return lib().nsref_i64x64_get_high(self.w)
+
+    def low(self):
+        return lib().nsref_i64x64_get_low(self.w)
+
+    def double(self):
+        return lib().nsref_i64x64_get_double(self.w)
+
+
+def seconds(s):
+    return lib().nsref_seconds(float(s))
+
+
+def seconds_batch(arr):
+    arr = np.ascontiguousarray(arr, dtype=np.float64)
+    out = np.empty(arr.shape, dtype=np.int64)
+    lib().nsref_seconds_batch(arr.ctypes.data, out.ctypes.data, arr.size)
+    return out
+
+
+def get_seconds(ts):
+    return lib().nsref_get_seconds(int(ts))
+
+
+def fanout_yans(x, y, z, chan, node, sender, tx_dbm, chain, speed, now_ts, uid_base):
+    n = len(x)
+    out = np.zeros(n, dtype=RX_RECORD_DTYPE)
+    arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+            ((x, np.float64), (y, np.float64), (z, np.float64), (chan, np.uint32), (node, np.uint32))]
+    k = lib().nsref_fanout_yans(*[a.ctypes.data for a in arrs], n, sender, tx_dbm, C.byref(chain), speed,
+                                now_ts, uid_base, out.ctypes.data)
+    return out[:k]
+
+
+def fanout_spectrum(x, y, z, node, sender, chain, speed, max_loss_db, psd_tx, now_ts, uid_base):
+    n = len(x)
+    psd_tx = np.ascontiguousarray(psd_tx, dtype=np.float64)
+    nb = psd_tx.size
+    out = np.zeros(n, dtype=RX_RECORD_DTYPE)
+    psd_out = np.zeros((n, nb), dtype=np.float64)
+    arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+            ((x, np.float64), (y, np.float64), (z, np.float64), (node, np.uint32))]
+    k = lib().nsref_fanout_spectrum(*[a.ctypes.data for a in arrs], n, sender, C.byref(chain), speed, max_loss_db,
+                                    psd_tx.ctypes.data, nb, now_ts, uid_base, out.ctypes.data, psd_out.ctypes.data)
+    return out[:k], psd_out[:k]
+
+
+def load_distribution(path):
+    """bench-simulator ReadDistribution (bench-simulator.cc:59-76): doubles -> (uint64_t)(d*1e9)."""
+    vals = []
+    with open(path) as f:
+        for tok in f.read().split():
+            try:
+                vals.append(float(tok))
+            except ValueError:
+                continue
+    return np.array([lib().nsref_distribution_ns(v) for v in vals], dtype=np.uint64)
+
+
+def churn_run(dist_ns, total, scheduler=SCHED_MAP, log_cap=0):
+    dist_ns = np.ascontiguousarray(dist_ns, dtype=np.uint64)
+    res = ChurnResult()
+    if log_cap:
+        lts = np.zeros(log_cap, dtype=np.uint64)
+        luid = np.zeros(log_cap, dtype=np.uint32)
+        lib().nsref_churn_run(dist_ns.ctypes.data, dist_ns.size, total, scheduler, lts.ctypes.data,
+                              luid.ctypes.data, log_cap, C.byref(res))
+        return res, lts, luid
+    lib().nsref_churn_run(dist_ns.ctypes.data, dist_ns.size, total, scheduler, None, None, 0, C.byref(res))
+    return res, None, None
+
+
+class Sim:
+    """Restated DefaultSimulatorImpl with Python closures (for semantics tests)."""
+
+    def __init__(self, scheduler=SCHED_MAP):
+        self.L = lib()
+        self.h = self.L.nsref_sim_new(scheduler)
+        self._keep = []
+
+    def _fn(self, cb):
+        f = EVENT_FN(lambda user, arg: cb())
+        self._keep.append(f)
+        return f
+
+    def schedule(self, delay, cb):
+        return self.L.nsref_sim_schedule(self.h, delay, self._fn(cb), None, 0)
+
+    def schedule_with_context(self, ctx, delay, cb):
+        self.L.nsref_sim_schedule_with_context(self.h, ctx, delay, self._fn(cb), None, 0)
+
+    def schedule_now(self, cb):
+        return self.L.nsref_sim_schedule_now(self.h, self._fn(cb), None, 0)
+
+    def schedule_destroy(self, cb):
+        return self.L.nsref_sim_schedule_destroy(self.h, self._fn(cb), None, 0)
+
+    def remove(self, eid):
+        self.L.nsref_sim_remove(self.h, C.byref(eid))
+
+    def cancel(self, eid):
+        self.L.nsref_sim_cancel(self.h, C.byref(eid))
+
+    def is_expired(self, eid):
+        return bool(self.L.nsref_sim_is_expired(self.h, C.byref(eid)))
+
+    def run(self):
+        self.L.nsref_sim_run(self.h)
+
+    def stop(self, delay=None):
+        if delay is None:
+            self.L.nsref_sim_stop(self.h)
+        else:
+            self.L.nsref_sim_stop_at(self.h, delay)
+
+    def destroy(self):
+        self.L.nsref_sim_destroy(self.h)
+
+    def now(self):
+        return self.L.nsref_sim_now(self.h)
+
+    def context(self):
+        return self.L.nsref_sim_context(self.h)
+
+    def dispatched(self):
+        return self.L.nsref_sim_dispatched(self.h)
+
+    def next_uid(self):
+        return self.L.nsref_sim_next_uid(self.h)
+
+    def close(self):
+        if self.h:
+            self.L.nsref_sim_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
