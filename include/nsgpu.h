@@ -1,0 +1,117 @@
+/*
+ * nsgpu.h — C-ABI of libnsgpu.so, the MI355X (gfx950) discrete-event engine that sits behind
+ * ns-3's SimulatorImpl / Scheduler plugin surface (ybaddi/ns-3-dev-dnemu, ns-3.13-dev).
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes, and returns an int status
+ * (NSGPU_OK = 0).  On failure nsgpu_last_error() describes it; the ns-3 side maps a non-zero
+ * status to NS_FATAL_ERROR (SURVEY §8(b) error convention).  Pointers named d_* are device
+ * (HBM) pointers; `stream` is a hipStream_t (NULL = the default stream).  Calls are made from
+ * the single simulation thread (ns-3 is single-threaded w.r.t. the simulator).
+ *
+ * Which reference interface each group replaces is cited next to it; INTEGRATION.md shows
+ * the ns-3 classes (ns3::HipBatchScheduler, ns3::HipSimulatorImpl) that bind them.
+ */
+#ifndef NSGPU_H
+#define NSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "nsgpu_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  NSGPU_OK = 0,
+  NSGPU_EINVAL = 1,   /* bad argument (shape, null pointer, capacity) */
+  NSGPU_EHIP = 2,     /* HIP runtime error */
+  NSGPU_ENOMEM = 3,   /* device allocation or fixed capacity exhausted */
+  NSGPU_ESTATE = 4    /* call not valid in the current state (e.g. empty queue) */
+};
+
+/* ---------------- library / device plumbing ---------------- */
+int         nsgpu_version(void);                 /* 100 * major + minor */
+const char *nsgpu_last_error(void);
+int         nsgpu_device_count(int *count);
+int         nsgpu_set_device(int device);
+int         nsgpu_malloc(void **d_ptr, size_t bytes);
+int         nsgpu_free(void *d_ptr);
+int         nsgpu_memcpy_htod(void *d_dst, const void *h_src, size_t bytes, void *stream);
+int         nsgpu_memcpy_dtoh(void *h_dst, const void *d_src, size_t bytes, void *stream);
+int         nsgpu_memset(void *d_dst, int value, size_t bytes, void *stream);
+int         nsgpu_stream_create(void **stream);
+int         nsgpu_stream_destroy(void *stream);
+int         nsgpu_stream_sync(void *stream);
+int         nsgpu_event_create(void **event);              /* hipEvent_t, for timing on a given stream */
+int         nsgpu_event_destroy(void *event);
+int         nsgpu_event_record(void *event, void *stream);
+int         nsgpu_event_elapsed_ms(void *start, void *stop, float *ms);  /* synchronises `stop` */
+
+/* ---------------- Time (src/core/model/nstime.h:388-439,586-589; int64x64-128.{h,cc}) ----------------
+ * d_out[i] = Seconds (d_seconds[i]).GetTimeStep () at the default NS resolution, bit-exact
+ * with the reference's 64.64 fixed point. */
+int nsgpu_seconds_to_ts(const double *d_seconds, int64_t *d_out, int64_t n, void *stream);
+
+/* ---------------- Broadcast-channel fan-out ----------------
+ * Replaces the receiver loop of YansWifiChannel::Send (src/wifi/model/yans-wifi-channel.cc:77-115):
+ * MobilityModel::GetDistanceFrom (mobility-model.cc:79-84), PropagationLossModel::CalcRxPower
+ * (propagation-loss-model.cc:64-74) and ConstantSpeedPropagationDelayModel::GetDelay
+ * (propagation-delay-model.cc:90-96) for every receiver in parallel.
+ *
+ * The phy list is SoA in HBM, in m_phyList (YansWifiChannel::Add) order.  One call handles
+ * n_tx transmissions; transmission t writes its records at d_out + t * (nphy - 1) (survivors
+ * first, in list order; the remaining slots of the stride are left untouched) and its survivor
+ * count at d_count[t].  Record k of transmission t has uid = uid_base[t] + k — exactly the uids
+ * ScheduleWithContext would hand out, since each survivor consumes one. */
+typedef struct nsgpu_phy_soa {
+  const double   *x, *y, *z;   /* positions (ConstantPositionMobilityModel), metres */
+  const uint32_t *channel;     /* YansWifiPhy::GetChannelNumber () */
+  const uint32_t *node;        /* NetDevice->GetNode ()->GetId (), 0xffffffff if none */
+} nsgpu_phy_soa;
+
+typedef struct nsgpu_tx_desc {
+  uint64_t now_ts;      /* Simulator::Now () of the Send call */
+  double   tx_dbm;      /* txPowerDbm */
+  uint32_t sender;      /* index of the sending phy in the list */
+  uint32_t uid_base;    /* DefaultSimulatorImpl::m_uid at the Send call */
+} nsgpu_tx_desc;
+
+int nsgpu_fanout_yans(const nsgpu_phy_soa *phys, int64_t nphy, const nsgpu_tx_desc *d_tx, int64_t n_tx,
+                      const nsgpu_loss_chain *loss, double speed,
+                      nsgpu_rx_record *d_out, uint32_t *d_count, void *d_workspace, void *stream);
+
+/* SingleModelSpectrumChannel::StartTx (src/spectrum/model/single-model-spectrum-channel.cc:106-183):
+ * loss with tx = 0 dBm, receivers with -gain > max_loss_db are dropped before uid allocation
+ * (compaction), survivors get d_psd_out[(t * (nphy-1) + k) * nbands + b] = psd_tx[t][b] * 10^(gain/10).
+ * rx_dbm in the record holds the gain (dB).  speed <= 0 means no delay model (delay 0). */
+int nsgpu_fanout_spectrum(const nsgpu_phy_soa *phys, int64_t nphy, const nsgpu_tx_desc *d_tx, int64_t n_tx,
+                          const nsgpu_loss_chain *loss, double speed, double max_loss_db,
+                          const double *d_psd_tx, int32_t nbands,
+                          nsgpu_rx_record *d_out, double *d_psd_out, uint32_t *d_count,
+                          void *d_workspace, void *stream);
+int nsgpu_fanout_workspace_bytes(int64_t nphy, int64_t n_tx, uint64_t *bytes);
+
+/* ---------------- GPU-resident bench-simulator churn (config 1) ----------------
+ * Runs utils/bench-simulator.cc's RunBench + Simulator::Run (bench-simulator.cc:79-127) over
+ * MapScheduler order entirely on the device: n initial events Schedule (NanoSeconds (d[i])),
+ * each dispatch k <= total schedules a child at now + d[k mod n].  Pop order is bit-exact;
+ * it is reported as counters, an order-sensitive digest and (optionally) the full pop log. */
+typedef struct nsgpu_hold_stats {
+  uint64_t dispatched;   /* RemoveNext calls */
+  uint64_t holds;        /* Bench::m_n */
+  uint64_t final_ts;     /* ts of the last dispatched event */
+  uint64_t digest;       /* sum_k nsgpu_dispatch_digest_term (k, ts_k, uid_k) */
+  uint64_t rounds;       /* device rounds (parallel dispatch batches) */
+  uint32_t max_batch;    /* largest batch dispatched in one round */
+  uint32_t next_uid;     /* DefaultSimulatorImpl::m_uid after the run */
+} nsgpu_hold_stats;
+
+int nsgpu_hold_workspace_bytes(uint32_t n, uint64_t *bytes);
+int nsgpu_hold_run(const uint64_t *d_dist, uint32_t n, uint32_t total, nsgpu_hold_stats *d_stats,
+                   uint64_t *d_log_ts, uint32_t *d_log_uid, uint64_t log_cap, void *d_workspace, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSGPU_H */

@@ -12,6 +12,12 @@
 
 #include <stdint.h>
 
+#if defined(__HIP__)
+#define NSGPU_HD __host__ __device__
+#else
+#define NSGPU_HD
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -68,12 +74,12 @@ typedef struct nsgpu_rx_record {
 
 /* Order-sensitive digest of a dispatch sequence: sum over k of mix(k, ts_k, uid_k).
  * Used to compare long dispatch orders (pop order) without moving whole logs. */
-static inline uint64_t nsgpu_mix64(uint64_t z) {
+NSGPU_HD static inline uint64_t nsgpu_mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
   return z ^ (z >> 31);
 }
-static inline uint64_t nsgpu_dispatch_digest_term(uint64_t rank, uint64_t ts, uint32_t uid) {
+NSGPU_HD static inline uint64_t nsgpu_dispatch_digest_term(uint64_t rank, uint64_t ts, uint32_t uid) {
   return nsgpu_mix64(rank * 0x9e3779b97f4a7c15ULL ^ nsgpu_mix64(ts ^ ((uint64_t)uid << 40) ^ (uint64_t)uid));
 }
 

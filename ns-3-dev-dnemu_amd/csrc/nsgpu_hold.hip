@@ -1,0 +1,280 @@
+// nsgpu_hold.hip — GPU-resident run of utils/bench-simulator.cc (config 1, "hold" churn).
+//
+// Reference semantics (restated in oracle/nsref_sched.cc):
+//   RunBench (bench-simulator.cc:79-107): Schedule (NanoSeconds (d[i]), &Bench::Cb) for i < N,
+//     so the initial events are (ts = d[i], uid = 4 + i, ctx = 0xffffffff);
+//   Cb (:109-127): the k-th dispatch (k = 0,1,..) schedules a child at now + d[k mod N]
+//     with uid = 4 + N + k while k <= total; later dispatches schedule nothing.
+//   Dispatch order is MapScheduler's (ts, uid) order (map-scheduler.cc:79-91, scheduler.h:105-121).
+//
+// Device design (MI355X): the run is one persistent workgroup that keeps the whole pending
+// set (a (ts, uid)-sorted array) in LDS and advances in rounds:
+//   1. the B smallest pending events are the candidates; candidate r would be dispatch K + r,
+//      so its child time ts_r + d[(K + r) mod N] is known without executing anything;
+//   2. a workgroup prefix-min over the candidates' child times finds the longest prefix p in
+//      which no earlier candidate's child precedes a later candidate (child uids are larger
+//      than every pending uid, so a child at an equal ts sorts after) — exactly the events
+//      MapScheduler would pop next, in the same order;
+//   3. the p events are committed (counters, order-sensitive digest, optional pop log), their
+//      children are ranked by counting and merged into the sorted array in place (every
+//      surviving element only moves left, so one read phase + one write phase suffice).
+// The prefix check is what makes parallel dispatch bit-exact: no uid or order is guessed.
+#include "nsgpu_device.h"
+#include "nsgpu_internal.h"
+
+namespace nsgpu {
+
+constexpr int HOLD_THREADS = 1024;
+constexpr int HOLD_BATCH = 1024;          // candidates examined per round (<= HOLD_THREADS)
+constexpr int HOLD_MAX_PENDING = 11264;   // LDS capacity for the sorted pending array
+constexpr int HOLD_PER_THREAD = (HOLD_MAX_PENDING + HOLD_THREADS - 1) / HOLD_THREADS;  // 11
+
+// ---------------------------------------------------------------------------------------
+// Initial insert: the N scheduled events sorted by (ts, uid) — rank by counting, tiled in LDS.
+// (N <= HOLD_MAX_PENDING; O(N^2) comparisons spread over the whole chip: ~1e8 for N = 1e4.)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void hold_init_rank(const uint64_t *__restrict__ dist, uint32_t n,
+                                                      uint64_t *__restrict__ out_ts, uint32_t *__restrict__ out_uid) {
+  __shared__ uint64_t tile[256];
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const uint64_t my = i < n ? dist[i] : 0;
+  uint32_t rank = 0;
+  for (uint32_t base = 0; base < n; base += 256) {
+    uint32_t j = base + threadIdx.x;
+    tile[threadIdx.x] = j < n ? dist[j] : ~0ull;
+    __syncthreads();
+    const uint32_t lim = min(256u, n - base);
+    for (uint32_t q = 0; q < lim; q++) {
+      uint64_t t = tile[q];
+      // key (t, 4 + base + q) < key (my, 4 + i)
+      rank += (t < my) || (t == my && base + q < i);
+    }
+    __syncthreads();
+  }
+  if (i < n) {
+    out_ts[rank] = my;
+    out_uid[rank] = 4u + i;
+  }
+}
+
+struct HoldLds {
+  uint64_t ts[HOLD_MAX_PENDING];
+  uint32_t uid[HOLD_MAX_PENDING];
+  uint64_t cts[HOLD_BATCH];   // child ts (unsorted, by candidate index); sorted after ranking
+  uint32_t cuid[HOLD_BATCH];
+  uint64_t sts[HOLD_BATCH];   // children sorted
+  uint32_t suid[HOLD_BATCH];
+  uint64_t wave_min[HOLD_THREADS / 64];
+  uint32_t wave_first[HOLD_THREADS / 64];
+  uint32_t p;                 // committed prefix this round
+};
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t w = __shfl_xor(v, o);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// Exclusive prefix-min across the 64 lanes of a wave.
+__device__ __forceinline__ uint64_t wave_exscan_min_u64(uint64_t v, int lane) {
+  uint64_t inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t w = __shfl_up(inc, o);
+    if (lane >= o) inc = w < inc ? w : inc;
+  }
+  uint64_t ex = __shfl_up(inc, 1);
+  return lane == 0 ? ~0ull : ex;
+}
+
+// lower_bound over a sorted (ts, uid) range in LDS: number of elements < (kts, kuid).
+__device__ __forceinline__ uint32_t lds_lower_bound(const uint64_t *ts, const uint32_t *uid, uint32_t lo,
+                                                     uint32_t hi, uint64_t kts, uint32_t kuid) {
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (key_less(ts[mid], uid[mid], kts, kuid)) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(HOLD_THREADS) void hold_run(const uint64_t *__restrict__ dist, uint32_t n,
+                                                         uint32_t total, const uint64_t *__restrict__ init_ts,
+                                                         const uint32_t *__restrict__ init_uid,
+                                                         nsgpu_hold_stats *__restrict__ stats,
+                                                         uint64_t *__restrict__ log_ts,
+                                                         uint32_t *__restrict__ log_uid, uint64_t log_cap) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  HoldLds &L = *reinterpret_cast<HoldLds *>(smem_raw);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+
+  for (uint32_t j = tid; j < n; j += HOLD_THREADS) {
+    L.ts[j] = init_ts[j];
+    L.uid[j] = init_uid[j];
+  }
+  __syncthreads();
+
+  uint32_t P = n;         // pending count
+  uint64_t K = 0;         // dispatched so far
+  uint64_t digest = 0;    // per-thread partial of the order-sensitive digest
+  uint64_t rounds = 0;
+  uint64_t last_ts = 0;
+  uint32_t max_p = 0;
+  const uint64_t holds_limit = (uint64_t)total + 1;  // dispatches k <= total schedule a child
+
+  while (P > 0) {
+    const uint32_t B = P < HOLD_BATCH ? P : HOLD_BATCH;
+    // ---- 1. candidates and their (speculative) child times ----
+    uint64_t my_ts = 0, child = ~0ull;
+    uint32_t my_uid = 0;
+    if (tid < (int)B) {
+      my_ts = L.ts[tid];
+      my_uid = L.uid[tid];
+      const uint64_t k = K + tid;
+      if (k < holds_limit) child = my_ts + dist[k % n];
+    }
+    // ---- 2. exclusive prefix-min of child times; first violation = first r with prefmin < ts_r ----
+    uint64_t ex = wave_exscan_min_u64(child, lane);
+    uint64_t wmin = wave_min_u64(child);
+    if (lane == 0) L.wave_min[wid] = wmin;
+    __syncthreads();
+    uint64_t carry = ~0ull;
+    for (int w = 0; w < wid; w++) carry = L.wave_min[w] < carry ? L.wave_min[w] : carry;
+    uint64_t prefmin = ex < carry ? ex : carry;
+    const bool bad = (tid < (int)B) && (tid > 0) && (prefmin < my_ts);
+    const unsigned long long ballot = __ballot(bad);
+    if (lane == 0) L.wave_first[wid] = ballot ? (uint32_t)(wid * 64 + __ffsll((long long)ballot) - 1) : 0xffffffffu;
+    __syncthreads();
+    uint32_t p = B;
+    for (int w = 0; w < HOLD_THREADS / 64; w++) p = L.wave_first[w] < p ? L.wave_first[w] : p;
+
+    // ---- 3. commit dispatches K .. K+p-1 ----
+    const bool commit = tid < (int)p;
+    if (commit) {
+      const uint64_t k = K + tid;
+      digest += digest_term(k, my_ts, my_uid);
+      if (k < log_cap) {
+        log_ts[k] = my_ts;
+        log_uid[k] = my_uid;
+      }
+      if (tid == (int)p - 1) last_ts = my_ts;
+    }
+    // children of committed events: the first m of them (k <= total)
+    const uint64_t rem_holds = K < holds_limit ? holds_limit - K : 0;
+    const uint32_t m = (uint32_t)(rem_holds < p ? rem_holds : p);
+    if (tid < (int)m) {
+      L.cts[tid] = child;
+      L.cuid[tid] = (uint32_t)(4u + n + (K + tid));  // Schedule order = dispatch order
+    }
+    __syncthreads();
+    // ---- 4. rank children by counting, write the sorted child list ----
+    if (tid < (int)m) {
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < m; j++) r += key_less(L.cts[j], L.cuid[j], child, L.cuid[tid]);
+      L.sts[r] = child;
+      L.suid[r] = L.cuid[tid];
+    }
+    __syncthreads();
+    // ---- 5. merge children into pending[p..P): read phase ----
+    uint64_t rts[HOLD_PER_THREAD];
+    uint32_t ruid[HOLD_PER_THREAD];
+    uint32_t rpos[HOLD_PER_THREAD];
+#pragma unroll
+    for (int q = 0; q < HOLD_PER_THREAD; q++) {
+      const uint32_t j = p + tid + q * HOLD_THREADS;
+      rpos[q] = 0xffffffffu;
+      if (j < P) {
+        rts[q] = L.ts[j];
+        ruid[q] = L.uid[j];
+        rpos[q] = (j - p) + lds_lower_bound(L.sts, L.suid, 0, m, rts[q], ruid[q]);
+      }
+    }
+    uint64_t cts_mine = 0;
+    uint32_t cuid_mine = 0, cpos = 0xffffffffu;
+    if (tid < (int)m) {
+      cts_mine = L.sts[tid];
+      cuid_mine = L.suid[tid];
+      cpos = tid + (lds_lower_bound(L.ts, L.uid, p, P, cts_mine, cuid_mine) - p);
+    }
+    __syncthreads();
+    // ---- 6. write phase ----
+#pragma unroll
+    for (int q = 0; q < HOLD_PER_THREAD; q++) {
+      if (rpos[q] != 0xffffffffu) {
+        L.ts[rpos[q]] = rts[q];
+        L.uid[rpos[q]] = ruid[q];
+      }
+    }
+    if (cpos != 0xffffffffu) {
+      L.ts[cpos] = cts_mine;
+      L.uid[cpos] = cuid_mine;
+    }
+    __syncthreads();
+    K += p;
+    P = P - p + m;
+    rounds++;
+    max_p = p > max_p ? p : max_p;
+  }
+
+  // ---- final reductions ----
+  __shared__ uint64_t red[HOLD_THREADS / 64];
+  uint64_t d = digest;
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+  if (lane == 0) red[wid] = d;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t s = 0;
+    for (int w = 0; w < HOLD_THREADS / 64; w++) s += red[w];
+    stats->digest = s;
+    stats->dispatched = K;
+    stats->holds = K < holds_limit ? K : holds_limit;
+    stats->rounds = rounds;
+    stats->max_batch = max_p;
+    stats->next_uid = (uint32_t)(4u + n + (K < holds_limit ? K : holds_limit));
+  }
+  // last committed ts lives in the thread that committed the final event of the last round
+  if (last_ts != 0 || (K > 0 && tid == 0)) {
+    // only the maximum matters: committed ts are non-decreasing in dispatch order
+    atomicMax((unsigned long long *)&stats->final_ts, (unsigned long long)last_ts);
+  }
+}
+
+}  // namespace nsgpu
+
+using namespace nsgpu;
+
+extern "C" int nsgpu_hold_workspace_bytes(uint32_t n, uint64_t *bytes) {
+  *bytes = (uint64_t)n * (sizeof(uint64_t) + sizeof(uint32_t)) + 256;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_hold_run(const uint64_t *d_dist, uint32_t n, uint32_t total, nsgpu_hold_stats *d_stats,
+                              uint64_t *d_log_ts, uint32_t *d_log_uid, uint64_t log_cap, void *d_workspace,
+                              void *stream) {
+  if (n == 0 || n > (uint32_t)HOLD_MAX_PENDING)
+    return set_error(NSGPU_EINVAL, "nsgpu_hold_run: n=%u outside [1, %d] (pending set must fit LDS)", n,
+                     HOLD_MAX_PENDING);
+  if ((uint64_t)n + (uint64_t)total + 5 > 0xffffffffull)
+    return set_error(NSGPU_EINVAL, "nsgpu_hold_run: uid space (uint32, SURVEY H2) would wrap");
+  if (!d_dist || !d_stats || !d_workspace) return set_error(NSGPU_EINVAL, "nsgpu_hold_run: null pointer");
+  if (log_cap && (!d_log_ts || !d_log_uid)) return set_error(NSGPU_EINVAL, "nsgpu_hold_run: null log buffers");
+  hipStream_t s = (hipStream_t)stream;
+  uint64_t *ws_ts = (uint64_t *)d_workspace;
+  uint32_t *ws_uid = (uint32_t *)(ws_ts + n);
+  NSGPU_HIP(hipMemsetAsync(d_stats, 0, sizeof(nsgpu_hold_stats), s));
+  hipLaunchKernelGGL(hold_init_rank, dim3((n + 255) / 256), dim3(256), 0, s, d_dist, n, ws_ts, ws_uid);
+  NSGPU_HIP(hipGetLastError());
+  static bool attr_set = false;
+  if (!attr_set) {
+    NSGPU_HIP(hipFuncSetAttribute((const void *)hold_run, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(HoldLds)));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(hold_run, dim3(1), dim3(HOLD_THREADS), sizeof(HoldLds), s, d_dist, n, total, ws_ts, ws_uid,
+                     d_stats, d_log_ts, d_log_uid, log_cap);
+  NSGPU_HIP(hipGetLastError());
+  return NSGPU_OK;
+}

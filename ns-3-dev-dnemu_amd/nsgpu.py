@@ -1,0 +1,276 @@
+"""Python binding of libnsgpu.so (include/nsgpu.h) — host plumbing for tests and bench.py.
+
+This module only forwards to the C-ABI: every computation runs in the HIP kernels of
+libnsgpu.so.  There is no CPU fallback: if the library (or a GPU) is missing, calls raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnsgpu.so")
+
+
+class NsgpuError(RuntimeError):
+    pass
+
+
+class PhySoA(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("y", C.c_void_p), ("z", C.c_void_p), ("channel", C.c_void_p),
+                ("node", C.c_void_p)]
+
+
+class LossModel(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p0", C.c_double), ("p1", C.c_double), ("p2", C.c_double)]
+
+
+class LossChain(C.Structure):
+    _fields_ = [("n", C.c_int32), ("pad_", C.c_int32), ("m", LossModel * 4)]
+
+
+class HoldStats(C.Structure):
+    _fields_ = [("dispatched", C.c_uint64), ("holds", C.c_uint64), ("final_ts", C.c_uint64),
+                ("digest", C.c_uint64), ("rounds", C.c_uint64), ("max_batch", C.c_uint32),
+                ("next_uid", C.c_uint32)]
+
+
+TX_DESC_DTYPE = np.dtype([("now_ts", "<u8"), ("tx_dbm", "<f8"), ("sender", "<u4"), ("uid_base", "<u4")])
+RX_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("context", "<u4"), ("phy", "<u4"),
+                            ("pad_", "<u4"), ("rx_dbm", "<f8")])
+
+LOSS_NONE, LOSS_LOG_DISTANCE, LOSS_FRIIS, LOSS_FIXED_RSS, LOSS_RANGE = 0, 1, 2, 3, 4
+
+# symbol -> (restype, argtypes); the list is also what tests check the .so exports.
+_vp, _i64, _u64, _u32, _i32, _d = C.c_void_p, C.c_int64, C.c_uint64, C.c_uint32, C.c_int32, C.c_double
+SIGNATURES = {
+    "nsgpu_version": (C.c_int, []),
+    "nsgpu_last_error": (C.c_char_p, []),
+    "nsgpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "nsgpu_set_device": (C.c_int, [C.c_int]),
+    "nsgpu_malloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
+    "nsgpu_free": (C.c_int, [_vp]),
+    "nsgpu_memcpy_htod": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
+    "nsgpu_memcpy_dtoh": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
+    "nsgpu_memset": (C.c_int, [_vp, C.c_int, C.c_size_t, _vp]),
+    "nsgpu_stream_create": (C.c_int, [C.POINTER(C.c_void_p)]),
+    "nsgpu_stream_destroy": (C.c_int, [_vp]),
+    "nsgpu_stream_sync": (C.c_int, [_vp]),
+    "nsgpu_event_create": (C.c_int, [C.POINTER(C.c_void_p)]),
+    "nsgpu_event_destroy": (C.c_int, [_vp]),
+    "nsgpu_event_record": (C.c_int, [_vp, _vp]),
+    "nsgpu_event_elapsed_ms": (C.c_int, [_vp, _vp, C.POINTER(C.c_float)]),
+    "nsgpu_seconds_to_ts": (C.c_int, [_vp, _vp, _i64, _vp]),
+    "nsgpu_fanout_yans": (C.c_int, [C.POINTER(PhySoA), _i64, _vp, _i64, C.POINTER(LossChain), _d, _vp, _vp, _vp,
+                                    _vp]),
+    "nsgpu_fanout_spectrum": (C.c_int, [C.POINTER(PhySoA), _i64, _vp, _i64, C.POINTER(LossChain), _d, _d, _vp,
+                                        _i32, _vp, _vp, _vp, _vp, _vp]),
+    "nsgpu_fanout_workspace_bytes": (C.c_int, [_i64, _i64, C.POINTER(C.c_uint64)]),
+    "nsgpu_hold_workspace_bytes": (C.c_int, [_u32, C.POINTER(C.c_uint64)]),
+    "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libnsgpu.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NsgpuError(f"{LIB_PATH} is missing: build it with `make -C ns-3-dev-dnemu_amd` "
+                             "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def check(status):
+    if status != 0:
+        raise NsgpuError(f"nsgpu error {status}: {lib().nsgpu_last_error().decode()}")
+
+
+def device_count():
+    n = C.c_int(0)
+    check(lib().nsgpu_device_count(C.byref(n)))
+    return n.value
+
+
+class DeviceBuffer:
+    """A hipMalloc'd buffer (owned), with numpy upload/download."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(lib().nsgpu_malloc(C.byref(p), max(self.nbytes, 1)))
+        self.ptr = p.value
+
+    @classmethod
+    def from_array(cls, arr, stream=None):
+        arr = np.ascontiguousarray(arr)
+        b = cls(arr.nbytes)
+        if arr.nbytes:
+            check(lib().nsgpu_memcpy_htod(b.ptr, arr.ctypes.data, arr.nbytes, stream))
+            check(lib().nsgpu_stream_sync(stream))
+        return b
+
+    def zero(self, stream=None):
+        check(lib().nsgpu_memset(self.ptr, 0, self.nbytes, stream))
+
+    def download(self, dtype, count=None, stream=None):
+        dtype = np.dtype(dtype)
+        count = self.nbytes // dtype.itemsize if count is None else count
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            check(lib().nsgpu_memcpy_dtoh(out.ctypes.data, self.ptr, out.nbytes, stream))
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().nsgpu_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Stream:
+    def __init__(self):
+        p = C.c_void_p()
+        check(lib().nsgpu_stream_create(C.byref(p)))
+        self.handle = p.value
+
+    def sync(self):
+        check(lib().nsgpu_stream_sync(self.handle))
+
+    def __del__(self):
+        try:
+            lib().nsgpu_stream_destroy(self.handle)
+        except Exception:
+            pass
+
+
+class Timer:
+    """HIP events recorded on the stream the kernels are launched on."""
+
+    def __init__(self):
+        a, b = C.c_void_p(), C.c_void_p()
+        check(lib().nsgpu_event_create(C.byref(a)))
+        check(lib().nsgpu_event_create(C.byref(b)))
+        self.a, self.b = a.value, b.value
+
+    def start(self, stream):
+        check(lib().nsgpu_event_record(self.a, stream))
+
+    def stop(self, stream):
+        check(lib().nsgpu_event_record(self.b, stream))
+
+    def elapsed_ms(self):
+        ms = C.c_float()
+        check(lib().nsgpu_event_elapsed_ms(self.a, self.b, C.byref(ms)))
+        return ms.value
+
+
+def loss_chain(*models):
+    ch = LossChain()
+    ch.n = len(models)
+    for i, (k, a, b, c) in enumerate(models):
+        ch.m[i].kind, ch.m[i].p0, ch.m[i].p1, ch.m[i].p2 = k, a, b, c
+    return ch
+
+
+# ---------------- operations ----------------
+def seconds_to_ts(values, stream=None):
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    din = DeviceBuffer.from_array(v, stream)
+    dout = DeviceBuffer(v.nbytes)
+    check(lib().nsgpu_seconds_to_ts(din.ptr, dout.ptr, v.size, stream))
+    return dout.download(np.int64, v.size, stream)
+
+
+class PhyList:
+    """m_phyList of a broadcast channel, resident in HBM as SoA."""
+
+    def __init__(self, x, y, z, channel, node, stream=None):
+        self.n = len(x)
+        self.bufs = [DeviceBuffer.from_array(np.asarray(a, dtype=t), stream) for a, t in
+                     ((x, np.float64), (y, np.float64), (z, np.float64), (channel, np.uint32), (node, np.uint32))]
+        self.soa = PhySoA(*[b.ptr for b in self.bufs])
+
+
+class Fanout:
+    """Batched broadcast fan-out (Yans / single-model spectrum) over a resident PhyList."""
+
+    def __init__(self, phys, max_tx, nbands=0, stream=None):
+        self.phys, self.max_tx, self.nbands, self.stream = phys, max_tx, nbands, stream
+        ws = C.c_uint64()
+        check(lib().nsgpu_fanout_workspace_bytes(phys.n, max_tx, C.byref(ws)))
+        self.ws = DeviceBuffer(ws.value)
+        self.out = DeviceBuffer(max_tx * (phys.n - 1) * RX_RECORD_DTYPE.itemsize)
+        self.count = DeviceBuffer(max_tx * 4)
+        self.tx = DeviceBuffer(max_tx * TX_DESC_DTYPE.itemsize)
+        self.psd_out = DeviceBuffer(max_tx * (phys.n - 1) * max(nbands, 1) * 8) if nbands else None
+        self.psd_tx = DeviceBuffer(max_tx * max(nbands, 1) * 8) if nbands else None
+
+    def upload_tx(self, tx):
+        tx = np.ascontiguousarray(tx, dtype=TX_DESC_DTYPE)
+        assert len(tx) <= self.max_tx
+        check(lib().nsgpu_memcpy_htod(self.tx.ptr, tx.ctypes.data, tx.nbytes, self.stream))
+        return len(tx)
+
+    def launch_yans(self, n_tx, chain, speed):
+        check(lib().nsgpu_fanout_yans(C.byref(self.phys.soa), self.phys.n, self.tx.ptr, n_tx, C.byref(chain), speed,
+                                      self.out.ptr, self.count.ptr, self.ws.ptr, self.stream))
+
+    def launch_spectrum(self, n_tx, chain, speed, max_loss_db):
+        check(lib().nsgpu_fanout_spectrum(C.byref(self.phys.soa), self.phys.n, self.tx.ptr, n_tx, C.byref(chain),
+                                          speed, max_loss_db, self.psd_tx.ptr if self.psd_tx else None,
+                                          self.nbands, self.out.ptr, self.psd_out.ptr if self.psd_out else None,
+                                          self.count.ptr, self.ws.ptr, self.stream))
+
+    def results(self, n_tx):
+        counts = self.count.download(np.uint32, n_tx, self.stream)
+        recs = self.out.download(RX_RECORD_DTYPE, n_tx * (self.phys.n - 1), self.stream)
+        recs = recs.reshape(n_tx, self.phys.n - 1)
+        out = [recs[t, :counts[t]] for t in range(n_tx)]
+        psd = None
+        if self.nbands:
+            p = self.psd_out.download(np.float64, n_tx * (self.phys.n - 1) * self.nbands, self.stream)
+            p = p.reshape(n_tx, self.phys.n - 1, self.nbands)
+            psd = [p[t, :counts[t]] for t in range(n_tx)]
+        return out, psd
+
+
+class HoldRun:
+    """GPU-resident utils/bench-simulator.cc run (config 1)."""
+
+    def __init__(self, dist_ns, total, log_cap=0, stream=None):
+        self.dist_ns = np.ascontiguousarray(dist_ns, dtype=np.uint64)
+        self.n, self.total, self.log_cap, self.stream = self.dist_ns.size, int(total), int(log_cap), stream
+        self.d_dist = DeviceBuffer.from_array(self.dist_ns, stream)
+        ws = C.c_uint64()
+        check(lib().nsgpu_hold_workspace_bytes(self.n, C.byref(ws)))
+        self.ws = DeviceBuffer(ws.value)
+        self.stats = DeviceBuffer(C.sizeof(HoldStats))
+        self.log_ts = DeviceBuffer(max(log_cap, 1) * 8)
+        self.log_uid = DeviceBuffer(max(log_cap, 1) * 4)
+
+    def launch(self):
+        check(lib().nsgpu_hold_run(self.d_dist.ptr, self.n, self.total, self.stats.ptr,
+                                   self.log_ts.ptr if self.log_cap else None,
+                                   self.log_uid.ptr if self.log_cap else None, self.log_cap, self.ws.ptr,
+                                   self.stream))
+
+    def result(self):
+        raw = self.stats.download(np.uint8, C.sizeof(HoldStats), self.stream)
+        st = HoldStats.from_buffer_copy(raw.tobytes())
+        if self.log_cap:
+            return st, self.log_ts.download(np.uint64, self.log_cap, self.stream), \
+                self.log_uid.download(np.uint32, self.log_cap, self.stream)
+        return st, None, None
