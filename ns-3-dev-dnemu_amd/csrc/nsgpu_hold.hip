@@ -34,7 +34,9 @@ constexpr int HOLD_PER_THREAD = (HOLD_MAX_PENDING + HOLD_THREADS - 1) / HOLD_THR
 // (N <= HOLD_MAX_PENDING; O(N^2) comparisons spread over the whole chip: ~1e8 for N = 1e4.)
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void hold_init_rank(const uint64_t *__restrict__ dist, uint32_t n,
-                                                      uint64_t *__restrict__ out_ts, uint32_t *__restrict__ out_uid) {
+                                                      uint64_t *__restrict__ out_ts, uint32_t *__restrict__ out_uid,
+                                                      const uint32_t *__restrict__ wide_flag) {
+  if (*wide_flag == 0) return;  // the packed kernel handles this distribution
   __shared__ uint64_t tile[256];
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const uint64_t my = i < n ? dist[i] : 0;
@@ -99,12 +101,14 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const uint64_t *ts, const ui
   return lo;
 }
 
-__global__ __launch_bounds__(HOLD_THREADS) void hold_run(const uint64_t *__restrict__ dist, uint32_t n,
+__global__ __launch_bounds__(HOLD_THREADS) void hold_run_wide(const uint64_t *__restrict__ dist, uint32_t n,
                                                          uint32_t total, const uint64_t *__restrict__ init_ts,
                                                          const uint32_t *__restrict__ init_uid,
                                                          nsgpu_hold_stats *__restrict__ stats,
                                                          uint64_t *__restrict__ log_ts,
-                                                         uint32_t *__restrict__ log_uid, uint64_t log_cap) {
+                                                         uint32_t *__restrict__ log_uid, uint64_t log_cap,
+                                                         const uint32_t *__restrict__ wide_flag) {
+  if (*wide_flag == 0) return;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   HoldLds &L = *reinterpret_cast<HoldLds *>(smem_raw);
   const int tid = threadIdx.x;
@@ -242,15 +246,273 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run(const uint64_t *__restr
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Packed variant (the fast path).  When every delay is < 2^31 ns the pending set always lies
+// in [now, now + max_d] (each event was scheduled by an already-dispatched parent), so a key
+// (ts, uid) packs losslessly into one u64 as ((ts - base) << 32) | uid with base = the last
+// dispatched ts, re-based every round.  Unsigned u64 order on packed keys == (ts, uid) order.
+// Per round (1024 threads, one workgroup):
+//   A  candidates = S[0..B); child key = ((rel + d) << 32) | (4 + n + k) for dispatch k <= total
+//   B  exclusive prefix-min of child keys -> first violation p (2 barriers)
+//   C  commit p dispatches; stage the m children (1 barrier)
+//   D  per child: rank among children (sliced counting, LDS atomics) and lower_bound in S[p..P)
+//      (binary search); histogram H[lb - p] += 1 (1 barrier)
+//   E  each thread owns a contiguous chunk of S[p..P): shift(q) = #children with lb <= q is an
+//      inclusive scan of H (thread-local sums + workgroup scan, 1 barrier); new index = q - p + shift
+//   F  write S (re-based) after a read barrier; H is cleared by its owners in the same pass.
+// ---------------------------------------------------------------------------------------
+constexpr int HP_MAX = 11264;                                  // max pending
+constexpr int HP_CHUNK = (HP_MAX + HOLD_THREADS - 1) / HOLD_THREADS;  // 11 per thread
+constexpr int HP_SORT = 16384;                                 // bitonic buffer for the initial insert
+
+struct HoldPackedLds {
+  union {
+    struct {
+      uint64_t S[HP_MAX];          // sorted packed keys
+      uint32_t H[HP_MAX + 1];      // histogram of children lower bounds (relative to p)
+    } m;
+    uint64_t sortbuf[HP_SORT];     // initial insert (aliases S and H)
+  } u;
+  uint64_t Ck[HOLD_BATCH];         // children keys (by candidate index)
+  uint32_t Rk[HOLD_BATCH];         // children ranks
+  uint64_t Wmin[HOLD_THREADS / 64];
+  uint32_t Wfirst[HOLD_THREADS / 64];
+  uint32_t Wsum[HOLD_THREADS / 64];
+};
+
+__device__ __forceinline__ uint32_t wave_exscan_add_u32(uint32_t v, int lane) {
+  uint32_t inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t w = __shfl_up(inc, o);
+    if (lane >= o) inc += w;
+  }
+  return inc - v;
+}
+
+__global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *__restrict__ dist32, uint32_t n,
+                                                                uint32_t total, nsgpu_hold_stats *__restrict__ stats,
+                                                                uint64_t *__restrict__ log_ts,
+                                                                uint32_t *__restrict__ log_uid, uint64_t log_cap,
+                                                                const uint32_t *__restrict__ wide_flag) {
+  if (*wide_flag != 0) return;  // some delay >= 2^31 ns: the wide kernel handles it
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  HoldPackedLds &L = *reinterpret_cast<HoldPackedLds *>(smem_raw);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const uint64_t INF = ~0ull;
+
+  // ---- initial insert: Schedule (NanoSeconds (d[i])) -> key (d[i], 4 + i), base = 0; bitonic sort ----
+  for (int i = tid; i < HP_SORT; i += HOLD_THREADS)
+    L.u.sortbuf[i] = i < (int)n ? (((uint64_t)dist32[i] << 32) | (uint32_t)(4u + i)) : INF;
+  __syncthreads();
+  for (int k = 2; k <= HP_SORT; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < HP_SORT; i += HOLD_THREADS) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = L.u.sortbuf[i], b = L.u.sortbuf[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            L.u.sortbuf[i] = b;
+            L.u.sortbuf[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // S = sortbuf[0..n) already in place; clear H (it aliases the tail of the sort buffer)
+  for (int i = tid; i <= HP_MAX; i += HOLD_THREADS) L.u.m.H[i] = 0;
+  __syncthreads();
+
+  uint32_t P = n;
+  uint64_t K = 0;
+  uint32_t Kmod = 0;       // K mod n
+  uint64_t base = 0;       // absolute ts of packed rel 0
+  uint64_t digest = 0;
+  uint64_t rounds = 0;
+  uint64_t final_ts = 0;
+  uint32_t max_p = 0;
+  const uint64_t HL = (uint64_t)total + 1;   // dispatches k < HL schedule a child
+  const uint32_t uid0 = 4u + n;
+
+  // prefetch the delay of candidate tid for the first round
+  uint32_t dnext = 0;
+  {
+    uint32_t idx = (uint32_t)tid % n;
+    dnext = dist32[idx];
+  }
+
+  while (P > 0) {
+    const uint32_t B = P < HOLD_BATCH ? P : HOLD_BATCH;
+    // ---- A ----
+    uint64_t key = INF, child = INF;
+    if (tid < (int)B) {
+      key = L.u.m.S[tid];
+      const uint64_t k = K + tid;
+      if (k < HL) child = (((key >> 32) + dnext) << 32) | (uint32_t)(uid0 + (uint32_t)k);
+    }
+    if (tid < HOLD_BATCH) L.Rk[tid] = 0;
+    // ---- B ----
+    uint64_t inc = child;
+    for (int o = 1; o < 64; o <<= 1) {
+      uint64_t w = __shfl_up(inc, o);
+      if (lane >= o) inc = w < inc ? w : inc;
+    }
+    uint64_t ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = INF;
+    if (lane == 63) L.Wmin[wid] = inc;
+    __syncthreads();
+    uint64_t carry = INF;
+    for (int w = 0; w < wid; w++) {
+      uint64_t v = L.Wmin[w];
+      carry = v < carry ? v : carry;
+    }
+    const uint64_t prefmin = ex < carry ? ex : carry;
+    const bool bad = (tid < (int)B) && (tid > 0) && (prefmin < key);
+    const unsigned long long bal = __ballot(bad);
+    if (lane == 0) L.Wfirst[wid] = bal ? (uint32_t)(wid * 64 + __ffsll((unsigned long long)bal) - 1) : 0xffffffffu;
+    __syncthreads();
+    uint32_t p = B;
+#pragma unroll
+    for (int w = 0; w < HOLD_THREADS / 64; w++) {
+      uint32_t v = L.Wfirst[w];
+      p = v < p ? v : p;
+    }
+    const uint32_t m = K < HL ? (uint32_t)((HL - K) < p ? (HL - K) : p) : 0u;
+    const uint64_t last_key = L.u.m.S[p - 1];  // the last dispatched event: the new base
+    // ---- C ----
+    if (tid < (int)p) {
+      const uint64_t k = K + tid;
+      const uint64_t ts = base + (key >> 32);
+      digest += digest_term(k, ts, (uint32_t)key);
+      if (k < log_cap) {
+        log_ts[k] = ts;
+        log_uid[k] = (uint32_t)key;
+      }
+    }
+    if (tid < (int)m) L.Ck[tid] = child;
+    // prefetch next round's delay (dispatch K + p + tid)
+    {
+      uint32_t idx = Kmod + p + (uint32_t)tid;
+      if (idx >= n) idx %= n;
+      dnext = dist32[idx];
+    }
+    __syncthreads();
+    // ---- D ----
+    uint32_t lb = 0;
+    if (m > 0) {
+      const uint32_t nsl = HOLD_THREADS / m;          // slices per child (>= 1)
+      const uint32_t c = tid % m, sl = tid / m;
+      if (sl < nsl) {
+        const uint64_t ck = L.Ck[c];
+        const uint32_t j0 = (uint32_t)(((uint64_t)sl * m) / nsl), j1 = (uint32_t)(((uint64_t)(sl + 1) * m) / nsl);
+        uint32_t cnt = 0;
+        for (uint32_t j = j0; j < j1; j++) cnt += L.Ck[j] < ck;
+        if (cnt) atomicAdd(&L.Rk[c], cnt);
+      }
+      if (tid < (int)m) {
+        uint32_t lo = p, hi = P;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (L.u.m.S[mid] < child) lo = mid + 1;
+          else hi = mid;
+        }
+        lb = lo;
+        if (lb < P) atomicAdd(&L.u.m.H[lb - p], 1u);
+      }
+    }
+    __syncthreads();
+    // ---- E ----
+    const uint32_t R = P - p;                          // survivors
+    const uint32_t chunk = (R + HOLD_THREADS - 1) / HOLD_THREADS;
+    const uint32_t q0 = tid * chunk;
+    uint64_t sv[HP_CHUNK];
+    uint32_t sh[HP_CHUNK];
+    uint32_t local = 0;
+#pragma unroll
+    for (int q = 0; q < HP_CHUNK; q++) {
+      const uint32_t r = q0 + q;
+      sh[q] = 0;
+      sv[q] = INF;
+      if (q < (int)chunk && r < R) {
+        sv[q] = L.u.m.S[p + r];
+        local += L.u.m.H[r];
+        L.u.m.H[r] = 0;
+        sh[q] = local;
+      }
+    }
+    const uint32_t wex = wave_exscan_add_u32(local, lane);
+    if (lane == 63) L.Wsum[wid] = wex + local;
+    uint32_t cpos = 0xffffffffu;
+    uint64_t cval = 0;
+    if (tid < (int)m) {
+      cpos = L.Rk[tid] + (lb - p);
+      cval = child;
+    }
+    __syncthreads();
+    uint32_t off = wex;
+    for (int w = 0; w < wid; w++) off += L.Wsum[w];
+    // ---- F ----
+    const uint64_t rebase = last_key & 0xffffffff00000000ull;
+#pragma unroll
+    for (int q = 0; q < HP_CHUNK; q++) {
+      const uint32_t r = q0 + q;
+      if (q < (int)chunk && r < R) L.u.m.S[r + off + sh[q]] = sv[q] - rebase;
+    }
+    if (cpos != 0xffffffffu) L.u.m.S[cpos] = cval - rebase;
+    __syncthreads();
+    base += last_key >> 32;
+    final_ts = base;
+    K += p;
+    Kmod += p;
+    if (Kmod >= n) Kmod %= n;
+    P = R + m;
+    rounds++;
+    max_p = p > max_p ? p : max_p;
+  }
+
+  uint64_t d = digest;
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+  if (lane == 0) L.Wmin[wid] = d;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t s = 0;
+    for (int w = 0; w < HOLD_THREADS / 64; w++) s += L.Wmin[w];
+    stats->digest = s;
+    stats->dispatched = K;
+    stats->holds = K < HL ? K : HL;
+    stats->rounds = rounds;
+    stats->max_batch = max_p;
+    stats->next_uid = (uint32_t)(uid0 + (K < HL ? K : HL));
+    stats->final_ts = final_ts;
+  }
+}
+
+// Packs the u64 distribution into u32 (requires max < 2^31) and reports whether it fits.
+__global__ void hold_pack_dist(const uint64_t *__restrict__ dist, uint32_t n, uint32_t *__restrict__ out,
+                               uint32_t *__restrict__ overflow) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t v = dist[i];
+    out[i] = (uint32_t)v;
+    if (v >= (1ull << 31)) atomicOr(overflow, 1u);
+  }
+}
+
 }  // namespace nsgpu
 
 using namespace nsgpu;
 
 extern "C" int nsgpu_hold_workspace_bytes(uint32_t n, uint64_t *bytes) {
-  *bytes = (uint64_t)n * (sizeof(uint64_t) + sizeof(uint32_t)) + 256;
+  *bytes = (uint64_t)n * (sizeof(uint64_t) + sizeof(uint32_t) + sizeof(uint32_t)) + 256;
   return NSGPU_OK;
 }
 
+// Runs the packed kernel when every delay is < 2^31 ns, else the wide one.  The choice is made
+// on the device (hold_pack_dist sets a flag; the kernel of the other variant exits at once), so
+// a launch never synchronises with the host.
 extern "C" int nsgpu_hold_run(const uint64_t *d_dist, uint32_t n, uint32_t total, nsgpu_hold_stats *d_stats,
                               uint64_t *d_log_ts, uint32_t *d_log_uid, uint64_t log_cap, void *d_workspace,
                               void *stream) {
@@ -264,17 +526,24 @@ extern "C" int nsgpu_hold_run(const uint64_t *d_dist, uint32_t n, uint32_t total
   hipStream_t s = (hipStream_t)stream;
   uint64_t *ws_ts = (uint64_t *)d_workspace;
   uint32_t *ws_uid = (uint32_t *)(ws_ts + n);
-  NSGPU_HIP(hipMemsetAsync(d_stats, 0, sizeof(nsgpu_hold_stats), s));
-  hipLaunchKernelGGL(hold_init_rank, dim3((n + 255) / 256), dim3(256), 0, s, d_dist, n, ws_ts, ws_uid);
-  NSGPU_HIP(hipGetLastError());
-  static bool attr_set = false;
-  if (!attr_set) {
-    NSGPU_HIP(hipFuncSetAttribute((const void *)hold_run, hipFuncAttributeMaxDynamicSharedMemorySize,
+  uint32_t *ws_d32 = ws_uid + n;
+  uint32_t *ws_flag = (uint32_t *)((char *)d_workspace + (uint64_t)n * 16);
+  static bool attrs = false;
+  if (!attrs) {
+    NSGPU_HIP(hipFuncSetAttribute((const void *)hold_run_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sizeof(HoldLds)));
-    attr_set = true;
+    NSGPU_HIP(hipFuncSetAttribute((const void *)hold_run_packed, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(HoldPackedLds)));
+    attrs = true;
   }
-  hipLaunchKernelGGL(hold_run, dim3(1), dim3(HOLD_THREADS), sizeof(HoldLds), s, d_dist, n, total, ws_ts, ws_uid,
-                     d_stats, d_log_ts, d_log_uid, log_cap);
+  NSGPU_HIP(hipMemsetAsync(d_stats, 0, sizeof(nsgpu_hold_stats), s));
+  NSGPU_HIP(hipMemsetAsync(ws_flag, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(hold_pack_dist, dim3((n + 255) / 256), dim3(256), 0, s, d_dist, n, ws_d32, ws_flag);
+  hipLaunchKernelGGL(hold_run_packed, dim3(1), dim3(HOLD_THREADS), sizeof(HoldPackedLds), s, ws_d32, n, total,
+                     d_stats, d_log_ts, d_log_uid, log_cap, ws_flag);
+  hipLaunchKernelGGL(hold_init_rank, dim3((n + 255) / 256), dim3(256), 0, s, d_dist, n, ws_ts, ws_uid, ws_flag);
+  hipLaunchKernelGGL(hold_run_wide, dim3(1), dim3(HOLD_THREADS), sizeof(HoldLds), s, d_dist, n, total, ws_ts,
+                     ws_uid, d_stats, d_log_ts, d_log_uid, log_cap, ws_flag);
   NSGPU_HIP(hipGetLastError());
   return NSGPU_OK;
 }

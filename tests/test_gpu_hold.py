@@ -45,3 +45,27 @@ def test_hold_full_size_digest(bench_dist):
     st, _, _ = run_gpu(bench_dist, total)
     assert (st.dispatched, st.holds, st.final_ts, st.next_uid, st.digest) == \
         (res.dispatched, res.holds, res.final_ts, res.next_uid, res.digest)
+
+
+def test_hold_wide_delays():
+    # utils/generate-distributions.pl draws U[0, 1e7) seconds: delays >= 2^31 ns take the wide kernel
+    rng = np.random.default_rng(11)
+    secs = rng.random(300) * 1e7
+    dist = (secs * 1000000000).astype(np.uint64)
+    total = 3000
+    cap = len(dist) + total + 1
+    res, lts, luid = nsref.churn_run(dist, total, log_cap=cap)
+    st, gts, guid = run_gpu(dist, total, log_cap=cap)
+    assert np.array_equal(gts, lts) and np.array_equal(guid, luid)
+    assert st.digest == res.digest and st.next_uid == res.next_uid
+
+
+def test_hold_mixed_boundary():
+    # one delay exactly at the packed limit (2^31 - 1) and one just above it (wide path)
+    for top in ((1 << 31) - 1, 1 << 31):
+        dist = np.array([top, 1, 2, top, 0, 5], dtype=np.uint64)
+        total = 200
+        cap = len(dist) + total + 1
+        res, lts, luid = nsref.churn_run(dist, total, log_cap=cap)
+        st, gts, guid = run_gpu(dist, total, log_cap=cap)
+        assert np.array_equal(gts, lts) and np.array_equal(guid, luid), top
