@@ -108,6 +108,9 @@ typedef struct nsgpu_hold_stats {
 } nsgpu_hold_stats;
 
 int nsgpu_hold_workspace_bytes(uint32_t n, uint64_t *bytes);
+/* Diagnostic: when d_phase_cycles (7 x uint64, device) is non-NULL, later nsgpu_hold_run calls
+ * record per-round-phase s_memtime cycle sums there (NULL turns it off). */
+int nsgpu_hold_set_profile(uint64_t *d_phase_cycles);
 int nsgpu_hold_run(const uint64_t *d_dist, uint32_t n, uint32_t total, nsgpu_hold_stats *d_stats,
                    uint64_t *d_log_ts, uint32_t *d_log_uid, uint64_t log_cap, void *d_workspace, void *stream);
 

@@ -294,7 +294,8 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
                                                                 uint32_t total, nsgpu_hold_stats *__restrict__ stats,
                                                                 uint64_t *__restrict__ log_ts,
                                                                 uint32_t *__restrict__ log_uid, uint64_t log_cap,
-                                                                const uint32_t *__restrict__ wide_flag) {
+                                                                const uint32_t *__restrict__ wide_flag,
+                                                                uint64_t *__restrict__ prof) {
   if (*wide_flag != 0) return;  // some delay >= 2^31 ns: the wide kernel handles it
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   HoldPackedLds &L = *reinterpret_cast<HoldPackedLds *>(smem_raw);
@@ -345,6 +346,14 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
     dnext = dist32[idx];
   }
 
+  uint64_t pacc[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev = prof ? __builtin_amdgcn_s_memtime() : 0;
+#define HSTAMP(i)                                     \
+  if (prof) {                                         \
+    const uint64_t tnow_ = __builtin_amdgcn_s_memtime(); \
+    pacc[i] += tnow_ - tprev;                         \
+    tprev = tnow_;                                    \
+  }
   while (P > 0) {
     const uint32_t B = P < HOLD_BATCH ? P : HOLD_BATCH;
     // ---- A ----
@@ -365,6 +374,7 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
     if (lane == 0) ex = INF;
     if (lane == 63) L.Wmin[wid] = inc;
     __syncthreads();
+    HSTAMP(0)
     uint64_t carry = INF;
     for (int w = 0; w < wid; w++) {
       uint64_t v = L.Wmin[w];
@@ -375,6 +385,7 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
     const unsigned long long bal = __ballot(bad);
     if (lane == 0) L.Wfirst[wid] = bal ? (uint32_t)(wid * 64 + __ffsll((unsigned long long)bal) - 1) : 0xffffffffu;
     __syncthreads();
+    HSTAMP(1)
     uint32_t p = B;
 #pragma unroll
     for (int w = 0; w < HOLD_THREADS / 64; w++) {
@@ -401,6 +412,7 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
       dnext = dist32[idx];
     }
     __syncthreads();
+    HSTAMP(2)
     // ---- D ----
     uint32_t lb = 0;
     if (m > 0) {
@@ -410,7 +422,15 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
         const uint64_t ck = L.Ck[c];
         const uint32_t j0 = (uint32_t)(((uint64_t)sl * m) / nsl), j1 = (uint32_t)(((uint64_t)(sl + 1) * m) / nsl);
         uint32_t cnt = 0;
-        for (uint32_t j = j0; j < j1; j++) cnt += L.Ck[j] < ck;
+        uint32_t j = j0;
+        for (; j + 8 <= j1; j += 8) {  // 8 independent LDS reads in flight
+          uint64_t v[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) v[u] = L.Ck[j + u];
+#pragma unroll
+          for (int u = 0; u < 8; u++) cnt += v[u] < ck;
+        }
+        for (; j < j1; j++) cnt += L.Ck[j] < ck;
         if (cnt) atomicAdd(&L.Rk[c], cnt);
       }
       if (tid < (int)m) {
@@ -425,6 +445,7 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
       }
     }
     __syncthreads();
+    HSTAMP(3)
     // ---- E ----
     const uint32_t R = P - p;                          // survivors
     const uint32_t chunk = (R + HOLD_THREADS - 1) / HOLD_THREADS;
@@ -453,6 +474,7 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
       cval = child;
     }
     __syncthreads();
+    HSTAMP(4)
     uint32_t off = wex;
     for (int w = 0; w < wid; w++) off += L.Wsum[w];
     // ---- F ----
@@ -464,6 +486,7 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
     }
     if (cpos != 0xffffffffu) L.u.m.S[cpos] = cval - rebase;
     __syncthreads();
+    HSTAMP(5)
     base += last_key >> 32;
     final_ts = base;
     K += p;
@@ -474,6 +497,9 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
     max_p = p > max_p ? p : max_p;
   }
 
+#undef HSTAMP
+  if (prof && tid == 0)
+    for (int i = 0; i < 7; i++) prof[i] = pacc[i];
   uint64_t d = digest;
   for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
   if (lane == 0) L.Wmin[wid] = d;
@@ -510,6 +536,13 @@ extern "C" int nsgpu_hold_workspace_bytes(uint32_t n, uint64_t *bytes) {
   return NSGPU_OK;
 }
 
+// Diagnostic: per-phase cycle sums of the packed kernel (wave 0's view, s_memtime), off by default.
+static uint64_t *g_hold_prof = nullptr;
+extern "C" int nsgpu_hold_set_profile(uint64_t *d_phase_cycles) {
+  g_hold_prof = d_phase_cycles;
+  return NSGPU_OK;
+}
+
 // Runs the packed kernel when every delay is < 2^31 ns, else the wide one.  The choice is made
 // on the device (hold_pack_dist sets a flag; the kernel of the other variant exits at once), so
 // a launch never synchronises with the host.
@@ -540,7 +573,7 @@ extern "C" int nsgpu_hold_run(const uint64_t *d_dist, uint32_t n, uint32_t total
   NSGPU_HIP(hipMemsetAsync(ws_flag, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(hold_pack_dist, dim3((n + 255) / 256), dim3(256), 0, s, d_dist, n, ws_d32, ws_flag);
   hipLaunchKernelGGL(hold_run_packed, dim3(1), dim3(HOLD_THREADS), sizeof(HoldPackedLds), s, ws_d32, n, total,
-                     d_stats, d_log_ts, d_log_uid, log_cap, ws_flag);
+                     d_stats, d_log_ts, d_log_uid, log_cap, ws_flag, g_hold_prof);
   hipLaunchKernelGGL(hold_init_rank, dim3((n + 255) / 256), dim3(256), 0, s, d_dist, n, ws_ts, ws_uid, ws_flag);
   hipLaunchKernelGGL(hold_run_wide, dim3(1), dim3(HOLD_THREADS), sizeof(HoldLds), s, d_dist, n, total, ws_ts,
                      ws_uid, d_stats, d_log_ts, d_log_uid, log_cap, ws_flag);

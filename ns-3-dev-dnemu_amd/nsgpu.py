@@ -67,6 +67,7 @@ SIGNATURES = {
                                         _i32, _vp, _vp, _vp, _vp, _vp]),
     "nsgpu_fanout_workspace_bytes": (C.c_int, [_i64, _i64, C.POINTER(C.c_uint64)]),
     "nsgpu_hold_workspace_bytes": (C.c_int, [_u32, C.POINTER(C.c_uint64)]),
+    "nsgpu_hold_set_profile": (C.c_int, [_vp]),
     "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
 }
 
