@@ -114,6 +114,24 @@ int nsgpu_hold_set_profile(uint64_t *d_phase_cycles);
 int nsgpu_hold_run(const uint64_t *d_dist, uint32_t n, uint32_t total, nsgpu_hold_stats *d_stats,
                    uint64_t *d_log_ts, uint32_t *d_log_uid, uint64_t log_cap, void *d_workspace, void *stream);
 
+/* ---------------- GPU-resident point-to-point subset (configs 2, 4) ----------------
+ * Replaces, for a topology of PointToPointNetDevices, the handler chain
+ *   PointToPointNetDevice::{Send,TransmitStart,TransmitComplete,Receive} (point-to-point-net-device.cc:206-346,462-518)
+ *   PointToPointChannel::TransmitStart (point-to-point-channel.cc:82-103)
+ *   Queue/DropTailQueue::{Enqueue,Dequeue,Drop} (queue.cc:61-200, drop-tail-queue.cc:83-132)
+ *   Ipv4L3Protocol::{Receive,IpForward} with static next-hop routes (ipv4-l3-protocol.cc:434-537,815-841)
+ *   UdpL4Protocol::Receive -> PacketSink, OnOffApplication (onoff-application.cc:132-252)
+ * and the DefaultSimulatorImpl run loop over them, entirely on the device.  nsgpu_p2p_reset
+ * loads the post-setup state; nsgpu_p2p_run runs Simulator::Run to the Stop event (async). */
+typedef struct nsgpu_p2p nsgpu_p2p;
+int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap, uint64_t log_cap, nsgpu_p2p **out);
+int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream);
+int nsgpu_p2p_run(nsgpu_p2p *h, void *stream);
+int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc, nsgpu_app_counters *appc,
+                      uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_n, uint32_t *error,
+                      void *stream);
+int nsgpu_p2p_destroy(nsgpu_p2p *h);
+
 #ifdef __cplusplus
 }
 #endif

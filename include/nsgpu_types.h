@@ -72,6 +72,84 @@ typedef struct nsgpu_rx_record {
   double rx_dbm;     /* CalcRxPower (txPowerDbm, sender, receiver) */
 } nsgpu_rx_record;
 
+/* ---------------- point-to-point scenario (GPU-resident p2p / DropTail / IPv4 / UDP subset) ----------------
+ * A topology of PointToPointNetDevices joined by PointToPointChannels, IPv4 forwarding by static
+ * next-hop tables, OnOff (UDP, constant on/off times) sources and PacketSink sinks.  All arrays are
+ * host pointers; devices and applications are listed in ns-3 creation order (Node::AddDevice /
+ * Node::AddApplication), which fixes the setup-time uids (node-list.cc:124-131, node.cc:111-145). */
+enum nsgpu_app_kind { NSGPU_APP_ONOFF = 0, NSGPU_APP_SINK = 1 };
+
+typedef struct nsgpu_p2p_scenario {
+  uint32_t n_nodes;
+  uint32_t n_devices;
+  uint32_t n_apps;
+  uint32_t n_dst;              /* columns of the route table (destination slots) */
+  /* devices (PointToPointNetDevice + DropTailQueue), index = creation order */
+  const uint32_t *dev_node;    /* owning node */
+  const uint32_t *dev_peer;    /* device at the other end of the channel */
+  const uint64_t *dev_bps;     /* DataRate (bit/s), point-to-point-net-device.cc:57 */
+  const int64_t  *dev_ifg_ns;  /* InterframeGap */
+  const int64_t  *dev_delay_ns;/* PointToPointChannel Delay of the device's channel */
+  const uint32_t *dev_qmax;    /* DropTailQueue MaxPackets (PACKETS mode), drop-tail-queue.cc:37-43 */
+  /* IPv4 static routing: route[node * n_dst + slot] = output device, or 0xffffffff = no route */
+  const uint32_t *route;
+  /* applications in AddApplication order */
+  const uint32_t *app_kind;    /* nsgpu_app_kind */
+  const uint32_t *app_node;
+  const int64_t  *app_start_ns;
+  const int64_t  *app_stop_ns; /* 0 = never (application.cc:90-93) */
+  /* OnOff parameters (ignored for sinks), onoff-application.cc:47-86 */
+  const uint32_t *app_dst_node;
+  const uint32_t *app_dst_slot;
+  const uint64_t *app_rate_bps;
+  const uint32_t *app_pkt_size;
+  const double   *app_on_s;    /* ConstantVariable OnTime (seconds; converted by Seconds () at each use) */
+  const double   *app_off_s;   /* ConstantVariable OffTime */
+  const uint32_t *app_max_bytes;
+  const uint32_t *app_ttl;     /* IP TTL of the flow's packets */
+  int64_t stop_ns;             /* Simulator::Stop (Seconds (x)) from main, as ns */
+  /* Setup-time Schedule calls in program order (they fix every later uid):
+   *   NSGPU_SETUP_NODE k   NodeListPriv::Add      -> ScheduleWithContext (k, 0, &Node::Start)
+   *   NSGPU_SETUP_DEVICE d Node::AddDevice        -> ScheduleWithContext (node, 0, &NetDevice::Start)
+   *   NSGPU_SETUP_APP a    Node::AddApplication   -> ScheduleWithContext (node, 0, &Application::Start)
+   *   NSGPU_SETUP_STOP     Simulator::Stop (t)    -> Schedule (t, &Simulator::Stop), context 0xffffffff
+   *   NSGPU_SETUP_UID      any other setup call that consumes one uid without a dispatched event */
+  uint32_t n_setup;
+  uint32_t pad_;
+  const uint32_t *setup_kind;
+  const uint32_t *setup_index;
+} nsgpu_p2p_scenario;
+
+enum nsgpu_setup_kind { NSGPU_SETUP_NODE = 0, NSGPU_SETUP_DEVICE = 1, NSGPU_SETUP_APP = 2, NSGPU_SETUP_STOP = 3,
+                        NSGPU_SETUP_UID = 4 };
+
+/* Counters of a p2p run (both the oracle and the GPU engine fill this). */
+typedef struct nsgpu_p2p_stats {
+  uint64_t dispatched;        /* RemoveNext calls, setup and cancelled ones included */
+  uint64_t cancelled;         /* dispatches of cancelled events */
+  uint64_t digest;            /* order-sensitive digest of the (ts, uid) pop order */
+  uint64_t final_ts;          /* Now () when Run returned */
+  uint32_t next_uid;          /* DefaultSimulatorImpl::m_uid when Run returned */
+  uint32_t windows;           /* GPU: parallel dispatch windows (0 for the oracle) */
+  uint64_t ttl_drops;
+  uint64_t no_route_drops;
+  uint64_t max_window;
+} nsgpu_p2p_stats;
+
+/* Per-device counters: Queue (queue.cc:61-200) + device. */
+typedef struct nsgpu_dev_counters {
+  uint32_t enq_packets, enq_bytes;     /* m_nTotalReceivedPackets/Bytes */
+  uint32_t drop_packets, drop_bytes;   /* m_nTotalDroppedPackets/Bytes */
+  uint32_t deq_packets, tx_packets;    /* Dequeue calls returning a packet; TransmitStart calls */
+  uint32_t rx_packets, pad_;           /* PointToPointNetDevice::Receive calls */
+} nsgpu_dev_counters;
+
+/* Per-application counters: OnOff sent packets/bytes, PacketSink received packets/bytes. */
+typedef struct nsgpu_app_counters {
+  uint32_t tx_packets, rx_packets;
+  uint64_t tx_bytes, rx_bytes;
+} nsgpu_app_counters;
+
 /* Order-sensitive digest of a dispatch sequence: sum over k of mix(k, ts_k, uid_k).
  * Used to compare long dispatch orders (pop order) without moving whole logs. */
 NSGPU_HD static inline uint64_t nsgpu_mix64(uint64_t z) {

@@ -68,6 +68,11 @@ SIGNATURES = {
     "nsgpu_fanout_workspace_bytes": (C.c_int, [_i64, _i64, C.POINTER(C.c_uint64)]),
     "nsgpu_hold_workspace_bytes": (C.c_int, [_u32, C.POINTER(C.c_uint64)]),
     "nsgpu_hold_set_profile": (C.c_int, [_vp]),
+    "nsgpu_p2p_create": (C.c_int, [_vp, _u64, _u64, C.POINTER(C.c_void_p)]),
+    "nsgpu_p2p_reset": (C.c_int, [_vp, _vp]),
+    "nsgpu_p2p_run": (C.c_int, [_vp, _vp]),
+    "nsgpu_p2p_results": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
+    "nsgpu_p2p_destroy": (C.c_int, [_vp]),
     "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
 }
 

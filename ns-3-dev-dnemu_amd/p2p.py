@@ -1,0 +1,300 @@
+"""Point-to-point scenarios for the GPU-resident p2p subset (include/nsgpu_types.h: nsgpu_p2p_scenario).
+
+Host-side plumbing only: builds the plain arrays ns-3's helpers would produce (creation order of
+nodes, devices and applications, which fixes the setup-time uids) and drives the C-ABI
+(nsgpu_p2p_*).  No simulation logic lives here.
+
+Builders mirror the reference helpers:
+  * grid(): PointToPointGridHelper (src/point-to-point-layout/model/point-to-point-grid.cc:33-72):
+    node (y, x) is created row by row; after each node its row link (x-1 -> x) then its column link
+    ((y-1, x) -> (y, x)) are installed with PointToPointHelper::Install (point-to-point-helper.cc:228-242),
+    which adds device A then device B.
+  * Routes are harness-computed static next-hop tables (global routing is infeasible at
+    128x128 on the reference CPU): XY routing on grids, BFS shortest paths otherwise.
+"""
+import ctypes as C
+from collections import deque
+
+import numpy as np
+
+import nsgpu
+
+APP_ONOFF, APP_SINK = 0, 1
+SETUP_NODE, SETUP_DEVICE, SETUP_APP, SETUP_STOP, SETUP_UID = 0, 1, 2, 3, 4
+NO_ROUTE = 0xFFFFFFFF
+
+
+class ScenarioStruct(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint32), ("n_devices", C.c_uint32), ("n_apps", C.c_uint32), ("n_dst", C.c_uint32),
+        ("dev_node", C.c_void_p), ("dev_peer", C.c_void_p), ("dev_bps", C.c_void_p), ("dev_ifg_ns", C.c_void_p),
+        ("dev_delay_ns", C.c_void_p), ("dev_qmax", C.c_void_p), ("route", C.c_void_p),
+        ("app_kind", C.c_void_p), ("app_node", C.c_void_p), ("app_start_ns", C.c_void_p),
+        ("app_stop_ns", C.c_void_p), ("app_dst_node", C.c_void_p), ("app_dst_slot", C.c_void_p),
+        ("app_rate_bps", C.c_void_p), ("app_pkt_size", C.c_void_p), ("app_on_s", C.c_void_p),
+        ("app_off_s", C.c_void_p), ("app_max_bytes", C.c_void_p), ("app_ttl", C.c_void_p),
+        ("stop_ns", C.c_int64), ("n_setup", C.c_uint32), ("pad_", C.c_uint32),
+        ("setup_kind", C.c_void_p), ("setup_index", C.c_void_p),
+    ]
+
+
+class P2PStats(C.Structure):
+    _fields_ = [("dispatched", C.c_uint64), ("cancelled", C.c_uint64), ("digest", C.c_uint64),
+                ("final_ts", C.c_uint64), ("next_uid", C.c_uint32), ("windows", C.c_uint32),
+                ("ttl_drops", C.c_uint64), ("no_route_drops", C.c_uint64), ("max_window", C.c_uint64)]
+
+
+DEV_COUNTERS_DTYPE = np.dtype([("enq_packets", "<u4"), ("enq_bytes", "<u4"), ("drop_packets", "<u4"),
+                               ("drop_bytes", "<u4"), ("deq_packets", "<u4"), ("tx_packets", "<u4"),
+                               ("rx_packets", "<u4"), ("pad_", "<u4")])
+APP_COUNTERS_DTYPE = np.dtype([("tx_packets", "<u4"), ("rx_packets", "<u4"), ("tx_bytes", "<u8"),
+                               ("rx_bytes", "<u8")])
+
+
+class Scenario:
+    """Arrays of a nsgpu_p2p_scenario plus the order of setup-time Schedule calls."""
+
+    def __init__(self, n_nodes):
+        self.n_nodes = n_nodes
+        self.dev = []     # (node, peer, bps, ifg, delay, qmax)
+        self.apps = []    # dicts
+        self.setup = []   # (kind, index)
+        self.stop_ns = -1
+        for n in range(n_nodes):
+            self.setup.append((SETUP_NODE, n))
+        self.route = None
+        self.n_dst = 0
+        self.dst_slot = {}
+
+    # PointToPointHelper::Install (a, b): device on a, then device on b, one channel
+    def link(self, a, b, bps, delay_ns, qmax=100, ifg_ns=0):
+        da, db = len(self.dev), len(self.dev) + 1
+        self.dev.append([a, db, bps, ifg_ns, delay_ns, qmax])
+        self.setup.append((SETUP_DEVICE, da))
+        self.dev.append([b, da, bps, ifg_ns, delay_ns, qmax])
+        self.setup.append((SETUP_DEVICE, db))
+        return da, db
+
+    def add_sink(self, node, start_ns, stop_ns):
+        self.apps.append(dict(kind=APP_SINK, node=node, start=start_ns, stop=stop_ns, dst=0, rate=0, size=0,
+                              on=0.0, off=0.0, maxb=0, ttl=0))
+        self.setup.append((SETUP_APP, len(self.apps) - 1))
+        return len(self.apps) - 1
+
+    def add_onoff(self, node, dst, start_ns, stop_ns, rate_bps=500000, size=512, on_s=1.0, off_s=1.0,
+                  max_bytes=0, ttl=64):
+        self.apps.append(dict(kind=APP_ONOFF, node=node, start=start_ns, stop=stop_ns, dst=dst, rate=rate_bps,
+                              size=size, on=on_s, off=off_s, maxb=max_bytes, ttl=ttl))
+        self.setup.append((SETUP_APP, len(self.apps) - 1))
+        return len(self.apps) - 1
+
+    def stop(self, t_ns):  # Simulator::Stop (t)
+        self.stop_ns = t_ns
+        self.setup.append((SETUP_STOP, 0))
+
+    # ---------------- routing ----------------
+    def _neighbors(self):
+        nb = [[] for _ in range(self.n_nodes)]
+        for d, (node, peer, *_r) in enumerate(self.dev):
+            nb[node].append((self.dev[peer][0], d))
+        return nb
+
+    def route_bfs(self):
+        """Static next-hop table towards every OnOff destination (BFS shortest paths, lowest device first)."""
+        dsts = sorted({a["dst"] for a in self.apps if a["kind"] == APP_ONOFF})
+        self.dst_slot = {d: i for i, d in enumerate(dsts)}
+        self.n_dst = max(1, len(dsts))
+        nb = self._neighbors()
+        R = np.full((self.n_nodes, self.n_dst), NO_ROUTE, dtype=np.uint32)
+        for dst, slot in self.dst_slot.items():
+            dist = np.full(self.n_nodes, -1, dtype=np.int64)
+            dist[dst] = 0
+            q = deque([dst])
+            while q:
+                u = q.popleft()
+                for v, _d in nb[u]:
+                    if dist[v] < 0:
+                        dist[v] = dist[u] + 1
+                        q.append(v)
+            for n in range(self.n_nodes):
+                if n == dst or dist[n] < 0:
+                    continue
+                best = None
+                for v, d in sorted(nb[n], key=lambda t: t[1]):
+                    if dist[v] == dist[n] - 1:
+                        best = d
+                        break
+                R[n, slot] = best
+        self.route = R
+
+    # ---------------- C view ----------------
+    def c_struct(self):
+        dev = np.array(self.dev, dtype=np.int64).reshape(-1, 6) if self.dev else np.zeros((0, 6), np.int64)
+        A = self.apps
+        arrays = dict(
+            dev_node=dev[:, 0].astype(np.uint32), dev_peer=dev[:, 1].astype(np.uint32),
+            dev_bps=dev[:, 2].astype(np.uint64), dev_ifg_ns=dev[:, 3].astype(np.int64),
+            dev_delay_ns=dev[:, 4].astype(np.int64), dev_qmax=dev[:, 5].astype(np.uint32),
+            route=np.ascontiguousarray(self.route, dtype=np.uint32),
+            app_kind=np.array([a["kind"] for a in A], np.uint32),
+            app_node=np.array([a["node"] for a in A], np.uint32),
+            app_start_ns=np.array([a["start"] for a in A], np.int64),
+            app_stop_ns=np.array([a["stop"] for a in A], np.int64),
+            app_dst_node=np.array([a["dst"] for a in A], np.uint32),
+            app_dst_slot=np.array([self.dst_slot.get(a["dst"], 0) if a["kind"] == APP_ONOFF else 0 for a in A],
+                                  np.uint32),
+            app_rate_bps=np.array([a["rate"] for a in A], np.uint64),
+            app_pkt_size=np.array([a["size"] for a in A], np.uint32),
+            app_on_s=np.array([a["on"] for a in A], np.float64),
+            app_off_s=np.array([a["off"] for a in A], np.float64),
+            app_max_bytes=np.array([a["maxb"] for a in A], np.uint32),
+            app_ttl=np.array([a["ttl"] for a in A], np.uint32),
+            setup_kind=np.array([k for k, _ in self.setup], np.uint32),
+            setup_index=np.array([i for _, i in self.setup], np.uint32),
+        )
+        s = ScenarioStruct()
+        s.n_nodes, s.n_devices, s.n_apps, s.n_dst = self.n_nodes, len(self.dev), len(A), self.n_dst
+        for k, v in arrays.items():
+            setattr(s, k, v.ctypes.data if v.size else None)
+        s.stop_ns = self.stop_ns
+        s.n_setup = len(self.setup)
+        s._keep = arrays  # keep the arrays alive with the struct
+        return s
+
+
+def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="columns", start_ns=100_000_000,
+         stop_ns=2_000_000_000, sim_stop_ns=2_100_000_000, rate_bps=500_000, size=512, on_s=1e9, off_s=0.0,
+         ttl=255, n_flows=None):
+    """PointToPointGridHelper topology (point-to-point-grid.cc:33-72) with OnOff/PacketSink flows.
+
+    flows="columns": one flow per column from row 0 to the last row;
+    routes are XY (row first, then column) static next hops."""
+    sc = Scenario(0)
+    sc.setup = []
+    nid = lambda y, x: y * cols + x  # noqa: E731
+    row_dev = {}
+    col_dev = {}
+    for y in range(rows):
+        for x in range(cols):
+            sc.setup.append((SETUP_NODE, nid(y, x)))  # rowNodes.Create (1)
+            sc.n_nodes += 1
+            if x > 0:
+                da, db = sc.link(nid(y, x - 1), nid(y, x), bps, delay_ns, qmax)
+                row_dev[(nid(y, x - 1), nid(y, x))] = da
+                row_dev[(nid(y, x), nid(y, x - 1))] = db
+            if y > 0:
+                da, db = sc.link(nid(y - 1, x), nid(y, x), bps, delay_ns, qmax)
+                col_dev[(nid(y - 1, x), nid(y, x))] = da
+                col_dev[(nid(y, x), nid(y - 1, x))] = db
+    fl = []
+    if flows == "columns":
+        ncol = cols if n_flows is None else min(cols, n_flows)
+        fl = [(nid(0, x), nid(rows - 1, x)) for x in range(ncol)]
+    else:
+        fl = list(flows)
+    # sinks first (PacketSinkHelper.Install), then the OnOff sources
+    sinks = {}
+    for _s, d in fl:
+        if d not in sinks:
+            sinks[d] = sc.add_sink(d, 0, 0)
+    for s_, d in fl:
+        sc.add_onoff(s_, d, start_ns, stop_ns, rate_bps=rate_bps, size=size, on_s=on_s, off_s=off_s, ttl=ttl)
+    sc.stop(sim_stop_ns)
+    # XY routes towards each destination
+    dsts = sorted({d for _s, d in fl})
+    sc.dst_slot = {d: i for i, d in enumerate(dsts)}
+    sc.n_dst = max(1, len(dsts))
+    R = np.full((sc.n_nodes, sc.n_dst), NO_ROUTE, dtype=np.uint32)
+    ys, xs = np.divmod(np.arange(sc.n_nodes), cols)
+    for d, slot in sc.dst_slot.items():
+        yd, xd = divmod(d, cols)
+        for n in range(sc.n_nodes):
+            y, x = ys[n], xs[n]
+            if n == d:
+                continue
+            if x != xd:
+                nxt = nid(y, x + (1 if xd > x else -1))
+                R[n, slot] = row_dev[(n, nxt)]
+            else:
+                nxt = nid(y + (1 if yd > y else -1), x)
+                R[n, slot] = col_dev[(n, nxt)]
+    sc.route = R
+    return sc
+
+
+def random_topology(n_nodes, n_links, n_flows, seed, bps_choices=(1_000_000, 5_000_000, 10_000_000),
+                    delay_choices=(100_000, 1_000_000, 2_000_000), qmax=20, stop_ns=1_000_000_000):
+    """Connected random topology with OnOff flows (on/off cycling, max bytes) for parity tests."""
+    rng = np.random.default_rng(seed)
+    sc = Scenario(n_nodes)
+    edges = set()
+    for n in range(1, n_nodes):  # spanning tree
+        m = int(rng.integers(0, n))
+        edges.add((m, n))
+    while len(edges) < n_links:
+        a, b = sorted(rng.choice(n_nodes, 2, replace=False).tolist())
+        edges.add((a, b))
+    for a, b in sorted(edges):
+        sc.link(a, b, int(rng.choice(bps_choices)), int(rng.choice(delay_choices)), qmax)
+    flows = []
+    for _ in range(n_flows):
+        s_, d = rng.choice(n_nodes, 2, replace=False).tolist()
+        flows.append((s_, d))
+    sinks = {}
+    for _s, d in flows:
+        if d not in sinks:
+            sinks[d] = sc.add_sink(d, int(rng.integers(0, 50_000_000)), 0)
+    for s_, d in flows:
+        st = int(rng.integers(50_000_000, 300_000_000))
+        sc.add_onoff(s_, d, st, int(st + rng.integers(200_000_000, 600_000_000)),
+                     rate_bps=int(rng.choice([200_000, 500_000, 2_000_000])), size=int(rng.choice([64, 512, 1000])),
+                     on_s=float(rng.choice([0.05, 0.1, 1.0])), off_s=float(rng.choice([0.0, 0.02, 0.05])),
+                     max_bytes=int(rng.choice([0, 0, 20000])), ttl=64)
+    sc.stop(stop_ns)
+    sc.route_bfs()
+    return sc
+
+
+class Engine:
+    """The GPU engine for one scenario (nsgpu_p2p_create / reset / run / results)."""
+
+    def __init__(self, scenario, log_cap=0, pool_cap=0, stream=None):
+        self.s = scenario.c_struct()
+        self.stream = stream
+        self.log_cap = log_cap
+        h = C.c_void_p()
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_create(C.byref(self.s), pool_cap, log_cap, C.byref(h)))
+        self.h = h.value
+
+    def reset(self):
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_reset(self.h, self.stream))
+
+    def launch(self):
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_run(self.h, self.stream))
+
+    def results(self, log_n=0):
+        st = P2PStats()
+        devc = np.zeros(self.s.n_devices, DEV_COUNTERS_DTYPE)
+        appc = np.zeros(self.s.n_apps, APP_COUNTERS_DTYPE)
+        log_n = min(log_n, self.log_cap)
+        lts = np.zeros(log_n, np.uint64)
+        luid = np.zeros(log_n, np.uint32)
+        lctx = np.zeros(log_n, np.uint32)
+        err = C.c_uint32()
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_results(self.h, C.byref(st), devc.ctypes.data, appc.ctypes.data,
+                                                  lts.ctypes.data if log_n else None,
+                                                  luid.ctypes.data if log_n else None,
+                                                  lctx.ctypes.data if log_n else None, log_n, C.byref(err),
+                                                  self.stream))
+        return st, devc, appc, (lts, luid, lctx)
+
+    def run(self, log_n=0):
+        self.reset()
+        self.launch()
+        return self.results(log_n)
+
+    def __del__(self):
+        try:
+            nsgpu.lib().nsgpu_p2p_destroy(self.h)
+        except Exception:
+            pass

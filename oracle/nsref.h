@@ -112,6 +112,13 @@ typedef struct nsref_churn_result {
 int nsref_churn_run(const uint64_t *dist_ns, uint32_t n, uint32_t total, int scheduler,
                     uint64_t *log_ts, uint32_t *log_uid, uint64_t log_cap, nsref_churn_result *out);
 
+/* ---------------- point-to-point subset (configs 2, 4, 5) ----------------
+ * Sequential run of a nsgpu_p2p_scenario (see nsref_p2p.cc for the restated reference code).
+ * devc/appc (optional) receive n_devices / n_apps counters; the optional log receives the pop order. */
+int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
+                  nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
+                  uint64_t log_cap, double *run_seconds);
+
 /* bench-simulator ReadDistribution: (uint64_t)(data * 1000000000)  (bench-simulator.cc:66) */
 uint64_t nsref_distribution_ns(double seconds);
 

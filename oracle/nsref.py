@@ -129,6 +129,9 @@ def lib():
         L.nsref_churn_run.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_void_p,
                                       C.c_uint64, C.POINTER(ChurnResult)]
         L.nsref_churn_run.restype = C.c_int
+        L.nsref_p2p_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_uint64, C.c_void_p]
+        L.nsref_p2p_run.restype = C.c_int
         L.nsref_distribution_ns.argtypes = [C.c_double]
         L.nsref_distribution_ns.restype = C.c_uint64
         _lib = L
@@ -337,3 +340,18 @@ class Sim:
             self.close()
         except Exception:
             pass
+
+
+def p2p_run(scenario_struct, stats_struct, devc, appc, log_cap=0):
+    """Sequential oracle run of a nsgpu_p2p_scenario (ctypes struct built by the caller).
+
+    devc / appc: numpy structured arrays (n_devices / n_apps) filled in place.
+    Returns (run_seconds, (log_ts, log_uid, log_ctx))."""
+    secs = C.c_double()
+    lts = np.zeros(log_cap, np.uint64)
+    luid = np.zeros(log_cap, np.uint32)
+    lctx = np.zeros(log_cap, np.uint32)
+    lib().nsref_p2p_run(C.byref(scenario_struct), C.byref(stats_struct), devc.ctypes.data, appc.ctypes.data,
+                        lts.ctypes.data if log_cap else None, luid.ctypes.data if log_cap else None,
+                        lctx.ctypes.data if log_cap else None, log_cap, C.byref(secs))
+    return secs.value, (lts, luid, lctx)

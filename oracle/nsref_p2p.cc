@@ -1,0 +1,313 @@
+// nsref_p2p.cc — CPU ORACLE (test infrastructure only; see nsref.h header).
+// Sequential restatement of the point-to-point / DropTail / IPv4-forward / UDP handler chain and of
+// the OnOff + PacketSink applications, driven by the restated DefaultSimulatorImpl + MapScheduler.
+// Every Schedule* call is made in the same order as the reference code makes it, so uids,
+// timestamps and the pop order follow the reference:
+//   setup:     NodeListPriv::Add (node-list.cc:124-131), Node::AddDevice (node.cc:111-123),
+//              Node::AddApplication (node.cc:137-145), Node::DoStart (node.cc:183-199),
+//              Application::DoStart (application.cc:87-95)
+//   OnOff:     onoff-application.cc:132-252 (StartApplication, CancelEvents, StartSending, StopSending,
+//              ScheduleNextTx, ScheduleStartEvent, ScheduleStopEvent, SendPacket)
+//   device:    point-to-point-net-device.cc:206-269 (TransmitStart, TransmitComplete), :304-346 (Receive),
+//              :462-518 (Send); point-to-point-channel.cc:82-103 (TransmitStart)
+//   queue:     queue.cc:61-200, drop-tail-queue.cc:83-132
+//   IPv4:      ipv4-l3-protocol.cc:434-537 (Receive), :815-841 (IpForward: TTL), static next-hop routing
+//   UDP/sink:  udp-l4-protocol.cc:312-407 -> udp-socket-impl.cc:864-905 -> PacketSink (no events)
+// Packet sizes: payload + 8 (UDP) + 20 (IPv4) + 2 (PPP, added in PointToPointNetDevice::Send).
+#include <vector>
+#include <deque>
+#include <chrono>
+#include <string.h>
+#include <stdio.h>
+#include "nsref_engine.hpp"
+
+namespace {
+
+struct Pkt {
+  uint32_t app;   // sending OnOff
+  uint32_t seq;
+  uint32_t size;  // current size in bytes (headers included as they are added)
+  uint32_t ttl;
+};
+
+struct Model;
+
+struct Dev {
+  bool busy = false;  // m_txMachineState == BUSY
+  Pkt cur{};
+  std::deque<Pkt> q;  // DropTailQueue::m_packets
+  nsgpu_dev_counters c{};
+};
+
+struct App {
+  bool started = false;  // Object::m_started
+  bool sink_active = false;
+  nsgpu_event_id sendEvent{0, 0, 0, 0};       // OnOffApplication::m_sendEvent
+  nsgpu_event_id startStopEvent{0, 0, 0, 0};  // m_startStopEvent
+  uint64_t lastStartTime = 0;
+  uint32_t residualBits = 0;
+  uint32_t totBytes = 0;
+  uint32_t seq = 0;
+  nsgpu_app_counters c{};
+};
+
+struct Model {
+  nsref_sim sim{NSREF_SCHED_MAP};
+  nsgpu_p2p_scenario s;
+  std::vector<Dev> dev;
+  std::vector<App> app;
+  std::vector<std::vector<uint32_t>> node_apps;
+  std::vector<int32_t> sink_of_node;
+  uint64_t ttl_drops = 0, no_route_drops = 0;
+
+  template <class F>
+  struct Ev : EventImpl {
+    F f;
+    explicit Ev(F x) : f(x) {}
+    void Notify() override { f(); }
+  };
+  template <class F>
+  nsgpu_event_id schedule(int64_t delay, F f) { return sim.Schedule(delay, new Ev<F>(f)); }
+  template <class F>
+  void schedule_ctx(uint32_t ctx, int64_t delay, F f) { sim.ScheduleWithContext(ctx, delay, new Ev<F>(f)); }
+  bool running(const nsgpu_event_id &id) { return !sim.IsExpired(id); }  // EventId::IsRunning
+  void cancel(const nsgpu_event_id &id) { sim.Cancel(id); }
+
+  // ---------------- Queue / DropTailQueue ----------------
+  bool enqueue(uint32_t d, const Pkt &p) {  // Queue::Enqueue -> DropTailQueue::DoEnqueue
+    Dev &D = dev[d];
+    if (D.q.size() >= s.dev_qmax[d]) {  // Drop (p): m_nTotalDroppedPackets++, bytes
+      D.c.drop_packets++;
+      D.c.drop_bytes += p.size;
+      return false;
+    }
+    D.q.push_back(p);
+    D.c.enq_packets++;
+    D.c.enq_bytes += p.size;
+    return true;
+  }
+  bool dequeue(uint32_t d, Pkt &out) {
+    Dev &D = dev[d];
+    if (D.q.empty()) return false;
+    out = D.q.front();
+    D.q.pop_front();
+    D.c.deq_packets++;
+    return true;
+  }
+
+  // ---------------- PointToPointNetDevice / PointToPointChannel ----------------
+  void transmit_start(uint32_t d, const Pkt &p) {  // point-to-point-net-device.cc:206-234
+    Dev &D = dev[d];
+    D.busy = true;
+    D.cur = p;
+    D.c.tx_packets++;
+    // Time txTime = Seconds (m_bps.CalculateTxTime (p->GetSize ())) (data-rate.cc:224-227)
+    const double tx_s = static_cast<double>(p.size) * 8 / s.dev_bps[d];
+    const int64_t txTime = nsref_seconds(tx_s);
+    const int64_t txCompleteTime = txTime + s.dev_ifg_ns[d];
+    schedule(txCompleteTime, [this, d]() { transmit_complete(d); });
+    // PointToPointChannel::TransmitStart (point-to-point-channel.cc:82-103)
+    const uint32_t peer = s.dev_peer[d];
+    schedule_ctx(s.dev_node[peer], txTime + s.dev_delay_ns[d], [this, peer, p]() { receive(peer, p); });
+  }
+  void transmit_complete(uint32_t d) {  // :236-269
+    Dev &D = dev[d];
+    D.busy = false;
+    Pkt p;
+    if (!dequeue(d, p)) return;
+    transmit_start(d, p);
+  }
+  void device_send(uint32_t d, Pkt p) {  // :462-518
+    p.size += 2;  // AddHeader (PppHeader)
+    Dev &D = dev[d];
+    if (!D.busy) {
+      if (enqueue(d, p)) {
+        Pkt q;
+        dequeue(d, q);
+        transmit_start(d, q);
+      }
+      // else MacTxDrop: counted by the queue's drop counters
+    } else {
+      enqueue(d, p);
+    }
+  }
+  void receive(uint32_t d, Pkt p) {  // :304-346 (no error model)
+    dev[d].c.rx_packets++;
+    p.size -= 2;  // ProcessHeader strips the PPP header
+    ip_receive(s.dev_node[d], p);
+  }
+
+  // ---------------- IPv4 + UDP ----------------
+  void ip_receive(uint32_t n, Pkt p) {  // Ipv4L3Protocol::Receive -> RouteInput
+    const uint32_t a = p.app;
+    if (s.app_dst_node[a] == n) {  // LocalDeliver -> UdpL4Protocol::Receive -> PacketSink::HandleRead
+      const int32_t k = sink_of_node[n];
+      if (k >= 0 && app[k].sink_active) {
+        app[k].c.rx_packets++;
+        app[k].c.rx_bytes += p.size - 28;
+      }
+      return;
+    }
+    const uint32_t out = s.route[(uint64_t)n * s.n_dst + s.app_dst_slot[a]];
+    if (out == 0xffffffffu) {  // DROP_NO_ROUTE
+      no_route_drops++;
+      return;
+    }
+    // IpForward (ipv4-l3-protocol.cc:815-841)
+    p.ttl -= 1;
+    if (p.ttl == 0) {  // DROP_TTL_EXPIRED (scenarios keep paths shorter than the TTL: no ICMP)
+      ttl_drops++;
+      return;
+    }
+    device_send(out, p);
+  }
+  void ip_send(uint32_t n, const Pkt &p) {  // UdpSocketImpl::Send -> Ipv4L3Protocol::Send (RouteOutput)
+    const uint32_t out = s.route[(uint64_t)n * s.n_dst + s.app_dst_slot[p.app]];
+    if (out == 0xffffffffu) {
+      no_route_drops++;
+      return;
+    }
+    device_send(out, p);
+  }
+
+  // ---------------- OnOffApplication ----------------
+  void cancel_events(uint32_t a) {  // :165-178
+    App &A = app[a];
+    if (running(A.sendEvent)) {
+      const int64_t delta = (int64_t)sim.m_currentTs - (int64_t)A.lastStartTime;
+      uint64_t d[2], inv[2], t[2], r[2], b[2];
+      nsref_i64x64_from_int(delta, d);
+      nsref_i64x64_invert(1000000000ull, inv);
+      nsref_i64x64_mul_by_invert(d, inv, t);  // delta.To (Time::S)
+      nsref_i64x64_from_parts((int64_t)s.app_rate_bps[a], 0, r);
+      nsref_i64x64_mul(t, r, b);  // * m_cbrRate.GetBitRate ()
+      A.residualBits += (uint32_t)nsref_i64x64_get_high(b);
+    }
+    cancel(A.sendEvent);
+    cancel(A.startStopEvent);
+  }
+  void schedule_start_event(uint32_t a) {  // :209-215
+    app[a].startStopEvent = schedule(nsref_seconds(s.app_off_s[a]), [this, a]() { start_sending(a); });
+  }
+  void schedule_stop_event(uint32_t a) {  // :217-223
+    app[a].startStopEvent = schedule(nsref_seconds(s.app_on_s[a]), [this, a]() { stop_sending(a); });
+  }
+  void schedule_next_tx(uint32_t a) {  // :193-207
+    App &A = app[a];
+    if (s.app_max_bytes[a] == 0 || A.totBytes < s.app_max_bytes[a]) {
+      const uint32_t bits = s.app_pkt_size[a] * 8 - A.residualBits;
+      const int64_t nextTime = nsref_seconds(bits / static_cast<double>(s.app_rate_bps[a]));
+      A.sendEvent = schedule(nextTime, [this, a]() { send_packet(a); });
+    } else {
+      stop_application(a);
+    }
+  }
+  void start_sending(uint32_t a) {  // :180-185
+    app[a].lastStartTime = sim.m_currentTs;
+    schedule_next_tx(a);
+    schedule_stop_event(a);
+  }
+  void stop_sending(uint32_t a) {  // :187-191
+    cancel_events(a);
+    schedule_start_event(a);
+  }
+  void send_packet(uint32_t a) {  // :226-236
+    App &A = app[a];
+    Pkt p{a, A.seq++, s.app_pkt_size[a] + 8 + 20, s.app_ttl[a]};
+    A.c.tx_packets++;
+    A.c.tx_bytes += s.app_pkt_size[a];
+    ip_send(s.app_node[a], p);
+    A.totBytes += s.app_pkt_size[a];
+    A.lastStartTime = sim.m_currentTs;
+    A.residualBits = 0;
+    schedule_next_tx(a);
+  }
+  void start_application(uint32_t a) {  // :132-150 (socket setup schedules nothing)
+    if (s.app_kind[a] == NSGPU_APP_SINK) {
+      app[a].sink_active = true;
+      return;
+    }
+    cancel_events(a);
+    schedule_start_event(a);
+  }
+  void stop_application(uint32_t a) {  // :152-163
+    if (s.app_kind[a] == NSGPU_APP_SINK) {
+      app[a].sink_active = false;
+      return;
+    }
+    cancel_events(a);
+  }
+
+  // ---------------- setup ----------------
+  void app_object_start(uint32_t a) {  // Object::Start -> Application::DoStart (application.cc:87-95)
+    if (app[a].started) return;
+    app[a].started = true;
+    schedule(s.app_start_ns[a], [this, a]() { start_application(a); });
+    if (s.app_stop_ns[a] != 0) schedule(s.app_stop_ns[a], [this, a]() { stop_application(a); });
+  }
+  void node_start(uint32_t n) {  // Node::DoStart: devices (no events), then applications in order
+    for (uint32_t a : node_apps[n]) app_object_start(a);
+  }
+  void setup() {
+    dev.resize(s.n_devices);
+    app.resize(s.n_apps);
+    node_apps.assign(s.n_nodes, {});
+    sink_of_node.assign(s.n_nodes, -1);
+    for (uint32_t a = 0; a < s.n_apps; a++) {
+      node_apps[s.app_node[a]].push_back(a);
+      if (s.app_kind[a] == NSGPU_APP_SINK) sink_of_node[s.app_node[a]] = (int32_t)a;
+    }
+    for (uint32_t i = 0; i < s.n_setup; i++) {
+      const uint32_t k = s.setup_index[i];
+      switch (s.setup_kind[i]) {
+        case NSGPU_SETUP_NODE:  // NodeListPriv::Add
+          schedule_ctx(k, 0, [this, k]() { node_start(k); });
+          break;
+        case NSGPU_SETUP_DEVICE:  // Node::AddDevice -> NetDevice::Start (already started by Node::Start)
+          schedule_ctx(s.dev_node[k], 0, []() {});
+          break;
+        case NSGPU_SETUP_APP:  // Node::AddApplication -> Application::Start (Object::Start is idempotent)
+          schedule_ctx(s.app_node[k], 0, [this, k]() { app_object_start(k); });
+          break;
+        case NSGPU_SETUP_STOP:  // Simulator::Stop (Time) (default-simulator-impl.cc:179-183)
+          schedule(s.stop_ns, [this]() { sim.m_stop = true; });
+          break;
+        default:
+          sim.m_uid++;
+      }
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
+                             nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
+                             uint64_t log_cap, double *run_seconds) {
+  Model *m = new Model();
+  m->s = *sc;
+  m->sim.want_digest = true;
+  m->sim.log_ts = log_ts;
+  m->sim.log_uid = log_uid;
+  m->sim.log_ctx = log_ctx;
+  m->sim.log_cap = log_ts ? log_cap : 0;
+  m->setup();
+  auto t0 = std::chrono::steady_clock::now();
+  m->sim.Run();
+  auto t1 = std::chrono::steady_clock::now();
+  if (run_seconds) *run_seconds = std::chrono::duration<double>(t1 - t0).count();
+  memset(stats, 0, sizeof(*stats));
+  stats->dispatched = m->sim.m_dispatched;
+  stats->cancelled = m->sim.m_cancelled;
+  stats->digest = m->sim.m_digest;
+  stats->final_ts = m->sim.m_currentTs;
+  stats->next_uid = m->sim.m_uid;
+  stats->ttl_drops = m->ttl_drops;
+  stats->no_route_drops = m->no_route_drops;
+  if (devc)
+    for (uint32_t d = 0; d < sc->n_devices; d++) devc[d] = m->dev[d].c;
+  if (appc)
+    for (uint32_t a = 0; a < sc->n_apps; a++) appc[a] = m->app[a].c;
+  delete m;
+  return 0;
+}

@@ -1,0 +1,62 @@
+"""GPU-resident point-to-point subset vs the oracle (configs 2/4 handler chain).
+
+Bit-exact: the full (ts, uid, context) pop order on small scenarios; dispatch count, cancelled
+dispatches, digest, final time, next uid and every per-device / per-application counter on the
+larger grids."""
+import numpy as np
+import pytest
+
+import nsref
+import p2p
+
+pytestmark = pytest.mark.gpu
+
+
+def both(sc, log_cap=0):
+    s = sc.c_struct()
+    st = p2p.P2PStats()
+    devc = np.zeros(s.n_devices, p2p.DEV_COUNTERS_DTYPE)
+    appc = np.zeros(s.n_apps, p2p.APP_COUNTERS_DTYPE)
+    _, olog = nsref.p2p_run(s, st, devc, appc, log_cap)
+    eng = p2p.Engine(sc, log_cap=log_cap)
+    gst, gdevc, gappc, glog = eng.run(log_n=log_cap)
+    return (st, devc, appc, olog), (gst, gdevc, gappc, glog)
+
+
+def assert_same(o, g, log=True):
+    st, devc, appc, olog = o
+    gst, gdevc, gappc, glog = g
+    for f in ("dispatched", "cancelled", "digest", "final_ts", "next_uid", "ttl_drops", "no_route_drops"):
+        assert getattr(gst, f) == getattr(st, f), (f, getattr(gst, f), getattr(st, f))
+    assert np.array_equal(gdevc, devc)
+    assert np.array_equal(gappc, appc)
+    if log:
+        n = int(min(st.dispatched, len(olog[0])))
+        for a, b, name in zip(glog, olog, ("ts", "uid", "ctx")):
+            assert np.array_equal(a[:n], b[:n]), name
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_topologies_full_pop_order(seed):
+    sc = p2p.random_topology(15, 25, 8, seed)
+    o, g = both(sc, log_cap=300000)
+    assert_same(o, g)
+
+
+def test_grid_8x8_full_pop_order():
+    o, g = both(p2p.grid(8, 8), log_cap=60000)
+    assert_same(o, g)
+
+
+def test_grid_congested_drops():
+    # 1 Mb/s links with 4 sources per destination column: DropTail overflows
+    g = p2p.grid(5, 5, bps=1_000_000, qmax=5, rate_bps=2_000_000, stop_ns=400_000_000,
+                 sim_stop_ns=500_000_000)
+    o, gg = both(g, log_cap=200000)
+    assert o[1]["drop_packets"].sum() > 0
+    assert_same(o, gg)
+
+
+def test_grid_32x32_counters_digest():
+    o, g = both(p2p.grid(32, 32))
+    assert_same(o, g, log=False)

@@ -1,0 +1,55 @@
+"""CPU checks of the point-to-point oracle and the scenario builders (no GPU).
+
+Conservation laws of the restated reference chain (queue.cc / drop-tail-queue.cc / p2p device):
+every packet a device transmits is received by its peer unless the run stopped first, every
+enqueued packet is dequeued or still queued, and without drops every sent packet reaches its sink."""
+import numpy as np
+
+import nsref
+import p2p
+
+
+def run_oracle(sc, log_cap=0):
+    s = sc.c_struct()
+    st = p2p.P2PStats()
+    devc = np.zeros(s.n_devices, p2p.DEV_COUNTERS_DTYPE)
+    appc = np.zeros(s.n_apps, p2p.APP_COUNTERS_DTYPE)
+    secs, log = nsref.p2p_run(s, st, devc, appc, log_cap)
+    return st, devc, appc, log
+
+
+def test_grid_builder_mirrors_helper_order():
+    g = p2p.grid(3, 4)
+    # node (y, x) creation interleaved with its row link then column link (point-to-point-grid.cc:45-64)
+    kinds = [k for k, _ in g.setup]
+    assert kinds[:3] == [p2p.SETUP_NODE, p2p.SETUP_NODE, p2p.SETUP_DEVICE]
+    assert len(g.dev) == 2 * (3 * 3 + 2 * 4)  # rows*(cols-1) + (rows-1)*cols links
+    assert sum(1 for k in kinds if k == p2p.SETUP_NODE) == 12
+    # every node routes to every destination, by XY
+    for d, slot in g.dst_slot.items():
+        col = g.route[:, slot]
+        assert col[d] == p2p.NO_ROUTE and (np.delete(col, d) != p2p.NO_ROUTE).all()
+
+
+def test_grid_no_drop_conservation():
+    g = p2p.grid(6, 6, stop_ns=500_000_000, sim_stop_ns=600_000_000)
+    st, devc, appc, _ = run_oracle(g)
+    onoff = np.array([a["kind"] == p2p.APP_ONOFF for a in g.apps])
+    assert devc["drop_packets"].sum() == 0
+    assert appc["tx_packets"][onoff].sum() == appc["rx_packets"][~onoff].sum() > 0
+    assert (devc["enq_packets"] == devc["deq_packets"]).all()
+    assert st.cancelled >= 0 and st.ttl_drops == 0 and st.no_route_drops == 0
+
+
+def test_random_topology_queue_conservation():
+    for seed in range(5):
+        sc = p2p.random_topology(15, 25, 8, seed)
+        st, devc, appc, (lts, luid, lctx) = run_oracle(sc, log_cap=200000)
+        assert st.dispatched > 100
+        # a queue never holds more than MaxPackets, every enqueue is dequeued or still queued
+        assert (devc["enq_packets"] >= devc["deq_packets"]).all()
+        assert ((devc["enq_packets"] - devc["deq_packets"]) <= 20).all()
+        # pop order is (ts, uid) ascending
+        n = int(min(st.dispatched, 200000))
+        key = lts[:n].astype(object) * (1 << 32) + luid[:n].astype(object)
+        assert all(key[i] < key[i + 1] for i in range(n - 1))
