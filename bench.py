@@ -1,19 +1,24 @@
 """bench.py — simulated events/s of the nsgpu engine on MI355X (driver contract: one JSON line).
 
-Workload (round 1): SURVEY §8(d) config 1, utils/bench-simulator.cc churn — 10,000 pending
-events, delays U[0,1) s (tests/golden/bench_dist_u01_10k.txt), 5e6 holds, MapScheduler pop
-order, run entirely on the device (nsgpu_hold_run).  One step = one full bench-simulator run
-(10,000 inserts + 5,010,001 dispatches); inputs are resident in HBM before the timed region.
+Workloads (--workload):
+  p2p-grid (default): SURVEY §8(d) config 4 — PointToPointGridHelper 128x128 (16,384 nodes,
+      32,512 links / 65,024 devices+DropTail queues), 10 Mb/s, 1 ms, DropTail 100 packets, one OnOff
+      UDP flow (500 kb/s, 512 B) per column from the top row to the bottom row, 0.1-2.0 s, static XY
+      routes, Simulator::Stop at 2.1 s.  Everything after ns-3's setup phase — the
+      setup-time Node/NetDevice/Application::Start events included — runs on the device in one
+      persistent kernel (nsgpu_p2p_run).  One step = one full simulation from the post-setup state.
+  churn: config 1, utils/bench-simulator.cc — 10,000 pending, U[0,1) s delays, 5e6 holds,
+      GPU-resident Bench::Cb (nsgpu_hold_run).
 
-The churn is one logical process (all events have context 0xffffffff), so it does not shard:
-with --gpus N every rank runs an independent replica ("replicas only") and `value`
-is the events of all ranks divided by the slowest rank's time.
+Neither workload shards inside one simulation yet, so with --gpus N every rank runs an
+independent replica ("replicas", weak scaling) and `value` is the events of all ranks divided by
+the slowest rank's time.
 
-roofline: the dominant kernel is hold_run; algorithmic bytes = 72 B per dispatched event
-(24 B insert + 24 B window read + 24 B dispatch write) x events per launch,
-divided by the kernel's average duration measured with HIP events on its stream.
-cpu_baseline: the oracle's restatement of DefaultSimulatorImpl + MapScheduler + Bench::Cb
-("port"), on one host core, same distribution and hold count.
+roofline: dominant kernel = the persistent engine kernel; algorithmic bytes per event from
+SURVEY §8(d) (queue: 72 B/event; p2p hop: 208 B per hop = 104 B per event) x events per launch,
+divided by the kernel's average duration measured with HIP events on its own stream.
+cpu_baseline: the oracle's sequential restatement of the same reference path (DefaultSimulatorImpl
++ MapScheduler + the handler chain, "port"), on one host core, same scenario.
 """
 import argparse
 import json
@@ -26,9 +31,7 @@ sys.path.insert(0, os.path.join(REPO, "ns-3-dev-dnemu_amd"))
 
 METRIC = "simulated events/sec (whole node) at 1/2/4/8 GPUs; speedup vs ns-3 CPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-BYTES_PER_EVENT = 72    # SURVEY §8(d) event-queue algorithmic bytes
 DIST_FILE = os.path.join(REPO, "tests", "golden", "bench_dist_u01_10k.txt")
-TOTAL_HOLDS = 5_000_000
 
 
 def load_distribution(path):
@@ -43,25 +46,84 @@ def load_distribution(path):
     return (np.array(vals, dtype=np.float64) * 1000000000).astype(np.uint64)
 
 
-def cpu_baseline(dist, total):
+def oracle():
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import nsref
-    runs = []
-    for _ in range(3):
-        res, _, _ = nsref.churn_run(dist, total, nsref.SCHED_MAP)
-        runs.append(res)
-    best = min(runs, key=lambda r: r.run_seconds)
-    return {
-        "value": best.dispatched / best.run_seconds,
-        "unit": "events/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"full config-1 run ({len(dist)} pending, {total} holds, {best.dispatched} dispatches), "
-                  "oracle restatement of DefaultSimulatorImpl+MapScheduler+Bench::Cb, g++ -O2, best of 3, "
-                  f"Simulator::Run only ({best.run_seconds:.3f} s)",
-        "digest_match": None,
-        "_digest": best.digest,
-    }
+    return nsref
+
+
+# ---------------------------------------------------------------- workloads
+class Churn:
+    bytes_per_event = 72
+    kernel = "nsgpu::hold_run_packed"
+
+    def __init__(self, args, stream):
+        import nsgpu
+        self.dist = load_distribution(DIST_FILE)
+        self.holds = args.holds
+        self.run = nsgpu.HoldRun(self.dist, self.holds, stream=stream)
+        self.workload = (f"bench-simulator churn (config 1): {len(self.dist)} pending, U[0,1) s delays, "
+                         f"{self.holds} holds, MapScheduler (ts,uid) order, GPU-resident Bench::Cb")
+
+    def step(self):
+        self.run.launch()
+
+    def result(self):
+        st, _, _ = self.run.result()
+        return int(st.dispatched), int(st.digest), {"rounds_per_step": int(st.rounds), "max_batch": int(st.max_batch)}
+
+    def cpu_baseline(self):
+        nsref = oracle()
+        best = None
+        for _ in range(3):
+            res, _, _ = nsref.churn_run(self.dist, self.holds, nsref.SCHED_MAP)
+            best = res if best is None or res.run_seconds < best.run_seconds else best
+        return best.dispatched / best.run_seconds, best.digest, (
+            f"full config-1 run ({len(self.dist)} pending, {self.holds} holds, {best.dispatched} dispatches), oracle "
+            f"restatement of DefaultSimulatorImpl+MapScheduler+Bench::Cb, g++ -O2, best of 3, Simulator::Run only "
+            f"({best.run_seconds:.3f} s)")
+
+
+class P2PGrid:
+    bytes_per_event = 104  # 208 B per GPU-resident p2p hop, 2 events per hop
+    kernel = "nsgpu::p2p_run"
+
+    def __init__(self, args, stream):
+        import p2p
+        self.p2p = p2p
+        n = args.grid
+        self.scenario = p2p.grid(n, n)
+        self.engine = p2p.Engine(self.scenario, stream=stream)
+        self.workload = (f"PointToPointGridHelper {n}x{n} (config 4): {n * n} nodes, {len(self.scenario.dev)} "
+                         f"devices, 10Mb/s 1ms DropTail(100), {n} OnOff UDP flows 500kb/s 512B top->bottom "
+                         f"0.1-2.0s, static XY routes, Stop 2.1s; whole run GPU-resident")
+
+    def step(self):
+        self.engine.reset()
+        self.engine.launch()
+
+    def result(self):
+        st, devc, appc, _ = self.engine.results()
+        return int(st.dispatched), int(st.digest), {
+            "windows_per_step": int(st.windows), "max_window": int(st.max_window),
+            "cancelled_per_step": int(st.cancelled), "delivered_packets": int(appc["rx_packets"].sum())}
+
+    def cpu_baseline(self):
+        import numpy as np
+        nsref = oracle()
+        s = self.scenario.c_struct()
+        st = self.p2p.P2PStats()
+        devc = np.zeros(s.n_devices, self.p2p.DEV_COUNTERS_DTYPE)
+        appc = np.zeros(s.n_apps, self.p2p.APP_COUNTERS_DTYPE)
+        secs, _ = nsref.p2p_run(s, st, devc, appc)
+        return st.dispatched / secs, st.digest, (
+            f"full run of the same scenario ({st.dispatched} dispatches), oracle restatement of "
+            f"DefaultSimulatorImpl+MapScheduler+p2p/DropTail/IPv4/UDP/OnOff chain, g++ -O2, Simulator::Run only "
+            f"({secs:.3f} s); the reference ns-3 itself is slower still (packet objects, headers, callbacks, "
+            f"trace sinks: SURVEY §6 probe 82 k ev/s at 16x16 with global routing)")
+
+
+WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid}
 
 
 def main():
@@ -69,39 +131,39 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--holds", type=int, default=TOTAL_HOLDS)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="p2p-grid")
+    ap.add_argument("--grid", type=int, default=128)
+    ap.add_argument("--holds", type=int, default=5_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist_pg = None
+    tdist = None
     if world > 1:
         import torch
-        import torch.distributed as tdist
+        import torch.distributed as td
         torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
-        dist_pg = tdist
+        td.init_process_group("nccl")
+        tdist = td
 
-    import numpy as np
     import nsgpu
 
     nsgpu.check(nsgpu.lib().nsgpu_set_device(local_rank))
-    dist = load_distribution(DIST_FILE)
     stream = nsgpu.Stream()
-    run = nsgpu.HoldRun(dist, args.holds, stream=stream.handle)
+    wl = WORKLOADS[args.workload](args, stream.handle)
     timer = nsgpu.Timer()
 
     for _ in range(args.warmup):
-        run.launch()
+        wl.step()
     stream.sync()
 
     def barrier():
-        if dist_pg is not None:
+        if tdist is not None:
             import torch
             torch.cuda.synchronize()
-            dist_pg.barrier()
+            tdist.barrier()
             torch.cuda.synchronize()
 
     barrier()
@@ -109,27 +171,24 @@ def main():
     t0 = time.perf_counter()
     timer.start(stream.handle)
     for _ in range(args.steps):
-        run.launch()
+        wl.step()
     timer.stop(stream.handle)
     stream.sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms_total = timer.elapsed_ms()
-    st, _, _ = run.result()
+    kernel_ms = timer.elapsed_ms() / args.steps  # one engine launch per step (+ resets / tiny setup kernels)
+    events_per_step, digest, extra = wl.result()
 
-    if dist_pg is not None:
+    if tdist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist_pg.all_reduce(t, op=dist_pg.ReduceOp.MAX)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    events_per_step = int(st.dispatched)
     value = events_per_step * args.steps * world / elapsed
-    kernel_ms = kernel_ms_total / args.steps  # one hold_run launch per step (+ a tiny init-rank kernel)
-    achieved = BYTES_PER_EVENT * events_per_step / (kernel_ms / 1e3) / 1e9
-
+    achieved = wl.bytes_per_event * events_per_step / (kernel_ms / 1e3) / 1e9
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "traffic_hold_run.json")
+    tpath = os.path.join(REPO, "profiles", f"traffic_{args.workload}.json")
     if os.path.exists(tpath):
         try:
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
@@ -150,14 +209,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",
-            "config": {
-                "workload": f"bench-simulator churn (config 1): {len(dist)} pending, U[0,1) s delays, "
-                            f"{args.holds} holds, MapScheduler (ts,uid) order, GPU-resident Bench::Cb",
-                "events_per_step": events_per_step,
-                "parallelism": "replicas" if world > 1 else "single",
-                "rounds_per_step": int(st.rounds),
-                "max_batch": int(st.max_batch),
-            },
+            "config": dict({"workload": wl.workload, "events_per_step": events_per_step,
+                            "parallelism": "replicas" if world > 1 else "single"}, **extra),
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -165,20 +218,20 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
-                "kernel": "nsgpu::hold_run",
+                "kernel": wl.kernel,
                 "kernel_ms": kernel_ms,
-                "bytes_per_event": BYTES_PER_EVENT,
+                "bytes_per_event": wl.bytes_per_event,
             },
         }
         if not args.no_cpu_baseline:
-            cb = cpu_baseline(dist, args.holds)
-            cb["digest_match"] = bool(cb.pop("_digest") == st.digest)
-            out["cpu_baseline"] = cb
-            out["speedup_vs_cpu"] = value / world / cb["value"]
+            cv, cdigest, sample = wl.cpu_baseline()
+            out["cpu_baseline"] = {"value": cv, "unit": "events/s", "cores": 1, "kind": "port", "sample": sample,
+                                   "digest_match": bool(cdigest == digest)}
+            out["speedup_vs_cpu"] = value / world / cv
         print(json.dumps(out), flush=True)
 
-    if dist_pg is not None:
-        dist_pg.destroy_process_group()
+    if tdist is not None:
+        tdist.destroy_process_group()
 
 
 if __name__ == "__main__":
