@@ -114,6 +114,45 @@ int nsgpu_hold_set_profile(uint64_t *d_phase_cycles);
 int nsgpu_hold_run(const uint64_t *d_dist, uint32_t n, uint32_t total, nsgpu_hold_stats *d_stats,
                    uint64_t *d_log_ts, uint32_t *d_log_uid, uint64_t log_cap, void *d_workspace, void *stream);
 
+/* ---------------- HipBatchScheduler (host closures) ----------------
+ * The ns3::Scheduler interface (src/core/model/scheduler.h:75-97) — Insert, IsEmpty, PeekNext,
+ * RemoveNext, Remove — with MapScheduler's (ts, uid) order (map-scheduler.cc:51-100).  Pending
+ * events are kept sorted in HBM; staged inserts are sorted and merged on the device in bulk and
+ * the next `batch` events are popped to the host in one copy.  `handle` is the caller's EventImpl*
+ * (never dereferenced).  ns3::HipBatchScheduler forwards to these. */
+typedef struct nsgpu_sched nsgpu_sched;
+int nsgpu_sched_create(uint32_t batch, void *stream, nsgpu_sched **out);
+int nsgpu_sched_destroy(nsgpu_sched *s);
+int nsgpu_sched_insert(nsgpu_sched *s, const nsgpu_event *ev, uint64_t n);
+int nsgpu_sched_is_empty(nsgpu_sched *s, int *empty);
+int nsgpu_sched_size(nsgpu_sched *s, uint64_t *n);
+int nsgpu_sched_peek_next(nsgpu_sched *s, nsgpu_event *out);
+int nsgpu_sched_remove_next(nsgpu_sched *s, nsgpu_event *out);
+int nsgpu_sched_remove(nsgpu_sched *s, const nsgpu_event *ev);
+
+/* ---------------- HipSimulatorImpl host runtime (host closures) ----------------
+ * DefaultSimulatorImpl's semantics (default-simulator-impl.cc:49-353: uid from 4, ScheduleDestroy
+ * consumes a uid, IsExpired rule, cancelled events still dequeued, Stop/Stop (Time)) over the
+ * HipBatchScheduler, with C callbacks as the closures.  ns3::HipSimulatorImpl implements the same
+ * logic with ns-3's EventImpl* (INTEGRATION.md). */
+typedef void (*nsgpu_event_fn)(void *user, uint64_t arg);
+typedef struct nsgpu_sim nsgpu_sim;
+int nsgpu_sim_create(uint32_t batch, void *stream, nsgpu_sim **out);
+int nsgpu_sim_free(nsgpu_sim *s);
+int nsgpu_sim_schedule(nsgpu_sim *s, int64_t delay, nsgpu_event_fn fn, void *user, uint64_t arg, nsgpu_event_id *id);
+int nsgpu_sim_schedule_with_context(nsgpu_sim *s, uint32_t ctx, int64_t delay, nsgpu_event_fn fn, void *user,
+                                    uint64_t arg);
+int nsgpu_sim_schedule_now(nsgpu_sim *s, nsgpu_event_fn fn, void *user, uint64_t arg, nsgpu_event_id *id);
+int nsgpu_sim_schedule_destroy(nsgpu_sim *s, nsgpu_event_fn fn, void *user, uint64_t arg, nsgpu_event_id *id);
+int nsgpu_sim_is_expired(nsgpu_sim *s, const nsgpu_event_id *id, int *expired);
+int nsgpu_sim_cancel(nsgpu_sim *s, const nsgpu_event_id *id);
+int nsgpu_sim_remove(nsgpu_sim *s, const nsgpu_event_id *id);
+int nsgpu_sim_run(nsgpu_sim *s);
+int nsgpu_sim_stop(nsgpu_sim *s);
+int nsgpu_sim_stop_at(nsgpu_sim *s, int64_t delay);
+int nsgpu_sim_destroy(nsgpu_sim *s);
+int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *dispatched, uint32_t *next_uid);
+
 /* ---------------- GPU-resident point-to-point subset (configs 2, 4) ----------------
  * Replaces, for a topology of PointToPointNetDevices, the handler chain
  *   PointToPointNetDevice::{Send,TransmitStart,TransmitComplete,Receive} (point-to-point-net-device.cc:206-346,462-518)

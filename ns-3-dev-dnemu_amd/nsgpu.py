@@ -68,6 +68,28 @@ SIGNATURES = {
     "nsgpu_fanout_workspace_bytes": (C.c_int, [_i64, _i64, C.POINTER(C.c_uint64)]),
     "nsgpu_hold_workspace_bytes": (C.c_int, [_u32, C.POINTER(C.c_uint64)]),
     "nsgpu_hold_set_profile": (C.c_int, [_vp]),
+    "nsgpu_sched_create": (C.c_int, [_u32, _vp, C.POINTER(C.c_void_p)]),
+    "nsgpu_sched_destroy": (C.c_int, [_vp]),
+    "nsgpu_sched_insert": (C.c_int, [_vp, _vp, _u64]),
+    "nsgpu_sched_is_empty": (C.c_int, [_vp, C.POINTER(C.c_int)]),
+    "nsgpu_sched_size": (C.c_int, [_vp, C.POINTER(C.c_uint64)]),
+    "nsgpu_sched_peek_next": (C.c_int, [_vp, _vp]),
+    "nsgpu_sched_remove_next": (C.c_int, [_vp, _vp]),
+    "nsgpu_sched_remove": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_create": (C.c_int, [_u32, _vp, C.POINTER(C.c_void_p)]),
+    "nsgpu_sim_free": (C.c_int, [_vp]),
+    "nsgpu_sim_schedule": (C.c_int, [_vp, _i64, _vp, _vp, _u64, _vp]),
+    "nsgpu_sim_schedule_with_context": (C.c_int, [_vp, _u32, _i64, _vp, _vp, _u64]),
+    "nsgpu_sim_schedule_now": (C.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "nsgpu_sim_schedule_destroy": (C.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "nsgpu_sim_is_expired": (C.c_int, [_vp, _vp, C.POINTER(C.c_int)]),
+    "nsgpu_sim_cancel": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_remove": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_run": (C.c_int, [_vp]),
+    "nsgpu_sim_stop": (C.c_int, [_vp]),
+    "nsgpu_sim_stop_at": (C.c_int, [_vp, _i64]),
+    "nsgpu_sim_destroy": (C.c_int, [_vp]),
+    "nsgpu_sim_state": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "nsgpu_p2p_create": (C.c_int, [_vp, _u64, _u64, C.POINTER(C.c_void_p)]),
     "nsgpu_p2p_reset": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_run": (C.c_int, [_vp, _vp]),
@@ -280,3 +302,142 @@ class HoldRun:
             return st, self.log_ts.download(np.uint64, self.log_cap, self.stream), \
                 self.log_uid.download(np.uint32, self.log_cap, self.stream)
         return st, None, None
+
+
+# ---------------- HipBatchScheduler / HipSimulatorImpl host runtime ----------------
+EVENT_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("context", "<u4"), ("handle", "<u8")])
+
+
+class EventId(C.Structure):  # nsgpu_event_id
+    _fields_ = [("impl", C.c_uint64), ("ts", C.c_uint64), ("context", C.c_uint32), ("uid", C.c_uint32)]
+
+
+EVENT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)
+
+
+class Sched:
+    """ns3::Scheduler interface over the HBM-resident batch scheduler (nsgpu_sched_*)."""
+
+    def __init__(self, batch=4096, stream=None):
+        h = C.c_void_p()
+        check(lib().nsgpu_sched_create(batch, stream, C.byref(h)))
+        self.h = h.value
+
+    def insert(self, events):
+        ev = np.ascontiguousarray(events, dtype=EVENT_DTYPE)
+        check(lib().nsgpu_sched_insert(self.h, ev.ctypes.data, ev.size))
+
+    def is_empty(self):
+        e = C.c_int()
+        check(lib().nsgpu_sched_is_empty(self.h, C.byref(e)))
+        return bool(e.value)
+
+    def size(self):
+        n = C.c_uint64()
+        check(lib().nsgpu_sched_size(self.h, C.byref(n)))
+        return n.value
+
+    def _one(self, f):
+        out = np.zeros(1, EVENT_DTYPE)
+        check(f(self.h, out.ctypes.data))
+        return out[0]
+
+    def peek_next(self):
+        return self._one(lib().nsgpu_sched_peek_next)
+
+    def remove_next(self):
+        return self._one(lib().nsgpu_sched_remove_next)
+
+    def remove(self, ev):
+        e = np.array([tuple(ev)], dtype=EVENT_DTYPE)
+        check(lib().nsgpu_sched_remove(self.h, e.ctypes.data))
+
+    def __del__(self):
+        try:
+            lib().nsgpu_sched_destroy(self.h)
+        except Exception:
+            pass
+
+
+class Sim:
+    """HipSimulatorImpl host runtime with Python closures (the checker's Sim has the same interface)."""
+
+    def __init__(self, batch=64, stream=None):
+        h = C.c_void_p()
+        check(lib().nsgpu_sim_create(batch, stream, C.byref(h)))
+        self.h = h.value
+        self._keep = []
+
+    def _fn(self, cb):
+        f = EVENT_FN(lambda user, arg: cb())
+        self._keep.append(f)
+        return f
+
+    def schedule(self, delay, cb):
+        i = EventId()
+        check(lib().nsgpu_sim_schedule(self.h, delay, C.cast(self._fn(cb), C.c_void_p), None, 0, C.byref(i)))
+        return i
+
+    def schedule_with_context(self, ctx, delay, cb):
+        check(lib().nsgpu_sim_schedule_with_context(self.h, ctx, delay, C.cast(self._fn(cb), C.c_void_p), None, 0))
+
+    def schedule_now(self, cb):
+        i = EventId()
+        check(lib().nsgpu_sim_schedule_now(self.h, C.cast(self._fn(cb), C.c_void_p), None, 0, C.byref(i)))
+        return i
+
+    def schedule_destroy(self, cb):
+        i = EventId()
+        check(lib().nsgpu_sim_schedule_destroy(self.h, C.cast(self._fn(cb), C.c_void_p), None, 0, C.byref(i)))
+        return i
+
+    def remove(self, eid):
+        check(lib().nsgpu_sim_remove(self.h, C.byref(eid)))
+
+    def cancel(self, eid):
+        check(lib().nsgpu_sim_cancel(self.h, C.byref(eid)))
+
+    def is_expired(self, eid):
+        e = C.c_int()
+        check(lib().nsgpu_sim_is_expired(self.h, C.byref(eid), C.byref(e)))
+        return bool(e.value)
+
+    def run(self):
+        check(lib().nsgpu_sim_run(self.h))
+
+    def stop(self, delay=None):
+        if delay is None:
+            check(lib().nsgpu_sim_stop(self.h))
+        else:
+            check(lib().nsgpu_sim_stop_at(self.h, delay))
+
+    def destroy(self):
+        check(lib().nsgpu_sim_destroy(self.h))
+
+    def _state(self):
+        now, ctx, disp, uid = C.c_uint64(), C.c_uint32(), C.c_uint64(), C.c_uint32()
+        check(lib().nsgpu_sim_state(self.h, C.byref(now), C.byref(ctx), C.byref(disp), C.byref(uid)))
+        return now.value, ctx.value, disp.value, uid.value
+
+    def now(self):
+        return self._state()[0]
+
+    def context(self):
+        return self._state()[1]
+
+    def dispatched(self):
+        return self._state()[2]
+
+    def next_uid(self):
+        return self._state()[3]
+
+    def close(self):
+        if self.h:
+            lib().nsgpu_sim_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
