@@ -121,7 +121,9 @@ typedef struct nsgpu_p2p_scenario {
 } nsgpu_p2p_scenario;
 
 enum nsgpu_setup_kind { NSGPU_SETUP_NODE = 0, NSGPU_SETUP_DEVICE = 1, NSGPU_SETUP_APP = 2, NSGPU_SETUP_STOP = 3,
-                        NSGPU_SETUP_UID = 4 };
+                        NSGPU_SETUP_UID = 4, NSGPU_SETUP_NOOP = 5 };
+/* NSGPU_SETUP_NOOP k: ScheduleWithContext (k, 0, <no-op>) — e.g. the LoopbackNetDevice that
+ * Ipv4L3Protocol::SetupLoopback adds to every node (ipv4-l3-protocol.cc:227-244 -> node.cc:118). */
 
 /* Counters of a p2p run (both the oracle and the GPU engine fill this). */
 typedef struct nsgpu_p2p_stats {
@@ -134,6 +136,7 @@ typedef struct nsgpu_p2p_stats {
   uint64_t ttl_drops;
   uint64_t no_route_drops;
   uint64_t max_window;
+  uint64_t unreach_drops;     /* UDP datagrams with no bound endpoint (ICMP port unreachable not modelled) */
 } nsgpu_p2p_stats;
 
 /* Per-device counters: Queue (queue.cc:61-200) + device. */

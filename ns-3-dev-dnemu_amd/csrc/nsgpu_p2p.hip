@@ -40,12 +40,14 @@ enum EvKind : uint32_t {
   K_TX_COMPLETE = 9,    // PointToPointNetDevice::TransmitComplete
   K_RECEIVE = 10,       // PointToPointNetDevice::Receive
   K_STOP = 11,          // Simulator::Stop
-  K_NKINDS = 12
+  K_FWD_UP = 12,        // Ipv4EndPoint::DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink (zero-delay leaf)
+  K_NKINDS = 13
 };
 
 constexpr int P2P_THREADS = 1024;
 constexpr int WCAP = SORT_N;  // events per window
 constexpr uint32_t NOCTX = 0xffffffffu;
+constexpr int INLINE_MAX = 32;  // inline children pending at one ts on one node
 
 struct Pkt {
   uint32_t app, seq, size, ttl;
@@ -96,6 +98,8 @@ struct P2PDev {
 struct P2PLds {
   SortLds sort;
   uint32_t nchild[WCAP];
+  uint32_t ninl[WCAP];     // inline (zero-delay leaf) children dispatched inside the window, per rank
+  uint32_t iprefix[WCAP];  // exclusive prefix of ninl in rank order
   uint32_t wsum[P2P_THREADS / 64];
   uint64_t wmin[P2P_THREADS / 64];
   uint64_t wmin2[P2P_THREADS / 64];
@@ -221,12 +225,14 @@ __device__ void ip_send(const P2PDev &M, Emit &E, uint32_t n, const Pkt &p, uint
 }
 
 __device__ void ip_receive(const P2PDev &M, Emit &E, uint32_t n, Pkt p, int32_t sink, uint64_t *ttl_drops,
-                           uint64_t *no_route) {
-  if (M.app_dst_node[p.app] == n) {  // LocalDeliver -> UDP -> PacketSink::HandleRead
-    if (sink >= 0 && (M.app_flags[sink] & 2u)) {
-      M.appc[sink].rx_packets++;
-      M.appc[sink].rx_bytes += p.size - 28;
+                           uint64_t *no_route, uint64_t *unreach) {
+  if (M.app_dst_node[p.app] == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
+    if (sink < 0 || !(M.app_flags[sink] & 2u)) {  // no bound endpoint: RX_ENDPOINT_UNREACH
+      (*unreach)++;
+      return;
     }
+    // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120)
+    E.child(0, E.ctx, K_FWD_UP, (uint32_t)sink, p);
     return;
   }
   const uint32_t out = M.route[(uint64_t)n * M.n_dst + M.app_dst_slot[p.app]];
@@ -352,7 +358,7 @@ __device__ void appobj_start(const P2PDev &M, Emit &E, uint32_t a) {  // Applica
 
 // Runs one event; returns true if it was a cancelled dispatch.
 __device__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a, const Pkt &pkt, int32_t sink,
-                          uint64_t *ttl_drops, uint64_t *no_route, bool *stop) {
+                          uint64_t *ttl_drops, uint64_t *no_route, uint64_t *unreach, bool *stop) {
   const uint32_t kind = kind_word & 0xffu;
   const uint32_t gen = kind_word >> 8;
   switch (kind) {
@@ -418,9 +424,15 @@ __device__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t
       M.devc[a].rx_packets++;
       Pkt p = pkt;
       p.size -= 2;
-      ip_receive(M, E, M.dev_node[a], p, sink, ttl_drops, no_route);
+      ip_receive(M, E, M.dev_node[a], p, sink, ttl_drops, no_route, unreach);
       return false;
     }
+    case K_FWD_UP:  // DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink::HandleRead (a = sink app)
+      if (M.app_flags[a] & 2u) {
+        M.appc[a].rx_packets++;
+        M.appc[a].rx_bytes += pkt.size - 28;
+      }
+      return false;
     case K_STOP:
       *stop = true;
       return false;
@@ -439,7 +451,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
   int cur = 0;
   uint64_t K = 0;            // dispatched so far
   uint32_t uid = M.uid_init; // next uid
-  uint64_t digest = 0, cancelled = 0, ttl_drops = 0, no_route = 0;
+  uint64_t digest = 0, cancelled = 0, ttl_drops = 0, no_route = 0, unreach = 0;
   uint64_t windows = 0, max_window = 0, last_ts = 0;
   if (tid == 0) L.stop_flag = 0;
   __syncthreads();
@@ -484,13 +496,14 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
     uint64_t span = wend - tmin;
     if (span > 0xfffffffeull) span = 0xfffffffeull;
     uint64_t bound = (span << 32) | 0xffffffffull;
+    uint64_t stop_packed = INF;
     if (stopkey != INF && stopkey - tmin <= span) {
       // Stop caps the window at its own key (it is dispatched; later events are not)
       for (uint64_t i = tid; i < P; i += P2P_THREADS)
         if ((kindv[i] & 0xffu) == K_STOP) L.sort.k[1][0] = ((ts[i] - tmin) << 32) | uidv[i];
       __syncthreads();
-      const uint64_t sk = L.sort.k[1][0];
-      bound = sk < bound ? sk : bound;
+      stop_packed = L.sort.k[1][0];
+      bound = stop_packed < bound ? stop_packed : bound;
       __syncthreads();
     }
     // ---- count; if the window would exceed WCAP, bisect for the largest key bound that fits ----
@@ -521,6 +534,10 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       cnt = count_le(bound);
     }
     const uint32_t W = cnt;
+    // zero-delay leaf children (Ipv4EndPoint::DoForwardUp) run inside the window; when the window
+    // ends at the Stop event, those at the Stop's ts sort after it and are never dispatched
+    const bool has_stop = stop_packed != INF && bound >= stop_packed;
+    const uint64_t inline_ts_limit = has_stop ? (stop_packed >> 32) : INF;  // relative ts (exclusive)
     // ---- 2. partition: window -> sort registers; rest -> next pool ----
     const int nxt = cur ^ 1;
     uint64_t skey[4];
@@ -618,9 +635,13 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       L.sort.v[0][r] = rank_pool[q];
       L.sort.k[0][r] = rank_key[q];
       L.nchild[g] = 0;
+      L.ninl[g] = 0;
     }
     __syncthreads();
     // ---- 4. handlers: the first entry of each node group runs the group's events in rank order ----
+    // Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) are
+    // run by the same thread at their key position: after every node event with ts <= theirs, before
+    // the first with a larger ts (their uid is larger than every pending uid).
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int g = 256 * wid + 64 * q + lane;
@@ -628,67 +649,159 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       const uint32_t c = (uint32_t)(L.sort.k[1][g] >> 32);
       if (g > 0 && (uint32_t)(L.sort.k[1][g - 1] >> 32) == c) continue;  // not the group head
       const int32_t sink = c < M.n_nodes ? sink_of_node[c] : -1;
-      for (int h = g; h < (int)W && (uint32_t)(L.sort.k[1][h] >> 32) == c; h++) {
-        const uint32_t r = L.sort.v[1][h];
+      uint32_t pend[INLINE_MAX];  // child slots of pending inline children, all at ts pend_ts
+      uint32_t npend = 0;
+      uint64_t pend_ts = 0;
+      for (int h = g; h <= (int)W; h++) {
+        const bool more = h < (int)W && (uint32_t)(L.sort.k[1][h] >> 32) == c;
+        const uint32_t r = more ? L.sort.v[1][h] : 0;
+        const uint64_t rel = more ? (L.sort.k[0][r] >> 32) : INF;
+        if (npend && rel > pend_ts) {  // flush inline children that sort before this event
+          for (uint32_t i = 0; i < npend; i++) {
+            const uint32_t sl = pend[i];
+            Emit E0;
+            E0.M = &M;
+            E0.now = tmin + pend_ts;
+            E0.ctx = c;
+            E0.slot0 = 0;
+            E0.n = 0;
+            bool st0 = false;
+            run_event(M, E0, M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl], sink, &ttl_drops, &no_route, &unreach,
+                      &st0);
+          }
+          npend = 0;
+        }
+        if (!more) break;
         const uint32_t pi = L.sort.v[0][r];
         Emit E;
         E.M = &M;
-        E.now = tmin + (L.sort.k[0][r] >> 32);
+        E.now = tmin + rel;
         E.ctx = c;
         E.slot0 = r * M.maxc;
         E.n = 0;
         bool stop = false;
         const bool was_cancelled = run_event(M, E, M.ev_kind[cur][pi], M.ev_a[cur][pi], M.ev_pkt[cur][pi], sink,
-                                             &ttl_drops, &no_route, &stop);
+                                             &ttl_drops, &no_route, &unreach, &stop);
         cancelled += was_cancelled;
         L.nchild[r] = E.n;
         if (stop) L.stop_flag = 1;
+        uint32_t ni = 0;
+        for (uint32_t j = 0; j < E.n; j++) {
+          const uint32_t sl = E.slot0 + j;
+          if ((M.ch_kind[sl] & 0xffu) == K_FWD_UP && rel < inline_ts_limit) {
+            if (npend == INLINE_MAX) {
+              atomicOr(M.error, 16u);
+            } else {
+              pend[npend++] = sl;
+              pend_ts = rel;
+              ni++;
+            }
+          }
+        }
+        L.ninl[r] = ni;
       }
     }
     __syncthreads();
-    // ---- 5. uids: exclusive scan of child counts in rank order; digest; children -> next pool ----
-    uint32_t nc[4], tsum = 0;
+    // ---- 5. uids: exclusive scan of child counts in rank order; dispatch ranks; children -> next pool ----
+    uint32_t nc[4], ni4[4], tsum = 0, isum = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       nc[q] = L.nchild[tid * 4 + q];
+      ni4[q] = L.ninl[tid * 4 + q];
       tsum += nc[q];
+      isum += ni4[q];
     }
-    uint32_t total_children;
+    uint32_t total_children, total_inline;
     uint32_t base = block_exscan(tsum, L.wsum, &total_children);
+    uint32_t ibase = block_exscan(isum, L.wsum, &total_inline);
+    {
+      uint32_t ib = ibase;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        L.iprefix[tid * 4 + q] = ib;
+        ib += ni4[q];
+      }
+    }
+    __syncthreads();
+    // dispatch rank of main event r = r + #inline children with ts < ts_r; of the i-th inline child
+    // of r = (#main events with ts <= ts_r) + iprefix[r] + i  (inline children are key-sorted by r)
+    auto first_same = [&](uint32_t r, uint64_t rel) -> uint32_t {
+      uint32_t lo = 0, hi = r;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((L.sort.k[0][mid] >> 32) < rel) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo;
+    };
+    auto last_same = [&](uint32_t r, uint64_t rel) -> uint32_t {
+      uint32_t lo = r + 1, hi = W;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((L.sort.k[0][mid] >> 32) <= rel) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo - 1;
+    };
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const uint32_t r = tid * 4 + q;
       if (r < W) {
         const uint64_t pk = L.sort.k[0][r];
-        const uint64_t t = tmin + (pk >> 32);
+        const uint64_t rel = pk >> 32;
+        const uint64_t t = tmin + rel;
         const uint32_t u = (uint32_t)pk;
-        digest += digest_term(K + r, t, u);
-        if (K + r < M.log_cap) {
-          M.log_ts[K + r] = t;
-          M.log_uid[K + r] = u;
-          M.log_ctx[K + r] = M.ev_ctx[cur][L.sort.v[0][r]];
+        const bool dup_prev = r > 0 && (L.sort.k[0][r - 1] >> 32) == rel;
+        const uint32_t f = total_inline ? (dup_prev ? first_same(r, rel) : r) : r;
+        const uint64_t rk = K + r + (total_inline ? L.iprefix[f] : 0);
+        digest += digest_term(rk, t, u);
+        if (rk < M.log_cap) {
+          M.log_ts[rk] = t;
+          M.log_uid[rk] = u;
+          M.log_ctx[rk] = M.ev_ctx[cur][L.sort.v[0][r]];
         }
         if (r == W - 1) last_ts = t;
+        uint32_t lastr = 0;
+        if (ni4[q]) lastr = (r + 1 < W && (L.sort.k[0][r + 1] >> 32) == rel) ? last_same(r, rel) : r;
+        uint32_t ii = 0, nonin = base - (ibase);  // non-inline children before this rank
         for (uint32_t j = 0; j < nc[q]; j++) {
-          const uint32_t s = r * M.maxc + j;
-          const uint64_t o = P + base + j;
+          const uint32_t sl = r * M.maxc + j;
+          const uint32_t cu = uid + base + j;
+          if ((M.ch_kind[sl] & 0xffu) == K_FWD_UP) {
+            if (rel < inline_ts_limit) {  // dispatched inside this window
+              const uint64_t crk = K + lastr + 1 + L.iprefix[r] + ii;
+              digest += digest_term(crk, t, cu);
+              if (crk < M.log_cap) {
+                M.log_ts[crk] = t;
+                M.log_uid[crk] = cu;
+                M.log_ctx[crk] = M.ch_ctx[sl];
+              }
+              ii++;
+            }
+            continue;  // never re-queued
+          }
+          const uint64_t o = P + nonin;
+          nonin++;
           if (o < M.pool_cap) {
-            M.ev_ts[nxt][o] = M.ch_ts[s];
-            M.ev_uid[nxt][o] = uid + base + j;
-            M.ev_ctx[nxt][o] = M.ch_ctx[s];
-            M.ev_kind[nxt][o] = M.ch_kind[s];
-            M.ev_a[nxt][o] = M.ch_a[s];
-            M.ev_pkt[nxt][o] = M.ch_pkt[s];
+            M.ev_ts[nxt][o] = M.ch_ts[sl];
+            M.ev_uid[nxt][o] = cu;
+            M.ev_ctx[nxt][o] = M.ch_ctx[sl];
+            M.ev_kind[nxt][o] = M.ch_kind[sl];
+            M.ev_a[nxt][o] = M.ch_a[sl];
+            M.ev_pkt[nxt][o] = M.ch_pkt[sl];
           } else {
             atomicOr(M.error, 1u);
           }
         }
         base += nc[q];
+        ibase += ni4[q];
       }
     }
-    K += W;
+    // (inline children at the Stop's ts are scheduled — uids consumed — but never dispatched; the run
+    //  ends with this window, so the pool bookkeeping below only has to be right for other windows)
+    K += W + total_inline;
     uid += total_children;
-    P += total_children;
+    P += total_children - total_inline;
     cur = nxt;
     windows++;
     max_window = W > max_window ? W : max_window;
@@ -703,8 +816,8 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
 
   // ---- reduce and publish counters ----
   __syncthreads();
-  uint64_t vals[4] = {digest, cancelled, ttl_drops, no_route};
-  for (int k = 0; k < 4; k++) {
+  uint64_t vals[5] = {digest, cancelled, ttl_drops, no_route, unreach};
+  for (int k = 0; k < 5; k++) {
     uint64_t v = vals[k];
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if (lane == 0) L.wmin[wid] = v;
@@ -724,6 +837,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
     M.stats->cancelled = vals[1];
     M.stats->ttl_drops = vals[2];
     M.stats->no_route_drops = vals[3];
+    M.stats->unreach_drops = vals[4];
     M.stats->next_uid = uid;
     M.stats->windows = (uint32_t)windows;
     M.stats->max_window = max_window;
@@ -916,6 +1030,10 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
         if (k >= A) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "setup: app %u", k); }
         its.push_back(0); iuid.push_back(uid); ictx.push_back(sc->app_node[k]); ikind.push_back(K_APPOBJ_START); ia.push_back(k);
         break;
+      case NSGPU_SETUP_NOOP:
+        if (k >= N) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "setup: noop node %u", k); }
+        its.push_back(0); iuid.push_back(uid); ictx.push_back(k); ikind.push_back(K_DEV_START); ia.push_back(k);
+        break;
       case NSGPU_SETUP_STOP:
         if (sc->stop_ns < 0) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "setup: negative stop"); }
         its.push_back((uint64_t)sc->stop_ns); iuid.push_back(uid); ictx.push_back(NOCTX); ikind.push_back(K_STOP); ia.push_back(0);
@@ -1031,6 +1149,6 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
   NSGPU_HIP(hipStreamSynchronize(s));
   if (error) *error = err;
   if (err) return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, "
-                                          "4 = window limit, 8 = window cut)", err);
+                                          "4 = window limit, 8 = window cut, 16 = inline children)", err);
   return NSGPU_OK;
 }

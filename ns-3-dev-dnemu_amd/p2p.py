@@ -20,7 +20,7 @@ import numpy as np
 import nsgpu
 
 APP_ONOFF, APP_SINK = 0, 1
-SETUP_NODE, SETUP_DEVICE, SETUP_APP, SETUP_STOP, SETUP_UID = 0, 1, 2, 3, 4
+SETUP_NODE, SETUP_DEVICE, SETUP_APP, SETUP_STOP, SETUP_UID, SETUP_NOOP = 0, 1, 2, 3, 4, 5
 NO_ROUTE = 0xFFFFFFFF
 
 
@@ -41,7 +41,8 @@ class ScenarioStruct(C.Structure):
 class P2PStats(C.Structure):
     _fields_ = [("dispatched", C.c_uint64), ("cancelled", C.c_uint64), ("digest", C.c_uint64),
                 ("final_ts", C.c_uint64), ("next_uid", C.c_uint32), ("windows", C.c_uint32),
-                ("ttl_drops", C.c_uint64), ("no_route_drops", C.c_uint64), ("max_window", C.c_uint64)]
+                ("ttl_drops", C.c_uint64), ("no_route_drops", C.c_uint64), ("max_window", C.c_uint64),
+                ("unreach_drops", C.c_uint64)]
 
 
 DEV_COUNTERS_DTYPE = np.dtype([("enq_packets", "<u4"), ("enq_bytes", "<u4"), ("drop_packets", "<u4"),
@@ -55,16 +56,31 @@ class Scenario:
     """Arrays of a nsgpu_p2p_scenario plus the order of setup-time Schedule calls."""
 
     def __init__(self, n_nodes):
-        self.n_nodes = n_nodes
+        self.n_nodes = 0
         self.dev = []     # (node, peer, bps, ifg, delay, qmax)
         self.apps = []    # dicts
         self.setup = []   # (kind, index)
         self.stop_ns = -1
-        for n in range(n_nodes):
-            self.setup.append((SETUP_NODE, n))
         self.route = None
         self.n_dst = 0
         self.dst_slot = {}
+        for _ in range(n_nodes):
+            self.add_node()
+
+    def add_node(self):
+        # the first Node creates the NodeListPriv singleton: ScheduleDestroy (&NodeListPriv::Delete)
+        # consumes a uid (node-list.cc:80-90), then NodeListPriv::Add schedules Node::Start (:124-131)
+        if self.n_nodes == 0:
+            self.setup.append((SETUP_UID, 0))
+        self.setup.append((SETUP_NODE, self.n_nodes))
+        self.n_nodes += 1
+        return self.n_nodes - 1
+
+    def install_stack(self):
+        # InternetStackHelper::Install: Ipv4L3Protocol::SetupLoopback adds a LoopbackNetDevice to each
+        # node (ipv4-l3-protocol.cc:227-244) -> Node::AddDevice -> ScheduleWithContext (node, 0, Start)
+        for n in range(self.n_nodes):
+            self.setup.append((SETUP_NOOP, n))
 
     # PointToPointHelper::Install (a, b): device on a, then device on b, one channel
     def link(self, a, b, bps, delay_ns, qmax=100, ifg_ns=0):
@@ -73,6 +89,8 @@ class Scenario:
         self.setup.append((SETUP_DEVICE, da))
         self.dev.append([b, da, bps, ifg_ns, delay_ns, qmax])
         self.setup.append((SETUP_DEVICE, db))
+        if da == 0:  # the first channel creates the ChannelListPriv singleton: ScheduleDestroy (channel-list.cc:80-90)
+            self.setup.append((SETUP_UID, 0))
         return da, db
 
     def add_sink(self, node, start_ns, stop_ns):
@@ -170,14 +188,12 @@ def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="column
     flows="columns": one flow per column from row 0 to the last row (SURVEY §8(d) config 4);
     routes are XY (row first, then column) static next hops."""
     sc = Scenario(0)
-    sc.setup = []
     nid = lambda y, x: y * cols + x  # noqa: E731
     row_dev = {}
     col_dev = {}
     for y in range(rows):
         for x in range(cols):
-            sc.setup.append((SETUP_NODE, nid(y, x)))  # rowNodes.Create (1)
-            sc.n_nodes += 1
+            sc.add_node()  # rowNodes.Create (1)
             if x > 0:
                 da, db = sc.link(nid(y, x - 1), nid(y, x), bps, delay_ns, qmax)
                 row_dev[(nid(y, x - 1), nid(y, x))] = da
@@ -186,6 +202,7 @@ def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="column
                 da, db = sc.link(nid(y - 1, x), nid(y, x), bps, delay_ns, qmax)
                 col_dev[(nid(y - 1, x), nid(y, x))] = da
                 col_dev[(nid(y, x), nid(y - 1, x))] = db
+    sc.install_stack()  # PointToPointGridHelper::InstallStack (point-to-point-grid.cc:79-89)
     fl = []
     if flows == "columns":
         ncol = cols if n_flows is None else min(cols, n_flows)
@@ -236,6 +253,7 @@ def random_topology(n_nodes, n_links, n_flows, seed, bps_choices=(1_000_000, 5_0
         edges.add((a, b))
     for a, b in sorted(edges):
         sc.link(a, b, int(rng.choice(bps_choices)), int(rng.choice(delay_choices)), qmax)
+    sc.install_stack()
     flows = []
     for _ in range(n_flows):
         s_, d = rng.choice(n_nodes, 2, replace=False).tolist()

@@ -17,6 +17,7 @@
 #include <vector>
 #include <deque>
 #include <chrono>
+#include <functional>
 #include <string.h>
 #include <stdio.h>
 #include "nsref_engine.hpp"
@@ -58,7 +59,7 @@ struct Model {
   std::vector<App> app;
   std::vector<std::vector<uint32_t>> node_apps;
   std::vector<int32_t> sink_of_node;
-  uint64_t ttl_drops = 0, no_route_drops = 0;
+  uint64_t ttl_drops = 0, no_route_drops = 0, unreach_drops = 0;
 
   template <class F>
   struct Ev : EventImpl {
@@ -140,12 +141,21 @@ struct Model {
   // ---------------- IPv4 + UDP ----------------
   void ip_receive(uint32_t n, Pkt p) {  // Ipv4L3Protocol::Receive -> RouteInput
     const uint32_t a = p.app;
-    if (s.app_dst_node[a] == n) {  // LocalDeliver -> UdpL4Protocol::Receive -> PacketSink::HandleRead
+    if (s.app_dst_node[a] == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
       const int32_t k = sink_of_node[n];
-      if (k >= 0 && app[k].sink_active) {
-        app[k].c.rx_packets++;
-        app[k].c.rx_bytes += p.size - 28;
+      if (k < 0 || !app[k].sink_active) {  // no bound endpoint: RX_ENDPOINT_UNREACH
+        unreach_drops++;
+        return;
       }
+      // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120)
+      const uint32_t bytes = p.size - 28;
+      sim.ScheduleNow(new Ev<std::function<void()>>([this, k, bytes]() {
+        // DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink::HandleRead
+        if (app[k].sink_active) {
+          app[k].c.rx_packets++;
+          app[k].c.rx_bytes += bytes;
+        }
+      }));
       return;
     }
     const uint32_t out = s.route[(uint64_t)n * s.n_dst + s.app_dst_slot[a]];
@@ -272,7 +282,10 @@ struct Model {
         case NSGPU_SETUP_STOP:  // Simulator::Stop (Time) (default-simulator-impl.cc:179-183)
           schedule(s.stop_ns, [this]() { sim.m_stop = true; });
           break;
-        default:
+        case NSGPU_SETUP_NOOP:  // e.g. LoopbackNetDevice added by Ipv4L3Protocol::SetupLoopback
+          schedule_ctx(k, 0, []() {});
+          break;
+        default:  // a setup call consuming a uid without a queued event (ScheduleDestroy)
           sim.m_uid++;
       }
     }
@@ -304,6 +317,7 @@ extern "C" int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stat
   stats->next_uid = m->sim.m_uid;
   stats->ttl_drops = m->ttl_drops;
   stats->no_route_drops = m->no_route_drops;
+  stats->unreach_drops = m->unreach_drops;
   if (devc)
     for (uint32_t d = 0; d < sc->n_devices; d++) devc[d] = m->dev[d].c;
   if (appc)

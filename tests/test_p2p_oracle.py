@@ -22,7 +22,11 @@ def test_grid_builder_mirrors_helper_order():
     g = p2p.grid(3, 4)
     # node (y, x) creation interleaved with its row link then column link (point-to-point-grid.cc:45-64)
     kinds = [k for k, _ in g.setup]
-    assert kinds[:3] == [p2p.SETUP_NODE, p2p.SETUP_NODE, p2p.SETUP_DEVICE]
+    # NodeListPriv singleton's ScheduleDestroy, node 0, node 1, its row link (2 devices), then the
+    # ChannelListPriv singleton's ScheduleDestroy (channel created after both devices)
+    assert kinds[:6] == [p2p.SETUP_UID, p2p.SETUP_NODE, p2p.SETUP_NODE, p2p.SETUP_DEVICE, p2p.SETUP_DEVICE,
+                         p2p.SETUP_UID]
+    assert kinds.count(p2p.SETUP_NOOP) == 12  # one LoopbackNetDevice per node
     assert len(g.dev) == 2 * (3 * 3 + 2 * 4)  # rows*(cols-1) + (rows-1)*cols links
     assert sum(1 for k in kinds if k == p2p.SETUP_NODE) == 12
     # every node routes to every destination, by XY
