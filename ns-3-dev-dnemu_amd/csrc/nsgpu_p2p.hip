@@ -93,6 +93,7 @@ struct P2PDev {
   uint32_t *log_uid, *log_ctx;
   uint64_t log_cap;
   uint64_t max_windows;
+  uint64_t *prof;  // diagnostic: per-phase s_memtime cycle sums (wave 0 view), or null
 };
 
 struct P2PLds {
@@ -455,6 +456,14 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
   uint64_t windows = 0, max_window = 0, last_ts = 0;
   if (tid == 0) L.stop_flag = 0;
   __syncthreads();
+  uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev = M.prof ? __builtin_amdgcn_s_memtime() : 0;
+#define PSTAMP(i)                                        \
+  if (M.prof) {                                          \
+    const uint64_t tnow_ = __builtin_amdgcn_s_memtime(); \
+    pacc[i] += tnow_ - tprev;                            \
+    tprev = tnow_;                                       \
+  }
 
   while (P > 0) {
     if (windows >= M.max_windows) {
@@ -464,6 +473,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
     const uint64_t *ts = M.ev_ts[cur];
     const uint32_t *uidv = M.ev_uid[cur];
     const uint32_t *kindv = M.ev_kind[cur];
+    PSTAMP(6);
     // ---- 1. tmin, W_end = min (ts + L(kind)), stop key ----
     uint64_t tmin = INF, wend = INF, stopkey = INF;
     for (uint64_t i = tid; i < P; i += P2P_THREADS) {
@@ -506,6 +516,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       bound = stop_packed < bound ? stop_packed : bound;
       __syncthreads();
     }
+    PSTAMP(0);
     // ---- count; if the window would exceed WCAP, bisect for the largest key bound that fits ----
     // (any key prefix of a safe window is safe: its children still sort after every kept event)
     auto count_le = [&](uint64_t bnd) -> uint32_t {
@@ -538,6 +549,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
     // ends at the Stop event, those at the Stop's ts sort after it and are never dispatched
     const bool has_stop = stop_packed != INF && bound >= stop_packed;
     const uint64_t inline_ts_limit = has_stop ? (stop_packed >> 32) : INF;  // relative ts (exclusive)
+    PSTAMP(1);
     // ---- 2. partition: window -> sort registers; rest -> next pool ----
     const int nxt = cur ^ 1;
     uint64_t skey[4];
@@ -592,6 +604,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       __syncthreads();
       P = tot_out;  // survivors; children are appended after them
     }
+    PSTAMP(2);
     // ---- 3. sort by key -> dispatch rank ----
     bitonic_sort_4096(skey, sval, L.sort);
     // rank r = 256*wid + 64*q + lane holds pool index sval[q]; publish pool index by rank
@@ -638,6 +651,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       L.ninl[g] = 0;
     }
     __syncthreads();
+    PSTAMP(3);
     // ---- 4. handlers: the first entry of each node group runs the group's events in rank order ----
     // Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) are
     // run by the same thread at their key position: after every node event with ts <= theirs, before
@@ -702,6 +716,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       }
     }
     __syncthreads();
+    PSTAMP(4);
     // ---- 5. uids: exclusive scan of child counts in rank order; dispatch ranks; children -> next pool ----
     uint32_t nc[4], ni4[4], tsum = 0, isum = 0;
 #pragma unroll
@@ -814,6 +829,9 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
     __threadfence_block();
   }
 
+  if (M.prof && tid == 0)
+    for (int i = 0; i < 8; i++) M.prof[i] = pacc[i];
+#undef PSTAMP
   // ---- reduce and publish counters ----
   __syncthreads();
   uint64_t vals[5] = {digest, cancelled, ttl_drops, no_route, unreach};
@@ -1120,6 +1138,12 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
   NSGPU_HIP(hipMemsetAsync(M.stats, 0, sizeof(nsgpu_p2p_stats), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_set_profile(nsgpu_p2p *h, uint64_t *d_phase_cycles) {
+  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_profile: null");
+  h->M.prof = d_phase_cycles;
   return NSGPU_OK;
 }
 

@@ -95,6 +95,7 @@ SIGNATURES = {
     "nsgpu_p2p_run": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_results": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
     "nsgpu_p2p_destroy": (C.c_int, [_vp]),
+    "nsgpu_p2p_set_profile": (C.c_int, [_vp, _vp]),
     "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
 }
 
