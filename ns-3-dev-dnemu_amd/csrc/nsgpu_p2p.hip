@@ -44,10 +44,11 @@ enum EvKind : uint32_t {
   K_NKINDS = 13
 };
 
-constexpr int P2P_THREADS = 1024;
+constexpr int P2P_THREADS = 512;
 constexpr int WCAP = SORT_N;  // events per window
+constexpr int RPT = WCAP / P2P_THREADS;  // window ranks per thread
 constexpr uint32_t NOCTX = 0xffffffffu;
-constexpr int INLINE_MAX = 32;  // inline children pending at one ts on one node
+constexpr uint32_t NOCHAIN = 0xffffffffu;
 
 struct Pkt {
   uint32_t app, seq, size, ttl;
@@ -94,6 +95,7 @@ struct P2PDev {
   uint64_t log_cap;
   uint64_t max_windows;
   uint64_t *prof;  // diagnostic: per-phase s_memtime cycle sums (wave 0 view), or null
+  uint32_t *node_head;  // per-node chain head of the current window (NOCHAIN between windows)
 };
 
 struct P2PLds {
@@ -442,7 +444,8 @@ __device__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t
   }
 }
 
-__global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *__restrict__ sink_of_node) {
+__global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict__ Mp, const int32_t *__restrict__ sink_of_node) {
+  const P2PDev &M = *Mp;  // in global memory: fields come through scalar loads, not 70 SGPR kernel args
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   P2PLds &L = *reinterpret_cast<P2PLds *>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -550,15 +553,8 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
     const bool has_stop = stop_packed != INF && bound >= stop_packed;
     const uint64_t inline_ts_limit = has_stop ? (stop_packed >> 32) : INF;  // relative ts (exclusive)
     PSTAMP(1);
-    // ---- 2. partition: window -> sort registers; rest -> next pool ----
+    // ---- 2. partition: window -> LDS list (packed key, pool index); rest -> next pool ----
     const int nxt = cur ^ 1;
-    uint64_t skey[4];
-    uint32_t sval[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      skey[q] = INF;
-      sval[q] = 0xffffffffu;
-    }
     {
       // each thread handles a contiguous range of the pool; window slots by block scan
       const uint64_t per = (P + P2P_THREADS - 1) / P2P_THREADS;
@@ -573,7 +569,6 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       uint32_t tot_in, tot_out;
       uint32_t win_off = block_exscan(nin, L.wsum, &tot_in);
       uint32_t out_off = block_exscan(nout, L.wsum, &tot_out);
-      // stage window (key, pool index) in LDS buffer 0 at win_off..; copy the rest to the next pool
       for (uint64_t i = i0; i < i1; i++) {
         const uint64_t t = ts[i];
         const uint64_t pk = ((t - tmin) << 32) | uidv[i];
@@ -592,100 +587,184 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
           out_off++;
         }
       }
+      P = tot_out;  // survivors; children are appended after them
+    }
+    // clear the bucket histogram (sort.v[1]) and fill counters (nchild)
+    for (int i = tid; i < WCAP; i += P2P_THREADS) {
+      L.sort.v[1][i] = 0;
+      L.nchild[i] = 0;
+    }
+    __syncthreads();
+    PSTAMP(2);
+    // ---- 3. dispatch rank: bucket sort of the packed keys by relative ts (bitonic if a bucket is crowded) ----
+    {
+      uint64_t rmax = 0;
+      for (int i = tid; i < (int)W; i += P2P_THREADS) {
+        const uint64_t r = L.sort.k[0][i] >> 32;
+        rmax = r > rmax ? r : rmax;
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(rmax, o);
+        rmax = w > rmax ? w : rmax;
+      }
+      if (lane == 0) L.wmin[wid] = rmax;
       __syncthreads();
+      rmax = 0;
+      for (int w = 0; w < P2P_THREADS / 64; w++) rmax = L.wmin[w] > rmax ? L.wmin[w] : rmax;
+      const uint64_t denom = rmax + 1;
+      for (int i = tid; i < (int)W; i += P2P_THREADS) {
+        const uint32_t bk = (uint32_t)(((L.sort.k[0][i] >> 32) * (uint64_t)WCAP) / denom);
+        atomicAdd(&L.sort.v[1][bk], 1u);
+      }
+      __syncthreads();
+      // exclusive scan of the 4096 bucket counts (4 per thread) and the largest bucket
+      uint32_t bc[RPT], bs = 0, bmax = 0;
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int i = 256 * wid + 64 * q + lane;
-        if (i < (int)W) {
-          skey[q] = L.sort.k[0][i];
-          sval[q] = L.sort.v[0][i];
+      for (int q = 0; q < RPT; q++) {
+        bc[q] = L.sort.v[1][tid * RPT + q];
+        bs += bc[q];
+        bmax = bc[q] > bmax ? bc[q] : bmax;
+      }
+      uint32_t btot;
+      uint32_t bstart = block_exscan(bs, L.wsum, &btot);
+#pragma unroll
+      for (int q = 0; q < RPT; q++) {
+        L.sort.v[1][tid * RPT + q] = bstart;
+        bstart += bc[q];
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = __shfl_xor(bmax, o);
+        bmax = w > bmax ? w : bmax;
+      }
+      if (lane == 0) L.wcnt[wid] = bmax;
+      __syncthreads();
+      bmax = 0;
+      for (int w = 0; w < P2P_THREADS / 64; w++) bmax = L.wcnt[w] > bmax ? L.wcnt[w] : bmax;
+      if (bmax > 32) {
+        // crowded buckets (e.g. the setup burst at ts 0): workgroup bitonic sort
+        uint64_t skey[RPT];
+        uint32_t sval[RPT];
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+          const int i = 64 * RPT * wid + 64 * q + lane;
+          skey[q] = i < (int)W ? L.sort.k[0][i] : INF;
+          sval[q] = i < (int)W ? L.sort.v[0][i] : 0xffffffffu;
+        }
+        __syncthreads();
+        bitonic_sort<P2P_THREADS>(skey, sval, L.sort);
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+          const int r = 64 * RPT * wid + 64 * q + lane;
+          L.sort.k[0][r] = skey[q];
+          L.sort.v[0][r] = sval[q];
+        }
+      } else {
+        // scatter into buckets (sort.k[1] keys, ninl pool indices), then sort each bucket in place
+        for (int i = tid; i < (int)W; i += P2P_THREADS) {
+          const uint64_t pk = L.sort.k[0][i];
+          const uint32_t bk = (uint32_t)(((pk >> 32) * (uint64_t)WCAP) / denom);
+          const uint32_t pos = L.sort.v[1][bk] + atomicAdd(&L.nchild[bk], 1u);
+          L.sort.k[1][pos] = pk;
+          L.ninl[pos] = L.sort.v[0][i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+          const uint32_t bk = tid * RPT + q;
+          const uint32_t c = L.nchild[bk];
+          if (c > 1) {
+            const uint32_t s0 = L.sort.v[1][bk];
+            for (uint32_t x = s0 + 1; x < s0 + c; x++) {  // insertion sort (c <= 32)
+              const uint64_t kx = L.sort.k[1][x];
+              const uint32_t vx = L.ninl[x];
+              uint32_t y = x;
+              while (y > s0 && L.sort.k[1][y - 1] > kx) {
+                L.sort.k[1][y] = L.sort.k[1][y - 1];
+                L.ninl[y] = L.ninl[y - 1];
+                y--;
+              }
+              L.sort.k[1][y] = kx;
+              L.ninl[y] = vx;
+            }
+          }
+        }
+        __syncthreads();
+        for (int r = tid; r < (int)W; r += P2P_THREADS) {
+          L.sort.k[0][r] = L.sort.k[1][r];
+          L.sort.v[0][r] = L.ninl[r];
         }
       }
       __syncthreads();
-      P = tot_out;  // survivors; children are appended after them
     }
-    PSTAMP(2);
-    // ---- 3. sort by key -> dispatch rank ----
-    bitonic_sort_4096(skey, sval, L.sort);
-    // rank r = 256*wid + 64*q + lane holds pool index sval[q]; publish pool index by rank
-    // (L.sort.v[0] reused as rank -> pool index), then sort (ctx << 32 | rank) to group by node
-    uint64_t gkey[4];
-    uint32_t gval[4];
+    // ---- group by node: per-node chains through a global head array (one atomicExch per event) ----
+    uint32_t rctx[RPT];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int r = 256 * wid + 64 * q + lane;
+    for (int q = 0; q < RPT; q++) {
+      const int r = tid + P2P_THREADS * q;
+      rctx[q] = NOCTX;
       if (r < (int)W) {
-        const uint32_t pi = sval[q];
-        L.sort.v[0][r] = pi;
-        L.sort.k[0][r] = skey[q];
-        const uint32_t c = M.ev_ctx[cur][pi];
-        gkey[q] = ((uint64_t)c << 32) | (uint32_t)r;
-        gval[q] = (uint32_t)r;
-      } else {
-        gkey[q] = INF;
-        gval[q] = 0xffffffffu;
+        const uint32_t c = M.ev_ctx[cur][L.sort.v[0][r]];
+        rctx[q] = c;
+        L.sort.v[1][r] = c < M.n_nodes ? atomicExch(&M.node_head[c], (uint32_t)r) : NOCHAIN;
       }
-    }
-    __syncthreads();
-    // copy rank->pool map out of the sort buffers before the second sort reuses them
-    uint32_t rank_pool[4];
-    uint64_t rank_key[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int r = 256 * wid + 64 * q + lane;
-      rank_pool[q] = r < (int)W ? L.sort.v[0][r] : 0;
-      rank_key[q] = r < (int)W ? L.sort.k[0][r] : INF;
-    }
-    __syncthreads();
-    bitonic_sort_4096(gkey, gval, L.sort);
-    // publish: grouped position g -> rank (buffer v[1]); rank -> pool index (v[0]); rank -> key (k[0])
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int g = 256 * wid + 64 * q + lane;
-      L.sort.v[1][g] = gval[q];
-      L.sort.k[1][g] = gkey[q];
-      const int r = g;  // rank-indexed arrays
-      L.sort.v[0][r] = rank_pool[q];
-      L.sort.k[0][r] = rank_key[q];
-      L.nchild[g] = 0;
-      L.ninl[g] = 0;
+      if (r < WCAP) {
+        L.nchild[r] = 0;
+        L.ninl[r] = 0;
+      }
     }
     __syncthreads();
     PSTAMP(3);
-    // ---- 4. handlers: the first entry of each node group runs the group's events in rank order ----
-    // Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) are
-    // run by the same thread at their key position: after every node event with ts <= theirs, before
-    // the first with a larger ts (their uid is larger than every pending uid).
+    // ---- 4. handlers: the node's last exchanger walks the node's chain in rank order ----
+    // Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) run at
+    // their key position: after the node's events with ts <= theirs, before the first with a larger ts.
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int g = 256 * wid + 64 * q + lane;
-      if (g >= (int)W) continue;
-      const uint32_t c = (uint32_t)(L.sort.k[1][g] >> 32);
-      if (g > 0 && (uint32_t)(L.sort.k[1][g - 1] >> 32) == c) continue;  // not the group head
+    for (int q = 0; q < RPT; q++) {
+      const int r0 = tid + P2P_THREADS * q;
+      if (r0 >= (int)W) continue;
+      const uint32_t c = rctx[q];
+      if (c < M.n_nodes) {
+        const uint32_t head = __hip_atomic_load(&M.node_head[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (head != (uint32_t)r0) continue;  // not the chain holder
+        __hip_atomic_store(&M.node_head[c], NOCHAIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       const int32_t sink = c < M.n_nodes ? sink_of_node[c] : -1;
-      uint32_t pend[INLINE_MAX];  // child slots of pending inline children, all at ts pend_ts
-      uint32_t npend = 0;
-      uint64_t pend_ts = 0;
-      for (int h = g; h <= (int)W; h++) {
-        const bool more = h < (int)W && (uint32_t)(L.sort.k[1][h] >> 32) == c;
-        const uint32_t r = more ? L.sort.v[1][h] : 0;
-        const uint64_t rel = more ? (L.sort.k[0][r] >> 32) : INF;
-        if (npend && rel > pend_ts) {  // flush inline children that sort before this event
-          for (uint32_t i = 0; i < npend; i++) {
-            const uint32_t sl = pend[i];
-            Emit E0;
-            E0.M = &M;
-            E0.now = tmin + pend_ts;
-            E0.ctx = c;
-            E0.slot0 = 0;
-            E0.n = 0;
-            bool st0 = false;
-            run_event(M, E0, M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl], sink, &ttl_drops, &no_route, &unreach,
-                      &st0);
+      uint32_t n = 0;
+      for (uint32_t x = (uint32_t)r0; x != NOCHAIN; x = L.sort.v[1][x]) n++;
+      int64_t last = -1;
+      uint32_t ts0_rank = 0, pending = 0;
+      uint64_t cur_rel = 0;
+      for (uint32_t it = 0; it <= n; it++) {
+        uint32_t r = NOCHAIN;
+        if (it < n)
+          for (uint32_t x = (uint32_t)r0; x != NOCHAIN; x = L.sort.v[1][x])
+            if ((int64_t)x > last && x < r) r = x;
+        const uint64_t rel = it < n ? (L.sort.k[0][r] >> 32) : INF;
+        if (it > 0 && rel > cur_rel && pending) {
+          // flush the inline children of this node's events at cur_rel (ranks in [ts0_rank, r))
+          for (uint32_t x = (uint32_t)r0; x != NOCHAIN; x = L.sort.v[1][x]) {
+            if (x < ts0_rank || x >= r) continue;
+            const uint32_t ncr = L.nchild[x];
+            for (uint32_t j = 0; j < ncr; j++) {
+              const uint32_t sl = x * M.maxc + j;
+              if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
+              Emit E0;
+              E0.M = &M;
+              E0.now = tmin + cur_rel;
+              E0.ctx = c;
+              E0.slot0 = 0;
+              E0.n = 0;
+              bool st0 = false;
+              run_event(M, E0, M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl], sink, &ttl_drops, &no_route, &unreach,
+                        &st0);
+            }
           }
-          npend = 0;
+          pending = 0;
         }
-        if (!more) break;
+        if (it == n) break;
+        if (it == 0 || rel > cur_rel) {
+          ts0_rank = r;
+          cur_rel = rel;
+        }
         const uint32_t pi = L.sort.v[0][r];
         Emit E;
         E.M = &M;
@@ -700,29 +779,21 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
         L.nchild[r] = E.n;
         if (stop) L.stop_flag = 1;
         uint32_t ni = 0;
-        for (uint32_t j = 0; j < E.n; j++) {
-          const uint32_t sl = E.slot0 + j;
-          if ((M.ch_kind[sl] & 0xffu) == K_FWD_UP && rel < inline_ts_limit) {
-            if (npend == INLINE_MAX) {
-              atomicOr(M.error, 16u);
-            } else {
-              pend[npend++] = sl;
-              pend_ts = rel;
-              ni++;
-            }
-          }
-        }
+        if (rel < inline_ts_limit)
+          for (uint32_t j = 0; j < E.n; j++) ni += (M.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
         L.ninl[r] = ni;
+        pending += ni;
+        last = r;
       }
     }
     __syncthreads();
     PSTAMP(4);
     // ---- 5. uids: exclusive scan of child counts in rank order; dispatch ranks; children -> next pool ----
-    uint32_t nc[4], ni4[4], tsum = 0, isum = 0;
+    uint32_t nc[RPT], ni4[RPT], tsum = 0, isum = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      nc[q] = L.nchild[tid * 4 + q];
-      ni4[q] = L.ninl[tid * 4 + q];
+    for (int q = 0; q < RPT; q++) {
+      nc[q] = L.nchild[tid * RPT + q];
+      ni4[q] = L.ninl[tid * RPT + q];
       tsum += nc[q];
       isum += ni4[q];
     }
@@ -732,8 +803,8 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
     {
       uint32_t ib = ibase;
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        L.iprefix[tid * 4 + q] = ib;
+      for (int q = 0; q < RPT; q++) {
+        L.iprefix[tid * RPT + q] = ib;
         ib += ni4[q];
       }
     }
@@ -759,8 +830,8 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(P2PDev M, const int32_t *
       return lo - 1;
     };
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const uint32_t r = tid * 4 + q;
+    for (int q = 0; q < RPT; q++) {
+      const uint32_t r = tid * RPT + q;
       if (r < W) {
         const uint64_t pk = L.sort.k[0][r];
         const uint64_t rel = pk >> 32;
@@ -878,6 +949,7 @@ struct nsgpu_p2p {
   nsgpu_p2p_scenario sc;
   std::vector<void *> allocs;
   int32_t *sink_of_node = nullptr;
+  P2PDev *d_M = nullptr;  // device copy of M (kernel argument by pointer)
   // pristine initial pool (device) for resets
   uint64_t *init_ts = nullptr;
   uint32_t *init_uid = nullptr, *init_ctx = nullptr, *init_kind = nullptr, *init_a = nullptr;
@@ -1029,6 +1101,7 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   TRY(dalloc(h, &M.app_seq, A));
   TRY(dalloc(h, &M.app_last_start, A));
   TRY(dalloc(h, &M.appc, A));
+  TRY(dalloc(h, &M.node_head, N));
   // ---- setup-time events (node-list.cc:124-131, node.cc:111-145, default-simulator-impl.cc:179-183) ----
   std::vector<uint64_t> its;
   std::vector<uint32_t> iuid, ictx, ikind, ia;
@@ -1109,6 +1182,7 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
     }
     attr = true;
   }
+  TRY(dalloc(h, &h->d_M, 1));
   *out = h;
   return NSGPU_OK;
 }
@@ -1136,6 +1210,7 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.app_seq, 0, A * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.app_last_start, 0, A * sizeof(uint64_t), s));
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
+  NSGPU_HIP(hipMemsetAsync(M.node_head, 0xff, M.n_nodes * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.stats, 0, sizeof(nsgpu_p2p_stats), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
   return NSGPU_OK;
@@ -1149,7 +1224,8 @@ extern "C" int nsgpu_p2p_set_profile(nsgpu_p2p *h, uint64_t *d_phase_cycles) {
 
 extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_run: null");
-  hipLaunchKernelGGL(p2p_run, dim3(1), dim3(P2P_THREADS), sizeof(P2PLds), (hipStream_t)stream, h->M,
+  NSGPU_HIP(hipMemcpyAsync(h->d_M, &h->M, sizeof(P2PDev), hipMemcpyHostToDevice, (hipStream_t)stream));
+  hipLaunchKernelGGL(p2p_run, dim3(1), dim3(P2P_THREADS), sizeof(P2PLds), (hipStream_t)stream, h->d_M,
                      h->sink_of_node);
   NSGPU_HIP(hipGetLastError());
   return NSGPU_OK;
@@ -1173,6 +1249,6 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
   NSGPU_HIP(hipStreamSynchronize(s));
   if (error) *error = err;
   if (err) return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, "
-                                          "4 = window limit, 8 = window cut, 16 = inline children)", err);
+                                          "4 = window limit, 8 = window cut)", err);
   return NSGPU_OK;
 }
