@@ -170,7 +170,7 @@ int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev_counters *
                       uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_n, uint32_t *error,
                       void *stream);
 int nsgpu_p2p_destroy(nsgpu_p2p *h);
-/* Diagnostic: per-window-phase s_memtime cycle sums (8 x uint64, device) for later runs; NULL = off. */
+/* Diagnostic: per-window-phase s_memtime cycle sums (16 x uint64, device) for later runs; NULL = off. */
 int nsgpu_p2p_set_profile(nsgpu_p2p *h, uint64_t *d_phase_cycles);
 
 #ifdef __cplusplus

@@ -360,7 +360,7 @@ __device__ void appobj_start(const P2PDev &M, Emit &E, uint32_t a) {  // Applica
 }
 
 // Runs one event; returns true if it was a cancelled dispatch.
-__device__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a, const Pkt &pkt, int32_t sink,
+__device__ __noinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a, const Pkt &pkt, int32_t sink,
                           uint64_t *ttl_drops, uint64_t *no_route, uint64_t *unreach, bool *stop) {
   const uint32_t kind = kind_word & 0xffu;
   const uint32_t gen = kind_word >> 8;
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
   uint64_t windows = 0, max_window = 0, last_ts = 0;
   if (tid == 0) L.stop_flag = 0;
   __syncthreads();
-  uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t pacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tprev = M.prof ? __builtin_amdgcn_s_memtime() : 0;
 #define PSTAMP(i)                                        \
   if (M.prof) {                                          \
@@ -640,24 +640,13 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
       __syncthreads();
       bmax = 0;
       for (int w = 0; w < P2P_THREADS / 64; w++) bmax = L.wcnt[w] > bmax ? L.wcnt[w] : bmax;
+      PSTAMP(7);
       if (bmax > 32) {
-        // crowded buckets (e.g. the setup burst at ts 0): workgroup bitonic sort
-        uint64_t skey[RPT];
-        uint32_t sval[RPT];
-#pragma unroll
-        for (int q = 0; q < RPT; q++) {
-          const int i = 64 * RPT * wid + 64 * q + lane;
-          skey[q] = i < (int)W ? L.sort.k[0][i] : INF;
-          sval[q] = i < (int)W ? L.sort.v[0][i] : 0xffffffffu;
-        }
+        if (M.prof) pacc[9]++;
+        // crowded buckets (equal timestamps: lockstep sources, the setup burst at ts 0): wave-run
+        // sort + cross-run ranking
         __syncthreads();
-        bitonic_sort<P2P_THREADS>(skey, sval, L.sort);
-#pragma unroll
-        for (int q = 0; q < RPT; q++) {
-          const int r = 64 * RPT * wid + 64 * q + lane;
-          L.sort.k[0][r] = skey[q];
-          L.sort.v[0][r] = sval[q];
-        }
+        run_rank_sort<P2P_THREADS>(L.sort, W);
       } else {
         // scatter into buckets (sort.k[1] keys, ninl pool indices), then sort each bucket in place
         for (int i = tid; i < (int)W; i += P2P_THREADS) {
@@ -668,7 +657,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
           L.ninl[pos] = L.sort.v[0][i];
         }
         __syncthreads();
-#pragma unroll
+#pragma unroll 1
         for (int q = 0; q < RPT; q++) {
           const uint32_t bk = tid * RPT + q;
           const uint32_t c = L.nchild[bk];
@@ -695,16 +684,17 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
         }
       }
       __syncthreads();
+      PSTAMP(8);
     }
     // ---- group by node: per-node chains through a global head array (one atomicExch per event) ----
-    uint32_t rctx[RPT];
+    // (sort.k[1] is free after the sort: it holds each rank's context)
+    uint32_t *const Lctx = reinterpret_cast<uint32_t *>(&L.sort.k[1][0]);
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
       const int r = tid + P2P_THREADS * q;
-      rctx[q] = NOCTX;
       if (r < (int)W) {
         const uint32_t c = M.ev_ctx[cur][L.sort.v[0][r]];
-        rctx[q] = c;
+        Lctx[r] = c;
         L.sort.v[1][r] = c < M.n_nodes ? atomicExch(&M.node_head[c], (uint32_t)r) : NOCHAIN;
       }
       if (r < WCAP) {
@@ -717,11 +707,11 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
     // ---- 4. handlers: the node's last exchanger walks the node's chain in rank order ----
     // Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) run at
     // their key position: after the node's events with ts <= theirs, before the first with a larger ts.
-#pragma unroll
+#pragma unroll 1
     for (int q = 0; q < RPT; q++) {
       const int r0 = tid + P2P_THREADS * q;
       if (r0 >= (int)W) continue;
-      const uint32_t c = rctx[q];
+      const uint32_t c = Lctx[r0];
       if (c < M.n_nodes) {
         const uint32_t head = __hip_atomic_load(&M.node_head[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (head != (uint32_t)r0) continue;  // not the chain holder
@@ -829,7 +819,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
       }
       return lo - 1;
     };
-#pragma unroll
+#pragma unroll 1
     for (int q = 0; q < RPT; q++) {
       const uint32_t r = tid * RPT + q;
       if (r < W) {
@@ -848,9 +838,10 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
         }
         if (r == W - 1) last_ts = t;
         uint32_t lastr = 0;
-        if (ni4[q]) lastr = (r + 1 < W && (L.sort.k[0][r + 1] >> 32) == rel) ? last_same(r, rel) : r;
+        const uint32_t nir = L.ninl[r], ncr = L.nchild[r];
+        if (nir) lastr = (r + 1 < W && (L.sort.k[0][r + 1] >> 32) == rel) ? last_same(r, rel) : r;
         uint32_t ii = 0, nonin = base - (ibase);  // non-inline children before this rank
-        for (uint32_t j = 0; j < nc[q]; j++) {
+        for (uint32_t j = 0; j < ncr; j++) {
           const uint32_t sl = r * M.maxc + j;
           const uint32_t cu = uid + base + j;
           if ((M.ch_kind[sl] & 0xffu) == K_FWD_UP) {
@@ -879,8 +870,8 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
             atomicOr(M.error, 1u);
           }
         }
-        base += nc[q];
-        ibase += ni4[q];
+        base += ncr;
+        ibase += nir;
       }
     }
     // (inline children at the Stop's ts are scheduled — uids consumed — but never dispatched; the run
@@ -901,7 +892,7 @@ __global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict_
   }
 
   if (M.prof && tid == 0)
-    for (int i = 0; i < 8; i++) M.prof[i] = pacc[i];
+    for (int i = 0; i < 16; i++) M.prof[i] = pacc[i];
 #undef PSTAMP
   // ---- reduce and publish counters ----
   __syncthreads();
