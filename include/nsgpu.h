@@ -161,7 +161,8 @@ int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *di
  *   Ipv4L3Protocol::{Receive,IpForward} with static next-hop routes (ipv4-l3-protocol.cc:434-537,815-841)
  *   UdpL4Protocol::Receive -> PacketSink, OnOffApplication (onoff-application.cc:132-252)
  * and the DefaultSimulatorImpl run loop over them, entirely on the device.  nsgpu_p2p_reset
- * loads the post-setup state; nsgpu_p2p_run runs Simulator::Run to the Stop event (async). */
+ * loads the post-setup state; nsgpu_p2p_run runs Simulator::Run to the Stop event and returns when it
+ * is done (graph replays of the window pipeline on an engine stream, ordered after `stream`). */
 typedef struct nsgpu_p2p nsgpu_p2p;
 int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap, uint64_t log_cap, nsgpu_p2p **out);
 int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream);
@@ -170,8 +171,8 @@ int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev_counters *
                       uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_n, uint32_t *error,
                       void *stream);
 int nsgpu_p2p_destroy(nsgpu_p2p *h);
-/* Diagnostic: per-window-phase s_memtime cycle sums (16 x uint64, device) for later runs; NULL = off. */
-int nsgpu_p2p_set_profile(nsgpu_p2p *h, uint64_t *d_phase_cycles);
+/* GPU time (ms, HIP events on the engine stream) of the last nsgpu_p2p_run. */
+int nsgpu_p2p_last_run_ms(nsgpu_p2p *h, double *gpu_ms);
 
 #ifdef __cplusplus
 }

@@ -8,23 +8,26 @@
 //   queue      queue.cc:61-200, drop-tail-queue.cc:83-132
 //   IPv4/UDP   ipv4-l3-protocol.cc:434-537,815-841 (static next-hop routes, TTL)
 //
-// Engine (MI355X): one persistent 1024-thread workgroup runs the whole simulation in windows.
-// Pending events live in HBM (SoA, double-buffered pool).  Per window:
-//   1. W_end = min over pending e of (ts_e + L(kind_e)), L = the smallest delay any child of that
-//      kind of handler can have (DefaultSimulatorImpl's uids make a child sort after every pending
-//      event with ts <= its own ts, so every pending event with ts <= W_end is safe to dispatch);
-//      a Simulator::Stop event caps the window at its key; an over-full window is cut to its first
-//      WCAP keys by bisection (a key prefix of a safe window is safe);
-//   2. window keys are packed ((ts - tmin) << 32 | uid) and bitonic-sorted -> global dispatch rank;
-//   3. a second sort on (context << 32 | rank) groups the window by logical process (node); the
-//      first thread of each group runs that node's events sequentially in rank order, so node
-//      state (device tx state, DropTail rings, OnOff state, sink counters) needs no atomics;
-//   4. handlers write their children (in Schedule-call order) to per-rank slots; an exclusive scan
-//      of child counts in rank order gives each child the uid DefaultSimulatorImpl would assign;
-//      children are appended to the next pool.
+// Engine (MI355X).  The simulation advances in conservative windows; each window is a fixed pipeline
+// of short multi-CU kernels (a CU is 64 lanes per clock, so no phase may live on one CU), replayed
+// from a hipGraph of NWIN windows until the device-side `done` flag is set:
+//   k_reduce     W_end = min over pending e of (ts_e + L(kind_e)), L = the smallest delay any child of
+//                that kind of handler can have: DefaultSimulatorImpl's uids make a child sort after every
+//                pending event with ts <= its own, so every pending event with ts <= W_end is safe;
+//   k_partition  window keys ((ts - tmin) << 32 | uid, capped at the Simulator::Stop key) -> window
+//                list, the rest -> the other pool buffer (wave-aggregated atomic slots);
+//   k_refit      only when the window overflowed WCAP: bisection for the largest key prefix that fits
+//                (a key prefix of a safe window is safe), single workgroup;
+//   k_rank       dispatch rank of every window key by tiled all-pairs counting (WCAP^2 / 256 CUs);
+//   k_scatter    rank order; per-node chains through node_head (one atomicExch per event);
+//   k_handle     the chain holder of each node runs that node's events in rank order, so node state
+//                (device tx state, DropTail rings, OnOff state, sink counters) needs no atomics;
+//                children go to per-rank slots in Schedule-call order;
+//   k_scan       exclusive scans of child counts in rank order (uids), run bookkeeping;
+//   k_append     digest/log of the dispatch order, children -> pool with the uids DefaultSimulatorImpl
+//                would assign.
 #include "nsgpu_device.h"
 #include "nsgpu_internal.h"
-#include "nsgpu_sort.h"
 
 namespace nsgpu {
 
@@ -44,14 +47,34 @@ enum EvKind : uint32_t {
   K_NKINDS = 13
 };
 
-constexpr int P2P_THREADS = 512;
-constexpr int WCAP = SORT_N;  // events per window
-constexpr int RPT = WCAP / P2P_THREADS;  // window ranks per thread
+constexpr int WCAP = 4096;       // events per window
+constexpr int TB = 256;          // threads per block, pool sweeps and k_rank
+constexpr int RB = 64;           // threads per block, per-rank kernels (spread over CUs)
+constexpr int NT = WCAP / TB;    // rank tiles per side
+constexpr int GRID_POOL = 256;   // blocks of the pool sweeps (grid-stride)
+constexpr int SCAN_THREADS = 1024;
+constexpr int CH = 16;           // chain entries a handler thread sorts in LDS
+constexpr int NWIN = 32;         // windows per graph replay
 constexpr uint32_t NOCTX = 0xffffffffu;
 constexpr uint32_t NOCHAIN = 0xffffffffu;
 
 struct Pkt {
   uint32_t app, seq, size, ttl;
+};
+
+// Device-resident run control (one per engine); every field is written by one kernel of the window
+// pipeline and read by later ones, never read and written by different blocks of one kernel except
+// through atomics.
+struct Ctl {
+  uint64_t P;                  // pending events in pool `cur`
+  uint64_t K;                  // dispatched so far
+  uint64_t tmin, wend, stopts; // window reduction (atomicMin); ~0 between windows
+  uint64_t bound, span, inline_lim;
+  uint64_t windows, max_window, last_ts, max_windows;
+  uint64_t digest, cancelled, ttl_drops, no_route, unreach;
+  uint64_t K0, tmin0, inline_lim0;  // the window k_append works on (set by k_scan)
+  uint32_t uid, cur, W, nxtP, overflow, done, stop_seen, scan_ran;
+  uint32_t stopuid, uid0, W0, Pbase, total_children, total_inline, pad0, pad1;
 };
 
 // Device-resident model + engine state (all pointers are HBM).
@@ -81,37 +104,25 @@ struct P2PDev {
   uint32_t *ev_uid[2], *ev_ctx[2], *ev_kind[2], *ev_a[2];
   Pkt *ev_pkt[2];
   uint64_t pool_cap;
+  // the window (WCAP entries each): partition order (w*), rank order (s*, link, counts, prefixes)
+  uint64_t *wkey, *skey;
+  uint32_t *wpi, *wrank, *spi, *sctx, *link, *nchild, *ninl, *cpref, *ipref, *gbnd;
+  uint32_t *node_head;  // per-node chain head of the current window (NOCHAIN between windows)
   // children of the current window: slot = rank * maxc + j
   uint64_t *ch_ts;
   uint32_t *ch_ctx, *ch_kind, *ch_a;
   Pkt *ch_pkt;
-  // run state / outputs
-  uint32_t n_init;         // initial pending count (pool 0)
-  uint32_t uid_init;       // m_uid after setup
-  nsgpu_p2p_stats *stats;
-  uint32_t *error;         // non-zero = capacity exceeded (code)
+  // run control / outputs
+  uint32_t n_init;    // initial pending count (pool 0)
+  uint32_t uid_init;  // m_uid after setup
+  Ctl *C;
+  uint32_t *error;  // non-zero = capacity exceeded (code)
   uint64_t *log_ts;
   uint32_t *log_uid, *log_ctx;
   uint64_t log_cap;
-  uint64_t max_windows;
-  uint64_t *prof;  // diagnostic: per-phase s_memtime cycle sums (wave 0 view), or null
-  uint32_t *node_head;  // per-node chain head of the current window (NOCHAIN between windows)
 };
 
-struct P2PLds {
-  SortLds sort;
-  uint32_t nchild[WCAP];
-  uint32_t ninl[WCAP];     // inline (zero-delay leaf) children dispatched inside the window, per rank
-  uint32_t iprefix[WCAP];  // exclusive prefix of ninl in rank order
-  uint32_t wsum[P2P_THREADS / 64];
-  uint64_t wmin[P2P_THREADS / 64];
-  uint64_t wmin2[P2P_THREADS / 64];
-  uint32_t wcnt[P2P_THREADS / 64];
-  uint32_t wcnt2[P2P_THREADS / 64];
-  uint32_t stop_flag;
-};
-
-// ---------------- block reductions / scans (1024 threads) ----------------
+// ---------------- wave / block helpers ----------------
 __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) {
     uint64_t w = __shfl_xor(v, o);
@@ -119,7 +130,18 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
   }
   return v;
 }
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t w = __shfl_xor(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
@@ -131,14 +153,15 @@ __device__ __forceinline__ uint32_t wave_exscan32(uint32_t v, int lane) {
   }
   return inc - v;
 }
-// Block exclusive scan of one value per thread; returns the exclusive prefix, *total = block sum.
+// Block exclusive scan of one value per thread (NTH threads); *total = block sum.
+template <int NTH>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uint32_t *total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t ex = wave_exscan32(v, lane);
   if (lane == 63) wsum[wid] = ex + v;
   __syncthreads();
   uint32_t off = 0, tot = 0;
-  for (int w = 0; w < P2P_THREADS / 64; w++) {
+  for (int w = 0; w < NTH / 64; w++) {
     const uint32_t s = wsum[w];
     off += w < wid ? s : 0;
     tot += s;
@@ -444,488 +467,495 @@ __device__ __noinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_w
   }
 }
 
-__global__ __launch_bounds__(P2P_THREADS) void p2p_run(const P2PDev *__restrict__ Mp, const int32_t *__restrict__ sink_of_node) {
-  const P2PDev &M = *Mp;  // in global memory: fields come through scalar loads, not 70 SGPR kernel args
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  P2PLds &L = *reinterpret_cast<P2PLds *>(smem_raw);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint64_t INF = ~0ull;
+// ================================ window pipeline ================================
+// Window bound from the reduction: packed key bound, span, Stop key (shared by k_partition/k_refit).
+struct WinBound {
+  uint64_t tmin, span, bound, stop_packed;
+};
+__device__ __forceinline__ WinBound window_bound(const Ctl &C) {
+  WinBound b;
+  b.tmin = C.tmin;
+  uint64_t span = C.wend - b.tmin;
+  if (span > 0xfffffffeull) span = 0xfffffffeull;
+  b.span = span;
+  b.bound = (span << 32) | 0xffffffffull;
+  b.stop_packed = ~0ull;
+  if (C.stopts != ~0ull && C.stopts - b.tmin <= span) {
+    // Stop caps the window at its own key (it is dispatched; later events are not)
+    b.stop_packed = ((C.stopts - b.tmin) << 32) | C.stopuid;
+    b.bound = b.stop_packed < b.bound ? b.stop_packed : b.bound;
+  }
+  return b;
+}
+__device__ __forceinline__ void publish_bound(Ctl &C, const WinBound &b) {
+  C.bound = b.bound;
+  C.span = b.span;
+  // zero-delay leaf children (Ipv4EndPoint::DoForwardUp) run inside the window; when the window ends
+  // at the Stop event, those at the Stop's ts sort after it and are never dispatched
+  const bool has_stop = b.stop_packed != ~0ull && b.bound >= b.stop_packed;
+  C.inline_lim = has_stop ? (b.stop_packed >> 32) : ~0ull;
+}
 
-  uint64_t P = M.n_init;
-  int cur = 0;
-  uint64_t K = 0;            // dispatched so far
-  uint32_t uid = M.uid_init; // next uid
-  uint64_t digest = 0, cancelled = 0, ttl_drops = 0, no_route = 0, unreach = 0;
-  uint64_t windows = 0, max_window = 0, last_ts = 0;
-  if (tid == 0) L.stop_flag = 0;
+// ---- k_reduce: tmin, W_end, the pending Stop ----
+__global__ __launch_bounds__(TB) void k_reduce(const P2PDev *__restrict__ Mp) {
+  const P2PDev &M = *Mp;
+  Ctl &C = *M.C;
+  if (blockIdx.x == 0 && threadIdx.x == 0) C.scan_ran = 0;
+  if (C.done) return;
+  const uint64_t P = C.P;
+  const int cur = C.cur;
+  const uint64_t *ts = M.ev_ts[cur];
+  const uint32_t *kindv = M.ev_kind[cur];
+  uint64_t tmin = ~0ull, wend = ~0ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < P; i += (uint64_t)gridDim.x * TB) {
+    const uint64_t t = ts[i];
+    const uint32_t k = kindv[i] & 0xffu;
+    tmin = t < tmin ? t : tmin;
+    const uint64_t e = t + (uint64_t)M.lookahead[k];
+    wend = e < wend ? e : wend;
+    if (k == K_STOP) {  // at most one Stop event is pending
+      C.stopts = t;
+      C.stopuid = M.ev_uid[cur][i];
+    }
+  }
+  __shared__ uint64_t s0[TB / 64], s1[TB / 64];
+  tmin = wave_min64(tmin);
+  wend = wave_min64(wend);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    s0[wid] = tmin;
+    s1[wid] = wend;
+  }
   __syncthreads();
-  uint64_t pacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t tprev = M.prof ? __builtin_amdgcn_s_memtime() : 0;
-#define PSTAMP(i)                                        \
-  if (M.prof) {                                          \
-    const uint64_t tnow_ = __builtin_amdgcn_s_memtime(); \
-    pacc[i] += tnow_ - tprev;                            \
-    tprev = tnow_;                                       \
-  }
-
-  while (P > 0) {
-    if (windows >= M.max_windows) {
-      if (tid == 0) atomicOr(M.error, 4u);
-      break;
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < TB / 64; w++) {
+      tmin = s0[w] < tmin ? s0[w] : tmin;
+      wend = s1[w] < wend ? s1[w] : wend;
     }
-    const uint64_t *ts = M.ev_ts[cur];
-    const uint32_t *uidv = M.ev_uid[cur];
-    const uint32_t *kindv = M.ev_kind[cur];
-    PSTAMP(6);
-    // ---- 1. tmin, W_end = min (ts + L(kind)), stop key ----
-    uint64_t tmin = INF, wend = INF, stopkey = INF;
-    for (uint64_t i = tid; i < P; i += P2P_THREADS) {
-      const uint64_t t = ts[i];
-      const uint32_t k = kindv[i] & 0xffu;
-      tmin = t < tmin ? t : tmin;
-      const uint64_t e = t + (uint64_t)M.lookahead[k];
-      wend = e < wend ? e : wend;
-      if (k == K_STOP) stopkey = t;  // at most one Stop event is pending
-    }
-    tmin = wave_min64(tmin);
-    wend = wave_min64(wend);
-    stopkey = wave_min64(stopkey);
-    if (lane == 0) {
-      L.wmin[wid] = tmin;
-      L.wmin2[wid] = wend;
-      L.sort.k[0][wid] = stopkey;
-    }
-    __syncthreads();
-    tmin = INF;
-    wend = INF;
-    stopkey = INF;
-    for (int w = 0; w < P2P_THREADS / 64; w++) {
-      tmin = L.wmin[w] < tmin ? L.wmin[w] : tmin;
-      wend = L.wmin2[w] < wend ? L.wmin2[w] : wend;
-      stopkey = L.sort.k[0][w] < stopkey ? L.sort.k[0][w] : stopkey;
-    }
-    __syncthreads();
-    // packed key bound: ((ts - tmin) << 32) | uid <= bound
-    uint64_t span = wend - tmin;
-    if (span > 0xfffffffeull) span = 0xfffffffeull;
-    uint64_t bound = (span << 32) | 0xffffffffull;
-    uint64_t stop_packed = INF;
-    if (stopkey != INF && stopkey - tmin <= span) {
-      // Stop caps the window at its own key (it is dispatched; later events are not)
-      for (uint64_t i = tid; i < P; i += P2P_THREADS)
-        if ((kindv[i] & 0xffu) == K_STOP) L.sort.k[1][0] = ((ts[i] - tmin) << 32) | uidv[i];
-      __syncthreads();
-      stop_packed = L.sort.k[1][0];
-      bound = stop_packed < bound ? stop_packed : bound;
-      __syncthreads();
-    }
-    PSTAMP(0);
-    // ---- count; if the window would exceed WCAP, bisect for the largest key bound that fits ----
-    // (any key prefix of a safe window is safe: its children still sort after every kept event)
-    auto count_le = [&](uint64_t bnd) -> uint32_t {
-      uint32_t c = 0;
-      for (uint64_t i = tid; i < P; i += P2P_THREADS) {
-        const uint64_t t = ts[i];
-        if (t - tmin <= span) c += ((((t - tmin) << 32) | uidv[i]) <= bnd);
-      }
-      c = wave_sum32(c);
-      if (lane == 0) L.wcnt[wid] = c;
-      __syncthreads();
-      uint32_t tot = 0;
-      for (int w = 0; w < P2P_THREADS / 64; w++) tot += L.wcnt[w];
-      __syncthreads();
-      return tot;
-    };
-    uint32_t cnt = count_le(bound);
-    if (cnt > (uint32_t)WCAP) {
-      uint64_t lo_b = 0, hi_b = bound;  // count (hi_b) > WCAP
-      while (hi_b - lo_b > 1) {
-        const uint64_t mid = lo_b + (hi_b - lo_b) / 2;
-        if (count_le(mid) <= (uint32_t)WCAP) lo_b = mid;
-        else hi_b = mid;
-      }
-      bound = lo_b;
-      cnt = count_le(bound);
-    }
-    const uint32_t W = cnt;
-    // zero-delay leaf children (Ipv4EndPoint::DoForwardUp) run inside the window; when the window
-    // ends at the Stop event, those at the Stop's ts sort after it and are never dispatched
-    const bool has_stop = stop_packed != INF && bound >= stop_packed;
-    const uint64_t inline_ts_limit = has_stop ? (stop_packed >> 32) : INF;  // relative ts (exclusive)
-    PSTAMP(1);
-    // ---- 2. partition: window -> LDS list (packed key, pool index); rest -> next pool ----
-    const int nxt = cur ^ 1;
-    {
-      // each thread handles a contiguous range of the pool; window slots by block scan
-      const uint64_t per = (P + P2P_THREADS - 1) / P2P_THREADS;
-      const uint64_t i0 = (uint64_t)tid * per, i1 = i0 + per < P ? i0 + per : P;
-      uint32_t nin = 0, nout = 0;
-      for (uint64_t i = i0; i < i1; i++) {
-        const uint64_t t = ts[i];
-        const bool in = (t - tmin <= span) && ((((t - tmin) << 32) | uidv[i]) <= bound);
-        nin += in;
-        nout += !in;
-      }
-      uint32_t tot_in, tot_out;
-      uint32_t win_off = block_exscan(nin, L.wsum, &tot_in);
-      uint32_t out_off = block_exscan(nout, L.wsum, &tot_out);
-      for (uint64_t i = i0; i < i1; i++) {
-        const uint64_t t = ts[i];
-        const uint64_t pk = ((t - tmin) << 32) | uidv[i];
-        const bool in = (t - tmin <= span) && (pk <= bound);
-        if (in) {
-          L.sort.k[0][win_off] = pk;
-          L.sort.v[0][win_off] = (uint32_t)i;
-          win_off++;
-        } else {
-          M.ev_ts[nxt][out_off] = t;
-          M.ev_uid[nxt][out_off] = uidv[i];
-          M.ev_ctx[nxt][out_off] = M.ev_ctx[cur][i];
-          M.ev_kind[nxt][out_off] = kindv[i];
-          M.ev_a[nxt][out_off] = M.ev_a[cur][i];
-          M.ev_pkt[nxt][out_off] = M.ev_pkt[cur][i];
-          out_off++;
-        }
-      }
-      P = tot_out;  // survivors; children are appended after them
-    }
-    // clear the bucket histogram (sort.v[1]) and fill counters (nchild)
-    for (int i = tid; i < WCAP; i += P2P_THREADS) {
-      L.sort.v[1][i] = 0;
-      L.nchild[i] = 0;
-    }
-    __syncthreads();
-    PSTAMP(2);
-    // ---- 3. dispatch rank: bucket sort of the packed keys by relative ts (bitonic if a bucket is crowded) ----
-    {
-      uint64_t rmax = 0;
-      for (int i = tid; i < (int)W; i += P2P_THREADS) {
-        const uint64_t r = L.sort.k[0][i] >> 32;
-        rmax = r > rmax ? r : rmax;
-      }
-      for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t w = __shfl_xor(rmax, o);
-        rmax = w > rmax ? w : rmax;
-      }
-      if (lane == 0) L.wmin[wid] = rmax;
-      __syncthreads();
-      rmax = 0;
-      for (int w = 0; w < P2P_THREADS / 64; w++) rmax = L.wmin[w] > rmax ? L.wmin[w] : rmax;
-      const uint64_t denom = rmax + 1;
-      for (int i = tid; i < (int)W; i += P2P_THREADS) {
-        const uint32_t bk = (uint32_t)(((L.sort.k[0][i] >> 32) * (uint64_t)WCAP) / denom);
-        atomicAdd(&L.sort.v[1][bk], 1u);
-      }
-      __syncthreads();
-      // exclusive scan of the 4096 bucket counts (4 per thread) and the largest bucket
-      uint32_t bc[RPT], bs = 0, bmax = 0;
-#pragma unroll
-      for (int q = 0; q < RPT; q++) {
-        bc[q] = L.sort.v[1][tid * RPT + q];
-        bs += bc[q];
-        bmax = bc[q] > bmax ? bc[q] : bmax;
-      }
-      uint32_t btot;
-      uint32_t bstart = block_exscan(bs, L.wsum, &btot);
-#pragma unroll
-      for (int q = 0; q < RPT; q++) {
-        L.sort.v[1][tid * RPT + q] = bstart;
-        bstart += bc[q];
-      }
-      for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t w = __shfl_xor(bmax, o);
-        bmax = w > bmax ? w : bmax;
-      }
-      if (lane == 0) L.wcnt[wid] = bmax;
-      __syncthreads();
-      bmax = 0;
-      for (int w = 0; w < P2P_THREADS / 64; w++) bmax = L.wcnt[w] > bmax ? L.wcnt[w] : bmax;
-      PSTAMP(7);
-      if (bmax > 32) {
-        if (M.prof) pacc[9]++;
-        // crowded buckets (equal timestamps: lockstep sources, the setup burst at ts 0): wave-run
-        // sort + cross-run ranking
-        __syncthreads();
-        run_rank_sort<P2P_THREADS>(L.sort, W);
-      } else {
-        // scatter into buckets (sort.k[1] keys, ninl pool indices), then sort each bucket in place
-        for (int i = tid; i < (int)W; i += P2P_THREADS) {
-          const uint64_t pk = L.sort.k[0][i];
-          const uint32_t bk = (uint32_t)(((pk >> 32) * (uint64_t)WCAP) / denom);
-          const uint32_t pos = L.sort.v[1][bk] + atomicAdd(&L.nchild[bk], 1u);
-          L.sort.k[1][pos] = pk;
-          L.ninl[pos] = L.sort.v[0][i];
-        }
-        __syncthreads();
-#pragma unroll 1
-        for (int q = 0; q < RPT; q++) {
-          const uint32_t bk = tid * RPT + q;
-          const uint32_t c = L.nchild[bk];
-          if (c > 1) {
-            const uint32_t s0 = L.sort.v[1][bk];
-            for (uint32_t x = s0 + 1; x < s0 + c; x++) {  // insertion sort (c <= 32)
-              const uint64_t kx = L.sort.k[1][x];
-              const uint32_t vx = L.ninl[x];
-              uint32_t y = x;
-              while (y > s0 && L.sort.k[1][y - 1] > kx) {
-                L.sort.k[1][y] = L.sort.k[1][y - 1];
-                L.ninl[y] = L.ninl[y - 1];
-                y--;
-              }
-              L.sort.k[1][y] = kx;
-              L.ninl[y] = vx;
-            }
-          }
-        }
-        __syncthreads();
-        for (int r = tid; r < (int)W; r += P2P_THREADS) {
-          L.sort.k[0][r] = L.sort.k[1][r];
-          L.sort.v[0][r] = L.ninl[r];
-        }
-      }
-      __syncthreads();
-      PSTAMP(8);
-    }
-    // ---- group by node: per-node chains through a global head array (one atomicExch per event) ----
-    // (sort.k[1] is free after the sort: it holds each rank's context)
-    uint32_t *const Lctx = reinterpret_cast<uint32_t *>(&L.sort.k[1][0]);
-#pragma unroll
-    for (int q = 0; q < RPT; q++) {
-      const int r = tid + P2P_THREADS * q;
-      if (r < (int)W) {
-        const uint32_t c = M.ev_ctx[cur][L.sort.v[0][r]];
-        Lctx[r] = c;
-        L.sort.v[1][r] = c < M.n_nodes ? atomicExch(&M.node_head[c], (uint32_t)r) : NOCHAIN;
-      }
-      if (r < WCAP) {
-        L.nchild[r] = 0;
-        L.ninl[r] = 0;
-      }
-    }
-    __syncthreads();
-    PSTAMP(3);
-    // ---- 4. handlers: the node's last exchanger walks the node's chain in rank order ----
-    // Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) run at
-    // their key position: after the node's events with ts <= theirs, before the first with a larger ts.
-#pragma unroll 1
-    for (int q = 0; q < RPT; q++) {
-      const int r0 = tid + P2P_THREADS * q;
-      if (r0 >= (int)W) continue;
-      const uint32_t c = Lctx[r0];
-      if (c < M.n_nodes) {
-        const uint32_t head = __hip_atomic_load(&M.node_head[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (head != (uint32_t)r0) continue;  // not the chain holder
-        __hip_atomic_store(&M.node_head[c], NOCHAIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      const int32_t sink = c < M.n_nodes ? sink_of_node[c] : -1;
-      uint32_t n = 0;
-      for (uint32_t x = (uint32_t)r0; x != NOCHAIN; x = L.sort.v[1][x]) n++;
-      int64_t last = -1;
-      uint32_t ts0_rank = 0, pending = 0;
-      uint64_t cur_rel = 0;
-      for (uint32_t it = 0; it <= n; it++) {
-        uint32_t r = NOCHAIN;
-        if (it < n)
-          for (uint32_t x = (uint32_t)r0; x != NOCHAIN; x = L.sort.v[1][x])
-            if ((int64_t)x > last && x < r) r = x;
-        const uint64_t rel = it < n ? (L.sort.k[0][r] >> 32) : INF;
-        if (it > 0 && rel > cur_rel && pending) {
-          // flush the inline children of this node's events at cur_rel (ranks in [ts0_rank, r))
-          for (uint32_t x = (uint32_t)r0; x != NOCHAIN; x = L.sort.v[1][x]) {
-            if (x < ts0_rank || x >= r) continue;
-            const uint32_t ncr = L.nchild[x];
-            for (uint32_t j = 0; j < ncr; j++) {
-              const uint32_t sl = x * M.maxc + j;
-              if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
-              Emit E0;
-              E0.M = &M;
-              E0.now = tmin + cur_rel;
-              E0.ctx = c;
-              E0.slot0 = 0;
-              E0.n = 0;
-              bool st0 = false;
-              run_event(M, E0, M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl], sink, &ttl_drops, &no_route, &unreach,
-                        &st0);
-            }
-          }
-          pending = 0;
-        }
-        if (it == n) break;
-        if (it == 0 || rel > cur_rel) {
-          ts0_rank = r;
-          cur_rel = rel;
-        }
-        const uint32_t pi = L.sort.v[0][r];
-        Emit E;
-        E.M = &M;
-        E.now = tmin + rel;
-        E.ctx = c;
-        E.slot0 = r * M.maxc;
-        E.n = 0;
-        bool stop = false;
-        const bool was_cancelled = run_event(M, E, M.ev_kind[cur][pi], M.ev_a[cur][pi], M.ev_pkt[cur][pi], sink,
-                                             &ttl_drops, &no_route, &unreach, &stop);
-        cancelled += was_cancelled;
-        L.nchild[r] = E.n;
-        if (stop) L.stop_flag = 1;
-        uint32_t ni = 0;
-        if (rel < inline_ts_limit)
-          for (uint32_t j = 0; j < E.n; j++) ni += (M.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
-        L.ninl[r] = ni;
-        pending += ni;
-        last = r;
-      }
-    }
-    __syncthreads();
-    PSTAMP(4);
-    // ---- 5. uids: exclusive scan of child counts in rank order; dispatch ranks; children -> next pool ----
-    uint32_t nc[RPT], ni4[RPT], tsum = 0, isum = 0;
-#pragma unroll
-    for (int q = 0; q < RPT; q++) {
-      nc[q] = L.nchild[tid * RPT + q];
-      ni4[q] = L.ninl[tid * RPT + q];
-      tsum += nc[q];
-      isum += ni4[q];
-    }
-    uint32_t total_children, total_inline;
-    uint32_t base = block_exscan(tsum, L.wsum, &total_children);
-    uint32_t ibase = block_exscan(isum, L.wsum, &total_inline);
-    {
-      uint32_t ib = ibase;
-#pragma unroll
-      for (int q = 0; q < RPT; q++) {
-        L.iprefix[tid * RPT + q] = ib;
-        ib += ni4[q];
-      }
-    }
-    __syncthreads();
-    // dispatch rank of main event r = r + #inline children with ts < ts_r; of the i-th inline child
-    // of r = (#main events with ts <= ts_r) + iprefix[r] + i  (inline children are key-sorted by r)
-    auto first_same = [&](uint32_t r, uint64_t rel) -> uint32_t {
-      uint32_t lo = 0, hi = r;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((L.sort.k[0][mid] >> 32) < rel) lo = mid + 1;
-        else hi = mid;
-      }
-      return lo;
-    };
-    auto last_same = [&](uint32_t r, uint64_t rel) -> uint32_t {
-      uint32_t lo = r + 1, hi = W;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((L.sort.k[0][mid] >> 32) <= rel) lo = mid + 1;
-        else hi = mid;
-      }
-      return lo - 1;
-    };
-#pragma unroll 1
-    for (int q = 0; q < RPT; q++) {
-      const uint32_t r = tid * RPT + q;
-      if (r < W) {
-        const uint64_t pk = L.sort.k[0][r];
-        const uint64_t rel = pk >> 32;
-        const uint64_t t = tmin + rel;
-        const uint32_t u = (uint32_t)pk;
-        const bool dup_prev = r > 0 && (L.sort.k[0][r - 1] >> 32) == rel;
-        const uint32_t f = total_inline ? (dup_prev ? first_same(r, rel) : r) : r;
-        const uint64_t rk = K + r + (total_inline ? L.iprefix[f] : 0);
-        digest += digest_term(rk, t, u);
-        if (rk < M.log_cap) {
-          M.log_ts[rk] = t;
-          M.log_uid[rk] = u;
-          M.log_ctx[rk] = M.ev_ctx[cur][L.sort.v[0][r]];
-        }
-        if (r == W - 1) last_ts = t;
-        uint32_t lastr = 0;
-        const uint32_t nir = L.ninl[r], ncr = L.nchild[r];
-        if (nir) lastr = (r + 1 < W && (L.sort.k[0][r + 1] >> 32) == rel) ? last_same(r, rel) : r;
-        uint32_t ii = 0, nonin = base - (ibase);  // non-inline children before this rank
-        for (uint32_t j = 0; j < ncr; j++) {
-          const uint32_t sl = r * M.maxc + j;
-          const uint32_t cu = uid + base + j;
-          if ((M.ch_kind[sl] & 0xffu) == K_FWD_UP) {
-            if (rel < inline_ts_limit) {  // dispatched inside this window
-              const uint64_t crk = K + lastr + 1 + L.iprefix[r] + ii;
-              digest += digest_term(crk, t, cu);
-              if (crk < M.log_cap) {
-                M.log_ts[crk] = t;
-                M.log_uid[crk] = cu;
-                M.log_ctx[crk] = M.ch_ctx[sl];
-              }
-              ii++;
-            }
-            continue;  // never re-queued
-          }
-          const uint64_t o = P + nonin;
-          nonin++;
-          if (o < M.pool_cap) {
-            M.ev_ts[nxt][o] = M.ch_ts[sl];
-            M.ev_uid[nxt][o] = cu;
-            M.ev_ctx[nxt][o] = M.ch_ctx[sl];
-            M.ev_kind[nxt][o] = M.ch_kind[sl];
-            M.ev_a[nxt][o] = M.ch_a[sl];
-            M.ev_pkt[nxt][o] = M.ch_pkt[sl];
-          } else {
-            atomicOr(M.error, 1u);
-          }
-        }
-        base += ncr;
-        ibase += nir;
-      }
-    }
-    // (inline children at the Stop's ts are scheduled — uids consumed — but never dispatched; the run
-    //  ends with this window, so the pool bookkeeping below only has to be right for other windows)
-    K += W + total_inline;
-    uid += total_children;
-    P += total_children - total_inline;
-    cur = nxt;
-    windows++;
-    max_window = W > max_window ? W : max_window;
-    __syncthreads();
-    if (L.stop_flag) break;
-    if (P > M.pool_cap) {
-      if (tid == 0) atomicOr(M.error, 1u);
-      break;
-    }
-    __threadfence_block();
-  }
-
-  if (M.prof && tid == 0)
-    for (int i = 0; i < 16; i++) M.prof[i] = pacc[i];
-#undef PSTAMP
-  // ---- reduce and publish counters ----
-  __syncthreads();
-  uint64_t vals[5] = {digest, cancelled, ttl_drops, no_route, unreach};
-  for (int k = 0; k < 5; k++) {
-    uint64_t v = vals[k];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (lane == 0) L.wmin[wid] = v;
-    __syncthreads();
-    if (tid == 0) {
-      uint64_t s = 0;
-      for (int w = 0; w < P2P_THREADS / 64; w++) s += L.wmin[w];
-      vals[k] = s;
-    }
-    __syncthreads();
-  }
-  // last dispatched ts: carried by the thread that saw rank W-1 of the final window
-  if (last_ts) atomicMax((unsigned long long *)&M.stats->final_ts, (unsigned long long)last_ts);
-  if (tid == 0) {
-    M.stats->dispatched = K;
-    M.stats->digest = vals[0];
-    M.stats->cancelled = vals[1];
-    M.stats->ttl_drops = vals[2];
-    M.stats->no_route_drops = vals[3];
-    M.stats->unreach_drops = vals[4];
-    M.stats->next_uid = uid;
-    M.stats->windows = (uint32_t)windows;
-    M.stats->max_window = max_window;
+    if (tmin != ~0ull) atomicMin((unsigned long long *)&C.tmin, (unsigned long long)tmin);
+    if (wend != ~0ull) atomicMin((unsigned long long *)&C.wend, (unsigned long long)wend);
   }
 }
 
-}  // namespace nsgpu
+// Classifies pool entry i against the window bound and moves it: window -> (wkey, wpi) list,
+// otherwise -> the other pool buffer.  All 64 lanes of the wave must call it (ballots).
+__device__ __forceinline__ void partition_one(const P2PDev &M, Ctl &C, const WinBound &b, int cur, uint64_t i,
+                                              bool valid) {
+  const int lane = threadIdx.x & 63;
+  uint64_t t = 0, pk = 0;
+  bool in = false;
+  if (valid) {
+    t = M.ev_ts[cur][i];
+    pk = ((t - b.tmin) << 32) | M.ev_uid[cur][i];
+    in = (t - b.tmin <= b.span) && pk <= b.bound;
+  }
+  const uint64_t bin = __ballot(valid && in), bout = __ballot(valid && !in);
+  uint32_t basein = 0, baseout = 0;
+  if (lane == 0) {
+    if (bin) basein = atomicAdd(&C.W, (uint32_t)__popcll(bin));
+    if (bout) baseout = atomicAdd(&C.nxtP, (uint32_t)__popcll(bout));
+  }
+  basein = __shfl(basein, 0);
+  baseout = __shfl(baseout, 0);
+  const uint64_t below = (1ull << lane) - 1ull;
+  if (valid && in) {
+    const uint32_t slot = basein + (uint32_t)__popcll(bin & below);
+    if (slot < (uint32_t)WCAP) {
+      M.wkey[slot] = pk;
+      M.wpi[slot] = (uint32_t)i;
+    } else {
+      C.overflow = 1;
+    }
+  } else if (valid) {
+    const uint64_t o = baseout + (uint64_t)__popcll(bout & below);
+    const int nxt = cur ^ 1;
+    if (o < M.pool_cap) {
+      M.ev_ts[nxt][o] = t;
+      M.ev_uid[nxt][o] = M.ev_uid[cur][i];
+      M.ev_ctx[nxt][o] = M.ev_ctx[cur][i];
+      M.ev_kind[nxt][o] = M.ev_kind[cur][i];
+      M.ev_a[nxt][o] = M.ev_a[cur][i];
+      M.ev_pkt[nxt][o] = M.ev_pkt[cur][i];
+    } else {
+      atomicOr(M.error, 1u);
+    }
+  }
+}
 
+// ---- k_partition ----
+__global__ __launch_bounds__(TB) void k_partition(const P2PDev *__restrict__ Mp) {
+  const P2PDev &M = *Mp;
+  Ctl &C = *M.C;
+  if (C.done) return;
+  const WinBound b = window_bound(C);
+  if (blockIdx.x == 0 && threadIdx.x == 0) publish_bound(C, b);
+  const uint64_t P = C.P;
+  const int cur = C.cur;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * TB; i0 < P; i0 += (uint64_t)gridDim.x * TB) {
+    const uint64_t i = i0 + threadIdx.x;
+    partition_one(M, C, b, cur, i, i < P);
+  }
+}
+
+// ---- k_refit: the window overflowed WCAP; cut it to the largest key prefix that fits ----
+__global__ __launch_bounds__(SCAN_THREADS) void k_refit(const P2PDev *__restrict__ Mp) {
+  const P2PDev &M = *Mp;
+  Ctl &C = *M.C;
+  if (C.done || !C.overflow) return;
+  __shared__ uint32_t wc[SCAN_THREADS / 64];
+  WinBound b = window_bound(C);
+  const uint64_t P = C.P;
+  const int cur = C.cur;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  auto count_le = [&](uint64_t bnd) -> uint32_t {
+    uint32_t c = 0;
+    for (uint64_t i = threadIdx.x; i < P; i += SCAN_THREADS) {
+      const uint64_t t = M.ev_ts[cur][i];
+      if (t - b.tmin <= b.span) c += ((((t - b.tmin) << 32) | M.ev_uid[cur][i]) <= bnd);
+    }
+    c = wave_sum32(c);
+    if (lane == 0) wc[wid] = c;
+    __syncthreads();
+    uint32_t tot = 0;
+    for (int w = 0; w < SCAN_THREADS / 64; w++) tot += wc[w];
+    __syncthreads();
+    return tot;
+  };
+  uint64_t lo_b = 0, hi_b = b.bound;  // count (hi_b) > WCAP
+  while (hi_b - lo_b > 1) {
+    const uint64_t mid = lo_b + (hi_b - lo_b) / 2;
+    if (count_le(mid) <= (uint32_t)WCAP) lo_b = mid;
+    else hi_b = mid;
+  }
+  b.bound = lo_b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    C.W = 0;
+    C.nxtP = 0;
+    C.overflow = 0;
+    publish_bound(C, b);
+  }
+  __syncthreads();
+  for (uint64_t i0 = 0; i0 < P; i0 += SCAN_THREADS) {
+    const uint64_t i = i0 + threadIdx.x;
+    partition_one(M, C, b, cur, i, i < P);
+  }
+}
+
+// ---- k_rank: rank of each window key = # of smaller keys (keys are distinct: uids) ----
+__global__ __launch_bounds__(TB) void k_rank(const P2PDev *__restrict__ Mp) {
+  const P2PDev &M = *Mp;
+  const Ctl &C = *M.C;
+  if (C.done) return;
+  const uint32_t W = C.W;
+  const uint32_t ti = blockIdx.x / NT, tj = blockIdx.x % NT;
+  if (ti * TB >= W || tj * TB >= W) return;
+  __shared__ uint64_t tk[TB];
+  const uint32_t j = tj * TB + threadIdx.x;
+  tk[threadIdx.x] = j < W ? M.wkey[j] : ~0ull;
+  __syncthreads();
+  const uint32_t i = ti * TB + threadIdx.x;
+  if (i >= W) return;
+  const uint64_t x = M.wkey[i];
+  uint32_t c = 0;
+#pragma unroll 16
+  for (int y = 0; y < TB; y++) c += tk[y] < x;
+  if (c) atomicAdd(&M.wrank[i], c);
+}
+
+// ---- k_scatter: rank order; per-node chains ----
+__global__ __launch_bounds__(RB) void k_scatter(const P2PDev *__restrict__ Mp) {
+  const P2PDev &M = *Mp;
+  const Ctl &C = *M.C;
+  if (C.done) return;
+  const uint32_t i = blockIdx.x * RB + threadIdx.x;
+  if (i >= C.W) return;
+  const uint32_t r = M.wrank[i];
+  M.wrank[i] = 0;
+  const uint32_t pi = M.wpi[i];
+  M.skey[r] = M.wkey[i];
+  M.spi[r] = pi;
+  const uint32_t c = M.ev_ctx[C.cur][pi];
+  M.sctx[r] = c;
+  M.link[r] = c < M.n_nodes ? atomicExch(&M.node_head[c], r) : NOCHAIN;
+}
+
+// ---- k_handle: the node's last exchanger runs the node's chain in rank order ----
+// Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) run at
+// their key position: after the node's events with ts <= theirs, before the first with a larger ts.
+__global__ __launch_bounds__(RB) void k_handle(const P2PDev *__restrict__ Mp,
+                                               const int32_t *__restrict__ sink_of_node) {
+  const P2PDev &M = *Mp;
+  Ctl &C = *M.C;
+  if (C.done) return;
+  const uint32_t W = C.W;
+  const uint32_t r0 = blockIdx.x * RB + threadIdx.x;
+  if (r0 >= W) return;
+  const uint32_t c = M.sctx[r0];
+  if (c < M.n_nodes) {
+    if (M.node_head[c] != r0) return;  // not the chain holder
+    M.node_head[c] = NOCHAIN;
+  }
+  __shared__ uint32_t chs[RB * CH];
+  uint32_t *my = &chs[threadIdx.x * CH];
+  uint32_t n = 0;
+  for (uint32_t x = r0; x != NOCHAIN; x = M.link[x]) {
+    if (n < (uint32_t)CH) my[n] = x;
+    n++;
+  }
+  const bool small = n <= (uint32_t)CH;
+  if (small)
+    for (uint32_t a = 1; a < n; a++) {  // insertion sort: ascending rank
+      const uint32_t v = my[a];
+      uint32_t b = a;
+      while (b > 0 && my[b - 1] > v) {
+        my[b] = my[b - 1];
+        b--;
+      }
+      my[b] = v;
+    }
+  const uint64_t tmin = C.tmin;
+  const uint64_t inline_lim = C.inline_lim;
+  const int cur = C.cur;
+  const int32_t sink = c < M.n_nodes ? sink_of_node[c] : -1;
+  uint64_t cancelled = 0, ttl_drops = 0, no_route = 0, unreach = 0;
+  bool stop = false;
+  int64_t last = -1;
+  uint32_t ts0_it = 0, pending = 0;
+  uint64_t cur_rel = 0;
+  auto rank_at = [&](uint32_t it) -> uint32_t {
+    if (small) return my[it];
+    uint32_t best = NOCHAIN;  // it-th smallest: the smallest rank above `last`
+    for (uint32_t x = r0; x != NOCHAIN; x = M.link[x])
+      if ((int64_t)x > last && x < best) best = x;
+    return best;
+  };
+  for (uint32_t it = 0; it <= n; it++) {
+    const uint32_t r = it < n ? rank_at(it) : NOCHAIN;
+    const uint64_t rel = it < n ? (M.skey[r] >> 32) : ~0ull;
+    if (it > 0 && rel > cur_rel && pending) {
+      // flush the inline children of this node's events at cur_rel (chain positions [ts0_it, it))
+      for (uint32_t jt = ts0_it; jt < it; jt++) {
+        const uint32_t x = small ? my[jt] : NOCHAIN;
+        uint32_t xr = x;
+        if (!small) {  // recover the jt-th rank by selection (long chains only)
+          int64_t lst = -1;
+          for (uint32_t s = 0; s <= jt; s++) {
+            uint32_t best = NOCHAIN;
+            for (uint32_t y = r0; y != NOCHAIN; y = M.link[y])
+              if ((int64_t)y > lst && y < best) best = y;
+            lst = best;
+          }
+          xr = (uint32_t)lst;
+        }
+        const uint32_t ncr = M.nchild[xr];
+        for (uint32_t j = 0; j < ncr; j++) {
+          const uint32_t sl = xr * M.maxc + j;
+          if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
+          Emit E0;
+          E0.M = &M;
+          E0.now = tmin + cur_rel;
+          E0.ctx = c;
+          E0.slot0 = 0;
+          E0.n = 0;
+          bool st0 = false;
+          run_event(M, E0, M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl], sink, &ttl_drops, &no_route, &unreach, &st0);
+        }
+      }
+      pending = 0;
+    }
+    if (it == n) break;
+    if (it == 0 || rel > cur_rel) {
+      ts0_it = it;
+      cur_rel = rel;
+    }
+    const uint32_t pi = M.spi[r];
+    Emit E;
+    E.M = &M;
+    E.now = tmin + rel;
+    E.ctx = c;
+    E.slot0 = r * M.maxc;
+    E.n = 0;
+    bool st = false;
+    cancelled += run_event(M, E, M.ev_kind[cur][pi], M.ev_a[cur][pi], M.ev_pkt[cur][pi], sink, &ttl_drops,
+                           &no_route, &unreach, &st);
+    stop |= st;
+    uint32_t ni = 0;
+    if (rel < inline_lim)
+      for (uint32_t j = 0; j < E.n; j++) ni += (M.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
+    M.nchild[r] = E.n;
+    M.ninl[r] = ni;
+    pending += ni;
+    last = r;
+  }
+  if (stop) C.stop_seen = 1;
+  if (cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)cancelled);
+  if (ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)ttl_drops);
+  if (no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)no_route);
+  if (unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)unreach);
+}
+
+// ---- k_scan: child / inline prefixes in rank order, same-ts groups, run bookkeeping ----
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(const P2PDev *__restrict__ Mp) {
+  const P2PDev &M = *Mp;
+  Ctl &C = *M.C;
+  if (C.done) return;
+  constexpr int RPT = WCAP / SCAN_THREADS;
+  __shared__ uint32_t wsum[SCAN_THREADS / 64];
+  __shared__ uint32_t gstart[WCAP];
+  const uint32_t W = C.W;
+  const int tid = threadIdx.x;
+  uint32_t nc[RPT], ni[RPT], hd[RPT], sc = 0, si = 0, sh = 0;
+  uint64_t prev_rel = 0;
+  if (tid * RPT < (int)W && tid > 0) prev_rel = M.skey[tid * RPT - 1] >> 32;
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    nc[q] = ni[q] = hd[q] = 0;
+    if (r < W) {
+      nc[q] = M.nchild[r];
+      ni[q] = M.ninl[r];
+      const uint64_t rel = M.skey[r] >> 32;
+      hd[q] = r == 0 || rel != prev_rel;
+      prev_rel = rel;
+    }
+    sc += nc[q];
+    si += ni[q];
+    sh += hd[q];
+  }
+  uint32_t tc, tinl, ng;
+  uint32_t bc = block_exscan<SCAN_THREADS>(sc, wsum, &tc);
+  uint32_t bi = block_exscan<SCAN_THREADS>(si, wsum, &tinl);
+  uint32_t bh = block_exscan<SCAN_THREADS>(sh, wsum, &ng);
+  uint32_t g[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    bh += hd[q];
+    g[q] = bh - 1;  // same-ts group of rank r
+    if (r < W) {
+      M.cpref[r] = bc;
+      M.ipref[r] = bi;
+      if (hd[q]) gstart[g[q]] = r;
+    }
+    bc += nc[q];
+    bi += ni[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    if (r < W) {
+      const uint32_t first = gstart[g[q]];
+      const uint32_t last = (g[q] + 1 < ng ? gstart[g[q] + 1] : W) - 1;
+      M.gbnd[r] = first | (last << 16);
+    }
+  }
+  if (tid == 0) {
+    C.K0 = C.K;
+    C.uid0 = C.uid;
+    C.W0 = W;
+    C.Pbase = C.nxtP;
+    C.tmin0 = C.tmin;
+    C.inline_lim0 = C.inline_lim;
+    C.total_children = tc;
+    C.total_inline = tinl;
+    // (inline children at the Stop's ts are scheduled — uids consumed — but never dispatched; the run
+    //  ends with this window, so the pool bookkeeping only has to be right for other windows)
+    const uint64_t newP = (uint64_t)C.nxtP + tc - tinl;
+    C.K += W + tinl;
+    C.uid += tc;
+    C.P = newP;
+    C.cur ^= 1;
+    C.windows++;
+    if (W > C.max_window) C.max_window = W;
+    C.tmin = ~0ull;
+    C.wend = ~0ull;
+    C.stopts = ~0ull;
+    C.W = 0;
+    C.nxtP = 0;
+    bool done = C.stop_seen || newP == 0;
+    if (newP > M.pool_cap) {
+      atomicOr(M.error, 1u);
+      done = true;
+    }
+    if (C.windows >= C.max_windows && !done) {
+      atomicOr(M.error, 4u);
+      done = true;
+    }
+    C.scan_ran = 1;
+    if (done) C.done = 1;
+  }
+}
+
+// ---- k_append: dispatch ranks (digest, log), children -> pool ----
+__global__ __launch_bounds__(RB) void k_append(const P2PDev *__restrict__ Mp) {
+  const P2PDev &M = *Mp;
+  Ctl &C = *M.C;
+  if (!C.scan_ran) return;
+  const uint32_t W = C.W0;
+  const uint32_t r = blockIdx.x * RB + threadIdx.x;
+  if (blockIdx.x * RB >= W) return;  // whole block idle (uniform)
+  uint64_t digest = 0;
+  if (r < W) {
+    const uint64_t K0 = C.K0, tmin = C.tmin0, inline_lim = C.inline_lim0;
+    const uint32_t uid0 = C.uid0, tinl = C.total_inline;
+    const uint64_t pk = M.skey[r];
+    const uint64_t rel = pk >> 32;
+    const uint64_t t = tmin + rel;
+    const uint32_t u = (uint32_t)pk;
+    const uint32_t gb = M.gbnd[r];
+    const uint32_t first = gb & 0xffffu, last = gb >> 16;
+    const uint32_t ip = M.ipref[r], cp = M.cpref[r];
+    // dispatch rank of main event r = r + #inline children with ts < ts_r; of the i-th inline child
+    // of r = (#main events with ts <= ts_r) + iprefix[r] + i  (inline children are key-sorted by r)
+    const uint64_t rk = K0 + r + (tinl ? M.ipref[first] : 0);
+    digest += digest_term(rk, t, u);
+    if (rk < M.log_cap) {
+      M.log_ts[rk] = t;
+      M.log_uid[rk] = u;
+      M.log_ctx[rk] = M.sctx[r];
+    }
+    if (r == W - 1) C.last_ts = t;
+    const uint32_t ncr = M.nchild[r];
+    uint32_t ii = 0;
+    uint64_t o = (uint64_t)C.Pbase + (cp - ip);  // non-inline children before this rank
+    const int dst = C.cur;                       // (already flipped by k_scan: the next pool)
+    for (uint32_t j = 0; j < ncr; j++) {
+      const uint32_t sl = r * M.maxc + j;
+      const uint32_t cu = uid0 + cp + j;
+      const uint32_t kw = M.ch_kind[sl];
+      if ((kw & 0xffu) == K_FWD_UP) {
+        if (rel < inline_lim) {  // dispatched inside this window
+          const uint64_t crk = K0 + last + 1 + ip + ii;
+          digest += digest_term(crk, t, cu);
+          if (crk < M.log_cap) {
+            M.log_ts[crk] = t;
+            M.log_uid[crk] = cu;
+            M.log_ctx[crk] = M.ch_ctx[sl];
+          }
+          ii++;
+        }
+        continue;  // never re-queued
+      }
+      if (o < M.pool_cap) {
+        M.ev_ts[dst][o] = M.ch_ts[sl];
+        M.ev_uid[dst][o] = cu;
+        M.ev_ctx[dst][o] = M.ch_ctx[sl];
+        M.ev_kind[dst][o] = kw;
+        M.ev_a[dst][o] = M.ch_a[sl];
+        M.ev_pkt[dst][o] = M.ch_pkt[sl];
+      } else {
+        atomicOr(M.error, 1u);
+      }
+      o++;
+    }
+  }
+  digest = wave_sum64(digest);
+  if ((threadIdx.x & 63) == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
+}
+
+}  // namespace nsgpu
 // ====================================================================================================
 // Host side: scenario upload, setup-time event list, launch, results.
 // ====================================================================================================
@@ -941,6 +971,13 @@ struct nsgpu_p2p {
   std::vector<void *> allocs;
   int32_t *sink_of_node = nullptr;
   P2PDev *d_M = nullptr;  // device copy of M (kernel argument by pointer)
+  Ctl C0{};               // run control after reset
+  uint64_t max_windows = ~0ull;
+  hipStream_t s = nullptr;  // engine stream (graph capture and replay)
+  hipGraphExec_t gexec = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr;
+  uint32_t *done_host = nullptr;  // pinned, 2 slots
+  float last_ms = 0.f;
   // pristine initial pool (device) for resets
   uint64_t *init_ts = nullptr;
   uint32_t *init_uid = nullptr, *init_ctx = nullptr, *init_kind = nullptr, *init_a = nullptr;
@@ -980,6 +1017,12 @@ int dupload(nsgpu_p2p *h, const T **dst, const T *src, size_t n) {
 
 extern "C" int nsgpu_p2p_destroy(nsgpu_p2p *h) {
   if (!h) return NSGPU_OK;
+  if (h->s) (void)hipStreamSynchronize(h->s);
+  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  for (hipEvent_t e : {h->ev[0], h->ev[1], h->t0, h->t1})
+    if (e) (void)hipEventDestroy(e);
+  if (h->done_host) (void)hipHostFree(h->done_host);
+  if (h->s) (void)hipStreamDestroy(h->s);
   for (void *p : h->allocs) (void)hipFree(p);
   delete h;
   return NSGPU_OK;
@@ -1143,13 +1186,16 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   TRY(dalloc(h, &M.ch_kind, chn));
   TRY(dalloc(h, &M.ch_a, chn));
   TRY(dalloc(h, &M.ch_pkt, chn));
-  TRY(dalloc(h, &M.stats, 1));
+  TRY(dalloc(h, &M.wkey, WCAP));
+  TRY(dalloc(h, &M.skey, WCAP));
+  for (uint32_t **p : {&M.wpi, &M.wrank, &M.spi, &M.sctx, &M.link, &M.nchild, &M.ninl, &M.cpref, &M.ipref, &M.gbnd})
+    TRY(dalloc(h, p, WCAP));
+  TRY(dalloc(h, &M.C, 1));
   TRY(dalloc(h, &M.error, 4));
   M.log_cap = log_cap;
   TRY(dalloc(h, &M.log_ts, log_cap));
   TRY(dalloc(h, &M.log_uid, log_cap));
   TRY(dalloc(h, &M.log_ctx, log_cap));
-  M.max_windows = ~0ull;
   const uint64_t *c_ts;
   const uint32_t *c_uid, *c_ctx, *c_kind, *c_a;
   TRY(dupload(h, &c_ts, its.data(), its.size()));
@@ -1162,18 +1208,41 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   h->init_ctx = (uint32_t *)c_ctx;
   h->init_kind = (uint32_t *)c_kind;
   h->init_a = (uint32_t *)c_a;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void *)p2p_run, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)sizeof(P2PLds));
-    if (e != hipSuccess) {
-      nsgpu_p2p_destroy(h);
-      return set_error(NSGPU_EHIP, "hipFuncSetAttribute(p2p_run, %zu B LDS): %s", sizeof(P2PLds),
-                       hipGetErrorString(e));
-    }
-    attr = true;
-  }
+  // run control after reset
+  Ctl &C0 = h->C0;
+  memset(&C0, 0, sizeof(C0));
+  C0.P = M.n_init;
+  C0.uid = uid;
+  C0.tmin = C0.wend = C0.stopts = ~0ull;
+  C0.max_windows = h->max_windows;
+  C0.done = M.n_init == 0;
   TRY(dalloc(h, &h->d_M, 1));
+  if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
+    h->s = nullptr;
+    nsgpu_p2p_destroy(h);
+    return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipStreamCreate failed");
+  }
+  for (hipEvent_t *e : {&h->ev[0], &h->ev[1]})
+    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+      *e = nullptr;
+      nsgpu_p2p_destroy(h);
+      return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipEventCreate failed");
+    }
+  for (hipEvent_t *e : {&h->t0, &h->t1})
+    if (hipEventCreate(e) != hipSuccess) {
+      *e = nullptr;
+      nsgpu_p2p_destroy(h);
+      return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipEventCreate failed");
+    }
+  if (hipHostMalloc((void **)&h->done_host, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+    h->done_host = nullptr;
+    nsgpu_p2p_destroy(h);
+    return set_error(NSGPU_ENOMEM, "nsgpu_p2p_create: hipHostMalloc failed");
+  }
+  if (hipMemcpy(h->d_M, &h->M, sizeof(P2PDev), hipMemcpyHostToDevice) != hipSuccess) {
+    nsgpu_p2p_destroy(h);
+    return set_error(NSGPU_EHIP, "nsgpu_p2p_create: upload failed");
+  }
   *out = h;
   return NSGPU_OK;
 }
@@ -1202,23 +1271,72 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.app_last_start, 0, A * sizeof(uint64_t), s));
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
   NSGPU_HIP(hipMemsetAsync(M.node_head, 0xff, M.n_nodes * sizeof(uint32_t), s));
-  NSGPU_HIP(hipMemsetAsync(M.stats, 0, sizeof(nsgpu_p2p_stats), s));
+  NSGPU_HIP(hipMemsetAsync(M.wrank, 0, WCAP * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemcpyAsync(M.C, &h->C0, sizeof(Ctl), hipMemcpyHostToDevice, s));
   return NSGPU_OK;
 }
 
-extern "C" int nsgpu_p2p_set_profile(nsgpu_p2p *h, uint64_t *d_phase_cycles) {
-  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_profile: null");
-  h->M.prof = d_phase_cycles;
+static int build_graph(nsgpu_p2p *h) {
+  // NWIN windows of the pipeline; kernels read every run-dependent value from the device (Ctl), so
+  // one instantiated graph serves every run of this engine
+  hipGraph_t g = nullptr;
+  NSGPU_HIP(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
+  for (int w = 0; w < NWIN; w++) {
+    hipLaunchKernelGGL(k_reduce, dim3(GRID_POOL), dim3(TB), 0, h->s, h->d_M);
+    hipLaunchKernelGGL(k_partition, dim3(GRID_POOL), dim3(TB), 0, h->s, h->d_M);
+    hipLaunchKernelGGL(k_refit, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->d_M);
+    hipLaunchKernelGGL(k_rank, dim3(NT * NT), dim3(TB), 0, h->s, h->d_M);
+    hipLaunchKernelGGL(k_scatter, dim3(WCAP / RB), dim3(RB), 0, h->s, h->d_M);
+    hipLaunchKernelGGL(k_handle, dim3(WCAP / RB), dim3(RB), 0, h->s, h->d_M, h->sink_of_node);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->d_M);
+    hipLaunchKernelGGL(k_append, dim3(WCAP / RB), dim3(RB), 0, h->s, h->d_M);
+  }
+  hipError_t e = hipStreamEndCapture(h->s, &g);
+  if (e != hipSuccess) return set_error(NSGPU_EHIP, "nsgpu_p2p: graph capture: %s", hipGetErrorString(e));
+  e = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    h->gexec = nullptr;
+    return set_error(NSGPU_EHIP, "nsgpu_p2p: graph instantiate: %s", hipGetErrorString(e));
+  }
   return NSGPU_OK;
 }
 
+// Runs the simulation to completion (blocking): graph replays of NWIN windows on the engine stream,
+// ordered after the work already queued on `stream`; work queued on `stream` later runs after it.
 extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_run: null");
-  NSGPU_HIP(hipMemcpyAsync(h->d_M, &h->M, sizeof(P2PDev), hipMemcpyHostToDevice, (hipStream_t)stream));
-  hipLaunchKernelGGL(p2p_run, dim3(1), dim3(P2P_THREADS), sizeof(P2PLds), (hipStream_t)stream, h->d_M,
-                     h->sink_of_node);
-  NSGPU_HIP(hipGetLastError());
+  if (!h->gexec) {
+    int rc = build_graph(h);
+    if (rc) return rc;
+  }
+  hipStream_t cs = (hipStream_t)stream;
+  NSGPU_HIP(hipEventRecord(h->ev[0], cs));
+  NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev[0], 0));
+  NSGPU_HIP(hipEventRecord(h->t0, h->s));
+  h->done_host[0] = h->done_host[1] = 0;
+  // two replays in flight: replay i+1 is queued before the done flag of replay i is examined
+  for (uint64_t it = 0;; it++) {
+    NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
+    NSGPU_HIP(hipMemcpyAsync(&h->done_host[it & 1], &h->M.C->done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
+    NSGPU_HIP(hipEventRecord(h->ev[it & 1], h->s));
+    if (it > 0) {
+      NSGPU_HIP(hipEventSynchronize(h->ev[(it - 1) & 1]));
+      if (h->done_host[(it - 1) & 1]) break;
+    }
+  }
+  NSGPU_HIP(hipEventRecord(h->t1, h->s));
+  NSGPU_HIP(hipEventSynchronize(h->t1));
+  NSGPU_HIP(hipEventElapsedTime(&h->last_ms, h->t0, h->t1));
+  NSGPU_HIP(hipEventRecord(h->ev[0], h->s));
+  NSGPU_HIP(hipStreamWaitEvent(cs, h->ev[0], 0));
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_last_run_ms(nsgpu_p2p *h, double *gpu_ms) {
+  if (!h || !gpu_ms) return set_error(NSGPU_EINVAL, "nsgpu_p2p_last_run_ms: null");
+  *gpu_ms = h->last_ms;
   return NSGPU_OK;
 }
 
@@ -1228,7 +1346,8 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_results: null");
   hipStream_t s = (hipStream_t)stream;
   const P2PDev &M = h->M;
-  if (stats) NSGPU_HIP(hipMemcpyAsync(stats, M.stats, sizeof(*stats), hipMemcpyDeviceToHost, s));
+  Ctl c;
+  NSGPU_HIP(hipMemcpyAsync(&c, M.C, sizeof(Ctl), hipMemcpyDeviceToHost, s));
   if (devc) NSGPU_HIP(hipMemcpyAsync(devc, M.devc, M.n_devices * sizeof(*devc), hipMemcpyDeviceToHost, s));
   if (appc) NSGPU_HIP(hipMemcpyAsync(appc, M.appc, M.n_apps * sizeof(*appc), hipMemcpyDeviceToHost, s));
   if (log_n > M.log_cap) log_n = M.log_cap;
@@ -1238,6 +1357,19 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
   uint32_t err = 0;
   NSGPU_HIP(hipMemcpyAsync(&err, M.error, 4, hipMemcpyDeviceToHost, s));
   NSGPU_HIP(hipStreamSynchronize(s));
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    stats->dispatched = c.K;
+    stats->digest = c.digest;
+    stats->cancelled = c.cancelled;
+    stats->final_ts = c.last_ts;
+    stats->next_uid = c.uid;
+    stats->windows = (uint32_t)c.windows;
+    stats->ttl_drops = c.ttl_drops;
+    stats->no_route_drops = c.no_route;
+    stats->max_window = c.max_window;
+    stats->unreach_drops = c.unreach;
+  }
   if (error) *error = err;
   if (err) return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, "
                                           "4 = window limit, 8 = window cut)", err);

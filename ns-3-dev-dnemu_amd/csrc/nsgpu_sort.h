@@ -240,4 +240,85 @@ __device__ __forceinline__ void run_rank_sort(SortLds &L, uint32_t n) {
   }
 }
 
+// Workgroup merge sort of n <= SORT_N keys in L.k[0]/L.v[0][0, n) (ascending; equal keys keep no
+// particular order).  Work-efficient for a CU (16-lane SIMDs: a wave64 VALU op is 4 cycles), unlike a
+// bitonic network: each thread sorts 8 keys in registers, then log2(n / 8) merge rounds in which a
+// thread finds its 8-output diagonal of the merged block by a merge-path search and merges serially.
+// Only the first pow2ceil(n) / 8 threads work.  Result in L.k[0]/L.v[0][0, n).
+template <int THREADS>
+__device__ __forceinline__ void merge_sort(SortLds &L, uint32_t n) {
+  constexpr int VT = 8;
+  int npad = VT;
+  while (npad < (int)n) npad <<= 1;
+  const int t = threadIdx.x;
+  const bool act = t * VT < npad;
+  if (act) {
+    uint64_t k[VT];
+    uint32_t v[VT];
+#pragma unroll
+    for (int q = 0; q < VT; q++) {
+      const int i = t * VT + q;
+      k[q] = i < (int)n ? L.k[0][i] : ~0ull;
+      v[q] = i < (int)n ? L.v[0][i] : 0xffffffffu;
+    }
+    // odd-even transposition network, 8 passes
+#pragma unroll
+    for (int pass = 0; pass < VT; pass++) {
+#pragma unroll
+      for (int q = pass & 1; q + 1 < VT; q += 2) cswap(k[q], v[q], k[q + 1], v[q + 1], true);
+    }
+#pragma unroll
+    for (int q = 0; q < VT; q++) {
+      L.k[0][t * VT + q] = k[q];
+      L.v[0][t * VT + q] = v[q];
+    }
+  }
+  __syncthreads();
+  int src = 0;
+#pragma unroll 1
+  for (int blk = VT; blk < npad; blk <<= 1) {
+    if (act) {
+      const uint64_t *sk = L.k[src];
+      const uint32_t *sv = L.v[src];
+      const int d = (t * VT) & (2 * blk - 1);  // output diagonal inside the merged block
+      const int s0 = t * VT - d;                // merged block start; A = [s0, s0+blk), B = [s0+blk, s0+2blk)
+      int lo = d > blk ? d - blk : 0, hi = d < blk ? d : blk;
+      while (lo < hi) {  // merge path: # of A keys among the first d outputs (A first on ties)
+        const int mid = (lo + hi) >> 1;
+        if (!(sk[s0 + blk + d - 1 - mid] < sk[s0 + mid])) lo = mid + 1;
+        else hi = mid;
+      }
+      int ia = s0 + lo, ib = s0 + blk + d - lo;
+      const int ea = s0 + blk, eb = s0 + 2 * blk;
+      uint64_t ka = ia < ea ? sk[ia] : ~0ull, kb = ib < eb ? sk[ib] : ~0ull;
+      uint64_t *dk = L.k[src ^ 1];
+      uint32_t *dv = L.v[src ^ 1];
+#pragma unroll
+      for (int q = 0; q < VT; q++) {
+        const bool takea = ib >= eb || (ia < ea && !(kb < ka));
+        if (takea) {
+          dk[t * VT + q] = ka;
+          dv[t * VT + q] = sv[ia];
+          ia++;
+          ka = ia < ea ? sk[ia] : ~0ull;
+        } else {
+          dk[t * VT + q] = kb;
+          dv[t * VT + q] = sv[ib];
+          ib++;
+          kb = ib < eb ? sk[ib] : ~0ull;
+        }
+      }
+    }
+    src ^= 1;
+    __syncthreads();
+  }
+  if (src == 1) {
+    for (int i = t; i < (int)n; i += THREADS) {
+      L.k[0][i] = L.k[1][i];
+      L.v[0][i] = L.v[1][i];
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace nsgpu

@@ -95,7 +95,7 @@ SIGNATURES = {
     "nsgpu_p2p_run": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_results": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
     "nsgpu_p2p_destroy": (C.c_int, [_vp]),
-    "nsgpu_p2p_set_profile": (C.c_int, [_vp, _vp]),
+    "nsgpu_p2p_last_run_ms": (C.c_int, [_vp, C.POINTER(C.c_double)]),
     "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
 }
 

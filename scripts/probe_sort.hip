@@ -4,6 +4,9 @@
 #include <stdlib.h>
 #include "../ns-3-dev-dnemu_amd/csrc/nsgpu_sort.h"
 using namespace nsgpu;
+#ifndef ALG
+#define ALG 1
+#endif
 __global__ __launch_bounds__(512) void k(const uint64_t *in, uint32_t n, uint64_t *out, uint64_t *cyc, int reps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   SortLds &L = *reinterpret_cast<SortLds *>(smem);
@@ -15,7 +18,8 @@ __global__ __launch_bounds__(512) void k(const uint64_t *in, uint32_t n, uint64_
     }
     __syncthreads();
     t0 = __builtin_amdgcn_s_memtime();
-    run_rank_sort<512>(L, n);
+    if (ALG == 0) run_rank_sort<512>(L, n);
+    else merge_sort<512>(L, n);
     acc += __builtin_amdgcn_s_memtime() - t0;
   }
   for (int i = threadIdx.x; i < (int)n; i += 512) out[i] = L.k[0][i];
@@ -35,6 +39,6 @@ int main(int argc, char **argv) {
   hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
   int ok = 1;
   for (uint32_t i = 1; i < n; i++) ok &= o[i - 1] < o[i];
-  printf("n %u distinct %d: sorted %d, %llu cycles/sort\n", n, distinct, ok, (unsigned long long)c);
+  printf("alg %d n %u distinct %d: sorted %d, %llu cycles/sort\n", ALG, n, distinct, ok, (unsigned long long)c);
   return 0;
 }
