@@ -14,9 +14,10 @@ Neither workload shards inside one simulation yet, so with --gpus N every rank r
 independent replica ("replicas", weak scaling) and `value` is the events of all ranks divided by
 the slowest rank's time.
 
-roofline: dominant kernel = the persistent engine kernel; algorithmic bytes per event from
-SURVEY §8(d) (queue: 72 B/event; p2p hop: 208 B per hop = 104 B per event) x events per launch,
-divided by the kernel's average duration measured with HIP events on its own stream.
+roofline: dominant kernel = the churn's persistent kernel, or for p2p-grid the window-pipeline
+kernel with the largest average launch time (per-kernel HIP events in a separate bracketed run);
+algorithmic bytes per event from SURVEY §8(d) (queue: 72 B/event; p2p hop: 208 B per hop = 104 B
+per event) x events per launch (p2p: the average window), divided by that average duration.
 cpu_baseline: the oracle's sequential restatement of the same reference path (DefaultSimulatorImpl
 + MapScheduler + the handler chain, "port"), on one host core, same scenario.
 """
@@ -68,6 +69,10 @@ class Churn:
     def step(self):
         self.run.launch()
 
+    def roofline(self, step_kernel_ms, events_per_step):
+        # one persistent launch per step: the step's device time is the kernel's
+        return {"kernel": self.kernel, "kernel_ms": step_kernel_ms, "events_per_launch": events_per_step}
+
     def result(self):
         st, _, _ = self.run.result()
         return int(st.dispatched), int(st.digest), {"rounds_per_step": int(st.rounds), "max_batch": int(st.max_batch)}
@@ -101,6 +106,20 @@ class P2PGrid:
     def step(self):
         self.engine.reset()
         self.engine.launch()
+
+    def roofline(self, step_kernel_ms, events_per_step):
+        # the window pipeline is 8 kernels per window; a separate eager run brackets each kernel of
+        # every 4th window with HIP events on the engine stream, and the kernel with the largest
+        # total time is the dominant one (events per launch = the average window)
+        prof = self.engine.profile(sample_every=4)
+        st, _, _, _ = self.engine.results()
+        windows = max(int(st.windows), 1)
+        name = max(prof, key=lambda k: prof[k][0])
+        return {"kernel": "nsgpu::" + name, "kernel_ms": prof[name][0],
+                "events_per_launch": events_per_step / windows,
+                "step_device_ms": step_kernel_ms, "windows_per_step": windows,
+                "pipeline_ms_per_window": {k: round(v[0] * 1e3, 3) for k, v in prof.items()},
+                "pipeline_unit": "us per launch (HIP events, sampled windows)"}
 
     def result(self):
         st, devc, appc, _ = self.engine.results()
@@ -186,7 +205,9 @@ def main():
         elapsed = float(t.item())
 
     value = events_per_step * args.steps * world / elapsed
-    achieved = wl.bytes_per_event * events_per_step / (kernel_ms / 1e3) / 1e9
+    # dominant kernel: name, events one launch processes, average launch duration (HIP events)
+    rl = wl.roofline(kernel_ms, events_per_step)
+    achieved = wl.bytes_per_event * rl["events_per_launch"] / (rl["kernel_ms"] / 1e3) / 1e9
     traffic = None
     tpath = os.path.join(REPO, "profiles", f"traffic_{args.workload}.json")
     if os.path.exists(tpath):
@@ -218,9 +239,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
-                "kernel": wl.kernel,
-                "kernel_ms": kernel_ms,
                 "bytes_per_event": wl.bytes_per_event,
+                **rl,
             },
         }
         if not args.no_cpu_baseline:

@@ -173,6 +173,19 @@ int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev_counters *
 int nsgpu_p2p_destroy(nsgpu_p2p *h);
 /* GPU time (ms, HIP events on the engine stream) of the last nsgpu_p2p_run. */
 int nsgpu_p2p_last_run_ms(nsgpu_p2p *h, double *gpu_ms);
+/* Launch mode of nsgpu_p2p_run: 0 = hipGraph replays (default), 1 = the same kernels launched one by
+ * one (also selected by the environment variable NSGPU_P2P_EAGER; used under rocprofv3). */
+int nsgpu_p2p_set_eager(nsgpu_p2p *h, int eager);
+/* The window pipeline's kernels: count and names (launch order). */
+int nsgpu_p2p_kernel_count(int *n);
+const char *nsgpu_p2p_kernel_name(int k);
+/* Per-kernel device time of one full run (from the state nsgpu_p2p_reset loaded): every
+ * sample_every-th window brackets each kernel with HIP events on the engine stream; kernel_ms[k] and
+ * launches[k] (nsgpu_p2p_kernel_count entries) accumulate the bracketed time and launch count. */
+int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_every, double *kernel_ms, uint64_t *launches);
+/* Diagnostic: in-kernel phase timers (s_memrealtime ticks, 100 MHz) of the pipeline kernels; only the
+ * lib/libnsgpu_prof.so build (-DNSGPU_PHASE_PROF) records them, the product library returns ESTATE. */
+int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset);
 
 #ifdef __cplusplus
 }

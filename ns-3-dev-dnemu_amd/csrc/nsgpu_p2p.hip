@@ -9,23 +9,23 @@
 //   IPv4/UDP   ipv4-l3-protocol.cc:434-537,815-841 (static next-hop routes, TTL)
 //
 // Engine (MI355X).  The simulation advances in conservative windows; each window is a fixed pipeline
-// of short multi-CU kernels (a CU is 64 lanes per clock, so no phase may live on one CU), replayed
-// from a hipGraph of NWIN windows until the device-side `done` flag is set:
-//   k_reduce     W_end = min over pending e of (ts_e + L(kind_e)), L = the smallest delay any child of
+// of five short multi-CU kernels (a CU is 64 lanes per clock, so no phase may live on one CU),
+// replayed from a hipGraph of NWIN windows until the device-side `done` flag is set:
+//   k_partition  W_end = min over pending e of (ts_e + L(kind_e)) comes from the previous window
+//                (leftovers folded here, children in k_append), L = the smallest delay any child of
 //                that kind of handler can have: DefaultSimulatorImpl's uids make a child sort after every
-//                pending event with ts <= its own, so every pending event with ts <= W_end is safe;
-//   k_partition  window keys ((ts - tmin) << 32 | uid, capped at the Simulator::Stop key) -> window
-//                list, the rest -> the other pool buffer (wave-aggregated atomic slots);
-//   k_refit      only when the window overflowed WCAP: bisection for the largest key prefix that fits
-//                (a key prefix of a safe window is safe), single workgroup;
-//   k_rank       dispatch rank of every window key by tiled all-pairs counting (WCAP^2 / 256 CUs);
-//   k_scatter    rank order; per-node chains through node_head (one atomicExch per event);
-//   k_handle     the chain holder of each node runs that node's events in rank order, so node state
+//                pending event with ts <= its own, so every pending event with ts <= W_end is safe.
+//                Window events -> slot records ((ts - tmin) << 32 | uid keys, capped at the
+//                Simulator::Stop key) and per-node slot tables; the rest -> the other pool buffer;
+//   k_refit      only when the window overflowed WCAP: 256-way radix bisection for the largest key
+//                prefix that fits (a key prefix of a safe window is safe), single workgroup;
+//   k_handle_rank  the holder of each node runs that node's events in key order, so node state
 //                (device tx state, DropTail rings, OnOff state, sink counters) needs no atomics;
-//                children go to per-rank slots in Schedule-call order;
-//   k_scan       exclusive scans of child counts in rank order (uids), run bookkeeping;
+//                children go to per-slot records in Schedule-call order.  The same launch's other
+//                blocks rank the window keys by tiled all-pairs counting;
+//   k_scan       rank order; exclusive scans of child counts (uids), run bookkeeping;
 //   k_append     digest/log of the dispatch order, children -> pool with the uids DefaultSimulatorImpl
-//                would assign.
+//                would assign, and their part of the next window's reduction.
 #include "nsgpu_device.h"
 #include "nsgpu_internal.h"
 
@@ -48,12 +48,16 @@ enum EvKind : uint32_t {
 };
 
 constexpr int WCAP = 4096;       // events per window
-constexpr int TB = 256;          // threads per block, pool sweeps and k_rank
-constexpr int RB = 64;           // threads per block, per-rank kernels (spread over CUs)
-constexpr int NT = WCAP / TB;    // rank tiles per side
-constexpr int GRID_POOL = 256;   // blocks of the pool sweeps (grid-stride)
+constexpr int TB = 256;          // threads per block, pool sweeps
+constexpr int HB = 64;           // threads per block, per-slot kernels (spread over CUs)
+constexpr int NHB = WCAP / HB;   // handler blocks of k_handle_rank
+constexpr int RJ = 256;          // keys per rank tile column
+constexpr int NJT = WCAP / RJ;   // rank tile columns
+constexpr int NRB = NHB * NJT;   // rank tile blocks of k_handle_rank
+constexpr int GRID_POOL = 256;   // blocks of the pool sweep (grid-stride)
 constexpr int SCAN_THREADS = 1024;
-constexpr int CH = 16;           // chain entries a handler thread sorts in LDS
+constexpr int CH = 16;           // events of one node a handler thread sorts in LDS
+constexpr int NSLOT = 8;         // per-node slot table entries
 constexpr int NWIN = 32;         // windows per graph replay
 constexpr uint32_t NOCTX = 0xffffffffu;
 constexpr uint32_t NOCHAIN = 0xffffffffu;
@@ -62,22 +66,29 @@ struct Pkt {
   uint32_t app, seq, size, ttl;
 };
 
-// Device-resident run control (one per engine); every field is written by one kernel of the window
-// pipeline and read by later ones, never read and written by different blocks of one kernel except
-// through atomics.
-struct Ctl {
-  uint64_t P;                  // pending events in pool `cur`
-  uint64_t K;                  // dispatched so far
-  uint64_t tmin, wend, stopts; // window reduction (atomicMin); ~0 between windows
-  uint64_t bound, span, inline_lim;
-  uint64_t windows, max_window, last_ts, max_windows;
-  uint64_t digest, cancelled, ttl_drops, no_route, unreach;
-  uint64_t K0, tmin0, inline_lim0;  // the window k_append works on (set by k_scan)
-  uint32_t uid, cur, W, nxtP, overflow, done, stop_seen, scan_ran;
-  uint32_t stopuid, uid0, W0, Pbase, total_children, total_inline, pad0, pad1;
+// Reduction of a pending set: the next window's bound (atomicMin), the pending Stop.
+struct Red {
+  uint64_t tmin, wend, stopts;
+  uint32_t stopuid, pad;
 };
 
-// Device-resident model + engine state (all pointers are HBM).
+// Device-resident run control (one per engine).  Every field is written by one kernel of the
+// window pipeline and read by later ones, never read and written by different blocks of one kernel
+// except through atomics.  Window k: red[(k + 1) & 1] holds the pending set's reduction that bounds
+// it; its leftovers and children fold into red[k & 1].
+struct Ctl {
+  Red red[2];
+  uint64_t P;                          // pending events in pool `cur` (besides the last window's children)
+  uint64_t K;                          // dispatched so far (after the last scanned window)
+  uint64_t tmin, bound, inline_lim;    // current window (k_pa / refit)
+  uint64_t windows, max_window, last_ts, max_windows;
+  uint64_t digest, cancelled, ttl_drops, no_route, unreach;
+  uint64_t pK0, ptmin, pinline_lim;    // the last scanned window, appended by the next k_pa
+  uint32_t uid, cur, W, nxtP, overflow, prep, done, stop_seen;
+  uint32_t puid0, pW, pvalid, pinl;
+};
+
+// Device-resident model + engine state (all pointers are HBM).  Passed to the kernels by value.
 struct P2PDev {
   // scenario
   uint32_t n_nodes, n_devices, n_apps, n_dst, qcap, maxc;
@@ -90,6 +101,7 @@ struct P2PDev {
   const uint64_t *app_rate;
   const double *app_on_s, *app_off_s;
   const uint32_t *node_app_off, *node_app_list;  // CSR: apps of each node in AddApplication order
+  const int32_t *sink_of_node;                    // PacketSink of each node (-1: none)
   int64_t lookahead[K_NKINDS];
   // model state
   uint32_t *dev_busy, *q_head, *q_count;
@@ -99,19 +111,28 @@ struct P2PDev {
   uint32_t *app_send_gen, *app_ss_gen, *app_residual, *app_tot, *app_seq;
   uint64_t *app_last_start;
   nsgpu_app_counters *appc;
-  // event pools (double-buffered SoA)
+  // pending pool (double-buffered SoA)
   uint64_t *ev_ts[2];
   uint32_t *ev_uid[2], *ev_ctx[2], *ev_kind[2], *ev_a[2];
   Pkt *ev_pkt[2];
   uint64_t pool_cap;
-  // the window (WCAP entries each): partition order (w*), rank order (s*, link, counts, prefixes)
-  uint64_t *wkey, *skey;
-  uint32_t *wpi, *wrank, *spi, *sctx, *link, *nchild, *ninl, *cpref, *ipref, *gbnd;
-  uint32_t *node_head;  // per-node chain head of the current window (NOCHAIN between windows)
-  // children of the current window: slot = rank * maxc + j
+  // the current window (WCAP slots): slot records (k_pa) ...
+  uint64_t *wkey;
+  uint32_t *wctx, *wkind, *wa, *widx;
+  Pkt *wpkt;
+  // ... handler outputs: child counts and child records (slot * maxc + j, Schedule-call order) ...
+  uint32_t *nchild, *ninl;
   uint64_t *ch_ts;
   uint32_t *ch_ctx, *ch_kind, *ch_a;
   Pkt *ch_pkt;
+  // ... dispatch info per slot (k_scan), and the keys / contexts k_scan keeps for the next k_pa
+  // (which rewrites wkey / wctx with the next window while it appends this one)
+  uint4 *sinfo;
+  uint64_t *pwkey;
+  uint32_t *pwctx;
+  uint32_t *wrank;  // rank accumulators of the current window (0 between windows)
+  // per-node slot tables of the current window (node_cnt is 0 between windows)
+  uint32_t *node_cnt, *node_slot;
   // run control / outputs
   uint32_t n_init;    // initial pending count (pool 0)
   uint32_t uid_init;  // m_uid after setup
@@ -172,106 +193,114 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uin
 }
 
 // ---------------- model (runs on the thread that owns the event's node) ----------------
+// Children of the event being run go to its slot's child records in Schedule-call order; the ones
+// that stay pending fold into the next window's reduction (tmn, wnd).
 struct Emit {
-  const P2PDev *M;
   uint64_t now;
   uint32_t ctx;
-  uint32_t slot0;  // rank * maxc
+  uint32_t slot0;  // slot * maxc
   uint32_t n;
-  __device__ void child(int64_t delay, uint32_t ctx_, uint32_t kind, uint32_t a, Pkt p) {
+  uint64_t *ch_ts;
+  uint32_t *ch_ctx, *ch_kind, *ch_a;
+  Pkt *ch_pkt;
+  const int64_t *lookahead;
+  uint64_t tmn, wnd;
+  __device__ __forceinline__ void child(int64_t delay, uint32_t ctx_, uint32_t kind, uint32_t a, Pkt p) {
     const uint32_t s = slot0 + n++;
-    M->ch_ts[s] = now + (uint64_t)delay;
-    M->ch_ctx[s] = ctx_;
-    M->ch_kind[s] = kind;
-    M->ch_a[s] = a;
-    M->ch_pkt[s] = p;
+    const uint64_t ts = now + (uint64_t)delay;
+    ch_ts[s] = ts;
+    ch_ctx[s] = ctx_;
+    ch_kind[s] = kind;
+    ch_a[s] = a;
+    ch_pkt[s] = p;
+    if ((kind & 0xffu) != K_FWD_UP) {  // DoForwardUp is a leaf run inside the window, never re-queued
+      tmn = ts < tmn ? ts : tmn;
+      const uint64_t e = ts + (uint64_t)lookahead[kind & 0xffu];
+      wnd = e < wnd ? e : wnd;
+    }
   }
 };
 
-__device__ __forceinline__ int64_t tx_time(const P2PDev &M, uint32_t d, uint32_t size) {
-  // Seconds (m_bps.CalculateTxTime (size)): static_cast<double>(bytes)*8/m_bps (data-rate.cc:224-227)
-  return seconds_to_ts(static_cast<double>(size) * 8 / (double)M.dev_bps[d]);
-}
+// Run statistics of one handler thread.
+struct HStat {
+  uint64_t cancelled, ttl_drops, no_route, unreach;
+  bool stop;
+};
 
-__device__ void transmit_start(const P2PDev &M, Emit &E, uint32_t d, const Pkt &p) {
-  M.dev_busy[d] = 1;
-  M.devc[d].tx_packets++;
-  const int64_t txTime = tx_time(M, d, p.size);
-  E.child(txTime + M.dev_ifg[d], E.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});  // Schedule (txCompleteTime)
+// Device step of an event (second phase of every handler, run by all lanes together so the wave
+// does not serialise one copy per event kind):
+//   SEND  PointToPointNetDevice::Send (point-to-point-net-device.cc:462-518): PppHeader, enqueue
+//         (DropTail: queue.cc:61-97, drop-tail-queue.cc:83-100), and if the device is idle dequeue
+//         + TransmitStart;
+//   KICK  TransmitComplete (:304-346): device idle, dequeue, TransmitStart if a packet was queued.
+// TransmitStart (:206-269) + PointToPointChannel::TransmitStart (point-to-point-channel.cc:82-103):
+//   Schedule (txTime + ifg, TransmitComplete); ScheduleWithContext (peer node, txTime + delay, Receive).
+enum : uint32_t { ACT_NONE = 0, ACT_SEND = 1, ACT_KICK = 2 };
+struct Act {
+  uint32_t op, dev;
+  Pkt p;
+};
+
+__device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &act) {
+  if (act.op == ACT_NONE) return;
+  const uint32_t d = act.dev;
+  // every operand of the step at once
+  const uint32_t busy = M.dev_busy[d], cnt = M.q_count[d], head = M.q_head[d], qmax = M.dev_qmax[d];
+  nsgpu_dev_counters dc = M.devc[d];
+  const uint64_t bps = M.dev_bps[d];
+  const int64_t ifg = M.dev_ifg[d], delay = M.dev_delay[d];
   const uint32_t peer = M.dev_peer[d];
-  E.child(txTime + M.dev_delay[d], M.dev_node[peer], K_RECEIVE, peer, p);   // channel ScheduleWithContext
-}
-
-__device__ bool enqueue(const P2PDev &M, uint32_t d, const Pkt &p) {
-  const uint32_t cnt = M.q_count[d];
-  if (cnt >= M.dev_qmax[d]) {
-    M.devc[d].drop_packets++;
-    M.devc[d].drop_bytes += p.size;
-    return false;
-  }
-  const uint32_t pos = (M.q_head[d] + cnt) % M.qcap;
-  M.q_buf[(uint64_t)d * M.qcap + pos] = p;
-  M.q_count[d] = cnt + 1;
-  M.devc[d].enq_packets++;
-  M.devc[d].enq_bytes += p.size;
-  return true;
-}
-
-__device__ bool dequeue(const P2PDev &M, uint32_t d, Pkt &out) {
-  const uint32_t cnt = M.q_count[d];
-  if (cnt == 0) return false;
-  const uint32_t h = M.q_head[d];
-  out = M.q_buf[(uint64_t)d * M.qcap + h];
-  M.q_head[d] = (h + 1) % M.qcap;
-  M.q_count[d] = cnt - 1;
-  M.devc[d].deq_packets++;
-  return true;
-}
-
-__device__ void device_send(const P2PDev &M, Emit &E, uint32_t d, Pkt p) {
-  p.size += 2;  // PppHeader
-  if (M.dev_busy[d] == 0) {
-    if (enqueue(M, d, p)) {
-      Pkt q;
-      dequeue(M, d, q);
-      transmit_start(M, E, d, q);
+  const uint32_t peer_node = M.dev_node[peer];
+  Pkt *qb = M.q_buf + (uint64_t)d * M.qcap;
+  uint32_t ncnt = cnt, nhead = head, nbusy = busy;
+  bool go = false;
+  Pkt tx{0, 0, 0, 0};
+  if (act.op == ACT_SEND) {
+    Pkt p = act.p;
+    p.size += 2;  // PppHeader
+    if (cnt >= qmax) {
+      dc.drop_packets++;
+      dc.drop_bytes += p.size;
+    } else {
+      dc.enq_packets++;
+      dc.enq_bytes += p.size;
+      if (busy == 0) {  // Enqueue + Dequeue: the head of the queue leaves at once
+        if (cnt == 0) {
+          tx = p;  // (the ring slot would be written and read back: skip it)
+        } else {
+          qb[(head + cnt) % M.qcap] = p;
+          tx = qb[head];
+        }
+        nhead = (head + 1) % M.qcap;
+        dc.deq_packets++;
+        go = true;
+      } else {
+        qb[(head + cnt) % M.qcap] = p;
+        ncnt = cnt + 1;
+      }
     }
-  } else {
-    enqueue(M, d, p);
-  }
-}
-
-__device__ void ip_send(const P2PDev &M, Emit &E, uint32_t n, const Pkt &p, uint64_t *no_route) {
-  const uint32_t out = M.route[(uint64_t)n * M.n_dst + M.app_dst_slot[p.app]];
-  if (out == 0xffffffffu) {
-    (*no_route)++;
-    return;
-  }
-  device_send(M, E, out, p);
-}
-
-__device__ void ip_receive(const P2PDev &M, Emit &E, uint32_t n, Pkt p, int32_t sink, uint64_t *ttl_drops,
-                           uint64_t *no_route, uint64_t *unreach) {
-  if (M.app_dst_node[p.app] == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
-    if (sink < 0 || !(M.app_flags[sink] & 2u)) {  // no bound endpoint: RX_ENDPOINT_UNREACH
-      (*unreach)++;
-      return;
+  } else {  // ACT_KICK
+    nbusy = 0;
+    if (cnt > 0) {
+      tx = qb[head];
+      nhead = (head + 1) % M.qcap;
+      ncnt = cnt - 1;
+      dc.deq_packets++;
+      go = true;
     }
-    // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120)
-    E.child(0, E.ctx, K_FWD_UP, (uint32_t)sink, p);
-    return;
   }
-  const uint32_t out = M.route[(uint64_t)n * M.n_dst + M.app_dst_slot[p.app]];
-  if (out == 0xffffffffu) {
-    (*no_route)++;
-    return;
+  if (go) {
+    nbusy = 1;
+    dc.tx_packets++;
+    // Seconds (m_bps.CalculateTxTime (size)): static_cast<double>(bytes)*8/m_bps (data-rate.cc:224-227)
+    const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)bps);
+    E.child(txTime + ifg, E.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
+    E.child(txTime + delay, peer_node, K_RECEIVE, peer, tx);
   }
-  p.ttl -= 1;  // IpForward
-  if (p.ttl == 0) {
-    (*ttl_drops)++;
-    return;
-  }
-  device_send(M, E, out, p);
+  if (nbusy != busy) M.dev_busy[d] = nbusy;
+  if (ncnt != cnt) M.q_count[d] = ncnt;
+  if (nhead != head) M.q_head[d] = nhead;
+  M.devc[d] = dc;
 }
 
 // int64x64 residual-bits update of OnOffApplication::CancelEvents (onoff-application.cc:170-173):
@@ -299,7 +328,7 @@ __device__ __forceinline__ u128 divu(u128 a, u128 b) {
   quo = rem / div;
   return result + quo;
 }
-__device__ int64_t residual_bits(int64_t delta_ns, uint64_t rate) {
+__device__ __noinline__ int64_t residual_bits(int64_t delta_ns, uint64_t rate) {
   // Invert (1e9) (int64x64-128.cc:119-134)
   u128 one = ((u128)1) << 64;
   i128 inv = (i128)divu(one, (u128)1000000000ull);
@@ -333,7 +362,7 @@ __device__ int64_t residual_bits(int64_t delta_ns, uint64_t rate) {
   return rn ? -h : h;
 }
 
-__device__ void cancel_events(const P2PDev &M, uint32_t a, uint64_t now) {
+__device__ __forceinline__ void cancel_events(const P2PDev &M, uint32_t a, uint64_t now) {
   uint32_t f = M.app_flags[a];
   if (f & 4u) {  // m_sendEvent.IsRunning ()
     const int64_t delta = (int64_t)now - (int64_t)M.app_last_start[a];
@@ -342,39 +371,50 @@ __device__ void cancel_events(const P2PDev &M, uint32_t a, uint64_t now) {
   M.app_flags[a] = f & ~(4u | 8u);  // Cancel (m_sendEvent); Cancel (m_startStopEvent)
 }
 
-__device__ void schedule_start_event(const P2PDev &M, Emit &E, uint32_t a) {
+__device__ __forceinline__ void schedule_start_event(const P2PDev &M, Emit &E, uint32_t a) {
   const uint32_t g = (M.app_ss_gen[a] + 1) & 0xffffffu;
   M.app_ss_gen[a] = g;
   M.app_flags[a] |= 8u;
   E.child(seconds_to_ts(M.app_off_s[a]), E.ctx, K_START_SENDING | (g << 8), a, Pkt{0, 0, 0, 0});
 }
-__device__ void schedule_stop_event(const P2PDev &M, Emit &E, uint32_t a) {
+__device__ __forceinline__ void schedule_stop_event(const P2PDev &M, Emit &E, uint32_t a) {
   const uint32_t g = (M.app_ss_gen[a] + 1) & 0xffffffu;
   M.app_ss_gen[a] = g;
   M.app_flags[a] |= 8u;
   E.child(seconds_to_ts(M.app_on_s[a]), E.ctx, K_STOP_SENDING | (g << 8), a, Pkt{0, 0, 0, 0});
 }
-__device__ void stop_application(const P2PDev &M, uint32_t a, uint64_t now) {
+__device__ __forceinline__ void stop_application(const P2PDev &M, uint32_t a, uint64_t now) {
   if (M.app_kind[a] == NSGPU_APP_SINK) {
     M.app_flags[a] &= ~2u;
     return;
   }
   cancel_events(M, a, now);
 }
-__device__ void schedule_next_tx(const P2PDev &M, Emit &E, uint32_t a) {
+// OnOffApplication::ScheduleNextTx (onoff-application.cc:228-252); the child is returned, not
+// emitted: in SendPacket it is scheduled after the packet's device children.
+struct Post {
+  bool valid;
+  int64_t delay;
+  uint32_t kind, a;
+};
+__device__ __forceinline__ Post schedule_next_tx(const P2PDev &M, uint32_t a, uint64_t now) {
+  Post po{false, 0, 0, 0};
   const uint32_t maxb = M.app_max_bytes[a];
   if (maxb == 0 || M.app_tot[a] < maxb) {
     const uint32_t bits = M.app_pkt_size[a] * 8 - M.app_residual[a];
-    const int64_t next = seconds_to_ts(bits / static_cast<double>(M.app_rate[a]));
     const uint32_t g = (M.app_send_gen[a] + 1) & 0xffffffu;
     M.app_send_gen[a] = g;
     M.app_flags[a] |= 4u;
-    E.child(next, E.ctx, K_SEND | (g << 8), a, Pkt{0, 0, 0, 0});
+    po.valid = true;
+    po.delay = seconds_to_ts(bits / static_cast<double>(M.app_rate[a]));
+    po.kind = K_SEND | (g << 8);
+    po.a = a;
   } else {
-    stop_application(M, a, E.now);
+    stop_application(M, a, now);
   }
+  return po;
 }
-__device__ void appobj_start(const P2PDev &M, Emit &E, uint32_t a) {  // Application::DoStart
+__device__ __forceinline__ void appobj_start(const P2PDev &M, Emit &E, uint32_t a) {  // Application::DoStart
   uint32_t f = M.app_flags[a];
   if (f & 1u) return;
   M.app_flags[a] = f | 1u;
@@ -382,498 +422,873 @@ __device__ void appobj_start(const P2PDev &M, Emit &E, uint32_t a) {  // Applica
   if (M.app_stop[a] != 0) E.child(M.app_stop[a], E.ctx, K_APP_STOP, a, Pkt{0, 0, 0, 0});
 }
 
-// Runs one event; returns true if it was a cancelled dispatch.
-__device__ __noinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a, const Pkt &pkt, int32_t sink,
-                          uint64_t *ttl_drops, uint64_t *no_route, uint64_t *unreach, bool *stop) {
+// Ipv4 route lookup: the static next-hop device of node n towards the packet's destination.
+__device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const Pkt &p) {
+  return M.route[(uint64_t)n * M.n_dst + M.app_dst_slot[p.app]];
+}
+
+// One event: the kind-specific first phase, then the device step, then a trailing child.  Returns
+// true if it was a cancelled dispatch.
+__device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a, const Pkt &pkt,
+                                          int32_t sink, HStat &hs) {
   const uint32_t kind = kind_word & 0xffu;
   const uint32_t gen = kind_word >> 8;
-  switch (kind) {
-    case K_NODE_START: {
-      for (uint32_t i = M.node_app_off[a]; i < M.node_app_off[a + 1]; i++) appobj_start(M, E, M.node_app_list[i]);
-      return false;
-    }
-    case K_DEV_START:
-      return false;
-    case K_APPOBJ_START:
-      appobj_start(M, E, a);
-      return false;
-    case K_APP_START:
-      if (M.app_kind[a] == NSGPU_APP_SINK) {
-        M.app_flags[a] |= 2u;
+  Act act{ACT_NONE, 0, Pkt{0, 0, 0, 0}};
+  Post post{false, 0, 0, 0};
+  bool cancelled = false;
+  if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive (ipv4-l3-protocol.cc:434-537)
+    M.devc[a].rx_packets++;
+    Pkt p = pkt;
+    p.size -= 2;
+    const uint32_t n = M.dev_node[a];
+    if (M.app_dst_node[p.app] == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
+      if (sink < 0 || !(M.app_flags[sink] & 2u)) {  // no bound endpoint: RX_ENDPOINT_UNREACH
+        hs.unreach++;
       } else {
-        cancel_events(M, a, E.now);
-        schedule_start_event(M, E, a);
+        // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120)
+        E.child(0, E.ctx, K_FWD_UP, (uint32_t)sink, p);
       }
-      return false;
-    case K_APP_STOP:
-      stop_application(M, a, E.now);
-      return false;
-    case K_START_SENDING: {
-      const uint32_t f = M.app_flags[a];
-      if (!((f & 8u) && M.app_ss_gen[a] == gen)) return true;  // cancelled
-      M.app_flags[a] = f & ~8u;
-      M.app_last_start[a] = E.now;
-      schedule_next_tx(M, E, a);
-      schedule_stop_event(M, E, a);
-      return false;
+    } else {
+      const uint32_t out = route_of(M, n, p);
+      if (out == 0xffffffffu) {
+        hs.no_route++;
+      } else {
+        p.ttl -= 1;  // IpForward (:815-841)
+        if (p.ttl == 0) hs.ttl_drops++;
+        else act = Act{ACT_SEND, out, p};
+      }
     }
-    case K_STOP_SENDING: {
-      const uint32_t f = M.app_flags[a];
-      if (!((f & 8u) && M.app_ss_gen[a] == gen)) return true;
-      M.app_flags[a] = f & ~8u;
-      cancel_events(M, a, E.now);
-      schedule_start_event(M, E, a);
-      return false;
-    }
-    case K_SEND: {
-      const uint32_t f = M.app_flags[a];
-      if (!((f & 4u) && M.app_send_gen[a] == gen)) return true;
+  } else if (kind == K_TX_COMPLETE) {
+    act = Act{ACT_KICK, a, Pkt{0, 0, 0, 0}};
+  } else if (kind == K_SEND) {  // OnOffApplication::SendPacket (onoff-application.cc:254-270)
+    const uint32_t f = M.app_flags[a];
+    if (!((f & 4u) && M.app_send_gen[a] == gen)) {
+      cancelled = true;
+    } else {
       M.app_flags[a] = f & ~4u;
       const uint32_t sz = M.app_pkt_size[a];
       Pkt p{a, M.app_seq[a]++, sz + 8 + 20, M.app_ttl[a]};
       M.appc[a].tx_packets++;
       M.appc[a].tx_bytes += sz;
-      ip_send(M, E, M.app_node[a], p, no_route);
+      const uint32_t out = route_of(M, M.app_node[a], p);
+      if (out == 0xffffffffu) hs.no_route++;
+      else act = Act{ACT_SEND, out, p};
       M.app_tot[a] += sz;
       M.app_last_start[a] = E.now;
       M.app_residual[a] = 0;
-      schedule_next_tx(M, E, a);
-      return false;
+      post = schedule_next_tx(M, a, E.now);
     }
-    case K_TX_COMPLETE: {
-      M.dev_busy[a] = 0;
-      Pkt p;
-      if (dequeue(M, a, p)) transmit_start(M, E, a, p);
-      return false;
-    }
-    case K_RECEIVE: {
-      M.devc[a].rx_packets++;
-      Pkt p = pkt;
-      p.size -= 2;
-      ip_receive(M, E, M.dev_node[a], p, sink, ttl_drops, no_route, unreach);
-      return false;
-    }
-    case K_FWD_UP:  // DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink::HandleRead (a = sink app)
-      if (M.app_flags[a] & 2u) {
-        M.appc[a].rx_packets++;
-        M.appc[a].rx_bytes += pkt.size - 28;
+  } else {
+    switch (kind) {
+      case K_NODE_START:
+        for (uint32_t i = M.node_app_off[a]; i < M.node_app_off[a + 1]; i++) appobj_start(M, E, M.node_app_list[i]);
+        break;
+      case K_APPOBJ_START:
+        appobj_start(M, E, a);
+        break;
+      case K_APP_START:
+        if (M.app_kind[a] == NSGPU_APP_SINK) {
+          M.app_flags[a] |= 2u;
+        } else {
+          cancel_events(M, a, E.now);
+          schedule_start_event(M, E, a);
+        }
+        break;
+      case K_APP_STOP:
+        stop_application(M, a, E.now);
+        break;
+      case K_START_SENDING: {  // onoff-application.cc:196-206
+        const uint32_t f = M.app_flags[a];
+        if (!((f & 8u) && M.app_ss_gen[a] == gen)) {
+          cancelled = true;
+          break;
+        }
+        M.app_flags[a] = f & ~8u;
+        M.app_last_start[a] = E.now;
+        post = schedule_next_tx(M, a, E.now);
+        if (post.valid) E.child(post.delay, E.ctx, post.kind, post.a, Pkt{0, 0, 0, 0});
+        post.valid = false;
+        schedule_stop_event(M, E, a);
+        break;
       }
-      return false;
-    case K_STOP:
-      *stop = true;
-      return false;
-    default:
-      return false;
+      case K_STOP_SENDING: {  // onoff-application.cc:208-216
+        const uint32_t f = M.app_flags[a];
+        if (!((f & 8u) && M.app_ss_gen[a] == gen)) {
+          cancelled = true;
+          break;
+        }
+        M.app_flags[a] = f & ~8u;
+        cancel_events(M, a, E.now);
+        schedule_start_event(M, E, a);
+        break;
+      }
+      case K_FWD_UP:  // DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink::HandleRead (a = sink app)
+        if (M.app_flags[a] & 2u) {
+          M.appc[a].rx_packets++;
+          M.appc[a].rx_bytes += pkt.size - 28;
+        }
+        break;
+      case K_STOP:
+        hs.stop = true;
+        break;
+      default:  // K_DEV_START: no-op
+        break;
+    }
   }
+  device_act(M, E, act);
+  if (post.valid) E.child(post.delay, E.ctx, post.kind, post.a, Pkt{0, 0, 0, 0});
+  return cancelled;
 }
 
+// Diagnostic build (-DNSGPU_PHASE_PROF, lib/libnsgpu_prof.so only): thread 0 of block 0 of each
+// pipeline kernel accumulates s_memrealtime (100 MHz) deltas between phase marks into g_phase.
+#ifdef NSGPU_PHASE_PROF
+__device__ uint64_t g_phase[64];
+#define PH_BEGIN() uint64_t ph_t_ = (threadIdx.x == 0 && blockIdx.x == 0) ? __builtin_amdgcn_s_memrealtime() : 0
+#define PH_MARK(i)                                                                      \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                                          \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                             \
+      atomicAdd((unsigned long long *)&g_phase[i], (unsigned long long)(t_ - ph_t_));   \
+      ph_t_ = t_;                                                                       \
+    }                                                                                   \
+  } while (0)
+#else
+#define PH_BEGIN() (void)0
+#define PH_MARK(i) (void)0
+#endif
+
 // ================================ window pipeline ================================
-// Window bound from the reduction: packed key bound, span, Stop key (shared by k_partition/k_refit).
+// Window bound of a pending set's reduction: packed key bound, span, Stop key.
 struct WinBound {
   uint64_t tmin, span, bound, stop_packed;
 };
-__device__ __forceinline__ WinBound window_bound(const Ctl &C) {
+__device__ __forceinline__ WinBound window_bound(const Red &R) {
   WinBound b;
-  b.tmin = C.tmin;
-  uint64_t span = C.wend - b.tmin;
+  b.tmin = R.tmin;
+  uint64_t span = R.wend - b.tmin;
   if (span > 0xfffffffeull) span = 0xfffffffeull;
   b.span = span;
   b.bound = (span << 32) | 0xffffffffull;
   b.stop_packed = ~0ull;
-  if (C.stopts != ~0ull && C.stopts - b.tmin <= span) {
+  if (R.stopts != ~0ull && R.stopts - b.tmin <= span) {
     // Stop caps the window at its own key (it is dispatched; later events are not)
-    b.stop_packed = ((C.stopts - b.tmin) << 32) | C.stopuid;
+    b.stop_packed = ((R.stopts - b.tmin) << 32) | R.stopuid;
     b.bound = b.stop_packed < b.bound ? b.stop_packed : b.bound;
   }
   return b;
 }
 __device__ __forceinline__ void publish_bound(Ctl &C, const WinBound &b) {
+  C.tmin = b.tmin;
   C.bound = b.bound;
-  C.span = b.span;
   // zero-delay leaf children (Ipv4EndPoint::DoForwardUp) run inside the window; when the window ends
   // at the Stop event, those at the Stop's ts sort after it and are never dispatched
   const bool has_stop = b.stop_packed != ~0ull && b.bound >= b.stop_packed;
   C.inline_lim = has_stop ? (b.stop_packed >> 32) : ~0ull;
 }
 
-// ---- k_reduce: tmin, W_end, the pending Stop ----
-__global__ __launch_bounds__(TB) void k_reduce(const P2PDev *__restrict__ Mp) {
-  const P2PDev &M = *Mp;
-  Ctl &C = *M.C;
-  if (blockIdx.x == 0 && threadIdx.x == 0) C.scan_ran = 0;
-  if (C.done) return;
-  const uint64_t P = C.P;
-  const int cur = C.cur;
-  const uint64_t *ts = M.ev_ts[cur];
-  const uint32_t *kindv = M.ev_kind[cur];
-  uint64_t tmin = ~0ull, wend = ~0ull;
-  for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < P; i += (uint64_t)gridDim.x * TB) {
-    const uint64_t t = ts[i];
-    const uint32_t k = kindv[i] & 0xffu;
-    tmin = t < tmin ? t : tmin;
-    const uint64_t e = t + (uint64_t)M.lookahead[k];
-    wend = e < wend ? e : wend;
-    if (k == K_STOP) {  // at most one Stop event is pending
-      C.stopts = t;
-      C.stopuid = M.ev_uid[cur][i];
+// Reduces (tmn, wnd) over the workgroup and one lane folds them into R (atomicMin): one atomic
+// pair per workgroup, not per wave (a word takes ~11 ns per atomic).  All threads must call it.
+template <int NTH>
+__device__ __forceinline__ void publish_min(Red &R, uint64_t tmn, uint64_t wnd) {
+  tmn = wave_min64(tmn);
+  wnd = wave_min64(wnd);
+  if constexpr (NTH > 64) {
+    __shared__ uint64_t s0[NTH / 64], s1[NTH / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) {
+      s0[wid] = tmn;
+      s1[wid] = wnd;
     }
-  }
-  __shared__ uint64_t s0[TB / 64], s1[TB / 64];
-  tmin = wave_min64(tmin);
-  wend = wave_min64(wend);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) {
-    s0[wid] = tmin;
-    s1[wid] = wend;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < TB / 64; w++) {
-      tmin = s0[w] < tmin ? s0[w] : tmin;
-      wend = s1[w] < wend ? s1[w] : wend;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < NTH / 64; w++) {
+      tmn = s0[w] < tmn ? s0[w] : tmn;
+      wnd = s1[w] < wnd ? s1[w] : wnd;
     }
-    if (tmin != ~0ull) atomicMin((unsigned long long *)&C.tmin, (unsigned long long)tmin);
-    if (wend != ~0ull) atomicMin((unsigned long long *)&C.wend, (unsigned long long)wend);
+  } else if ((threadIdx.x & 63) != 0) {
+    return;
   }
+  if (tmn != ~0ull) atomicMin((unsigned long long *)&R.tmin, (unsigned long long)tmn);
+  if (wnd != ~0ull) atomicMin((unsigned long long *)&R.wend, (unsigned long long)wnd);
 }
 
-// Classifies pool entry i against the window bound and moves it: window -> (wkey, wpi) list,
-// otherwise -> the other pool buffer.  All 64 lanes of the wave must call it (ballots).
-__device__ __forceinline__ void partition_one(const P2PDev &M, Ctl &C, const WinBound &b, int cur, uint64_t i,
-                                              bool valid) {
-  const int lane = threadIdx.x & 63;
-  uint64_t t = 0, pk = 0;
-  bool in = false;
-  if (valid) {
-    t = M.ev_ts[cur][i];
-    pk = ((t - b.tmin) << 32) | M.ev_uid[cur][i];
-    in = (t - b.tmin <= b.span) && pk <= b.bound;
+// A pending event in registers.
+struct Ev {
+  uint64_t ts;
+  uint32_t uid, ctx, kind, a;
+  Pkt p;
+};
+
+// Writes window slot `slot` (and the node's slot table).
+__device__ __forceinline__ void put_window(const P2PDev &M, uint32_t slot, uint64_t pk, const Ev &e) {
+  M.wkey[slot] = pk;
+  M.wctx[slot] = e.ctx;
+  M.wkind[slot] = e.kind;
+  M.wa[slot] = e.a;
+  M.wpkt[slot] = e.p;
+  uint32_t idx = 0;
+  if (e.ctx < M.n_nodes) {
+    idx = atomicAdd(&M.node_cnt[e.ctx], 1u);
+    if (idx < (uint32_t)NSLOT) M.node_slot[(uint64_t)e.ctx * NSLOT + idx] = slot;
   }
-  const uint64_t bin = __ballot(valid && in), bout = __ballot(valid && !in);
+  M.widx[slot] = idx;
+}
+__device__ __forceinline__ void put_pool(const P2PDev &M, int pool, uint64_t o, const Ev &e) {
+  if (o < M.pool_cap) {
+    M.ev_ts[pool][o] = e.ts;
+    M.ev_uid[pool][o] = e.uid;
+    M.ev_ctx[pool][o] = e.ctx;
+    M.ev_kind[pool][o] = e.kind;
+    M.ev_a[pool][o] = e.a;
+    M.ev_pkt[pool][o] = e.p;
+  } else {
+    atomicOr(M.error, 1u);
+  }
+}
+__device__ __forceinline__ Ev load_pool(const P2PDev &M, int pool, uint64_t i) {
+  return Ev{M.ev_ts[pool][i], M.ev_uid[pool][i], M.ev_ctx[pool][i], M.ev_kind[pool][i], M.ev_a[pool][i],
+            M.ev_pkt[pool][i]};
+}
+
+// Classifies a pending event against the window bound: window -> slot records (+ the node's slot
+// table), otherwise -> pool `nxt` (and the next window's reduction).  A window candidate past WCAP
+// sets C.overflow and also goes to pool `nxt` (the refit takes it from there).  All 64 lanes of the
+// wave must call it (ballots).
+__device__ __forceinline__ void classify(const P2PDev &M, Ctl &C, const WinBound &b, int nxt, bool valid,
+                                         const Ev &e, Red &R, uint64_t &tmn, uint64_t &wnd) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
+  const bool in = valid && (e.ts - b.tmin <= b.span) && pk <= b.bound;
+  const uint64_t bin = __ballot(in);
+  const uint64_t bout0 = __ballot(valid && !in);
   uint32_t basein = 0, baseout = 0;
-  if (lane == 0) {
+  if (lane == 0) {  // both slot ranges at once (overflowed candidates are few: a second add)
     if (bin) basein = atomicAdd(&C.W, (uint32_t)__popcll(bin));
-    if (bout) baseout = atomicAdd(&C.nxtP, (uint32_t)__popcll(bout));
+    if (bout0) baseout = atomicAdd(&C.nxtP, (uint32_t)__popcll(bout0));
   }
   basein = __shfl(basein, 0);
   baseout = __shfl(baseout, 0);
   const uint64_t below = (1ull << lane) - 1ull;
-  if (valid && in) {
-    const uint32_t slot = basein + (uint32_t)__popcll(bin & below);
-    if (slot < (uint32_t)WCAP) {
-      M.wkey[slot] = pk;
-      M.wpi[slot] = (uint32_t)i;
-    } else {
+  const uint32_t slot = basein + (uint32_t)__popcll(bin & below);
+  const bool to_win = in && slot < (uint32_t)WCAP;
+  const bool ovf = in && !to_win;
+  const uint64_t bovf = __ballot(ovf);
+  uint32_t baseovf = 0;
+  if (bovf) {
+    if (lane == 0) {
       C.overflow = 1;
+      baseovf = atomicAdd(&C.nxtP, (uint32_t)__popcll(bovf));
     }
+    baseovf = __shfl(baseovf, 0);
+  }
+  if (to_win) {
+    put_window(M, slot, pk, e);
   } else if (valid) {
-    const uint64_t o = baseout + (uint64_t)__popcll(bout & below);
-    const int nxt = cur ^ 1;
-    if (o < M.pool_cap) {
-      M.ev_ts[nxt][o] = t;
-      M.ev_uid[nxt][o] = M.ev_uid[cur][i];
-      M.ev_ctx[nxt][o] = M.ev_ctx[cur][i];
-      M.ev_kind[nxt][o] = M.ev_kind[cur][i];
-      M.ev_a[nxt][o] = M.ev_a[cur][i];
-      M.ev_pkt[nxt][o] = M.ev_pkt[cur][i];
-    } else {
-      atomicOr(M.error, 1u);
+    const uint64_t o = ovf ? baseovf + (uint64_t)__popcll(bovf & below) : baseout + (uint64_t)__popcll(bout0 & below);
+    put_pool(M, nxt, o, e);
+    if (!ovf) {
+      tmn = e.ts < tmn ? e.ts : tmn;
+      const uint64_t x = e.ts + (uint64_t)M.lookahead[e.kind & 0xffu];
+      wnd = x < wnd ? x : wnd;
+      if ((e.kind & 0xffu) == K_STOP) {  // at most one Stop event is pending
+        R.stopts = e.ts;
+        R.stopuid = e.uid;
+      }
     }
   }
 }
 
-// ---- k_partition ----
-__global__ __launch_bounds__(TB) void k_partition(const P2PDev *__restrict__ Mp) {
-  const P2PDev &M = *Mp;
+// ---- k_pa: append the last scanned window (dispatch log / digest; its children get their uids and
+// become pending) and partition the pending set into the next window ----
+// Pending set = pool `cur` (P entries) + the non-inline children of the last window.  Thread g <
+// WCAP takes slot g of the last window; thread WCAP + i (grid-stride) takes pool entry i.
+constexpr int PFC = 4;  // children per slot loaded ahead
+__global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
+  PH_BEGIN();
   Ctl &C = *M.C;
-  if (C.done) return;
-  const WinBound b = window_bound(C);
-  if (blockIdx.x == 0 && threadIdx.x == 0) publish_bound(C, b);
-  const uint64_t P = C.P;
-  const int cur = C.cur;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * TB; i0 < P; i0 += (uint64_t)gridDim.x * TB) {
-    const uint64_t i = i0 + threadIdx.x;
-    partition_one(M, C, b, cur, i, i < P);
-  }
-}
-
-// ---- k_refit: the window overflowed WCAP; cut it to the largest key prefix that fits ----
-__global__ __launch_bounds__(SCAN_THREADS) void k_refit(const P2PDev *__restrict__ Mp) {
-  const P2PDev &M = *Mp;
-  Ctl &C = *M.C;
-  if (C.done || !C.overflow) return;
-  __shared__ uint32_t wc[SCAN_THREADS / 64];
-  WinBound b = window_bound(C);
-  const uint64_t P = C.P;
-  const int cur = C.cur;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  auto count_le = [&](uint64_t bnd) -> uint32_t {
-    uint32_t c = 0;
-    for (uint64_t i = threadIdx.x; i < P; i += SCAN_THREADS) {
-      const uint64_t t = M.ev_ts[cur][i];
-      if (t - b.tmin <= b.span) c += ((((t - b.tmin) << 32) | M.ev_uid[cur][i]) <= bnd);
+  const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * TB;
+  const bool slot_role = g < (uint64_t)WCAP;  // wave-uniform
+  if (C.prep || C.done >= 2) return;  // window already prepared by the refit / run over
+  const bool partition = C.done == 0;
+  const int cur = C.cur, nxt = cur ^ 1;
+  const uint64_t win = C.windows;
+  const WinBound b = window_bound(C.red[(win + 1) & 1]);
+  Red &R = C.red[win & 1];
+  if (partition && blockIdx.x == 0 && threadIdx.x == 0) publish_bound(C, b);
+  const uint64_t P = partition ? C.P : 0;
+  const uint32_t pW = C.pvalid ? C.pW : 0;
+  uint64_t spk = 0;
+  uint4 si = make_uint4(0, 0, 0, 0);
+  uint32_t ncr = 0, sctx = 0;
+  Ev ce[PFC];
+  if (slot_role && g < pW) {  // the last window's slot and its first children, all at once
+    const uint32_t s = (uint32_t)g;
+    spk = M.pwkey[s];
+    si = M.sinfo[s];
+    ncr = M.nchild[s];
+    sctx = M.pwctx[s];
+#pragma unroll
+    for (int j = 0; j < PFC; j++) {
+      const uint32_t sl = s * M.maxc + j;
+      if ((uint32_t)j < M.maxc)
+        ce[j] = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
     }
-    c = wave_sum32(c);
-    if (lane == 0) wc[wid] = c;
-    __syncthreads();
-    uint32_t tot = 0;
-    for (int w = 0; w < SCAN_THREADS / 64; w++) tot += wc[w];
-    __syncthreads();
-    return tot;
-  };
-  uint64_t lo_b = 0, hi_b = b.bound;  // count (hi_b) > WCAP
-  while (hi_b - lo_b > 1) {
-    const uint64_t mid = lo_b + (hi_b - lo_b) / 2;
-    if (count_le(mid) <= (uint32_t)WCAP) lo_b = mid;
-    else hi_b = mid;
   }
-  b.bound = lo_b;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    C.W = 0;
-    C.nxtP = 0;
-    C.overflow = 0;
-    publish_bound(C, b);
+  PH_MARK(0);
+  uint64_t tmn = ~0ull, wnd = ~0ull, digest = 0;
+  if (slot_role) {
+    // ---- slot g of the last window: dispatch rank (log, digest), inline children, children -> pending
+    const bool vs = g < pW;
+    const uint32_t s = (uint32_t)g;
+    const uint64_t rel = spk >> 32;
+    const uint64_t t = C.ptmin + rel;
+    const uint32_t uid0 = C.puid0;
+    const uint64_t K0 = C.pK0, ilim = C.pinline_lim;
+    if (vs) {
+      const uint64_t rk = K0 + si.x;
+      digest += digest_term(rk, t, (uint32_t)spk);
+      if (rk < M.log_cap) {
+        M.log_ts[rk] = t;
+        M.log_uid[rk] = (uint32_t)spk;
+        M.log_ctx[rk] = sctx;
+      }
+    }
+    if (__ballot(vs)) {
+      uint32_t ii = 0;
+      for (uint32_t j = 0; j < M.maxc; j++) {
+        const bool has = vs && j < ncr;
+        if (!__ballot(has)) break;
+        Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+        bool valid = false;
+        if (has) {
+          if (j < (uint32_t)PFC) {
+#pragma unroll
+            for (int q = 0; q < PFC; q++)
+              if ((uint32_t)q == j) e = ce[q];
+          } else {
+            const uint32_t sl = s * M.maxc + j;
+            e = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
+          }
+          e.uid = uid0 + si.z + j;
+          if ((e.kind & 0xffu) == K_FWD_UP) {  // leaf: dispatched inside its window (or never), not queued
+            if (rel < ilim) {
+              const uint64_t crk = K0 + si.y + ii;
+              digest += digest_term(crk, t, e.uid);
+              if (crk < M.log_cap) {
+                M.log_ts[crk] = t;
+                M.log_uid[crk] = e.uid;
+                M.log_ctx[crk] = e.ctx;
+              }
+              ii++;
+            }
+          } else {
+            valid = partition;
+          }
+        }
+        if (__ballot(valid)) classify(M, C, b, nxt, valid, e, R, tmn, wnd);
+      }
+    }
+  } else {
+    // ---- pool entries (grid-stride; the first one was loaded ahead)
+    for (uint64_t i = g - WCAP; i < P; i += stride - WCAP) {  // (the pool role has stride - WCAP threads)
+      const Ev e = load_pool(M, cur, i);
+      classify(M, C, b, nxt, true, e, R, tmn, wnd);
+    }
   }
-  __syncthreads();
-  for (uint64_t i0 = 0; i0 < P; i0 += SCAN_THREADS) {
-    const uint64_t i = i0 + threadIdx.x;
-    partition_one(M, C, b, cur, i, i < P);
-  }
+  PH_MARK(1);
+  publish_min<TB>(R, tmn, wnd);
+  digest = wave_sum64(digest);
+  if ((threadIdx.x & 63) == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
+  PH_MARK(2);
 }
 
-// ---- k_rank: rank of each window key = # of smaller keys (keys are distinct: uids) ----
-__global__ __launch_bounds__(TB) void k_rank(const P2PDev *__restrict__ Mp) {
-  const P2PDev &M = *Mp;
-  const Ctl &C = *M.C;
-  if (C.done) return;
+// ---- k_handle_rank: the holder of each node (slot index 0 in its table) runs the node's window
+// events in key order, so node state (device tx state, DropTail rings, OnOff state, sink counters)
+// needs no atomics; children go to per-slot records in Schedule-call order.  The launch's other
+// blocks rank the window keys by tiled all-pairs counting (keys are distinct: uids).
+// Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) run at
+// their key position: after the node's events with ts <= theirs, before the first with a larger ts.
+__device__ __forceinline__ uint32_t nth_slot_scan(const P2PDev &M, uint32_t W, uint32_t c, uint64_t after) {
+  // slot of the smallest key > `after` among the window events of node c (long tables only)
+  uint64_t best = ~0ull;
+  uint32_t bs = NOCHAIN;
+  for (uint32_t x = 0; x < W; x++)
+    if (M.wctx[x] == c) {
+      const uint64_t k = M.wkey[x];
+      if (k > after && k < best) {
+        best = k;
+        bs = x;
+      }
+    }
+  return bs;
+}
+
+__device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0) {
+  __shared__ uint32_t chs[HB * CH];
+  __shared__ uint64_t chk[HB * CH];
+  // slot i0's record, ahead of the run control
+  const uint32_t idx0 = M.widx[i0], c = M.wctx[i0];
+  const uint64_t key0 = M.wkey[i0];
+  const uint32_t kind0 = M.wkind[i0], a0 = M.wa[i0];
+  const Pkt pkt0 = M.wpkt[i0];
   const uint32_t W = C.W;
-  const uint32_t ti = blockIdx.x / NT, tj = blockIdx.x % NT;
-  if (ti * TB >= W || tj * TB >= W) return;
-  __shared__ uint64_t tk[TB];
-  const uint32_t j = tj * TB + threadIdx.x;
-  tk[threadIdx.x] = j < W ? M.wkey[j] : ~0ull;
-  __syncthreads();
-  const uint32_t i = ti * TB + threadIdx.x;
-  if (i >= W) return;
+  Red &R = C.red[C.windows & 1];
+  uint64_t tmn = ~0ull, wnd = ~0ull;
+  HStat hs{0, 0, 0, 0, false};
+#ifdef NSGPU_PHASE_PROF
+  uint64_t tq[4] = {0, 0, 0, 0};
+  const uint64_t tq0 = __builtin_amdgcn_s_memrealtime();
+#define HQ(k) tq[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define HQ(k) (void)0
+#endif
+  if (i0 < W && idx0 == 0) {  // the holder
+    uint32_t n = 1;
+    int32_t sink = -1;
+    if (c < M.n_nodes) {
+      n = M.node_cnt[c];
+      sink = M.sink_of_node[c];
+      M.node_cnt[c] = 0;
+    }
+    HQ(0);
+    uint32_t *my = &chs[threadIdx.x * CH];
+    uint64_t *mk = &chk[threadIdx.x * CH];
+    const bool small = n <= (uint32_t)CH;
+    if (small && n > 1) {
+      const uint32_t ns = n < (uint32_t)NSLOT ? n : (uint32_t)NSLOT;
+      for (uint32_t j = 0; j < ns; j++) my[j] = M.node_slot[(uint64_t)c * NSLOT + j];
+      if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
+        uint32_t m = NSLOT;
+        for (uint32_t x = 0; x < W && m < n; x++)
+          if (M.wctx[x] == c && M.widx[x] >= (uint32_t)NSLOT) my[m++] = x;
+      }
+      for (uint32_t j = 0; j < n; j++) mk[j] = M.wkey[my[j]];
+      for (uint32_t a = 1; a < n; a++) {  // insertion sort by key
+        const uint32_t v = my[a];
+        const uint64_t kv = mk[a];
+        uint32_t bb = a;
+        while (bb > 0 && mk[bb - 1] > kv) {
+          my[bb] = my[bb - 1];
+          mk[bb] = mk[bb - 1];
+          bb--;
+        }
+        my[bb] = v;
+        mk[bb] = kv;
+      }
+    }
+    HQ(1);
+    const uint64_t tmin = C.tmin;
+    const uint64_t inline_lim = C.inline_lim;
+    Emit E;
+    E.ctx = c;
+    E.ch_ts = M.ch_ts;
+    E.ch_ctx = M.ch_ctx;
+    E.ch_kind = M.ch_kind;
+    E.ch_a = M.ch_a;
+    E.ch_pkt = M.ch_pkt;
+    E.lookahead = M.lookahead;
+    E.tmn = ~0ull;
+    E.wnd = ~0ull;
+    uint64_t lastk = 0;
+    uint32_t ts0_it = 0, pending = 0;
+    uint64_t cur_rel = 0;
+    for (uint32_t it = 0; it <= n; it++) {
+      uint32_t s = NOCHAIN;
+      uint64_t key = ~0ull;
+      if (it < n) {
+        if (n == 1) {
+          s = i0;
+          key = key0;
+        } else if (small) {
+          s = my[it];
+          key = mk[it];
+        } else {
+          s = nth_slot_scan(M, W, c, lastk);
+          key = M.wkey[s];
+        }
+      }
+      const uint64_t rel = it < n ? (key >> 32) : ~0ull;
+      if (it > 0 && rel > cur_rel && pending) {
+        // flush the inline children of this node's events at cur_rel (positions [ts0_it, it))
+        uint64_t aft = 0;
+        for (uint32_t jt = 0; jt < it; jt++) {
+          const uint32_t xr = n == 1 ? i0 : small ? my[jt] : nth_slot_scan(M, W, c, aft);
+          aft = n == 1 ? key0 : small ? mk[jt] : M.wkey[xr];
+          if (jt < ts0_it) continue;
+          const uint32_t ncr = M.nchild[xr];
+          for (uint32_t j = 0; j < ncr; j++) {
+            const uint32_t sl = xr * M.maxc + j;
+            if ((E.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
+            const uint32_t sa = E.ch_a[sl];  // DoForwardUp -> PacketSink::HandleRead
+            if (M.app_flags[sa] & 2u) {
+              M.appc[sa].rx_packets++;
+              M.appc[sa].rx_bytes += E.ch_pkt[sl].size - 28;
+            }
+          }
+        }
+        pending = 0;
+      }
+      if (it == n) break;
+      if (it == 0 || rel > cur_rel) {
+        ts0_it = it;
+        cur_rel = rel;
+      }
+      E.now = tmin + rel;
+      E.slot0 = s * M.maxc;
+      E.n = 0;
+      const bool own = s == i0;
+      const uint32_t kw = own ? kind0 : M.wkind[s];
+      const uint32_t ea = own ? a0 : M.wa[s];
+      const Pkt ep = own ? pkt0 : M.wpkt[s];
+      hs.cancelled += run_event(M, E, kw, ea, ep, sink, hs);
+      uint32_t ni = 0;
+      if (rel < inline_lim)
+        for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
+      M.nchild[s] = E.n;
+      M.ninl[s] = ni;
+      pending += ni;
+      lastk = key;
+    }
+    tmn = E.tmn;
+    wnd = E.wnd;
+    HQ(2);
+  }
+#ifdef NSGPU_PHASE_PROF
+  {
+    uint64_t d0 = tq[0] ? tq[0] - tq0 : 0, d1 = tq[1] ? tq[1] - tq[0] : 0, d2 = tq[2] ? tq[2] - tq[1] : 0;
+    d0 = wave_max64(d0);
+    d1 = wave_max64(d1);
+    d2 = wave_max64(d2);
+    const uint32_t nh = wave_sum32(tq[0] ? 1u : 0u);
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+      atomicAdd((unsigned long long *)&g_phase[12], (unsigned long long)d0);
+      atomicAdd((unsigned long long *)&g_phase[13], (unsigned long long)d1);
+      atomicAdd((unsigned long long *)&g_phase[14], (unsigned long long)d2);
+      atomicAdd((unsigned long long *)&g_phase[15], (unsigned long long)nh);
+    }
+  }
+#endif
+  publish_min<HB>(R, tmn, wnd);
+  if (hs.stop) C.stop_seen = 1;
+  if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
+  if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
+  if (hs.no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)hs.no_route);
+  if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
+}
+
+__device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_t t) {
+  const uint32_t ti = t / NJT, tj = t % NJT;
+  __shared__ uint64_t tk[RJ];
+  // tile keys and the own key ahead of the run control
+#pragma unroll
+  for (int q = 0; q < RJ / HB; q++) tk[q * HB + threadIdx.x] = M.wkey[tj * RJ + q * HB + threadIdx.x];
+  const uint32_t i = ti * HB + threadIdx.x;
   const uint64_t x = M.wkey[i];
+  const uint32_t W = C.W;
+  if (ti * HB >= W || tj * RJ >= W) return;  // uniform over the block
+  __syncthreads();
+  if (i >= W) return;
   uint32_t c = 0;
+  const int jn = W - tj * RJ < (uint32_t)RJ ? (int)(W - tj * RJ) : RJ;  // (slots past W hold stale keys)
+  if (jn == RJ) {
 #pragma unroll 16
-  for (int y = 0; y < TB; y++) c += tk[y] < x;
+    for (int y = 0; y < RJ; y++) c += tk[y] < x;
+  } else {
+    for (int y = 0; y < jn; y++) c += tk[y] < x;
+  }
   if (c) atomicAdd(&M.wrank[i], c);
 }
 
-// ---- k_scatter: rank order; per-node chains ----
-__global__ __launch_bounds__(RB) void k_scatter(const P2PDev *__restrict__ Mp) {
-  const P2PDev &M = *Mp;
-  const Ctl &C = *M.C;
-  if (C.done) return;
-  const uint32_t i = blockIdx.x * RB + threadIdx.x;
-  if (i >= C.W) return;
-  const uint32_t r = M.wrank[i];
-  M.wrank[i] = 0;
-  const uint32_t pi = M.wpi[i];
-  M.skey[r] = M.wkey[i];
-  M.spi[r] = pi;
-  const uint32_t c = M.ev_ctx[C.cur][pi];
-  M.sctx[r] = c;
-  M.link[r] = c < M.n_nodes ? atomicExch(&M.node_head[c], r) : NOCHAIN;
+__global__ __launch_bounds__(HB) void k_handle_rank(const P2PDev M) {
+  PH_BEGIN();
+  Ctl &C = *M.C;
+  if (C.done || C.overflow) {
+    if (C.done == 1 && blockIdx.x == 0 && threadIdx.x == 0) C.done = 2;  // the final window is appended
+    return;
+  }
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  PH_MARK(8);
+  if (blockIdx.x < (uint32_t)NHB) handle_node(M, C, blockIdx.x * HB + threadIdx.x);
+  else rank_tile(M, C, blockIdx.x - NHB);
+  PH_MARK(9);
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t th1 = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x < (uint32_t)NHB) atomicMax((unsigned long long *)&g_phase[10], (unsigned long long)(th1 - th0));
+  else atomicMax((unsigned long long *)&g_phase[11], (unsigned long long)(th1 - th0));
+#endif
 }
 
-// ---- k_handle: the node's last exchanger runs the node's chain in rank order ----
-// Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) run at
-// their key position: after the node's events with ts <= theirs, before the first with a larger ts.
-__global__ __launch_bounds__(RB) void k_handle(const P2PDev *__restrict__ Mp,
-                                               const int32_t *__restrict__ sink_of_node) {
-  const P2PDev &M = *Mp;
-  Ctl &C = *M.C;
-  if (C.done) return;
-  const uint32_t W = C.W;
-  const uint32_t r0 = blockIdx.x * RB + threadIdx.x;
-  if (r0 >= W) return;
-  const uint32_t c = M.sctx[r0];
-  if (c < M.n_nodes) {
-    if (M.node_head[c] != r0) return;  // not the chain holder
-    M.node_head[c] = NOCHAIN;
+// ---- refit (k_scan's block, only when the window overflowed WCAP) ----
+// Pending set = pool `nxt` (the non-window events and the overflowed candidates) + the WCAP recorded
+// window slots.  The slots go back to the pool, a 256-way radix bisection finds the largest key
+// prefix that fits (a key prefix of a safe window is safe), and the pool is partitioned in place
+// (chunked: every chunk is read before any of its compacted writes land).
+__device__ void refit(const P2PDev &M, Ctl &C) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t s_lo, s_hi;
+  __shared__ uint32_t s_clo, s_nw, s_no;
+  __shared__ uint32_t wsum[2][SCAN_THREADS / 64];
+  const int cur = C.cur, nxt = cur ^ 1;
+  const uint64_t win = C.windows;
+  WinBound b = window_bound(C.red[(win + 1) & 1]);
+  Red &R = C.red[win & 1];
+  const uint64_t P0 = C.nxtP;
+  // 1. the recorded slots -> pool nxt (every one of the WCAP slots was written)
+  for (int s = threadIdx.x; s < WCAP; s += SCAN_THREADS) {
+    const uint32_t c = M.wctx[s];
+    if (c < M.n_nodes) M.node_cnt[c] = 0;
+    const uint64_t pk = M.wkey[s];
+    Ev e{b.tmin + (pk >> 32), (uint32_t)pk, c, M.wkind[s], M.wa[s], M.wpkt[s]};
+    put_pool(M, nxt, P0 + s, e);
   }
-  __shared__ uint32_t chs[RB * CH];
-  uint32_t *my = &chs[threadIdx.x * CH];
-  uint32_t n = 0;
-  for (uint32_t x = r0; x != NOCHAIN; x = M.link[x]) {
-    if (n < (uint32_t)CH) my[n] = x;
-    n++;
+  const uint64_t P = P0 + WCAP;
+  if (threadIdx.x == 0) {
+    s_lo = 0;        // count(keys <= lo) <= WCAP (the smallest key is >= 4: uids start at 4)
+    s_hi = b.bound;  // count(keys <= hi) > WCAP
+    s_clo = 0;
   }
-  const bool small = n <= (uint32_t)CH;
-  if (small)
-    for (uint32_t a = 1; a < n; a++) {  // insertion sort: ascending rank
-      const uint32_t v = my[a];
-      uint32_t b = a;
-      while (b > 0 && my[b - 1] > v) {
-        my[b] = my[b - 1];
-        b--;
+  __syncthreads();
+  // 2. bisection
+  while (s_hi - s_lo > 1) {
+    const uint64_t lo = s_lo, hi = s_hi;
+    const uint64_t range = hi - lo;  // keys in (lo, hi]: bucket (k - lo - 1) >> sh in [0, 256)
+    int sh = 0;
+    while (((range - 1) >> sh) >= 256) sh++;
+    for (int j = threadIdx.x; j < 256; j += SCAN_THREADS) hist[j] = 0;
+    __syncthreads();
+    for (uint64_t i = threadIdx.x; i < P; i += SCAN_THREADS) {
+      const uint64_t t = M.ev_ts[nxt][i];
+      bool hit = false;
+      uint32_t bk = 0;
+      if (t - b.tmin <= b.span) {
+        const uint64_t k = ((t - b.tmin) << 32) | M.ev_uid[nxt][i];
+        hit = k > lo && k <= hi;
+        bk = hit ? (uint32_t)((k - lo - 1) >> sh) : 0u;
       }
-      my[b] = v;
-    }
-  const uint64_t tmin = C.tmin;
-  const uint64_t inline_lim = C.inline_lim;
-  const int cur = C.cur;
-  const int32_t sink = c < M.n_nodes ? sink_of_node[c] : -1;
-  uint64_t cancelled = 0, ttl_drops = 0, no_route = 0, unreach = 0;
-  bool stop = false;
-  int64_t last = -1;
-  uint32_t ts0_it = 0, pending = 0;
-  uint64_t cur_rel = 0;
-  auto rank_at = [&](uint32_t it) -> uint32_t {
-    if (small) return my[it];
-    uint32_t best = NOCHAIN;  // it-th smallest: the smallest rank above `last`
-    for (uint32_t x = r0; x != NOCHAIN; x = M.link[x])
-      if ((int64_t)x > last && x < best) best = x;
-    return best;
-  };
-  for (uint32_t it = 0; it <= n; it++) {
-    const uint32_t r = it < n ? rank_at(it) : NOCHAIN;
-    const uint64_t rel = it < n ? (M.skey[r] >> 32) : ~0ull;
-    if (it > 0 && rel > cur_rel && pending) {
-      // flush the inline children of this node's events at cur_rel (chain positions [ts0_it, it))
-      for (uint32_t jt = ts0_it; jt < it; jt++) {
-        const uint32_t x = small ? my[jt] : NOCHAIN;
-        uint32_t xr = x;
-        if (!small) {  // recover the jt-th rank by selection (long chains only)
-          int64_t lst = -1;
-          for (uint32_t s = 0; s <= jt; s++) {
-            uint32_t best = NOCHAIN;
-            for (uint32_t y = r0; y != NOCHAIN; y = M.link[y])
-              if ((int64_t)y > lst && y < best) best = y;
-            lst = best;
-          }
-          xr = (uint32_t)lst;
-        }
-        const uint32_t ncr = M.nchild[xr];
-        for (uint32_t j = 0; j < ncr; j++) {
-          const uint32_t sl = xr * M.maxc + j;
-          if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
-          Emit E0;
-          E0.M = &M;
-          E0.now = tmin + cur_rel;
-          E0.ctx = c;
-          E0.slot0 = 0;
-          E0.n = 0;
-          bool st0 = false;
-          run_event(M, E0, M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl], sink, &ttl_drops, &no_route, &unreach, &st0);
-        }
+      // wave-aggregate the common case (every hitting lane in one bucket): one LDS atomic
+      const uint64_t m = __ballot(hit);
+      if (m) {
+        const int first = __ffsll((unsigned long long)m) - 1;
+        const uint32_t b0 = __shfl(bk, first);
+        const uint64_t same = __ballot(hit && bk == b0);
+        if ((threadIdx.x & 63) == first) atomicAdd(&hist[b0], (uint32_t)__popcll(same));
+        if (hit && bk != b0) atomicAdd(&hist[bk], 1u);
       }
-      pending = 0;
     }
-    if (it == n) break;
-    if (it == 0 || rel > cur_rel) {
-      ts0_it = it;
-      cur_rel = rel;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t c = s_clo;
+      int j = -1;
+      while (j + 1 < 256 && c + hist[j + 1] <= (uint32_t)WCAP) c += hist[++j];
+      // keys <= lo + (j + 1) << sh: c <= WCAP; keys <= lo + (j + 2) << sh: > WCAP
+      const uint64_t nlo = lo + ((uint64_t)(j + 1) << sh);
+      const uint64_t nhi = lo + ((uint64_t)(j + 2) << sh);
+      s_lo = nlo;
+      s_clo = c;
+      s_hi = nhi < hi ? nhi : hi;
     }
-    const uint32_t pi = M.spi[r];
-    Emit E;
-    E.M = &M;
-    E.now = tmin + rel;
-    E.ctx = c;
-    E.slot0 = r * M.maxc;
-    E.n = 0;
-    bool st = false;
-    cancelled += run_event(M, E, M.ev_kind[cur][pi], M.ev_a[cur][pi], M.ev_pkt[cur][pi], sink, &ttl_drops,
-                           &no_route, &unreach, &st);
-    stop |= st;
-    uint32_t ni = 0;
-    if (rel < inline_lim)
-      for (uint32_t j = 0; j < E.n; j++) ni += (M.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
-    M.nchild[r] = E.n;
-    M.ninl[r] = ni;
-    pending += ni;
-    last = r;
+    __syncthreads();
   }
-  if (stop) C.stop_seen = 1;
-  if (cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)cancelled);
-  if (ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)ttl_drops);
-  if (no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)no_route);
-  if (unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)unreach);
+  b.bound = s_lo;
+  if (threadIdx.x == 0) {
+    publish_bound(C, b);
+    R.tmin = R.wend = R.stopts = ~0ull;
+    s_nw = 0;
+    s_no = 0;
+  }
+  __syncthreads();
+  // 3. in-place partition of pool nxt
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t tmn = ~0ull, wnd = ~0ull;
+  for (uint64_t c0 = 0; c0 < P; c0 += SCAN_THREADS) {
+    const uint64_t i = c0 + threadIdx.x;
+    const bool valid = i < P;
+    Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+    if (valid) e = load_pool(M, nxt, i);
+    const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
+    const bool in = valid && (e.ts - b.tmin <= b.span) && pk <= b.bound;
+    const bool out = valid && !in;
+    const uint64_t bi = __ballot(in), bo = __ballot(out);
+    const uint64_t below = (1ull << lane) - 1ull;
+    if (lane == 0) {
+      wsum[0][wid] = (uint32_t)__popcll(bi);
+      wsum[1][wid] = (uint32_t)__popcll(bo);
+    }
+    __syncthreads();  // (also: every read of this chunk is done)
+    uint32_t oi = s_nw, oo = s_no, ti = 0, to = 0;
+    for (int w = 0; w < SCAN_THREADS / 64; w++) {
+      oi += w < wid ? wsum[0][w] : 0;
+      oo += w < wid ? wsum[1][w] : 0;
+      ti += wsum[0][w];
+      to += wsum[1][w];
+    }
+    if (in) put_window(M, oi + (uint32_t)__popcll(bi & below), pk, e);
+    if (out) {
+      put_pool(M, nxt, oo + (uint64_t)__popcll(bo & below), e);
+      tmn = e.ts < tmn ? e.ts : tmn;
+      const uint64_t x = e.ts + (uint64_t)M.lookahead[e.kind & 0xffu];
+      wnd = x < wnd ? x : wnd;
+      if ((e.kind & 0xffu) == K_STOP) {
+        R.stopts = e.ts;
+        R.stopuid = e.uid;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_nw += ti;
+      s_no += to;
+    }
+    __syncthreads();
+  }
+  publish_min<SCAN_THREADS>(R, tmn, wnd);
+  if (threadIdx.x == 0) {
+    C.W = s_nw;
+    C.nxtP = s_no;
+    C.overflow = 0;
+    C.prep = 1;    // the next k_pa leaves this window alone
+    C.pvalid = 0;  // (the last window was appended by the k_pa that overflowed)
+  }
 }
 
-// ---- k_scan: child / inline prefixes in rank order, same-ts groups, run bookkeeping ----
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan(const P2PDev *__restrict__ Mp) {
-  const P2PDev &M = *Mp;
+// ---- k_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(const P2PDev M) {
   Ctl &C = *M.C;
   if (C.done) return;
+  if (C.overflow) {
+    refit(M, C);
+    return;
+  }
   constexpr int RPT = WCAP / SCAN_THREADS;
-  __shared__ uint32_t wsum[SCAN_THREADS / 64];
-  __shared__ uint32_t gstart[WCAP];
-  const uint32_t W = C.W;
+  __shared__ uint32_t l_slot[WCAP], l_cnt[WCAP], l_rel[WCAP], gstart[WCAP];
+  PH_BEGIN();
   const int tid = threadIdx.x;
-  uint32_t nc[RPT], ni[RPT], hd[RPT], sc = 0, si = 0, sh = 0;
-  uint64_t prev_rel = 0;
-  if (tid * RPT < (int)W && tid > 0) prev_rel = M.skey[tid * RPT - 1] >> 32;
+  // the window's slots, ahead of the run control
+  uint32_t pr[RPT], pc[RPT], pctx[RPT];
+  uint64_t pkey[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t i = tid + q * SCAN_THREADS;
+    pr[q] = M.wrank[i];
+    pc[q] = M.nchild[i] | (M.ninl[i] << 16);
+    pkey[q] = M.wkey[i];
+    pctx[q] = M.wctx[i];
+  }
+  const uint32_t W = C.W;
+  PH_MARK(16);
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {  // slot order -> rank order; keys / contexts kept for the next k_pa
+    const uint32_t i = tid + q * SCAN_THREADS;
+    if (i < W) {
+      const uint32_t r = pr[q];
+      M.wrank[i] = 0;
+      M.pwkey[i] = pkey[q];
+      M.pwctx[i] = pctx[q];
+      l_slot[r] = i;
+      l_cnt[r] = pc[q];
+      l_rel[r] = (uint32_t)(pkey[q] >> 32);
+    }
+  }
+  __syncthreads();
+  PH_MARK(17);
+  uint32_t nc[RPT], ni[RPT], hd[RPT];
+  uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
+  uint32_t prev_rel = (tid * RPT < (int)W && tid > 0) ? l_rel[tid * RPT - 1] : 0;
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
     nc[q] = ni[q] = hd[q] = 0;
     if (r < W) {
-      nc[q] = M.nchild[r];
-      ni[q] = M.ninl[r];
-      const uint64_t rel = M.skey[r] >> 32;
+      nc[q] = l_cnt[r] & 0xffffu;
+      ni[q] = l_cnt[r] >> 16;
+      const uint32_t rel = l_rel[r];
       hd[q] = r == 0 || rel != prev_rel;
       prev_rel = rel;
     }
-    sc += nc[q];
-    si += ni[q];
-    sh += hd[q];
+    sum += (uint64_t)nc[q] | ((uint64_t)ni[q] << 21) | ((uint64_t)hd[q] << 42);
   }
-  uint32_t tc, tinl, ng;
-  uint32_t bc = block_exscan<SCAN_THREADS>(sc, wsum, &tc);
-  uint32_t bi = block_exscan<SCAN_THREADS>(si, wsum, &tinl);
-  uint32_t bh = block_exscan<SCAN_THREADS>(sh, wsum, &ng);
-  uint32_t g[RPT];
+  // block exclusive scan of the packed sums (no field exceeds 21 bits: <= WCAP * maxc)
+  const int lane = tid & 63, wid = tid >> 6;
+  uint64_t inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t w = __shfl_up(inc, o);
+    if (lane >= o) inc += w;
+  }
+  __shared__ uint64_t wsum64[SCAN_THREADS / 64];
+  if (lane == 63) wsum64[wid] = inc;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+  for (int w = 0; w < SCAN_THREADS / 64; w++) {
+    const uint64_t s = wsum64[w];
+    off += w < wid ? s : 0;
+    tot += s;
+  }
+  const uint64_t ex = off + inc - sum;
+  const uint32_t tc = (uint32_t)(tot & 0x1fffffu), tinl = (uint32_t)((tot >> 21) & 0x1fffffu),
+                 ng = (uint32_t)(tot >> 42);
+  uint32_t bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu), bh = (uint32_t)(ex >> 42);
+  uint32_t g[RPT], ipr[RPT], cpr[RPT];
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
     bh += hd[q];
     g[q] = bh - 1;  // same-ts group of rank r
-    if (r < W) {
-      M.cpref[r] = bc;
-      M.ipref[r] = bi;
-      if (hd[q]) gstart[g[q]] = r;
-    }
+    cpr[q] = bc;
+    ipr[q] = bi;
+    if (r < W && hd[q]) gstart[g[q]] = r;
     bc += nc[q];
     bi += ni[q];
   }
   __syncthreads();
+  PH_MARK(18);
+  // l_cnt is dead: reuse it for the inline prefix by rank
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    if (r < W) l_cnt[r] = ipr[q];
+  }
+  __syncthreads();
+  // per-slot dispatch info for k_pa (one 16-B record per slot):
+  //   x: dispatch rank of the event, relative to K0 = r + #inline children with ts < ts_r
+  //   y: dispatch rank of its first inline child = (#main events with ts <= ts_r) + iprefix[r]
+  //   z: child prefix (uids uid0 + z + j), w: inline prefix
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
     if (r < W) {
       const uint32_t first = gstart[g[q]];
       const uint32_t last = (g[q] + 1 < ng ? gstart[g[q] + 1] : W) - 1;
-      M.gbnd[r] = first | (last << 16);
+      M.sinfo[l_slot[r]] = make_uint4(r + (tinl ? l_cnt[first] : 0), last + 1 + ipr[q], cpr[q], ipr[q]);
     }
   }
+  PH_MARK(19);
   if (tid == 0) {
-    C.K0 = C.K;
-    C.uid0 = C.uid;
-    C.W0 = W;
-    C.Pbase = C.nxtP;
-    C.tmin0 = C.tmin;
-    C.inline_lim0 = C.inline_lim;
-    C.total_children = tc;
-    C.total_inline = tinl;
+    const uint64_t win = C.windows;
+    C.pK0 = C.K;
+    C.puid0 = C.uid;
+    C.ptmin = C.tmin;
+    C.pinline_lim = C.inline_lim;
+    C.pW = W;
+    C.pinl = tinl;
+    C.pvalid = 1;
+    if (W) C.last_ts = C.tmin + l_rel[W - 1];
     // (inline children at the Stop's ts are scheduled — uids consumed — but never dispatched; the run
-    //  ends with this window, so the pool bookkeeping only has to be right for other windows)
+    //  ends with this window, so the pending count only has to be right for other windows)
     const uint64_t newP = (uint64_t)C.nxtP + tc - tinl;
     C.K += W + tinl;
     C.uid += tc;
-    C.P = newP;
+    C.P = C.nxtP;
     C.cur ^= 1;
-    C.windows++;
+    C.red[(win + 1) & 1].tmin = C.red[(win + 1) & 1].wend = C.red[(win + 1) & 1].stopts = ~0ull;  // consumed
+    C.windows = win + 1;
     if (W > C.max_window) C.max_window = W;
-    C.tmin = ~0ull;
-    C.wend = ~0ull;
-    C.stopts = ~0ull;
     C.W = 0;
     C.nxtP = 0;
+    C.prep = 0;
     bool done = C.stop_seen || newP == 0;
     if (newP > M.pool_cap) {
       atomicOr(M.error, 1u);
@@ -883,76 +1298,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const P2PDev *__restrict_
       atomicOr(M.error, 4u);
       done = true;
     }
-    C.scan_ran = 1;
     if (done) C.done = 1;
   }
-}
-
-// ---- k_append: dispatch ranks (digest, log), children -> pool ----
-__global__ __launch_bounds__(RB) void k_append(const P2PDev *__restrict__ Mp) {
-  const P2PDev &M = *Mp;
-  Ctl &C = *M.C;
-  if (!C.scan_ran) return;
-  const uint32_t W = C.W0;
-  const uint32_t r = blockIdx.x * RB + threadIdx.x;
-  if (blockIdx.x * RB >= W) return;  // whole block idle (uniform)
-  uint64_t digest = 0;
-  if (r < W) {
-    const uint64_t K0 = C.K0, tmin = C.tmin0, inline_lim = C.inline_lim0;
-    const uint32_t uid0 = C.uid0, tinl = C.total_inline;
-    const uint64_t pk = M.skey[r];
-    const uint64_t rel = pk >> 32;
-    const uint64_t t = tmin + rel;
-    const uint32_t u = (uint32_t)pk;
-    const uint32_t gb = M.gbnd[r];
-    const uint32_t first = gb & 0xffffu, last = gb >> 16;
-    const uint32_t ip = M.ipref[r], cp = M.cpref[r];
-    // dispatch rank of main event r = r + #inline children with ts < ts_r; of the i-th inline child
-    // of r = (#main events with ts <= ts_r) + iprefix[r] + i  (inline children are key-sorted by r)
-    const uint64_t rk = K0 + r + (tinl ? M.ipref[first] : 0);
-    digest += digest_term(rk, t, u);
-    if (rk < M.log_cap) {
-      M.log_ts[rk] = t;
-      M.log_uid[rk] = u;
-      M.log_ctx[rk] = M.sctx[r];
-    }
-    if (r == W - 1) C.last_ts = t;
-    const uint32_t ncr = M.nchild[r];
-    uint32_t ii = 0;
-    uint64_t o = (uint64_t)C.Pbase + (cp - ip);  // non-inline children before this rank
-    const int dst = C.cur;                       // (already flipped by k_scan: the next pool)
-    for (uint32_t j = 0; j < ncr; j++) {
-      const uint32_t sl = r * M.maxc + j;
-      const uint32_t cu = uid0 + cp + j;
-      const uint32_t kw = M.ch_kind[sl];
-      if ((kw & 0xffu) == K_FWD_UP) {
-        if (rel < inline_lim) {  // dispatched inside this window
-          const uint64_t crk = K0 + last + 1 + ip + ii;
-          digest += digest_term(crk, t, cu);
-          if (crk < M.log_cap) {
-            M.log_ts[crk] = t;
-            M.log_uid[crk] = cu;
-            M.log_ctx[crk] = M.ch_ctx[sl];
-          }
-          ii++;
-        }
-        continue;  // never re-queued
-      }
-      if (o < M.pool_cap) {
-        M.ev_ts[dst][o] = M.ch_ts[sl];
-        M.ev_uid[dst][o] = cu;
-        M.ev_ctx[dst][o] = M.ch_ctx[sl];
-        M.ev_kind[dst][o] = kw;
-        M.ev_a[dst][o] = M.ch_a[sl];
-        M.ev_pkt[dst][o] = M.ch_pkt[sl];
-      } else {
-        atomicOr(M.error, 1u);
-      }
-      o++;
-    }
-  }
-  digest = wave_sum64(digest);
-  if ((threadIdx.x & 63) == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
+  PH_MARK(20);
 }
 
 }  // namespace nsgpu
@@ -962,6 +1310,7 @@ __global__ __launch_bounds__(RB) void k_append(const P2PDev *__restrict__ Mp) {
 #include <vector>
 #include <algorithm>
 #include <string.h>
+#include <stdlib.h>
 
 using namespace nsgpu;
 
@@ -969,8 +1318,6 @@ struct nsgpu_p2p {
   P2PDev M;
   nsgpu_p2p_scenario sc;
   std::vector<void *> allocs;
-  int32_t *sink_of_node = nullptr;
-  P2PDev *d_M = nullptr;  // device copy of M (kernel argument by pointer)
   Ctl C0{};               // run control after reset
   uint64_t max_windows = ~0ull;
   hipStream_t s = nullptr;  // engine stream (graph capture and replay)
@@ -978,6 +1325,7 @@ struct nsgpu_p2p {
   hipEvent_t ev[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr;
   uint32_t *done_host = nullptr;  // pinned, 2 slots
   float last_ms = 0.f;
+  bool eager = getenv("NSGPU_P2P_EAGER") != nullptr;  // kernels one by one instead of graph replays
   // pristine initial pool (device) for resets
   uint64_t *init_ts = nullptr;
   uint32_t *init_uid = nullptr, *init_ctx = nullptr, *init_kind = nullptr, *init_a = nullptr;
@@ -1120,7 +1468,7 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   TRY(dupload(h, &M.node_app_list, node_list.data(), A));
   const int32_t *sinkp;
   TRY(dupload(h, &sinkp, sink.data(), N));
-  h->sink_of_node = (int32_t *)sinkp;
+  M.sink_of_node = sinkp;
   // ---- state ----
   TRY(dalloc(h, &M.dev_busy, D));
   TRY(dalloc(h, &M.q_head, D));
@@ -1135,7 +1483,8 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   TRY(dalloc(h, &M.app_seq, A));
   TRY(dalloc(h, &M.app_last_start, A));
   TRY(dalloc(h, &M.appc, A));
-  TRY(dalloc(h, &M.node_head, N));
+  TRY(dalloc(h, &M.node_cnt, N));
+  TRY(dalloc(h, &M.node_slot, (size_t)N * NSLOT));
   // ---- setup-time events (node-list.cc:124-131, node.cc:111-145, default-simulator-impl.cc:179-183) ----
   std::vector<uint64_t> its;
   std::vector<uint32_t> iuid, ictx, ikind, ia;
@@ -1187,9 +1536,11 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   TRY(dalloc(h, &M.ch_a, chn));
   TRY(dalloc(h, &M.ch_pkt, chn));
   TRY(dalloc(h, &M.wkey, WCAP));
-  TRY(dalloc(h, &M.skey, WCAP));
-  for (uint32_t **p : {&M.wpi, &M.wrank, &M.spi, &M.sctx, &M.link, &M.nchild, &M.ninl, &M.cpref, &M.ipref, &M.gbnd})
-    TRY(dalloc(h, p, WCAP));
+  TRY(dalloc(h, &M.pwkey, WCAP));
+  TRY(dalloc(h, &M.wpkt, WCAP));
+  TRY(dalloc(h, &M.sinfo, WCAP));
+  for (uint32_t **p : {&M.wctx, &M.wkind, &M.wa, &M.widx, &M.nchild, &M.ninl, &M.pwctx}) TRY(dalloc(h, p, WCAP));
+  TRY(dalloc(h, &M.wrank, WCAP));
   TRY(dalloc(h, &M.C, 1));
   TRY(dalloc(h, &M.error, 4));
   M.log_cap = log_cap;
@@ -1213,10 +1564,22 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   memset(&C0, 0, sizeof(C0));
   C0.P = M.n_init;
   C0.uid = uid;
-  C0.tmin = C0.wend = C0.stopts = ~0ull;
+  // reduction of the initial pool: window 0 is bounded by red[1] (k_pa / k_handle_rank fold later
+  // pending sets in for the next windows)
+  for (int b = 0; b < 2; b++) {
+    C0.red[b].tmin = C0.red[b].wend = C0.red[b].stopts = ~0ull;
+    C0.red[b].stopuid = 0;
+  }
+  for (size_t i = 0; i < its.size(); i++) {
+    C0.red[1].tmin = std::min<uint64_t>(C0.red[1].tmin, its[i]);
+    C0.red[1].wend = std::min<uint64_t>(C0.red[1].wend, its[i] + (uint64_t)M.lookahead[ikind[i] & 0xffu]);
+    if ((ikind[i] & 0xffu) == K_STOP) {
+      C0.red[1].stopts = its[i];
+      C0.red[1].stopuid = iuid[i];
+    }
+  }
   C0.max_windows = h->max_windows;
-  C0.done = M.n_init == 0;
-  TRY(dalloc(h, &h->d_M, 1));
+  C0.done = M.n_init == 0 ? 2 : 0;
   if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
     h->s = nullptr;
     nsgpu_p2p_destroy(h);
@@ -1238,10 +1601,6 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
     h->done_host = nullptr;
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_ENOMEM, "nsgpu_p2p_create: hipHostMalloc failed");
-  }
-  if (hipMemcpy(h->d_M, &h->M, sizeof(P2PDev), hipMemcpyHostToDevice) != hipSuccess) {
-    nsgpu_p2p_destroy(h);
-    return set_error(NSGPU_EHIP, "nsgpu_p2p_create: upload failed");
   }
   *out = h;
   return NSGPU_OK;
@@ -1270,28 +1629,36 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.app_seq, 0, A * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.app_last_start, 0, A * sizeof(uint64_t), s));
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
-  NSGPU_HIP(hipMemsetAsync(M.node_head, 0xff, M.n_nodes * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(M.node_cnt, 0, M.n_nodes * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.wrank, 0, WCAP * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemcpyAsync(M.C, &h->C0, sizeof(Ctl), hipMemcpyHostToDevice, s));
   return NSGPU_OK;
 }
 
+// The window pipeline, in launch order (graph capture, eager runs and the per-kernel profile).
+namespace {
+constexpr int NKERN = 3;
+const char *const KERNEL_NAMES[NKERN] = {"k_pa", "k_handle_rank", "k_scan"};
+void launch_kernel(nsgpu_p2p *h, int k, hipStream_t s) {
+  switch (k) {
+    case 0: hipLaunchKernelGGL(k_pa, dim3(GRID_POOL), dim3(TB), 0, s, h->M); break;
+    case 1: hipLaunchKernelGGL(k_handle_rank, dim3(NHB + NRB), dim3(HB), 0, s, h->M); break;
+    default: hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, s, h->M); break;
+  }
+}
+void launch_windows(nsgpu_p2p *h, hipStream_t s) {
+  for (int w = 0; w < NWIN; w++)
+    for (int k = 0; k < NKERN; k++) launch_kernel(h, k, s);
+}
+}  // namespace
+
 static int build_graph(nsgpu_p2p *h) {
   // NWIN windows of the pipeline; kernels read every run-dependent value from the device (Ctl), so
   // one instantiated graph serves every run of this engine
   hipGraph_t g = nullptr;
   NSGPU_HIP(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
-  for (int w = 0; w < NWIN; w++) {
-    hipLaunchKernelGGL(k_reduce, dim3(GRID_POOL), dim3(TB), 0, h->s, h->d_M);
-    hipLaunchKernelGGL(k_partition, dim3(GRID_POOL), dim3(TB), 0, h->s, h->d_M);
-    hipLaunchKernelGGL(k_refit, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->d_M);
-    hipLaunchKernelGGL(k_rank, dim3(NT * NT), dim3(TB), 0, h->s, h->d_M);
-    hipLaunchKernelGGL(k_scatter, dim3(WCAP / RB), dim3(RB), 0, h->s, h->d_M);
-    hipLaunchKernelGGL(k_handle, dim3(WCAP / RB), dim3(RB), 0, h->s, h->d_M, h->sink_of_node);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->d_M);
-    hipLaunchKernelGGL(k_append, dim3(WCAP / RB), dim3(RB), 0, h->s, h->d_M);
-  }
+  launch_windows(h, h->s);
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (e != hipSuccess) return set_error(NSGPU_EHIP, "nsgpu_p2p: graph capture: %s", hipGetErrorString(e));
   e = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
@@ -1303,11 +1670,12 @@ static int build_graph(nsgpu_p2p *h) {
   return NSGPU_OK;
 }
 
-// Runs the simulation to completion (blocking): graph replays of NWIN windows on the engine stream,
-// ordered after the work already queued on `stream`; work queued on `stream` later runs after it.
+// Runs the simulation to completion (blocking): replays of NWIN windows on the engine stream (one
+// hipGraph launch each, or the same kernels launched one by one in eager mode), ordered after the
+// work already queued on `stream`; work queued on `stream` later runs after it.
 extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_run: null");
-  if (!h->gexec) {
+  if (!h->eager && !h->gexec) {
     int rc = build_graph(h);
     if (rc) return rc;
   }
@@ -1318,12 +1686,17 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   h->done_host[0] = h->done_host[1] = 0;
   // two replays in flight: replay i+1 is queued before the done flag of replay i is examined
   for (uint64_t it = 0;; it++) {
-    NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
+    if (h->eager) {
+      launch_windows(h, h->s);
+      NSGPU_HIP(hipGetLastError());
+    } else {
+      NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
+    }
     NSGPU_HIP(hipMemcpyAsync(&h->done_host[it & 1], &h->M.C->done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
     NSGPU_HIP(hipEventRecord(h->ev[it & 1], h->s));
     if (it > 0) {
       NSGPU_HIP(hipEventSynchronize(h->ev[(it - 1) & 1]));
-      if (h->done_host[(it - 1) & 1]) break;
+      if (h->done_host[(it - 1) & 1] >= 2) break;  // 2: the final window is appended
     }
   }
   NSGPU_HIP(hipEventRecord(h->t1, h->s));
@@ -1332,6 +1705,94 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipEventRecord(h->ev[0], h->s));
   NSGPU_HIP(hipStreamWaitEvent(cs, h->ev[0], 0));
   return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset) {
+#ifdef NSGPU_PHASE_PROF
+  if (!out || n <= 0) return set_error(NSGPU_EINVAL, "nsgpu_p2p_phase_read: null");
+  if (n > 64) n = 64;
+  NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), n * sizeof(uint64_t)));
+  if (reset) {
+    uint64_t z[64] = {0};
+    NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
+  }
+  return NSGPU_OK;
+#else
+  (void)out, (void)n, (void)reset;
+  return set_error(NSGPU_ESTATE, "nsgpu_p2p_phase_read: library built without NSGPU_PHASE_PROF");
+#endif
+}
+
+extern "C" int nsgpu_p2p_set_eager(nsgpu_p2p *h, int eager) {
+  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_eager: null");
+  h->eager = eager != 0;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_kernel_count(int *n) {
+  if (!n) return set_error(NSGPU_EINVAL, "nsgpu_p2p_kernel_count: null");
+  *n = NKERN;
+  return NSGPU_OK;
+}
+
+extern "C" const char *nsgpu_p2p_kernel_name(int k) { return k >= 0 && k < NKERN ? KERNEL_NAMES[k] : nullptr; }
+
+// Per-kernel device time: runs the simulation to completion with the pipeline's kernels launched
+// one by one on the engine stream; in every `sample_every`-th window each kernel is bracketed by
+// two HIP events on that stream, and kernel_ms[k] / launches[k] accumulate the bracketed time and
+// the bracketed launches of kernel k (NKERN entries each).  Other windows run unbracketed.
+extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_every, double *kernel_ms,
+                                 uint64_t *launches) {
+  if (!h || !kernel_ms || !launches) return set_error(NSGPU_EINVAL, "nsgpu_p2p_profile: null");
+  if (sample_every == 0) sample_every = 1;
+  for (int k = 0; k < NKERN; k++) kernel_ms[k] = 0.0, launches[k] = 0;
+  hipEvent_t eb[NKERN], ea[NKERN];
+  for (int k = 0; k < NKERN; k++) {
+    NSGPU_HIP(hipEventCreate(&eb[k]));
+    NSGPU_HIP(hipEventCreate(&ea[k]));
+  }
+  hipStream_t cs = (hipStream_t)stream;
+  NSGPU_HIP(hipEventRecord(h->ev[0], cs));
+  NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev[0], 0));
+  int rc = NSGPU_OK;
+  for (uint64_t w = 0; rc == NSGPU_OK; w++) {
+    const bool sample = (w % sample_every) == 0;
+    for (int k = 0; k < NKERN; k++) {
+      if (sample) (void)hipEventRecord(eb[k], h->s);
+      launch_kernel(h, k, h->s);
+      if (sample) (void)hipEventRecord(ea[k], h->s);
+    }
+    if (hipGetLastError() != hipSuccess) {
+      rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: launch failed");
+      break;
+    }
+    if (sample || (w % NWIN) == NWIN - 1) {
+      uint32_t done = 0;
+      if (hipMemcpyAsync(&h->done_host[0], &h->M.C->done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->s) !=
+              hipSuccess ||
+          hipStreamSynchronize(h->s) != hipSuccess) {
+        rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: sync failed");
+        break;
+      }
+      done = h->done_host[0] >= 2;
+      if (sample)
+        for (int k = 0; k < NKERN; k++) {
+          float ms = 0.f;
+          if (hipEventElapsedTime(&ms, eb[k], ea[k]) == hipSuccess) {
+            kernel_ms[k] += ms;
+            launches[k]++;
+          }
+        }
+      if (done) break;
+    }
+  }
+  for (int k = 0; k < NKERN; k++) {
+    (void)hipEventDestroy(eb[k]);
+    (void)hipEventDestroy(ea[k]);
+  }
+  (void)hipEventRecord(h->ev[0], h->s);
+  (void)hipStreamWaitEvent(cs, h->ev[0], 0);
+  return rc;
 }
 
 extern "C" int nsgpu_p2p_last_run_ms(nsgpu_p2p *h, double *gpu_ms) {

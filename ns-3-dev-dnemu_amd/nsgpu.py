@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libnsgpu.so")
+# NSGPU_LIB selects another build of the same library (e.g. the phase-profiling diagnostic build)
+LIB_PATH = os.environ.get("NSGPU_LIB") or os.path.join(_HERE, "lib", "libnsgpu.so")
 
 
 class NsgpuError(RuntimeError):
@@ -96,6 +97,11 @@ SIGNATURES = {
     "nsgpu_p2p_results": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
     "nsgpu_p2p_destroy": (C.c_int, [_vp]),
     "nsgpu_p2p_last_run_ms": (C.c_int, [_vp, C.POINTER(C.c_double)]),
+    "nsgpu_p2p_set_eager": (C.c_int, [_vp, C.c_int]),
+    "nsgpu_p2p_phase_read": (C.c_int, [_vp, C.c_int, C.c_int]),
+    "nsgpu_p2p_kernel_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "nsgpu_p2p_kernel_name": (C.c_char_p, [C.c_int]),
+    "nsgpu_p2p_profile": (C.c_int, [_vp, _vp, _u32, _vp, _vp]),
     "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
 }
 

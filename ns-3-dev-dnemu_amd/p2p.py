@@ -290,6 +290,25 @@ class Engine:
     def launch(self):
         nsgpu.check(nsgpu.lib().nsgpu_p2p_run(self.h, self.stream))
 
+    def set_eager(self, eager=True):
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_set_eager(self.h, int(eager)))
+
+    def profile(self, sample_every=4):
+        """One full run with per-kernel HIP-event brackets (nsgpu_p2p_profile); returns
+        {kernel name: (average ms per launch, bracketed launches)}."""
+        n = C.c_int()
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_kernel_count(C.byref(n)))
+        ms = np.zeros(n.value, np.float64)
+        cnt = np.zeros(n.value, np.uint64)
+        self.reset()
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_profile(self.h, self.stream, sample_every, ms.ctypes.data,
+                                                  cnt.ctypes.data))
+        out = {}
+        for k in range(n.value):
+            name = nsgpu.lib().nsgpu_p2p_kernel_name(k).decode()
+            out[name] = (float(ms[k] / cnt[k]) if cnt[k] else 0.0, int(cnt[k]))
+        return out
+
     def results(self, log_n=0):
         st = P2PStats()
         devc = np.zeros(self.s.n_devices, DEV_COUNTERS_DTYPE)

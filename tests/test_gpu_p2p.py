@@ -60,3 +60,24 @@ def test_grid_congested_drops():
 def test_grid_32x32_counters_digest():
     o, g = both(p2p.grid(32, 32))
     assert_same(o, g, log=False)
+
+
+def test_eager_launches_match_graph_replays():
+    """The kernels launched one by one (profiling mode) compute exactly what the graph replays do."""
+    sc = p2p.grid(12, 12)
+    eng = p2p.Engine(sc, log_cap=100000)
+    a = eng.run(log_n=100000)
+    eng.set_eager(True)
+    b = eng.run(log_n=100000)
+    assert_same((a[0], a[1], a[2], a[3]), b)
+    prof = eng.profile(sample_every=2)
+    assert set(prof) >= {"k_pa", "k_handle_rank", "k_scan"}
+    assert all(ms >= 0 for ms, _ in prof.values())
+    c = eng.results()
+    assert c[0].digest == a[0].digest and c[0].dispatched == a[0].dispatched
+
+
+def test_grid_128x128_counters_digest():
+    """The bench workload itself (config 4): every counter, the digest, final time and next uid."""
+    o, g = both(p2p.grid(128, 128))
+    assert_same(o, g, log=False)
