@@ -108,10 +108,11 @@ class P2PGrid:
         self.engine.launch()
 
     def roofline(self, step_kernel_ms, events_per_step):
-        # the window pipeline is 8 kernels per window; a separate eager run brackets each kernel of
-        # every 4th window with HIP events on the engine stream, and the kernel with the largest
-        # total time is the dominant one (events per launch = the average window)
-        prof = self.engine.profile(sample_every=4)
+        # the window pipeline is 3 kernels per window; a separate eager run launches each kernel of
+        # every 8th window with start/stop HIP events recorded by the command processor at the
+        # kernel's own start and end (hipExtLaunchKernel), and the kernel with the largest average
+        # time is the dominant one (events per launch = the average window)
+        prof = self.engine.profile(sample_every=8)
         st, _, _, _ = self.engine.results()
         windows = max(int(st.windows), 1)
         name = max(prof, key=lambda k: prof[k][0])
@@ -119,13 +120,14 @@ class P2PGrid:
                 "events_per_launch": events_per_step / windows,
                 "step_device_ms": step_kernel_ms, "windows_per_step": windows,
                 "pipeline_ms_per_window": {k: round(v[0] * 1e3, 3) for k, v in prof.items()},
-                "pipeline_unit": "us per launch (HIP events, sampled windows)"}
+                "pipeline_unit": "us per launch (hipExtLaunchKernel start/stop events, sampled windows)"}
 
     def result(self):
         st, devc, appc, _ = self.engine.results()
         return int(st.dispatched), int(st.digest), {
             "windows_per_step": int(st.windows), "max_window": int(st.max_window),
-            "cancelled_per_step": int(st.cancelled), "delivered_packets": int(appc["rx_packets"].sum())}
+            "cancelled_per_step": int(st.cancelled), "refits_per_step": int(st.refits),
+            "delivered_packets": int(appc["rx_packets"].sum())}
 
     def cpu_baseline(self):
         import numpy as np

@@ -179,8 +179,9 @@ int nsgpu_p2p_set_eager(nsgpu_p2p *h, int eager);
 /* The window pipeline's kernels: count and names (launch order). */
 int nsgpu_p2p_kernel_count(int *n);
 const char *nsgpu_p2p_kernel_name(int k);
-/* Per-kernel device time of one full run (from the state nsgpu_p2p_reset loaded): every
- * sample_every-th window brackets each kernel with HIP events on the engine stream; kernel_ms[k] and
+/* Per-kernel device time of one full run (from the state nsgpu_p2p_reset loaded): in every
+ * sample_every-th window each kernel is launched with start / stop HIP events that the command
+ * processor records at the kernel's own start and end (hipExtLaunchKernel); kernel_ms[k] and
  * launches[k] (nsgpu_p2p_kernel_count entries) accumulate the bracketed time and launch count. */
 int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_every, double *kernel_ms, uint64_t *launches);
 /* Diagnostic: in-kernel phase timers (s_memrealtime ticks, 100 MHz) of the pipeline kernels; only the

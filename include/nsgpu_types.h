@@ -137,6 +137,7 @@ typedef struct nsgpu_p2p_stats {
   uint64_t no_route_drops;
   uint64_t max_window;
   uint64_t unreach_drops;     /* UDP datagrams with no bound endpoint (ICMP port unreachable not modelled) */
+  uint64_t refits;            /* GPU: windows cut back to the window capacity (0 for the oracle) */
 } nsgpu_p2p_stats;
 
 /* Per-device counters: Queue (queue.cc:61-200) + device. */

@@ -26,6 +26,7 @@
 //   k_scan       rank order; exclusive scans of child counts (uids), run bookkeeping;
 //   k_append     digest/log of the dispatch order, children -> pool with the uids DefaultSimulatorImpl
 //                would assign, and their part of the next window's reduction.
+#include <hip/hip_ext.h>
 #include "nsgpu_device.h"
 #include "nsgpu_internal.h"
 
@@ -81,7 +82,7 @@ struct Ctl {
   uint64_t P;                          // pending events in pool `cur` (besides the last window's children)
   uint64_t K;                          // dispatched so far (after the last scanned window)
   uint64_t tmin, bound, inline_lim;    // current window (k_pa / refit)
-  uint64_t windows, max_window, last_ts, max_windows;
+  uint64_t windows, max_window, last_ts, max_windows, refits;
   uint64_t digest, cancelled, ttl_drops, no_route, unreach;
   uint64_t pK0, ptmin, pinline_lim;    // the last scanned window, appended by the next k_pa
   uint32_t uid, cur, W, nxtP, overflow, prep, done, stop_seen;
@@ -1149,6 +1150,7 @@ __device__ void refit(const P2PDev &M, Ctl &C) {
   if (threadIdx.x == 0) {
     C.W = s_nw;
     C.nxtP = s_no;
+    C.refits++;
     C.overflow = 0;
     C.prep = 1;    // the next k_pa leaves this window alone
     C.pvalid = 0;  // (the last window was appended by the k_pa that overflowed)
@@ -1640,11 +1642,13 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
 namespace {
 constexpr int NKERN = 3;
 const char *const KERNEL_NAMES[NKERN] = {"k_pa", "k_handle_rank", "k_scan"};
-void launch_kernel(nsgpu_p2p *h, int k, hipStream_t s) {
+// ev0 / ev1: optional HIP events the command processor records at the kernel's start and end
+// (hipExtLaunchKernelGGL: no separate marker packets between the pipeline's kernels).
+void launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   switch (k) {
-    case 0: hipLaunchKernelGGL(k_pa, dim3(GRID_POOL), dim3(TB), 0, s, h->M); break;
-    case 1: hipLaunchKernelGGL(k_handle_rank, dim3(NHB + NRB), dim3(HB), 0, s, h->M); break;
-    default: hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, s, h->M); break;
+    case 0: hipExtLaunchKernelGGL(k_pa, dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M); break;
+    case 1: hipExtLaunchKernelGGL(k_handle_rank, dim3(NHB + NRB), dim3(HB), 0, s, ev0, ev1, 0, h->M); break;
+    default: hipExtLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M); break;
   }
 }
 void launch_windows(nsgpu_p2p *h, hipStream_t s) {
@@ -1746,50 +1750,61 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
   if (!h || !kernel_ms || !launches) return set_error(NSGPU_EINVAL, "nsgpu_p2p_profile: null");
   if (sample_every == 0) sample_every = 1;
   for (int k = 0; k < NKERN; k++) kernel_ms[k] = 0.0, launches[k] = 0;
-  hipEvent_t eb[NKERN], ea[NKERN];
-  for (int k = 0; k < NKERN; k++) {
-    NSGPU_HIP(hipEventCreate(&eb[k]));
-    NSGPU_HIP(hipEventCreate(&ea[k]));
-  }
-  hipStream_t cs = (hipStream_t)stream;
-  NSGPU_HIP(hipEventRecord(h->ev[0], cs));
-  NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev[0], 0));
+  // up to NS sampled windows; the events are read after the run (no synchronisation in between
+  // beyond the done-flag checks every NWIN windows that nsgpu_p2p_run makes too)
+  constexpr int NS = 512;
+  std::vector<hipEvent_t> ev(2 * NKERN * NS, nullptr);
   int rc = NSGPU_OK;
-  for (uint64_t w = 0; rc == NSGPU_OK; w++) {
-    const bool sample = (w % sample_every) == 0;
-    for (int k = 0; k < NKERN; k++) {
-      if (sample) (void)hipEventRecord(eb[k], h->s);
-      launch_kernel(h, k, h->s);
-      if (sample) (void)hipEventRecord(ea[k], h->s);
+  for (auto &e : ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      e = nullptr;
+      rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: hipEventCreate failed");
+      break;
     }
+  hipStream_t cs = (hipStream_t)stream;
+  if (rc == NSGPU_OK && (hipEventRecord(h->ev[0], cs) != hipSuccess || hipStreamWaitEvent(h->s, h->ev[0], 0) != hipSuccess))
+    rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: stream join failed");
+  int ns = 0;
+  for (uint64_t w = 0; rc == NSGPU_OK; w++) {
+    const bool sample = (w % sample_every) == 0 && ns < NS;
+    for (int k = 0; k < NKERN; k++) {
+      if (sample) launch_kernel(h, k, h->s, ev[(2 * ns) * NKERN + k], ev[(2 * ns + 1) * NKERN + k]);
+      else launch_kernel(h, k, h->s);
+    }
+    if (sample) ns++;
     if (hipGetLastError() != hipSuccess) {
       rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: launch failed");
       break;
     }
-    if (sample || (w % NWIN) == NWIN - 1) {
-      uint32_t done = 0;
+    if ((w % NWIN) == NWIN - 1) {
       if (hipMemcpyAsync(&h->done_host[0], &h->M.C->done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->s) !=
               hipSuccess ||
           hipStreamSynchronize(h->s) != hipSuccess) {
         rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: sync failed");
         break;
       }
-      done = h->done_host[0] >= 2;
-      if (sample)
-        for (int k = 0; k < NKERN; k++) {
-          float ms = 0.f;
-          if (hipEventElapsedTime(&ms, eb[k], ea[k]) == hipSuccess) {
-            kernel_ms[k] += ms;
-            launches[k]++;
-          }
-        }
-      if (done) break;
+      if (h->done_host[0] >= 2) break;  // the final window is appended
     }
   }
-  for (int k = 0; k < NKERN; k++) {
-    (void)hipEventDestroy(eb[k]);
-    (void)hipEventDestroy(ea[k]);
+  if (rc == NSGPU_OK) {
+    Ctl c;
+    if (hipMemcpyAsync(&c, h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s) != hipSuccess ||
+        hipStreamSynchronize(h->s) != hipSuccess)
+      rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: sync failed");
+    // pipeline passes that did work: every window, one more per refit, the final append; later
+    // sampled passes of the last NWIN batch hold early-exit launches and are not counted
+    const uint64_t real = c.windows + c.refits + 1;
+    for (int i = 0; i < ns && (uint64_t)i * sample_every < real; i++)
+      for (int k = 0; k < NKERN; k++) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ev[(2 * i) * NKERN + k], ev[(2 * i + 1) * NKERN + k]) == hipSuccess) {
+          kernel_ms[k] += ms;
+          launches[k]++;
+        }
+      }
   }
+  for (auto e : ev)
+    if (e) (void)hipEventDestroy(e);
   (void)hipEventRecord(h->ev[0], h->s);
   (void)hipStreamWaitEvent(cs, h->ev[0], 0);
   return rc;
@@ -1830,6 +1845,7 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
     stats->no_route_drops = c.no_route;
     stats->max_window = c.max_window;
     stats->unreach_drops = c.unreach;
+    stats->refits = c.refits;
   }
   if (error) *error = err;
   if (err) return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, "

@@ -42,7 +42,7 @@ class P2PStats(C.Structure):
     _fields_ = [("dispatched", C.c_uint64), ("cancelled", C.c_uint64), ("digest", C.c_uint64),
                 ("final_ts", C.c_uint64), ("next_uid", C.c_uint32), ("windows", C.c_uint32),
                 ("ttl_drops", C.c_uint64), ("no_route_drops", C.c_uint64), ("max_window", C.c_uint64),
-                ("unreach_drops", C.c_uint64)]
+                ("unreach_drops", C.c_uint64), ("refits", C.c_uint64)]
 
 
 DEV_COUNTERS_DTYPE = np.dtype([("enq_packets", "<u4"), ("enq_bytes", "<u4"), ("drop_packets", "<u4"),
