@@ -188,6 +188,32 @@ int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_every, double 
  * lib/libnsgpu_prof.so build (-DNSGPU_PHASE_PROF) records them, the product library returns ESTATE. */
 int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset);
 
+/* ---------------- partitioned (multi-GPU) point-to-point runs ----------------
+ * Replaces src/mpi's DistributedSimulatorImpl (distributed-simulator-impl.cc:146-326: LBTS by
+ * MPI_Allgather of LbtsMessage) and MpiInterface::SendPacket / ReceiveMessages
+ * (mpi-interface.cc:414-506: remote packets) for the GPU-resident p2p subset: one process per GPU,
+ * node n simulated by rank node_owner[n] (Node::GetSystemId, node.cc:76-108).  Per window an RCCL
+ * allgather of window bounds (X0), an allgather of window summaries — the LBTS and the global
+ * dispatch order (X1) — and an all-to-all of remote events (X2), captured into the window graph.
+ * The run reproduces the SEQUENTIAL DefaultSimulatorImpl pop order and uids (not the per-rank uids
+ * of DistributedSimulatorImpl).  dispatched / final_ts / next_uid / windows in nsgpu_p2p_results are
+ * run-global; digest and drop counters are this rank's share; counters are valid for owned nodes,
+ * and the log holds the entries this rank dispatched (zeros elsewhere). */
+typedef struct nsgpu_comm nsgpu_comm;
+int nsgpu_comm_unique_id(uint8_t *id);   /* 128 bytes, rank 0; share it with every rank */
+int nsgpu_comm_init(const uint8_t *id, int nranks, int rank, nsgpu_comm **out);  /* on the rank's device */
+int nsgpu_comm_destroy(nsgpu_comm *c);
+/* comm == NULL: a loopback member (all partitions in one process on one device, see below). */
+int nsgpu_p2p_create_dist(const nsgpu_p2p_scenario *sc, const uint32_t *node_owner, int rank, int nranks,
+                          nsgpu_comm *comm, uint64_t pool_cap, uint64_t log_cap, nsgpu_p2p **out);
+/* Loopback group: partitions 0..n-1 (created with comm == NULL) run on this device with the
+ * collectives replaced by device-to-device copies — the partitioned algorithm on one GPU. */
+typedef struct nsgpu_p2p_group nsgpu_p2p_group;
+int nsgpu_p2p_group_create(nsgpu_p2p **members, int n, nsgpu_p2p_group **out);
+int nsgpu_p2p_group_reset(nsgpu_p2p_group *g, void *stream);
+int nsgpu_p2p_group_run(nsgpu_p2p_group *g, void *stream);
+int nsgpu_p2p_group_destroy(nsgpu_p2p_group *g);
+
 #ifdef __cplusplus
 }
 #endif

@@ -87,6 +87,8 @@ struct Ctl {
   uint64_t pK0, ptmin, pinline_lim;    // the last scanned window, appended by the next k_pa
   uint32_t uid, cur, W, nxtP, overflow, prep, done, stop_seen;
   uint32_t puid0, pW, pvalid, pinl;
+  uint32_t collected, pad1;  // partitioned: k_refit_d already moved the window slots to the pool
+  uint64_t pcol;             // (and the pool count after that)
 };
 
 // Device-resident model + engine state (all pointers are HBM).  Passed to the kernels by value.
@@ -134,6 +136,13 @@ struct P2PDev {
   uint32_t *wrank;  // rank accumulators of the current window (0 between windows)
   // per-node slot tables of the current window (node_cnt is 0 between windows)
   uint32_t *node_cnt, *node_slot;
+  // partitioned run (dist != 0): this engine owns the nodes n with owner[n] == rank
+  uint32_t dist, rank, nranks, pad_d;
+  const uint32_t *owner;
+  uint64_t *x0_send, *x0_recv;  // X0: 2 u64 per rank
+  uint8_t *x1_send, *x1_recv;   // X1: X1B bytes per rank
+  uint8_t *x2_send, *x2_recv;   // X2: X2B bytes per peer
+  uint32_t *gacc;               // 6 x WCAP accumulators of k_gtile
   // run control / outputs
   uint32_t n_init;    // initial pending count (pool 0)
   uint32_t uid_init;  // m_uid after setup
@@ -622,6 +631,36 @@ struct Ev {
   Pkt p;
 };
 
+// ---- exchange records of a partitioned run (fixed sizes: they are captured into the window graph) ----
+// X1: a rank's window summary, allgathered.  LbtsMessage's role (distributed-simulator-impl.h:36-84:
+// rx/tx counts, smallest next time) is played by the pending-set reduction `red` and the counts.
+struct X1Hdr {
+  uint32_t W, tc, tinl, pad;  // window events, their children, their inline (DoForwardUp) children
+  uint64_t nxtP, lastkey;     // pending events left out of the window; largest window key
+  Red red;                    // reduction of this rank's pending set after the window (next LBTS)
+  uint64_t pad2[8];
+};
+struct X1Ent {  // one window event: key and child counts (children | inline children << 16)
+  uint64_t key;
+  uint32_t cnt, pad;
+};
+constexpr size_t X1B = sizeof(X1Hdr) + sizeof(X1Ent) * WCAP;
+// X2: remote events for one peer (children whose node another rank owns), all-to-all; the record is
+// the pending event itself, uid included (mpi-interface.cc:414-506 sends {rx ns, node, dev, packet}).
+struct X2Hdr {
+  uint32_t n, pad[3];
+};
+constexpr int CAPX = 1024;  // remote events per peer per window
+constexpr size_t X2B = sizeof(X2Hdr) + sizeof(Ev) * CAPX;
+constexpr size_t X0B = 16;  // X0: one rank's largest fitting window bound (+ pad)
+constexpr int MAXR = 64;    // ranks
+__device__ __forceinline__ X1Hdr *x1hdr(uint8_t *b, uint32_t q) { return (X1Hdr *)(b + (size_t)q * X1B); }
+__device__ __forceinline__ X1Ent *x1ent(uint8_t *b, uint32_t q) {
+  return (X1Ent *)(b + (size_t)q * X1B + sizeof(X1Hdr));
+}
+__device__ __forceinline__ X2Hdr *x2hdr(uint8_t *b, uint32_t q) { return (X2Hdr *)(b + (size_t)q * X2B); }
+__device__ __forceinline__ Ev *x2rec(uint8_t *b, uint32_t q) { return (Ev *)(b + (size_t)q * X2B + sizeof(X2Hdr)); }
+
 // Writes window slot `slot` (and the node's slot table).
 __device__ __forceinline__ void put_window(const P2PDev &M, uint32_t slot, uint64_t pk, const Ev &e) {
   M.wkey[slot] = pk;
@@ -711,13 +750,15 @@ __global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
   Ctl &C = *M.C;
   const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * TB;
-  const bool slot_role = g < (uint64_t)WCAP;  // wave-uniform
+  const uint64_t RR = M.dist ? (uint64_t)M.nranks * CAPX : 0;  // remote-event threads (partitioned)
+  const bool slot_role = g < (uint64_t)WCAP;                   // (roles are wave-uniform)
+  const bool remote_role = !slot_role && g < WCAP + RR;
   if (C.prep || C.done >= 2) return;  // window already prepared by the refit / run over
   const bool partition = C.done == 0;
   const int cur = C.cur, nxt = cur ^ 1;
   const uint64_t win = C.windows;
   const WinBound b = window_bound(C.red[(win + 1) & 1]);
-  Red &R = C.red[win & 1];
+  Red &R = M.dist ? x1hdr(M.x1_send, 0)->red : C.red[win & 1];
   if (partition && blockIdx.x == 0 && threadIdx.x == 0) publish_bound(C, b);
   const uint64_t P = partition ? C.P : 0;
   const uint32_t pW = C.pvalid ? C.pW : 0;
@@ -785,16 +826,24 @@ __global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
               }
               ii++;
             }
-          } else {
-            valid = partition;
+          } else {  // (partitioned: a child on another rank's node went there through X2)
+            valid = partition && (!M.dist || M.owner[e.ctx] == M.rank);
           }
         }
         if (__ballot(valid)) classify(M, C, b, nxt, valid, e, R, tmn, wnd);
       }
     }
+  } else if (remote_role) {
+    // ---- remote events received through X2 (partitioned): record idx % CAPX from rank idx / CAPX
+    const uint64_t idx = g - WCAP;
+    const uint32_t q = (uint32_t)(idx / CAPX), rec = (uint32_t)(idx % CAPX);
+    const bool valid = partition && rec < x2hdr(M.x2_recv, q)->n;
+    Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+    if (valid) e = x2rec(M.x2_recv, q)[rec];
+    if (__ballot(valid)) classify(M, C, b, nxt, valid, e, R, tmn, wnd);
   } else {
-    // ---- pool entries (grid-stride; the first one was loaded ahead)
-    for (uint64_t i = g - WCAP; i < P; i += stride - WCAP) {  // (the pool role has stride - WCAP threads)
+    // ---- pool entries (grid-stride over the threads of the pool role)
+    for (uint64_t i = g - WCAP - RR; i < P; i += stride - WCAP - RR) {
       const Ev e = load_pool(M, cur, i);
       classify(M, C, b, nxt, true, e, R, tmn, wnd);
     }
@@ -836,9 +885,11 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
   const uint32_t kind0 = M.wkind[i0], a0 = M.wa[i0];
   const Pkt pkt0 = M.wpkt[i0];
   const uint32_t W = C.W;
-  Red &R = C.red[C.windows & 1];
+  Red &R = M.dist ? x1hdr(M.x1_send, 0)->red : C.red[C.windows & 1];
   uint64_t tmn = ~0ull, wnd = ~0ull;
   HStat hs{0, 0, 0, 0, false};
+  uint32_t dtc = 0, dti = 0;  // partitioned: the X1 summary's child totals and largest key
+  uint64_t dlk = 0;
 #ifdef NSGPU_PHASE_PROF
   uint64_t tq[4] = {0, 0, 0, 0};
   const uint64_t tq0 = __builtin_amdgcn_s_memrealtime();
@@ -950,6 +1001,12 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
         for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
       M.nchild[s] = E.n;
       M.ninl[s] = ni;
+      if (M.dist) {
+        x1ent(M.x1_send, 0)[s] = X1Ent{key, E.n | (ni << 16), 0};
+        dtc += E.n;
+        dti += ni;
+        dlk = key > dlk ? key : dlk;
+      }
       pending += ni;
       lastk = key;
     }
@@ -973,6 +1030,17 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
   }
 #endif
   publish_min<HB>(R, tmn, wnd);
+  if (M.dist) {
+    dtc = wave_sum32(dtc);
+    dti = wave_sum32(dti);
+    dlk = wave_max64(dlk);
+    if ((threadIdx.x & 63) == 0) {
+      X1Hdr *h = x1hdr(M.x1_send, 0);
+      if (dtc) atomicAdd(&h->tc, dtc);
+      if (dti) atomicAdd(&h->tinl, dti);
+      if (dlk) atomicMax((unsigned long long *)&h->lastkey, (unsigned long long)dlk);
+    }
+  }
   if (hs.stop) C.stop_seen = 1;
   if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
   if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
@@ -1024,37 +1092,37 @@ __global__ __launch_bounds__(HB) void k_handle_rank(const P2PDev M) {
 #endif
 }
 
-// ---- refit (k_scan's block, only when the window overflowed WCAP) ----
-// Pending set = pool `nxt` (the non-window events and the overflowed candidates) + the WCAP recorded
-// window slots.  The slots go back to the pool, a 256-way radix bisection finds the largest key
-// prefix that fits (a key prefix of a safe window is safe), and the pool is partitioned in place
-// (chunked: every chunk is read before any of its compacted writes land).
-__device__ void refit(const P2PDev &M, Ctl &C) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint64_t s_lo, s_hi;
-  __shared__ uint32_t s_clo, s_nw, s_no;
-  __shared__ uint32_t wsum[2][SCAN_THREADS / 64];
-  const int cur = C.cur, nxt = cur ^ 1;
-  const uint64_t win = C.windows;
-  WinBound b = window_bound(C.red[(win + 1) & 1]);
-  Red &R = C.red[win & 1];
+// ---- refit: the window overflowed WCAP (single-GPU: k_scan's block; partitioned: k_refit_d + k_cut) ----
+// Pending set = pool `nxt` (the non-window events and the overflowed candidates) + the recorded
+// window slots.  The slots go back to the pool (refit_collect), a 256-way radix bisection finds the
+// largest key prefix that fits (refit_bisect; a key prefix of a safe window is safe), and the pool
+// is partitioned in place (refit_partition; chunked: every chunk is read before any of its
+// compacted writes land).  All SCAN_THREADS threads of one workgroup call each step.
+__device__ __forceinline__ uint64_t refit_collect(const P2PDev &M, Ctl &C, const WinBound &b, uint32_t nrec) {
+  const int nxt = C.cur ^ 1;
   const uint64_t P0 = C.nxtP;
-  // 1. the recorded slots -> pool nxt (every one of the WCAP slots was written)
-  for (int s = threadIdx.x; s < WCAP; s += SCAN_THREADS) {
+  for (uint32_t s = threadIdx.x; s < nrec; s += SCAN_THREADS) {
     const uint32_t c = M.wctx[s];
     if (c < M.n_nodes) M.node_cnt[c] = 0;
     const uint64_t pk = M.wkey[s];
     Ev e{b.tmin + (pk >> 32), (uint32_t)pk, c, M.wkind[s], M.wa[s], M.wpkt[s]};
     put_pool(M, nxt, P0 + s, e);
   }
-  const uint64_t P = P0 + WCAP;
+  __syncthreads();
+  return P0 + nrec;
+}
+
+__device__ uint64_t refit_bisect(const P2PDev &M, Ctl &C, const WinBound &b, uint64_t P) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t s_lo, s_hi;
+  __shared__ uint32_t s_clo;
+  const int nxt = C.cur ^ 1;
   if (threadIdx.x == 0) {
     s_lo = 0;        // count(keys <= lo) <= WCAP (the smallest key is >= 4: uids start at 4)
     s_hi = b.bound;  // count(keys <= hi) > WCAP
     s_clo = 0;
   }
   __syncthreads();
-  // 2. bisection
   while (s_hi - s_lo > 1) {
     const uint64_t lo = s_lo, hi = s_hi;
     const uint64_t range = hi - lo;  // keys in (lo, hi]: bucket (k - lo - 1) >> sh in [0, 256)
@@ -1095,7 +1163,17 @@ __device__ void refit(const P2PDev &M, Ctl &C) {
     }
     __syncthreads();
   }
-  b.bound = s_lo;
+  const uint64_t r = s_lo;
+  __syncthreads();
+  return r;
+}
+
+// Partitions pool nxt [0, P) in place with bound b.bound: window -> slots, the rest compacted and
+// folded into R (reset first).  Sets C.W, C.nxtP and publishes the bound.
+__device__ void refit_partition(const P2PDev &M, Ctl &C, const WinBound &b, uint64_t P, Red &R) {
+  __shared__ uint32_t s_nw, s_no;
+  __shared__ uint32_t wsum[2][SCAN_THREADS / 64];
+  const int nxt = C.cur ^ 1;
   if (threadIdx.x == 0) {
     publish_bound(C, b);
     R.tmin = R.wend = R.stopts = ~0ull;
@@ -1103,7 +1181,6 @@ __device__ void refit(const P2PDev &M, Ctl &C) {
     s_no = 0;
   }
   __syncthreads();
-  // 3. in-place partition of pool nxt
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint64_t tmn = ~0ull, wnd = ~0ull;
   for (uint64_t c0 = 0; c0 < P; c0 += SCAN_THREADS) {
@@ -1152,6 +1229,16 @@ __device__ void refit(const P2PDev &M, Ctl &C) {
     C.nxtP = s_no;
     C.refits++;
     C.overflow = 0;
+  }
+}
+
+__device__ void refit(const P2PDev &M, Ctl &C) {
+  const uint64_t win = C.windows;
+  WinBound b = window_bound(C.red[(win + 1) & 1]);
+  const uint64_t P = refit_collect(M, C, b, WCAP);
+  b.bound = refit_bisect(M, C, b, P);
+  refit_partition(M, C, b, P, C.red[win & 1]);
+  if (threadIdx.x == 0) {
     C.prep = 1;    // the next k_pa leaves this window alone
     C.pvalid = 0;  // (the last window was appended by the k_pa that overflowed)
   }
@@ -1305,6 +1392,227 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const P2PDev M) {
   PH_MARK(20);
 }
 
+// ================================ partitioned run (multi-GPU) ================================
+// DistributedSimulatorImpl (src/mpi/model/distributed-simulator-impl.cc:146-326) gives every rank
+// the nodes of its system id and grants it min over ranks of (next ts) + lookahead after an
+// MPI_Allgather of LbtsMessage (:276-313); remote packets travel as {rx ns, node, dev, serialized
+// packet} (mpi-interface.cc:414-506).  Here every rank runs the single-GPU engine's conservative
+// windows over its own nodes, and three fixed-size collectives per window (RCCL, captured into the
+// window graph with the kernels) make the partitioned run reproduce the SEQUENTIAL pop order — uids
+// included, which DistributedSimulatorImpl itself does not (its uids are per rank):
+//   k_pa        as single-GPU, plus the remote events of the last X2;
+//   k_refit_d   this rank's largest fitting window bound (its own bisection if its window overflowed);
+//   X0          allgather of those bounds;
+//   k_cut       every rank cuts its window at the smallest (a key prefix of a safe window is safe);
+//   k_handle_rank  handlers (no rank tiles), writing this rank's X1 summary and window entries;
+//   X1          allgather of the summaries;
+//   k_gtile     per own event, over the merged windows: # smaller keys (global dispatch rank) and the
+//               child / inline-child sums below it and below its same-ts group (uid prefixes);
+//   k_dfin      own events' dispatch info, remote children -> X2 with their final uids, and the run
+//               bookkeeping from the merged summaries: the LBTS (next window's bound) and `done`;
+//   X2          all-to-all of remote events.
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_refit_d(const P2PDev M) {
+  Ctl &C = *M.C;
+  if (C.done) return;
+  const uint64_t win = C.windows;
+  const WinBound b = window_bound(C.red[(win + 1) & 1]);
+  uint64_t lb = b.bound;
+  if (C.overflow) {
+    const uint64_t P = refit_collect(M, C, b, WCAP);
+    lb = refit_bisect(M, C, b, P);
+    if (threadIdx.x == 0) {
+      C.collected = 1;
+      C.pcol = P;
+    }
+  }
+  if (threadIdx.x == 0) {
+    M.x0_send[0] = lb;
+    M.x0_send[1] = 0;
+  }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_cut(const P2PDev M) {
+  Ctl &C = *M.C;
+  if (C.done) return;
+  const uint64_t win = C.windows;
+  WinBound b = window_bound(C.red[(win + 1) & 1]);
+  uint64_t g = ~0ull;
+  for (uint32_t q = 0; q < M.nranks; q++) g = M.x0_recv[2 * q] < g ? M.x0_recv[2 * q] : g;
+  X1Hdr *h = x1hdr(M.x1_send, 0);
+  const bool collected = C.collected != 0;
+  if (C.overflow || g < b.bound) {  // (uniform: every thread reads the same words)
+    const uint32_t nrec = C.W < (uint32_t)WCAP ? C.W : (uint32_t)WCAP;
+    const uint64_t P = collected ? C.pcol : refit_collect(M, C, b, nrec);
+    b.bound = g;
+    refit_partition(M, C, b, P, h->red);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    C.collected = 0;
+    h->W = C.W;
+    h->nxtP = C.nxtP;
+    // the window the next k_pa appends (run-global values: identical on every rank)
+    C.pK0 = C.K;
+    C.puid0 = C.uid;
+    C.ptmin = C.tmin;
+    C.pinline_lim = C.inline_lim;
+    C.pW = C.W;
+    C.pvalid = 1;
+  }
+  for (uint32_t q = threadIdx.x; q < M.nranks; q += SCAN_THREADS) x2hdr(M.x2_send, q)->n = 0;
+}
+
+constexpr int GTB = 1024;  // blocks of k_gtile (grid-stride over tiles)
+__global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
+  Ctl &C = *M.C;
+  if (C.done) return;
+  __shared__ uint64_t tk[RJ];
+  __shared__ uint32_t tc[RJ];
+  __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR];
+  const uint32_t W = C.pW;
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t q = 0; q < M.nranks; q++) {
+      const uint32_t wq = x1hdr(M.x1_recv, q)->W;
+      s_w[q] = wq;
+      s_off[q] = acc;
+      acc += (wq + RJ - 1) / RJ;
+    }
+    s_off[M.nranks] = acc;
+  }
+  __syncthreads();
+  const uint32_t njt = s_off[M.nranks];
+  const uint64_t T = (uint64_t)((W + HB - 1) / HB) * njt;
+  for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {  // (uniform over the block)
+    const uint32_t ti = (uint32_t)(t / njt), tj = (uint32_t)(t % njt);
+    uint32_t q = 0;
+    while (tj >= s_off[q + 1]) q++;
+    const uint32_t j0 = (tj - s_off[q]) * RJ;
+    const uint32_t n = s_w[q] - j0 < (uint32_t)RJ ? s_w[q] - j0 : (uint32_t)RJ;
+    const X1Ent *E = x1ent(M.x1_recv, q) + j0;
+    for (uint32_t k = threadIdx.x; k < n; k += HB) {
+      tk[k] = E[k].key;
+      tc[k] = E[k].cnt;
+    }
+    __syncthreads();
+    const uint32_t i = ti * HB + threadIdx.x;
+    if (i < W) {
+      const uint64_t x = M.wkey[i];
+      const uint64_t lo = x & 0xffffffff00000000ull, hi = lo + (1ull << 32);
+      uint32_t gr = 0, cp = 0, ip = 0, fi = 0, ipf = 0, lp = 0;
+      for (uint32_t y = 0; y < n; y++) {
+        const uint64_t k = tk[y];
+        const uint32_t c = tc[y];
+        const uint32_t nc = c & 0xffffu, ni = c >> 16;
+        const bool lt = k < x, blo = k < lo;
+        gr += lt;
+        cp += lt ? nc : 0u;
+        ip += lt ? ni : 0u;
+        fi += blo;
+        ipf += blo ? ni : 0u;
+        lp += k < hi;
+      }
+      uint32_t *A = M.gacc;
+      if (gr) atomicAdd(&A[i], gr);
+      if (cp) atomicAdd(&A[WCAP + i], cp);
+      if (ip) atomicAdd(&A[2 * WCAP + i], ip);
+      if (fi) atomicAdd(&A[3 * WCAP + i], fi);
+      if (ipf) atomicAdd(&A[4 * WCAP + i], ipf);
+      if (lp) atomicAdd(&A[5 * WCAP + i], lp);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(HB) void k_dfin(const P2PDev M) {
+  Ctl &C = *M.C;
+  if (C.done) return;
+  const uint32_t W = C.pW;
+  uint32_t tinl_g = 0;
+  for (uint32_t q = 0; q < M.nranks; q++) tinl_g += x1hdr(M.x1_recv, q)->tinl;
+  const uint32_t s = blockIdx.x * HB + threadIdx.x;
+  if (s < W) {
+    uint32_t *A = M.gacc;
+    const uint32_t gr = A[s], cp = A[WCAP + s], ip = A[2 * WCAP + s], ipf = A[4 * WCAP + s],
+                   lp = A[5 * WCAP + s];
+    for (int k = 0; k < 6; k++) A[k * WCAP + s] = 0;
+    // as k_scan: (dispatch rank rel. K0, rank of the first inline child, child prefix, inline prefix)
+    M.sinfo[s] = make_uint4(gr + (tinl_g ? ipf : 0), lp + ip, cp, ip);
+    M.pwkey[s] = M.wkey[s];
+    M.pwctx[s] = M.wctx[s];
+    const uint32_t ncr = M.nchild[s], uid0 = C.puid0;
+    for (uint32_t j = 0; j < ncr; j++) {
+      const uint32_t sl = s * M.maxc + j;
+      const uint32_t kw = M.ch_kind[sl];
+      if ((kw & 0xffu) == K_FWD_UP) continue;
+      const uint32_t ctx = M.ch_ctx[sl];
+      const uint32_t q = M.owner[ctx];
+      if (q == M.rank) continue;
+      const uint32_t pos = atomicAdd(&x2hdr(M.x2_send, q)->n, 1u);
+      if (pos < (uint32_t)CAPX)
+        x2rec(M.x2_send, q)[pos] = Ev{M.ch_ts[sl], uid0 + cp + j, ctx, kw, M.ch_a[sl], M.ch_pkt[sl]};
+      else
+        atomicOr(M.error, 16u);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t Wg = 0, tcg = 0;
+    uint64_t nPg = 0, lk = 0;
+    Red rg{~0ull, ~0ull, ~0ull, 0, 0};
+    for (uint32_t q = 0; q < M.nranks; q++) {
+      const X1Hdr *h = x1hdr(M.x1_recv, q);
+      Wg += h->W;
+      tcg += h->tc;
+      nPg += h->nxtP + h->tc - h->tinl;
+      if (h->W && h->lastkey > lk) lk = h->lastkey;
+      rg.tmin = h->red.tmin < rg.tmin ? h->red.tmin : rg.tmin;
+      rg.wend = h->red.wend < rg.wend ? h->red.wend : rg.wend;
+      if (h->red.stopts < rg.stopts) {
+        rg.stopts = h->red.stopts;
+        rg.stopuid = h->red.stopuid;
+      }
+    }
+    const uint64_t win = C.windows;
+    C.K += Wg + tinl_g;
+    C.uid += tcg;
+    if (Wg) C.last_ts = C.tmin + (lk >> 32);
+    C.red[win & 1] = rg;  // bounds the next window (k_pa reads red[(win + 2) & 1])
+    C.windows = win + 1;
+    if (Wg > C.max_window) C.max_window = Wg;
+    C.P = C.nxtP;
+    C.cur ^= 1;
+    C.W = 0;
+    C.nxtP = 0;
+    // the window that held Simulator::Stop ends the run (every rank knows it from the bound)
+    bool done = C.inline_lim != ~0ull || nPg == 0;
+    if (C.windows >= C.max_windows && !done) {
+      atomicOr(M.error, 4u);
+      done = true;
+    }
+    if (done) C.done = 1;
+    X1Hdr *hs = x1hdr(M.x1_send, 0);
+    hs->W = hs->tc = hs->tinl = 0;
+    hs->nxtP = 0;
+    hs->lastkey = 0;
+    hs->red.tmin = hs->red.wend = hs->red.stopts = ~0ull;
+    hs->red.stopuid = 0;
+  }
+}
+
+// Loopback transport (nsgpu_p2p_group_*: every partition on one device): one block per copy.
+struct CopyDesc {
+  const uint8_t *src;
+  uint8_t *dst;
+  uint64_t bytes;  // multiple of 16
+};
+__global__ __launch_bounds__(256) void k_copies(const CopyDesc *__restrict__ d) {
+  const CopyDesc c = d[blockIdx.x];
+  const uint4 *src = (const uint4 *)c.src;
+  uint4 *dst = (uint4 *)c.dst;
+  for (uint64_t i = threadIdx.x; i < c.bytes / 16; i += 256) dst[i] = src[i];
+}
+
 }  // namespace nsgpu
 // ====================================================================================================
 // Host side: scenario upload, setup-time event list, launch, results.
@@ -1313,8 +1621,53 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const P2PDev M) {
 #include <algorithm>
 #include <string.h>
 #include <stdlib.h>
+#include <rccl/rccl.h>
 
 using namespace nsgpu;
+
+// ---- RCCL communicator of a partitioned run (one rank per GPU process) ----
+struct nsgpu_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0;
+};
+
+#define NCCL_TRY(x)                                                                            \
+  do {                                                                                         \
+    ncclResult_t r_ = (x);                                                                     \
+    if (r_ != ncclSuccess) return set_error(NSGPU_EHIP, "%s: %s", #x, ncclGetErrorString(r_)); \
+  } while (0)
+
+extern "C" int nsgpu_comm_unique_id(uint8_t *id) {
+  if (!id) return set_error(NSGPU_EINVAL, "nsgpu_comm_unique_id: null");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_comm_init(const uint8_t *id, int nranks, int rank, nsgpu_comm **out) {
+  if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks)
+    return set_error(NSGPU_EINVAL, "nsgpu_comm_init: bad arguments");
+  ncclUniqueId u;
+  memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+  nsgpu_comm *c = new nsgpu_comm();
+  const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return set_error(NSGPU_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  c->nranks = nranks;
+  c->rank = rank;
+  *out = c;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_comm_destroy(nsgpu_comm *c) {
+  if (!c) return NSGPU_OK;
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  delete c;
+  return NSGPU_OK;
+}
 
 struct nsgpu_p2p {
   P2PDev M;
@@ -1332,6 +1685,9 @@ struct nsgpu_p2p {
   uint64_t *init_ts = nullptr;
   uint32_t *init_uid = nullptr, *init_ctx = nullptr, *init_kind = nullptr, *init_a = nullptr;
   uint32_t n_apps = 0;
+  // partitioned run
+  nsgpu_comm *comm = nullptr;  // RCCL transport (null: a loopback group member)
+  X1Hdr x1h0{};                // empty X1 summary (reset template)
 };
 
 namespace {
@@ -1378,8 +1734,10 @@ extern "C" int nsgpu_p2p_destroy(nsgpu_p2p *h) {
   return NSGPU_OK;
 }
 
-extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap, uint64_t log_cap,
-                                nsgpu_p2p **out) {
+// owner == null: the whole scenario on this device; otherwise the partition `rank` of `nranks`
+// (node n belongs to rank owner[n]).
+static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, int rank, int nranks,
+                         nsgpu_comm *comm, uint64_t pool_cap, uint64_t log_cap, nsgpu_p2p **out) {
   if (!sc || !out) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: null");
   *out = nullptr;
   const uint32_t N = sc->n_nodes, D = sc->n_devices, A = sc->n_apps;
@@ -1393,6 +1751,13 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
     if (sc->dev_delay_ns[d] < 0 || sc->dev_ifg_ns[d] < 0)
       return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: device %u: negative delay", d);
     qcap = std::max(qcap, sc->dev_qmax[d]);
+  }
+  if (owner) {
+    if (nranks < 1 || nranks > MAXR || rank < 0 || rank >= nranks ||
+        (uint64_t)nranks * CAPX + WCAP >= (uint64_t)GRID_POOL * TB)
+      return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: rank %d of %d (at most %d ranks)", rank, nranks, MAXR);
+    for (uint32_t n = 0; n < N; n++)
+      if (owner[n] >= (uint32_t)nranks) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: node %u: owner %u", n, owner[n]);
   }
   std::vector<uint32_t> napps(N + 1, 0);
   std::vector<int32_t> sink(N, -1);
@@ -1519,6 +1884,26 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
     }
     uid++;
   }
+  // reduction of the whole initial pending set: window 0 is bounded by red[1] on every rank
+  Red red0{~0ull, ~0ull, ~0ull, 0, 0};
+  for (size_t i = 0; i < its.size(); i++) {
+    red0.tmin = std::min<uint64_t>(red0.tmin, its[i]);
+    red0.wend = std::min<uint64_t>(red0.wend, its[i] + (uint64_t)M.lookahead[ikind[i] & 0xffu]);
+    if ((ikind[i] & 0xffu) == K_STOP) {
+      red0.stopts = its[i];
+      red0.stopuid = iuid[i];
+    }
+  }
+  if (owner) {  // this rank's initial events (Simulator::Stop: rank 0)
+    size_t k = 0;
+    for (size_t i = 0; i < its.size(); i++) {
+      const bool mine = ictx[i] == NOCTX ? rank == 0 : owner[ictx[i]] == (uint32_t)rank;
+      if (!mine) continue;
+      its[k] = its[i], iuid[k] = iuid[i], ictx[k] = ictx[i], ikind[k] = ikind[i], ia[k] = ia[i];
+      k++;
+    }
+    its.resize(k), iuid.resize(k), ictx.resize(k), ikind.resize(k), ia.resize(k);
+  }
   M.n_init = (uint32_t)its.size();
   M.uid_init = uid;
   M.pool_cap = pool_cap ? pool_cap : std::max<uint64_t>(4ull * M.n_init + 65536, 1ull << 20);
@@ -1543,6 +1928,22 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   TRY(dalloc(h, &M.sinfo, WCAP));
   for (uint32_t **p : {&M.wctx, &M.wkind, &M.wa, &M.widx, &M.nchild, &M.ninl, &M.pwctx}) TRY(dalloc(h, p, WCAP));
   TRY(dalloc(h, &M.wrank, WCAP));
+  if (owner) {
+    M.dist = 1;
+    M.rank = (uint32_t)rank;
+    M.nranks = (uint32_t)nranks;
+    TRY(dupload(h, &M.owner, owner, N));
+    TRY(dalloc(h, &M.x0_send, 2));
+    TRY(dalloc(h, &M.x0_recv, 2 * (size_t)nranks));
+    TRY(dalloc(h, &M.x1_send, X1B));
+    TRY(dalloc(h, &M.x1_recv, X1B * nranks));
+    TRY(dalloc(h, &M.x2_send, X2B * nranks));
+    TRY(dalloc(h, &M.x2_recv, X2B * nranks));
+    TRY(dalloc(h, &M.gacc, 6 * (size_t)WCAP));
+    h->comm = comm;
+    memset(&h->x1h0, 0, sizeof(X1Hdr));
+    h->x1h0.red.tmin = h->x1h0.red.wend = h->x1h0.red.stopts = ~0ull;
+  }
   TRY(dalloc(h, &M.C, 1));
   TRY(dalloc(h, &M.error, 4));
   M.log_cap = log_cap;
@@ -1568,20 +1969,11 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   C0.uid = uid;
   // reduction of the initial pool: window 0 is bounded by red[1] (k_pa / k_handle_rank fold later
   // pending sets in for the next windows)
-  for (int b = 0; b < 2; b++) {
-    C0.red[b].tmin = C0.red[b].wend = C0.red[b].stopts = ~0ull;
-    C0.red[b].stopuid = 0;
-  }
-  for (size_t i = 0; i < its.size(); i++) {
-    C0.red[1].tmin = std::min<uint64_t>(C0.red[1].tmin, its[i]);
-    C0.red[1].wend = std::min<uint64_t>(C0.red[1].wend, its[i] + (uint64_t)M.lookahead[ikind[i] & 0xffu]);
-    if ((ikind[i] & 0xffu) == K_STOP) {
-      C0.red[1].stopts = its[i];
-      C0.red[1].stopuid = iuid[i];
-    }
-  }
+  C0.red[0].tmin = C0.red[0].wend = C0.red[0].stopts = ~0ull;
+  C0.red[0].stopuid = 0;
+  C0.red[1] = red0;
   C0.max_windows = h->max_windows;
-  C0.done = M.n_init == 0 ? 2 : 0;
+  C0.done = red0.tmin == ~0ull ? 2 : 0;  // (no event anywhere)
   if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
     h->s = nullptr;
     nsgpu_p2p_destroy(h);
@@ -1606,6 +1998,20 @@ extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap,
   }
   *out = h;
   return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap, uint64_t log_cap,
+                                nsgpu_p2p **out) {
+  return create_engine(sc, nullptr, 0, 1, nullptr, pool_cap, log_cap, out);
+}
+
+extern "C" int nsgpu_p2p_create_dist(const nsgpu_p2p_scenario *sc, const uint32_t *node_owner, int rank,
+                                     int nranks, nsgpu_comm *comm, uint64_t pool_cap, uint64_t log_cap,
+                                     nsgpu_p2p **out) {
+  if (!node_owner) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: null owner map");
+  if (comm && (comm->nranks != nranks || comm->rank != rank))
+    return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: communicator is rank %d of %d", comm->rank, comm->nranks);
+  return create_engine(sc, node_owner, rank, nranks, comm, pool_cap, log_cap, out);
 }
 
 // Restores the initial (post-setup) state on the device, asynchronously.
@@ -1634,6 +2040,22 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.node_cnt, 0, M.n_nodes * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.wrank, 0, WCAP * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
+  if (M.dist) {
+    const size_t R = M.nranks;
+    NSGPU_HIP(hipMemsetAsync(M.x0_send, 0, X0B, s));
+    NSGPU_HIP(hipMemsetAsync(M.x0_recv, 0, X0B * R, s));
+    NSGPU_HIP(hipMemsetAsync(M.x1_send, 0, X1B, s));
+    NSGPU_HIP(hipMemcpyAsync(M.x1_send, &h->x1h0, sizeof(X1Hdr), hipMemcpyHostToDevice, s));
+    NSGPU_HIP(hipMemsetAsync(M.x1_recv, 0, X1B * R, s));
+    NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, X2B * R, s));
+    NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, X2B * R, s));
+    NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 6 * WCAP * sizeof(uint32_t), s));
+    if (M.log_cap) {  // every rank writes only the entries it dispatches: the union is the log
+      NSGPU_HIP(hipMemsetAsync(M.log_ts, 0, M.log_cap * 8, s));
+      NSGPU_HIP(hipMemsetAsync(M.log_uid, 0, M.log_cap * 4, s));
+      NSGPU_HIP(hipMemsetAsync(M.log_ctx, 0, M.log_cap * 4, s));
+    }
+  }
   NSGPU_HIP(hipMemcpyAsync(M.C, &h->C0, sizeof(Ctl), hipMemcpyHostToDevice, s));
   return NSGPU_OK;
 }
@@ -1657,14 +2079,39 @@ void launch_windows(nsgpu_p2p *h, hipStream_t s) {
 }
 }  // namespace
 
+// The partitioned window (one RCCL member): 6 kernels and 3 collectives, on stream s.
+static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s) {
+  ncclComm_t comm = h->comm->comm;
+  const P2PDev &M = h->M;
+  for (int w = 0; w < NWIN; w++) {
+    hipLaunchKernelGGL(k_pa, dim3(GRID_POOL), dim3(TB), 0, s, M);
+    hipLaunchKernelGGL(k_refit_d, dim3(1), dim3(SCAN_THREADS), 0, s, M);
+    NCCL_TRY(ncclAllGather(M.x0_send, M.x0_recv, X0B, ncclUint8, comm, s));
+    hipLaunchKernelGGL(k_cut, dim3(1), dim3(SCAN_THREADS), 0, s, M);
+    hipLaunchKernelGGL(k_handle_rank, dim3(NHB), dim3(HB), 0, s, M);
+    NCCL_TRY(ncclAllGather(M.x1_send, M.x1_recv, X1B, ncclUint8, comm, s));
+    hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k_dfin, dim3(NHB), dim3(HB), 0, s, M);
+    NCCL_TRY(ncclAllToAll(M.x2_send, M.x2_recv, X2B, ncclUint8, comm, s));
+  }
+  return NSGPU_OK;
+}
+
 static int build_graph(nsgpu_p2p *h) {
   // NWIN windows of the pipeline; kernels read every run-dependent value from the device (Ctl), so
   // one instantiated graph serves every run of this engine
   hipGraph_t g = nullptr;
-  NSGPU_HIP(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
-  launch_windows(h, h->s);
+  NSGPU_HIP(hipStreamBeginCapture(h->s, h->M.dist ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal));
+  int rc = NSGPU_OK;
+  if (h->M.dist) rc = launch_windows_dist(h, h->s);
+  else launch_windows(h, h->s);
   hipError_t e = hipStreamEndCapture(h->s, &g);
-  if (e != hipSuccess) return set_error(NSGPU_EHIP, "nsgpu_p2p: graph capture: %s", hipGetErrorString(e));
+  if (rc != NSGPU_OK || e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (rc != NSGPU_OK) return rc;
+    return set_error(NSGPU_EHIP, "nsgpu_p2p: graph capture: %s", hipGetErrorString(e));
+  }
   e = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   if (e != hipSuccess) {
@@ -1674,13 +2121,16 @@ static int build_graph(nsgpu_p2p *h) {
   return NSGPU_OK;
 }
 
-// Runs the simulation to completion (blocking): replays of NWIN windows on the engine stream (one
-// hipGraph launch each, or the same kernels launched one by one in eager mode), ordered after the
-// work already queued on `stream`; work queued on `stream` later runs after it.
 extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_run: null");
+  if (h->M.dist && !h->comm)
+    return set_error(NSGPU_ESTATE, "nsgpu_p2p_run: a loopback partition runs with its group (nsgpu_p2p_group_run)");
   if (!h->eager && !h->gexec) {
     int rc = build_graph(h);
+    if (rc && h->M.dist) {  // RCCL collectives that refuse stream capture: launch them eagerly
+      h->eager = true;
+      rc = NSGPU_OK;
+    }
     if (rc) return rc;
   }
   hipStream_t cs = (hipStream_t)stream;
@@ -1691,7 +2141,12 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   // two replays in flight: replay i+1 is queued before the done flag of replay i is examined
   for (uint64_t it = 0;; it++) {
     if (h->eager) {
-      launch_windows(h, h->s);
+      if (h->M.dist) {
+        const int rc = launch_windows_dist(h, h->s);
+        if (rc) return rc;
+      } else {
+        launch_windows(h, h->s);
+      }
       NSGPU_HIP(hipGetLastError());
     } else {
       NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
@@ -1748,6 +2203,7 @@ extern "C" const char *nsgpu_p2p_kernel_name(int k) { return k >= 0 && k < NKERN
 extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_every, double *kernel_ms,
                                  uint64_t *launches) {
   if (!h || !kernel_ms || !launches) return set_error(NSGPU_EINVAL, "nsgpu_p2p_profile: null");
+  if (h->M.dist) return set_error(NSGPU_ESTATE, "nsgpu_p2p_profile: single-device engines only");
   if (sample_every == 0) sample_every = 1;
   for (int k = 0; k < NKERN; k++) kernel_ms[k] = 0.0, launches[k] = 0;
   // up to NS sampled windows; the events are read after the run (no synchronisation in between
@@ -1850,5 +2306,129 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
   if (error) *error = err;
   if (err) return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, "
                                           "4 = window limit, 8 = window cut)", err);
+  return NSGPU_OK;
+}
+
+// ====================================================================================================
+// Loopback group: every partition of one scenario on this device, the collectives replaced by
+// device-to-device copies (k_copies) on one stream — the partitioned algorithm's parity harness on
+// a single GPU.  Members are nsgpu_p2p_create_dist engines with comm == NULL, rank i at index i.
+// ====================================================================================================
+struct nsgpu_p2p_group {
+  std::vector<nsgpu_p2p *> m;
+  CopyDesc *d_x[3] = {nullptr, nullptr, nullptr};  // X0, X1, X2: n x n copies each
+  hipStream_t s = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  uint32_t *done_host = nullptr;
+};
+
+static void launch_windows_group(nsgpu_p2p_group *g, hipStream_t s) {
+  const unsigned n = (unsigned)g->m.size();
+  for (int w = 0; w < NWIN; w++) {
+    for (auto *h : g->m) hipLaunchKernelGGL(k_pa, dim3(GRID_POOL), dim3(TB), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_refit_d, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
+    hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[0]);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_cut, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_handle_rank, dim3(NHB), dim3(HB), 0, s, h->M);
+    hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[1]);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_dfin, dim3(NHB), dim3(HB), 0, s, h->M);
+    hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[2]);
+  }
+}
+
+extern "C" int nsgpu_p2p_group_destroy(nsgpu_p2p_group *g) {
+  if (!g) return NSGPU_OK;
+  if (g->s) (void)hipStreamSynchronize(g->s);
+  if (g->gexec) (void)hipGraphExecDestroy(g->gexec);
+  for (hipEvent_t e : {g->ev[0], g->ev[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (g->done_host) (void)hipHostFree(g->done_host);
+  for (CopyDesc *d : g->d_x)
+    if (d) (void)hipFree(d);
+  if (g->s) (void)hipStreamDestroy(g->s);
+  delete g;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_group_create(nsgpu_p2p **members, int n, nsgpu_p2p_group **out) {
+  if (!members || !out || n < 1) return set_error(NSGPU_EINVAL, "nsgpu_p2p_group_create: bad arguments");
+  *out = nullptr;
+  for (int i = 0; i < n; i++) {
+    const nsgpu_p2p *h = members[i];
+    if (!h || !h->M.dist || h->comm || h->M.nranks != (uint32_t)n || h->M.rank != (uint32_t)i)
+      return set_error(NSGPU_EINVAL, "nsgpu_p2p_group_create: member %d is not loopback partition %d of %d", i, i, n);
+  }
+  nsgpu_p2p_group *g = new nsgpu_p2p_group();
+  g->m.assign(members, members + n);
+  std::vector<CopyDesc> x[3];
+  for (int r = 0; r < n; r++)
+    for (int q = 0; q < n; q++) {
+      const P2PDev &R = members[r]->M, &Q = members[q]->M;
+      x[0].push_back(CopyDesc{(const uint8_t *)Q.x0_send, (uint8_t *)(R.x0_recv + 2 * q), X0B});
+      x[1].push_back(CopyDesc{Q.x1_send, R.x1_recv + (size_t)q * X1B, X1B});
+      x[2].push_back(CopyDesc{Q.x2_send + (size_t)r * X2B, R.x2_recv + (size_t)q * X2B, X2B});
+    }
+  for (int k = 0; k < 3; k++) {
+    if (hipMalloc(&g->d_x[k], x[k].size() * sizeof(CopyDesc)) != hipSuccess ||
+        hipMemcpy(g->d_x[k], x[k].data(), x[k].size() * sizeof(CopyDesc), hipMemcpyHostToDevice) != hipSuccess) {
+      nsgpu_p2p_group_destroy(g);
+      return set_error(NSGPU_ENOMEM, "nsgpu_p2p_group_create: copy descriptors");
+    }
+  }
+  if (hipStreamCreateWithFlags(&g->s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev[1], hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc((void **)&g->done_host, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+    nsgpu_p2p_group_destroy(g);
+    return set_error(NSGPU_EHIP, "nsgpu_p2p_group_create: stream / events");
+  }
+  *out = g;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_group_reset(nsgpu_p2p_group *g, void *stream) {
+  if (!g) return set_error(NSGPU_EINVAL, "nsgpu_p2p_group_reset: null");
+  for (nsgpu_p2p *h : g->m) {
+    const int rc = nsgpu_p2p_reset(h, stream);
+    if (rc) return rc;
+  }
+  return NSGPU_OK;
+}
+
+// Runs every partition to the end of the simulation (blocking), like nsgpu_p2p_run.
+extern "C" int nsgpu_p2p_group_run(nsgpu_p2p_group *g, void *stream) {
+  if (!g) return set_error(NSGPU_EINVAL, "nsgpu_p2p_group_run: null");
+  if (!g->gexec) {
+    hipGraph_t gr = nullptr;
+    NSGPU_HIP(hipStreamBeginCapture(g->s, hipStreamCaptureModeThreadLocal));
+    launch_windows_group(g, g->s);
+    hipError_t e = hipStreamEndCapture(g->s, &gr);
+    if (e != hipSuccess) return set_error(NSGPU_EHIP, "nsgpu_p2p_group: graph capture: %s", hipGetErrorString(e));
+    e = hipGraphInstantiate(&g->gexec, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    if (e != hipSuccess) {
+      g->gexec = nullptr;
+      return set_error(NSGPU_EHIP, "nsgpu_p2p_group: graph instantiate: %s", hipGetErrorString(e));
+    }
+  }
+  hipStream_t cs = (hipStream_t)stream;
+  NSGPU_HIP(hipEventRecord(g->ev[0], cs));
+  NSGPU_HIP(hipStreamWaitEvent(g->s, g->ev[0], 0));
+  g->done_host[0] = g->done_host[1] = 0;
+  const uint32_t *done = &g->m[0]->M.C->done;  // (run-global: the same on every partition)
+  for (uint64_t it = 0;; it++) {
+    NSGPU_HIP(hipGraphLaunch(g->gexec, g->s));
+    NSGPU_HIP(hipMemcpyAsync(&g->done_host[it & 1], done, sizeof(uint32_t), hipMemcpyDeviceToHost, g->s));
+    NSGPU_HIP(hipEventRecord(g->ev[it & 1], g->s));
+    if (it > 0) {
+      NSGPU_HIP(hipEventSynchronize(g->ev[(it - 1) & 1]));
+      if (g->done_host[(it - 1) & 1] >= 2) break;
+    }
+  }
+  NSGPU_HIP(hipEventRecord(g->ev[0], g->s));
+  NSGPU_HIP(hipEventSynchronize(g->ev[0]));
+  NSGPU_HIP(hipStreamWaitEvent(cs, g->ev[0], 0));
   return NSGPU_OK;
 }

@@ -102,6 +102,14 @@ SIGNATURES = {
     "nsgpu_p2p_kernel_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nsgpu_p2p_kernel_name": (C.c_char_p, [C.c_int]),
     "nsgpu_p2p_profile": (C.c_int, [_vp, _vp, _u32, _vp, _vp]),
+    "nsgpu_comm_unique_id": (C.c_int, [_vp]),
+    "nsgpu_comm_init": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "nsgpu_comm_destroy": (C.c_int, [_vp]),
+    "nsgpu_p2p_create_dist": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _vp, _u64, _u64, C.POINTER(C.c_void_p)]),
+    "nsgpu_p2p_group_create": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p)]),
+    "nsgpu_p2p_group_reset": (C.c_int, [_vp, _vp]),
+    "nsgpu_p2p_group_run": (C.c_int, [_vp, _vp]),
+    "nsgpu_p2p_group_destroy": (C.c_int, [_vp]),
     "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
 }
 

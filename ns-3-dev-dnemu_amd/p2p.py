@@ -189,19 +189,18 @@ def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="column
     routes are XY (row first, then column) static next hops."""
     sc = Scenario(0)
     nid = lambda y, x: y * cols + x  # noqa: E731
-    row_dev = {}
-    col_dev = {}
+    n = rows * cols
+    # the device of each node towards its four grid neighbours (XY routing's next hops)
+    right, left, down, up = (np.full(n, NO_ROUTE, np.uint32) for _ in range(4))
     for y in range(rows):
         for x in range(cols):
             sc.add_node()  # rowNodes.Create (1)
             if x > 0:
                 da, db = sc.link(nid(y, x - 1), nid(y, x), bps, delay_ns, qmax)
-                row_dev[(nid(y, x - 1), nid(y, x))] = da
-                row_dev[(nid(y, x), nid(y, x - 1))] = db
+                right[nid(y, x - 1)], left[nid(y, x)] = da, db
             if y > 0:
                 da, db = sc.link(nid(y - 1, x), nid(y, x), bps, delay_ns, qmax)
-                col_dev[(nid(y - 1, x), nid(y, x))] = da
-                col_dev[(nid(y, x), nid(y - 1, x))] = db
+                down[nid(y - 1, x)], up[nid(y, x)] = da, db
     sc.install_stack()  # PointToPointGridHelper::InstallStack (point-to-point-grid.cc:79-89)
     fl = []
     if flows == "columns":
@@ -217,24 +216,17 @@ def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="column
     for s_, d in fl:
         sc.add_onoff(s_, d, start_ns, stop_ns, rate_bps=rate_bps, size=size, on_s=on_s, off_s=off_s, ttl=ttl)
     sc.stop(sim_stop_ns)
-    # XY routes towards each destination
+    # XY routes towards each destination: along the row first, then along the column
     dsts = sorted({d for _s, d in fl})
     sc.dst_slot = {d: i for i, d in enumerate(dsts)}
     sc.n_dst = max(1, len(dsts))
-    R = np.full((sc.n_nodes, sc.n_dst), NO_ROUTE, dtype=np.uint32)
-    ys, xs = np.divmod(np.arange(sc.n_nodes), cols)
+    R = np.full((n, sc.n_dst), NO_ROUTE, dtype=np.uint32)
+    ys, xs = np.divmod(np.arange(n), cols)
     for d, slot in sc.dst_slot.items():
         yd, xd = divmod(d, cols)
-        for n in range(sc.n_nodes):
-            y, x = ys[n], xs[n]
-            if n == d:
-                continue
-            if x != xd:
-                nxt = nid(y, x + (1 if xd > x else -1))
-                R[n, slot] = row_dev[(n, nxt)]
-            else:
-                nxt = nid(y + (1 if yd > y else -1), x)
-                R[n, slot] = col_dev[(n, nxt)]
+        col = np.where(xs != xd, np.where(xd > xs, right, left), np.where(yd > ys, down, up))
+        col[d] = NO_ROUTE
+        R[:, slot] = col
     sc.route = R
     return sc
 
@@ -333,5 +325,134 @@ class Engine:
     def __del__(self):
         try:
             nsgpu.lib().nsgpu_p2p_destroy(self.h)
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- partitioned runs
+STAT_FIELDS = [f for f, _ in P2PStats._fields_]
+RUN_GLOBAL_FIELDS = ("dispatched", "final_ts", "next_uid", "windows", "max_window")
+
+
+def stats_to_dict(st):
+    return {f: int(getattr(st, f)) for f in STAT_FIELDS}
+
+
+def stats_from_dict(d):
+    st = P2PStats()
+    for k, v in d.items():
+        setattr(st, k, v)
+    return st
+
+
+def owner_blocks(n_nodes, nranks):
+    """Node -> rank map of contiguous, balanced node-id blocks, the way the reference's distributed
+    examples give nodes their system id (Node (sid), node.cc:76-108; src/mpi/examples): a grid built
+    row by row splits into row bands."""
+    if nranks < 1:
+        raise ValueError("nranks >= 1")
+    return (np.arange(n_nodes, dtype=np.int64) * nranks // max(n_nodes, 1)).astype(np.uint32)
+
+
+def merge_results(per_rank, owner, s):
+    """One result from the per-rank results (stats, devc, appc, log) of a partitioned run: the
+    run-global fields (dispatch count, final time, next uid, windows) from rank 0, per-rank tallies
+    summed (the digest modulo 2^64), every device / application counter from the rank owning its
+    node, and the dispatch log as the union of the entries each rank wrote (zeros elsewhere)."""
+    owner = np.asarray(owner)
+    out = {}
+    for f in STAT_FIELDS:
+        if f in RUN_GLOBAL_FIELDS:
+            out[f] = int(getattr(per_rank[0][0], f))
+        else:
+            out[f] = sum(int(getattr(r[0], f)) for r in per_rank) & ((1 << 64) - 1)
+    dev_node, app_node = s._keep["dev_node"], s._keep["app_node"]
+    devc = per_rank[0][1].copy()
+    appc = per_rank[0][2].copy()
+    for r, (_st, dc, ac, _log) in enumerate(per_rank):
+        m = owner[dev_node] == r
+        devc[m] = dc[m]
+        m = owner[app_node] == r
+        appc[m] = ac[m]
+    log = tuple(np.sum([rr[3][i] for rr in per_rank], axis=0, dtype=per_rank[0][3][i].dtype) for i in range(3))
+    return stats_from_dict(out), devc, appc, log
+
+
+class Comm:
+    """RCCL communicator of a partitioned run (nsgpu_comm_*), one rank per GPU process; create it
+    after selecting the rank's device."""
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * 128)()
+        nsgpu.check(nsgpu.lib().nsgpu_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, uid, nranks, rank):
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        h = C.c_void_p()
+        nsgpu.check(nsgpu.lib().nsgpu_comm_init(buf, nranks, rank, C.byref(h)))
+        self.h = h.value
+        self.nranks, self.rank = nranks, rank
+
+    def __del__(self):
+        try:
+            nsgpu.lib().nsgpu_comm_destroy(self.h)
+        except Exception:
+            pass
+
+
+class DistEngine(Engine):
+    """Partition `rank` of `nranks` of a scenario (nsgpu_p2p_create_dist): the nodes with
+    owner[n] == rank.  With a Comm it runs on its own (one process per GPU, RCCL collectives);
+    without one it is a LoopbackGroup member."""
+
+    def __init__(self, scenario, owner, rank, nranks, comm=None, log_cap=0, pool_cap=0, stream=None):
+        self.s = scenario.c_struct()
+        self.owner = np.ascontiguousarray(owner, dtype=np.uint32)
+        if len(self.owner) != self.s.n_nodes:
+            raise ValueError("owner: one rank per node")
+        self.stream = stream
+        self.log_cap = log_cap
+        self.comm = comm
+        h = C.c_void_p()
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_create_dist(C.byref(self.s), self.owner.ctypes.data, rank, nranks,
+                                                       comm.h if comm is not None else None, pool_cap, log_cap,
+                                                       C.byref(h)))
+        self.h = h.value
+
+
+class LoopbackGroup:
+    """Every partition of one scenario on this GPU (nsgpu_p2p_group_*): the partitioned algorithm
+    with device-to-device copies in place of the RCCL collectives — its parity harness on one device."""
+
+    def __init__(self, scenario, nranks, owner=None, log_cap=0, pool_cap=0, stream=None):
+        self.owner = owner_blocks(scenario.n_nodes, nranks) if owner is None else np.asarray(owner, np.uint32)
+        self.members = [DistEngine(scenario, self.owner, r, nranks, None, log_cap, pool_cap, stream)
+                        for r in range(nranks)]
+        self.stream = stream
+        arr = (C.c_void_p * nranks)(*[m.h for m in self.members])
+        h = C.c_void_p()
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_group_create(arr, nranks, C.byref(h)))
+        self.h = h.value
+
+    def reset(self):
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_group_reset(self.h, self.stream))
+
+    def launch(self):
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_group_run(self.h, self.stream))
+
+    def results(self, log_n=0):
+        per = [m.results(log_n) for m in self.members]
+        return merge_results(per, self.owner, self.members[0].s)
+
+    def run(self, log_n=0):
+        self.reset()
+        self.launch()
+        return self.results(log_n)
+
+    def __del__(self):
+        try:
+            nsgpu.lib().nsgpu_p2p_group_destroy(self.h)
         except Exception:
             pass
