@@ -10,9 +10,11 @@ Workloads (--workload):
   churn: config 1, utils/bench-simulator.cc — 10,000 pending, U[0,1) s delays, 5e6 holds,
       GPU-resident Bench::Cb (nsgpu_hold_run).
 
-Neither workload shards inside one simulation yet, so with --gpus N every rank runs an
-independent replica ("replicas", weak scaling) and `value` is the events of all ranks divided by
-the slowest rank's time.
+With --gpus N (one process per GPU under torch.distributed.run) p2p-grid runs ONE simulation of a
+grid weak-scaled to 128 x 128N, partitioned into N row bands with the partitioned engine (RCCL
+allgathers + all-to-all every window; `--partitioned` forces that engine on one rank); `value` is
+the run's events / the slowest rank's time.  churn is a single logical process: its ranks run
+independent replicas and their events add up.
 
 roofline: dominant kernel = the churn's persistent kernel, or for p2p-grid the window-pipeline
 kernel with the largest average launch time (per-kernel HIP events in a separate bracketed run);
@@ -144,6 +146,62 @@ class P2PGrid:
             f"trace sinks: SURVEY §6 probe 82 k ev/s at 16x16 with global routing)")
 
 
+class P2PGridDist:
+    """Config 4 weak-scaled over N ranks (one GPU each): PointToPointGridHelper 128 x 128N, one OnOff
+    flow per column from row 0 to row 127, node ids (creation order) split into N contiguous row bands
+    (Node (systemId)); every flow crosses every band.  One partition per rank, RCCL collectives per
+    window; the whole simulation is one run, so `value` counts its events once."""
+    bytes_per_event = 104
+    kernel = "nsgpu::p2p partitioned window"
+
+    def __init__(self, args, stream, rank, world, td):
+        import numpy as np
+        import p2p
+        self.p2p, self.rank, self.world, self.td = p2p, rank, world, td
+        n = args.grid
+        self.scenario = p2p.grid(n, n * world)
+        owner = p2p.owner_blocks(self.scenario.n_nodes, world)
+        uid = [p2p.Comm.unique_id() if rank == 0 else None]
+        if td is not None:
+            td.broadcast_object_list(uid, src=0)
+        self.comm = p2p.Comm(uid[0], world, rank)
+        self.engine = p2p.DistEngine(self.scenario, owner, rank, world, self.comm, stream=stream)
+        cut = int(np.count_nonzero(owner[self.scenario.c_struct()._keep["dev_node"]] !=
+                                   owner[self.scenario.c_struct()._keep["dev_node"][
+                                       self.scenario.c_struct()._keep["dev_peer"]]])) // 2
+        self.workload = (f"PointToPointGridHelper {n}x{n * world} (config 4 weak-scaled, {n}x{n} nodes per GPU): "
+                         f"{self.scenario.n_nodes} nodes, {len(self.scenario.dev)} devices, 10Mb/s 1ms DropTail(100), "
+                         f"{n * world} OnOff UDP flows 500kb/s 512B top->bottom 0.1-2.0s, static XY routes, Stop 2.1s; "
+                         f"{world} row-band partitions ({cut} cut links), RCCL X0/X1 allgather + X2 all-to-all "
+                         f"per window, sequential (ts, uid) order")
+
+    def step(self):
+        self.engine.reset()
+        self.engine.launch()
+
+    def roofline(self, step_kernel_ms, events_per_step):
+        # the partitioned window is 6 kernels + 3 collectives: the roofline unit is one window
+        # (per rank: its share of the events) against the window's device time on this rank
+        st, _, _, _ = self.engine.results()
+        windows = max(int(st.windows), 1)
+        return {"kernel": self.kernel, "kernel_ms": step_kernel_ms / windows,
+                "events_per_launch": events_per_step / self.world / windows,
+                "step_device_ms": step_kernel_ms, "windows_per_step": windows,
+                "launch_unit": "one partitioned window on one rank (k_pa, k_refit_d, X0, k_cut, "
+                               "k_handle_rank, X1, k_gtile, k_dfin, X2)"}
+
+    def result(self):
+        st, devc, appc, _ = self.engine.results()
+        digest = int(st.digest)
+        if self.td is not None:  # the run digest is the sum of the ranks' shares
+            parts = [None] * self.world
+            self.td.all_gather_object(parts, digest)
+            digest = sum(parts) & ((1 << 64) - 1)
+        return int(st.dispatched), digest, {
+            "windows_per_step": int(st.windows), "max_window": int(st.max_window),
+            "ranks": self.world}
+
+
 WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid}
 
 
@@ -156,24 +214,30 @@ def main():
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--holds", type=int, default=5_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--partitioned", action="store_true",
+                    help="p2p-grid through the partitioned engine even on one rank (RCCL with one rank)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    tdist = None
-    if world > 1:
-        import torch
-        import torch.distributed as td
-        torch.cuda.set_device(local_rank)
-        td.init_process_group("nccl")
-        tdist = td
 
+    # libnsgpu (and the /opt/rocm HIP runtime and RCCL it links) first: torch, imported below only
+    # for the gloo bootstrap / barrier / max-over-ranks timing, then binds to the same libraries
     import nsgpu
 
     nsgpu.check(nsgpu.lib().nsgpu_set_device(local_rank))
+    tdist = None
+    if world > 1:
+        import torch.distributed as td
+        td.init_process_group("gloo")  # env:// (MASTER_ADDR / MASTER_PORT / RANK / WORLD_SIZE)
+        tdist = td
     stream = nsgpu.Stream()
-    wl = WORKLOADS[args.workload](args, stream.handle)
+    partitioned = args.workload == "p2p-grid" and (world > 1 or args.partitioned)
+    if partitioned:
+        wl = P2PGridDist(args, stream.handle, rank, world, tdist)
+    else:
+        wl = WORKLOADS[args.workload](args, stream.handle)
     timer = nsgpu.Timer()
 
     for _ in range(args.warmup):
@@ -181,11 +245,10 @@ def main():
     stream.sync()
 
     def barrier():
+        nsgpu.device_synchronize()
         if tdist is not None:
-            import torch
-            torch.cuda.synchronize()
             tdist.barrier()
-            torch.cuda.synchronize()
+        nsgpu.device_synchronize()
 
     barrier()
     stream.sync()
@@ -197,16 +260,17 @@ def main():
     stream.sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = timer.elapsed_ms() / args.steps  # one engine launch per step (+ resets / tiny setup kernels)
+    kernel_ms = timer.elapsed_ms() / args.steps  # device time of one step on this rank's stream
     events_per_step, digest, extra = wl.result()
 
     if tdist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    value = events_per_step * args.steps * world / elapsed
+    # a partitioned run is ONE simulation: its (global) events once; replicas (churn) add up
+    value = events_per_step * args.steps * (1 if partitioned else world) / elapsed
     # dominant kernel: name, events one launch processes, average launch duration (HIP events)
     rl = wl.roofline(kernel_ms, events_per_step)
     achieved = wl.bytes_per_event * rl["events_per_launch"] / (rl["kernel_ms"] / 1e3) / 1e9
@@ -233,7 +297,8 @@ def main():
             "dtype": "int64",
             "data": "synthetic",
             "config": dict({"workload": wl.workload, "events_per_step": events_per_step,
-                            "parallelism": "replicas" if world > 1 else "single"}, **extra),
+                            "parallelism": (f"partitioned x{world} (RCCL)" if partitioned else
+                                            "replicas" if world > 1 else "single")}, **extra),
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -245,11 +310,11 @@ def main():
                 **rl,
             },
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1 and not partitioned:
             cv, cdigest, sample = wl.cpu_baseline()
             out["cpu_baseline"] = {"value": cv, "unit": "events/s", "cores": 1, "kind": "port", "sample": sample,
                                    "digest_match": bool(cdigest == digest)}
-            out["speedup_vs_cpu"] = value / world / cv
+            out["speedup_vs_cpu"] = value / cv
         print(json.dumps(out), flush=True)
 
     if tdist is not None:

@@ -40,6 +40,7 @@ int         nsgpu_free(void *d_ptr);
 int         nsgpu_memcpy_htod(void *d_dst, const void *h_src, size_t bytes, void *stream);
 int         nsgpu_memcpy_dtoh(void *h_dst, const void *d_src, size_t bytes, void *stream);
 int         nsgpu_memset(void *d_dst, int value, size_t bytes, void *stream);
+int         nsgpu_device_synchronize(void);
 int         nsgpu_stream_create(void **stream);
 int         nsgpu_stream_destroy(void *stream);
 int         nsgpu_stream_sync(void *stream);

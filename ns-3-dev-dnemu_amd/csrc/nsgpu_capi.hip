@@ -52,6 +52,10 @@ int nsgpu_memset(void *d_dst, int value, size_t bytes, void *stream) {
   NSGPU_HIP(hipMemsetAsync(d_dst, value, bytes, (hipStream_t)stream));
   return NSGPU_OK;
 }
+int nsgpu_device_synchronize(void) {
+  NSGPU_HIP(hipDeviceSynchronize());
+  return NSGPU_OK;
+}
 int nsgpu_stream_create(void **stream) {
   hipStream_t s;
   NSGPU_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));

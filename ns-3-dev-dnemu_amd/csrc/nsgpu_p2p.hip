@@ -745,12 +745,15 @@ __device__ __forceinline__ void classify(const P2PDev &M, Ctl &C, const WinBound
 // Pending set = pool `cur` (P entries) + the non-inline children of the last window.  Thread g <
 // WCAP takes slot g of the last window; thread WCAP + i (grid-stride) takes pool entry i.
 constexpr int PFC = 4;  // children per slot loaded ahead
+// DIST: the partitioned engine's variant (remote-event role, X1 reduction target, owner filter);
+// the single-GPU instantiation carries none of it.
+template <bool DIST>
 __global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
   PH_BEGIN();
   Ctl &C = *M.C;
   const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * TB;
-  const uint64_t RR = M.dist ? (uint64_t)M.nranks * CAPX : 0;  // remote-event threads (partitioned)
+  const uint64_t RR = DIST ? (uint64_t)M.nranks * CAPX : 0;  // remote-event threads (partitioned)
   const bool slot_role = g < (uint64_t)WCAP;                   // (roles are wave-uniform)
   const bool remote_role = !slot_role && g < WCAP + RR;
   if (C.prep || C.done >= 2) return;  // window already prepared by the refit / run over
@@ -758,7 +761,7 @@ __global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
   const int cur = C.cur, nxt = cur ^ 1;
   const uint64_t win = C.windows;
   const WinBound b = window_bound(C.red[(win + 1) & 1]);
-  Red &R = M.dist ? x1hdr(M.x1_send, 0)->red : C.red[win & 1];
+  Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[win & 1];
   if (partition && blockIdx.x == 0 && threadIdx.x == 0) publish_bound(C, b);
   const uint64_t P = partition ? C.P : 0;
   const uint32_t pW = C.pvalid ? C.pW : 0;
@@ -827,13 +830,13 @@ __global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
               ii++;
             }
           } else {  // (partitioned: a child on another rank's node went there through X2)
-            valid = partition && (!M.dist || M.owner[e.ctx] == M.rank);
+            valid = partition && (!DIST || M.owner[e.ctx] == M.rank);
           }
         }
         if (__ballot(valid)) classify(M, C, b, nxt, valid, e, R, tmn, wnd);
       }
     }
-  } else if (remote_role) {
+  } else if (DIST && remote_role) {
     // ---- remote events received through X2 (partitioned): record idx % CAPX from rank idx / CAPX
     const uint64_t idx = g - WCAP;
     const uint32_t q = (uint32_t)(idx / CAPX), rec = (uint32_t)(idx % CAPX);
@@ -876,6 +879,7 @@ __device__ __forceinline__ uint32_t nth_slot_scan(const P2PDev &M, uint32_t W, u
   return bs;
 }
 
+template <bool DIST>
 __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0) {
   __shared__ uint32_t chs[HB * CH];
   __shared__ uint64_t chk[HB * CH];
@@ -885,7 +889,7 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
   const uint32_t kind0 = M.wkind[i0], a0 = M.wa[i0];
   const Pkt pkt0 = M.wpkt[i0];
   const uint32_t W = C.W;
-  Red &R = M.dist ? x1hdr(M.x1_send, 0)->red : C.red[C.windows & 1];
+  Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[C.windows & 1];
   uint64_t tmn = ~0ull, wnd = ~0ull;
   HStat hs{0, 0, 0, 0, false};
   uint32_t dtc = 0, dti = 0;  // partitioned: the X1 summary's child totals and largest key
@@ -1001,7 +1005,7 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
         for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
       M.nchild[s] = E.n;
       M.ninl[s] = ni;
-      if (M.dist) {
+      if (DIST) {
         x1ent(M.x1_send, 0)[s] = X1Ent{key, E.n | (ni << 16), 0};
         dtc += E.n;
         dti += ni;
@@ -1030,7 +1034,7 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
   }
 #endif
   publish_min<HB>(R, tmn, wnd);
-  if (M.dist) {
+  if (DIST) {
     dtc = wave_sum32(dtc);
     dti = wave_sum32(dti);
     dlk = wave_max64(dlk);
@@ -1071,6 +1075,7 @@ __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_
   if (c) atomicAdd(&M.wrank[i], c);
 }
 
+template <bool DIST>
 __global__ __launch_bounds__(HB) void k_handle_rank(const P2PDev M) {
   PH_BEGIN();
   Ctl &C = *M.C;
@@ -1082,7 +1087,7 @@ __global__ __launch_bounds__(HB) void k_handle_rank(const P2PDev M) {
   const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
 #endif
   PH_MARK(8);
-  if (blockIdx.x < (uint32_t)NHB) handle_node(M, C, blockIdx.x * HB + threadIdx.x);
+  if (blockIdx.x < (uint32_t)NHB) handle_node<DIST>(M, C, blockIdx.x * HB + threadIdx.x);
   else rank_tile(M, C, blockIdx.x - NHB);
   PH_MARK(9);
 #ifdef NSGPU_PHASE_PROF
@@ -2068,8 +2073,8 @@ const char *const KERNEL_NAMES[NKERN] = {"k_pa", "k_handle_rank", "k_scan"};
 // (hipExtLaunchKernelGGL: no separate marker packets between the pipeline's kernels).
 void launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   switch (k) {
-    case 0: hipExtLaunchKernelGGL(k_pa, dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M); break;
-    case 1: hipExtLaunchKernelGGL(k_handle_rank, dim3(NHB + NRB), dim3(HB), 0, s, ev0, ev1, 0, h->M); break;
+    case 0: hipExtLaunchKernelGGL(k_pa<false>, dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M); break;
+    case 1: hipExtLaunchKernelGGL(k_handle_rank<false>, dim3(NHB + NRB), dim3(HB), 0, s, ev0, ev1, 0, h->M); break;
     default: hipExtLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M); break;
   }
 }
@@ -2084,11 +2089,11 @@ static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s) {
   ncclComm_t comm = h->comm->comm;
   const P2PDev &M = h->M;
   for (int w = 0; w < NWIN; w++) {
-    hipLaunchKernelGGL(k_pa, dim3(GRID_POOL), dim3(TB), 0, s, M);
+    hipLaunchKernelGGL(k_pa<true>, dim3(GRID_POOL), dim3(TB), 0, s, M);
     hipLaunchKernelGGL(k_refit_d, dim3(1), dim3(SCAN_THREADS), 0, s, M);
     NCCL_TRY(ncclAllGather(M.x0_send, M.x0_recv, X0B, ncclUint8, comm, s));
     hipLaunchKernelGGL(k_cut, dim3(1), dim3(SCAN_THREADS), 0, s, M);
-    hipLaunchKernelGGL(k_handle_rank, dim3(NHB), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k_handle_rank<true>, dim3(NHB), dim3(HB), 0, s, M);
     NCCL_TRY(ncclAllGather(M.x1_send, M.x1_recv, X1B, ncclUint8, comm, s));
     hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, M);
     hipLaunchKernelGGL(k_dfin, dim3(NHB), dim3(HB), 0, s, M);
@@ -2326,11 +2331,11 @@ struct nsgpu_p2p_group {
 static void launch_windows_group(nsgpu_p2p_group *g, hipStream_t s) {
   const unsigned n = (unsigned)g->m.size();
   for (int w = 0; w < NWIN; w++) {
-    for (auto *h : g->m) hipLaunchKernelGGL(k_pa, dim3(GRID_POOL), dim3(TB), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_pa<true>, dim3(GRID_POOL), dim3(TB), 0, s, h->M);
     for (auto *h : g->m) hipLaunchKernelGGL(k_refit_d, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[0]);
     for (auto *h : g->m) hipLaunchKernelGGL(k_cut, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
-    for (auto *h : g->m) hipLaunchKernelGGL(k_handle_rank, dim3(NHB), dim3(HB), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_handle_rank<true>, dim3(NHB), dim3(HB), 0, s, h->M);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[1]);
     for (auto *h : g->m) hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, h->M);
     for (auto *h : g->m) hipLaunchKernelGGL(k_dfin, dim3(NHB), dim3(HB), 0, s, h->M);

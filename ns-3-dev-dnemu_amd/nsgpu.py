@@ -54,6 +54,7 @@ SIGNATURES = {
     "nsgpu_memcpy_htod": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
     "nsgpu_memcpy_dtoh": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
     "nsgpu_memset": (C.c_int, [_vp, C.c_int, C.c_size_t, _vp]),
+    "nsgpu_device_synchronize": (C.c_int, []),
     "nsgpu_stream_create": (C.c_int, [C.POINTER(C.c_void_p)]),
     "nsgpu_stream_destroy": (C.c_int, [_vp]),
     "nsgpu_stream_sync": (C.c_int, [_vp]),
@@ -181,6 +182,10 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def device_synchronize():
+    check(lib().nsgpu_device_synchronize())
 
 
 class Stream:
