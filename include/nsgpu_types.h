@@ -77,7 +77,12 @@ typedef struct nsgpu_rx_record {
  * next-hop tables, OnOff (UDP, constant on/off times) sources and PacketSink sinks.  All arrays are
  * host pointers; devices and applications are listed in ns-3 creation order (Node::AddDevice /
  * Node::AddApplication), which fixes the setup-time uids (node-list.cc:124-131, node.cc:111-145). */
-enum nsgpu_app_kind { NSGPU_APP_ONOFF = 0, NSGPU_APP_SINK = 1 };
+enum nsgpu_app_kind { NSGPU_APP_ONOFF = 0, NSGPU_APP_SINK = 1, NSGPU_APP_ECHO_CLIENT = 2, NSGPU_APP_ECHO_SERVER = 3 };
+/* UdpEchoClient (udp-echo-client.cc): app_dst_node = the server's node, app_pkt_size = PacketSize,
+ * app_count = MaxPackets, app_interval_ns = Interval, app_src_slot = the route-table slot of the
+ * client's own node (the echo comes back there).  UdpEchoServer (udp-echo-server.cc): the node's bound
+ * UDP endpoint, like a PacketSink; HandleRead sends every datagram back to its sender.  A node has
+ * at most one bound endpoint (PacketSink or UdpEchoServer). */
 
 typedef struct nsgpu_p2p_scenario {
   uint32_t n_nodes;
@@ -118,7 +123,35 @@ typedef struct nsgpu_p2p_scenario {
   uint32_t pad_;
   const uint32_t *setup_kind;
   const uint32_t *setup_index;
+  /* UdpEchoClient parameters (NULL when the scenario has no echo client) */
+  const uint32_t *app_count;
+  const int64_t  *app_interval_ns;
+  const uint32_t *app_src_slot;
 } nsgpu_p2p_scenario;
+
+/* Packet descriptor flag: the datagram is an echo reply travelling back to its client (app). */
+#define NSGPU_PKT_REPLY 0x80000000u
+
+/* ---------------- trace records (ascii / pcap replay) ----------------
+ * One record per call of a default ascii trace sink of PointToPointHelper::EnableAsciiInternal
+ * (point-to-point-helper.cc:113-219, trace-helper.cc:303-390): TxQueue/Enqueue "+", TxQueue/Dequeue
+ * "-", TxQueue/Drop "d", MacRx "r".  The pcap PromiscSniffer calls are implied: every Dequeue is
+ * followed by the sniffer on the same device (Send :462-518, TransmitComplete :236-269), every MacRx is
+ * preceded by it (Receive :304-346, packet with the PPP header).  Records are written unordered; the
+ * trace order is (ts, uid, seq): the pop order of the dispatched event, then call order inside it. */
+enum nsgpu_trace_kind { NSGPU_TR_ENQUEUE = 0, NSGPU_TR_DEQUEUE = 1, NSGPU_TR_DROP = 2, NSGPU_TR_RX = 3 };
+typedef struct nsgpu_trace_record {
+  uint64_t ts;    /* Now () of the call (ns) */
+  uint32_t uid;   /* uid of the dispatched event that made the call */
+  uint16_t seq;   /* call index inside that event */
+  uint8_t  kind;  /* nsgpu_trace_kind */
+  uint8_t  pad_;
+  uint32_t dev;   /* device (its queue) */
+  /* the packet as the sink sees it: flow (| NSGPU_PKT_REPLY), IPv4 identification, size in bytes
+   * (PPP header included except for MacRx), IPv4 TTL */
+  uint32_t app, ipid, size, ttl;
+  uint32_t pad2_;
+} nsgpu_trace_record;  /* 40 bytes */
 
 enum nsgpu_setup_kind { NSGPU_SETUP_NODE = 0, NSGPU_SETUP_DEVICE = 1, NSGPU_SETUP_APP = 2, NSGPU_SETUP_STOP = 3,
                         NSGPU_SETUP_UID = 4, NSGPU_SETUP_NOOP = 5 };

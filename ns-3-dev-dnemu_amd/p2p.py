@@ -19,7 +19,8 @@ import numpy as np
 
 import nsgpu
 
-APP_ONOFF, APP_SINK = 0, 1
+APP_ONOFF, APP_SINK, APP_ECHO_CLIENT, APP_ECHO_SERVER = 0, 1, 2, 3
+SENDERS = (APP_ONOFF, APP_ECHO_CLIENT)  # applications that originate datagrams towards app["dst"]
 SETUP_NODE, SETUP_DEVICE, SETUP_APP, SETUP_STOP, SETUP_UID, SETUP_NOOP = 0, 1, 2, 3, 4, 5
 NO_ROUTE = 0xFFFFFFFF
 
@@ -35,6 +36,7 @@ class ScenarioStruct(C.Structure):
         ("app_off_s", C.c_void_p), ("app_max_bytes", C.c_void_p), ("app_ttl", C.c_void_p),
         ("stop_ns", C.c_int64), ("n_setup", C.c_uint32), ("pad_", C.c_uint32),
         ("setup_kind", C.c_void_p), ("setup_index", C.c_void_p),
+        ("app_count", C.c_void_p), ("app_interval_ns", C.c_void_p), ("app_src_slot", C.c_void_p),
     ]
 
 
@@ -64,6 +66,8 @@ class Scenario:
         self.route = None
         self.n_dst = 0
         self.dst_slot = {}
+        # addressing (host side only: the trace codec prints it, the engines never read it)
+        self.dev_addr = {}   # device -> IPv4 address (u32) of its interface
         for _ in range(n_nodes):
             self.add_node()
 
@@ -93,18 +97,40 @@ class Scenario:
             self.setup.append((SETUP_UID, 0))
         return da, db
 
-    def add_sink(self, node, start_ns, stop_ns):
-        self.apps.append(dict(kind=APP_SINK, node=node, start=start_ns, stop=stop_ns, dst=0, rate=0, size=0,
-                              on=0.0, off=0.0, maxb=0, ttl=0))
-        self.setup.append((SETUP_APP, len(self.apps) - 1))
+    def _app(self, **kw):
+        a = dict(dst=0, rate=0, size=0, on=0.0, off=0.0, maxb=0, ttl=64, count=0, interval=0, port=0,
+                 remote_addr=None, remote_port=0)
+        a.update(kw)
+        self.apps.append(a)
+        self.setup.append((SETUP_APP, len(self.apps) - 1))  # Node::AddApplication
         return len(self.apps) - 1
 
+    def add_sink(self, node, start_ns, stop_ns, port=9):
+        return self._app(kind=APP_SINK, node=node, start=start_ns, stop=stop_ns, port=port, ttl=0)
+
     def add_onoff(self, node, dst, start_ns, stop_ns, rate_bps=500000, size=512, on_s=1.0, off_s=1.0,
-                  max_bytes=0, ttl=64):
-        self.apps.append(dict(kind=APP_ONOFF, node=node, start=start_ns, stop=stop_ns, dst=dst, rate=rate_bps,
-                              size=size, on=on_s, off=off_s, maxb=max_bytes, ttl=ttl))
-        self.setup.append((SETUP_APP, len(self.apps) - 1))
-        return len(self.apps) - 1
+                  max_bytes=0, ttl=64, remote_addr=None, remote_port=9):
+        return self._app(kind=APP_ONOFF, node=node, start=start_ns, stop=stop_ns, dst=dst, rate=rate_bps, size=size,
+                         on=on_s, off=off_s, maxb=max_bytes, ttl=ttl, remote_addr=remote_addr, remote_port=remote_port)
+
+    def add_echo_server(self, node, start_ns, stop_ns, port=9):  # UdpEchoServerHelper (port).Install
+        return self._app(kind=APP_ECHO_SERVER, node=node, start=start_ns, stop=stop_ns, port=port, ttl=64)
+
+    def add_echo_client(self, node, dst, start_ns, stop_ns, count=1, interval_ns=1_000_000_000, size=1024,
+                        ttl=64, remote_addr=None, remote_port=9):  # UdpEchoClientHelper (address, port).Install
+        return self._app(kind=APP_ECHO_CLIENT, node=node, start=start_ns, stop=stop_ns, dst=dst, size=size,
+                         count=count, interval=interval_ns, ttl=ttl, remote_addr=remote_addr,
+                         remote_port=remote_port)
+
+    # Ipv4AddressHelper::Assign on the two devices of a link, then NewNetwork (ipv4-address-helper.cc)
+    def assign_link(self, da, db, network):
+        self.dev_addr[da] = network + 1
+        self.dev_addr[db] = network + 2
+
+    def _slot_nodes(self):
+        # route-table columns: every datagram destination (sender apps' dst), and echo clients' own nodes
+        return sorted({a["dst"] for a in self.apps if a["kind"] in SENDERS}
+                      | {a["node"] for a in self.apps if a["kind"] == APP_ECHO_CLIENT})
 
     def stop(self, t_ns):  # Simulator::Stop (t)
         self.stop_ns = t_ns
@@ -119,7 +145,7 @@ class Scenario:
 
     def route_bfs(self):
         """Static next-hop table towards every OnOff destination (BFS shortest paths, lowest device first)."""
-        dsts = sorted({a["dst"] for a in self.apps if a["kind"] == APP_ONOFF})
+        dsts = self._slot_nodes()
         self.dst_slot = {d: i for i, d in enumerate(dsts)}
         self.n_dst = max(1, len(dsts))
         nb = self._neighbors()
@@ -159,8 +185,12 @@ class Scenario:
             app_start_ns=np.array([a["start"] for a in A], np.int64),
             app_stop_ns=np.array([a["stop"] for a in A], np.int64),
             app_dst_node=np.array([a["dst"] for a in A], np.uint32),
-            app_dst_slot=np.array([self.dst_slot.get(a["dst"], 0) if a["kind"] == APP_ONOFF else 0 for a in A],
+            app_dst_slot=np.array([self.dst_slot.get(a["dst"], 0) if a["kind"] in SENDERS else 0 for a in A],
                                   np.uint32),
+            app_count=np.array([a["count"] for a in A], np.uint32),
+            app_interval_ns=np.array([a["interval"] for a in A], np.int64),
+            app_src_slot=np.array([self.dst_slot.get(a["node"], 0) if a["kind"] == APP_ECHO_CLIENT else 0
+                                   for a in A], np.uint32),
             app_rate_bps=np.array([a["rate"] for a in A], np.uint64),
             app_pkt_size=np.array([a["size"] for a in A], np.uint32),
             app_on_s=np.array([a["on"] for a in A], np.float64),
@@ -180,6 +210,26 @@ class Scenario:
         return s
 
 
+def ip(dotted):
+    a, b, c, d = (int(v) for v in dotted.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def first_cc():
+    """examples/tutorial/first.cc:27-69: two nodes, 5Mbps / 2ms point-to-point, 10.1.1.0/24,
+    UdpEchoServer (port 9) on node 1 from 1 s to 10 s, UdpEchoClient on node 0 from 2 s to 10 s
+    (MaxPackets 1, Interval 1 s, PacketSize 1024).  No Simulator::Stop: Run ends with an empty queue."""
+    sc = Scenario(2)  # nodes.Create (2)
+    da, db = sc.link(0, 1, 5_000_000, 2_000_000)  # pointToPoint.Install (nodes)
+    sc.install_stack()  # stack.Install (nodes)
+    sc.assign_link(da, db, ip("10.1.1.0"))  # address.Assign (devices)
+    sc.add_echo_server(1, 1_000_000_000, 10_000_000_000, port=9)
+    sc.add_echo_client(0, 1, 2_000_000_000, 10_000_000_000, count=1, interval_ns=1_000_000_000, size=1024,
+                       remote_addr=sc.dev_addr[db], remote_port=9)
+    sc.route_bfs()
+    return sc
+
+
 def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="columns", start_ns=100_000_000,
          stop_ns=2_000_000_000, sim_stop_ns=2_100_000_000, rate_bps=500_000, size=512, on_s=1e9, off_s=0.0,
          ttl=255, n_flows=None):
@@ -192,16 +242,25 @@ def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="column
     n = rows * cols
     # the device of each node towards its four grid neighbours (XY routing's next hops)
     right, left, down, up = (np.full(n, NO_ROUTE, np.uint32) for _ in range(4))
+    row_links, col_links = [], []
     for y in range(rows):
         for x in range(cols):
             sc.add_node()  # rowNodes.Create (1)
             if x > 0:
                 da, db = sc.link(nid(y, x - 1), nid(y, x), bps, delay_ns, qmax)
                 right[nid(y, x - 1)], left[nid(y, x)] = da, db
+                row_links.append((da, db))
             if y > 0:
                 da, db = sc.link(nid(y - 1, x), nid(y, x), bps, delay_ns, qmax)
                 down[nid(y - 1, x)], up[nid(y, x)] = da, db
+                col_links.append((da, db))
     sc.install_stack()  # PointToPointGridHelper::InstallStack (point-to-point-grid.cc:79-89)
+    # AssignIpv4Addresses (point-to-point-grid.cc:97-132): every row link, then every column link, one
+    # /24 each (rowIp 10.0.0.0, colIp 11.0.0.0: disjoint at 128x128)
+    for k, (da, db) in enumerate(row_links):
+        sc.assign_link(da, db, ip("10.0.0.0") + (k << 8))
+    for k, (da, db) in enumerate(col_links):
+        sc.assign_link(da, db, ip("11.0.0.0") + (k << 8))
     fl = []
     if flows == "columns":
         ncol = cols if n_flows is None else min(cols, n_flows)
@@ -214,7 +273,12 @@ def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="column
         if d not in sinks:
             sinks[d] = sc.add_sink(d, 0, 0)
     for s_, d in fl:
-        sc.add_onoff(s_, d, start_ns, stop_ns, rate_bps=rate_bps, size=size, on_s=on_s, off_s=off_s, ttl=ttl)
+        # PointToPointGridHelper::GetIpv4Address (point-to-point-grid.cc:243-265): the node's left row
+        # device, the right one in column 0
+        yd, xd = divmod(d, cols)
+        raddr = sc.dev_addr[int(right[d] if xd == 0 else left[d])] if cols > 1 else None
+        sc.add_onoff(s_, d, start_ns, stop_ns, rate_bps=rate_bps, size=size, on_s=on_s, off_s=off_s, ttl=ttl,
+                     remote_addr=raddr)
     sc.stop(sim_stop_ns)
     # XY routes towards each destination: along the row first, then along the column
     dsts = sorted({d for _s, d in fl})

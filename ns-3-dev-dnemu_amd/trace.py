@@ -1,0 +1,150 @@
+"""Trace replay: ns-3 ascii and pcap trace files from nsgpu_trace_record streams.
+
+The engines (the GPU p2p engine, and the oracle that checks it) record one nsgpu_trace_record per
+call of a default ascii trace sink (include/nsgpu_types.h); this module turns the records into the
+bytes ns-3 writes, host side and after the run:
+
+  * ascii: AsciiTraceHelper::Default{Enqueue,Dequeue,Drop,Receive}SinkWithContext
+    (src/network/helper/trace-helper.cc:303-390) as connected by PointToPointHelper::EnableAsciiInternal
+    with a stream (src/point-to-point/helper/point-to-point-helper.cc:186-219, EnableAsciiAll (stream)):
+    "<c> <Now ().GetSeconds ()> <context> <packet>" where the packet prints through its metadata
+    (Packet::Print, src/network/model/packet.cc:427-476) as
+    ns3::PppHeader (...) ns3::Ipv4Header (...) ns3::UdpHeader (...) Payload (size=N);
+    PppHeader::Print (ppp-header.cc:57-72), Ipv4Header::Print (ipv4-header.cc:301-338, this fork's
+    DSCP/ECN fields), UdpHeader::Print (udp-header.cc:156-162).
+  * pcap: PcapHelper::CreateFile (DLT_PPP, snaplen 65535) + the PromiscSniffer sink
+    (point-to-point-helper.cc:81-110): one file per device, PcapFileWrapper::Write (Time, Packet)
+    (pcap-file-wrapper.cc:104-111: GetMicroSeconds () split into s / us), the serialized bytes
+    PPP (2) + IPv4 (20, checksum 0: ChecksumEnabled is false) + UDP (8, checksum 0) + zero payload.
+
+The packet descriptor of a record (flow, IPv4 identification, size, TTL) plus the scenario's
+addressing (Scenario.dev_addr, application ports) determine every byte.  Pinned against the
+reference's own first.cc output (tests/golden/survey_reference_runs.json: ascii and pcap md5s).
+"""
+import struct
+
+import numpy as np
+
+import p2p
+
+TR_ENQUEUE, TR_DEQUEUE, TR_DROP, TR_RX = 0, 1, 2, 3
+PKT_REPLY = 0x80000000
+TRACE_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("seq", "<u2"), ("kind", "u1"), ("pad_", "u1"),
+                               ("dev", "<u4"), ("app", "<u4"), ("ipid", "<u4"), ("size", "<u4"),
+                               ("ttl", "<u4"), ("pad2_", "<u4")])  # nsgpu_trace_record
+_CHAR = {TR_ENQUEUE: "+", TR_DEQUEUE: "-", TR_DROP: "d", TR_RX: "r"}
+_SOURCE = {TR_ENQUEUE: "TxQueue/Enqueue", TR_DEQUEUE: "TxQueue/Dequeue", TR_DROP: "TxQueue/Drop", TR_RX: "MacRx"}
+PPP_HDR = 2
+
+
+def dotted(a):
+    return "%d.%d.%d.%d" % (a >> 24, (a >> 16) & 255, (a >> 8) & 255, a & 255)
+
+
+def sort_records(tr):
+    """Trace order: the pop order of the dispatching event (ts, uid), then call order inside it."""
+    tr = np.asarray(tr, dtype=TRACE_RECORD_DTYPE)
+    return tr[np.lexsort((tr["seq"], tr["uid"], tr["ts"]))]
+
+
+def seconds_text(ts_ns):
+    """std::ostream << double (precision 6, %g) of Time::GetSeconds ()."""
+    return "%g" % (ts_ns / 1e9)
+
+
+class Codec:
+    """Addressing of a p2p.Scenario as ns-3 would print it: interface indices, addresses, ports."""
+
+    def __init__(self, sc):
+        self.sc = sc
+        self.dev_node = [d[0] for d in sc.dev]
+        # Node::AddDevice order fixes GetIfIndex: point-to-point devices and the loopback (setup list)
+        self.ifindex = {}
+        nxt = [0] * sc.n_nodes
+        for kind, k in sc.setup:
+            if kind == p2p.SETUP_DEVICE:
+                n = sc.dev[k][0]
+                self.ifindex[k] = nxt[n]
+                nxt[n] += 1
+            elif kind == p2p.SETUP_NOOP:  # LoopbackNetDevice
+                nxt[k] += 1
+        # ephemeral ports of the sender sockets: Ipv4EndPointDemux::AllocateEphemeralPort (49153, 49154, ...
+        # per node, ipv4-end-point-demux.cc:350-370) in StartApplication order (start time, then app order)
+        self.eport = {}
+        per_node = {}
+        order = sorted((a["start"], i) for i, a in enumerate(sc.apps) if a["kind"] in p2p.SENDERS)
+        for _t, i in order:
+            n = sc.apps[i]["node"]
+            per_node[n] = per_node.get(n, 49152) + 1
+            self.eport[i] = per_node[n]
+        self.echo_server = {a["node"]: i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_ECHO_SERVER}
+        # an application without an explicit remote address targets its node's first interface
+        self.first_addr = {}
+        for d in sorted(self.ifindex, key=lambda d: self.ifindex[d]):
+            self.first_addr.setdefault(self.dev_node[d], sc.dev_addr.get(d, 0))
+        self.route = sc.route
+        self.slot = sc.dst_slot
+
+    def _out_addr(self, node, dst_node):
+        d = int(self.route[node, self.slot[dst_node]])
+        return self.sc.dev_addr.get(d, 0)
+
+    def headers(self, app_word):
+        """(src, dst, sport, dport) of a datagram of flow app_word."""
+        a = app_word & ~PKT_REPLY
+        A = self.sc.apps[a]
+        req_src = self._out_addr(A["node"], A["dst"])
+        req_dst = A["remote_addr"] if A["remote_addr"] is not None else self.first_addr.get(A["dst"], 0)
+        if app_word & PKT_REPLY:  # UdpEchoServer::HandleRead -> SendTo (packet, 0, from)
+            return self._out_addr(A["dst"], A["node"]), req_src, A["remote_port"], self.eport[a]
+        return req_src, req_dst, self.eport[a], A["remote_port"]
+
+    # ---------------- ascii ----------------
+    def packet_text(self, r):
+        src, dst, sp, dp = self.headers(int(r["app"]))
+        ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
+        parts = []
+        if r["kind"] != TR_RX:
+            parts.append("ns3::PppHeader (Point-to-Point Protocol: IP (0x0021))")
+        parts.append("ns3::Ipv4Header (tos 0x0 DSCP Default ECN Not-ECT ttl %d id %d protocol 17 offset (bytes) 0 "
+                     "flags [none] length: %d %s > %s)" % (int(r["ttl"]) & 255, int(r["ipid"]) & 0xffff, ip_len,
+                                                           dotted(src), dotted(dst)))
+        parts.append("ns3::UdpHeader (length: %d %d > %d)" % (ip_len - 20, sp, dp))
+        parts.append("Payload (size=%d)" % (ip_len - 28))
+        return " ".join(parts)
+
+    def ascii(self, tr):
+        """The EnableAsciiAll (stream) file of a sorted record stream, as one string."""
+        out = []
+        for r in tr:
+            d = int(r["dev"])
+            ctx = "/NodeList/%d/DeviceList/%d/$ns3::PointToPointNetDevice/%s" % (
+                self.dev_node[d], self.ifindex[d], _SOURCE[int(r["kind"])])
+            out.append("%s %s %s %s\n" % (_CHAR[int(r["kind"])], seconds_text(int(r["ts"])), ctx, self.packet_text(r)))
+        return "".join(out)
+
+    # ---------------- pcap ----------------
+    def packet_bytes(self, r):
+        """Serialized packet with its PPP header (what the sniffer sees)."""
+        src, dst, sp, dp = self.headers(int(r["app"]))
+        ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
+        ipv4 = struct.pack(">BBHHHBBHII", 0x45, 0, ip_len, int(r["ipid"]) & 0xffff, 0, int(r["ttl"]) & 255, 17, 0,
+                           src, dst)
+        udp = struct.pack(">HHHH", sp, dp, ip_len - 20, 0)
+        return struct.pack(">H", 0x0021) + ipv4 + udp + bytes(ip_len - 28)
+
+    def pcaps(self, tr):
+        """EnablePcapAll: {(node, ifindex): file bytes} for every point-to-point device."""
+        files = {}
+        for d in range(len(self.sc.dev)):
+            files[(self.dev_node[d], self.ifindex[d])] = bytearray(struct.pack("<IHHiIII", 0xa1b2c3d4, 2, 4, 0, 0,
+                                                                               65535, 9))  # DLT_PPP
+        for r in tr:
+            if r["kind"] not in (TR_DEQUEUE, TR_RX):  # the sniffer runs after Dequeue and before MacRx
+                continue
+            d = int(r["dev"])
+            pkt = self.packet_bytes(r)
+            us = int(r["ts"]) // 1000
+            f = files[(self.dev_node[d], self.ifindex[d])]
+            f += struct.pack("<IIII", us // 1000000, us % 1000000, len(pkt), len(pkt)) + pkt
+        return {k: bytes(v) for k, v in files.items()}

@@ -118,6 +118,12 @@ int nsref_churn_run(const uint64_t *dist_ns, uint32_t n, uint32_t total, int sch
 int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
                   nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
                   uint64_t log_cap, double *run_seconds);
+/* The same run, also recording every ascii trace sink call (nsgpu_trace_record, pop order) when
+ * trace_n is non-NULL: *trace_n = records made, the first trace_cap of them copied to trace. */
+int nsref_p2p_run_trace(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
+                        nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
+                        uint64_t log_cap, double *run_seconds, nsgpu_trace_record *trace, uint64_t trace_cap,
+                        uint64_t *trace_n);
 
 /* bench-simulator ReadDistribution: (uint64_t)(data * 1000000000)  (bench-simulator.cc:66) */
 uint64_t nsref_distribution_ns(double seconds);

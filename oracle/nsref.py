@@ -132,6 +132,9 @@ def lib():
         L.nsref_p2p_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_uint64, C.c_void_p]
         L.nsref_p2p_run.restype = C.c_int
+        L.nsref_p2p_run_trace.argtypes = [C.c_void_p] * 7 + [C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                              C.c_void_p]
+        L.nsref_p2p_run_trace.restype = C.c_int
         L.nsref_distribution_ns.argtypes = [C.c_double]
         L.nsref_distribution_ns.restype = C.c_uint64
         _lib = L
@@ -355,3 +358,24 @@ def p2p_run(scenario_struct, stats_struct, devc, appc, log_cap=0):
                         lts.ctypes.data if log_cap else None, luid.ctypes.data if log_cap else None,
                         lctx.ctypes.data if log_cap else None, log_cap, C.byref(secs))
     return secs.value, (lts, luid, lctx)
+
+
+TRACE_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("seq", "<u2"), ("kind", "u1"), ("pad_", "u1"),
+                               ("dev", "<u4"), ("app", "<u4"), ("ipid", "<u4"), ("size", "<u4"),
+                               ("ttl", "<u4"), ("pad2_", "<u4")])  # nsgpu_trace_record
+
+
+def p2p_run_trace(scenario_struct, stats_struct, devc, appc, log_cap=0):
+    """p2p_run that also returns the ascii trace sink calls (TRACE_RECORD_DTYPE, pop order)."""
+    secs = C.c_double()
+    lts = np.zeros(log_cap, np.uint64)
+    luid = np.zeros(log_cap, np.uint32)
+    lctx = np.zeros(log_cap, np.uint32)
+    n = C.c_uint64()
+    args = [C.byref(scenario_struct), C.byref(stats_struct), devc.ctypes.data, appc.ctypes.data,
+            lts.ctypes.data if log_cap else None, luid.ctypes.data if log_cap else None,
+            lctx.ctypes.data if log_cap else None, log_cap, C.byref(secs)]
+    lib().nsref_p2p_run_trace(*args, None, 0, C.byref(n))  # count
+    tr = np.zeros(n.value, TRACE_RECORD_DTYPE)
+    lib().nsref_p2p_run_trace(*args, tr.ctypes.data, n.value, C.byref(n))
+    return secs.value, (lts, luid, lctx), tr

@@ -13,6 +13,12 @@
 //   queue:     queue.cc:61-200, drop-tail-queue.cc:83-132
 //   IPv4:      ipv4-l3-protocol.cc:434-537 (Receive), :815-841 (IpForward: TTL), static next-hop routing
 //   UDP/sink:  udp-l4-protocol.cc:312-407 -> udp-socket-impl.cc:864-905 -> PacketSink (no events)
+//   echo:      udp-echo-client.cc (StartApplication, StopApplication, ScheduleTransmit, Send, HandleRead),
+//              udp-echo-server.cc (StartApplication, StopApplication, HandleRead -> SendTo)
+//   IPv4 id:   Ipv4L3Protocol::BuildHeader (ipv4-l3-protocol.cc): m_identification++ per originated packet
+//   traces:    the ascii default sinks hooked by PointToPointHelper::EnableAsciiInternal
+//              (point-to-point-helper.cc:113-219): Queue Enqueue/Dequeue/Drop (queue.cc:61-97,
+//              drop-tail-queue.cc:83-100), device MacRx (point-to-point-net-device.cc:304-346)
 // Packet sizes: payload + 8 (UDP) + 20 (IPv4) + 2 (PPP, added in PointToPointNetDevice::Send).
 #include <vector>
 #include <deque>
@@ -25,8 +31,8 @@
 namespace {
 
 struct Pkt {
-  uint32_t app;   // sending OnOff
-  uint32_t seq;
+  uint32_t app;   // sending application (| NSGPU_PKT_REPLY: an echo on its way back to this client)
+  uint32_t ipid;  // IPv4 identification (the sending node's m_identification)
   uint32_t size;  // current size in bytes (headers included as they are added)
   uint32_t ttl;
 };
@@ -48,7 +54,7 @@ struct App {
   uint64_t lastStartTime = 0;
   uint32_t residualBits = 0;
   uint32_t totBytes = 0;
-  uint32_t seq = 0;
+  uint32_t sent = 0;  // UdpEchoClient::m_sent
   nsgpu_app_counters c{};
 };
 
@@ -59,6 +65,36 @@ struct Model {
   std::vector<App> app;
   std::vector<std::vector<uint32_t>> node_apps;
   std::vector<int32_t> sink_of_node;
+  std::vector<uint32_t> node_ipid;  // Ipv4L3Protocol::m_identification
+  std::vector<nsgpu_trace_record> *trace = nullptr;
+  uint16_t tr_seq = 0;
+  uint32_t tr_uid = 0;
+  uint64_t tr_ts = ~0ull;
+  void tr(uint8_t kind, uint32_t d, const Pkt &p) {
+    if (!trace) return;
+    if (sim.m_currentUid != tr_uid || sim.m_currentTs != tr_ts) {  // a new dispatched event
+      tr_uid = sim.m_currentUid;
+      tr_ts = sim.m_currentTs;
+      tr_seq = 0;
+    }
+    nsgpu_trace_record r{};
+    r.ts = sim.m_currentTs;
+    r.uid = sim.m_currentUid;
+    r.seq = tr_seq++;
+    r.kind = kind;
+    r.dev = d;
+    r.app = p.app;
+    r.ipid = p.ipid;
+    r.size = p.size;
+    r.ttl = p.ttl;
+    trace->push_back(r);
+  }
+  uint32_t pkt_dst_node(const Pkt &p) const {
+    return (p.app & NSGPU_PKT_REPLY) ? s.app_node[p.app & ~NSGPU_PKT_REPLY] : s.app_dst_node[p.app];
+  }
+  uint32_t pkt_dst_slot(const Pkt &p) const {
+    return (p.app & NSGPU_PKT_REPLY) ? s.app_src_slot[p.app & ~NSGPU_PKT_REPLY] : s.app_dst_slot[p.app];
+  }
   uint64_t ttl_drops = 0, no_route_drops = 0, unreach_drops = 0;
 
   template <class F>
@@ -78,11 +114,13 @@ struct Model {
   bool enqueue(uint32_t d, const Pkt &p) {  // Queue::Enqueue -> DropTailQueue::DoEnqueue
     Dev &D = dev[d];
     if (D.q.size() >= s.dev_qmax[d]) {  // Drop (p): m_nTotalDroppedPackets++, bytes
+      tr(NSGPU_TR_DROP, d, p);
       D.c.drop_packets++;
       D.c.drop_bytes += p.size;
       return false;
     }
     D.q.push_back(p);
+    tr(NSGPU_TR_ENQUEUE, d, p);
     D.c.enq_packets++;
     D.c.enq_bytes += p.size;
     return true;
@@ -92,6 +130,7 @@ struct Model {
     if (D.q.empty()) return false;
     out = D.q.front();
     D.q.pop_front();
+    tr(NSGPU_TR_DEQUEUE, d, out);
     D.c.deq_packets++;
     return true;
   }
@@ -135,30 +174,35 @@ struct Model {
   void receive(uint32_t d, Pkt p) {  // :304-346 (no error model)
     dev[d].c.rx_packets++;
     p.size -= 2;  // ProcessHeader strips the PPP header
+    tr(NSGPU_TR_RX, d, p);  // m_macRxTrace
     ip_receive(s.dev_node[d], p);
   }
 
   // ---------------- IPv4 + UDP ----------------
   void ip_receive(uint32_t n, Pkt p) {  // Ipv4L3Protocol::Receive -> RouteInput
-    const uint32_t a = p.app;
-    if (s.app_dst_node[a] == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
-      const int32_t k = sink_of_node[n];
+    if (pkt_dst_node(p) == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
+      // the bound endpoint: the client's own socket for an echo reply, else the node's sink / echo server
+      const int32_t k = (p.app & NSGPU_PKT_REPLY) ? (int32_t)(p.app & ~NSGPU_PKT_REPLY) : sink_of_node[n];
       if (k < 0 || !app[k].sink_active) {  // no bound endpoint: RX_ENDPOINT_UNREACH
         unreach_drops++;
         return;
       }
       // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120)
-      const uint32_t bytes = p.size - 28;
-      sim.ScheduleNow(new Ev<std::function<void()>>([this, k, bytes]() {
-        // DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink::HandleRead
-        if (app[k].sink_active) {
-          app[k].c.rx_packets++;
-          app[k].c.rx_bytes += bytes;
+      sim.ScheduleNow(new Ev<std::function<void()>>([this, k, p, n]() {
+        // DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink / UdpEchoClient / UdpEchoServer::HandleRead
+        if (!app[k].sink_active) return;
+        app[k].c.rx_packets++;
+        app[k].c.rx_bytes += p.size - 28;
+        if (s.app_kind[k] == NSGPU_APP_ECHO_SERVER) {  // socket->SendTo (packet, 0, from)
+          Pkt r{p.app | NSGPU_PKT_REPLY, 0, p.size, s.app_ttl[k]};
+          app[k].c.tx_packets++;
+          app[k].c.tx_bytes += p.size - 28;
+          ip_send(n, r);
         }
       }));
       return;
     }
-    const uint32_t out = s.route[(uint64_t)n * s.n_dst + s.app_dst_slot[a]];
+    const uint32_t out = s.route[(uint64_t)n * s.n_dst + pkt_dst_slot(p)];
     if (out == 0xffffffffu) {  // DROP_NO_ROUTE
       no_route_drops++;
       return;
@@ -171,12 +215,13 @@ struct Model {
     }
     device_send(out, p);
   }
-  void ip_send(uint32_t n, const Pkt &p) {  // UdpSocketImpl::Send -> Ipv4L3Protocol::Send (RouteOutput)
-    const uint32_t out = s.route[(uint64_t)n * s.n_dst + s.app_dst_slot[p.app]];
+  void ip_send(uint32_t n, Pkt p) {  // UdpSocketImpl::DoSendTo (RouteOutput) -> Ipv4L3Protocol::Send
+    const uint32_t out = s.route[(uint64_t)n * s.n_dst + pkt_dst_slot(p)];
     if (out == 0xffffffffu) {
       no_route_drops++;
       return;
     }
+    p.ipid = node_ipid[n]++;  // BuildHeader: SetIdentification (m_identification++)
     device_send(out, p);
   }
 
@@ -223,7 +268,7 @@ struct Model {
   }
   void send_packet(uint32_t a) {  // :226-236
     App &A = app[a];
-    Pkt p{a, A.seq++, s.app_pkt_size[a] + 8 + 20, s.app_ttl[a]};
+    Pkt p{a, 0, s.app_pkt_size[a] + 8 + 20, s.app_ttl[a]};
     A.c.tx_packets++;
     A.c.tx_bytes += s.app_pkt_size[a];
     ip_send(s.app_node[a], p);
@@ -232,17 +277,38 @@ struct Model {
     A.residualBits = 0;
     schedule_next_tx(a);
   }
+  // ---------------- UdpEchoClient ----------------
+  void echo_send(uint32_t a) {  // UdpEchoClient::Send
+    App &A = app[a];
+    A.c.tx_packets++;
+    A.c.tx_bytes += s.app_pkt_size[a];
+    ip_send(s.app_node[a], Pkt{a, 0, s.app_pkt_size[a] + 8 + 20, s.app_ttl[a]});  // m_socket->Send (p)
+    ++A.sent;
+    if (A.sent < s.app_count[a])  // ScheduleTransmit (m_interval)
+      A.sendEvent = schedule(s.app_interval_ns[a], [this, a]() { echo_send(a); });
+  }
+
   void start_application(uint32_t a) {  // :132-150 (socket setup schedules nothing)
-    if (s.app_kind[a] == NSGPU_APP_SINK) {
+    if (s.app_kind[a] == NSGPU_APP_SINK || s.app_kind[a] == NSGPU_APP_ECHO_SERVER) {  // Bind (port)
       app[a].sink_active = true;
+      return;
+    }
+    if (s.app_kind[a] == NSGPU_APP_ECHO_CLIENT) {  // Bind, Connect, SetRecvCallback, ScheduleTransmit (0)
+      app[a].sink_active = true;
+      app[a].sendEvent = schedule(0, [this, a]() { echo_send(a); });
       return;
     }
     cancel_events(a);
     schedule_start_event(a);
   }
   void stop_application(uint32_t a) {  // :152-163
-    if (s.app_kind[a] == NSGPU_APP_SINK) {
+    if (s.app_kind[a] == NSGPU_APP_SINK || s.app_kind[a] == NSGPU_APP_ECHO_SERVER) {  // m_socket->Close ()
       app[a].sink_active = false;
+      return;
+    }
+    if (s.app_kind[a] == NSGPU_APP_ECHO_CLIENT) {  // Close; Simulator::Cancel (m_sendEvent)
+      app[a].sink_active = false;
+      cancel(app[a].sendEvent);
       return;
     }
     cancel_events(a);
@@ -263,9 +329,11 @@ struct Model {
     app.resize(s.n_apps);
     node_apps.assign(s.n_nodes, {});
     sink_of_node.assign(s.n_nodes, -1);
+    node_ipid.assign(s.n_nodes, 0);
     for (uint32_t a = 0; a < s.n_apps; a++) {
       node_apps[s.app_node[a]].push_back(a);
-      if (s.app_kind[a] == NSGPU_APP_SINK) sink_of_node[s.app_node[a]] = (int32_t)a;
+      if (s.app_kind[a] == NSGPU_APP_SINK || s.app_kind[a] == NSGPU_APP_ECHO_SERVER)
+        sink_of_node[s.app_node[a]] = (int32_t)a;
     }
     for (uint32_t i = 0; i < s.n_setup; i++) {
       const uint32_t k = s.setup_index[i];
@@ -294,10 +362,13 @@ struct Model {
 
 }  // namespace
 
-extern "C" int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
-                             nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
-                             uint64_t log_cap, double *run_seconds) {
+extern "C" int nsref_p2p_run_trace(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats,
+                                   nsgpu_dev_counters *devc, nsgpu_app_counters *appc, uint64_t *log_ts,
+                                   uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap, double *run_seconds,
+                                   nsgpu_trace_record *trace, uint64_t trace_cap, uint64_t *trace_n) {
   Model *m = new Model();
+  std::vector<nsgpu_trace_record> tv;
+  if (trace_n) m->trace = &tv;
   m->s = *sc;
   m->sim.want_digest = true;
   m->sim.log_ts = log_ts;
@@ -322,6 +393,17 @@ extern "C" int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stat
     for (uint32_t d = 0; d < sc->n_devices; d++) devc[d] = m->dev[d].c;
   if (appc)
     for (uint32_t a = 0; a < sc->n_apps; a++) appc[a] = m->app[a].c;
+  if (trace_n) {
+    *trace_n = tv.size();
+    for (uint64_t i = 0; i < tv.size() && i < trace_cap; i++) trace[i] = tv[i];
+  }
   delete m;
   return 0;
+}
+
+extern "C" int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
+                             nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
+                             uint64_t log_cap, double *run_seconds) {
+  return nsref_p2p_run_trace(sc, stats, devc, appc, log_ts, log_uid, log_ctx, log_cap, run_seconds, nullptr, 0,
+                             nullptr);
 }
