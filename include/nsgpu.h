@@ -177,6 +177,15 @@ int nsgpu_p2p_last_run_ms(nsgpu_p2p *h, double *gpu_ms);
 /* Launch mode of nsgpu_p2p_run: 0 = hipGraph replays (default), 1 = the same kernels launched one by
  * one (also selected by the environment variable NSGPU_P2P_EAGER; used under rocprofv3). */
 int nsgpu_p2p_set_eager(nsgpu_p2p *h, int eager);
+/* Ascii/pcap trace records (SURVEY 8(b) nsgpu_trace_drain; replaces the trace sinks that
+ * PointToPointHelper::EnableAsciiAll / EnablePcapAll hook, point-to-point-helper.cc:81-219 and
+ * trace-helper.cc:303-390): nsgpu_p2p_set_trace gives the engine a device buffer of `cap`
+ * nsgpu_trace_record (call before the first run; a group member before nsgpu_p2p_group_create);
+ * every run then records each Enqueue / Dequeue / Drop / MacRx sink call, unordered (trace order is
+ * (ts, uid, seq)).  nsgpu_p2p_trace_read copies up to `cap` records of the last run and sets *n to
+ * the number the run made (NSGPU_ENOMEM when that exceeds the buffer or `cap`). */
+int nsgpu_p2p_set_trace(nsgpu_p2p *h, uint64_t cap);
+int nsgpu_p2p_trace_read(nsgpu_p2p *h, nsgpu_trace_record *out, uint64_t cap, uint64_t *n, void *stream);
 /* The window pipeline's kernels: count and names (launch order). */
 int nsgpu_p2p_kernel_count(int *n);
 const char *nsgpu_p2p_kernel_name(int k);

@@ -63,8 +63,10 @@ constexpr int NWIN = 32;         // windows per graph replay
 constexpr uint32_t NOCTX = 0xffffffffu;
 constexpr uint32_t NOCHAIN = 0xffffffffu;
 
+// Packet descriptor: flow (sending app), IPv4 identification (Ipv4L3Protocol::m_identification of
+// the originating node), size in bytes with the headers added so far, IPv4 TTL.
 struct Pkt {
-  uint32_t app, seq, size, ttl;
+  uint32_t app, ipid, size, ttl;
 };
 
 // Reduction of a pending set: the next window's bound (atomicMin), the pending Stop.
@@ -111,7 +113,8 @@ struct P2PDev {
   Pkt *q_buf;
   nsgpu_dev_counters *devc;
   uint32_t *app_flags;    // bit0 started, bit1 sink active, bit2 send live, bit3 start/stop live
-  uint32_t *app_send_gen, *app_ss_gen, *app_residual, *app_tot, *app_seq;
+  uint32_t *app_send_gen, *app_ss_gen, *app_residual, *app_tot;
+  uint32_t *node_ipid;    // Ipv4L3Protocol::m_identification per node
   uint64_t *app_last_start;
   nsgpu_app_counters *appc;
   // pending pool (double-buffered SoA)
@@ -151,6 +154,10 @@ struct P2PDev {
   uint64_t *log_ts;
   uint32_t *log_uid, *log_ctx;
   uint64_t log_cap;
+  // ascii/pcap trace sink calls (nsgpu_p2p_set_trace; null: tracing off), unordered
+  nsgpu_trace_record *trace;
+  uint64_t trace_cap;
+  unsigned long long *trace_n;
 };
 
 // ---------------- wave / block helpers ----------------
@@ -215,6 +222,8 @@ struct Emit {
   Pkt *ch_pkt;
   const int64_t *lookahead;
   uint64_t tmn, wnd;
+  uint32_t uid;    // uid of the event being run (its trace records)
+  uint32_t trseq;  // trace sink calls made by it so far
   __device__ __forceinline__ void child(int64_t delay, uint32_t ctx_, uint32_t kind, uint32_t a, Pkt p) {
     const uint32_t s = slot0 + n++;
     const uint64_t ts = now + (uint64_t)delay;
@@ -246,6 +255,27 @@ struct HStat {
 // TransmitStart (:206-269) + PointToPointChannel::TransmitStart (point-to-point-channel.cc:82-103):
 //   Schedule (txTime + ifg, TransmitComplete); ScheduleWithContext (peer node, txTime + delay, Receive).
 enum : uint32_t { ACT_NONE = 0, ACT_SEND = 1, ACT_KICK = 2 };
+
+// One ascii trace sink call (AsciiTraceHelper::Default*SinkWithContext, trace-helper.cc:303-390, as
+// hooked by PointToPointHelper::EnableAsciiInternal, point-to-point-helper.cc:113-219): appended
+// unordered; the host orders the records by (ts, uid, seq).
+__device__ __forceinline__ void trace_call(const P2PDev &M, Emit &E, uint32_t kind, uint32_t d, const Pkt &p) {
+  if (!M.trace) return;
+  nsgpu_trace_record r;
+  r.ts = E.now;
+  r.uid = E.uid;
+  r.seq = (uint16_t)E.trseq++;
+  r.kind = (uint8_t)kind;
+  r.pad_ = 0;
+  r.dev = d;
+  r.app = p.app;
+  r.ipid = p.ipid;
+  r.size = p.size;
+  r.ttl = p.ttl;
+  r.pad2_ = 0;
+  const unsigned long long i = atomicAdd(M.trace_n, 1ull);
+  if (i < M.trace_cap) M.trace[i] = r;
+}
 struct Act {
   uint32_t op, dev;
   Pkt p;
@@ -269,9 +299,11 @@ __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &
     Pkt p = act.p;
     p.size += 2;  // PppHeader
     if (cnt >= qmax) {
+      trace_call(M, E, NSGPU_TR_DROP, d, p);  // Queue::Drop: m_traceDrop
       dc.drop_packets++;
       dc.drop_bytes += p.size;
     } else {
+      trace_call(M, E, NSGPU_TR_ENQUEUE, d, p);  // Queue::Enqueue: m_traceEnqueue
       dc.enq_packets++;
       dc.enq_bytes += p.size;
       if (busy == 0) {  // Enqueue + Dequeue: the head of the queue leaves at once
@@ -282,6 +314,7 @@ __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &
           tx = qb[head];
         }
         nhead = (head + 1) % M.qcap;
+        trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);  // Queue::Dequeue: m_traceDequeue
         dc.deq_packets++;
         go = true;
       } else {
@@ -295,6 +328,7 @@ __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &
       tx = qb[head];
       nhead = (head + 1) % M.qcap;
       ncnt = cnt - 1;
+      trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);
       dc.deq_packets++;
       go = true;
     }
@@ -449,7 +483,8 @@ __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kin
   if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive (ipv4-l3-protocol.cc:434-537)
     M.devc[a].rx_packets++;
     Pkt p = pkt;
-    p.size -= 2;
+    p.size -= 2;                             // ProcessHeader strips the PppHeader
+    trace_call(M, E, NSGPU_TR_RX, a, p);     // m_macRxTrace
     const uint32_t n = M.dev_node[a];
     if (M.app_dst_node[p.app] == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
       if (sink < 0 || !(M.app_flags[sink] & 2u)) {  // no bound endpoint: RX_ENDPOINT_UNREACH
@@ -477,12 +512,17 @@ __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kin
     } else {
       M.app_flags[a] = f & ~4u;
       const uint32_t sz = M.app_pkt_size[a];
-      Pkt p{a, M.app_seq[a]++, sz + 8 + 20, M.app_ttl[a]};
+      Pkt p{a, 0, sz + 8 + 20, M.app_ttl[a]};
       M.appc[a].tx_packets++;
       M.appc[a].tx_bytes += sz;
-      const uint32_t out = route_of(M, M.app_node[a], p);
-      if (out == 0xffffffffu) hs.no_route++;
-      else act = Act{ACT_SEND, out, p};
+      const uint32_t an = M.app_node[a];
+      const uint32_t out = route_of(M, an, p);  // UdpSocketImpl::DoSendTo: RouteOutput
+      if (out == 0xffffffffu) {
+        hs.no_route++;
+      } else {
+        p.ipid = M.node_ipid[an]++;  // Ipv4L3Protocol::BuildHeader: SetIdentification (m_identification++)
+        act = Act{ACT_SEND, out, p};
+      }
       M.app_tot[a] += sz;
       M.app_last_start[a] = E.now;
       M.app_residual[a] = 0;
@@ -995,6 +1035,8 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
       E.now = tmin + rel;
       E.slot0 = s * M.maxc;
       E.n = 0;
+      E.uid = (uint32_t)key;
+      E.trseq = 0;
       const bool own = s == i0;
       const uint32_t kw = own ? kind0 : M.wkind[s];
       const uint32_t ea = own ? a0 : M.wa[s];
@@ -1852,7 +1894,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.app_ss_gen, A));
   TRY(dalloc(h, &M.app_residual, A));
   TRY(dalloc(h, &M.app_tot, A));
-  TRY(dalloc(h, &M.app_seq, A));
+  TRY(dalloc(h, &M.node_ipid, N));
   TRY(dalloc(h, &M.app_last_start, A));
   TRY(dalloc(h, &M.appc, A));
   TRY(dalloc(h, &M.node_cnt, N));
@@ -2039,7 +2081,8 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.app_ss_gen, 0, A * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.app_residual, 0, A * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.app_tot, 0, A * sizeof(uint32_t), s));
-  NSGPU_HIP(hipMemsetAsync(M.app_seq, 0, A * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(M.node_ipid, 0, M.n_nodes * sizeof(uint32_t), s));
+  if (M.trace) NSGPU_HIP(hipMemsetAsync(M.trace_n, 0, sizeof(unsigned long long), s));
   NSGPU_HIP(hipMemsetAsync(M.app_last_start, 0, A * sizeof(uint64_t), s));
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
   NSGPU_HIP(hipMemsetAsync(M.node_cnt, 0, M.n_nodes * sizeof(uint32_t), s));
@@ -2185,6 +2228,49 @@ extern "C" int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset) {
   (void)out, (void)n, (void)reset;
   return set_error(NSGPU_ESTATE, "nsgpu_p2p_phase_read: library built without NSGPU_PHASE_PROF");
 #endif
+}
+
+// Trace sink records (ascii/pcap replay): a device buffer of `cap` records, cleared by every reset.
+// The kernels take the engine descriptor by value, so an instantiated graph is rebuilt.
+extern "C" int nsgpu_p2p_set_trace(nsgpu_p2p *h, uint64_t cap) {
+  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_trace: null");
+  if (h->M.trace) return set_error(NSGPU_ESTATE, "nsgpu_p2p_set_trace: tracing is already on");
+  if (cap == 0) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_trace: zero capacity");
+  nsgpu_trace_record *tb = nullptr;
+  unsigned long long *tn = nullptr;
+  int rc = dalloc(h, &tb, cap);
+  if (!rc) rc = dalloc(h, &tn, 1);
+  if (rc) return rc;
+  h->M.trace = tb;
+  h->M.trace_n = tn;
+  NSGPU_HIP(hipMemset(h->M.trace_n, 0, sizeof(unsigned long long)));
+  h->M.trace_cap = cap;
+  if (h->gexec) {
+    (void)hipGraphExecDestroy(h->gexec);
+    h->gexec = nullptr;
+  }
+  return NSGPU_OK;
+}
+
+// Copies the trace records of the last run (unordered; *n = how many the run made, which may exceed
+// both the buffer and `cap`: NSGPU_ENOMEM then).
+extern "C" int nsgpu_p2p_trace_read(nsgpu_p2p *h, nsgpu_trace_record *out, uint64_t cap, uint64_t *n, void *stream) {
+  if (!h || !n) return set_error(NSGPU_EINVAL, "nsgpu_p2p_trace_read: null");
+  if (!h->M.trace) return set_error(NSGPU_ESTATE, "nsgpu_p2p_trace_read: tracing is off (nsgpu_p2p_set_trace)");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long total = 0;
+  NSGPU_HIP(hipMemcpyAsync(&total, h->M.trace_n, sizeof(total), hipMemcpyDeviceToHost, s));
+  NSGPU_HIP(hipStreamSynchronize(s));
+  *n = total;
+  const uint64_t m = std::min<uint64_t>(std::min<uint64_t>(total, h->M.trace_cap), cap);
+  if (m && out) {
+    NSGPU_HIP(hipMemcpyAsync(out, h->M.trace, m * sizeof(nsgpu_trace_record), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+  }
+  if (total > h->M.trace_cap || (out && total > cap))
+    return set_error(NSGPU_ENOMEM, "nsgpu_p2p_trace_read: %llu records, buffer %llu", total,
+                     (unsigned long long)std::min<uint64_t>(h->M.trace_cap, cap));
+  return NSGPU_OK;
 }
 
 extern "C" int nsgpu_p2p_set_eager(nsgpu_p2p *h, int eager) {

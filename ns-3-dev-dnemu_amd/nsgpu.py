@@ -99,6 +99,8 @@ SIGNATURES = {
     "nsgpu_p2p_destroy": (C.c_int, [_vp]),
     "nsgpu_p2p_last_run_ms": (C.c_int, [_vp, C.POINTER(C.c_double)]),
     "nsgpu_p2p_set_eager": (C.c_int, [_vp, C.c_int]),
+    "nsgpu_p2p_set_trace": (C.c_int, [_vp, _u64]),
+    "nsgpu_p2p_trace_read": (C.c_int, [_vp, _vp, _u64, C.POINTER(C.c_uint64), _vp]),
     "nsgpu_p2p_phase_read": (C.c_int, [_vp, C.c_int, C.c_int]),
     "nsgpu_p2p_kernel_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nsgpu_p2p_kernel_name": (C.c_char_p, [C.c_int]),

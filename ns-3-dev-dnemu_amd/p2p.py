@@ -19,6 +19,11 @@ import numpy as np
 
 import nsgpu
 
+# nsgpu_trace_record (include/nsgpu_types.h): one ascii trace sink call
+TRACE_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("seq", "<u2"), ("kind", "u1"), ("pad_", "u1"),
+                               ("dev", "<u4"), ("app", "<u4"), ("ipid", "<u4"), ("size", "<u4"),
+                               ("ttl", "<u4"), ("pad2_", "<u4")])
+
 APP_ONOFF, APP_SINK, APP_ECHO_CLIENT, APP_ECHO_SERVER = 0, 1, 2, 3
 SENDERS = (APP_ONOFF, APP_ECHO_CLIENT)  # applications that originate datagrams towards app["dst"]
 SETUP_NODE, SETUP_DEVICE, SETUP_APP, SETUP_STOP, SETUP_UID, SETUP_NOOP = 0, 1, 2, 3, 4, 5
@@ -349,6 +354,19 @@ class Engine:
     def set_eager(self, eager=True):
         nsgpu.check(nsgpu.lib().nsgpu_p2p_set_eager(self.h, int(eager)))
 
+    def set_trace(self, cap):
+        """Record the ascii/pcap trace sink calls of every run (nsgpu_p2p_set_trace), up to `cap`."""
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_set_trace(self.h, int(cap)))
+        self.trace_cap = int(cap)
+
+    def trace(self):
+        """The last run's trace records (trace.TRACE_RECORD_DTYPE), unordered."""
+        n = C.c_uint64()
+        out = np.zeros(self.trace_cap, TRACE_RECORD_DTYPE)
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_trace_read(self.h, out.ctypes.data, self.trace_cap, C.byref(n),
+                                                     self.stream))
+        return out[:n.value]
+
     def profile(self, sample_every=4):
         """One full run with per-kernel HIP-event brackets (nsgpu_p2p_profile); returns
         {kernel name: (average ms per launch, bracketed launches)}."""
@@ -490,10 +508,13 @@ class LoopbackGroup:
     """Every partition of one scenario on this GPU (nsgpu_p2p_group_*): the partitioned algorithm
     with device-to-device copies in place of the RCCL collectives — its parity harness on one device."""
 
-    def __init__(self, scenario, nranks, owner=None, log_cap=0, pool_cap=0, stream=None):
+    def __init__(self, scenario, nranks, owner=None, log_cap=0, pool_cap=0, stream=None, trace_cap=0):
         self.owner = owner_blocks(scenario.n_nodes, nranks) if owner is None else np.asarray(owner, np.uint32)
         self.members = [DistEngine(scenario, self.owner, r, nranks, None, log_cap, pool_cap, stream)
                         for r in range(nranks)]
+        if trace_cap:
+            for m in self.members:
+                m.set_trace(trace_cap)
         self.stream = stream
         arr = (C.c_void_p * nranks)(*[m.h for m in self.members])
         h = C.c_void_p()
@@ -505,6 +526,10 @@ class LoopbackGroup:
 
     def launch(self):
         nsgpu.check(nsgpu.lib().nsgpu_p2p_group_run(self.h, self.stream))
+
+    def trace(self):
+        """Every partition's trace records (each rank records the sink calls of its own nodes)."""
+        return np.concatenate([m.trace() for m in self.members])
 
     def results(self, log_n=0):
         per = [m.results(log_n) for m in self.members]

@@ -29,9 +29,7 @@ import p2p
 
 TR_ENQUEUE, TR_DEQUEUE, TR_DROP, TR_RX = 0, 1, 2, 3
 PKT_REPLY = 0x80000000
-TRACE_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("seq", "<u2"), ("kind", "u1"), ("pad_", "u1"),
-                               ("dev", "<u4"), ("app", "<u4"), ("ipid", "<u4"), ("size", "<u4"),
-                               ("ttl", "<u4"), ("pad2_", "<u4")])  # nsgpu_trace_record
+TRACE_RECORD_DTYPE = p2p.TRACE_RECORD_DTYPE  # nsgpu_trace_record
 _CHAR = {TR_ENQUEUE: "+", TR_DEQUEUE: "-", TR_DROP: "d", TR_RX: "r"}
 _SOURCE = {TR_ENQUEUE: "TxQueue/Enqueue", TR_DEQUEUE: "TxQueue/Dequeue", TR_DROP: "TxQueue/Drop", TR_RX: "MacRx"}
 PPP_HDR = 2
