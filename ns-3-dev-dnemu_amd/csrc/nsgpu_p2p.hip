@@ -45,7 +45,8 @@ enum EvKind : uint32_t {
   K_RECEIVE = 10,       // PointToPointNetDevice::Receive
   K_STOP = 11,          // Simulator::Stop
   K_FWD_UP = 12,        // Ipv4EndPoint::DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink (zero-delay leaf)
-  K_NKINDS = 13
+  K_FWD_UP_Q = 13,      // DoForwardUp -> UdpEchoServer / UdpEchoClient::HandleRead (queued: it schedules)
+  K_NKINDS = 14
 };
 
 constexpr int WCAP = 4096;       // events per window
@@ -105,6 +106,8 @@ struct P2PDev {
   const int64_t *app_start, *app_stop;
   const uint64_t *app_rate;
   const double *app_on_s, *app_off_s;
+  const uint32_t *app_count, *app_src_slot;  // UdpEchoClient MaxPackets, route slot of its own node
+  const int64_t *app_interval;               // UdpEchoClient Interval
   const uint32_t *node_app_off, *node_app_list;  // CSR: apps of each node in AddApplication order
   const int32_t *sink_of_node;                    // PacketSink of each node (-1: none)
   int64_t lookahead[K_NKINDS];
@@ -428,8 +431,13 @@ __device__ __forceinline__ void schedule_stop_event(const P2PDev &M, Emit &E, ui
   E.child(seconds_to_ts(M.app_on_s[a]), E.ctx, K_STOP_SENDING | (g << 8), a, Pkt{0, 0, 0, 0});
 }
 __device__ __forceinline__ void stop_application(const P2PDev &M, uint32_t a, uint64_t now) {
-  if (M.app_kind[a] == NSGPU_APP_SINK) {
+  const uint32_t k = M.app_kind[a];
+  if (k == NSGPU_APP_SINK || k == NSGPU_APP_ECHO_SERVER) {  // m_socket->Close ()
     M.app_flags[a] &= ~2u;
+    return;
+  }
+  if (k == NSGPU_APP_ECHO_CLIENT) {  // UdpEchoClient::StopApplication: Close; Simulator::Cancel (m_sendEvent)
+    M.app_flags[a] &= ~(2u | 4u);
     return;
   }
   cancel_events(M, a, now);
@@ -467,8 +475,10 @@ __device__ __forceinline__ void appobj_start(const P2PDev &M, Emit &E, uint32_t 
 }
 
 // Ipv4 route lookup: the static next-hop device of node n towards the packet's destination.
+// An echo reply (NSGPU_PKT_REPLY) travels back to its client's node.
 __device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const Pkt &p) {
-  return M.route[(uint64_t)n * M.n_dst + M.app_dst_slot[p.app]];
+  const uint32_t slot = (p.app & NSGPU_PKT_REPLY) ? M.app_src_slot[p.app & ~NSGPU_PKT_REPLY] : M.app_dst_slot[p.app];
+  return M.route[(uint64_t)n * M.n_dst + slot];
 }
 
 // One event: the kind-specific first phase, then the device step, then a trailing child.  Returns
@@ -486,12 +496,19 @@ __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kin
     p.size -= 2;                             // ProcessHeader strips the PppHeader
     trace_call(M, E, NSGPU_TR_RX, a, p);     // m_macRxTrace
     const uint32_t n = M.dev_node[a];
-    if (M.app_dst_node[p.app] == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
-      if (sink < 0 || !(M.app_flags[sink] & 2u)) {  // no bound endpoint: RX_ENDPOINT_UNREACH
+    const bool reply = (p.app & NSGPU_PKT_REPLY) != 0;
+    const uint32_t fa = p.app & ~NSGPU_PKT_REPLY;
+    if ((reply ? M.app_node[fa] : M.app_dst_node[p.app]) == n) {
+      // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407): the bound endpoint is the
+      // client's own socket for an echo reply, else the node's PacketSink / UdpEchoServer
+      const int32_t k = reply ? (int32_t)fa : sink;
+      if (k < 0 || !(M.app_flags[k] & 2u)) {  // no bound endpoint: RX_ENDPOINT_UNREACH
         hs.unreach++;
       } else {
-        // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120)
-        E.child(0, E.ctx, K_FWD_UP, (uint32_t)sink, p);
+        // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120);
+        // run inline for a PacketSink, queued for the echo applications (their HandleRead schedules)
+        const bool q = reply || M.app_kind[k] == NSGPU_APP_ECHO_SERVER;
+        E.child(0, E.ctx, q ? K_FWD_UP_Q : K_FWD_UP, (uint32_t)k, p);
       }
     } else {
       const uint32_t out = route_of(M, n, p);
@@ -509,6 +526,27 @@ __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kin
     const uint32_t f = M.app_flags[a];
     if (!((f & 4u) && M.app_send_gen[a] == gen)) {
       cancelled = true;
+    } else if (M.app_kind[a] == NSGPU_APP_ECHO_CLIENT) {  // UdpEchoClient::Send (udp-echo-client.cc)
+      M.app_flags[a] = f & ~4u;
+      const uint32_t sz = M.app_pkt_size[a];
+      Pkt p{a, 0, sz + 8 + 20, M.app_ttl[a]};
+      M.appc[a].tx_packets++;
+      M.appc[a].tx_bytes += sz;
+      const uint32_t an = M.app_node[a];
+      const uint32_t out = route_of(M, an, p);  // m_socket->Send (p)
+      if (out == 0xffffffffu) {
+        hs.no_route++;
+      } else {
+        p.ipid = M.node_ipid[an]++;
+        act = Act{ACT_SEND, out, p};
+      }
+      const uint32_t sent = ++M.app_tot[a];  // ++m_sent
+      if (sent < M.app_count[a]) {           // ScheduleTransmit (m_interval)
+        const uint32_t g = (M.app_send_gen[a] + 1) & 0xffffffu;
+        M.app_send_gen[a] = g;
+        M.app_flags[a] |= 4u;
+        post = Post{true, M.app_interval[a], K_SEND | (g << 8), a};
+      }
     } else {
       M.app_flags[a] = f & ~4u;
       const uint32_t sz = M.app_pkt_size[a];
@@ -537,8 +575,14 @@ __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kin
         appobj_start(M, E, a);
         break;
       case K_APP_START:
-        if (M.app_kind[a] == NSGPU_APP_SINK) {
+        if (M.app_kind[a] == NSGPU_APP_SINK || M.app_kind[a] == NSGPU_APP_ECHO_SERVER) {  // Bind (port)
           M.app_flags[a] |= 2u;
+        } else if (M.app_kind[a] == NSGPU_APP_ECHO_CLIENT) {
+          // UdpEchoClient::StartApplication: Bind, Connect, SetRecvCallback, ScheduleTransmit (Seconds (0))
+          const uint32_t g = (M.app_send_gen[a] + 1) & 0xffffffu;
+          M.app_send_gen[a] = g;
+          M.app_flags[a] |= 2u | 4u;
+          E.child(0, E.ctx, K_SEND | (g << 8), a, Pkt{0, 0, 0, 0});
         } else {
           cancel_events(M, a, E.now);
           schedule_start_event(M, E, a);
@@ -576,6 +620,25 @@ __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kin
         if (M.app_flags[a] & 2u) {
           M.appc[a].rx_packets++;
           M.appc[a].rx_bytes += pkt.size - 28;
+        }
+        break;
+      case K_FWD_UP_Q:  // DoForwardUp -> UdpSocketImpl::ForwardUp -> UdpEcho{Server,Client}::HandleRead (a = endpoint app)
+        if (M.app_flags[a] & 2u) {
+          M.appc[a].rx_packets++;
+          M.appc[a].rx_bytes += pkt.size - 28;
+          if (M.app_kind[a] == NSGPU_APP_ECHO_SERVER) {  // socket->SendTo (packet, 0, from)
+            Pkt r{pkt.app | NSGPU_PKT_REPLY, 0, pkt.size, M.app_ttl[a]};
+            M.appc[a].tx_packets++;
+            M.appc[a].tx_bytes += pkt.size - 28;
+            const uint32_t an = M.app_node[a];
+            const uint32_t out = route_of(M, an, r);
+            if (out == 0xffffffffu) {
+              hs.no_route++;
+            } else {
+              r.ipid = M.node_ipid[an]++;
+              act = Act{ACT_SEND, out, r};
+            }
+          }
         }
         break;
       case K_STOP:
@@ -1809,13 +1872,30 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   std::vector<uint32_t> napps(N + 1, 0);
   std::vector<int32_t> sink(N, -1);
   uint32_t min_pkt = 0xffffffffu;
+  bool has_echo = false;
+  int64_t echo_ivl = (int64_t)1 << 61;
   for (uint32_t a = 0; a < A; a++) {
     if (sc->app_node[a] >= N) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: app %u: bad node", a);
     napps[sc->app_node[a] + 1]++;
-    if (sc->app_kind[a] == NSGPU_APP_SINK) {
+    const uint32_t ak = sc->app_kind[a];
+    if (ak == NSGPU_APP_SINK || ak == NSGPU_APP_ECHO_SERVER) {  // the node's bound UDP endpoint
       if (sink[sc->app_node[a]] >= 0)
-        return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: node %u has two PacketSinks", sc->app_node[a]);
+        return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: node %u has two bound endpoints", sc->app_node[a]);
       sink[sc->app_node[a]] = (int32_t)a;
+      if (ak == NSGPU_APP_ECHO_SERVER) {
+        if (sc->app_ttl[a] == 0) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: UdpEchoServer %u: ttl", a);
+        has_echo = true;
+      }
+    } else if (ak == NSGPU_APP_ECHO_CLIENT) {
+      if (!sc->app_count || !sc->app_interval_ns || !sc->app_src_slot || sc->app_dst_node[a] >= N ||
+          sc->app_dst_slot[a] >= sc->n_dst || sc->app_src_slot[a] >= sc->n_dst || sc->app_pkt_size[a] == 0 ||
+          sc->app_ttl[a] == 0 || sc->app_dst_node[a] == sc->app_node[a] || sc->app_interval_ns[a] < 0)
+        return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: UdpEchoClient %u: bad destination/size/ttl/interval", a);
+      has_echo = true;
+      min_pkt = std::min(min_pkt, sc->app_pkt_size[a]);
+      echo_ivl = std::min(echo_ivl, sc->app_interval_ns[a]);
+    } else if (ak != NSGPU_APP_ONOFF) {
+      return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: app %u: unknown kind %u", a, ak);
     } else {
       if (sc->app_dst_node[a] >= N || sc->app_dst_slot[a] >= sc->n_dst || sc->app_rate_bps[a] == 0 ||
           sc->app_pkt_size[a] == 0 || sc->app_ttl[a] == 0 || sc->app_dst_node[a] == sc->app_node[a])
@@ -1855,9 +1935,14 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   M.lookahead[K_APP_START] = 0;      // StartSending after OffTime (may be 0)
   M.lookahead[K_START_SENDING] = 0;  // first send after residual-shortened interval
   M.lookahead[K_STOP_SENDING] = 0;   // StartSending after OffTime
-  M.lookahead[K_SEND] = std::min(tx_min, send_ivl);
+  M.lookahead[K_SEND] = std::min(std::min(tx_min, send_ivl), echo_ivl);
   M.lookahead[K_TX_COMPLETE] = tx_min;
   M.lookahead[K_RECEIVE] = tx_min;
+  M.lookahead[K_FWD_UP_Q] = tx_min;  // UdpEchoServer reply: device children
+  // A datagram for a UDP echo endpoint is delivered by a queued zero-delay DoForwardUp (its handler
+  // schedules): the window must then end at the delivering Receive's time, so that the DoForwardUp is
+  // the next window's first event at that time.
+  if (has_echo) M.lookahead[K_RECEIVE] = 0;
   // ---- scenario upload ----
   TRY(dupload(h, &M.dev_node, sc->dev_node, D));
   TRY(dupload(h, &M.dev_peer, sc->dev_peer, D));
@@ -1878,6 +1963,19 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dupload(h, &M.app_rate, sc->app_rate_bps, A));
   TRY(dupload(h, &M.app_on_s, sc->app_on_s, A));
   TRY(dupload(h, &M.app_off_s, sc->app_off_s, A));
+  {
+    std::vector<uint32_t> cnt(A, 0), src(A, 0);
+    std::vector<int64_t> ivl(A, 0);
+    for (uint32_t a = 0; a < A; a++)
+      if (sc->app_kind[a] == NSGPU_APP_ECHO_CLIENT) {
+        cnt[a] = sc->app_count[a];
+        ivl[a] = sc->app_interval_ns[a];
+        src[a] = sc->app_src_slot[a];
+      }
+    TRY(dupload(h, &M.app_count, cnt.data(), A));
+    TRY(dupload(h, &M.app_interval, ivl.data(), A));
+    TRY(dupload(h, &M.app_src_slot, src.data(), A));
+  }
   TRY(dupload(h, &M.node_app_off, napps.data(), N + 1));
   TRY(dupload(h, &M.node_app_list, node_list.data(), A));
   const int32_t *sinkp;

@@ -90,3 +90,101 @@ def test_partitioned_trace_union(nranks):
     grp = p2p.LoopbackGroup(g, nranks, trace_cap=len(otr) + 16)
     grp.run()
     assert_same_trace(g, otr, trace.sort_records(grp.trace()))
+
+
+# ---------------------------------------------------------------- UDP echo (config 1: first.cc)
+def gpu_full(sc, log_cap, trace_cap):
+    eng = p2p.Engine(sc, log_cap=log_cap)
+    eng.set_trace(trace_cap)
+    st, devc, appc, log = eng.run(log_n=log_cap)
+    return st, devc, appc, log, trace.sort_records(eng.trace())
+
+
+def oracle_full(sc, log_cap):
+    s = sc.c_struct()
+    st = p2p.P2PStats()
+    devc = np.zeros(s.n_devices, p2p.DEV_COUNTERS_DTYPE)
+    appc = np.zeros(s.n_apps, p2p.APP_COUNTERS_DTYPE)
+    _secs, log, tr = nsref.p2p_run_trace(s, st, devc, appc, log_cap)
+    return st, devc, appc, log, trace.sort_records(tr)
+
+
+def assert_same_run(sc, o, g):
+    st, devc, appc, olog, otr = o
+    gst, gdevc, gappc, glog, gtr = g
+    for f in ("dispatched", "cancelled", "digest", "final_ts", "next_uid", "ttl_drops", "no_route_drops"):
+        assert getattr(gst, f) == getattr(st, f), (f, getattr(gst, f), getattr(st, f))
+    assert np.array_equal(gdevc, devc)
+    assert np.array_equal(gappc, appc)
+    n = int(min(st.dispatched, len(olog[0])))
+    for a, b, name in zip(glog, olog, ("ts", "uid", "ctx")):
+        assert np.array_equal(a[:n], b[:n]), name
+    assert_same_trace(sc, otr, gtr)
+
+
+def test_first_cc_on_gpu_matches_reference_md5s():
+    """examples/tutorial/first.cc on the GPU engine: the 19 events of the reference run and its
+    ascii / pcap files byte for byte (md5s recorded from the unmodified reference)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "survey_reference_runs.json")) as f:
+        ref = json.load(f)["first_cc"]
+    sc = p2p.first_cc()
+    o = oracle_full(sc, 64)
+    g = gpu_full(sc, 64, 64)
+    assert_same_run(sc, o, g)
+    gst, _gdevc, gappc, _glog, gtr = g
+    assert gst.dispatched == ref["events_dispatched"] == 19
+    assert int(gappc["rx_packets"].sum()) == ref["received_lines"]
+    codec = trace.Codec(sc)
+    assert hashlib.md5(codec.ascii(gtr).encode()).hexdigest() == ref["ascii_md5"]
+    pc = codec.pcaps(gtr)
+    assert hashlib.md5(pc[(0, 0)]).hexdigest() == ref["node0_pcap_md5"]
+    assert hashlib.md5(pc[(1, 0)]).hexdigest().startswith(ref["node1_pcap_md5_prefix"])
+
+
+def test_echo_count_interval_and_stop_cancel_gpu():
+    sc = p2p.Scenario(2)
+    da, db = sc.link(0, 1, 5_000_000, 2_000_000)
+    sc.install_stack()
+    sc.assign_link(da, db, p2p.ip("10.1.1.0"))
+    sc.add_echo_server(1, 1_000_000_000, 10_000_000_000)
+    sc.add_echo_client(0, 1, 2_000_000_000, 2_600_000_000, count=3, interval_ns=500_000_000,
+                       remote_addr=sc.dev_addr[db])
+    sc.route_bfs()
+    o = oracle_full(sc, 256)
+    assert o[0].cancelled == 1
+    assert_same_run(sc, o, gpu_full(sc, 256, 256))
+
+
+def echo_grid(rows, cols, interval_ns, count, qmax=100):
+    """A grid with UdpEchoServers on the bottom row and UdpEchoClients on the top row (one pair per
+    column, diagonal partner), plus the column OnOff flows' PacketSinks replaced by the servers."""
+    g = p2p.grid(rows, cols, qmax=qmax, flows=[])
+    for c in range(cols):
+        g.add_echo_server((rows - 1) * cols + c, 50_000_000, 900_000_000)
+    for c in range(cols):
+        dst = (rows - 1) * cols + (cols - 1 - c)
+        g.add_echo_client(c, dst, 100_000_000 + 1_000_000 * c, 800_000_000, count=count, interval_ns=interval_ns,
+                          size=512)
+    g.route_bfs()
+    return g
+
+
+@pytest.mark.parametrize("interval_ns,count,qmax", [(200_000_000, 3, 100), (300_000, 40, 4)])
+def test_echo_grid(interval_ns, count, qmax):
+    g = echo_grid(4, 4, interval_ns, count, qmax)
+    o = oracle_full(g, 100000)
+    assert o[2]["rx_packets"].sum() > 0
+    if qmax == 4:
+        assert o[1]["drop_packets"].sum() > 0
+    assert_same_run(g, o, gpu_full(g, 100000, 200000))
+
+
+@pytest.mark.parametrize("nranks", [2])
+def test_echo_grid_partitioned(nranks):
+    g = echo_grid(4, 4, 300_000, 40, 4)
+    _st, _devc, _appc, _log, otr = oracle_full(g, 0)
+    grp = p2p.LoopbackGroup(g, nranks, trace_cap=len(otr) + 16)
+    grp.run()
+    assert_same_trace(g, otr, trace.sort_records(grp.trace()))
