@@ -235,6 +235,73 @@ def first_cc():
     return sc
 
 
+def dumbbell(n_leaves=4, leaf_bps=1_000_000, leaf_delay_ns=2_000_000, router_bps=5_000_000,
+             router_delay_ns=5_000_000, qmax=100, rate_bps=1_000_000, size=512, max_bytes=512,
+             start_ns=1_000_000_000, stop_ns=5_000_000_000, sim_stop_ns=5_000_000_000):
+    """src/mpi/examples/simple-distributed.cc (config 5) with n_leaves leaves per side: left leaves
+    (system id 0), router 1 (0), router 2 (1), right leaves (1); routers 5Mbps/5ms, leaves 1Mbps/2ms;
+    PacketSinks (port 50000) on the right leaves and OnOff (OnTime 1, OffTime 0, 1Mbps, 512 B,
+    MaxBytes 512) from left leaf i to right leaf i, all from 1 s to 5 s; Simulator::Stop (5 s).
+    Routes: the dumbbell's unique shortest paths (what the example's global / nix-vector routing
+    finds), written directly.  Returns the scenario; `dumbbell_owner` gives the example's system ids."""
+    n = n_leaves
+    sc = Scenario(0)
+    for _ in range(n):  # leftLeafNodes.Create (n, 0)
+        sc.add_node()
+    r1, r2 = sc.add_node(), sc.add_node()  # CreateObject<Node> (0), CreateObject<Node> (1)
+    for _ in range(n):  # rightLeafNodes.Create (n, 1)
+        sc.add_node()
+    left = lambda i: i  # noqa: E731
+    right = lambda i: n + 2 + i  # noqa: E731
+    ra, rb = sc.link(r1, r2, router_bps, router_delay_ns, qmax)  # routerLink.Install (routerNodes)
+    lleaf, lrout, rleaf, rrout = [], [], [], []
+    for i in range(n):
+        da, db = sc.link(left(i), r1, leaf_bps, leaf_delay_ns, qmax)
+        lleaf.append(da)
+        lrout.append(db)
+    for i in range(n):
+        da, db = sc.link(right(i), r2, leaf_bps, leaf_delay_ns, qmax)
+        rleaf.append(da)
+        rrout.append(db)
+    sc.install_stack()  # stack.InstallAll ()
+    sc.assign_link(ra, rb, ip("10.2.1.0"))
+    for i in range(n):  # leftAddress 10.1.1.0 + NewNetwork per leaf
+        sc.assign_link(lleaf[i], lrout[i], ip("10.1.1.0") + (i << 8))
+    for i in range(n):
+        sc.assign_link(rleaf[i], rrout[i], ip("10.3.1.0") + (i << 8))
+    for i in range(n):  # sinkHelper.Install (rightLeafNodes.Get (i)); Start (1 s), Stop (5 s)
+        sc.add_sink(right(i), start_ns, stop_ns, port=50000)
+    for i in range(n):
+        sc.add_onoff(left(i), right(i), start_ns, stop_ns, rate_bps=rate_bps, size=size, on_s=1.0, off_s=0.0,
+                     max_bytes=max_bytes, remote_addr=sc.dev_addr[rleaf[i]], remote_port=50000)
+    sc.stop(sim_stop_ns)
+    dsts = sc._slot_nodes()
+    sc.dst_slot = {d: k for k, d in enumerate(dsts)}
+    sc.n_dst = max(1, len(dsts))
+    R = np.full((sc.n_nodes, sc.n_dst), NO_ROUTE, dtype=np.uint32)
+    for d, k in sc.dst_slot.items():
+        j = d - (n + 2)
+        R[:n, k] = lleaf            # left leaf -> its router
+        R[r1, k] = ra               # router 1 -> router 2
+        R[r2, k] = rrout[j]         # router 2 -> right leaf j
+        R[n + 2:, k] = rleaf        # other right leaves -> router 2
+        R[d, k] = NO_ROUTE          # (local delivery)
+    sc.route = R
+    return sc
+
+
+def dumbbell_owner(n_leaves, nranks=2):
+    """Node (systemId) of simple-distributed.cc: left side + router 1 on 0, router 2 + right side on 1
+    (nranks > 2: the right side's leaves spread over ranks 1..nranks-1 in contiguous blocks)."""
+    n = n_leaves
+    own = np.zeros(2 * n + 2, np.uint32)
+    own[n + 1:] = 1
+    if nranks > 2:
+        blk = -(-n // (nranks - 1))
+        own[n + 2:] = 1 + np.arange(n) // blk
+    return own
+
+
 def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="columns", start_ns=100_000_000,
          stop_ns=2_000_000_000, sim_stop_ns=2_100_000_000, rate_bps=500_000, size=512, on_s=1e9, off_s=0.0,
          ttl=255, n_flows=None):
