@@ -127,6 +127,14 @@ typedef struct nsgpu_p2p_scenario {
   const uint32_t *app_count;
   const int64_t  *app_interval_ns;
   const uint32_t *app_src_slot;
+  /* Compressed next-hop table, used when `route` is NULL (large topologies: the dense table is
+   * n_nodes x n_dst): node n forwards towards slot k through route_exc_dev[j] for the j in
+   * [route_exc_off[n], route_exc_off[n + 1]) with route_exc_slot[j] == k (slots ascending within a
+   * node), else through route_default[n] (0xffffffff: no route). */
+  const uint32_t *route_default;   /* n_nodes */
+  const uint64_t *route_exc_off;   /* n_nodes + 1 */
+  const uint32_t *route_exc_slot;
+  const uint32_t *route_exc_dev;
 } nsgpu_p2p_scenario;
 
 /* Packet descriptor flag: the datagram is an echo reply travelling back to its client (app). */

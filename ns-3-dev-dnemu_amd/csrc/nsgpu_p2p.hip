@@ -101,7 +101,9 @@ struct P2PDev {
   const uint32_t *dev_node, *dev_peer, *dev_qmax;
   const uint64_t *dev_bps;
   const int64_t *dev_ifg, *dev_delay;
-  const uint32_t *route;
+  const uint32_t *route;  // dense [node][slot], or null: the compressed table below
+  const uint32_t *route_def, *route_exc_slot, *route_exc_dev;
+  const uint64_t *route_exc_off;
   const uint32_t *app_kind, *app_node, *app_dst_node, *app_dst_slot, *app_pkt_size, *app_max_bytes, *app_ttl;
   const int64_t *app_start, *app_stop;
   const uint64_t *app_rate;
@@ -478,7 +480,16 @@ __device__ __forceinline__ void appobj_start(const P2PDev &M, Emit &E, uint32_t 
 // An echo reply (NSGPU_PKT_REPLY) travels back to its client's node.
 __device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const Pkt &p) {
   const uint32_t slot = (p.app & NSGPU_PKT_REPLY) ? M.app_src_slot[p.app & ~NSGPU_PKT_REPLY] : M.app_dst_slot[p.app];
-  return M.route[(uint64_t)n * M.n_dst + slot];
+  if (M.route) return M.route[(uint64_t)n * M.n_dst + slot];
+  // compressed: binary search of the node's exceptions (a dumbbell router holds one per leaf)
+  const uint64_t e1 = M.route_exc_off[n + 1];
+  uint64_t lo = M.route_exc_off[n], hi = e1;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (M.route_exc_slot[mid] < slot) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < e1 && M.route_exc_slot[lo] == slot) ? M.route_exc_dev[lo] : M.route_def[n];
 }
 
 // One event: the kind-specific first phase, then the device step, then a trailing child.  Returns
@@ -1869,6 +1880,22 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     for (uint32_t n = 0; n < N; n++)
       if (owner[n] >= (uint32_t)nranks) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: node %u: owner %u", n, owner[n]);
   }
+  if (!sc->route) {  // compressed next-hop table
+    if (!sc->route_default || !sc->route_exc_off || !sc->route_exc_slot || !sc->route_exc_dev ||
+        sc->route_exc_off[0] != 0)
+      return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: no route table");
+    for (uint32_t n = 0; n < N; n++) {
+      if (sc->route_exc_off[n + 1] < sc->route_exc_off[n])
+        return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: route_exc_off not ascending at node %u", n);
+      if (sc->route_default[n] != 0xffffffffu && sc->route_default[n] >= D)
+        return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: node %u: bad default route", n);
+      for (uint64_t j = sc->route_exc_off[n]; j < sc->route_exc_off[n + 1]; j++)
+        if ((j > sc->route_exc_off[n] && sc->route_exc_slot[j] <= sc->route_exc_slot[j - 1]) ||
+            sc->route_exc_slot[j] >= sc->n_dst || (sc->route_exc_dev[j] != 0xffffffffu && sc->route_exc_dev[j] >= D))
+          return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: node %u: bad route exception %llu", n,
+                           (unsigned long long)j);
+    }
+  }
   std::vector<uint32_t> napps(N + 1, 0);
   std::vector<int32_t> sink(N, -1);
   uint32_t min_pkt = 0xffffffffu;
@@ -1950,7 +1977,15 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dupload(h, &M.dev_bps, sc->dev_bps, D));
   TRY(dupload(h, &M.dev_ifg, sc->dev_ifg_ns, D));
   TRY(dupload(h, &M.dev_delay, sc->dev_delay_ns, D));
-  TRY(dupload(h, &M.route, sc->route, (size_t)N * sc->n_dst));
+  if (sc->route) {
+    TRY(dupload(h, &M.route, sc->route, (size_t)N * sc->n_dst));
+  } else {
+    const uint64_t ne = sc->route_exc_off[N];
+    TRY(dupload(h, &M.route_def, sc->route_default, N));
+    TRY(dupload(h, &M.route_exc_off, sc->route_exc_off, N + 1));
+    TRY(dupload(h, &M.route_exc_slot, sc->route_exc_slot, ne));
+    TRY(dupload(h, &M.route_exc_dev, sc->route_exc_dev, ne));
+  }
   TRY(dupload(h, &M.app_kind, sc->app_kind, A));
   TRY(dupload(h, &M.app_node, sc->app_node, A));
   TRY(dupload(h, &M.app_dst_node, sc->app_dst_node, A));

@@ -42,6 +42,8 @@ class ScenarioStruct(C.Structure):
         ("stop_ns", C.c_int64), ("n_setup", C.c_uint32), ("pad_", C.c_uint32),
         ("setup_kind", C.c_void_p), ("setup_index", C.c_void_p),
         ("app_count", C.c_void_p), ("app_interval_ns", C.c_void_p), ("app_src_slot", C.c_void_p),
+        ("route_default", C.c_void_p), ("route_exc_off", C.c_void_p), ("route_exc_slot", C.c_void_p),
+        ("route_exc_dev", C.c_void_p),
     ]
 
 
@@ -69,6 +71,7 @@ class Scenario:
         self.setup = []   # (kind, index)
         self.stop_ns = -1
         self.route = None
+        self.route_c = None  # compressed next hops: (default[n], exc_off[n+1], exc_slot, exc_dev)
         self.n_dst = 0
         self.dst_slot = {}
         # addressing (host side only: the trace codec prints it, the engines never read it)
@@ -176,6 +179,14 @@ class Scenario:
                 R[n, slot] = best
         self.route = R
 
+    def next_hop(self, n, slot):
+        if self.route is not None:
+            return int(self.route[n, slot])
+        dflt, off, es, ed = self.route_c
+        lo, hi = int(off[n]), int(off[n + 1])
+        j = lo + int(np.searchsorted(es[lo:hi], slot))
+        return int(ed[j]) if j < hi and es[j] == slot else int(dflt[n])
+
     # ---------------- C view ----------------
     def c_struct(self):
         dev = np.array(self.dev, dtype=np.int64).reshape(-1, 6) if self.dev else np.zeros((0, 6), np.int64)
@@ -184,7 +195,8 @@ class Scenario:
             dev_node=dev[:, 0].astype(np.uint32), dev_peer=dev[:, 1].astype(np.uint32),
             dev_bps=dev[:, 2].astype(np.uint64), dev_ifg_ns=dev[:, 3].astype(np.int64),
             dev_delay_ns=dev[:, 4].astype(np.int64), dev_qmax=dev[:, 5].astype(np.uint32),
-            route=np.ascontiguousarray(self.route, dtype=np.uint32),
+            route=(np.ascontiguousarray(self.route, dtype=np.uint32) if self.route is not None
+                   else np.zeros(0, np.uint32)),
             app_kind=np.array([a["kind"] for a in A], np.uint32),
             app_node=np.array([a["node"] for a in A], np.uint32),
             app_start_ns=np.array([a["start"] for a in A], np.int64),
@@ -205,6 +217,12 @@ class Scenario:
             setup_kind=np.array([k for k, _ in self.setup], np.uint32),
             setup_index=np.array([i for _, i in self.setup], np.uint32),
         )
+        if self.route is None:
+            dflt, off, es, ed = self.route_c
+            arrays.update(route_default=np.ascontiguousarray(dflt, np.uint32),
+                          route_exc_off=np.ascontiguousarray(off, np.uint64),
+                          route_exc_slot=np.ascontiguousarray(es, np.uint32),
+                          route_exc_dev=np.ascontiguousarray(ed, np.uint32))
         s = ScenarioStruct()
         s.n_nodes, s.n_devices, s.n_apps, s.n_dst = self.n_nodes, len(self.dev), len(A), self.n_dst
         for k, v in arrays.items():
@@ -237,7 +255,7 @@ def first_cc():
 
 def dumbbell(n_leaves=4, leaf_bps=1_000_000, leaf_delay_ns=2_000_000, router_bps=5_000_000,
              router_delay_ns=5_000_000, qmax=100, rate_bps=1_000_000, size=512, max_bytes=512,
-             start_ns=1_000_000_000, stop_ns=5_000_000_000, sim_stop_ns=5_000_000_000):
+             start_ns=1_000_000_000, stop_ns=5_000_000_000, sim_stop_ns=5_000_000_000, compressed=None):
     """src/mpi/examples/simple-distributed.cc (config 5) with n_leaves leaves per side: left leaves
     (system id 0), router 1 (0), router 2 (1), right leaves (1); routers 5Mbps/5ms, leaves 1Mbps/2ms;
     PacketSinks (port 50000) on the right leaves and OnOff (OnTime 1, OffTime 0, 1Mbps, 512 B,
@@ -278,6 +296,21 @@ def dumbbell(n_leaves=4, leaf_bps=1_000_000, leaf_delay_ns=2_000_000, router_bps
     dsts = sc._slot_nodes()
     sc.dst_slot = {d: k for k, d in enumerate(dsts)}
     sc.n_dst = max(1, len(dsts))
+    if compressed is None:
+        compressed = sc.n_nodes * sc.n_dst > (1 << 24)
+    if compressed:
+        # every node has one way out except router 2 (one exception per right leaf = slot j) and the
+        # right leaves (their own slot: local delivery, never looked up)
+        dflt = np.full(sc.n_nodes, NO_ROUTE, np.uint32)
+        dflt[:n] = lleaf
+        dflt[r1] = ra
+        dflt[n + 2:] = rleaf
+        cnt = np.zeros(sc.n_nodes, np.uint64)
+        cnt[r2] = n
+        off = np.zeros(sc.n_nodes + 1, np.uint64)
+        off[1:] = np.cumsum(cnt)
+        sc.route_c = (dflt, off, np.arange(n, dtype=np.uint32), np.asarray(rrout, np.uint32))
+        return sc
     R = np.full((sc.n_nodes, sc.n_dst), NO_ROUTE, dtype=np.uint32)
     for d, k in sc.dst_slot.items():
         j = d - (n + 2)

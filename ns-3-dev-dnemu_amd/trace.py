@@ -80,11 +80,10 @@ class Codec:
         self.first_addr = {}
         for d in sorted(self.ifindex, key=lambda d: self.ifindex[d]):
             self.first_addr.setdefault(self.dev_node[d], sc.dev_addr.get(d, 0))
-        self.route = sc.route
         self.slot = sc.dst_slot
 
     def _out_addr(self, node, dst_node):
-        d = int(self.route[node, self.slot[dst_node]])
+        d = int(self.sc.next_hop(node, self.slot[dst_node]))
         return self.sc.dev_addr.get(d, 0)
 
     def headers(self, app_word):

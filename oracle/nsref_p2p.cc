@@ -92,6 +92,19 @@ struct Model {
   uint32_t pkt_dst_node(const Pkt &p) const {
     return (p.app & NSGPU_PKT_REPLY) ? s.app_node[p.app & ~NSGPU_PKT_REPLY] : s.app_dst_node[p.app];
   }
+  // static next hop of node n towards route slot k: the dense table, or the compressed one
+  // (per-node default + ascending (slot, device) exceptions; include/nsgpu_types.h)
+  uint32_t next_hop(uint32_t n, uint32_t k) const {
+    if (s.route) return s.route[(uint64_t)n * s.n_dst + k];
+    uint64_t lo = s.route_exc_off[n], hi = s.route_exc_off[n + 1];
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (s.route_exc_slot[mid] < k) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < s.route_exc_off[n + 1] && s.route_exc_slot[lo] == k) return s.route_exc_dev[lo];
+    return s.route_default[n];
+  }
   uint32_t pkt_dst_slot(const Pkt &p) const {
     return (p.app & NSGPU_PKT_REPLY) ? s.app_src_slot[p.app & ~NSGPU_PKT_REPLY] : s.app_dst_slot[p.app];
   }
@@ -202,7 +215,7 @@ struct Model {
       }));
       return;
     }
-    const uint32_t out = s.route[(uint64_t)n * s.n_dst + pkt_dst_slot(p)];
+    const uint32_t out = next_hop(n, pkt_dst_slot(p));
     if (out == 0xffffffffu) {  // DROP_NO_ROUTE
       no_route_drops++;
       return;
@@ -216,7 +229,7 @@ struct Model {
     device_send(out, p);
   }
   void ip_send(uint32_t n, Pkt p) {  // UdpSocketImpl::DoSendTo (RouteOutput) -> Ipv4L3Protocol::Send
-    const uint32_t out = s.route[(uint64_t)n * s.n_dst + pkt_dst_slot(p)];
+    const uint32_t out = next_hop(n, pkt_dst_slot(p));
     if (out == 0xffffffffu) {
       no_route_drops++;
       return;
