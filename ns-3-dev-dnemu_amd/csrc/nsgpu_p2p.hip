@@ -993,6 +993,28 @@ __device__ __forceinline__ uint32_t nth_slot_scan(const P2PDev &M, uint32_t W, u
   return bs;
 }
 
+// Long chains (a hub node with more than CH events in the window): the next CH slots of node c
+// with keys > `after`, ascending, into my / mk — one pass over the window per CH events instead of
+// one per event.  Returns how many it found.
+__device__ __forceinline__ uint32_t chain_refill(const P2PDev &M, uint32_t W, uint32_t c, uint64_t after, uint32_t *my,
+                                                 uint64_t *mk) {
+  uint32_t m = 0;
+  for (uint32_t x = 0; x < W; x++) {
+    if (M.wctx[x] != c) continue;
+    const uint64_t k = M.wkey[x];
+    if (k <= after || (m == (uint32_t)CH && k >= mk[CH - 1])) continue;
+    uint32_t b = m < (uint32_t)CH ? m++ : (uint32_t)CH - 1;
+    while (b > 0 && mk[b - 1] > k) {
+      mk[b] = mk[b - 1];
+      my[b] = my[b - 1];
+      b--;
+    }
+    mk[b] = k;
+    my[b] = x;
+  }
+  return m;
+}
+
 template <bool DIST>
 __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0) {
   __shared__ uint32_t chs[HB * CH];
@@ -1064,6 +1086,7 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
     E.wnd = ~0ull;
     uint64_t lastk = 0;
     uint32_t ts0_it = 0, pending = 0;
+    uint32_t bp = 0, bl = 0;  // long chains: position / length of the my / mk batch
     uint64_t cur_rel = 0;
     for (uint32_t it = 0; it <= n; it++) {
       uint32_t s = NOCHAIN;
@@ -1076,8 +1099,13 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
           s = my[it];
           key = mk[it];
         } else {
-          s = nth_slot_scan(M, W, c, lastk);
-          key = M.wkey[s];
+          if (bp == bl) {
+            bl = chain_refill(M, W, c, lastk, my, mk);
+            bp = 0;
+          }
+          s = bl ? my[bp] : i0;  // (bl == 0 cannot happen: node_cnt counts the node's slots)
+          key = bl ? mk[bp] : key0;
+          bp++;
         }
       }
       const uint64_t rel = it < n ? (key >> 32) : ~0ull;
