@@ -7,6 +7,8 @@ Workloads (--workload):
       routes (SURVEY H9), Simulator::Stop at 2.1 s.  Everything after ns-3's setup phase — the
       setup-time Node/NetDevice/Application::Start events included — runs on the device in one
       persistent kernel (nsgpu_p2p_run).  One step = one full simulation from the post-setup state.
+  wifi-fanout: config 3's YansWifiChannel::Send receiver loop at 10,000 nodes, batched (receiver
+      events/s; a measurement of the fan-out kernel, not the default line).
   churn: config 1, utils/bench-simulator.cc — 10,000 pending, U[0,1) s delays, 5e6 holds,
       GPU-resident Bench::Cb (nsgpu_hold_run).
 
@@ -202,7 +204,81 @@ class P2PGridDist:
             "ranks": self.world}
 
 
-WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid}
+class WifiFanout:
+    """Config 3's hot loop: YansWifiChannel::Send (yans-wifi-channel.cc:77-115) over the
+    wifi-simple-adhoc-grid scaled to 10,000 nodes (100 x 100, 100 m spacing, one channel),
+    YansWifiChannelHelper::Default () (LogDistance n=3, L0=46.6777 dB at 1 m; ConstantSpeed 3e8),
+    16.0206 dBm: one step = one batched launch of --fanout-tx transmissions, each producing the 9,999
+    receiver events (ts, uid, context, phy, rxPowerDbm) its ScheduleWithContext calls would.  An
+    "event" here is one scheduled receiver event; bytes per event 64."""
+    bytes_per_event = 64
+    kernel = "nsgpu::fan_count + fan_write (one batched launch)"
+
+    def __init__(self, args, stream):
+        import numpy as np
+        import nsgpu
+        self.nsgpu = nsgpu
+        side = 100
+        xs, ys = np.meshgrid(np.arange(side) * 100.0, np.arange(side) * 100.0)
+        self.x, self.y = xs.ravel(), ys.ravel()
+        self.z = np.zeros_like(self.x)
+        self.chan = np.ones(self.x.size, np.uint32)
+        self.node = np.arange(self.x.size, dtype=np.uint32)
+        self.n_tx = args.fanout_tx
+        n = self.x.size
+        self.phys = nsgpu.PhyList(self.x, self.y, self.z, self.chan, self.node, stream=stream)
+        self.fo = nsgpu.Fanout(self.phys, self.n_tx, stream=stream)
+        tx = np.zeros(self.n_tx, dtype=nsgpu.TX_DESC_DTYPE)
+        t = np.arange(self.n_tx)
+        tx["now_ts"] = 1_000_000_000 + t * 1_000_000
+        tx["tx_dbm"] = 16.0206
+        tx["sender"] = (t * 7919) % n
+        tx["uid_base"] = 4 + t * (n - 1)
+        self.tx = tx
+        self.fo.upload_tx(tx)
+        self.chain = nsgpu.loss_chain((nsgpu.LOSS_LOG_DISTANCE, 3.0, 1.0, 46.6777))
+        self.workload = (f"wifi-simple-adhoc-grid scaled to {n} nodes (config 3): YansWifiChannel::Send fan-out, "
+                         f"100x100 grid 100 m, LogDistance(3, 46.6777) + ConstantSpeed, {self.n_tx} transmissions "
+                         f"per step x {n - 1} receivers")
+
+    def step(self):
+        self.fo.launch_yans(self.n_tx, self.chain, 3e8)
+
+    def roofline(self, step_kernel_ms, events_per_step):
+        return {"kernel": self.kernel, "kernel_ms": step_kernel_ms, "events_per_launch": events_per_step}
+
+    def result(self):
+        self.recs, _ = self.fo.results(self.n_tx)
+        total = sum(len(r) for r in self.recs)
+        return total, total, {"transmissions_per_step": self.n_tx}
+
+    def cpu_baseline(self):
+        import numpy as np
+        nsref = oracle()
+        chain = nsref.loss_chain((nsref.LOSS_LOG_DISTANCE, 3.0, 1.0, 46.6777))
+        k = min(self.n_tx, 256)
+        ok = True
+        t0 = time.perf_counter()
+        outs = [nsref.fanout_yans(self.x, self.y, self.z, self.chan, self.node, int(self.tx["sender"][i]), 16.0206,
+                                  chain, 3e8, int(self.tx["now_ts"][i]), int(self.tx["uid_base"][i]))
+                for i in range(k)]
+        secs = time.perf_counter() - t0
+        total = 0
+        for i, want in enumerate(outs):
+            got = self.recs[i]
+            total += len(want)
+            ok = ok and len(got) == len(want) and all(np.array_equal(got[f], want[f]) for f in
+                                                      ("ts", "uid", "context", "phy"))
+            ok = ok and bool(np.max(np.abs(got["rx_dbm"] - want["rx_dbm"]) / np.abs(want["rx_dbm"])) <= 1e-9)
+        digest = sum(len(r) for r in self.recs) if ok else -1
+        return total / secs, digest, (
+            f"first {k} of the step's transmissions ({total} receiver events) through the oracle's restatement "
+            f"of the YansWifiChannel::Send loop (nsref_fanout_yans, g++ -O2, one core, incl. its ctypes call); "
+            f"digest_match = those {k} transmissions' records equal the GPU's (ts/uid/context/phy exact, "
+            f"rxPowerDbm within 1e-9 relative)")
+
+
+WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid, "wifi-fanout": WifiFanout}
 
 
 def main():
@@ -213,6 +289,7 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="p2p-grid")
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--holds", type=int, default=5_000_000)
+    ap.add_argument("--fanout-tx", type=int, default=1024, help="wifi-fanout: transmissions per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--partitioned", action="store_true",
                     help="p2p-grid through the partitioned engine even on one rank (RCCL with one rank)")
