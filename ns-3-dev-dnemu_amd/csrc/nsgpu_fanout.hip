@@ -60,8 +60,13 @@ __global__ __launch_bounds__(FAN_THREADS) void fan_count(FanArgs a) {
   const int64_t t = blockIdx.y;
   const nsgpu_tx_desc tx = a.tx[t];
   const int64_t j = (int64_t)blockIdx.x * FAN_THREADS + threadIdx.x;
-  double d, rx;
-  const bool s = fan_eval<KIND>(a, tx, j, d, rx);
+  bool s;
+  if (KIND == FAN_YANS) {  // every same-channel phy but the sender receives: no loss evaluation needed
+    s = j < a.nphy && j != (int64_t)tx.sender && a.phys.channel[j] == a.phys.channel[tx.sender];
+  } else {
+    double d, rx;
+    s = fan_eval<KIND>(a, tx, j, d, rx);
+  }
   const unsigned long long b = __ballot(s);
   __shared__ uint32_t wc[FAN_THREADS / 64];
   if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = (uint32_t)__popcll(b);
