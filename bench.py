@@ -212,7 +212,7 @@ class WifiFanout:
     receiver events (ts, uid, context, phy, rxPowerDbm) its ScheduleWithContext calls would.  An
     "event" here is one scheduled receiver event; bytes per event 64."""
     bytes_per_event = 64
-    kernel = "nsgpu::fan_count + fan_write (one batched launch)"
+    kernel = "nsgpu::fan_write_ranked (one batched launch)"
 
     def __init__(self, args, stream):
         import numpy as np

@@ -69,6 +69,11 @@ typedef struct nsgpu_phy_soa {
   const double   *x, *y, *z;   /* positions (ConstantPositionMobilityModel), metres */
   const uint32_t *channel;     /* YansWifiPhy::GetChannelNumber () */
   const uint32_t *node;        /* NetDevice->GetNode ()->GetId (), 0xffffffff if none */
+  /* Optional (both NULL: not given), built once per phy list by the caller: chan_rank[j] = how many
+   * phys before j in m_phyList share j's channel, chan_count[j] = how many phys share it.  With them
+   * nsgpu_fanout_yans places receiver records (and their uids) directly, without a counting pass. */
+  const uint32_t *chan_rank;
+  const uint32_t *chan_count;
 } nsgpu_phy_soa;
 
 typedef struct nsgpu_tx_desc {

@@ -79,6 +79,32 @@ __global__ __launch_bounds__(FAN_THREADS) void fan_count(FanArgs a) {
 }
 
 // Pass 2: block offset from the preceding blocks' counts, local rank, write records.
+// Yans with a channel-rank table (nsgpu_phy_soa.chan_rank): receiver j of transmission t is record
+// chan_rank[j] - (j > sender) — the ScheduleWithContext order of the receiver loop — so one pass.
+__global__ __launch_bounds__(FAN_THREADS) void fan_write_ranked(FanArgs a) {
+  const int64_t t = blockIdx.y;
+  const nsgpu_tx_desc tx = a.tx[t];
+  const int64_t j = (int64_t)blockIdx.x * FAN_THREADS + threadIdx.x;
+  if (j >= a.nphy) return;
+  if (j == (int64_t)tx.sender) {
+    a.count[t] = a.phys.chan_count[j] - 1;
+    return;
+  }
+  if (a.phys.channel[j] != a.phys.channel[tx.sender]) return;  // :88-91
+  const double dist = distance3(a.phys.x[tx.sender], a.phys.y[tx.sender], a.phys.z[tx.sender], a.phys.x[j],
+                                a.phys.y[j], a.phys.z[j]);
+  const double rx = calc_rx_power(a.loss, tx.tx_dbm, dist);
+  const uint32_t off = a.phys.chan_rank[j] - (j > (int64_t)tx.sender ? 1u : 0u);
+  nsgpu_rx_record r;
+  r.ts = tx.now_ts + (uint64_t)seconds_to_ts(dist / a.speed);
+  r.uid = tx.uid_base + off;
+  r.context = a.phys.node[j];
+  r.phy = (uint32_t)j;
+  r.pad_ = 0;
+  r.rx_dbm = rx;
+  a.out[t * (a.nphy - 1) + off] = r;
+}
+
 template <int KIND>
 __global__ __launch_bounds__(FAN_THREADS) void fan_write(FanArgs a) {
   const int64_t t = blockIdx.y;
@@ -160,7 +186,11 @@ static int fan_launch(int kind, const nsgpu_phy_soa *phys, int64_t nphy, const n
   a.nblocks = (int32_t)((nphy + FAN_THREADS - 1) / FAN_THREADS);
   dim3 grid(a.nblocks, (unsigned)n_tx);
   hipStream_t s = (hipStream_t)stream;
-  if (kind == FAN_YANS) {
+  if ((phys->chan_rank == nullptr) != (phys->chan_count == nullptr))
+    return set_error(NSGPU_EINVAL, "nsgpu_fanout: chan_rank and chan_count go together");
+  if (kind == FAN_YANS && phys->chan_rank) {
+    hipLaunchKernelGGL(fan_write_ranked, grid, dim3(FAN_THREADS), 0, s, a);
+  } else if (kind == FAN_YANS) {
     hipLaunchKernelGGL(fan_count<FAN_YANS>, grid, dim3(FAN_THREADS), 0, s, a);
     hipLaunchKernelGGL(fan_write<FAN_YANS>, grid, dim3(FAN_THREADS), 0, s, a);
   } else {

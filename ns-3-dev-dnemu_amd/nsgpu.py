@@ -19,7 +19,7 @@ class NsgpuError(RuntimeError):
 
 class PhySoA(C.Structure):
     _fields_ = [("x", C.c_void_p), ("y", C.c_void_p), ("z", C.c_void_p), ("channel", C.c_void_p),
-                ("node", C.c_void_p)]
+                ("node", C.c_void_p), ("chan_rank", C.c_void_p), ("chan_count", C.c_void_p)]
 
 
 class LossModel(C.Structure):
@@ -251,6 +251,17 @@ class PhyList:
         self.n = len(x)
         self.bufs = [DeviceBuffer.from_array(np.asarray(a, dtype=t), stream) for a, t in
                      ((x, np.float64), (y, np.float64), (z, np.float64), (channel, np.uint32), (node, np.uint32))]
+        # per-channel rank / size of every phy (m_phyList order): Yans records are placed without counting
+        ch = np.asarray(channel, dtype=np.uint32)
+        order = np.argsort(ch, kind="stable")
+        sch = ch[order]
+        first = np.r_[True, sch[1:] != sch[:-1]] if ch.size else np.zeros(0, bool)
+        start = np.maximum.accumulate(np.where(first, np.arange(ch.size), 0)) if ch.size else np.zeros(0, np.int64)
+        rank = np.empty(ch.size, np.uint32)
+        rank[order] = (np.arange(ch.size) - start).astype(np.uint32)
+        _u, inv, cnt = np.unique(ch, return_inverse=True, return_counts=True)
+        count = cnt[inv].astype(np.uint32)
+        self.bufs += [DeviceBuffer.from_array(rank, stream), DeviceBuffer.from_array(count, stream)]
         self.soa = PhySoA(*[b.ptr for b in self.bufs])
 
 

@@ -32,8 +32,11 @@ def compare(got, want, what):
     assert rel.max(initial=0) <= RTOL, (what, rel.max())
 
 
+@pytest.mark.parametrize("ranked", [True, False])
 @pytest.mark.parametrize("loss_kind", ["logdistance", "friis", "chain"])
-def test_yans_fanout(loss_kind):
+def test_yans_fanout(loss_kind, ranked):
+    """ranked: records placed through the phy list's channel-rank table (one pass); otherwise the
+    counting pass + block prefix (a caller that passes no table)."""
     import nsgpu
     x, y, z, chan, node = grid(40, 100.0, channels=3, seed=1)
     node[7] = 0xFFFFFFFF  # a phy without a NetDevice
@@ -41,6 +44,9 @@ def test_yans_fanout(loss_kind):
               "chain": [(1, 3.0, 1.0, 46.6777), (4, 2500.0, 0, 0)]}[loss_kind]
     ch_o, ch_g = nsref.loss_chain(*models), nsgpu.loss_chain(*models)
     phys = nsgpu.PhyList(x, y, z, chan, node)
+    if not ranked:
+        phys.soa.chan_rank = None
+        phys.soa.chan_count = None
     senders = [0, 5, 777, 1599, 1234, 42]
     tx = np.zeros(len(senders), dtype=nsgpu.TX_DESC_DTYPE)
     tx["now_ts"] = [0, 10**9, 123456789, 5, 2**40, 999]
