@@ -95,14 +95,15 @@ __global__ __launch_bounds__(FAN_THREADS) void fan_write_ranked(FanArgs a) {
                                 a.phys.y[j], a.phys.z[j]);
   const double rx = calc_rx_power(a.loss, tx.tx_dbm, dist);
   const uint32_t off = a.phys.chan_rank[j] - (j > (int64_t)tx.sender ? 1u : 0u);
-  nsgpu_rx_record r;
-  r.ts = tx.now_ts + (uint64_t)seconds_to_ts(dist / a.speed);
-  r.uid = tx.uid_base + off;
-  r.context = a.phys.node[j];
-  r.phy = (uint32_t)j;
-  r.pad_ = 0;
-  r.rx_dbm = rx;
-  a.out[t * (a.nphy - 1) + off] = r;
+  // the 32-B record as two 16-B non-temporal stores: written once, read back only by the host
+  const uint64_t ts = tx.now_ts + (uint64_t)seconds_to_ts(dist / a.speed);
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 *dst = reinterpret_cast<u32x4 *>(a.out + (t * (a.nphy - 1) + off));
+  const uint64_t rxb = (uint64_t)__double_as_longlong(rx);
+  const u32x4 w0 = {(uint32_t)ts, (uint32_t)(ts >> 32), tx.uid_base + off, a.phys.node[j]};
+  const u32x4 w1 = {(uint32_t)j, 0u, (uint32_t)rxb, (uint32_t)(rxb >> 32)};
+  __builtin_nontemporal_store(w0, dst);
+  __builtin_nontemporal_store(w1, dst + 1);
 }
 
 template <int KIND>
