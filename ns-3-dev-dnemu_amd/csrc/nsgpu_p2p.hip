@@ -8,24 +8,14 @@
 //   queue      queue.cc:61-200, drop-tail-queue.cc:83-132
 //   IPv4/UDP   ipv4-l3-protocol.cc:434-537,815-841 (static next-hop routes, TTL)
 //
-// Engine (MI355X).  The simulation advances in conservative windows; each window is a fixed pipeline
-// of five short multi-CU kernels (a CU is 64 lanes per clock, so no phase may live on one CU),
-// replayed from a hipGraph of NWIN windows until the device-side `done` flag is set:
-//   k_partition  W_end = min over pending e of (ts_e + L(kind_e)) comes from the previous window
-//                (leftovers folded here, children in k_append), L = the smallest delay any child of
-//                that kind of handler can have: DefaultSimulatorImpl's uids make a child sort after every
-//                pending event with ts <= its own, so every pending event with ts <= W_end is safe.
-//                Window events -> slot records ((ts - tmin) << 32 | uid keys, capped at the
-//                Simulator::Stop key) and per-node slot tables; the rest -> the other pool buffer;
-//   k_refit      only when the window overflowed WCAP: 256-way radix bisection for the largest key
-//                prefix that fits (a key prefix of a safe window is safe), single workgroup;
-//   k_handle_rank  the holder of each node runs that node's events in key order, so node state
-//                (device tx state, DropTail rings, OnOff state, sink counters) needs no atomics;
-//                children go to per-slot records in Schedule-call order.  The same launch's other
-//                blocks rank the window keys by tiled all-pairs counting;
-//   k_scan       rank order; exclusive scans of child counts (uids), run bookkeeping;
-//   k_append     digest/log of the dispatch order, children -> pool with the uids DefaultSimulatorImpl
-//                would assign, and their part of the next window's reduction.
+// Engines (MI355X).  The simulation advances in conservative windows: W_end = min over pending e of
+// (ts_e + L(kind_e)), L = the smallest delay any child of that kind of handler can have, capped at
+// the Simulator::Stop key; DefaultSimulatorImpl's uids make a child sort after every pending event
+// with ts <= its own, so every pending event with key <= that bound is safe to dispatch.
+//   * single GPU: nsgpu_p2p_win.h — k2_pa / k2_handle / k2_scan per window (in-place pool, hub blocks,
+//     sorted runs for windows larger than WCAP), replayed from a hipGraph;
+//   * partitioned (one rank per GPU, or a loopback group on one GPU): k_pa<true>, k_refit_d, X0,
+//     k_cut, k_handle_rank<true>, X1, k_gtile, k_dfin, X2 below.
 #include <hip/hip_ext.h>
 #include "nsgpu_device.h"
 #include "nsgpu_internal.h"
@@ -46,7 +36,8 @@ enum EvKind : uint32_t {
   K_STOP = 11,          // Simulator::Stop
   K_FWD_UP = 12,        // Ipv4EndPoint::DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink (zero-delay leaf)
   K_FWD_UP_Q = 13,      // DoForwardUp -> UdpEchoServer / UdpEchoClient::HandleRead (queued: it schedules)
-  K_NKINDS = 14
+  K_FWD_UP_D = 14,      // a PacketSink DoForwardUp queued like any event: its ts group is cut by a run chunk
+  K_NKINDS = 15
 };
 
 constexpr int WCAP = 4096;       // events per window
@@ -92,6 +83,14 @@ struct Ctl {
   uint32_t puid0, pW, pvalid, pinl;
   uint32_t collected, pad1;  // partitioned: k_refit_d already moved the window slots to the pool
   uint64_t pcol;             // (and the pool count after that)
+  // ---- single-GPU engine (k2_*: in-place pool, sorted runs, hub blocks) ----
+  uint64_t P_end, live, nfree;  // pool scan range, live pool entries, free-stack entries
+  uint64_t r0, rW;              // sorted run: start of the next chunk, run length
+  uint64_t split_lo, split_hi;  // run chunk: rel ts of a same-ts group cut at its start / end (~0: none)
+  uint64_t wkmax;               // largest window key of the forming window (radix sort width)
+  uint64_t npush, nF;           // this window: pool slots freed, children parked in the fresh buffer
+  uint32_t mode, rt, nhub, wbase;  // engine mode, red[] accumulating index, hub nodes, chunk base
+  uint32_t force_run, pad3;        // a hub too large to sort in a block: dispatch the window as a run
 };
 
 // Device-resident model + engine state (all pointers are HBM).  Passed to the kernels by value.
@@ -163,6 +162,22 @@ struct P2PDev {
   nsgpu_trace_record *trace;
   uint64_t trace_cap;
   unsigned long long *trace_n;
+  // ---- single-GPU engine (k2_*) ----
+  uint64_t runcap;        // capacity of the window record arrays (a sorted run may hold the whole pool)
+  uint32_t *wsrc;         // pool slot each window record came from (NOSRC: a child of the last window)
+  uint64_t *f_ts;         // fresh buffer: children of the last window that stay pending (moved into
+  uint32_t *f_uid, *f_ctx, *f_kind, *f_a;  // the pool by k2_handle's maintenance blocks)
+  Pkt *f_pkt;
+  uint64_t fcap;
+  uint32_t *fstack;       // free pool slots (stack)
+  uint32_t *hub_list;     // nodes with more than CH window events (hub blocks)
+  struct HubEv *hx;       // hub blocks: per-slot node-part results
+  uint64_t *hub_key;      // hub blocks: the hub's events in key order (NHUB x WCAP)
+  uint32_t *hub_slot;
+  uint64_t *s_key2;       // radix sort / compaction scratch
+  uint32_t *s_val, *s_val2, *s_hist, *g_u32;
+  Pkt *g_pkt;
+  uint64_t *cmp_cnt;      // compaction: live entries written
 };
 
 // ---------------- wave / block helpers ----------------
@@ -229,7 +244,9 @@ struct Emit {
   uint64_t tmn, wnd;
   uint32_t uid;    // uid of the event being run (its trace records)
   uint32_t trseq;  // trace sink calls made by it so far
+  bool demote;     // the event's ts group is cut by a run chunk: its DoForwardUp leaves are queued
   __device__ __forceinline__ void child(int64_t delay, uint32_t ctx_, uint32_t kind, uint32_t a, Pkt p) {
+    if (demote && kind == K_FWD_UP) kind = K_FWD_UP_D;
     const uint32_t s = slot0 + n++;
     const uint64_t ts = now + (uint64_t)delay;
     ch_ts[s] = ts;
@@ -492,17 +509,25 @@ __device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const 
   return (lo < e1 && M.route_exc_slot[lo] == slot) ? M.route_exc_dev[lo] : M.route_def[n];
 }
 
-// One event: the kind-specific first phase, then the device step, then a trailing child.  Returns
-// true if it was a cancelled dispatch.
-__device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a, const Pkt &pkt,
-                                          int32_t sink, HStat &hs) {
+// One event: the kind-specific first phase (node part: node and application state, its own children),
+// then the device step, then a trailing child.  The node part never reads device queue / tx state and
+// the device step never reads node state, so a hub node's events can run them in two passes.
+struct NodeOut {
+  Act act;
+  Post post;
+  bool cancelled;
+};
+// rx_atomic: the device's rx counter is also added to by other lanes (hub blocks).
+__device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a,
+                                             const Pkt &pkt, int32_t sink, HStat &hs, bool rx_atomic = false) {
   const uint32_t kind = kind_word & 0xffu;
   const uint32_t gen = kind_word >> 8;
   Act act{ACT_NONE, 0, Pkt{0, 0, 0, 0}};
   Post post{false, 0, 0, 0};
   bool cancelled = false;
   if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive (ipv4-l3-protocol.cc:434-537)
-    M.devc[a].rx_packets++;
+    if (rx_atomic) atomicAdd(&M.devc[a].rx_packets, 1u);
+    else M.devc[a].rx_packets++;
     Pkt p = pkt;
     p.size -= 2;                             // ProcessHeader strips the PppHeader
     trace_call(M, E, NSGPU_TR_RX, a, p);     // m_macRxTrace
@@ -628,6 +653,7 @@ __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kin
         break;
       }
       case K_FWD_UP:  // DoForwardUp -> UdpSocketImpl::ForwardUp -> PacketSink::HandleRead (a = sink app)
+      case K_FWD_UP_D:
         if (M.app_flags[a] & 2u) {
           M.appc[a].rx_packets++;
           M.appc[a].rx_bytes += pkt.size - 28;
@@ -659,9 +685,14 @@ __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kin
         break;
     }
   }
-  device_act(M, E, act);
-  if (post.valid) E.child(post.delay, E.ctx, post.kind, post.a, Pkt{0, 0, 0, 0});
-  return cancelled;
+  return NodeOut{act, post, cancelled};
+}
+__device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a, const Pkt &pkt,
+                                          int32_t sink, HStat &hs) {
+  const NodeOut o = node_part(M, E, kind_word, a, pkt, sink, hs);
+  device_act(M, E, o.act);
+  if (o.post.valid) E.child(o.post.delay, E.ctx, o.post.kind, o.post.a, Pkt{0, 0, 0, 0});
+  return o.cancelled;
 }
 
 // Diagnostic build (-DNSGPU_PHASE_PROF, lib/libnsgpu_prof.so only): thread 0 of block 0 of each
@@ -1104,6 +1135,7 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
     E.lookahead = M.lookahead;
     E.tmn = ~0ull;
     E.wnd = ~0ull;
+    E.demote = false;
     uint64_t lastk = 0;
     uint32_t ts0_it = 0, pending = 0;
     uint32_t bp = 0, bl = 0;  // long chains: position / length of the my / mk batch
@@ -1401,165 +1433,7 @@ __device__ void refit_partition(const P2PDev &M, Ctl &C, const WinBound &b, uint
   }
 }
 
-__device__ void refit(const P2PDev &M, Ctl &C) {
-  const uint64_t win = C.windows;
-  WinBound b = window_bound(C.red[(win + 1) & 1]);
-  const uint64_t P = refit_collect(M, C, b, WCAP);
-  b.bound = refit_bisect(M, C, b, P);
-  refit_partition(M, C, b, P, C.red[win & 1]);
-  if (threadIdx.x == 0) {
-    C.prep = 1;    // the next k_pa leaves this window alone
-    C.pvalid = 0;  // (the last window was appended by the k_pa that overflowed)
-  }
-}
-
-// ---- k_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan(const P2PDev M) {
-  Ctl &C = *M.C;
-  if (C.done) return;
-  if (C.overflow) {
-    refit(M, C);
-    return;
-  }
-  constexpr int RPT = WCAP / SCAN_THREADS;
-  __shared__ uint32_t l_slot[WCAP], l_cnt[WCAP], l_rel[WCAP], gstart[WCAP];
-  PH_BEGIN();
-  const int tid = threadIdx.x;
-  // the window's slots, ahead of the run control
-  uint32_t pr[RPT], pc[RPT], pctx[RPT];
-  uint64_t pkey[RPT];
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t i = tid + q * SCAN_THREADS;
-    pr[q] = M.wrank[i];
-    pc[q] = M.nchild[i] | (M.ninl[i] << 16);
-    pkey[q] = M.wkey[i];
-    pctx[q] = M.wctx[i];
-  }
-  const uint32_t W = C.W;
-  PH_MARK(16);
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {  // slot order -> rank order; keys / contexts kept for the next k_pa
-    const uint32_t i = tid + q * SCAN_THREADS;
-    if (i < W) {
-      const uint32_t r = pr[q];
-      M.wrank[i] = 0;
-      M.pwkey[i] = pkey[q];
-      M.pwctx[i] = pctx[q];
-      l_slot[r] = i;
-      l_cnt[r] = pc[q];
-      l_rel[r] = (uint32_t)(pkey[q] >> 32);
-    }
-  }
-  __syncthreads();
-  PH_MARK(17);
-  uint32_t nc[RPT], ni[RPT], hd[RPT];
-  uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
-  uint32_t prev_rel = (tid * RPT < (int)W && tid > 0) ? l_rel[tid * RPT - 1] : 0;
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    nc[q] = ni[q] = hd[q] = 0;
-    if (r < W) {
-      nc[q] = l_cnt[r] & 0xffffu;
-      ni[q] = l_cnt[r] >> 16;
-      const uint32_t rel = l_rel[r];
-      hd[q] = r == 0 || rel != prev_rel;
-      prev_rel = rel;
-    }
-    sum += (uint64_t)nc[q] | ((uint64_t)ni[q] << 21) | ((uint64_t)hd[q] << 42);
-  }
-  // block exclusive scan of the packed sums (no field exceeds 21 bits: <= WCAP * maxc)
-  const int lane = tid & 63, wid = tid >> 6;
-  uint64_t inc = sum;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t w = __shfl_up(inc, o);
-    if (lane >= o) inc += w;
-  }
-  __shared__ uint64_t wsum64[SCAN_THREADS / 64];
-  if (lane == 63) wsum64[wid] = inc;
-  __syncthreads();
-  uint64_t off = 0, tot = 0;
-  for (int w = 0; w < SCAN_THREADS / 64; w++) {
-    const uint64_t s = wsum64[w];
-    off += w < wid ? s : 0;
-    tot += s;
-  }
-  const uint64_t ex = off + inc - sum;
-  const uint32_t tc = (uint32_t)(tot & 0x1fffffu), tinl = (uint32_t)((tot >> 21) & 0x1fffffu),
-                 ng = (uint32_t)(tot >> 42);
-  uint32_t bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu), bh = (uint32_t)(ex >> 42);
-  uint32_t g[RPT], ipr[RPT], cpr[RPT];
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    bh += hd[q];
-    g[q] = bh - 1;  // same-ts group of rank r
-    cpr[q] = bc;
-    ipr[q] = bi;
-    if (r < W && hd[q]) gstart[g[q]] = r;
-    bc += nc[q];
-    bi += ni[q];
-  }
-  __syncthreads();
-  PH_MARK(18);
-  // l_cnt is dead: reuse it for the inline prefix by rank
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    if (r < W) l_cnt[r] = ipr[q];
-  }
-  __syncthreads();
-  // per-slot dispatch info for k_pa (one 16-B record per slot):
-  //   x: dispatch rank of the event, relative to K0 = r + #inline children with ts < ts_r
-  //   y: dispatch rank of its first inline child = (#main events with ts <= ts_r) + iprefix[r]
-  //   z: child prefix (uids uid0 + z + j), w: inline prefix
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    if (r < W) {
-      const uint32_t first = gstart[g[q]];
-      const uint32_t last = (g[q] + 1 < ng ? gstart[g[q] + 1] : W) - 1;
-      M.sinfo[l_slot[r]] = make_uint4(r + (tinl ? l_cnt[first] : 0), last + 1 + ipr[q], cpr[q], ipr[q]);
-    }
-  }
-  PH_MARK(19);
-  if (tid == 0) {
-    const uint64_t win = C.windows;
-    C.pK0 = C.K;
-    C.puid0 = C.uid;
-    C.ptmin = C.tmin;
-    C.pinline_lim = C.inline_lim;
-    C.pW = W;
-    C.pinl = tinl;
-    C.pvalid = 1;
-    if (W) C.last_ts = C.tmin + l_rel[W - 1];
-    // (inline children at the Stop's ts are scheduled — uids consumed — but never dispatched; the run
-    //  ends with this window, so the pending count only has to be right for other windows)
-    const uint64_t newP = (uint64_t)C.nxtP + tc - tinl;
-    C.K += W + tinl;
-    C.uid += tc;
-    C.P = C.nxtP;
-    C.cur ^= 1;
-    C.red[(win + 1) & 1].tmin = C.red[(win + 1) & 1].wend = C.red[(win + 1) & 1].stopts = ~0ull;  // consumed
-    C.windows = win + 1;
-    if (W > C.max_window) C.max_window = W;
-    C.W = 0;
-    C.nxtP = 0;
-    C.prep = 0;
-    bool done = C.stop_seen || newP == 0;
-    if (newP > M.pool_cap) {
-      atomicOr(M.error, 1u);
-      done = true;
-    }
-    if (C.windows >= C.max_windows && !done) {
-      atomicOr(M.error, 4u);
-      done = true;
-    }
-    if (done) C.done = 1;
-  }
-  PH_MARK(20);
-}
+#include "nsgpu_p2p_win.h"
 
 // ================================ partitioned run (multi-GPU) ================================
 // DistributedSimulatorImpl (src/mpi/model/distributed-simulator-impl.cc:146-326) gives every rank
@@ -1848,6 +1722,7 @@ struct nsgpu_p2p {
   hipGraphExec_t gexec = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr;
   uint32_t *done_host = nullptr;  // pinned, 2 slots
+  Ctl *snap = nullptr;            // pinned, 2 run-control snapshots (single engine)
   float last_ms = 0.f;
   bool eager = getenv("NSGPU_P2P_EAGER") != nullptr;  // kernels one by one instead of graph replays
   // pristine initial pool (device) for resets
@@ -1897,6 +1772,7 @@ extern "C" int nsgpu_p2p_destroy(nsgpu_p2p *h) {
   for (hipEvent_t e : {h->ev[0], h->ev[1], h->t0, h->t1})
     if (e) (void)hipEventDestroy(e);
   if (h->done_host) (void)hipHostFree(h->done_host);
+  if (h->snap) (void)hipHostFree(h->snap);
   if (h->s) (void)hipStreamDestroy(h->s);
   for (void *p : h->allocs) (void)hipFree(p);
   delete h;
@@ -2150,12 +2026,36 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.ch_kind, chn));
   TRY(dalloc(h, &M.ch_a, chn));
   TRY(dalloc(h, &M.ch_pkt, chn));
-  TRY(dalloc(h, &M.wkey, WCAP));
+  // window records: WCAP for the partitioned engine; the single engine's hold a whole sorted run
+  M.fcap = chn;
+  M.runcap = owner ? (uint64_t)WCAP : M.pool_cap + M.fcap;
+  if (!owner && M.runcap >= 0xffffffffull) {
+    nsgpu_p2p_destroy(h);
+    return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: pool_cap too large for 32-bit slots");
+  }
+  TRY(dalloc(h, &M.wkey, M.runcap));
+  TRY(dalloc(h, &M.wpkt, M.runcap));
+  for (uint32_t **p : {&M.wctx, &M.wkind, &M.wa}) TRY(dalloc(h, p, M.runcap));
   TRY(dalloc(h, &M.pwkey, WCAP));
-  TRY(dalloc(h, &M.wpkt, WCAP));
   TRY(dalloc(h, &M.sinfo, WCAP));
-  for (uint32_t **p : {&M.wctx, &M.wkind, &M.wa, &M.widx, &M.nchild, &M.ninl, &M.pwctx}) TRY(dalloc(h, p, WCAP));
+  for (uint32_t **p : {&M.widx, &M.nchild, &M.ninl, &M.pwctx}) TRY(dalloc(h, p, WCAP));
   TRY(dalloc(h, &M.wrank, WCAP));
+  if (!owner) {  // in-place pool, fresh buffer, free stack, hub blocks, radix sort / compaction scratch
+    TRY(dalloc(h, &M.wsrc, M.runcap));
+    TRY(dalloc(h, &M.f_ts, M.fcap));
+    for (uint32_t **p : {&M.f_uid, &M.f_ctx, &M.f_kind, &M.f_a}) TRY(dalloc(h, p, M.fcap));
+    TRY(dalloc(h, &M.f_pkt, M.fcap));
+    TRY(dalloc(h, &M.fstack, M.pool_cap));
+    TRY(dalloc(h, &M.hub_list, MAXHUB));
+    TRY(dalloc(h, &M.hx, WCAP));
+    TRY(dalloc(h, &M.hub_key, (size_t)NHUB * WCAP));
+    TRY(dalloc(h, &M.hub_slot, (size_t)NHUB * WCAP));
+    TRY(dalloc(h, &M.s_key2, M.runcap));
+    for (uint32_t **p : {&M.s_val, &M.s_val2, &M.g_u32}) TRY(dalloc(h, p, M.runcap));
+    TRY(dalloc(h, &M.s_hist, 256 * ((M.runcap + RS_TILE - 1) / RS_TILE)));
+    TRY(dalloc(h, &M.g_pkt, M.runcap));
+    TRY(dalloc(h, &M.cmp_cnt, 1));
+  }
   if (owner) {
     M.dist = 1;
     M.rank = (uint32_t)rank;
@@ -2202,6 +2102,8 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   C0.red[1] = red0;
   C0.max_windows = h->max_windows;
   C0.done = red0.tmin == ~0ull ? 2 : 0;  // (no event anywhere)
+  C0.P_end = C0.live = M.n_init;  // single engine: the in-place pool starts as the setup events
+  C0.rt = 0;                      // window 0 is bounded by red[1] and folds into red[0]
   if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
     h->s = nullptr;
     nsgpu_p2p_destroy(h);
@@ -2219,6 +2121,11 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
       nsgpu_p2p_destroy(h);
       return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipEventCreate failed");
     }
+  if (hipHostMalloc((void **)&h->snap, 2 * sizeof(Ctl), hipHostMallocDefault) != hipSuccess) {
+    h->snap = nullptr;
+    nsgpu_p2p_destroy(h);
+    return set_error(NSGPU_ENOMEM, "nsgpu_p2p_create: hipHostMalloc failed");
+  }
   if (hipHostMalloc((void **)&h->done_host, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     h->done_host = nullptr;
     nsgpu_p2p_destroy(h);
@@ -2292,14 +2199,14 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
 // The window pipeline, in launch order (graph capture, eager runs and the per-kernel profile).
 namespace {
 constexpr int NKERN = 3;
-const char *const KERNEL_NAMES[NKERN] = {"k_pa", "k_handle_rank", "k_scan"};
+const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_scan"};
 // ev0 / ev1: optional HIP events the command processor records at the kernel's start and end
 // (hipExtLaunchKernelGGL: no separate marker packets between the pipeline's kernels).
 void launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   switch (k) {
-    case 0: hipExtLaunchKernelGGL(k_pa<false>, dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M); break;
-    case 1: hipExtLaunchKernelGGL(k_handle_rank<false>, dim3(NHB + NRB), dim3(HB), 0, s, ev0, ev1, 0, h->M); break;
-    default: hipExtLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M); break;
+    case 0: hipExtLaunchKernelGGL(k2_pa, dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M); break;
+    case 1: hipExtLaunchKernelGGL(k2_handle, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M); break;
+    default: hipExtLaunchKernelGGL(k2_scan, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M); break;
   }
 }
 void launch_windows(nsgpu_p2p *h, hipStream_t s) {
@@ -2307,6 +2214,61 @@ void launch_windows(nsgpu_p2p *h, hipStream_t s) {
     for (int k = 0; k < NKERN; k++) launch_kernel(h, k, s);
 }
 }  // namespace
+
+// The host-driven steps of the single engine (rare; on the engine stream, after the pipeline has
+// paused itself): the radix sort that turns an overflowing window into a sorted run, and the pool
+// compaction.  `c` is the run control the pause left.
+static int host_step(nsgpu_p2p *h, const Ctl &c) {
+  hipStream_t s = h->s;
+  const P2PDev &M = h->M;
+  if (c.mode == MODE_SORT) {
+    const uint64_t n = c.rW;
+    const int bits = c.wkmax ? 64 - __builtin_clzll(c.wkmax) : 1;
+    const int passes = (bits + 7) / 8;
+    const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    uint64_t *kin = M.wkey, *kout = M.s_key2;
+    uint32_t *vin = nullptr, *vout = M.s_val;
+    for (int p = 0; p < passes; p++) {
+      hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_T), 0, s, kin, n, 8 * p, M.s_hist, ntiles);
+      hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), 0, s, M.s_hist, (uint64_t)256 * ntiles);
+      hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_T), 0, s, kin, vin, kout, vout, n, 8 * p, M.s_hist,
+                         ntiles);
+      std::swap(kin, kout);
+      vin = vout;
+      vout = vin == M.s_val ? M.s_val2 : M.s_val;
+    }
+    if (kin != M.wkey) NSGPU_HIP(hipMemcpyAsync(M.wkey, kin, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    if (vin) {
+      const uint32_t gg = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+      for (uint32_t *a : {M.wctx, M.wkind, M.wa}) {
+        hipLaunchKernelGGL(k_rs_gather<uint32_t>, dim3(gg), dim3(256), 0, s, vin, a, M.g_u32, n);
+        NSGPU_HIP(hipMemcpyAsync(a, M.g_u32, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      }
+      hipLaunchKernelGGL(k_rs_gather<Pkt>, dim3(gg), dim3(256), 0, s, vin, M.wpkt, M.g_pkt, n);
+      NSGPU_HIP(hipMemcpyAsync(M.wpkt, M.g_pkt, n * sizeof(Pkt), hipMemcpyDeviceToDevice, s));
+    }
+    hipLaunchKernelGGL(k_after_sort, dim3(1), dim3(1), 0, s, M);
+    NSGPU_HIP(hipGetLastError());
+  } else if (c.mode == MODE_COMPACT) {
+    NSGPU_HIP(hipMemsetAsync(M.cmp_cnt, 0, sizeof(uint64_t), s));
+    hipLaunchKernelGGL(k_cmp, dim3(1024), dim3(256), 0, s, M, c.P_end);
+    NSGPU_HIP(hipGetLastError());
+    uint64_t live = 0;
+    NSGPU_HIP(hipMemcpyAsync(&live, M.cmp_cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+    if (live != c.live) return set_error(NSGPU_EHIP, "nsgpu_p2p: compaction found %llu live events, expected %llu",
+                                          (unsigned long long)live, (unsigned long long)c.live);
+    NSGPU_HIP(hipMemcpyAsync(M.ev_ts[0], M.ev_ts[1], live * 8, hipMemcpyDeviceToDevice, s));
+    NSGPU_HIP(hipMemcpyAsync(M.ev_uid[0], M.ev_uid[1], live * 4, hipMemcpyDeviceToDevice, s));
+    NSGPU_HIP(hipMemcpyAsync(M.ev_ctx[0], M.ev_ctx[1], live * 4, hipMemcpyDeviceToDevice, s));
+    NSGPU_HIP(hipMemcpyAsync(M.ev_kind[0], M.ev_kind[1], live * 4, hipMemcpyDeviceToDevice, s));
+    NSGPU_HIP(hipMemcpyAsync(M.ev_a[0], M.ev_a[1], live * 4, hipMemcpyDeviceToDevice, s));
+    NSGPU_HIP(hipMemcpyAsync(M.ev_pkt[0], M.ev_pkt[1], live * sizeof(Pkt), hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_after_compact, dim3(1), dim3(1), 0, s, M, live);
+    NSGPU_HIP(hipGetLastError());
+  }
+  return NSGPU_OK;
+}
 
 // The partitioned window (one RCCL member): 6 kernels and 3 collectives, on stream s.
 static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s) {
@@ -2367,24 +2329,52 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev[0], 0));
   NSGPU_HIP(hipEventRecord(h->t0, h->s));
   h->done_host[0] = h->done_host[1] = 0;
-  // two replays in flight: replay i+1 is queued before the done flag of replay i is examined
-  for (uint64_t it = 0;; it++) {
-    if (h->eager) {
-      if (h->M.dist) {
+  if (h->M.dist) {
+    // two replays in flight: replay i+1 is queued before the done flag of replay i is examined
+    for (uint64_t it = 0;; it++) {
+      if (h->eager) {
         const int rc = launch_windows_dist(h, h->s);
         if (rc) return rc;
+        NSGPU_HIP(hipGetLastError());
       } else {
-        launch_windows(h, h->s);
+        NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
       }
-      NSGPU_HIP(hipGetLastError());
-    } else {
-      NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
+      NSGPU_HIP(hipMemcpyAsync(&h->done_host[it & 1], &h->M.C->done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
+      NSGPU_HIP(hipEventRecord(h->ev[it & 1], h->s));
+      if (it > 0) {
+        NSGPU_HIP(hipEventSynchronize(h->ev[(it - 1) & 1]));
+        if (h->done_host[(it - 1) & 1] >= 2) break;  // 2: the final window is appended
+      }
     }
-    NSGPU_HIP(hipMemcpyAsync(&h->done_host[it & 1], &h->M.C->done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
-    NSGPU_HIP(hipEventRecord(h->ev[it & 1], h->s));
-    if (it > 0) {
-      NSGPU_HIP(hipEventSynchronize(h->ev[(it - 1) & 1]));
-      if (h->done_host[(it - 1) & 1] >= 2) break;  // 2: the final window is appended
+  } else {
+    // two replays in flight: replay i+1 is queued before the run control after replay i is examined;
+    // a pipeline that paused itself for a host-driven step (sort, compaction) makes the replay queued
+    // behind it a no-op, and the step is run once that replay has drained
+    int cur = 0;
+    bool have_prev = false;
+    for (;;) {
+      if (h->eager) {
+        launch_windows(h, h->s);
+        NSGPU_HIP(hipGetLastError());
+      } else {
+        NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
+      }
+      NSGPU_HIP(hipMemcpyAsync(&h->snap[cur], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+      NSGPU_HIP(hipEventRecord(h->ev[cur], h->s));
+      if (have_prev) {
+        NSGPU_HIP(hipEventSynchronize(h->ev[cur ^ 1]));
+        const Ctl &c = h->snap[cur ^ 1];
+        if (c.done >= 2) break;  // 2: the final window is appended
+        if (c.mode >= MODE_SORT) {
+          NSGPU_HIP(hipEventSynchronize(h->ev[cur]));
+          const int rc = host_step(h, h->snap[cur]);
+          if (rc) return rc;
+          have_prev = false;
+          continue;
+        }
+      }
+      have_prev = true;
+      cur ^= 1;
     }
   }
   NSGPU_HIP(hipEventRecord(h->t1, h->s));
@@ -2493,6 +2483,8 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
   if (rc == NSGPU_OK && (hipEventRecord(h->ev[0], cs) != hipSuccess || hipStreamWaitEvent(h->s, h->ev[0], 0) != hipSuccess))
     rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: stream join failed");
   int ns = 0;
+  // the run control is read after every window (so no sampled pass is a paused no-op and the
+  // host-driven steps run as soon as the pipeline asks)
   for (uint64_t w = 0; rc == NSGPU_OK; w++) {
     const bool sample = (w % sample_every) == 0 && ns < NS;
     for (int k = 0; k < NKERN; k++) {
@@ -2504,25 +2496,16 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
       rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: launch failed");
       break;
     }
-    if ((w % NWIN) == NWIN - 1) {
-      if (hipMemcpyAsync(&h->done_host[0], &h->M.C->done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->s) !=
-              hipSuccess ||
-          hipStreamSynchronize(h->s) != hipSuccess) {
-        rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: sync failed");
-        break;
-      }
-      if (h->done_host[0] >= 2) break;  // the final window is appended
+    if (hipMemcpyAsync(&h->snap[0], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s) != hipSuccess ||
+        hipStreamSynchronize(h->s) != hipSuccess) {
+      rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: sync failed");
+      break;
     }
+    if (h->snap[0].done >= 2) break;  // the final window is appended
+    if (h->snap[0].mode >= MODE_SORT) rc = host_step(h, h->snap[0]);
   }
   if (rc == NSGPU_OK) {
-    Ctl c;
-    if (hipMemcpyAsync(&c, h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s) != hipSuccess ||
-        hipStreamSynchronize(h->s) != hipSuccess)
-      rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: sync failed");
-    // pipeline passes that did work: every window, one more per refit, the final append; later
-    // sampled passes of the last NWIN batch hold early-exit launches and are not counted
-    const uint64_t real = c.windows + c.refits + 1;
-    for (int i = 0; i < ns && (uint64_t)i * sample_every < real; i++)
+    for (int i = 0; i < ns; i++)
       for (int k = 0; k < NKERN; k++) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, ev[(2 * i) * NKERN + k], ev[(2 * i + 1) * NKERN + k]) == hipSuccess) {

@@ -1,0 +1,1057 @@
+// nsgpu_p2p_win.h — the single-GPU window pipeline of the GPU-resident p2p subset (included by
+// nsgpu_p2p.hip inside namespace nsgpu, after the shared model code).
+//
+// Per conservative window three kernels, replayed from a hipGraph:
+//   k2_pa      appends the last window (dispatch log / digest; its children get their uids) and forms
+//              the next one: every pending event with key <= the bound (W_end = min over pending of
+//              ts + lookahead(kind), capped at Simulator::Stop's key) becomes a window record.  The
+//              pending pool is kept IN PLACE: it is only read (ts, uid, kind) — window events are
+//              tombstoned afterwards and their slots reused, children that stay pending are parked
+//              in a fresh buffer and moved into free slots by k2_handle.
+//   k2_handle  the holder of each node runs the node's window events in key order; nodes with more
+//              than CH events (hubs: a dumbbell router) get a whole block that takes the node's
+//              events in key order, runs their node parts (stateless forwarding in parallel,
+//              node-state work serially) and then the device steps with the device state kept in
+//              registers.  Other blocks rank the window keys (all-pairs counting) and do the pool
+//              maintenance.
+//   k2_scan    rank order, exclusive scans of child counts (uids), run bookkeeping.
+// A window larger than WCAP (config 5's hundreds of thousands of same-time events) is a SORTED RUN:
+// k2_scan pauses the graph, the host radix-sorts the window records by key (k_rs_*), and the run is
+// then dispatched in rank-order chunks of WCAP — every child of a run event sorts after every run
+// event (the window rule), so chunks need no re-selection.  A zero-delay PacketSink DoForwardUp
+// whose ts group a chunk boundary cuts is queued like any other event (K_FWD_UP_D) instead of being
+// run inline, which keeps its (ts, uid) position.  When the pool holds many tombstones the host
+// compacts it (k_cmp).
+
+enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3 };
+constexpr uint64_t TOMB = ~0ull;        // ev_ts of a free pool slot
+constexpr uint32_t NOSRC = 0xffffffffu;
+constexpr int NHUB = 32;                // hub blocks of k2_handle
+constexpr int NMB = 128;                // maintenance blocks of k2_handle
+constexpr int MAXHUB = WCAP / (CH + 1) + 1;
+constexpr int K2_GRID = NHB + NRB + NHUB + NMB;
+
+// Node-part result of one hub event (k2_handle hub blocks, between the two passes).
+struct HubEv {
+  uint32_t op, dev;
+  Pkt p;
+  int64_t pdelay;      // trailing child (OnOffApplication::ScheduleNextTx after SendPacket)
+  uint32_t pkind, pa;  // pkind == 0: none
+  uint32_t n, seq;     // children and trace sink calls the node part made
+  uint32_t cancelled, pad;
+};
+
+constexpr int HUBL = 1024;  // events of a hub a block sorts in LDS (more: the window is dispatched as a run)
+
+// Wave-aggregated counter allocation: one index per lane with `want` (active lanes only).
+__device__ __forceinline__ uint32_t wave_alloc32(uint32_t *ctr, bool want) {
+  const uint64_t m = __ballot(want);
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (m) {
+    const int first = __ffsll((unsigned long long)m) - 1;
+    if (lane == first) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, first);
+  }
+  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+__device__ __forceinline__ uint64_t wave_alloc64(uint64_t *ctr, bool want) {
+  const uint64_t m = __ballot(want);
+  const int lane = threadIdx.x & 63;
+  unsigned long long base = 0;
+  if (m) {
+    const int first = __ffsll((unsigned long long)m) - 1;
+    if (lane == first) base = atomicAdd((unsigned long long *)ctr, (unsigned long long)__popcll(m));
+    base = __shfl(base, first);
+  }
+  return (uint64_t)base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+// Window record `slot` of node `ctx` -> the node's slot table (local slot index); the node that
+// reaches CH + 1 events becomes a hub.
+__device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t slot, uint32_t ctx) {
+  uint32_t idx = 0;
+  if (ctx < M.n_nodes) {
+    idx = atomicAdd(&M.node_cnt[ctx], 1u);
+    if (idx < (uint32_t)NSLOT) M.node_slot[(uint64_t)ctx * NSLOT + idx] = slot;
+    if (idx == (uint32_t)CH) {
+      const uint32_t hh = atomicAdd(&C.nhub, 1u);
+      if (hh < (uint32_t)MAXHUB) M.hub_list[hh] = ctx;
+    }
+    if (idx == (uint32_t)HUBL) C.force_run = 1;
+  }
+  M.widx[slot] = idx;
+}
+
+// A pending event against the window bound: window record (normal mode, key <= bound), else pending:
+// a child (src == NOSRC) is parked in the fresh buffer, a pool entry stays where it is; both fold
+// into the next window's reduction.  Lanes that call it must be converged (ballots).
+__device__ __forceinline__ void k2_place(const P2PDev &M, Ctl &C, const WinBound &b, bool run, bool valid,
+                                         const Ev &e, uint32_t src, Red &R, uint64_t &tmn, uint64_t &wnd,
+                                         uint64_t &kmax) {
+  const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
+  const bool in = valid && !run && (e.ts - b.tmin <= b.span) && pk <= b.bound;
+  const bool park = valid && !in && src == NOSRC;
+  const uint32_t slot = wave_alloc32(&C.W, in);
+  const uint64_t fi = wave_alloc64(&C.nF, park);
+  if (in) {
+    if (slot < M.runcap) {
+      M.wkey[slot] = pk;
+      M.wctx[slot] = e.ctx;
+      M.wkind[slot] = e.kind;
+      M.wa[slot] = e.a;
+      M.wpkt[slot] = e.p;
+      M.wsrc[slot] = src;
+      if (slot < (uint32_t)WCAP) node_table_add(M, C, slot, e.ctx);
+      kmax = pk > kmax ? pk : kmax;
+    } else {
+      atomicOr(M.error, 1u);
+    }
+  } else if (valid) {
+    if (park) {
+      if (fi < M.fcap) {
+        M.f_ts[fi] = e.ts;
+        M.f_uid[fi] = e.uid;
+        M.f_ctx[fi] = e.ctx;
+        M.f_kind[fi] = e.kind;
+        M.f_a[fi] = e.a;
+        M.f_pkt[fi] = e.p;
+      } else {
+        atomicOr(M.error, 1u);
+      }
+    }
+    tmn = e.ts < tmn ? e.ts : tmn;
+    const uint64_t x = e.ts + (uint64_t)M.lookahead[e.kind & 0xffu];
+    wnd = x < wnd ? x : wnd;
+    if ((e.kind & 0xffu) == K_STOP) {  // at most one Stop event is pending
+      R.stopts = e.ts;
+      R.stopuid = e.uid;
+    }
+  }
+}
+
+// ---- k2_pa ----
+__global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
+  PH_BEGIN();
+  Ctl &C = *M.C;
+  const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * TB;
+  const bool slot_role = g < (uint64_t)WCAP;  // (roles are wave-uniform)
+  if (C.done >= 2 || C.mode >= MODE_SORT) return;
+  const bool run = C.mode == MODE_RUN;
+  const bool partition = C.done == 0;
+  const uint32_t rt = C.rt;
+  Red &R = C.red[rt];
+  const WinBound b = window_bound(C.red[rt ^ 1]);
+  if (!run && partition && g == 0) {
+    publish_bound(C, b);
+    C.split_lo = C.split_hi = ~0ull;
+  }
+  const uint32_t pW = C.pvalid ? C.pW : 0;
+  uint64_t spk = 0;
+  uint4 si = make_uint4(0, 0, 0, 0);
+  uint32_t ncr = 0, sctx = 0;
+  Ev ce[PFC];
+  if (slot_role && g < pW) {  // the last window's slot and its first children, all at once
+    const uint32_t s = (uint32_t)g;
+    spk = M.pwkey[s];
+    si = M.sinfo[s];
+    ncr = M.nchild[s];
+    sctx = M.pwctx[s];
+#pragma unroll
+    for (int j = 0; j < PFC; j++) {
+      const uint32_t sl = s * M.maxc + j;
+      if ((uint32_t)j < M.maxc) ce[j] = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
+    }
+  }
+  PH_MARK(0);
+  uint64_t tmn = ~0ull, wnd = ~0ull, digest = 0, kmax = 0;
+  if (slot_role) {
+    // ---- slot g of the last window: dispatch rank (log, digest), inline children, children -> pending
+    const bool vs = g < pW;
+    const uint32_t s = (uint32_t)g;
+    const uint64_t rel = spk >> 32;
+    const uint64_t t = C.ptmin + rel;
+    const uint32_t uid0 = C.puid0;
+    const uint64_t K0 = C.pK0, ilim = C.pinline_lim;
+    if (vs) {
+      const uint64_t rk = K0 + si.x;
+      digest += digest_term(rk, t, (uint32_t)spk);
+      if (rk < M.log_cap) {
+        M.log_ts[rk] = t;
+        M.log_uid[rk] = (uint32_t)spk;
+        M.log_ctx[rk] = sctx;
+      }
+    }
+    if (__ballot(vs)) {
+      uint32_t ii = 0;
+      for (uint32_t j = 0; j < M.maxc; j++) {
+        const bool has = vs && j < ncr;
+        if (!__ballot(has)) break;
+        Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+        bool valid = false;
+        if (has) {
+          if (j < (uint32_t)PFC) {
+#pragma unroll
+            for (int q = 0; q < PFC; q++)
+              if ((uint32_t)q == j) e = ce[q];
+          } else {
+            const uint32_t sl = s * M.maxc + j;
+            e = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
+          }
+          e.uid = uid0 + si.z + j;
+          if ((e.kind & 0xffu) == K_FWD_UP) {  // leaf: dispatched inside its window (or never), not queued
+            if (rel < ilim) {
+              const uint64_t crk = K0 + si.y + ii;
+              digest += digest_term(crk, t, e.uid);
+              if (crk < M.log_cap) {
+                M.log_ts[crk] = t;
+                M.log_uid[crk] = e.uid;
+                M.log_ctx[crk] = e.ctx;
+              }
+              ii++;
+            }
+          } else {
+            valid = partition;
+          }
+        }
+        k2_place(M, C, b, run, valid, e, NOSRC, R, tmn, wnd, kmax);
+      }
+    }
+  } else if (partition && !run) {
+    // ---- the pool, in place: read (ts, uid, kind) of every slot; window events are copied out
+    const uint64_t P = C.P_end;
+    const uint64_t w0 = (g - WCAP) & ~63ull, ws = (stride - WCAP);
+    for (uint64_t base = w0; base < P; base += ws) {  // wave-uniform trip count
+      const uint64_t i = base + (threadIdx.x & 63);
+      uint64_t ts = TOMB;
+      if (i < P) ts = M.ev_ts[0][i];
+      const bool valid = ts != TOMB;
+      Ev e{ts, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+      if (valid) {
+        e.uid = M.ev_uid[0][i];
+        e.kind = M.ev_kind[0][i];
+        if (e.ts - b.tmin <= b.span && (((e.ts - b.tmin) << 32) | e.uid) <= b.bound) {  // a window event
+          e.ctx = M.ev_ctx[0][i];
+          e.a = M.ev_a[0][i];
+          e.p = M.ev_pkt[0][i];
+        }
+      }
+      k2_place(M, C, b, false, valid, e, (uint32_t)i, R, tmn, wnd, kmax);
+    }
+  } else if (partition && run) {
+    // ---- the next chunk of the sorted run: per-node slot tables, chunk bounds
+    const uint64_t r0 = C.r0, rW = C.rW;
+    const uint32_t Wc = (uint32_t)(rW - r0 < (uint64_t)WCAP ? rW - r0 : (uint64_t)WCAP);
+    const uint64_t s = g - WCAP;
+    if (s == 0) {
+      C.W = Wc;
+      C.wbase = (uint32_t)r0;
+      const uint64_t r1 = r0 + Wc;
+      const uint64_t klo = M.wkey[r0] >> 32, khi = M.wkey[r1 - 1] >> 32;
+      C.split_lo = (r0 > 0 && (M.wkey[r0 - 1] >> 32) == klo) ? klo : ~0ull;
+      C.split_hi = (r1 < rW && (M.wkey[r1] >> 32) == khi) ? khi : ~0ull;
+    }
+    if (s < Wc) node_table_add(M, C, (uint32_t)s, M.wctx[r0 + s]);
+  }
+  PH_MARK(1);
+  publish_min<TB>(R, tmn, wnd);
+  digest = wave_sum64(digest);
+  kmax = wave_max64(kmax);
+  if ((threadIdx.x & 63) == 0) {
+    if (digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
+    if (kmax) atomicMax((unsigned long long *)&C.wkmax, (unsigned long long)kmax);
+  }
+  PH_MARK(2);
+}
+
+// ---- k2_handle: holders ----
+// The roles of k2_handle's blocks share one LDS buffer (holders: per-thread sort lists; hub blocks:
+// the hub's list), so that every block of the launch is resident at once.
+constexpr int K2_LDS_WORDS = HB * CH * 3;  // 12 KB: >= HUBL * 3 words
+static_assert(HUBL * 3 <= K2_LDS_WORDS, "hub list does not fit the shared buffer");
+__device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i0, uint32_t W, uint32_t base, Red &R,
+                                             uint32_t *lds) {
+  uint32_t *chs = lds;
+  uint64_t *chk = reinterpret_cast<uint64_t *>(lds + HB * CH);
+  uint64_t tmn = ~0ull, wnd = ~0ull;
+  HStat hs{0, 0, 0, 0, false};
+  if (i0 < W && M.widx[i0] == 0) {  // the holder
+    const uint32_t c = M.wctx[base + i0];
+    uint32_t n = 1;
+    int32_t sink = -1;
+    if (c < M.n_nodes) {
+      n = M.node_cnt[c];
+      sink = M.sink_of_node[c];
+    }
+    if (n <= (uint32_t)CH) {  // (a hub's events are its hub block's)
+      if (c < M.n_nodes) M.node_cnt[c] = 0;
+      const uint64_t key0 = M.wkey[base + i0];
+      uint32_t *my = &chs[threadIdx.x * CH];
+      uint64_t *mk = &chk[threadIdx.x * CH];
+      my[0] = i0;
+      mk[0] = key0;
+      if (n > 1) {
+        const uint32_t ns = n < (uint32_t)NSLOT ? n : (uint32_t)NSLOT;
+        for (uint32_t j = 0; j < ns; j++) my[j] = M.node_slot[(uint64_t)c * NSLOT + j];
+        if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
+          uint32_t m = NSLOT;
+          for (uint32_t x = 0; x < W && m < n; x++)
+            if (M.wctx[base + x] == c && M.widx[x] >= (uint32_t)NSLOT) my[m++] = x;
+        }
+        for (uint32_t j = 0; j < n; j++) mk[j] = M.wkey[base + my[j]];
+        for (uint32_t a = 1; a < n; a++) {  // insertion sort by key
+          const uint32_t v = my[a];
+          const uint64_t kv = mk[a];
+          uint32_t bb = a;
+          while (bb > 0 && mk[bb - 1] > kv) {
+            my[bb] = my[bb - 1];
+            mk[bb] = mk[bb - 1];
+            bb--;
+          }
+          my[bb] = v;
+          mk[bb] = kv;
+        }
+      }
+      const uint64_t tmin = C.tmin, inline_lim = C.inline_lim, slo = C.split_lo, shi = C.split_hi;
+      Emit E;
+      E.ctx = c;
+      E.ch_ts = M.ch_ts;
+      E.ch_ctx = M.ch_ctx;
+      E.ch_kind = M.ch_kind;
+      E.ch_a = M.ch_a;
+      E.ch_pkt = M.ch_pkt;
+      E.lookahead = M.lookahead;
+      E.tmn = ~0ull;
+      E.wnd = ~0ull;
+      uint32_t ts0_it = 0, pending = 0;
+      uint64_t cur_rel = 0;
+      for (uint32_t it = 0; it <= n; it++) {
+        const uint64_t rel = it < n ? (mk[it] >> 32) : ~0ull;
+        if (it > 0 && rel > cur_rel && pending) {
+          // flush the inline children of this node's events at cur_rel (positions [ts0_it, it))
+          for (uint32_t jt = ts0_it; jt < it; jt++) {
+            const uint32_t xr = my[jt];
+            const uint32_t ncr = M.nchild[xr];
+            for (uint32_t j = 0; j < ncr; j++) {
+              const uint32_t sl = xr * M.maxc + j;
+              if ((E.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
+              const uint32_t sa = E.ch_a[sl];  // DoForwardUp -> PacketSink::HandleRead
+              if (M.app_flags[sa] & 2u) {
+                M.appc[sa].rx_packets++;
+                M.appc[sa].rx_bytes += E.ch_pkt[sl].size - 28;
+              }
+            }
+          }
+          pending = 0;
+        }
+        if (it == n) break;
+        if (it == 0 || rel > cur_rel) {
+          ts0_it = it;
+          cur_rel = rel;
+        }
+        const uint32_t s = my[it];
+        E.now = tmin + rel;
+        E.slot0 = s * M.maxc;
+        E.n = 0;
+        E.uid = (uint32_t)mk[it];
+        E.trseq = 0;
+        E.demote = rel == slo || rel == shi;
+        hs.cancelled += run_event(M, E, M.wkind[base + s], M.wa[base + s], M.wpkt[base + s], sink, hs);
+        uint32_t ni = 0;
+        if (rel < inline_lim)
+          for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
+        M.nchild[s] = E.n;
+        M.ninl[s] = ni;
+        pending += ni;
+      }
+      tmn = E.tmn;
+      wnd = E.wnd;
+    }
+  }
+  publish_min<HB>(R, tmn, wnd);
+  if (hs.stop) C.stop_seen = 1;
+  if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
+  if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
+  if (hs.no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)hs.no_route);
+  if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
+}
+
+// ---- k2_handle: hub blocks ----
+// Device state of the device a hub's serial device pass is on, in registers.
+struct DevCache {
+  uint32_t d, busy, cnt, head, qmax, peer, peer_node;
+  uint64_t bps;
+  int64_t ifg, delay;
+  uint32_t q[6];  // enq_packets, enq_bytes, drop_packets, drop_bytes, deq_packets, tx_packets
+  __device__ __forceinline__ void flush(const P2PDev &M) {
+    if (d == NOSRC) return;
+    M.dev_busy[d] = busy;
+    M.q_count[d] = cnt;
+    M.q_head[d] = head;
+    uint32_t *w = reinterpret_cast<uint32_t *>(&M.devc[d]);  // not rx_packets: the node pass adds it atomically
+    *reinterpret_cast<uint4 *>(w) = make_uint4(q[0], q[1], q[2], q[3]);
+    *reinterpret_cast<uint2 *>(w + 4) = make_uint2(q[4], q[5]);
+  }
+  __device__ __forceinline__ void load(const P2PDev &M, uint32_t dd) {
+    d = dd;
+    busy = M.dev_busy[d];
+    cnt = M.q_count[d];
+    head = M.q_head[d];
+    qmax = M.dev_qmax[d];
+    bps = M.dev_bps[d];
+    ifg = M.dev_ifg[d];
+    delay = M.dev_delay[d];
+    peer = M.dev_peer[d];
+    peer_node = M.dev_node[peer];
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(&M.devc[d]);
+    const uint4 a = *reinterpret_cast<const uint4 *>(w);
+    const uint2 b2 = *reinterpret_cast<const uint2 *>(w + 4);
+    q[0] = a.x, q[1] = a.y, q[2] = a.z, q[3] = a.w, q[4] = b2.x, q[5] = b2.y;
+  }
+};
+
+// device_act with the device state in a register cache (the same steps, point-to-point-net-device.cc
+// :206-269,462-518, queue.cc:61-97, drop-tail-queue.cc:83-100).
+__device__ __forceinline__ void device_act_cached(const P2PDev &M, Emit &E, const Act &act, DevCache &D) {
+  if (act.op == ACT_NONE) return;
+  if (D.d != act.dev) {
+    D.flush(M);
+    D.load(M, act.dev);
+  }
+  const uint32_t d = act.dev;
+  Pkt *qb = M.q_buf + (uint64_t)d * M.qcap;
+  bool go = false;
+  Pkt tx{0, 0, 0, 0};
+  if (act.op == ACT_SEND) {
+    Pkt p = act.p;
+    p.size += 2;  // PppHeader
+    if (D.cnt >= D.qmax) {
+      trace_call(M, E, NSGPU_TR_DROP, d, p);
+      D.q[2]++;
+      D.q[3] += p.size;
+    } else {
+      trace_call(M, E, NSGPU_TR_ENQUEUE, d, p);
+      D.q[0]++;
+      D.q[1] += p.size;
+      if (D.busy == 0) {
+        if (D.cnt == 0) {
+          tx = p;
+        } else {
+          qb[(D.head + D.cnt) % M.qcap] = p;
+          tx = qb[D.head];
+        }
+        D.head = (D.head + 1) % M.qcap;
+        trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);
+        D.q[4]++;
+        go = true;
+      } else {
+        qb[(D.head + D.cnt) % M.qcap] = p;
+        D.cnt++;
+      }
+    }
+  } else {  // ACT_KICK
+    D.busy = 0;
+    if (D.cnt > 0) {
+      tx = qb[D.head];
+      D.head = (D.head + 1) % M.qcap;
+      D.cnt--;
+      trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);
+      D.q[4]++;
+      go = true;
+    }
+  }
+  if (go) {
+    D.busy = 1;
+    D.q[5]++;
+    const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)D.bps);
+    E.child(txTime + D.ifg, E.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
+    E.child(txTime + D.delay, D.peer_node, K_RECEIVE, D.peer, tx);
+  }
+}
+
+// Events whose node part touches no node state: TransmitComplete, and a Receive that IpForward
+// sends on (its node is not the datagram's destination).
+__device__ __forceinline__ bool stateless_event(const P2PDev &M, uint32_t c, uint32_t kind, const Pkt &p) {
+  if (kind == K_TX_COMPLETE) return true;
+  if (kind != K_RECEIVE) return false;
+  const bool reply = (p.app & NSGPU_PKT_REPLY) != 0;
+  return (reply ? M.app_node[p.app & ~NSGPU_PKT_REPLY] : M.app_dst_node[p.app]) != c;
+}
+
+__device__ __forceinline__ void bitonic_sort_lds(uint64_t *k, uint32_t *v, uint32_t n) {
+  uint32_t P = 1;
+  while (P < n) P <<= 1;
+  for (uint32_t i = n + threadIdx.x; i < P; i += HB) k[i] = ~0ull;
+  __syncthreads();
+  for (uint32_t kk = 2; kk <= P; kk <<= 1)
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < P; i += HB) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const bool asc = (i & kk) == 0;
+          const uint64_t a = k[i], bb = k[l];
+          if ((a > bb) == asc) {
+            k[i] = bb;
+            k[l] = a;
+            const uint32_t t = v[i];
+            v[i] = v[l];
+            v[l] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// A hub node's window events, by one block: (1) its events in key order (slot order in a sorted run
+// chunk; otherwise at most HUBL of them, bitonic-sorted in LDS) into the block's global scratch list;
+// (2a) node parts without node state (TransmitComplete; Receive -> IpForward) in parallel; (2b) the
+// other node parts serially in key order; (3) the device steps and trailing children serially in key
+// order, the device state in registers.  Node parts never read device state and device steps never
+// read node state (node_part), so this is the sequential order's result.
+__device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32_t base, bool sorted, Red &R,
+                         uint32_t hb, uint32_t *lds) {
+  const int lane = threadIdx.x;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint64_t *gk = M.hub_key + (uint64_t)hb * WCAP;
+  uint32_t *gs = M.hub_slot + (uint64_t)hb * WCAP;
+  // 1. the node's window events, in slot order
+  uint32_t n = 0;
+  for (uint32_t x0 = 0; x0 < W; x0 += HB) {
+    const uint32_t x = x0 + lane;
+    const bool m = x < W && M.wctx[base + x] == c;
+    const uint64_t bm = __ballot(m);
+    if (m) {
+      const uint32_t p = n + (uint32_t)__popcll(bm & below);
+      gs[p] = x;
+      gk[p] = M.wkey[base + x];
+    }
+    n += (uint32_t)__popcll(bm);
+  }
+  __syncthreads();
+  if (!sorted) {  // (n <= HUBL here: a larger hub makes its window a sorted run, k2_pa)
+    uint64_t *lk = reinterpret_cast<uint64_t *>(lds);
+    uint32_t *ls = lds + 2 * HUBL;
+    for (uint32_t j = lane; j < n; j += HB) {
+      lk[j] = gk[j];
+      ls[j] = gs[j];
+    }
+    __syncthreads();
+    bitonic_sort_lds(lk, ls, n);
+    for (uint32_t j = lane; j < n; j += HB) {
+      gk[j] = lk[j];
+      gs[j] = ls[j];
+    }
+    __syncthreads();
+  }
+  const uint64_t tmin = C.tmin, inline_lim = C.inline_lim, slo = C.split_lo, shi = C.split_hi;
+  const int32_t sink = M.sink_of_node[c];
+  Emit E;
+  E.ctx = c;
+  E.ch_ts = M.ch_ts;
+  E.ch_ctx = M.ch_ctx;
+  E.ch_kind = M.ch_kind;
+  E.ch_a = M.ch_a;
+  E.ch_pkt = M.ch_pkt;
+  E.lookahead = M.lookahead;
+  E.tmn = ~0ull;
+  E.wnd = ~0ull;
+  E.demote = false;
+  HStat hs{0, 0, 0, 0, false};
+  // 2a. stateless node parts, in parallel (Receive: rx counter, MacRx trace, route, TTL)
+  for (uint32_t j = lane; j < n; j += HB) {
+    const uint32_t s = gs[j];
+    const uint64_t key = gk[j];
+    const uint32_t kind = M.wkind[base + s] & 0xffu, a = M.wa[base + s];
+    Pkt p = M.wpkt[base + s];
+    if (!stateless_event(M, c, kind, p)) continue;
+    E.now = tmin + (key >> 32);
+    E.uid = (uint32_t)key;
+    E.trseq = 0;
+    HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0};
+    if (kind == K_TX_COMPLETE) {
+      h.op = ACT_KICK;
+      h.dev = a;
+    } else {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive -> IpForward
+      atomicAdd(&M.devc[a].rx_packets, 1u);
+      p.size -= 2;
+      trace_call(M, E, NSGPU_TR_RX, a, p);
+      const uint32_t out = route_of(M, c, p);
+      if (out == 0xffffffffu) {
+        hs.no_route++;
+      } else {
+        p.ttl -= 1;
+        if (p.ttl == 0) {
+          hs.ttl_drops++;
+        } else {
+          h.op = ACT_SEND;
+          h.dev = out;
+          h.p = p;
+        }
+      }
+    }
+    h.seq = E.trseq;
+    M.hx[s] = h;
+  }
+  // 2b. node parts that read or write node / application state: serially, in key order
+  if (lane == 0) {
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t s = gs[j];
+      const uint64_t key = gk[j];
+      const uint32_t kw = M.wkind[base + s], a = M.wa[base + s];
+      const Pkt p = M.wpkt[base + s];
+      if (stateless_event(M, c, kw & 0xffu, p)) continue;
+      const uint64_t rel = key >> 32;
+      E.now = tmin + rel;
+      E.slot0 = s * M.maxc;
+      E.n = 0;
+      E.uid = (uint32_t)key;
+      E.trseq = 0;
+      E.demote = rel == slo || rel == shi;
+      const NodeOut o = node_part(M, E, kw, a, p, sink, hs, true);
+      M.hx[s] = HubEv{o.act.op, o.act.dev, o.act.p, o.post.delay, o.post.valid ? o.post.kind : 0u, o.post.a, E.n,
+                      E.trseq, o.cancelled ? 1u : 0u, 0};
+    }
+  }
+  __syncthreads();
+  // 3. device steps and trailing children, serially in key order, the device state in registers
+  if (lane == 0) {
+    DevCache D;
+    D.d = NOSRC;
+    uint32_t ts0_it = 0, pending = 0;
+    uint64_t cur_rel = 0;
+    for (uint32_t it = 0; it <= n; it++) {
+      const uint64_t key = it < n ? gk[it] : ~0ull;
+      const uint64_t rel = it < n ? (key >> 32) : ~0ull;
+      if (it > 0 && rel > cur_rel && pending) {
+        // the inline DoForwardUp leaves of this node's events at cur_rel (positions [ts0_it, it))
+        for (uint32_t jt = ts0_it; jt < it; jt++) {
+          const uint32_t xr = gs[jt];
+          const uint32_t ncr = M.nchild[xr];
+          for (uint32_t j = 0; j < ncr; j++) {
+            const uint32_t sl = xr * M.maxc + j;
+            if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
+            const uint32_t sa = M.ch_a[sl];
+            if (M.app_flags[sa] & 2u) {
+              M.appc[sa].rx_packets++;
+              M.appc[sa].rx_bytes += M.ch_pkt[sl].size - 28;
+            }
+          }
+        }
+        pending = 0;
+      }
+      if (it == n) break;
+      if (it == 0 || rel > cur_rel) {
+        ts0_it = it;
+        cur_rel = rel;
+      }
+      const uint32_t s = gs[it];
+      const HubEv h = M.hx[s];
+      E.now = tmin + rel;
+      E.slot0 = s * M.maxc;
+      E.n = h.n;
+      E.uid = (uint32_t)key;
+      E.trseq = h.seq;
+      E.demote = rel == slo || rel == shi;
+      hs.cancelled += h.cancelled;
+      device_act_cached(M, E, Act{h.op, h.dev, h.p}, D);
+      if (h.pkind) E.child(h.pdelay, c, h.pkind, h.pa, Pkt{0, 0, 0, 0});
+      uint32_t ni = 0;
+      if (rel < inline_lim)
+        for (uint32_t j = 0; j < E.n; j++) ni += (M.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
+      M.nchild[s] = E.n;
+      M.ninl[s] = ni;
+      pending += ni;
+    }
+    D.flush(M);
+  }
+  publish_min<HB>(R, E.tmn, E.wnd);
+  const uint64_t nr = wave_sum64(hs.no_route), td = wave_sum64(hs.ttl_drops);
+  if (lane == 0) {
+    if (hs.stop) C.stop_seen = 1;
+    if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
+    if (td) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)td);
+    if (nr) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)nr);
+    if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
+  }
+  __syncthreads();
+}
+
+// ---- k2_handle: pool maintenance (tombstones, free slots, fresh children -> pool) ----
+__device__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool handle, uint32_t W) {
+  const uint64_t tstride = (uint64_t)NMB * HB;
+  const uint64_t nfree = C.nfree, nF = C.nF, Pe = C.P_end;
+  if (!run) {
+    for (uint64_t w0 = (uint64_t)mb * HB; w0 < W; w0 += tstride) {  // wave-uniform
+      const uint64_t s = w0 + threadIdx.x;
+      const uint32_t src = s < W ? M.wsrc[s] : NOSRC;
+      const bool f = src != NOSRC;
+      if (f) M.ev_ts[0][src] = TOMB;
+      const uint64_t p = wave_alloc64(&C.npush, f);
+      if (f) M.fstack[nfree + p] = src;
+    }
+    if (!handle) {  // the window becomes a sorted run: its slot tables are not used
+      const uint64_t ws = W < (uint32_t)WCAP ? W : (uint32_t)WCAP;
+      for (uint64_t s = (uint64_t)mb * HB + threadIdx.x; s < ws; s += tstride) {
+        const uint32_t c = M.wctx[s];
+        if (c < M.n_nodes) M.node_cnt[c] = 0;
+      }
+    }
+  }
+  for (uint64_t j = (uint64_t)mb * HB + threadIdx.x; j < nF; j += tstride) {
+    const uint64_t dst = j < nfree ? (uint64_t)M.fstack[nfree - 1 - j] : Pe + (j - nfree);
+    if (dst < M.pool_cap) {
+      M.ev_ts[0][dst] = M.f_ts[j];
+      M.ev_uid[0][dst] = M.f_uid[j];
+      M.ev_ctx[0][dst] = M.f_ctx[j];
+      M.ev_kind[0][dst] = M.f_kind[j];
+      M.ev_a[0][dst] = M.f_a[j];
+      M.ev_pkt[0][dst] = M.f_pkt[j];
+    } else {
+      atomicOr(M.error, 1u);
+    }
+  }
+}
+
+__global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
+  __shared__ uint64_t lds64[K2_LDS_WORDS / 2];
+  uint32_t *lds = reinterpret_cast<uint32_t *>(lds64);
+  PH_BEGIN();
+  Ctl &C = *M.C;
+  if (C.done || C.mode >= MODE_SORT) {
+    if (C.done == 1 && blockIdx.x == 0 && threadIdx.x == 0) C.done = 2;  // the final window is appended
+    return;
+  }
+  const bool run = C.mode == MODE_RUN;
+  const uint32_t W = C.W, base = run ? C.wbase : 0;
+  const bool handle = run || (W <= (uint32_t)WCAP && !C.force_run);
+  Red &R = C.red[C.rt];
+  const uint32_t bx = blockIdx.x;
+  PH_MARK(8);
+  if (bx < (uint32_t)NHB) {
+    if (handle) handle_node2(M, C, bx * HB + threadIdx.x, W, base, R, lds);
+  } else if (bx < (uint32_t)(NHB + NRB)) {
+    if (!run && handle) rank_tile(M, C, bx - NHB);
+  } else if (bx < (uint32_t)(NHB + NRB + NHUB)) {
+    if (handle) {
+      const uint32_t hb = bx - (NHB + NRB);
+      const uint32_t nh = C.nhub < (uint32_t)MAXHUB ? C.nhub : (uint32_t)MAXHUB;
+      for (uint32_t h = hb; h < nh; h += NHUB) hub_node(M, C, M.hub_list[h], W, base, run, R, hb, lds);
+    }
+  } else {
+    maintain(M, C, bx - (NHB + NRB + NHUB), run, handle, W);
+  }
+  PH_MARK(9);
+}
+
+// ---- k2_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
+__global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
+  Ctl &C = *M.C;
+  if (C.done || C.mode >= MODE_SORT) return;
+  constexpr int RPT = WCAP / SCAN_THREADS;
+  __shared__ uint32_t l_slot[WCAP], l_cnt[WCAP], l_rel[WCAP], gstart[WCAP];
+  PH_BEGIN();
+  const int tid = threadIdx.x;
+  const bool run = C.mode == MODE_RUN;
+  const uint32_t W = C.W;
+  const bool handled = run || (W <= (uint32_t)WCAP && !C.force_run);
+  const uint32_t base = run ? C.wbase : 0;
+  // ---- pool bookkeeping: the free stack loses the slots the fresh children took and gains the
+  // window's; its pushed part is moved down over the popped hole
+  const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
+  const uint64_t consumed = nF < nfree ? nF : nfree;
+  const uint64_t mv = consumed < npush ? consumed : npush;
+  for (uint64_t i = tid; i < mv; i += SCAN_THREADS) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
+  if (handled) {
+    const uint32_t nh = C.nhub < (uint32_t)MAXHUB ? C.nhub : (uint32_t)MAXHUB;
+    for (uint32_t h = tid; h < nh; h += SCAN_THREADS) M.node_cnt[M.hub_list[h]] = 0;
+  }
+  if (!handled) {  // the window overflowed WCAP: it becomes a sorted run (host radix sort), nothing dispatched yet
+    __syncthreads();
+    if (tid == 0) {
+      C.nfree = nfree - consumed + npush;
+      C.P_end += nF > nfree ? nF - nfree : 0;
+      C.live = C.live - npush + nF;
+      C.npush = 0;
+      C.nF = 0;
+      C.nhub = 0;
+      C.rW = W;
+      C.r0 = 0;
+      C.W = 0;
+      C.pvalid = 0;
+      C.refits++;
+      C.force_run = 0;
+      C.mode = MODE_SORT;
+    }
+    return;
+  }
+  uint32_t pr[RPT], pc[RPT], pctx[RPT];
+  uint64_t pkey[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t i = tid + q * SCAN_THREADS;
+    pr[q] = run ? i : M.wrank[i];
+    pc[q] = M.nchild[i] | (M.ninl[i] << 16);
+    pkey[q] = i < W ? M.wkey[base + i] : 0;  // (a run's last chunk ends before the array does)
+    pctx[q] = i < W ? M.wctx[base + i] : 0;
+  }
+  PH_MARK(16);
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {  // slot order -> rank order; keys / contexts kept for the next k2_pa
+    const uint32_t i = tid + q * SCAN_THREADS;
+    if (i < W) {
+      const uint32_t r = pr[q];
+      if (!run) M.wrank[i] = 0;
+      M.pwkey[i] = pkey[q];
+      M.pwctx[i] = pctx[q];
+      l_slot[r] = i;
+      l_cnt[r] = pc[q];
+      l_rel[r] = (uint32_t)(pkey[q] >> 32);
+    }
+  }
+  __syncthreads();
+  PH_MARK(17);
+  uint32_t nc[RPT], ni[RPT], hd[RPT];
+  uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
+  uint32_t prev_rel = (tid * RPT < (int)W && tid > 0) ? l_rel[tid * RPT - 1] : 0;
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    nc[q] = ni[q] = hd[q] = 0;
+    if (r < W) {
+      nc[q] = l_cnt[r] & 0xffffu;
+      ni[q] = l_cnt[r] >> 16;
+      const uint32_t rel = l_rel[r];
+      hd[q] = r == 0 || rel != prev_rel;
+      prev_rel = rel;
+    }
+    sum += (uint64_t)nc[q] | ((uint64_t)ni[q] << 21) | ((uint64_t)hd[q] << 42);
+  }
+  const int lane = tid & 63, wid = tid >> 6;
+  uint64_t inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t w = __shfl_up(inc, o);
+    if (lane >= o) inc += w;
+  }
+  __shared__ uint64_t wsum64[SCAN_THREADS / 64];
+  if (lane == 63) wsum64[wid] = inc;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+  for (int w = 0; w < SCAN_THREADS / 64; w++) {
+    const uint64_t s = wsum64[w];
+    off += w < wid ? s : 0;
+    tot += s;
+  }
+  const uint64_t ex = off + inc - sum;
+  const uint32_t tc = (uint32_t)(tot & 0x1fffffu), tinl = (uint32_t)((tot >> 21) & 0x1fffffu),
+                 ng = (uint32_t)(tot >> 42);
+  uint32_t bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu), bh = (uint32_t)(ex >> 42);
+  uint32_t g[RPT], ipr[RPT], cpr[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    bh += hd[q];
+    g[q] = bh - 1;
+    cpr[q] = bc;
+    ipr[q] = bi;
+    if (r < W && hd[q]) gstart[g[q]] = r;
+    bc += nc[q];
+    bi += ni[q];
+  }
+  __syncthreads();
+  PH_MARK(18);
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    if (r < W) l_cnt[r] = ipr[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    if (r < W) {
+      const uint32_t first = gstart[g[q]];
+      const uint32_t last = (g[q] + 1 < ng ? gstart[g[q] + 1] : W) - 1;
+      M.sinfo[l_slot[r]] = make_uint4(r + (tinl ? l_cnt[first] : 0), last + 1 + ipr[q], cpr[q], ipr[q]);
+    }
+  }
+  PH_MARK(19);
+  if (tid == 0) {
+    C.pK0 = C.K;
+    C.puid0 = C.uid;
+    C.ptmin = C.tmin;
+    C.pinline_lim = C.inline_lim;
+    C.pW = W;
+    C.pinl = tinl;
+    C.pvalid = 1;
+    if (W) C.last_ts = C.tmin + l_rel[W - 1];
+    C.K += W + tinl;
+    C.uid += tc;
+    C.nfree = nfree - consumed + npush;
+    C.P_end += nF > nfree ? nF - nfree : 0;
+    C.live = C.live - npush + nF;
+    C.npush = 0;
+    C.nF = 0;
+    C.nhub = 0;
+    C.force_run = 0;  // (a run chunk's slot tables may set it; it only matters for a normal window)
+    bool flip = true;
+    if (run) {
+      C.r0 += W;
+      if (C.r0 >= C.rW) C.mode = MODE_NORMAL;
+      else flip = false;  // the run's chunks keep folding into the same reduction
+    }
+    if (flip) {
+      const uint32_t rt = C.rt;
+      C.red[rt ^ 1].tmin = C.red[rt ^ 1].wend = C.red[rt ^ 1].stopts = ~0ull;  // consumed
+      C.rt = rt ^ 1;
+      C.wkmax = 0;
+    }
+    C.windows++;
+    if (W > C.max_window) C.max_window = W;
+    C.W = 0;
+    const uint64_t pending = C.live + (tc - tinl) + (C.mode == MODE_RUN ? C.rW - C.r0 : 0);
+    bool done = C.stop_seen || pending == 0;
+    if (C.P_end > M.pool_cap) {
+      atomicOr(M.error, 1u);
+      done = true;
+    }
+    if (C.windows >= C.max_windows && !done) {
+      atomicOr(M.error, 4u);
+      done = true;
+    }
+    if (done) C.done = 1;
+    else if (C.mode == MODE_NORMAL && C.P_end > 65536 && C.live * 4 < C.P_end) C.mode = MODE_COMPACT;
+  }
+  PH_MARK(20);
+}
+
+// ================================ host-driven steps (rare) ================================
+// ---- LSD radix sort of (key, slot) pairs: 8-bit digits, tiles of RS_TILE, stable ----
+constexpr int RS_T = 256, RS_IPT = 16, RS_TILE = RS_T * RS_IPT;
+
+__global__ __launch_bounds__(RS_T) void k_rs_hist(const uint64_t *__restrict__ keys, uint64_t n, int shift,
+                                                  uint32_t *__restrict__ hist, uint32_t ntiles) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+  for (int k = 0; k < RS_IPT; k++) {
+    const uint64_t i = b0 + (uint64_t)k * RS_T + threadIdx.x;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// Exclusive scan of m counts in place (digit-major: every tile's offset of every digit), one block.
+__global__ __launch_bounds__(1024) void k_rs_scan(uint32_t *__restrict__ hist, uint64_t m) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t c0 = 0; c0 < m; c0 += 4096) {
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint64_t i = c0 + threadIdx.x * 4 + q;
+      v[q] = i < m ? hist[i] : 0u;
+      s += v[q];
+    }
+    uint32_t tot;
+    const uint32_t ex = block_exscan<1024>(s, wsum, &tot);
+    uint32_t run = carry + ex;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint64_t i = c0 + threadIdx.x * 4 + q;
+      if (i < m) hist[i] = run;
+      run += v[q];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                     uint64_t n, int shift, const uint32_t *__restrict__ hist,
+                                                     uint32_t ntiles) {
+  __shared__ uint32_t off[256];
+  __shared__ uint32_t wc[RS_T / 64][256];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  off[tid] = hist[(uint64_t)tid * ntiles + blockIdx.x];
+  for (int w = 0; w < RS_T / 64; w++) wc[w][tid] = 0;
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int k = 0; k < RS_IPT; k++) {
+    const uint64_t i = b0 + (uint64_t)k * RS_T + tid;
+    const bool valid = i < n;
+    const uint64_t key = valid ? kin[i] : 0;
+    const uint32_t v = valid ? (vin ? vin[i] : (uint32_t)i) : 0u;
+    const uint32_t d = (uint32_t)(key >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bt = 0; bt < 8; bt++) {
+      const bool bit = (d >> bt) & 1u;
+      const uint64_t bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & below);
+    if (valid && rank == 0) wc[wid][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t o = off[d] + rank;
+      for (int w = 0; w < wid; w++) o += wc[w][d];
+      kout[o] = key;
+      vout[o] = v;
+    }
+    __syncthreads();
+    uint32_t t = 0;
+    for (int w = 0; w < RS_T / 64; w++) {
+      t += wc[w][tid];
+      wc[w][tid] = 0;
+    }
+    off[tid] += t;
+    __syncthreads();
+  }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_rs_gather(const uint32_t *__restrict__ perm, const T *__restrict__ src,
+                                                   T *__restrict__ dst, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) dst[i] = src[perm[i]];
+}
+
+// ---- pool compaction: live entries of [0, P_end) -> pool 1, dense (order is irrelevant) ----
+__global__ __launch_bounds__(256) void k_cmp(const P2PDev M, uint64_t P) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t b0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) & ~63ull; b0 < P; b0 += stride) {
+    const uint64_t i = b0 + (threadIdx.x & 63);
+    const uint64_t ts = i < P ? M.ev_ts[0][i] : TOMB;
+    const bool live = ts != TOMB;
+    const uint64_t o = wave_alloc64(M.cmp_cnt, live);
+    if (live) {
+      M.ev_ts[1][o] = ts;
+      M.ev_uid[1][o] = M.ev_uid[0][i];
+      M.ev_ctx[1][o] = M.ev_ctx[0][i];
+      M.ev_kind[1][o] = M.ev_kind[0][i];
+      M.ev_a[1][o] = M.ev_a[0][i];
+      M.ev_pkt[1][o] = M.ev_pkt[0][i];
+    }
+  }
+}
+
+// Mode transitions the host makes after a host-driven step.
+__global__ void k_after_sort(const P2PDev M) {
+  M.C->mode = MODE_RUN;
+  M.C->r0 = 0;
+}
+__global__ void k_after_compact(const P2PDev M, uint64_t live) {
+  M.C->P_end = live;
+  M.C->live = live;
+  M.C->nfree = 0;
+  M.C->mode = MODE_NORMAL;
+}

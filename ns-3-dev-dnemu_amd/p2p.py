@@ -323,6 +323,28 @@ def dumbbell(n_leaves=4, leaf_bps=1_000_000, leaf_delay_ns=2_000_000, router_bps
     return sc
 
 
+def incast(n_src, bps=10_000_000, delay_ns=1_000_000, qmax=100, rate_bps=1_000_000, size=512, max_bytes=0,
+           start_ns=1_000_000_000, stop_ns=1_050_000_000, sim_stop_ns=1_100_000_000):
+    """Incast star: node 0 is a hub with a PacketSink, nodes 1..n_src each link to it (PointToPointHelper
+    per leaf, creation order) and run an OnOff flow to it (OnTime 1, OffTime 0), all started at the
+    same time — so every window holds n_src same-time Receives at one node that is also the sink
+    (the hub node path with local deliveries, and with n_src > WCAP a sorted run whose chunks cut a
+    same-time group of zero-delay DoForwardUp leaves)."""
+    sc = Scenario(n_src + 1)
+    for i in range(1, n_src + 1):
+        da, db = sc.link(i, 0, bps, delay_ns, qmax)
+    sc.install_stack()
+    for i in range(n_src):
+        sc.assign_link(2 * i, 2 * i + 1, ip("10.0.0.0") + (i << 8))
+    sc.add_sink(0, 0, 0)
+    for i in range(1, n_src + 1):
+        sc.add_onoff(i, 0, start_ns, stop_ns, rate_bps=rate_bps, size=size, on_s=1.0, off_s=0.0, max_bytes=max_bytes,
+                     remote_addr=sc.dev_addr[1])
+    sc.stop(sim_stop_ns)
+    sc.route_bfs()
+    return sc
+
+
 def dumbbell_owner(n_leaves, nranks=2):
     """Node (systemId) of simple-distributed.cc: left side + router 1 on 0, router 2 + right side on 1
     (nranks > 2: the right side's leaves spread over ranks 1..nranks-1 in contiguous blocks)."""

@@ -71,7 +71,7 @@ def test_eager_launches_match_graph_replays():
     b = eng.run(log_n=100000)
     assert_same((a[0], a[1], a[2], a[3]), b)
     prof = eng.profile(sample_every=2)
-    assert set(prof) >= {"k_pa", "k_handle_rank", "k_scan"}
+    assert set(prof) >= {"k2_pa", "k2_handle", "k2_scan"}
     assert all(ms >= 0 for ms, _ in prof.values())
     c = eng.results()
     assert c[0].digest == a[0].digest and c[0].dispatched == a[0].dispatched
