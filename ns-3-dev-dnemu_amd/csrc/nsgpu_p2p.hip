@@ -498,9 +498,11 @@ __device__ __forceinline__ void appobj_start(const P2PDev &M, Emit &E, uint32_t 
 __device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const Pkt &p) {
   const uint32_t slot = (p.app & NSGPU_PKT_REPLY) ? M.app_src_slot[p.app & ~NSGPU_PKT_REPLY] : M.app_dst_slot[p.app];
   if (M.route) return M.route[(uint64_t)n * M.n_dst + slot];
-  // compressed: binary search of the node's exceptions (a dumbbell router holds one per leaf)
+  // compressed: binary search of the node's exceptions (a dumbbell router holds one per leaf); a node
+  // with an exception for every slot has them at their slot's position (ascending, distinct)
   const uint64_t e1 = M.route_exc_off[n + 1];
   uint64_t lo = M.route_exc_off[n], hi = e1;
+  if (hi - lo == M.n_dst) return M.route_exc_dev[lo + slot];
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     if (M.route_exc_slot[mid] < slot) lo = mid + 1;
@@ -2223,7 +2225,13 @@ static int host_step(nsgpu_p2p *h, const Ctl &c) {
   const P2PDev &M = h->M;
   if (c.mode == MODE_SORT) {
     const uint64_t n = c.rW;
-    const int bits = c.wkmax ? 64 - __builtin_clzll(c.wkmax) : 1;
+    NSGPU_HIP(hipMemsetAsync(M.cmp_cnt, 0, sizeof(uint64_t), s));
+    hipLaunchKernelGGL(k_rs_or, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 2048)), dim3(256), 0, s, M.wkey, n,
+                       (unsigned long long *)M.cmp_cnt);
+    uint64_t kor = 0;
+    NSGPU_HIP(hipMemcpyAsync(&kor, M.cmp_cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+    const int bits = kor ? 64 - __builtin_clzll(kor) : 1;
     const int passes = (bits + 7) / 8;
     const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     uint64_t *kin = M.wkey, *kout = M.s_key2;

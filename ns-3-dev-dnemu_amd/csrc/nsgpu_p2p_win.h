@@ -38,7 +38,7 @@ struct HubEv {
   int64_t pdelay;      // trailing child (OnOffApplication::ScheduleNextTx after SendPacket)
   uint32_t pkind, pa;  // pkind == 0: none
   uint32_t n, seq;     // children and trace sink calls the node part made
-  uint32_t cancelled, pad;
+  uint32_t cancelled, pad;  // pad: the node part's inline DoForwardUp children
 };
 
 constexpr int HUBL = 1024;  // events of a hub a block sorts in LDS (more: the window is dispatched as a run)
@@ -67,9 +67,17 @@ __device__ __forceinline__ uint64_t wave_alloc64(uint64_t *ctr, bool want) {
   return (uint64_t)base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
+constexpr uint32_t NOHOLD = 0xffffffffu;  // widx of a window event no holder runs (NetDevice::Start)
+
 // Window record `slot` of node `ctx` -> the node's slot table (local slot index); the node that
-// reaches CH + 1 events becomes a hub.
-__device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t slot, uint32_t ctx) {
+// reaches CH + 1 events becomes a hub.  NetDevice::Start is a no-op (the device was started by
+// Node::Start): it is dispatched (logged, uid-ranked) but no holder runs it — a dumbbell router has
+// one per leaf link at time 0.
+__device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t slot, uint32_t ctx, uint32_t kind) {
+  if ((kind & 0xffu) == K_DEV_START) {  // (k2_handle writes its zero child counts: k2_pa still reads the
+    M.widx[slot] = NOHOLD;               //  last window's counts of this slot)
+    return;
+  }
   uint32_t idx = 0;
   if (ctx < M.n_nodes) {
     idx = atomicAdd(&M.node_cnt[ctx], 1u);
@@ -87,13 +95,22 @@ __device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t
 // a child (src == NOSRC) is parked in the fresh buffer, a pool entry stays where it is; both fold
 // into the next window's reduction.  Lanes that call it must be converged (ballots).
 __device__ __forceinline__ void k2_place(const P2PDev &M, Ctl &C, const WinBound &b, bool run, bool valid,
-                                         const Ev &e, uint32_t src, Red &R, uint64_t &tmn, uint64_t &wnd,
-                                         uint64_t &kmax) {
+                                         const Ev &e, uint32_t src, Red &R, uint64_t &tmn, uint64_t &wnd) {
   const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
   const bool in = valid && !run && (e.ts - b.tmin <= b.span) && pk <= b.bound;
   const bool park = valid && !in && src == NOSRC;
-  const uint32_t slot = wave_alloc32(&C.W, in);
-  const uint64_t fi = wave_alloc64(&C.nF, park);
+  // both counters at once (one lane, two atomics in flight): window slots and fresh-buffer entries
+  const uint64_t bin = __ballot(in), bpk = __ballot(park);
+  const int lane = threadIdx.x & 63;
+  uint32_t bw = 0;
+  unsigned long long bf = 0;
+  if (lane == 0) {  // (every lane of the wave calls k2_place)
+    if (bin) bw = atomicAdd(&C.W, (uint32_t)__popcll(bin));
+    if (bpk) bf = atomicAdd((unsigned long long *)&C.nF, (unsigned long long)__popcll(bpk));
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t slot = (uint32_t)__shfl(bw, 0) + (uint32_t)__popcll(bin & below);
+  const uint64_t fi = (uint64_t)__shfl(bf, 0) + (uint64_t)__popcll(bpk & below);
   if (in) {
     if (slot < M.runcap) {
       M.wkey[slot] = pk;
@@ -102,8 +119,7 @@ __device__ __forceinline__ void k2_place(const P2PDev &M, Ctl &C, const WinBound
       M.wa[slot] = e.a;
       M.wpkt[slot] = e.p;
       M.wsrc[slot] = src;
-      if (slot < (uint32_t)WCAP) node_table_add(M, C, slot, e.ctx);
-      kmax = pk > kmax ? pk : kmax;
+      if (slot < (uint32_t)WCAP) node_table_add(M, C, slot, e.ctx, e.kind);
     } else {
       atomicOr(M.error, 1u);
     }
@@ -165,7 +181,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     }
   }
   PH_MARK(0);
-  uint64_t tmn = ~0ull, wnd = ~0ull, digest = 0, kmax = 0;
+  uint64_t tmn = ~0ull, wnd = ~0ull, digest = 0;
   if (slot_role) {
     // ---- slot g of the last window: dispatch rank (log, digest), inline children, children -> pending
     const bool vs = g < pW;
@@ -215,7 +231,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
             valid = partition;
           }
         }
-        k2_place(M, C, b, run, valid, e, NOSRC, R, tmn, wnd, kmax);
+        k2_place(M, C, b, run, valid, e, NOSRC, R, tmn, wnd);
       }
     }
   } else if (partition && !run) {
@@ -224,20 +240,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     const uint64_t w0 = (g - WCAP) & ~63ull, ws = (stride - WCAP);
     for (uint64_t base = w0; base < P; base += ws) {  // wave-uniform trip count
       const uint64_t i = base + (threadIdx.x & 63);
-      uint64_t ts = TOMB;
-      if (i < P) ts = M.ev_ts[0][i];
-      const bool valid = ts != TOMB;
-      Ev e{ts, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-      if (valid) {
-        e.uid = M.ev_uid[0][i];
-        e.kind = M.ev_kind[0][i];
-        if (e.ts - b.tmin <= b.span && (((e.ts - b.tmin) << 32) | e.uid) <= b.bound) {  // a window event
-          e.ctx = M.ev_ctx[0][i];
-          e.a = M.ev_a[0][i];
-          e.p = M.ev_pkt[0][i];
-        }
-      }
-      k2_place(M, C, b, false, valid, e, (uint32_t)i, R, tmn, wnd, kmax);
+      Ev e{TOMB, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+      if (i < P) e = load_pool(M, 0, i);  // every field at once: one memory round trip
+      k2_place(M, C, b, false, e.ts != TOMB, e, (uint32_t)i, R, tmn, wnd);
     }
   } else if (partition && run) {
     // ---- the next chunk of the sorted run: per-node slot tables, chunk bounds
@@ -252,16 +257,12 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       C.split_lo = (r0 > 0 && (M.wkey[r0 - 1] >> 32) == klo) ? klo : ~0ull;
       C.split_hi = (r1 < rW && (M.wkey[r1] >> 32) == khi) ? khi : ~0ull;
     }
-    if (s < Wc) node_table_add(M, C, (uint32_t)s, M.wctx[r0 + s]);
+    if (s < Wc) node_table_add(M, C, (uint32_t)s, M.wctx[r0 + s], M.wkind[r0 + s]);
   }
   PH_MARK(1);
   publish_min<TB>(R, tmn, wnd);
   digest = wave_sum64(digest);
-  kmax = wave_max64(kmax);
-  if ((threadIdx.x & 63) == 0) {
-    if (digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
-    if (kmax) atomicMax((unsigned long long *)&C.wkmax, (unsigned long long)kmax);
-  }
+  if ((threadIdx.x & 63) == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
   PH_MARK(2);
 }
 
@@ -276,7 +277,12 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
   uint64_t *chk = reinterpret_cast<uint64_t *>(lds + HB * CH);
   uint64_t tmn = ~0ull, wnd = ~0ull;
   HStat hs{0, 0, 0, 0, false};
-  if (i0 < W && M.widx[i0] == 0) {  // the holder
+  const uint32_t wi = i0 < W ? M.widx[i0] : 1u;
+  if (wi == NOHOLD) {  // NetDevice::Start: dispatched, no children
+    M.nchild[i0] = 0;
+    M.ninl[i0] = 0;
+  }
+  if (wi == 0) {  // the holder
     const uint32_t c = M.wctx[base + i0];
     uint32_t n = 1;
     int32_t sink = -1;
@@ -297,7 +303,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
         if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
           uint32_t m = NSLOT;
           for (uint32_t x = 0; x < W && m < n; x++)
-            if (M.wctx[base + x] == c && M.widx[x] >= (uint32_t)NSLOT) my[m++] = x;
+            if (M.wctx[base + x] == c && M.widx[x] >= (uint32_t)NSLOT && M.widx[x] != NOHOLD) my[m++] = x;
         }
         for (uint32_t j = 0; j < n; j++) mk[j] = M.wkey[base + my[j]];
         for (uint32_t a = 1; a < n; a++) {  // insertion sort by key
@@ -473,7 +479,7 @@ __device__ __forceinline__ void device_act_cached(const P2PDev &M, Emit &E, cons
 // Events whose node part touches no node state: TransmitComplete, and a Receive that IpForward
 // sends on (its node is not the datagram's destination).
 __device__ __forceinline__ bool stateless_event(const P2PDev &M, uint32_t c, uint32_t kind, const Pkt &p) {
-  if (kind == K_TX_COMPLETE) return true;
+  if (kind == K_TX_COMPLETE || kind == K_DEV_START) return true;  // (NetDevice::Start: no-op)
   if (kind != K_RECEIVE) return false;
   const bool reply = (p.app & NSGPU_PKT_REPLY) != 0;
   return (reply ? M.app_node[p.app & ~NSGPU_PKT_REPLY] : M.app_dst_node[p.app]) != c;
@@ -504,6 +510,162 @@ __device__ __forceinline__ void bitonic_sort_lds(uint64_t *k, uint32_t *v, uint3
     }
 }
 
+// ---- parallel device steps of one device (a hub whose device steps all use one queue) ----
+// With c = the queue length while the device transmits and c = -1 while it is idle (idle implies an
+// empty queue), Send is c -> min (c + 1, qmax) (c == qmax: Queue::Drop; c == -1: Enqueue + Dequeue +
+// TransmitStart at once) and TransmitComplete is c -> c - 1 (a dequeue + TransmitStart if c >= 1).
+// Maps of the form x -> clamp (x + a, lo, hi) are closed under composition, so a wave scan of the
+// segments' composed maps gives every event its input state; a second scan of enqueue / dequeue counts
+// gives the ring positions.  Results (traces, counters, children, state) equal the serial pass's.
+struct CMap {
+  int32_t a, lo, hi;
+};
+__device__ __forceinline__ int32_t clampi(int32_t x, int32_t l, int32_t h) { return x < l ? l : (x > h ? h : x); }
+__device__ __forceinline__ CMap cmap_then(const CMap &f, const CMap &g) {  // g after f
+  return CMap{f.a + g.a, clampi(f.lo + g.a, g.lo, g.hi), clampi(f.hi + g.a, g.lo, g.hi)};
+}
+constexpr int32_t CBIG = 1 << 28;
+
+// Returns false (nothing done) when the batch would reuse a ring slot (more enqueues than the ring
+// holds beyond the queued packets): the serial pass runs instead.
+__device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d, const uint32_t *gs,
+                                const uint64_t *gk, uint32_t n, uint32_t j0s, uint32_t j1s, uint64_t tmin, HStat &hs) {
+  const int lane = threadIdx.x;
+  const int32_t qmax = (int32_t)M.dev_qmax[d];
+  const uint32_t busy0 = M.dev_busy[d], cnt0 = M.q_count[d], head0 = M.q_head[d], qcap = M.qcap;
+  const int32_t c0 = busy0 ? (int32_t)cnt0 : -1;
+  const uint64_t bps = M.dev_bps[d];
+  const int64_t ifg = M.dev_ifg[d], delay = M.dev_delay[d];
+  const uint32_t peer = M.dev_peer[d], peer_node = M.dev_node[peer];
+  Pkt *qb = M.q_buf + (uint64_t)d * qcap;
+  // pass A: the segment's composed map and its enqueue / dequeue counts
+  CMap f{0, -CBIG, CBIG};
+  for (uint32_t j = j0s; j < j1s; j++) {
+    const HubEv h = M.hx[gs[j]];
+    if (h.op == ACT_SEND) f = cmap_then(f, CMap{1, -CBIG, qmax});
+    else if (h.op == ACT_KICK) f = cmap_then(f, CMap{-1, -CBIG, CBIG});
+  }
+  CMap inc = f;
+  for (int o = 1; o < 64; o <<= 1) {
+    const CMap g{__shfl_up(inc.a, o), __shfl_up(inc.lo, o), __shfl_up(inc.hi, o)};
+    if (lane >= o) inc = cmap_then(g, inc);
+  }
+  CMap ex{__shfl_up(inc.a, 1), __shfl_up(inc.lo, 1), __shfl_up(inc.hi, 1)};
+  if (lane == 0) ex = CMap{0, -CBIG, CBIG};
+  const int32_t cin = clampi(c0 + ex.a, ex.lo, ex.hi);
+  const int32_t cfin = clampi(c0 + __shfl(inc.a, 63), __shfl(inc.lo, 63), __shfl(inc.hi, 63));
+  uint32_t ne = 0, nd = 0;
+  {
+    int32_t x = cin;
+    for (uint32_t j = j0s; j < j1s; j++) {
+      const uint32_t op = M.hx[gs[j]].op;
+      if (op == ACT_SEND) {
+        if (x < qmax) ne++;
+        if (x == -1) nd++;
+        x = x + 1 < qmax ? x + 1 : qmax;
+      } else if (op == ACT_KICK) {
+        if (x >= 1) nd++;
+        x -= 1;
+      }
+    }
+  }
+  const uint32_t ebefore = wave_exscan32(ne, lane), dbefore = wave_exscan32(nd, lane);
+  const uint32_t dtot = __shfl(dbefore + nd, 63), etot = __shfl(ebefore + ne, 63);
+  if (cnt0 + etot > qcap) return false;
+  // pass B1: enqueued packets into the ring (before any TransmitComplete reads one)
+  {
+    int32_t x = cin;
+    uint32_t e = ebefore;
+    for (uint32_t j = j0s; j < j1s; j++) {
+      const HubEv h = M.hx[gs[j]];
+      if (h.op == ACT_SEND) {
+        if (x >= 0 && x < qmax) {
+          Pkt p = h.p;
+          p.size += 2;
+          qb[(head0 + cnt0 + e) % qcap] = p;
+        }
+        if (x < qmax) e++;
+        x = x + 1 < qmax ? x + 1 : qmax;
+      } else if (h.op == ACT_KICK) {
+        x -= 1;
+      }
+    }
+  }
+  __syncthreads();
+  // pass B2: traces, counters, TransmitStart children, trailing children
+  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0, q5 = 0;
+  {
+    int32_t x = cin;
+    uint32_t dq = dbefore;
+    for (uint32_t j = j0s; j < j1s; j++) {
+      const uint32_t s = gs[j];
+      const uint64_t key = gk[j];
+      const HubEv h = M.hx[s];
+      E.now = tmin + (key >> 32);
+      E.slot0 = s * M.maxc;
+      E.n = h.n;
+      E.uid = (uint32_t)key;
+      E.trseq = h.seq;
+      E.demote = false;
+      hs.cancelled += h.cancelled;
+      bool go = false;
+      Pkt tx{0, 0, 0, 0};
+      if (h.op == ACT_SEND) {
+        Pkt p = h.p;
+        p.size += 2;  // PppHeader
+        if (x >= qmax) {
+          trace_call(M, E, NSGPU_TR_DROP, d, p);
+          q2++;
+          q3 += p.size;
+        } else {
+          trace_call(M, E, NSGPU_TR_ENQUEUE, d, p);
+          q0++;
+          q1 += p.size;
+          if (x == -1) {  // Enqueue + Dequeue: the packet leaves at once
+            tx = p;
+            trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);
+            q4++;
+            dq++;
+            go = true;
+          }
+        }
+        x = x + 1 < qmax ? x + 1 : qmax;
+      } else if (h.op == ACT_KICK) {
+        if (x >= 1) {
+          tx = qb[(head0 + dq) % qcap];
+          trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);
+          q4++;
+          dq++;
+          go = true;
+        }
+        x -= 1;
+      }
+      if (go) {
+        q5++;
+        const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)bps);
+        E.child(txTime + ifg, c, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
+        E.child(txTime + delay, peer_node, K_RECEIVE, peer, tx);
+      }
+      if (h.pkind) E.child(h.pdelay, c, h.pkind, h.pa, Pkt{0, 0, 0, 0});
+      M.nchild[s] = E.n;
+      M.ninl[s] = 0;
+    }
+  }
+  q0 = wave_sum32(q0), q1 = wave_sum32(q1), q2 = wave_sum32(q2), q3 = wave_sum32(q3), q4 = wave_sum32(q4),
+  q5 = wave_sum32(q5);
+  if (lane == 0) {
+    M.dev_busy[d] = cfin >= 0 ? 1u : 0u;
+    M.q_count[d] = cfin >= 0 ? (uint32_t)cfin : 0u;
+    M.q_head[d] = (head0 + dtot) % qcap;
+    uint32_t *w = reinterpret_cast<uint32_t *>(&M.devc[d]);  // not rx_packets: the node pass adds it atomically
+    const uint4 a = *reinterpret_cast<const uint4 *>(w);
+    const uint2 b2 = *reinterpret_cast<const uint2 *>(w + 4);
+    *reinterpret_cast<uint4 *>(w) = make_uint4(a.x + q0, a.y + q1, a.z + q2, a.w + q3);
+    *reinterpret_cast<uint2 *>(w + 4) = make_uint2(b2.x + q4, b2.y + q5);
+  }
+  return true;
+}
+
 // A hub node's window events, by one block: (1) its events in key order (slot order in a sorted run
 // chunk; otherwise at most HUBL of them, bitonic-sorted in LDS) into the block's global scratch list;
 // (2a) node parts without node state (TransmitComplete; Receive -> IpForward) in parallel; (2b) the
@@ -520,7 +682,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   uint32_t n = 0;
   for (uint32_t x0 = 0; x0 < W; x0 += HB) {
     const uint32_t x = x0 + lane;
-    const bool m = x < W && M.wctx[base + x] == c;
+    const bool m = x < W && M.wctx[base + x] == c && M.widx[x] != NOHOLD;
     const uint64_t bm = __ballot(m);
     if (m) {
       const uint32_t p = n + (uint32_t)__popcll(bm & below);
@@ -559,121 +721,177 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   E.wnd = ~0ull;
   E.demote = false;
   HStat hs{0, 0, 0, 0, false};
-  // 2a. stateless node parts, in parallel (Receive: rx counter, MacRx trace, route, TTL)
-  for (uint32_t j = lane; j < n; j += HB) {
-    const uint32_t s = gs[j];
-    const uint64_t key = gk[j];
-    const uint32_t kind = M.wkind[base + s] & 0xffu, a = M.wa[base + s];
-    Pkt p = M.wpkt[base + s];
-    if (!stateless_event(M, c, kind, p)) continue;
-    E.now = tmin + (key >> 32);
-    E.uid = (uint32_t)key;
-    E.trseq = 0;
-    HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0};
-    if (kind == K_TX_COMPLETE) {
-      h.op = ACT_KICK;
-      h.dev = a;
-    } else {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive -> IpForward
-      atomicAdd(&M.devc[a].rx_packets, 1u);
-      p.size -= 2;
-      trace_call(M, E, NSGPU_TR_RX, a, p);
-      const uint32_t out = route_of(M, c, p);
-      if (out == 0xffffffffu) {
-        hs.no_route++;
-      } else {
-        p.ttl -= 1;
-        if (p.ttl == 0) {
-          hs.ttl_drops++;
-        } else {
-          h.op = ACT_SEND;
-          h.dev = out;
-          h.p = p;
-        }
-      }
-    }
-    h.seq = E.trseq;
-    M.hx[s] = h;
-  }
-  // 2b. node parts that read or write node / application state: serially, in key order
-  if (lane == 0) {
-    for (uint32_t j = 0; j < n; j++) {
+  // the passes go through the list 64 events at a time: every lane loads one event's record into
+  // LDS (one memory round trip per batch), then the serial work reads LDS
+  uint64_t *b_key = reinterpret_cast<uint64_t *>(lds);  // [HB]
+  uint32_t *b_s = lds + 2 * HB, *b_kind = lds + 3 * HB, *b_a = lds + 4 * HB, *b_sl = lds + 5 * HB;
+  Pkt *b_pkt = reinterpret_cast<Pkt *>(lds + 6 * HB);    // [HB]
+  HubEv *b_h = reinterpret_cast<HubEv *>(lds + 10 * HB);  // [HB]
+  // 2. node parts: the stateless ones (TransmitComplete, NetDevice::Start, Receive -> IpForward: rx
+  //    counter, MacRx trace, route, TTL) by their own lane, the others serially by lane 0 in key order
+  for (uint32_t j0 = 0; j0 < n; j0 += HB) {
+    const uint32_t j = j0 + lane;
+    if (j < n) {
       const uint32_t s = gs[j];
       const uint64_t key = gk[j];
       const uint32_t kw = M.wkind[base + s], a = M.wa[base + s];
-      const Pkt p = M.wpkt[base + s];
-      if (stateless_event(M, c, kw & 0xffu, p)) continue;
-      const uint64_t rel = key >> 32;
-      E.now = tmin + rel;
-      E.slot0 = s * M.maxc;
-      E.n = 0;
-      E.uid = (uint32_t)key;
-      E.trseq = 0;
-      E.demote = rel == slo || rel == shi;
-      const NodeOut o = node_part(M, E, kw, a, p, sink, hs, true);
-      M.hx[s] = HubEv{o.act.op, o.act.dev, o.act.p, o.post.delay, o.post.valid ? o.post.kind : 0u, o.post.a, E.n,
-                      E.trseq, o.cancelled ? 1u : 0u, 0};
+      Pkt p = M.wpkt[base + s];
+      const uint32_t kind = kw & 0xffu;
+      const bool sl = stateless_event(M, c, kind, p);
+      b_s[lane] = s;
+      b_key[lane] = key;
+      b_kind[lane] = kw;
+      b_a[lane] = a;
+      b_pkt[lane] = p;
+      b_sl[lane] = sl;
+      if (sl) {
+        E.now = tmin + (key >> 32);
+        E.uid = (uint32_t)key;
+        E.trseq = 0;
+        HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0};
+        if (kind == K_TX_COMPLETE) {
+          h.op = ACT_KICK;
+          h.dev = a;
+        } else if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive -> IpForward
+          atomicAdd(&M.devc[a].rx_packets, 1u);
+          p.size -= 2;
+          trace_call(M, E, NSGPU_TR_RX, a, p);
+          const uint32_t out = route_of(M, c, p);
+          if (out == 0xffffffffu) {
+            hs.no_route++;
+          } else {
+            p.ttl -= 1;
+            if (p.ttl == 0) {
+              hs.ttl_drops++;
+            } else {
+              h.op = ACT_SEND;
+              h.dev = out;
+              h.p = p;
+            }
+          }
+        }
+        h.seq = E.trseq;
+        M.hx[s] = h;
+      }
     }
+    __syncthreads();
+    if (lane == 0) {
+      const uint32_t nb = n - j0 < (uint32_t)HB ? n - j0 : (uint32_t)HB;
+      for (uint32_t q = 0; q < nb; q++) {
+        if (b_sl[q]) continue;
+        const uint32_t s = b_s[q];
+        const uint64_t rel = b_key[q] >> 32;
+        E.now = tmin + rel;
+        E.slot0 = s * M.maxc;
+        E.n = 0;
+        E.uid = (uint32_t)b_key[q];
+        E.trseq = 0;
+        E.demote = rel == slo || rel == shi;
+        const NodeOut o = node_part(M, E, b_kind[q], b_a[q], b_pkt[q], sink, hs, true);
+        uint32_t ni = 0;
+        for (uint32_t jj = 0; jj < E.n; jj++) ni += (M.ch_kind[E.slot0 + jj] & 0xffu) == K_FWD_UP;
+        M.hx[s] = HubEv{o.act.op, o.act.dev, o.act.p, o.post.delay, o.post.valid ? o.post.kind : 0u, o.post.a, E.n,
+                        E.trseq, o.cancelled ? 1u : 0u, ni};
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  // 3. device steps and trailing children, serially in key order, the device state in registers
-  if (lane == 0) {
+  // 3. device steps and trailing children.  When every device step of the hub is on one device and no
+  //    event has inline children (a dumbbell router's burst), the steps are resolved in parallel
+  //    (hub_device_scan); otherwise serially in key order with the device state in registers.
+  const uint32_t mseg = (n + HB - 1) / HB, j0s = lane * mseg, j1s = j0s + mseg < n ? j0s + mseg : n;
+  uint32_t dmin = NOSRC, dmax = 0, inl = 0;
+  for (uint32_t j = j0s; j < j1s; j++) {
+    const HubEv h = M.hx[gs[j]];
+    if (h.op != ACT_NONE) {
+      dmin = h.dev < dmin ? h.dev : dmin;
+      dmax = h.dev > dmax ? h.dev : dmax;
+    }
+    inl |= h.pad;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t x = __shfl_xor(dmin, o), y = __shfl_xor(dmax, o), z = __shfl_xor(inl, o);
+    dmin = x < dmin ? x : dmin;
+    dmax = y > dmax ? y : dmax;
+    inl |= z;
+  }
+  bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && M.dev_qmax[dmin] >= 1 &&
+              !(M.dev_busy[dmin] == 0 && M.q_count[dmin] != 0);
+  if (fast) fast = hub_device_scan(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs);
+  if (!fast) {
     DevCache D;
     D.d = NOSRC;
     uint32_t ts0_it = 0, pending = 0;
     uint64_t cur_rel = 0;
-    for (uint32_t it = 0; it <= n; it++) {
-      const uint64_t key = it < n ? gk[it] : ~0ull;
-      const uint64_t rel = it < n ? (key >> 32) : ~0ull;
-      if (it > 0 && rel > cur_rel && pending) {
-        // the inline DoForwardUp leaves of this node's events at cur_rel (positions [ts0_it, it))
-        for (uint32_t jt = ts0_it; jt < it; jt++) {
-          const uint32_t xr = gs[jt];
-          const uint32_t ncr = M.nchild[xr];
-          for (uint32_t j = 0; j < ncr; j++) {
-            const uint32_t sl = xr * M.maxc + j;
-            if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
-            const uint32_t sa = M.ch_a[sl];
-            if (M.app_flags[sa] & 2u) {
-              M.appc[sa].rx_packets++;
-              M.appc[sa].rx_bytes += M.ch_pkt[sl].size - 28;
+    for (uint32_t j0 = 0; j0 <= n; j0 += HB) {
+      const uint32_t j = j0 + lane;
+      if (j < n) {
+        const uint32_t s = gs[j];
+        b_s[lane] = s;
+        b_key[lane] = gk[j];
+        b_h[lane] = M.hx[s];
+      }
+      __syncthreads();
+      if (lane == 0) {
+        const uint32_t nb = n - j0 < (uint32_t)HB ? n - j0 : (uint32_t)HB;
+        for (uint32_t q = 0; q <= nb; q++) {
+          const uint32_t it = j0 + q;
+          if (q == nb && it < n) break;  // (the next batch continues; the final flush runs at it == n)
+          const uint64_t key = it < n ? b_key[q] : ~0ull;
+          const uint64_t rel = it < n ? (key >> 32) : ~0ull;
+          if (it > 0 && rel > cur_rel && pending) {
+            // the inline DoForwardUp leaves of this node's events at cur_rel (positions [ts0_it, it))
+            for (uint32_t jt = ts0_it; jt < it; jt++) {
+              const uint32_t xr = gs[jt];
+              const uint32_t ncr = M.nchild[xr];
+              for (uint32_t jj = 0; jj < ncr; jj++) {
+                const uint32_t sl = xr * M.maxc + jj;
+                if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
+                const uint32_t sa = M.ch_a[sl];
+                if (M.app_flags[sa] & 2u) {
+                  M.appc[sa].rx_packets++;
+                  M.appc[sa].rx_bytes += M.ch_pkt[sl].size - 28;
+                }
+              }
             }
+            pending = 0;
           }
+          if (it == n) break;
+          if (it == 0 || rel > cur_rel) {
+            ts0_it = it;
+            cur_rel = rel;
+          }
+          const uint32_t s = b_s[q];
+          const HubEv h = b_h[q];
+          E.now = tmin + rel;
+          E.slot0 = s * M.maxc;
+          E.n = h.n;
+          E.uid = (uint32_t)key;
+          E.trseq = h.seq;
+          E.demote = rel == slo || rel == shi;
+          hs.cancelled += h.cancelled;
+          device_act_cached(M, E, Act{h.op, h.dev, h.p}, D);
+          if (h.pkind) E.child(h.pdelay, c, h.pkind, h.pa, Pkt{0, 0, 0, 0});
+          const uint32_t ni = rel < inline_lim ? h.pad : 0u;
+          M.nchild[s] = E.n;
+          M.ninl[s] = ni;
+          pending += ni;
         }
-        pending = 0;
       }
-      if (it == n) break;
-      if (it == 0 || rel > cur_rel) {
-        ts0_it = it;
-        cur_rel = rel;
-      }
-      const uint32_t s = gs[it];
-      const HubEv h = M.hx[s];
-      E.now = tmin + rel;
-      E.slot0 = s * M.maxc;
-      E.n = h.n;
-      E.uid = (uint32_t)key;
-      E.trseq = h.seq;
-      E.demote = rel == slo || rel == shi;
-      hs.cancelled += h.cancelled;
-      device_act_cached(M, E, Act{h.op, h.dev, h.p}, D);
-      if (h.pkind) E.child(h.pdelay, c, h.pkind, h.pa, Pkt{0, 0, 0, 0});
-      uint32_t ni = 0;
-      if (rel < inline_lim)
-        for (uint32_t j = 0; j < E.n; j++) ni += (M.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
-      M.nchild[s] = E.n;
-      M.ninl[s] = ni;
-      pending += ni;
+      __syncthreads();
     }
-    D.flush(M);
+    if (lane == 0) D.flush(M);
   }
   publish_min<HB>(R, E.tmn, E.wnd);
-  const uint64_t nr = wave_sum64(hs.no_route), td = wave_sum64(hs.ttl_drops);
+  const uint64_t nr = wave_sum64(hs.no_route), td = wave_sum64(hs.ttl_drops), cn = wave_sum64(hs.cancelled),
+                 ur = wave_sum64(hs.unreach);
+  const bool stop = __ballot(hs.stop) != 0;
   if (lane == 0) {
-    if (hs.stop) C.stop_seen = 1;
-    if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
+    if (stop) C.stop_seen = 1;
+    if (cn) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)cn);
     if (td) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)td);
     if (nr) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)nr);
-    if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
+    if (ur) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)ur);
   }
   __syncthreads();
 }
@@ -905,7 +1123,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       const uint32_t rt = C.rt;
       C.red[rt ^ 1].tmin = C.red[rt ^ 1].wend = C.red[rt ^ 1].stopts = ~0ull;  // consumed
       C.rt = rt ^ 1;
-      C.wkmax = 0;
     }
     C.windows++;
     if (W > C.max_window) C.max_window = W;
@@ -929,6 +1146,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
 // ================================ host-driven steps (rare) ================================
 // ---- LSD radix sort of (key, slot) pairs: 8-bit digits, tiles of RS_TILE, stable ----
 constexpr int RS_T = 256, RS_IPT = 16, RS_TILE = RS_T * RS_IPT;
+
+// OR of the keys (-> the significant bits, i.e. the digit passes the sort needs).
+__global__ __launch_bounds__(256) void k_rs_or(const uint64_t *__restrict__ keys, uint64_t n, unsigned long long *out) {
+  uint64_t v = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) v |= keys[i];
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0 && v) atomicOr(out, (unsigned long long)v);
+}
 
 __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint64_t *__restrict__ keys, uint64_t n, int shift,
                                                   uint32_t *__restrict__ hist, uint32_t ntiles) {
