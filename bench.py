@@ -5,8 +5,11 @@ Workloads (--workload):
       32,512 links / 65,024 devices+DropTail queues), 10 Mb/s, 1 ms, DropTail 100 packets, one OnOff
       UDP flow (500 kb/s, 512 B) per column from the top row to the bottom row, 0.1-2.0 s, static XY
       routes (SURVEY H9), Simulator::Stop at 2.1 s.  Everything after ns-3's setup phase — the
-      setup-time Node/NetDevice/Application::Start events included — runs on the device in one
-      persistent kernel (nsgpu_p2p_run).  One step = one full simulation from the post-setup state.
+      setup-time Node/NetDevice/Application::Start events included — runs on the device as a
+      hipGraph-replayed pipeline of three kernels per conservative window (nsgpu_p2p_run).  One step =
+      one full simulation from the post-setup state.
+  dumbbell: config 5 — src/mpi/examples/simple-distributed.cc with 2 x 499,999 leaves (1,000,000 nodes)
+      on one GPU, whole simulation per step.
   wifi-fanout: config 3's YansWifiChannel::Send receiver loop at 10,000 nodes, batched (receiver
       events/s; a measurement of the fan-out kernel, not the default line).
   churn: config 1, utils/bench-simulator.cc — 10,000 pending, U[0,1) s delays, 5e6 holds,
@@ -93,6 +96,16 @@ class Churn:
             f"({best.run_seconds:.3f} s)")
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 class P2PGrid:
     bytes_per_event = 104  # 208 B per GPU-resident p2p hop, 2 events per hop
     kernel = "nsgpu::p2p_run"
@@ -105,7 +118,8 @@ class P2PGrid:
         self.engine = p2p.Engine(self.scenario, stream=stream)
         self.workload = (f"PointToPointGridHelper {n}x{n} (config 4): {n * n} nodes, {len(self.scenario.dev)} "
                          f"devices, 10Mb/s 1ms DropTail(100), {n} OnOff UDP flows 500kb/s 512B top->bottom "
-                         f"0.1-2.0s, static XY routes, Stop 2.1s; whole run GPU-resident")
+                         f"0.1-2.0s as CBR (OnTime 1e9 s, OffTime 0 s: always on), static XY routes, Stop 2.1s; "
+                         f"whole run GPU-resident")
 
     def step(self):
         self.engine.reset()
@@ -146,6 +160,25 @@ class P2PGrid:
             f"DefaultSimulatorImpl+MapScheduler+p2p/DropTail/IPv4/UDP/OnOff chain, g++ -O2, Simulator::Run only "
             f"({secs:.3f} s); the reference ns-3 itself is slower still (packet objects, headers, callbacks, "
             f"trace sinks: SURVEY §6 probe 82 k ev/s at 16x16 with global routing)")
+
+
+class P2PDumbbell(P2PGrid):
+    """Config 5: src/mpi/examples/simple-distributed.cc at the BASELINE size — 2 routers (5 Mb/s, 5 ms) and
+    2 x 499,999 leaves (1 Mb/s, 2 ms), PacketSinks on the right leaves, OnOff (1 Mb/s, 512 B, MaxBytes
+    512, OnTime 1 / OffTime 0) from left leaf i to right leaf i, 1-5 s, Stop 5 s; compressed next-hop
+    routes.  One step = the whole simulation (8.5 M events) on ONE GPU (single engine): the routers'
+    same-time bursts are sorted runs and hub blocks."""
+
+    def __init__(self, args, stream):
+        import p2p
+        self.p2p = p2p
+        n = args.dumbbell_leaves
+        self.scenario = p2p.dumbbell(n)
+        self.engine = p2p.Engine(self.scenario, stream=stream)
+        self.workload = (f"simple-distributed.cc dumbbell (config 5): {self.scenario.n_nodes} nodes (2 x {n} leaves), "
+                         f"routers 5Mb/s 5ms, leaves 1Mb/s 2ms, DropTail(100), {n} OnOff UDP flows 1Mb/s 512B "
+                         f"MaxBytes 512 (OnTime 1, OffTime 0) left i -> right i, 1-5s, Stop 5s; compressed static "
+                         f"routes; whole run GPU-resident on one GPU")
 
 
 class P2PGridDist:
@@ -278,7 +311,7 @@ class WifiFanout:
             f"rxPowerDbm within 1e-9 relative)")
 
 
-WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid, "wifi-fanout": WifiFanout}
+WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid, "dumbbell": P2PDumbbell, "wifi-fanout": WifiFanout}
 
 
 def main():
@@ -289,6 +322,7 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="p2p-grid")
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--holds", type=int, default=5_000_000)
+    ap.add_argument("--dumbbell-leaves", type=int, default=499_999, help="dumbbell: leaves per side")
     ap.add_argument("--fanout-tx", type=int, default=1024, help="wifi-fanout: transmissions per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--partitioned", action="store_true",
@@ -390,7 +424,7 @@ def main():
         if not args.no_cpu_baseline and world == 1 and not partitioned:
             cv, cdigest, sample = wl.cpu_baseline()
             out["cpu_baseline"] = {"value": cv, "unit": "events/s", "cores": 1, "kind": "port", "sample": sample,
-                                   "digest_match": bool(cdigest == digest)}
+                                   "cpu_model": cpu_model(), "digest_match": bool(cdigest == digest)}
             out["speedup_vs_cpu"] = value / cv
         print(json.dumps(out), flush=True)
 

@@ -137,12 +137,20 @@ int nsgpu_sched_remove_next(nsgpu_sched *s, nsgpu_event *out);
 int nsgpu_sched_remove(nsgpu_sched *s, const nsgpu_event *ev);
 
 /* ---------------- HipSimulatorImpl host runtime (host closures) ----------------
- * DefaultSimulatorImpl's semantics (default-simulator-impl.cc:49-353: uid from 4, ScheduleDestroy
- * consumes a uid, IsExpired rule, cancelled events still dequeued, Stop/Stop (Time)) over the
- * HipBatchScheduler, with C callbacks as the closures.  ns3::HipSimulatorImpl implements the same
- * logic with ns-3's EventImpl* (INTEGRATION.md). */
+ * Replaces DefaultSimulatorImpl's run loop (default-simulator-impl.cc:117-165) for events whose
+ * closures stay on the host, keeping its semantics (:49-353: uid from 4, ScheduleDestroy consumes a
+ * uid, IsExpired rule, cancelled events still dequeued, Stop/Stop (Time)).  Events live in the
+ * HipBatchScheduler and are dispatched in WINDOWS (nsgpu_sim_pop_window, SURVEY 8(b)'s
+ * nsgpu_pop_window): every pending event of the smallest timestamp, or — with a GPU-resident p2p engine
+ * attached (nsgpu_sim_attach_p2p) — the next host event after the engine has dispatched every device
+ * event before it, in one (ts, uid) order.  Two ways to use it:
+ *   - C callbacks: nsgpu_sim_schedule* + nsgpu_sim_run;
+ *   - raw handles (ns3::HipSimulatorImpl, the handle being an EventImpl*): nsgpu_sim_insert, then
+ *     nsgpu_sim_pop_window / nsgpu_sim_begin per event (handles come back with bit 0 set).
+ * INTEGRATION.md shows the ns-3 side. */
 typedef void (*nsgpu_event_fn)(void *user, uint64_t arg);
 typedef struct nsgpu_sim nsgpu_sim;
+typedef struct nsgpu_p2p nsgpu_p2p;
 int nsgpu_sim_create(uint32_t batch, void *stream, nsgpu_sim **out);
 int nsgpu_sim_free(nsgpu_sim *s);
 int nsgpu_sim_schedule(nsgpu_sim *s, int64_t delay, nsgpu_event_fn fn, void *user, uint64_t arg, nsgpu_event_id *id);
@@ -158,6 +166,27 @@ int nsgpu_sim_stop(nsgpu_sim *s);
 int nsgpu_sim_stop_at(nsgpu_sim *s, int64_t delay);
 int nsgpu_sim_destroy(nsgpu_sim *s);
 int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *dispatched, uint32_t *next_uid);
+int nsgpu_sim_current_uid(nsgpu_sim *s, uint32_t *uid);
+/* windows: *n = 0 when nothing is left to dispatch or a Stop was dispatched */
+int nsgpu_sim_pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n);
+/* window event *e is dispatched next: *skip = 0 run it (Now/Context/uid set, dispatch counted), 1 a
+ * closure of this window removed it, 2 a Stop was dispatched before it (it stays pending) */
+int nsgpu_sim_begin(nsgpu_sim *s, const nsgpu_event *e, int *skip);
+/* raw handles: handle must be even (an object pointer); *uid = the uid it got (ScheduleWithContext
+ * order); remove_key: Scheduler::Remove of a pending event; key_expired: IsExpired's time rule */
+int nsgpu_sim_insert(nsgpu_sim *s, uint64_t ts, uint32_t ctx, uint64_t handle, uint32_t *uid);
+int nsgpu_sim_consume_uid(nsgpu_sim *s, uint32_t *uid);
+int nsgpu_sim_remove_key(nsgpu_sim *s, uint64_t ts, uint32_t uid, uint32_t ctx, uint64_t handle);
+int nsgpu_sim_key_expired(nsgpu_sim *s, uint64_t ts, uint32_t uid, int *expired);
+/* dispatch accounting of the host events (the engine accounts for the device ones): count, cancelled
+ * ones, digest (sum of nsgpu_dispatch_digest_term over their global ranks); optional log at global ranks */
+int nsgpu_sim_host_stats(nsgpu_sim *s, uint64_t *host_dispatched, uint64_t *cancelled, uint64_t *digest);
+int nsgpu_sim_set_log(nsgpu_sim *s, uint64_t *ts, uint32_t *uid, uint32_t *ctx, uint64_t cap);
+/* mixed host / device runs: the engine's events join this runtime's order (attach before scheduling;
+ * the runtime continues from the engine's post-setup uid); a closure may make one of the engine's
+ * OnOff applications send a datagram now (UdpSocket::Send from a host application) */
+int nsgpu_sim_attach_p2p(nsgpu_sim *s, nsgpu_p2p *h);
+int nsgpu_sim_p2p_send(nsgpu_sim *s, uint32_t app);
 
 /* ---------------- GPU-resident point-to-point subset (configs 2, 4) ----------------
  * Replaces, for a topology of PointToPointNetDevices, the handler chain
@@ -169,7 +198,6 @@ int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *di
  * and the DefaultSimulatorImpl run loop over them, entirely on the device.  nsgpu_p2p_reset
  * loads the post-setup state; nsgpu_p2p_run runs Simulator::Run to the Stop event and returns when it
  * is done (graph replays of the window pipeline on an engine stream, ordered after `stream`). */
-typedef struct nsgpu_p2p nsgpu_p2p;
 int nsgpu_p2p_create(const nsgpu_p2p_scenario *sc, uint64_t pool_cap, uint64_t log_cap, nsgpu_p2p **out);
 int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream);
 int nsgpu_p2p_run(nsgpu_p2p *h, void *stream);
@@ -199,6 +227,19 @@ const char *nsgpu_p2p_kernel_name(int k);
  * processor records at the kernel's own start and end (hipExtLaunchKernel); kernel_ms[k] and
  * launches[k] (nsgpu_p2p_kernel_count entries) accumulate the bracketed time and launch count. */
 int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_every, double *kernel_ms, uint64_t *launches);
+/* Mixed host / device runs (driven by nsgpu_sim, see above): the uid the program's own Schedule calls
+ * start from (after the setup-time ones); advance = dispatch every device event with a key below
+ * (hts, huid) (hts = UINT64_MAX: all of them), with *uid / *dispatched the global uid counter and
+ * dispatch count in and out; *ended = 1 when the run is over (Simulator::Stop reached, or nothing
+ * pending on the device and no host key).  inject_send: while paused, application `app` (an OnOff
+ * flow) sends one datagram at `now` on behalf of the host closure with uid cur_uid and context cur_ctx
+ * (its Schedule calls inherit the context; its trace calls continue from *trace_seq).  counters: the device / application counters at this point. */
+int nsgpu_p2p_setup_uid(nsgpu_p2p *h, uint32_t *uid);
+int nsgpu_p2p_advance(nsgpu_p2p *h, uint64_t hts, uint32_t huid, uint32_t *uid, uint64_t *dispatched, int *ended,
+                      void *stream);
+int nsgpu_p2p_inject_send(nsgpu_p2p *h, uint32_t app, uint64_t now, uint32_t cur_uid, uint32_t cur_ctx,
+                          uint32_t *uid, uint32_t *trace_seq, void *stream);
+int nsgpu_p2p_counters(nsgpu_p2p *h, nsgpu_dev_counters *devc, nsgpu_app_counters *appc, void *stream);
 /* Diagnostic: in-kernel phase timers (s_memrealtime ticks, 100 MHz) of the pipeline kernels; only the
  * lib/libnsgpu_prof.so build (-DNSGPU_PHASE_PROF) records them, the product library returns ESTATE. */
 int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset);

@@ -90,7 +90,10 @@ struct Ctl {
   uint64_t wkmax;               // largest window key of the forming window (radix sort width)
   uint64_t npush, nF;           // this window: pool slots freed, children parked in the fresh buffer
   uint32_t mode, rt, nhub, wbase;  // engine mode, red[] accumulating index, hub nodes, chunk base
-  uint32_t force_run, pad3;        // a hub too large to sort in a block: dispatch the window as a run
+  uint32_t force_run, hcap;        // a hub too large to sort in a block: dispatch the window as a run;
+                                   // the window is cut at the next host event (pause after it)
+  uint64_t hts, hrel;              // next host event (nsgpu_p2p_advance): ts (~0: none); the rel ts of the
+  uint32_t huid, pad4;             //   window's last timestamp (W_end or the host event's); the host uid
 };
 
 // Device-resident model + engine state (all pointers are HBM).  Passed to the kernels by value.
@@ -2105,6 +2108,8 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   C0.max_windows = h->max_windows;
   C0.done = red0.tmin == ~0ull ? 2 : 0;  // (no event anywhere)
   C0.P_end = C0.live = M.n_init;  // single engine: the in-place pool starts as the setup events
+  C0.hts = ~0ull;                 // no host closure pending (nsgpu_p2p_advance sets one)
+  C0.hrel = ~0ull;
   C0.rt = 0;                      // window 0 is bounded by red[1] and folds into red[0]
   if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
     h->s = nullptr;
@@ -2320,6 +2325,120 @@ static int build_graph(nsgpu_p2p *h) {
   return NSGPU_OK;
 }
 
+// Replays the single engine's window pipeline until the run is over (done >= 2) or the pipeline paused
+// for a host closure (*paused).  Two replays in flight: replay i+1 is queued before the run control
+// after replay i is examined; a pipeline that paused itself (host-driven sort or compaction, a host
+// closure) makes the replay queued behind it a no-op, and the step runs once that replay has drained.
+static int drive(nsgpu_p2p *h, bool *paused) {
+  *paused = false;
+  int cur = 0;
+  bool have_prev = false;
+  for (;;) {
+    if (h->eager) {
+      launch_windows(h, h->s);
+      NSGPU_HIP(hipGetLastError());
+    } else {
+      NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
+    }
+    NSGPU_HIP(hipMemcpyAsync(&h->snap[cur], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+    NSGPU_HIP(hipEventRecord(h->ev[cur], h->s));
+    if (have_prev) {
+      NSGPU_HIP(hipEventSynchronize(h->ev[cur ^ 1]));
+      const Ctl &c = h->snap[cur ^ 1];
+      if (c.done >= 2) break;  // 2: the final window is appended
+      if (c.mode >= MODE_SORT) {
+        NSGPU_HIP(hipEventSynchronize(h->ev[cur]));
+        if (h->snap[cur].mode == MODE_HOST) {
+          *paused = true;
+          break;
+        }
+        const int rc = host_step(h, h->snap[cur]);
+        if (rc) return rc;
+        have_prev = false;
+        continue;
+      }
+    }
+    have_prev = true;
+    cur ^= 1;
+  }
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  return NSGPU_OK;
+}
+
+// ---- mixed host / device runs: the host-closure runtime (nsgpu_sim) drives the engine ----
+extern "C" int nsgpu_p2p_setup_uid(nsgpu_p2p *h, uint32_t *uid) {
+  if (!h || !uid) return set_error(NSGPU_EINVAL, "nsgpu_p2p_setup_uid: null");
+  *uid = h->C0.uid;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_advance(nsgpu_p2p *h, uint64_t hts, uint32_t huid, uint32_t *uid, uint64_t *dispatched,
+                                 int *ended, void *stream) {
+  if (!h || !uid || !dispatched || !ended) return set_error(NSGPU_EINVAL, "nsgpu_p2p_advance: null");
+  if (h->M.dist) return set_error(NSGPU_ESTATE, "nsgpu_p2p_advance: single-device engines only");
+  *ended = 0;
+  if (!h->eager && !h->gexec) {
+    const int rc = build_graph(h);
+    if (rc) return rc;
+  }
+  hipStream_t cs = (hipStream_t)stream;
+  NSGPU_HIP(hipEventRecord(h->ev[0], cs));
+  NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev[0], 0));
+  NSGPU_HIP(hipMemcpyAsync(&h->snap[0], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  if (h->snap[0].done >= 2) {
+    *ended = 1;
+    return NSGPU_OK;
+  }
+  hipLaunchKernelGGL(k_host_resume, dim3(1), dim3(1), 0, h->s, h->M, hts, huid, *uid, *dispatched);
+  NSGPU_HIP(hipGetLastError());
+  bool paused = false;
+  const int rc = drive(h, &paused);
+  if (rc) return rc;
+  NSGPU_HIP(hipMemcpyAsync(&h->snap[0], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  *uid = h->snap[0].uid;
+  *dispatched = h->snap[0].K;
+  *ended = paused ? 0 : 1;
+  NSGPU_HIP(hipEventRecord(h->ev[0], h->s));
+  NSGPU_HIP(hipStreamWaitEvent(cs, h->ev[0], 0));
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_inject_send(nsgpu_p2p *h, uint32_t app, uint64_t now, uint32_t cur_uid, uint32_t cur_ctx,
+                                     uint32_t *uid, uint32_t *trace_seq, void *stream) {
+  if (!h || !uid || !trace_seq) return set_error(NSGPU_EINVAL, "nsgpu_p2p_inject_send: null");
+  if (h->M.dist) return set_error(NSGPU_ESTATE, "nsgpu_p2p_inject_send: single-device engines only");
+  if (app >= h->M.n_apps || h->sc.app_kind[app] != NSGPU_APP_ONOFF)
+    return set_error(NSGPU_EINVAL, "nsgpu_p2p_inject_send: app %u is not an OnOff flow", app);
+  hipStream_t s = h->s;
+  hipStream_t cs = (hipStream_t)stream;
+  NSGPU_HIP(hipEventRecord(h->ev[0], cs));
+  NSGPU_HIP(hipStreamWaitEvent(s, h->ev[0], 0));
+  NSGPU_HIP(hipMemcpyAsync(&h->snap[0], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+  NSGPU_HIP(hipStreamSynchronize(s));
+  if (h->snap[0].mode != MODE_HOST) return set_error(NSGPU_ESTATE, "nsgpu_p2p_inject_send: the engine is not paused for a host closure");
+  hipLaunchKernelGGL(k_set_uid, dim3(1), dim3(1), 0, s, h->M, *uid);  // (the host closures' Schedule calls)
+  hipLaunchKernelGGL(k_inject, dim3(1), dim3(1), 0, s, h->M, app, now, cur_uid, cur_ctx, *trace_seq, h->M.s_val);
+  NSGPU_HIP(hipGetLastError());
+  uint32_t outv[2];
+  NSGPU_HIP(hipMemcpyAsync(outv, h->M.s_val, sizeof(outv), hipMemcpyDeviceToHost, s));
+  NSGPU_HIP(hipStreamSynchronize(s));
+  *uid = outv[0];
+  *trace_seq = outv[1];
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_p2p_counters(nsgpu_p2p *h, nsgpu_dev_counters *devc, nsgpu_app_counters *appc, void *stream) {
+  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_counters: null");
+  hipStream_t cs = (hipStream_t)stream;
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  if (devc) NSGPU_HIP(hipMemcpyAsync(devc, h->M.devc, h->M.n_devices * sizeof(*devc), hipMemcpyDeviceToHost, cs));
+  if (appc) NSGPU_HIP(hipMemcpyAsync(appc, h->M.appc, h->M.n_apps * sizeof(*appc), hipMemcpyDeviceToHost, cs));
+  NSGPU_HIP(hipStreamSynchronize(cs));
+  return NSGPU_OK;
+}
+
 extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_run: null");
   if (h->M.dist && !h->comm)
@@ -2355,35 +2474,10 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
       }
     }
   } else {
-    // two replays in flight: replay i+1 is queued before the run control after replay i is examined;
-    // a pipeline that paused itself for a host-driven step (sort, compaction) makes the replay queued
-    // behind it a no-op, and the step is run once that replay has drained
-    int cur = 0;
-    bool have_prev = false;
-    for (;;) {
-      if (h->eager) {
-        launch_windows(h, h->s);
-        NSGPU_HIP(hipGetLastError());
-      } else {
-        NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
-      }
-      NSGPU_HIP(hipMemcpyAsync(&h->snap[cur], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
-      NSGPU_HIP(hipEventRecord(h->ev[cur], h->s));
-      if (have_prev) {
-        NSGPU_HIP(hipEventSynchronize(h->ev[cur ^ 1]));
-        const Ctl &c = h->snap[cur ^ 1];
-        if (c.done >= 2) break;  // 2: the final window is appended
-        if (c.mode >= MODE_SORT) {
-          NSGPU_HIP(hipEventSynchronize(h->ev[cur]));
-          const int rc = host_step(h, h->snap[cur]);
-          if (rc) return rc;
-          have_prev = false;
-          continue;
-        }
-      }
-      have_prev = true;
-      cur ^= 1;
-    }
+    bool paused = false;
+    const int rc = drive(h, &paused);
+    if (rc) return rc;
+    if (paused) return set_error(NSGPU_ESTATE, "nsgpu_p2p_run: paused for a host closure (use nsgpu_p2p_advance)");
   }
   NSGPU_HIP(hipEventRecord(h->t1, h->s));
   NSGPU_HIP(hipEventSynchronize(h->t1));

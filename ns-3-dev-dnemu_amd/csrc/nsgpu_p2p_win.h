@@ -23,7 +23,7 @@
 // run inline, which keeps its (ts, uid) position.  When the pool holds many tombstones the host
 // compacts it (k_cmp).
 
-enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3 };
+enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3, MODE_HOST = 4 };
 constexpr uint64_t TOMB = ~0ull;        // ev_ts of a free pool slot
 constexpr uint32_t NOSRC = 0xffffffffu;
 constexpr int NHUB = 32;                // hub blocks of k2_handle
@@ -39,6 +39,7 @@ struct HubEv {
   uint32_t pkind, pa;  // pkind == 0: none
   uint32_t n, seq;     // children and trace sink calls the node part made
   uint32_t cancelled, pad;  // pad: the node part's inline DoForwardUp children
+  uint32_t ctx, pad2;       // the event's context (its Schedule calls inherit it)
 };
 
 constexpr int HUBL = 1024;  // events of a hub a block sorts in LDS (more: the window is dispatched as a run)
@@ -68,6 +69,26 @@ __device__ __forceinline__ uint64_t wave_alloc64(uint64_t *ctr, bool want) {
 }
 
 constexpr uint32_t NOHOLD = 0xffffffffu;  // widx of a window event no holder runs (NetDevice::Start)
+
+// The node whose state an event touches (its logical process).  Events scheduled by the handlers carry
+// it as their context; a host closure runs in context 0xffffffff and Simulator::Schedule inherits the
+// current context, so e.g. the TransmitComplete of a datagram a host closure sent has none
+// (point-to-point-net-device.cc:226, default-simulator-impl.cc:188-204).
+__device__ __forceinline__ uint32_t lp_of(const P2PDev &M, uint32_t ctx, uint32_t kind_word, uint32_t a) {
+  if (ctx != NOCTX) return ctx;
+  switch (kind_word & 0xffu) {
+    case K_TX_COMPLETE:
+    case K_RECEIVE:
+      return M.dev_node[a];
+    case K_NODE_START:
+      return a;
+    case K_STOP:
+    case K_DEV_START:
+      return NOCTX;
+    default:
+      return M.app_node[a];
+  }
+}
 
 // Window record `slot` of node `ctx` -> the node's slot table (local slot index); the node that
 // reaches CH + 1 events becomes a hub.  NetDevice::Start is a no-op (the device was started by
@@ -119,7 +140,7 @@ __device__ __forceinline__ void k2_place(const P2PDev &M, Ctl &C, const WinBound
       M.wa[slot] = e.a;
       M.wpkt[slot] = e.p;
       M.wsrc[slot] = src;
-      if (slot < (uint32_t)WCAP) node_table_add(M, C, slot, e.ctx, e.kind);
+      if (slot < (uint32_t)WCAP) node_table_add(M, C, slot, lp_of(M, e.ctx, e.kind, e.a), e.kind);
     } else {
       atomicOr(M.error, 1u);
     }
@@ -158,10 +179,35 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const bool partition = C.done == 0;
   const uint32_t rt = C.rt;
   Red &R = C.red[rt];
-  const WinBound b = window_bound(C.red[rt ^ 1]);
+  WinBound b = window_bound(C.red[rt ^ 1]);
+  // a pending host closure (nsgpu_p2p_advance) cuts the window at its key, like Simulator::Stop: the
+  // window holds the device events before it, and the pipeline pauses for the host after the window
+  const uint64_t hts = C.hts;
+  bool hcap = false;
+  uint64_t hrel = ~0ull;
+  if (hts != ~0ull && !run) {
+    if (hts < b.tmin || b.tmin == ~0ull) {
+      b.bound = 0;  // (every device key is >= 4: uids start at 4)
+      hcap = true;
+    } else if (hts - b.tmin <= b.span) {
+      const uint64_t hk = ((hts - b.tmin) << 32) | C.huid;
+      if (hk <= b.bound) {
+        b.bound = hk;
+        hcap = true;
+        hrel = hts - b.tmin;
+      }
+    }
+  }
   if (!run && partition && g == 0) {
     publish_bound(C, b);
-    C.split_lo = C.split_hi = ~0ull;
+    // the window's last timestamp (W_end, or the host event's): other children of this window can land
+    // there with smaller uids than a DoForwardUp leaf its events schedule, so those leaves are queued
+    // (K_FWD_UP_D), not run inline; a leaf of an earlier timestamp has every same-time event in the window
+    const uint64_t edge = hcap ? hrel : b.span;
+    C.split_lo = ~0ull;
+    C.split_hi = edge;
+    C.hrel = edge;
+    C.hcap = hcap;
   }
   const uint32_t pW = C.pvalid ? C.pW : 0;
   uint64_t spk = 0;
@@ -255,9 +301,12 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       const uint64_t r1 = r0 + Wc;
       const uint64_t klo = M.wkey[r0] >> 32, khi = M.wkey[r1 - 1] >> 32;
       C.split_lo = (r0 > 0 && (M.wkey[r0 - 1] >> 32) == klo) ? klo : ~0ull;
-      C.split_hi = (r1 < rW && (M.wkey[r1] >> 32) == khi) ? khi : ~0ull;
+      C.split_hi = (r1 < rW && (M.wkey[r1] >> 32) == khi) ? khi : C.hrel;
     }
-    if (s < Wc) node_table_add(M, C, (uint32_t)s, M.wctx[r0 + s], M.wkind[r0 + s]);
+    if (s < Wc) {
+      const uint32_t kw = M.wkind[r0 + s];
+      node_table_add(M, C, (uint32_t)s, lp_of(M, M.wctx[r0 + s], kw, M.wa[r0 + s]), kw);
+    }
   }
   PH_MARK(1);
   publish_min<TB>(R, tmn, wnd);
@@ -283,7 +332,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
     M.ninl[i0] = 0;
   }
   if (wi == 0) {  // the holder
-    const uint32_t c = M.wctx[base + i0];
+    const uint32_t c = lp_of(M, M.wctx[base + i0], M.wkind[base + i0], M.wa[base + i0]);
     uint32_t n = 1;
     int32_t sink = -1;
     if (c < M.n_nodes) {
@@ -303,7 +352,9 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
         if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
           uint32_t m = NSLOT;
           for (uint32_t x = 0; x < W && m < n; x++)
-            if (M.wctx[base + x] == c && M.widx[x] >= (uint32_t)NSLOT && M.widx[x] != NOHOLD) my[m++] = x;
+            if (M.widx[x] >= (uint32_t)NSLOT && M.widx[x] != NOHOLD &&
+                lp_of(M, M.wctx[base + x], M.wkind[base + x], M.wa[base + x]) == c)
+              my[m++] = x;
         }
         for (uint32_t j = 0; j < n; j++) mk[j] = M.wkey[base + my[j]];
         for (uint32_t a = 1; a < n; a++) {  // insertion sort by key
@@ -357,6 +408,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
           cur_rel = rel;
         }
         const uint32_t s = my[it];
+        E.ctx = M.wctx[base + s];  // (Schedule calls inherit the event's context)
         E.now = tmin + rel;
         E.slot0 = s * M.maxc;
         E.n = 0;
@@ -601,6 +653,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
       const uint32_t s = gs[j];
       const uint64_t key = gk[j];
       const HubEv h = M.hx[s];
+      E.ctx = h.ctx;
       E.now = tmin + (key >> 32);
       E.slot0 = s * M.maxc;
       E.n = h.n;
@@ -643,10 +696,10 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
       if (go) {
         q5++;
         const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)bps);
-        E.child(txTime + ifg, c, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
+        E.child(txTime + ifg, h.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
         E.child(txTime + delay, peer_node, K_RECEIVE, peer, tx);
       }
-      if (h.pkind) E.child(h.pdelay, c, h.pkind, h.pa, Pkt{0, 0, 0, 0});
+      if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
       M.nchild[s] = E.n;
       M.ninl[s] = 0;
     }
@@ -682,7 +735,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   uint32_t n = 0;
   for (uint32_t x0 = 0; x0 < W; x0 += HB) {
     const uint32_t x = x0 + lane;
-    const bool m = x < W && M.wctx[base + x] == c && M.widx[x] != NOHOLD;
+    const bool m = x < W && M.widx[x] != NOHOLD && lp_of(M, M.wctx[base + x], M.wkind[base + x], M.wa[base + x]) == c;
     const uint64_t bm = __ballot(m);
     if (m) {
       const uint32_t p = n + (uint32_t)__popcll(bm & below);
@@ -725,8 +778,9 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   // LDS (one memory round trip per batch), then the serial work reads LDS
   uint64_t *b_key = reinterpret_cast<uint64_t *>(lds);  // [HB]
   uint32_t *b_s = lds + 2 * HB, *b_kind = lds + 3 * HB, *b_a = lds + 4 * HB, *b_sl = lds + 5 * HB;
-  Pkt *b_pkt = reinterpret_cast<Pkt *>(lds + 6 * HB);    // [HB]
-  HubEv *b_h = reinterpret_cast<HubEv *>(lds + 10 * HB);  // [HB]
+  uint32_t *b_ctx = lds + 6 * HB;
+  Pkt *b_pkt = reinterpret_cast<Pkt *>(lds + 7 * HB);     // [HB]
+  HubEv *b_h = reinterpret_cast<HubEv *>(lds + 11 * HB);  // [HB]
   // 2. node parts: the stateless ones (TransmitComplete, NetDevice::Start, Receive -> IpForward: rx
   //    counter, MacRx trace, route, TTL) by their own lane, the others serially by lane 0 in key order
   for (uint32_t j0 = 0; j0 < n; j0 += HB) {
@@ -734,10 +788,11 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     if (j < n) {
       const uint32_t s = gs[j];
       const uint64_t key = gk[j];
-      const uint32_t kw = M.wkind[base + s], a = M.wa[base + s];
+      const uint32_t kw = M.wkind[base + s], a = M.wa[base + s], ctx = M.wctx[base + s];
       Pkt p = M.wpkt[base + s];
       const uint32_t kind = kw & 0xffu;
       const bool sl = stateless_event(M, c, kind, p);
+      b_ctx[lane] = ctx;
       b_s[lane] = s;
       b_key[lane] = key;
       b_kind[lane] = kw;
@@ -748,7 +803,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
         E.now = tmin + (key >> 32);
         E.uid = (uint32_t)key;
         E.trseq = 0;
-        HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0};
+        HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, ctx, 0};
         if (kind == K_TX_COMPLETE) {
           h.op = ACT_KICK;
           h.dev = a;
@@ -781,6 +836,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
         if (b_sl[q]) continue;
         const uint32_t s = b_s[q];
         const uint64_t rel = b_key[q] >> 32;
+        E.ctx = b_ctx[q];
         E.now = tmin + rel;
         E.slot0 = s * M.maxc;
         E.n = 0;
@@ -791,7 +847,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
         uint32_t ni = 0;
         for (uint32_t jj = 0; jj < E.n; jj++) ni += (M.ch_kind[E.slot0 + jj] & 0xffu) == K_FWD_UP;
         M.hx[s] = HubEv{o.act.op, o.act.dev, o.act.p, o.post.delay, o.post.valid ? o.post.kind : 0u, o.post.a, E.n,
-                        E.trseq, o.cancelled ? 1u : 0u, ni};
+                        E.trseq, o.cancelled ? 1u : 0u, ni, b_ctx[q], 0};
       }
     }
     __syncthreads();
@@ -863,6 +919,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           }
           const uint32_t s = b_s[q];
           const HubEv h = b_h[q];
+          E.ctx = h.ctx;
           E.now = tmin + rel;
           E.slot0 = s * M.maxc;
           E.n = h.n;
@@ -871,7 +928,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           E.demote = rel == slo || rel == shi;
           hs.cancelled += h.cancelled;
           device_act_cached(M, E, Act{h.op, h.dev, h.p}, D);
-          if (h.pkind) E.child(h.pdelay, c, h.pkind, h.pa, Pkt{0, 0, 0, 0});
+          if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
           const uint32_t ni = rel < inline_lim ? h.pad : 0u;
           M.nchild[s] = E.n;
           M.ninl[s] = ni;
@@ -1128,7 +1185,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     if (W > C.max_window) C.max_window = W;
     C.W = 0;
     const uint64_t pending = C.live + (tc - tinl) + (C.mode == MODE_RUN ? C.rW - C.r0 : 0);
-    bool done = C.stop_seen || pending == 0;
+    bool done = C.stop_seen || (pending == 0 && C.hts == ~0ull);
     if (C.P_end > M.pool_cap) {
       atomicOr(M.error, 1u);
       done = true;
@@ -1137,8 +1194,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       atomicOr(M.error, 4u);
       done = true;
     }
-    if (done) C.done = 1;
-    else if (C.mode == MODE_NORMAL && C.P_end > 65536 && C.live * 4 < C.P_end) C.mode = MODE_COMPACT;
+    if (done) {
+      C.done = 1;
+    } else if (C.mode == MODE_NORMAL && C.hcap) {  // the window was cut at the next host closure: pause
+      C.hcap = 0;
+      C.mode = MODE_HOST;
+    } else if (C.mode == MODE_NORMAL && C.P_end > 65536 && C.live * 4 < C.P_end) {
+      C.mode = MODE_COMPACT;
+    }
   }
   PH_MARK(20);
 }
@@ -1279,4 +1342,79 @@ __global__ void k_after_compact(const P2PDev M, uint64_t live) {
   M.C->live = live;
   M.C->nfree = 0;
   M.C->mode = MODE_NORMAL;
+}
+
+// ---- mixed host / device runs (nsgpu_p2p_advance, nsgpu_p2p_inject_send) ----
+// Resume after a pause for the host: the next host key, and the uid / dispatch counters the host
+// closures advanced (every host dispatch and Schedule call counts, as in DefaultSimulatorImpl).
+__global__ void k_host_resume(const P2PDev M, uint64_t hts, uint32_t huid, uint32_t uid, uint64_t K) {
+  Ctl &C = *M.C;
+  C.hts = hts;
+  C.huid = huid;
+  C.uid = uid;
+  C.K = K;
+  if (C.mode == MODE_HOST) C.mode = MODE_NORMAL;
+}
+
+__global__ void k_set_uid(const P2PDev M, uint32_t uid) { M.C->uid = uid; }
+
+// A host application's UdpSocket::Send of one datagram of application `a`'s flow, made by the host
+// closure running now (uid `cur`): the same steps as OnOffApplication::SendPacket's send
+// (onoff-application.cc:226-236 -> udp-socket-impl.cc DoSendTo -> Ipv4L3Protocol::Send -> the device),
+// its Schedule calls taking uids from uid0.  The children become pending in place and fold into the
+// reduction that bounds the next window.
+__global__ void k_inject(const P2PDev M, uint32_t a, uint64_t now, uint32_t cur, uint32_t ctx, uint32_t seq,
+                         uint32_t *out) {
+  Ctl &C = *M.C;
+  Emit E;
+  E.now = now;
+  E.ctx = ctx;  // the host closure's context: its Schedule calls inherit it
+  E.slot0 = 0;
+  E.n = 0;
+  E.ch_ts = M.f_ts;  // (the fresh buffer is empty while the pipeline is paused)
+  E.ch_ctx = M.f_ctx;
+  E.ch_kind = M.f_kind;
+  E.ch_a = M.f_a;
+  E.ch_pkt = M.f_pkt;
+  E.lookahead = M.lookahead;
+  E.tmn = ~0ull;
+  E.wnd = ~0ull;
+  E.uid = cur;
+  E.trseq = seq;
+  E.demote = false;
+  const uint32_t sz = M.app_pkt_size[a];
+  Pkt p{a, 0, sz + 8 + 20, M.app_ttl[a]};
+  M.appc[a].tx_packets++;
+  M.appc[a].tx_bytes += sz;
+  const uint32_t an = M.app_node[a];
+  const uint32_t o = route_of(M, an, p);
+  if (o == 0xffffffffu) {
+    C.no_route++;
+  } else {
+    p.ipid = M.node_ipid[an]++;
+    device_act(M, E, Act{ACT_SEND, o, p});
+  }
+  const uint32_t uid0 = C.uid;
+  for (uint32_t j = 0; j < E.n; j++) {
+    uint64_t dst;
+    if (C.nfree) dst = M.fstack[--C.nfree];
+    else dst = C.P_end++;
+    if (dst >= M.pool_cap) {
+      atomicOr(M.error, 1u);
+      break;
+    }
+    M.ev_ts[0][dst] = M.f_ts[j];
+    M.ev_uid[0][dst] = uid0 + j;
+    M.ev_ctx[0][dst] = M.f_ctx[j];
+    M.ev_kind[0][dst] = M.f_kind[j];
+    M.ev_a[0][dst] = M.f_a[j];
+    M.ev_pkt[0][dst] = M.f_pkt[j];
+    C.live++;
+  }
+  Red &R = C.red[C.rt ^ 1];  // bounds the next window (k2_scan flipped rt)
+  if (E.tmn < R.tmin) R.tmin = E.tmn;
+  if (E.wnd < R.wend) R.wend = E.wnd;
+  C.uid = uid0 + E.n;
+  out[0] = C.uid;
+  out[1] = E.trseq;
 }

@@ -92,6 +92,21 @@ SIGNATURES = {
     "nsgpu_sim_stop_at": (C.c_int, [_vp, _i64]),
     "nsgpu_sim_destroy": (C.c_int, [_vp]),
     "nsgpu_sim_state": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "nsgpu_sim_current_uid": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_pop_window": (C.c_int, [_vp, _vp, _u32, _vp]),
+    "nsgpu_sim_begin": (C.c_int, [_vp, _vp, _vp]),
+    "nsgpu_sim_insert": (C.c_int, [_vp, _u64, _u32, _u64, _vp]),
+    "nsgpu_sim_consume_uid": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_remove_key": (C.c_int, [_vp, _u64, _u32, _u32, _u64]),
+    "nsgpu_sim_key_expired": (C.c_int, [_vp, _u64, _u32, _vp]),
+    "nsgpu_sim_host_stats": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "nsgpu_sim_set_log": (C.c_int, [_vp, _vp, _vp, _vp, _u64]),
+    "nsgpu_sim_attach_p2p": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_p2p_send": (C.c_int, [_vp, _u32]),
+    "nsgpu_p2p_setup_uid": (C.c_int, [_vp, _vp]),
+    "nsgpu_p2p_advance": (C.c_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp]),
+    "nsgpu_p2p_inject_send": (C.c_int, [_vp, _u32, _u64, _u32, _u32, _vp, _vp, _vp]),
+    "nsgpu_p2p_counters": (C.c_int, [_vp, _vp, _vp, _vp]),
     "nsgpu_p2p_create": (C.c_int, [_vp, _u64, _u64, C.POINTER(C.c_void_p)]),
     "nsgpu_p2p_reset": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_run": (C.c_int, [_vp, _vp]),
@@ -463,6 +478,45 @@ class Sim:
 
     def next_uid(self):
         return self._state()[3]
+
+    # ---- windows (the pull interface ns3::HipSimulatorImpl uses) ----
+    def insert_raw(self, ts, ctx, handle):
+        u = C.c_uint32()
+        check(lib().nsgpu_sim_insert(self.h, ts, ctx, handle, C.byref(u)))
+        return u.value
+
+    def pop_window(self, cap=1024):
+        out = np.zeros(cap, EVENT_DTYPE)
+        n = C.c_uint32()
+        check(lib().nsgpu_sim_pop_window(self.h, out.ctypes.data, cap, C.byref(n)))
+        return out[:n.value]
+
+    def begin(self, ev):
+        e = np.array([tuple(ev)], dtype=EVENT_DTYPE)
+        skip = C.c_int()
+        check(lib().nsgpu_sim_begin(self.h, e.ctypes.data, C.byref(skip)))
+        return skip.value
+
+    def remove_key(self, ts, uid, ctx=0, handle=0):
+        check(lib().nsgpu_sim_remove_key(self.h, ts, uid, ctx, handle))
+
+    # ---- mixed host / device runs ----
+    def attach_p2p(self, engine):
+        check(lib().nsgpu_sim_attach_p2p(self.h, engine.h))
+        self._engine = engine
+
+    def p2p_send(self, app):
+        check(lib().nsgpu_sim_p2p_send(self.h, app))
+
+    def set_log(self, cap):
+        self.log = (np.zeros(cap, np.uint64), np.zeros(cap, np.uint32), np.zeros(cap, np.uint32))
+        check(lib().nsgpu_sim_set_log(self.h, self.log[0].ctypes.data, self.log[1].ctypes.data,
+                                      self.log[2].ctypes.data, cap))
+
+    def host_stats(self):
+        n, c, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib().nsgpu_sim_host_stats(self.h, C.byref(n), C.byref(c), C.byref(d)))
+        return n.value, c.value, d.value
 
     def close(self):
         if self.h:

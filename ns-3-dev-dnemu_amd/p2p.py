@@ -505,6 +505,13 @@ class Engine:
             out[name] = (float(ms[k] / cnt[k]) if cnt[k] else 0.0, int(cnt[k]))
         return out
 
+    def counters(self):
+        """Device / application counters now (nsgpu_p2p_counters: e.g. from a host closure)."""
+        devc = np.zeros(self.s.n_devices, DEV_COUNTERS_DTYPE)
+        appc = np.zeros(self.s.n_apps, APP_COUNTERS_DTYPE)
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_counters(self.h, devc.ctypes.data, appc.ctypes.data, self.stream))
+        return devc, appc
+
     def results(self, log_n=0):
         st = P2PStats()
         devc = np.zeros(self.s.n_devices, DEV_COUNTERS_DTYPE)

@@ -125,6 +125,14 @@ int nsref_p2p_run_trace(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, ns
                         uint64_t log_cap, double *run_seconds, nsgpu_trace_record *trace, uint64_t trace_cap,
                         uint64_t *trace_n);
 
+/* The same run with a host application interleaved (see nsref_p2p.cc): samples receives `count`
+ * snapshots of application app_obs's counters. */
+int nsref_p2p_run_probe(const nsgpu_p2p_scenario *sc, int64_t t0, int64_t period, uint32_t count, uint32_t app_send,
+                        uint32_t app_obs, nsgpu_app_counters *samples, nsgpu_p2p_stats *stats,
+                        nsgpu_dev_counters *devc, nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid,
+                        uint32_t *log_ctx, uint64_t log_cap, nsgpu_trace_record *trace, uint64_t trace_cap,
+                        uint64_t *trace_n);
+
 /* bench-simulator ReadDistribution: (uint64_t)(data * 1000000000)  (bench-simulator.cc:66) */
 uint64_t nsref_distribution_ns(double seconds);
 

@@ -134,6 +134,8 @@ def lib():
         L.nsref_p2p_run.restype = C.c_int
         L.nsref_p2p_run_trace.argtypes = [C.c_void_p] * 7 + [C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
                                                               C.c_void_p]
+        L.nsref_p2p_run_probe.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_uint32, C.c_uint32, C.c_uint32] + \
+            [C.c_void_p] * 7 + [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
         L.nsref_p2p_run_trace.restype = C.c_int
         L.nsref_distribution_ns.argtypes = [C.c_double]
         L.nsref_distribution_ns.restype = C.c_uint64
@@ -379,3 +381,24 @@ def p2p_run_trace(scenario_struct, stats_struct, devc, appc, log_cap=0):
     tr = np.zeros(n.value, TRACE_RECORD_DTYPE)
     lib().nsref_p2p_run_trace(*args, tr.ctypes.data, n.value, C.byref(n))
     return secs.value, (lts, luid, lctx), tr
+
+
+APP_COUNTERS_DTYPE = np.dtype([("tx_packets", "<u4"), ("rx_packets", "<u4"), ("tx_bytes", "<u8"),
+                               ("rx_bytes", "<u8")])  # nsgpu_app_counters
+
+
+def p2p_run_probe(scenario_struct, stats_struct, devc, appc, t0, period, count, app_send, app_obs, log_cap=0):
+    """p2p run with the host probe application of nsref_p2p_run_probe; returns (log, trace, samples)."""
+    from numpy import zeros
+    lts = zeros(log_cap, np.uint64)
+    luid = zeros(log_cap, np.uint32)
+    lctx = zeros(log_cap, np.uint32)
+    samples = zeros(count, APP_COUNTERS_DTYPE)
+    n = C.c_uint64()
+    args = [C.byref(scenario_struct), t0, period, count, app_send, app_obs, samples.ctypes.data, C.byref(stats_struct),
+            devc.ctypes.data, appc.ctypes.data, lts.ctypes.data if log_cap else None,
+            luid.ctypes.data if log_cap else None, lctx.ctypes.data if log_cap else None, log_cap]
+    lib().nsref_p2p_run_probe(*args, None, 0, C.byref(n))
+    tr = np.zeros(n.value, TRACE_RECORD_DTYPE)
+    lib().nsref_p2p_run_probe(*args, tr.ctypes.data, n.value, C.byref(n))
+    return (lts, luid, lctx), tr, samples

@@ -414,6 +414,58 @@ extern "C" int nsref_p2p_run_trace(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats
   return 0;
 }
 
+// A host application interleaved with the handler chain (the mixed-mode contract of nsgpu_sim +
+// nsgpu_p2p): a closure scheduled with Simulator::Schedule (t0) right after setup, which, every `period`
+// for `count` rounds, reads application app_obs's counters (a trace / stats callback) and sends one
+// datagram of application app_send's flow through its socket now (UdpSocket::Send from a host
+// application: onoff-application.cc:226-236's send without the OnOff state), then re-schedules itself.
+extern "C" int nsref_p2p_run_probe(const nsgpu_p2p_scenario *sc, int64_t t0, int64_t period, uint32_t count,
+                                   uint32_t app_send, uint32_t app_obs, nsgpu_app_counters *samples,
+                                   nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc, nsgpu_app_counters *appc,
+                                   uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap,
+                                   nsgpu_trace_record *trace, uint64_t trace_cap, uint64_t *trace_n) {
+  Model *m = new Model();
+  std::vector<nsgpu_trace_record> tv;
+  if (trace_n) m->trace = &tv;
+  m->s = *sc;
+  m->sim.want_digest = true;
+  m->sim.log_ts = log_ts;
+  m->sim.log_uid = log_uid;
+  m->sim.log_ctx = log_ctx;
+  m->sim.log_cap = log_ts ? log_cap : 0;
+  m->setup();
+  uint32_t k = 0;
+  std::function<void()> probe = [&]() {
+    samples[k] = m->app[app_obs].c;
+    App &A = m->app[app_send];
+    A.c.tx_packets++;
+    A.c.tx_bytes += sc->app_pkt_size[app_send];
+    m->ip_send(sc->app_node[app_send], Pkt{app_send, 0, sc->app_pkt_size[app_send] + 8 + 20, sc->app_ttl[app_send]});
+    if (++k < count) m->schedule(period, [&]() { probe(); });
+  };
+  if (count) m->schedule(t0, [&]() { probe(); });
+  m->sim.Run();
+  memset(stats, 0, sizeof(*stats));
+  stats->dispatched = m->sim.m_dispatched;
+  stats->cancelled = m->sim.m_cancelled;
+  stats->digest = m->sim.m_digest;
+  stats->final_ts = m->sim.m_currentTs;
+  stats->next_uid = m->sim.m_uid;
+  stats->ttl_drops = m->ttl_drops;
+  stats->no_route_drops = m->no_route_drops;
+  stats->unreach_drops = m->unreach_drops;
+  if (devc)
+    for (uint32_t d = 0; d < sc->n_devices; d++) devc[d] = m->dev[d].c;
+  if (appc)
+    for (uint32_t a = 0; a < sc->n_apps; a++) appc[a] = m->app[a].c;
+  if (trace_n) {
+    *trace_n = tv.size();
+    for (uint64_t i = 0; i < tv.size() && i < trace_cap; i++) trace[i] = tv[i];
+  }
+  delete m;
+  return 0;
+}
+
 extern "C" int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
                              nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
                              uint64_t log_cap, double *run_seconds) {

@@ -52,3 +52,18 @@ def test_dumbbell_65536_nodes_single_gpu():
         assert getattr(gst, f) == getattr(st, f), (f, getattr(gst, f), getattr(st, f))
     assert np.array_equal(gdevc, devc)
     assert np.array_equal(gappc, appc)
+
+
+def test_dumbbell_65536_nodes_eight_partitions():
+    """The same 65,536-node dumbbell partitioned 8 ways the way simple-distributed.cc assigns system ids
+    (left side + router 1 on rank 0; router 2 and the right leaves over ranks 1-7), all partitions on
+    one GPU through the loopback group: the sequential counters and digest."""
+    n = 32_767
+    sc = p2p.dumbbell(n)
+    st, devc, appc, _log, _tr = oracle_full(sc, 0)
+    grp = p2p.LoopbackGroup(sc, 8, owner=p2p.dumbbell_owner(n, 8))
+    gst, gdevc, gappc, _ = grp.run()
+    for f in ("dispatched", "cancelled", "digest", "final_ts", "next_uid", "ttl_drops", "no_route_drops"):
+        assert getattr(gst, f) == getattr(st, f), (f, getattr(gst, f), getattr(st, f))
+    assert np.array_equal(gdevc, devc)
+    assert np.array_equal(gappc, appc)

@@ -1,0 +1,134 @@
+"""Mixed host / device runs: host closures (C callbacks, here Python ones through ctypes) interleaved
+with the GPU-resident p2p engine's events in ONE (ts, uid) order (include/nsgpu.h: nsgpu_sim_attach_p2p,
+nsgpu_sim_pop_window; the engine pauses its window pipeline at the next host event's key).
+
+The host application (oracle: nsref_p2p_run_probe, oracle/nsref_p2p.cc) is scheduled right after
+setup and, every `period`, reads a PacketSink's counters (a trace / stats callback reading device
+state at its point of the order) and sends one datagram of an OnOff flow through its socket
+(UdpSocket::Send from a host application: device events created by a host closure), then
+re-schedules itself.  The full pop log (device and host dispatches), the trace records, every
+counter, the samples, digest, dispatch count and next uid must equal the oracle's."""
+import numpy as np
+import pytest
+
+import nsgpu
+import nsref
+import p2p
+import trace
+from test_gpu_trace import assert_same_trace
+
+pytestmark = pytest.mark.gpu
+
+
+def run_gpu(sc, t0, period, count, app_send, app_obs, log_cap, trace_cap):
+    eng = p2p.Engine(sc, log_cap=log_cap)
+    eng.set_trace(trace_cap)
+    eng.reset()
+    sim = nsgpu.Sim()
+    sim.attach_p2p(eng)
+    sim.set_log(log_cap)
+    samples = []
+    k = [0]
+
+    def probe():
+        samples.append(eng.counters()[1][app_obs].copy())
+        sim.p2p_send(app_send)
+        k[0] += 1
+        if k[0] < count:
+            sim.schedule(period, probe)
+
+    if count:
+        sim.schedule(t0, probe)
+    sim.run()
+    st, devc, appc, (lts, luid, lctx) = eng.results(log_n=log_cap)
+    host_n, _host_c, host_d = sim.host_stats()
+    m = sim.log[1] != 0  # the host dispatches' ranks
+    lts, luid, lctx = lts.copy(), luid.copy(), lctx.copy()
+    lts[m], luid[m], lctx[m] = sim.log[0][m], sim.log[1][m], sim.log[2][m]
+    out = dict(dispatched=sim.dispatched(), digest=(int(st.digest) + host_d) & ((1 << 64) - 1),
+               next_uid=sim.next_uid(), host=host_n)
+    return out, devc, appc, (lts, luid, lctx), trace.sort_records(eng.trace()), np.array(samples)
+
+
+def run_oracle(sc, t0, period, count, app_send, app_obs, log_cap):
+    s = sc.c_struct()
+    st = p2p.P2PStats()
+    devc = np.zeros(s.n_devices, p2p.DEV_COUNTERS_DTYPE)
+    appc = np.zeros(s.n_apps, p2p.APP_COUNTERS_DTYPE)
+    log, tr, samples = nsref.p2p_run_probe(s, st, devc, appc, t0, period, count, app_send, app_obs, log_cap)
+    return st, devc, appc, log, trace.sort_records(tr), samples
+
+
+def check_same(sc, o, g):
+    st, devc, appc, olog, otr, osamp = o
+    gout, gdevc, gappc, glog, gtr, gsamp = g
+    assert gout["dispatched"] == st.dispatched
+    assert gout["digest"] == st.digest
+    assert gout["next_uid"] == st.next_uid
+    assert np.array_equal(gdevc, devc)
+    assert np.array_equal(gappc, appc)
+    n = int(min(st.dispatched, len(olog[0])))
+    for a, b, name in zip(glog, olog, ("ts", "uid", "ctx")):
+        assert np.array_equal(a[:n], b[:n]), name
+    assert len(gsamp) == len(osamp)
+    for f in ("tx_packets", "rx_packets", "tx_bytes", "rx_bytes"):
+        assert np.array_equal(gsamp[f], osamp[f]), f
+    assert_same_trace(sc, otr, gtr)
+
+
+def flows_grid():
+    g = p2p.grid(5, 5, qmax=6, rate_bps=2_000_000, stop_ns=300_000_000, sim_stop_ns=350_000_000,
+                 flows=[(0, 24), (4, 20), (2, 22), (10, 14)])
+    return g
+
+
+@pytest.mark.parametrize("t0,period,count", [
+    (150_000_000, 7_300_001, 20),     # between device events
+    (100_000_000, 1_000_000, 60),     # the OnOff start time itself: ties with setup-scheduled events
+    (0, 433_600, 40),                 # from time 0 (ties with the setup events), at the 542-B tx time
+])
+def test_host_probe_interleaved_with_device_events(t0, period, count):
+    sc = flows_grid()
+    app_send = [i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_ONOFF][1]
+    app_obs = [i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_SINK][0]
+    o = run_oracle(sc, t0, period, count, app_send, app_obs, 400000)
+    g = run_gpu(sc, t0, period, count, app_send, app_obs, 400000, 400000)
+    assert g[0]["host"] == count
+    check_same(sc, o, g)
+
+
+def test_host_probe_after_device_stop_is_not_run():
+    """Simulator::Stop (a device event of the scenario) ends Run: host closures after it never run."""
+    sc = flows_grid()
+    app_send = [i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_ONOFF][0]
+    app_obs = [i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_SINK][0]
+    o = run_oracle(sc, 200_000_000, 20_000_000, 30, app_send, app_obs, 400000)
+    g = run_gpu(sc, 200_000_000, 20_000_000, 30, app_send, app_obs, 400000, 400000)
+    assert 0 < len(g[5]) < 30
+    o = (o[0], o[1], o[2], o[3], o[4], o[5][:len(g[5])])  # (the oracle's sample buffer has `count` slots)
+    check_same(sc, o, g)
+
+
+def test_pull_windows_same_time_group_and_remove():
+    """The raw-handle pull interface (what ns3::HipSimulatorImpl::Run uses): a window is every event of
+    the smallest time; an event scheduled during the window sorts after it; a window event removed by
+    an earlier one of the same window is skipped; dispatch order equals the (ts, uid) order."""
+    s = nsgpu.Sim(batch=4)
+    order = []
+    uids = {}
+    for h, ts in ((2, 50), (4, 10), (6, 10), (8, 10), (10, 30)):
+        uids[h] = (ts, s.insert_raw(ts, 0, h))
+    while True:
+        w = s.pop_window()
+        if len(w) == 0:
+            break
+        assert len(set(int(x) for x in w["ts"])) == 1
+        for ev in w:
+            if s.begin(ev) != 0:
+                continue
+            h = int(ev["handle"]) & ~1
+            order.append(h)
+            if h == 4:  # removes a later event of its own window and schedules one at the same time
+                s.remove_key(*uids[8])
+                uids[12] = (10, s.insert_raw(10, 0, 12))
+    assert order == [4, 6, 12, 10, 2]
