@@ -167,6 +167,9 @@ int nsgpu_sim_stop_at(nsgpu_sim *s, int64_t delay);
 int nsgpu_sim_destroy(nsgpu_sim *s);
 int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *dispatched, uint32_t *next_uid);
 int nsgpu_sim_current_uid(nsgpu_sim *s, uint32_t *uid);
+int nsgpu_sim_next(nsgpu_sim *s, uint64_t *ts, int *empty);          /* Next () / IsFinished () */
+int nsgpu_sim_set_stop(nsgpu_sim *s, int stop);                      /* Stop (); Run clears it */
+int nsgpu_sim_drain(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n);  /* DoDispose */
 /* windows: *n = 0 when nothing is left to dispatch or a Stop was dispatched */
 int nsgpu_sim_pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n);
 /* window event *e is dispatched next: *skip = 0 run it (Now/Context/uid set, dispatch counted), 1 a

@@ -1719,7 +1719,8 @@ extern "C" int nsgpu_comm_destroy(nsgpu_comm *c) {
 
 struct nsgpu_p2p {
   P2PDev M;
-  nsgpu_p2p_scenario sc;
+  nsgpu_p2p_scenario sc;  // (its host pointers are the caller's: not used after nsgpu_p2p_create)
+  std::vector<uint32_t> app_kind;
   std::vector<void *> allocs;
   Ctl C0{};               // run control after reset
   uint64_t max_windows = ~0ull;
@@ -1876,6 +1877,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
       send_ivl = std::min(send_ivl, seconds_to_ts((sc->app_pkt_size[a] * 8) / static_cast<double>(sc->app_rate_bps[a])));
   nsgpu_p2p *h = new nsgpu_p2p();
   h->sc = *sc;
+  h->app_kind.assign(sc->app_kind, sc->app_kind + A);
   h->n_apps = A;
   P2PDev &M = h->M;
   memset(&M, 0, sizeof(M));
@@ -2409,7 +2411,7 @@ extern "C" int nsgpu_p2p_inject_send(nsgpu_p2p *h, uint32_t app, uint64_t now, u
                                      uint32_t *uid, uint32_t *trace_seq, void *stream) {
   if (!h || !uid || !trace_seq) return set_error(NSGPU_EINVAL, "nsgpu_p2p_inject_send: null");
   if (h->M.dist) return set_error(NSGPU_ESTATE, "nsgpu_p2p_inject_send: single-device engines only");
-  if (app >= h->M.n_apps || h->sc.app_kind[app] != NSGPU_APP_ONOFF)
+  if (app >= h->M.n_apps || h->app_kind[app] != NSGPU_APP_ONOFF)
     return set_error(NSGPU_EINVAL, "nsgpu_p2p_inject_send: app %u is not an OnOff flow", app);
   hipStream_t s = h->s;
   hipStream_t cs = (hipStream_t)stream;

@@ -342,6 +342,45 @@ int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *di
   return NSGPU_OK;
 }
 
+// Next () / IsFinished (): the time of the next host event (device events of an attached engine
+// are not counted: they never outlive Run); *empty = 1 when none is pending.
+int nsgpu_sim_next(nsgpu_sim *s, uint64_t *ts, int *empty) {
+  if (!s || !ts || !empty) return set_error(NSGPU_EINVAL, "nsgpu_sim_next: null");
+  uint64_t n = 0;
+  int rc = nsgpu_sched_size(s->events, &n);
+  if (rc) return rc;
+  *empty = n == 0;
+  *ts = 0;
+  if (n) {
+    nsgpu_event e;
+    if ((rc = nsgpu_sched_peek_next(s->events, &e))) return rc;
+    *ts = e.ts;
+  }
+  return NSGPU_OK;
+}
+
+// Stop () sets the flag that ends the current Run at the next dispatch; Run clears it (:153-165).
+int nsgpu_sim_set_stop(nsgpu_sim *s, int stop) {
+  if (!s) return set_error(NSGPU_EINVAL, "nsgpu_sim_set_stop: null");
+  s->stop = stop != 0;
+  return NSGPU_OK;
+}
+
+// DoDispose: hands back up to `cap` pending events (not dispatched) so the caller can release them.
+int nsgpu_sim_drain(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n) {
+  if (!s || !out || !n) return set_error(NSGPU_EINVAL, "nsgpu_sim_drain: null");
+  *n = 0;
+  for (uint32_t k = 0; k < cap; k++) {
+    uint64_t size = 0;
+    int rc = nsgpu_sched_size(s->events, &size);
+    if (rc) return rc;
+    if (!size) break;
+    if ((rc = nsgpu_sched_remove_next(s->events, &out[k]))) return rc;
+    *n = k + 1;
+  }
+  return NSGPU_OK;
+}
+
 int nsgpu_sim_current_uid(nsgpu_sim *s, uint32_t *uid) {
   if (!s || !uid) return set_error(NSGPU_EINVAL, "nsgpu_sim_current_uid: null");
   *uid = s->cur_uid;

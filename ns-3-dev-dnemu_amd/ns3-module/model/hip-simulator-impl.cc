@@ -1,13 +1,30 @@
 /* -*- Mode:C++; c-file-style:"gnu"; indent-tabs-mode:nil; -*- */
 #include "hip-simulator-impl.h"
-#include "hip-batch-scheduler.h"
 #include "ns3/simulator.h"
-#include "ns3/assert.h"
+#include "ns3/fatal-error.h"
 #include "ns3/object-factory.h"
+#include <algorithm>
 
 namespace ns3 {
 
 NS_OBJECT_ENSURE_REGISTERED (HipSimulatorImpl);
+
+#define NSGPU_RT(call)                                                      \
+  do {                                                                      \
+      if ((call) != NSGPU_OK)                                               \
+        {                                                                   \
+          NS_FATAL_ERROR ("libnsgpu: " << nsgpu_last_error ());             \
+        }                                                                   \
+    } while (false)
+
+namespace {
+/* the runtime hands raw handles back with bit 0 set (include/nsgpu.h, nsgpu_sim_insert) */
+EventImpl *
+HandleToEvent (uint64_t handle)
+{
+  return reinterpret_cast<EventImpl *> (static_cast<uintptr_t> (handle & ~static_cast<uint64_t> (1)));
+}
+} // anonymous namespace
 
 TypeId
 HipSimulatorImpl::GetTypeId (void)
@@ -19,38 +36,68 @@ HipSimulatorImpl::GetTypeId (void)
   return tid;
 }
 
-// uid 0 invalid, 1 "now", 2 "destroy": the first scheduled event gets 4 (as DefaultSimulatorImpl)
 HipSimulatorImpl::HipSimulatorImpl ()
-  : m_stop (false), m_nextUid (4), m_uid (0), m_ts (0), m_context (0xffffffff), m_pending (0), m_dispatched (0)
+  : m_rt (0),
+    m_window (4096)
 {
-  m_events = CreateObject<HipBatchScheduler> ();
+  NSGPU_RT (nsgpu_sim_create (4096, 0, &m_rt));
 }
 
 HipSimulatorImpl::~HipSimulatorImpl ()
 {
+  nsgpu_sim_free (m_rt);
+}
+
+void
+HipSimulatorImpl::AttachDeviceSubset (nsgpu_p2p *engine)
+{
+  NSGPU_RT (nsgpu_sim_attach_p2p (m_rt, engine));
+}
+
+uint64_t
+HipSimulatorImpl::NowTs (void) const
+{
+  uint64_t now = 0;
+  NSGPU_RT (nsgpu_sim_state (m_rt, &now, 0, 0, 0));
+  return now;
+}
+
+uint64_t
+HipSimulatorImpl::GetEventCount (void) const
+{
+  uint64_t n = 0;
+  NSGPU_RT (nsgpu_sim_state (m_rt, 0, 0, &n, 0));
+  return n;
 }
 
 void
 HipSimulatorImpl::DoDispose (void)
 {
-  while (!m_events->IsEmpty ())
+  // pending closures were Ref'ed for the queue (Simulator::Schedule hands over one reference)
+  uint32_t n = 0;
+  do
     {
-      m_events->RemoveNext ().impl->Unref ();
+      NSGPU_RT (nsgpu_sim_drain (m_rt, &m_window[0], m_window.size (), &n));
+      for (uint32_t i = 0; i < n; i++)
+        {
+          HandleToEvent (m_window[i].handle)->Unref ();
+        }
     }
-  m_events = 0;
+  while (n > 0);
   SimulatorImpl::DoDispose ();
 }
 
 void
 HipSimulatorImpl::Destroy ()
 {
-  while (!m_destroy.empty ())
+  // ScheduleDestroy order; an event cancelled or removed meanwhile does not run
+  std::vector<EventId> pending;
+  pending.swap (m_atDestroy);
+  for (std::vector<EventId>::iterator i = pending.begin (); i != pending.end (); ++i)
     {
-      Ptr<EventImpl> ev = m_destroy.front ().PeekEventImpl ();
-      m_destroy.pop_front ();
-      if (!ev->IsCancelled ())
+      if (!i->PeekEventImpl ()->IsCancelled ())
         {
-          ev->Invoke ();
+          i->PeekEventImpl ()->Invoke ();
         }
     }
 }
@@ -58,16 +105,10 @@ HipSimulatorImpl::Destroy ()
 void
 HipSimulatorImpl::SetScheduler (ObjectFactory schedulerFactory)
 {
-  // Simulator::GetImpl calls this after construction (simulator.cc:79-114): move pending events
-  Ptr<Scheduler> s = schedulerFactory.Create<Scheduler> ();
-  if (m_events != 0)
-    {
-      while (!m_events->IsEmpty ())
-        {
-          s->Insert (m_events->RemoveNext ());
-        }
-    }
-  m_events = s;
+  // Simulator::GetImpl hands over the SchedulerType factory (simulator.cc:79-114).  The runtime's
+  // queue is the device-resident HipBatchScheduler whatever the factory: every ns-3 scheduler pops
+  // in the same (ts, uid) order (scheduler.h:105-140), so the dispatch order does not change.
+  (void) schedulerFactory;
 }
 
 uint32_t
@@ -76,66 +117,82 @@ HipSimulatorImpl::GetSystemId (void) const
   return 0;
 }
 
-void
-HipSimulatorImpl::Insert (uint64_t ts, uint32_t context, EventImpl *event)
+EventId
+HipSimulatorImpl::Enqueue (uint64_t ts, uint32_t context, EventImpl *event)
 {
-  Scheduler::Event ev;
-  ev.impl = event;
-  ev.key.m_ts = ts;
-  ev.key.m_context = context;
-  ev.key.m_uid = m_nextUid++;
-  m_pending++;
-  m_events->Insert (ev);
-}
-
-void
-HipSimulatorImpl::Dispatch (void)
-{
-  Scheduler::Event next = m_events->RemoveNext ();
-  NS_ASSERT (next.key.m_ts >= m_ts);
-  m_pending--;
-  m_ts = next.key.m_ts;           // Now / Context / Uid are updated before Invoke
-  m_context = next.key.m_context;
-  m_uid = next.key.m_uid;
-  m_dispatched++;
-  next.impl->Invoke ();           // a cancelled EventImpl is still dequeued, Invoke skips it
-  next.impl->Unref ();
+  uint32_t uid = 0;
+  NSGPU_RT (nsgpu_sim_insert (m_rt, ts, context, reinterpret_cast<uintptr_t> (event), &uid));
+  return EventId (event, ts, context, uid);
 }
 
 bool
 HipSimulatorImpl::IsFinished (void) const
 {
-  return m_events->IsEmpty () || m_stop;
+  uint64_t ts = 0;
+  int empty = 1;
+  NSGPU_RT (nsgpu_sim_next (m_rt, &ts, &empty));
+  return empty != 0;
 }
 
 Time
 HipSimulatorImpl::Next (void) const
 {
-  NS_ASSERT (!m_events->IsEmpty ());
-  return TimeStep (m_events->PeekNext ().key.m_ts);
+  uint64_t ts = 0;
+  int empty = 1;
+  NSGPU_RT (nsgpu_sim_next (m_rt, &ts, &empty));
+  if (empty)
+    {
+      NS_FATAL_ERROR ("HipSimulatorImpl::Next: no pending event");
+    }
+  return TimeStep (ts);
+}
+
+void
+HipSimulatorImpl::RunWindows (uint32_t limit)
+{
+  uint32_t done = 0;
+  while (done < limit)
+    {
+      uint32_t n = 0;
+      const uint32_t cap = std::min<uint32_t> (limit - done, m_window.size ());
+      NSGPU_RT (nsgpu_sim_pop_window (m_rt, &m_window[0], cap, &n));
+      if (n == 0)
+        {
+          return;  // nothing pending (host or device), or a Stop was dispatched
+        }
+      for (uint32_t i = 0; i < n; i++)
+        {
+          int skip = 0;
+          NSGPU_RT (nsgpu_sim_begin (m_rt, &m_window[i], &skip));
+          if (skip != 0)
+            {
+              continue;  // removed by a closure of this window (released there), or after a Stop
+            }
+          EventImpl *ev = HandleToEvent (m_window[i].handle);
+          ev->Invoke ();  // Invoke skips a cancelled closure; the dispatch still counts (H16)
+          ev->Unref ();
+          done++;
+        }
+    }
 }
 
 void
 HipSimulatorImpl::Run (void)
 {
-  m_stop = false;
-  while (!m_events->IsEmpty () && !m_stop)
-    {
-      Dispatch ();
-    }
-  NS_ASSERT (!m_events->IsEmpty () || m_pending == 0);
+  NSGPU_RT (nsgpu_sim_set_stop (m_rt, 0));
+  RunWindows (0xffffffffu);
 }
 
 void
 HipSimulatorImpl::RunOneEvent (void)
 {
-  Dispatch ();
+  RunWindows (1);
 }
 
 void
 HipSimulatorImpl::Stop (void)
 {
-  m_stop = true;
+  NSGPU_RT (nsgpu_sim_set_stop (m_rt, 1));
 }
 
 void
@@ -147,46 +204,50 @@ HipSimulatorImpl::Stop (Time const &time)
 EventId
 HipSimulatorImpl::Schedule (Time const &time, EventImpl *event)
 {
-  Time t = time + TimeStep (m_ts);
-  NS_ASSERT (t.IsPositive () && t >= TimeStep (m_ts));
-  uint32_t uid = m_nextUid;
-  Insert ((uint64_t) t.GetTimeStep (), m_context, event);
-  return EventId (event, (uint64_t) t.GetTimeStep (), m_context, uid);
+  const int64_t ts = time.GetTimeStep () + static_cast<int64_t> (NowTs ());
+  if (time.IsStrictlyNegative () || ts < 0)
+    {
+      NS_FATAL_ERROR ("HipSimulatorImpl::Schedule: an event in the past");
+    }
+  return Enqueue (static_cast<uint64_t> (ts), GetContext (), event);
 }
 
 void
 HipSimulatorImpl::ScheduleWithContext (uint32_t context, Time const &time, EventImpl *event)
 {
-  Insert (m_ts + time.GetTimeStep (), context, event);
+  Enqueue (NowTs () + time.GetTimeStep (), context, event);
 }
 
 EventId
 HipSimulatorImpl::ScheduleNow (EventImpl *event)
 {
-  uint32_t uid = m_nextUid;
-  Insert (m_ts, m_context, event);
-  return EventId (event, m_ts, m_context, uid);
+  return Enqueue (NowTs (), GetContext (), event);
 }
 
 EventId
 HipSimulatorImpl::ScheduleDestroy (EventImpl *event)
 {
-  EventId id (Ptr<EventImpl> (event, false), m_ts, 0xffffffff, 2);
-  m_destroy.push_back (id);
-  m_nextUid++;                    // destroy events consume a uid too
+  // uid 2 marks a destroy event; its own uid is consumed all the same
+  NSGPU_RT (nsgpu_sim_consume_uid (m_rt, 0));
+  EventId id (Ptr<EventImpl> (event, false), NowTs (), 0xffffffff, 2);
+  m_atDestroy.push_back (id);
   return id;
 }
 
 Time
 HipSimulatorImpl::Now (void) const
 {
-  return TimeStep (m_ts);
+  return TimeStep (NowTs ());
 }
 
 Time
 HipSimulatorImpl::GetDelayLeft (const EventId &id) const
 {
-  return IsExpired (id) ? TimeStep (0) : TimeStep (id.GetTs () - m_ts);
+  if (IsExpired (id))
+    {
+      return TimeStep (0);
+    }
+  return TimeStep (id.GetTs () - NowTs ());
 }
 
 void
@@ -194,13 +255,10 @@ HipSimulatorImpl::Remove (const EventId &id)
 {
   if (id.GetUid () == 2)
     {
-      for (DestroyList::iterator i = m_destroy.begin (); i != m_destroy.end (); i++)
+      std::vector<EventId>::iterator i = std::find (m_atDestroy.begin (), m_atDestroy.end (), id);
+      if (i != m_atDestroy.end ())
         {
-          if (*i == id)
-            {
-              m_destroy.erase (i);
-              break;
-            }
+          m_atDestroy.erase (i);
         }
       return;
     }
@@ -208,15 +266,10 @@ HipSimulatorImpl::Remove (const EventId &id)
     {
       return;
     }
-  Scheduler::Event ev;
-  ev.impl = id.PeekEventImpl ();
-  ev.key.m_ts = id.GetTs ();
-  ev.key.m_context = id.GetContext ();
-  ev.key.m_uid = id.GetUid ();
-  m_events->Remove (ev);
-  ev.impl->Cancel ();
-  ev.impl->Unref ();
-  m_pending--;
+  NSGPU_RT (nsgpu_sim_remove_key (m_rt, id.GetTs (), id.GetUid (), id.GetContext (),
+                                  reinterpret_cast<uintptr_t> (id.PeekEventImpl ())));
+  id.PeekEventImpl ()->Cancel ();
+  id.PeekEventImpl ()->Unref ();  // the queue's reference
 }
 
 void
@@ -231,41 +284,32 @@ HipSimulatorImpl::Cancel (const EventId &id)
 bool
 HipSimulatorImpl::IsExpired (const EventId &ev) const
 {
-  if (ev.GetUid () == 2)
+  EventImpl *impl = ev.PeekEventImpl ();
+  if (impl == 0 || impl->IsCancelled ())
     {
-      if (ev.PeekEventImpl () == 0 || ev.PeekEventImpl ()->IsCancelled ())
-        {
-          return true;
-        }
-      for (DestroyList::const_iterator i = m_destroy.begin (); i != m_destroy.end (); i++)
-        {
-          if (*i == ev)
-            {
-              return false;
-            }
-        }
       return true;
     }
-  return ev.PeekEventImpl () == 0 || ev.GetTs () < m_ts ||
-         (ev.GetTs () == m_ts && ev.GetUid () <= m_uid) || ev.PeekEventImpl ()->IsCancelled ();
+  if (ev.GetUid () == 2)
+    {
+      return std::find (m_atDestroy.begin (), m_atDestroy.end (), ev) == m_atDestroy.end ();
+    }
+  int expired = 0;
+  NSGPU_RT (nsgpu_sim_key_expired (m_rt, ev.GetTs (), ev.GetUid (), &expired));
+  return expired != 0;
 }
 
 Time
 HipSimulatorImpl::GetMaximumSimulationTime (void) const
 {
-  return TimeStep (0x7fffffffffffffffLL);
+  return TimeStep (0x7fffffffffffffffLL);  // the int64 ns horizon of Time
 }
 
 uint32_t
 HipSimulatorImpl::GetContext (void) const
 {
-  return m_context;
-}
-
-uint64_t
-HipSimulatorImpl::GetEventCount (void) const
-{
-  return m_dispatched;
+  uint32_t ctx = 0;
+  NSGPU_RT (nsgpu_sim_state (m_rt, 0, &ctx, 0, 0));
+  return ctx;
 }
 
 } // namespace ns3

@@ -1,21 +1,24 @@
 /* -*- Mode:C++; c-file-style:"gnu"; indent-tabs-mode:nil; -*- */
 /*
- * ns3::HipSimulatorImpl — SimulatorImpl (src/core/model/simulator-impl.h:35-200) whose event list is
- * the device-resident HipBatchScheduler and whose Run() can hand GPU-resident model subsets to
- * libnsgpu.so.  Selected with
+ * ns3::HipSimulatorImpl — a SimulatorImpl (src/core/model/simulator-impl.h:35-200) whose run loop is the
+ * windowed runtime of libnsgpu (include/nsgpu.h, nsgpu_sim_*): the pending EventImpl* live in the
+ * device-resident HipBatchScheduler, Run() pulls one WINDOW per call (every pending event of the
+ * smallest timestamp; with a GPU-resident p2p subset attached, the engine first dispatches every device
+ * event before the next host event) and invokes its closures here, on the host.  The uid counter,
+ * Now/Context and the dispatch rank live in the runtime, so host closures and device events share one
+ * (ts, uid) order.  Selected with
  *   NS_GLOBAL_VALUE="SimulatorImplementationType=ns3::HipSimulatorImpl"
  * (GlobalValue g_simTypeImpl, src/core/model/simulator.cc:44-48).
- * Host-closure semantics equal DefaultSimulatorImpl's (default-simulator-impl.cc:49-353); the same
- * rules are implemented and tested in libnsgpu's nsgpu_sim_* runtime.
  */
 #ifndef HIP_SIMULATOR_IMPL_H
 #define HIP_SIMULATOR_IMPL_H
 
 #include "ns3/simulator-impl.h"
-#include "ns3/scheduler.h"
 #include "ns3/event-impl.h"
+#include "ns3/event-id.h"
 #include "ns3/ptr.h"
-#include <list>
+#include "nsgpu.h"
+#include <vector>
 
 namespace ns3 {
 
@@ -48,24 +51,23 @@ public:
   virtual uint32_t GetSystemId (void) const;
   virtual uint32_t GetContext (void) const;
 
-  // number of RemoveNext dispatches (cancelled ones included)
+  /* A GPU-resident point-to-point subset (nsgpu_p2p, e.g. from NsgpuP2pScenario) joins this
+   * simulator's event order; call before anything is scheduled on it. */
+  void AttachDeviceSubset (nsgpu_p2p *engine);
+  /* Dispatches so far (RemoveNext calls, cancelled events included: SURVEY H16), host and device. */
   uint64_t GetEventCount (void) const;
 
 private:
   virtual void DoDispose (void);
-  void Dispatch (void);
-  void Insert (uint64_t ts, uint32_t context, EventImpl *event);
+  /* Pulls and runs windows until the runtime has nothing left or Stop; at most `limit` events. */
+  void RunWindows (uint32_t limit);
+  EventId Enqueue (uint64_t ts, uint32_t context, EventImpl *event);
+  uint64_t NowTs (void) const;
 
-  typedef std::list<EventId> DestroyList;
-  DestroyList m_destroy;
-  Ptr<Scheduler> m_events;
-  bool m_stop;
-  uint32_t m_nextUid;
-  uint32_t m_uid;
-  uint64_t m_ts;
-  uint32_t m_context;
-  int m_pending;
-  uint64_t m_dispatched;
+  nsgpu_sim *m_rt;
+  std::vector<nsgpu_event> m_window;
+  /* ScheduleDestroy'd events: they only run at Destroy (), never through the runtime's queue */
+  std::vector<EventId> m_atDestroy;
 };
 
 } // namespace ns3

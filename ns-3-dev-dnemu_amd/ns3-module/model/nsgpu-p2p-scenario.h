@@ -1,0 +1,73 @@
+/* -*- Mode:C++; c-file-style:"gnu"; indent-tabs-mode:nil; -*- */
+/*
+ * ns3::NsgpuP2pScenario — records a point-to-point topology in the order an ns-3 program builds it with
+ * the stock helpers (NodeContainer::Create -> NodeListPriv::Add, PointToPointHelper::Install -> two
+ * Node::AddDevice, InternetStackHelper::Install -> the loopback device, ApplicationHelper::Install ->
+ * Node::AddApplication, Simulator::Stop), so that the setup-time Schedule calls — and therefore every
+ * uid — come out as the reference's (node-list.cc:124-131, node.cc:111-145, point-to-point-helper.cc
+ * :228-242, ipv4-l3-protocol.cc:227-244), and turns it into the GPU-resident engine (include/nsgpu.h,
+ * nsgpu_p2p_create).  The engine's events then join a HipSimulatorImpl's order through
+ * HipSimulatorImpl::AttachDeviceSubset.  tests/ use the Python twin of this class (ns-3-dev-dnemu_amd/p2p.py).
+ */
+#ifndef NSGPU_P2P_SCENARIO_H
+#define NSGPU_P2P_SCENARIO_H
+
+#include "ns3/nstime.h"
+#include "nsgpu.h"
+#include <stdint.h>
+#include <vector>
+#include <utility>
+
+namespace ns3 {
+
+class NsgpuP2pScenario
+{
+public:
+  NsgpuP2pScenario ();
+  ~NsgpuP2pScenario ();
+
+  uint32_t AddNode (void);
+  /* PointToPointHelper::Install (a, b): device on a, then device on b; returns both device indices */
+  std::pair<uint32_t, uint32_t> Link (uint32_t a, uint32_t b, uint64_t bps, Time delay, uint32_t queueMaxPackets,
+                                      Time interframeGap);
+  void InstallStack (void);
+  uint32_t AddPacketSink (uint32_t node, Time start, Time stop);
+  uint32_t AddOnOff (uint32_t node, uint32_t dstNode, Time start, Time stop, uint64_t rateBps, uint32_t packetSize,
+                     double onSeconds, double offSeconds, uint32_t maxBytes, uint32_t ttl);
+  void Stop (Time at);
+  /* IPv4 next hops: shortest paths towards every flow destination (fewest hops, lowest device first) */
+  void RouteShortestPaths (void);
+  /* The engine (owned by this object); `poolCap` / `logCap` as nsgpu_p2p_create's */
+  nsgpu_p2p *CreateEngine (uint64_t poolCap, uint64_t logCap);
+
+private:
+  struct Dev
+  {
+    uint32_t node, peer, qmax;
+    uint64_t bps;
+    int64_t ifg, delay;
+  };
+  struct App
+  {
+    uint32_t kind, node, dst, size, maxBytes, ttl;
+    int64_t start, stop;
+    uint64_t rate;
+    double on, off;
+  };
+  uint32_t AddApp (const App &a);
+
+  uint32_t m_nodes;
+  std::vector<Dev> m_dev;
+  std::vector<App> m_app;
+  std::vector<std::pair<uint32_t, uint32_t> > m_setup;  // (nsgpu_setup_kind, index), program order
+  std::vector<uint32_t> m_route;                        // [node][slot]
+  std::vector<uint32_t> m_dstSlot;                      // node -> route slot (0xffffffff: none)
+  uint32_t m_nDst;
+  int64_t m_stop;
+  bool m_firstLink;
+  nsgpu_p2p *m_engine;
+};
+
+} // namespace ns3
+
+#endif /* NSGPU_P2P_SCENARIO_H */

@@ -93,6 +93,9 @@ SIGNATURES = {
     "nsgpu_sim_destroy": (C.c_int, [_vp]),
     "nsgpu_sim_state": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "nsgpu_sim_current_uid": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_next": (C.c_int, [_vp, _vp, _vp]),
+    "nsgpu_sim_set_stop": (C.c_int, [_vp, C.c_int]),
+    "nsgpu_sim_drain": (C.c_int, [_vp, _vp, _u32, _vp]),
     "nsgpu_sim_pop_window": (C.c_int, [_vp, _vp, _u32, _vp]),
     "nsgpu_sim_begin": (C.c_int, [_vp, _vp, _vp]),
     "nsgpu_sim_insert": (C.c_int, [_vp, _u64, _u32, _u64, _vp]),
