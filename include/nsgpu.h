@@ -98,6 +98,31 @@ int nsgpu_fanout_spectrum(const nsgpu_phy_soa *phys, int64_t nphy, const nsgpu_t
                           void *d_workspace, void *stream);
 int nsgpu_fanout_workspace_bytes(int64_t nphy, int64_t n_tx, uint64_t *bytes);
 
+/* ---------------- Wi-Fi PHY receive subset (config 3) ----------------
+ * Replaces, for a transmission schedule fixed before Run (nsgpu_wifi_scenario in nsgpu_types.h), the
+ * event chain YansWifiPhy::SendPacket (src/wifi/model/yans-wifi-phy.cc:499-522) -> YansWifiChannel::Send
+ * (yans-wifi-channel.cc:77-115) -> YansWifiChannel::Receive (:117-122) -> YansWifiPhy::StartReceivePacket
+ * (yans-wifi-phy.cc:399-496) with InterferenceHelper (interference-helper.cc:129-212) and
+ * WifiPhyStateHelper, and EndReceive's state part (yans-wifi-phy.cc:770-799).  The fan-out is fused into
+ * the receive kernel.  Results equal a sequential DefaultSimulatorImpl run: uids, timestamps, decisions.
+ *
+ * nsgpu_wifi_create copies the scenario to HBM (host pointers; rx_log != 0 also keeps every Receive's
+ * nsgpu_wifi_rx_log, n_tx * n_phy records).  nsgpu_wifi_run enqueues one whole run on `stream`
+ * (asynchronous).  The readers synchronise with that stream and fail with NSGPU_ENOMEM / NSGPU_ESTATE
+ * when the run hit a capacity (ni_cap, more than 64 transmissions within one arrival spread) or the
+ * reference's fatal error (SendPacket while in TX). */
+typedef struct nsgpu_wifi nsgpu_wifi;
+int nsgpu_wifi_tx_duration_ns(uint32_t size, uint32_t modclass, uint64_t rate_bps, uint32_t bw_hz, uint32_t preamble,
+                              int64_t *ns);  /* WifiPhy::CalculateTxDuration (wifi-phy.cc:141-296) */
+int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgpu_wifi **out);
+int nsgpu_wifi_run(nsgpu_wifi *h, void *stream);
+int nsgpu_wifi_get_stats(nsgpu_wifi *h, nsgpu_wifi_stats *out);
+int nsgpu_wifi_read_phys(nsgpu_wifi *h, nsgpu_wifi_phy_counters *out);   /* n_phy */
+int nsgpu_wifi_read_tx_base(nsgpu_wifi *h, uint32_t *out);               /* n_tx: uid base of each fan-out (0: after Stop) */
+int nsgpu_wifi_read_ends(nsgpu_wifi *h, nsgpu_wifi_end_record *out, uint64_t cap, uint64_t *n);  /* unordered */
+int nsgpu_wifi_read_rx_log(nsgpu_wifi *h, nsgpu_wifi_rx_log *out);        /* n_tx * n_phy */
+int nsgpu_wifi_destroy(nsgpu_wifi *h);
+
 /* ---------------- GPU-resident bench-simulator churn (config 1) ----------------
  * Runs utils/bench-simulator.cc's RunBench + Simulator::Run (bench-simulator.cc:79-127) over
  * MapScheduler order entirely on the device: n initial events Schedule (NanoSeconds (d[i])),

@@ -206,6 +206,103 @@ NSGPU_HD static inline uint64_t nsgpu_dispatch_digest_term(uint64_t rank, uint64
   return nsgpu_mix64(rank * 0x9e3779b97f4a7c15ULL ^ nsgpu_mix64(ts ^ ((uint64_t)uid << 40) ^ (uint64_t)uid));
 }
 
+/* ---------------- Wi-Fi PHY receive subset ----------------
+ * YansWifiChannel::Send (yans-wifi-channel.cc:77-115) -> YansWifiChannel::Receive (:117-122) ->
+ * YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496) with its InterferenceHelper
+ * (interference-helper.cc:129-212, 365-391) and WifiPhyStateHelper (wifi-phy-state-helper.cc:123-185,
+ * 255-322, 392-416), EndReceive's state part (yans-wifi-phy.cc:770-799: NotifyRxEnd + DoSwitchFromRx)
+ * and SendPacket's (:499-522).  The scenario is a PHY harness in the style of wifi-test.cc:181-260:
+ * every transmission is a SendPacket call scheduled before Run (its uid is a setup uid), so the
+ * transmission schedule is an input; the MAC, its DCF and EndReceive's m_random draw stay on the host
+ * (SURVEY H13).  Channel switching is not modelled (no SWITCHING state). */
+enum nsgpu_wifi_modclass { NSGPU_WIFI_DSSS = 0, NSGPU_WIFI_OFDM = 1, NSGPU_WIFI_ERP_OFDM = 2 };
+enum nsgpu_wifi_preamble { NSGPU_WIFI_PREAMBLE_LONG = 0, NSGPU_WIFI_PREAMBLE_SHORT = 1 };
+
+typedef struct nsgpu_wifi_scenario {
+  int64_t n_phy;                /* YansWifiChannel::m_phyList, in Add order */
+  const double *x, *y, *z;      /* ConstantPositionMobilityModel positions */
+  const uint32_t *channel;      /* GetChannelNumber () */
+  const uint32_t *node;         /* context of the Receive events (0xffffffff: no NetDevice) */
+  nsgpu_loss_chain loss;
+  double speed;                 /* ConstantSpeedPropagationDelayModel Speed */
+  double rx_gain_db;            /* YansWifiPhy RxGain (default 1) */
+  double ed_threshold_dbm;      /* EnergyDetectionThreshold (default -96) */
+  double cca_threshold_dbm;     /* CcaMode1Threshold (default -99) */
+  int64_t n_tx;                 /* SendPacket calls, in (ts, uid) order */
+  const uint64_t *tx_ts;
+  const uint32_t *tx_uid;       /* setup uids: all below uid_start */
+  const uint32_t *tx_phy;
+  const uint32_t *tx_size;      /* packet->GetSize () at the PHY */
+  const double *tx_dbm;         /* GetPowerDbm (txPowerLevel) + TxGain: the channel's txPowerDbm */
+  const uint32_t *tx_modclass;  /* the payload WifiMode (wifi-phy.cc:236-301) */
+  const uint64_t *tx_rate_bps;
+  const uint32_t *tx_bw_hz;
+  const uint32_t *tx_preamble;  /* nsgpu_wifi_preamble */
+  uint32_t uid_start;           /* DefaultSimulatorImpl::m_uid when Run starts */
+  uint32_t ni_cap;              /* NiChanges capacity per phy (GPU); a longer list fails the run */
+  uint64_t stop_ts;             /* Simulator::Stop event (ts, uid); stop_ts = ~0: none */
+  uint32_t stop_uid;
+  uint32_t pad_;
+} nsgpu_wifi_scenario;
+
+/* Outcome of one Receive event (StartReceivePacket's switch, yans-wifi-phy.cc:416-478). */
+enum nsgpu_wifi_rx_outcome { NSGPU_WIFI_SYNC = 0, NSGPU_WIFI_DROP_RX = 1, NSGPU_WIFI_DROP_TX = 2,
+                             NSGPU_WIFI_DROP_ED = 3, NSGPU_WIFI_NOT_RUN = 255 };
+#define NSGPU_WIFI_F_CCA_EVAL   1u  /* maybeCcaBusy: GetEnergyDuration (CcaMode1Threshold) evaluated */
+#define NSGPU_WIFI_F_CCA_SWITCH 2u  /* ... and non-zero: SwitchMaybeToCcaBusy */
+#define NSGPU_WIFI_F_NEAR_ED    4u  /* rxPowerW within 1e-9 (relative) of EnergyDetectionThreshold */
+#define NSGPU_WIFI_F_NEAR_CCA   8u  /* a noise+interference sum within 1e-9 of CcaMode1Threshold */
+
+/* One Receive event, at slot [tx * n_phy + phy] (the sender's own slot stays NOT_RUN). */
+typedef struct nsgpu_wifi_rx_log {
+  uint64_t ts;       /* send time + delay */
+  uint32_t uid;      /* uid base of the transmission + rank among the receivers */
+  uint8_t outcome;   /* nsgpu_wifi_rx_outcome */
+  uint8_t flags;     /* NSGPU_WIFI_F_* */
+  uint16_t pad_;
+  int64_t cca_ns;    /* GetEnergyDuration result when evaluated, else 0 */
+} nsgpu_wifi_rx_log;
+
+/* One EndReceive event (the Simulator::Schedule of a syncing StartReceivePacket, yans-wifi-phy.cc:469-471). */
+#define NSGPU_WIFI_END_CANCELLED  1u  /* SendPacket while in Rx cancelled it (:510-514); still dispatched */
+#define NSGPU_WIFI_END_DISPATCHED 2u  /* before the Stop event */
+typedef struct nsgpu_wifi_end_record {
+  uint64_t ts;
+  uint64_t sync_ts;  /* the Receive event that synced */
+  uint32_t uid;
+  uint32_t phy;
+  uint32_t tx;       /* transmission index of the packet */
+  uint32_t flags;
+} nsgpu_wifi_end_record;
+
+typedef struct nsgpu_wifi_phy_counters {
+  uint32_t rx, sync, drop_rx, drop_tx, drop_ed, cca_switches, end, end_cancelled;
+  uint32_t ni_len;   /* NiChanges length when the run ended */
+  uint32_t ni_max;
+  int64_t end_tx, end_rx, end_cca_busy;  /* WifiPhyStateHelper m_endTx / m_endRx / m_endCcaBusy */
+  double first_power;                    /* InterferenceHelper::m_firstPower */
+  uint32_t rxing, pad_;
+} nsgpu_wifi_phy_counters;
+
+typedef struct nsgpu_wifi_stats {
+  uint64_t dispatched;      /* SendPacket + Receive + EndReceive (+ Stop) dispatches, cancelled ones included */
+  uint64_t tx, rx, sync, drop_rx, drop_tx, drop_ed, cca_evals, cca_switches, end, end_cancelled;
+  uint64_t ni_inserts;      /* NiChange entries inserted */
+  uint64_t near_threshold;  /* Receive events flagged NEAR_ED or NEAR_CCA */
+  uint64_t digest;          /* sum of nsgpu_wifi_term over the dispatched events */
+  uint64_t final_ts;        /* Now () when Run returned */
+  uint32_t next_uid;        /* m_uid when Run returned */
+  uint32_t ni_max;
+} nsgpu_wifi_stats;
+
+/* Digest term of a dispatched event: SendPacket (0, ts, uid, uid base of its fan-out, 0); Receive
+ * (1, ts, tx, phy, outcome | (flags & 3) << 8 | cca_ns << 16); EndReceive (2, ts, uid, phy, cancelled);
+ * Stop (3, ts, uid, 0, 0).  A Receive's uid is base + rank, so the SendPacket term pins it. */
+NSGPU_HD static inline uint64_t nsgpu_wifi_term(uint64_t kind, uint64_t ts, uint64_t a, uint64_t b, uint64_t c) {
+  return nsgpu_mix64(nsgpu_mix64(ts ^ (kind << 60)) + nsgpu_mix64(a * 0x9e3779b97f4a7c15ULL + b) +
+                     c * 0xd1b54a32d192ed03ULL);
+}
+
 #ifdef __cplusplus
 }
 #endif

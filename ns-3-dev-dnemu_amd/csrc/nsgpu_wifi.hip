@@ -1,0 +1,792 @@
+// nsgpu_wifi.hip — the Wi-Fi PHY receive subset on the device (include/nsgpu.h: nsgpu_wifi_*).
+//
+// Replaces, for a transmission schedule fixed before Run (nsgpu_wifi_scenario, the wifi-test.cc:181-260
+// harness shape): YansWifiPhy::SendPacket (yans-wifi-phy.cc:499-522) -> YansWifiChannel::Send
+// (yans-wifi-channel.cc:77-115) -> YansWifiChannel::Receive (:117-122) -> YansWifiPhy::StartReceivePacket
+// (yans-wifi-phy.cc:399-496) with InterferenceHelper::Add / AppendEvent / GetEnergyDuration
+// (interference-helper.cc:129-212, 365-391), the WifiPhyStateHelper transitions
+// (wifi-phy-state-helper.cc:122-183, 254-322, 391-423) and EndReceive's state part (yans-wifi-phy.cc:770-799).
+//
+// Decomposition.  A phy's receive state (NiChanges, m_firstPower, m_rxing, m_endTx/Rx/CcaBusy) is touched
+// only by the events addressed to it: the Receive events of the other phys' transmissions, its own
+// SendPacket calls and its own EndReceive events.  With the schedule fixed, each phy's event sequence is
+// known up front, so lane j runs phy j's sequence in (ts, uid) order (k_wifi_phy).  Lane j computes the
+// fan-out arithmetic of receiver j itself (distance, loss chain, delay: the 64-B fan-out record of
+// nsgpu_fanout_yans never goes to HBM) while it consumes the transmission.
+//
+// Order inside one phy needs no global uid.  Uids are handed out in dispatch order, and every
+// transmission's uid is a setup uid (below every run-time uid), so between two events of phy j at the
+// same ts:
+//   SendPacket before any Receive / EndReceive;
+//   Receive(T1) before Receive(T2)       iff T1 precedes T2 in the schedule (their fan-outs' uid bases);
+//   Receive(T) before EndReceive(R)      iff T was dispatched before the syncing Receive R: t_T <= ts_R;
+//   EndReceive(R1) before EndReceive(R2) iff R1 precedes R2 (ts, then schedule order).
+// A transmission's arrivals come at t_T + d with d > 0, so the next Receive of phy j is the smallest arrival
+// among the transmissions t_T below it: a 64-transmission window after the first unconsumed one.
+//
+// The uids follow from counts (k_sync_hist, k_tx_base, k_sync_place, k_sync_rank): a Receive's syncing
+// consumes one uid (the EndReceive), a transmission's fan-out consumes one per receiver.  With
+// F(k) = fan-out uids of transmissions [0, k) and S(x) = syncs dispatched before x:
+//   uid base of transmission k = uid_start + F(k) + #{syncs R: ts_R < t_k}
+//   uid of EndReceive(R)       = uid_start + F(#{T: t_T <= ts_R}) + #{syncs before R in (ts, uid) order}.
+// Syncs are bucketed by the number of transmissions before them; a bucket holds the syncs between two
+// transmission times, so ranking inside it is a short scan.
+//
+// Roofline: latency-bound per phy (a serial chain of dependent list updates); per Receive event the
+// algorithmic HBM traffic is the transmission descriptor read (broadcast, 48 B, cache-resident) plus the
+// NiChange entries touched (2 x 16 B written, ~2 x 16 B read).  DESIGN.md §4.6 states the figures.
+#include <algorithm>
+#include <vector>
+#include "nsgpu_device.h"
+#include "nsgpu_internal.h"
+
+namespace nsgpu {
+namespace {
+
+constexpr uint64_t INF = ~0ull;
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr int PE_CAP = 8;  // pending EndReceive events of one phy: the live one + cancelled ones
+constexpr uint32_t ERR_WINDOW = 1, ERR_NICAP = 2, ERR_TX_IN_TX = 4, ERR_PENDING = 8, ERR_SYNCCAP = 16;
+enum Acc { A_DIGEST, A_DISPATCHED, A_RX, A_SYNC, A_DROP_RX, A_DROP_TX, A_DROP_ED, A_CCA_EVAL, A_CCA_SWITCH,
+           A_END, A_END_CANCELLED, A_NI_INSERTS, A_NEAR, A_NI_MAX, A_LAST_TS, A_N };
+
+struct NiEnt {  // InterferenceHelper::NiChange (interference-helper.cc:91-110)
+  int64_t t;
+  double d;
+};
+
+struct SyncRec {  // one syncing Receive, i.e. one EndReceive
+  uint64_t ts;      // the Receive
+  uint64_t end_ts;  // its EndReceive
+  uint32_t tx, phy;
+  uint32_t flags;   // NSGPU_WIFI_END_*
+  uint32_t m;       // transmissions dispatched before the Receive (t_T <= ts)
+  uint32_t uid;     // the Receive's uid
+  uint32_t pad_;
+};
+
+struct WifiDev {
+  int64_t nphy;
+  uint32_t ktx;  // dispatched transmissions: those with a key below the Stop event's
+  uint32_t uid_start;
+  const double *x, *y, *z;
+  const uint32_t *chan, *chan_rank;
+  nsgpu_loss_chain loss;
+  double speed, rx_gain_db, edW, ccaW;
+  uint64_t stop_ts;
+  const uint64_t *tx_ts;
+  const uint32_t *tx_phy, *tx_chan, *tx_uid;
+  const int64_t *tx_dur;
+  const double *tx_dbm, *tx_x, *tx_y, *tx_z;
+  const uint64_t *fcum;  // [ktx + 1] fan-out uids of transmissions [0, k)
+  const uint32_t *own_off, *own_idx;
+  uint32_t ni_mask;
+  NiEnt *ni;  // [nphy][ni_mask + 1] ring of each phy's NiChanges
+  SyncRec *sync;
+  unsigned long long *n_sync;
+  uint64_t sync_cap;
+  nsgpu_wifi_phy_counters *pc;
+  nsgpu_wifi_rx_log *rx_log;  // nullable: [ktx][nphy]
+  unsigned long long *acc;    // [A_N]
+  uint32_t *err;
+  uint32_t *hist, *off, *cur, *bucket, *base;
+  nsgpu_wifi_end_record *ends;
+};
+
+// ConstantSpeedPropagationDelayModel::GetDelay + DefaultSimulatorImpl::ScheduleWithContext's m_currentTs +
+__device__ __forceinline__ uint64_t arrival(const WifiDev &D, uint32_t k, double px, double py, double pz,
+                                            double &dist) {
+  dist = distance3(D.tx_x[k], D.tx_y[k], D.tx_z[k], px, py, pz);  // GetDistanceFrom (sender, receiver)
+  return D.tx_ts[k] + (uint64_t)seconds_to_ts(dist / D.speed);
+}
+
+// InterferenceHelper::AddNiChangeEvent (interference-helper.cc:378-383): insert at upper_bound (time).
+__device__ __forceinline__ void ni_insert(NiEnt *ring, uint32_t head, uint32_t &len, uint32_t m, int64_t t, double d) {
+  uint32_t q = len;
+  while (q > 0) {
+    const NiEnt e = ring[(head + q - 1) & m];
+    if (e.t <= t) break;
+    ring[(head + q) & m] = e;
+    q--;
+  }
+  ring[(head + q) & m] = NiEnt{t, d};
+  len++;
+}
+
+__device__ __forceinline__ bool near_thr(double v, double thr) { return fabs(v - thr) <= 1e-9 * thr; }
+
+__global__ void k_rx_log_init(nsgpu_wifi_rx_log *log, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    log[i] = nsgpu_wifi_rx_log{0, 0, NSGPU_WIFI_NOT_RUN, 0, 0, 0};
+}
+
+// One lane = one phy: its SendPacket / Receive / EndReceive sequence in (ts, uid) order.
+__global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
+  const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (j >= D.nphy) return;
+  const double px = D.x[j], py = D.y[j], pz = D.z[j];
+  const uint32_t ch = D.chan[j];
+  const uint32_t m = D.ni_mask;
+  NiEnt *ring = D.ni + (uint64_t)j * (m + 1);
+  // InterferenceHelper (m_niChanges as a ring [head, head + len), m_firstPower) and WifiPhyStateHelper;
+  // the two m_rxing flags are set and cleared together (yans-wifi-phy.cc:466-468, :510-514, :776-797)
+  uint32_t head = 0, len = 0, ni_max = 0;
+  double firstPower = 0.0;
+  bool rxing = false;
+  int64_t endTx = 0, endRx = 0, endCca = 0;
+  // pending EndReceive events
+  uint64_t pe_ts[PE_CAP], pe_sts[PE_CAP];
+  uint32_t pe_tx[PE_CAP], pe_slot[PE_CAP];
+  bool pe_can[PE_CAP];
+  int npe = 0, live = -1;
+  // transmissions: [p, p + 64) is the window, bit i of `done` = transmission p + i consumed here
+  uint32_t p = 0;
+  uint64_t done = 0;
+  uint32_t oc = D.own_off[j];
+  const uint32_t oe = D.own_off[j + 1];
+  bool have_c = false;
+  uint64_t c_ts = INF;
+  uint32_t c_k = NONE;
+  double c_dist = 0.0;
+  uint32_t err = 0;
+  nsgpu_wifi_phy_counters c = {};
+  uint64_t digest = 0, disp = 0, last_ts = 0, ni_ins = 0, cca_eval = 0, near = 0;
+
+  for (;;) {
+    if (!have_c) {  // the next Receive: the smallest arrival of an unconsumed transmission
+      c_ts = INF;
+      c_k = NONE;
+      uint32_t i = 0;
+      for (; i < 64; i++) {
+        const uint32_t k = p + i;
+        if (k >= D.ktx) break;
+        if (D.tx_ts[k] >= c_ts) break;  // its arrival (and every later one) comes after c_ts
+        if ((done >> i) & 1ull) continue;
+        if (D.tx_phy[k] == (uint32_t)j) continue;  // our own SendPacket: taken in order below
+        if (D.tx_chan[k] != ch) {                   // not on our channel: no Receive (:88-91)
+          done |= 1ull << i;
+          continue;
+        }
+        double dist;
+        const uint64_t a = arrival(D, k, px, py, pz, dist);
+        if (a < c_ts) c_ts = a, c_k = k, c_dist = dist;
+      }
+      if (i == 64 && p + 64 < D.ktx && D.tx_ts[p + 64] < c_ts) {
+        err |= ERR_WINDOW;
+        break;
+      }
+      while (done & 1ull) done >>= 1, p++;
+      have_c = true;
+    }
+    const uint32_t ok = oc < oe ? D.own_idx[oc] : NONE;
+    int e = -1;
+    for (int q = 0; q < npe; q++)
+      if (e < 0 || pe_ts[q] < pe_ts[e] ||
+          (pe_ts[q] == pe_ts[e] && (pe_sts[q] < pe_sts[e] || (pe_sts[q] == pe_sts[e] && pe_tx[q] < pe_tx[e]))))
+        e = q;
+    int kind = -1;
+    uint64_t now = INF;
+    if (ok != NONE) kind = 0, now = D.tx_ts[ok];
+    if (c_k != NONE && c_ts < now) kind = 1, now = c_ts;
+    if (e >= 0 && (pe_ts[e] < now || (pe_ts[e] == now && kind == 1 && D.tx_ts[c_k] > pe_sts[e])))
+      kind = 2, now = pe_ts[e];
+    if (kind < 0) break;
+    if (kind != 0 && now >= D.stop_ts) break;  // Stop (a setup uid) runs first; nothing after it does
+    const int64_t nw = (int64_t)now;
+
+    if (kind == 0) {  // YansWifiPhy::SendPacket (yans-wifi-phy.cc:499-522)
+      if (endTx > nw) {  // SwitchToTx from TX: NS_FATAL_ERROR (wifi-phy-state-helper.cc:285-287)
+        err |= ERR_TX_IN_TX;
+        break;
+      }
+      if (rxing) {  // m_endRxEvent.Cancel (); NotifyRxEnd (); SwitchToTx's RX case (:263-268)
+        pe_can[live] = true;
+        live = -1;
+        rxing = false;
+        endRx = nw;
+      }
+      endTx = nw + D.tx_dur[ok];
+      if (ok - p >= 64) {
+        err |= ERR_WINDOW;
+        break;
+      }
+      done |= 1ull << (ok - p);
+      while (done & 1ull) done >>= 1, p++;
+      oc++;
+      last_ts = now;
+      continue;
+    }
+
+    if (kind == 2) {  // YansWifiPhy::EndReceive (yans-wifi-phy.cc:770-799), its state part
+      const bool can = pe_can[e];
+      if (!can) rxing = false;  // NotifyRxEnd (); DoSwitchFromRx (wifi-phy-state-helper.cc:391-402)
+      c.end++;
+      c.end_cancelled += can ? 1u : 0u;
+      SyncRec r;
+      r.ts = pe_sts[e];
+      r.end_ts = pe_ts[e];
+      r.tx = pe_tx[e];
+      r.phy = (uint32_t)j;
+      r.flags = (can ? NSGPU_WIFI_END_CANCELLED : 0u) | NSGPU_WIFI_END_DISPATCHED;
+      r.m = 0;
+      r.uid = 0;
+      r.pad_ = 0;
+      D.sync[pe_slot[e]] = r;
+      const int l = npe - 1;
+      if (live == e) live = -1;
+      if (e != l) {
+        pe_ts[e] = pe_ts[l], pe_sts[e] = pe_sts[l], pe_tx[e] = pe_tx[l], pe_slot[e] = pe_slot[l], pe_can[e] = pe_can[l];
+        if (live == l) live = e;
+      }
+      npe--;
+      disp++;
+      last_ts = now;
+      continue;
+    }
+
+    // YansWifiChannel::Receive -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496)
+    const uint32_t k = c_k;
+    const double rxPowerDbm = calc_rx_power(D.loss, D.tx_dbm[k], c_dist) + D.rx_gain_db;
+    const double rxPowerW = pow(10.0, rxPowerDbm / 10.0) / 1000.0;  // DbmToW (:727-732)
+    const int64_t endNew = nw + D.tx_dur[k];
+    // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
+    if (len + 2 > m + 1) {
+      err |= ERR_NICAP;
+      break;
+    }
+    if (!rxing) {
+      while (len > 0 && ring[head].t <= nw) {  // fold the entries up to upper_bound (now)
+        firstPower += ring[head].d;
+        head = (head + 1) & m;
+        len--;
+      }
+      head = (head - 1) & m;
+      ring[head] = NiEnt{nw, rxPowerW};
+      len++;
+    } else {
+      ni_insert(ring, head, len, m, nw, rxPowerW);
+    }
+    ni_insert(ring, head, len, m, endNew, -rxPowerW);
+    ni_ins += 2;
+    ni_max = len > ni_max ? len : ni_max;
+    // the state switch (WifiPhyStateHelper::GetState, wifi-phy-state-helper.cc:159-183)
+    const int st = endTx > nw ? 2 : rxing ? 1 : endCca > nw ? 3 : 0;
+    uint32_t outcome, flags = 0;
+    bool maybe = false;
+    if (st == 1 || st == 2) {  // drop; noise after the current Rx / Tx (:431-457)
+      outcome = st == 1 ? NSGPU_WIFI_DROP_RX : NSGPU_WIFI_DROP_TX;
+      int64_t until = (st == 1 ? endRx : endTx) - nw;  // GetDelayUntilIdle (:122-151)
+      until = until > 0 ? until : 0;
+      maybe = endNew > nw + until;
+    } else {
+      if (near_thr(rxPowerW, D.edW)) flags |= NSGPU_WIFI_F_NEAR_ED;
+      if (rxPowerW > D.edW) {  // sync (:461-472): SwitchToRx, NotifyRxStart, Schedule (EndReceive)
+        outcome = NSGPU_WIFI_SYNC;
+        if (npe == PE_CAP) {
+          err |= ERR_PENDING;
+          break;
+        }
+        const unsigned long long slot = atomicAdd(D.n_sync, 1ull);
+        if (slot >= D.sync_cap) {
+          err |= ERR_SYNCCAP;
+          break;
+        }
+        rxing = true;
+        endRx = endNew;
+        pe_ts[npe] = (uint64_t)endNew, pe_sts[npe] = now, pe_tx[npe] = k, pe_slot[npe] = (uint32_t)slot, pe_can[npe] = false;
+        live = npe++;
+        c.sync++;
+      } else {
+        outcome = NSGPU_WIFI_DROP_ED;
+        maybe = true;
+      }
+    }
+    int64_t cca = 0;
+    if (maybe) {  // maybeCcaBusy (:482-495): InterferenceHelper::GetEnergyDuration (interference-helper.cc:171-190)
+      flags |= NSGPU_WIFI_F_CCA_EVAL;
+      double noise = firstPower;
+      int64_t end = nw;
+      for (uint32_t q = 0; q < len; q++) {
+        const NiEnt en = ring[(head + q) & m];
+        noise += en.d;
+        end = en.t;
+        if (end < nw) continue;
+        if (near_thr(noise, D.ccaW)) flags |= NSGPU_WIFI_F_NEAR_CCA;
+        if (noise < D.ccaW) break;
+      }
+      cca = end > nw ? end - nw : 0;
+      if (cca != 0) {  // SwitchMaybeToCcaBusy (wifi-phy-state-helper.cc:404-423)
+        flags |= NSGPU_WIFI_F_CCA_SWITCH;
+        endCca = endCca > nw + cca ? endCca : nw + cca;
+        c.cca_switches++;
+      }
+      cca_eval++;
+    }
+    c.rx++;
+    c.drop_rx += outcome == NSGPU_WIFI_DROP_RX;
+    c.drop_tx += outcome == NSGPU_WIFI_DROP_TX;
+    c.drop_ed += outcome == NSGPU_WIFI_DROP_ED;
+    near += (flags & (NSGPU_WIFI_F_NEAR_ED | NSGPU_WIFI_F_NEAR_CCA)) ? 1 : 0;
+    digest += nsgpu_wifi_term(1, now, k, (uint64_t)j, (uint64_t)outcome | (uint64_t)(flags & 3u) << 8 | (uint64_t)cca << 16);
+    if (D.rx_log) {
+      nsgpu_wifi_rx_log *l = D.rx_log + (uint64_t)k * D.nphy + j;
+      l->outcome = (uint8_t)outcome;
+      l->flags = (uint8_t)flags;
+      l->cca_ns = cca;
+    }
+    done |= 1ull << (k - p);
+    while (done & 1ull) done >>= 1, p++;
+    have_c = false;
+    disp++;
+    last_ts = now;
+  }
+  // EndReceive events left pending at the end: scheduled (uid consumed), never dispatched
+  for (int q = 0; q < npe; q++) {
+    SyncRec r;
+    r.ts = pe_sts[q];
+    r.end_ts = pe_ts[q];
+    r.tx = pe_tx[q];
+    r.phy = (uint32_t)j;
+    r.flags = pe_can[q] ? NSGPU_WIFI_END_CANCELLED : 0u;
+    r.m = 0;
+    r.uid = 0;
+    r.pad_ = 0;
+    D.sync[pe_slot[q]] = r;
+  }
+  c.ni_len = len;
+  c.ni_max = ni_max;
+  c.end_tx = endTx;
+  c.end_rx = endRx;
+  c.end_cca_busy = endCca;
+  c.first_power = firstPower;
+  c.rxing = rxing ? 1u : 0u;
+  D.pc[j] = c;
+  if (err) atomicOr(D.err, err);
+  atomicAdd(&D.acc[A_DIGEST], (unsigned long long)digest);
+  atomicAdd(&D.acc[A_DISPATCHED], (unsigned long long)disp);
+  atomicAdd(&D.acc[A_RX], (unsigned long long)c.rx);
+  atomicAdd(&D.acc[A_SYNC], (unsigned long long)c.sync);
+  atomicAdd(&D.acc[A_DROP_RX], (unsigned long long)c.drop_rx);
+  atomicAdd(&D.acc[A_DROP_TX], (unsigned long long)c.drop_tx);
+  atomicAdd(&D.acc[A_DROP_ED], (unsigned long long)c.drop_ed);
+  atomicAdd(&D.acc[A_CCA_EVAL], (unsigned long long)cca_eval);
+  atomicAdd(&D.acc[A_CCA_SWITCH], (unsigned long long)c.cca_switches);
+  atomicAdd(&D.acc[A_END], (unsigned long long)c.end);
+  atomicAdd(&D.acc[A_END_CANCELLED], (unsigned long long)c.end_cancelled);
+  atomicAdd(&D.acc[A_NI_INSERTS], (unsigned long long)ni_ins);
+  atomicAdd(&D.acc[A_NEAR], (unsigned long long)near);
+  atomicMax(&D.acc[A_NI_MAX], (unsigned long long)ni_max);
+  atomicMax(&D.acc[A_LAST_TS], (unsigned long long)last_ts);
+}
+
+// Syncs per bucket m = #transmissions with t_T <= ts (binary search over the schedule).
+__global__ __launch_bounds__(256) void k_sync_hist(const WifiDev D) {
+  const uint64_t n = *D.n_sync < D.sync_cap ? *D.n_sync : D.sync_cap;
+  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < n; s += (uint64_t)gridDim.x * 256) {
+    const uint64_t ts = D.sync[s].ts;
+    uint32_t lo = 0, hi = D.ktx;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (D.tx_ts[mid] <= ts) lo = mid + 1; else hi = mid;
+    }
+    D.sync[s].m = lo;
+    atomicAdd(&D.hist[lo], 1u);
+  }
+}
+
+// One block: off = exclusive scan of hist[0 .. ktx]; uid base of every transmission; their digest terms.
+__global__ __launch_bounds__(1024) void k_tx_base(const WifiDev D) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  const uint32_t n = D.ktx + 1;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < n; c0 += 1024) {
+    const uint32_t i = c0 + threadIdx.x;
+    const uint32_t v = i < n ? D.hist[i] : 0u;
+    uint32_t x = v;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t before = carry;
+    for (int w = 0; w < wid; w++) before += wsum[w];
+    if (i < n) D.off[i] = before + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) D.off[n] = carry;
+  __syncthreads();
+  unsigned long long dg = 0;
+  for (uint32_t k = threadIdx.x; k < D.ktx; k += 1024) {
+    const uint32_t b = D.uid_start + (uint32_t)D.fcum[k] + D.off[k + 1];  // syncs with ts < t_k: buckets 0..k
+    D.base[k] = b;
+    dg += nsgpu_wifi_term(0, D.tx_ts[k], D.tx_uid[k], b, 0);
+  }
+  atomicAdd(&D.acc[A_DIGEST], dg);
+}
+
+__device__ __forceinline__ uint32_t rx_rank(const WifiDev &D, uint32_t j, uint32_t k) {
+  const uint32_t s = D.tx_phy[k];
+  return D.chan_rank[j] - (j > s ? 1u : 0u);  // ScheduleWithContext order of the receiver loop
+}
+
+__global__ __launch_bounds__(256) void k_sync_place(const WifiDev D) {
+  const uint64_t n = *D.n_sync < D.sync_cap ? *D.n_sync : D.sync_cap;
+  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < n; s += (uint64_t)gridDim.x * 256) {
+    SyncRec &r = D.sync[s];
+    r.uid = D.base[r.tx] + rx_rank(D, r.phy, r.tx);
+    const uint32_t pos = D.off[r.m] + atomicAdd(&D.cur[r.m], 1u);
+    D.bucket[pos] = (uint32_t)s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sync_rank(const WifiDev D) {
+  const uint64_t n = *D.n_sync < D.sync_cap ? *D.n_sync : D.sync_cap;
+  unsigned long long dg = 0;
+  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < n; s += (uint64_t)gridDim.x * 256) {
+    const SyncRec r = D.sync[s];
+    const uint32_t lo = D.off[r.m], hi = D.off[r.m + 1];
+    uint32_t before = 0;
+    for (uint32_t q = lo; q < hi; q++) {
+      const SyncRec o = D.sync[D.bucket[q]];
+      before += (o.ts < r.ts || (o.ts == r.ts && o.uid < r.uid)) ? 1u : 0u;
+    }
+    const uint32_t uid = D.uid_start + (uint32_t)D.fcum[r.m] + lo + before;
+    nsgpu_wifi_end_record e;
+    e.ts = r.end_ts;
+    e.sync_ts = r.ts;
+    e.uid = uid;
+    e.phy = r.phy;
+    e.tx = r.tx;
+    e.flags = r.flags;
+    D.ends[s] = e;
+    if (r.flags & NSGPU_WIFI_END_DISPATCHED)
+      dg += nsgpu_wifi_term(2, r.end_ts, uid, r.phy, (r.flags & NSGPU_WIFI_END_CANCELLED) ? 1 : 0);
+  }
+  if (dg) atomicAdd(&D.acc[A_DIGEST], dg);
+}
+
+// Rx log: every scheduled Receive's key (the ones after the Stop included).
+__global__ __launch_bounds__(256) void k_rx_log_keys(const WifiDev D) {
+  const uint64_t n = (uint64_t)D.ktx * (uint64_t)D.nphy;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t k = (uint32_t)(i / (uint64_t)D.nphy), j = (uint32_t)(i % (uint64_t)D.nphy);
+    if (j == D.tx_phy[k] || D.chan[j] != D.tx_chan[k]) continue;
+    double dist;
+    D.rx_log[i].ts = arrival(D, k, D.x[j], D.y[j], D.z[j], dist);
+    D.rx_log[i].uid = D.base[k] + rx_rank(D, j, k);
+  }
+}
+
+// WifiPhy::CalculateTxDuration — wifi-phy.cc:141-296 (preamble + PLCP header + payload, in us)
+int64_t tx_duration_ns(uint32_t size, uint32_t mc, uint64_t rate, uint32_t bw, uint32_t preamble) {
+  uint32_t pre, hdr, pay;
+  if (mc == NSGPU_WIFI_OFDM || mc == NSGPU_WIFI_ERP_OFDM) {
+    const uint32_t sym = bw == 10000000 ? 8 : bw == 5000000 ? 16 : 4;
+    pre = mc == NSGPU_WIFI_ERP_OFDM ? 4 : sym * 4;                            // 16 / 32 / 64 (:196-214), ERP 4
+    hdr = mc == NSGPU_WIFI_ERP_OFDM ? 16 : sym;                               // 4 / 8 / 16 (:148-166), ERP 16
+    const double ndbps = (double)(rate * sym) / 1e6;                          // N_DBPS (:262)
+    const uint32_t nsym = (uint32_t)lrint(ceil((16 + size * 8.0 + 6.0) / ndbps));  // (:265)
+    pay = nsym * sym + (mc == NSGPU_WIFI_ERP_OFDM ? 6u : 0u);
+  } else {  // DSSS (:173-183, :216-226, :281-283)
+    pre = preamble == NSGPU_WIFI_PREAMBLE_SHORT ? 72 : 144;
+    hdr = preamble == NSGPU_WIFI_PREAMBLE_SHORT ? 24 : 48;
+    pay = (uint32_t)lrint(ceil((size * 8.0) / (rate / 1.0e6)));
+  }
+  return (int64_t)(pre + hdr + pay) * 1000;  // MicroSeconds (duration)
+}
+
+}  // namespace
+}  // namespace nsgpu
+
+using namespace nsgpu;
+
+struct nsgpu_wifi {
+  WifiDev D;
+  int64_t n_tx;
+  uint64_t stop_ts;
+  uint32_t stop_uid;
+  bool has_stop;
+  std::vector<void *> allocs;
+  hipStream_t last = nullptr;
+  bool ran = false;
+};
+
+extern "C" int nsgpu_wifi_tx_duration_ns(uint32_t size, uint32_t modclass, uint64_t rate_bps, uint32_t bw_hz,
+                                         uint32_t preamble, int64_t *ns) {
+  if (!ns || rate_bps == 0 || modclass > NSGPU_WIFI_ERP_OFDM) return set_error(NSGPU_EINVAL, "nsgpu_wifi_tx_duration_ns: bad mode");
+  *ns = tx_duration_ns(size, modclass, rate_bps, bw_hz, preamble);
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_destroy(nsgpu_wifi *h) {
+  if (!h) return NSGPU_OK;
+  if (h->last) (void)hipStreamSynchronize(h->last);
+  for (void *p : h->allocs) (void)hipFree(p);
+  delete h;
+  return NSGPU_OK;
+}
+
+template <class T>
+static int dalloc(nsgpu_wifi *h, T **p, size_t n, const T *src = nullptr) {
+  void *v = nullptr;
+  NSGPU_HIP(hipMalloc(&v, std::max<size_t>(n, 1) * sizeof(T)));
+  h->allocs.push_back(v);
+  if (src && n) NSGPU_HIP(hipMemcpy(v, src, n * sizeof(T), hipMemcpyHostToDevice));
+  *p = (T *)v;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgpu_wifi **out) {
+  if (!sc || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: null");
+  *out = nullptr;
+  const int64_t N = sc->n_phy, K = sc->n_tx;
+  if (N < 1 || N > 0x7fffffff || K < 0 || K > 0x7fffffff) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: n_phy %lld n_tx %lld", (long long)N, (long long)K);
+  if (!sc->x || !sc->y || !sc->z || !sc->channel || !sc->node) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: phy arrays");
+  if (K && (!sc->tx_ts || !sc->tx_uid || !sc->tx_phy || !sc->tx_size || !sc->tx_dbm || !sc->tx_modclass ||
+            !sc->tx_rate_bps || !sc->tx_bw_hz || !sc->tx_preamble))
+    return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: transmission arrays");
+  if (!(sc->speed > 0)) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: speed must be > 0");
+  if (sc->loss.n < 0 || sc->loss.n > NSGPU_MAX_LOSS_CHAIN) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: loss chain");
+  const bool has_stop = sc->stop_ts != ~0ull;
+  if (has_stop && sc->stop_uid >= sc->uid_start) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: the Stop uid must be a setup uid");
+  // schedule: (ts, uid) order, setup uids, senders in range; dispatched = keys below the Stop event's
+  uint32_t ktx = 0;
+  for (int64_t k = 0; k < K; k++) {
+    if (sc->tx_phy[k] >= (uint64_t)N) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: tx %lld sender", (long long)k);
+    if (sc->tx_uid[k] >= sc->uid_start) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: tx %lld uid is not a setup uid", (long long)k);
+    if (sc->tx_rate_bps[k] == 0 || sc->tx_modclass[k] > NSGPU_WIFI_ERP_OFDM) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: tx %lld mode", (long long)k);
+    if (k && !key_less(sc->tx_ts[k - 1], sc->tx_uid[k - 1], sc->tx_ts[k], sc->tx_uid[k]))
+      return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: transmissions not in (ts, uid) order at %lld", (long long)k);
+    if (!has_stop || key_less(sc->tx_ts[k], sc->tx_uid[k], sc->stop_ts, sc->stop_uid)) ktx = (uint32_t)k + 1;
+  }
+  uint32_t cap = 4;
+  while (cap < sc->ni_cap && cap < (1u << 20)) cap <<= 1;
+  // channel ranks (YansWifiChannel::Send's receiver order), fan-out sizes, own-transmission lists
+  std::vector<uint32_t> rank((size_t)N), count_of;
+  std::vector<uint32_t> chans(sc->channel, sc->channel + N);
+  std::sort(chans.begin(), chans.end());
+  chans.erase(std::unique(chans.begin(), chans.end()), chans.end());
+  std::vector<uint32_t> seen(chans.size(), 0);
+  for (int64_t j = 0; j < N; j++) {
+    const size_t c = std::lower_bound(chans.begin(), chans.end(), sc->channel[j]) - chans.begin();
+    rank[j] = seen[c]++;
+  }
+  std::vector<uint64_t> fcum((size_t)ktx + 1, 0);
+  std::vector<uint32_t> tx_chan((size_t)std::max<int64_t>(K, 1)), own_off((size_t)N + 1, 0), own_idx;
+  std::vector<double> tx_x((size_t)std::max<int64_t>(K, 1)), tx_y(tx_x.size()), tx_z(tx_x.size());
+  std::vector<int64_t> tx_dur((size_t)std::max<int64_t>(K, 1));
+  int64_t dur_min = INT64_MAX;
+  for (int64_t k = 0; k < K; k++) {
+    const uint32_t s = sc->tx_phy[k];
+    tx_chan[k] = sc->channel[s];
+    tx_x[k] = sc->x[s], tx_y[k] = sc->y[s], tx_z[k] = sc->z[s];
+    tx_dur[k] = tx_duration_ns(sc->tx_size[k], sc->tx_modclass[k], sc->tx_rate_bps[k], sc->tx_bw_hz[k], sc->tx_preamble[k]);
+    dur_min = std::min(dur_min, tx_dur[k]);
+    if ((uint32_t)k < ktx) {
+      const size_t c = std::lower_bound(chans.begin(), chans.end(), tx_chan[k]) - chans.begin();
+      fcum[k + 1] = fcum[k] + (seen[c] - 1);
+      own_off[s + 1]++;
+    }
+  }
+  for (int64_t j = 0; j < N; j++) own_off[j + 1] += own_off[j];
+  own_idx.resize(std::max<uint32_t>(own_off[N], 1));
+  {
+    std::vector<uint32_t> fill(own_off.begin(), own_off.end() - 1);
+    for (uint32_t k = 0; k < ktx; k++) own_idx[fill[sc->tx_phy[k]]++] = k;
+  }
+  // syncs of one phy are at least one frame apart (a sync needs the phy out of RX and TX), and at most
+  // one per transmission
+  double xmin = 0, xmax = 0, ymin = 0, ymax = 0, zmin = 0, zmax = 0;
+  for (int64_t j = 0; j < N; j++) {
+    if (j == 0 || sc->x[j] < xmin) xmin = sc->x[j];
+    if (j == 0 || sc->x[j] > xmax) xmax = sc->x[j];
+    if (j == 0 || sc->y[j] < ymin) ymin = sc->y[j];
+    if (j == 0 || sc->y[j] > ymax) ymax = sc->y[j];
+    if (j == 0 || sc->z[j] < zmin) zmin = sc->z[j];
+    if (j == 0 || sc->z[j] > zmax) zmax = sc->z[j];
+  }
+  uint64_t per_phy = ktx;
+  if (ktx) {
+    const double diag = sqrt((xmax - xmin) * (xmax - xmin) + (ymax - ymin) * (ymax - ymin) + (zmax - zmin) * (zmax - zmin));
+    const double span = (double)(sc->tx_ts[ktx - 1] - sc->tx_ts[0]) + diag / sc->speed * 1e9 + 2.0;
+    per_phy = std::min<uint64_t>(ktx, (uint64_t)(span / (double)std::max<int64_t>(dur_min, 1)) + 2);
+  }
+  const uint64_t sync_cap = std::max<uint64_t>(per_phy * (uint64_t)N, 1);
+  if ((uint64_t)sc->uid_start + fcum[ktx] + std::min<uint64_t>(sync_cap, fcum[ktx]) > 0xffffffffull)  // syncs <= receives
+    return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: the run would overflow the 32-bit uid counter");
+
+  nsgpu_wifi *h = new nsgpu_wifi();
+  h->n_tx = K;
+  h->stop_ts = sc->stop_ts;
+  h->stop_uid = sc->stop_uid;
+  h->has_stop = has_stop;
+  WifiDev &D = h->D;
+  D.nphy = N;
+  D.ktx = ktx;
+  D.uid_start = sc->uid_start;
+  D.loss = sc->loss;
+  D.speed = sc->speed;
+  D.rx_gain_db = sc->rx_gain_db;
+  D.edW = pow(10.0, sc->ed_threshold_dbm / 10.0) / 1000.0;    // SetEdThreshold (yans-wifi-phy.cc:228-232)
+  D.ccaW = pow(10.0, sc->cca_threshold_dbm / 10.0) / 1000.0;  // SetCcaMode1Threshold (:234-238)
+  D.stop_ts = has_stop ? sc->stop_ts : INF;
+  D.ni_mask = cap - 1;
+  D.sync_cap = sync_cap;
+  int rc = NSGPU_OK;
+#define TRY(x)                    \
+  do {                            \
+    if ((rc = (x)) != NSGPU_OK) { \
+      nsgpu_wifi_destroy(h);      \
+      return rc;                  \
+    }                             \
+  } while (0)
+  TRY(dalloc(h, (double **)&D.x, N, sc->x));
+  TRY(dalloc(h, (double **)&D.y, N, sc->y));
+  TRY(dalloc(h, (double **)&D.z, N, sc->z));
+  TRY(dalloc(h, (uint32_t **)&D.chan, N, sc->channel));
+  TRY(dalloc(h, (uint32_t **)&D.chan_rank, N, rank.data()));
+  TRY(dalloc(h, (uint64_t **)&D.tx_ts, K, sc->tx_ts));
+  TRY(dalloc(h, (uint32_t **)&D.tx_phy, K, sc->tx_phy));
+  TRY(dalloc(h, (uint32_t **)&D.tx_uid, K, sc->tx_uid));
+  TRY(dalloc(h, (uint32_t **)&D.tx_chan, K, tx_chan.data()));
+  TRY(dalloc(h, (int64_t **)&D.tx_dur, K, tx_dur.data()));
+  TRY(dalloc(h, (double **)&D.tx_dbm, K, sc->tx_dbm));
+  TRY(dalloc(h, (double **)&D.tx_x, K, tx_x.data()));
+  TRY(dalloc(h, (double **)&D.tx_y, K, tx_y.data()));
+  TRY(dalloc(h, (double **)&D.tx_z, K, tx_z.data()));
+  TRY(dalloc(h, (uint64_t **)&D.fcum, fcum.size(), fcum.data()));
+  TRY(dalloc(h, (uint32_t **)&D.own_off, own_off.size(), own_off.data()));
+  TRY(dalloc(h, (uint32_t **)&D.own_idx, own_idx.size(), own_idx.data()));
+  TRY(dalloc(h, &D.ni, (size_t)N * cap));
+  TRY(dalloc(h, &D.sync, sync_cap));
+  TRY(dalloc(h, &D.n_sync, 1));
+  TRY(dalloc(h, &D.pc, N));
+  D.rx_log = nullptr;
+  if (rx_log) TRY(dalloc(h, &D.rx_log, std::max<uint64_t>((uint64_t)ktx * (uint64_t)N, 1)));
+  TRY(dalloc(h, &D.acc, A_N));
+  TRY(dalloc(h, &D.err, 1));
+  TRY(dalloc(h, &D.hist, (size_t)ktx + 1));
+  TRY(dalloc(h, &D.off, (size_t)ktx + 2));
+  TRY(dalloc(h, &D.cur, (size_t)ktx + 1));
+  TRY(dalloc(h, &D.bucket, sync_cap));
+  TRY(dalloc(h, &D.base, std::max<uint32_t>(ktx, 1)));
+  TRY(dalloc(h, &D.ends, sync_cap));
+#undef TRY
+  *out = h;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_run(nsgpu_wifi *h, void *stream) {
+  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_wifi_run: null");
+  const WifiDev &D = h->D;
+  hipStream_t s = (hipStream_t)stream;
+  NSGPU_HIP(hipMemsetAsync(D.n_sync, 0, sizeof(unsigned long long), s));
+  NSGPU_HIP(hipMemsetAsync(D.acc, 0, A_N * sizeof(unsigned long long), s));
+  NSGPU_HIP(hipMemsetAsync(D.err, 0, sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(D.hist, 0, ((size_t)D.ktx + 1) * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(D.cur, 0, ((size_t)D.ktx + 1) * sizeof(uint32_t), s));
+  const uint64_t nlog = (uint64_t)D.ktx * (uint64_t)D.nphy;
+  if (D.rx_log && nlog) hipLaunchKernelGGL(k_rx_log_init, dim3(1024), dim3(256), 0, s, D.rx_log, nlog);
+  hipLaunchKernelGGL(k_wifi_phy, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, s, D);
+  hipLaunchKernelGGL(k_sync_hist, dim3(1024), dim3(256), 0, s, D);
+  hipLaunchKernelGGL(k_tx_base, dim3(1), dim3(1024), 0, s, D);
+  hipLaunchKernelGGL(k_sync_place, dim3(1024), dim3(256), 0, s, D);
+  hipLaunchKernelGGL(k_sync_rank, dim3(1024), dim3(256), 0, s, D);
+  if (D.rx_log && nlog) hipLaunchKernelGGL(k_rx_log_keys, dim3(1024), dim3(256), 0, s, D);
+  NSGPU_HIP(hipGetLastError());
+  h->last = s;
+  h->ran = true;
+  return NSGPU_OK;
+}
+
+static int wifi_check(nsgpu_wifi *h, uint64_t *n_sync) {
+  if (!h || !h->ran) return set_error(NSGPU_ESTATE, "nsgpu_wifi: no run yet");
+  NSGPU_HIP(hipStreamSynchronize(h->last));
+  uint32_t err = 0;
+  unsigned long long ns = 0;
+  NSGPU_HIP(hipMemcpy(&err, h->D.err, sizeof(err), hipMemcpyDeviceToHost));
+  NSGPU_HIP(hipMemcpy(&ns, h->D.n_sync, sizeof(ns), hipMemcpyDeviceToHost));
+  if (err & ERR_TX_IN_TX) return set_error(NSGPU_ESTATE, "nsgpu_wifi: SendPacket while in TX (the reference's NS_FATAL_ERROR)");
+  if (err & ERR_NICAP) return set_error(NSGPU_ENOMEM, "nsgpu_wifi: a NiChanges list outgrew ni_cap %u", h->D.ni_mask + 1);
+  if (err & ERR_WINDOW) return set_error(NSGPU_ENOMEM, "nsgpu_wifi: more than 64 transmissions inside one arrival spread");
+  if (err & ERR_PENDING) return set_error(NSGPU_ENOMEM, "nsgpu_wifi: more than %d pending EndReceive events on a phy", PE_CAP);
+  if ((err & ERR_SYNCCAP) || ns > h->D.sync_cap) return set_error(NSGPU_ENOMEM, "nsgpu_wifi: sync capacity");
+  if (n_sync) *n_sync = ns;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_get_stats(nsgpu_wifi *h, nsgpu_wifi_stats *out) {
+  uint64_t ns = 0;
+  int rc = wifi_check(h, &ns);
+  if (rc != NSGPU_OK) return rc;
+  if (!out) return set_error(NSGPU_EINVAL, "nsgpu_wifi_get_stats: null");
+  unsigned long long a[A_N];
+  NSGPU_HIP(hipMemcpy(a, h->D.acc, sizeof(a), hipMemcpyDeviceToHost));
+  const WifiDev &D = h->D;
+  uint64_t fk = 0;
+  NSGPU_HIP(hipMemcpy(&fk, D.fcum + D.ktx, sizeof(fk), hipMemcpyDeviceToHost));
+  nsgpu_wifi_stats st = {};
+  st.tx = D.ktx;
+  st.rx = a[A_RX];
+  st.sync = a[A_SYNC];
+  st.drop_rx = a[A_DROP_RX];
+  st.drop_tx = a[A_DROP_TX];
+  st.drop_ed = a[A_DROP_ED];
+  st.cca_evals = a[A_CCA_EVAL];
+  st.cca_switches = a[A_CCA_SWITCH];
+  st.end = a[A_END];
+  st.end_cancelled = a[A_END_CANCELLED];
+  st.ni_inserts = a[A_NI_INSERTS];
+  st.near_threshold = a[A_NEAR];
+  st.ni_max = (uint32_t)a[A_NI_MAX];
+  st.dispatched = a[A_DISPATCHED] + D.ktx + (h->has_stop ? 1 : 0);
+  st.digest = a[A_DIGEST] + (h->has_stop ? nsgpu_wifi_term(3, h->stop_ts, h->stop_uid, 0, 0) : 0);
+  st.final_ts = h->has_stop ? h->stop_ts : a[A_LAST_TS];
+  st.next_uid = (uint32_t)(D.uid_start + fk + ns);
+  *out = st;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_read_phys(nsgpu_wifi *h, nsgpu_wifi_phy_counters *out) {
+  int rc = wifi_check(h, nullptr);
+  if (rc != NSGPU_OK) return rc;
+  NSGPU_HIP(hipMemcpy(out, h->D.pc, (size_t)h->D.nphy * sizeof(*out), hipMemcpyDeviceToHost));
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_read_tx_base(nsgpu_wifi *h, uint32_t *out) {
+  int rc = wifi_check(h, nullptr);
+  if (rc != NSGPU_OK) return rc;
+  for (int64_t k = 0; k < h->n_tx; k++) out[k] = 0;
+  if (h->D.ktx) NSGPU_HIP(hipMemcpy(out, h->D.base, (size_t)h->D.ktx * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_read_ends(nsgpu_wifi *h, nsgpu_wifi_end_record *out, uint64_t cap, uint64_t *n) {
+  uint64_t ns = 0;
+  int rc = wifi_check(h, &ns);
+  if (rc != NSGPU_OK) return rc;
+  if (n) *n = ns;
+  if (out && ns) {
+    if (ns > cap) return set_error(NSGPU_EINVAL, "nsgpu_wifi_read_ends: %llu records, cap %llu", (unsigned long long)ns, (unsigned long long)cap);
+    NSGPU_HIP(hipMemcpy(out, h->D.ends, ns * sizeof(*out), hipMemcpyDeviceToHost));
+  }
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_read_rx_log(nsgpu_wifi *h, nsgpu_wifi_rx_log *out) {
+  int rc = wifi_check(h, nullptr);
+  if (rc != NSGPU_OK) return rc;
+  if (!h->D.rx_log) return set_error(NSGPU_ESTATE, "nsgpu_wifi_read_rx_log: created without rx_log");
+  const uint64_t nlog = (uint64_t)h->D.ktx * (uint64_t)h->D.nphy;
+  if (nlog) NSGPU_HIP(hipMemcpy(out, h->D.rx_log, nlog * sizeof(*out), hipMemcpyDeviceToHost));
+  for (uint64_t i = nlog; i < (uint64_t)h->n_tx * (uint64_t)h->D.nphy; i++)
+    out[i] = nsgpu_wifi_rx_log{0, 0, NSGPU_WIFI_NOT_RUN, 0, 0, 0};
+  return NSGPU_OK;
+}

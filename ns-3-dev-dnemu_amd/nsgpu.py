@@ -132,6 +132,15 @@ SIGNATURES = {
     "nsgpu_p2p_group_run": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_group_destroy": (C.c_int, [_vp]),
     "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
+    "nsgpu_wifi_tx_duration_ns": (C.c_int, [_u32, _u32, _u64, _u32, _u32, _vp]),
+    "nsgpu_wifi_create": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p)]),
+    "nsgpu_wifi_run": (C.c_int, [_vp, _vp]),
+    "nsgpu_wifi_get_stats": (C.c_int, [_vp, _vp]),
+    "nsgpu_wifi_read_phys": (C.c_int, [_vp, _vp]),
+    "nsgpu_wifi_read_tx_base": (C.c_int, [_vp, _vp]),
+    "nsgpu_wifi_read_ends": (C.c_int, [_vp, _vp, _u64, _vp]),
+    "nsgpu_wifi_read_rx_log": (C.c_int, [_vp, _vp]),
+    "nsgpu_wifi_destroy": (C.c_int, [_vp]),
 }
 
 _lib = None

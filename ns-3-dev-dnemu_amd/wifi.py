@@ -1,0 +1,218 @@
+"""Wi-Fi PHY scenarios for the device receive subset (include/nsgpu_types.h: nsgpu_wifi_scenario).
+
+Host-side plumbing only: the phy list, positions and transmission schedule an ns-3 PHY harness would
+build, and the C-ABI calls (nsgpu_wifi_*).  No simulation logic lives here.
+
+The harness is the shape of src/wifi/test/wifi-test.cc:181-260 scaled up: YansWifiPhy objects on one
+YansWifiChannel (YansWifiChannelHelper::Default: LogDistance exponent 3, reference loss 46.6777 dB at
+1 m, ConstantSpeed 3e8 m/s — src/wifi/helper/yans-wifi-helper.cc:96-102), YansWifiPhy defaults
+(RxGain 1 dB, TxGain 1 dB, TxPowerStart 16.0206 dBm, EnergyDetectionThreshold -96 dBm,
+CcaMode1Threshold -99 dBm — src/wifi/model/yans-wifi-phy.cc:50-126), and every transmission a
+Simulator::Schedule (t, &YansWifiPhy::SendPacket, phy, packet, mode, preamble, 0) made before Run,
+in the order of the schedule builder below (that order fixes their setup uids).
+"""
+import ctypes as C
+
+import numpy as np
+
+import nsgpu
+
+DSSS, OFDM, ERP_OFDM = 0, 1, 2
+PREAMBLE_LONG, PREAMBLE_SHORT = 0, 1
+SYNC, DROP_RX, DROP_TX, DROP_ED, NOT_RUN = 0, 1, 2, 3, 255
+F_CCA_EVAL, F_CCA_SWITCH, F_NEAR_ED, F_NEAR_CCA = 1, 2, 4, 8
+END_CANCELLED, END_DISPATCHED = 1, 2
+NO_STOP = (1 << 64) - 1
+
+# 802.11b DSSS 1 Mbps (WifiPhy::GetDsssRate1Mbps: 22 MHz, wifi-phy.cc:325-336)
+DSSS_1M = (DSSS, 1000000, 22000000)
+# a 1000-B UDP datagram as a broadcast data frame at the PHY: +8 UDP +20 IPv4 +8 LLC/SNAP +24 MAC header +4 FCS
+FRAME_1000B = 1000 + 8 + 20 + 8 + 24 + 4
+
+
+class WifiScenarioStruct(C.Structure):
+    _fields_ = [
+        ("n_phy", C.c_int64), ("x", C.c_void_p), ("y", C.c_void_p), ("z", C.c_void_p),
+        ("channel", C.c_void_p), ("node", C.c_void_p), ("loss", nsgpu.LossChain), ("speed", C.c_double),
+        ("rx_gain_db", C.c_double), ("ed_threshold_dbm", C.c_double), ("cca_threshold_dbm", C.c_double),
+        ("n_tx", C.c_int64), ("tx_ts", C.c_void_p), ("tx_uid", C.c_void_p), ("tx_phy", C.c_void_p),
+        ("tx_size", C.c_void_p), ("tx_dbm", C.c_void_p), ("tx_modclass", C.c_void_p), ("tx_rate_bps", C.c_void_p),
+        ("tx_bw_hz", C.c_void_p), ("tx_preamble", C.c_void_p), ("uid_start", C.c_uint32), ("ni_cap", C.c_uint32),
+        ("stop_ts", C.c_uint64), ("stop_uid", C.c_uint32), ("pad_", C.c_uint32),
+    ]
+
+
+class WifiStats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("dispatched", "tx", "rx", "sync", "drop_rx", "drop_tx", "drop_ed",
+                                          "cca_evals", "cca_switches", "end", "end_cancelled", "ni_inserts",
+                                          "near_threshold", "digest", "final_ts")] + \
+               [("next_uid", C.c_uint32), ("ni_max", C.c_uint32)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+RX_LOG_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("outcome", "u1"), ("flags", "u1"), ("pad_", "<u2"),
+                         ("cca_ns", "<i8")])
+END_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("sync_ts", "<u8"), ("uid", "<u4"), ("phy", "<u4"), ("tx", "<u4"),
+                             ("flags", "<u4")])
+PHY_COUNTERS_DTYPE = np.dtype([(f, "<u4") for f in ("rx", "sync", "drop_rx", "drop_tx", "drop_ed", "cca_switches",
+                                                    "end", "end_cancelled", "ni_len", "ni_max")] +
+                              [("end_tx", "<i8"), ("end_rx", "<i8"), ("end_cca_busy", "<i8"),
+                               ("first_power", "<f8"), ("rxing", "<u4"), ("pad_", "<u4")])
+TX_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("phy", "<u4"), ("size", "<u4"), ("dbm", "<f8"),
+                     ("modclass", "<u4"), ("rate", "<u8"), ("bw", "<u4"), ("preamble", "<u4")])
+
+
+def tx_duration_ns(size, mode=DSSS_1M, preamble=PREAMBLE_LONG):
+    """WifiPhy::CalculateTxDuration through the C-ABI (nsgpu_wifi_tx_duration_ns)."""
+    out = C.c_int64()
+    nsgpu.check(nsgpu.lib().nsgpu_wifi_tx_duration_ns(size, mode[0], mode[1], mode[2], preamble, C.byref(out)))
+    return out.value
+
+
+class Scenario:
+    """Phys (m_phyList order) and a transmission schedule (TX_DTYPE, (ts, uid) order)."""
+
+    def __init__(self, x, y, z, tx, channel=None, node=None, loss=((nsgpu.LOSS_LOG_DISTANCE, 3.0, 1.0, 46.6777),),
+                 speed=300000000.0, rx_gain_db=1.0, ed_threshold_dbm=-96.0, cca_threshold_dbm=-99.0,
+                 uid_start=None, stop_ts=None, stop_uid=None, ni_cap=256):
+        n = len(x)
+        self.x = np.ascontiguousarray(x, np.float64)
+        self.y = np.ascontiguousarray(y, np.float64)
+        self.z = np.ascontiguousarray(z, np.float64)
+        self.channel = np.ascontiguousarray(np.ones(n, np.uint32) if channel is None else channel, np.uint32)
+        self.node = np.ascontiguousarray(np.arange(n, dtype=np.uint32) if node is None else node, np.uint32)
+        self.tx = np.ascontiguousarray(tx, TX_DTYPE)
+        self.loss = loss
+        self.speed, self.rx_gain_db = speed, rx_gain_db
+        self.ed, self.cca = ed_threshold_dbm, cca_threshold_dbm
+        self.uid_start = int(uid_start if uid_start is not None else (self.tx["uid"].max(initial=3) + 2))
+        self.stop_ts = NO_STOP if stop_ts is None else int(stop_ts)
+        self.stop_uid = 0 if stop_uid is None else int(stop_uid)
+        self.ni_cap = ni_cap
+        self._cols = {}
+
+    @property
+    def n_phy(self):
+        return len(self.x)
+
+    def c_struct(self):
+        s = WifiScenarioStruct()
+        s.n_phy = self.n_phy
+        s.x, s.y, s.z = self.x.ctypes.data, self.y.ctypes.data, self.z.ctypes.data
+        s.channel, s.node = self.channel.ctypes.data, self.node.ctypes.data
+        s.loss = nsgpu.loss_chain(*self.loss)
+        s.speed, s.rx_gain_db = self.speed, self.rx_gain_db
+        s.ed_threshold_dbm, s.cca_threshold_dbm = self.ed, self.cca
+        s.n_tx = len(self.tx)
+        for f, col, dt in (("tx_ts", "ts", np.uint64), ("tx_uid", "uid", np.uint32), ("tx_phy", "phy", np.uint32),
+                           ("tx_size", "size", np.uint32), ("tx_dbm", "dbm", np.float64),
+                           ("tx_modclass", "modclass", np.uint32), ("tx_rate_bps", "rate", np.uint64),
+                           ("tx_bw_hz", "bw", np.uint32), ("tx_preamble", "preamble", np.uint32)):
+            a = np.ascontiguousarray(self.tx[col], dt)
+            self._cols[f] = a  # keep alive with the struct
+            setattr(s, f, a.ctypes.data)
+        s.uid_start, s.ni_cap = self.uid_start, self.ni_cap
+        s.stop_ts, s.stop_uid = self.stop_ts, self.stop_uid
+        return s
+
+
+def grid(n_side, spacing=100.0):
+    """GridPositionAllocator, row first (grid-position-allocator: x = i % width, y = i / width), z = 0."""
+    i = np.arange(n_side * n_side)
+    return ((i % n_side) * spacing).astype(np.float64), ((i // n_side) * spacing).astype(np.float64), \
+        np.zeros(n_side * n_side, np.float64)
+
+
+def periodic_broadcast(n_phy, period_s=1.0, start_s=0.0, stop_s=2.0, size=FRAME_1000B, mode=DSSS_1M,
+                       preamble=PREAMBLE_LONG, tx_dbm=16.0206 + 1.0, seed=1, senders=None, first_uid=4):
+    """Every sender (default: every phy) transmits once per period from a seeded random phase
+    (ns resolution).  The harness schedules them sender by sender, period by period, so the setup uids
+    are first_uid, first_uid + 1, ... in that order; the schedule comes back in (ts, uid) order.
+    Returns (tx, next free uid)."""
+    rng = np.random.default_rng(seed)
+    senders = np.arange(n_phy) if senders is None else np.asarray(senders)
+    period = int(round(period_s * 1e9))
+    phase = rng.integers(0, period, len(senders))
+    rows = []
+    for s, ph in zip(senders, phase):
+        t = int(round(start_s * 1e9)) + int(ph)
+        while t < int(round(stop_s * 1e9)):
+            rows.append((t, int(s)))
+            t += period
+    tx = np.zeros(len(rows), TX_DTYPE)
+    if rows:
+        r = np.array(rows, dtype=np.int64)
+        tx["ts"], tx["phy"] = r[:, 0], r[:, 1]
+    tx["uid"] = first_uid + np.arange(len(rows))
+    tx["size"], tx["dbm"] = size, tx_dbm
+    tx["modclass"], tx["rate"], tx["bw"], tx["preamble"] = mode[0], mode[1], mode[2], preamble
+    tx = np.sort(tx, order=["ts", "uid"])
+    return tx, first_uid + len(rows)
+
+
+def wifi_grid(n_side=100, spacing=100.0, period_s=1.0, stop_s=2.0, size=FRAME_1000B, seed=1, ni_cap=512):
+    """Config 3's PHY workload: n_side x n_side phys, every phy broadcasting once per period, Stop at stop_s."""
+    x, y, z = grid(n_side, spacing)
+    tx, nxt = periodic_broadcast(len(x), period_s=period_s, stop_s=stop_s, size=size, seed=seed)
+    return Scenario(x, y, z, tx, uid_start=nxt + 1, stop_ts=int(round(stop_s * 1e9)), stop_uid=nxt, ni_cap=ni_cap)
+
+
+class Engine:
+    """The device receive subset for one scenario (nsgpu_wifi_create / run / readers)."""
+
+    def __init__(self, scenario, rx_log=False, stream=None):
+        self.sc = scenario
+        self.s = scenario.c_struct()
+        self.stream = stream
+        self.rx_log = rx_log
+        h = C.c_void_p()
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_create(C.byref(self.s), int(rx_log), C.byref(h)))
+        self.h = h.value
+
+    def launch(self):
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_run(self.h, self.stream))
+
+    def run(self):
+        self.launch()
+        return self.stats()
+
+    def stats(self):
+        st = WifiStats()
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_get_stats(self.h, C.byref(st)))
+        return st
+
+    def phys(self):
+        out = np.zeros(self.sc.n_phy, PHY_COUNTERS_DTYPE)
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_read_phys(self.h, out.ctypes.data))
+        return out
+
+    def tx_base(self):
+        out = np.zeros(len(self.sc.tx), np.uint32)
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_read_tx_base(self.h, out.ctypes.data))
+        return out
+
+    def ends(self):
+        """EndReceive records in uid order."""
+        n = C.c_uint64()
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_read_ends(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, END_RECORD_DTYPE)
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_read_ends(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return np.sort(out, order="uid")
+
+    def rx_log_read(self):
+        out = np.zeros(len(self.sc.tx) * self.sc.n_phy, RX_LOG_DTYPE)
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_read_rx_log(self.h, out.ctypes.data))
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            nsgpu.lib().nsgpu_wifi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

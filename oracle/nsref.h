@@ -136,6 +136,17 @@ int nsref_p2p_run_probe(const nsgpu_p2p_scenario *sc, int64_t t0, int64_t period
 /* bench-simulator ReadDistribution: (uint64_t)(data * 1000000000)  (bench-simulator.cc:66) */
 uint64_t nsref_distribution_ns(double seconds);
 
+/* ---------------- Wi-Fi PHY receive subset (nsref_wifi.cc) ----------------
+ * WifiPhy::CalculateTxDuration (wifi-phy.cc:141-296) in ns, and a sequential run of a
+ * nsgpu_wifi_scenario (SendPacket / YansWifiChannel::Send / StartReceivePacket / InterferenceHelper /
+ * WifiPhyStateHelper / EndReceive's state part).  Any output pointer may be NULL.  rx_log has
+ * n_tx * n_phy slots.  Returns 0, -1 (SendPacket while in TX: the reference's NS_FATAL_ERROR) or
+ * -2 (more EndReceive records than ends_cap; *n_ends still holds the count). */
+int64_t nsref_wifi_tx_duration(uint32_t size, uint32_t modclass, uint64_t rate_bps, uint32_t bw_hz, uint32_t preamble);
+int nsref_wifi_run(const nsgpu_wifi_scenario *sc, nsgpu_wifi_stats *stats, nsgpu_wifi_phy_counters *phys,
+                   uint32_t *tx_base, nsgpu_wifi_end_record *ends, uint64_t ends_cap, uint64_t *n_ends,
+                   nsgpu_wifi_rx_log *rx_log);
+
 #ifdef __cplusplus
 }
 #endif

@@ -402,3 +402,35 @@ def p2p_run_probe(scenario_struct, stats_struct, devc, appc, t0, period, count, 
     tr = np.zeros(n.value, TRACE_RECORD_DTYPE)
     lib().nsref_p2p_run_probe(*args, tr.ctypes.data, n.value, C.byref(n))
     return (lts, luid, lctx), tr, samples
+
+
+def wifi_tx_duration(size, modclass, rate_bps, bw_hz, preamble):
+    """WifiPhy::CalculateTxDuration restated (ns)."""
+    f = lib().nsref_wifi_tx_duration
+    f.restype = C.c_int64
+    f.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
+    return f(size, modclass, rate_bps, bw_hz, preamble)
+
+
+def wifi_run(scenario_struct, stats_struct, phys, tx_base, end_dtype, rx_log=None):
+    """Sequential oracle run of a nsgpu_wifi_scenario (ctypes struct built by the caller).
+
+    phys (n_phy counters), tx_base (n_tx uint32) and rx_log (n_tx * n_phy, or None) are numpy arrays
+    filled in place; returns (run_seconds, EndReceive records as `end_dtype`, in uid order)."""
+    import time
+    f = lib().nsref_wifi_run
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p, C.c_void_p]
+    n = C.c_uint64()
+    t0 = time.perf_counter()
+    rc = f(C.byref(scenario_struct), C.byref(stats_struct), phys.ctypes.data, tx_base.ctypes.data, None, 0,
+           C.byref(n), rx_log.ctypes.data if rx_log is not None else None)
+    secs = time.perf_counter() - t0
+    if rc != 0:
+        raise RuntimeError(f"nsref_wifi_run: {rc}")
+    ends = np.zeros(n.value, end_dtype)
+    rc = f(C.byref(scenario_struct), C.byref(stats_struct), phys.ctypes.data, tx_base.ctypes.data,
+           ends.ctypes.data, n.value, C.byref(n), rx_log.ctypes.data if rx_log is not None else None)
+    if rc != 0:
+        raise RuntimeError(f"nsref_wifi_run: {rc}")
+    return secs, np.sort(ends, order="uid")

@@ -1,0 +1,125 @@
+"""Wi-Fi PHY receive subset on the GPU (nsgpu_wifi_*) against the CPU oracle (oracle/nsref_wifi.cc).
+
+Equal: every Receive's key (ts, uid), outcome (sync / drop in RX / drop in TX / below ED), CCA evaluation
+and CCA-busy duration, every EndReceive's key and cancel flag, every fan-out's uid base, per-phy
+counters and final state times, NiChange counts, and the run totals (dispatch count, digest, next uid).
+Received power is computed with ROCm's pow/log10 (about 1 ulp from glibc: within 1e-9 relative,
+north_star): m_firstPower is compared within that tolerance, and decisions within 1e-9 of a threshold
+are flagged (near_threshold) — the tests require that none of them differ."""
+import os
+
+import numpy as np
+import pytest
+
+import nsgpu
+import nsref
+import wifi
+from test_wifi_oracle import random_scenario, run_oracle, tie_scenario
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN_SCHEDULE = os.path.join(os.path.dirname(__file__), "golden", "wifi_grid100_schedule.csv")
+
+
+def grid100_committed():
+    """10,000 phys on the 100 x 100 grid (100 m, YansWifiChannelHelper::Default's LogDistance) and the
+    committed 300-frame schedule (scripts/make_wifi_schedule.py)."""
+    rows = np.loadtxt(GOLDEN_SCHEDULE, delimiter=",", skiprows=1, dtype=np.int64)
+    x, y, z = wifi.grid(100, 100.0)
+    tx = np.zeros(len(rows), wifi.TX_DTYPE)
+    tx["ts"], tx["phy"], tx["uid"] = rows[:, 0], rows[:, 1], 4 + np.arange(len(rows))
+    tx["size"], tx["dbm"] = wifi.FRAME_1000B, 16.0206 + 1.0
+    tx["modclass"], tx["rate"], tx["bw"], tx["preamble"] = wifi.DSSS, 1000000, 22000000, wifi.PREAMBLE_LONG
+    n = len(rows)
+    return wifi.Scenario(x, y, z, tx, uid_start=5 + n, stop_ts=80_000_000, stop_uid=4 + n, ni_cap=512)
+
+
+def compare(sc, rx_log=True):
+    st, phys, base, ends, log = run_oracle(sc, rx_log=rx_log)
+    eng = wifi.Engine(sc, rx_log=rx_log)
+    g = eng.run()
+    gd, od = g.as_dict(), st.as_dict()
+    assert g.near_threshold == 0 and st.near_threshold == 0
+    assert gd == od, {k: (gd[k], od[k]) for k in gd if gd[k] != od[k]}
+    assert np.array_equal(eng.tx_base(), base)
+    ge = eng.ends()
+    assert len(ge) == len(ends)
+    assert np.array_equal(ge, ends)
+    gp = eng.phys()
+    for f in wifi.PHY_COUNTERS_DTYPE.names:
+        if f == "first_power":
+            np.testing.assert_allclose(gp[f], phys[f], rtol=1e-9, atol=1e-24)
+        else:
+            assert np.array_equal(gp[f], phys[f]), f
+    if rx_log:
+        gl = eng.rx_log_read()
+        for f in ("ts", "uid", "outcome", "flags", "cca_ns"):
+            assert np.array_equal(gl[f], log[f]), (f, np.nonzero(gl[f] != log[f])[0][:10])
+    eng.close()
+    return st
+
+
+def test_micro_scenarios():
+    from test_wifi_oracle import line, one_tx
+    x, y, z = line([0.0, 50.0, 100.0])
+    tx = np.concatenate([one_tx(0, 1, 4), one_tx(0, 2, 5), one_tx(9_000_000, 0, 6)])
+    compare(wifi.Scenario(x, y, z, tx, uid_start=8, stop_ts=10 ** 9, stop_uid=7))
+    x, y, z = line([0.0, 100.0])
+    tx = np.concatenate([one_tx(0, 0, 4), one_tx(1_000_000, 1, 5)])
+    st = compare(wifi.Scenario(x, y, z, tx, uid_start=7, stop_ts=10 ** 9, stop_uid=6))
+    assert st.end_cancelled == 1
+
+
+@pytest.mark.parametrize("seed,channels", [(1, (1,)), (2, (1,)), (3, (1, 6)), (4, (1, 6, 11)), (5, (1,)), ("ties", None)])
+def test_small_scenarios_match_oracle(seed, channels):
+    sc = tie_scenario() if seed == "ties" else random_scenario(seed, channels=channels)
+    compare(sc)
+
+
+def test_no_stop_event_and_empty_schedule():
+    sc = random_scenario(7)
+    sc.stop_ts = wifi.NO_STOP
+    compare(sc)
+    x, y, z = wifi.grid(3)
+    compare(wifi.Scenario(x, y, z, np.zeros(0, wifi.TX_DTYPE), uid_start=4))
+
+
+def test_grid_100x100_committed_schedule():
+    """Config 3's grid (10,000 phys, LogDistance default) with the committed 300-frame schedule: 3 M
+    Receive events, every one compared."""
+    st = compare(grid100_committed())
+    assert st.rx == 300 * 9999
+    assert st.sync > 1000 and st.drop_rx > 10000 and st.drop_tx > 1000 and st.cca_switches > 10000
+    assert st.end_cancelled > 0
+
+
+def test_wifi_grid_bench_config_prefix():
+    """The bench workload (wifi.wifi_grid: every phy broadcasting once a second) cut at 0.15 s simulated:
+    ~15 M events, totals / per-phy state / EndReceive records compared (no per-Receive log)."""
+    sc = wifi.wifi_grid(n_side=100, stop_s=0.15)
+    st = compare(sc, rx_log=False)
+    assert st.dispatched > 10_000_000
+
+
+def test_capacity_overflow_fails_loudly():
+    sc = grid100_committed()
+    sc.ni_cap = 8
+    eng = wifi.Engine(sc)
+    eng.launch()
+    with pytest.raises(nsgpu.NsgpuError, match="ni_cap"):
+        eng.stats()
+    eng.close()
+
+
+def test_send_while_transmitting_is_fatal_like_the_reference():
+    from test_wifi_oracle import line, one_tx
+    x, y, z = line([0.0, 100.0])
+    tx = np.concatenate([one_tx(0, 0, 4), one_tx(1000, 0, 5)])
+    sc = wifi.Scenario(x, y, z, tx, uid_start=7, stop_ts=10 ** 9, stop_uid=6)
+    with pytest.raises(RuntimeError):
+        run_oracle(sc)
+    eng = wifi.Engine(sc)
+    eng.launch()
+    with pytest.raises(nsgpu.NsgpuError, match="TX"):
+        eng.stats()
+    eng.close()
