@@ -10,8 +10,10 @@ Workloads (--workload):
       one full simulation from the post-setup state.
   dumbbell: config 5 — src/mpi/examples/simple-distributed.cc with 2 x 499,999 leaves (1,000,000 nodes)
       on one GPU, whole simulation per step.
-  wifi-fanout: config 3's YansWifiChannel::Send receiver loop at 10,000 nodes, batched (receiver
-      events/s; a measurement of the fan-out kernel, not the default line).
+  wifi-grid: config 3 — 10,000 YansWifiPhys on a 100 x 100 grid, every phy broadcasting once a second,
+      2 s: the whole SendPacket / Receive / EndReceive event chain on the device (nsgpu_wifi_run).
+  wifi-fanout: config 3's YansWifiChannel::Send receiver loop alone at 10,000 nodes, batched (receiver
+      events/s; a measurement of the fan-out kernel).
   churn: config 1, utils/bench-simulator.cc — 10,000 pending, U[0,1) s delays, 5e6 holds,
       GPU-resident Bench::Cb (nsgpu_hold_run).
 
@@ -311,7 +313,67 @@ class WifiFanout:
             f"rxPowerDbm within 1e-9 relative)")
 
 
-WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid, "dumbbell": P2PDumbbell, "wifi-fanout": WifiFanout}
+class WifiGrid:
+    """Config 3: wifi-simple-adhoc-grid scaled to 10,000 nodes as a PHY harness (wifi.wifi_grid): 100 x 100
+    phys, 100 m, one channel, YansWifiChannelHelper::Default (LogDistance 3 / 46.6777 dB, ConstantSpeed),
+    YansWifiPhy defaults (16.0206 dBm + 1 dB TxGain, RxGain 1 dB, ED -96 dBm, CCA -99 dBm), every phy
+    broadcasting a 1000-B UDP datagram (1064-B frame, DSSS 1 Mb/s, long preamble) once a second from a
+    seeded random phase, Stop at --wifi-stop s.  One step = the whole run: every SendPacket, Receive
+    (StartReceivePacket + InterferenceHelper + state machine) and EndReceive event (nsgpu_wifi_run).
+    Bytes per event: the fan-out's 64 B per receiver; the dominant kernel is the per-phy
+    kernel k_wifi_phy, one launch per step."""
+    bytes_per_event = 64
+    kernel = "nsgpu::k_wifi_phy"
+
+    def __init__(self, args, stream):
+        import wifi
+        self.wifi = wifi
+        self.side, self.stop = args.wifi_side, args.wifi_stop
+        self.scenario = wifi.wifi_grid(n_side=self.side, stop_s=self.stop)
+        self.engine = wifi.Engine(self.scenario, stream=stream)
+        self.workload = (f"wifi-simple-adhoc-grid scaled to {self.side * self.side} nodes (config 3) as a YansWifiPhy "
+                         f"harness: {self.side}x{self.side} grid 100 m, LogDistance(3, 46.6777)+ConstantSpeed, every phy "
+                         f"broadcasting 1064-B DSSS 1Mb/s frames once a second (seeded phases), {len(self.scenario.tx)} "
+                         f"SendPacket calls, Stop {self.stop}s; whole run on the GPU")
+
+    def step(self):
+        self.engine.launch()
+
+    def roofline(self, step_kernel_ms, events_per_step):
+        prof = self.engine.profile()
+        return {"kernel": self.kernel, "kernel_ms": prof["k_wifi_phy"], "events_per_launch": events_per_step,
+                "step_device_ms": step_kernel_ms, "kernels_ms": prof}
+
+    def result(self):
+        st = self.engine.stats()
+        return int(st.dispatched), int(st.digest), {
+            "receive_events": int(st.rx), "syncs": int(st.sync), "cca_busy_switches": int(st.cca_switches),
+            "end_receive_cancelled": int(st.end_cancelled), "ni_max": int(st.ni_max),
+            "near_threshold": int(st.near_threshold)}
+
+    def cpu_baseline(self):
+        import numpy as np
+        nsref = oracle()
+        wifi = self.wifi
+        sample_stop = min(self.stop, 0.1)
+        sc = wifi.wifi_grid(n_side=self.side, stop_s=sample_stop)
+        st = wifi.WifiStats()
+        secs, _ = nsref.wifi_run(sc.c_struct(), st, np.zeros(sc.n_phy, wifi.PHY_COUNTERS_DTYPE),
+                                 np.zeros(len(sc.tx), np.uint32), wifi.END_RECORD_DTYPE)
+        eng = wifi.Engine(sc, stream=self.engine.stream)
+        g = eng.run()
+        eng.close()
+        # digest_match compares the sample run (GPU vs oracle); the full run is the GPU's alone
+        self._sample_match = g.digest == st.digest and g.dispatched == st.dispatched
+        return st.dispatched / secs, "sample", (
+            f"the same workload cut at Stop {sample_stop}s ({st.dispatched} dispatches, {len(sc.tx)} SendPacket) "
+            f"through the oracle's sequential restatement (DefaultSimulatorImpl order + YansWifiChannel::Send + "
+            f"StartReceivePacket/InterferenceHelper/WifiPhyStateHelper, g++ -O2, one core, the first of its two "
+            f"passes timed: {secs:.2f} s); digest_match = that sample's GPU run has the oracle's digest and count")
+
+
+WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid, "dumbbell": P2PDumbbell, "wifi-fanout": WifiFanout,
+             "wifi-grid": WifiGrid}
 
 
 def main():
@@ -324,6 +386,8 @@ def main():
     ap.add_argument("--holds", type=int, default=5_000_000)
     ap.add_argument("--dumbbell-leaves", type=int, default=499_999, help="dumbbell: leaves per side")
     ap.add_argument("--fanout-tx", type=int, default=1024, help="wifi-fanout: transmissions per step")
+    ap.add_argument("--wifi-side", type=int, default=100, help="wifi-grid: phys per grid side")
+    ap.add_argument("--wifi-stop", type=float, default=2.0, help="wifi-grid: Simulator::Stop (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--partitioned", action="store_true",
                     help="p2p-grid through the partitioned engine even on one rank (RCCL with one rank)")
@@ -424,7 +488,8 @@ def main():
         if not args.no_cpu_baseline and world == 1 and not partitioned:
             cv, cdigest, sample = wl.cpu_baseline()
             out["cpu_baseline"] = {"value": cv, "unit": "events/s", "cores": 1, "kind": "port", "sample": sample,
-                                   "cpu_model": cpu_model(), "digest_match": bool(cdigest == digest)}
+                                   "cpu_model": cpu_model(),
+                                   "digest_match": bool(getattr(wl, "_sample_match", cdigest == digest))}
             out["speedup_vs_cpu"] = value / cv
         print(json.dumps(out), flush=True)
 

@@ -122,6 +122,10 @@ int nsgpu_wifi_read_tx_base(nsgpu_wifi *h, uint32_t *out);               /* n_tx
 int nsgpu_wifi_read_ends(nsgpu_wifi *h, nsgpu_wifi_end_record *out, uint64_t cap, uint64_t *n);  /* unordered */
 int nsgpu_wifi_read_rx_log(nsgpu_wifi *h, nsgpu_wifi_rx_log *out);        /* n_tx * n_phy */
 int nsgpu_wifi_destroy(nsgpu_wifi *h);
+/* Diagnostics: the kernels of one run and a run with each bracketed by HIP events (ms[k], k < count). */
+int nsgpu_wifi_kernel_count(int *n);
+const char *nsgpu_wifi_kernel_name(int k);
+int nsgpu_wifi_profile(nsgpu_wifi *h, void *stream, double *ms);
 
 /* ---------------- GPU-resident bench-simulator churn (config 1) ----------------
  * Runs utils/bench-simulator.cc's RunBench + Simulator::Run (bench-simulator.cc:79-127) over

@@ -65,6 +65,15 @@ struct SyncRec {  // one syncing Receive, i.e. one EndReceive
   uint32_t pad_;
 };
 
+struct TxDesc {  // one transmission, packed for the per-phy scan (64 B: four 16-B loads)
+  double x, y, z;  // the sender's position
+  double dbm;      // txPowerDbm
+  uint64_t ts;
+  int64_t dur;     // CalculateTxDuration
+  uint32_t phy, chan;
+  uint32_t pad_[2];
+};
+
 struct WifiDev {
   int64_t nphy;
   uint32_t ktx;  // dispatched transmissions: those with a key below the Stop event's
@@ -78,6 +87,7 @@ struct WifiDev {
   const uint32_t *tx_phy, *tx_chan, *tx_uid;
   const int64_t *tx_dur;
   const double *tx_dbm, *tx_x, *tx_y, *tx_z;
+  const TxDesc *txd;
   const uint64_t *fcum;  // [ktx + 1] fan-out uids of transmissions [0, k)
   const uint32_t *own_off, *own_idx;
   uint32_t ni_mask;
@@ -120,6 +130,28 @@ __global__ void k_rx_log_init(nsgpu_wifi_rx_log *log, uint64_t n) {
     log[i] = nsgpu_wifi_rx_log{0, 0, NSGPU_WIFI_NOT_RUN, 0, 0, 0};
 }
 
+constexpr int NB = 8;  // ring entries loaded per batch (independent loads, one latency)
+
+// Advances the prefix cursor over the ring entries [cur_n, len) with t < lim (fold: t <= lim).  The cursor
+// caches m_firstPower + d_0 + ... + d_{cur_n - 1}, summed in list order exactly like the reference's loops
+// (AppendEvent's fold, GetEnergyDuration's walk).  Entries under the cursor are in the past, so no
+// insertion (always at upper_bound (t >= now)) lands before it.
+template <bool LE>
+__device__ __forceinline__ void cursor_advance(const NiEnt *ring, uint32_t head, uint32_t len, uint32_t m,
+                                               int64_t lim, uint32_t &cur_n, double &cur_s) {
+  while (cur_n < len) {
+    NiEnt e[NB];
+#pragma unroll
+    for (int u = 0; u < NB; u++) e[u] = ring[(head + cur_n + u) & m];
+#pragma unroll
+    for (int u = 0; u < NB; u++) {
+      if (cur_n >= len || (LE ? e[u].t > lim : e[u].t >= lim)) return;
+      cur_s += e[u].d;
+      cur_n++;
+    }
+  }
+}
+
 // One lane = one phy: its SendPacket / Receive / EndReceive sequence in (ts, uid) order.
 __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -132,6 +164,8 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
   // the two m_rxing flags are set and cleared together (yans-wifi-phy.cc:466-468, :510-514, :776-797)
   uint32_t head = 0, len = 0, ni_max = 0;
   double firstPower = 0.0;
+  uint32_t cur_n = 0;      // prefix cursor: entries [0, cur_n) summed into cur_s
+  double cur_s = 0.0;
   bool rxing = false;
   int64_t endTx = 0, endRx = 0, endCca = 0;
   // pending EndReceive events
@@ -144,10 +178,13 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
   uint64_t done = 0;
   uint32_t oc = D.own_off[j];
   const uint32_t oe = D.own_off[j + 1];
+  uint32_t ok = oc < oe ? D.own_idx[oc] : NONE;
+  uint64_t ok_ts = ok != NONE ? D.txd[ok].ts : INF;
   bool have_c = false;
-  uint64_t c_ts = INF;
+  uint64_t c_ts = INF, c_tts = 0;
   uint32_t c_k = NONE;
-  double c_dist = 0.0;
+  double c_dist = 0.0, c_dbm = 0.0;
+  int64_t c_dur = 0;
   uint32_t err = 0;
   nsgpu_wifi_phy_counters c = {};
   uint64_t digest = 0, disp = 0, last_ts = 0, ni_ins = 0, cca_eval = 0, near = 0;
@@ -160,25 +197,26 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
       for (; i < 64; i++) {
         const uint32_t k = p + i;
         if (k >= D.ktx) break;
-        if (D.tx_ts[k] >= c_ts) break;  // its arrival (and every later one) comes after c_ts
+        const TxDesc t = D.txd[k];
+        if (t.ts >= c_ts) break;  // its arrival (and every later one) comes after c_ts
         if ((done >> i) & 1ull) continue;
-        if (D.tx_phy[k] == (uint32_t)j) continue;  // our own SendPacket: taken in order below
-        if (D.tx_chan[k] != ch) {                   // not on our channel: no Receive (:88-91)
+        if (t.phy == (uint32_t)j) continue;  // our own SendPacket: taken in order below
+        if (t.chan != ch) {                  // not on our channel: no Receive (yans-wifi-channel.cc:88-91)
           done |= 1ull << i;
           continue;
         }
-        double dist;
-        const uint64_t a = arrival(D, k, px, py, pz, dist);
-        if (a < c_ts) c_ts = a, c_k = k, c_dist = dist;
+        // GetDistanceFrom (sender, receiver); ConstantSpeedPropagationDelayModel::GetDelay
+        const double dist = distance3(t.x, t.y, t.z, px, py, pz);
+        const uint64_t a = t.ts + (uint64_t)seconds_to_ts(dist / D.speed);
+        if (a < c_ts) c_ts = a, c_k = k, c_dist = dist, c_tts = t.ts, c_dbm = t.dbm, c_dur = t.dur;
       }
-      if (i == 64 && p + 64 < D.ktx && D.tx_ts[p + 64] < c_ts) {
+      if (i == 64 && p + 64 < D.ktx && D.txd[p + 64].ts < c_ts) {
         err |= ERR_WINDOW;
         break;
       }
       while (done & 1ull) done >>= 1, p++;
       have_c = true;
     }
-    const uint32_t ok = oc < oe ? D.own_idx[oc] : NONE;
     int e = -1;
     for (int q = 0; q < npe; q++)
       if (e < 0 || pe_ts[q] < pe_ts[e] ||
@@ -186,10 +224,9 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
         e = q;
     int kind = -1;
     uint64_t now = INF;
-    if (ok != NONE) kind = 0, now = D.tx_ts[ok];
+    if (ok != NONE) kind = 0, now = ok_ts;
     if (c_k != NONE && c_ts < now) kind = 1, now = c_ts;
-    if (e >= 0 && (pe_ts[e] < now || (pe_ts[e] == now && kind == 1 && D.tx_ts[c_k] > pe_sts[e])))
-      kind = 2, now = pe_ts[e];
+    if (e >= 0 && (pe_ts[e] < now || (pe_ts[e] == now && kind == 1 && c_tts > pe_sts[e]))) kind = 2, now = pe_ts[e];
     if (kind < 0) break;
     if (kind != 0 && now >= D.stop_ts) break;  // Stop (a setup uid) runs first; nothing after it does
     const int64_t nw = (int64_t)now;
@@ -205,7 +242,7 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
         rxing = false;
         endRx = nw;
       }
-      endTx = nw + D.tx_dur[ok];
+      endTx = nw + D.txd[ok].dur;
       if (ok - p >= 64) {
         err |= ERR_WINDOW;
         break;
@@ -213,6 +250,8 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
       done |= 1ull << (ok - p);
       while (done & 1ull) done >>= 1, p++;
       oc++;
+      ok = oc < oe ? D.own_idx[oc] : NONE;
+      ok_ts = ok != NONE ? D.txd[ok].ts : INF;
       last_ts = now;
       continue;
     }
@@ -246,20 +285,20 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
 
     // YansWifiChannel::Receive -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496)
     const uint32_t k = c_k;
-    const double rxPowerDbm = calc_rx_power(D.loss, D.tx_dbm[k], c_dist) + D.rx_gain_db;
+    const double rxPowerDbm = calc_rx_power(D.loss, c_dbm, c_dist) + D.rx_gain_db;
     const double rxPowerW = pow(10.0, rxPowerDbm / 10.0) / 1000.0;  // DbmToW (:727-732)
-    const int64_t endNew = nw + D.tx_dur[k];
+    const int64_t endNew = nw + c_dur;
     // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
     if (len + 2 > m + 1) {
       err |= ERR_NICAP;
       break;
     }
-    if (!rxing) {
-      while (len > 0 && ring[head].t <= nw) {  // fold the entries up to upper_bound (now)
-        firstPower += ring[head].d;
-        head = (head + 1) & m;
-        len--;
-      }
+    if (!rxing) {  // fold the entries up to upper_bound (now) into m_firstPower, drop them
+      cursor_advance<true>(ring, head, len, m, nw, cur_n, cur_s);
+      head = (head + cur_n) & m;
+      len -= cur_n;
+      firstPower = cur_s;
+      cur_n = 0;
       head = (head - 1) & m;
       ring[head] = NiEnt{nw, rxPowerW};
       len++;
@@ -304,15 +343,30 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
     int64_t cca = 0;
     if (maybe) {  // maybeCcaBusy (:482-495): InterferenceHelper::GetEnergyDuration (interference-helper.cc:171-190)
       flags |= NSGPU_WIFI_F_CCA_EVAL;
-      double noise = firstPower;
+      // the entries before now only add up (`continue`): the cursor holds their sum
+      cursor_advance<false>(ring, head, len, m, nw, cur_n, cur_s);
+      double noise = cur_s;
       int64_t end = nw;
-      for (uint32_t q = 0; q < len; q++) {
-        const NiEnt en = ring[(head + q) & m];
-        noise += en.d;
-        end = en.t;
-        if (end < nw) continue;
-        if (near_thr(noise, D.ccaW)) flags |= NSGPU_WIFI_F_NEAR_CCA;
-        if (noise < D.ccaW) break;
+      for (uint32_t q = cur_n; q < len; q += NB) {
+        NiEnt en[NB];
+#pragma unroll
+        for (int u = 0; u < NB; u++) en[u] = ring[(head + q + u) & m];
+        bool stop = false;
+#pragma unroll
+        for (int u = 0; u < NB; u++) {
+          if (q + u >= len) {
+            stop = true;
+            break;
+          }
+          noise += en[u].d;
+          end = en[u].t;  // >= now: the cursor stopped at the first entry not before now
+          if (near_thr(noise, D.ccaW)) flags |= NSGPU_WIFI_F_NEAR_CCA;
+          if (noise < D.ccaW) {
+            stop = true;
+            break;
+          }
+        }
+        if (stop) break;
       }
       cca = end > nw ? end - nw : 0;
       if (cca != 0) {  // SwitchMaybeToCcaBusy (wifi-phy-state-helper.cc:404-423)
@@ -660,6 +714,12 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   TRY(dalloc(h, (double **)&D.tx_x, K, tx_x.data()));
   TRY(dalloc(h, (double **)&D.tx_y, K, tx_y.data()));
   TRY(dalloc(h, (double **)&D.tx_z, K, tx_z.data()));
+  {
+    std::vector<TxDesc> txd((size_t)std::max<int64_t>(K, 1));
+    for (int64_t k = 0; k < K; k++)
+      txd[k] = TxDesc{tx_x[k], tx_y[k], tx_z[k], sc->tx_dbm[k], sc->tx_ts[k], tx_dur[k], sc->tx_phy[k], tx_chan[k], {0, 0}};
+    TRY(dalloc(h, (TxDesc **)&D.txd, K, txd.data()));
+  }
   TRY(dalloc(h, (uint64_t **)&D.fcum, fcum.size(), fcum.data()));
   TRY(dalloc(h, (uint32_t **)&D.own_off, own_off.size(), own_off.data()));
   TRY(dalloc(h, (uint32_t **)&D.own_idx, own_idx.size(), own_idx.data()));
@@ -682,10 +742,12 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   return NSGPU_OK;
 }
 
-extern "C" int nsgpu_wifi_run(nsgpu_wifi *h, void *stream) {
-  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_wifi_run: null");
+static const char *const WIFI_KERNELS[] = {"k_wifi_phy", "k_sync_hist", "k_tx_base", "k_sync_place", "k_sync_rank"};
+constexpr int WIFI_NK = 5;
+
+// One whole run on `s`; with `ev` (WIFI_NK + 1 events) each kernel of the chain is bracketed.
+static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
   const WifiDev &D = h->D;
-  hipStream_t s = (hipStream_t)stream;
   NSGPU_HIP(hipMemsetAsync(D.n_sync, 0, sizeof(unsigned long long), s));
   NSGPU_HIP(hipMemsetAsync(D.acc, 0, A_N * sizeof(unsigned long long), s));
   NSGPU_HIP(hipMemsetAsync(D.err, 0, sizeof(uint32_t), s));
@@ -693,16 +755,53 @@ extern "C" int nsgpu_wifi_run(nsgpu_wifi *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(D.cur, 0, ((size_t)D.ktx + 1) * sizeof(uint32_t), s));
   const uint64_t nlog = (uint64_t)D.ktx * (uint64_t)D.nphy;
   if (D.rx_log && nlog) hipLaunchKernelGGL(k_rx_log_init, dim3(1024), dim3(256), 0, s, D.rx_log, nlog);
+  if (ev) NSGPU_HIP(hipEventRecord(ev[0], s));
   hipLaunchKernelGGL(k_wifi_phy, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, s, D);
+  if (ev) NSGPU_HIP(hipEventRecord(ev[1], s));
   hipLaunchKernelGGL(k_sync_hist, dim3(1024), dim3(256), 0, s, D);
+  if (ev) NSGPU_HIP(hipEventRecord(ev[2], s));
   hipLaunchKernelGGL(k_tx_base, dim3(1), dim3(1024), 0, s, D);
+  if (ev) NSGPU_HIP(hipEventRecord(ev[3], s));
   hipLaunchKernelGGL(k_sync_place, dim3(1024), dim3(256), 0, s, D);
+  if (ev) NSGPU_HIP(hipEventRecord(ev[4], s));
   hipLaunchKernelGGL(k_sync_rank, dim3(1024), dim3(256), 0, s, D);
+  if (ev) NSGPU_HIP(hipEventRecord(ev[5], s));
   if (D.rx_log && nlog) hipLaunchKernelGGL(k_rx_log_keys, dim3(1024), dim3(256), 0, s, D);
   NSGPU_HIP(hipGetLastError());
   h->last = s;
   h->ran = true;
   return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_run(nsgpu_wifi *h, void *stream) {
+  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_wifi_run: null");
+  return wifi_launch(h, (hipStream_t)stream, nullptr);
+}
+
+extern "C" int nsgpu_wifi_kernel_count(int *n) {
+  *n = WIFI_NK;
+  return NSGPU_OK;
+}
+
+extern "C" const char *nsgpu_wifi_kernel_name(int k) { return k >= 0 && k < WIFI_NK ? WIFI_KERNELS[k] : ""; }
+
+// One run with every kernel of the chain bracketed by HIP events on `stream`: ms[k] = kernel k's time.
+extern "C" int nsgpu_wifi_profile(nsgpu_wifi *h, void *stream, double *ms) {
+  if (!h || !ms) return set_error(NSGPU_EINVAL, "nsgpu_wifi_profile: null");
+  hipEvent_t ev[WIFI_NK + 1] = {};
+  int rc = NSGPU_OK;
+  for (auto &e : ev)
+    if (hipEventCreate(&e) != hipSuccess) rc = set_error(NSGPU_EHIP, "nsgpu_wifi_profile: hipEventCreate");
+  if (rc == NSGPU_OK) rc = wifi_launch(h, (hipStream_t)stream, ev);
+  if (rc == NSGPU_OK && hipEventSynchronize(ev[WIFI_NK]) != hipSuccess) rc = set_error(NSGPU_EHIP, "nsgpu_wifi_profile: sync");
+  for (int k = 0; rc == NSGPU_OK && k < WIFI_NK; k++) {
+    float f = 0;
+    if (hipEventElapsedTime(&f, ev[k], ev[k + 1]) != hipSuccess) rc = set_error(NSGPU_EHIP, "nsgpu_wifi_profile: elapsed");
+    ms[k] = f;
+  }
+  for (auto &e : ev)
+    if (e) (void)hipEventDestroy(e);
+  return rc;
 }
 
 static int wifi_check(nsgpu_wifi *h, uint64_t *n_sync) {

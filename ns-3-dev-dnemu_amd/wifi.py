@@ -178,6 +178,14 @@ class Engine:
         self.launch()
         return self.stats()
 
+    def profile(self):
+        """One run with each kernel bracketed by HIP events (nsgpu_wifi_profile): {kernel: ms}."""
+        n = C.c_int()
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_kernel_count(C.byref(n)))
+        ms = np.zeros(n.value, np.float64)
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_profile(self.h, self.stream, ms.ctypes.data))
+        return {nsgpu.lib().nsgpu_wifi_kernel_name(k).decode(): float(ms[k]) for k in range(n.value)}
+
     def stats(self):
         st = WifiStats()
         nsgpu.check(nsgpu.lib().nsgpu_wifi_get_stats(self.h, C.byref(st)))
