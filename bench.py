@@ -87,15 +87,40 @@ class Churn:
         return int(st.dispatched), int(st.digest), {"rounds_per_step": int(st.rounds), "max_batch": int(st.max_batch)}
 
     def cpu_baseline(self):
+        """MapScheduler (the default, SchedulerType = ns3::MapScheduler) on the full run is the baseline value;
+        HeapScheduler on the full run and CalendarScheduler at 50k holds (past ~4.29 s of
+        simulated time the reference's CalendarScheduler crashes, H3 — the full run is attempted and the
+        crash point reported) ride along in `schedulers`."""
         nsref = oracle()
-        best = None
-        for _ in range(3):
-            res, _, _ = nsref.churn_run(self.dist, self.holds, nsref.SCHED_MAP)
-            best = res if best is None or res.run_seconds < best.run_seconds else best
+
+        def best_of(sched, holds, k=3):
+            best = None
+            for _ in range(k):
+                res, _, _ = nsref.churn_run(self.dist, holds, sched)
+                best = res if best is None or res.run_seconds < best.run_seconds else best
+            return best
+
+        best = best_of(nsref.SCHED_MAP, self.holds)
+        heap = best_of(nsref.SCHED_HEAP, self.holds)
+        cal = best_of(nsref.SCHED_CALENDAR, 50_000)
+        try:
+            nsref.churn_run(self.dist, self.holds, nsref.SCHED_CALENDAR)
+            cal_full = "completed"
+        except nsref.CalendarCrash as e:
+            cal_full = (f"crashes (SURVEY H3) after {e.result.dispatched} of {best.dispatched} dispatches, "
+                        f"at {e.result.final_ts} ns")
+        self.schedulers = {
+            "map": {"events_per_s": best.dispatched / best.run_seconds, "dispatches": int(best.dispatched),
+                    "digest_match": True},
+            "heap": {"events_per_s": heap.dispatched / heap.run_seconds, "dispatches": int(heap.dispatched),
+                     "digest_match": heap.digest == best.digest},
+            "calendar_50k_holds": {"events_per_s": cal.dispatched / cal.run_seconds, "dispatches": int(cal.dispatched)},
+            "calendar_full_run": cal_full,
+        }
         return best.dispatched / best.run_seconds, best.digest, (
             f"full config-1 run ({len(self.dist)} pending, {self.holds} holds, {best.dispatched} dispatches), oracle "
             f"restatement of DefaultSimulatorImpl+MapScheduler+Bench::Cb, g++ -O2, best of 3, Simulator::Run only "
-            f"({best.run_seconds:.3f} s)")
+            f"({best.run_seconds:.3f} s); Heap / Calendar in cpu_baseline.schedulers")
 
 
 def cpu_model():
@@ -490,6 +515,8 @@ def main():
             out["cpu_baseline"] = {"value": cv, "unit": "events/s", "cores": 1, "kind": "port", "sample": sample,
                                    "cpu_model": cpu_model(),
                                    "digest_match": bool(getattr(wl, "_sample_match", cdigest == digest))}
+            if getattr(wl, "schedulers", None):
+                out["cpu_baseline"]["schedulers"] = wl.schedulers
             out["speedup_vs_cpu"] = value / cv
         print(json.dumps(out), flush=True)
 

@@ -276,6 +276,17 @@ int nsgpu_p2p_counters(nsgpu_p2p *h, nsgpu_dev_counters *devc, nsgpu_app_counter
  * lib/libnsgpu_prof.so build (-DNSGPU_PHASE_PROF) records them, the product library returns ESTATE. */
 int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset);
 
+/* ---------------- global routing ----------------
+ * Replaces GlobalRouteManager::PopulateRoutingTables (SPFCalculate, global-route-manager-impl.cc:
+ * 1327-1490) + Ipv4GlobalRouting::LookupGlobal (ipv4-global-routing.cc:136-242, RandomEcmpRouting off)
+ * for point-to-point topologies with unit metrics: route_out[node * n_dst + k] (host memory) = the device
+ * through which `node` forwards a datagram to any address of node dst_node[k]; 0xffffffff for the
+ * destination itself and for unreachable nodes.  dev_addr / dev_ifindex: each device's IPv4 address and
+ * interface index (both NULL: the lowest device wins ties).  One GPU BFS per destination. */
+int nsgpu_route_global(uint32_t n_nodes, uint32_t n_devices, const uint32_t *dev_node, const uint32_t *dev_peer,
+                       const uint32_t *dev_addr, const uint32_t *dev_ifindex, uint32_t n_dst, const uint32_t *dst_node,
+                       uint32_t *route_out, void *stream);
+
 /* ---------------- partitioned (multi-GPU) point-to-point runs ----------------
  * Replaces src/mpi's DistributedSimulatorImpl (distributed-simulator-impl.cc:146-326: LBTS by
  * MPI_Allgather of LbtsMessage) and MpiInterface::SendPacket / ReceiveMessages

@@ -58,6 +58,7 @@ SIGNATURES = {
     "nsgpu_stream_create": (C.c_int, [C.POINTER(C.c_void_p)]),
     "nsgpu_stream_destroy": (C.c_int, [_vp]),
     "nsgpu_stream_sync": (C.c_int, [_vp]),
+    "nsgpu_route_global": (C.c_int, [_u32, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     "nsgpu_event_create": (C.c_int, [C.POINTER(C.c_void_p)]),
     "nsgpu_event_destroy": (C.c_int, [_vp]),
     "nsgpu_event_record": (C.c_int, [_vp, _vp]),
@@ -543,3 +544,13 @@ class Sim:
             self.close()
         except Exception:
             pass
+
+
+def route_global(dev_node, dev_peer, dev_addr, dev_ifindex, n_nodes, dst_node, stream=None):
+    """nsgpu_route_global: uint32 [n_nodes, n_dst] next-hop devices (0xffffffff: none / local)."""
+    arrs = [np.ascontiguousarray(a, dtype=np.uint32) for a in (dev_node, dev_peer, dev_addr, dev_ifindex)]
+    dst = np.ascontiguousarray(dst_node, dtype=np.uint32)
+    out = np.zeros((n_nodes, dst.size), np.uint32)
+    check(lib().nsgpu_route_global(n_nodes, arrs[0].size, *[a.ctypes.data for a in arrs], dst.size, dst.ctypes.data,
+                                   out.ctypes.data, stream))
+    return out

@@ -76,6 +76,9 @@ class Scenario:
         self.dst_slot = {}
         # addressing (host side only: the trace codec prints it, the engines never read it)
         self.dev_addr = {}   # device -> IPv4 address (u32) of its interface
+        self.dev_mask = {}   # device -> network mask (u32)
+        self.dev_ifindex = {}  # device -> Ipv4 interface index (loopback 0, then Assign order per node)
+        self._nif = {}
         for _ in range(n_nodes):
             self.add_node()
 
@@ -131,9 +134,14 @@ class Scenario:
                          remote_port=remote_port)
 
     # Ipv4AddressHelper::Assign on the two devices of a link, then NewNetwork (ipv4-address-helper.cc)
-    def assign_link(self, da, db, network):
-        self.dev_addr[da] = network + 1
-        self.dev_addr[db] = network + 2
+    def assign_link(self, da, db, network, mask=0xFFFFFF00):
+        for d, host in ((da, 1), (db, 2)):
+            node = self.dev[d][0]
+            self.dev_addr[d] = network + host
+            self.dev_mask[d] = mask
+            # Ipv4L3Protocol::AddInterface: the loopback is interface 0 (SetupLoopback at Install)
+            self.dev_ifindex[d] = self._nif.get(node, 1)
+            self._nif[node] = self.dev_ifindex[d] + 1
 
     def _slot_nodes(self):
         # route-table columns: every datagram destination (sender apps' dst), and echo clients' own nodes
@@ -152,31 +160,59 @@ class Scenario:
         return nb
 
     def route_bfs(self):
-        """Static next-hop table towards every OnOff destination (BFS shortest paths, lowest device first)."""
+        """Next-hop table towards every datagram destination with ns-3's global-routing choice.
+
+        GlobalRouteManager::PopulateRoutingTables + Ipv4GlobalRouting::LookupGlobal (RandomEcmpRouting
+        off) over point-to-point links with unit metrics pick, for a destination address of node D,
+        the first host route SPFIntraAddRouter installed for D: D's first root exit direction.  An exit
+        list only grows by SPFVertex::MergeRootExitDirections, which sorts it by (next-hop address,
+        outgoing interface) (global-route-manager-impl.cc:314-326); it holds the first hops of every
+        shortest path.  So node R forwards through the device d whose peer lies one hop closer to D and
+        whose (peer address, interface index) is smallest.  CheckForStubNode (:1245-1323) gives a node
+        with a single link a default route through it.  Without addresses (tests that assign none) the
+        lowest device wins.  oracle/nsref_route.cc restates the SPF itself; tests/test_routing_oracle.py
+        checks this table against it, tests/test_gpu_routing.py the GPU builder (nsgpu_route_global)."""
         dsts = self._slot_nodes()
         self.dst_slot = {d: i for i, d in enumerate(dsts)}
         self.n_dst = max(1, len(dsts))
-        nb = self._neighbors()
+        dev = np.array([r[:2] for r in self.dev], dtype=np.int64).reshape(-1, 2)
+        dnode, dpeer = dev[:, 0], dev[:, 1]
+        pnode = dnode[dpeer] if len(dev) else dnode
+        nd = len(dev)
+        has_addr = len(self.dev_addr) == nd and nd > 0
+        if has_addr:
+            tie = (np.array([self.dev_addr[int(p)] for p in dpeer], np.int64) << 32) | \
+                np.array([self.dev_ifindex[d] for d in range(nd)], np.int64)
+        else:
+            tie = np.arange(nd, dtype=np.int64)
+        # CSR of each node's devices (ascending device index)
+        order = np.argsort(dnode, kind="stable")
+        off = np.zeros(self.n_nodes + 1, np.int64)
+        np.add.at(off, dnode + 1, 1)
+        off = np.cumsum(off)
+        ndev = np.diff(off)
         R = np.full((self.n_nodes, self.n_dst), NO_ROUTE, dtype=np.uint32)
         for dst, slot in self.dst_slot.items():
             dist = np.full(self.n_nodes, -1, dtype=np.int64)
             dist[dst] = 0
-            q = deque([dst])
-            while q:
-                u = q.popleft()
-                for v, _d in nb[u]:
-                    if dist[v] < 0:
-                        dist[v] = dist[u] + 1
-                        q.append(v)
-            for n in range(self.n_nodes):
-                if n == dst or dist[n] < 0:
-                    continue
-                best = None
-                for v, d in sorted(nb[n], key=lambda t: t[1]):
-                    if dist[v] == dist[n] - 1:
-                        best = d
-                        break
-                R[n, slot] = best
+            front = np.array([dst], np.int64)
+            lev = 0
+            while front.size:  # level-synchronous BFS over the undirected links
+                lev += 1
+                cnt = ndev[front]
+                idx = np.repeat(off[front], cnt) + (np.arange(cnt.sum()) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+                nb = np.unique(pnode[order[idx]])
+                nb = nb[dist[nb] < 0]
+                dist[nb] = lev
+                front = nb
+            ok = (dist[dnode] > 0) & (dist[pnode] == dist[dnode] - 1)
+            cand = np.where(ok, tie, np.iinfo(np.int64).max)
+            best = np.full(self.n_nodes, np.iinfo(np.int64).max, np.int64)
+            np.minimum.at(best, dnode, cand)
+            win = ok & (cand == best[dnode])
+            R[dnode[win], slot] = np.nonzero(win)[0].astype(np.uint32)
+            stub = (ndev == 1) & (np.arange(self.n_nodes) != dst)
+            R[stub, slot] = order[off[:-1][stub]].astype(np.uint32)
         self.route = R
 
     def next_hop(self, n, slot):
@@ -434,9 +470,11 @@ def random_topology(n_nodes, n_links, n_flows, seed, bps_choices=(1_000_000, 5_0
     while len(edges) < n_links:
         a, b = sorted(rng.choice(n_nodes, 2, replace=False).tolist())
         edges.add((a, b))
-    for a, b in sorted(edges):
-        sc.link(a, b, int(rng.choice(bps_choices)), int(rng.choice(delay_choices)), qmax)
+    links = [sc.link(a, b, int(rng.choice(bps_choices)), int(rng.choice(delay_choices)), qmax)
+             for a, b in sorted(edges)]
     sc.install_stack()
+    for k, (da, db) in enumerate(links):  # Ipv4AddressHelper ("10.1.0.0", "255.255.255.0"), NewNetwork per link
+        sc.assign_link(da, db, ip("10.1.0.0") + (k << 8))
     flows = []
     for _ in range(n_flows):
         s_, d = rng.choice(n_nodes, 2, replace=False).tolist()

@@ -69,7 +69,7 @@ int64_t nsref_fanout_spectrum(const double *x, const double *y, const double *z,
 
 /* ---------------- Sequential engine: DefaultSimulatorImpl + Map/Heap scheduler ----------------
  * (src/core/model/default-simulator-impl.cc:49-353, map-scheduler.cc:51-100, heap-scheduler.cc:44-217) */
-enum { NSREF_SCHED_MAP = 0, NSREF_SCHED_HEAP = 1, NSREF_SCHED_LIST = 2 };
+enum { NSREF_SCHED_MAP = 0, NSREF_SCHED_HEAP = 1, NSREF_SCHED_LIST = 2, NSREF_SCHED_CALENDAR = 3 };
 
 typedef void (*nsref_fn)(void *user, uint64_t arg);
 typedef struct nsref_sim nsref_sim;
@@ -109,6 +109,8 @@ typedef struct nsref_churn_result {
   double   init_seconds; /* wall time of the initial inserts (:83-90) */
 } nsref_churn_result;
 
+/* Returns 0, or -3 when the CalendarScheduler reaches the reference's H3 crash (calendar-scheduler.cc:
+ * 128,157,182-185: every pending event later than 2^32 ns); *out then describes the run up to it. */
 int nsref_churn_run(const uint64_t *dist_ns, uint32_t n, uint32_t total, int scheduler,
                     uint64_t *log_ts, uint32_t *log_uid, uint64_t log_cap, nsref_churn_result *out);
 
@@ -146,6 +148,16 @@ int64_t nsref_wifi_tx_duration(uint32_t size, uint32_t modclass, uint64_t rate_b
 int nsref_wifi_run(const nsgpu_wifi_scenario *sc, nsgpu_wifi_stats *stats, nsgpu_wifi_phy_counters *phys,
                    uint32_t *tx_base, nsgpu_wifi_end_record *ends, uint64_t ends_cap, uint64_t *n_ends,
                    nsgpu_wifi_rx_log *rx_log);
+
+/* ---------------- Global routing (nsref_route.cc) ----------------
+ * GlobalRouteManager::PopulateRoutingTables + Ipv4GlobalRouting::RouteInput/LookupGlobal over a
+ * point-to-point topology: route_out[node * n_dst + k] = the device the node's first matching route
+ * to dst_addr[k] leaves through, 0xfffffffe when the address is the node's own (local delivery),
+ * 0xffffffff when no route matches.  dev_ifindex: the device's Ipv4 interface index (loopback is 0).
+ * Returns 0, or -1 on an inconsistent interface numbering. */
+int nsref_global_routes(uint32_t n_nodes, uint32_t n_devices, const uint32_t *dev_node, const uint32_t *dev_peer,
+                        const uint32_t *dev_addr, const uint32_t *dev_mask, const uint32_t *dev_ifindex,
+                        uint32_t n_dst, const uint32_t *dst_addr, uint32_t *route_out);
 
 #ifdef __cplusplus
 }

@@ -37,7 +37,7 @@ class ChurnResult(C.Structure):
 
 
 LOSS_NONE, LOSS_LOG_DISTANCE, LOSS_FRIIS, LOSS_FIXED_RSS, LOSS_RANGE = 0, 1, 2, 3, 4
-SCHED_MAP, SCHED_HEAP, SCHED_LIST = 0, 1, 2
+SCHED_MAP, SCHED_HEAP, SCHED_LIST, SCHED_CALENDAR = 0, 1, 2, 3
 
 EVENT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)
 
@@ -264,17 +264,25 @@ def load_distribution(path):
     return np.array([lib().nsref_distribution_ns(v) for v in vals], dtype=np.uint64)
 
 
+class CalendarCrash(RuntimeError):
+    """The reference's CalendarScheduler crashes here; .result describes the run up to it."""
+
+    def __init__(self, result):
+        super().__init__(f"CalendarScheduler sentinel reached after {result.dispatched} dispatches (SURVEY H3)")
+        self.result = result
+
+
 def churn_run(dist_ns, total, scheduler=SCHED_MAP, log_cap=0):
     dist_ns = np.ascontiguousarray(dist_ns, dtype=np.uint64)
     res = ChurnResult()
-    if log_cap:
-        lts = np.zeros(log_cap, dtype=np.uint64)
-        luid = np.zeros(log_cap, dtype=np.uint32)
-        lib().nsref_churn_run(dist_ns.ctypes.data, dist_ns.size, total, scheduler, lts.ctypes.data,
-                              luid.ctypes.data, log_cap, C.byref(res))
-        return res, lts, luid
-    lib().nsref_churn_run(dist_ns.ctypes.data, dist_ns.size, total, scheduler, None, None, 0, C.byref(res))
-    return res, None, None
+    lts = np.zeros(log_cap, dtype=np.uint64) if log_cap else None
+    luid = np.zeros(log_cap, dtype=np.uint32) if log_cap else None
+    rc = lib().nsref_churn_run(dist_ns.ctypes.data, dist_ns.size, total, scheduler,
+                               lts.ctypes.data if log_cap else None, luid.ctypes.data if log_cap else None, log_cap,
+                               C.byref(res))
+    if rc == -3:
+        raise CalendarCrash(res)
+    return res, lts, luid
 
 
 class Sim:
@@ -434,3 +442,18 @@ def wifi_run(scenario_struct, stats_struct, phys, tx_base, end_dtype, rx_log=Non
     if rc != 0:
         raise RuntimeError(f"nsref_wifi_run: {rc}")
     return secs, np.sort(ends, order="uid")
+
+
+def global_routes(dev_node, dev_peer, dev_addr, dev_mask, dev_ifindex, n_nodes, dst_addr):
+    """GlobalRouteManager::PopulateRoutingTables + LookupGlobal restated (nsref_route.cc): uint32
+    [n_nodes, n_dst] of output devices (0xfffffffe local delivery, 0xffffffff no route)."""
+    f = lib().nsref_global_routes
+    f.restype = C.c_int
+    f.argtypes = [C.c_uint32, C.c_uint32] + [C.c_void_p] * 5 + [C.c_uint32, C.c_void_p, C.c_void_p]
+    arrs = [np.ascontiguousarray(a, dtype=np.uint32) for a in (dev_node, dev_peer, dev_addr, dev_mask, dev_ifindex)]
+    dst = np.ascontiguousarray(dst_addr, dtype=np.uint32)
+    out = np.zeros((n_nodes, dst.size), np.uint32)
+    rc = f(n_nodes, arrs[0].size, *[a.ctypes.data for a in arrs], dst.size, dst.ctypes.data, out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"nsref_global_routes: {rc}")
+    return out

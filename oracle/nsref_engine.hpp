@@ -171,6 +171,149 @@ struct ListScheduler : Scheduler {  // list-scheduler.cc:50-96: sorted std::list
   }
 };
 
+// CalendarScheduler (calendar-scheduler.cc:45-348): Brown's calendar queue, buckets of sorted lists,
+// resized by doubling/halving with a width sampled from the next events.  SURVEY H3: the "no event
+// within one year" fallback of DoRemoveNext starts from a sentinel whose ts is 0xffffffff (the
+// initializer `{0, {~0u, ~0u}}` puts ~0u in the 64-bit m_ts), so once every pending event is later than
+// 2^32 ns the sentinel wins, an arbitrary (or empty) bucket is popped and the impl-less sentinel is
+// returned: the reference crashes there (free(): invalid pointer / null Invoke).  The restatement throws
+// CalendarCrash at that point instead of reproducing the undefined behaviour.
+struct CalendarCrash {};
+
+struct CalendarScheduler : Scheduler {
+  typedef std::list<Event> Bucket;
+  std::vector<Bucket> m_buckets;
+  uint32_t m_nBuckets = 0;
+  uint64_t m_width = 0, m_lastPrio = 0, m_bucketTop = 0;
+  uint32_t m_lastBucket = 0;
+  uint32_t m_qSize = 0;
+  CalendarScheduler() { Init(2, 1, 0); }
+  void Init(uint32_t nBuckets, uint64_t width, uint64_t startPrio) {  // :57-69
+    m_buckets.assign(nBuckets, Bucket());
+    m_nBuckets = nBuckets;
+    m_width = width;
+    m_lastPrio = startPrio;
+    m_lastBucket = Hash(startPrio);
+    m_bucketTop = (startPrio / width + 1) * width;
+  }
+  uint32_t Hash(uint64_t ts) const { return (uint32_t)((ts / m_width) % m_nBuckets); }  // :81-86
+  void DoInsert(const Event &ev) {  // :88-107: before the first later key of the bucket
+    Bucket &b = m_buckets[Hash(ev.key.ts)];
+    for (auto i = b.begin(); i != b.end(); ++i)
+      if (KeyLess()(ev.key, i->key)) {
+        b.insert(i, ev);
+        return;
+      }
+    b.push_back(ev);
+  }
+  void Insert(const Event &ev) override {  // :109-115
+    DoInsert(ev);
+    m_qSize++;
+    ResizeUp();
+  }
+  bool IsEmpty() const override { return m_qSize == 0; }
+  static Event Sentinel() { return Event{nullptr, {0xffffffffull, 0xffffffffu, 0u}}; }
+  Event PeekNext() const override {  // :121-150
+    uint32_t i = m_lastBucket;
+    uint64_t bucketTop = m_bucketTop;
+    Event minEvent = Sentinel();
+    do {
+      if (!m_buckets[i].empty()) {
+        const Event &next = m_buckets[i].front();
+        if (next.key.ts < bucketTop) return next;
+        if (KeyLess()(next.key, minEvent.key)) minEvent = next;
+      }
+      i++;
+      i %= m_nBuckets;
+      bucketTop += m_width;
+    } while (i != m_lastBucket);
+    if (minEvent.impl == nullptr) throw CalendarCrash();
+    return minEvent;
+  }
+  Event DoRemoveNext() {  // :152-188
+    uint32_t i = m_lastBucket;
+    uint64_t bucketTop = m_bucketTop;
+    Event minEvent = Sentinel();
+    do {
+      if (!m_buckets[i].empty()) {
+        Event next = m_buckets[i].front();
+        if (next.key.ts < bucketTop) {
+          m_lastBucket = i;
+          m_lastPrio = next.key.ts;
+          m_bucketTop = bucketTop;
+          m_buckets[i].pop_front();
+          return next;
+        }
+        if (KeyLess()(next.key, minEvent.key)) minEvent = next;
+      }
+      i++;
+      i %= m_nBuckets;
+      bucketTop += m_width;
+    } while (i != m_lastBucket);
+    if (minEvent.impl == nullptr) throw CalendarCrash();  // H3
+    m_lastPrio = minEvent.key.ts;
+    m_lastBucket = Hash(minEvent.key.ts);
+    m_bucketTop = (minEvent.key.ts / m_width + 1) * m_width;
+    m_buckets[m_lastBucket].pop_front();
+    return minEvent;
+  }
+  Event RemoveNext() override {  // :190-203
+    Event ev = DoRemoveNext();
+    m_qSize--;
+    ResizeDown();
+    return ev;
+  }
+  void Remove(const Event &ev) override {  // :205-226
+    Bucket &b = m_buckets[Hash(ev.key.ts)];
+    for (auto i = b.begin(); i != b.end(); ++i)
+      if (i->key.uid == ev.key.uid) {
+        b.erase(i);
+        m_qSize--;
+        ResizeDown();
+        return;
+      }
+    abort();
+  }
+  void ResizeUp() {  // :228-236
+    if (m_qSize > m_nBuckets * 2 && m_nBuckets < 32768) Resize(m_nBuckets * 2);
+  }
+  void ResizeDown() {  // :237-244
+    if (m_qSize < m_nBuckets / 2) Resize(m_nBuckets / 2);
+  }
+  uint64_t CalculateNewWidth() {  // :246-322 (returned through uint32_t, as the reference does)
+    if (m_qSize < 2) return 1;
+    uint32_t nSamples = m_qSize <= 5 ? m_qSize : 5 + m_qSize / 10;
+    if (nSamples > 25) nSamples = 25;
+    std::vector<Event> samples;
+    const uint32_t lastBucket = m_lastBucket;
+    const uint64_t bucketTop = m_bucketTop, lastPrio = m_lastPrio;
+    for (uint32_t i = 0; i < nSamples; i++) samples.push_back(DoRemoveNext());
+    for (const Event &e : samples) DoInsert(e);
+    m_lastBucket = lastBucket;
+    m_bucketTop = bucketTop;
+    m_lastPrio = lastPrio;
+    uint64_t totalSeparation = 0;
+    for (uint32_t k = 1; k < samples.size(); k++) totalSeparation += samples[k].key.ts - samples[k - 1].key.ts;
+    const uint64_t twiceAvg = totalSeparation / (nSamples - 1) * 2;
+    totalSeparation = 0;
+    for (uint32_t k = 1; k < samples.size(); k++) {
+      const uint64_t diff = samples[k].key.ts - samples[k - 1].key.ts;
+      if (diff <= twiceAvg) totalSeparation += diff;
+    }
+    totalSeparation *= 3;
+    if (totalSeparation < 1) totalSeparation = 1;
+    return (uint32_t)totalSeparation;
+  }
+  void DoResize(uint32_t newSize, uint64_t newWidth) {  // :323-339
+    std::vector<Bucket> old;
+    old.swap(m_buckets);
+    Init(newSize, newWidth, m_lastPrio);
+    for (auto &b : old)
+      for (const Event &e : b) DoInsert(e);
+  }
+  void Resize(uint32_t newSize) { DoResize(newSize, CalculateNewWidth()); }  // :340-348
+};
+
 }  // namespace nsref_detail
 using namespace nsref_detail;
 
@@ -196,11 +339,16 @@ struct nsref_sim {
   explicit nsref_sim(int sched) {
     if (sched == NSREF_SCHED_HEAP) m_events = new HeapScheduler();
     else if (sched == NSREF_SCHED_LIST) m_events = new ListScheduler();
+    else if (sched == NSREF_SCHED_CALENDAR) m_events = new CalendarScheduler();
     else m_events = new MapScheduler();
   }
+  bool crashed = false;  // the scheduler reached a point where the reference crashes
   ~nsref_sim() {
-    // DoDispose (:66-75): drain and unref
-    while (!m_events->IsEmpty()) m_events->RemoveNext().impl->Unref();
+    // DoDispose (:66-75): drain and unref (after a restated crash the pending events are leaked)
+    try {
+      while (!crashed && !m_events->IsEmpty()) m_events->RemoveNext().impl->Unref();
+    } catch (const CalendarCrash &) {
+    }
     delete m_events;
     for (EventImpl *e : m_pinned) e->Unref();
   }

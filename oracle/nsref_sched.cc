@@ -105,19 +105,20 @@ extern "C" int nsref_churn_run(const uint64_t *dist_ns, uint32_t n, uint32_t tot
   b.n = n;
   b.m_total = total;
   b.sim = &sim;
-  auto t0 = std::chrono::steady_clock::now();
-  for (uint32_t i = 0; i < n; i++) sim.Schedule((int64_t)dist_ns[i], new BenchCb(&b));  // RunBench :84-88
-  auto t1 = std::chrono::steady_clock::now();
-  // Simulator::Run with an order-sensitive digest of the pop order folded in by the dispatch hook.
-  uint64_t digest = 0, last_ts = 0;
-  sim.m_stop = false;
-  while (!sim.m_events->IsEmpty() && !sim.m_stop) {
-    const Event next = sim.m_events->PeekNext();
-    digest += nsgpu_dispatch_digest_term(sim.m_dispatched, next.key.ts, next.key.uid);
-    last_ts = next.key.ts;
-    sim.ProcessOneEvent();
+  auto t0 = std::chrono::steady_clock::now(), t1 = t0;
+  // Simulator::Run; the order-sensitive digest of the pop order is folded in by ProcessOneEvent
+  sim.want_digest = true;
+  int rc = 0;
+  try {
+    for (uint32_t i = 0; i < n; i++) sim.Schedule((int64_t)dist_ns[i], new BenchCb(&b));  // RunBench :84-88
+    t1 = std::chrono::steady_clock::now();
+    sim.Run();
+  } catch (const CalendarCrash &) {
+    rc = -3;  // where the reference's CalendarScheduler crashes
+    sim.crashed = true;
   }
   auto t2 = std::chrono::steady_clock::now();
+  const uint64_t digest = sim.m_digest, last_ts = sim.m_currentTs;
   out->dispatched = sim.m_dispatched;
   out->holds = b.m_n;
   out->final_ts = last_ts;
@@ -126,5 +127,5 @@ extern "C" int nsref_churn_run(const uint64_t *dist_ns, uint32_t n, uint32_t tot
   out->pad_ = 0;
   out->init_seconds = std::chrono::duration<double>(t1 - t0).count();
   out->run_seconds = std::chrono::duration<double>(t2 - t1).count();
-  return 0;
+  return rc;
 }
