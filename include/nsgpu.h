@@ -69,9 +69,12 @@ typedef struct nsgpu_phy_soa {
   const double   *x, *y, *z;   /* positions (ConstantPositionMobilityModel), metres */
   const uint32_t *channel;     /* YansWifiPhy::GetChannelNumber () */
   const uint32_t *node;        /* NetDevice->GetNode ()->GetId (), 0xffffffff if none */
-  /* Optional (both NULL: not given), built once per phy list by the caller: chan_rank[j] = how many
+  /* Optional (both NULL: not given), built with the phy list by the caller: chan_rank[j] = how many
    * phys before j in m_phyList share j's channel, chan_count[j] = how many phys share it.  With them
-   * nsgpu_fanout_yans places receiver records (and their uids) directly, without a counting pass. */
+   * nsgpu_fanout_yans places receiver records (and their uids) directly, without a counting pass; d_out
+   * must then be 16-byte aligned.  The tables describe the channel numbers they were built from: rebuild
+   * them whenever YansWifiChannel::Add changes m_phyList or a phy's channel number changes
+   * (YansWifiPhy::SetChannelNumber, yans-wifi-phy.cc:328-358), or pass NULL (two-pass path) while stale. */
   const uint32_t *chan_rank;
   const uint32_t *chan_count;
 } nsgpu_phy_soa;
@@ -97,6 +100,26 @@ int nsgpu_fanout_spectrum(const nsgpu_phy_soa *phys, int64_t nphy, const nsgpu_t
                           nsgpu_rx_record *d_out, double *d_psd_out, uint32_t *d_count,
                           void *d_workspace, void *stream);
 int nsgpu_fanout_workspace_bytes(int64_t nphy, int64_t n_tx, uint64_t *bytes);
+
+/* MultiModelSpectrumChannel::StartTx (src/spectrum/model/multi-model-spectrum-channel.cc:226-331) with
+ * SpectrumConverter (spectrum-converter.cc).  The receivers are visited per rx SpectrumModel in ascending
+ * model index (= SpectrumModelUid order of m_rxSpectrumModelInfoMap) and in AddRx order within a model:
+ * d_iter[q] is the phy at visit position q, d_iter_pos its inverse (build both with the phy list, and again
+ * whenever AddRx changes it).  d_rx_model[j]: phy j's rx model; d_tx_model[t] / d_psd_tx[t * max_bands + b]:
+ * transmission t's PSD and its model.  The PSD is converted once per (transmission, rx model); each
+ * survivor (-gain <= max_loss_db) gets a record as in nsgpu_fanout_spectrum (uid_base + rank in visit
+ * order, rx_dbm = gain) and d_psd_out[(t * (nphy-1) + k) * max_bands + b] = converted[b] * 10^(gain/10)
+ * for its model's bands.  d_trace (optional, [t * (nphy-1) + i]): the PropagationLoss trace call of every
+ * non-sender receiver, in visit order, cut or not.  A single model with no conversion is
+ * SingleModelSpectrumChannel::StartTx plus its trace.  Workspace: nsgpu_fanout_multi_workspace_bytes. */
+int nsgpu_fanout_spectrum_multi(const nsgpu_phy_soa *phys, const int32_t *d_rx_model, const uint32_t *d_iter,
+                                const uint32_t *d_iter_pos, int64_t nphy, const nsgpu_spectrum_models *models,
+                                const nsgpu_tx_desc *d_tx, const int32_t *d_tx_model, const double *d_psd_tx,
+                                int64_t n_tx, const nsgpu_loss_chain *loss, double speed, double max_loss_db,
+                                nsgpu_rx_record *d_out, double *d_psd_out, nsgpu_loss_trace *d_trace,
+                                uint32_t *d_count, void *d_workspace, void *stream);
+int nsgpu_fanout_multi_workspace_bytes(int64_t nphy, int64_t n_tx, int32_t n_models, int32_t max_bands,
+                                       uint64_t *bytes);
 
 /* ---------------- Wi-Fi PHY receive subset (config 3) ----------------
  * Replaces, for a transmission schedule fixed before Run (nsgpu_wifi_scenario in nsgpu_types.h), the

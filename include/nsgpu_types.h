@@ -72,6 +72,25 @@ typedef struct nsgpu_rx_record {
   double rx_dbm;     /* CalcRxPower (txPowerDbm, sender, receiver) */
 } nsgpu_rx_record;
 
+/* SpectrumModels a MultiModelSpectrumChannel knows, indexed in ascending SpectrumModelUid order (the
+ * iteration order of its m_rxSpectrumModelInfoMap, multi-model-spectrum-channel.cc:246-249): model m has
+ * the bands [band_off[m], band_off[m+1]) of fl / fh (BandInfo, Hz).  Pointers are device memory. */
+typedef struct nsgpu_spectrum_models {
+  int32_t n_models;
+  int32_t max_bands;          /* largest band count of any model (the PSD stride) */
+  const uint32_t *band_off;   /* [n_models + 1] */
+  const double *fl, *fh;      /* [band_off[n_models]] */
+} nsgpu_spectrum_models;
+
+/* One PropagationLoss trace call of a spectrum channel's StartTx: m_propagationLossTrace (txPhy, rxPhy,
+ * -gainDb), fired for every receiver before the MaxLossDb cut (multi-model-spectrum-channel.cc:290-291,
+ * single-model-spectrum-channel.cc:145-146). */
+typedef struct nsgpu_loss_trace {
+  uint32_t rx_phy;
+  uint32_t pad_;
+  double loss_db;
+} nsgpu_loss_trace;
+
 /* ---------------- point-to-point scenario (GPU-resident p2p / DropTail / IPv4 / UDP subset) ----------------
  * A topology of PointToPointNetDevices joined by PointToPointChannels, IPv4 forwarding by static
  * next-hop tables, OnOff (UDP, constant on/off times) sources and PacketSink sinks.  All arrays are

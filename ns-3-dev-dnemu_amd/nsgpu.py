@@ -22,6 +22,11 @@ class PhySoA(C.Structure):
                 ("node", C.c_void_p), ("chan_rank", C.c_void_p), ("chan_count", C.c_void_p)]
 
 
+class SpectrumModels(C.Structure):  # nsgpu_spectrum_models
+    _fields_ = [("n_models", C.c_int32), ("max_bands", C.c_int32), ("band_off", C.c_void_p), ("fl", C.c_void_p),
+                ("fh", C.c_void_p)]
+
+
 class LossModel(C.Structure):
     _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p0", C.c_double), ("p1", C.c_double), ("p2", C.c_double)]
 
@@ -36,6 +41,7 @@ class HoldStats(C.Structure):
                 ("next_uid", C.c_uint32)]
 
 
+LOSS_TRACE_DTYPE = np.dtype([("rx_phy", "<u4"), ("pad_", "<u4"), ("loss_db", "<f8")])  # nsgpu_loss_trace
 TX_DESC_DTYPE = np.dtype([("now_ts", "<u8"), ("tx_dbm", "<f8"), ("sender", "<u4"), ("uid_base", "<u4")])
 RX_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("context", "<u4"), ("phy", "<u4"),
                             ("pad_", "<u4"), ("rx_dbm", "<f8")])
@@ -69,6 +75,10 @@ SIGNATURES = {
     "nsgpu_fanout_spectrum": (C.c_int, [C.POINTER(PhySoA), _i64, _vp, _i64, C.POINTER(LossChain), _d, _d, _vp,
                                         _i32, _vp, _vp, _vp, _vp, _vp]),
     "nsgpu_fanout_workspace_bytes": (C.c_int, [_i64, _i64, C.POINTER(C.c_uint64)]),
+    "nsgpu_fanout_spectrum_multi": (C.c_int, [C.POINTER(PhySoA), _vp, _vp, _vp, _i64, C.POINTER(SpectrumModels), _vp,
+                                              _vp, _vp, _i64, C.POINTER(LossChain), _d, _d, _vp, _vp, _vp, _vp, _vp,
+                                              _vp]),
+    "nsgpu_fanout_multi_workspace_bytes": (C.c_int, [_i64, _i64, _i32, _i32, C.POINTER(C.c_uint64)]),
     "nsgpu_hold_workspace_bytes": (C.c_int, [_u32, C.POINTER(C.c_uint64)]),
     "nsgpu_hold_set_profile": (C.c_int, [_vp]),
     "nsgpu_sched_create": (C.c_int, [_u32, _vp, C.POINTER(C.c_void_p)]),
@@ -282,8 +292,13 @@ class PhyList:
         self.n = len(x)
         self.bufs = [DeviceBuffer.from_array(np.asarray(a, dtype=t), stream) for a, t in
                      ((x, np.float64), (y, np.float64), (z, np.float64), (channel, np.uint32), (node, np.uint32))]
+        self.stream = stream
+        self.channel = np.array(channel, dtype=np.uint32)
+        self._rank_tables()
+
+    def _rank_tables(self):
         # per-channel rank / size of every phy (m_phyList order): Yans records are placed without counting
-        ch = np.asarray(channel, dtype=np.uint32)
+        ch = self.channel
         order = np.argsort(ch, kind="stable")
         sch = ch[order]
         first = np.r_[True, sch[1:] != sch[:-1]] if ch.size else np.zeros(0, bool)
@@ -292,8 +307,83 @@ class PhyList:
         rank[order] = (np.arange(ch.size) - start).astype(np.uint32)
         _u, inv, cnt = np.unique(ch, return_inverse=True, return_counts=True)
         count = cnt[inv].astype(np.uint32)
-        self.bufs += [DeviceBuffer.from_array(rank, stream), DeviceBuffer.from_array(count, stream)]
+        self.bufs[5:] = [DeviceBuffer.from_array(rank, self.stream), DeviceBuffer.from_array(count, self.stream)]
         self.soa = PhySoA(*[b.ptr for b in self.bufs])
+
+    def set_channel(self, j, ch):
+        """YansWifiPhy::SetChannelNumber (yans-wifi-phy.cc:328-358) on phy j: the channel array and the rank
+        tables that depend on it are updated together (include/nsgpu.h, nsgpu_phy_soa)."""
+        self.channel[j] = ch
+        self.bufs[3] = DeviceBuffer.from_array(self.channel, self.stream)
+        self._rank_tables()
+
+
+class MultiModelFanout:
+    """MultiModelSpectrumChannel::StartTx over a resident phy list (nsgpu_fanout_spectrum_multi).
+
+    models: list of (fl, fh) band-edge arrays in ascending SpectrumModelUid order; rx_model[j]: phy j's
+    model index.  The visit order (m_rxSpectrumModelInfoMap by model, AddRx order within) is built here."""
+
+    def __init__(self, phys, rx_model, models, max_tx, stream=None):
+        self.phys, self.max_tx, self.stream = phys, max_tx, stream
+        self.rx_model = np.asarray(rx_model, np.int32)
+        self.nb = np.array([len(fl) for fl, _ in models], np.int64)
+        self.max_bands = int(self.nb.max())
+        off = np.zeros(len(models) + 1, np.uint32)
+        off[1:] = np.cumsum(self.nb)
+        fl = np.concatenate([np.asarray(a, np.float64) for a, _ in models])
+        fh = np.concatenate([np.asarray(b, np.float64) for _, b in models])
+        it = np.argsort(self.rx_model, kind="stable").astype(np.uint32)
+        pos = np.empty_like(it)
+        pos[it] = np.arange(it.size, dtype=np.uint32)
+        self.bufs = [DeviceBuffer.from_array(a, stream) for a in (self.rx_model, it, pos, off, fl, fh)]
+        self.models = SpectrumModels(len(models), self.max_bands, self.bufs[3].ptr, self.bufs[4].ptr, self.bufs[5].ptr)
+        n = phys.n
+        ws = C.c_uint64()
+        check(lib().nsgpu_fanout_multi_workspace_bytes(n, max_tx, len(models), self.max_bands, C.byref(ws)))
+        self.ws = DeviceBuffer(ws.value)
+        self.out = DeviceBuffer(max_tx * (n - 1) * RX_RECORD_DTYPE.itemsize)
+        self.psd_out = DeviceBuffer(max_tx * (n - 1) * self.max_bands * 8)
+        self.trace = DeviceBuffer(max_tx * (n - 1) * LOSS_TRACE_DTYPE.itemsize)
+        self.count = DeviceBuffer(max_tx * 4)
+        self.tx = DeviceBuffer(max_tx * TX_DESC_DTYPE.itemsize)
+        self.tx_model = DeviceBuffer(max_tx * 4)
+        self.psd_tx = DeviceBuffer(max_tx * self.max_bands * 8)
+
+    def upload_tx(self, tx, tx_model, psd_tx):
+        """psd_tx: [n_tx, max_bands] (each row's first nbands(tx_model) values used)."""
+        tx = np.ascontiguousarray(tx, dtype=TX_DESC_DTYPE)
+        assert len(tx) <= self.max_tx
+        tm = np.ascontiguousarray(tx_model, np.int32)
+        p = np.zeros((len(tx), self.max_bands), np.float64)
+        for t, row in enumerate(psd_tx):
+            p[t, :len(row)] = row
+        for src, dst in ((tx, self.tx), (tm, self.tx_model), (p, self.psd_tx)):
+            check(lib().nsgpu_memcpy_htod(dst.ptr, src.ctypes.data, src.nbytes, self.stream))
+        return len(tx)
+
+    def launch(self, n_tx, chain, speed, max_loss_db, trace=True):
+        check(lib().nsgpu_fanout_spectrum_multi(C.byref(self.phys.soa), self.bufs[0].ptr, self.bufs[1].ptr,
+                                                self.bufs[2].ptr, self.phys.n, C.byref(self.models), self.tx.ptr,
+                                                self.tx_model.ptr, self.psd_tx.ptr, n_tx, C.byref(chain), speed,
+                                                max_loss_db, self.out.ptr, self.psd_out.ptr,
+                                                self.trace.ptr if trace else None, self.count.ptr, self.ws.ptr,
+                                                self.stream))
+
+    def results(self, n_tx):
+        """Per transmission: (records, PSD rows trimmed to each receiver's model, loss-trace entries)."""
+        n = self.phys.n
+        counts = self.count.download(np.uint32, n_tx, self.stream)
+        recs = self.out.download(RX_RECORD_DTYPE, n_tx * (n - 1), self.stream).reshape(n_tx, n - 1)
+        psd = self.psd_out.download(np.float64, n_tx * (n - 1) * self.max_bands, self.stream)
+        psd = psd.reshape(n_tx, n - 1, self.max_bands)
+        tr = self.trace.download(LOSS_TRACE_DTYPE, n_tx * (n - 1), self.stream).reshape(n_tx, n - 1)
+        out = []
+        for t in range(n_tx):
+            r = recs[t, :counts[t]]
+            rows = [psd[t, k, :self.nb[self.rx_model[r["phy"][k]]]] for k in range(len(r))]
+            out.append((r, rows, tr[t]))
+        return out
 
 
 class Fanout:

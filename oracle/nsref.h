@@ -67,6 +67,21 @@ int64_t nsref_fanout_spectrum(const double *x, const double *y, const double *z,
                               uint64_t now_ts, uint32_t uid_base,
                               nsgpu_rx_record *out, double *psd_out);
 
+/* MultiModelSpectrumChannel::StartTx (src/spectrum/model/multi-model-spectrum-channel.cc:226-331) with the
+ * SpectrumConverter of spectrum-converter.cc: receivers grouped by rx SpectrumModel (ascending model index
+ * = ascending SpectrumModelUid), AddRx order within a model; the tx PSD (model tx_model) converted once per
+ * rx model, then scaled by each survivor's 10^(gain/10).  Models: n_models, band_off[n_models+1], fl/fh.
+ * Records go to out[k], PSDs to psd_out[k * psd_stride + b]; every non-sender receiver (cut or not) gets a
+ * PropagationLoss trace entry trace[i] (receiver iteration order); *n_trace = entries written. */
+int64_t nsref_fanout_spectrum_multi(const double *x, const double *y, const double *z, const uint32_t *node,
+                                    const int32_t *rx_model, int64_t nphy, int64_t sender,
+                                    int32_t n_models, const uint32_t *band_off, const double *fl, const double *fh,
+                                    int32_t tx_model, const double *psd_tx,
+                                    const nsgpu_loss_chain *loss, double speed, double max_loss_db,
+                                    uint64_t now_ts, uint32_t uid_base,
+                                    nsgpu_rx_record *out, double *psd_out, int32_t psd_stride,
+                                    nsgpu_loss_trace *trace, int64_t *n_trace);
+
 /* ---------------- Sequential engine: DefaultSimulatorImpl + Map/Heap scheduler ----------------
  * (src/core/model/default-simulator-impl.cc:49-353, map-scheduler.cc:51-100, heap-scheduler.cc:44-217) */
 enum { NSREF_SCHED_MAP = 0, NSREF_SCHED_HEAP = 1, NSREF_SCHED_LIST = 2, NSREF_SCHED_CALENDAR = 3 };

@@ -457,3 +457,37 @@ def global_routes(dev_node, dev_peer, dev_addr, dev_mask, dev_ifindex, n_nodes, 
     if rc != 0:
         raise RuntimeError(f"nsref_global_routes: {rc}")
     return out
+
+
+LOSS_TRACE_DTYPE = np.dtype([("rx_phy", "<u4"), ("pad_", "<u4"), ("loss_db", "<f8")])  # nsgpu_loss_trace
+
+
+def fanout_spectrum_multi(x, y, z, node, rx_model, sender, models, tx_model, psd_tx, chain, speed, max_loss_db,
+                          now_ts, uid_base):
+    """MultiModelSpectrumChannel::StartTx restated; models: [(fl, fh), ...] in ascending SpectrumModelUid.
+    Returns (records, [psd row per record], loss-trace entries)."""
+    f = lib().nsref_fanout_spectrum_multi
+    f.restype = C.c_int64
+    f.argtypes = [C.c_void_p] * 5 + [C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                     C.c_void_p, C.POINTER(LossChain), C.c_double, C.c_double, C.c_uint64,
+                                     C.c_uint32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+    n = len(x)
+    nb = [len(a) for a, _ in models]
+    off = np.zeros(len(models) + 1, np.uint32)
+    off[1:] = np.cumsum(nb)
+    fl = np.concatenate([np.asarray(a, np.float64) for a, _ in models])
+    fh = np.concatenate([np.asarray(b, np.float64) for _, b in models])
+    stride = max(nb)
+    arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+            ((x, np.float64), (y, np.float64), (z, np.float64), (node, np.uint32), (rx_model, np.int32))]
+    psd = np.ascontiguousarray(psd_tx, np.float64)
+    out = np.zeros(n, RX_RECORD_DTYPE)
+    psd_out = np.zeros((n, stride), np.float64)
+    tr = np.zeros(n, LOSS_TRACE_DTYPE)
+    nt = C.c_int64()
+    k = f(*[a.ctypes.data for a in arrs], n, sender, len(models), off.ctypes.data, fl.ctypes.data, fh.ctypes.data,
+          tx_model, psd.ctypes.data, C.byref(chain), speed, max_loss_db, now_ts, uid_base, out.ctypes.data,
+          psd_out.ctypes.data, stride, tr.ctypes.data, C.byref(nt))
+    rm = np.asarray(rx_model)
+    rows = [psd_out[i, :nb[rm[out["phy"][i]]]] for i in range(k)]
+    return out[:k], rows, tr[:nt.value]

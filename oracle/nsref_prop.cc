@@ -3,6 +3,8 @@
 // channel fan-out loops.  Built with -ffp-contract=off so that
 // dx*dx+dy*dy+dz*dz rounds exactly like the reference's default -O2 x86-64 build.
 #include "nsref.h"
+#include <algorithm>
+#include <vector>
 #include <math.h>
 
 static const double PI = 3.14159265358979323846;  // propagation-loss-model.cc:34
@@ -108,6 +110,66 @@ int64_t nsref_fanout_spectrum(const double *x, const double *y, const double *z,
     r.rx_dbm = gainDb;
     out[k++] = r;
   }
+  return k;
+}
+
+// SpectrumConverter (spectrum-converter.cc): coefficient of input band `from` in output band `to`
+static double converter_coeff(double ffl, double ffh, double tfl, double tfh) {  // GetCoefficient
+  double coeff = std::min(ffh, tfh) - std::max(ffl, tfl);
+  coeff = std::max(0.0, coeff);
+  coeff = std::min(1.0, coeff / (tfh - tfl));
+  return coeff;
+}
+
+// MultiModelSpectrumChannel::StartTx — multi-model-spectrum-channel.cc:226-331
+int64_t nsref_fanout_spectrum_multi(const double *x, const double *y, const double *z, const uint32_t *node,
+                                    const int32_t *rx_model, int64_t nphy, int64_t sender,
+                                    int32_t n_models, const uint32_t *band_off, const double *fl, const double *fh,
+                                    int32_t tx_model, const double *psd_tx,
+                                    const nsgpu_loss_chain *loss, double speed, double max_loss_db,
+                                    uint64_t now_ts, uint32_t uid_base,
+                                    nsgpu_rx_record *out, double *psd_out, int32_t psd_stride,
+                                    nsgpu_loss_trace *trace, int64_t *n_trace) {
+  int64_t k = 0, nt = 0;
+  std::vector<double> conv;
+  const uint32_t t0 = band_off[tx_model], ntb = band_off[tx_model + 1] - t0;
+  for (int32_t m = 0; m < n_models; m++) {  // for each rx SpectrumModel (:246-329)
+    const uint32_t r0 = band_off[m], nrb = band_off[m + 1] - r0;
+    bool any = false;
+    for (int64_t j = 0; j < nphy && !any; j++) any = rx_model[j] == m;
+    if (!any) continue;  // (only models some phy was added with are in the map)
+    conv.assign(nrb, 0.0);
+    if (m == tx_model) {  // no spectrum conversion needed (:254-258)
+      for (uint32_t b = 0; b < nrb; b++) conv[b] = psd_tx[b];
+    } else {  // SpectrumConverter::Convert: sum over input bands in order
+      for (uint32_t b = 0; b < nrb; b++) {
+        double sum = 0;
+        for (uint32_t f = 0; f < ntb; f++)
+          sum += psd_tx[f] * converter_coeff(fl[t0 + f], fh[t0 + f], fl[r0 + b], fh[r0 + b]);
+        conv[b] = sum;
+      }
+    }
+    for (int64_t j = 0; j < nphy; j++) {  // m_rxPhyList: AddRx order
+      if (rx_model[j] != m || j == sender) continue;
+      double d = nsref_distance(x[sender], y[sender], z[sender], x[j], y[j], z[j]);
+      double gainDb = nsref_calc_rx_power(0, d, loss);
+      if (trace) trace[nt] = nsgpu_loss_trace{(uint32_t)j, 0u, -gainDb};
+      nt++;
+      if ((-gainDb) > max_loss_db) continue;  // beyond range
+      double gainLinear = pow(10.0, gainDb / 10.0);
+      for (uint32_t b = 0; b < nrb; b++) psd_out[k * psd_stride + b] = conv[b] * gainLinear;
+      int64_t delay = speed > 0 ? nsref_const_speed_delay(d, speed) : 0;
+      nsgpu_rx_record r;
+      r.ts = now_ts + (uint64_t)delay;
+      r.uid = uid_base + (uint32_t)k;
+      r.context = node[j];
+      r.phy = (uint32_t)j;
+      r.pad_ = 0;
+      r.rx_dbm = gainDb;
+      out[k++] = r;
+    }
+  }
+  if (n_trace) *n_trace = nt;
   return k;
 }
 
