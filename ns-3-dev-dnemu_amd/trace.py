@@ -45,6 +45,55 @@ def sort_records(tr):
     return tr[np.lexsort((tr["seq"], tr["uid"], tr["ts"]))]
 
 
+# ---------------- pcap file format (PcapFile, src/network/utils/pcap-file.cc) ----------------
+PCAP_MAGIC = 0xa1b2c3d4
+DLT_EN10MB, DLT_PPP = 1, 9
+
+
+def pcap_file_header(snaplen=65535, linktype=DLT_PPP, tz=0):
+    """PcapFile::Init (pcap-file.cc:300-346): magic, version 2.4, thiszone, sigfigs 0, snaplen, network
+    (native little-endian, no swap)."""
+    return struct.pack("<IHHiIII", PCAP_MAGIC, 2, 4, tz, 0, snaplen, linktype)
+
+
+def pcap_record(sec, usec, data, total_len=None, snaplen=65535):
+    """PcapFile::WritePacketHeader + Write (pcap-file.cc:348-381): inclLen = min (totalLen, snapLen),
+    origLen = totalLen, then the first inclLen bytes of the packet."""
+    total = len(data) if total_len is None else total_len
+    incl = min(total, snaplen)
+    return struct.pack("<IIII", sec, usec, incl, total) + bytes(data[:incl])
+
+
+def pcap_read(buf):
+    """(file header fields, [(sec, usec, inclLen, origLen, data)]) of a native-endian pcap file."""
+    magic, vmaj, vmin, tz, sig, snap, link = struct.unpack_from("<IHHiIII", buf, 0)
+    assert magic == PCAP_MAGIC, hex(magic)
+    recs, off = [], 24
+    while off + 16 <= len(buf):
+        sec, usec, incl, orig = struct.unpack_from("<IIII", buf, off)
+        recs.append((sec, usec, incl, orig, bytes(buf[off + 16:off + 16 + incl])))
+        off += 16 + incl
+    return (vmaj, vmin, tz, sig, snap, link), recs
+
+
+def pcap_diff(a, b, snaplen=65535):
+    """PcapFile::Diff (pcap-file.cc:465-535): (differ, sec, usec) — the time of the first record whose
+    timestamp, read length or data differ (reading at most snaplen bytes of each), or of the last record
+    read when one file ends first."""
+    _ha, ra = pcap_read(a)
+    _hb, rb = pcap_read(b)
+    sec = usec = 0
+    for i in range(max(len(ra), len(rb))):
+        if (i < len(ra)) != (i < len(rb)):
+            return True, sec, usec
+        s1, u1, _i1, _o1, d1 = ra[i]
+        s2, u2, _i2, _o2, d2 = rb[i]
+        sec, usec = s1, u1
+        if (s1, u1) != (s2, u2) or d1[:snaplen] != d2[:snaplen]:
+            return True, sec, usec
+    return False, sec, usec
+
+
 def seconds_text(ts_ns):
     """std::ostream << double (precision 6, %g) of Time::GetSeconds ()."""
     return "%g" % (ts_ns / 1e9)
@@ -134,8 +183,7 @@ class Codec:
         """EnablePcapAll: {(node, ifindex): file bytes} for every point-to-point device."""
         files = {}
         for d in range(len(self.sc.dev)):
-            files[(self.dev_node[d], self.ifindex[d])] = bytearray(struct.pack("<IHHiIII", 0xa1b2c3d4, 2, 4, 0, 0,
-                                                                               65535, 9))  # DLT_PPP
+            files[(self.dev_node[d], self.ifindex[d])] = bytearray(pcap_file_header(65535, DLT_PPP))
         for r in tr:
             if r["kind"] not in (TR_DEQUEUE, TR_RX):  # the sniffer runs after Dequeue and before MacRx
                 continue
@@ -143,5 +191,5 @@ class Codec:
             pkt = self.packet_bytes(r)
             us = int(r["ts"]) // 1000
             f = files[(self.dev_node[d], self.ifindex[d])]
-            f += struct.pack("<IIII", us // 1000000, us % 1000000, len(pkt), len(pkt)) + pkt
+            f += pcap_record(us // 1000000, us % 1000000, pkt)
         return {k: bytes(v) for k, v in files.items()}
