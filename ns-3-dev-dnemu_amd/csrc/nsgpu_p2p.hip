@@ -717,6 +717,35 @@ __device__ uint64_t g_phase[64];
 #define PH_BEGIN() (void)0
 #define PH_MARK(i) (void)0
 #endif
+// Per-block start / end times (s_memrealtime) of the window kernels in one sampled window
+// (diagnostic build only): g_blk[kernel][block] = {start, end}, window g_blk_win.
+#ifdef NSGPU_PHASE_PROF
+constexpr int BLK_MAX = 2048;
+__device__ uint64_t g_blk[3][BLK_MAX][2];
+__device__ uint64_t g_blk_win = 1000;
+#define BLK_T0() uint64_t bt0_ = __builtin_amdgcn_s_memrealtime(), btm_ = bt0_
+// per-block phase mark in the sampled window: g_phase[i] += time since the block's previous mark
+#define BLK_MARK(i, win)                                                                         \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && (win) == g_blk_win) {                                                \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                      \
+      atomicAdd((unsigned long long *)&g_phase[i], (unsigned long long)(t_ - btm_));             \
+      atomicAdd((unsigned long long *)&g_phase[(i) + 1], 1ull);                                  \
+      btm_ = t_;                                                                                 \
+    }                                                                                            \
+  } while (0)
+#define BLK_REC(k, win)                                                                          \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && (win) == g_blk_win && blockIdx.x < (uint32_t)BLK_MAX) {              \
+      g_blk[k][blockIdx.x][0] = bt0_;                                                            \
+      g_blk[k][blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();                                \
+    }                                                                                            \
+  } while (0)
+#else
+#define BLK_T0() (void)0
+#define BLK_REC(k, win) (void)0
+#define BLK_MARK(i, win) (void)0
+#endif
 
 // ================================ window pipeline ================================
 // Window bound of a pending set's reduction: packed key bound, span, Stop key.
@@ -2492,7 +2521,11 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
 extern "C" int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset) {
 #ifdef NSGPU_PHASE_PROF
   if (!out || n <= 0) return set_error(NSGPU_EINVAL, "nsgpu_p2p_phase_read: null");
-  if (n > 64) n = 64;
+  if (n > 64) {  // the rest: the per-block times of the sampled window (g_blk)
+    const int nb = std::min(n - 64, 3 * BLK_MAX * 2);
+    NSGPU_HIP(hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_blk), nb * sizeof(uint64_t)));
+    n = 64;
+  }
   NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), n * sizeof(uint64_t)));
   if (reset) {
     uint64_t z[64] = {0};

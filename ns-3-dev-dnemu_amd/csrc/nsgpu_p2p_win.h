@@ -114,49 +114,14 @@ __device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t
 
 // A pending event against the window bound: window record (normal mode, key <= bound), else pending:
 // a child (src == NOSRC) is parked in the fresh buffer, a pool entry stays where it is; both fold
-// into the next window's reduction.  Lanes that call it must be converged (ballots).
-__device__ __forceinline__ void k2_place(const P2PDev &M, Ctl &C, const WinBound &b, bool run, bool valid,
-                                         const Ev &e, uint32_t src, Red &R, uint64_t &tmn, uint64_t &wnd) {
+// into the next window's reduction.
+__device__ __forceinline__ void k2_classify(const P2PDev &M, const WinBound &b, bool run, bool valid, const Ev &e,
+                                            uint32_t src, Red &R, uint64_t &tmn, uint64_t &wnd, bool &in,
+                                            bool &park) {
   const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
-  const bool in = valid && !run && (e.ts - b.tmin <= b.span) && pk <= b.bound;
-  const bool park = valid && !in && src == NOSRC;
-  // both counters at once (one lane, two atomics in flight): window slots and fresh-buffer entries
-  const uint64_t bin = __ballot(in), bpk = __ballot(park);
-  const int lane = threadIdx.x & 63;
-  uint32_t bw = 0;
-  unsigned long long bf = 0;
-  if (lane == 0) {  // (every lane of the wave calls k2_place)
-    if (bin) bw = atomicAdd(&C.W, (uint32_t)__popcll(bin));
-    if (bpk) bf = atomicAdd((unsigned long long *)&C.nF, (unsigned long long)__popcll(bpk));
-  }
-  const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t slot = (uint32_t)__shfl(bw, 0) + (uint32_t)__popcll(bin & below);
-  const uint64_t fi = (uint64_t)__shfl(bf, 0) + (uint64_t)__popcll(bpk & below);
-  if (in) {
-    if (slot < M.runcap) {
-      M.wkey[slot] = pk;
-      M.wctx[slot] = e.ctx;
-      M.wkind[slot] = e.kind;
-      M.wa[slot] = e.a;
-      M.wpkt[slot] = e.p;
-      M.wsrc[slot] = src;
-      if (slot < (uint32_t)WCAP) node_table_add(M, C, slot, lp_of(M, e.ctx, e.kind, e.a), e.kind);
-    } else {
-      atomicOr(M.error, 1u);
-    }
-  } else if (valid) {
-    if (park) {
-      if (fi < M.fcap) {
-        M.f_ts[fi] = e.ts;
-        M.f_uid[fi] = e.uid;
-        M.f_ctx[fi] = e.ctx;
-        M.f_kind[fi] = e.kind;
-        M.f_a[fi] = e.a;
-        M.f_pkt[fi] = e.p;
-      } else {
-        atomicOr(M.error, 1u);
-      }
-    }
+  in = valid && !run && (e.ts - b.tmin <= b.span) && pk <= b.bound;
+  park = valid && !in && src == NOSRC;
+  if (valid && !in) {
     tmn = e.ts < tmn ? e.ts : tmn;
     const uint64_t x = e.ts + (uint64_t)M.lookahead[e.kind & 0xffu];
     wnd = x < wnd ? x : wnd;
@@ -167,22 +132,111 @@ __device__ __forceinline__ void k2_place(const P2PDev &M, Ctl &C, const WinBound
   }
 }
 
+// Writes a classified event: window record `slot`, or fresh-buffer entry `fi` (a parked child).
+__device__ __forceinline__ void k2_write(const P2PDev &M, Ctl &C, const WinBound &b, const Ev &e, uint32_t src,
+                                         bool in, bool park, uint32_t slot, uint64_t fi) {
+  if (in) {
+    if (slot < M.runcap) {
+      M.wkey[slot] = ((e.ts - b.tmin) << 32) | e.uid;
+      M.wctx[slot] = e.ctx;
+      M.wkind[slot] = e.kind;
+      M.wa[slot] = e.a;
+      M.wpkt[slot] = e.p;
+      M.wsrc[slot] = src;
+      if (slot < (uint32_t)WCAP) node_table_add(M, C, slot, lp_of(M, e.ctx, e.kind, e.a), e.kind);
+    } else {
+      atomicOr(M.error, 1u);
+    }
+  } else if (park) {
+    if (fi < M.fcap) {
+      M.f_ts[fi] = e.ts;
+      M.f_uid[fi] = e.uid;
+      M.f_ctx[fi] = e.ctx;
+      M.f_kind[fi] = e.kind;
+      M.f_a[fi] = e.a;
+      M.f_pkt[fi] = e.p;
+    } else {
+      atomicOr(M.error, 1u);
+    }
+  }
+}
+
+// Block-wide allocation of window slots (C.W) and fresh-buffer entries (C.nF): per-thread counts in,
+// each thread's first index out, ONE atomic per counter per block (a device-scope atomic on a shared
+// word costs ~10 ns and they serialise: per-wave allocation cost k2_pa ~3 us a window).  Every thread
+// of the block calls it.
+template <int NT>
+__device__ __forceinline__ void block_alloc2(Ctl &C, uint32_t nw, uint32_t nf, uint32_t &w0, uint64_t &f0) {
+  __shared__ uint64_t s_w[NT / 64];
+  __shared__ uint64_t s_base[2];
+  const uint64_t v = (uint64_t)nw | ((uint64_t)nf << 32);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t x = __shfl_up(inc, o);
+    if (lane >= o) inc += x;
+  }
+  if (lane == 63) s_w[wid] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t tot = 0;
+    for (int w = 0; w < NT / 64; w++) {
+      const uint64_t x = s_w[w];
+      s_w[w] = tot;
+      tot += x;
+    }
+    const uint32_t tw = (uint32_t)tot, tf = (uint32_t)(tot >> 32);
+    s_base[0] = tw ? atomicAdd(&C.W, tw) : 0u;
+    s_base[1] = tf ? (uint64_t)atomicAdd((unsigned long long *)&C.nF, (unsigned long long)tf) : 0ull;
+  }
+  __syncthreads();
+  const uint64_t ex = s_w[wid] + inc - v;
+  w0 = (uint32_t)s_base[0] + (uint32_t)ex;
+  f0 = s_base[1] + (ex >> 32);
+  __syncthreads();  // (s_w / s_base are reused by the next call)
+}
+
 // ---- k2_pa ----
 __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   PH_BEGIN();
+  BLK_T0();
   Ctl &C = *M.C;
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t c_win = C.windows;
+#endif
   const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
-  const uint64_t stride = (uint64_t)gridDim.x * TB;
-  const bool slot_role = g < (uint64_t)WCAP;  // (roles are wave-uniform)
-  if (C.done >= 2 || C.mode >= MODE_SORT) return;
-  const bool run = C.mode == MODE_RUN;
-  const bool partition = C.done == 0;
-  const uint32_t rt = C.rt;
+  const bool slot_role = g < (uint64_t)WCAP;  // (roles are block-uniform)
+  // Everything this kernel reads of the run control and of the last window's slot, loaded at once:
+  // these lines were written by k2_scan on another XCD, so every dependent level is a trip to memory.
+  // (The slot arrays are WCAP long: a slot past the last window's size is loaded and ignored.)
+  const uint32_t c_done = C.done, c_mode = C.mode, rt = C.rt, c_pvalid = C.pvalid, c_pW = C.pW, c_huid = C.huid;
+  const uint32_t uid0 = C.puid0;
+  const Red red0 = C.red[0], red1 = C.red[1];
+  const uint64_t hts = C.hts, c_ptmin = C.ptmin, K0 = C.pK0, ilim = C.pinline_lim, c_P = C.P_end;
+  uint64_t spk = 0;
+  uint4 si = make_uint4(0, 0, 0, 0);
+  uint32_t ncr = 0, sctx = 0;
+  Ev ce[PFC];
+  if (slot_role) {  // the slot and its first children
+    const uint32_t s = (uint32_t)g;
+    spk = M.pwkey[s];
+    si = M.sinfo[s];
+    ncr = M.nchild[s];
+    sctx = M.pwctx[s];
+#pragma unroll
+    for (int j = 0; j < PFC; j++) {
+      const uint32_t sl = s * M.maxc + j;
+      if ((uint32_t)j < M.maxc) ce[j] = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
+    }
+  }
+  if (c_done >= 2 || c_mode >= MODE_SORT) return;
+  if (slot_role) BLK_MARK(32, c_win);  // snapshot + slot loads issued (waits at first use)
+  const bool run = c_mode == MODE_RUN;
+  const bool partition = c_done == 0;
   Red &R = C.red[rt];
-  WinBound b = window_bound(C.red[rt ^ 1]);
+  WinBound b = window_bound(rt ? red0 : red1);
   // a pending host closure (nsgpu_p2p_advance) cuts the window at its key, like Simulator::Stop: the
   // window holds the device events before it, and the pipeline pauses for the host after the window
-  const uint64_t hts = C.hts;
   bool hcap = false;
   uint64_t hrel = ~0ull;
   if (hts != ~0ull && !run) {
@@ -190,7 +244,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       b.bound = 0;  // (every device key is >= 4: uids start at 4)
       hcap = true;
     } else if (hts - b.tmin <= b.span) {
-      const uint64_t hk = ((hts - b.tmin) << 32) | C.huid;
+      const uint64_t hk = ((hts - b.tmin) << 32) | c_huid;
       if (hk <= b.bound) {
         b.bound = hk;
         hcap = true;
@@ -209,23 +263,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     C.hrel = edge;
     C.hcap = hcap;
   }
-  const uint32_t pW = C.pvalid ? C.pW : 0;
-  uint64_t spk = 0;
-  uint4 si = make_uint4(0, 0, 0, 0);
-  uint32_t ncr = 0, sctx = 0;
-  Ev ce[PFC];
-  if (slot_role && g < pW) {  // the last window's slot and its first children, all at once
-    const uint32_t s = (uint32_t)g;
-    spk = M.pwkey[s];
-    si = M.sinfo[s];
-    ncr = M.nchild[s];
-    sctx = M.pwctx[s];
-#pragma unroll
-    for (int j = 0; j < PFC; j++) {
-      const uint32_t sl = s * M.maxc + j;
-      if ((uint32_t)j < M.maxc) ce[j] = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
-    }
-  }
+  const uint32_t pW = c_pvalid ? c_pW : 0;
   PH_MARK(0);
   uint64_t tmn = ~0ull, wnd = ~0ull, digest = 0;
   if (slot_role) {
@@ -233,9 +271,8 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     const bool vs = g < pW;
     const uint32_t s = (uint32_t)g;
     const uint64_t rel = spk >> 32;
-    const uint64_t t = C.ptmin + rel;
-    const uint32_t uid0 = C.puid0;
-    const uint64_t K0 = C.pK0, ilim = C.pinline_lim;
+    const uint64_t t = c_ptmin + rel;
+    BLK_MARK(34, c_win);  // bound, publish_bound
     if (vs) {
       const uint64_t rk = K0 + si.x;
       digest += digest_term(rk, t, (uint32_t)spk);
@@ -245,18 +282,22 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
         M.log_ctx[rk] = sctx;
       }
     }
-    if (__ballot(vs)) {
-      uint32_t ii = 0;
-      for (uint32_t j = 0; j < M.maxc; j++) {
-        const bool has = vs && j < ncr;
-        if (!__ballot(has)) break;
+    // the slot's children in groups of PFC, one block allocation per group (block-uniform loop)
+    const uint32_t nl = vs ? ncr : 0u;
+    uint32_t ii = 0;
+    for (uint32_t j0 = 0; __syncthreads_or(j0 < nl); j0 += PFC) {
+      Ev ge[PFC];
+      bool gin[PFC], gpk[PFC];
+      uint32_t cw = 0, cf = 0;
+#pragma unroll
+      for (int q = 0; q < PFC; q++) {
+        const uint32_t j = j0 + q;
+        const bool has = j < nl;
         Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
         bool valid = false;
         if (has) {
-          if (j < (uint32_t)PFC) {
-#pragma unroll
-            for (int q = 0; q < PFC; q++)
-              if ((uint32_t)q == j) e = ce[q];
+          if (j0 == 0) {
+            e = ce[q];
           } else {
             const uint32_t sl = s * M.maxc + j;
             e = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
@@ -277,18 +318,56 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
             valid = partition;
           }
         }
-        k2_place(M, C, b, run, valid, e, NOSRC, R, tmn, wnd);
+        k2_classify(M, b, run, valid, e, NOSRC, R, tmn, wnd, gin[q], gpk[q]);
+        ge[q] = e;
+        cw += gin[q];
+        cf += gpk[q];
       }
+      BLK_MARK(36, c_win);  // digest/log, classify (slot data arrived)
+      uint32_t w0;
+      uint64_t f0;
+      block_alloc2<TB>(C, cw, cf, w0, f0);
+      BLK_MARK(38, c_win);  // block allocation (atomics)
+#pragma unroll
+      for (int q = 0; q < PFC; q++) {
+        k2_write(M, C, b, ge[q], NOSRC, gin[q], gpk[q], w0, f0);
+        w0 += gin[q];
+        f0 += gpk[q];
+      }
+      BLK_MARK(40, c_win);  // writes (node-table atomics)
     }
   } else if (partition && !run) {
-    // ---- the pool, in place: read (ts, uid, kind) of every slot; window events are copied out
-    const uint64_t P = C.P_end;
-    const uint64_t w0 = (g - WCAP) & ~63ull, ws = (stride - WCAP);
-    for (uint64_t base = w0; base < P; base += ws) {  // wave-uniform trip count
-      const uint64_t i = base + (threadIdx.x & 63);
-      Ev e{TOMB, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-      if (i < P) e = load_pool(M, 0, i);  // every field at once: one memory round trip
-      k2_place(M, C, b, false, e.ts != TOMB, e, (uint32_t)i, R, tmn, wnd);
+    // ---- the pool, in place: read (ts, uid, kind) of every slot; window events are copied out.
+    // Chunks of PPT x TB entries per block (loads of a chunk all in flight), one allocation per chunk;
+    // blocks past the pool's end do nothing (no atomics).
+    constexpr int PPT = 4;
+    const uint64_t P = c_P;
+    const uint64_t pb = blockIdx.x - (uint64_t)(WCAP / TB), npb = gridDim.x - (uint64_t)(WCAP / TB);
+    for (uint64_t c0 = pb * TB * PPT; c0 < P; c0 += npb * TB * PPT) {  // block-uniform trip count
+      Ev ge[PPT];
+      bool gin[PPT], gpk[PPT];
+      uint32_t cw = 0;
+#pragma unroll
+      for (int q = 0; q < PPT; q++) {
+        const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
+        ge[q] = Ev{TOMB, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+        if (i < P) ge[q] = load_pool(M, 0, i);  // every field at once: one memory round trip
+      }
+#pragma unroll
+      for (int q = 0; q < PPT; q++) {
+        const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
+        k2_classify(M, b, false, ge[q].ts != TOMB, ge[q], (uint32_t)i, R, tmn, wnd, gin[q], gpk[q]);
+        cw += gin[q];
+      }
+      uint32_t w0;
+      uint64_t f0;
+      block_alloc2<TB>(C, cw, 0u, w0, f0);
+#pragma unroll
+      for (int q = 0; q < PPT; q++) {
+        const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
+        k2_write(M, C, b, ge[q], (uint32_t)i, gin[q], false, w0, 0);
+        w0 += gin[q];
+      }
     }
   } else if (partition && run) {
     // ---- the next chunk of the sorted run: per-node slot tables, chunk bounds
@@ -309,10 +388,22 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     }
   }
   PH_MARK(1);
+  if (slot_role) BLK_MARK(42, c_win);
   publish_min<TB>(R, tmn, wnd);
   digest = wave_sum64(digest);
-  if ((threadIdx.x & 63) == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
+  {  // one digest atomic per block
+    __shared__ uint64_t s_dg[TB / 64];
+    if ((threadIdx.x & 63) == 0) s_dg[threadIdx.x >> 6] = digest;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t dg = 0;
+      for (int w = 0; w < TB / 64; w++) dg += s_dg[w];
+      if (dg) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)dg);
+    }
+  }
   PH_MARK(2);
+  if (slot_role) BLK_MARK(44, c_win);  // publish_min, digest
+  BLK_REC(0, c_win);
 }
 
 // ---- k2_handle: holders ----
@@ -320,19 +411,34 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 // the hub's list), so that every block of the launch is resident at once.
 constexpr int K2_LDS_WORDS = HB * CH * 3;  // 12 KB: >= HUBL * 3 words
 static_assert(HUBL * 3 <= K2_LDS_WORDS, "hub list does not fit the shared buffer");
+// Run control a window kernel reads, loaded once at its entry (all fields at once: one memory trip).
+struct HCtl {
+  uint64_t tmin, inline_lim, slo, shi;
+};
+// Slot i0's window record, loaded ahead (speculatively at base 0; reloaded for a run chunk).
+struct SlotPre {
+  uint32_t widx, ctx, kind, a;
+  uint64_t key;
+};
 __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i0, uint32_t W, uint32_t base, Red &R,
-                                             uint32_t *lds) {
+                                             uint32_t *lds, const HCtl &hc, SlotPre sp) {
   uint32_t *chs = lds;
   uint64_t *chk = reinterpret_cast<uint64_t *>(lds + HB * CH);
   uint64_t tmn = ~0ull, wnd = ~0ull;
   HStat hs{0, 0, 0, 0, false};
-  const uint32_t wi = i0 < W ? M.widx[i0] : 1u;
+  if (base != 0 && i0 < W) {
+    sp.ctx = M.wctx[base + i0];
+    sp.kind = M.wkind[base + i0];
+    sp.a = M.wa[base + i0];
+    sp.key = M.wkey[base + i0];
+  }
+  const uint32_t wi = i0 < W ? sp.widx : 1u;
   if (wi == NOHOLD) {  // NetDevice::Start: dispatched, no children
     M.nchild[i0] = 0;
     M.ninl[i0] = 0;
   }
   if (wi == 0) {  // the holder
-    const uint32_t c = lp_of(M, M.wctx[base + i0], M.wkind[base + i0], M.wa[base + i0]);
+    const uint32_t c = lp_of(M, sp.ctx, sp.kind, sp.a);
     uint32_t n = 1;
     int32_t sink = -1;
     if (c < M.n_nodes) {
@@ -341,7 +447,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
     }
     if (n <= (uint32_t)CH) {  // (a hub's events are its hub block's)
       if (c < M.n_nodes) M.node_cnt[c] = 0;
-      const uint64_t key0 = M.wkey[base + i0];
+      const uint64_t key0 = sp.key;
       uint32_t *my = &chs[threadIdx.x * CH];
       uint64_t *mk = &chk[threadIdx.x * CH];
       my[0] = i0;
@@ -370,7 +476,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
           mk[bb] = kv;
         }
       }
-      const uint64_t tmin = C.tmin, inline_lim = C.inline_lim, slo = C.split_lo, shi = C.split_hi;
+      const uint64_t tmin = hc.tmin, inline_lim = hc.inline_lim, slo = hc.slo, shi = hc.shi;
       Emit E;
       E.ctx = c;
       E.ch_ts = M.ch_ts;
@@ -726,7 +832,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
 // order, the device state in registers.  Node parts never read device state and device steps never
 // read node state (node_part), so this is the sequential order's result.
 __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32_t base, bool sorted, Red &R,
-                         uint32_t hb, uint32_t *lds) {
+                         uint32_t hb, uint32_t *lds, const HCtl &hc) {
   const int lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1ull;
   uint64_t *gk = M.hub_key + (uint64_t)hb * WCAP;
@@ -760,7 +866,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     }
     __syncthreads();
   }
-  const uint64_t tmin = C.tmin, inline_lim = C.inline_lim, slo = C.split_lo, shi = C.split_hi;
+  const uint64_t tmin = hc.tmin, inline_lim = hc.inline_lim, slo = hc.slo, shi = hc.shi;
   const int32_t sink = M.sink_of_node[c];
   Emit E;
   E.ctx = c;
@@ -954,9 +1060,9 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
 }
 
 // ---- k2_handle: pool maintenance (tombstones, free slots, fresh children -> pool) ----
-__device__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool handle, uint32_t W) {
+__device__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool handle, uint32_t W, uint64_t nfree,
+                         uint64_t nF, uint64_t Pe) {
   const uint64_t tstride = (uint64_t)NMB * HB;
-  const uint64_t nfree = C.nfree, nF = C.nF, Pe = C.P_end;
   if (!run) {
     for (uint64_t w0 = (uint64_t)mb * HB; w0 < W; w0 += tstride) {  // wave-uniform
       const uint64_t s = w0 + threadIdx.x;
@@ -994,52 +1100,83 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds64);
   PH_BEGIN();
   Ctl &C = *M.C;
-  if (C.done || C.mode >= MODE_SORT) {
-    if (C.done == 1 && blockIdx.x == 0 && threadIdx.x == 0) C.done = 2;  // the final window is appended
+  BLK_T0();
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t c_win = C.windows;
+#endif
+  // the run control and (holder blocks) the slot's record, all loaded at once
+  const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_wbase = C.wbase, c_fr = C.force_run, rt = C.rt,
+                 c_nhub = C.nhub;
+  const HCtl hc{C.tmin, C.inline_lim, C.split_lo, C.split_hi};
+  const uint64_t c_nfree = C.nfree, c_nF = C.nF, c_Pe = C.P_end;
+  const uint32_t bx = blockIdx.x;
+  SlotPre sp{1u, 0, 0, 0, 0};
+  if (bx < (uint32_t)NHB) {
+    const uint32_t i0 = bx * HB + threadIdx.x;
+    sp = SlotPre{M.widx[i0], M.wctx[i0], M.wkind[i0], M.wa[i0], M.wkey[i0]};
+  }
+  if (c_done || c_mode >= MODE_SORT) {
+    if (c_done == 1 && blockIdx.x == 0 && threadIdx.x == 0) C.done = 2;  // the final window is appended
     return;
   }
-  const bool run = C.mode == MODE_RUN;
-  const uint32_t W = C.W, base = run ? C.wbase : 0;
-  const bool handle = run || (W <= (uint32_t)WCAP && !C.force_run);
-  Red &R = C.red[C.rt];
-  const uint32_t bx = blockIdx.x;
+  const bool run = c_mode == MODE_RUN;
+  const uint32_t base = run ? c_wbase : 0;
+  const bool handle = run || (W <= (uint32_t)WCAP && !c_fr);
+  Red &R = C.red[rt];
   PH_MARK(8);
   if (bx < (uint32_t)NHB) {
-    if (handle) handle_node2(M, C, bx * HB + threadIdx.x, W, base, R, lds);
+    if (handle) handle_node2(M, C, bx * HB + threadIdx.x, W, base, R, lds, hc, sp);
   } else if (bx < (uint32_t)(NHB + NRB)) {
     if (!run && handle) rank_tile(M, C, bx - NHB);
   } else if (bx < (uint32_t)(NHB + NRB + NHUB)) {
     if (handle) {
       const uint32_t hb = bx - (NHB + NRB);
-      const uint32_t nh = C.nhub < (uint32_t)MAXHUB ? C.nhub : (uint32_t)MAXHUB;
-      for (uint32_t h = hb; h < nh; h += NHUB) hub_node(M, C, M.hub_list[h], W, base, run, R, hb, lds);
+      const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
+      for (uint32_t h = hb; h < nh; h += NHUB) hub_node(M, C, M.hub_list[h], W, base, run, R, hb, lds, hc);
     }
   } else {
-    maintain(M, C, bx - (NHB + NRB + NHUB), run, handle, W);
+    maintain(M, C, bx - (NHB + NRB + NHUB), run, handle, W, c_nfree, c_nF, c_Pe);
   }
   PH_MARK(9);
+  BLK_REC(1, c_win);
 }
 
 // ---- k2_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
 __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   Ctl &C = *M.C;
-  if (C.done || C.mode >= MODE_SORT) return;
   constexpr int RPT = WCAP / SCAN_THREADS;
   __shared__ uint32_t l_slot[WCAP], l_cnt[WCAP], l_rel[WCAP], gstart[WCAP];
   PH_BEGIN();
+  BLK_T0();
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t c_win = C.windows;
+#endif
   const int tid = threadIdx.x;
-  const bool run = C.mode == MODE_RUN;
-  const uint32_t W = C.W;
-  const bool handled = run || (W <= (uint32_t)WCAP && !C.force_run);
-  const uint32_t base = run ? C.wbase : 0;
+  // the run control and the window's slots (speculatively at base 0), all loaded at once
+  const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run, c_wbase = C.wbase;
+  const uint32_t c_nhub = C.nhub;
+  const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
+  uint32_t pr[RPT], pc[RPT], pctx[RPT];
+  uint64_t pkey[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t i = tid + q * SCAN_THREADS;
+    pr[q] = M.wrank[i];
+    pc[q] = M.nchild[i] | (M.ninl[i] << 16);
+    pkey[q] = M.wkey[i];
+    pctx[q] = M.wctx[i];
+  }
+  if (c_done || c_mode >= MODE_SORT) return;
+  const bool run = c_mode == MODE_RUN;
+  const bool handled = run || (W <= (uint32_t)WCAP && !c_fr);
+  const uint32_t base = run ? c_wbase : 0;
   // ---- pool bookkeeping: the free stack loses the slots the fresh children took and gains the
   // window's; its pushed part is moved down over the popped hole
-  const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
   const uint64_t consumed = nF < nfree ? nF : nfree;
   const uint64_t mv = consumed < npush ? consumed : npush;
   for (uint64_t i = tid; i < mv; i += SCAN_THREADS) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
   if (handled) {
-    const uint32_t nh = C.nhub < (uint32_t)MAXHUB ? C.nhub : (uint32_t)MAXHUB;
+    const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
     for (uint32_t h = tid; h < nh; h += SCAN_THREADS) M.node_cnt[M.hub_list[h]] = 0;
   }
   if (!handled) {  // the window overflowed WCAP: it becomes a sorted run (host radix sort), nothing dispatched yet
@@ -1061,15 +1198,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     }
     return;
   }
-  uint32_t pr[RPT], pc[RPT], pctx[RPT];
-  uint64_t pkey[RPT];
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t i = tid + q * SCAN_THREADS;
-    pr[q] = run ? i : M.wrank[i];
-    pc[q] = M.nchild[i] | (M.ninl[i] << 16);
-    pkey[q] = i < W ? M.wkey[base + i] : 0;  // (a run's last chunk ends before the array does)
-    pctx[q] = i < W ? M.wctx[base + i] : 0;
+    if (run) pr[q] = i;
+    if (base != 0 && i < W) {
+      pkey[q] = M.wkey[base + i];
+      pctx[q] = M.wctx[base + i];
+    }
+    if (i >= W) pkey[q] = pctx[q] = 0;  // (a run's last chunk ends before the array does)
   }
   PH_MARK(16);
 #pragma unroll
@@ -1204,6 +1341,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     }
   }
   PH_MARK(20);
+  BLK_REC(2, c_win);
 }
 
 // ================================ host-driven steps (rare) ================================

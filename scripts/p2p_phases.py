@@ -21,13 +21,11 @@ nsgpu.check(nsgpu.lib().nsgpu_p2p_last_run_ms(eng.h, C.byref(ms)))
 nsgpu.check(nsgpu.lib().nsgpu_p2p_phase_read(buf.ctypes.data, 64, 1))
 w = max(int(st.windows), 1)
 print(f"grid {n}: {st.dispatched} events, {w} windows, {ms.value:.1f} ms ({1e3 * ms.value / w:.2f} us/window)")
-names = {0: "k_pa: entry->ctl", 1: "k_pa: sweep", 2: "k_pa: publish_min+digest",
-         8: "handle_rank: entry->ctl", 9: "handle_rank: body (block 0)",
-         12: "handle: holder+node_cnt (lane max)", 13: "handle: gather+sort (lane max)",
-         14: "handle: event loop (lane max)",
-         16: "scan: entry->W", 17: "scan: slot loads+lds", 18: "scan: scan", 19: "scan: sinfo stores",
-         20: "scan: bookkeeping", 24: "append: entry->ctl", 25: "append: body", 26: "append: publish"}
+names = {0: "k2_pa: entry -> last-window slot loads", 1: "k2_pa: append + partition", 2: "k2_pa: publish_min+digest",
+         8: "k2_handle: entry -> ctl (block 0)", 9: "k2_handle: body (block 0: holders)",
+         16: "k2_scan: entry -> slot loads", 17: "k2_scan: rank scatter to LDS", 18: "k2_scan: scan",
+         19: "k2_scan: sinfo stores", 20: "k2_scan: bookkeeping"}
 for i, nm in names.items():
     print(f"  {nm:32s} {buf[i] * 10.0 / w / 1e3:8.3f} us/window")
-print(f"  holders in block 0: {buf[15] / w:.1f} per window")
-print(f"  max handle thread {buf[10] * 10.0 / 1e3:.2f} us, max rank thread {buf[11] * 10.0 / 1e3:.2f} us")
+prof = eng.profile(sample_every=4)
+print("  kernel us/launch (hipExtLaunchKernel events):", {k: round(v[0] * 1e3, 2) for k, v in prof.items()})
