@@ -139,12 +139,19 @@ typedef struct nsgpu_p2p_scenario {
    *   NSGPU_SETUP_STOP     Simulator::Stop (t)    -> Schedule (t, &Simulator::Stop), context 0xffffffff
    *   NSGPU_SETUP_UID      any other setup call that consumes one uid without a dispatched event */
   uint32_t n_setup;
-  uint32_t pad_;
+  /* 1: ICMP errors are generated (Ipv4L3Protocol::IpForward TTL expiry -> Icmpv4L4Protocol::
+   * SendTimeExceededTtl, LocalDeliver RX_ENDPOINT_UNREACH -> SendDestUnreachPort; ipv4-l3-protocol.cc,
+   * icmpv4-l4-protocol.cc:85-160) and routed back to the offending datagram's sender through
+   * app_src_slot; the lookahead then also covers the 58-byte ICMP frames.  0: the triggers are only
+   * counted (ttl_drops / unreach_drops), i.e. the scenario asserts they never happen. */
+  uint32_t icmp;
   const uint32_t *setup_kind;
   const uint32_t *setup_index;
   /* UdpEchoClient parameters (NULL when the scenario has no echo client) */
   const uint32_t *app_count;
   const int64_t  *app_interval_ns;
+  /* route-table slot of each sending application's own node: where an echo reply and (icmp = 1) an
+   * ICMP error about the application's datagrams are routed; 0xffffffff: none */
   const uint32_t *app_src_slot;
   /* Compressed next-hop table, used when `route` is NULL (large topologies: the dense table is
    * n_nodes x n_dst): node n forwards towards slot k through route_exc_dev[j] for the j in
@@ -156,8 +163,18 @@ typedef struct nsgpu_p2p_scenario {
   const uint32_t *route_exc_dev;
 } nsgpu_p2p_scenario;
 
-/* Packet descriptor flag: the datagram is an echo reply travelling back to its client (app). */
+/* Packet descriptor flags (the descriptor {app, ipid, size, ttl} of a datagram): an echo reply
+ * travelling back to its client (app) ... */
 #define NSGPU_PKT_REPLY 0x80000000u
+/* ... or an ICMP error about a datagram of flow (app & NSGPU_PKT_APP), travelling back to that datagram's
+ * sender: NSGPU_PKT_ICMP_UNREACH = destination unreachable (port), else time exceeded (TTL);
+ * NSGPU_PKT_ICMP_OF_REPLY = the offending datagram was an echo reply.  An ICMP descriptor packs the
+ * offending datagram's IPv4 header fields: ipid = own | offending << 16 (16 bits each), size = 56 (the
+ * ICMP packet's IPv4 length), ttl = own TTL | offending TTL << 8 | offending IPv4 length << 16. */
+#define NSGPU_PKT_ICMP 0x40000000u
+#define NSGPU_PKT_ICMP_UNREACH 0x20000000u
+#define NSGPU_PKT_ICMP_OF_REPLY 0x10000000u
+#define NSGPU_PKT_APP 0x0fffffffu
 
 /* ---------------- trace records (ascii / pcap replay) ----------------
  * One record per call of a default ascii trace sink of PointToPointHelper::EnableAsciiInternal
@@ -196,8 +213,9 @@ typedef struct nsgpu_p2p_stats {
   uint64_t ttl_drops;
   uint64_t no_route_drops;
   uint64_t max_window;
-  uint64_t unreach_drops;     /* UDP datagrams with no bound endpoint (ICMP port unreachable not modelled) */
+  uint64_t unreach_drops;     /* UDP datagrams with no bound endpoint */
   uint64_t refits;            /* GPU: windows cut back to the window capacity (0 for the oracle) */
+  uint64_t icmp_sent;         /* ICMP errors sent (scenario icmp = 1) */
 } nsgpu_p2p_stats;
 
 /* Per-device counters: Queue (queue.cc:61-200) + device. */

@@ -77,7 +77,7 @@ struct Ctl {
   uint64_t K;                          // dispatched so far (after the last scanned window)
   uint64_t tmin, bound, inline_lim;    // current window (k_pa / refit)
   uint64_t windows, max_window, last_ts, max_windows, refits;
-  uint64_t digest, cancelled, ttl_drops, no_route, unreach;
+  uint64_t digest, cancelled, ttl_drops, no_route, unreach, icmp;
   uint64_t pK0, ptmin, pinline_lim;    // the last scanned window, appended by the next k_pa
   uint32_t uid, cur, W, nxtP, overflow, prep, done, stop_seen;
   uint32_t puid0, pW, pvalid, pinl;
@@ -114,6 +114,7 @@ struct P2PDev {
   const int64_t *app_interval;               // UdpEchoClient Interval
   const uint32_t *node_app_off, *node_app_list;  // CSR: apps of each node in AddApplication order
   const int32_t *sink_of_node;                    // PacketSink of each node (-1: none)
+  uint32_t icmp;                                  // ICMP errors are generated (scenario icmp)
   int64_t lookahead[K_NKINDS];
   // model state
   uint32_t *dev_busy, *q_head, *q_count;
@@ -267,7 +268,7 @@ struct Emit {
 
 // Run statistics of one handler thread.
 struct HStat {
-  uint64_t cancelled, ttl_drops, no_route, unreach;
+  uint64_t cancelled, ttl_drops, no_route, unreach, icmp;
   bool stop;
 };
 
@@ -496,10 +497,38 @@ __device__ __forceinline__ void appobj_start(const P2PDev &M, Emit &E, uint32_t 
   if (M.app_stop[a] != 0) E.child(M.app_stop[a], E.ctx, K_APP_STOP, a, Pkt{0, 0, 0, 0});
 }
 
+// Addressing of a packet descriptor: the node it is addressed to and that node's route-table slot.
+// An echo reply (NSGPU_PKT_REPLY) travels back to its client's node; an ICMP error (NSGPU_PKT_ICMP) to the
+// offending datagram's sender (icmpv4-l4-protocol.cc:131-160: SendMessage (p, header.GetSource (), ...)).
+__device__ __forceinline__ uint32_t pkt_dst_node(const P2PDev &M, const Pkt &p) {
+  if (p.app & NSGPU_PKT_ICMP) {
+    const uint32_t fa = p.app & NSGPU_PKT_APP;
+    return (p.app & NSGPU_PKT_ICMP_OF_REPLY) ? M.app_dst_node[fa] : M.app_node[fa];
+  }
+  if (p.app & NSGPU_PKT_REPLY) return M.app_node[p.app & ~NSGPU_PKT_REPLY];
+  return M.app_dst_node[p.app];
+}
+__device__ __forceinline__ uint32_t pkt_dst_slot(const P2PDev &M, const Pkt &p) {
+  if (p.app & NSGPU_PKT_ICMP) {
+    const uint32_t fa = p.app & NSGPU_PKT_APP;
+    return (p.app & NSGPU_PKT_ICMP_OF_REPLY) ? M.app_dst_slot[fa] : M.app_src_slot[fa];
+  }
+  if (p.app & NSGPU_PKT_REPLY) return M.app_src_slot[p.app & ~NSGPU_PKT_REPLY];
+  return M.app_dst_slot[p.app];
+}
+// The ICMP error about datagram p (its IPv4 header as the error embeds it): Icmpv4TimeExceeded /
+// Icmpv4DestinationUnreachable + the 4-byte Icmpv4Header over the offending header and 8 payload bytes:
+// a 56-byte IPv4 packet with the default TTL 64 (icmpv4.cc:306-309,407-410; Ipv4L3Protocol::Send).
+__device__ __forceinline__ Pkt icmp_error(const Pkt &p, bool unreach) {
+  const uint32_t of = (p.app & NSGPU_PKT_REPLY) ? NSGPU_PKT_ICMP_OF_REPLY : 0u;
+  return Pkt{NSGPU_PKT_ICMP | (unreach ? NSGPU_PKT_ICMP_UNREACH : 0u) | of | (p.app & NSGPU_PKT_APP),
+             (p.ipid & 0xffffu) << 16, 56u, 64u | ((p.ttl & 0xffu) << 8) | (p.size << 16)};
+}
+
 // Ipv4 route lookup: the static next-hop device of node n towards the packet's destination.
-// An echo reply (NSGPU_PKT_REPLY) travels back to its client's node.
 __device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const Pkt &p) {
-  const uint32_t slot = (p.app & NSGPU_PKT_REPLY) ? M.app_src_slot[p.app & ~NSGPU_PKT_REPLY] : M.app_dst_slot[p.app];
+  const uint32_t slot = pkt_dst_slot(M, p);
+  if (slot == 0xffffffffu) return 0xffffffffu;
   if (M.route) return M.route[(uint64_t)n * M.n_dst + slot];
   // compressed: binary search of the node's exceptions (a dumbbell router holds one per leaf); a node
   // with an exception for every slot has them at their slot's position (ascending, distinct)
@@ -512,6 +541,19 @@ __device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const 
     else hi = mid;
   }
   return (lo < e1 && M.route_exc_slot[lo] == slot) ? M.route_exc_dev[lo] : M.route_def[n];
+}
+
+// Icmpv4L4Protocol::SendMessage (icmpv4-l4-protocol.cc:85-129): RouteOutput towards the error's
+// destination, then Ipv4L3Protocol::Send from node n (its m_identification++); no route: dropped.
+__device__ __forceinline__ Act icmp_act(const P2PDev &M, uint32_t n, Pkt e, HStat &hs) {
+  const uint32_t out = route_of(M, n, e);
+  if (out == 0xffffffffu) {
+    hs.no_route++;
+    return Act{ACT_NONE, 0, Pkt{0, 0, 0, 0}};
+  }
+  e.ipid |= M.node_ipid[n]++ & 0xffffu;
+  hs.icmp++;
+  return Act{ACT_SEND, out, e};
 }
 
 // One event: the kind-specific first phase (node part: node and application state, its own children),
@@ -539,12 +581,15 @@ __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t 
     const uint32_t n = M.dev_node[a];
     const bool reply = (p.app & NSGPU_PKT_REPLY) != 0;
     const uint32_t fa = p.app & ~NSGPU_PKT_REPLY;
-    if ((reply ? M.app_node[fa] : M.app_dst_node[p.app]) == n) {
+    if (pkt_dst_node(M, p) == n) {
       // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407): the bound endpoint is the
-      // client's own socket for an echo reply, else the node's PacketSink / UdpEchoServer
+      // client's own socket for an echo reply, else the node's PacketSink / UdpEchoServer.  An ICMP error
+      // ends in Icmpv4L4Protocol::Receive -> UdpL4Protocol::ReceiveIcmp (no event, no counter).
       const int32_t k = reply ? (int32_t)fa : sink;
-      if (k < 0 || !(M.app_flags[k] & 2u)) {  // no bound endpoint: RX_ENDPOINT_UNREACH
+      if (p.app & NSGPU_PKT_ICMP) {
+      } else if (k < 0 || !(M.app_flags[k] & 2u)) {  // no bound endpoint: RX_ENDPOINT_UNREACH
         hs.unreach++;
+        if (M.icmp) act = icmp_act(M, n, icmp_error(p, true), hs);  // SendDestUnreachPort (ip, copy)
       } else {
         // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120);
         // run inline for a PacketSink, queued for the echo applications (their HandleRead schedules)
@@ -557,8 +602,12 @@ __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t 
         hs.no_route++;
       } else {
         p.ttl -= 1;  // IpForward (:815-841)
-        if (p.ttl == 0) hs.ttl_drops++;
-        else act = Act{ACT_SEND, out, p};
+        if ((p.ttl & 0xffu) == 0) {
+          hs.ttl_drops++;  // (no ICMP about an ICMP message)
+          if (M.icmp && !(p.app & NSGPU_PKT_ICMP)) act = icmp_act(M, n, icmp_error(p, false), hs);
+        } else {
+          act = Act{ACT_SEND, out, p};
+        }
       }
     }
   } else if (kind == K_TX_COMPLETE) {
@@ -1112,7 +1161,7 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
   const uint32_t W = C.W;
   Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[C.windows & 1];
   uint64_t tmn = ~0ull, wnd = ~0ull;
-  HStat hs{0, 0, 0, 0, false};
+  HStat hs{0, 0, 0, 0, 0, false};
   uint32_t dtc = 0, dti = 0;  // partitioned: the X1 summary's child totals and largest key
   uint64_t dlk = 0;
 #ifdef NSGPU_PHASE_PROF
@@ -1280,6 +1329,7 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
   if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
   if (hs.no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)hs.no_route);
   if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
+  if (hs.icmp) atomicAdd((unsigned long long *)&C.icmp, (unsigned long long)hs.icmp);
 }
 
 __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_t t) {
@@ -1884,10 +1934,19 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
       return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: app %u: unknown kind %u", a, ak);
     } else {
       if (sc->app_dst_node[a] >= N || sc->app_dst_slot[a] >= sc->n_dst || sc->app_rate_bps[a] == 0 ||
-          sc->app_pkt_size[a] == 0 || sc->app_ttl[a] == 0 || sc->app_dst_node[a] == sc->app_node[a])
-        return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: OnOff %u: bad destination/rate/size/ttl", a);
+          sc->app_pkt_size[a] == 0 || sc->app_ttl[a] == 0 || sc->app_dst_node[a] == sc->app_node[a] ||
+          (sc->app_src_slot && sc->app_src_slot[a] != 0xffffffffu && sc->app_src_slot[a] >= sc->n_dst))
+        return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: OnOff %u: bad destination/rate/size/ttl/source slot", a);
       min_pkt = std::min(min_pkt, sc->app_pkt_size[a]);
     }
+    // SendRealOut fragments a datagram above the device MTU (ipv4-l3-protocol.cc:722-731; PointToPointNetDevice
+    // Mtu 1500): not modelled, so payloads are bounded by 1500 - 20 (IPv4) - 8 (UDP)
+    if (ak == NSGPU_APP_ECHO_CLIENT || ak == NSGPU_APP_ONOFF) {
+      if (sc->app_pkt_size[a] > 1472)
+        return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: app %u: %u-byte payload needs IPv4 fragmentation", a,
+                         sc->app_pkt_size[a]);
+    }
+    if (A > NSGPU_PKT_APP) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: more than 2^28 applications");
   }
   uint32_t maxapps = 0;
   for (uint32_t n = 0; n < N; n++) maxapps = std::max(maxapps, napps[n + 1]);
@@ -1898,8 +1957,11 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   const int64_t INFL = (int64_t)1 << 61;
   int64_t tx_min = INFL;
   if (min_pkt != 0xffffffffu)
-    for (uint32_t d = 0; d < D; d++)
+    for (uint32_t d = 0; d < D; d++) {
       tx_min = std::min(tx_min, seconds_to_ts(static_cast<double>(min_pkt + 30) * 8 / (double)sc->dev_bps[d]));
+      // an ICMP error is a 56-byte IPv4 packet (+2 PPP)
+      if (sc->icmp) tx_min = std::min(tx_min, seconds_to_ts(static_cast<double>(56 + 2) * 8 / (double)sc->dev_bps[d]));
+    }
   int64_t send_ivl = INFL;
   for (uint32_t a = 0; a < A; a++)
     if (sc->app_kind[a] == NSGPU_APP_ONOFF)
@@ -1961,12 +2023,13 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   {
     std::vector<uint32_t> cnt(A, 0), src(A, 0);
     std::vector<int64_t> ivl(A, 0);
-    for (uint32_t a = 0; a < A; a++)
+    for (uint32_t a = 0; a < A; a++) {
+      src[a] = sc->app_src_slot ? sc->app_src_slot[a] : 0xffffffffu;
       if (sc->app_kind[a] == NSGPU_APP_ECHO_CLIENT) {
         cnt[a] = sc->app_count[a];
         ivl[a] = sc->app_interval_ns[a];
-        src[a] = sc->app_src_slot[a];
       }
+    }
     TRY(dupload(h, &M.app_count, cnt.data(), A));
     TRY(dupload(h, &M.app_interval, ivl.data(), A));
     TRY(dupload(h, &M.app_src_slot, src.data(), A));
@@ -1976,6 +2039,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   const int32_t *sinkp;
   TRY(dupload(h, &sinkp, sink.data(), N));
   M.sink_of_node = sinkp;
+  M.icmp = sc->icmp ? 1u : 0u;
   // ---- state ----
   TRY(dalloc(h, &M.dev_busy, D));
   TRY(dalloc(h, &M.q_head, D));
@@ -2693,6 +2757,7 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
     stats->no_route_drops = c.no_route;
     stats->max_window = c.max_window;
     stats->unreach_drops = c.unreach;
+    stats->icmp_sent = c.icmp;
     stats->refits = c.refits;
   }
   if (error) *error = err;

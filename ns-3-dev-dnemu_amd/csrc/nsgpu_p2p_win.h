@@ -539,6 +539,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
   if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
   if (hs.no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)hs.no_route);
   if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
+  if (hs.icmp) atomicAdd((unsigned long long *)&C.icmp, (unsigned long long)hs.icmp);
 }
 
 // ---- k2_handle: hub blocks ----
@@ -639,8 +640,8 @@ __device__ __forceinline__ void device_act_cached(const P2PDev &M, Emit &E, cons
 __device__ __forceinline__ bool stateless_event(const P2PDev &M, uint32_t c, uint32_t kind, const Pkt &p) {
   if (kind == K_TX_COMPLETE || kind == K_DEV_START) return true;  // (NetDevice::Start: no-op)
   if (kind != K_RECEIVE) return false;
-  const bool reply = (p.app & NSGPU_PKT_REPLY) != 0;
-  return (reply ? M.app_node[p.app & ~NSGPU_PKT_REPLY] : M.app_dst_node[p.app]) != c;
+  if (M.icmp && (p.ttl & 0xffu) <= 1u) return false;  // a TTL expiry sends an ICMP error: m_identification++
+  return pkt_dst_node(M, p) != c;
 }
 
 __device__ __forceinline__ void bitonic_sort_lds(uint64_t *k, uint32_t *v, uint32_t n) {
@@ -1047,7 +1048,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   }
   publish_min<HB>(R, E.tmn, E.wnd);
   const uint64_t nr = wave_sum64(hs.no_route), td = wave_sum64(hs.ttl_drops), cn = wave_sum64(hs.cancelled),
-                 ur = wave_sum64(hs.unreach);
+                 ur = wave_sum64(hs.unreach), ic = wave_sum64(hs.icmp);
   const bool stop = __ballot(hs.stop) != 0;
   if (lane == 0) {
     if (stop) C.stop_seen = 1;
@@ -1055,6 +1056,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     if (td) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)td);
     if (nr) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)nr);
     if (ur) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)ur);
+    if (ic) atomicAdd((unsigned long long *)&C.icmp, (unsigned long long)ic);
   }
   __syncthreads();
 }

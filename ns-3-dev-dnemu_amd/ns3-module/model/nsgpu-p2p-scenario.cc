@@ -1,7 +1,6 @@
 /* -*- Mode:C++; c-file-style:"gnu"; indent-tabs-mode:nil; -*- */
 #include "nsgpu-p2p-scenario.h"
 #include "ns3/fatal-error.h"
-#include <deque>
 #include <algorithm>
 
 namespace ns3 {
@@ -9,6 +8,7 @@ namespace ns3 {
 NsgpuP2pScenario::NsgpuP2pScenario ()
   : m_nodes (0),
     m_nDst (0),
+    m_icmp (true),
     m_stop (-1),
     m_firstLink (true),
     m_engine (0)
@@ -44,6 +44,8 @@ NsgpuP2pScenario::Link (uint32_t a, uint32_t b, uint64_t bps, Time delay, uint32
   m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_DEVICE, da));
   m_dev.push_back (y);
   m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_DEVICE, db));
+  m_addr.resize (m_dev.size (), 0u);
+  m_ifindex.resize (m_dev.size (), 0u);
   if (m_firstLink)
     {
       m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_UID, 0u));  // ChannelListPriv's ScheduleDestroy
@@ -93,68 +95,61 @@ NsgpuP2pScenario::Stop (Time at)
 }
 
 void
-NsgpuP2pScenario::RouteShortestPaths (void)
+NsgpuP2pScenario::Assign (uint32_t da, uint32_t db, uint32_t network, uint32_t mask)
+{
+  m_nif.resize (m_nodes, 1u);
+  const uint32_t d[2] = {da, db};
+  for (int k = 0; k < 2; k++)
+    {
+      m_addr[d[k]] = (network & mask) + 1 + k;
+      m_ifindex[d[k]] = m_nif[m_dev[d[k]].node]++;
+    }
+}
+
+void
+NsgpuP2pScenario::SetIcmp (bool on)
+{
+  m_icmp = on;
+}
+
+void
+NsgpuP2pScenario::PopulateRoutingTables (void)
 {
   m_dstSlot.assign (m_nodes, 0xffffffffu);
   m_nDst = 0;
   for (size_t i = 0; i < m_app.size (); i++)
     {
-      if (m_app[i].kind == NSGPU_APP_ONOFF && m_dstSlot[m_app[i].dst] == 0xffffffffu)
+      if (m_app[i].kind == NSGPU_APP_ONOFF)
         {
           m_dstSlot[m_app[i].dst] = 0;  // mark; numbered below in node order
+          if (m_icmp)
+            {
+              m_dstSlot[m_app[i].node] = 0;  // an ICMP error goes back to the sender
+            }
         }
     }
+  std::vector<uint32_t> dst;
   for (uint32_t n = 0; n < m_nodes; n++)
     {
       if (m_dstSlot[n] != 0xffffffffu)
         {
           m_dstSlot[n] = m_nDst++;
+          dst.push_back (n);
         }
     }
-  std::vector<std::vector<std::pair<uint32_t, uint32_t> > > nb (m_nodes);  // (neighbour, device), device order
-  for (uint32_t d = 0; d < m_dev.size (); d++)
+  const size_t D = m_dev.size ();
+  std::vector<uint32_t> devNode (D), devPeer (D);
+  bool addressed = D > 0;
+  for (size_t d = 0; d < D; d++)
     {
-      nb[m_dev[d].node].push_back (std::make_pair (m_dev[m_dev[d].peer].node, d));
+      devNode[d] = m_dev[d].node, devPeer[d] = m_dev[d].peer;
+      addressed = addressed && m_addr[d] != 0;
     }
   m_route.assign ((size_t) m_nodes * std::max (m_nDst, 1u), 0xffffffffu);
-  for (uint32_t dst = 0; dst < m_nodes; dst++)
+  if (m_nDst > 0 && nsgpu_route_global (m_nodes, D, &devNode[0], &devPeer[0], addressed ? &m_addr[0] : 0,
+                                        addressed ? &m_ifindex[0] : 0, m_nDst, &dst[0], &m_route[0], 0) != NSGPU_OK)
     {
-      if (m_dstSlot[dst] == 0xffffffffu)
-        {
-          continue;
-        }
-      std::vector<int64_t> dist (m_nodes, -1);
-      std::deque<uint32_t> q;
-      dist[dst] = 0;
-      q.push_back (dst);
-      while (!q.empty ())
-        {
-          const uint32_t u = q.front ();
-          q.pop_front ();
-          for (size_t k = 0; k < nb[u].size (); k++)
-            {
-              if (dist[nb[u][k].first] < 0)
-                {
-                  dist[nb[u][k].first] = dist[u] + 1;
-                  q.push_back (nb[u][k].first);
-                }
-            }
-        }
-      for (uint32_t n = 0; n < m_nodes; n++)
-        {
-          if (n == dst || dist[n] < 0)
-            {
-              continue;
-            }
-          for (size_t k = 0; k < nb[n].size (); k++)  // devices in creation order: the lowest first
-            {
-              if (dist[nb[n][k].first] == dist[n] - 1)
-                {
-                  m_route[(size_t) n * m_nDst + m_dstSlot[dst]] = nb[n][k].second;
-                  break;
-                }
-            }
-        }
+      NS_FATAL_ERROR ("libnsgpu: " << nsgpu_last_error ());
     }
 }
 
@@ -174,7 +169,7 @@ NsgpuP2pScenario::CreateEngine (uint64_t poolCap, uint64_t logCap)
       devNode[d] = m_dev[d].node, devPeer[d] = m_dev[d].peer, devQmax[d] = m_dev[d].qmax;
       devBps[d] = m_dev[d].bps, devIfg[d] = m_dev[d].ifg, devDelay[d] = m_dev[d].delay;
     }
-  std::vector<uint32_t> kind (A), node (A), dst (A), slot (A), size (A), maxb (A), ttl (A), zero (A, 0);
+  std::vector<uint32_t> kind (A), node (A), dst (A), slot (A), src (A), size (A), maxb (A), ttl (A), zero (A, 0);
   std::vector<int64_t> start (A), stop (A), ivl (A, 0);
   std::vector<uint64_t> rate (A);
   std::vector<double> on (A), off (A);
@@ -183,6 +178,7 @@ NsgpuP2pScenario::CreateEngine (uint64_t poolCap, uint64_t logCap)
       const App &a = m_app[i];
       kind[i] = a.kind, node[i] = a.node, dst[i] = a.dst, size[i] = a.size, maxb[i] = a.maxBytes, ttl[i] = a.ttl;
       slot[i] = a.kind == NSGPU_APP_ONOFF ? m_dstSlot[a.dst] : 0;
+      src[i] = a.kind == NSGPU_APP_ONOFF ? m_dstSlot[a.node] : 0xffffffffu;
       start[i] = a.start, stop[i] = a.stop, rate[i] = a.rate, on[i] = a.on, off[i] = a.off;
     }
   std::vector<uint32_t> sk (m_setup.size ()), si (m_setup.size ());
@@ -201,8 +197,9 @@ NsgpuP2pScenario::CreateEngine (uint64_t poolCap, uint64_t logCap)
   sc.app_kind = &kind[0], sc.app_node = &node[0], sc.app_start_ns = &start[0], sc.app_stop_ns = &stop[0];
   sc.app_dst_node = &dst[0], sc.app_dst_slot = &slot[0], sc.app_rate_bps = &rate[0], sc.app_pkt_size = &size[0];
   sc.app_on_s = &on[0], sc.app_off_s = &off[0], sc.app_max_bytes = &maxb[0], sc.app_ttl = &ttl[0];
-  sc.app_count = &zero[0], sc.app_interval_ns = &ivl[0], sc.app_src_slot = &zero[0];
+  sc.app_count = &zero[0], sc.app_interval_ns = &ivl[0], sc.app_src_slot = &src[0];
   sc.stop_ns = m_stop;
+  sc.icmp = m_icmp ? 1u : 0u;
   sc.n_setup = m_setup.size ();
   sc.setup_kind = &sk[0];
   sc.setup_index = &si[0];

@@ -35,8 +35,17 @@ public:
   uint32_t AddOnOff (uint32_t node, uint32_t dstNode, Time start, Time stop, uint64_t rateBps, uint32_t packetSize,
                      double onSeconds, double offSeconds, uint32_t maxBytes, uint32_t ttl);
   void Stop (Time at);
-  /* IPv4 next hops: shortest paths towards every flow destination (fewest hops, lowest device first) */
-  void RouteShortestPaths (void);
+  /* Ipv4AddressHelper (network, mask).Assign on the two devices of a link (host .1 on a, .2 on b) and
+   * Ipv4L3Protocol::AddInterface's interface numbering (the loopback is interface 0) */
+  void Assign (uint32_t da, uint32_t db, uint32_t network, uint32_t mask = 0xffffff00u);
+  /* InternetStackHelper installs Icmpv4L4Protocol: TTL expiries and unbound arrivals send ICMP errors back
+   * to the sender (icmpv4-l4-protocol.cc:131-165).  On by default, as in the reference. */
+  void SetIcmp (bool on);
+  /* Ipv4GlobalRoutingHelper::PopulateRoutingTables on the GPU (nsgpu_route_global): next hops towards every
+   * flow destination and, with ICMP, every sender.  With every device addressed the ties are global
+   * routing's (lowest peer address, then interface); an unaddressed topology takes the lowest device. */
+  void PopulateRoutingTables (void);
+  void RouteShortestPaths (void) { PopulateRoutingTables (); }
   /* The engine (owned by this object); `poolCap` / `logCap` as nsgpu_p2p_create's */
   nsgpu_p2p *CreateEngine (uint64_t poolCap, uint64_t logCap);
 
@@ -62,7 +71,10 @@ private:
   std::vector<std::pair<uint32_t, uint32_t> > m_setup;  // (nsgpu_setup_kind, index), program order
   std::vector<uint32_t> m_route;                        // [node][slot]
   std::vector<uint32_t> m_dstSlot;                      // node -> route slot (0xffffffff: none)
+  std::vector<uint32_t> m_addr, m_ifindex;              // per device (address 0: unassigned)
+  std::vector<uint32_t> m_nif;                          // next interface index per node
   uint32_t m_nDst;
+  bool m_icmp;
   int64_t m_stop;
   bool m_firstLink;
   nsgpu_p2p *m_engine;

@@ -39,7 +39,7 @@ class ScenarioStruct(C.Structure):
         ("app_stop_ns", C.c_void_p), ("app_dst_node", C.c_void_p), ("app_dst_slot", C.c_void_p),
         ("app_rate_bps", C.c_void_p), ("app_pkt_size", C.c_void_p), ("app_on_s", C.c_void_p),
         ("app_off_s", C.c_void_p), ("app_max_bytes", C.c_void_p), ("app_ttl", C.c_void_p),
-        ("stop_ns", C.c_int64), ("n_setup", C.c_uint32), ("pad_", C.c_uint32),
+        ("stop_ns", C.c_int64), ("n_setup", C.c_uint32), ("icmp", C.c_uint32),
         ("setup_kind", C.c_void_p), ("setup_index", C.c_void_p),
         ("app_count", C.c_void_p), ("app_interval_ns", C.c_void_p), ("app_src_slot", C.c_void_p),
         ("route_default", C.c_void_p), ("route_exc_off", C.c_void_p), ("route_exc_slot", C.c_void_p),
@@ -51,7 +51,7 @@ class P2PStats(C.Structure):
     _fields_ = [("dispatched", C.c_uint64), ("cancelled", C.c_uint64), ("digest", C.c_uint64),
                 ("final_ts", C.c_uint64), ("next_uid", C.c_uint32), ("windows", C.c_uint32),
                 ("ttl_drops", C.c_uint64), ("no_route_drops", C.c_uint64), ("max_window", C.c_uint64),
-                ("unreach_drops", C.c_uint64), ("refits", C.c_uint64)]
+                ("unreach_drops", C.c_uint64), ("refits", C.c_uint64), ("icmp_sent", C.c_uint64)]
 
 
 DEV_COUNTERS_DTYPE = np.dtype([("enq_packets", "<u4"), ("enq_bytes", "<u4"), ("drop_packets", "<u4"),
@@ -64,7 +64,8 @@ APP_COUNTERS_DTYPE = np.dtype([("tx_packets", "<u4"), ("rx_packets", "<u4"), ("t
 class Scenario:
     """Arrays of a nsgpu_p2p_scenario plus the order of setup-time Schedule calls."""
 
-    def __init__(self, n_nodes):
+    def __init__(self, n_nodes, icmp=False):
+        self.icmp = icmp  # ICMP errors generated and routed back to senders (nsgpu_p2p_scenario.icmp)
         self.n_nodes = 0
         self.dev = []     # (node, peer, bps, ifg, delay, qmax)
         self.apps = []    # dicts
@@ -144,9 +145,11 @@ class Scenario:
             self._nif[node] = self.dev_ifindex[d] + 1
 
     def _slot_nodes(self):
-        # route-table columns: every datagram destination (sender apps' dst), and echo clients' own nodes
+        # route-table columns: every datagram destination (sender apps' dst), echo clients' own nodes, and
+        # with ICMP every sender's node (an error goes back to the offending datagram's sender)
         return sorted({a["dst"] for a in self.apps if a["kind"] in SENDERS}
-                      | {a["node"] for a in self.apps if a["kind"] == APP_ECHO_CLIENT})
+                      | {a["node"] for a in self.apps if a["kind"] == APP_ECHO_CLIENT or
+                         (self.icmp and a["kind"] in SENDERS)})
 
     def stop(self, t_ns):  # Simulator::Stop (t)
         self.stop_ns = t_ns
@@ -242,7 +245,7 @@ class Scenario:
                                   np.uint32),
             app_count=np.array([a["count"] for a in A], np.uint32),
             app_interval_ns=np.array([a["interval"] for a in A], np.int64),
-            app_src_slot=np.array([self.dst_slot.get(a["node"], 0) if a["kind"] == APP_ECHO_CLIENT else 0
+            app_src_slot=np.array([self.dst_slot.get(a["node"], NO_ROUTE) if a["kind"] in SENDERS else NO_ROUTE
                                    for a in A], np.uint32),
             app_rate_bps=np.array([a["rate"] for a in A], np.uint64),
             app_pkt_size=np.array([a["size"] for a in A], np.uint32),
@@ -265,6 +268,7 @@ class Scenario:
             setattr(s, k, v.ctypes.data if v.size else None)
         s.stop_ns = self.stop_ns
         s.n_setup = len(self.setup)
+        s.icmp = 1 if self.icmp else 0
         s._keep = arrays  # keep the arrays alive with the struct
         return s
 
@@ -395,12 +399,12 @@ def dumbbell_owner(n_leaves, nranks=2):
 
 def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="columns", start_ns=100_000_000,
          stop_ns=2_000_000_000, sim_stop_ns=2_100_000_000, rate_bps=500_000, size=512, on_s=1e9, off_s=0.0,
-         ttl=255, n_flows=None):
+         ttl=255, n_flows=None, icmp=False):
     """PointToPointGridHelper topology (point-to-point-grid.cc:33-72) with OnOff/PacketSink flows.
 
     flows="columns": one flow per column from row 0 to the last row (SURVEY §8(d) config 4);
     routes are XY (row first, then column) static next hops."""
-    sc = Scenario(0)
+    sc = Scenario(0, icmp=icmp)
     nid = lambda y, x: y * cols + x  # noqa: E731
     n = rows * cols
     # the device of each node towards its four grid neighbours (XY routing's next hops)
@@ -443,8 +447,9 @@ def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="column
         sc.add_onoff(s_, d, start_ns, stop_ns, rate_bps=rate_bps, size=size, on_s=on_s, off_s=off_s, ttl=ttl,
                      remote_addr=raddr)
     sc.stop(sim_stop_ns)
-    # XY routes towards each destination: along the row first, then along the column
-    dsts = sorted({d for _s, d in fl})
+    # XY routes towards each destination (with ICMP also towards every source): along the row first,
+    # then along the column — global routing's choice on this helper's addressing (test_routing_oracle.py)
+    dsts = sc._slot_nodes()
     sc.dst_slot = {d: i for i, d in enumerate(dsts)}
     sc.n_dst = max(1, len(dsts))
     R = np.full((n, sc.n_dst), NO_ROUTE, dtype=np.uint32)
@@ -459,10 +464,13 @@ def grid(rows, cols, bps=10_000_000, delay_ns=1_000_000, qmax=100, flows="column
 
 
 def random_topology(n_nodes, n_links, n_flows, seed, bps_choices=(1_000_000, 5_000_000, 10_000_000),
-                    delay_choices=(100_000, 1_000_000, 2_000_000), qmax=20, stop_ns=1_000_000_000):
-    """Connected random topology with OnOff flows (on/off cycling, max bytes) for parity tests."""
+                    delay_choices=(100_000, 1_000_000, 2_000_000), qmax=20, stop_ns=1_000_000_000, ttl=64,
+                    icmp=False, sink_window=None):
+    """Connected random topology with OnOff flows (on/off cycling, max bytes) for parity tests.
+    ttl: the flows' IP TTL (small values expire on long paths); sink_window: (start, stop) of every
+    PacketSink (late starts / early stops leave datagrams without a bound endpoint)."""
     rng = np.random.default_rng(seed)
-    sc = Scenario(n_nodes)
+    sc = Scenario(n_nodes, icmp=icmp)
     edges = set()
     for n in range(1, n_nodes):  # spanning tree
         m = int(rng.integers(0, n))
@@ -482,13 +490,14 @@ def random_topology(n_nodes, n_links, n_flows, seed, bps_choices=(1_000_000, 5_0
     sinks = {}
     for _s, d in flows:
         if d not in sinks:
-            sinks[d] = sc.add_sink(d, int(rng.integers(0, 50_000_000)), 0)
+            t0 = int(rng.integers(0, 50_000_000))
+            sinks[d] = sc.add_sink(d, *(sink_window if sink_window else (t0, 0)))
     for s_, d in flows:
         st = int(rng.integers(50_000_000, 300_000_000))
         sc.add_onoff(s_, d, st, int(st + rng.integers(200_000_000, 600_000_000)),
                      rate_bps=int(rng.choice([200_000, 500_000, 2_000_000])), size=int(rng.choice([64, 512, 1000])),
                      on_s=float(rng.choice([0.05, 0.1, 1.0])), off_s=float(rng.choice([0.0, 0.02, 0.05])),
-                     max_bytes=int(rng.choice([0, 0, 20000])), ttl=64)
+                     max_bytes=int(rng.choice([0, 0, 20000])), ttl=ttl)
     sc.stop(stop_ns)
     sc.route_bfs()
     return sc

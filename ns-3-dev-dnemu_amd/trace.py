@@ -29,6 +29,7 @@ import p2p
 
 TR_ENQUEUE, TR_DEQUEUE, TR_DROP, TR_RX = 0, 1, 2, 3
 PKT_REPLY = 0x80000000
+PKT_ICMP, PKT_ICMP_UNREACH, PKT_ICMP_OF_REPLY, PKT_APP = 0x40000000, 0x20000000, 0x10000000, 0x0FFFFFFF
 TRACE_RECORD_DTYPE = p2p.TRACE_RECORD_DTYPE  # nsgpu_trace_record
 _CHAR = {TR_ENQUEUE: "+", TR_DEQUEUE: "-", TR_DROP: "d", TR_RX: "r"}
 _SOURCE = {TR_ENQUEUE: "TxQueue/Enqueue", TR_DEQUEUE: "TxQueue/Dequeue", TR_DROP: "TxQueue/Drop", TR_RX: "MacRx"}
@@ -135,6 +136,31 @@ class Codec:
         d = int(self.sc.next_hop(node, self.slot[dst_node]))
         return self.sc.dev_addr.get(d, 0)
 
+    def _walk(self, node, dst_node, hops):
+        """The node a datagram from `node` towards `dst_node` reaches after `hops` hops."""
+        for _ in range(hops):
+            d = int(self.sc.next_hop(node, self.slot[dst_node]))
+            node = self.dev_node[int(self.sc.dev[d][1])]
+        return node
+
+    def icmp_fields(self, r):
+        """An ICMP error record (include/nsgpu_types.h NSGPU_PKT_ICMP): its own (src, dst) and the offending
+        datagram's embedded IPv4 header (src, dst, sport, dport, ttl, id, length)."""
+        a = int(r["app"])
+        fa = a & PKT_APP
+        of_reply = bool(a & PKT_ICMP_OF_REPLY)
+        A = self.sc.apps[fa]
+        osrc, odst, osp, odp = self.headers(fa | (PKT_REPLY if of_reply else 0))
+        sender, dest = (A["dst"], A["node"]) if of_reply else (A["node"], A["dst"])
+        if a & PKT_ICMP_UNREACH:  # LocalDeliver at the datagram's destination
+            origin = dest
+        else:  # IpForward where the TTL reached 0: the sender's TTL-th hop
+            t0 = self.sc.apps[self.echo_server[sender]]["ttl"] if of_reply else A["ttl"]
+            origin = self._walk(sender, dest, t0)
+        own_src = self._out_addr(origin, sender)
+        return own_src, osrc, (osrc, odst, osp, odp, (int(r["ttl"]) >> 8) & 255, int(r["ipid"]) >> 16,
+                               int(r["ttl"]) >> 16)
+
     def headers(self, app_word):
         """(src, dst, sport, dport) of a datagram of flow app_word."""
         a = app_word & ~PKT_REPLY
@@ -146,7 +172,15 @@ class Codec:
         return req_src, req_dst, self.eport[a], A["remote_port"]
 
     # ---------------- ascii ----------------
+    @staticmethod
+    def _ipv4_text(ttl, ipid, proto, length, src, dst):
+        """Ipv4Header::Print (ipv4-header.cc:301-338, this fork's DSCP/ECN fields)."""
+        return ("tos 0x0 DSCP Default ECN Not-ECT ttl %d id %d protocol %d offset (bytes) 0 flags [none] length: %d "
+                "%s > %s" % (ttl & 255, ipid & 0xffff, proto, length, dotted(src), dotted(dst)))
+
     def packet_text(self, r):
+        if int(r["app"]) & PKT_ICMP:
+            return self.icmp_text(r)
         src, dst, sp, dp = self.headers(int(r["app"]))
         ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
         parts = []
@@ -157,6 +191,24 @@ class Codec:
                                                            dotted(src), dotted(dst)))
         parts.append("ns3::UdpHeader (length: %d %d > %d)" % (ip_len - 20, sp, dp))
         parts.append("Payload (size=%d)" % (ip_len - 28))
+        return " ".join(parts)
+
+    def icmp_text(self, r):
+        """Icmpv4Header::Print + Icmpv4TimeExceeded / Icmpv4DestinationUnreachable::Print (icmpv4.cc:91-94,
+        336-347, 435-446): the embedded header, then " org data=" and its 8 payload bytes, each followed
+        by a space."""
+        own_src, own_dst, (osrc, odst, osp, odp, ottl, oid, olen) = self.icmp_fields(r)
+        ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
+        unreach = bool(int(r["app"]) & PKT_ICMP_UNREACH)
+        data = struct.pack(">HHHH", osp, odp, olen - 20, 0)
+        parts = []
+        if r["kind"] != TR_RX:
+            parts.append("ns3::PppHeader (Point-to-Point Protocol: IP (0x0021))")
+        parts.append("ns3::Ipv4Header (%s)" % self._ipv4_text(int(r["ttl"]), int(r["ipid"]), 1, ip_len, own_src, own_dst))
+        parts.append("ns3::Icmpv4Header (type=%d, code=%d)" % ((3, 3) if unreach else (11, 0)))
+        parts.append("ns3::%s (%s org data=%s)" % (
+            "Icmpv4DestinationUnreachable" if unreach else "Icmpv4TimeExceeded",
+            self._ipv4_text(ottl, oid, 17, olen, osrc, odst), "".join("%d " % b for b in data)))
         return " ".join(parts)
 
     def ascii(self, tr):
@@ -172,6 +224,15 @@ class Codec:
     # ---------------- pcap ----------------
     def packet_bytes(self, r):
         """Serialized packet with its PPP header (what the sniffer sees)."""
+        if int(r["app"]) & PKT_ICMP:  # IPv4 (protocol 1) + Icmpv4Header + TimeExceeded / DestinationUnreachable
+            own_src, own_dst, (osrc, odst, osp, odp, ottl, oid, olen) = self.icmp_fields(r)
+            ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
+            unreach = bool(int(r["app"]) & PKT_ICMP_UNREACH)
+            ipv4 = struct.pack(">BBHHHBBHII", 0x45, 0, ip_len, int(r["ipid"]) & 0xffff, 0, int(r["ttl"]) & 255, 1, 0,
+                               own_src, own_dst)
+            icmp = struct.pack(">BBH", *((3, 3, 0) if unreach else (11, 0, 0))) + bytes(4)  # unused / next-hop MTU 0
+            org = struct.pack(">BBHHHBBHII", 0x45, 0, olen, oid & 0xffff, 0, ottl, 17, 0, osrc, odst)
+            return struct.pack(">H", 0x0021) + ipv4 + icmp + org + struct.pack(">HHHH", osp, odp, olen - 20, 0)
         src, dst, sp, dp = self.headers(int(r["app"]))
         ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
         ipv4 = struct.pack(">BBHHHBBHII", 0x45, 0, ip_len, int(r["ipid"]) & 0xffff, 0, int(r["ttl"]) & 255, 17, 0,

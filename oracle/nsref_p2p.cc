@@ -89,7 +89,13 @@ struct Model {
     r.ttl = p.ttl;
     trace->push_back(r);
   }
+  // The node a packet is addressed to: an echo reply goes back to its client, an ICMP error to the
+  // offending datagram's sender (icmpv4-l4-protocol.cc:131-160: SendMessage (p, header.GetSource (), ...)).
   uint32_t pkt_dst_node(const Pkt &p) const {
+    if (p.app & NSGPU_PKT_ICMP) {
+      const uint32_t fa = p.app & NSGPU_PKT_APP;
+      return (p.app & NSGPU_PKT_ICMP_OF_REPLY) ? s.app_dst_node[fa] : s.app_node[fa];
+    }
     return (p.app & NSGPU_PKT_REPLY) ? s.app_node[p.app & ~NSGPU_PKT_REPLY] : s.app_dst_node[p.app];
   }
   // static next hop of node n towards route slot k: the dense table, or the compressed one
@@ -105,10 +111,15 @@ struct Model {
     if (lo < s.route_exc_off[n + 1] && s.route_exc_slot[lo] == k) return s.route_exc_dev[lo];
     return s.route_default[n];
   }
+  uint32_t src_slot(uint32_t a) const { return s.app_src_slot ? s.app_src_slot[a] : 0xffffffffu; }
   uint32_t pkt_dst_slot(const Pkt &p) const {
-    return (p.app & NSGPU_PKT_REPLY) ? s.app_src_slot[p.app & ~NSGPU_PKT_REPLY] : s.app_dst_slot[p.app];
+    if (p.app & NSGPU_PKT_ICMP) {
+      const uint32_t fa = p.app & NSGPU_PKT_APP;
+      return (p.app & NSGPU_PKT_ICMP_OF_REPLY) ? s.app_dst_slot[fa] : src_slot(fa);
+    }
+    return (p.app & NSGPU_PKT_REPLY) ? src_slot(p.app & ~NSGPU_PKT_REPLY) : s.app_dst_slot[p.app];
   }
-  uint64_t ttl_drops = 0, no_route_drops = 0, unreach_drops = 0;
+  uint64_t ttl_drops = 0, no_route_drops = 0, unreach_drops = 0, icmp_sent = 0;
 
   template <class F>
   struct Ev : EventImpl {
@@ -192,12 +203,36 @@ struct Model {
   }
 
   // ---------------- IPv4 + UDP ----------------
+  // ---------------- ICMP (icmpv4-l4-protocol.cc:85-160, icmpv4.cc:306-440) ----------------
+  // The error about datagram p (p's IPv4 header as embedded: TTL, identification, length) is a 56-byte
+  // IPv4 packet (Icmpv4Header 4 + TimeExceeded / DestinationUnreachable 4 + header 20 + 8 payload bytes)
+  // sent from node n to p's sender with the default TTL 64: SendMessage -> RouteOutput ->
+  // Ipv4L3Protocol::Send (m_identification++); no route: "drop icmp message".
+  void icmp_send(uint32_t n, const Pkt &p, bool unreach) {
+    const uint32_t of = (p.app & NSGPU_PKT_REPLY) ? NSGPU_PKT_ICMP_OF_REPLY : 0u;
+    Pkt e{NSGPU_PKT_ICMP | (unreach ? NSGPU_PKT_ICMP_UNREACH : 0u) | of | (p.app & NSGPU_PKT_APP),
+          (p.ipid & 0xffffu) << 16, 56u, 64u | ((p.ttl & 0xffu) << 8) | (p.size << 16)};
+    const uint32_t k = pkt_dst_slot(e);
+    const uint32_t out = k == 0xffffffffu ? 0xffffffffu : next_hop(n, k);
+    if (out == 0xffffffffu) {
+      no_route_drops++;
+      return;
+    }
+    e.ipid |= node_ipid[n]++ & 0xffffu;
+    icmp_sent++;
+    device_send(out, e);
+  }
+
   void ip_receive(uint32_t n, Pkt p) {  // Ipv4L3Protocol::Receive -> RouteInput
     if (pkt_dst_node(p) == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
+      // an ICMP error ends in Icmpv4L4Protocol::Receive -> HandleTimeExceeded / HandleDestUnreach ->
+      // UdpL4Protocol::ReceiveIcmp -> the endpoint's (null) ICMP callback: nothing is scheduled
+      if (p.app & NSGPU_PKT_ICMP) return;
       // the bound endpoint: the client's own socket for an echo reply, else the node's sink / echo server
       const int32_t k = (p.app & NSGPU_PKT_REPLY) ? (int32_t)(p.app & ~NSGPU_PKT_REPLY) : sink_of_node[n];
       if (k < 0 || !app[k].sink_active) {  // no bound endpoint: RX_ENDPOINT_UNREACH
         unreach_drops++;
+        if (s.icmp) icmp_send(n, p, true);  // Ipv4L3Protocol::LocalDeliver: SendDestUnreachPort (ip, copy)
         return;
       }
       // Ipv4EndPoint::ForwardUp: ScheduleNow (&Ipv4EndPoint::DoForwardUp) (ipv4-end-point.cc:112-120)
@@ -222,8 +257,9 @@ struct Model {
     }
     // IpForward (ipv4-l3-protocol.cc:815-841)
     p.ttl -= 1;
-    if (p.ttl == 0) {  // DROP_TTL_EXPIRED (scenarios keep paths shorter than the TTL: no ICMP)
+    if ((p.ttl & 0xffu) == 0) {  // DROP_TTL_EXPIRED, after SendTimeExceededTtl (never about an ICMP message)
       ttl_drops++;
+      if (s.icmp && !(p.app & NSGPU_PKT_ICMP)) icmp_send(n, p, false);
       return;
     }
     device_send(out, p);
@@ -402,6 +438,7 @@ extern "C" int nsref_p2p_run_trace(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats
   stats->ttl_drops = m->ttl_drops;
   stats->no_route_drops = m->no_route_drops;
   stats->unreach_drops = m->unreach_drops;
+  stats->icmp_sent = m->icmp_sent;
   if (devc)
     for (uint32_t d = 0; d < sc->n_devices; d++) devc[d] = m->dev[d].c;
   if (appc)
@@ -454,6 +491,7 @@ extern "C" int nsref_p2p_run_probe(const nsgpu_p2p_scenario *sc, int64_t t0, int
   stats->ttl_drops = m->ttl_drops;
   stats->no_route_drops = m->no_route_drops;
   stats->unreach_drops = m->unreach_drops;
+  stats->icmp_sent = m->icmp_sent;
   if (devc)
     for (uint32_t d = 0; d < sc->n_devices; d++) devc[d] = m->dev[d].c;
   if (appc)
