@@ -101,6 +101,7 @@ struct P2PDev {
   // scenario
   uint32_t n_nodes, n_devices, n_apps, n_dst, qcap, maxc;
   const uint32_t *dev_node, *dev_peer, *dev_qmax;
+  const uint32_t *dev_peer_node;  // dev_node[dev_peer[d]] (one load instead of two dependent ones)
   const uint64_t *dev_bps;
   const int64_t *dev_ifg, *dev_delay;
   const uint32_t *route;  // dense [node][slot], or null: the compressed table below
@@ -316,7 +317,7 @@ __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &
   const uint64_t bps = M.dev_bps[d];
   const int64_t ifg = M.dev_ifg[d], delay = M.dev_delay[d];
   const uint32_t peer = M.dev_peer[d];
-  const uint32_t peer_node = M.dev_node[peer];
+  const uint32_t peer_node = M.dev_peer_node[d];
   Pkt *qb = M.q_buf + (uint64_t)d * M.qcap;
   uint32_t ncnt = cnt, nhead = head, nbusy = busy;
   bool go = false;
@@ -1995,6 +1996,11 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   // ---- scenario upload ----
   TRY(dupload(h, &M.dev_node, sc->dev_node, D));
   TRY(dupload(h, &M.dev_peer, sc->dev_peer, D));
+  {
+    std::vector<uint32_t> pn(D);
+    for (uint32_t d = 0; d < D; d++) pn[d] = sc->dev_node[sc->dev_peer[d]];
+    TRY(dupload(h, &M.dev_peer_node, pn.data(), D));
+  }
   TRY(dupload(h, &M.dev_qmax, sc->dev_qmax, D));
   TRY(dupload(h, &M.dev_bps, sc->dev_bps, D));
   TRY(dupload(h, &M.dev_ifg, sc->dev_ifg_ns, D));

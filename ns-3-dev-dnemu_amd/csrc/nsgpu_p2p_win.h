@@ -568,7 +568,7 @@ struct DevCache {
     ifg = M.dev_ifg[d];
     delay = M.dev_delay[d];
     peer = M.dev_peer[d];
-    peer_node = M.dev_node[peer];
+    peer_node = M.dev_peer_node[d];
     const uint32_t *w = reinterpret_cast<const uint32_t *>(&M.devc[d]);
     const uint4 a = *reinterpret_cast<const uint4 *>(w);
     const uint2 b2 = *reinterpret_cast<const uint2 *>(w + 4);
@@ -695,7 +695,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
   const int32_t c0 = busy0 ? (int32_t)cnt0 : -1;
   const uint64_t bps = M.dev_bps[d];
   const int64_t ifg = M.dev_ifg[d], delay = M.dev_delay[d];
-  const uint32_t peer = M.dev_peer[d], peer_node = M.dev_node[peer];
+  const uint32_t peer = M.dev_peer[d], peer_node = M.dev_peer_node[d];
   Pkt *qb = M.q_buf + (uint64_t)d * qcap;
   // pass A: the segment's composed map and its enqueue / dequeue counts
   CMap f{0, -CBIG, CBIG};
