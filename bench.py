@@ -477,8 +477,10 @@ def main():
     traffic = None
     tpath = os.path.join(REPO, "profiles", f"traffic_{args.workload}.json")
     if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+        try:  # the PMC passes' HBM bytes per launch of the kernel the roofline names (scripts/pmc_traffic.py)
+            tj = json.load(open(tpath))
+            short = rl["kernel"].split("::")[-1]
+            traffic = tj.get("kernels", {}).get(short, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 

@@ -17,6 +17,7 @@
 //   * partitioned (one rank per GPU, or a loopback group on one GPU): k_pa<true>, k_refit_d, X0,
 //     k_cut, k_handle_rank<true>, X1, k_gtile, k_dfin, X2 below.
 #include <hip/hip_ext.h>
+#include <stddef.h>
 #include "nsgpu_device.h"
 #include "nsgpu_internal.h"
 
@@ -46,11 +47,14 @@ constexpr int HB = 64;           // threads per block, per-slot kernels (spread 
 constexpr int NHB = WCAP / HB;   // handler blocks of k_handle_rank
 constexpr int RJ = 256;          // keys per rank tile column
 constexpr int NJT = WCAP / RJ;   // rank tile columns
-constexpr int NRB = NHB * NJT;   // rank tile blocks of k_handle_rank
+constexpr int RTR = 1;           // window keys (rows) per thread of a rank tile (4: same traffic, slower)
+constexpr int NRT = WCAP / (HB * RTR);  // rank tile rows
+constexpr int NRB = NRT * NJT;   // rank tile blocks (k2_handle)
 constexpr int GRID_POOL = 256;   // blocks of the pool sweep (grid-stride)
 constexpr int SCAN_THREADS = 1024;
 constexpr int CH = 16;           // events of one node a handler thread sorts in LDS
-constexpr int NSLOT = 8;         // per-node slot table entries
+constexpr int NSLOT = 7;         // per-node slot table entries
+constexpr int NTAB = NSLOT + 1;  // words per node table record (count + slots)
 constexpr int NWIN = 32;         // windows per graph replay
 constexpr uint32_t NOCTX = 0xffffffffu;
 constexpr uint32_t NOCHAIN = 0xffffffffu;
@@ -60,6 +64,21 @@ constexpr uint32_t NOCHAIN = 0xffffffffu;
 struct Pkt {
   uint32_t app, ipid, size, ttl;
 };
+
+// Per-device record of the transmit path: the tx state (busy, queue count / head), the static
+// parameters a TransmitStart / TransmitComplete reads and the device's counters, in ONE 128-B line —
+// a device step touches one line instead of eleven scattered SoA words (each a separate line fetch
+// from another XCD's writes: measured 2.8 -> 1.6 MB HBM fetch per k2_handle launch on config 4).
+struct DevRec {
+  uint32_t busy, cnt, head, qmax;  // PointToPointNetDevice m_txMachineState, DropTail count / ring head, MaxPackets
+  uint32_t peer, peer_node, pad0, pad1;
+  uint64_t bps;                    // DataRate
+  int64_t ifg, delay;              // InterframeGap, channel Delay
+  uint64_t pad2;
+  nsgpu_dev_counters c;            // (copied out strided by nsgpu_p2p_results / _counters)
+  uint64_t pad3[4];
+};
+static_assert(sizeof(DevRec) == 128 && offsetof(DevRec, c) == 64, "DevRec is one 128-B line");
 
 // Reduction of a pending set: the next window's bound (atomicMin), the pending Stop.
 struct Red {
@@ -100,10 +119,7 @@ struct Ctl {
 struct P2PDev {
   // scenario
   uint32_t n_nodes, n_devices, n_apps, n_dst, qcap, maxc;
-  const uint32_t *dev_node, *dev_peer, *dev_qmax;
-  const uint32_t *dev_peer_node;  // dev_node[dev_peer[d]] (one load instead of two dependent ones)
-  const uint64_t *dev_bps;
-  const int64_t *dev_ifg, *dev_delay;
+  const uint32_t *dev_node;
   const uint32_t *route;  // dense [node][slot], or null: the compressed table below
   const uint32_t *route_def, *route_exc_slot, *route_exc_dev;
   const uint64_t *route_exc_off;
@@ -118,9 +134,8 @@ struct P2PDev {
   uint32_t icmp;                                  // ICMP errors are generated (scenario icmp)
   int64_t lookahead[K_NKINDS];
   // model state
-  uint32_t *dev_busy, *q_head, *q_count;
+  DevRec *dev;  // per-device tx state + transmit parameters (one record per device)
   Pkt *q_buf;
-  nsgpu_dev_counters *devc;
   uint32_t *app_flags;    // bit0 started, bit1 sink active, bit2 send live, bit3 start/stop live
   uint32_t *app_send_gen, *app_ss_gen, *app_residual, *app_tot;
   uint32_t *node_ipid;    // Ipv4L3Protocol::m_identification per node
@@ -146,8 +161,9 @@ struct P2PDev {
   uint64_t *pwkey;
   uint32_t *pwctx;
   uint32_t *wrank;  // rank accumulators of the current window (0 between windows)
-  // per-node slot tables of the current window (node_cnt is 0 between windows)
-  uint32_t *node_cnt, *node_slot;
+  // per-node slot tables of the current window, one 32-B record per node: [0] the node's window
+  // events (0 between windows), [1 .. NSLOT] their first slots (one line per node, not two)
+  uint32_t *node_tab;
   // partitioned run (dist != 0): this engine owns the nodes n with owner[n] == rank
   uint32_t dist, rank, nranks, pad_d;
   const uint32_t *owner;
@@ -312,12 +328,13 @@ __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &
   if (act.op == ACT_NONE) return;
   const uint32_t d = act.dev;
   // every operand of the step at once
-  const uint32_t busy = M.dev_busy[d], cnt = M.q_count[d], head = M.q_head[d], qmax = M.dev_qmax[d];
-  nsgpu_dev_counters dc = M.devc[d];
-  const uint64_t bps = M.dev_bps[d];
-  const int64_t ifg = M.dev_ifg[d], delay = M.dev_delay[d];
-  const uint32_t peer = M.dev_peer[d];
-  const uint32_t peer_node = M.dev_peer_node[d];
+  const DevRec dr = M.dev[d];
+  const uint32_t busy = dr.busy, cnt = dr.cnt, head = dr.head, qmax = dr.qmax;
+  nsgpu_dev_counters dc = dr.c;
+  const uint64_t bps = dr.bps;
+  const int64_t ifg = dr.ifg, delay = dr.delay;
+  const uint32_t peer = dr.peer;
+  const uint32_t peer_node = dr.peer_node;
   Pkt *qb = M.q_buf + (uint64_t)d * M.qcap;
   uint32_t ncnt = cnt, nhead = head, nbusy = busy;
   bool go = false;
@@ -368,10 +385,10 @@ __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &
     E.child(txTime + ifg, E.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
     E.child(txTime + delay, peer_node, K_RECEIVE, peer, tx);
   }
-  if (nbusy != busy) M.dev_busy[d] = nbusy;
-  if (ncnt != cnt) M.q_count[d] = ncnt;
-  if (nhead != head) M.q_head[d] = nhead;
-  M.devc[d] = dc;
+  if (nbusy != busy) M.dev[d].busy = nbusy;
+  if (ncnt != cnt) M.dev[d].cnt = ncnt;
+  if (nhead != head) M.dev[d].head = nhead;
+  M.dev[d].c = dc;
 }
 
 // int64x64 residual-bits update of OnOffApplication::CancelEvents (onoff-application.cc:170-173):
@@ -574,12 +591,13 @@ __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t 
   Post post{false, 0, 0, 0};
   bool cancelled = false;
   if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive (ipv4-l3-protocol.cc:434-537)
-    if (rx_atomic) atomicAdd(&M.devc[a].rx_packets, 1u);
-    else M.devc[a].rx_packets++;
+    if (rx_atomic) atomicAdd(&M.dev[a].c.rx_packets, 1u);
+    else M.dev[a].c.rx_packets++;
     Pkt p = pkt;
     p.size -= 2;                             // ProcessHeader strips the PppHeader
     trace_call(M, E, NSGPU_TR_RX, a, p);     // m_macRxTrace
-    const uint32_t n = M.dev_node[a];
+    // the receiving node: the context ScheduleWithContext gave the Receive (point-to-point-channel.cc:100)
+    const uint32_t n = E.ctx < M.n_nodes ? E.ctx : M.dev_node[a];
     const bool reply = (p.app & NSGPU_PKT_REPLY) != 0;
     const uint32_t fa = p.app & ~NSGPU_PKT_REPLY;
     if (pkt_dst_node(M, p) == n) {
@@ -899,8 +917,8 @@ __device__ __forceinline__ void put_window(const P2PDev &M, uint32_t slot, uint6
   M.wpkt[slot] = e.p;
   uint32_t idx = 0;
   if (e.ctx < M.n_nodes) {
-    idx = atomicAdd(&M.node_cnt[e.ctx], 1u);
-    if (idx < (uint32_t)NSLOT) M.node_slot[(uint64_t)e.ctx * NSLOT + idx] = slot;
+    idx = atomicAdd(&M.node_tab[(uint64_t)e.ctx * NTAB], 1u);
+    if (idx < (uint32_t)NSLOT) M.node_tab[(uint64_t)e.ctx * NTAB + 1 + idx] = slot;
   }
   M.widx[slot] = idx;
 }
@@ -1176,9 +1194,9 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
     uint32_t n = 1;
     int32_t sink = -1;
     if (c < M.n_nodes) {
-      n = M.node_cnt[c];
+      n = M.node_tab[(uint64_t)c * NTAB];
       sink = M.sink_of_node[c];
-      M.node_cnt[c] = 0;
+      M.node_tab[(uint64_t)c * NTAB] = 0;
     }
     HQ(0);
     uint32_t *my = &chs[threadIdx.x * CH];
@@ -1186,7 +1204,7 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
     const bool small = n <= (uint32_t)CH;
     if (small && n > 1) {
       const uint32_t ns = n < (uint32_t)NSLOT ? n : (uint32_t)NSLOT;
-      for (uint32_t j = 0; j < ns; j++) my[j] = M.node_slot[(uint64_t)c * NSLOT + j];
+      for (uint32_t j = 0; j < ns; j++) my[j] = M.node_tab[(uint64_t)c * NTAB + 1 + j];
       if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
         uint32_t m = NSLOT;
         for (uint32_t x = 0; x < W && m < n; x++)
@@ -1333,27 +1351,47 @@ __device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0
   if (hs.icmp) atomicAdd((unsigned long long *)&C.icmp, (unsigned long long)hs.icmp);
 }
 
+// Rank tile t: rows [ti * HB * RTR, +HB * RTR) of the window (RTR keys per thread) against the RJ keys
+// of column tile tj: each row's count of smaller keys is added to its rank (keys are distinct: uids).
+// Wide rows: each column tile's keys are loaded by NRT blocks, not WCAP / HB.
 __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_t t) {
   const uint32_t ti = t / NJT, tj = t % NJT;
   __shared__ uint64_t tk[RJ];
-  // tile keys and the own key ahead of the run control
+  // the window size first: a config-4 window fills ~1/4 of the WCAP x WCAP tiles, and the tiles past
+  // it load nothing (these blocks are off the launch's critical path, the holders are on it)
+  const uint32_t W = C.W;
+  const uint32_t r0 = ti * HB * RTR;
+  if (r0 >= W || tj * RJ >= W) return;  // uniform over the block
 #pragma unroll
   for (int q = 0; q < RJ / HB; q++) tk[q * HB + threadIdx.x] = M.wkey[tj * RJ + q * HB + threadIdx.x];
-  const uint32_t i = ti * HB + threadIdx.x;
-  const uint64_t x = M.wkey[i];
-  const uint32_t W = C.W;
-  if (ti * HB >= W || tj * RJ >= W) return;  // uniform over the block
+  uint64_t x[RTR];
+#pragma unroll
+  for (int r = 0; r < RTR; r++) {
+    const uint32_t i = r0 + r * HB + threadIdx.x;
+    x[r] = i < W ? M.wkey[i] : 0;
+  }
   __syncthreads();
-  if (i >= W) return;
-  uint32_t c = 0;
+  uint32_t c[RTR] = {};
   const int jn = W - tj * RJ < (uint32_t)RJ ? (int)(W - tj * RJ) : RJ;  // (slots past W hold stale keys)
   if (jn == RJ) {
-#pragma unroll 16
-    for (int y = 0; y < RJ; y++) c += tk[y] < x;
+#pragma unroll 8
+    for (int y = 0; y < RJ; y++) {
+      const uint64_t k = tk[y];
+#pragma unroll
+      for (int r = 0; r < RTR; r++) c[r] += k < x[r];
+    }
   } else {
-    for (int y = 0; y < jn; y++) c += tk[y] < x;
+    for (int y = 0; y < jn; y++) {
+      const uint64_t k = tk[y];
+#pragma unroll
+      for (int r = 0; r < RTR; r++) c[r] += k < x[r];
+    }
   }
-  if (c) atomicAdd(&M.wrank[i], c);
+#pragma unroll
+  for (int r = 0; r < RTR; r++) {
+    const uint32_t i = r0 + r * HB + threadIdx.x;
+    if (i < W && c[r]) atomicAdd(&M.wrank[i], c[r]);
+  }
 }
 
 template <bool DIST>
@@ -1389,7 +1427,7 @@ __device__ __forceinline__ uint64_t refit_collect(const P2PDev &M, Ctl &C, const
   const uint64_t P0 = C.nxtP;
   for (uint32_t s = threadIdx.x; s < nrec; s += SCAN_THREADS) {
     const uint32_t c = M.wctx[s];
-    if (c < M.n_nodes) M.node_cnt[c] = 0;
+    if (c < M.n_nodes) M.node_tab[(uint64_t)c * NTAB] = 0;
     const uint64_t pk = M.wkey[s];
     Ev e{b.tmin + (pk >> 32), (uint32_t)pk, c, M.wkind[s], M.wa[s], M.wpkt[s]};
     put_pool(M, nxt, P0 + s, e);
@@ -1814,6 +1852,7 @@ struct nsgpu_p2p {
   // pristine initial pool (device) for resets
   uint64_t *init_ts = nullptr;
   uint32_t *init_uid = nullptr, *init_ctx = nullptr, *init_kind = nullptr, *init_a = nullptr;
+  const DevRec *dev_init = nullptr;  // device records after reset (tx state idle)
   uint32_t n_apps = 0;
   // partitioned run
   nsgpu_comm *comm = nullptr;  // RCCL transport (null: a loopback group member)
@@ -1995,16 +2034,6 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   if (has_echo) M.lookahead[K_RECEIVE] = 0;
   // ---- scenario upload ----
   TRY(dupload(h, &M.dev_node, sc->dev_node, D));
-  TRY(dupload(h, &M.dev_peer, sc->dev_peer, D));
-  {
-    std::vector<uint32_t> pn(D);
-    for (uint32_t d = 0; d < D; d++) pn[d] = sc->dev_node[sc->dev_peer[d]];
-    TRY(dupload(h, &M.dev_peer_node, pn.data(), D));
-  }
-  TRY(dupload(h, &M.dev_qmax, sc->dev_qmax, D));
-  TRY(dupload(h, &M.dev_bps, sc->dev_bps, D));
-  TRY(dupload(h, &M.dev_ifg, sc->dev_ifg_ns, D));
-  TRY(dupload(h, &M.dev_delay, sc->dev_delay_ns, D));
   if (sc->route) {
     TRY(dupload(h, &M.route, sc->route, (size_t)N * sc->n_dst));
   } else {
@@ -2047,11 +2076,24 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   M.sink_of_node = sinkp;
   M.icmp = sc->icmp ? 1u : 0u;
   // ---- state ----
-  TRY(dalloc(h, &M.dev_busy, D));
-  TRY(dalloc(h, &M.q_head, D));
-  TRY(dalloc(h, &M.q_count, D));
+  {  // the device records' reset image: tx state idle, the static parameters
+    std::vector<DevRec> dr(D);
+    for (uint32_t d = 0; d < D; d++) {
+      DevRec r{};
+      r.qmax = sc->dev_qmax[d];
+      r.peer = sc->dev_peer[d];
+      r.peer_node = sc->dev_node[sc->dev_peer[d]];
+      r.bps = sc->dev_bps[d];
+      r.ifg = sc->dev_ifg_ns[d];
+      r.delay = sc->dev_delay_ns[d];
+      dr[d] = r;
+    }
+    const DevRec *init;
+    TRY(dupload(h, &init, dr.data(), D));
+    h->dev_init = init;
+    TRY(dalloc(h, &M.dev, D));
+  }
   TRY(dalloc(h, &M.q_buf, (size_t)D * qcap));
-  TRY(dalloc(h, &M.devc, D));
   TRY(dalloc(h, &M.app_flags, A));
   TRY(dalloc(h, &M.app_send_gen, A));
   TRY(dalloc(h, &M.app_ss_gen, A));
@@ -2060,8 +2102,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.node_ipid, N));
   TRY(dalloc(h, &M.app_last_start, A));
   TRY(dalloc(h, &M.appc, A));
-  TRY(dalloc(h, &M.node_cnt, N));
-  TRY(dalloc(h, &M.node_slot, (size_t)N * NSLOT));
+  TRY(dalloc(h, &M.node_tab, (size_t)N * NTAB));
   // ---- setup-time events (node-list.cc:124-131, node.cc:111-145, default-simulator-impl.cc:179-183) ----
   std::vector<uint64_t> its;
   std::vector<uint32_t> iuid, ictx, ikind, ia;
@@ -2268,10 +2309,7 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemcpyAsync(M.ev_ctx[0], h->init_ctx, n0 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   NSGPU_HIP(hipMemcpyAsync(M.ev_kind[0], h->init_kind, n0 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   NSGPU_HIP(hipMemcpyAsync(M.ev_a[0], h->init_a, n0 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  NSGPU_HIP(hipMemsetAsync(M.dev_busy, 0, D * sizeof(uint32_t), s));
-  NSGPU_HIP(hipMemsetAsync(M.q_head, 0, D * sizeof(uint32_t), s));
-  NSGPU_HIP(hipMemsetAsync(M.q_count, 0, D * sizeof(uint32_t), s));
-  NSGPU_HIP(hipMemsetAsync(M.devc, 0, D * sizeof(nsgpu_dev_counters), s));
+  NSGPU_HIP(hipMemcpyAsync(M.dev, h->dev_init, D * sizeof(DevRec), hipMemcpyDeviceToDevice, s));
   NSGPU_HIP(hipMemsetAsync(M.app_flags, 0, A * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.app_send_gen, 0, A * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.app_ss_gen, 0, A * sizeof(uint32_t), s));
@@ -2281,7 +2319,7 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   if (M.trace) NSGPU_HIP(hipMemsetAsync(M.trace_n, 0, sizeof(unsigned long long), s));
   NSGPU_HIP(hipMemsetAsync(M.app_last_start, 0, A * sizeof(uint64_t), s));
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
-  NSGPU_HIP(hipMemsetAsync(M.node_cnt, 0, M.n_nodes * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(M.node_tab, 0, (size_t)M.n_nodes * NTAB * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.wrank, 0, WCAP * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
   if (M.dist) {
@@ -2534,7 +2572,9 @@ extern "C" int nsgpu_p2p_counters(nsgpu_p2p *h, nsgpu_dev_counters *devc, nsgpu_
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_counters: null");
   hipStream_t cs = (hipStream_t)stream;
   NSGPU_HIP(hipStreamSynchronize(h->s));
-  if (devc) NSGPU_HIP(hipMemcpyAsync(devc, h->M.devc, h->M.n_devices * sizeof(*devc), hipMemcpyDeviceToHost, cs));
+  if (devc)
+    NSGPU_HIP(hipMemcpy2DAsync(devc, sizeof(*devc), &h->M.dev[0].c, sizeof(DevRec), sizeof(*devc), h->M.n_devices,
+                               hipMemcpyDeviceToHost, cs));
   if (appc) NSGPU_HIP(hipMemcpyAsync(appc, h->M.appc, h->M.n_apps * sizeof(*appc), hipMemcpyDeviceToHost, cs));
   NSGPU_HIP(hipStreamSynchronize(cs));
   return NSGPU_OK;
@@ -2742,7 +2782,9 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
   const P2PDev &M = h->M;
   Ctl c;
   NSGPU_HIP(hipMemcpyAsync(&c, M.C, sizeof(Ctl), hipMemcpyDeviceToHost, s));
-  if (devc) NSGPU_HIP(hipMemcpyAsync(devc, M.devc, M.n_devices * sizeof(*devc), hipMemcpyDeviceToHost, s));
+  if (devc)
+    NSGPU_HIP(hipMemcpy2DAsync(devc, sizeof(*devc), &M.dev[0].c, sizeof(DevRec), sizeof(*devc), M.n_devices,
+                               hipMemcpyDeviceToHost, s));
   if (appc) NSGPU_HIP(hipMemcpyAsync(appc, M.appc, M.n_apps * sizeof(*appc), hipMemcpyDeviceToHost, s));
   if (log_n > M.log_cap) log_n = M.log_cap;
   if (log_ts && log_n) NSGPU_HIP(hipMemcpyAsync(log_ts, M.log_ts, log_n * 8, hipMemcpyDeviceToHost, s));

@@ -101,8 +101,8 @@ __device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t
   }
   uint32_t idx = 0;
   if (ctx < M.n_nodes) {
-    idx = atomicAdd(&M.node_cnt[ctx], 1u);
-    if (idx < (uint32_t)NSLOT) M.node_slot[(uint64_t)ctx * NSLOT + idx] = slot;
+    idx = atomicAdd(&M.node_tab[(uint64_t)ctx * NTAB], 1u);
+    if (idx < (uint32_t)NSLOT) M.node_tab[(uint64_t)ctx * NTAB + 1 + idx] = slot;
     if (idx == (uint32_t)CH) {
       const uint32_t hh = atomicAdd(&C.nhub, 1u);
       if (hh < (uint32_t)MAXHUB) M.hub_list[hh] = ctx;
@@ -442,11 +442,11 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
     uint32_t n = 1;
     int32_t sink = -1;
     if (c < M.n_nodes) {
-      n = M.node_cnt[c];
+      n = M.node_tab[(uint64_t)c * NTAB];
       sink = M.sink_of_node[c];
     }
     if (n <= (uint32_t)CH) {  // (a hub's events are its hub block's)
-      if (c < M.n_nodes) M.node_cnt[c] = 0;
+      if (c < M.n_nodes) M.node_tab[(uint64_t)c * NTAB] = 0;
       const uint64_t key0 = sp.key;
       uint32_t *my = &chs[threadIdx.x * CH];
       uint64_t *mk = &chk[threadIdx.x * CH];
@@ -454,7 +454,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
       mk[0] = key0;
       if (n > 1) {
         const uint32_t ns = n < (uint32_t)NSLOT ? n : (uint32_t)NSLOT;
-        for (uint32_t j = 0; j < ns; j++) my[j] = M.node_slot[(uint64_t)c * NSLOT + j];
+        for (uint32_t j = 0; j < ns; j++) my[j] = M.node_tab[(uint64_t)c * NTAB + 1 + j];
         if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
           uint32_t m = NSLOT;
           for (uint32_t x = 0; x < W && m < n; x++)
@@ -551,25 +551,26 @@ struct DevCache {
   uint32_t q[6];  // enq_packets, enq_bytes, drop_packets, drop_bytes, deq_packets, tx_packets
   __device__ __forceinline__ void flush(const P2PDev &M) {
     if (d == NOSRC) return;
-    M.dev_busy[d] = busy;
-    M.q_count[d] = cnt;
-    M.q_head[d] = head;
-    uint32_t *w = reinterpret_cast<uint32_t *>(&M.devc[d]);  // not rx_packets: the node pass adds it atomically
+    M.dev[d].busy = busy;
+    M.dev[d].cnt = cnt;
+    M.dev[d].head = head;
+    uint32_t *w = reinterpret_cast<uint32_t *>(&M.dev[d].c);  // not rx_packets: the node pass adds it atomically
     *reinterpret_cast<uint4 *>(w) = make_uint4(q[0], q[1], q[2], q[3]);
     *reinterpret_cast<uint2 *>(w + 4) = make_uint2(q[4], q[5]);
   }
   __device__ __forceinline__ void load(const P2PDev &M, uint32_t dd) {
     d = dd;
-    busy = M.dev_busy[d];
-    cnt = M.q_count[d];
-    head = M.q_head[d];
-    qmax = M.dev_qmax[d];
-    bps = M.dev_bps[d];
-    ifg = M.dev_ifg[d];
-    delay = M.dev_delay[d];
-    peer = M.dev_peer[d];
-    peer_node = M.dev_peer_node[d];
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(&M.devc[d]);
+    const DevRec dr = M.dev[d];
+    busy = dr.busy;
+    cnt = dr.cnt;
+    head = dr.head;
+    qmax = dr.qmax;
+    bps = dr.bps;
+    ifg = dr.ifg;
+    delay = dr.delay;
+    peer = dr.peer;
+    peer_node = dr.peer_node;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(&M.dev[d].c);
     const uint4 a = *reinterpret_cast<const uint4 *>(w);
     const uint2 b2 = *reinterpret_cast<const uint2 *>(w + 4);
     q[0] = a.x, q[1] = a.y, q[2] = a.z, q[3] = a.w, q[4] = b2.x, q[5] = b2.y;
@@ -690,12 +691,13 @@ constexpr int32_t CBIG = 1 << 28;
 __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d, const uint32_t *gs,
                                 const uint64_t *gk, uint32_t n, uint32_t j0s, uint32_t j1s, uint64_t tmin, HStat &hs) {
   const int lane = threadIdx.x;
-  const int32_t qmax = (int32_t)M.dev_qmax[d];
-  const uint32_t busy0 = M.dev_busy[d], cnt0 = M.q_count[d], head0 = M.q_head[d], qcap = M.qcap;
+  const DevRec dr = M.dev[d];
+  const int32_t qmax = (int32_t)dr.qmax;
+  const uint32_t busy0 = dr.busy, cnt0 = dr.cnt, head0 = dr.head, qcap = M.qcap;
   const int32_t c0 = busy0 ? (int32_t)cnt0 : -1;
-  const uint64_t bps = M.dev_bps[d];
-  const int64_t ifg = M.dev_ifg[d], delay = M.dev_delay[d];
-  const uint32_t peer = M.dev_peer[d], peer_node = M.dev_peer_node[d];
+  const uint64_t bps = dr.bps;
+  const int64_t ifg = dr.ifg, delay = dr.delay;
+  const uint32_t peer = dr.peer, peer_node = dr.peer_node;
   Pkt *qb = M.q_buf + (uint64_t)d * qcap;
   // pass A: the segment's composed map and its enqueue / dequeue counts
   CMap f{0, -CBIG, CBIG};
@@ -814,10 +816,10 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
   q0 = wave_sum32(q0), q1 = wave_sum32(q1), q2 = wave_sum32(q2), q3 = wave_sum32(q3), q4 = wave_sum32(q4),
   q5 = wave_sum32(q5);
   if (lane == 0) {
-    M.dev_busy[d] = cfin >= 0 ? 1u : 0u;
-    M.q_count[d] = cfin >= 0 ? (uint32_t)cfin : 0u;
-    M.q_head[d] = (head0 + dtot) % qcap;
-    uint32_t *w = reinterpret_cast<uint32_t *>(&M.devc[d]);  // not rx_packets: the node pass adds it atomically
+    M.dev[d].busy = cfin >= 0 ? 1u : 0u;
+    M.dev[d].cnt = cfin >= 0 ? (uint32_t)cfin : 0u;
+    M.dev[d].head = (head0 + dtot) % qcap;
+    uint32_t *w = reinterpret_cast<uint32_t *>(&M.dev[d].c);  // not rx_packets: the node pass adds it atomically
     const uint4 a = *reinterpret_cast<const uint4 *>(w);
     const uint2 b2 = *reinterpret_cast<const uint2 *>(w + 4);
     *reinterpret_cast<uint4 *>(w) = make_uint4(a.x + q0, a.y + q1, a.z + q2, a.w + q3);
@@ -915,7 +917,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           h.op = ACT_KICK;
           h.dev = a;
         } else if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive -> IpForward
-          atomicAdd(&M.devc[a].rx_packets, 1u);
+          atomicAdd(&M.dev[a].c.rx_packets, 1u);
           p.size -= 2;
           trace_call(M, E, NSGPU_TR_RX, a, p);
           const uint32_t out = route_of(M, c, p);
@@ -978,8 +980,8 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     dmax = y > dmax ? y : dmax;
     inl |= z;
   }
-  bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && M.dev_qmax[dmin] >= 1 &&
-              !(M.dev_busy[dmin] == 0 && M.q_count[dmin] != 0);
+  bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && M.dev[dmin].qmax >= 1 &&
+              !(M.dev[dmin].busy == 0 && M.dev[dmin].cnt != 0);
   if (fast) fast = hub_device_scan(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs);
   if (!fast) {
     DevCache D;
@@ -1078,7 +1080,7 @@ __device__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool ha
       const uint64_t ws = W < (uint32_t)WCAP ? W : (uint32_t)WCAP;
       for (uint64_t s = (uint64_t)mb * HB + threadIdx.x; s < ws; s += tstride) {
         const uint32_t c = M.wctx[s];
-        if (c < M.n_nodes) M.node_cnt[c] = 0;
+        if (c < M.n_nodes) M.node_tab[(uint64_t)c * NTAB] = 0;
       }
     }
   }
@@ -1179,7 +1181,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   for (uint64_t i = tid; i < mv; i += SCAN_THREADS) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
   if (handled) {
     const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
-    for (uint32_t h = tid; h < nh; h += SCAN_THREADS) M.node_cnt[M.hub_list[h]] = 0;
+    for (uint32_t h = tid; h < nh; h += SCAN_THREADS) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
   }
   if (!handled) {  // the window overflowed WCAP: it becomes a sorted run (host radix sort), nothing dispatched yet
     __syncthreads();

@@ -1,11 +1,16 @@
-"""Turn two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of the p2p bench into
-profiles/traffic_p2p-grid.json: average HBM bytes per launch of the dominant kernel.
+"""Turn two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of a bench workload into
+profiles/traffic_<workload>.json: average HBM bytes per launch of each named kernel.
 
 Corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
 WRITE_SIZE are in KiB; FETCH_SIZE is doubled on gfx950 (128-B requests tallied at 64 B).
-Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substring> <out.json>
+Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <out.json> <kernel-substring>...
+(the first kernel's entry is also written at the top level, for older readers)
 """
-import csv, glob, json, os, sys
+import csv
+import glob
+import json
+import os
+import sys
 
 
 def per_dispatch(d, counter, kernel):
@@ -25,14 +30,18 @@ def per_dispatch(d, counter, kernel):
 
 
 def main():
-    fdir, wdir, kernel, out = sys.argv[1:5]
-    fetch_kib, nf = per_dispatch(fdir, "FETCH_SIZE", kernel)
-    write_kib, nw = per_dispatch(wdir, "WRITE_SIZE", kernel)
-    rd = 2.0 * fetch_kib * 1024.0
-    wr = write_kib * 1024.0
-    res = {"kernel": kernel, "fetch_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-           "hbm_bytes_per_launch": rd + wr, "dispatches": [nf, nw],
-           "correction": "FETCH_SIZE KiB x1024 x2 (gfx950), WRITE_SIZE KiB x1024"}
+    fdir, wdir, out = sys.argv[1:4]
+    kernels = sys.argv[4:]
+    res = {"correction": "FETCH_SIZE KiB x1024 x2 (gfx950), WRITE_SIZE KiB x1024", "kernels": {}}
+    for k in kernels:
+        fetch_kib, nf = per_dispatch(fdir, "FETCH_SIZE", k)
+        write_kib, nw = per_dispatch(wdir, "WRITE_SIZE", k)
+        rd = 2.0 * fetch_kib * 1024.0
+        wr = write_kib * 1024.0
+        res["kernels"][k] = {"fetch_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                             "hbm_bytes_per_launch": rd + wr, "dispatches": [nf, nw]}
+    first = res["kernels"][kernels[0]]
+    res.update({"kernel": kernels[0], **first})
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
