@@ -351,13 +351,21 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       for (int q = 0; q < PPT; q++) {
         const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
         ge[q] = Ev{TOMB, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-        if (i < P) ge[q] = load_pool(M, 0, i);  // every field at once: one memory round trip
+        // the key fields only: most pool entries stay pending (these blocks are off the critical path,
+        // so the window entries' second load costs no window time, and the pool's other 24 B a slot
+        // are not fetched for the rest)
+        if (i < P) ge[q] = Ev{M.ev_ts[0][i], M.ev_uid[0][i], 0, M.ev_kind[0][i], 0, Pkt{0, 0, 0, 0}};
       }
 #pragma unroll
       for (int q = 0; q < PPT; q++) {
         const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
         k2_classify(M, b, false, ge[q].ts != TOMB, ge[q], (uint32_t)i, R, tmn, wnd, gin[q], gpk[q]);
         cw += gin[q];
+        if (gin[q]) {  // the window entry's record (its loads overlap the block allocation below)
+          ge[q].ctx = M.ev_ctx[0][i];
+          ge[q].a = M.ev_a[0][i];
+          ge[q].p = M.ev_pkt[0][i];
+        }
       }
       uint32_t w0;
       uint64_t f0;
@@ -1160,6 +1168,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run, c_wbase = C.wbase;
   const uint32_t c_nhub = C.nhub;
   const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
+  // the bookkeeping's run control as well (thread 0 writes it back at the end; loaded now, its trip
+  // overlaps the slot loads instead of following the scan)
+  struct Book {
+    uint64_t K, tmin, inline_lim, live, P_end, r0, rW, windows, max_window, max_windows, hts;
+    uint32_t uid, rt, stop_seen, hcap;
+  } bk{};
+  if (tid == 0)
+    bk = Book{C.K, C.tmin, C.inline_lim, C.live, C.P_end, C.r0, C.rW, C.windows, C.max_window, C.max_windows, C.hts,
+              C.uid, C.rt, C.stop_seen, C.hcap};
   uint32_t pr[RPT], pc[RPT], pctx[RPT];
   uint64_t pkey[RPT];
 #pragma unroll
@@ -1294,55 +1311,62 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   }
   PH_MARK(19);
   if (tid == 0) {
-    C.pK0 = C.K;
-    C.puid0 = C.uid;
-    C.ptmin = C.tmin;
-    C.pinline_lim = C.inline_lim;
+    C.pK0 = bk.K;
+    C.puid0 = bk.uid;
+    C.ptmin = bk.tmin;
+    C.pinline_lim = bk.inline_lim;
     C.pW = W;
     C.pinl = tinl;
     C.pvalid = 1;
-    if (W) C.last_ts = C.tmin + l_rel[W - 1];
-    C.K += W + tinl;
-    C.uid += tc;
+    if (W) C.last_ts = bk.tmin + l_rel[W - 1];
+    C.K = bk.K + W + tinl;
+    C.uid = bk.uid + tc;
     C.nfree = nfree - consumed + npush;
-    C.P_end += nF > nfree ? nF - nfree : 0;
-    C.live = C.live - npush + nF;
+    const uint64_t P_end = bk.P_end + (nF > nfree ? nF - nfree : 0);
+    const uint64_t live = bk.live - npush + nF;
+    C.P_end = P_end;
+    C.live = live;
     C.npush = 0;
     C.nF = 0;
     C.nhub = 0;
     C.force_run = 0;  // (a run chunk's slot tables may set it; it only matters for a normal window)
+    uint32_t mode = c_mode;
+    uint64_t r0 = bk.r0;
     bool flip = true;
     if (run) {
-      C.r0 += W;
-      if (C.r0 >= C.rW) C.mode = MODE_NORMAL;
+      r0 += W;
+      C.r0 = r0;
+      if (r0 >= bk.rW) mode = MODE_NORMAL;
       else flip = false;  // the run's chunks keep folding into the same reduction
     }
     if (flip) {
-      const uint32_t rt = C.rt;
+      const uint32_t rt = bk.rt;
       C.red[rt ^ 1].tmin = C.red[rt ^ 1].wend = C.red[rt ^ 1].stopts = ~0ull;  // consumed
       C.rt = rt ^ 1;
     }
-    C.windows++;
-    if (W > C.max_window) C.max_window = W;
+    const uint64_t windows = bk.windows + 1;
+    C.windows = windows;
+    if (W > bk.max_window) C.max_window = W;
     C.W = 0;
-    const uint64_t pending = C.live + (tc - tinl) + (C.mode == MODE_RUN ? C.rW - C.r0 : 0);
-    bool done = C.stop_seen || (pending == 0 && C.hts == ~0ull);
-    if (C.P_end > M.pool_cap) {
+    const uint64_t pending = live + (tc - tinl) + (mode == MODE_RUN ? bk.rW - r0 : 0);
+    bool done = bk.stop_seen || (pending == 0 && bk.hts == ~0ull);
+    if (P_end > M.pool_cap) {
       atomicOr(M.error, 1u);
       done = true;
     }
-    if (C.windows >= C.max_windows && !done) {
+    if (windows >= bk.max_windows && !done) {
       atomicOr(M.error, 4u);
       done = true;
     }
     if (done) {
       C.done = 1;
-    } else if (C.mode == MODE_NORMAL && C.hcap) {  // the window was cut at the next host closure: pause
+    } else if (mode == MODE_NORMAL && bk.hcap) {  // the window was cut at the next host closure: pause
       C.hcap = 0;
-      C.mode = MODE_HOST;
-    } else if (C.mode == MODE_NORMAL && C.P_end > 65536 && C.live * 4 < C.P_end) {
-      C.mode = MODE_COMPACT;
+      mode = MODE_HOST;
+    } else if (mode == MODE_NORMAL && P_end > 65536 && live * 4 < P_end) {
+      mode = MODE_COMPACT;
     }
+    if (mode != c_mode) C.mode = mode;
   }
   PH_MARK(20);
   BLK_REC(2, c_win);
