@@ -169,7 +169,9 @@ struct P2PDev {
   const uint32_t *owner;
   uint64_t *x0_send, *x0_recv;  // X0: 2 u64 per rank
   uint8_t *x1_send, *x1_recv;   // X1: X1B bytes per rank
-  uint8_t *x2_send, *x2_recv;   // X2: X2B bytes per peer
+  uint8_t *x2_send, *x2_recv;   // X2: x2b bytes per peer
+  uint32_t capx, pad_x;         // X2 records per peer per window (the run's largest cut between two ranks)
+  uint64_t x2b;                 // X2 bytes per peer
   uint32_t *gacc;               // 6 x WCAP accumulators of k_gtile
   // run control / outputs
   uint32_t n_init;    // initial pending count (pool 0)
@@ -897,16 +899,23 @@ constexpr size_t X1B = sizeof(X1Hdr) + sizeof(X1Ent) * WCAP;
 struct X2Hdr {
   uint32_t n, pad[3];
 };
-constexpr int CAPX = 1024;  // remote events per peer per window
-constexpr size_t X2B = sizeof(X2Hdr) + sizeof(Ev) * CAPX;
+// X2 records per peer: a device starts at most one transmission per window (its TransmitComplete is a
+// child, and children sort after the window), and Receive is the only child scheduled on another
+// node, so rank p sends rank q at most as many records per window as p has devices whose peer q owns
+// (nsgpu_p2p_create_dist sizes X2 to the largest such cut, rounded up to 16; at most CAPX_MAX).
+constexpr int CAPX_MAX = 1024;
 constexpr size_t X0B = 16;  // X0: one rank's largest fitting window bound (+ pad)
 constexpr int MAXR = 64;    // ranks
 __device__ __forceinline__ X1Hdr *x1hdr(uint8_t *b, uint32_t q) { return (X1Hdr *)(b + (size_t)q * X1B); }
 __device__ __forceinline__ X1Ent *x1ent(uint8_t *b, uint32_t q) {
   return (X1Ent *)(b + (size_t)q * X1B + sizeof(X1Hdr));
 }
-__device__ __forceinline__ X2Hdr *x2hdr(uint8_t *b, uint32_t q) { return (X2Hdr *)(b + (size_t)q * X2B); }
-__device__ __forceinline__ Ev *x2rec(uint8_t *b, uint32_t q) { return (Ev *)(b + (size_t)q * X2B + sizeof(X2Hdr)); }
+__device__ __forceinline__ X2Hdr *x2hdr(const P2PDev &M, uint8_t *b, uint32_t q) {
+  return (X2Hdr *)(b + (size_t)q * M.x2b);
+}
+__device__ __forceinline__ Ev *x2rec(const P2PDev &M, uint8_t *b, uint32_t q) {
+  return (Ev *)(b + (size_t)q * M.x2b + sizeof(X2Hdr));
+}
 
 // Writes window slot `slot` (and the node's slot table).
 __device__ __forceinline__ void put_window(const P2PDev &M, uint32_t slot, uint64_t pk, const Ev &e) {
@@ -1000,7 +1009,8 @@ __global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
   Ctl &C = *M.C;
   const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * TB;
-  const uint64_t RR = DIST ? (uint64_t)M.nranks * CAPX : 0;  // remote-event threads (partitioned)
+  // remote-event threads (partitioned), whole blocks: the roles must stay wave-uniform (ballots)
+  const uint64_t RR = DIST ? ((uint64_t)M.nranks * M.capx + TB - 1) / TB * TB : 0;
   const bool slot_role = g < (uint64_t)WCAP;                   // (roles are wave-uniform)
   const bool remote_role = !slot_role && g < WCAP + RR;
   if (C.prep || C.done >= 2) return;  // window already prepared by the refit / run over
@@ -1084,12 +1094,12 @@ __global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
       }
     }
   } else if (DIST && remote_role) {
-    // ---- remote events received through X2 (partitioned): record idx % CAPX from rank idx / CAPX
+    // ---- remote events received through X2 (partitioned): record idx % capx from rank idx / capx
     const uint64_t idx = g - WCAP;
-    const uint32_t q = (uint32_t)(idx / CAPX), rec = (uint32_t)(idx % CAPX);
-    const bool valid = partition && rec < x2hdr(M.x2_recv, q)->n;
+    const uint32_t q = (uint32_t)(idx / M.capx), rec = (uint32_t)(idx % M.capx);
+    const bool valid = partition && q < M.nranks && rec < x2hdr(M, M.x2_recv, q)->n;
     Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-    if (valid) e = x2rec(M.x2_recv, q)[rec];
+    if (valid) e = x2rec(M, M.x2_recv, q)[rec];
     if (__ballot(valid)) classify(M, C, b, nxt, valid, e, R, tmn, wnd);
   } else {
     // ---- pool entries (grid-stride over the threads of the pool role)
@@ -1626,7 +1636,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_cut(const P2PDev M) {
     C.pW = C.W;
     C.pvalid = 1;
   }
-  for (uint32_t q = threadIdx.x; q < M.nranks; q += SCAN_THREADS) x2hdr(M.x2_send, q)->n = 0;
+  for (uint32_t q = threadIdx.x; q < M.nranks; q += SCAN_THREADS) x2hdr(M, M.x2_send, q)->n = 0;
 }
 
 constexpr int GTB = 1024;  // blocks of k_gtile (grid-stride over tiles)
@@ -1715,9 +1725,9 @@ __global__ __launch_bounds__(HB) void k_dfin(const P2PDev M) {
       const uint32_t ctx = M.ch_ctx[sl];
       const uint32_t q = M.owner[ctx];
       if (q == M.rank) continue;
-      const uint32_t pos = atomicAdd(&x2hdr(M.x2_send, q)->n, 1u);
-      if (pos < (uint32_t)CAPX)
-        x2rec(M.x2_send, q)[pos] = Ev{M.ch_ts[sl], uid0 + cp + j, ctx, kw, M.ch_a[sl], M.ch_pkt[sl]};
+      const uint32_t pos = atomicAdd(&x2hdr(M, M.x2_send, q)->n, 1u);
+      if (pos < M.capx)
+        x2rec(M, M.x2_send, q)[pos] = Ev{M.ch_ts[sl], uid0 + cp + j, ctx, kw, M.ch_a[sl], M.ch_pkt[sl]};
       else
         atomicOr(M.error, 16u);
     }
@@ -1924,7 +1934,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   }
   if (owner) {
     if (nranks < 1 || nranks > MAXR || rank < 0 || rank >= nranks ||
-        (uint64_t)nranks * CAPX + WCAP >= (uint64_t)GRID_POOL * TB)
+        (uint64_t)nranks * CAPX_MAX + TB + WCAP >= (uint64_t)GRID_POOL * TB)
       return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: rank %d of %d (at most %d ranks)", rank, nranks, MAXR);
     for (uint32_t n = 0; n < N; n++)
       if (owner[n] >= (uint32_t)nranks) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: node %u: owner %u", n, owner[n]);
@@ -2212,8 +2222,19 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.x0_recv, 2 * (size_t)nranks));
     TRY(dalloc(h, &M.x1_send, X1B));
     TRY(dalloc(h, &M.x1_recv, X1B * nranks));
-    TRY(dalloc(h, &M.x2_send, X2B * nranks));
-    TRY(dalloc(h, &M.x2_recv, X2B * nranks));
+    {  // X2 capacity: the largest number of devices of one rank whose peer another rank owns
+      std::vector<uint32_t> cut((size_t)nranks * nranks, 0);
+      for (uint32_t d = 0; d < D; d++) {
+        const uint32_t p = owner[sc->dev_node[d]], q = owner[sc->dev_node[sc->dev_peer[d]]];
+        if (p != q) cut[(size_t)p * nranks + q]++;
+      }
+      uint32_t mx = 1;
+      for (uint32_t c : cut) mx = std::max(mx, c);
+      M.capx = std::min<uint32_t>((mx + 15) / 16 * 16, CAPX_MAX);
+      M.x2b = sizeof(X2Hdr) + sizeof(Ev) * (uint64_t)M.capx;
+    }
+    TRY(dalloc(h, &M.x2_send, M.x2b * nranks));
+    TRY(dalloc(h, &M.x2_recv, M.x2b * nranks));
     TRY(dalloc(h, &M.gacc, 6 * (size_t)WCAP));
     h->comm = comm;
     memset(&h->x1h0, 0, sizeof(X1Hdr));
@@ -2329,8 +2350,8 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
     NSGPU_HIP(hipMemsetAsync(M.x1_send, 0, X1B, s));
     NSGPU_HIP(hipMemcpyAsync(M.x1_send, &h->x1h0, sizeof(X1Hdr), hipMemcpyHostToDevice, s));
     NSGPU_HIP(hipMemsetAsync(M.x1_recv, 0, X1B * R, s));
-    NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, X2B * R, s));
-    NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, X2B * R, s));
+    NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, M.x2b * R, s));
+    NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, M.x2b * R, s));
     NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 6 * WCAP * sizeof(uint32_t), s));
     if (M.log_cap) {  // every rank writes only the entries it dispatches: the union is the log
       NSGPU_HIP(hipMemsetAsync(M.log_ts, 0, M.log_cap * 8, s));
@@ -2435,7 +2456,7 @@ static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s) {
     NCCL_TRY(ncclAllGather(M.x1_send, M.x1_recv, X1B, ncclUint8, comm, s));
     hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, M);
     hipLaunchKernelGGL(k_dfin, dim3(NHB), dim3(HB), 0, s, M);
-    NCCL_TRY(ncclAllToAll(M.x2_send, M.x2_recv, X2B, ncclUint8, comm, s));
+    NCCL_TRY(ncclAllToAll(M.x2_send, M.x2_recv, M.x2b, ncclUint8, comm, s));
   }
   return NSGPU_OK;
 }
@@ -2810,7 +2831,7 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
   }
   if (error) *error = err;
   if (err) return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, "
-                                          "4 = window limit, 8 = window cut)", err);
+                                          "4 = window limit, 8 = window cut, 16 = a window's remote events beyond the X2 capacity)", err);
   return NSGPU_OK;
 }
 
@@ -2873,7 +2894,7 @@ extern "C" int nsgpu_p2p_group_create(nsgpu_p2p **members, int n, nsgpu_p2p_grou
       const P2PDev &R = members[r]->M, &Q = members[q]->M;
       x[0].push_back(CopyDesc{(const uint8_t *)Q.x0_send, (uint8_t *)(R.x0_recv + 2 * q), X0B});
       x[1].push_back(CopyDesc{Q.x1_send, R.x1_recv + (size_t)q * X1B, X1B});
-      x[2].push_back(CopyDesc{Q.x2_send + (size_t)r * X2B, R.x2_recv + (size_t)q * X2B, X2B});
+      x[2].push_back(CopyDesc{Q.x2_send + (size_t)r * Q.x2b, R.x2_recv + (size_t)q * R.x2b, Q.x2b});
     }
   for (int k = 0; k < 3; k++) {
     if (hipMalloc(&g->d_x[k], x[k].size() * sizeof(CopyDesc)) != hipSuccess ||
