@@ -172,7 +172,7 @@ struct P2PDev {
   uint8_t *x2_send, *x2_recv;   // X2: x2b bytes per peer
   uint32_t capx, pad_x;         // X2 records per peer per window (the run's largest cut between two ranks)
   uint64_t x2b;                 // X2 bytes per peer
-  uint32_t *gacc;               // 6 x WCAP accumulators of k_gtile
+  uint32_t *gacc;               // k_gtile's accumulators: 2 x WCAP packed 64-bit words
   // run control / outputs
   uint32_t n_init;    // initial pending count (pool 0)
   uint32_t uid_init;  // m_uid after setup
@@ -906,6 +906,7 @@ struct X2Hdr {
 constexpr int CAPX_MAX = 1024;
 constexpr size_t X0B = 16;  // X0: one rank's largest fitting window bound (+ pad)
 constexpr int MAXR = 64;    // ranks
+static_assert((uint64_t)MAXR * WCAP < (1u << 21), "k_gtile's packed rank fields");
 __device__ __forceinline__ X1Hdr *x1hdr(uint8_t *b, uint32_t q) { return (X1Hdr *)(b + (size_t)q * X1B); }
 __device__ __forceinline__ X1Ent *x1ent(uint8_t *b, uint32_t q) {
   return (X1Ent *)(b + (size_t)q * X1B + sizeof(X1Hdr));
@@ -1676,7 +1677,7 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
     if (i < W) {
       const uint64_t x = M.wkey[i];
       const uint64_t lo = x & 0xffffffff00000000ull, hi = lo + (1ull << 32);
-      uint32_t gr = 0, cp = 0, ip = 0, fi = 0, ipf = 0, lp = 0;
+      uint32_t gr = 0, cp = 0, ip = 0, ipf = 0, lp = 0;
       for (uint32_t y = 0; y < n; y++) {
         const uint64_t k = tk[y];
         const uint32_t c = tc[y];
@@ -1685,17 +1686,16 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
         gr += lt;
         cp += lt ? nc : 0u;
         ip += lt ? ni : 0u;
-        fi += blo;
         ipf += blo ? ni : 0u;
         lp += k < hi;
       }
-      uint32_t *A = M.gacc;
-      if (gr) atomicAdd(&A[i], gr);
-      if (cp) atomicAdd(&A[WCAP + i], cp);
-      if (ip) atomicAdd(&A[2 * WCAP + i], ip);
-      if (fi) atomicAdd(&A[3 * WCAP + i], fi);
-      if (ipf) atomicAdd(&A[4 * WCAP + i], ipf);
-      if (lp) atomicAdd(&A[5 * WCAP + i], lp);
+      // two packed 64-bit accumulators instead of five words: (rank, group end, inline prefix: each at
+      // most MAXR x WCAP < 2^21) and (child prefix < 2^32, the group's inline prefix)
+      unsigned long long *A = reinterpret_cast<unsigned long long *>(M.gacc);
+      const uint64_t w0 = (uint64_t)gr | ((uint64_t)lp << 21) | ((uint64_t)ip << 42);
+      const uint64_t w1 = (uint64_t)cp | ((uint64_t)ipf << 32);
+      if (w0) atomicAdd(&A[i], (unsigned long long)w0);
+      if (w1) atomicAdd(&A[WCAP + i], (unsigned long long)w1);
     }
     __syncthreads();
   }
@@ -1709,10 +1709,12 @@ __global__ __launch_bounds__(HB) void k_dfin(const P2PDev M) {
   for (uint32_t q = 0; q < M.nranks; q++) tinl_g += x1hdr(M.x1_recv, q)->tinl;
   const uint32_t s = blockIdx.x * HB + threadIdx.x;
   if (s < W) {
-    uint32_t *A = M.gacc;
-    const uint32_t gr = A[s], cp = A[WCAP + s], ip = A[2 * WCAP + s], ipf = A[4 * WCAP + s],
-                   lp = A[5 * WCAP + s];
-    for (int k = 0; k < 6; k++) A[k * WCAP + s] = 0;
+    uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);
+    const uint64_t w0 = A[s], w1 = A[WCAP + s];
+    A[s] = 0;
+    A[WCAP + s] = 0;
+    const uint32_t gr = (uint32_t)(w0 & 0x1fffffu), lp = (uint32_t)((w0 >> 21) & 0x1fffffu),
+                   ip = (uint32_t)(w0 >> 42), cp = (uint32_t)w1, ipf = (uint32_t)(w1 >> 32);
     // as k_scan: (dispatch rank rel. K0, rank of the first inline child, child prefix, inline prefix)
     M.sinfo[s] = make_uint4(gr + (tinl_g ? ipf : 0), lp + ip, cp, ip);
     M.pwkey[s] = M.wkey[s];
@@ -2222,6 +2224,8 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.x0_recv, 2 * (size_t)nranks));
     TRY(dalloc(h, &M.x1_send, X1B));
     TRY(dalloc(h, &M.x1_recv, X1B * nranks));
+    if ((uint64_t)nranks * WCAP * M.maxc >= (1ull << 32))  // (k_gtile's packed child prefix)
+      return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: %d ranks x %u children per event", nranks, M.maxc);
     {  // X2 capacity: the largest number of devices of one rank whose peer another rank owns
       std::vector<uint32_t> cut((size_t)nranks * nranks, 0);
       for (uint32_t d = 0; d < D; d++) {
@@ -2235,7 +2239,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     }
     TRY(dalloc(h, &M.x2_send, M.x2b * nranks));
     TRY(dalloc(h, &M.x2_recv, M.x2b * nranks));
-    TRY(dalloc(h, &M.gacc, 6 * (size_t)WCAP));
+    TRY(dalloc(h, &M.gacc, 4 * (size_t)WCAP));
     h->comm = comm;
     memset(&h->x1h0, 0, sizeof(X1Hdr));
     h->x1h0.red.tmin = h->x1h0.red.wend = h->x1h0.red.stopts = ~0ull;
@@ -2352,7 +2356,7 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
     NSGPU_HIP(hipMemsetAsync(M.x1_recv, 0, X1B * R, s));
     NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, M.x2b * R, s));
     NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, M.x2b * R, s));
-    NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 6 * WCAP * sizeof(uint32_t), s));
+    NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 4 * WCAP * sizeof(uint32_t), s));
     if (M.log_cap) {  // every rank writes only the entries it dispatches: the union is the log
       NSGPU_HIP(hipMemsetAsync(M.log_ts, 0, M.log_cap * 8, s));
       NSGPU_HIP(hipMemsetAsync(M.log_uid, 0, M.log_cap * 4, s));
