@@ -273,6 +273,11 @@ int nsgpu_p2p_set_eager(nsgpu_p2p *h, int eager);
  * (ts, uid, seq)).  nsgpu_p2p_trace_read copies up to `cap` records of the last run and sets *n to
  * the number the run made (NSGPU_ENOMEM when that exceeds the buffer or `cap`). */
 int nsgpu_p2p_set_trace(nsgpu_p2p *h, uint64_t cap);
+/* The sinks recorded: bit k = nsgpu_trace_kind k.  Default 0xf (the device sinks above); 0x70 adds the
+ * Ipv4L3Protocol Tx / Rx / Drop sinks InternetStackHelper::EnableAsciiIpv4All hooks
+ * (internet-stack-helper.cc:593-730).  Call before nsgpu_p2p_run (a group member: before
+ * nsgpu_p2p_group_create). */
+int nsgpu_p2p_set_trace_kinds(nsgpu_p2p *h, uint32_t mask);
 int nsgpu_p2p_trace_read(nsgpu_p2p *h, nsgpu_trace_record *out, uint64_t cap, uint64_t *n, void *stream);
 /* The window pipeline's kernels: count and names (launch order). */
 int nsgpu_p2p_kernel_count(int *n);

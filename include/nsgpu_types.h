@@ -183,7 +183,15 @@ typedef struct nsgpu_p2p_scenario {
  * followed by the sniffer on the same device (Send :462-518, TransmitComplete :236-269), every MacRx is
  * preceded by it (Receive :304-346, packet with the PPP header).  Records are written unordered; the
  * trace order is (ts, uid, seq): the pop order of the dispatched event, then call order inside it. */
-enum nsgpu_trace_kind { NSGPU_TR_ENQUEUE = 0, NSGPU_TR_DEQUEUE = 1, NSGPU_TR_DROP = 2, NSGPU_TR_RX = 3 };
+enum nsgpu_trace_kind { NSGPU_TR_ENQUEUE = 0, NSGPU_TR_DEQUEUE = 1, NSGPU_TR_DROP = 2, NSGPU_TR_RX = 3,
+                        /* Ipv4L3Protocol's trace sources as InternetStackHelper::EnableAsciiIpv4 hooks them
+                         * (internet-stack-helper.cc:593-730, every interface): "t" Tx (SendRealOut,
+                         * ipv4-l3-protocol.cc:764, the packet with its new IPv4 header), "r" Rx (Receive
+                         * :455, as received), "d" Drop (DROP_TTL_EXPIRED :835 — after the time exceeded an
+                         * ICMP-enabled node sends —, DROP_NO_ROUTE :505; the received header; a UDP datagram's ipid & 0xffff).
+                         * dev: the sending device (Tx), the receiving one (Rx, DROP_NO_ROUTE), the forwarding
+                         * route's (DROP_TTL_EXPIRED: IpForward's interface); size: the IPv4 length. */
+                        NSGPU_TR_IP_TX = 4, NSGPU_TR_IP_RX = 5, NSGPU_TR_IP_DROP = 6 };
 typedef struct nsgpu_trace_record {
   uint64_t ts;    /* Now () of the call (ns) */
   uint32_t uid;   /* uid of the dispatched event that made the call */

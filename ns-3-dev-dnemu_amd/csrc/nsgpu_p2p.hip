@@ -98,7 +98,7 @@ struct Ctl {
   uint64_t windows, max_window, last_ts, max_windows, refits;
   uint64_t digest, cancelled, ttl_drops, no_route, unreach, icmp;
   uint64_t pK0, ptmin, pinline_lim;    // the last scanned window, appended by the next k_pa
-  uint32_t uid, cur, W, nxtP, overflow, prep, done, stop_seen;
+  uint32_t uid, cur, W, nxtP, overflow, prep, done, stop_seen;  // (W, nxtP: one 64-bit word for classify)
   uint32_t puid0, pW, pvalid, pinl;
   uint32_t collected, pad1;  // partitioned: k_refit_d already moved the window slots to the pool
   uint64_t pcol;             // (and the pool count after that)
@@ -114,6 +114,8 @@ struct Ctl {
   uint64_t hts, hrel;              // next host event (nsgpu_p2p_advance): ts (~0: none); the rel ts of the
   uint32_t huid, pad4;             //   window's last timestamp (W_end or the host event's); the host uid
 };
+
+static_assert(offsetof(Ctl, nxtP) == offsetof(Ctl, W) + 4 && offsetof(Ctl, W) % 8 == 0, "classify's 64-bit add");
 
 // Device-resident model + engine state (all pointers are HBM).  Passed to the kernels by value.
 struct P2PDev {
@@ -185,6 +187,7 @@ struct P2PDev {
   nsgpu_trace_record *trace;
   uint64_t trace_cap;
   unsigned long long *trace_n;
+  uint32_t trace_kinds, pad_tk;  // nsgpu_trace_kind bits recorded (nsgpu_p2p_set_trace_kinds)
   // ---- single-GPU engine (k2_*) ----
   uint64_t runcap;        // capacity of the window record arrays (a sorted run may hold the whole pool)
   uint32_t *wsrc;         // pool slot each window record came from (NOSRC: a child of the last window)
@@ -305,7 +308,7 @@ enum : uint32_t { ACT_NONE = 0, ACT_SEND = 1, ACT_KICK = 2 };
 // hooked by PointToPointHelper::EnableAsciiInternal, point-to-point-helper.cc:113-219): appended
 // unordered; the host orders the records by (ts, uid, seq).
 __device__ __forceinline__ void trace_call(const P2PDev &M, Emit &E, uint32_t kind, uint32_t d, const Pkt &p) {
-  if (!M.trace) return;
+  if (!M.trace || !((M.trace_kinds >> kind) & 1u)) return;
   nsgpu_trace_record r;
   r.ts = E.now;
   r.uid = E.uid;
@@ -325,6 +328,19 @@ struct Act {
   uint32_t op, dev;
   Pkt p;
 };
+// Ipv4L3Protocol::m_dropTrace (ipv4-l3-protocol.cc:505,835): the datagram as received (a UDP datagram's
+// 16-bit identification); d = the receiving device (DROP_NO_ROUTE) or the forwarding route's
+// (DROP_TTL_EXPIRED).
+__device__ __forceinline__ void trace_ip_drop(const P2PDev &M, Emit &E, uint32_t d, Pkt p) {
+  if (!(p.app & NSGPU_PKT_ICMP)) p.ipid &= 0xffffu;
+  trace_call(M, E, NSGPU_TR_IP_DROP, d, p);
+}
+// The TTL-expired datagram a time-exceeded error e was made from (icmp_error below embeds its flow, reply
+// flag, identification and length; it arrived with TTL 1): its Drop record follows the error's Send.
+__device__ __forceinline__ void trace_te_drop(const P2PDev &M, Emit &E, uint32_t d, const Pkt &e) {
+  const uint32_t app = (e.app & NSGPU_PKT_APP) | ((e.app & NSGPU_PKT_ICMP_OF_REPLY) ? NSGPU_PKT_REPLY : 0u);
+  trace_call(M, E, NSGPU_TR_IP_DROP, d, Pkt{app, e.ipid >> 16, e.ttl >> 16, 1u});
+}
 
 __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &act) {
   if (act.op == ACT_NONE) return;
@@ -342,6 +358,7 @@ __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &
   bool go = false;
   Pkt tx{0, 0, 0, 0};
   if (act.op == ACT_SEND) {
+    trace_call(M, E, NSGPU_TR_IP_TX, d, act.p);  // SendRealOut: m_txTrace, then the device's Send
     Pkt p = act.p;
     p.size += 2;  // PppHeader
     if (cnt >= qmax) {
@@ -583,6 +600,8 @@ struct NodeOut {
   Act act;
   Post post;
   bool cancelled;
+  uint32_t xdrop;  // forwarding device + 1 of a TTL-expired datagram whose time-exceeded error is act:
+                   // its Drop record follows the device step (0: none)
 };
 // rx_atomic: the device's rx counter is also added to by other lanes (hub blocks).
 __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a,
@@ -592,12 +611,14 @@ __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t 
   Act act{ACT_NONE, 0, Pkt{0, 0, 0, 0}};
   Post post{false, 0, 0, 0};
   bool cancelled = false;
+  uint32_t xdrop = 0;
   if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive (ipv4-l3-protocol.cc:434-537)
     if (rx_atomic) atomicAdd(&M.dev[a].c.rx_packets, 1u);
     else M.dev[a].c.rx_packets++;
     Pkt p = pkt;
     p.size -= 2;                             // ProcessHeader strips the PppHeader
     trace_call(M, E, NSGPU_TR_RX, a, p);     // m_macRxTrace
+    trace_call(M, E, NSGPU_TR_IP_RX, a, p);  // Ipv4L3Protocol::Receive: m_rxTrace (:455)
     // the receiving node: the context ScheduleWithContext gave the Receive (point-to-point-channel.cc:100)
     const uint32_t n = E.ctx < M.n_nodes ? E.ctx : M.dev_node[a];
     const bool reply = (p.app & NSGPU_PKT_REPLY) != 0;
@@ -621,11 +642,18 @@ __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t 
       const uint32_t out = route_of(M, n, p);
       if (out == 0xffffffffu) {
         hs.no_route++;
+        trace_ip_drop(M, E, a, p);  // DROP_NO_ROUTE
       } else {
         p.ttl -= 1;  // IpForward (:815-841)
         if ((p.ttl & 0xffu) == 0) {
           hs.ttl_drops++;  // (no ICMP about an ICMP message)
           if (M.icmp && !(p.app & NSGPU_PKT_ICMP)) act = icmp_act(M, n, icmp_error(p, false), hs);
+          if (act.op == ACT_SEND) {
+            xdrop = out + 1;
+          } else {
+            p.ttl += 1;
+            trace_ip_drop(M, E, out, p);  // DROP_TTL_EXPIRED (:835: on the forwarding route's interface)
+          }
         } else {
           act = Act{ACT_SEND, out, p};
         }
@@ -760,12 +788,13 @@ __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t 
         break;
     }
   }
-  return NodeOut{act, post, cancelled};
+  return NodeOut{act, post, cancelled, xdrop};
 }
 __device__ __forceinline__ bool run_event(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a, const Pkt &pkt,
                                           int32_t sink, HStat &hs) {
   const NodeOut o = node_part(M, E, kind_word, a, pkt, sink, hs);
   device_act(M, E, o.act);
+  if (o.xdrop) trace_te_drop(M, E, o.xdrop - 1, o.act.p);
   if (o.post.valid) E.child(o.post.delay, E.ctx, o.post.kind, o.post.a, Pkt{0, 0, 0, 0});
   return o.cancelled;
 }
@@ -961,9 +990,11 @@ __device__ __forceinline__ void classify(const P2PDev &M, Ctl &C, const WinBound
   const uint64_t bin = __ballot(in);
   const uint64_t bout0 = __ballot(valid && !in);
   uint32_t basein = 0, baseout = 0;
-  if (lane == 0) {  // both slot ranges at once (overflowed candidates are few: a second add)
-    if (bin) basein = atomicAdd(&C.W, (uint32_t)__popcll(bin));
-    if (bout0) baseout = atomicAdd(&C.nxtP, (uint32_t)__popcll(bout0));
+  if (lane == 0 && (bin | bout0)) {  // both slot ranges in ONE 64-bit add on the adjacent words (W, nxtP)
+    const unsigned long long v = (unsigned long long)__popcll(bin) | ((unsigned long long)__popcll(bout0) << 32);
+    const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long *>(&C.W), v);
+    basein = (uint32_t)old;
+    baseout = (uint32_t)(old >> 32);
   }
   basein = __shfl(basein, 0);
   baseout = __shfl(baseout, 0);
@@ -2087,6 +2118,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dupload(h, &sinkp, sink.data(), N));
   M.sink_of_node = sinkp;
   M.icmp = sc->icmp ? 1u : 0u;
+  M.trace_kinds = 0xfu;
   // ---- state ----
   {  // the device records' reset image: tx state idle, the static parameters
     std::vector<DevRec> dr(D);
@@ -2688,6 +2720,18 @@ extern "C" int nsgpu_p2p_set_trace(nsgpu_p2p *h, uint64_t cap) {
   h->M.trace_n = tn;
   NSGPU_HIP(hipMemset(h->M.trace_n, 0, sizeof(unsigned long long)));
   h->M.trace_cap = cap;
+  if (h->gexec) {
+    (void)hipGraphExecDestroy(h->gexec);
+    h->gexec = nullptr;
+  }
+  return NSGPU_OK;
+}
+
+// Which trace sinks the runs record (bit k = nsgpu_trace_kind k).
+extern "C" int nsgpu_p2p_set_trace_kinds(nsgpu_p2p *h, uint32_t mask) {
+  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_trace_kinds: null");
+  if (mask & ~0x7fu) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_trace_kinds: unknown kind bits 0x%x", mask);
+  h->M.trace_kinds = mask;
   if (h->gexec) {
     (void)hipGraphExecDestroy(h->gexec);
     h->gexec = nullptr;

@@ -39,7 +39,7 @@ struct HubEv {
   uint32_t pkind, pa;  // pkind == 0: none
   uint32_t n, seq;     // children and trace sink calls the node part made
   uint32_t cancelled, pad;  // pad: the node part's inline DoForwardUp children
-  uint32_t ctx, pad2;       // the event's context (its Schedule calls inherit it)
+  uint32_t ctx, xdrop;      // the event's context (its Schedule calls inherit it); NodeOut::xdrop
 };
 
 constexpr int HUBL = 1024;  // events of a hub a block sorts in LDS (more: the window is dispatched as a run)
@@ -598,6 +598,7 @@ __device__ __forceinline__ void device_act_cached(const P2PDev &M, Emit &E, cons
   bool go = false;
   Pkt tx{0, 0, 0, 0};
   if (act.op == ACT_SEND) {
+    trace_call(M, E, NSGPU_TR_IP_TX, d, act.p);
     Pkt p = act.p;
     p.size += 2;  // PppHeader
     if (D.cnt >= D.qmax) {
@@ -781,6 +782,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
       bool go = false;
       Pkt tx{0, 0, 0, 0};
       if (h.op == ACT_SEND) {
+        trace_call(M, E, NSGPU_TR_IP_TX, d, h.p);
         Pkt p = h.p;
         p.size += 2;  // PppHeader
         if (x >= qmax) {
@@ -816,6 +818,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
         E.child(txTime + ifg, h.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
         E.child(txTime + delay, peer_node, K_RECEIVE, peer, tx);
       }
+      if (h.xdrop) trace_te_drop(M, E, h.xdrop - 1, h.p);
       if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
       M.nchild[s] = E.n;
       M.ninl[s] = 0;
@@ -928,13 +931,16 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           atomicAdd(&M.dev[a].c.rx_packets, 1u);
           p.size -= 2;
           trace_call(M, E, NSGPU_TR_RX, a, p);
+          trace_call(M, E, NSGPU_TR_IP_RX, a, p);
           const uint32_t out = route_of(M, c, p);
           if (out == 0xffffffffu) {
             hs.no_route++;
+            trace_ip_drop(M, E, a, p);
           } else {
             p.ttl -= 1;
-            if (p.ttl == 0) {
+            if (p.ttl == 0) {  // (ICMP off: stateless_event)
               hs.ttl_drops++;
+              trace_ip_drop(M, E, out, Pkt{p.app, p.ipid, p.size, 1u});
             } else {
               h.op = ACT_SEND;
               h.dev = out;
@@ -964,7 +970,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
         uint32_t ni = 0;
         for (uint32_t jj = 0; jj < E.n; jj++) ni += (M.ch_kind[E.slot0 + jj] & 0xffu) == K_FWD_UP;
         M.hx[s] = HubEv{o.act.op, o.act.dev, o.act.p, o.post.delay, o.post.valid ? o.post.kind : 0u, o.post.a, E.n,
-                        E.trseq, o.cancelled ? 1u : 0u, ni, b_ctx[q], 0};
+                        E.trseq, o.cancelled ? 1u : 0u, ni, b_ctx[q], o.xdrop};
       }
     }
     __syncthreads();
@@ -1045,6 +1051,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           E.demote = rel == slo || rel == shi;
           hs.cancelled += h.cancelled;
           device_act_cached(M, E, Act{h.op, h.dev, h.p}, D);
+          if (h.xdrop) trace_te_drop(M, E, h.xdrop - 1, h.p);
           if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
           const uint32_t ni = rel < inline_lim ? h.pad : 0u;
           M.nchild[s] = E.n;

@@ -129,6 +129,7 @@ SIGNATURES = {
     "nsgpu_p2p_last_run_ms": (C.c_int, [_vp, C.POINTER(C.c_double)]),
     "nsgpu_p2p_set_eager": (C.c_int, [_vp, C.c_int]),
     "nsgpu_p2p_set_trace": (C.c_int, [_vp, _u64]),
+    "nsgpu_p2p_set_trace_kinds": (C.c_int, [_vp, C.c_uint32]),
     "nsgpu_p2p_trace_read": (C.c_int, [_vp, _vp, _u64, C.POINTER(C.c_uint64), _vp]),
     "nsgpu_p2p_phase_read": (C.c_int, [_vp, C.c_int, C.c_int]),
     "nsgpu_p2p_kernel_count": (C.c_int, [C.POINTER(C.c_int)]),

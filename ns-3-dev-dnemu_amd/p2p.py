@@ -20,6 +20,7 @@ import numpy as np
 import nsgpu
 
 # nsgpu_trace_record (include/nsgpu_types.h): one ascii trace sink call
+TRACE_DEVICE_KINDS, TRACE_IPV4_KINDS = 0x0F, 0x70  # nsgpu_trace_kind bits: the device sinks, Ipv4L3Protocol's
 TRACE_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("seq", "<u2"), ("kind", "u1"), ("pad_", "u1"),
                                ("dev", "<u4"), ("app", "<u4"), ("ipid", "<u4"), ("size", "<u4"),
                                ("ttl", "<u4"), ("pad2_", "<u4")])
@@ -523,9 +524,12 @@ class Engine:
     def set_eager(self, eager=True):
         nsgpu.check(nsgpu.lib().nsgpu_p2p_set_eager(self.h, int(eager)))
 
-    def set_trace(self, cap):
-        """Record the ascii/pcap trace sink calls of every run (nsgpu_p2p_set_trace), up to `cap`."""
+    def set_trace(self, cap, kinds=TRACE_DEVICE_KINDS):
+        """Record the ascii/pcap trace sink calls of every run (nsgpu_p2p_set_trace), up to `cap`: the
+        nsgpu_trace_kind bits in `kinds` (nsgpu_p2p_set_trace_kinds; TRACE_IPV4_KINDS adds the
+        Ipv4L3Protocol Tx / Rx / Drop sinks)."""
         nsgpu.check(nsgpu.lib().nsgpu_p2p_set_trace(self.h, int(cap)))
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_set_trace_kinds(self.h, int(kinds)))
         self.trace_cap = int(cap)
 
     def trace(self):
@@ -684,13 +688,14 @@ class LoopbackGroup:
     """Every partition of one scenario on this GPU (nsgpu_p2p_group_*): the partitioned algorithm
     with device-to-device copies in place of the RCCL collectives — its parity harness on one device."""
 
-    def __init__(self, scenario, nranks, owner=None, log_cap=0, pool_cap=0, stream=None, trace_cap=0):
+    def __init__(self, scenario, nranks, owner=None, log_cap=0, pool_cap=0, stream=None, trace_cap=0,
+                 trace_kinds=None):
         self.owner = owner_blocks(scenario.n_nodes, nranks) if owner is None else np.asarray(owner, np.uint32)
         self.members = [DistEngine(scenario, self.owner, r, nranks, None, log_cap, pool_cap, stream)
                         for r in range(nranks)]
         if trace_cap:
             for m in self.members:
-                m.set_trace(trace_cap)
+                m.set_trace(trace_cap, TRACE_DEVICE_KINDS if trace_kinds is None else trace_kinds)
         self.stream = stream
         arr = (C.c_void_p * nranks)(*[m.h for m in self.members])
         h = C.c_void_p()

@@ -28,11 +28,14 @@ import numpy as np
 import p2p
 
 TR_ENQUEUE, TR_DEQUEUE, TR_DROP, TR_RX = 0, 1, 2, 3
+TR_IP_TX, TR_IP_RX, TR_IP_DROP = 4, 5, 6  # Ipv4L3Protocol Tx / Rx / Drop (InternetStackHelper::EnableAsciiIpv4)
+_L3 = (TR_RX, TR_IP_TX, TR_IP_RX, TR_IP_DROP)  # records of the packet without its PppHeader
 PKT_REPLY = 0x80000000
 PKT_ICMP, PKT_ICMP_UNREACH, PKT_ICMP_OF_REPLY, PKT_APP = 0x40000000, 0x20000000, 0x10000000, 0x0FFFFFFF
 TRACE_RECORD_DTYPE = p2p.TRACE_RECORD_DTYPE  # nsgpu_trace_record
-_CHAR = {TR_ENQUEUE: "+", TR_DEQUEUE: "-", TR_DROP: "d", TR_RX: "r"}
-_SOURCE = {TR_ENQUEUE: "TxQueue/Enqueue", TR_DEQUEUE: "TxQueue/Dequeue", TR_DROP: "TxQueue/Drop", TR_RX: "MacRx"}
+_CHAR = {TR_ENQUEUE: "+", TR_DEQUEUE: "-", TR_DROP: "d", TR_RX: "r", TR_IP_TX: "t", TR_IP_RX: "r", TR_IP_DROP: "d"}
+_SOURCE = {TR_ENQUEUE: "TxQueue/Enqueue", TR_DEQUEUE: "TxQueue/Dequeue", TR_DROP: "TxQueue/Drop", TR_RX: "MacRx",
+           TR_IP_TX: "Tx", TR_IP_RX: "Rx", TR_IP_DROP: "Drop"}
 PPP_HDR = 2
 
 
@@ -182,9 +185,9 @@ class Codec:
         if int(r["app"]) & PKT_ICMP:
             return self.icmp_text(r)
         src, dst, sp, dp = self.headers(int(r["app"]))
-        ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
+        ip_len = int(r["size"]) - (0 if r["kind"] in _L3 else PPP_HDR)
         parts = []
-        if r["kind"] != TR_RX:
+        if r["kind"] not in _L3:
             parts.append("ns3::PppHeader (Point-to-Point Protocol: IP (0x0021))")
         parts.append("ns3::Ipv4Header (tos 0x0 DSCP Default ECN Not-ECT ttl %d id %d protocol 17 offset (bytes) 0 "
                      "flags [none] length: %d %s > %s)" % (int(r["ttl"]) & 255, int(r["ipid"]) & 0xffff, ip_len,
@@ -198,11 +201,11 @@ class Codec:
         336-347, 435-446): the embedded header, then " org data=" and its 8 payload bytes, each followed
         by a space."""
         own_src, own_dst, (osrc, odst, osp, odp, ottl, oid, olen) = self.icmp_fields(r)
-        ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
+        ip_len = int(r["size"]) - (0 if r["kind"] in _L3 else PPP_HDR)
         unreach = bool(int(r["app"]) & PKT_ICMP_UNREACH)
         data = struct.pack(">HHHH", osp, odp, olen - 20, 0)
         parts = []
-        if r["kind"] != TR_RX:
+        if r["kind"] not in _L3:
             parts.append("ns3::PppHeader (Point-to-Point Protocol: IP (0x0021))")
         parts.append("ns3::Ipv4Header (%s)" % self._ipv4_text(int(r["ttl"]), int(r["ipid"]), 1, ip_len, own_src, own_dst))
         parts.append("ns3::Icmpv4Header (type=%d, code=%d)" % ((3, 3) if unreach else (11, 0)))
@@ -212,12 +215,20 @@ class Codec:
         return " ".join(parts)
 
     def ascii(self, tr):
-        """The EnableAsciiAll (stream) file of a sorted record stream, as one string."""
+        """The ascii file of a sorted record stream, as one string: PointToPointHelper::EnableAsciiAll
+        (stream) lines for the device records and InternetStackHelper::EnableAsciiIpv4All (stream) lines
+        (internet-stack-helper.cc:650-730, INTERFACE_CONTEXT: "<c> <s> /NodeList/<n>/$ns3::Ipv4L3Protocol/
+        <Tx|Rx|Drop>(<interface>) <packet>", the packet from its Ipv4Header on) for the Ipv4 records, in
+        record order (both helpers given one stream)."""
         out = []
         for r in tr:
             d = int(r["dev"])
-            ctx = "/NodeList/%d/DeviceList/%d/$ns3::PointToPointNetDevice/%s" % (
-                self.dev_node[d], self.ifindex[d], _SOURCE[int(r["kind"])])
+            k = int(r["kind"])
+            if k >= TR_IP_TX:
+                ctx = "/NodeList/%d/$ns3::Ipv4L3Protocol/%s(%d)" % (self.dev_node[d], _SOURCE[k], self.sc.dev_ifindex[d])
+            else:
+                ctx = "/NodeList/%d/DeviceList/%d/$ns3::PointToPointNetDevice/%s" % (
+                    self.dev_node[d], self.ifindex[d], _SOURCE[k])
             out.append("%s %s %s %s\n" % (_CHAR[int(r["kind"])], seconds_text(int(r["ts"])), ctx, self.packet_text(r)))
         return "".join(out)
 
@@ -226,7 +237,7 @@ class Codec:
         """Serialized packet with its PPP header (what the sniffer sees)."""
         if int(r["app"]) & PKT_ICMP:  # IPv4 (protocol 1) + Icmpv4Header + TimeExceeded / DestinationUnreachable
             own_src, own_dst, (osrc, odst, osp, odp, ottl, oid, olen) = self.icmp_fields(r)
-            ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
+            ip_len = int(r["size"]) - (0 if r["kind"] in _L3 else PPP_HDR)
             unreach = bool(int(r["app"]) & PKT_ICMP_UNREACH)
             ipv4 = struct.pack(">BBHHHBBHII", 0x45, 0, ip_len, int(r["ipid"]) & 0xffff, 0, int(r["ttl"]) & 255, 1, 0,
                                own_src, own_dst)
@@ -234,7 +245,7 @@ class Codec:
             org = struct.pack(">BBHHHBBHII", 0x45, 0, olen, oid & 0xffff, 0, ottl, 17, 0, osrc, odst)
             return struct.pack(">H", 0x0021) + ipv4 + icmp + org + struct.pack(">HHHH", osp, odp, olen - 20, 0)
         src, dst, sp, dp = self.headers(int(r["app"]))
-        ip_len = int(r["size"]) - (0 if r["kind"] == TR_RX else PPP_HDR)
+        ip_len = int(r["size"]) - (0 if r["kind"] in _L3 else PPP_HDR)
         ipv4 = struct.pack(">BBHHHBBHII", 0x45, 0, ip_len, int(r["ipid"]) & 0xffff, 0, int(r["ttl"]) & 255, 17, 0,
                            src, dst)
         udp = struct.pack(">HHHH", sp, dp, ip_len - 20, 0)

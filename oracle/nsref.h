@@ -137,6 +137,8 @@ int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_de
                   uint64_t log_cap, double *run_seconds);
 /* The same run, also recording every ascii trace sink call (nsgpu_trace_record, pop order) when
  * trace_n is non-NULL: *trace_n = records made, the first trace_cap of them copied to trace. */
+/* Trace kinds the next nsref_p2p_run_trace / _probe runs record: bit k = nsgpu_trace_kind k (default 0xf). */
+void nsref_p2p_set_trace_kinds(uint32_t mask);
 int nsref_p2p_run_trace(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
                         nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
                         uint64_t log_cap, double *run_seconds, nsgpu_trace_record *trace, uint64_t trace_cap,

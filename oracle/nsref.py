@@ -137,6 +137,8 @@ def lib():
         L.nsref_p2p_run_probe.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_uint32, C.c_uint32, C.c_uint32] + \
             [C.c_void_p] * 7 + [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
         L.nsref_p2p_run_trace.restype = C.c_int
+        L.nsref_p2p_set_trace_kinds.argtypes = [C.c_uint32]
+        L.nsref_p2p_set_trace_kinds.restype = None
         L.nsref_distribution_ns.argtypes = [C.c_double]
         L.nsref_distribution_ns.restype = C.c_uint64
         _lib = L
@@ -375,8 +377,13 @@ TRACE_RECORD_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("seq", "<u2"), ("
                                ("ttl", "<u4"), ("pad2_", "<u4")])  # nsgpu_trace_record
 
 
-def p2p_run_trace(scenario_struct, stats_struct, devc, appc, log_cap=0):
-    """p2p_run that also returns the ascii trace sink calls (TRACE_RECORD_DTYPE, pop order)."""
+TRACE_DEVICE_KINDS, TRACE_IPV4_KINDS = 0x0F, 0x70  # nsgpu_trace_kind bits: the device sinks, Ipv4L3Protocol's
+
+
+def p2p_run_trace(scenario_struct, stats_struct, devc, appc, log_cap=0, kinds=TRACE_DEVICE_KINDS):
+    """p2p_run that also returns the ascii trace sink calls (TRACE_RECORD_DTYPE, pop order) of the
+    nsgpu_trace_kind bits in `kinds`."""
+    lib().nsref_p2p_set_trace_kinds(kinds)
     secs = C.c_double()
     lts = np.zeros(log_cap, np.uint64)
     luid = np.zeros(log_cap, np.uint32)
@@ -388,6 +395,7 @@ def p2p_run_trace(scenario_struct, stats_struct, devc, appc, log_cap=0):
     lib().nsref_p2p_run_trace(*args, None, 0, C.byref(n))  # count
     tr = np.zeros(n.value, TRACE_RECORD_DTYPE)
     lib().nsref_p2p_run_trace(*args, tr.ctypes.data, n.value, C.byref(n))
+    lib().nsref_p2p_set_trace_kinds(TRACE_DEVICE_KINDS)
     return secs.value, (lts, luid, lctx), tr
 
 
@@ -395,8 +403,10 @@ APP_COUNTERS_DTYPE = np.dtype([("tx_packets", "<u4"), ("rx_packets", "<u4"), ("t
                                ("rx_bytes", "<u8")])  # nsgpu_app_counters
 
 
-def p2p_run_probe(scenario_struct, stats_struct, devc, appc, t0, period, count, app_send, app_obs, log_cap=0):
+def p2p_run_probe(scenario_struct, stats_struct, devc, appc, t0, period, count, app_send, app_obs, log_cap=0,
+                  kinds=TRACE_DEVICE_KINDS):
     """p2p run with the host probe application of nsref_p2p_run_probe; returns (log, trace, samples)."""
+    lib().nsref_p2p_set_trace_kinds(kinds)
     from numpy import zeros
     lts = zeros(log_cap, np.uint64)
     luid = zeros(log_cap, np.uint32)
@@ -409,6 +419,7 @@ def p2p_run_probe(scenario_struct, stats_struct, devc, appc, t0, period, count, 
     lib().nsref_p2p_run_probe(*args, None, 0, C.byref(n))
     tr = np.zeros(n.value, TRACE_RECORD_DTYPE)
     lib().nsref_p2p_run_probe(*args, tr.ctypes.data, n.value, C.byref(n))
+    lib().nsref_p2p_set_trace_kinds(TRACE_DEVICE_KINDS)
     return (lts, luid, lctx), tr, samples
 
 

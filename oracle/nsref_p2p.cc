@@ -70,8 +70,9 @@ struct Model {
   uint16_t tr_seq = 0;
   uint32_t tr_uid = 0;
   uint64_t tr_ts = ~0ull;
+  uint32_t tr_kinds = 0xfu;  // nsgpu_trace_kind bits recorded (nsref_p2p_set_trace_kinds)
   void tr(uint8_t kind, uint32_t d, const Pkt &p) {
-    if (!trace) return;
+    if (!trace || !((tr_kinds >> kind) & 1u)) return;
     if (sim.m_currentUid != tr_uid || sim.m_currentTs != tr_ts) {  // a new dispatched event
       tr_uid = sim.m_currentUid;
       tr_ts = sim.m_currentTs;
@@ -199,7 +200,19 @@ struct Model {
     dev[d].c.rx_packets++;
     p.size -= 2;  // ProcessHeader strips the PPP header
     tr(NSGPU_TR_RX, d, p);  // m_macRxTrace
-    ip_receive(s.dev_node[d], p);
+    tr(NSGPU_TR_IP_RX, d, p);  // Ipv4L3Protocol::Receive: m_rxTrace (ipv4-l3-protocol.cc:455)
+    ip_receive(s.dev_node[d], p, d);
+  }
+  // SendRealOut: m_txTrace (the packet with its IPv4 header), then the interface's device (:764-765)
+  void ip_out(uint32_t out, const Pkt &p) {
+    tr(NSGPU_TR_IP_TX, out, p);
+    device_send(out, p);
+  }
+  // m_dropTrace (header, packet, reason, ipv4, interface): the header as received; a UDP datagram's
+  // record keeps its 16-bit id (an ICMP descriptor's packs the embedded one too)
+  void ip_drop(uint32_t d, Pkt p) {
+    if (!(p.app & NSGPU_PKT_ICMP)) p.ipid &= 0xffffu;
+    tr(NSGPU_TR_IP_DROP, d, p);
   }
 
   // ---------------- IPv4 + UDP ----------------
@@ -220,10 +233,10 @@ struct Model {
     }
     e.ipid |= node_ipid[n]++ & 0xffffu;
     icmp_sent++;
-    device_send(out, e);
+    ip_out(out, e);
   }
 
-  void ip_receive(uint32_t n, Pkt p) {  // Ipv4L3Protocol::Receive -> RouteInput
+  void ip_receive(uint32_t n, Pkt p, uint32_t rx_dev) {  // Ipv4L3Protocol::Receive -> RouteInput
     if (pkt_dst_node(p) == n) {  // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407)
       // an ICMP error ends in Icmpv4L4Protocol::Receive -> HandleTimeExceeded / HandleDestUnreach ->
       // UdpL4Protocol::ReceiveIcmp -> the endpoint's (null) ICMP callback: nothing is scheduled
@@ -251,18 +264,21 @@ struct Model {
       return;
     }
     const uint32_t out = next_hop(n, pkt_dst_slot(p));
-    if (out == 0xffffffffu) {  // DROP_NO_ROUTE
+    if (out == 0xffffffffu) {  // DROP_NO_ROUTE (:505)
       no_route_drops++;
+      ip_drop(rx_dev, p);
       return;
     }
     // IpForward (ipv4-l3-protocol.cc:815-841)
+    const Pkt received = p;
     p.ttl -= 1;
     if ((p.ttl & 0xffu) == 0) {  // DROP_TTL_EXPIRED, after SendTimeExceededTtl (never about an ICMP message)
       ttl_drops++;
       if (s.icmp && !(p.app & NSGPU_PKT_ICMP)) icmp_send(n, p, false);
+      ip_drop(out, received);  // (:835: the forwarding route's interface, the header as received)
       return;
     }
-    device_send(out, p);
+    ip_out(out, p);
   }
   void ip_send(uint32_t n, Pkt p) {  // UdpSocketImpl::DoSendTo (RouteOutput) -> Ipv4L3Protocol::Send
     const uint32_t out = next_hop(n, pkt_dst_slot(p));
@@ -271,7 +287,7 @@ struct Model {
       return;
     }
     p.ipid = node_ipid[n]++;  // BuildHeader: SetIdentification (m_identification++)
-    device_send(out, p);
+    ip_out(out, p);
   }
 
   // ---------------- OnOffApplication ----------------
@@ -409,7 +425,13 @@ struct Model {
   }
 };
 
+uint32_t g_trace_kinds = 0xfu;
+
 }  // namespace
+
+// The trace kinds the next runs record (bit k = nsgpu_trace_kind k; default 0xf, the device sinks):
+// nsgpu_p2p_set_trace_kinds' counterpart.
+extern "C" void nsref_p2p_set_trace_kinds(uint32_t mask) { g_trace_kinds = mask; }
 
 extern "C" int nsref_p2p_run_trace(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats,
                                    nsgpu_dev_counters *devc, nsgpu_app_counters *appc, uint64_t *log_ts,
@@ -418,6 +440,7 @@ extern "C" int nsref_p2p_run_trace(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats
   Model *m = new Model();
   std::vector<nsgpu_trace_record> tv;
   if (trace_n) m->trace = &tv;
+  m->tr_kinds = g_trace_kinds;
   m->s = *sc;
   m->sim.want_digest = true;
   m->sim.log_ts = log_ts;
@@ -464,6 +487,7 @@ extern "C" int nsref_p2p_run_probe(const nsgpu_p2p_scenario *sc, int64_t t0, int
   Model *m = new Model();
   std::vector<nsgpu_trace_record> tv;
   if (trace_n) m->trace = &tv;
+  m->tr_kinds = g_trace_kinds;
   m->s = *sc;
   m->sim.want_digest = true;
   m->sim.log_ts = log_ts;

@@ -93,19 +93,19 @@ def test_partitioned_trace_union(nranks):
 
 
 # ---------------------------------------------------------------- UDP echo (config 1: first.cc)
-def gpu_full(sc, log_cap, trace_cap):
+def gpu_full(sc, log_cap, trace_cap, kinds=nsref.TRACE_DEVICE_KINDS):
     eng = p2p.Engine(sc, log_cap=log_cap)
-    eng.set_trace(trace_cap)
+    eng.set_trace(trace_cap, kinds)
     st, devc, appc, log = eng.run(log_n=log_cap)
     return st, devc, appc, log, trace.sort_records(eng.trace())
 
 
-def oracle_full(sc, log_cap):
+def oracle_full(sc, log_cap, kinds=nsref.TRACE_DEVICE_KINDS):
     s = sc.c_struct()
     st = p2p.P2PStats()
     devc = np.zeros(s.n_devices, p2p.DEV_COUNTERS_DTYPE)
     appc = np.zeros(s.n_apps, p2p.APP_COUNTERS_DTYPE)
-    _secs, log, tr = nsref.p2p_run_trace(s, st, devc, appc, log_cap)
+    _secs, log, tr = nsref.p2p_run_trace(s, st, devc, appc, log_cap, kinds=kinds)
     return st, devc, appc, log, trace.sort_records(tr)
 
 
