@@ -14,8 +14,8 @@
 // with ts <= its own, so every pending event with key <= that bound is safe to dispatch.
 //   * single GPU: nsgpu_p2p_win.h — k2_pa / k2_handle / k2_scan per window (in-place pool, hub blocks,
 //     sorted runs for windows larger than WCAP), replayed from a hipGraph;
-//   * partitioned (one rank per GPU, or a loopback group on one GPU): k_pa<true>, k_refit_d, X0,
-//     k_cut, k_handle_rank<true>, X1, k_gtile, k_dfin, X2 below.
+//   * partitioned (one rank per GPU, or a loopback group on one GPU): the same k2_pa / k2_handle over
+//     each rank's nodes, then k_gtile / k_dfin2 below, with the X0 / X1 / X2 exchanges.
 #include <hip/hip_ext.h>
 #include <stddef.h>
 #include "nsgpu_device.h"
@@ -44,7 +44,7 @@ enum EvKind : uint32_t {
 constexpr int WCAP = 4096;       // events per window
 constexpr int TB = 256;          // threads per block, pool sweeps
 constexpr int HB = 64;           // threads per block, per-slot kernels (spread over CUs)
-constexpr int NHB = WCAP / HB;   // handler blocks of k_handle_rank
+constexpr int NHB = WCAP / HB;   // holder blocks of k2_handle
 constexpr int RJ = 256;          // keys per rank tile column
 constexpr int NJT = WCAP / RJ;   // rank tile columns
 constexpr int RTR = 1;           // window keys (rows) per thread of a rank tile (4: same traffic, slower)
@@ -57,7 +57,6 @@ constexpr int NSLOT = 7;         // per-node slot table entries
 constexpr int NTAB = NSLOT + 1;  // words per node table record (count + slots)
 constexpr int NWIN = 32;         // windows per graph replay
 constexpr uint32_t NOCTX = 0xffffffffu;
-constexpr uint32_t NOCHAIN = 0xffffffffu;
 
 // Packet descriptor: flow (sending app), IPv4 identification (Ipv4L3Protocol::m_identification of
 // the originating node), size in bytes with the headers added so far, IPv4 TTL.
@@ -92,16 +91,16 @@ struct Red {
 // it; its leftovers and children fold into red[k & 1].
 struct Ctl {
   Red red[2];
-  uint64_t P;                          // pending events in pool `cur` (besides the last window's children)
   uint64_t K;                          // dispatched so far (after the last scanned window)
-  uint64_t tmin, bound, inline_lim;    // current window (k_pa / refit)
+  uint64_t tmin, bound, inline_lim;    // current window (k2_pa / the partitioned cut)
   uint64_t windows, max_window, last_ts, max_windows, refits;
   uint64_t digest, cancelled, ttl_drops, no_route, unreach, icmp;
-  uint64_t pK0, ptmin, pinline_lim;    // the last scanned window, appended by the next k_pa
-  uint32_t uid, cur, W, nxtP, overflow, prep, done, stop_seen;  // (W, nxtP: one 64-bit word for classify)
-  uint32_t puid0, pW, pvalid, pinl;
-  uint32_t collected, pad1;  // partitioned: k_refit_d already moved the window slots to the pool
-  uint64_t pcol;             // (and the pool count after that)
+  uint64_t pK0, ptmin, pinline_lim;    // the last scanned window, appended by the next k2_pa
+  // (W, nxtP, overflow, prep): a partitioned rank's X0 payload, sent from here — its window candidates,
+  // (unused), a hub too large for a block, the window is the cut of the last one
+  uint32_t puid0, pW, uid, hdl;
+  uint32_t W, nxtP, overflow, prep;  // (16-B aligned: the X0 payload)
+  uint32_t done, stop_seen, pvalid, pinl;
   // ---- single-GPU engine (k2_*: in-place pool, sorted runs, hub blocks) ----
   uint64_t P_end, live, nfree;  // pool scan range, live pool entries, free-stack entries
   uint64_t r0, rW;              // sorted run: start of the next chunk, run length
@@ -115,7 +114,7 @@ struct Ctl {
   uint32_t huid, pad4;             //   window's last timestamp (W_end or the host event's); the host uid
 };
 
-static_assert(offsetof(Ctl, nxtP) == offsetof(Ctl, W) + 4 && offsetof(Ctl, W) % 8 == 0, "classify's 64-bit add");
+static_assert(offsetof(Ctl, prep) == offsetof(Ctl, W) + 12 && offsetof(Ctl, W) % 16 == 0, "the X0 payload");
 
 // Device-resident model + engine state (all pointers are HBM).  Passed to the kernels by value.
 struct P2PDev {
@@ -169,7 +168,8 @@ struct P2PDev {
   // partitioned run (dist != 0): this engine owns the nodes n with owner[n] == rank
   uint32_t dist, rank, nranks, pad_d;
   const uint32_t *owner;
-  uint64_t *x0_send, *x0_recv;  // X0: 2 u64 per rank
+  uint64_t *x0_send, *x0_recv;  // X0: 16 B per rank (x0_send points at the run control's X0 payload)
+  uint64_t *xk_send, *xk_recv;  // the cut's exchange (host-driven): one rank's largest fitting key (16 B)
   uint8_t *x1_send, *x1_recv;   // X1: X1B bytes per rank
   uint8_t *x2_send, *x2_recv;   // X2: x2b bytes per peer
   uint32_t capx, pad_x;         // X2 records per peer per window (the run's largest cut between two ranks)
@@ -913,8 +913,8 @@ struct Ev {
 // X1: a rank's window summary, allgathered.  LbtsMessage's role (distributed-simulator-impl.h:36-84:
 // rx/tx counts, smallest next time) is played by the pending-set reduction `red` and the counts.
 struct X1Hdr {
-  uint32_t W, tc, tinl, pad;  // window events, their children, their inline (DoForwardUp) children
-  uint64_t nxtP, lastkey;     // pending events left out of the window; largest window key
+  uint32_t W, tc, tinl, needc;  // window events, their children, their inline children; pool compaction wanted
+  uint64_t pad0, lastkey;     // largest window key
   Red red;                    // reduction of this rank's pending set after the window (next LBTS)
   uint64_t pad2[8];
 };
@@ -947,451 +947,7 @@ __device__ __forceinline__ Ev *x2rec(const P2PDev &M, uint8_t *b, uint32_t q) {
   return (Ev *)(b + (size_t)q * M.x2b + sizeof(X2Hdr));
 }
 
-// Writes window slot `slot` (and the node's slot table).
-__device__ __forceinline__ void put_window(const P2PDev &M, uint32_t slot, uint64_t pk, const Ev &e) {
-  M.wkey[slot] = pk;
-  M.wctx[slot] = e.ctx;
-  M.wkind[slot] = e.kind;
-  M.wa[slot] = e.a;
-  M.wpkt[slot] = e.p;
-  uint32_t idx = 0;
-  if (e.ctx < M.n_nodes) {
-    idx = atomicAdd(&M.node_tab[(uint64_t)e.ctx * NTAB], 1u);
-    if (idx < (uint32_t)NSLOT) M.node_tab[(uint64_t)e.ctx * NTAB + 1 + idx] = slot;
-  }
-  M.widx[slot] = idx;
-}
-__device__ __forceinline__ void put_pool(const P2PDev &M, int pool, uint64_t o, const Ev &e) {
-  if (o < M.pool_cap) {
-    M.ev_ts[pool][o] = e.ts;
-    M.ev_uid[pool][o] = e.uid;
-    M.ev_ctx[pool][o] = e.ctx;
-    M.ev_kind[pool][o] = e.kind;
-    M.ev_a[pool][o] = e.a;
-    M.ev_pkt[pool][o] = e.p;
-  } else {
-    atomicOr(M.error, 1u);
-  }
-}
-__device__ __forceinline__ Ev load_pool(const P2PDev &M, int pool, uint64_t i) {
-  return Ev{M.ev_ts[pool][i], M.ev_uid[pool][i], M.ev_ctx[pool][i], M.ev_kind[pool][i], M.ev_a[pool][i],
-            M.ev_pkt[pool][i]};
-}
-
-// Classifies a pending event against the window bound: window -> slot records (+ the node's slot
-// table), otherwise -> pool `nxt` (and the next window's reduction).  A window candidate past WCAP
-// sets C.overflow and also goes to pool `nxt` (the refit takes it from there).  All 64 lanes of the
-// wave must call it (ballots).
-__device__ __forceinline__ void classify(const P2PDev &M, Ctl &C, const WinBound &b, int nxt, bool valid,
-                                         const Ev &e, Red &R, uint64_t &tmn, uint64_t &wnd) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
-  const bool in = valid && (e.ts - b.tmin <= b.span) && pk <= b.bound;
-  const uint64_t bin = __ballot(in);
-  const uint64_t bout0 = __ballot(valid && !in);
-  uint32_t basein = 0, baseout = 0;
-  if (lane == 0 && (bin | bout0)) {  // both slot ranges in ONE 64-bit add on the adjacent words (W, nxtP)
-    const unsigned long long v = (unsigned long long)__popcll(bin) | ((unsigned long long)__popcll(bout0) << 32);
-    const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long *>(&C.W), v);
-    basein = (uint32_t)old;
-    baseout = (uint32_t)(old >> 32);
-  }
-  basein = __shfl(basein, 0);
-  baseout = __shfl(baseout, 0);
-  const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t slot = basein + (uint32_t)__popcll(bin & below);
-  const bool to_win = in && slot < (uint32_t)WCAP;
-  const bool ovf = in && !to_win;
-  const uint64_t bovf = __ballot(ovf);
-  uint32_t baseovf = 0;
-  if (bovf) {
-    if (lane == 0) {
-      C.overflow = 1;
-      baseovf = atomicAdd(&C.nxtP, (uint32_t)__popcll(bovf));
-    }
-    baseovf = __shfl(baseovf, 0);
-  }
-  if (to_win) {
-    put_window(M, slot, pk, e);
-  } else if (valid) {
-    const uint64_t o = ovf ? baseovf + (uint64_t)__popcll(bovf & below) : baseout + (uint64_t)__popcll(bout0 & below);
-    put_pool(M, nxt, o, e);
-    if (!ovf) {
-      tmn = e.ts < tmn ? e.ts : tmn;
-      const uint64_t x = e.ts + (uint64_t)M.lookahead[e.kind & 0xffu];
-      wnd = x < wnd ? x : wnd;
-      if ((e.kind & 0xffu) == K_STOP) {  // at most one Stop event is pending
-        R.stopts = e.ts;
-        R.stopuid = e.uid;
-      }
-    }
-  }
-}
-
-// ---- k_pa: append the last scanned window (dispatch log / digest; its children get their uids and
-// become pending) and partition the pending set into the next window ----
-// Pending set = pool `cur` (P entries) + the non-inline children of the last window.  Thread g <
-// WCAP takes slot g of the last window; thread WCAP + i (grid-stride) takes pool entry i.
-constexpr int PFC = 4;  // children per slot loaded ahead
-// DIST: the partitioned engine's variant (remote-event role, X1 reduction target, owner filter);
-// the single-GPU instantiation carries none of it.
-template <bool DIST>
-__global__ __launch_bounds__(TB) void k_pa(const P2PDev M) {
-  PH_BEGIN();
-  Ctl &C = *M.C;
-  const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
-  const uint64_t stride = (uint64_t)gridDim.x * TB;
-  // remote-event threads (partitioned), whole blocks: the roles must stay wave-uniform (ballots)
-  const uint64_t RR = DIST ? ((uint64_t)M.nranks * M.capx + TB - 1) / TB * TB : 0;
-  const bool slot_role = g < (uint64_t)WCAP;                   // (roles are wave-uniform)
-  const bool remote_role = !slot_role && g < WCAP + RR;
-  if (C.prep || C.done >= 2) return;  // window already prepared by the refit / run over
-  const bool partition = C.done == 0;
-  const int cur = C.cur, nxt = cur ^ 1;
-  const uint64_t win = C.windows;
-  const WinBound b = window_bound(C.red[(win + 1) & 1]);
-  Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[win & 1];
-  if (partition && blockIdx.x == 0 && threadIdx.x == 0) publish_bound(C, b);
-  const uint64_t P = partition ? C.P : 0;
-  const uint32_t pW = C.pvalid ? C.pW : 0;
-  uint64_t spk = 0;
-  uint4 si = make_uint4(0, 0, 0, 0);
-  uint32_t ncr = 0, sctx = 0;
-  Ev ce[PFC];
-  if (slot_role && g < pW) {  // the last window's slot and its first children, all at once
-    const uint32_t s = (uint32_t)g;
-    spk = M.pwkey[s];
-    si = M.sinfo[s];
-    ncr = M.nchild[s];
-    sctx = M.pwctx[s];
-#pragma unroll
-    for (int j = 0; j < PFC; j++) {
-      const uint32_t sl = s * M.maxc + j;
-      if ((uint32_t)j < M.maxc)
-        ce[j] = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
-    }
-  }
-  PH_MARK(0);
-  uint64_t tmn = ~0ull, wnd = ~0ull, digest = 0;
-  if (slot_role) {
-    // ---- slot g of the last window: dispatch rank (log, digest), inline children, children -> pending
-    const bool vs = g < pW;
-    const uint32_t s = (uint32_t)g;
-    const uint64_t rel = spk >> 32;
-    const uint64_t t = C.ptmin + rel;
-    const uint32_t uid0 = C.puid0;
-    const uint64_t K0 = C.pK0, ilim = C.pinline_lim;
-    if (vs) {
-      const uint64_t rk = K0 + si.x;
-      digest += digest_term(rk, t, (uint32_t)spk);
-      if (rk < M.log_cap) {
-        M.log_ts[rk] = t;
-        M.log_uid[rk] = (uint32_t)spk;
-        M.log_ctx[rk] = sctx;
-      }
-    }
-    if (__ballot(vs)) {
-      uint32_t ii = 0;
-      for (uint32_t j = 0; j < M.maxc; j++) {
-        const bool has = vs && j < ncr;
-        if (!__ballot(has)) break;
-        Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-        bool valid = false;
-        if (has) {
-          if (j < (uint32_t)PFC) {
-#pragma unroll
-            for (int q = 0; q < PFC; q++)
-              if ((uint32_t)q == j) e = ce[q];
-          } else {
-            const uint32_t sl = s * M.maxc + j;
-            e = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
-          }
-          e.uid = uid0 + si.z + j;
-          if ((e.kind & 0xffu) == K_FWD_UP) {  // leaf: dispatched inside its window (or never), not queued
-            if (rel < ilim) {
-              const uint64_t crk = K0 + si.y + ii;
-              digest += digest_term(crk, t, e.uid);
-              if (crk < M.log_cap) {
-                M.log_ts[crk] = t;
-                M.log_uid[crk] = e.uid;
-                M.log_ctx[crk] = e.ctx;
-              }
-              ii++;
-            }
-          } else {  // (partitioned: a child on another rank's node went there through X2)
-            valid = partition && (!DIST || M.owner[e.ctx] == M.rank);
-          }
-        }
-        if (__ballot(valid)) classify(M, C, b, nxt, valid, e, R, tmn, wnd);
-      }
-    }
-  } else if (DIST && remote_role) {
-    // ---- remote events received through X2 (partitioned): record idx % capx from rank idx / capx
-    const uint64_t idx = g - WCAP;
-    const uint32_t q = (uint32_t)(idx / M.capx), rec = (uint32_t)(idx % M.capx);
-    const bool valid = partition && q < M.nranks && rec < x2hdr(M, M.x2_recv, q)->n;
-    Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-    if (valid) e = x2rec(M, M.x2_recv, q)[rec];
-    if (__ballot(valid)) classify(M, C, b, nxt, valid, e, R, tmn, wnd);
-  } else {
-    // ---- pool entries (grid-stride over the threads of the pool role)
-    for (uint64_t i = g - WCAP - RR; i < P; i += stride - WCAP - RR) {
-      const Ev e = load_pool(M, cur, i);
-      classify(M, C, b, nxt, true, e, R, tmn, wnd);
-    }
-  }
-  PH_MARK(1);
-  publish_min<TB>(R, tmn, wnd);
-  digest = wave_sum64(digest);
-  if ((threadIdx.x & 63) == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
-  PH_MARK(2);
-}
-
-// ---- k_handle_rank: the holder of each node (slot index 0 in its table) runs the node's window
-// events in key order, so node state (device tx state, DropTail rings, OnOff state, sink counters)
-// needs no atomics; children go to per-slot records in Schedule-call order.  The launch's other
-// blocks rank the window keys by tiled all-pairs counting (keys are distinct: uids).
-// Zero-delay leaf children (K_FWD_UP: Ipv4EndPoint::DoForwardUp, ipv4-end-point.cc:112-120) run at
-// their key position: after the node's events with ts <= theirs, before the first with a larger ts.
-__device__ __forceinline__ uint32_t nth_slot_scan(const P2PDev &M, uint32_t W, uint32_t c, uint64_t after) {
-  // slot of the smallest key > `after` among the window events of node c (long tables only)
-  uint64_t best = ~0ull;
-  uint32_t bs = NOCHAIN;
-  for (uint32_t x = 0; x < W; x++)
-    if (M.wctx[x] == c) {
-      const uint64_t k = M.wkey[x];
-      if (k > after && k < best) {
-        best = k;
-        bs = x;
-      }
-    }
-  return bs;
-}
-
-// Long chains (a hub node with more than CH events in the window): the next CH slots of node c
-// with keys > `after`, ascending, into my / mk — one pass over the window per CH events instead of
-// one per event.  Returns how many it found.
-__device__ __forceinline__ uint32_t chain_refill(const P2PDev &M, uint32_t W, uint32_t c, uint64_t after, uint32_t *my,
-                                                 uint64_t *mk) {
-  uint32_t m = 0;
-  auto consider = [&](uint32_t x, uint32_t cx, uint64_t k) {
-    if (cx != c || k <= after || (m == (uint32_t)CH && k >= mk[CH - 1])) return;
-    uint32_t b = m < (uint32_t)CH ? m++ : (uint32_t)CH - 1;
-    while (b > 0 && mk[b - 1] > k) {
-      mk[b] = mk[b - 1];
-      my[b] = my[b - 1];
-      b--;
-    }
-    mk[b] = k;
-    my[b] = x;
-  };
-  // 8 slots per step, contexts and keys loaded together (16-B loads: one memory round trip per 8
-  // slots instead of one or two per slot)
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-  const uint32_t W8 = W & ~7u;
-  for (uint32_t x = 0; x < W8; x += 8) {
-    const u32x4 c0 = *reinterpret_cast<const u32x4 *>(M.wctx + x);
-    const u32x4 c1 = *reinterpret_cast<const u32x4 *>(M.wctx + x + 4);
-    const u64x2 k0 = *reinterpret_cast<const u64x2 *>(M.wkey + x);
-    const u64x2 k1 = *reinterpret_cast<const u64x2 *>(M.wkey + x + 2);
-    const u64x2 k2 = *reinterpret_cast<const u64x2 *>(M.wkey + x + 4);
-    const u64x2 k3 = *reinterpret_cast<const u64x2 *>(M.wkey + x + 6);
-    consider(x + 0, c0.x, k0.x);
-    consider(x + 1, c0.y, k0.y);
-    consider(x + 2, c0.z, k1.x);
-    consider(x + 3, c0.w, k1.y);
-    consider(x + 4, c1.x, k2.x);
-    consider(x + 5, c1.y, k2.y);
-    consider(x + 6, c1.z, k3.x);
-    consider(x + 7, c1.w, k3.y);
-  }
-  for (uint32_t x = W8; x < W; x++) consider(x, M.wctx[x], M.wkey[x]);
-  return m;
-}
-
-template <bool DIST>
-__device__ __forceinline__ void handle_node(const P2PDev &M, Ctl &C, uint32_t i0) {
-  __shared__ uint32_t chs[HB * CH];
-  __shared__ uint64_t chk[HB * CH];
-  // slot i0's record, ahead of the run control
-  const uint32_t idx0 = M.widx[i0], c = M.wctx[i0];
-  const uint64_t key0 = M.wkey[i0];
-  const uint32_t kind0 = M.wkind[i0], a0 = M.wa[i0];
-  const Pkt pkt0 = M.wpkt[i0];
-  const uint32_t W = C.W;
-  Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[C.windows & 1];
-  uint64_t tmn = ~0ull, wnd = ~0ull;
-  HStat hs{0, 0, 0, 0, 0, false};
-  uint32_t dtc = 0, dti = 0;  // partitioned: the X1 summary's child totals and largest key
-  uint64_t dlk = 0;
-#ifdef NSGPU_PHASE_PROF
-  uint64_t tq[4] = {0, 0, 0, 0};
-  const uint64_t tq0 = __builtin_amdgcn_s_memrealtime();
-#define HQ(k) tq[k] = __builtin_amdgcn_s_memrealtime()
-#else
-#define HQ(k) (void)0
-#endif
-  if (i0 < W && idx0 == 0) {  // the holder
-    uint32_t n = 1;
-    int32_t sink = -1;
-    if (c < M.n_nodes) {
-      n = M.node_tab[(uint64_t)c * NTAB];
-      sink = M.sink_of_node[c];
-      M.node_tab[(uint64_t)c * NTAB] = 0;
-    }
-    HQ(0);
-    uint32_t *my = &chs[threadIdx.x * CH];
-    uint64_t *mk = &chk[threadIdx.x * CH];
-    const bool small = n <= (uint32_t)CH;
-    if (small && n > 1) {
-      const uint32_t ns = n < (uint32_t)NSLOT ? n : (uint32_t)NSLOT;
-      for (uint32_t j = 0; j < ns; j++) my[j] = M.node_tab[(uint64_t)c * NTAB + 1 + j];
-      if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
-        uint32_t m = NSLOT;
-        for (uint32_t x = 0; x < W && m < n; x++)
-          if (M.wctx[x] == c && M.widx[x] >= (uint32_t)NSLOT) my[m++] = x;
-      }
-      for (uint32_t j = 0; j < n; j++) mk[j] = M.wkey[my[j]];
-      for (uint32_t a = 1; a < n; a++) {  // insertion sort by key
-        const uint32_t v = my[a];
-        const uint64_t kv = mk[a];
-        uint32_t bb = a;
-        while (bb > 0 && mk[bb - 1] > kv) {
-          my[bb] = my[bb - 1];
-          mk[bb] = mk[bb - 1];
-          bb--;
-        }
-        my[bb] = v;
-        mk[bb] = kv;
-      }
-    }
-    HQ(1);
-    const uint64_t tmin = C.tmin;
-    const uint64_t inline_lim = C.inline_lim;
-    Emit E;
-    E.ctx = c;
-    E.ch_ts = M.ch_ts;
-    E.ch_ctx = M.ch_ctx;
-    E.ch_kind = M.ch_kind;
-    E.ch_a = M.ch_a;
-    E.ch_pkt = M.ch_pkt;
-    E.lookahead = M.lookahead;
-    E.tmn = ~0ull;
-    E.wnd = ~0ull;
-    E.demote = false;
-    uint64_t lastk = 0;
-    uint32_t ts0_it = 0, pending = 0;
-    uint32_t bp = 0, bl = 0;  // long chains: position / length of the my / mk batch
-    uint64_t cur_rel = 0;
-    for (uint32_t it = 0; it <= n; it++) {
-      uint32_t s = NOCHAIN;
-      uint64_t key = ~0ull;
-      if (it < n) {
-        if (n == 1) {
-          s = i0;
-          key = key0;
-        } else if (small) {
-          s = my[it];
-          key = mk[it];
-        } else {
-          if (bp == bl) {
-            bl = chain_refill(M, W, c, lastk, my, mk);
-            bp = 0;
-          }
-          s = bl ? my[bp] : i0;  // (bl == 0 cannot happen: node_cnt counts the node's slots)
-          key = bl ? mk[bp] : key0;
-          bp++;
-        }
-      }
-      const uint64_t rel = it < n ? (key >> 32) : ~0ull;
-      if (it > 0 && rel > cur_rel && pending) {
-        // flush the inline children of this node's events at cur_rel (positions [ts0_it, it))
-        uint64_t aft = 0;
-        for (uint32_t jt = 0; jt < it; jt++) {
-          const uint32_t xr = n == 1 ? i0 : small ? my[jt] : nth_slot_scan(M, W, c, aft);
-          aft = n == 1 ? key0 : small ? mk[jt] : M.wkey[xr];
-          if (jt < ts0_it) continue;
-          const uint32_t ncr = M.nchild[xr];
-          for (uint32_t j = 0; j < ncr; j++) {
-            const uint32_t sl = xr * M.maxc + j;
-            if ((E.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
-            const uint32_t sa = E.ch_a[sl];  // DoForwardUp -> PacketSink::HandleRead
-            if (M.app_flags[sa] & 2u) {
-              M.appc[sa].rx_packets++;
-              M.appc[sa].rx_bytes += E.ch_pkt[sl].size - 28;
-            }
-          }
-        }
-        pending = 0;
-      }
-      if (it == n) break;
-      if (it == 0 || rel > cur_rel) {
-        ts0_it = it;
-        cur_rel = rel;
-      }
-      E.now = tmin + rel;
-      E.slot0 = s * M.maxc;
-      E.n = 0;
-      E.uid = (uint32_t)key;
-      E.trseq = 0;
-      const bool own = s == i0;
-      const uint32_t kw = own ? kind0 : M.wkind[s];
-      const uint32_t ea = own ? a0 : M.wa[s];
-      const Pkt ep = own ? pkt0 : M.wpkt[s];
-      hs.cancelled += run_event(M, E, kw, ea, ep, sink, hs);
-      uint32_t ni = 0;
-      if (rel < inline_lim)
-        for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
-      M.nchild[s] = E.n;
-      M.ninl[s] = ni;
-      if (DIST) {
-        x1ent(M.x1_send, 0)[s] = X1Ent{key, E.n | (ni << 16), 0};
-        dtc += E.n;
-        dti += ni;
-        dlk = key > dlk ? key : dlk;
-      }
-      pending += ni;
-      lastk = key;
-    }
-    tmn = E.tmn;
-    wnd = E.wnd;
-    HQ(2);
-  }
-#ifdef NSGPU_PHASE_PROF
-  {
-    uint64_t d0 = tq[0] ? tq[0] - tq0 : 0, d1 = tq[1] ? tq[1] - tq[0] : 0, d2 = tq[2] ? tq[2] - tq[1] : 0;
-    d0 = wave_max64(d0);
-    d1 = wave_max64(d1);
-    d2 = wave_max64(d2);
-    const uint32_t nh = wave_sum32(tq[0] ? 1u : 0u);
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-      atomicAdd((unsigned long long *)&g_phase[12], (unsigned long long)d0);
-      atomicAdd((unsigned long long *)&g_phase[13], (unsigned long long)d1);
-      atomicAdd((unsigned long long *)&g_phase[14], (unsigned long long)d2);
-      atomicAdd((unsigned long long *)&g_phase[15], (unsigned long long)nh);
-    }
-  }
-#endif
-  publish_min<HB>(R, tmn, wnd);
-  if (DIST) {
-    dtc = wave_sum32(dtc);
-    dti = wave_sum32(dti);
-    dlk = wave_max64(dlk);
-    if ((threadIdx.x & 63) == 0) {
-      X1Hdr *h = x1hdr(M.x1_send, 0);
-      if (dtc) atomicAdd(&h->tc, dtc);
-      if (dti) atomicAdd(&h->tinl, dti);
-      if (dlk) atomicMax((unsigned long long *)&h->lastkey, (unsigned long long)dlk);
-    }
-  }
-  if (hs.stop) C.stop_seen = 1;
-  if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
-  if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
-  if (hs.no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)hs.no_route);
-  if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
-  if (hs.icmp) atomicAdd((unsigned long long *)&C.icmp, (unsigned long long)hs.icmp);
-}
+constexpr int PFC = 4;  // children per slot k2_pa loads ahead
 
 // Rank tile t: rows [ti * HB * RTR, +HB * RTR) of the window (RTR keys per thread) against the RJ keys
 // of column tile tj: each row's count of smaller keys is added to its rank (keys are distinct: uids).
@@ -1436,56 +992,39 @@ __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_
   }
 }
 
-template <bool DIST>
-__global__ __launch_bounds__(HB) void k_handle_rank(const P2PDev M) {
-  PH_BEGIN();
-  Ctl &C = *M.C;
-  if (C.done || C.overflow) {
-    if (C.done == 1 && blockIdx.x == 0 && threadIdx.x == 0) C.done = 2;  // the final window is appended
-    return;
-  }
-#ifdef NSGPU_PHASE_PROF
-  const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  PH_MARK(8);
-  if (blockIdx.x < (uint32_t)NHB) handle_node<DIST>(M, C, blockIdx.x * HB + threadIdx.x);
-  else rank_tile(M, C, blockIdx.x - NHB);
-  PH_MARK(9);
-#ifdef NSGPU_PHASE_PROF
-  const uint64_t th1 = __builtin_amdgcn_s_memrealtime();
-  if (blockIdx.x < (uint32_t)NHB) atomicMax((unsigned long long *)&g_phase[10], (unsigned long long)(th1 - th0));
-  else atomicMax((unsigned long long *)&g_phase[11], (unsigned long long)(th1 - th0));
-#endif
-}
+#include "nsgpu_p2p_win.h"
 
-// ---- refit: the window overflowed WCAP (single-GPU: k_scan's block; partitioned: k_refit_d + k_cut) ----
-// Pending set = pool `nxt` (the non-window events and the overflowed candidates) + the recorded
-// window slots.  The slots go back to the pool (refit_collect), a 256-way radix bisection finds the
-// largest key prefix that fits (refit_bisect; a key prefix of a safe window is safe), and the pool
-// is partitioned in place (refit_partition; chunked: every chunk is read before any of its
-// compacted writes land).  All SCAN_THREADS threads of one workgroup call each step.
-__device__ __forceinline__ uint64_t refit_collect(const P2PDev &M, Ctl &C, const WinBound &b, uint32_t nrec) {
-  const int nxt = C.cur ^ 1;
-  const uint64_t P0 = C.nxtP;
-  for (uint32_t s = threadIdx.x; s < nrec; s += SCAN_THREADS) {
-    const uint32_t c = M.wctx[s];
-    if (c < M.n_nodes) M.node_tab[(uint64_t)c * NTAB] = 0;
-    const uint64_t pk = M.wkey[s];
-    Ev e{b.tmin + (pk >> 32), (uint32_t)pk, c, M.wkind[s], M.wa[s], M.wpkt[s]};
-    put_pool(M, nxt, P0 + s, e);
-  }
-  __syncthreads();
-  return P0 + nrec;
-}
+// ================================ partitioned run (multi-GPU) ================================
+// DistributedSimulatorImpl (src/mpi/model/distributed-simulator-impl.cc:146-326) gives every rank
+// the nodes of its system id and grants it min over ranks of (next ts) + lookahead after an
+// MPI_Allgather of LbtsMessage (:276-313); remote packets travel as {rx ns, node, dev, serialized
+// packet} (mpi-interface.cc:414-506).  Here every rank runs the single-GPU engine's window kernels
+// over its own nodes, and three fixed-size collectives per window (RCCL, captured into the window
+// graph with the kernels) make the partitioned run reproduce the SEQUENTIAL pop order — uids
+// included, which DistributedSimulatorImpl itself does not (its uids are per rank, SURVEY H6):
+//   k2_pa<true>  as single-GPU (in-place pool), plus the remote events of the last X2;
+//   X0           allgather of every rank's window size and hub flag (16 B, straight from Ctl);
+//   k2_handle    holders and hub blocks (no rank tiles), writing this rank's X1 summary and entries —
+//                unless some rank's window does not fit: then nothing runs and the host cuts the
+//                window on every rank at the smallest of their largest fitting keys (k_refit2,
+//                allgather, k_cut2; a key prefix of a safe window is safe);
+//   X1           allgather of the summaries;
+//   k_gtile      per own event, over the merged windows: # smaller keys (global dispatch rank) and the
+//                child / inline-child sums below it and below its same-ts group (uid prefixes);
+//   k_dfin2      own events' dispatch info, remote children -> X2 with their final uids, the pool
+//                bookkeeping, and the run bookkeeping from the merged summaries: the LBTS (the next
+//                window's bound), `done`, a compaction every rank makes;
+//   X2           all-to-all of remote events.
 
-__device__ uint64_t refit_bisect(const P2PDev &M, Ctl &C, const WinBound &b, uint64_t P) {
+// The largest key lo with at most T of the window's n candidates <= lo (256-way radix bisection over
+// (0, bound]; count (<= bound) > T).  All SCAN_THREADS threads of the block call it.
+__device__ uint64_t window_bisect(const P2PDev &M, uint64_t n, uint64_t bound, uint32_t T) {
   __shared__ uint32_t hist[256];
   __shared__ uint64_t s_lo, s_hi;
   __shared__ uint32_t s_clo;
-  const int nxt = C.cur ^ 1;
   if (threadIdx.x == 0) {
-    s_lo = 0;        // count(keys <= lo) <= WCAP (the smallest key is >= 4: uids start at 4)
-    s_hi = b.bound;  // count(keys <= hi) > WCAP
+    s_lo = 0;  // (every key is >= 4: uids start at 4)
+    s_hi = bound;
     s_clo = 0;
   }
   __syncthreads();
@@ -1496,31 +1035,16 @@ __device__ uint64_t refit_bisect(const P2PDev &M, Ctl &C, const WinBound &b, uin
     while (((range - 1) >> sh) >= 256) sh++;
     for (int j = threadIdx.x; j < 256; j += SCAN_THREADS) hist[j] = 0;
     __syncthreads();
-    for (uint64_t i = threadIdx.x; i < P; i += SCAN_THREADS) {
-      const uint64_t t = M.ev_ts[nxt][i];
-      bool hit = false;
-      uint32_t bk = 0;
-      if (t - b.tmin <= b.span) {
-        const uint64_t k = ((t - b.tmin) << 32) | M.ev_uid[nxt][i];
-        hit = k > lo && k <= hi;
-        bk = hit ? (uint32_t)((k - lo - 1) >> sh) : 0u;
-      }
-      // wave-aggregate the common case (every hitting lane in one bucket): one LDS atomic
-      const uint64_t m = __ballot(hit);
-      if (m) {
-        const int first = __ffsll((unsigned long long)m) - 1;
-        const uint32_t b0 = __shfl(bk, first);
-        const uint64_t same = __ballot(hit && bk == b0);
-        if ((threadIdx.x & 63) == first) atomicAdd(&hist[b0], (uint32_t)__popcll(same));
-        if (hit && bk != b0) atomicAdd(&hist[bk], 1u);
-      }
+    for (uint64_t i = threadIdx.x; i < n; i += SCAN_THREADS) {
+      const uint64_t k = M.wkey[i];
+      if (k > lo && k <= hi) atomicAdd(&hist[(uint32_t)((k - lo - 1) >> sh)], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
       uint32_t c = s_clo;
       int j = -1;
-      while (j + 1 < 256 && c + hist[j + 1] <= (uint32_t)WCAP) c += hist[++j];
-      // keys <= lo + (j + 1) << sh: c <= WCAP; keys <= lo + (j + 2) << sh: > WCAP
+      while (j + 1 < 256 && c + hist[j + 1] <= T) c += hist[++j];
+      // keys <= lo + (j + 1) << sh: c <= T; keys <= lo + (j + 2) << sh: > T
       const uint64_t nlo = lo + ((uint64_t)(j + 1) << sh);
       const uint64_t nhi = lo + ((uint64_t)(j + 2) << sh);
       s_lo = nlo;
@@ -1534,147 +1058,145 @@ __device__ uint64_t refit_bisect(const P2PDev &M, Ctl &C, const WinBound &b, uin
   return r;
 }
 
-// Partitions pool nxt [0, P) in place with bound b.bound: window -> slots, the rest compacted and
-// folded into R (reset first).  Sets C.W, C.nxtP and publishes the bound.
-__device__ void refit_partition(const P2PDev &M, Ctl &C, const WinBound &b, uint64_t P, Red &R) {
-  __shared__ uint32_t s_nw, s_no;
-  __shared__ uint32_t wsum[2][SCAN_THREADS / 64];
-  const int nxt = C.cur ^ 1;
+// Host-driven cut, step 1 (one block): this rank's largest fitting key -> xk_send.  A rank holds WCAP
+// window events, HUBL when a hub is too large for a block (Ctl::overflow).
+__global__ __launch_bounds__(SCAN_THREADS) void k_refit2(const P2PDev M) {
+  Ctl &C = *M.C;
+  const uint64_t bound = C.bound;
+  const uint32_t W = C.W;
+  const uint32_t T = C.overflow ? (uint32_t)HUBL : (uint32_t)WCAP;
+  const uint64_t n = W < M.runcap ? W : M.runcap;
+  uint64_t lb = bound;
+  if (W > T || C.overflow) lb = window_bisect(M, n, bound, T);
   if (threadIdx.x == 0) {
-    publish_bound(C, b);
-    R.tmin = R.wend = R.stopts = ~0ull;
+    M.xk_send[0] = lb;
+    M.xk_send[1] = 0;
+  }
+}
+
+// Host-driven cut, step 2 (one block, after the allgather of the keys): the window becomes its
+// candidates with key <= g (the smallest fitting key of all ranks), compacted in place with fresh slot
+// tables; the others become pending again (a pool entry stays where it is, a child or a remote event
+// is parked in the fresh buffer) and fold into this rank's reduction.  The next k2_pa finds the window
+// formed (C.prep).
+__global__ __launch_bounds__(SCAN_THREADS) void k_cut2(const P2PDev M) {
+  Ctl &C = *M.C;
+  __shared__ uint32_t s_nw, s_nf;
+  __shared__ uint32_t wsum[2][SCAN_THREADS / 64];
+  uint64_t g = ~0ull;
+  for (uint32_t q = 0; q < M.nranks; q++) g = M.xk_recv[2 * q] < g ? M.xk_recv[2 * q] : g;
+  const uint64_t bound = C.bound, tmin = C.tmin;
+  const uint32_t W = C.W;
+  const uint64_t n = W < M.runcap ? W : M.runcap;
+  const uint64_t nF0 = C.nF;
+  // the slot tables of the candidate slots (rebuilt below for the ones kept)
+  const uint64_t nt = n < (uint64_t)WCAP ? n : (uint64_t)WCAP;
+  for (uint64_t s = threadIdx.x; s < nt; s += SCAN_THREADS) {
+    const uint32_t c = lp_of(M, M.wctx[s], M.wkind[s], M.wa[s]);
+    if (c < M.n_nodes) M.node_tab[(uint64_t)c * NTAB] = 0;
+  }
+  if (threadIdx.x == 0) {
     s_nw = 0;
-    s_no = 0;
+    s_nf = 0;
+    C.nhub = 0;
+    C.overflow = 0;
   }
   __syncthreads();
+  Red &R = x1hdr(M.x1_send, 0)->red;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
   uint64_t tmn = ~0ull, wnd = ~0ull;
-  for (uint64_t c0 = 0; c0 < P; c0 += SCAN_THREADS) {
+  for (uint64_t c0 = 0; c0 < n; c0 += SCAN_THREADS) {
     const uint64_t i = c0 + threadIdx.x;
-    const bool valid = i < P;
-    Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-    if (valid) e = load_pool(M, nxt, i);
-    const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
-    const bool in = valid && (e.ts - b.tmin <= b.span) && pk <= b.bound;
-    const bool out = valid && !in;
-    const uint64_t bi = __ballot(in), bo = __ballot(out);
-    const uint64_t below = (1ull << lane) - 1ull;
+    const bool valid = i < n;
+    uint64_t key = 0;
+    uint32_t ctx = 0, kind = 0, a = 0, src = NOSRC;
+    Pkt p{0, 0, 0, 0};
+    if (valid) {
+      key = M.wkey[i];
+      ctx = M.wctx[i];
+      kind = M.wkind[i];
+      a = M.wa[i];
+      p = M.wpkt[i];
+      src = M.wsrc[i];
+    }
+    const bool keep = valid && key <= g;
+    const bool park = valid && !keep && src == NOSRC;
+    const uint64_t bk = __ballot(keep), bp = __ballot(park);
     if (lane == 0) {
-      wsum[0][wid] = (uint32_t)__popcll(bi);
-      wsum[1][wid] = (uint32_t)__popcll(bo);
+      wsum[0][wid] = (uint32_t)__popcll(bk);
+      wsum[1][wid] = (uint32_t)__popcll(bp);
     }
-    __syncthreads();  // (also: every read of this chunk is done)
-    uint32_t oi = s_nw, oo = s_no, ti = 0, to = 0;
+    __syncthreads();  // (also: every read of this chunk is done; kept records only move down)
+    uint32_t ok = s_nw, of = s_nf, tk = 0, tf = 0;
     for (int w = 0; w < SCAN_THREADS / 64; w++) {
-      oi += w < wid ? wsum[0][w] : 0;
-      oo += w < wid ? wsum[1][w] : 0;
-      ti += wsum[0][w];
-      to += wsum[1][w];
+      ok += w < wid ? wsum[0][w] : 0;
+      of += w < wid ? wsum[1][w] : 0;
+      tk += wsum[0][w];
+      tf += wsum[1][w];
     }
-    if (in) put_window(M, oi + (uint32_t)__popcll(bi & below), pk, e);
-    if (out) {
-      put_pool(M, nxt, oo + (uint64_t)__popcll(bo & below), e);
-      tmn = e.ts < tmn ? e.ts : tmn;
-      const uint64_t x = e.ts + (uint64_t)M.lookahead[e.kind & 0xffu];
+    if (keep) {
+      const uint64_t o = ok + (uint32_t)__popcll(bk & below);
+      M.wkey[o] = key;
+      M.wctx[o] = ctx;
+      M.wkind[o] = kind;
+      M.wa[o] = a;
+      M.wpkt[o] = p;
+      M.wsrc[o] = src;
+    } else if (valid) {
+      const uint64_t ts = tmin + (key >> 32);
+      tmn = ts < tmn ? ts : tmn;
+      const uint64_t x = ts + (uint64_t)M.lookahead[kind & 0xffu];
       wnd = x < wnd ? x : wnd;
-      if ((e.kind & 0xffu) == K_STOP) {
-        R.stopts = e.ts;
-        R.stopuid = e.uid;
+      if ((kind & 0xffu) == K_STOP) {
+        R.stopts = ts;
+        R.stopuid = (uint32_t)key;
+      }
+      if (park) {
+        const uint64_t fi = nF0 + of + (uint32_t)__popcll(bp & below);
+        if (fi < M.fcap) {
+          M.f_ts[fi] = ts;
+          M.f_uid[fi] = (uint32_t)key;
+          M.f_ctx[fi] = ctx;
+          M.f_kind[fi] = kind;
+          M.f_a[fi] = a;
+          M.f_pkt[fi] = p;
+        } else {
+          atomicOr(M.error, 1u);
+        }
       }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      s_nw += ti;
-      s_no += to;
+      s_nw += tk;
+      s_nf += tf;
     }
     __syncthreads();
   }
   publish_min<SCAN_THREADS>(R, tmn, wnd);
-  if (threadIdx.x == 0) {
-    C.W = s_nw;
-    C.nxtP = s_no;
-    C.refits++;
-    C.overflow = 0;
-  }
-}
-
-#include "nsgpu_p2p_win.h"
-
-// ================================ partitioned run (multi-GPU) ================================
-// DistributedSimulatorImpl (src/mpi/model/distributed-simulator-impl.cc:146-326) gives every rank
-// the nodes of its system id and grants it min over ranks of (next ts) + lookahead after an
-// MPI_Allgather of LbtsMessage (:276-313); remote packets travel as {rx ns, node, dev, serialized
-// packet} (mpi-interface.cc:414-506).  Here every rank runs the single-GPU engine's conservative
-// windows over its own nodes, and three fixed-size collectives per window (RCCL, captured into the
-// window graph with the kernels) make the partitioned run reproduce the SEQUENTIAL pop order — uids
-// included, which DistributedSimulatorImpl itself does not (its uids are per rank, SURVEY H6):
-//   k_pa        as single-GPU, plus the remote events of the last X2;
-//   k_refit_d   this rank's largest fitting window bound (its own bisection if its window overflowed);
-//   X0          allgather of those bounds;
-//   k_cut       every rank cuts its window at the smallest (a key prefix of a safe window is safe);
-//   k_handle_rank  handlers (no rank tiles), writing this rank's X1 summary and window entries;
-//   X1          allgather of the summaries;
-//   k_gtile     per own event, over the merged windows: # smaller keys (global dispatch rank) and the
-//               child / inline-child sums below it and below its same-ts group (uid prefixes);
-//   k_dfin      own events' dispatch info, remote children -> X2 with their final uids, and the run
-//               bookkeeping from the merged summaries: the LBTS (next window's bound) and `done`;
-//   X2          all-to-all of remote events.
-
-__global__ __launch_bounds__(SCAN_THREADS) void k_refit_d(const P2PDev M) {
-  Ctl &C = *M.C;
-  if (C.done) return;
-  const uint64_t win = C.windows;
-  const WinBound b = window_bound(C.red[(win + 1) & 1]);
-  uint64_t lb = b.bound;
-  if (C.overflow) {
-    const uint64_t P = refit_collect(M, C, b, WCAP);
-    lb = refit_bisect(M, C, b, P);
-    if (threadIdx.x == 0) {
-      C.collected = 1;
-      C.pcol = P;
-    }
-  }
-  if (threadIdx.x == 0) {
-    M.x0_send[0] = lb;
-    M.x0_send[1] = 0;
-  }
-}
-
-__global__ __launch_bounds__(SCAN_THREADS) void k_cut(const P2PDev M) {
-  Ctl &C = *M.C;
-  if (C.done) return;
-  const uint64_t win = C.windows;
-  WinBound b = window_bound(C.red[(win + 1) & 1]);
-  uint64_t g = ~0ull;
-  for (uint32_t q = 0; q < M.nranks; q++) g = M.x0_recv[2 * q] < g ? M.x0_recv[2 * q] : g;
-  X1Hdr *h = x1hdr(M.x1_send, 0);
-  const bool collected = C.collected != 0;
-  if (C.overflow || g < b.bound) {  // (uniform: every thread reads the same words)
-    const uint32_t nrec = C.W < (uint32_t)WCAP ? C.W : (uint32_t)WCAP;
-    const uint64_t P = collected ? C.pcol : refit_collect(M, C, b, nrec);
-    b.bound = g;
-    refit_partition(M, C, b, P, h->red);
-  }
   __syncthreads();
+  const uint32_t Wk = s_nw;
+  for (uint32_t s = threadIdx.x; s < Wk && s < (uint32_t)WCAP; s += SCAN_THREADS)
+    node_table_add(M, C, s, lp_of(M, M.wctx[s], M.wkind[s], M.wa[s]), M.wkind[s]);
   if (threadIdx.x == 0) {
-    C.collected = 0;
-    h->W = C.W;
-    h->nxtP = C.nxtP;
-    // the window the next k_pa appends (run-global values: identical on every rank)
-    C.pK0 = C.K;
-    C.puid0 = C.uid;
-    C.ptmin = C.tmin;
-    C.pinline_lim = C.inline_lim;
-    C.pW = C.W;
-    C.pvalid = 1;
+    WinBound b = window_bound(C.rt ? C.red[0] : C.red[1]);  // (the window's own reduction)
+    b.bound = g < b.bound ? g : b.bound;
+    publish_bound(C, b);
+    C.split_lo = ~0ull;
+    // leaves at the cut's timestamp are queued: pending events of that timestamp sort before them
+    C.split_hi = g < bound ? (g >> 32) : b.span;
+    if (g < bound) C.refits++;
+    C.W = Wk;
+    C.nF = nF0 + s_nf;
+    C.prep = 1;
+    C.mode = MODE_NORMAL;
   }
-  for (uint32_t q = threadIdx.x; q < M.nranks; q += SCAN_THREADS) x2hdr(M, M.x2_send, q)->n = 0;
 }
 
 constexpr int GTB = 1024;  // blocks of k_gtile (grid-stride over tiles)
 __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
   Ctl &C = *M.C;
-  if (C.done) return;
+  if (!C.hdl) return;  // (k2_handle ran nothing: a cut, a pause, the end)
   __shared__ uint64_t tk[RJ];
   __shared__ uint32_t tc[RJ];
   __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR];
@@ -1732,9 +1254,11 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
   }
 }
 
-__global__ __launch_bounds__(HB) void k_dfin(const P2PDev M) {
+// Block 0 also does the pool bookkeeping (k2_scan's) and, last, the run bookkeeping; the other blocks
+// read only fields block 0 leaves alone (pW, puid0, hdl, done < 2).
+__global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   Ctl &C = *M.C;
-  if (C.done) return;
+  if (!C.hdl) return;
   const uint32_t W = C.pW;
   uint32_t tinl_g = 0;
   for (uint32_t q = 0; q < M.nranks; q++) tinl_g += x1hdr(M.x1_recv, q)->tinl;
@@ -1746,7 +1270,7 @@ __global__ __launch_bounds__(HB) void k_dfin(const P2PDev M) {
     A[WCAP + s] = 0;
     const uint32_t gr = (uint32_t)(w0 & 0x1fffffu), lp = (uint32_t)((w0 >> 21) & 0x1fffffu),
                    ip = (uint32_t)(w0 >> 42), cp = (uint32_t)w1, ipf = (uint32_t)(w1 >> 32);
-    // as k_scan: (dispatch rank rel. K0, rank of the first inline child, child prefix, inline prefix)
+    // as k2_scan: (dispatch rank rel. K0, rank of the first inline child, child prefix, inline prefix)
     M.sinfo[s] = make_uint4(gr + (tinl_g ? ipf : 0), lp + ip, cp, ip);
     M.pwkey[s] = M.wkey[s];
     M.pwctx[s] = M.wctx[s];
@@ -1765,48 +1289,70 @@ __global__ __launch_bounds__(HB) void k_dfin(const P2PDev M) {
         atomicOr(M.error, 16u);
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    uint32_t Wg = 0, tcg = 0;
-    uint64_t nPg = 0, lk = 0;
-    Red rg{~0ull, ~0ull, ~0ull, 0, 0};
-    for (uint32_t q = 0; q < M.nranks; q++) {
-      const X1Hdr *h = x1hdr(M.x1_recv, q);
-      Wg += h->W;
-      tcg += h->tc;
-      nPg += h->nxtP + h->tc - h->tinl;
-      if (h->W && h->lastkey > lk) lk = h->lastkey;
-      rg.tmin = h->red.tmin < rg.tmin ? h->red.tmin : rg.tmin;
-      rg.wend = h->red.wend < rg.wend ? h->red.wend : rg.wend;
-      if (h->red.stopts < rg.stopts) {
-        rg.stopts = h->red.stopts;
-        rg.stopuid = h->red.stopuid;
-      }
+  if (blockIdx.x != 0) return;
+  // ---- pool bookkeeping (k2_scan's): the free stack loses the slots the fresh children took and gains
+  // the window's; its pushed part is moved down over the popped hole; the hubs' slot tables are cleared
+  const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
+  const uint64_t consumed = nF < nfree ? nF : nfree;
+  const uint64_t mv = consumed < npush ? consumed : npush;
+  for (uint64_t i = threadIdx.x; i < mv; i += HB) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
+  const uint32_t nh = C.nhub < (uint32_t)MAXHUB ? C.nhub : (uint32_t)MAXHUB;
+  for (uint32_t h = threadIdx.x; h < nh; h += HB) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint32_t Wg = 0, tcg = 0, needc = 0;
+  uint64_t lk = 0;
+  Red rg{~0ull, ~0ull, ~0ull, 0, 0};
+  for (uint32_t q = 0; q < M.nranks; q++) {
+    const X1Hdr *h = x1hdr(M.x1_recv, q);
+    Wg += h->W;
+    tcg += h->tc;
+    needc |= h->needc;
+    if (h->W && h->lastkey > lk) lk = h->lastkey;
+    rg.tmin = h->red.tmin < rg.tmin ? h->red.tmin : rg.tmin;
+    rg.wend = h->red.wend < rg.wend ? h->red.wend : rg.wend;
+    if (h->red.stopts < rg.stopts) {
+      rg.stopts = h->red.stopts;
+      rg.stopuid = h->red.stopuid;
     }
-    const uint64_t win = C.windows;
-    C.K += Wg + tinl_g;
-    C.uid += tcg;
-    if (Wg) C.last_ts = C.tmin + (lk >> 32);
-    C.red[win & 1] = rg;  // bounds the next window (k_pa reads red[(win + 2) & 1])
-    C.windows = win + 1;
-    if (Wg > C.max_window) C.max_window = Wg;
-    C.P = C.nxtP;
-    C.cur ^= 1;
-    C.W = 0;
-    C.nxtP = 0;
-    // the window that held Simulator::Stop ends the run (every rank knows it from the bound)
-    bool done = C.inline_lim != ~0ull || nPg == 0;
-    if (C.windows >= C.max_windows && !done) {
-      atomicOr(M.error, 4u);
-      done = true;
-    }
-    if (done) C.done = 1;
-    X1Hdr *hs = x1hdr(M.x1_send, 0);
-    hs->W = hs->tc = hs->tinl = 0;
-    hs->nxtP = 0;
-    hs->lastkey = 0;
-    hs->red.tmin = hs->red.wend = hs->red.stopts = ~0ull;
-    hs->red.stopuid = 0;
   }
+  C.K = C.pK0 + Wg + tinl_g;
+  C.uid = C.puid0 + tcg;
+  if (Wg) C.last_ts = C.ptmin + (lk >> 32);
+  const uint32_t rt = C.rt;
+  C.red[rt] = rg;  // bounds the next window (k2_pa reads red[rt ^ 1] after the flip)
+  C.rt = rt ^ 1;
+  const uint64_t windows = C.windows + 1;
+  C.windows = windows;
+  if (Wg > C.max_window) C.max_window = Wg;
+  const uint64_t P_end = C.P_end + (nF > nfree ? nF - nfree : 0);
+  C.nfree = nfree - consumed + npush;
+  C.P_end = P_end;
+  C.live = C.live - npush + nF;
+  C.npush = 0;
+  C.nF = 0;
+  C.nhub = 0;
+  C.W = 0;
+  C.overflow = 0;
+  C.prep = 0;
+  // the window that held Simulator::Stop ends the run (every rank knows it from the bound), as does an
+  // empty pending set on every rank
+  bool done = C.inline_lim != ~0ull || rg.tmin == ~0ull;
+  if (P_end > M.pool_cap) {
+    atomicOr(M.error, 1u);
+    done = true;
+  }
+  if (windows >= C.max_windows && !done) {
+    atomicOr(M.error, 4u);
+    done = true;
+  }
+  if (done) C.done = 1;
+  else if (needc) C.mode = MODE_COMPACT;  // (every rank: the pipelines stay in step)
+  X1Hdr *hs = x1hdr(M.x1_send, 0);
+  hs->W = hs->tc = hs->tinl = hs->needc = 0;
+  hs->lastkey = 0;
+  hs->red.tmin = hs->red.wend = hs->red.stopts = ~0ull;
+  hs->red.stopuid = 0;
 }
 
 // Loopback transport (nsgpu_p2p_group_*: every partition on one device): one block per copy.
@@ -2217,10 +1763,10 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.ch_kind, chn));
   TRY(dalloc(h, &M.ch_a, chn));
   TRY(dalloc(h, &M.ch_pkt, chn));
-  // window records: WCAP for the partitioned engine; the single engine's hold a whole sorted run
+  // window records: a whole sorted run (single engine), a whole window before its cut (partitioned)
   M.fcap = chn;
-  M.runcap = owner ? (uint64_t)WCAP : M.pool_cap + M.fcap;
-  if (!owner && M.runcap >= 0xffffffffull) {
+  M.runcap = M.pool_cap + M.fcap;
+  if (M.runcap >= 0xffffffffull) {
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: pool_cap too large for 32-bit slots");
   }
@@ -2231,29 +1777,31 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.sinfo, WCAP));
   for (uint32_t **p : {&M.widx, &M.nchild, &M.ninl, &M.pwctx}) TRY(dalloc(h, p, WCAP));
   TRY(dalloc(h, &M.wrank, WCAP));
-  if (!owner) {  // in-place pool, fresh buffer, free stack, hub blocks, radix sort / compaction scratch
-    TRY(dalloc(h, &M.wsrc, M.runcap));
-    TRY(dalloc(h, &M.f_ts, M.fcap));
-    for (uint32_t **p : {&M.f_uid, &M.f_ctx, &M.f_kind, &M.f_a}) TRY(dalloc(h, p, M.fcap));
-    TRY(dalloc(h, &M.f_pkt, M.fcap));
-    TRY(dalloc(h, &M.fstack, M.pool_cap));
-    TRY(dalloc(h, &M.hub_list, MAXHUB));
-    TRY(dalloc(h, &M.hx, WCAP));
-    TRY(dalloc(h, &M.hub_key, (size_t)NHUB * WCAP));
-    TRY(dalloc(h, &M.hub_slot, (size_t)NHUB * WCAP));
+  // in-place pool, fresh buffer, free stack, hub blocks, compaction; radix sort scratch (single engine)
+  TRY(dalloc(h, &M.wsrc, M.runcap));
+  TRY(dalloc(h, &M.f_ts, M.fcap));
+  for (uint32_t **p : {&M.f_uid, &M.f_ctx, &M.f_kind, &M.f_a}) TRY(dalloc(h, p, M.fcap));
+  TRY(dalloc(h, &M.f_pkt, M.fcap));
+  TRY(dalloc(h, &M.fstack, M.pool_cap));
+  TRY(dalloc(h, &M.hub_list, MAXHUB));
+  TRY(dalloc(h, &M.hx, WCAP));
+  TRY(dalloc(h, &M.hub_key, (size_t)NHUB * WCAP));
+  TRY(dalloc(h, &M.hub_slot, (size_t)NHUB * WCAP));
+  TRY(dalloc(h, &M.cmp_cnt, 1));
+  if (!owner) {
     TRY(dalloc(h, &M.s_key2, M.runcap));
     for (uint32_t **p : {&M.s_val, &M.s_val2, &M.g_u32}) TRY(dalloc(h, p, M.runcap));
     TRY(dalloc(h, &M.s_hist, 256 * ((M.runcap + RS_TILE - 1) / RS_TILE)));
     TRY(dalloc(h, &M.g_pkt, M.runcap));
-    TRY(dalloc(h, &M.cmp_cnt, 1));
   }
   if (owner) {
     M.dist = 1;
     M.rank = (uint32_t)rank;
     M.nranks = (uint32_t)nranks;
     TRY(dupload(h, &M.owner, owner, N));
-    TRY(dalloc(h, &M.x0_send, 2));
     TRY(dalloc(h, &M.x0_recv, 2 * (size_t)nranks));
+    TRY(dalloc(h, &M.xk_send, 2));
+    TRY(dalloc(h, &M.xk_recv, 2 * (size_t)nranks));
     TRY(dalloc(h, &M.x1_send, X1B));
     TRY(dalloc(h, &M.x1_recv, X1B * nranks));
     if ((uint64_t)nranks * WCAP * M.maxc >= (1ull << 32))  // (k_gtile's packed child prefix)
@@ -2277,6 +1825,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     h->x1h0.red.tmin = h->x1h0.red.wend = h->x1h0.red.stopts = ~0ull;
   }
   TRY(dalloc(h, &M.C, 1));
+  if (owner) M.x0_send = reinterpret_cast<uint64_t *>(&M.C->W);  // X0 sends (W, nxtP, overflow, prep)
   TRY(dalloc(h, &M.error, 4));
   M.log_cap = log_cap;
   TRY(dalloc(h, &M.log_ts, log_cap));
@@ -2297,7 +1846,6 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   // run control after reset
   Ctl &C0 = h->C0;
   memset(&C0, 0, sizeof(C0));
-  C0.P = M.n_init;
   C0.uid = uid;
   // reduction of the initial pool: window 0 is bounded by red[1] (k_pa / k_handle_rank fold later
   // pending sets in for the next windows)
@@ -2381,8 +1929,9 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
   if (M.dist) {
     const size_t R = M.nranks;
-    NSGPU_HIP(hipMemsetAsync(M.x0_send, 0, X0B, s));
     NSGPU_HIP(hipMemsetAsync(M.x0_recv, 0, X0B * R, s));
+    NSGPU_HIP(hipMemsetAsync(M.xk_send, 0, 16, s));
+    NSGPU_HIP(hipMemsetAsync(M.xk_recv, 0, 16 * R, s));
     NSGPU_HIP(hipMemsetAsync(M.x1_send, 0, X1B, s));
     NSGPU_HIP(hipMemcpyAsync(M.x1_send, &h->x1h0, sizeof(X1Hdr), hipMemcpyHostToDevice, s));
     NSGPU_HIP(hipMemsetAsync(M.x1_recv, 0, X1B * R, s));
@@ -2407,7 +1956,7 @@ const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_scan"};
 // (hipExtLaunchKernelGGL: no separate marker packets between the pipeline's kernels).
 void launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   switch (k) {
-    case 0: hipExtLaunchKernelGGL(k2_pa, dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M); break;
+    case 0: hipExtLaunchKernelGGL(k2_pa<false>, dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M); break;
     case 1: hipExtLaunchKernelGGL(k2_handle, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M); break;
     default: hipExtLaunchKernelGGL(k2_scan, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M); break;
   }
@@ -2421,8 +1970,7 @@ void launch_windows(nsgpu_p2p *h, hipStream_t s) {
 // The host-driven steps of the single engine (rare; on the engine stream, after the pipeline has
 // paused itself): the radix sort that turns an overflowing window into a sorted run, and the pool
 // compaction.  `c` is the run control the pause left.
-static int host_step(nsgpu_p2p *h, const Ctl &c) {
-  hipStream_t s = h->s;
+static int host_step(nsgpu_p2p *h, const Ctl &c, hipStream_t s) {
   const P2PDev &M = h->M;
   if (c.mode == MODE_SORT) {
     const uint64_t n = c.rW;
@@ -2479,22 +2027,41 @@ static int host_step(nsgpu_p2p *h, const Ctl &c) {
   return NSGPU_OK;
 }
 
-// The partitioned window (one RCCL member): 6 kernels and 3 collectives, on stream s.
-static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s) {
+// The partitioned window (one RCCL member): 4 kernels and 3 collectives, on stream s.
+static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s, int nwin = NWIN) {
   ncclComm_t comm = h->comm->comm;
   const P2PDev &M = h->M;
-  for (int w = 0; w < NWIN; w++) {
-    hipLaunchKernelGGL(k_pa<true>, dim3(GRID_POOL), dim3(TB), 0, s, M);
-    hipLaunchKernelGGL(k_refit_d, dim3(1), dim3(SCAN_THREADS), 0, s, M);
+  for (int w = 0; w < nwin; w++) {
+    hipLaunchKernelGGL(k2_pa<true>, dim3(GRID_POOL), dim3(TB), 0, s, M);
     NCCL_TRY(ncclAllGather(M.x0_send, M.x0_recv, X0B, ncclUint8, comm, s));
-    hipLaunchKernelGGL(k_cut, dim3(1), dim3(SCAN_THREADS), 0, s, M);
-    hipLaunchKernelGGL(k_handle_rank<true>, dim3(NHB), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k2_handle, dim3(K2_GRID), dim3(HB), 0, s, M);
     NCCL_TRY(ncclAllGather(M.x1_send, M.x1_recv, X1B, ncclUint8, comm, s));
     hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, M);
-    hipLaunchKernelGGL(k_dfin, dim3(NHB), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k_dfin2, dim3(NHB), dim3(HB), 0, s, M);
     NCCL_TRY(ncclAllToAll(M.x2_send, M.x2_recv, M.x2b, ncclUint8, comm, s));
   }
   return NSGPU_OK;
+}
+
+// The partitioned engine's host-driven steps (every rank makes the same ones: the pause that asks
+// for them is decided from exchanged data): the pool compaction, and the window cut — k_refit2, an
+// allgather of the keys (`cut`'s), k_cut2 — after which the cut window and the next one run as single
+// passes (`pass`), cut again while the next window does not fit either (the setup burst at t = 0: one
+// host step, not a paused graph replay per cut).  `snap`: pinned run-control snapshot of `C`.
+static int host_step(nsgpu_p2p *h, const Ctl &c, hipStream_t s);
+template <class X, class P>
+static int host_step_dist(const Ctl &c, hipStream_t s, X cut, P pass, const Ctl *C, Ctl *snap,
+                          nsgpu_p2p *h) {
+  if (c.mode != MODE_CUT) return host_step(h, c, s);
+  for (;;) {
+    int rc = cut();
+    if (!rc) rc = pass();  // the cut window
+    if (!rc) rc = pass();  // the next one (MODE_CUT again if it does not fit)
+    if (rc) return rc;
+    NSGPU_HIP(hipMemcpyAsync(snap, C, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+    if (snap->mode != MODE_CUT || snap->done >= 2) return NSGPU_OK;
+  }
 }
 
 static int build_graph(nsgpu_p2p *h) {
@@ -2548,7 +2115,55 @@ static int drive(nsgpu_p2p *h, bool *paused) {
           *paused = true;
           break;
         }
-        const int rc = host_step(h, h->snap[cur]);
+        const int rc = host_step(h, h->snap[cur], h->s);
+        if (rc) return rc;
+        have_prev = false;
+        continue;
+      }
+    }
+    have_prev = true;
+    cur ^= 1;
+  }
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  return NSGPU_OK;
+}
+
+// Replays the partitioned window pipeline until the run is over, as drive(): two replays in flight;
+// a pause (a cut, a compaction: every rank pauses in the same window) runs its host step once the
+// replay queued behind it has drained.
+static int drive_dist(nsgpu_p2p *h) {
+  int cur = 0;
+  bool have_prev = false;
+  auto cut = [h]() -> int {
+    hipLaunchKernelGGL(k_refit2, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->M);
+    NCCL_TRY(ncclAllGather(h->M.xk_send, h->M.xk_recv, 16, ncclUint8, h->comm->comm, h->s));
+    hipLaunchKernelGGL(k_cut2, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->M);
+    NSGPU_HIP(hipGetLastError());
+    return NSGPU_OK;
+  };
+  auto pass = [h]() -> int {
+    const int rc = launch_windows_dist(h, h->s, 1);
+    if (rc) return rc;
+    NSGPU_HIP(hipGetLastError());
+    return NSGPU_OK;
+  };
+  for (;;) {
+    if (h->eager) {
+      const int rc = launch_windows_dist(h, h->s);
+      if (rc) return rc;
+      NSGPU_HIP(hipGetLastError());
+    } else {
+      NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
+    }
+    NSGPU_HIP(hipMemcpyAsync(&h->snap[cur], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+    NSGPU_HIP(hipEventRecord(h->ev[cur], h->s));
+    if (have_prev) {
+      NSGPU_HIP(hipEventSynchronize(h->ev[cur ^ 1]));
+      const Ctl &c = h->snap[cur ^ 1];
+      if (c.done >= 2) break;  // 2: the final window is appended
+      if (c.mode >= MODE_SORT) {
+        NSGPU_HIP(hipEventSynchronize(h->ev[cur]));
+        const int rc = host_step_dist(h->snap[cur], h->s, cut, pass, h->M.C, &h->snap[cur ^ 1], h);
         if (rc) return rc;
         have_prev = false;
         continue;
@@ -2655,22 +2270,8 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipEventRecord(h->t0, h->s));
   h->done_host[0] = h->done_host[1] = 0;
   if (h->M.dist) {
-    // two replays in flight: replay i+1 is queued before the done flag of replay i is examined
-    for (uint64_t it = 0;; it++) {
-      if (h->eager) {
-        const int rc = launch_windows_dist(h, h->s);
-        if (rc) return rc;
-        NSGPU_HIP(hipGetLastError());
-      } else {
-        NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
-      }
-      NSGPU_HIP(hipMemcpyAsync(&h->done_host[it & 1], &h->M.C->done, sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
-      NSGPU_HIP(hipEventRecord(h->ev[it & 1], h->s));
-      if (it > 0) {
-        NSGPU_HIP(hipEventSynchronize(h->ev[(it - 1) & 1]));
-        if (h->done_host[(it - 1) & 1] >= 2) break;  // 2: the final window is appended
-      }
-    }
+    const int rc = drive_dist(h);
+    if (rc) return rc;
   } else {
     bool paused = false;
     const int rc = drive(h, &paused);
@@ -2818,7 +2419,7 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
       break;
     }
     if (h->snap[0].done >= 2) break;  // the final window is appended
-    if (h->snap[0].mode >= MODE_SORT) rc = host_step(h, h->snap[0]);
+    if (h->snap[0].mode >= MODE_SORT) rc = host_step(h, h->snap[0], h->s);
   }
   if (rc == NSGPU_OK) {
     for (int i = 0; i < ns; i++)
@@ -2890,24 +2491,23 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
 // ====================================================================================================
 struct nsgpu_p2p_group {
   std::vector<nsgpu_p2p *> m;
-  CopyDesc *d_x[3] = {nullptr, nullptr, nullptr};  // X0, X1, X2: n x n copies each
+  CopyDesc *d_x[4] = {nullptr, nullptr, nullptr, nullptr};  // X0, X1, X2, the cut's keys: n x n copies each
   hipStream_t s = nullptr;
   hipGraphExec_t gexec = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
   uint32_t *done_host = nullptr;
+  Ctl *snap = nullptr;  // pinned, 2 run-control snapshots of member 0 (the pauses are run-global)
 };
 
-static void launch_windows_group(nsgpu_p2p_group *g, hipStream_t s) {
+static void launch_windows_group(nsgpu_p2p_group *g, hipStream_t s, int nwin = NWIN) {
   const unsigned n = (unsigned)g->m.size();
-  for (int w = 0; w < NWIN; w++) {
-    for (auto *h : g->m) hipLaunchKernelGGL(k_pa<true>, dim3(GRID_POOL), dim3(TB), 0, s, h->M);
-    for (auto *h : g->m) hipLaunchKernelGGL(k_refit_d, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
+  for (int w = 0; w < nwin; w++) {
+    for (auto *h : g->m) hipLaunchKernelGGL(k2_pa<true>, dim3(GRID_POOL), dim3(TB), 0, s, h->M);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[0]);
-    for (auto *h : g->m) hipLaunchKernelGGL(k_cut, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
-    for (auto *h : g->m) hipLaunchKernelGGL(k_handle_rank<true>, dim3(NHB), dim3(HB), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL(k2_handle, dim3(K2_GRID), dim3(HB), 0, s, h->M);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[1]);
     for (auto *h : g->m) hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, h->M);
-    for (auto *h : g->m) hipLaunchKernelGGL(k_dfin, dim3(NHB), dim3(HB), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_dfin2, dim3(NHB), dim3(HB), 0, s, h->M);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[2]);
   }
 }
@@ -2919,6 +2519,7 @@ extern "C" int nsgpu_p2p_group_destroy(nsgpu_p2p_group *g) {
   for (hipEvent_t e : {g->ev[0], g->ev[1]})
     if (e) (void)hipEventDestroy(e);
   if (g->done_host) (void)hipHostFree(g->done_host);
+  if (g->snap) (void)hipHostFree(g->snap);
   for (CopyDesc *d : g->d_x)
     if (d) (void)hipFree(d);
   if (g->s) (void)hipStreamDestroy(g->s);
@@ -2936,15 +2537,16 @@ extern "C" int nsgpu_p2p_group_create(nsgpu_p2p **members, int n, nsgpu_p2p_grou
   }
   nsgpu_p2p_group *g = new nsgpu_p2p_group();
   g->m.assign(members, members + n);
-  std::vector<CopyDesc> x[3];
+  std::vector<CopyDesc> x[4];
   for (int r = 0; r < n; r++)
     for (int q = 0; q < n; q++) {
       const P2PDev &R = members[r]->M, &Q = members[q]->M;
       x[0].push_back(CopyDesc{(const uint8_t *)Q.x0_send, (uint8_t *)(R.x0_recv + 2 * q), X0B});
       x[1].push_back(CopyDesc{Q.x1_send, R.x1_recv + (size_t)q * X1B, X1B});
       x[2].push_back(CopyDesc{Q.x2_send + (size_t)r * Q.x2b, R.x2_recv + (size_t)q * R.x2b, Q.x2b});
+      x[3].push_back(CopyDesc{(const uint8_t *)Q.xk_send, (uint8_t *)(R.xk_recv + 2 * q), 16});
     }
-  for (int k = 0; k < 3; k++) {
+  for (int k = 0; k < 4; k++) {
     if (hipMalloc(&g->d_x[k], x[k].size() * sizeof(CopyDesc)) != hipSuccess ||
         hipMemcpy(g->d_x[k], x[k].data(), x[k].size() * sizeof(CopyDesc), hipMemcpyHostToDevice) != hipSuccess) {
       nsgpu_p2p_group_destroy(g);
@@ -2954,7 +2556,8 @@ extern "C" int nsgpu_p2p_group_create(nsgpu_p2p **members, int n, nsgpu_p2p_grou
   if (hipStreamCreateWithFlags(&g->s, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&g->ev[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&g->ev[1], hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void **)&g->done_host, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void **)&g->done_host, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&g->snap, 2 * sizeof(Ctl), hipHostMallocDefault) != hipSuccess) {
     nsgpu_p2p_group_destroy(g);
     return set_error(NSGPU_EHIP, "nsgpu_p2p_group_create: stream / events");
   }
@@ -2966,6 +2569,35 @@ extern "C" int nsgpu_p2p_group_reset(nsgpu_p2p_group *g, void *stream) {
   if (!g) return set_error(NSGPU_EINVAL, "nsgpu_p2p_group_reset: null");
   for (nsgpu_p2p *h : g->m) {
     const int rc = nsgpu_p2p_reset(h, stream);
+    if (rc) return rc;
+  }
+  return NSGPU_OK;
+}
+
+// The host-driven steps of a group (host_step_dist's, every member): the cut's keys go through k_copies.
+static int group_host_step(nsgpu_p2p_group *g, const Ctl &c0) {
+  hipStream_t s = g->s;
+  if (c0.mode == MODE_CUT) {
+    auto cut = [g, s]() -> int {
+      for (auto *h : g->m) hipLaunchKernelGGL(k_refit2, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
+      const unsigned n = (unsigned)g->m.size();
+      hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[3]);
+      for (auto *h : g->m) hipLaunchKernelGGL(k_cut2, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
+      NSGPU_HIP(hipGetLastError());
+      return NSGPU_OK;
+    };
+    auto pass = [g, s]() -> int {
+      launch_windows_group(g, s, 1);
+      NSGPU_HIP(hipGetLastError());
+      return NSGPU_OK;
+    };
+    return host_step_dist(c0, s, cut, pass, g->m[0]->M.C, &g->snap[0], g->m[0]);
+  }
+  for (auto *h : g->m) {
+    Ctl c;
+    NSGPU_HIP(hipMemcpyAsync(&c, h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+    const int rc = host_step(h, c, s);
     if (rc) return rc;
   }
   return NSGPU_OK;
@@ -2990,16 +2622,28 @@ extern "C" int nsgpu_p2p_group_run(nsgpu_p2p_group *g, void *stream) {
   hipStream_t cs = (hipStream_t)stream;
   NSGPU_HIP(hipEventRecord(g->ev[0], cs));
   NSGPU_HIP(hipStreamWaitEvent(g->s, g->ev[0], 0));
-  g->done_host[0] = g->done_host[1] = 0;
-  const uint32_t *done = &g->m[0]->M.C->done;  // (run-global: the same on every partition)
-  for (uint64_t it = 0;; it++) {
+  // as drive_dist: member 0's run control decides (done and the pauses are run-global)
+  const Ctl *C0 = g->m[0]->M.C;
+  int cur = 0;
+  bool have_prev = false;
+  for (;;) {
     NSGPU_HIP(hipGraphLaunch(g->gexec, g->s));
-    NSGPU_HIP(hipMemcpyAsync(&g->done_host[it & 1], done, sizeof(uint32_t), hipMemcpyDeviceToHost, g->s));
-    NSGPU_HIP(hipEventRecord(g->ev[it & 1], g->s));
-    if (it > 0) {
-      NSGPU_HIP(hipEventSynchronize(g->ev[(it - 1) & 1]));
-      if (g->done_host[(it - 1) & 1] >= 2) break;
+    NSGPU_HIP(hipMemcpyAsync(&g->snap[cur], C0, sizeof(Ctl), hipMemcpyDeviceToHost, g->s));
+    NSGPU_HIP(hipEventRecord(g->ev[cur], g->s));
+    if (have_prev) {
+      NSGPU_HIP(hipEventSynchronize(g->ev[cur ^ 1]));
+      const Ctl &c = g->snap[cur ^ 1];
+      if (c.done >= 2) break;
+      if (c.mode >= MODE_SORT) {
+        NSGPU_HIP(hipEventSynchronize(g->ev[cur]));
+        const int rc = group_host_step(g, g->snap[cur]);
+        if (rc) return rc;
+        have_prev = false;
+        continue;
+      }
     }
+    have_prev = true;
+    cur ^= 1;
   }
   NSGPU_HIP(hipEventRecord(g->ev[0], g->s));
   NSGPU_HIP(hipEventSynchronize(g->ev[0]));

@@ -23,7 +23,7 @@
 // run inline, which keeps its (ts, uid) position.  When the pool holds many tombstones the host
 // compacts it (k_cmp).
 
-enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3, MODE_HOST = 4 };
+enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3, MODE_HOST = 4, MODE_CUT = 5 };
 constexpr uint64_t TOMB = ~0ull;        // ev_ts of a free pool slot
 constexpr uint32_t NOSRC = 0xffffffffu;
 constexpr int NHUB = 32;                // hub blocks of k2_handle
@@ -43,6 +43,37 @@ struct HubEv {
 };
 
 constexpr int HUBL = 1024;  // events of a hub a block sorts in LDS (more: the window is dispatched as a run)
+
+// A handled window slot's child counts.  A partitioned rank also fills the slot's X1 entry (key, counts)
+// and accumulates its summary's totals per thread (x1_totals folds them).
+struct X1Acc {
+  uint32_t tc, ti;
+  uint64_t lk;
+};
+__device__ __forceinline__ void slot_done(const P2PDev &M, uint32_t s, uint64_t key, uint32_t n, uint32_t ni,
+                                          X1Acc &xa) {
+  M.nchild[s] = n;
+  M.ninl[s] = ni;
+  if (M.dist) {
+    x1ent(M.x1_send, 0)[s] = X1Ent{key, n | (ni << 16), 0};
+    xa.tc += n;
+    xa.ti += ni;
+    xa.lk = key > xa.lk ? key : xa.lk;
+  }
+}
+// All lanes of the wave call it.
+__device__ __forceinline__ void x1_totals(const P2PDev &M, X1Acc xa) {
+  if (!M.dist) return;
+  xa.tc = wave_sum32(xa.tc);
+  xa.ti = wave_sum32(xa.ti);
+  xa.lk = wave_max64(xa.lk);
+  if ((threadIdx.x & 63) == 0) {
+    X1Hdr *h = x1hdr(M.x1_send, 0);
+    if (xa.tc) atomicAdd(&h->tc, xa.tc);
+    if (xa.ti) atomicAdd(&h->tinl, xa.ti);
+    if (xa.lk) atomicMax((unsigned long long *)&h->lastkey, (unsigned long long)xa.lk);
+  }
+}
 
 // Wave-aggregated counter allocation: one index per lane with `want` (active lanes only).
 __device__ __forceinline__ uint32_t wave_alloc32(uint32_t *ctr, bool want) {
@@ -107,7 +138,10 @@ __device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t
       const uint32_t hh = atomicAdd(&C.nhub, 1u);
       if (hh < (uint32_t)MAXHUB) M.hub_list[hh] = ctx;
     }
-    if (idx == (uint32_t)HUBL) C.force_run = 1;
+    if (idx == (uint32_t)HUBL) {  // too many for a hub block: a sorted run; partitioned: a cut (k_refit2)
+      if (M.dist) C.overflow = 1;
+      else C.force_run = 1;
+    }
   }
   M.widx[slot] = idx;
 }
@@ -197,6 +231,11 @@ __device__ __forceinline__ void block_alloc2(Ctl &C, uint32_t nw, uint32_t nf, u
 }
 
 // ---- k2_pa ----
+// DIST: a partitioned rank's variant: children on other ranks' nodes are skipped (they travel through
+// X2), the remote events the last X2 brought are classified like children (a role of whole blocks
+// after the slot blocks), the rank's reduction goes to its X1 summary, and a window the host cut
+// (k_cut2: C.prep) is already formed.
+template <bool DIST>
 __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   PH_BEGIN();
   BLK_T0();
@@ -206,6 +245,8 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 #endif
   const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
   const bool slot_role = g < (uint64_t)WCAP;  // (roles are block-uniform)
+  const uint32_t rrb = DIST ? (M.nranks * M.capx + TB - 1) / TB : 0u;  // remote-event blocks
+  const bool remote_role = DIST && !slot_role && blockIdx.x < (uint32_t)(WCAP / TB) + rrb;
   // Everything this kernel reads of the run control and of the last window's slot, loaded at once:
   // these lines were written by k2_scan on another XCD, so every dependent level is a trip to memory.
   // (The slot arrays are WCAP long: a slot past the last window's size is loaded and ignored.)
@@ -229,11 +270,15 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       if ((uint32_t)j < M.maxc) ce[j] = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
     }
   }
+  if (DIST) {
+    if (blockIdx.x == 0 && threadIdx.x < M.nranks) x2hdr(M, M.x2_send, threadIdx.x)->n = 0;  // (X2 has sent them)
+    if (C.prep) return;
+  }
   if (c_done >= 2 || c_mode >= MODE_SORT) return;
   if (slot_role) BLK_MARK(32, c_win);  // snapshot + slot loads issued (waits at first use)
   const bool run = c_mode == MODE_RUN;
   const bool partition = c_done == 0;
-  Red &R = C.red[rt];
+  Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[rt];
   WinBound b = window_bound(rt ? red0 : red1);
   // a pending host closure (nsgpu_p2p_advance) cuts the window at its key, like Simulator::Stop: the
   // window holds the device events before it, and the pipeline pauses for the host after the window
@@ -314,8 +359,8 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
               }
               ii++;
             }
-          } else {
-            valid = partition;
+          } else {  // (partitioned: a child on another rank's node goes there through X2)
+            valid = partition && (!DIST || M.owner[e.ctx] == M.rank);
           }
         }
         k2_classify(M, b, run, valid, e, NOSRC, R, tmn, wnd, gin[q], gpk[q]);
@@ -336,13 +381,28 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       }
       BLK_MARK(40, c_win);  // writes (node-table atomics)
     }
+  } else if (DIST && remote_role) {
+    // ---- remote events the last X2 brought (partitioned): record idx % capx from rank idx / capx
+    if (partition) {
+      const uint64_t idx = g - WCAP;
+      const uint32_t q = (uint32_t)(idx / M.capx), rec = (uint32_t)(idx % M.capx);
+      const bool valid = q < M.nranks && rec < x2hdr(M, M.x2_recv, q)->n;
+      Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+      if (valid) e = x2rec(M, M.x2_recv, q)[rec];
+      bool gin, gpk;
+      k2_classify(M, b, false, valid, e, NOSRC, R, tmn, wnd, gin, gpk);
+      uint32_t w0;
+      uint64_t f0;
+      block_alloc2<TB>(C, gin, gpk, w0, f0);
+      k2_write(M, C, b, e, NOSRC, gin, gpk, w0, f0);
+    }
   } else if (partition && !run) {
     // ---- the pool, in place: read (ts, uid, kind) of every slot; window events are copied out.
     // Chunks of PPT x TB entries per block (loads of a chunk all in flight), one allocation per chunk;
     // blocks past the pool's end do nothing (no atomics).
     constexpr int PPT = 4;
     const uint64_t P = c_P;
-    const uint64_t pb = blockIdx.x - (uint64_t)(WCAP / TB), npb = gridDim.x - (uint64_t)(WCAP / TB);
+    const uint64_t pb = blockIdx.x - (uint64_t)(WCAP / TB + rrb), npb = gridDim.x - (uint64_t)(WCAP / TB + rrb);
     for (uint64_t c0 = pb * TB * PPT; c0 < P; c0 += npb * TB * PPT) {  // block-uniform trip count
       Ev ge[PPT];
       bool gin[PPT], gpk[PPT];
@@ -440,11 +500,9 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
     sp.a = M.wa[base + i0];
     sp.key = M.wkey[base + i0];
   }
+  X1Acc xa{0, 0, 0};
   const uint32_t wi = i0 < W ? sp.widx : 1u;
-  if (wi == NOHOLD) {  // NetDevice::Start: dispatched, no children
-    M.nchild[i0] = 0;
-    M.ninl[i0] = 0;
-  }
+  if (wi == NOHOLD) slot_done(M, i0, sp.key, 0, 0, xa);  // NetDevice::Start: dispatched, no children
   if (wi == 0) {  // the holder
     const uint32_t c = lp_of(M, sp.ctx, sp.kind, sp.a);
     uint32_t n = 1;
@@ -533,8 +591,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
         uint32_t ni = 0;
         if (rel < inline_lim)
           for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
-        M.nchild[s] = E.n;
-        M.ninl[s] = ni;
+        slot_done(M, s, mk[it], E.n, ni, xa);
         pending += ni;
       }
       tmn = E.tmn;
@@ -542,6 +599,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
     }
   }
   publish_min<HB>(R, tmn, wnd);
+  x1_totals(M, xa);
   if (hs.stop) C.stop_seen = 1;
   if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
   if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
@@ -698,7 +756,8 @@ constexpr int32_t CBIG = 1 << 28;
 // Returns false (nothing done) when the batch would reuse a ring slot (more enqueues than the ring
 // holds beyond the queued packets): the serial pass runs instead.
 __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d, const uint32_t *gs,
-                                const uint64_t *gk, uint32_t n, uint32_t j0s, uint32_t j1s, uint64_t tmin, HStat &hs) {
+                                const uint64_t *gk, uint32_t n, uint32_t j0s, uint32_t j1s, uint64_t tmin, HStat &hs,
+                                X1Acc &xa) {
   const int lane = threadIdx.x;
   const DevRec dr = M.dev[d];
   const int32_t qmax = (int32_t)dr.qmax;
@@ -820,8 +879,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
       }
       if (h.xdrop) trace_te_drop(M, E, h.xdrop - 1, h.p);
       if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
-      M.nchild[s] = E.n;
-      M.ninl[s] = 0;
+      slot_done(M, s, key, E.n, 0, xa);
     }
   }
   q0 = wave_sum32(q0), q1 = wave_sum32(q1), q2 = wave_sum32(q2), q3 = wave_sum32(q3), q4 = wave_sum32(q4),
@@ -996,7 +1054,8 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   }
   bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && M.dev[dmin].qmax >= 1 &&
               !(M.dev[dmin].busy == 0 && M.dev[dmin].cnt != 0);
-  if (fast) fast = hub_device_scan(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs);
+  X1Acc xa{0, 0, 0};
+  if (fast) fast = hub_device_scan(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs, xa);
   if (!fast) {
     DevCache D;
     D.d = NOSRC;
@@ -1054,8 +1113,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           if (h.xdrop) trace_te_drop(M, E, h.xdrop - 1, h.p);
           if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
           const uint32_t ni = rel < inline_lim ? h.pad : 0u;
-          M.nchild[s] = E.n;
-          M.ninl[s] = ni;
+          slot_done(M, s, key, E.n, ni, xa);
           pending += ni;
         }
       }
@@ -1064,6 +1122,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     if (lane == 0) D.flush(M);
   }
   publish_min<HB>(R, E.tmn, E.wnd);
+  x1_totals(M, xa);
   const uint64_t nr = wave_sum64(hs.no_route), td = wave_sum64(hs.ttl_drops), cn = wave_sum64(hs.cancelled),
                  ur = wave_sum64(hs.unreach), ic = wave_sum64(hs.icmp);
   const bool stop = __ballot(hs.stop) != 0;
@@ -1134,19 +1193,45 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
     const uint32_t i0 = bx * HB + threadIdx.x;
     sp = SlotPre{M.widx[i0], M.wctx[i0], M.wkind[i0], M.wa[i0], M.wkey[i0]};
   }
-  if (c_done || c_mode >= MODE_SORT) {
-    if (c_done == 1 && blockIdx.x == 0 && threadIdx.x == 0) C.done = 2;  // the final window is appended
+  // partitioned: every rank's X0 payload (window candidates, hub flag): a window some rank cannot hold
+  // is cut by the host (k_refit2 / k_cut2) before anything of it runs, on every rank
+  bool ovf = false;
+  if (M.dist)
+    for (uint32_t q = 0; q < M.nranks; q++) {
+      const uint4 x = reinterpret_cast<const uint4 *>(M.x0_recv)[q];
+      ovf |= x.x > (uint32_t)WCAP || x.z != 0;
+    }
+  if (c_done || c_mode >= MODE_SORT || ovf) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (c_done == 1) C.done = 2;  // the final window is appended
+      if (M.dist) {
+        C.hdl = 0;  // (k_gtile / k_dfin2: nothing ran)
+        if (!c_done && c_mode < MODE_SORT) C.mode = MODE_CUT;
+      }
+    }
     return;
+  }
+  if (M.dist && bx == 0 && threadIdx.x == 0) {  // the window k_dfin2 finishes and the next k2_pa appends
+    C.hdl = 1;
+    C.pK0 = C.K;
+    C.puid0 = C.uid;
+    C.ptmin = hc.tmin;
+    C.pinline_lim = hc.inline_lim;
+    C.pW = W;
+    C.pvalid = 1;
+    X1Hdr *h = x1hdr(M.x1_send, 0);
+    h->W = W;
+    h->needc = c_Pe > 65536 && C.live * 4 < c_Pe;  // this rank's pool wants a compaction
   }
   const bool run = c_mode == MODE_RUN;
   const uint32_t base = run ? c_wbase : 0;
   const bool handle = run || (W <= (uint32_t)WCAP && !c_fr);
-  Red &R = C.red[rt];
+  Red &R = M.dist ? x1hdr(M.x1_send, 0)->red : C.red[rt];
   PH_MARK(8);
   if (bx < (uint32_t)NHB) {
     if (handle) handle_node2(M, C, bx * HB + threadIdx.x, W, base, R, lds, hc, sp);
   } else if (bx < (uint32_t)(NHB + NRB)) {
-    if (!run && handle) rank_tile(M, C, bx - NHB);
+    if (!run && handle && !M.dist) rank_tile(M, C, bx - NHB);  // (partitioned: k_gtile ranks globally)
   } else if (bx < (uint32_t)(NHB + NRB + NHUB)) {
     if (handle) {
       const uint32_t hb = bx - (NHB + NRB);
