@@ -145,6 +145,17 @@ int nsgpu_wifi_read_tx_base(nsgpu_wifi *h, uint32_t *out);               /* n_tx
 int nsgpu_wifi_read_ends(nsgpu_wifi *h, nsgpu_wifi_end_record *out, uint64_t cap, uint64_t *n);  /* unordered */
 int nsgpu_wifi_read_rx_log(nsgpu_wifi *h, nsgpu_wifi_rx_log *out);        /* n_tx * n_phy */
 int nsgpu_wifi_destroy(nsgpu_wifi *h);
+/* Where a phy's InterferenceHelper::m_niChanges list lives (results are identical; the reference list's
+ * order, length and ni_cap are kept either way):
+ *   NSGPU_WIFI_STORE_LDS  two time-sorted queues per phy (start entries, end entries) in LDS, sized at
+ *                         create from the schedule (the most transmissions on the air at one instant);
+ *                         a run whose start queue overflows is repeated on the HBM ring by the readers;
+ *   NSGPU_WIFI_STORE_HBM  one sorted ring per phy in HBM (ni_cap entries);
+ *   NSGPU_WIFI_STORE_AUTO LDS when a block holds at least 16 phys' queues (the default).
+ * nsgpu_wifi_get_store reports the store the next run uses, its phys per block and the end-queue (LDS)
+ * or ring (HBM) capacity. */
+int nsgpu_wifi_set_store(nsgpu_wifi *h, int store);
+int nsgpu_wifi_get_store(nsgpu_wifi *h, int *store, uint32_t *phys_per_block, uint32_t *e_cap);
 /* Diagnostics: the kernels of one run and a run with each bracketed by HIP events (ms[k], k < count). */
 int nsgpu_wifi_kernel_count(int *n);
 const char *nsgpu_wifi_kernel_name(int k);

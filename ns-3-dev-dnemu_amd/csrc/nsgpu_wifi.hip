@@ -46,7 +46,8 @@ namespace {
 constexpr uint64_t INF = ~0ull;
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr int PE_CAP = 8;  // pending EndReceive events of one phy: the live one + cancelled ones
-constexpr uint32_t ERR_WINDOW = 1, ERR_NICAP = 2, ERR_TX_IN_TX = 4, ERR_PENDING = 8, ERR_SYNCCAP = 16;
+// (ERR_LDS: a SplitNi queue outgrew its LDS capacity — the run is repeated on the HBM ring store)
+constexpr uint32_t ERR_WINDOW = 1, ERR_NICAP = 2, ERR_TX_IN_TX = 4, ERR_PENDING = 8, ERR_SYNCCAP = 16, ERR_LDS = 32;
 enum Acc { A_DIGEST, A_DISPATCHED, A_RX, A_SYNC, A_DROP_RX, A_DROP_TX, A_DROP_ED, A_CCA_EVAL, A_CCA_SWITCH,
            A_END, A_END_CANCELLED, A_NI_INSERTS, A_NEAR, A_NI_MAX, A_LAST_TS, A_N };
 
@@ -152,20 +153,189 @@ __device__ __forceinline__ void cursor_advance(const NiEnt *ring, uint32_t head,
   }
 }
 
+// ---- InterferenceHelper::m_niChanges stores (the list a phy's Receive events read and update) ----
+// Both keep the reference list's order and its length (len: ni_cap, NiChange counts) and sum in list
+// order; they differ in where the entries live.
+//
+// RingNi: the list as one time-sorted ring per phy in HBM, insertions shifting entries from the back
+// (r02's kernel; the fallback when SplitNi's queues would not fit LDS).
+struct RingNi {
+  NiEnt *ring;
+  uint32_t m, head, len, cur_n;  // cur_n: prefix cursor, entries [0, cur_n) summed into cur_s
+  double cur_s;
+  __device__ __forceinline__ uint32_t length() const { return len; }
+  __device__ __forceinline__ bool room() const { return len + 2 <= m + 1; }
+  __device__ __forceinline__ bool phys_room() const { return true; }
+  __device__ __forceinline__ void on_receive(int64_t) {}
+  // AppendEvent, not receiving (interference-helper.cc:192-212): fold the entries up to upper_bound (now)
+  // into m_firstPower, drop them, the new entry first; returns m_firstPower
+  __device__ __forceinline__ double fold_start(int64_t nw, double p) {
+    cursor_advance<true>(ring, head, len, m, nw, cur_n, cur_s);
+    head = (head + cur_n) & m;
+    len -= cur_n;
+    cur_n = 0;
+    head = (head - 1) & m;
+    ring[head] = NiEnt{nw, p};
+    len++;
+    return cur_s;
+  }
+  __device__ __forceinline__ void insert_start(int64_t nw, double p) { ni_insert(ring, head, len, m, nw, p); }
+  __device__ __forceinline__ void insert_end(int64_t t, double d) { ni_insert(ring, head, len, m, t, d); }
+  // GetEnergyDuration (interference-helper.cc:171-190): the entries before now only add up (the cursor
+  // holds their sum); then noise += delta in list order until it drops below the threshold
+  __device__ __forceinline__ int64_t energy_end(int64_t nw, double ccaW, uint32_t &flags) {
+    cursor_advance<false>(ring, head, len, m, nw, cur_n, cur_s);
+    double noise = cur_s;
+    int64_t end = nw;
+    for (uint32_t q = cur_n; q < len; q += NB) {
+      NiEnt en[NB];
+#pragma unroll
+      for (int u = 0; u < NB; u++) en[u] = ring[(head + q + u) & m];
+      bool stop = false;
+#pragma unroll
+      for (int u = 0; u < NB; u++) {
+        if (q + u >= len) {
+          stop = true;
+          break;
+        }
+        noise += en[u].d;
+        end = en[u].t;  // >= now: the cursor stopped at the first entry not before now
+        if (near_thr(noise, ccaW)) flags |= NSGPU_WIFI_F_NEAR_CCA;
+        if (noise < ccaW) {
+          stop = true;
+          break;
+        }
+      }
+      if (stop) break;
+    }
+    return end;
+  }
+};
+
+// SplitNi: the same list as two time-sorted queues in LDS — S, the start entries (+P at a Receive), and
+// E, the end entries (-P at Receive + duration) — whose merge by time is the list: an end at t was
+// inserted at t - duration < t, so before every start at t (upper_bound puts later insertions after
+// equal times), and within S and within E insertion order is list order.  The cursor is eager: every
+// Receive first sums the entries before now into cur_s and drops them from the queues (no insertion
+// lands before the cursor, and the sums run in list order, so the values are the ring's).  Then
+//   a start insertion is an append to S (every start is at or before now), not a shift over the ~100
+//     pending ends a busy channel holds;
+//   the live entries are only those at or after now: E holds at most the transmissions whose
+//     [ts, ts + max delay + duration] interval covers one instant (host bound -> its LDS capacity), S the
+//     starts at exactly now;
+//   GetEnergyDuration walks E's entries at now, then S, then the rest of E, from LDS.
+// `ndead` counts the summed entries the reference list still holds (until the next fold), so length()
+// is the reference's list length.
+struct SplitNi {
+  int64_t *st, *et;  // entry i of this phy's S / E at [i * stride] (interleaved over the block's lanes)
+  double *sd, *ed;
+  uint32_t stride, scap, ecap, cap;  // queue capacities; cap = ni_cap (the reference list's limit)
+  uint32_t hs, ns, he, ne, ndead;
+  double cur_s;
+  __device__ __forceinline__ uint32_t sx(uint32_t i) const {
+    const uint32_t x = hs + i;
+    return (x < scap ? x : x - scap) * stride;
+  }
+  __device__ __forceinline__ uint32_t ex(uint32_t i) const {
+    const uint32_t x = he + i;
+    return (x < ecap ? x : x - ecap) * stride;
+  }
+  __device__ __forceinline__ uint32_t length() const { return ndead + ns + ne; }
+  __device__ __forceinline__ bool room() const { return length() + 2 <= cap; }
+  __device__ __forceinline__ bool phys_room() const { return ns + 1 <= scap && ne + 1 <= ecap; }
+  // sums the merged entries with t < lim (LE: t <= lim) into cur_s and drops them
+  template <bool LE>
+  __device__ __forceinline__ void advance(int64_t lim) {
+    for (;;) {
+      const int64_t te = ne ? et[ex(0)] : INT64_MAX, ts = ns ? st[sx(0)] : INT64_MAX;
+      const bool e = te <= ts;  // E first on equal times
+      const int64_t t = e ? te : ts;
+      if (t == INT64_MAX || (LE ? t > lim : t >= lim)) return;
+      if (e) {
+        cur_s += ed[ex(0)];
+        he = he + 1 == ecap ? 0 : he + 1;
+        ne--;
+      } else {
+        cur_s += sd[sx(0)];
+        hs = hs + 1 == scap ? 0 : hs + 1;
+        ns--;
+      }
+      ndead++;
+    }
+  }
+  __device__ __forceinline__ void on_receive(int64_t nw) { advance<false>(nw); }
+  __device__ __forceinline__ double fold_start(int64_t nw, double p) {
+    advance<true>(nw);  // (S is empty after it: every start is at or before now)
+    ndead = 0;
+    st[sx(0)] = nw;
+    sd[sx(0)] = p;
+    ns = 1;
+    return cur_s;
+  }
+  __device__ __forceinline__ void insert_start(int64_t nw, double p) {
+    st[sx(ns)] = nw;
+    sd[sx(ns)] = p;
+    ns++;
+  }
+  __device__ __forceinline__ void insert_end(int64_t t, double d) {  // upper_bound (t) from the back
+    uint32_t q = ne;
+    while (q > 0) {
+      const int64_t x = et[ex(q - 1)];
+      if (x <= t) break;
+      et[ex(q)] = x;
+      ed[ex(q)] = ed[ex(q - 1)];
+      q--;
+    }
+    et[ex(q)] = t;
+    ed[ex(q)] = d;
+    ne++;
+  }
+  __device__ __forceinline__ int64_t energy_end(int64_t nw, double ccaW, uint32_t &flags) {
+    // (on_receive advanced the cursor to now: S holds starts at now only, E ends at or after now)
+    double noise = cur_s;
+    int64_t end = nw;
+    bool stop = false;
+    auto step = [&](int64_t t, double d) {
+      noise += d;
+      end = t;
+      if (near_thr(noise, ccaW)) flags |= NSGPU_WIFI_F_NEAR_CCA;
+      stop = noise < ccaW;
+    };
+    uint32_t ie = 0;
+    while (!stop && ie < ne && et[ex(ie)] == nw) {
+      step(nw, ed[ex(ie)]);
+      ie++;
+    }
+    for (uint32_t q = 0; !stop && q < ns; q++) step(st[sx(q)], sd[sx(q)]);
+    while (!stop && ie < ne) {
+      int64_t bt[NB];
+      double bd[NB];
+#pragma unroll
+      for (int u = 0; u < NB; u++) {
+        const uint32_t i = ie + u < ne ? ie + u : ie;
+        bt[u] = et[ex(i)];
+        bd[u] = ed[ex(i)];
+      }
+#pragma unroll
+      for (int u = 0; u < NB; u++) {
+        if (stop || ie >= ne) break;
+        step(bt[u], bd[u]);
+        ie++;
+      }
+    }
+    return end;
+  }
+};
+
 // One lane = one phy: its SendPacket / Receive / EndReceive sequence in (ts, uid) order.
-__global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
-  const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (j >= D.nphy) return;
+template <class Ni>
+__device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &ni) {
   const double px = D.x[j], py = D.y[j], pz = D.z[j];
   const uint32_t ch = D.chan[j];
-  const uint32_t m = D.ni_mask;
-  NiEnt *ring = D.ni + (uint64_t)j * (m + 1);
-  // InterferenceHelper (m_niChanges as a ring [head, head + len), m_firstPower) and WifiPhyStateHelper;
-  // the two m_rxing flags are set and cleared together (yans-wifi-phy.cc:466-468, :510-514, :776-797)
-  uint32_t head = 0, len = 0, ni_max = 0;
+  // InterferenceHelper (m_niChanges: `ni`, m_firstPower) and WifiPhyStateHelper; the two m_rxing flags
+  // are set and cleared together (yans-wifi-phy.cc:466-468, :510-514, :776-797)
+  uint32_t ni_max = 0;
   double firstPower = 0.0;
-  uint32_t cur_n = 0;      // prefix cursor: entries [0, cur_n) summed into cur_s
-  double cur_s = 0.0;
   bool rxing = false;
   int64_t endTx = 0, endRx = 0, endCca = 0;
   // pending EndReceive events
@@ -289,25 +459,20 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
     const double rxPowerW = pow(10.0, rxPowerDbm / 10.0) / 1000.0;  // DbmToW (:727-732)
     const int64_t endNew = nw + c_dur;
     // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
-    if (len + 2 > m + 1) {
+    ni.on_receive(nw);
+    if (!ni.room()) {
       err |= ERR_NICAP;
       break;
     }
-    if (!rxing) {  // fold the entries up to upper_bound (now) into m_firstPower, drop them
-      cursor_advance<true>(ring, head, len, m, nw, cur_n, cur_s);
-      head = (head + cur_n) & m;
-      len -= cur_n;
-      firstPower = cur_s;
-      cur_n = 0;
-      head = (head - 1) & m;
-      ring[head] = NiEnt{nw, rxPowerW};
-      len++;
-    } else {
-      ni_insert(ring, head, len, m, nw, rxPowerW);
+    if (!ni.phys_room()) {
+      err |= ERR_LDS;
+      break;
     }
-    ni_insert(ring, head, len, m, endNew, -rxPowerW);
+    if (!rxing) firstPower = ni.fold_start(nw, rxPowerW);  // fold up to upper_bound (now) into m_firstPower
+    else ni.insert_start(nw, rxPowerW);
+    ni.insert_end(endNew, -rxPowerW);
     ni_ins += 2;
-    ni_max = len > ni_max ? len : ni_max;
+    ni_max = ni.length() > ni_max ? ni.length() : ni_max;
     // the state switch (WifiPhyStateHelper::GetState, wifi-phy-state-helper.cc:159-183)
     const int st = endTx > nw ? 2 : rxing ? 1 : endCca > nw ? 3 : 0;
     uint32_t outcome, flags = 0;
@@ -343,31 +508,7 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
     int64_t cca = 0;
     if (maybe) {  // maybeCcaBusy (:482-495): InterferenceHelper::GetEnergyDuration (interference-helper.cc:171-190)
       flags |= NSGPU_WIFI_F_CCA_EVAL;
-      // the entries before now only add up (`continue`): the cursor holds their sum
-      cursor_advance<false>(ring, head, len, m, nw, cur_n, cur_s);
-      double noise = cur_s;
-      int64_t end = nw;
-      for (uint32_t q = cur_n; q < len; q += NB) {
-        NiEnt en[NB];
-#pragma unroll
-        for (int u = 0; u < NB; u++) en[u] = ring[(head + q + u) & m];
-        bool stop = false;
-#pragma unroll
-        for (int u = 0; u < NB; u++) {
-          if (q + u >= len) {
-            stop = true;
-            break;
-          }
-          noise += en[u].d;
-          end = en[u].t;  // >= now: the cursor stopped at the first entry not before now
-          if (near_thr(noise, D.ccaW)) flags |= NSGPU_WIFI_F_NEAR_CCA;
-          if (noise < D.ccaW) {
-            stop = true;
-            break;
-          }
-        }
-        if (stop) break;
-      }
+      const int64_t end = ni.energy_end(nw, D.ccaW, flags);
       cca = end > nw ? end - nw : 0;
       if (cca != 0) {  // SwitchMaybeToCcaBusy (wifi-phy-state-helper.cc:404-423)
         flags |= NSGPU_WIFI_F_CCA_SWITCH;
@@ -407,7 +548,7 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
     r.pad_ = 0;
     D.sync[pe_slot[q]] = r;
   }
-  c.ni_len = len;
+  c.ni_len = ni.length();
   c.ni_max = ni_max;
   c.end_tx = endTx;
   c.end_rx = endRx;
@@ -431,6 +572,29 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
   atomicAdd(&D.acc[A_NEAR], (unsigned long long)near);
   atomicMax(&D.acc[A_NI_MAX], (unsigned long long)ni_max);
   atomicMax(&D.acc[A_LAST_TS], (unsigned long long)last_ts);
+}
+
+// HBM ring store: 64 phys per block.
+__global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
+  const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (j >= D.nphy) return;
+  RingNi ni{D.ni + (uint64_t)j * (D.ni_mask + 1), D.ni_mask, 0, 0, 0, 0.0};
+  phy_run(D, j, ni);
+}
+
+// LDS split store: blockDim.x phys per block, each with scap + ecap 16-B entries of the block's dynamic
+// LDS, interleaved over the lanes ([i * blockDim.x + lane]: lanes at equal depths hit distinct banks).
+__global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t scap, uint32_t ecap) {
+  extern __shared__ uint64_t wlds[];
+  const uint32_t P = blockDim.x, l = threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * P + l;
+  if (j >= D.nphy) return;
+  int64_t *et = reinterpret_cast<int64_t *>(wlds);
+  double *ed = reinterpret_cast<double *>(wlds + (size_t)ecap * P);
+  int64_t *st = reinterpret_cast<int64_t *>(wlds + (size_t)2 * ecap * P);
+  double *sd = reinterpret_cast<double *>(wlds + (size_t)(2 * ecap + scap) * P);
+  SplitNi ni{st + l, et + l, sd + l, ed + l, P, scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0};
+  phy_run(D, j, ni);
 }
 
 // Syncs per bucket m = #transmissions with t_T <= ts (binary search over the schedule).
@@ -569,7 +733,15 @@ struct nsgpu_wifi {
   std::vector<void *> allocs;
   hipStream_t last = nullptr;
   bool ran = false;
+  // NiChanges store (nsgpu_wifi_set_store): the LDS split queues when their capacities fit, else the HBM
+  // ring; lds_ok = the plan below exists, use_lds = the next run uses it
+  int store = NSGPU_WIFI_STORE_AUTO;
+  bool lds_ok = false, use_lds = false;
+  uint32_t lds_P = 0, lds_scap = 0, lds_ecap = 0;
+  size_t lds_bytes = 0;
 };
+
+constexpr uint32_t SCAP_LDS = 8;  // S: starts at one instant (more: ERR_LDS, the run repeats on the ring)
 
 extern "C" int nsgpu_wifi_tx_duration_ns(uint32_t size, uint32_t modclass, uint64_t rate_bps, uint32_t bw_hz,
                                          uint32_t preamble, int64_t *ns) {
@@ -666,8 +838,23 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
     if (j == 0 || sc->z[j] > zmax) zmax = sc->z[j];
   }
   uint64_t per_phy = ktx;
+  const double diag = sqrt((xmax - xmin) * (xmax - xmin) + (ymax - ymin) * (ymax - ymin) + (zmax - zmin) * (zmax - zmin));
+  // SplitNi's E queue: a phy's live end entries belong to receptions on the air at its current Receive,
+  // i.e. to transmissions whose [ts, ts + max delay + duration] interval covers that instant: the largest
+  // such overlap over the schedule bounds it (closed intervals; the sweep visits every start)
+  uint32_t overlap = 0;
   if (ktx) {
-    const double diag = sqrt((xmax - xmin) * (xmax - xmin) + (ymax - ymin) * (ymax - ymin) + (zmax - zmin) * (zmax - zmin));
+    const int64_t dmax = (int64_t)ceil(diag / sc->speed * 1e9) + 2;
+    std::vector<int64_t> ends(ktx);
+    for (uint32_t k = 0; k < ktx; k++) ends[k] = (int64_t)sc->tx_ts[k] + dmax + tx_dur[k];
+    std::sort(ends.begin(), ends.end());
+    uint32_t gone = 0;  // intervals that ended before the current start
+    for (uint32_t k = 0; k < ktx; k++) {
+      while (gone < ktx && ends[gone] < (int64_t)sc->tx_ts[k]) gone++;
+      overlap = std::max(overlap, k + 1 - gone);
+    }
+  }
+  if (ktx) {
     const double span = (double)(sc->tx_ts[ktx - 1] - sc->tx_ts[0]) + diag / sc->speed * 1e9 + 2.0;
     per_phy = std::min<uint64_t>(ktx, (uint64_t)(span / (double)std::max<int64_t>(dur_min, 1)) + 2);
   }
@@ -692,6 +879,24 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   D.stop_ts = has_stop ? sc->stop_ts : INF;
   D.ni_mask = cap - 1;
   D.sync_cap = sync_cap;
+  {  // the LDS plan: P phys per block, each with SCAP_LDS + ecap entries of 16 B
+    int dev = 0, lmax = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&lmax, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && lmax > 0) {
+      const uint32_t ecap = std::max<uint32_t>(overlap + 2, 8);
+      const size_t per = (size_t)(ecap + SCAP_LDS) * 16;
+      const size_t P = std::min<size_t>(64, (size_t)lmax / per);
+      if (P >= 1) {
+        h->lds_ok = true;
+        h->lds_P = (uint32_t)P;
+        h->lds_scap = SCAP_LDS;
+        h->lds_ecap = ecap;
+        h->lds_bytes = P * per;
+      }
+      // auto: the split queues when a block still holds 16 phys (below that the ring's 64-lane blocks win)
+      h->use_lds = h->lds_ok && P >= 16;
+    }
+  }
   int rc = NSGPU_OK;
 #define TRY(x)                    \
   do {                            \
@@ -756,7 +961,15 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
   const uint64_t nlog = (uint64_t)D.ktx * (uint64_t)D.nphy;
   if (D.rx_log && nlog) hipLaunchKernelGGL(k_rx_log_init, dim3(1024), dim3(256), 0, s, D.rx_log, nlog);
   if (ev) NSGPU_HIP(hipEventRecord(ev[0], s));
-  hipLaunchKernelGGL(k_wifi_phy, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, s, D);
+  if (h->use_lds) {
+    if (h->lds_bytes > 65536)
+      NSGPU_HIP(hipFuncSetAttribute((const void *)k_wifi_phy_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)h->lds_bytes));
+    hipLaunchKernelGGL(k_wifi_phy_lds, dim3((unsigned)((D.nphy + h->lds_P - 1) / h->lds_P)), dim3(h->lds_P),
+                       h->lds_bytes, s, D, h->lds_scap, h->lds_ecap);
+  } else {
+    hipLaunchKernelGGL(k_wifi_phy, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, s, D);
+  }
   if (ev) NSGPU_HIP(hipEventRecord(ev[1], s));
   hipLaunchKernelGGL(k_sync_hist, dim3(1024), dim3(256), 0, s, D);
   if (ev) NSGPU_HIP(hipEventRecord(ev[2], s));
@@ -770,6 +983,34 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
   NSGPU_HIP(hipGetLastError());
   h->last = s;
   h->ran = true;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_set_store(nsgpu_wifi *h, int store) {
+  if (!h) return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: null");
+  switch (store) {
+    case NSGPU_WIFI_STORE_AUTO:
+      h->use_lds = h->lds_ok && h->lds_P >= 16;
+      break;
+    case NSGPU_WIFI_STORE_LDS:
+      if (!h->lds_ok) return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: the split queues do not fit LDS");
+      h->use_lds = true;
+      break;
+    case NSGPU_WIFI_STORE_HBM:
+      h->use_lds = false;
+      break;
+    default:
+      return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: store %d", store);
+  }
+  h->store = store;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifi_get_store(nsgpu_wifi *h, int *store, uint32_t *phys_per_block, uint32_t *e_cap) {
+  if (!h || !store) return set_error(NSGPU_EINVAL, "nsgpu_wifi_get_store: null");
+  *store = h->use_lds ? NSGPU_WIFI_STORE_LDS : NSGPU_WIFI_STORE_HBM;
+  if (phys_per_block) *phys_per_block = h->use_lds ? h->lds_P : 64;
+  if (e_cap) *e_cap = h->use_lds ? h->lds_ecap : h->D.ni_mask + 1;
   return NSGPU_OK;
 }
 
@@ -811,6 +1052,16 @@ static int wifi_check(nsgpu_wifi *h, uint64_t *n_sync) {
   unsigned long long ns = 0;
   NSGPU_HIP(hipMemcpy(&err, h->D.err, sizeof(err), hipMemcpyDeviceToHost));
   NSGPU_HIP(hipMemcpy(&ns, h->D.n_sync, sizeof(ns), hipMemcpyDeviceToHost));
+  if ((err & ERR_LDS) && !(err & (ERR_TX_IN_TX | ERR_NICAP))) {
+    // an S queue outgrew its LDS capacity (more starts at one instant than SCAP_LDS): the same run on
+    // the HBM ring, and every later run of this handle too
+    h->use_lds = false;
+    int rc = wifi_launch(h, h->last, nullptr);
+    if (rc != NSGPU_OK) return rc;
+    NSGPU_HIP(hipStreamSynchronize(h->last));
+    NSGPU_HIP(hipMemcpy(&err, h->D.err, sizeof(err), hipMemcpyDeviceToHost));
+    NSGPU_HIP(hipMemcpy(&ns, h->D.n_sync, sizeof(ns), hipMemcpyDeviceToHost));
+  }
   if (err & ERR_TX_IN_TX) return set_error(NSGPU_ESTATE, "nsgpu_wifi: SendPacket while in TX (the reference's NS_FATAL_ERROR)");
   if (err & ERR_NICAP) return set_error(NSGPU_ENOMEM, "nsgpu_wifi: a NiChanges list outgrew ni_cap %u", h->D.ni_mask + 1);
   if (err & ERR_WINDOW) return set_error(NSGPU_ENOMEM, "nsgpu_wifi: more than 64 transmissions inside one arrival spread");

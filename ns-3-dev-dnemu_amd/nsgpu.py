@@ -153,6 +153,8 @@ SIGNATURES = {
     "nsgpu_wifi_read_ends": (C.c_int, [_vp, _vp, _u64, _vp]),
     "nsgpu_wifi_read_rx_log": (C.c_int, [_vp, _vp]),
     "nsgpu_wifi_destroy": (C.c_int, [_vp]),
+    "nsgpu_wifi_set_store": (C.c_int, [_vp, C.c_int]),
+    "nsgpu_wifi_get_store": (C.c_int, [_vp, _vp, _vp, _vp]),
     "nsgpu_wifi_kernel_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nsgpu_wifi_kernel_name": (C.c_char_p, [C.c_int]),
     "nsgpu_wifi_profile": (C.c_int, [_vp, _vp, _vp]),

@@ -19,6 +19,7 @@ import nsgpu
 
 DSSS, OFDM, ERP_OFDM = 0, 1, 2
 PREAMBLE_LONG, PREAMBLE_SHORT = 0, 1
+STORE_AUTO, STORE_LDS, STORE_HBM = 0, 1, 2  # nsgpu_wifi_store: where each phy's NiChanges list lives
 SYNC, DROP_RX, DROP_TX, DROP_ED, NOT_RUN = 0, 1, 2, 3, 255
 F_CCA_EVAL, F_CCA_SWITCH, F_NEAR_ED, F_NEAR_CCA = 1, 2, 4, 8
 END_CANCELLED, END_DISPATCHED = 1, 2
@@ -162,7 +163,7 @@ def wifi_grid(n_side=100, spacing=100.0, period_s=1.0, stop_s=2.0, size=FRAME_10
 class Engine:
     """The device receive subset for one scenario (nsgpu_wifi_create / run / readers)."""
 
-    def __init__(self, scenario, rx_log=False, stream=None):
+    def __init__(self, scenario, rx_log=False, stream=None, store=STORE_AUTO):
         self.sc = scenario
         self.s = scenario.c_struct()
         self.stream = stream
@@ -170,6 +171,13 @@ class Engine:
         h = C.c_void_p()
         nsgpu.check(nsgpu.lib().nsgpu_wifi_create(C.byref(self.s), int(rx_log), C.byref(h)))
         self.h = h.value
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_set_store(self.h, int(store)))
+
+    def store(self):
+        """(store the next run uses, phys per block, end-queue / ring capacity) — nsgpu_wifi_get_store."""
+        st, p, e = C.c_int(), C.c_uint32(), C.c_uint32()
+        nsgpu.check(nsgpu.lib().nsgpu_wifi_get_store(self.h, C.byref(st), C.byref(p), C.byref(e)))
+        return st.value, p.value, e.value
 
     def launch(self):
         nsgpu.check(nsgpu.lib().nsgpu_wifi_run(self.h, self.stream))

@@ -34,9 +34,9 @@ def grid100_committed():
     return wifi.Scenario(x, y, z, tx, uid_start=5 + n, stop_ts=80_000_000, stop_uid=4 + n, ni_cap=512)
 
 
-def compare(sc, rx_log=True):
+def compare(sc, rx_log=True, store=wifi.STORE_AUTO):
     st, phys, base, ends, log = run_oracle(sc, rx_log=rx_log)
-    eng = wifi.Engine(sc, rx_log=rx_log)
+    eng = wifi.Engine(sc, rx_log=rx_log, store=store)
     g = eng.run()
     gd, od = g.as_dict(), st.as_dict()
     assert g.near_threshold == 0 and st.near_threshold == 0
@@ -70,10 +70,39 @@ def test_micro_scenarios():
     assert st.end_cancelled == 1
 
 
+STORES = [pytest.param(wifi.STORE_LDS, id="lds"), pytest.param(wifi.STORE_HBM, id="hbm")]
+
+
+@pytest.mark.parametrize("store", STORES)
 @pytest.mark.parametrize("seed,channels", [(1, (1,)), (2, (1,)), (3, (1, 6)), (4, (1, 6, 11)), (5, (1,)), ("ties", None)])
-def test_small_scenarios_match_oracle(seed, channels):
+def test_small_scenarios_match_oracle(seed, channels, store):
     sc = tie_scenario() if seed == "ties" else random_scenario(seed, channels=channels)
-    compare(sc)
+    compare(sc, store=store)
+
+
+def test_auto_store_is_lds_on_the_bench_grid():
+    """The bench grid's end queues fit LDS (most transmissions on the air at once ~ 10 / ms x 8.5 ms)."""
+    eng = wifi.Engine(wifi.wifi_grid(n_side=100, stop_s=0.15))
+    store, per_block, ecap = eng.store()
+    eng.close()
+    assert store == wifi.STORE_LDS and per_block >= 16 and ecap < 512, (store, per_block, ecap)
+
+
+def test_start_queue_overflow_repeats_on_the_ring():
+    """12 senders on a circle around phy 0 (integer (3, 4, 5) offsets: equal distances in floating point)
+    transmitting at once: their 12 arrivals at phy 0 share one nanosecond, so its start queue holds
+    more than SCAP_LDS (8) entries at one instant while it receives — the LDS run reports it and the
+    readers repeat the run on the HBM ring; results equal the oracle's either way."""
+    pts = [(0, 0)] + [(sx * a, sy * b) for a, b in ((3, 4), (4, 3)) for sx in (1, -1) for sy in (1, -1)] + \
+          [(5, 0), (-5, 0), (0, 5), (0, -5)]
+    x = np.array([p[0] * 20.0 for p in pts])
+    y = np.array([p[1] * 20.0 for p in pts])
+    z = np.zeros_like(x)
+    from test_wifi_oracle import one_tx
+    tx = np.concatenate([one_tx(1000, k, 4 + k) for k in range(1, len(pts))])
+    n = len(pts) - 1
+    sc = wifi.Scenario(x, y, z, tx, uid_start=5 + n, stop_ts=10 ** 9, stop_uid=4 + n)
+    compare(sc, store=wifi.STORE_LDS)
 
 
 def test_no_stop_event_and_empty_schedule():
@@ -84,10 +113,11 @@ def test_no_stop_event_and_empty_schedule():
     compare(wifi.Scenario(x, y, z, np.zeros(0, wifi.TX_DTYPE), uid_start=4))
 
 
-def test_grid_100x100_committed_schedule():
+@pytest.mark.parametrize("store", STORES)
+def test_grid_100x100_committed_schedule(store):
     """Config 3's grid (10,000 phys, LogDistance default) with the committed 300-frame schedule: 3 M
     Receive events, every one compared."""
-    st = compare(grid100_committed())
+    st = compare(grid100_committed(), store=store)
     assert st.rx == 300 * 9999
     assert st.sync > 1000 and st.drop_rx > 10000 and st.drop_tx > 1000 and st.cca_switches > 10000
     assert st.end_cancelled > 0
@@ -101,10 +131,11 @@ def test_wifi_grid_bench_config_prefix():
     assert st.dispatched > 10_000_000
 
 
-def test_capacity_overflow_fails_loudly():
+@pytest.mark.parametrize("store", STORES)
+def test_capacity_overflow_fails_loudly(store):
     sc = grid100_committed()
     sc.ni_cap = 8
-    eng = wifi.Engine(sc)
+    eng = wifi.Engine(sc, store=store)
     eng.launch()
     with pytest.raises(nsgpu.NsgpuError, match="ni_cap"):
         eng.stats()
