@@ -366,8 +366,13 @@ class WifiGrid:
 
     def roofline(self, step_kernel_ms, events_per_step):
         prof = self.engine.profile()
-        return {"kernel": self.kernel, "kernel_ms": prof["k_wifi_phy"], "events_per_launch": events_per_step,
-                "step_device_ms": step_kernel_ms, "kernels_ms": prof}
+        store, per_block, ecap = self.engine.store()
+        lds = (store & 3) == self.wifi.STORE_LDS
+        kernel = "nsgpu::k_wifi_phy_lds" if lds else "nsgpu::k_wifi_phy"
+        return {"kernel": kernel, "kernel_ms": prof["k_wifi_phy"], "events_per_launch": events_per_step,
+                "step_device_ms": step_kernel_ms, "kernels_ms": prof,
+                "store": {"niChanges": "lds split queues" if lds else "hbm ring", "phys_per_block": per_block,
+                          "end_queue_cap": ecap, "reception_table": not (store & self.wifi.INLINE_RX)}}
 
     def result(self):
         st = self.engine.stats()

@@ -151,9 +151,13 @@ int nsgpu_wifi_destroy(nsgpu_wifi *h);
  *                         create from the schedule (the most transmissions on the air at one instant);
  *                         a run whose start queue overflows is repeated on the HBM ring by the readers;
  *   NSGPU_WIFI_STORE_HBM  one sorted ring per phy in HBM (ni_cap entries);
- *   NSGPU_WIFI_STORE_AUTO LDS when a block holds at least 16 phys' queues (the default).
- * nsgpu_wifi_get_store reports the store the next run uses, its phys per block and the end-queue (LDS)
- * or ring (HBM) capacity. */
+ *   NSGPU_WIFI_STORE_AUTO LDS when a block holds at least 8 phys' queues (the default).
+ * Independently, the receptions (arrival, rxPowerW of every receiver x transmission pair: the fan-out
+ * arithmetic) are computed up front into an HBM table by one parallel kernel when n_phy x transmissions
+ * x 16 B fits half of the free HBM at create; | NSGPU_WIFI_INLINE_RX computes them inside the per-phy
+ * kernel instead (same values: the same expressions).
+ * nsgpu_wifi_get_store reports the store the next run uses (| NSGPU_WIFI_INLINE_RX without the table),
+ * its phys per block and the end-queue (LDS) or ring (HBM) capacity. */
 int nsgpu_wifi_set_store(nsgpu_wifi *h, int store);
 int nsgpu_wifi_get_store(nsgpu_wifi *h, int *store, uint32_t *phys_per_block, uint32_t *e_cap);
 /* Diagnostics: the kernels of one run and a run with each bracketed by HIP events (ms[k], k < count). */

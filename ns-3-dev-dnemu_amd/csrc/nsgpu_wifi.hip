@@ -102,7 +102,21 @@ struct WifiDev {
   uint32_t *err;
   uint32_t *hist, *off, *cur, *bucket, *base;
   nsgpu_wifi_end_record *ends;
+  struct RxPre *pre;  // nullable: [nphy][ktx] receptions computed up front (k_wifi_rx)
 };
+
+// One (receiver, transmission) pair computed up front by k_wifi_rx: the Receive's arrival and its
+// rxPowerW, or a marker (PRE_OWN: the receiver's own SendPacket, PRE_NONE: another channel, no Receive).
+struct RxPre {
+  uint64_t at;
+  double w;
+};
+constexpr uint64_t PRE_NONE = ~0ull, PRE_OWN = ~0ull - 1;
+struct TsDur {  // a TxDesc's (ts, dur) half-line
+  uint64_t ts;
+  int64_t dur;
+};
+static_assert(offsetof(TxDesc, dur) == offsetof(TxDesc, ts) + 8 && offsetof(TxDesc, ts) % 16 == 0, "TsDur view");
 
 // ConstantSpeedPropagationDelayModel::GetDelay + DefaultSimulatorImpl::ScheduleWithContext's m_currentTs +
 __device__ __forceinline__ uint64_t arrival(const WifiDev &D, uint32_t k, double px, double py, double pz,
@@ -227,18 +241,18 @@ struct RingNi {
 // `ndead` counts the summed entries the reference list still holds (until the next fold), so length()
 // is the reference's list length.
 struct SplitNi {
-  int64_t *st, *et;  // entry i of this phy's S / E at [i * stride] (interleaved over the block's lanes)
+  int64_t *st, *et;  // this phy's S / E rings (LDS)
   double *sd, *ed;
-  uint32_t stride, scap, ecap, cap;  // queue capacities; cap = ni_cap (the reference list's limit)
+  uint32_t scap, ecap, cap;  // queue capacities; cap = ni_cap (the reference list's limit)
   uint32_t hs, ns, he, ne, ndead;
   double cur_s;
   __device__ __forceinline__ uint32_t sx(uint32_t i) const {
     const uint32_t x = hs + i;
-    return (x < scap ? x : x - scap) * stride;
+    return x < scap ? x : x - scap;
   }
   __device__ __forceinline__ uint32_t ex(uint32_t i) const {
     const uint32_t x = he + i;
-    return (x < ecap ? x : x - ecap) * stride;
+    return x < ecap ? x : x - ecap;
   }
   __device__ __forceinline__ uint32_t length() const { return ndead + ns + ne; }
   __device__ __forceinline__ bool room() const { return length() + 2 <= cap; }
@@ -307,29 +321,74 @@ struct SplitNi {
       ie++;
     }
     for (uint32_t q = 0; !stop && q < ns; q++) step(st[sx(q)], sd[sx(q)]);
-    while (!stop && ie < ne) {
-      int64_t bt[NB];
+    if (stop || ie >= ne) return end;
+    // The tail: end entries after now, all deltas negative, so the sums only fall (round-to-nearest is
+    // monotonic).  The walk stops at the first sum below the threshold; of the sums above it the last
+    // is the nearest to it, so the near-threshold test needs only that one and the stopping one, and
+    // the loop needs only the deltas (the stopping entry's time is read once at the end).
+    double prev = noise;
+    uint32_t i = ie, si = 0;
+    for (; i < ne && !stop; i += NB) {
       double bd[NB];
 #pragma unroll
-      for (int u = 0; u < NB; u++) {
-        const uint32_t i = ie + u < ne ? ie + u : ie;
-        bt[u] = et[ex(i)];
-        bd[u] = ed[ex(i)];
-      }
+      for (int u = 0; u < NB; u++) bd[u] = ed[ex(i + u < ne ? i + u : i)];
 #pragma unroll
       for (int u = 0; u < NB; u++) {
-        if (stop || ie >= ne) break;
-        step(bt[u], bd[u]);
-        ie++;
+        if (!stop && i + u < ne) {
+          prev = noise;
+          noise += bd[u];
+          if (noise < ccaW) stop = true, si = i + u;
+        }
       }
     }
+    if (stop) {
+      i = si;
+    } else {  // every entry added: the walk ends at the last one
+      i = ne - 1;
+      prev = noise;  // (the last sum is the nearest of the ones at or above the threshold)
+    }
+    end = et[ex(i)];
+    if (near_thr(prev, ccaW) || near_thr(noise, ccaW)) flags |= NSGPU_WIFI_F_NEAR_CCA;
     return end;
   }
 };
 
-// One lane = one phy: its SendPacket / Receive / EndReceive sequence in (ts, uid) order.
-template <class Ni>
-__device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &ni) {
+// DbmToW (yans-wifi-phy.cc:727-732) of CalcRxPower (propagation-loss-model.cc:64-74) + RxGain
+__device__ __forceinline__ double rx_power_w(const WifiDev &D, double tx_dbm, double dist) {
+  const double rxPowerDbm = calc_rx_power(D.loss, tx_dbm, dist) + D.rx_gain_db;
+  return pow(10.0, rxPowerDbm / 10.0) / 1000.0;
+}
+
+// The fan-out arithmetic of every (receiver j, transmission k) pair, all in parallel (the per-phy
+// kernel's serial chain then reads 16 B per Receive instead of running the distance / delay / loss /
+// DbmToW chain itself): YansWifiChannel::Send's receiver loop (yans-wifi-channel.cc:77-115).
+__global__ __launch_bounds__(256) void k_wifi_rx(const WifiDev D) {
+  const uint64_t K = D.ktx, n = (uint64_t)D.nphy * K;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t j = i / K, k = i - j * K;
+    const TxDesc t = D.txd[k];
+    RxPre r{PRE_NONE, 0.0};
+    if (t.phy == (uint32_t)j) {
+      r.at = PRE_OWN;
+    } else if (t.chan == D.chan[j]) {
+      const double dist = distance3(t.x, t.y, t.z, D.x[j], D.y[j], D.z[j]);
+      r.at = t.ts + (uint64_t)seconds_to_ts(dist / D.speed);
+      r.w = rx_power_w(D, t.dbm, dist);
+    }
+    D.pre[i] = r;
+  }
+}
+
+// A phy's pending EndReceive events (the live one + cancelled ones), one record per lane in LDS.
+struct PeSlots {
+  uint64_t ts[PE_CAP], sts[PE_CAP];
+  uint32_t tx[PE_CAP], slot[PE_CAP], can[PE_CAP];
+};
+
+// One lane = one phy: its SendPacket / Receive / EndReceive sequence in (ts, uid) order.  PRE: the
+// receptions come from k_wifi_rx's table.
+template <bool PRE, class Ni>
+__device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &ni, PeSlots *pe) {
   const double px = D.x[j], py = D.y[j], pz = D.z[j];
   const uint32_t ch = D.chan[j];
   // InterferenceHelper (m_niChanges: `ni`, m_firstPower) and WifiPhyStateHelper; the two m_rxing flags
@@ -338,11 +397,13 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
   double firstPower = 0.0;
   bool rxing = false;
   int64_t endTx = 0, endRx = 0, endCca = 0;
-  // pending EndReceive events
-  uint64_t pe_ts[PE_CAP], pe_sts[PE_CAP];
-  uint32_t pe_tx[PE_CAP], pe_slot[PE_CAP];
-  bool pe_can[PE_CAP];
+  // pending EndReceive events (in LDS: a lane indexes them with its own per-lane index)
+  uint64_t *pe_ts = pe->ts, *pe_sts = pe->sts;
+  uint32_t *pe_tx = pe->tx, *pe_slot = pe->slot, *pe_can = pe->can;
   int npe = 0, live = -1;
+  int e = -1;  // the first pending EndReceive (recomputed when the set changes)
+  bool e_dirty = false;
+  uint64_t e_ts = INF, e_sts = 0;
   // transmissions: [p, p + 64) is the window, bit i of `done` = transmission p + i consumed here
   uint32_t p = 0;
   uint64_t done = 0;
@@ -353,7 +414,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
   bool have_c = false;
   uint64_t c_ts = INF, c_tts = 0;
   uint32_t c_k = NONE;
-  double c_dist = 0.0, c_dbm = 0.0;
+  double c_dist = 0.0, c_dbm = 0.0, c_w = 0.0;
   int64_t c_dur = 0;
   uint32_t err = 0;
   nsgpu_wifi_phy_counters c = {};
@@ -363,40 +424,92 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
     if (!have_c) {  // the next Receive: the smallest arrival of an unconsumed transmission
       c_ts = INF;
       c_k = NONE;
-      uint32_t i = 0;
-      for (; i < 64; i++) {
-        const uint32_t k = p + i;
-        if (k >= D.ktx) break;
-        const TxDesc t = D.txd[k];
-        if (t.ts >= c_ts) break;  // its arrival (and every later one) comes after c_ts
-        if ((done >> i) & 1ull) continue;
-        if (t.phy == (uint32_t)j) continue;  // our own SendPacket: taken in order below
-        if (t.chan != ch) {                  // not on our channel: no Receive (yans-wifi-channel.cc:88-91)
-          done |= 1ull << i;
-          continue;
+      uint32_t at = 64;  // where the scan stopped (64: it went through the whole window)
+      if (PRE) {
+        const RxPre *row = D.pre + (uint64_t)j * D.ktx;
+        for (uint32_t i0 = 0; i0 < 64 && at == 64; i0 += 2) {
+          TsDur tp[2];  // two transmissions per memory trip (a scan usually reads the next two)
+          RxPre rp[2];
+#pragma unroll
+          for (int u = 0; u < 2; u++) {
+            const uint32_t k = p + i0 + u;
+            if (k < D.ktx) {
+              tp[u] = *reinterpret_cast<const TsDur *>(&D.txd[k].ts);
+              rp[u] = row[k];
+            } else {
+              tp[u].ts = INF;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 2; u++) {
+            const uint32_t i = i0 + u, k = p + i;
+            if (at != 64) break;
+            if (k >= D.ktx || tp[u].ts >= c_ts) {
+              at = i;
+              break;
+            }
+            if ((done >> i) & 1ull) continue;
+            if (rp[u].at == PRE_OWN) continue;
+            if (rp[u].at == PRE_NONE) {
+              done |= 1ull << i;
+              continue;
+            }
+            if (rp[u].at < c_ts) c_ts = rp[u].at, c_k = k, c_w = rp[u].w, c_tts = tp[u].ts, c_dur = tp[u].dur;
+          }
         }
-        // GetDistanceFrom (sender, receiver); ConstantSpeedPropagationDelayModel::GetDelay
-        const double dist = distance3(t.x, t.y, t.z, px, py, pz);
-        const uint64_t a = t.ts + (uint64_t)seconds_to_ts(dist / D.speed);
-        if (a < c_ts) c_ts = a, c_k = k, c_dist = dist, c_tts = t.ts, c_dbm = t.dbm, c_dur = t.dur;
+      } else {
+      for (uint32_t i0 = 0; i0 < 64 && at == 64; i0 += 2) {
+        TxDesc tp[2];  // two descriptors per memory trip (a scan usually reads the next two)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const uint32_t k = p + i0 + u;
+          if (k < D.ktx) tp[u] = D.txd[k];
+          else tp[u].ts = INF;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const uint32_t i = i0 + u, k = p + i;
+          const TxDesc &t = tp[u];
+          if (at != 64) break;
+          if (k >= D.ktx || t.ts >= c_ts) {  // its arrival (and every later one) comes after c_ts
+            at = i;
+            break;
+          }
+          if ((done >> i) & 1ull) continue;
+          if (t.phy == (uint32_t)j) continue;  // our own SendPacket: taken in order below
+          if (t.chan != ch) {                  // not on our channel: no Receive (yans-wifi-channel.cc:88-91)
+            done |= 1ull << i;
+            continue;
+          }
+          // GetDistanceFrom (sender, receiver); ConstantSpeedPropagationDelayModel::GetDelay
+          const double dist = distance3(t.x, t.y, t.z, px, py, pz);
+          const uint64_t a = t.ts + (uint64_t)seconds_to_ts(dist / D.speed);
+          if (a < c_ts) c_ts = a, c_k = k, c_dist = dist, c_tts = t.ts, c_dbm = t.dbm, c_dur = t.dur;
+        }
       }
-      if (i == 64 && p + 64 < D.ktx && D.txd[p + 64].ts < c_ts) {
+      }
+      if (at == 64 && p + 64 < D.ktx && D.txd[p + 64].ts < c_ts) {
         err |= ERR_WINDOW;
         break;
       }
       while (done & 1ull) done >>= 1, p++;
       have_c = true;
     }
-    int e = -1;
-    for (int q = 0; q < npe; q++)
-      if (e < 0 || pe_ts[q] < pe_ts[e] ||
-          (pe_ts[q] == pe_ts[e] && (pe_sts[q] < pe_sts[e] || (pe_sts[q] == pe_sts[e] && pe_tx[q] < pe_tx[e]))))
-        e = q;
+    if (e_dirty) {  // the first pending EndReceive (ts, then the syncing Receive's key), after a change
+      e = -1;
+      for (int q = 0; q < npe; q++)
+        if (e < 0 || pe_ts[q] < pe_ts[e] ||
+            (pe_ts[q] == pe_ts[e] && (pe_sts[q] < pe_sts[e] || (pe_sts[q] == pe_sts[e] && pe_tx[q] < pe_tx[e]))))
+          e = q;
+      e_ts = e >= 0 ? pe_ts[e] : INF;
+      e_sts = e >= 0 ? pe_sts[e] : 0;
+      e_dirty = false;
+    }
     int kind = -1;
     uint64_t now = INF;
     if (ok != NONE) kind = 0, now = ok_ts;
     if (c_k != NONE && c_ts < now) kind = 1, now = c_ts;
-    if (e >= 0 && (pe_ts[e] < now || (pe_ts[e] == now && kind == 1 && c_tts > pe_sts[e]))) kind = 2, now = pe_ts[e];
+    if (e >= 0 && (e_ts < now || (e_ts == now && kind == 1 && c_tts > e_sts))) kind = 2, now = e_ts;
     if (kind < 0) break;
     if (kind != 0 && now >= D.stop_ts) break;  // Stop (a setup uid) runs first; nothing after it does
     const int64_t nw = (int64_t)now;
@@ -448,6 +561,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
         if (live == l) live = e;
       }
       npe--;
+      e_dirty = true;
       disp++;
       last_ts = now;
       continue;
@@ -455,8 +569,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
 
     // YansWifiChannel::Receive -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496)
     const uint32_t k = c_k;
-    const double rxPowerDbm = calc_rx_power(D.loss, c_dbm, c_dist) + D.rx_gain_db;
-    const double rxPowerW = pow(10.0, rxPowerDbm / 10.0) / 1000.0;  // DbmToW (:727-732)
+    const double rxPowerW = PRE ? c_w : rx_power_w(D, c_dbm, c_dist);
     const int64_t endNew = nw + c_dur;
     // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
     ni.on_receive(nw);
@@ -499,6 +612,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
         endRx = endNew;
         pe_ts[npe] = (uint64_t)endNew, pe_sts[npe] = now, pe_tx[npe] = k, pe_slot[npe] = (uint32_t)slot, pe_can[npe] = false;
         live = npe++;
+        e_dirty = true;
         c.sync++;
       } else {
         outcome = NSGPU_WIFI_DROP_ED;
@@ -575,26 +689,32 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
 }
 
 // HBM ring store: 64 phys per block.
+template <bool PRE>
 __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (j >= D.nphy) return;
+  __shared__ PeSlots pes[64];
   RingNi ni{D.ni + (uint64_t)j * (D.ni_mask + 1), D.ni_mask, 0, 0, 0, 0.0};
-  phy_run(D, j, ni);
+  phy_run<PRE>(D, j, ni, &pes[threadIdx.x]);
 }
 
-// LDS split store: blockDim.x phys per block, each with scap + ecap 16-B entries of the block's dynamic
-// LDS, interleaved over the lanes ([i * blockDim.x + lane]: lanes at equal depths hit distinct banks).
+// LDS split store: blockDim.x phys per block, each with its S ring (scap entries), E ring (ecap) and
+// pending EndReceive records in the block's dynamic LDS (wifi_lds_bytes).
+__host__ __device__ constexpr size_t wifi_lds_per_phy(uint32_t scap, uint32_t ecap) {
+  return (size_t)(scap + ecap) * 16 + sizeof(PeSlots);
+}
+template <bool PRE>
 __global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t scap, uint32_t ecap) {
   extern __shared__ uint64_t wlds[];
   const uint32_t P = blockDim.x, l = threadIdx.x;
   const int64_t j = (int64_t)blockIdx.x * P + l;
   if (j >= D.nphy) return;
-  int64_t *et = reinterpret_cast<int64_t *>(wlds);
-  double *ed = reinterpret_cast<double *>(wlds + (size_t)ecap * P);
-  int64_t *st = reinterpret_cast<int64_t *>(wlds + (size_t)2 * ecap * P);
-  double *sd = reinterpret_cast<double *>(wlds + (size_t)(2 * ecap + scap) * P);
-  SplitNi ni{st + l, et + l, sd + l, ed + l, P, scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0};
-  phy_run(D, j, ni);
+  uint64_t *b = wlds + (size_t)l * (2 * (scap + ecap));
+  PeSlots *pe = reinterpret_cast<PeSlots *>(wlds + (size_t)P * (2 * (scap + ecap))) + l;
+  SplitNi ni{reinterpret_cast<int64_t *>(b + 2 * ecap), reinterpret_cast<int64_t *>(b),
+             reinterpret_cast<double *>(b + 2 * ecap + scap), reinterpret_cast<double *>(b + ecap),
+             scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0};
+  phy_run<PRE>(D, j, ni, pe);
 }
 
 // Syncs per bucket m = #transmissions with t_T <= ts (binary search over the schedule).
@@ -737,8 +857,9 @@ struct nsgpu_wifi {
   // ring; lds_ok = the plan below exists, use_lds = the next run uses it
   int store = NSGPU_WIFI_STORE_AUTO;
   bool lds_ok = false, use_lds = false;
-  uint32_t lds_P = 0, lds_scap = 0, lds_ecap = 0;
+  uint32_t lds_P = 0, lds_pmax = 0, lds_scap = 0, lds_ecap = 0;
   size_t lds_bytes = 0;
+  bool use_pre = false;  // the run reads its receptions from D.pre (allocated when the table fits HBM)
 };
 
 constexpr uint32_t SCAP_LDS = 8;  // S: starts at one instant (more: ERR_LDS, the run repeats on the ring)
@@ -884,17 +1005,26 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&lmax, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && lmax > 0) {
       const uint32_t ecap = std::max<uint32_t>(overlap + 2, 8);
-      const size_t per = (size_t)(ecap + SCAP_LDS) * 16;
-      const size_t P = std::min<size_t>(64, (size_t)lmax / per);
-      if (P >= 1) {
+      const size_t per = wifi_lds_per_phy(SCAP_LDS, ecap);
+      const size_t pmax = std::min<size_t>(64, (size_t)lmax / per);
+      // A lane's run is one serial chain of dependent steps, and a wave's step is the union of its lanes'
+      // branches (event kinds, CCA walks of different lengths): spread the phys over every SIMD (one wave
+      // each, 4 per CU) rather than packing 64 into a wave.
+      int ncu = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+      size_t P = (size_t)((N + 4 * (int64_t)ncu - 1) / (4 * (int64_t)ncu));
+      if (const char *e = getenv("NSGPU_WIFI_PHYS_PER_BLOCK")) P = (size_t)atoi(e);  // (diagnostic sweeps)
+      P = std::max<size_t>(1, std::min(P, pmax));
+      if (pmax >= 1) {
         h->lds_ok = true;
         h->lds_P = (uint32_t)P;
         h->lds_scap = SCAP_LDS;
         h->lds_ecap = ecap;
         h->lds_bytes = P * per;
       }
-      // auto: the split queues when a block still holds 16 phys (below that the ring's 64-lane blocks win)
-      h->use_lds = h->lds_ok && P >= 16;
+      // auto: the split queues when LDS holds 8 phys' queues per block (longer queues: the HBM ring)
+      h->lds_pmax = (uint32_t)pmax;
+      h->use_lds = h->lds_ok && pmax >= 8;
     }
   }
   int rc = NSGPU_OK;
@@ -942,13 +1072,24 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   TRY(dalloc(h, &D.bucket, sync_cap));
   TRY(dalloc(h, &D.base, std::max<uint32_t>(ktx, 1)));
   TRY(dalloc(h, &D.ends, sync_cap));
+  {  // the reception table (k_wifi_rx): n_phy x dispatched transmissions x 16 B, when half of free HBM holds it
+    size_t fr = 0, tot = 0;
+    const uint64_t bytes = (uint64_t)N * ktx * sizeof(RxPre);
+    D.pre = nullptr;
+    if (ktx && hipMemGetInfo(&fr, &tot) == hipSuccess && bytes <= fr / 2) {
+      TRY(dalloc(h, &D.pre, (size_t)N * ktx));
+      h->use_pre = true;
+    }
+  }
 #undef TRY
   *out = h;
   return NSGPU_OK;
 }
 
-static const char *const WIFI_KERNELS[] = {"k_wifi_phy", "k_sync_hist", "k_tx_base", "k_sync_place", "k_sync_rank"};
-constexpr int WIFI_NK = 5;
+// (k_wifi_rx: 0 ms when the run computes its receptions inline; k_wifi_phy: k_wifi_phy_lds with the LDS store)
+static const char *const WIFI_KERNELS[] = {"k_wifi_rx", "k_wifi_phy", "k_sync_hist", "k_tx_base", "k_sync_place",
+                                           "k_sync_rank"};
+constexpr int WIFI_NK = 6;
 
 // One whole run on `s`; with `ev` (WIFI_NK + 1 events) each kernel of the chain is bracketed.
 static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
@@ -961,24 +1102,34 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
   const uint64_t nlog = (uint64_t)D.ktx * (uint64_t)D.nphy;
   if (D.rx_log && nlog) hipLaunchKernelGGL(k_rx_log_init, dim3(1024), dim3(256), 0, s, D.rx_log, nlog);
   if (ev) NSGPU_HIP(hipEventRecord(ev[0], s));
-  if (h->use_lds) {
-    if (h->lds_bytes > 65536)
-      NSGPU_HIP(hipFuncSetAttribute((const void *)k_wifi_phy_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)h->lds_bytes));
-    hipLaunchKernelGGL(k_wifi_phy_lds, dim3((unsigned)((D.nphy + h->lds_P - 1) / h->lds_P)), dim3(h->lds_P),
-                       h->lds_bytes, s, D, h->lds_scap, h->lds_ecap);
-  } else {
-    hipLaunchKernelGGL(k_wifi_phy, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, s, D);
+  WifiDev Dk = D;
+  if (!h->use_pre) Dk.pre = nullptr;
+  if (Dk.pre) {
+    const uint64_t n = (uint64_t)D.nphy * D.ktx;
+    if (n) hipLaunchKernelGGL(k_wifi_rx, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, s, Dk);
   }
   if (ev) NSGPU_HIP(hipEventRecord(ev[1], s));
-  hipLaunchKernelGGL(k_sync_hist, dim3(1024), dim3(256), 0, s, D);
+  if (h->use_lds) {
+    const void *kf = Dk.pre ? (const void *)k_wifi_phy_lds<true> : (const void *)k_wifi_phy_lds<false>;
+    if (h->lds_bytes > 65536)
+      NSGPU_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes));
+    const dim3 g((unsigned)((D.nphy + h->lds_P - 1) / h->lds_P)), b(h->lds_P);
+    if (Dk.pre) hipLaunchKernelGGL(k_wifi_phy_lds<true>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
+    else hipLaunchKernelGGL(k_wifi_phy_lds<false>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
+  } else {
+    const dim3 g((unsigned)((D.nphy + 63) / 64)), b(64);
+    if (Dk.pre) hipLaunchKernelGGL(k_wifi_phy<true>, g, b, 0, s, Dk);
+    else hipLaunchKernelGGL(k_wifi_phy<false>, g, b, 0, s, Dk);
+  }
   if (ev) NSGPU_HIP(hipEventRecord(ev[2], s));
-  hipLaunchKernelGGL(k_tx_base, dim3(1), dim3(1024), 0, s, D);
+  hipLaunchKernelGGL(k_sync_hist, dim3(1024), dim3(256), 0, s, D);
   if (ev) NSGPU_HIP(hipEventRecord(ev[3], s));
-  hipLaunchKernelGGL(k_sync_place, dim3(1024), dim3(256), 0, s, D);
+  hipLaunchKernelGGL(k_tx_base, dim3(1), dim3(1024), 0, s, D);
   if (ev) NSGPU_HIP(hipEventRecord(ev[4], s));
-  hipLaunchKernelGGL(k_sync_rank, dim3(1024), dim3(256), 0, s, D);
+  hipLaunchKernelGGL(k_sync_place, dim3(1024), dim3(256), 0, s, D);
   if (ev) NSGPU_HIP(hipEventRecord(ev[5], s));
+  hipLaunchKernelGGL(k_sync_rank, dim3(1024), dim3(256), 0, s, D);
+  if (ev) NSGPU_HIP(hipEventRecord(ev[6], s));
   if (D.rx_log && nlog) hipLaunchKernelGGL(k_rx_log_keys, dim3(1024), dim3(256), 0, s, D);
   NSGPU_HIP(hipGetLastError());
   h->last = s;
@@ -988,9 +1139,12 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
 
 extern "C" int nsgpu_wifi_set_store(nsgpu_wifi *h, int store) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: null");
+  if (store & ~(NSGPU_WIFI_STORE_MASK | NSGPU_WIFI_INLINE_RX)) return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: store %d", store);
+  h->use_pre = h->D.pre != nullptr && !(store & NSGPU_WIFI_INLINE_RX);
+  store &= NSGPU_WIFI_STORE_MASK;
   switch (store) {
     case NSGPU_WIFI_STORE_AUTO:
-      h->use_lds = h->lds_ok && h->lds_P >= 16;
+      h->use_lds = h->lds_ok && h->lds_pmax >= 8;
       break;
     case NSGPU_WIFI_STORE_LDS:
       if (!h->lds_ok) return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: the split queues do not fit LDS");
@@ -1008,7 +1162,7 @@ extern "C" int nsgpu_wifi_set_store(nsgpu_wifi *h, int store) {
 
 extern "C" int nsgpu_wifi_get_store(nsgpu_wifi *h, int *store, uint32_t *phys_per_block, uint32_t *e_cap) {
   if (!h || !store) return set_error(NSGPU_EINVAL, "nsgpu_wifi_get_store: null");
-  *store = h->use_lds ? NSGPU_WIFI_STORE_LDS : NSGPU_WIFI_STORE_HBM;
+  *store = (h->use_lds ? NSGPU_WIFI_STORE_LDS : NSGPU_WIFI_STORE_HBM) | (h->use_pre ? 0 : NSGPU_WIFI_INLINE_RX);
   if (phys_per_block) *phys_per_block = h->use_lds ? h->lds_P : 64;
   if (e_cap) *e_cap = h->use_lds ? h->lds_ecap : h->D.ni_mask + 1;
   return NSGPU_OK;

@@ -70,7 +70,9 @@ def test_micro_scenarios():
     assert st.end_cancelled == 1
 
 
-STORES = [pytest.param(wifi.STORE_LDS, id="lds"), pytest.param(wifi.STORE_HBM, id="hbm")]
+STORES = [pytest.param(wifi.STORE_LDS, id="lds"), pytest.param(wifi.STORE_HBM, id="hbm"),
+          pytest.param(wifi.STORE_LDS | wifi.INLINE_RX, id="lds-inline"),
+          pytest.param(wifi.STORE_HBM | wifi.INLINE_RX, id="hbm-inline")]
 
 
 @pytest.mark.parametrize("store", STORES)
@@ -85,7 +87,10 @@ def test_auto_store_is_lds_on_the_bench_grid():
     eng = wifi.Engine(wifi.wifi_grid(n_side=100, stop_s=0.15))
     store, per_block, ecap = eng.store()
     eng.close()
-    assert store == wifi.STORE_LDS and per_block >= 16 and ecap < 512, (store, per_block, ecap)
+    assert store == wifi.STORE_LDS and 1 <= per_block <= 64 and ecap < 512, (store, per_block, ecap)
+    eng = wifi.Engine(wifi.wifi_grid(n_side=100, stop_s=0.15), store=wifi.STORE_HBM | wifi.INLINE_RX)
+    assert eng.store()[0] == wifi.STORE_HBM | wifi.INLINE_RX
+    eng.close()
 
 
 def test_start_queue_overflow_repeats_on_the_ring():
