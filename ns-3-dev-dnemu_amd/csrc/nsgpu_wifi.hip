@@ -243,9 +243,12 @@ struct RingNi {
 struct SplitNi {
   int64_t *st, *et;  // this phy's S / E rings (LDS)
   double *sd, *ed;
+  double *ec;        // E's running sums: ec[i] = cb + d[head] + ... + d[i] (summed in queue order)
   uint32_t scap, ecap, cap;  // queue capacities; cap = ni_cap (the reference list's limit)
   uint32_t hs, ns, he, ne, ndead;
   double cur_s;
+  double cb;         // the running sum before E's head
+  uint32_t nsum;     // terms summed into ec since its last rebase
   __device__ __forceinline__ uint32_t sx(uint32_t i) const {
     const uint32_t x = hs + i;
     return x < scap ? x : x - scap;
@@ -267,6 +270,7 @@ struct SplitNi {
       if (t == INT64_MAX || (LE ? t > lim : t >= lim)) return;
       if (e) {
         cur_s += ed[ex(0)];
+        cb = ec[ex(0)];
         he = he + 1 == ecap ? 0 : he + 1;
         ne--;
       } else {
@@ -303,6 +307,57 @@ struct SplitNi {
     et[ex(q)] = t;
     ed[ex(q)] = d;
     ne++;
+    double c = q ? ec[ex(q - 1)] : cb;  // the running sums from the new entry on (usually just its own)
+    for (uint32_t i = q; i < ne; i++) {
+      c += ed[ex(i)];
+      ec[ex(i)] = c;
+    }
+    nsum += ne - q;
+    // rebase before the sums grow far past the live part (their rounding error is relative to them)
+    if (nsum > 4096 || fabs(c) > 16.0 * fabs(c - cb)) {
+      cb = 0.0;
+      c = 0.0;
+      for (uint32_t i = 0; i < ne; i++) {
+        c += ed[ex(i)];
+        ec[ex(i)] = c;
+      }
+      nsum = ne;
+    }
+  }
+  // GetEnergyDuration's tail by bisection over E's running sums, certified: the walk's sum after entry i
+  // is v_i = noise + d_ie + ... + d_i summed in order, a = noise + (ec[i] - ec[ie - 1]) approximates it
+  // within far less than dl (both are within ~(n + 4096) ulps of the real sum, relative to the terms'
+  // magnitudes, which `scale` bounds), and both fall with i.  The first i with a_i < ccaW - dl after
+  // an a_{i-1} >= ccaW + dl is then exactly the walk's stop, and the near-threshold tests on v_{i-1}, v_i
+  // are decided when a is further than dl from the band's edge.  Otherwise (a sum within ~1e-10 of the
+  // threshold or the band's edge) the exact walk runs.  Returns false when undecided.
+  __device__ __forceinline__ bool tail_bisect(uint32_t ie, double noise, double ccaW, int64_t &end,
+                                              uint32_t &flags) const {
+    const double base = ie ? ec[ex(ie - 1)] : cb;
+    const double last = ec[ex(ne - 1)];
+    const double dl = 1e-10 * (noise + fabs(base) + fabs(last));
+    uint32_t lo = ie, hi = ne;  // the first i with a_i < ccaW - dl (ne: none)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (noise + (ec[ex(mid)] - base) < ccaW - dl) hi = mid;
+      else lo = mid + 1;
+    }
+    const double nb = 1e-9 * ccaW;  // near_thr's band
+    auto near_of = [&](double a, int &r) {  // 1 / 0 when decided, else r = -1
+      const double x = fabs(a - ccaW);
+      r = x > nb + dl ? 0 : (x < nb - dl ? 1 : -1);
+    };
+    int n0 = 0, n1 = 0;
+    if (lo > ie) {  // v_{lo-1}: the last sum at or above the threshold
+      const double a = noise + (ec[ex(lo - 1)] - base);
+      if (!(a >= ccaW + dl)) return false;
+      near_of(a, n0);
+    }  // (lo == ie: it is `noise` itself, tested exactly by the walk's head)
+    if (lo < ne) near_of(noise + (ec[ex(lo)] - base), n1);
+    if (n0 < 0 || n1 < 0) return false;
+    end = et[ex(lo < ne ? lo : ne - 1)];
+    if (n0 | n1) flags |= NSGPU_WIFI_F_NEAR_CCA;
+    return true;
   }
   __device__ __forceinline__ int64_t energy_end(int64_t nw, double ccaW, uint32_t &flags) {
     // (on_receive advanced the cursor to now: S holds starts at now only, E ends at or after now)
@@ -322,7 +377,8 @@ struct SplitNi {
     }
     for (uint32_t q = 0; !stop && q < ns; q++) step(st[sx(q)], sd[sx(q)]);
     if (stop || ie >= ne) return end;
-    // The tail: end entries after now, all deltas negative, so the sums only fall (round-to-nearest is
+    if (tail_bisect(ie, noise, ccaW, end, flags)) return end;
+    // The tail (undecided by the bisection): end entries after now, all deltas negative, so the sums only fall (round-to-nearest is
     // monotonic).  The walk stops at the first sum below the threshold; of the sums above it the last
     // is the nearest to it, so the near-threshold test needs only that one and the stopping one, and
     // the loop needs only the deltas (the stopping entry's time is read once at the end).
@@ -701,7 +757,7 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
 // LDS split store: blockDim.x phys per block, each with its S ring (scap entries), E ring (ecap) and
 // pending EndReceive records in the block's dynamic LDS (wifi_lds_bytes).
 __host__ __device__ constexpr size_t wifi_lds_per_phy(uint32_t scap, uint32_t ecap) {
-  return (size_t)(scap + ecap) * 16 + sizeof(PeSlots);
+  return (size_t)(scap + ecap) * 16 + (size_t)ecap * 8 + sizeof(PeSlots);
 }
 template <bool PRE>
 __global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t scap, uint32_t ecap) {
@@ -709,11 +765,12 @@ __global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t s
   const uint32_t P = blockDim.x, l = threadIdx.x;
   const int64_t j = (int64_t)blockIdx.x * P + l;
   if (j >= D.nphy) return;
-  uint64_t *b = wlds + (size_t)l * (2 * (scap + ecap));
-  PeSlots *pe = reinterpret_cast<PeSlots *>(wlds + (size_t)P * (2 * (scap + ecap))) + l;
-  SplitNi ni{reinterpret_cast<int64_t *>(b + 2 * ecap), reinterpret_cast<int64_t *>(b),
-             reinterpret_cast<double *>(b + 2 * ecap + scap), reinterpret_cast<double *>(b + ecap),
-             scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0};
+  const size_t w = 2 * scap + 3 * ecap;  // words per phy: E times, deltas, running sums; S times, deltas
+  uint64_t *b = wlds + (size_t)l * w;
+  PeSlots *pe = reinterpret_cast<PeSlots *>(wlds + (size_t)P * w) + l;
+  SplitNi ni{reinterpret_cast<int64_t *>(b + 3 * ecap), reinterpret_cast<int64_t *>(b),
+             reinterpret_cast<double *>(b + 3 * ecap + scap), reinterpret_cast<double *>(b + ecap),
+             reinterpret_cast<double *>(b + 2 * ecap), scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0, 0.0, 0};
   phy_run<PRE>(D, j, ni, pe);
 }
 
