@@ -485,7 +485,10 @@ def main():
         try:  # the PMC passes' HBM bytes per launch of the kernel the roofline names (scripts/pmc_traffic.py)
             tj = json.load(open(tpath))
             short = rl["kernel"].split("::")[-1]
-            traffic = tj.get("kernels", {}).get(short, {}).get("hbm_bytes_per_launch")
+            ks = tj.get("kernels", {})
+            # (an entry recorded under the kernel's family name also covers its variants: k_wifi_phy_lds)
+            key = short if short in ks else next((k for k in ks if short.startswith(k)), None)
+            traffic = ks.get(key, {}).get("hbm_bytes_per_launch") if key else None
         except Exception:
             traffic = None
 
