@@ -46,6 +46,25 @@ namespace {
 constexpr uint64_t INF = ~0ull;
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr int PE_CAP = 8;  // pending EndReceive events of one phy: the live one + cancelled ones
+// Diagnostic build only (-DNSGPU_PHASE_PROF, lib/libnsgpu_prof.so): lane 0 of each wave accumulates
+// s_memtime deltas between the per-phy loop's sections (scripts/wifi_phases.py reads them).
+#ifdef NSGPU_PHASE_PROF
+__device__ unsigned long long g_wifi_ph[8];
+#define WPH_T0() uint64_t wph_t = __builtin_amdgcn_s_memtime(); uint64_t wph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define WPH(i)                                              \
+  {                                                         \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();       \
+    wph[i] += t_ - wph_t;                                   \
+    wph_t = t_;                                             \
+  }
+#define WPH_END()                                                                              \
+  if ((threadIdx.x & 63) == 0)                                                                 \
+    for (int q_ = 0; q_ < 8; q_++) atomicAdd(&g_wifi_ph[q_], (unsigned long long)wph[q_]);
+#else
+#define WPH_T0()
+#define WPH(i)
+#define WPH_END()
+#endif
 // (ERR_LDS: a SplitNi queue outgrew its LDS capacity — the run is repeated on the HBM ring store)
 constexpr uint32_t ERR_WINDOW = 1, ERR_NICAP = 2, ERR_TX_IN_TX = 4, ERR_PENDING = 8, ERR_SYNCCAP = 16, ERR_LDS = 32;
 enum Acc { A_DIGEST, A_DISPATCHED, A_RX, A_SYNC, A_DROP_RX, A_DROP_TX, A_DROP_ED, A_CCA_EVAL, A_CCA_SWITCH,
@@ -475,6 +494,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
   uint32_t err = 0;
   nsgpu_wifi_phy_counters c = {};
   uint64_t digest = 0, disp = 0, last_ts = 0, ni_ins = 0, cca_eval = 0, near = 0;
+  WPH_T0();
 
   for (;;) {
     if (!have_c) {  // the next Receive: the smallest arrival of an unconsumed transmission
@@ -561,6 +581,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
       e_sts = e >= 0 ? pe_sts[e] : 0;
       e_dirty = false;
     }
+    WPH(0);  // selection + pending EndReceive choice
     int kind = -1;
     uint64_t now = INF;
     if (ok != NONE) kind = 0, now = ok_ts;
@@ -592,6 +613,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
       ok = oc < oe ? D.own_idx[oc] : NONE;
       ok_ts = ok != NONE ? D.txd[ok].ts : INF;
       last_ts = now;
+      WPH(1);
       continue;
     }
 
@@ -620,6 +642,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
       e_dirty = true;
       disp++;
       last_ts = now;
+      WPH(1);
       continue;
     }
 
@@ -642,6 +665,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
     ni.insert_end(endNew, -rxPowerW);
     ni_ins += 2;
     ni_max = ni.length() > ni_max ? ni.length() : ni_max;
+    WPH(2);  // NiChanges: cursor, fold / insert, end entry
     // the state switch (WifiPhyStateHelper::GetState, wifi-phy-state-helper.cc:159-183)
     const int st = endTx > nw ? 2 : rxing ? 1 : endCca > nw ? 3 : 0;
     uint32_t outcome, flags = 0;
@@ -675,6 +699,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
         maybe = true;
       }
     }
+    WPH(3);  // state decision, sync
     int64_t cca = 0;
     if (maybe) {  // maybeCcaBusy (:482-495): InterferenceHelper::GetEnergyDuration (interference-helper.cc:171-190)
       flags |= NSGPU_WIFI_F_CCA_EVAL;
@@ -687,6 +712,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
       }
       cca_eval++;
     }
+    WPH(4);  // CCA (GetEnergyDuration)
     c.rx++;
     c.drop_rx += outcome == NSGPU_WIFI_DROP_RX;
     c.drop_tx += outcome == NSGPU_WIFI_DROP_TX;
@@ -704,7 +730,9 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
     have_c = false;
     disp++;
     last_ts = now;
+    WPH(5);  // counters, digest, log
   }
+  WPH_END();
   // EndReceive events left pending at the end: scheduled (uid consumed), never dispatched
   for (int q = 0; q < npe; q++) {
     SyncRec r;
@@ -1229,6 +1257,18 @@ extern "C" int nsgpu_wifi_run(nsgpu_wifi *h, void *stream) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_wifi_run: null");
   return wifi_launch(h, (hipStream_t)stream, nullptr);
 }
+
+#ifdef NSGPU_PHASE_PROF
+extern "C" int nsgpu_wifi_phase_read(unsigned long long *out, int reset) {  // (diagnostic build only)
+  NSGPU_HIP(hipDeviceSynchronize());
+  NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wifi_ph), sizeof(unsigned long long) * 8));
+  if (reset) {
+    unsigned long long z[8] = {};
+    NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wifi_ph), z, sizeof(z)));
+  }
+  return NSGPU_OK;
+}
+#endif
 
 extern "C" int nsgpu_wifi_kernel_count(int *n) {
   *n = WIFI_NK;
