@@ -49,8 +49,8 @@ constexpr int PE_CAP = 8;  // pending EndReceive events of one phy: the live one
 // Diagnostic build only (-DNSGPU_PHASE_PROF, lib/libnsgpu_prof.so): lane 0 of each wave accumulates
 // s_memtime deltas between the per-phy loop's sections (scripts/wifi_phases.py reads them).
 #ifdef NSGPU_PHASE_PROF
-__device__ unsigned long long g_wifi_ph[8];
-#define WPH_T0() uint64_t wph_t = __builtin_amdgcn_s_memtime(); uint64_t wph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+__device__ unsigned long long g_wifi_ph[16];
+#define WPH_T0() uint64_t wph_t = __builtin_amdgcn_s_memtime(); uint64_t wph[10] = {};
 #define WPH(i)                                              \
   {                                                         \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();       \
@@ -58,8 +58,15 @@ __device__ unsigned long long g_wifi_ph[8];
     wph_t = t_;                                             \
   }
 #define WPH_END()                                                                              \
-  if ((threadIdx.x & 63) == 0)                                                                 \
-    for (int q_ = 0; q_ < 8; q_++) atomicAdd(&g_wifi_ph[q_], (unsigned long long)wph[q_]);
+  if ((threadIdx.x & 63) == 0) {                                                               \
+    uint64_t w_ = 0;                                                                           \
+    for (int q_ = 0; q_ < 10; q_++) {                                                          \
+      atomicAdd(&g_wifi_ph[q_], (unsigned long long)wph[q_]);                                  \
+      w_ += wph[q_];                                                                           \
+    }                                                                                          \
+    atomicMax(&g_wifi_ph[14], (unsigned long long)w_); /* the slowest wave */                  \
+    atomicAdd(&g_wifi_ph[15], 1ull);                   /* waves */                             \
+  }
 #else
 #define WPH_T0()
 #define WPH(i)
@@ -268,6 +275,29 @@ struct SplitNi {
   double cur_s;
   double cb;         // the running sum before E's head
   uint32_t nsum;     // terms summed into ec since its last rebase
+  // the queues' heads in registers (INT64_MAX: empty), so that a cursor step is one LDS trip (the next
+  // head's loads, issued together) instead of three dependent ones
+  int64_t hte, hts;
+  double hde, hce, hds;
+  __device__ __forceinline__ void reload_e() {
+    if (ne) {
+      const uint32_t x = ex(0);
+      hte = et[x];
+      hde = ed[x];
+      hce = ec[x];
+    } else {
+      hte = INT64_MAX;
+    }
+  }
+  __device__ __forceinline__ void reload_s() {
+    if (ns) {
+      const uint32_t x = sx(0);
+      hts = st[x];
+      hds = sd[x];
+    } else {
+      hts = INT64_MAX;
+    }
+  }
   __device__ __forceinline__ uint32_t sx(uint32_t i) const {
     const uint32_t x = hs + i;
     return x < scap ? x : x - scap;
@@ -283,19 +313,20 @@ struct SplitNi {
   template <bool LE>
   __device__ __forceinline__ void advance(int64_t lim) {
     for (;;) {
-      const int64_t te = ne ? et[ex(0)] : INT64_MAX, ts = ns ? st[sx(0)] : INT64_MAX;
-      const bool e = te <= ts;  // E first on equal times
-      const int64_t t = e ? te : ts;
+      const bool e = hte <= hts;  // E first on equal times
+      const int64_t t = e ? hte : hts;
       if (t == INT64_MAX || (LE ? t > lim : t >= lim)) return;
       if (e) {
-        cur_s += ed[ex(0)];
-        cb = ec[ex(0)];
+        cur_s += hde;
+        cb = hce;
         he = he + 1 == ecap ? 0 : he + 1;
         ne--;
+        reload_e();
       } else {
-        cur_s += sd[sx(0)];
+        cur_s += hds;
         hs = hs + 1 == scap ? 0 : hs + 1;
         ns--;
+        reload_s();
       }
       ndead++;
     }
@@ -307,11 +338,14 @@ struct SplitNi {
     st[sx(0)] = nw;
     sd[sx(0)] = p;
     ns = 1;
+    hts = nw;
+    hds = p;
     return cur_s;
   }
   __device__ __forceinline__ void insert_start(int64_t nw, double p) {
     st[sx(ns)] = nw;
     sd[sx(ns)] = p;
+    if (ns == 0) hts = nw, hds = p;
     ns++;
   }
   __device__ __forceinline__ void insert_end(int64_t t, double d) {  // upper_bound (t) from the back
@@ -330,6 +364,7 @@ struct SplitNi {
     for (uint32_t i = q; i < ne; i++) {
       c += ed[ex(i)];
       ec[ex(i)] = c;
+      if (i == 0) hte = t, hde = d, hce = c;  // (a new head)
     }
     nsum += ne - q;
     // rebase before the sums grow far past the live part (their rounding error is relative to them)
@@ -339,6 +374,7 @@ struct SplitNi {
       for (uint32_t i = 0; i < ne; i++) {
         c += ed[ex(i)];
         ec[ex(i)] = c;
+        if (i == 0) hce = c;
       }
       nsum = ne;
     }
@@ -651,7 +687,9 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
     const double rxPowerW = PRE ? c_w : rx_power_w(D, c_dbm, c_dist);
     const int64_t endNew = nw + c_dur;
     // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
+    WPH(6);  // (kind decision, Receive operands)
     ni.on_receive(nw);
+    WPH(7);  // the eager cursor
     if (!ni.room()) {
       err |= ERR_NICAP;
       break;
@@ -662,6 +700,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
     }
     if (!rxing) firstPower = ni.fold_start(nw, rxPowerW);  // fold up to upper_bound (now) into m_firstPower
     else ni.insert_start(nw, rxPowerW);
+    WPH(8);  // fold / start entry
     ni.insert_end(endNew, -rxPowerW);
     ni_ins += 2;
     ni_max = ni.length() > ni_max ? ni.length() : ni_max;
@@ -798,7 +837,8 @@ __global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t s
   PeSlots *pe = reinterpret_cast<PeSlots *>(wlds + (size_t)P * w) + l;
   SplitNi ni{reinterpret_cast<int64_t *>(b + 3 * ecap), reinterpret_cast<int64_t *>(b),
              reinterpret_cast<double *>(b + 3 * ecap + scap), reinterpret_cast<double *>(b + ecap),
-             reinterpret_cast<double *>(b + 2 * ecap), scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0, 0.0, 0};
+             reinterpret_cast<double *>(b + 2 * ecap), scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0, 0.0, 0,
+             INT64_MAX, INT64_MAX, 0.0, 0.0, 0.0};
   phy_run<PRE>(D, j, ni, pe);
 }
 
@@ -1261,9 +1301,9 @@ extern "C" int nsgpu_wifi_run(nsgpu_wifi *h, void *stream) {
 #ifdef NSGPU_PHASE_PROF
 extern "C" int nsgpu_wifi_phase_read(unsigned long long *out, int reset) {  // (diagnostic build only)
   NSGPU_HIP(hipDeviceSynchronize());
-  NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wifi_ph), sizeof(unsigned long long) * 8));
+  NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wifi_ph), sizeof(unsigned long long) * 16));
   if (reset) {
-    unsigned long long z[8] = {};
+    unsigned long long z[16] = {};
     NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wifi_ph), z, sizeof(z)));
   }
   return NSGPU_OK;
