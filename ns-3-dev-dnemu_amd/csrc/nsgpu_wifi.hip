@@ -279,6 +279,8 @@ struct SplitNi {
   // head's loads, issued together) instead of three dependent ones
   int64_t hte, hts;
   double hde, hce, hds;
+  int64_t tte;  // E's tail: its time and running sum (valid while ne > 0): an append reads no LDS
+  double tce;
   __device__ __forceinline__ void reload_e() {
     if (ne) {
       const uint32_t x = ex(0);
@@ -350,22 +352,35 @@ struct SplitNi {
   }
   __device__ __forceinline__ void insert_end(int64_t t, double d) {  // upper_bound (t) from the back
     uint32_t q = ne;
-    while (q > 0) {
-      const int64_t x = et[ex(q - 1)];
-      if (x <= t) break;
-      et[ex(q)] = x;
-      ed[ex(q)] = ed[ex(q - 1)];
-      q--;
+    double c;
+    if (ne == 0 || tte <= t) {  // an append (ends usually come in time order: equal durations)
+      const uint32_t x = ex(ne);
+      et[x] = t;
+      ed[x] = d;
+      c = (ne ? tce : cb) + d;
+      ec[x] = c;
+      if (ne == 0) hte = t, hde = d, hce = c;
+      ne++;
+      tte = t;
+    } else {
+      while (q > 0) {
+        const int64_t x = et[ex(q - 1)];
+        if (x <= t) break;
+        et[ex(q)] = x;
+        ed[ex(q)] = ed[ex(q - 1)];
+        q--;
+      }
+      et[ex(q)] = t;
+      ed[ex(q)] = d;
+      ne++;
+      c = q ? ec[ex(q - 1)] : cb;  // the running sums from the new entry on (the old tail stays last)
+      for (uint32_t i = q; i < ne; i++) {
+        c += ed[ex(i)];
+        ec[ex(i)] = c;
+        if (i == 0) hte = t, hde = d, hce = c;  // (a new head)
+      }
     }
-    et[ex(q)] = t;
-    ed[ex(q)] = d;
-    ne++;
-    double c = q ? ec[ex(q - 1)] : cb;  // the running sums from the new entry on (usually just its own)
-    for (uint32_t i = q; i < ne; i++) {
-      c += ed[ex(i)];
-      ec[ex(i)] = c;
-      if (i == 0) hte = t, hde = d, hce = c;  // (a new head)
-    }
+    tce = c;
     nsum += ne - q;
     // rebase before the sums grow far past the live part (their rounding error is relative to them)
     if (nsum > 4096 || fabs(c) > 16.0 * fabs(c - cb)) {
@@ -376,6 +391,7 @@ struct SplitNi {
         ec[ex(i)] = c;
         if (i == 0) hce = c;
       }
+      tce = c;
       nsum = ne;
     }
   }
@@ -389,7 +405,7 @@ struct SplitNi {
   __device__ __forceinline__ bool tail_bisect(uint32_t ie, double noise, double ccaW, int64_t &end,
                                               uint32_t &flags) const {
     const double base = ie ? ec[ex(ie - 1)] : cb;
-    const double last = ec[ex(ne - 1)];
+    const double last = tce;  // (ec of E's tail)
     const double dl = 1e-10 * (noise + fabs(base) + fabs(last));
     uint32_t lo = ie, hi = ne;  // the first i with a_i < ccaW - dl (ne: none)
     while (lo < hi) {
@@ -426,11 +442,11 @@ struct SplitNi {
       stop = noise < ccaW;
     };
     uint32_t ie = 0;
-    while (!stop && ie < ne && et[ex(ie)] == nw) {
-      step(nw, ed[ex(ie)]);
+    while (!stop && ie < ne && (ie ? et[ex(ie)] : hte) == nw) {  // (the heads are in registers)
+      step(nw, ie ? ed[ex(ie)] : hde);
       ie++;
     }
-    for (uint32_t q = 0; !stop && q < ns; q++) step(st[sx(q)], sd[sx(q)]);
+    for (uint32_t q = 0; !stop && q < ns; q++) step(q ? st[sx(q)] : hts, q ? sd[sx(q)] : hds);
     if (stop || ie >= ne) return end;
     if (tail_bisect(ie, noise, ccaW, end, flags)) return end;
     // The tail (undecided by the bisection): end entries after now, all deltas negative, so the sums only fall (round-to-nearest is
@@ -838,7 +854,7 @@ __global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t s
   SplitNi ni{reinterpret_cast<int64_t *>(b + 3 * ecap), reinterpret_cast<int64_t *>(b),
              reinterpret_cast<double *>(b + 3 * ecap + scap), reinterpret_cast<double *>(b + ecap),
              reinterpret_cast<double *>(b + 2 * ecap), scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0, 0.0, 0,
-             INT64_MAX, INT64_MAX, 0.0, 0.0, 0.0};
+             INT64_MAX, INT64_MAX, 0.0, 0.0, 0.0, INT64_MIN, 0.0};
   phy_run<PRE>(D, j, ni, pe);
 }
 
