@@ -623,6 +623,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
       while (done & 1ull) done >>= 1, p++;
       have_c = true;
     }
+    WPH(9);  // the scan for the next Receive (selection: the rest)
     if (e_dirty) {  // the first pending EndReceive (ts, then the syncing Receive's key), after a change
       e = -1;
       for (int q = 0; q < npe; q++)

@@ -21,8 +21,8 @@ nsgpu.check(f(buf, 1))
 eng.run()
 st = eng.stats()
 nsgpu.check(f(buf, 0))
-names = ["selection", "SendPacket/EndReceive", "NiChanges: end entry, running sums", "state/sync", "CCA",
-         "counters/digest", "kind decision, operands", "NiChanges: eager cursor", "NiChanges: fold / start"]
+names = ["pending EndReceive choice", "SendPacket/EndReceive", "NiChanges: end entry, running sums", "state/sync", "CCA",
+         "counters/digest", "kind decision, operands", "NiChanges: eager cursor", "NiChanges: fold / start", "scan for the next Receive"]
 tot = sum(buf[:10])
 print(f"dispatched {st.dispatched}, store {eng.store()}")
 for i, n in enumerate(names):
