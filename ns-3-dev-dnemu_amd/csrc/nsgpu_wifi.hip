@@ -129,6 +129,7 @@ struct WifiDev {
   uint32_t *hist, *off, *cur, *bucket, *base;
   nsgpu_wifi_end_record *ends;
   struct RxPre *pre;  // nullable: [nphy][ktx] receptions computed up front (k_wifi_rx)
+  const struct TsDur *tsdur;  // [ktx] (ts, dur) of every transmission, packed for the per-phy scan
 };
 
 // One (receiver, transmission) pair computed up front by k_wifi_rx: the Receive's arrival and its
@@ -562,7 +563,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
           for (int u = 0; u < 2; u++) {
             const uint32_t k = p + i0 + u;
             if (k < D.ktx) {
-              tp[u] = *reinterpret_cast<const TsDur *>(&D.txd[k].ts);
+              tp[u] = D.tsdur[k];
               rp[u] = row[k];
             } else {
               tp[u].ts = INF;
@@ -1196,6 +1197,9 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
     for (int64_t k = 0; k < K; k++)
       txd[k] = TxDesc{tx_x[k], tx_y[k], tx_z[k], sc->tx_dbm[k], sc->tx_ts[k], tx_dur[k], sc->tx_phy[k], tx_chan[k], {0, 0}};
     TRY(dalloc(h, (TxDesc **)&D.txd, K, txd.data()));
+    std::vector<TsDur> td((size_t)std::max<int64_t>(K, 1));  // (ts, dur) alone: 8 transmissions a line
+    for (int64_t k = 0; k < K; k++) td[k] = TsDur{sc->tx_ts[k], tx_dur[k]};
+    TRY(dalloc(h, (TsDur **)&D.tsdur, K, td.data()));
   }
   TRY(dalloc(h, (uint64_t **)&D.fcum, fcum.size(), fcum.data()));
   TRY(dalloc(h, (uint32_t **)&D.own_off, own_off.size(), own_off.data()));
