@@ -242,15 +242,15 @@ class P2PGridDist:
         self.engine.launch()
 
     def roofline(self, step_kernel_ms, events_per_step):
-        # the partitioned window is 6 kernels + 3 collectives: the roofline unit is one window
+        # the partitioned window is 4 kernels + 3 collectives: the roofline unit is one window
         # (per rank: its share of the events) against the window's device time on this rank
         st, _, _, _ = self.engine.results()
         windows = max(int(st.windows), 1)
         return {"kernel": self.kernel, "kernel_ms": step_kernel_ms / windows,
                 "events_per_launch": events_per_step / self.world / windows,
                 "step_device_ms": step_kernel_ms, "windows_per_step": windows,
-                "launch_unit": "one partitioned window on one rank (k_pa, k_refit_d, X0, k_cut, "
-                               "k_handle_rank, X1, k_gtile, k_dfin, X2)"}
+                "launch_unit": "one partitioned window on one rank (k2_pa<true>, X0, k2_handle, X1, k_gtile, "
+                               "k_dfin2, X2)"}
 
     def result(self):
         st, devc, appc, _ = self.engine.results()
