@@ -147,7 +147,7 @@ struct P2PDev {
   uint32_t *ev_uid[2], *ev_ctx[2], *ev_kind[2], *ev_a[2];
   Pkt *ev_pkt[2];
   uint64_t pool_cap;
-  // the current window (WCAP slots): slot records (k_pa) ...
+  // the current window (WCAP slots): slot records (k2_pa) ...
   uint64_t *wkey;
   uint32_t *wctx, *wkind, *wa, *widx;
   Pkt *wpkt;
@@ -156,7 +156,7 @@ struct P2PDev {
   uint64_t *ch_ts;
   uint32_t *ch_ctx, *ch_kind, *ch_a;
   Pkt *ch_pkt;
-  // ... dispatch info per slot (k_scan), and the keys / contexts k_scan keeps for the next k_pa
+  // ... dispatch info per slot (k2_scan / k_dfin2), and the keys / contexts kept for the next k2_pa
   // (which rewrites wkey / wctx with the next window while it appends this one)
   uint4 *sinfo;
   uint64_t *pwkey;
@@ -1847,7 +1847,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   Ctl &C0 = h->C0;
   memset(&C0, 0, sizeof(C0));
   C0.uid = uid;
-  // reduction of the initial pool: window 0 is bounded by red[1] (k_pa / k_handle_rank fold later
+  // reduction of the initial pool: window 0 is bounded by red[1] (k2_pa / k2_handle fold later
   // pending sets in for the next windows)
   C0.red[0].tmin = C0.red[0].wend = C0.red[0].stopts = ~0ull;
   C0.red[0].stopuid = 0;
