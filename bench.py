@@ -78,6 +78,9 @@ class Churn:
     def step(self):
         self.run.launch()
 
+    def close(self):
+        pass
+
     def roofline(self, step_kernel_ms, events_per_step):
         # one persistent launch per step: the step's device time is the kernel's
         return {"kernel": self.kernel, "kernel_ms": step_kernel_ms, "events_per_launch": events_per_step}
@@ -151,6 +154,9 @@ class P2PGrid:
     def step(self):
         self.engine.reset()
         self.engine.launch()
+
+    def close(self):
+        self.engine.close()
 
     def roofline(self, step_kernel_ms, events_per_step):
         # the window pipeline is 3 kernels per window; a separate eager run launches each kernel of
@@ -364,6 +370,9 @@ class WifiGrid:
     def step(self):
         self.engine.launch()
 
+    def close(self):
+        self.engine.close()
+
     def roofline(self, step_kernel_ms, events_per_step):
         prof = self.engine.profile()
         store, per_block, ecap = self.engine.store()
@@ -419,6 +428,9 @@ def main():
     ap.add_argument("--wifi-side", type=int, default=100, help="wifi-grid: phys per grid side")
     ap.add_argument("--wifi-stop", type=float, default=2.0, help="wifi-grid: Simulator::Stop (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="p2p-grid: skip the wifi-grid / dumbbell entries of the `secondary` list")
+    ap.add_argument("--secondary-steps", type=int, default=3, help="timed steps of each secondary workload")
     ap.add_argument("--partitioned", action="store_true",
                     help="p2p-grid through the partitioned engine even on one rank (RCCL with one rank)")
     args = ap.parse_args()
@@ -445,27 +457,57 @@ def main():
         wl = WORKLOADS[args.workload](args, stream.handle)
     timer = nsgpu.Timer()
 
-    for _ in range(args.warmup):
-        wl.step()
-    stream.sync()
-
     def barrier():
         nsgpu.device_synchronize()
         if tdist is not None:
             tdist.barrier()
         nsgpu.device_synchronize()
 
-    barrier()
-    stream.sync()
-    t0 = time.perf_counter()
-    timer.start(stream.handle)
-    for _ in range(args.steps):
-        wl.step()
-    timer.stop(stream.handle)
-    stream.sync()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = timer.elapsed_ms() / args.steps  # device time of one step on this rank's stream
+    def measure(wl, steps, warmup):
+        """W untimed steps, then K timed steps bracketed by barrier + device sync; returns (elapsed s of
+        this rank, device ms per step on the stream)."""
+        for _ in range(warmup):
+            wl.step()
+        stream.sync()
+        barrier()
+        stream.sync()
+        t0 = time.perf_counter()
+        timer.start(stream.handle)
+        for _ in range(steps):
+            wl.step()
+        timer.stop(stream.handle)
+        stream.sync()
+        barrier()
+        return time.perf_counter() - t0, timer.elapsed_ms() / steps
+
+    def roofline_of(wl, name, kernel_ms, events_per_step):
+        # dominant kernel: name, events one launch processes, average launch duration (HIP events)
+        rl = wl.roofline(kernel_ms, events_per_step)
+        achieved = wl.bytes_per_event * rl["events_per_launch"] / (rl["kernel_ms"] / 1e3) / 1e9
+        traffic = None
+        tpath = os.path.join(REPO, "profiles", f"traffic_{name}.json")
+        if os.path.exists(tpath):
+            try:  # the PMC passes' HBM bytes per launch of the kernel the roofline names (scripts/pmc_traffic.py)
+                tj = json.load(open(tpath))
+                short = rl["kernel"].split("::")[-1]
+                ks = tj.get("kernels", {})
+                # (an entry recorded under the kernel's family name also covers its variants: k_wifi_phy_lds)
+                key = short if short in ks else next((k for k in ks if short.startswith(k)), None)
+                traffic = ks.get(key, {}).get("hbm_bytes_per_launch") if key else None
+            except Exception:
+                traffic = None
+        return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "bytes_per_event": wl.bytes_per_event, **rl}
+
+    def cpu_baseline_of(wl, value, digest):
+        cv, cdigest, sample = wl.cpu_baseline()
+        cb = {"value": cv, "unit": "events/s", "cores": 1, "kind": "port", "sample": sample,
+              "cpu_model": cpu_model(), "digest_match": bool(getattr(wl, "_sample_match", cdigest == digest))}
+        if getattr(wl, "schedulers", None):
+            cb["schedulers"] = wl.schedulers
+        return cb, value / cv
+
+    elapsed, kernel_ms = measure(wl, args.steps, args.warmup)
     events_per_step, digest, extra = wl.result()
 
     if tdist is not None:
@@ -476,21 +518,7 @@ def main():
 
     # a partitioned run is ONE simulation: its (global) events once; replicas (churn) add up
     value = events_per_step * args.steps * (1 if partitioned else world) / elapsed
-    # dominant kernel: name, events one launch processes, average launch duration (HIP events)
-    rl = wl.roofline(kernel_ms, events_per_step)
-    achieved = wl.bytes_per_event * rl["events_per_launch"] / (rl["kernel_ms"] / 1e3) / 1e9
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", f"traffic_{args.workload}.json")
-    if os.path.exists(tpath):
-        try:  # the PMC passes' HBM bytes per launch of the kernel the roofline names (scripts/pmc_traffic.py)
-            tj = json.load(open(tpath))
-            short = rl["kernel"].split("::")[-1]
-            ks = tj.get("kernels", {})
-            # (an entry recorded under the kernel's family name also covers its variants: k_wifi_phy_lds)
-            key = short if short in ks else next((k for k in ks if short.startswith(k)), None)
-            traffic = ks.get(key, {}).get("hbm_bytes_per_launch") if key else None
-        except Exception:
-            traffic = None
+    roofline = roofline_of(wl, args.workload, kernel_ms, events_per_step)
 
     if rank == 0:
         out = {
@@ -509,25 +537,31 @@ def main():
             "config": dict({"workload": wl.workload, "events_per_step": events_per_step,
                             "parallelism": (f"partitioned x{world} (RCCL)" if partitioned else
                                             "replicas" if world > 1 else "single")}, **extra),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": traffic,
-                "bytes_per_event": wl.bytes_per_event,
-                **rl,
-            },
+            "roofline": roofline,
         }
         if not args.no_cpu_baseline and world == 1 and not partitioned:
-            cv, cdigest, sample = wl.cpu_baseline()
-            out["cpu_baseline"] = {"value": cv, "unit": "events/s", "cores": 1, "kind": "port", "sample": sample,
-                                   "cpu_model": cpu_model(),
-                                   "digest_match": bool(getattr(wl, "_sample_match", cdigest == digest))}
-            if getattr(wl, "schedulers", None):
-                out["cpu_baseline"]["schedulers"] = wl.schedulers
-            out["speedup_vs_cpu"] = value / cv
+            out["cpu_baseline"], out["speedup_vs_cpu"] = cpu_baseline_of(wl, value, digest)
+        # the north star's other GPU targets (configs 3 and 5) in the same line, on the same box: each a
+        # whole run per step, digest-checked against the oracle like the primary
+        secondary = []
+        if world == 1 and not partitioned and args.workload == "p2p-grid" and not args.no_secondary:
+            for name in ("wifi-grid", "dumbbell"):
+                wl2 = WORKLOADS[name](args, stream.handle)
+                el2, kms2 = measure(wl2, args.secondary_steps, 1)
+                ev2, dg2, ex2 = wl2.result()
+                v2 = ev2 * args.secondary_steps / el2
+                ent = {"workload": wl2.workload, "config": name, "value": v2, "unit": "events/s",
+                       "events_per_step": ev2, "steps": args.secondary_steps, "warmup": 1,
+                       "ms_per_step": el2 * 1e3 / args.secondary_steps, "extra": ex2,
+                       "roofline": roofline_of(wl2, name, kms2, ev2)}
+                if not args.no_cpu_baseline:
+                    ent["cpu_baseline"], ent["speedup_vs_cpu"] = cpu_baseline_of(wl2, v2, dg2)
+                    ent["digest_match"] = ent["cpu_baseline"]["digest_match"]
+                secondary.append(ent)
+                wl2.close()
+                del wl2
+        if secondary:
+            out["secondary"] = secondary
         print(json.dumps(out), flush=True)
 
     if tdist is not None:

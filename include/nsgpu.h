@@ -202,6 +202,8 @@ int nsgpu_sched_size(nsgpu_sched *s, uint64_t *n);
 int nsgpu_sched_peek_next(nsgpu_sched *s, nsgpu_event *out);
 int nsgpu_sched_remove_next(nsgpu_sched *s, nsgpu_event *out);
 int nsgpu_sched_remove(nsgpu_sched *s, const nsgpu_event *ev);
+/* front machinery statistics: refills so far, current front size, running refill wall-time estimate */
+int nsgpu_sched_stats(nsgpu_sched *s, uint64_t *refills, uint64_t *front, double *refill_us);
 
 /* ---------------- HipSimulatorImpl host runtime (host closures) ----------------
  * Replaces DefaultSimulatorImpl's run loop (default-simulator-impl.cc:117-165) for events whose
@@ -234,20 +236,36 @@ int nsgpu_sim_stop_at(nsgpu_sim *s, int64_t delay);
 int nsgpu_sim_destroy(nsgpu_sim *s);
 int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *dispatched, uint32_t *next_uid);
 int nsgpu_sim_current_uid(nsgpu_sim *s, uint32_t *uid);
-int nsgpu_sim_next(nsgpu_sim *s, uint64_t *ts, int *empty);          /* Next () / IsFinished () */
+int nsgpu_sim_next(nsgpu_sim *s, uint64_t *ts, int *empty);          /* Next (): host and device events */
+int nsgpu_sim_is_finished(nsgpu_sim *s, int *finished);              /* IsFinished (): empty || stopped */
 int nsgpu_sim_set_stop(nsgpu_sim *s, int stop);                      /* Stop (); Run clears it */
+int nsgpu_sim_run_one(nsgpu_sim *s);                                 /* RunOneEvent () (callbacks) */
+int nsgpu_sim_live_closures(nsgpu_sim *s, uint64_t *n);              /* callback closures still held */
 int nsgpu_sim_drain(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n);  /* DoDispose */
 /* windows: *n = 0 when nothing is left to dispatch or a Stop was dispatched */
 int nsgpu_sim_pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n);
 /* window event *e is dispatched next: *skip = 0 run it (Now/Context/uid set, dispatch counted), 1 a
  * closure of this window removed it, 2 a Stop was dispatched before it (it stays pending) */
 int nsgpu_sim_begin(nsgpu_sim *s, const nsgpu_event *e, int *skip);
+/* RunOneEvent (default-simulator-impl.cc:167-170): the next event as a one-event window, whatever
+ * the stop flag says (*n = 0: nothing pending) */
+int nsgpu_sim_pop_one(nsgpu_sim *s, nsgpu_event *out, uint32_t *n);
 /* raw handles: handle must be even (an object pointer); *uid = the uid it got (ScheduleWithContext
  * order); remove_key: Scheduler::Remove of a pending event; key_expired: IsExpired's time rule */
 int nsgpu_sim_insert(nsgpu_sim *s, uint64_t ts, uint32_t ctx, uint64_t handle, uint32_t *uid);
 int nsgpu_sim_consume_uid(nsgpu_sim *s, uint32_t *uid);
 int nsgpu_sim_remove_key(nsgpu_sim *s, uint64_t ts, uint32_t uid, uint32_t ctx, uint64_t handle);
 int nsgpu_sim_key_expired(nsgpu_sim *s, uint64_t ts, uint32_t uid, int *expired);
+/* the destroy list of raw handles (DefaultSimulatorImpl::m_destroyEvents, default-simulator-impl.cc
+ * :79-92,235-242,256-268,306-322), kept by the runtime; the caller keeps the reference each entry
+ * holds.  insert = ScheduleDestroy (consumes a uid; *ts = Now, the EventId's ts); pop = Destroy's
+ * front + pop_front (*found = 0: the list is empty — call it until then, since a destroy closure may
+ * schedule or remove destroy events); remove = Remove of a uid-2 EventId; pending = IsExpired's list
+ * lookup. */
+int nsgpu_sim_destroy_insert(nsgpu_sim *s, uint64_t handle, uint64_t *ts);
+int nsgpu_sim_destroy_pop(nsgpu_sim *s, uint64_t *handle, int *found);
+int nsgpu_sim_destroy_remove(nsgpu_sim *s, uint64_t handle, uint64_t ts, int *found);
+int nsgpu_sim_destroy_pending(nsgpu_sim *s, uint64_t handle, uint64_t ts, int *pending);
 /* dispatch accounting of the host events (the engine accounts for the device ones): count, cancelled
  * ones, digest (sum of nsgpu_dispatch_digest_term over their global ranks); optional log at global ranks */
 int nsgpu_sim_host_stats(nsgpu_sim *s, uint64_t *host_dispatched, uint64_t *cancelled, uint64_t *digest);
@@ -315,6 +333,9 @@ int nsgpu_p2p_advance(nsgpu_p2p *h, uint64_t hts, uint32_t huid, uint32_t *uid, 
 int nsgpu_p2p_inject_send(nsgpu_p2p *h, uint32_t app, uint64_t now, uint32_t cur_uid, uint32_t cur_ctx,
                           uint32_t *uid, uint32_t *trace_seq, void *stream);
 int nsgpu_p2p_counters(nsgpu_p2p *h, nsgpu_dev_counters *devc, nsgpu_app_counters *appc, void *stream);
+/* the engine's pending device events between advances: count, smallest timestamp (UINT64_MAX: none),
+ * and whether a device-dispatched Simulator::Stop ended its run */
+int nsgpu_p2p_pending(nsgpu_p2p *h, uint64_t *n, uint64_t *next_ts, int *stopped, void *stream);
 /* Diagnostic: in-kernel phase timers (s_memrealtime ticks, 100 MHz) of the pipeline kernels; only the
  * lib/libnsgpu_prof.so build (-DNSGPU_PHASE_PROF) records them, the product library returns ESTATE. */
 int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset);

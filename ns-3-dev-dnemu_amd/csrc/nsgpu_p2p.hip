@@ -112,6 +112,7 @@ struct Ctl {
                                    // the window is cut at the next host event (pause after it)
   uint64_t hts, hrel;              // next host event (nsgpu_p2p_advance): ts (~0: none); the rel ts of the
   uint32_t huid, pad4;             //   window's last timestamp (W_end or the host event's); the host uid
+  uint64_t pchild;                 // children of the last scanned window that stay pending (not inline)
 };
 
 static_assert(offsetof(Ctl, prep) == offsetof(Ctl, W) + 12 && offsetof(Ctl, W) % 16 == 0, "the X0 payload");
@@ -2088,6 +2089,12 @@ static int build_graph(nsgpu_p2p *h) {
   return NSGPU_OK;
 }
 
+// A run that set the engine's error word: capacity exceeded (the simulation is truncated).
+static int engine_error(uint32_t err) {
+  return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, 4 = window limit, "
+                                 "8 = window cut, 16 = a window's remote events beyond the X2 capacity)", err);
+}
+
 // Replays the single engine's window pipeline until the run is over (done >= 2) or the pipeline paused
 // for a host closure (*paused).  Two replays in flight: replay i+1 is queued before the run control
 // after replay i is examined; a pipeline that paused itself (host-driven sort or compaction, a host
@@ -2206,13 +2213,38 @@ extern "C" int nsgpu_p2p_advance(nsgpu_p2p *h, uint64_t hts, uint32_t huid, uint
   bool paused = false;
   const int rc = drive(h, &paused);
   if (rc) return rc;
+  uint32_t err = 0;
   NSGPU_HIP(hipMemcpyAsync(&h->snap[0], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipMemcpyAsync(&err, h->M.error, 4, hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipStreamSynchronize(h->s));
+  if (err) return engine_error(err);
   *uid = h->snap[0].uid;
   *dispatched = h->snap[0].K;
   *ended = paused ? 0 : 1;
   NSGPU_HIP(hipEventRecord(h->ev[0], h->s));
   NSGPU_HIP(hipStreamWaitEvent(cs, h->ev[0], 0));
+  return NSGPU_OK;
+}
+
+// The attached engine's pending device events (Next / IsFinished of the runtime): how many, the
+// smallest timestamp among them, and whether a device-dispatched Simulator::Stop ended the run.
+extern "C" int nsgpu_p2p_pending(nsgpu_p2p *h, uint64_t *n, uint64_t *next_ts, int *stopped, void *stream) {
+  if (!h || !n || !next_ts || !stopped) return set_error(NSGPU_EINVAL, "nsgpu_p2p_pending: null");
+  if (h->M.dist) return set_error(NSGPU_ESTATE, "nsgpu_p2p_pending: single-device engines only");
+  hipStream_t cs = (hipStream_t)stream;
+  NSGPU_HIP(hipEventRecord(h->ev[0], cs));
+  NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev[0], 0));
+  NSGPU_HIP(hipMemcpyAsync(&h->snap[0], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  const Ctl &c = h->snap[0];
+  *stopped = c.stop_seen ? 1 : 0;
+  if (c.done >= 1) {  // (1: the final window is dispatched, its children are not queued)
+    *n = 0;
+    *next_ts = ~0ull;
+    return NSGPU_OK;
+  }
+  *n = c.live + (c.pvalid ? c.pchild : 0) + (c.mode == MODE_RUN ? c.rW - c.r0 : 0);
+  *next_ts = c.red[0].tmin < c.red[1].tmin ? c.red[0].tmin : c.red[1].tmin;
   return NSGPU_OK;
 }
 
@@ -2279,8 +2311,12 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
     if (paused) return set_error(NSGPU_ESTATE, "nsgpu_p2p_run: paused for a host closure (use nsgpu_p2p_advance)");
   }
   NSGPU_HIP(hipEventRecord(h->t1, h->s));
+  uint32_t err = 0;
+  NSGPU_HIP(hipMemcpyAsync(&err, h->M.error, 4, hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipEventSynchronize(h->t1));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
   NSGPU_HIP(hipEventElapsedTime(&h->last_ms, h->t0, h->t1));
+  if (err) return engine_error(err);
   NSGPU_HIP(hipEventRecord(h->ev[0], h->s));
   NSGPU_HIP(hipStreamWaitEvent(cs, h->ev[0], 0));
   return NSGPU_OK;
@@ -2479,8 +2515,7 @@ extern "C" int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev
     stats->refits = c.refits;
   }
   if (error) *error = err;
-  if (err) return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, "
-                                          "4 = window limit, 8 = window cut, 16 = a window's remote events beyond the X2 capacity)", err);
+  if (err) return engine_error(err);
   return NSGPU_OK;
 }
 

@@ -1413,6 +1413,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     if (W) C.last_ts = bk.tmin + l_rel[W - 1];
     C.K = bk.K + W + tinl;
     C.uid = bk.uid + tc;
+    C.pchild = tc - tinl;
     C.nfree = nfree - consumed + npush;
     const uint64_t P_end = bk.P_end + (nF > nfree ? nF - nfree : 0);
     const uint64_t live = bk.live - npush + nF;

@@ -5,7 +5,10 @@
 // Contract (the reference semantics it keeps — default-simulator-impl.cc:49-353 — are listed so the
 // parity tests can cite them): uids from 4, ScheduleDestroy consumes one (:235-242); Now / Context / uid
 // are set before a closure runs (:117-131); a cancelled event is still dequeued and counted
-// (event-impl.cc:34-41); IsExpired's rule (:304-332); Stop / Stop (Time) (:167-183).
+// (event-impl.cc:34-41); IsExpired's rule (:304-332); Stop / Stop (Time) (:167-183); IsFinished is
+// "queue empty or stopped" (:133-137) and RunOneEvent dispatches one event whatever the stop flag says
+// (:167-170); Destroy pops the destroy list from the front until it is empty, so a destroy event
+// scheduled or removed by a destroy closure is honoured (:79-92, :256-268).
 //
 // Windows (nsgpu_sim_pop_window): with host closures only, a window is every pending event of the
 // smallest timestamp — an event a closure schedules has a larger uid, so it sorts after the whole
@@ -13,18 +16,27 @@
 // (nsgpu_sim_attach_p2p) the engine first dispatches every device event below the next host event's
 // key (nsgpu_p2p_advance pauses its window pipeline there), then that host event is the window.  The
 // runtime owns the uid counter and the dispatch rank; the engine continues from them at every advance.
+//
+// Inserts go straight into the scheduler's pinned stage ring (nsgpu_sched_host.h: one store each, no
+// device call); the ring is sorted and merged on the device once per front refill.  C-callback closures
+// live in a slab whose slots are recycled at dispatch / removal; an EventId names a slot and its
+// generation, so an id of a recycled slot reads as expired.
 #include <deque>
 #include <vector>
 #include <unordered_set>
-#include "nsgpu_internal.h"
+#include "nsgpu_sched_host.h"
 
 namespace {
 struct HostEvent {  // a C-callback closure + cancel flag (nsgpu_sim_schedule*); raw handles are the caller's
   nsgpu_event_fn fn;
   void *user;
   uint64_t arg;
-  bool cancelled;
-  bool is_stop;
+  uint32_t gen;  // bumped when the slot is released
+  bool cancelled, is_stop, live;
+};
+struct DestroyEv {  // an entry of the destroy list (DefaultSimulatorImpl::m_destroyEvents)
+  uint64_t handle;  // slab handle, or a caller's raw handle with RAW set
+  uint64_t ts;      // the EventId's ts (ScheduleDestroy's Now)
 };
 constexpr uint64_t RAW = 1;  // handle tag: a caller-owned handle (nsgpu_sim_insert), not a HostEvent
 }  // namespace
@@ -33,7 +45,7 @@ struct nsgpu_sim {
   nsgpu_sched *events = nullptr;
   nsgpu_p2p *p2p = nullptr;
   void *stream = nullptr;
-  bool stop = false, ended = false;
+  bool stop = false, ended = false, dev_stopped = false;
   uint32_t uid = 4;
   uint32_t cur_uid = 0;
   uint64_t cur_ts = 0;
@@ -42,23 +54,46 @@ struct nsgpu_sim {
   uint64_t *log_ts = nullptr;  // optional pop-order log of the host dispatches (global ranks)
   uint32_t *log_uid = nullptr, *log_ctx = nullptr;
   uint64_t log_cap = 0;
-  std::deque<nsgpu_event_id> destroy_events;
-  std::vector<HostEvent *> arena;              // live until the runtime is freed (EventIds stay valid)
+  std::deque<DestroyEv> destroy_events;
+  std::vector<HostEvent> slab;                 // C-callback closures; handle = (gen << 32 | slot) << 1
+  std::vector<uint32_t> free_slots;
   std::vector<nsgpu_event> win;                // the current window
   size_t win_next = 0;                         // first event of it not yet begun
   std::unordered_set<uint32_t> win_removed;    // window events a closure removed
   uint32_t p2p_seq = 0, p2p_seq_uid = 0;       // trace sink calls the running closure made on the engine
-  HostEvent *make(nsgpu_event_fn fn, void *user, uint64_t arg, bool is_stop = false) {
-    HostEvent *e = new HostEvent{fn, user, arg, false, is_stop};
-    arena.push_back(e);
-    return e;
+
+  uint64_t make(nsgpu_event_fn fn, void *user, uint64_t arg, bool is_stop = false) {
+    uint32_t i;
+    if (!free_slots.empty()) {
+      i = free_slots.back();
+      free_slots.pop_back();
+    } else {
+      i = (uint32_t)slab.size();
+      slab.push_back(HostEvent{nullptr, nullptr, 0, 1, false, false, false});
+    }
+    HostEvent &e = slab[i];
+    e.fn = fn, e.user = user, e.arg = arg, e.cancelled = false, e.is_stop = is_stop, e.live = true;
+    return (((uint64_t)e.gen << 32) | i) << 1;
   }
-  static HostEvent *impl(const nsgpu_event_id &id) { return (HostEvent *)(uintptr_t)id.impl; }
+  // the live closure a slab handle names, or null (released slot, other generation, raw handle)
+  HostEvent *get(uint64_t handle) {
+    if (handle & RAW) return nullptr;
+    const uint32_t i = (uint32_t)(handle >> 1), g = (uint32_t)(handle >> 33);
+    if (i >= slab.size() || !slab[i].live || slab[i].gen != g) return nullptr;
+    return &slab[i];
+  }
+  void release(uint64_t handle) {
+    HostEvent *e = get(handle);
+    if (!e) return;
+    e->live = false;
+    e->gen++;
+    free_slots.push_back((uint32_t)(handle >> 1));
+  }
   int insert(uint64_t ts, uint32_t ctx, uint64_t handle, uint32_t *out_uid) {
-    nsgpu_event ev{ts, uid, ctx, handle};
+    const nsgpu_event ev{ts, uid, ctx, handle};
     if (out_uid) *out_uid = uid;
     uid++;
-    return nsgpu_sched_insert(events, &ev, 1);
+    return nsgpu::sched_insert1(events, ev);
   }
   bool in_window(uint32_t u) const {
     for (size_t i = win_next; i < win.size(); i++)
@@ -67,14 +102,23 @@ struct nsgpu_sim {
   }
   // the time part of IsExpired (:304-332): the event's key is not after the one being dispatched
   bool key_expired(uint64_t ts, uint32_t u) const { return ts < cur_ts || (ts == cur_ts && u <= cur_uid); }
-  bool is_expired(const nsgpu_event_id &ev) const {
-    if (ev.uid == 2) {
-      if (impl(ev) == nullptr || impl(ev)->cancelled) return true;
-      for (auto &d : destroy_events)
-        if (d.impl == ev.impl && d.ts == ev.ts && d.context == ev.context && d.uid == ev.uid) return false;
-      return true;
-    }
-    return impl(ev) == nullptr || key_expired(ev.ts, ev.uid) || impl(ev)->cancelled;
+  bool destroy_pending(uint64_t handle, uint64_t ts) const {
+    for (const DestroyEv &d : destroy_events)
+      if (d.handle == handle && d.ts == ts) return true;
+    return false;
+  }
+  bool is_expired(const nsgpu_event_id &ev) {
+    HostEvent *e = get(ev.impl);
+    if (ev.uid == 2) return e == nullptr || e->cancelled || !destroy_pending(ev.impl, ev.ts);
+    return e == nullptr || key_expired(ev.ts, ev.uid) || e->cancelled;
+  }
+  // the attached engine's pending events (Next / IsFinished)
+  int device_pending(uint64_t *n, uint64_t *next_ts) {
+    *n = 0;
+    *next_ts = ~0ull;
+    if (!p2p || ended) return NSGPU_OK;
+    int stopped = 0;
+    return nsgpu_p2p_pending(p2p, n, next_ts, &stopped, stream);
   }
 };
 
@@ -98,7 +142,6 @@ int nsgpu_sim_create(uint32_t batch, void *stream, nsgpu_sim **out) {
 int nsgpu_sim_free(nsgpu_sim *s) {
   if (!s) return NSGPU_OK;
   nsgpu_sched_destroy(s->events);
-  for (HostEvent *e : s->arena) delete e;
   delete s;
   return NSGPU_OK;
 }
@@ -107,9 +150,8 @@ int nsgpu_sim_free(nsgpu_sim *s) {
 // Schedule calls precede the program's), so the runtime continues from the engine's post-setup uid.
 int nsgpu_sim_attach_p2p(nsgpu_sim *s, nsgpu_p2p *h) {
   if (!s || !h) return set_error(NSGPU_EINVAL, "nsgpu_sim_attach_p2p: null");
-  uint64_t n = 0;
-  nsgpu_sched_size(s->events, &n);
-  if (n || s->dispatched || s->uid != 4) return set_error(NSGPU_ESTATE, "nsgpu_sim_attach_p2p: attach before scheduling");
+  if (s->events->size || s->dispatched || s->uid != 4)
+    return set_error(NSGPU_ESTATE, "nsgpu_sim_attach_p2p: attach before scheduling");
   uint32_t u = 0;
   int rc = nsgpu_p2p_setup_uid(h, &u);
   if (rc) return rc;
@@ -128,16 +170,16 @@ int nsgpu_sim_schedule(nsgpu_sim *s, int64_t delay, nsgpu_event_fn fn, void *use
                        nsgpu_event_id *id) {  // :188-204
   const int64_t t = delay + (int64_t)s->cur_ts;
   if (t < 0 || t < (int64_t)s->cur_ts) return set_error(NSGPU_EINVAL, "Schedule: negative absolute time");
-  HostEvent *e = s->make(fn, user, arg);
+  const uint64_t h = s->make(fn, user, arg);
   uint32_t u;
-  const int rc = s->insert((uint64_t)t, s->cur_ctx, (uint64_t)(uintptr_t)e, &u);
-  if (id) *id = nsgpu_event_id{(uint64_t)(uintptr_t)e, (uint64_t)t, s->cur_ctx, u};
+  const int rc = s->insert((uint64_t)t, s->cur_ctx, h, &u);
+  if (id) *id = nsgpu_event_id{h, (uint64_t)t, s->cur_ctx, u};
   return rc;
 }
 
 int nsgpu_sim_schedule_with_context(nsgpu_sim *s, uint32_t ctx, int64_t delay, nsgpu_event_fn fn, void *user,
                                     uint64_t arg) {  // :206-219
-  return s->insert(s->cur_ts + (uint64_t)delay, ctx, (uint64_t)(uintptr_t)s->make(fn, user, arg), nullptr);
+  return s->insert(s->cur_ts + (uint64_t)delay, ctx, s->make(fn, user, arg), nullptr);
 }
 
 int nsgpu_sim_schedule_now(nsgpu_sim *s, nsgpu_event_fn fn, void *user, uint64_t arg, nsgpu_event_id *id) {
@@ -145,11 +187,10 @@ int nsgpu_sim_schedule_now(nsgpu_sim *s, nsgpu_event_fn fn, void *user, uint64_t
 }
 
 int nsgpu_sim_schedule_destroy(nsgpu_sim *s, nsgpu_event_fn fn, void *user, uint64_t arg, nsgpu_event_id *id) {
-  HostEvent *e = s->make(fn, user, arg);  // :235-242
-  nsgpu_event_id d{(uint64_t)(uintptr_t)e, s->cur_ts, 0xffffffffu, 2};
-  s->destroy_events.push_back(d);
+  const uint64_t h = s->make(fn, user, arg);  // :235-242
+  s->destroy_events.push_back(DestroyEv{h, s->cur_ts});
   s->uid++;
-  if (id) *id = d;
+  if (id) *id = nsgpu_event_id{h, s->cur_ts, 0xffffffffu, 2};
   return NSGPU_OK;
 }
 
@@ -159,23 +200,25 @@ int nsgpu_sim_is_expired(nsgpu_sim *s, const nsgpu_event_id *id, int *expired) {
 }
 
 int nsgpu_sim_cancel(nsgpu_sim *s, const nsgpu_event_id *id) {  // :292-302
-  if (!s->is_expired(*id)) nsgpu_sim::impl(*id)->cancelled = true;
+  if (!s->is_expired(*id)) s->get(id->impl)->cancelled = true;
   return NSGPU_OK;
 }
 
 int nsgpu_sim_remove(nsgpu_sim *s, const nsgpu_event_id *id) {  // :256-290
   if (id->uid == 2) {
     for (auto i = s->destroy_events.begin(); i != s->destroy_events.end(); i++) {
-      if (i->impl == id->impl && i->ts == id->ts && i->context == id->context && i->uid == id->uid) {
+      if (i->handle == id->impl && i->ts == id->ts) {
         s->destroy_events.erase(i);
+        s->release(id->impl);
         break;
       }
     }
     return NSGPU_OK;
   }
   if (s->is_expired(*id)) return NSGPU_OK;
-  nsgpu_sim::impl(*id)->cancelled = true;
-  return nsgpu_sim_remove_key(s, id->ts, id->uid, id->context, id->impl);
+  const int rc = nsgpu_sim_remove_key(s, id->ts, id->uid, id->context, id->impl);
+  s->release(id->impl);  // (the queue entry, dropped when it surfaces, is never dereferenced)
+  return rc;
 }
 
 // ---- raw handles (ns3::HipSimulatorImpl: the handle is an EventImpl*, never dereferenced here) ----
@@ -189,6 +232,49 @@ int nsgpu_sim_consume_uid(nsgpu_sim *s, uint32_t *uid) {  // ScheduleDestroy's u
   if (!s) return set_error(NSGPU_EINVAL, "nsgpu_sim_consume_uid: null");
   if (uid) *uid = s->uid;
   s->uid++;
+  return NSGPU_OK;
+}
+
+// The destroy list of raw handles (DefaultSimulatorImpl::m_destroyEvents, :235-242, :79-92, :256-268,
+// :306-322): the runtime keeps the list, the caller keeps the reference each entry holds.
+int nsgpu_sim_destroy_insert(nsgpu_sim *s, uint64_t handle, uint64_t *ts) {  // ScheduleDestroy
+  if (!s || (handle & RAW)) return set_error(NSGPU_EINVAL, "nsgpu_sim_destroy_insert: null runtime or odd handle");
+  s->destroy_events.push_back(DestroyEv{handle | RAW, s->cur_ts});
+  s->uid++;
+  if (ts) *ts = s->cur_ts;
+  return NSGPU_OK;
+}
+
+int nsgpu_sim_destroy_pop(nsgpu_sim *s, uint64_t *handle, int *found) {  // Destroy: front, then pop_front
+  if (!s || !handle || !found) return set_error(NSGPU_EINVAL, "nsgpu_sim_destroy_pop: null");
+  *found = 0;
+  while (!s->destroy_events.empty()) {
+    const DestroyEv d = s->destroy_events.front();
+    s->destroy_events.pop_front();
+    if (!(d.handle & RAW)) return set_error(NSGPU_ESTATE, "nsgpu_sim_destroy_pop: a callback destroy event (nsgpu_sim_destroy)");
+    *handle = d.handle & ~RAW;
+    *found = 1;
+    return NSGPU_OK;
+  }
+  return NSGPU_OK;
+}
+
+int nsgpu_sim_destroy_remove(nsgpu_sim *s, uint64_t handle, uint64_t ts, int *found) {  // Remove (uid 2)
+  if (!s || !found) return set_error(NSGPU_EINVAL, "nsgpu_sim_destroy_remove: null");
+  *found = 0;
+  for (auto i = s->destroy_events.begin(); i != s->destroy_events.end(); i++) {
+    if (i->handle == (handle | RAW) && i->ts == ts) {
+      s->destroy_events.erase(i);
+      *found = 1;
+      break;
+    }
+  }
+  return NSGPU_OK;
+}
+
+int nsgpu_sim_destroy_pending(nsgpu_sim *s, uint64_t handle, uint64_t ts, int *pending) {  // IsExpired (uid 2)
+  if (!s || !pending) return set_error(NSGPU_EINVAL, "nsgpu_sim_destroy_pending: null");
+  *pending = s->destroy_pending(handle | RAW, ts) ? 1 : 0;
   return NSGPU_OK;
 }
 
@@ -210,55 +296,73 @@ int nsgpu_sim_remove_key(nsgpu_sim *s, uint64_t ts, uint32_t uid, uint32_t ctx, 
 }
 
 // The next window (see the file header).  *n = 0: nothing is left to dispatch (the queue is empty and
-// the attached engine, if any, has run out), or a Stop was dispatched.
-int nsgpu_sim_pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n) {
-  if (!s || !out || !n || cap == 0) return set_error(NSGPU_EINVAL, "nsgpu_sim_pop_window: bad arguments");
+// the attached engine, if any, has run out), or a Stop was dispatched.  `force`: pop even after a Stop
+// (RunOneEvent).
+static int pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n, bool force) {
   *n = 0;
   s->win.clear();
   s->win_next = 0;
-  s->win_removed.clear();
-  if (s->stop || s->ended) return NSGPU_OK;
+  if (!s->win_removed.empty()) s->win_removed.clear();
+  if (s->stop && !force) return NSGPU_OK;
   int rc;
   nsgpu_event e;
-  uint64_t size = 0;
-  if ((rc = nsgpu_sched_size(s->events, &size))) return rc;
-  if (s->p2p) {
+  nsgpu_sched *q = s->events;
+  if (s->p2p && !s->ended) {
     bool have = false;
-    if (size) {
-      if ((rc = nsgpu_sched_peek_next(s->events, &e))) return rc;
+    if (q->size) {
+      if (!nsgpu::sched_next(q, &e, false, &rc)) return rc ? rc : set_error(NSGPU_ESTATE, "pop_window: lost events");
       have = true;
     }
     int ended = 0;
     rc = nsgpu_p2p_advance(s->p2p, have ? e.ts : ~0ull, have ? e.uid : 0u, &s->uid, &s->dispatched, &ended, s->stream);
     if (rc) return rc;
-    if (ended) {  // the device dispatched Simulator::Stop, or nothing is pending anywhere
+    if (ended) {  // the device dispatched Simulator::Stop, or nothing is pending on the device
+      uint64_t pn = 0, pts = 0;
+      int stopped = 0;
+      if ((rc = nsgpu_p2p_pending(s->p2p, &pn, &pts, &stopped, s->stream))) return rc;
       s->ended = true;
+      if (stopped) {  // the device Stop ends this Run (:153-165); the engine cannot resume after it
+        s->dev_stopped = true;
+        return NSGPU_OK;
+      }
+    } else {
+      if (!have) return NSGPU_OK;
+      if ((rc = nsgpu::sched_remove_next1(q, &e))) return rc;
+      out[0] = e;
+      s->win.push_back(e);
+      *n = 1;
       return NSGPU_OK;
     }
-    if (!have) return NSGPU_OK;
-    if ((rc = nsgpu_sched_remove_next(s->events, &e))) return rc;
-    out[0] = e;
-    s->win.push_back(e);
-    *n = 1;
+    if (!have) return NSGPU_OK;  // (the device drained: the host queue continues alone below)
+  } else if (s->dev_stopped && !force) {
     return NSGPU_OK;
   }
-  if (!size) return NSGPU_OK;
-  if ((rc = nsgpu_sched_remove_next(s->events, &e))) return rc;
+  if (!q->size) return NSGPU_OK;
+  if ((rc = nsgpu::sched_remove_next1(q, &e))) return rc;
   out[0] = e;
   s->win.push_back(e);
   uint32_t k = 1;
-  while (k < cap) {
-    if ((rc = nsgpu_sched_size(s->events, &size))) return rc;
-    if (!size) break;
+  while (k < cap && q->size) {
     nsgpu_event f;
-    if ((rc = nsgpu_sched_peek_next(s->events, &f))) return rc;
+    if (!nsgpu::sched_next(q, &f, false, &rc)) return rc ? rc : set_error(NSGPU_ESTATE, "pop_window: lost events");
     if (f.ts != e.ts) break;
-    if ((rc = nsgpu_sched_remove_next(s->events, &f))) return rc;
+    if ((rc = nsgpu::sched_remove_next1(q, &f))) return rc;
     out[k++] = f;
     s->win.push_back(f);
   }
   *n = k;
   return NSGPU_OK;
+}
+
+int nsgpu_sim_pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n) {
+  if (!s || !out || !n || cap == 0) return set_error(NSGPU_EINVAL, "nsgpu_sim_pop_window: bad arguments");
+  return pop_window(s, out, cap, n, false);
+}
+
+// RunOneEvent (:167-170): the next event, whatever the stop flag says.
+int nsgpu_sim_pop_one(nsgpu_sim *s, nsgpu_event *out, uint32_t *n) {
+  if (!s || !out || !n) return set_error(NSGPU_EINVAL, "nsgpu_sim_pop_one: bad arguments");
+  return pop_window(s, out, 1, n, true);
 }
 
 // Window event i is being dispatched: 0 = run its closure, 1 = a closure of this window removed it
@@ -267,13 +371,13 @@ int nsgpu_sim_pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t 
 int nsgpu_sim_begin(nsgpu_sim *s, const nsgpu_event *e, int *skip) {
   if (!s || !e || !skip) return set_error(NSGPU_EINVAL, "nsgpu_sim_begin: null");
   if (s->win_next < s->win.size() && s->win[s->win_next].uid == e->uid) s->win_next++;
-  if (s->win_removed.count(e->uid)) {
+  if (!s->win_removed.empty() && s->win_removed.count(e->uid)) {
     *skip = 1;
     return NSGPU_OK;
   }
-  if (s->stop) {
+  if (s->stop && s->win.size() > 1) {  // (a one-event window was popped for this dispatch: RunOneEvent)
     *skip = 2;
-    return nsgpu_sched_insert(s->events, e, 1);
+    return nsgpu::sched_insert1(s->events, *e);
   }
   *skip = 0;
   s->cur_ts = e->ts;
@@ -290,29 +394,52 @@ int nsgpu_sim_begin(nsgpu_sim *s, const nsgpu_event *e, int *skip) {
   return NSGPU_OK;
 }
 
+// Dispatches the popped window of C-callback closures.
+static int run_window(nsgpu_sim *s, const nsgpu_event *w, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) {
+    int skip = 0;
+    int rc = nsgpu_sim_begin(s, &w[i], &skip);
+    if (rc) return rc;
+    if (skip) continue;
+    if (w[i].handle & RAW) return set_error(NSGPU_ESTATE, "nsgpu_sim_run: a raw handle (dispatch it with nsgpu_sim_pop_window)");
+    HostEvent *e = s->get(w[i].handle);
+    if (!e) return set_error(NSGPU_ESTATE, "nsgpu_sim_run: a dispatched event names a released closure");
+    const HostEvent c = *e;
+    s->release(w[i].handle);
+    if (c.cancelled) {  // still dequeued and counted (event-impl.cc:34-41)
+      s->cancelled++;
+      continue;
+    }
+    if (c.is_stop) s->stop = true;
+    else c.fn(c.user, c.arg);
+  }
+  return NSGPU_OK;
+}
+
 int nsgpu_sim_run(nsgpu_sim *s) {  // Run (:153-165): windows of closures (and device events)
+  // A later Run continues after Stop (:153-165); the device pipeline cannot restart after a Stop it
+  // dispatched itself (its final window's children are not queued), so that case fails loudly.
+  if (s->dev_stopped)
+    return set_error(NSGPU_ESTATE, "nsgpu_sim_run: the attached engine dispatched Simulator::Stop; resuming after a "
+                                   "device-side Stop is not supported");
   s->stop = false;
   std::vector<nsgpu_event> w(1024);
   for (;;) {
     uint32_t n = 0;
-    int rc = nsgpu_sim_pop_window(s, w.data(), (uint32_t)w.size(), &n);
+    int rc = pop_window(s, w.data(), (uint32_t)w.size(), &n, false);
     if (rc) return rc;
     if (n == 0) break;
-    for (uint32_t i = 0; i < n; i++) {
-      int skip = 0;
-      if ((rc = nsgpu_sim_begin(s, &w[i], &skip))) return rc;
-      if (skip) continue;
-      if (w[i].handle & RAW) return set_error(NSGPU_ESTATE, "nsgpu_sim_run: a raw handle (dispatch it with nsgpu_sim_pop_window)");
-      HostEvent *e = (HostEvent *)(uintptr_t)w[i].handle;
-      if (e->cancelled) {  // still dequeued and counted (event-impl.cc:34-41)
-        s->cancelled++;
-        continue;
-      }
-      if (e->is_stop) s->stop = true;
-      else e->fn(e->user, e->arg);
-    }
+    if ((rc = run_window(s, w.data(), n))) return rc;
   }
   return NSGPU_OK;
+}
+
+int nsgpu_sim_run_one(nsgpu_sim *s) {  // RunOneEvent (:167-170)
+  nsgpu_event e;
+  uint32_t n = 0;
+  int rc = pop_window(s, &e, 1, &n, true);
+  if (rc || n == 0) return rc;
+  return run_window(s, &e, 1);
 }
 
 int nsgpu_sim_stop(nsgpu_sim *s) {
@@ -321,15 +448,19 @@ int nsgpu_sim_stop(nsgpu_sim *s) {
 }
 
 int nsgpu_sim_stop_at(nsgpu_sim *s, int64_t delay) {  // Stop (Time): Schedule (time, &Simulator::Stop)
-  return s->insert(s->cur_ts + (uint64_t)delay, s->cur_ctx, (uint64_t)(uintptr_t)s->make(nullptr, nullptr, 0, true),
-                   nullptr);
+  return s->insert(s->cur_ts + (uint64_t)delay, s->cur_ctx, s->make(nullptr, nullptr, 0, true), nullptr);
 }
 
-int nsgpu_sim_destroy(nsgpu_sim *s) {  // :76-91
+int nsgpu_sim_destroy(nsgpu_sim *s) {  // :79-92 — a destroy closure may schedule or remove destroy events
   while (!s->destroy_events.empty()) {
-    HostEvent *e = nsgpu_sim::impl(s->destroy_events.front());
+    const DestroyEv d = s->destroy_events.front();
     s->destroy_events.pop_front();
-    if (!e->cancelled) e->fn(e->user, e->arg);
+    if (d.handle & RAW) return set_error(NSGPU_ESTATE, "nsgpu_sim_destroy: a raw destroy handle (nsgpu_sim_destroy_pop)");
+    HostEvent *e = s->get(d.handle);
+    if (!e) continue;
+    const HostEvent c = *e;
+    s->release(d.handle);
+    if (!c.cancelled) c.fn(c.user, c.arg);
   }
   return NSGPU_OK;
 }
@@ -342,21 +473,36 @@ int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *di
   return NSGPU_OK;
 }
 
-// Next () / IsFinished (): the time of the next host event (device events of an attached engine
-// are not counted: they never outlive Run); *empty = 1 when none is pending.
+// Next (): the time of the next event, host or device (an attached engine's pending events count);
+// *empty = 1 when none is pending anywhere.
 int nsgpu_sim_next(nsgpu_sim *s, uint64_t *ts, int *empty) {
   if (!s || !ts || !empty) return set_error(NSGPU_EINVAL, "nsgpu_sim_next: null");
-  uint64_t n = 0;
-  int rc = nsgpu_sched_size(s->events, &n);
+  uint64_t dn = 0, dts = ~0ull;
+  int rc = s->device_pending(&dn, &dts);
   if (rc) return rc;
-  *empty = n == 0;
-  *ts = 0;
-  if (n) {
+  *ts = dn ? dts : ~0ull;
+  if (s->events->size) {
     nsgpu_event e;
-    if ((rc = nsgpu_sched_peek_next(s->events, &e))) return rc;
-    *ts = e.ts;
+    if (!nsgpu::sched_next(s->events, &e, false, &rc)) return rc ? rc : set_error(NSGPU_ESTATE, "next: lost events");
+    if (e.ts < *ts) *ts = e.ts;
   }
+  *empty = (s->events->size == 0 && dn == 0) ? 1 : 0;
+  if (*empty) *ts = 0;
   return NSGPU_OK;
+}
+
+// IsFinished () (:133-137): nothing pending (host or device), or Stop was called / dispatched.
+int nsgpu_sim_is_finished(nsgpu_sim *s, int *finished) {
+  if (!s || !finished) return set_error(NSGPU_EINVAL, "nsgpu_sim_is_finished: null");
+  if (s->stop || s->dev_stopped) {
+    *finished = 1;
+    return NSGPU_OK;
+  }
+  uint64_t ts = 0;
+  int empty = 1;
+  const int rc = nsgpu_sim_next(s, &ts, &empty);
+  *finished = empty;
+  return rc;
 }
 
 // Stop () sets the flag that ends the current Run at the next dispatch; Run clears it (:153-165).
@@ -370,12 +516,10 @@ int nsgpu_sim_set_stop(nsgpu_sim *s, int stop) {
 int nsgpu_sim_drain(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n) {
   if (!s || !out || !n) return set_error(NSGPU_EINVAL, "nsgpu_sim_drain: null");
   *n = 0;
-  for (uint32_t k = 0; k < cap; k++) {
-    uint64_t size = 0;
-    int rc = nsgpu_sched_size(s->events, &size);
+  for (uint32_t k = 0; k < cap && s->events->size; k++) {
+    const int rc = nsgpu::sched_remove_next1(s->events, &out[k]);
     if (rc) return rc;
-    if (!size) break;
-    if ((rc = nsgpu_sched_remove_next(s->events, &out[k]))) return rc;
+    s->release(out[k].handle);
     *n = k + 1;
   }
   return NSGPU_OK;
@@ -392,6 +536,13 @@ int nsgpu_sim_host_stats(nsgpu_sim *s, uint64_t *host_dispatched, uint64_t *canc
   if (host_dispatched) *host_dispatched = s->host_dispatched;
   if (cancelled) *cancelled = s->cancelled;
   if (digest) *digest = s->digest;
+  return NSGPU_OK;
+}
+
+// Closures held by the runtime (live slab slots): scheduled, destroy-listed or not yet released.
+int nsgpu_sim_live_closures(nsgpu_sim *s, uint64_t *n) {
+  if (!s || !n) return set_error(NSGPU_EINVAL, "nsgpu_sim_live_closures: null");
+  *n = s->slab.size() - s->free_slots.size();
   return NSGPU_OK;
 }
 

@@ -3,7 +3,6 @@
 #include "ns3/simulator.h"
 #include "ns3/fatal-error.h"
 #include "ns3/object-factory.h"
-#include <algorithm>
 
 namespace ns3 {
 
@@ -40,12 +39,30 @@ HipSimulatorImpl::HipSimulatorImpl ()
   : m_rt (0),
     m_window (4096)
 {
-  NSGPU_RT (nsgpu_sim_create (4096, 0, &m_rt));
+  // front size 0: adaptive (nsgpu_sched_host.h)
+  NSGPU_RT (nsgpu_sim_create (0, 0, &m_rt));
 }
 
 HipSimulatorImpl::~HipSimulatorImpl ()
 {
+  ReleaseDestroyList ();
   nsgpu_sim_free (m_rt);
+}
+
+void
+HipSimulatorImpl::ReleaseDestroyList (void)
+{
+  // the references the destroy list holds (m_destroyEvents' EventIds, default-simulator-impl.cc:235-242)
+  uint64_t handle = 0;
+  int found = 1;
+  while (m_rt != 0 && found)
+    {
+      NSGPU_RT (nsgpu_sim_destroy_pop (m_rt, &handle, &found));
+      if (found)
+        {
+          HandleToEvent (handle)->Unref ();
+        }
+    }
 }
 
 void
@@ -84,21 +101,31 @@ HipSimulatorImpl::DoDispose (void)
         }
     }
   while (n > 0);
+  ReleaseDestroyList ();
   SimulatorImpl::DoDispose ();
 }
 
 void
 HipSimulatorImpl::Destroy ()
 {
-  // ScheduleDestroy order; an event cancelled or removed meanwhile does not run
-  std::vector<EventId> pending;
-  pending.swap (m_atDestroy);
-  for (std::vector<EventId>::iterator i = pending.begin (); i != pending.end (); ++i)
+  // default-simulator-impl.cc:79-92: the front of the runtime's destroy list is popped before it runs,
+  // until the list is empty, so a destroy event a destroy closure schedules runs too and one it
+  // Removes does not
+  uint64_t handle = 0;
+  int found = 1;
+  for (;;)
     {
-      if (!i->PeekEventImpl ()->IsCancelled ())
+      NSGPU_RT (nsgpu_sim_destroy_pop (m_rt, &handle, &found));
+      if (!found)
         {
-          i->PeekEventImpl ()->Invoke ();
+          break;
         }
+      EventImpl *ev = HandleToEvent (handle);
+      if (!ev->IsCancelled ())
+        {
+          ev->Invoke ();
+        }
+      ev->Unref ();  // the list's reference
     }
 }
 
@@ -128,10 +155,10 @@ HipSimulatorImpl::Enqueue (uint64_t ts, uint32_t context, EventImpl *event)
 bool
 HipSimulatorImpl::IsFinished (void) const
 {
-  uint64_t ts = 0;
-  int empty = 1;
-  NSGPU_RT (nsgpu_sim_next (m_rt, &ts, &empty));
-  return empty != 0;
+  // default-simulator-impl.cc:133-137: nothing pending (host or device) or Stop was called
+  int finished = 1;
+  NSGPU_RT (nsgpu_sim_is_finished (m_rt, &finished));
+  return finished != 0;
 }
 
 Time
@@ -148,31 +175,19 @@ HipSimulatorImpl::Next (void) const
 }
 
 void
-HipSimulatorImpl::RunWindows (uint32_t limit)
+HipSimulatorImpl::Dispatch (uint32_t n)
 {
-  uint32_t done = 0;
-  while (done < limit)
+  for (uint32_t i = 0; i < n; i++)
     {
-      uint32_t n = 0;
-      const uint32_t cap = std::min<uint32_t> (limit - done, m_window.size ());
-      NSGPU_RT (nsgpu_sim_pop_window (m_rt, &m_window[0], cap, &n));
-      if (n == 0)
+      int skip = 0;
+      NSGPU_RT (nsgpu_sim_begin (m_rt, &m_window[i], &skip));
+      if (skip != 0)
         {
-          return;  // nothing pending (host or device), or a Stop was dispatched
+          continue;  // removed by a closure of this window (released there), or after a Stop
         }
-      for (uint32_t i = 0; i < n; i++)
-        {
-          int skip = 0;
-          NSGPU_RT (nsgpu_sim_begin (m_rt, &m_window[i], &skip));
-          if (skip != 0)
-            {
-              continue;  // removed by a closure of this window (released there), or after a Stop
-            }
-          EventImpl *ev = HandleToEvent (m_window[i].handle);
-          ev->Invoke ();  // Invoke skips a cancelled closure; the dispatch still counts (H16)
-          ev->Unref ();
-          done++;
-        }
+      EventImpl *ev = HandleToEvent (m_window[i].handle);
+      ev->Invoke ();  // Invoke skips a cancelled closure; the dispatch still counts (H16)
+      ev->Unref ();
     }
 }
 
@@ -180,13 +195,29 @@ void
 HipSimulatorImpl::Run (void)
 {
   NSGPU_RT (nsgpu_sim_set_stop (m_rt, 0));
-  RunWindows (0xffffffffu);
+  for (;;)
+    {
+      uint32_t n = 0;
+      NSGPU_RT (nsgpu_sim_pop_window (m_rt, &m_window[0], m_window.size (), &n));
+      if (n == 0)
+        {
+          return;  // nothing pending (host or device), or a Stop was dispatched
+        }
+      Dispatch (n);
+    }
 }
 
 void
 HipSimulatorImpl::RunOneEvent (void)
 {
-  RunWindows (1);
+  // default-simulator-impl.cc:167-170: one event, whatever the stop flag says
+  uint32_t n = 0;
+  NSGPU_RT (nsgpu_sim_pop_one (m_rt, &m_window[0], &n));
+  if (n == 0)
+    {
+      NS_FATAL_ERROR ("HipSimulatorImpl::RunOneEvent: no pending event");
+    }
+  Dispatch (n);
 }
 
 void
@@ -227,11 +258,13 @@ HipSimulatorImpl::ScheduleNow (EventImpl *event)
 EventId
 HipSimulatorImpl::ScheduleDestroy (EventImpl *event)
 {
-  // uid 2 marks a destroy event; its own uid is consumed all the same
-  NSGPU_RT (nsgpu_sim_consume_uid (m_rt, 0));
-  EventId id (Ptr<EventImpl> (event, false), NowTs (), 0xffffffff, 2);
-  m_atDestroy.push_back (id);
-  return id;
+  // uid 2 marks a destroy event; its own uid is consumed all the same.  The EventId
+  // adopts the caller's reference; the runtime's list entry holds one more (released by Destroy,
+  // Remove or DoDispose).
+  uint64_t ts = 0;
+  NSGPU_RT (nsgpu_sim_destroy_insert (m_rt, reinterpret_cast<uintptr_t> (event), &ts));
+  event->Ref ();
+  return EventId (Ptr<EventImpl> (event, false), ts, 0xffffffff, 2);
 }
 
 Time
@@ -255,10 +288,13 @@ HipSimulatorImpl::Remove (const EventId &id)
 {
   if (id.GetUid () == 2)
     {
-      std::vector<EventId>::iterator i = std::find (m_atDestroy.begin (), m_atDestroy.end (), id);
-      if (i != m_atDestroy.end ())
+      // the first list entry equal to id (default-simulator-impl.cc:256-268); its reference goes with it
+      int found = 0;
+      NSGPU_RT (nsgpu_sim_destroy_remove (m_rt, reinterpret_cast<uintptr_t> (id.PeekEventImpl ()), id.GetTs (),
+                                          &found));
+      if (found)
         {
-          m_atDestroy.erase (i);
+          id.PeekEventImpl ()->Unref ();
         }
       return;
     }
@@ -291,7 +327,9 @@ HipSimulatorImpl::IsExpired (const EventId &ev) const
     }
   if (ev.GetUid () == 2)
     {
-      return std::find (m_atDestroy.begin (), m_atDestroy.end (), ev) == m_atDestroy.end ();
+      int pending = 0;
+      NSGPU_RT (nsgpu_sim_destroy_pending (m_rt, reinterpret_cast<uintptr_t> (impl), ev.GetTs (), &pending));
+      return pending == 0;
     }
   int expired = 0;
   NSGPU_RT (nsgpu_sim_key_expired (m_rt, ev.GetTs (), ev.GetUid (), &expired));

@@ -59,15 +59,15 @@ public:
 
 private:
   virtual void DoDispose (void);
-  /* Pulls and runs windows until the runtime has nothing left or Stop; at most `limit` events. */
-  void RunWindows (uint32_t limit);
+  /* Runs the first n events of m_window (a popped window) in order. */
+  void Dispatch (uint32_t n);
+  /* Unrefs the destroy list's references (the list itself lives in the runtime). */
+  void ReleaseDestroyList (void);
   EventId Enqueue (uint64_t ts, uint32_t context, EventImpl *event);
   uint64_t NowTs (void) const;
 
   nsgpu_sim *m_rt;
   std::vector<nsgpu_event> m_window;
-  /* ScheduleDestroy'd events: they only run at Destroy (), never through the runtime's queue */
-  std::vector<EventId> m_atDestroy;
 };
 
 } // namespace ns3

@@ -117,6 +117,16 @@ SIGNATURES = {
     "nsgpu_sim_set_log": (C.c_int, [_vp, _vp, _vp, _vp, _u64]),
     "nsgpu_sim_attach_p2p": (C.c_int, [_vp, _vp]),
     "nsgpu_sim_p2p_send": (C.c_int, [_vp, _u32]),
+    "nsgpu_sim_is_finished": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_run_one": (C.c_int, [_vp]),
+    "nsgpu_sim_pop_one": (C.c_int, [_vp, _vp, _vp]),
+    "nsgpu_sim_live_closures": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_destroy_insert": (C.c_int, [_vp, _u64, _vp]),
+    "nsgpu_sim_destroy_pop": (C.c_int, [_vp, _vp, _vp]),
+    "nsgpu_sim_destroy_remove": (C.c_int, [_vp, _u64, _u64, _vp]),
+    "nsgpu_sim_destroy_pending": (C.c_int, [_vp, _u64, _u64, _vp]),
+    "nsgpu_sched_stats": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "nsgpu_p2p_pending": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "nsgpu_p2p_setup_uid": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_advance": (C.c_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "nsgpu_p2p_inject_send": (C.c_int, [_vp, _u32, _u64, _u32, _u32, _vp, _vp, _vp]),
@@ -562,6 +572,24 @@ class Sim:
     def run(self):
         check(lib().nsgpu_sim_run(self.h))
 
+    def run_one(self):
+        check(lib().nsgpu_sim_run_one(self.h))
+
+    def is_finished(self):
+        f = C.c_int()
+        check(lib().nsgpu_sim_is_finished(self.h, C.byref(f)))
+        return bool(f.value)
+
+    def next(self):
+        ts, empty = C.c_uint64(), C.c_int()
+        check(lib().nsgpu_sim_next(self.h, C.byref(ts), C.byref(empty)))
+        return None if empty.value else ts.value
+
+    def live_closures(self):
+        n = C.c_uint64()
+        check(lib().nsgpu_sim_live_closures(self.h, C.byref(n)))
+        return n.value
+
     def stop(self, delay=None):
         if delay is None:
             check(lib().nsgpu_sim_stop(self.h))
@@ -608,6 +636,46 @@ class Sim:
 
     def remove_key(self, ts, uid, ctx=0, handle=0):
         check(lib().nsgpu_sim_remove_key(self.h, ts, uid, ctx, handle))
+
+    def drain(self, cap=1024):
+        out = np.zeros(cap, EVENT_DTYPE)
+        n = C.c_uint32()
+        check(lib().nsgpu_sim_drain(self.h, out.ctypes.data, cap, C.byref(n)))
+        return out[:n.value]
+
+    def pop_one(self):
+        out = np.zeros(1, EVENT_DTYPE)
+        n = C.c_uint32()
+        check(lib().nsgpu_sim_pop_one(self.h, out.ctypes.data, C.byref(n)))
+        return out[:n.value]
+
+    def set_stop(self, stop):
+        check(lib().nsgpu_sim_set_stop(self.h, int(stop)))
+
+    def key_expired(self, ts, uid):
+        e = C.c_int()
+        check(lib().nsgpu_sim_key_expired(self.h, ts, uid, C.byref(e)))
+        return bool(e.value)
+
+    def destroy_insert(self, handle):
+        ts = C.c_uint64()
+        check(lib().nsgpu_sim_destroy_insert(self.h, handle, C.byref(ts)))
+        return ts.value
+
+    def destroy_pop(self):
+        h, f = C.c_uint64(), C.c_int()
+        check(lib().nsgpu_sim_destroy_pop(self.h, C.byref(h), C.byref(f)))
+        return h.value if f.value else None
+
+    def destroy_remove(self, handle, ts):
+        f = C.c_int()
+        check(lib().nsgpu_sim_destroy_remove(self.h, handle, ts, C.byref(f)))
+        return bool(f.value)
+
+    def destroy_pending(self, handle, ts):
+        p = C.c_int()
+        check(lib().nsgpu_sim_destroy_pending(self.h, handle, ts, C.byref(p)))
+        return bool(p.value)
 
     # ---- mixed host / device runs ----
     def attach_p2p(self, engine):

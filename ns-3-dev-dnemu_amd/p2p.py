@@ -584,9 +584,14 @@ class Engine:
         self.launch()
         return self.results(log_n)
 
+    def close(self):
+        if self.h:
+            nsgpu.lib().nsgpu_p2p_destroy(self.h)
+            self.h = None
+
     def __del__(self):
         try:
-            nsgpu.lib().nsgpu_p2p_destroy(self.h)
+            self.close()
         except Exception:
             pass
 

@@ -99,6 +99,8 @@ void       nsref_sim_remove(nsref_sim *s, const nsgpu_event_id *id);
 void       nsref_sim_cancel(nsref_sim *s, const nsgpu_event_id *id);
 int        nsref_sim_is_expired(nsref_sim *s, const nsgpu_event_id *id);
 void       nsref_sim_run(nsref_sim *s);
+void       nsref_sim_run_one(nsref_sim *s);       /* RunOneEvent (:167-170) */
+int        nsref_sim_is_finished(nsref_sim *s);   /* IsFinished (:133-137) */
 void       nsref_sim_stop(nsref_sim *s);
 void       nsref_sim_stop_at(nsref_sim *s, int64_t delay);
 void       nsref_sim_destroy(nsref_sim *s);

@@ -112,8 +112,10 @@ def lib():
             getattr(L, f).argtypes = [C.c_void_p, C.POINTER(EventId)]
         L.nsref_sim_is_expired.argtypes = [C.c_void_p, C.POINTER(EventId)]
         L.nsref_sim_is_expired.restype = C.c_int
-        for f in ("nsref_sim_run", "nsref_sim_stop", "nsref_sim_destroy"):
+        for f in ("nsref_sim_run", "nsref_sim_stop", "nsref_sim_destroy", "nsref_sim_run_one"):
             getattr(L, f).argtypes = [C.c_void_p]
+        L.nsref_sim_is_finished.argtypes = [C.c_void_p]
+        L.nsref_sim_is_finished.restype = C.c_int
         L.nsref_sim_stop_at.argtypes = [C.c_void_p, C.c_int64]
         L.nsref_sim_now.argtypes = [C.c_void_p]
         L.nsref_sim_now.restype = C.c_uint64
@@ -323,6 +325,12 @@ class Sim:
 
     def run(self):
         self.L.nsref_sim_run(self.h)
+
+    def run_one(self):
+        self.L.nsref_sim_run_one(self.h)
+
+    def is_finished(self):
+        return bool(self.L.nsref_sim_is_finished(self.h))
 
     def stop(self, delay=None):
         if delay is None:

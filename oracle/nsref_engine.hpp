@@ -379,6 +379,11 @@ struct nsref_sim {
     m_stop = false;
     while (!m_events->IsEmpty() && !m_stop) ProcessOneEvent();
   }
+  bool IsFinished() const { return m_events->IsEmpty() || m_stop; }  // :133-137
+  void RunOneEvent() {  // :167-170 (RemoveNext on an empty queue asserts)
+    if (m_events->IsEmpty()) abort();
+    ProcessOneEvent();
+  }
   nsgpu_event_id Schedule(int64_t delay, EventImpl *event) {  // :188-204
     int64_t tAbsolute = delay + (int64_t)m_currentTs;
     if (tAbsolute < 0 || tAbsolute < (int64_t)m_currentTs) abort();  // NS_ASSERTs

@@ -49,6 +49,8 @@ void nsref_sim_remove(nsref_sim *s, const nsgpu_event_id *id) { s->Remove(*id); 
 void nsref_sim_cancel(nsref_sim *s, const nsgpu_event_id *id) { s->Cancel(*id); }
 int nsref_sim_is_expired(nsref_sim *s, const nsgpu_event_id *id) { return s->IsExpired(*id) ? 1 : 0; }
 void nsref_sim_run(nsref_sim *s) { s->Run(); }
+void nsref_sim_run_one(nsref_sim *s) { s->RunOneEvent(); }
+int nsref_sim_is_finished(nsref_sim *s) { return s->IsFinished() ? 1 : 0; }
 void nsref_sim_stop(nsref_sim *s) { s->m_stop = true; }
 void nsref_sim_stop_at(nsref_sim *s, int64_t delay) { s->Schedule(delay, new StopEvent(s)); }
 void nsref_sim_destroy(nsref_sim *s) { s->Destroy(); }

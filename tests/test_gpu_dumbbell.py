@@ -40,18 +40,21 @@ def test_dumbbell_compressed_routes_match_dense():
     assert_same_run(sc, o, gpu_full(sc, 20000, 20000))
 
 
-LEAVES = 4_095  # 8,192 nodes; the BASELINE size (499,999 per side) is DESIGN.md 4.3's open item
+LEAVES = 499_999  # the BASELINE size: 2 routers + 2 x 499,999 leaves = 1,000,000 nodes
 
 
 @pytest.fixture(scope="module")
 def million():
-    """A large config-5 dumbbell: 2 routers + 2 x 4,095 leaves = 8,192 nodes (compressed routes).
-    The dumbbell's two routers are hub nodes: a window holds up to WCAP of their events, which one
-    holder thread walks with the O(W) per-event slot scan, so run time grows with
-    the leaf count squared; the BASELINE's 1,000,000 nodes does not finish in a test's time yet
-    (65,536 nodes: 53 s on one MI355X, bit-exact)."""
+    """Config 5 at its BASELINE size: 1,000,000 nodes (compressed routes), 8.5 M events.  The oracle's
+    sequential run (counters and digest, no trace) takes ~1-20 s on one host core; the scenario's Python
+    build ~20 s."""
+    import nsref
     sc = p2p.dumbbell(LEAVES)
-    st, devc, appc, _log, _tr = oracle_full(sc, 0)
+    s = sc.c_struct()
+    st = p2p.P2PStats()
+    devc = np.zeros(s.n_devices, p2p.DEV_COUNTERS_DTYPE)
+    appc = np.zeros(s.n_apps, p2p.APP_COUNTERS_DTYPE)
+    nsref.p2p_run(s, st, devc, appc)
     return sc, st, devc, appc
 
 
@@ -62,16 +65,20 @@ def _same_counters(gst, gdevc, gappc, st, devc, appc):
     assert np.array_equal(gappc, appc)
 
 
-def test_dumbbell_large_single_gpu(million):
+def test_dumbbell_million_nodes_single_gpu(million):
+    """simple-distributed.cc at 1,000,000 nodes on one engine: the sequential counters and digest."""
     sc, st, devc, appc = million
-    assert sc.n_nodes == 2 * LEAVES + 2 and st.dispatched > 60_000
-    gst, gdevc, gappc, _ = p2p.Engine(sc).run()
+    assert sc.n_nodes == 1_000_000 and st.dispatched == 8_500_495
+    eng = p2p.Engine(sc)
+    gst, gdevc, gappc, _ = eng.run()
+    eng.close()
     _same_counters(gst, gdevc, gappc, st, devc, appc)
 
 
-def test_dumbbell_large_eight_partitions(million):
-    """Partitioned 8 ways (left side + router 1 on rank 0, router 2 and the right leaves over ranks
-    1-7) through the loopback group: the sequential counters and digest."""
+def test_dumbbell_million_nodes_eight_partitions(million):
+    """The same 1,000,000-node run partitioned 8 ways the way simple-distributed.cc assigns system ids
+    (left side + router 1 on rank 0, router 2 and the right leaves over ranks 1-7), all partitions on
+    one GPU through the loopback group: the sequential counters and digest."""
     sc, st, devc, appc = million
     grp = p2p.LoopbackGroup(sc, 8, owner=p2p.dumbbell_owner(LEAVES, 8))
     gst, gdevc, gappc, _ = grp.run()
