@@ -295,6 +295,11 @@ int nsgpu_p2p_results(nsgpu_p2p *h, nsgpu_p2p_stats *stats, nsgpu_dev_counters *
 int nsgpu_p2p_destroy(nsgpu_p2p *h);
 /* GPU time (ms, HIP events on the engine stream) of the last nsgpu_p2p_run. */
 int nsgpu_p2p_last_run_ms(nsgpu_p2p *h, double *gpu_ms);
+/* 1: the engine runs wide windows — bounded by the cross-node lookahead (min over devices of the smallest
+ * frame's tx time + channel delay), a same-node TransmitComplete before the window's end running inside
+ * it.  Single engines whose nodes have at most 16 devices, unless NSGPU_P2P_NARROW=1 was
+ * set when the engine was created. */
+int nsgpu_p2p_get_wide(nsgpu_p2p *h, int *wide);
 /* Launch mode of nsgpu_p2p_run: 0 = hipGraph replays (default), 1 = the same kernels launched one by
  * one (also selected by the environment variable NSGPU_P2P_EAGER; used under rocprofv3). */
 int nsgpu_p2p_set_eager(nsgpu_p2p *h, int eager);

@@ -57,6 +57,7 @@ constexpr int NSLOT = 7;         // per-node slot table entries
 constexpr int NTAB = NSLOT + 1;  // words per node table record (count + slots)
 constexpr int NWIN = 32;         // windows per graph replay
 constexpr uint32_t NOCTX = 0xffffffffu;
+constexpr uint32_t LOCALBIT = 0x80000000u;  // child record kind: run inside the window as a local record
 
 // Packet descriptor: flow (sending app), IPv4 identification (Ipv4L3Protocol::m_identification of
 // the originating node), size in bytes with the headers added so far, IPv4 TTL.
@@ -83,6 +84,7 @@ static_assert(sizeof(DevRec) == 128 && offsetof(DevRec, c) == 64, "DevRec is one
 struct Red {
   uint64_t tmin, wend, stopts;
   uint32_t stopuid, pad;
+  uint64_t wendw;  // the wide bound: min over pending of ts + lookw (cross-node lookahead; single engine)
 };
 
 // Device-resident run control (one per engine).  Every field is written by one kernel of the
@@ -113,6 +115,13 @@ struct Ctl {
   uint64_t hts, hrel;              // next host event (nsgpu_p2p_advance): ts (~0: none); the rel ts of the
   uint32_t huid, pad4;             //   window's last timestamp (W_end or the host event's); the host uid
   uint64_t pchild;                 // children of the last scanned window that stay pending (not inline)
+  // ---- wide windows (single engine, nsgpu_p2p_win.h): same-node TransmitCompletes run inside them ----
+  uint64_t lim_rel;   // a TransmitComplete child with rel ts < lim_rel is a local record of this window
+  uint64_t nbound;    // the narrow bound of the forming window (an overflowing wide window is trimmed to it)
+  uint64_t tn0;       // trace records before this window's handlers (the local records' uid patch)
+  uint64_t span_t;    // adaptive span target of wide windows (kept between the narrow and the wide bound)
+  uint32_t plt;       // local records of the last scanned window (lrec)
+  uint32_t renarrow;  // the overflowing window is wide: trim its sorted run to nbound (host step)
 };
 
 static_assert(offsetof(Ctl, prep) == offsetof(Ctl, W) + 12 && offsetof(Ctl, W) % 16 == 0, "the X0 payload");
@@ -135,6 +144,8 @@ struct P2PDev {
   const int32_t *sink_of_node;                    // PacketSink of each node (-1: none)
   uint32_t icmp;                                  // ICMP errors are generated (scenario icmp)
   int64_t lookahead[K_NKINDS];
+  int64_t lookw[K_NKINDS];  // wide windows: the smallest delay of a child that does not run in the window
+  uint32_t wide, pad_w;     // wide windows on (single engine)
   // model state
   DevRec *dev;  // per-device tx state + transmit parameters (one record per device)
   Pkt *q_buf;
@@ -205,6 +216,10 @@ struct P2PDev {
   uint32_t *s_val, *s_val2, *s_hist, *g_u32;
   Pkt *g_pkt;
   uint64_t *cmp_cnt;      // compaction: live entries written
+  // ---- wide windows: local records (same-node TransmitCompletes run inside the window) ----
+  uint32_t *wpar;         // local record: parent record | child index << 24
+  uint32_t *lcnt;         // local records per region this window (one region per holder / hub block)
+  uint32_t *lrec;         // the last scanned window's local records (dense list, C.plt of them)
 };
 
 // ---------------- wave / block helpers ----------------
@@ -267,24 +282,40 @@ struct Emit {
   uint64_t *ch_ts;
   uint32_t *ch_ctx, *ch_kind, *ch_a;
   Pkt *ch_pkt;
-  const int64_t *lookahead;
-  uint64_t tmn, wnd;
-  uint32_t uid;    // uid of the event being run (its trace records)
-  uint32_t trseq;  // trace sink calls made by it so far
-  bool demote;     // the event's ts group is cut by a run chunk: its DoForwardUp leaves are queued
+  const int64_t *lookahead, *lookw;
+  uint64_t tmn, wnd, wndw;
+  uint64_t lim_abs;  // wide window: a TransmitComplete child before it is a local record (0: none)
+  uint32_t uid;      // uid of the event being run (its trace records; LOCALBIT | record: a local record's)
+  uint32_t trseq;    // trace sink calls made by it so far
+  bool demote;       // the event's ts group is cut by a run chunk: its DoForwardUp leaves are queued
+  int32_t lj;        // the local child this event made (an event makes at most one TransmitComplete): its
+  uint32_t la, lctx; //   index (-1: none), device and context
+  uint64_t lts;
   __device__ __forceinline__ void child(int64_t delay, uint32_t ctx_, uint32_t kind, uint32_t a, Pkt p) {
     if (demote && kind == K_FWD_UP) kind = K_FWD_UP_D;
     const uint32_t s = slot0 + n++;
     const uint64_t ts = now + (uint64_t)delay;
+    // a same-node TransmitComplete inside a wide window runs in it (the node's holder takes it next)
+    const bool local = kind == K_TX_COMPLETE && ts < lim_abs;
     ch_ts[s] = ts;
     ch_ctx[s] = ctx_;
-    ch_kind[s] = kind;
+    ch_kind[s] = local ? (kind | LOCALBIT) : kind;
+    if (local) {
+      lj = (int32_t)(s - slot0);
+      lts = ts;
+      la = a;
+      lctx = ctx_;
+    }
     ch_a[s] = a;
     ch_pkt[s] = p;
-    if ((kind & 0xffu) != K_FWD_UP) {  // DoForwardUp is a leaf run inside the window, never re-queued
+    if ((kind & 0xffu) != K_FWD_UP && !local) {  // DoForwardUp is a leaf run inside the window, never re-queued
       tmn = ts < tmn ? ts : tmn;
       const uint64_t e = ts + (uint64_t)lookahead[kind & 0xffu];
       wnd = e < wnd ? e : wnd;
+      if (lookw) {  // (wide engines)
+        const uint64_t ew = ts + (uint64_t)lookw[kind & 0xffu];
+        wndw = ew < wndw ? ew : wndw;
+      }
     }
   }
 };
@@ -851,25 +882,45 @@ __device__ uint64_t g_blk_win = 1000;
 // Window bound of a pending set's reduction: packed key bound, span, Stop key.
 struct WinBound {
   uint64_t tmin, span, bound, stop_packed;
+  uint64_t nbound;  // the narrow bound (span = the narrow lookahead's)
+  uint64_t lim;     // local records: a TransmitComplete child with rel ts < lim runs in the window (0: none)
 };
-__device__ __forceinline__ WinBound window_bound(const Red &R) {
+// wide: the single engine's wide windows — the span is span_t clamped between the narrow bound (min over
+// pending of ts + lookahead) and the wide one (ts + lookw, nsgpu_p2p_create); a same-node TransmitComplete
+// before the window's end then runs inside it (local record).
+__device__ __forceinline__ WinBound window_bound(const Red &R, bool wide = false, uint64_t span_t = 0) {
   WinBound b;
   b.tmin = R.tmin;
   uint64_t span = R.wend - b.tmin;
   if (span > 0xfffffffeull) span = 0xfffffffeull;
+  const uint64_t nspan = span;
+  if (wide && R.tmin != ~0ull && R.wendw != ~0ull && R.wendw > R.wend) {
+    uint64_t wspan = R.wendw - b.tmin;
+    if (wspan > 0xfffffffeull) wspan = 0xfffffffeull;
+    span = span_t < wspan ? span_t : wspan;
+    span = span > nspan ? span : nspan;
+  }
   b.span = span;
   b.bound = (span << 32) | 0xffffffffull;
+  b.nbound = (nspan << 32) | 0xffffffffull;
+  // a local child at the window's end could tie with a cross-node child there: strictly before it
+  b.lim = span > nspan ? span : 0;
   b.stop_packed = ~0ull;
   if (R.stopts != ~0ull && R.stopts - b.tmin <= span) {
-    // Stop caps the window at its own key (it is dispatched; later events are not)
+    // Stop caps the window at its own key (it is dispatched; later events are not); a child at the Stop's
+    // ts sorts after it (a larger uid)
     b.stop_packed = ((R.stopts - b.tmin) << 32) | R.stopuid;
     b.bound = b.stop_packed < b.bound ? b.stop_packed : b.bound;
+    b.nbound = b.stop_packed < b.nbound ? b.stop_packed : b.nbound;
+    b.lim = (R.stopts - b.tmin) < b.lim ? (R.stopts - b.tmin) : b.lim;
   }
   return b;
 }
 __device__ __forceinline__ void publish_bound(Ctl &C, const WinBound &b) {
   C.tmin = b.tmin;
   C.bound = b.bound;
+  C.nbound = b.nbound;
+  C.lim_rel = b.lim;
   // zero-delay leaf children (Ipv4EndPoint::DoForwardUp) run inside the window; when the window ends
   // at the Stop event, those at the Stop's ts sort after it and are never dispatched
   const bool has_stop = b.stop_packed != ~0ull && b.bound >= b.stop_packed;
@@ -878,29 +929,34 @@ __device__ __forceinline__ void publish_bound(Ctl &C, const WinBound &b) {
 
 // Reduces (tmn, wnd) over the workgroup and one lane folds them into R (atomicMin): one atomic
 // pair per workgroup, not per wave (a word takes ~11 ns per atomic).  All threads must call it.
-template <int NTH>
-__device__ __forceinline__ void publish_min(Red &R, uint64_t tmn, uint64_t wnd) {
+// WIDE: the wide bound (wndw) as well.
+template <int NTH, bool WIDE = false>
+__device__ __forceinline__ void publish_min(Red &R, uint64_t tmn, uint64_t wnd, uint64_t wndw = ~0ull) {
   tmn = wave_min64(tmn);
   wnd = wave_min64(wnd);
+  if constexpr (WIDE) wndw = wave_min64(wndw);
   if constexpr (NTH > 64) {
-    __shared__ uint64_t s0[NTH / 64], s1[NTH / 64];
+    __shared__ uint64_t s0[NTH / 64], s1[NTH / 64], s2[NTH / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     __syncthreads();
     if (lane == 0) {
       s0[wid] = tmn;
       s1[wid] = wnd;
+      if constexpr (WIDE) s2[wid] = wndw;
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
     for (int w = 1; w < NTH / 64; w++) {
       tmn = s0[w] < tmn ? s0[w] : tmn;
       wnd = s1[w] < wnd ? s1[w] : wnd;
+      if constexpr (WIDE) wndw = s2[w] < wndw ? s2[w] : wndw;
     }
   } else if ((threadIdx.x & 63) != 0) {
     return;
   }
   if (tmn != ~0ull) atomicMin((unsigned long long *)&R.tmin, (unsigned long long)tmn);
   if (wnd != ~0ull) atomicMin((unsigned long long *)&R.wend, (unsigned long long)wnd);
+  if (WIDE && wndw != ~0ull) atomicMin((unsigned long long *)&R.wendw, (unsigned long long)wndw);
 }
 
 // A pending event in registers.
@@ -917,13 +973,15 @@ struct X1Hdr {
   uint32_t W, tc, tinl, needc;  // window events, their children, their inline children; pool compaction wanted
   uint64_t pad0, lastkey;     // largest window key
   Red red;                    // reduction of this rank's pending set after the window (next LBTS)
-  uint64_t pad2[8];
+  uint64_t pad2[7];
 };
+static_assert(sizeof(X1Hdr) == 128, "X1 records: the loopback transport copies 16-byte words");
 struct X1Ent {  // one window event: key and child counts (children | inline children << 16)
   uint64_t key;
   uint32_t cnt, pad;
 };
 constexpr size_t X1B = sizeof(X1Hdr) + sizeof(X1Ent) * WCAP;
+static_assert(X1B % 16 == 0, "k_copies moves 16-byte words");
 // X2: remote events for one peer (children whose node another rank owns), all-to-all; the record is
 // the pending event itself, uid included (mpi-interface.cc:414-506 sends {rx ns, node, dev, packet}).
 struct X2Hdr {
@@ -1303,7 +1361,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   if (threadIdx.x != 0) return;
   uint32_t Wg = 0, tcg = 0, needc = 0;
   uint64_t lk = 0;
-  Red rg{~0ull, ~0ull, ~0ull, 0, 0};
+  Red rg{~0ull, ~0ull, ~0ull, 0, 0, ~0ull};
   for (uint32_t q = 0; q < M.nranks; q++) {
     const X1Hdr *h = x1hdr(M.x1_recv, q);
     Wg += h->W;
@@ -1352,7 +1410,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   X1Hdr *hs = x1hdr(M.x1_send, 0);
   hs->W = hs->tc = hs->tinl = hs->needc = 0;
   hs->lastkey = 0;
-  hs->red.tmin = hs->red.wend = hs->red.stopts = ~0ull;
+  hs->red.tmin = hs->red.wend = hs->red.stopts = hs->red.wendw = ~0ull;
   hs->red.stopuid = 0;
 }
 
@@ -1622,6 +1680,29 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   // schedules): the window must then end at the delivering Receive's time, so that the DoForwardUp is
   // the next window's first event at that time.
   if (has_echo) M.lookahead[K_RECEIVE] = 0;
+  // Wide windows (single engine, nsgpu_p2p_win.h): an event on another node is at least one transmission
+  // plus its channel delay away — Lx = min over devices of (smallest frame's tx time + delay) — and a
+  // same-node TransmitComplete before the window's end runs inside the window (a local record), so only
+  // the children that are neither bound the window: lookw = lookahead with tx_min replaced by Lx.
+  int64_t lx = INFL;
+  if (min_pkt != 0xffffffffu)
+    for (uint32_t d = 0; d < D; d++) {
+      int64_t t = seconds_to_ts(static_cast<double>(min_pkt + 30) * 8 / (double)sc->dev_bps[d]);
+      if (sc->icmp) t = std::min(t, seconds_to_ts(static_cast<double>(56 + 2) * 8 / (double)sc->dev_bps[d]));
+      lx = std::min(lx, t + sc->dev_delay_ns[d]);
+    }
+  for (int k = 0; k < K_NKINDS; k++) M.lookw[k] = M.lookahead[k];
+  M.lookw[K_SEND] = std::min(std::min(lx, send_ivl), echo_ivl);
+  M.lookw[K_TX_COMPLETE] = lx;
+  M.lookw[K_RECEIVE] = has_echo ? 0 : lx;
+  M.lookw[K_FWD_UP_Q] = lx;
+  {  // a node's pending local records are its busy devices' TransmitCompletes: at most its degree
+    std::vector<uint32_t> deg(N, 0);
+    uint32_t dmax = 0;
+    for (uint32_t d = 0; d < D; d++) dmax = std::max(dmax, ++deg[sc->dev_node[d]]);
+    const char *nw = getenv("NSGPU_P2P_NARROW");
+    M.wide = (!owner && dmax <= (uint32_t)LQ && lx > tx_min && lx < INFL && !(nw && nw[0] == '1')) ? 1u : 0u;
+  }
   // ---- scenario upload ----
   TRY(dupload(h, &M.dev_node, sc->dev_node, D));
   if (sc->route) {
@@ -1727,10 +1808,11 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     uid++;
   }
   // reduction of the whole initial pending set: window 0 is bounded by red[1] on every rank
-  Red red0{~0ull, ~0ull, ~0ull, 0, 0};
+  Red red0{~0ull, ~0ull, ~0ull, 0, 0, ~0ull};
   for (size_t i = 0; i < its.size(); i++) {
     red0.tmin = std::min<uint64_t>(red0.tmin, its[i]);
     red0.wend = std::min<uint64_t>(red0.wend, its[i] + (uint64_t)M.lookahead[ikind[i] & 0xffu]);
+    red0.wendw = std::min<uint64_t>(red0.wendw, its[i] + (uint64_t)M.lookw[ikind[i] & 0xffu]);
     if ((ikind[i] & 0xffu) == K_STOP) {
       red0.stopts = its[i];
       red0.stopuid = iuid[i];
@@ -1758,14 +1840,14 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.ev_a[b], M.pool_cap));
     TRY(dalloc(h, &M.ev_pkt[b], M.pool_cap));
   }
-  const size_t chn = (size_t)WCAP * M.maxc;
+  const size_t chn = (size_t)WTOT * M.maxc;  // children of gen-0 and local records
   TRY(dalloc(h, &M.ch_ts, chn));
   TRY(dalloc(h, &M.ch_ctx, chn));
   TRY(dalloc(h, &M.ch_kind, chn));
   TRY(dalloc(h, &M.ch_a, chn));
   TRY(dalloc(h, &M.ch_pkt, chn));
   // window records: a whole sorted run (single engine), a whole window before its cut (partitioned)
-  M.fcap = chn;
+  M.fcap = (size_t)NMAX * M.maxc;  // children parked in one window: at most every record's
   M.runcap = M.pool_cap + M.fcap;
   if (M.runcap >= 0xffffffffull) {
     nsgpu_p2p_destroy(h);
@@ -1774,10 +1856,16 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.wkey, M.runcap));
   TRY(dalloc(h, &M.wpkt, M.runcap));
   for (uint32_t **p : {&M.wctx, &M.wkind, &M.wa}) TRY(dalloc(h, p, M.runcap));
-  TRY(dalloc(h, &M.pwkey, WCAP));
-  TRY(dalloc(h, &M.sinfo, WCAP));
-  for (uint32_t **p : {&M.widx, &M.nchild, &M.ninl, &M.pwctx}) TRY(dalloc(h, p, WCAP));
-  TRY(dalloc(h, &M.wrank, WCAP));
+  TRY(dalloc(h, &M.pwkey, WTOT));
+  TRY(dalloc(h, &M.sinfo, WTOT));
+  TRY(dalloc(h, &M.widx, WCAP));
+  for (uint32_t **p : {&M.nchild, &M.ninl, &M.pwctx, &M.wrank, &M.wpar}) TRY(dalloc(h, p, WTOT));
+  TRY(dalloc(h, &M.lcnt, NLR));
+  TRY(dalloc(h, &M.lrec, NMAX));  // (k2_pa loads lrec[k] speculatively: zeroed, every entry stays < WTOT)
+  if (hipMemset(M.lrec, 0, NMAX * sizeof(uint32_t)) != hipSuccess || hipMemset(M.lcnt, 0, NLR * sizeof(uint32_t)) != hipSuccess) {
+    nsgpu_p2p_destroy(h);
+    return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipMemset failed");
+  }
   // in-place pool, fresh buffer, free stack, hub blocks, compaction; radix sort scratch (single engine)
   TRY(dalloc(h, &M.wsrc, M.runcap));
   TRY(dalloc(h, &M.f_ts, M.fcap));
@@ -1823,7 +1911,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.gacc, 4 * (size_t)WCAP));
     h->comm = comm;
     memset(&h->x1h0, 0, sizeof(X1Hdr));
-    h->x1h0.red.tmin = h->x1h0.red.wend = h->x1h0.red.stopts = ~0ull;
+    h->x1h0.red.tmin = h->x1h0.red.wend = h->x1h0.red.stopts = h->x1h0.red.wendw = ~0ull;
   }
   TRY(dalloc(h, &M.C, 1));
   if (owner) M.x0_send = reinterpret_cast<uint64_t *>(&M.C->W);  // X0 sends (W, nxtP, overflow, prep)
@@ -1850,7 +1938,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   C0.uid = uid;
   // reduction of the initial pool: window 0 is bounded by red[1] (k2_pa / k2_handle fold later
   // pending sets in for the next windows)
-  C0.red[0].tmin = C0.red[0].wend = C0.red[0].stopts = ~0ull;
+  C0.red[0].tmin = C0.red[0].wend = C0.red[0].stopts = C0.red[0].wendw = ~0ull;
   C0.red[0].stopuid = 0;
   C0.red[1] = red0;
   C0.max_windows = h->max_windows;
@@ -1859,6 +1947,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   C0.hts = ~0ull;                 // no host closure pending (nsgpu_p2p_advance sets one)
   C0.hrel = ~0ull;
   C0.rt = 0;                      // window 0 is bounded by red[1] and folds into red[0]
+  C0.span_t = ~0ull >> 2;         // wide windows start at their widest (adapted to the capacity)
   if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
     h->s = nullptr;
     nsgpu_p2p_destroy(h);
@@ -1926,7 +2015,8 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.app_last_start, 0, A * sizeof(uint64_t), s));
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
   NSGPU_HIP(hipMemsetAsync(M.node_tab, 0, (size_t)M.n_nodes * NTAB * sizeof(uint32_t), s));
-  NSGPU_HIP(hipMemsetAsync(M.wrank, 0, WCAP * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(M.wrank, 0, WTOT * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(M.lcnt, 0, NLR * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
   if (M.dist) {
     const size_t R = M.nranks;
@@ -1951,15 +2041,31 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
 
 // The window pipeline, in launch order (graph capture, eager runs and the per-kernel profile).
 namespace {
-constexpr int NKERN = 3;
-const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_scan"};
+constexpr int NKERN = 4;
+const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_scan", "k_tpatch"};
 // ev0 / ev1: optional HIP events the command processor records at the kernel's start and end
 // (hipExtLaunchKernelGGL: no separate marker packets between the pipeline's kernels).
-void launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+// Kernel k of the single engine's window (KERNEL_NAMES); a traced wide engine patches the local records'
+// trace uids (k_tpatch).  Returns whether kernel k is part of this engine's window.
+bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+  const bool wide = h->M.wide != 0;
   switch (k) {
-    case 0: hipExtLaunchKernelGGL(k2_pa<false>, dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M); break;
-    case 1: hipExtLaunchKernelGGL(k2_handle, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M); break;
-    default: hipExtLaunchKernelGGL(k2_scan, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M); break;
+    case 0:
+      if (wide) hipExtLaunchKernelGGL((k2_pa<false, true>), dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M);
+      else hipExtLaunchKernelGGL((k2_pa<false, false>), dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M);
+      return true;
+    case 1:
+      if (wide) hipExtLaunchKernelGGL(k2_handle<true>, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M);
+      else hipExtLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M);
+      return true;
+    case 2:
+      if (wide) hipExtLaunchKernelGGL(k2_scan<true>, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
+      else hipExtLaunchKernelGGL(k2_scan<false>, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
+      return true;
+    default:
+      if (!(wide && h->M.trace)) return false;
+      hipExtLaunchKernelGGL(k_tpatch, dim3(64), dim3(256), 0, s, ev0, ev1, 0, h->M);
+      return true;
   }
 }
 void launch_windows(nsgpu_p2p *h, hipStream_t s) {
@@ -2005,6 +2111,7 @@ static int host_step(nsgpu_p2p *h, const Ctl &c, hipStream_t s) {
       hipLaunchKernelGGL(k_rs_gather<Pkt>, dim3(gg), dim3(256), 0, s, vin, M.wpkt, M.g_pkt, n);
       NSGPU_HIP(hipMemcpyAsync(M.wpkt, M.g_pkt, n * sizeof(Pkt), hipMemcpyDeviceToDevice, s));
     }
+    if (c.renarrow) hipLaunchKernelGGL(k_renarrow, dim3(1), dim3(1024), 0, s, M);  // (a widened window)
     hipLaunchKernelGGL(k_after_sort, dim3(1), dim3(1), 0, s, M);
     NSGPU_HIP(hipGetLastError());
   } else if (c.mode == MODE_COMPACT) {
@@ -2033,9 +2140,9 @@ static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s, int nwin = NWIN) {
   ncclComm_t comm = h->comm->comm;
   const P2PDev &M = h->M;
   for (int w = 0; w < nwin; w++) {
-    hipLaunchKernelGGL(k2_pa<true>, dim3(GRID_POOL), dim3(TB), 0, s, M);
+    hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL), dim3(TB), 0, s, M);
     NCCL_TRY(ncclAllGather(M.x0_send, M.x0_recv, X0B, ncclUint8, comm, s));
-    hipLaunchKernelGGL(k2_handle, dim3(K2_GRID), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, M);
     NCCL_TRY(ncclAllGather(M.x1_send, M.x1_recv, X1B, ncclUint8, comm, s));
     hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, M);
     hipLaunchKernelGGL(k_dfin2, dim3(NHB), dim3(HB), 0, s, M);
@@ -2436,12 +2543,13 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
   if (rc == NSGPU_OK && (hipEventRecord(h->ev[0], cs) != hipSuccess || hipStreamWaitEvent(h->s, h->ev[0], 0) != hipSuccess))
     rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: stream join failed");
   int ns = 0;
+  bool used[NKERN] = {};  // the engine's window launches kernel k (its events are recorded)
   // the run control is read after every window (so no sampled pass is a paused no-op and the
   // host-driven steps run as soon as the pipeline asks)
   for (uint64_t w = 0; rc == NSGPU_OK; w++) {
     const bool sample = (w % sample_every) == 0 && ns < NS;
     for (int k = 0; k < NKERN; k++) {
-      if (sample) launch_kernel(h, k, h->s, ev[(2 * ns) * NKERN + k], ev[(2 * ns + 1) * NKERN + k]);
+      if (sample) used[k] = launch_kernel(h, k, h->s, ev[(2 * ns) * NKERN + k], ev[(2 * ns + 1) * NKERN + k]);
       else launch_kernel(h, k, h->s);
     }
     if (sample) ns++;
@@ -2461,7 +2569,7 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
     for (int i = 0; i < ns; i++)
       for (int k = 0; k < NKERN; k++) {
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, ev[(2 * i) * NKERN + k], ev[(2 * i + 1) * NKERN + k]) == hipSuccess) {
+        if (used[k] && hipEventElapsedTime(&ms, ev[(2 * i) * NKERN + k], ev[(2 * i + 1) * NKERN + k]) == hipSuccess) {
           kernel_ms[k] += ms;
           launches[k]++;
         }
@@ -2472,6 +2580,13 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
   (void)hipEventRecord(h->ev[0], h->s);
   (void)hipStreamWaitEvent(cs, h->ev[0], 0);
   return rc;
+}
+
+// Whether the engine runs wide windows (single engine, node degree <= LQ, not NSGPU_P2P_NARROW=1).
+extern "C" int nsgpu_p2p_get_wide(nsgpu_p2p *h, int *wide) {
+  if (!h || !wide) return set_error(NSGPU_EINVAL, "nsgpu_p2p_get_wide: null");
+  *wide = h->M.wide ? 1 : 0;
+  return NSGPU_OK;
 }
 
 extern "C" int nsgpu_p2p_last_run_ms(nsgpu_p2p *h, double *gpu_ms) {
@@ -2537,9 +2652,9 @@ struct nsgpu_p2p_group {
 static void launch_windows_group(nsgpu_p2p_group *g, hipStream_t s, int nwin = NWIN) {
   const unsigned n = (unsigned)g->m.size();
   for (int w = 0; w < nwin; w++) {
-    for (auto *h : g->m) hipLaunchKernelGGL(k2_pa<true>, dim3(GRID_POOL), dim3(TB), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL), dim3(TB), 0, s, h->M);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[0]);
-    for (auto *h : g->m) hipLaunchKernelGGL(k2_handle, dim3(K2_GRID), dim3(HB), 0, s, h->M);
+    for (auto *h : g->m) hipLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, h->M);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[1]);
     for (auto *h : g->m) hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, h->M);
     for (auto *h : g->m) hipLaunchKernelGGL(k_dfin2, dim3(NHB), dim3(HB), 0, s, h->M);

@@ -29,7 +29,34 @@ constexpr uint32_t NOSRC = 0xffffffffu;
 constexpr int NHUB = 32;                // hub blocks of k2_handle
 constexpr int NMB = 128;                // maintenance blocks of k2_handle
 constexpr int MAXHUB = WCAP / (CH + 1) + 1;
-constexpr int K2_GRID = NHB + NRB + NHUB + NMB;
+constexpr int K2_GRID_W = NHB + NHUB + NMB;  // holders, hub blocks, pool maintenance
+constexpr int K2_GRID = K2_GRID_W + NRB;       // + rank tiles (single engine; partitioned: k_gtile ranks)
+// ---- wide windows: local records (a node's same-node TransmitCompletes run inside the window) ----
+constexpr int LQ = 16;                   // a node's pending local records: its busy devices' (degree <= LQ)
+constexpr int LR = 128;                  // local records of one holder block per window (its region)
+constexpr int LRH = 512;                 // ... of one hub block
+constexpr int NLR = NHB + NHUB;          // regions: holder blocks, then hub blocks
+constexpr uint32_t LBASE = WCAP;         // local records live at [LBASE, LBASE + LCAP) of the record arrays
+constexpr int LCAP = NHB * LR + NHUB * LRH;
+constexpr int WTOT = WCAP + LCAP;        // record index space (gen-0 slots + local regions)
+constexpr int NMAX = 8192;               // records of one window, gen-0 + local (k2_scan's LDS capacity)
+constexpr int SLOTG = WCAP + NMAX;       // k2_pa's slot-role threads (single engine): gen-0 slots, then local
+static_assert(LCAP < (1 << 24) && WTOT < (1 << 24), "wpar packs a record index in 24 bits");
+__device__ __forceinline__ uint32_t region_base(uint32_t r) {
+  return LBASE + (r < (uint32_t)NHB ? r * LR : NHB * LR + (r - NHB) * LRH);
+}
+// Dense record d of a window of W gen-0 records and local regions with prefix pre[] (NLR + 1 entries).
+__device__ __forceinline__ uint32_t dense_rec(uint32_t d, uint32_t W, const uint32_t *pre) {
+  if (d < W) return d;
+  const uint32_t k = d - W;
+  uint32_t lo = 0, hi = NLR;  // the region r with pre[r] <= k < pre[r + 1]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= k) lo = mid;
+    else hi = mid;
+  }
+  return region_base(lo) + (k - pre[lo]);
+}
 
 // Node-part result of one hub event (k2_handle hub blocks, between the two passes).
 struct HubEv {
@@ -149,9 +176,10 @@ __device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t
 // A pending event against the window bound: window record (normal mode, key <= bound), else pending:
 // a child (src == NOSRC) is parked in the fresh buffer, a pool entry stays where it is; both fold
 // into the next window's reduction.
+template <bool WIDE>
 __device__ __forceinline__ void k2_classify(const P2PDev &M, const WinBound &b, bool run, bool valid, const Ev &e,
-                                            uint32_t src, Red &R, uint64_t &tmn, uint64_t &wnd, bool &in,
-                                            bool &park) {
+                                            uint32_t src, Red &R, uint64_t &tmn, uint64_t &wnd, uint64_t &wndw,
+                                            bool &in, bool &park) {
   const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
   in = valid && !run && (e.ts - b.tmin <= b.span) && pk <= b.bound;
   park = valid && !in && src == NOSRC;
@@ -159,6 +187,10 @@ __device__ __forceinline__ void k2_classify(const P2PDev &M, const WinBound &b, 
     tmn = e.ts < tmn ? e.ts : tmn;
     const uint64_t x = e.ts + (uint64_t)M.lookahead[e.kind & 0xffu];
     wnd = x < wnd ? x : wnd;
+    if constexpr (WIDE) {
+      const uint64_t xw = e.ts + (uint64_t)M.lookw[e.kind & 0xffu];
+      wndw = xw < wndw ? xw : wndw;
+    }
     if ((e.kind & 0xffu) == K_STOP) {  // at most one Stop event is pending
       R.stopts = e.ts;
       R.stopuid = e.uid;
@@ -235,8 +267,10 @@ __device__ __forceinline__ void block_alloc2(Ctl &C, uint32_t nw, uint32_t nf, u
 // X2), the remote events the last X2 brought are classified like children (a role of whole blocks
 // after the slot blocks), the rank's reduction goes to its X1 summary, and a window the host cut
 // (k_cut2: C.prep) is already formed.
-template <bool DIST>
+// WIDE: the single engine's wide windows (the last window's local records are appended too).
+template <bool DIST, bool WIDE>
 __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
+  static_assert(!(DIST && WIDE), "wide windows are the single engine's");
   PH_BEGIN();
   BLK_T0();
   Ctl &C = *M.C;
@@ -244,22 +278,29 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const uint64_t c_win = C.windows;
 #endif
   const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
-  const bool slot_role = g < (uint64_t)WCAP;  // (roles are block-uniform)
+  // slot role: one thread per record of the last window — its gen-0 slots, then (single engine) its local
+  // records (the dense list lrec); (roles are block-uniform)
+  constexpr uint32_t NSG = WIDE ? (uint32_t)SLOTG : (uint32_t)WCAP;
+  const bool slot_role = g < (uint64_t)NSG;
   const uint32_t rrb = DIST ? (M.nranks * M.capx + TB - 1) / TB : 0u;  // remote-event blocks
-  const bool remote_role = DIST && !slot_role && blockIdx.x < (uint32_t)(WCAP / TB) + rrb;
+  const bool remote_role = DIST && !slot_role && blockIdx.x < NSG / TB + rrb;
   // Everything this kernel reads of the run control and of the last window's slot, loaded at once:
   // these lines were written by k2_scan on another XCD, so every dependent level is a trip to memory.
   // (The slot arrays are WCAP long: a slot past the last window's size is loaded and ignored.)
   const uint32_t c_done = C.done, c_mode = C.mode, rt = C.rt, c_pvalid = C.pvalid, c_pW = C.pW, c_huid = C.huid;
-  const uint32_t uid0 = C.puid0;
+  const uint32_t uid0 = C.puid0, c_plt = WIDE ? C.plt : 0u;
   const Red red0 = C.red[0], red1 = C.red[1];
   const uint64_t hts = C.hts, c_ptmin = C.ptmin, K0 = C.pK0, ilim = C.pinline_lim, c_P = C.P_end;
+  const uint64_t c_span_t = WIDE ? C.span_t : 0;
   uint64_t spk = 0;
   uint4 si = make_uint4(0, 0, 0, 0);
   uint32_t ncr = 0, sctx = 0;
   Ev ce[PFC];
+  // the record this slot-role thread appends: gen-0 slot g, or local record lrec[g - WCAP] (lrec holds
+  // record indices from earlier windows past C.plt: loaded speculatively, always in range)
+  const uint32_t rec = (WIDE && g >= (uint64_t)WCAP && slot_role) ? M.lrec[g - WCAP] : (uint32_t)g;
   if (slot_role) {  // the slot and its first children
-    const uint32_t s = (uint32_t)g;
+    const uint32_t s = rec;
     spk = M.pwkey[s];
     si = M.sinfo[s];
     ncr = M.nchild[s];
@@ -279,7 +320,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const bool run = c_mode == MODE_RUN;
   const bool partition = c_done == 0;
   Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[rt];
-  WinBound b = window_bound(rt ? red0 : red1);
+  WinBound b = window_bound(rt ? red0 : red1, WIDE && !run, c_span_t);
   // a pending host closure (nsgpu_p2p_advance) cuts the window at its key, like Simulator::Stop: the
   // window holds the device events before it, and the pipeline pauses for the host after the window
   bool hcap = false;
@@ -287,6 +328,8 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   if (hts != ~0ull && !run) {
     if (hts < b.tmin || b.tmin == ~0ull) {
       b.bound = 0;  // (every device key is >= 4: uids start at 4)
+      b.nbound = 0;
+      b.lim = 0;
       hcap = true;
     } else if (hts - b.tmin <= b.span) {
       const uint64_t hk = ((hts - b.tmin) << 32) | c_huid;
@@ -294,11 +337,14 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
         b.bound = hk;
         hcap = true;
         hrel = hts - b.tmin;
+        b.nbound = hk < b.nbound ? hk : b.nbound;
+        b.lim = hrel < b.lim ? hrel : b.lim;  // (a child at the host event's ts sorts after it)
       }
     }
   }
   if (!run && partition && g == 0) {
     publish_bound(C, b);
+    if (WIDE && M.trace) C.tn0 = *M.trace_n;  // (the local records' trace uids are patched from here on)
     // the window's last timestamp (W_end, or the host event's): other children of this window can land
     // there with smaller uids than a DoForwardUp leaf its events schedule, so those leaves are queued
     // (K_FWD_UP_D), not run inline; a leaf of an earlier timestamp has every same-time event in the window
@@ -310,11 +356,11 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   }
   const uint32_t pW = c_pvalid ? c_pW : 0;
   PH_MARK(0);
-  uint64_t tmn = ~0ull, wnd = ~0ull, digest = 0;
+  uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull, digest = 0;
   if (slot_role) {
-    // ---- slot g of the last window: dispatch rank (log, digest), inline children, children -> pending
-    const bool vs = g < pW;
-    const uint32_t s = (uint32_t)g;
+    // ---- record `rec` of the last window: dispatch rank (log, digest), inline children, children -> pending
+    const bool vs = g < (uint64_t)WCAP ? g < pW : (c_pvalid && g - WCAP < c_plt);
+    const uint32_t s = rec;
     const uint64_t rel = spk >> 32;
     const uint64_t t = c_ptmin + rel;
     BLK_MARK(34, c_win);  // bound, publish_bound
@@ -359,11 +405,11 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
               }
               ii++;
             }
-          } else {  // (partitioned: a child on another rank's node goes there through X2)
+          } else if (!WIDE || !(e.kind & LOCALBIT)) {  // (partitioned: a child on another rank's node goes there through X2)
             valid = partition && (!DIST || M.owner[e.ctx] == M.rank);
-          }
+          }  // (a local record's child ran in the last window itself)
         }
-        k2_classify(M, b, run, valid, e, NOSRC, R, tmn, wnd, gin[q], gpk[q]);
+        k2_classify<WIDE>(M, b, run, valid, e, NOSRC, R, tmn, wnd, wndw, gin[q], gpk[q]);
         ge[q] = e;
         cw += gin[q];
         cf += gpk[q];
@@ -390,7 +436,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
       if (valid) e = x2rec(M, M.x2_recv, q)[rec];
       bool gin, gpk;
-      k2_classify(M, b, false, valid, e, NOSRC, R, tmn, wnd, gin, gpk);
+      k2_classify<WIDE>(M, b, false, valid, e, NOSRC, R, tmn, wnd, wndw, gin, gpk);
       uint32_t w0;
       uint64_t f0;
       block_alloc2<TB>(C, gin, gpk, w0, f0);
@@ -402,7 +448,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     // blocks past the pool's end do nothing (no atomics).
     constexpr int PPT = 4;
     const uint64_t P = c_P;
-    const uint64_t pb = blockIdx.x - (uint64_t)(WCAP / TB + rrb), npb = gridDim.x - (uint64_t)(WCAP / TB + rrb);
+    const uint64_t pb = blockIdx.x - (uint64_t)(NSG / TB + rrb), npb = gridDim.x - (uint64_t)(NSG / TB + rrb);
     for (uint64_t c0 = pb * TB * PPT; c0 < P; c0 += npb * TB * PPT) {  // block-uniform trip count
       Ev ge[PPT];
       bool gin[PPT], gpk[PPT];
@@ -419,7 +465,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 #pragma unroll
       for (int q = 0; q < PPT; q++) {
         const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
-        k2_classify(M, b, false, ge[q].ts != TOMB, ge[q], (uint32_t)i, R, tmn, wnd, gin[q], gpk[q]);
+        k2_classify<WIDE>(M, b, false, ge[q].ts != TOMB, ge[q], (uint32_t)i, R, tmn, wnd, wndw, gin[q], gpk[q]);
         cw += gin[q];
         if (gin[q]) {  // the window entry's record (its loads overlap the block allocation below)
           ge[q].ctx = M.ev_ctx[0][i];
@@ -441,7 +487,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     // ---- the next chunk of the sorted run: per-node slot tables, chunk bounds
     const uint64_t r0 = C.r0, rW = C.rW;
     const uint32_t Wc = (uint32_t)(rW - r0 < (uint64_t)WCAP ? rW - r0 : (uint64_t)WCAP);
-    const uint64_t s = g - WCAP;
+    const uint64_t s = g - NSG;
     if (s == 0) {
       C.W = Wc;
       C.wbase = (uint32_t)r0;
@@ -457,7 +503,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   }
   PH_MARK(1);
   if (slot_role) BLK_MARK(42, c_win);
-  publish_min<TB>(R, tmn, wnd);
+  publish_min<TB, WIDE>(R, tmn, wnd, wndw);
   digest = wave_sum64(digest);
   {  // one digest atomic per block
     __shared__ uint64_t s_dg[TB / 64];
@@ -477,22 +523,73 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 // ---- k2_handle: holders ----
 // The roles of k2_handle's blocks share one LDS buffer (holders: per-thread sort lists; hub blocks:
 // the hub's list), so that every block of the launch is resident at once.
-constexpr int K2_LDS_WORDS = HB * CH * 3;  // 12 KB: >= HUBL * 3 words
+constexpr int K2_LDS_WORDS = HB * CH * 3;                // holders: sort lists (12 KB; >= HUBL * 3)
+constexpr int K2_LDS_WORDS_W = K2_LDS_WORDS + HB * LQ * 2;  // wide engines: + local queues (20 KB)
 static_assert(HUBL * 3 <= K2_LDS_WORDS, "hub list does not fit the shared buffer");
 // Run control a window kernel reads, loaded once at its entry (all fields at once: one memory trip).
 struct HCtl {
   uint64_t tmin, inline_lim, slo, shi;
+  uint64_t lim;  // wide window: a TransmitComplete child with rel ts < lim is a local record (0: none)
 };
 // Slot i0's window record, loaded ahead (speculatively at base 0; reloaded for a run chunk).
 struct SlotPre {
   uint32_t widx, ctx, kind, a;
   uint64_t key;
 };
+
+// The local record of child E.lj of record `par` (a same-node TransmitComplete inside a wide window, marked
+// LOCALBIT by Emit::child): slot k of the caller's region (counter *cnt: LDS, shared by a holder block's
+// threads, or a hub block's lane 0), written like a window record; its key holds the rel ts (its uid is
+// assigned by k2_scan: uid0 + the parent's child prefix + j).  NOSRC: the region is full (error 32).
+__device__ __forceinline__ uint32_t local_record(const P2PDev &M, const Emit &E, uint32_t par, uint64_t tmin,
+                                                 uint32_t region, uint32_t *cnt, bool atomic) {
+  const uint32_t cap = region < (uint32_t)NHB ? (uint32_t)LR : (uint32_t)LRH;
+  const uint32_t k = atomic ? atomicAdd(cnt, 1u) : (*cnt)++;
+  if (k >= cap) {
+    atomicOr(M.error, 32u);
+    return NOSRC;
+  }
+  const uint32_t rec = region_base(region) + k;
+  M.wkey[rec] = ((E.lts - tmin) << 32) | 0xffffffffull;
+  M.wctx[rec] = E.lctx;
+  M.wkind[rec] = K_TX_COMPLETE;
+  M.wa[rec] = E.la;
+  M.wpkt[rec] = Pkt{0, 0, 0, 0};
+  M.wpar[rec] = par | ((uint32_t)E.lj << 24);
+  return rec;
+}
+// A node's pending local records, sorted by rel ts (ties: creation order = the parents' order); head qh.
+__device__ __forceinline__ void lq_push(const P2PDev &M, uint32_t *qrel, uint32_t *qrec, uint32_t stride, uint32_t &qh,
+                                        uint32_t &nq, uint32_t rel, uint32_t rec) {
+  if (nq == (uint32_t)LQ && qh > 0) {  // compact the consumed head away
+    for (uint32_t i = qh; i < nq; i++) {
+      qrel[(i - qh) * stride] = qrel[i * stride];
+      qrec[(i - qh) * stride] = qrec[i * stride];
+    }
+    nq -= qh;
+    qh = 0;
+  }
+  if (nq == (uint32_t)LQ) {
+    atomicOr(M.error, 32u);
+    return;
+  }
+  uint32_t p = nq;
+  while (p > qh && qrel[(p - 1) * stride] > rel) {
+    qrel[p * stride] = qrel[(p - 1) * stride];
+    qrec[p * stride] = qrec[(p - 1) * stride];
+    p--;
+  }
+  qrel[p * stride] = rel;
+  qrec[p * stride] = rec;
+  nq++;
+}
+
+template <bool WIDE>
 __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i0, uint32_t W, uint32_t base, Red &R,
-                                             uint32_t *lds, const HCtl &hc, SlotPre sp) {
+                                             uint32_t *lds, const HCtl &hc, SlotPre sp, uint32_t *lcnt_sh) {
   uint32_t *chs = lds;
   uint64_t *chk = reinterpret_cast<uint64_t *>(lds + HB * CH);
-  uint64_t tmn = ~0ull, wnd = ~0ull;
+  uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull;
   HStat hs{0, 0, 0, 0, false};
   if (base != 0 && i0 < W) {
     sp.ctx = M.wctx[base + i0];
@@ -551,14 +648,24 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
       E.ch_a = M.ch_a;
       E.ch_pkt = M.ch_pkt;
       E.lookahead = M.lookahead;
+      E.lookw = WIDE ? M.lookw : nullptr;
       E.tmn = ~0ull;
       E.wnd = ~0ull;
-      uint32_t ts0_it = 0, pending = 0;
+      E.wndw = ~0ull;
+      E.lim_abs = WIDE && hc.lim ? tmin + hc.lim : 0;
+      // the node's events in key order: its gen-0 window events (sorted above) merged with the local records
+      // its own TransmitStarts make (a gen-0 event first at equal ts: its uid is older)
+      uint32_t *qrel = lds + HB * CH * 3 + threadIdx.x, *qrec = qrel + HB * LQ;
+      uint32_t qh = 0, nq = 0, it = 0, ts0_it = 0, pending = 0;
       uint64_t cur_rel = 0;
-      for (uint32_t it = 0; it <= n; it++) {
-        const uint64_t rel = it < n ? (mk[it] >> 32) : ~0ull;
-        if (it > 0 && rel > cur_rel && pending) {
-          // flush the inline children of this node's events at cur_rel (positions [ts0_it, it))
+      bool started = false;
+      for (;;) {
+        const bool hg = it < n, hl = WIDE && qh < nq;
+        const uint64_t relg = hg ? (mk[it] >> 32) : ~0ull;
+        const bool take_l = hl && (uint64_t)qrel[qh * HB] < relg;
+        const uint64_t rel = take_l ? (uint64_t)qrel[qh * HB] : relg;
+        if (started && rel > cur_rel && pending) {
+          // flush the inline children of this node's gen-0 events at cur_rel (positions [ts0_it, it))
           for (uint32_t jt = ts0_it; jt < it; jt++) {
             const uint32_t xr = my[jt];
             const uint32_t ncr = M.nchild[xr];
@@ -574,31 +681,56 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
           }
           pending = 0;
         }
-        if (it == n) break;
-        if (it == 0 || rel > cur_rel) {
+        if (!hg && !hl) break;
+        if (!started || rel > cur_rel) {
           ts0_it = it;
           cur_rel = rel;
+          started = true;
         }
-        const uint32_t s = my[it];
-        E.ctx = M.wctx[base + s];  // (Schedule calls inherit the event's context)
+        uint32_t s, kw, a;
+        Pkt pk{0, 0, 0, 0};
+        uint64_t key = 0;
+        if (WIDE && take_l) {  // a local record: PointToPointNetDevice::TransmitComplete
+          s = qrec[qh * HB];
+          qh++;
+          E.ctx = M.wctx[s];
+          kw = K_TX_COMPLETE;
+          a = M.wa[s];
+          E.uid = LOCALBIT | s;
+          E.demote = false;
+        } else {
+          s = my[it];
+          key = mk[it];
+          it++;
+          E.ctx = M.wctx[base + s];  // (Schedule calls inherit the event's context)
+          kw = M.wkind[base + s];
+          a = M.wa[base + s];
+          pk = M.wpkt[base + s];
+          E.uid = (uint32_t)key;
+          E.demote = rel == slo || rel == shi;
+        }
         E.now = tmin + rel;
         E.slot0 = s * M.maxc;
         E.n = 0;
-        E.uid = (uint32_t)mk[it];
         E.trseq = 0;
-        E.demote = rel == slo || rel == shi;
-        hs.cancelled += run_event(M, E, M.wkind[base + s], M.wa[base + s], M.wpkt[base + s], sink, hs);
+        E.lj = -1;
+        hs.cancelled += run_event(M, E, kw, a, pk, sink, hs);
         uint32_t ni = 0;
         if (rel < inline_lim)
           for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
-        slot_done(M, s, mk[it], E.n, ni, xa);
+        slot_done(M, s, key, E.n, ni, xa);
         pending += ni;
+        if (WIDE && E.lj >= 0) {
+          const uint32_t r2 = local_record(M, E, s, tmin, blockIdx.x, lcnt_sh, true);
+          if (r2 != NOSRC) lq_push(M, qrel, qrec, HB, qh, nq, (uint32_t)(E.lts - tmin), r2);
+        }
       }
       tmn = E.tmn;
       wnd = E.wnd;
+      wndw = E.wndw;
     }
   }
-  publish_min<HB>(R, tmn, wnd);
+  publish_min<HB, WIDE>(R, tmn, wnd, wndw);
   x1_totals(M, xa);
   if (hs.stop) C.stop_seen = 1;
   if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
@@ -903,8 +1035,9 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
 // other node parts serially in key order; (3) the device steps and trailing children serially in key
 // order, the device state in registers.  Node parts never read device state and device steps never
 // read node state (node_part), so this is the sequential order's result.
+template <bool WIDE>
 __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32_t base, bool sorted, Red &R,
-                         uint32_t hb, uint32_t *lds, const HCtl &hc) {
+                         uint32_t hb, uint32_t *lds, const HCtl &hc, uint32_t *lcnt_sh) {
   const int lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1ull;
   uint64_t *gk = M.hub_key + (uint64_t)hb * WCAP;
@@ -948,8 +1081,12 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   E.ch_a = M.ch_a;
   E.ch_pkt = M.ch_pkt;
   E.lookahead = M.lookahead;
+  E.lookw = WIDE ? M.lookw : nullptr;
   E.tmn = ~0ull;
   E.wnd = ~0ull;
+  E.wndw = ~0ull;
+  E.lim_abs = WIDE && hc.lim ? hc.tmin + hc.lim : 0;
+  E.lj = -1;
   E.demote = false;
   HStat hs{0, 0, 0, 0, false};
   // the passes go through the list 64 events at a time: every lane loads one event's record into
@@ -1052,7 +1189,8 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     dmax = y > dmax ? y : dmax;
     inl |= z;
   }
-  bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && M.dev[dmin].qmax >= 1 &&
+  // (not in a wide window: a TransmitStart there makes a local record the scan cannot place)
+  bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && (!WIDE || hc.lim == 0) && M.dev[dmin].qmax >= 1 &&
               !(M.dev[dmin].busy == 0 && M.dev[dmin].cnt != 0);
   X1Acc xa{0, 0, 0};
   if (fast) fast = hub_device_scan(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs, xa);
@@ -1061,6 +1199,57 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     D.d = NOSRC;
     uint32_t ts0_it = 0, pending = 0;
     uint64_t cur_rel = 0;
+    bool started = false;
+    // local records (wide windows) of this hub, lane 0's queue: merged with the gen-0 events by rel ts
+    __shared__ uint32_t hq_rel[LQ], hq_rec[LQ];
+    uint32_t qh = 0, nq = 0;
+    // the inline DoForwardUp leaves of this node's gen-0 events at cur_rel (positions [ts0_it, it)), before
+    // anything at a later ts
+    auto flush = [&](uint32_t it) {
+      for (uint32_t jt = ts0_it; jt < it; jt++) {
+        const uint32_t xr = gs[jt];
+        const uint32_t ncr = M.nchild[xr];
+        for (uint32_t jj = 0; jj < ncr; jj++) {
+          const uint32_t sl = xr * M.maxc + jj;
+          if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
+          const uint32_t sa = M.ch_a[sl];
+          if (M.app_flags[sa] & 2u) {
+            M.appc[sa].rx_packets++;
+            M.appc[sa].rx_bytes += M.ch_pkt[sl].size - 28;
+          }
+        }
+      }
+      pending = 0;
+    };
+    auto new_local = [&](uint32_t par) {
+      if (!WIDE || E.lj < 0) return;
+      const uint32_t r2 = local_record(M, E, par, tmin, NHB + hb, lcnt_sh, false);
+      if (r2 != NOSRC) lq_push(M, hq_rel, hq_rec, 1, qh, nq, (uint32_t)(E.lts - tmin), r2);
+    };
+    // the local records due before rel (at equal ts the gen-0 event first); `it`: the next gen-0 position
+    auto run_locals = [&](uint64_t rel, uint32_t it) {
+      while (WIDE && qh < nq && (uint64_t)hq_rel[qh] < rel) {
+        const uint64_t lrel = hq_rel[qh];
+        if (started && lrel > cur_rel && pending) flush(it);
+        if (!started || lrel > cur_rel) {
+          ts0_it = it;
+          cur_rel = lrel;
+          started = true;
+        }
+        const uint32_t s = hq_rec[qh++];
+        E.ctx = M.wctx[s];
+        E.now = tmin + lrel;
+        E.slot0 = s * M.maxc;
+        E.n = 0;
+        E.uid = LOCALBIT | s;
+        E.trseq = 0;
+        E.demote = false;
+        E.lj = -1;
+        device_act_cached(M, E, Act{ACT_KICK, M.wa[s], Pkt{0, 0, 0, 0}}, D);  // TransmitComplete
+        slot_done(M, s, 0, E.n, 0, xa);
+        new_local(s);
+      }
+    };
     for (uint32_t j0 = 0; j0 <= n; j0 += HB) {
       const uint32_t j = j0 + lane;
       if (j < n) {
@@ -1077,27 +1266,13 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           if (q == nb && it < n) break;  // (the next batch continues; the final flush runs at it == n)
           const uint64_t key = it < n ? b_key[q] : ~0ull;
           const uint64_t rel = it < n ? (key >> 32) : ~0ull;
-          if (it > 0 && rel > cur_rel && pending) {
-            // the inline DoForwardUp leaves of this node's events at cur_rel (positions [ts0_it, it))
-            for (uint32_t jt = ts0_it; jt < it; jt++) {
-              const uint32_t xr = gs[jt];
-              const uint32_t ncr = M.nchild[xr];
-              for (uint32_t jj = 0; jj < ncr; jj++) {
-                const uint32_t sl = xr * M.maxc + jj;
-                if ((M.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
-                const uint32_t sa = M.ch_a[sl];
-                if (M.app_flags[sa] & 2u) {
-                  M.appc[sa].rx_packets++;
-                  M.appc[sa].rx_bytes += M.ch_pkt[sl].size - 28;
-                }
-              }
-            }
-            pending = 0;
-          }
+          run_locals(rel, it);
+          if (started && rel > cur_rel && pending) flush(it);
           if (it == n) break;
-          if (it == 0 || rel > cur_rel) {
+          if (!started || rel > cur_rel) {
             ts0_it = it;
             cur_rel = rel;
+            started = true;
           }
           const uint32_t s = b_s[q];
           const HubEv h = b_h[q];
@@ -1108,6 +1283,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           E.uid = (uint32_t)key;
           E.trseq = h.seq;
           E.demote = rel == slo || rel == shi;
+          E.lj = -1;
           hs.cancelled += h.cancelled;
           device_act_cached(M, E, Act{h.op, h.dev, h.p}, D);
           if (h.xdrop) trace_te_drop(M, E, h.xdrop - 1, h.p);
@@ -1115,13 +1291,14 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           const uint32_t ni = rel < inline_lim ? h.pad : 0u;
           slot_done(M, s, key, E.n, ni, xa);
           pending += ni;
+          new_local(s);
         }
       }
       __syncthreads();
     }
     if (lane == 0) D.flush(M);
   }
-  publish_min<HB>(R, E.tmn, E.wnd);
+  publish_min<HB, WIDE>(R, E.tmn, E.wnd, E.wndw);
   x1_totals(M, xa);
   const uint64_t nr = wave_sum64(hs.no_route), td = wave_sum64(hs.ttl_drops), cn = wave_sum64(hs.cancelled),
                  ur = wave_sum64(hs.unreach), ic = wave_sum64(hs.icmp);
@@ -1173,8 +1350,11 @@ __device__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool ha
   }
 }
 
+// WIDE: the single engine's wide windows (local records; the rank tiles rank the gen-0 records among
+// themselves, k2_scan places the local records).
+template <bool WIDE>
 __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
-  __shared__ uint64_t lds64[K2_LDS_WORDS / 2];
+  __shared__ uint64_t lds64[(WIDE ? K2_LDS_WORDS_W : K2_LDS_WORDS) / 2];
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds64);
   PH_BEGIN();
   Ctl &C = *M.C;
@@ -1185,7 +1365,9 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   // the run control and (holder blocks) the slot's record, all loaded at once
   const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_wbase = C.wbase, c_fr = C.force_run, rt = C.rt,
                  c_nhub = C.nhub;
-  const HCtl hc{C.tmin, C.inline_lim, C.split_lo, C.split_hi};
+  const HCtl hc{C.tmin, C.inline_lim, C.split_lo, C.split_hi, C.lim_rel};
+  __shared__ uint32_t s_lcnt;  // local records this block made (its region's count, wide windows)
+  if (threadIdx.x == 0) s_lcnt = 0;
   const uint64_t c_nfree = C.nfree, c_nF = C.nF, c_Pe = C.P_end;
   const uint32_t bx = blockIdx.x;
   SlotPre sp{1u, 0, 0, 0, 0};
@@ -1228,28 +1410,101 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   const bool handle = run || (W <= (uint32_t)WCAP && !c_fr);
   Red &R = M.dist ? x1hdr(M.x1_send, 0)->red : C.red[rt];
   PH_MARK(8);
+  __syncthreads();  // (s_lcnt)
   if (bx < (uint32_t)NHB) {
-    if (handle) handle_node2(M, C, bx * HB + threadIdx.x, W, base, R, lds, hc, sp);
-  } else if (bx < (uint32_t)(NHB + NRB)) {
-    if (!run && handle && !M.dist) rank_tile(M, C, bx - NHB);  // (partitioned: k_gtile ranks globally)
-  } else if (bx < (uint32_t)(NHB + NRB + NHUB)) {
+    if (handle) handle_node2<WIDE>(M, C, bx * HB + threadIdx.x, W, base, R, lds, hc, sp, &s_lcnt);
+  } else if (bx < (uint32_t)(NHB + NHUB)) {
     if (handle) {
-      const uint32_t hb = bx - (NHB + NRB);
+      const uint32_t hb = bx - NHB;
       const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
-      for (uint32_t h = hb; h < nh; h += NHUB) hub_node(M, C, M.hub_list[h], W, base, run, R, hb, lds, hc);
+      for (uint32_t h = hb; h < nh; h += NHUB) hub_node<WIDE>(M, C, M.hub_list[h], W, base, run, R, hb, lds, hc, &s_lcnt);
     }
+  } else if (bx < (uint32_t)K2_GRID_W) {
+    maintain(M, C, bx - (NHB + NHUB), run, handle, W, c_nfree, c_nF, c_Pe);
   } else {
-    maintain(M, C, bx - (NHB + NRB + NHUB), run, handle, W, c_nfree, c_nF, c_Pe);
+    if (!run && handle && !M.dist) rank_tile(M, C, bx - K2_GRID_W);  // (keys known before the handlers run)
+  }
+  if (WIDE && hc.lim && bx < (uint32_t)NLR) {  // this block's local region count (k2_scan reads it)
+    __syncthreads();
+    if (threadIdx.x == 0 && s_lcnt) {
+      const uint32_t cap = bx < (uint32_t)NHB ? (uint32_t)LR : (uint32_t)LRH;
+      M.lcnt[bx] = s_lcnt < cap ? s_lcnt : cap;
+    }
   }
   PH_MARK(9);
   BLK_REC(1, c_win);
 }
 
+// The local regions' prefix (NLR + 1 entries) from M.lcnt, into LDS; every thread of the block calls it.
+template <int NT>
+__device__ __forceinline__ void local_prefix(const P2PDev &M, bool any, uint32_t *pre) {
+  static_assert(NT >= NLR, "one thread per region");
+  const uint32_t v = (any && threadIdx.x < (uint32_t)NLR) ? M.lcnt[threadIdx.x] : 0u;
+  if (threadIdx.x < (uint32_t)NLR) pre[threadIdx.x + 1] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    pre[0] = 0;
+    for (int r = 1; r <= NLR; r++) pre[r] += pre[r - 1];
+  }
+  __syncthreads();
+}
+// Record index -> dense index (gen-0 slot, or W + its region's prefix + its offset in the region).
+__device__ __forceinline__ uint32_t dense_of(uint32_t rec, uint32_t W, const uint32_t *pre) {
+  if (rec < LBASE) return rec;
+  const uint32_t off = rec - LBASE;
+  if (off < (uint32_t)(NHB * LR)) return W + pre[off / LR] + off % LR;
+  const uint32_t o2 = off - (uint32_t)(NHB * LR);
+  return W + pre[NHB + o2 / LRH] + o2 % LRH;
+}
+// First position of a sorted LDS array whose value is >= v.
+template <typename T>
+__device__ __forceinline__ uint32_t lds_lower(const T *a, uint32_t n, T v) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (a[m] < v) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+// Ascending bitonic sort of n keys in LDS (n a power of two) by the whole block; ends synchronised.
+template <int NT>
+__device__ __forceinline__ void bitonic_lds64(uint64_t *a, uint32_t n) {
+  for (uint32_t k = 2; k <= n; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < n / 2; i += NT) {
+        const uint32_t x = ((i & ~(j - 1)) << 1) | (i & (j - 1)), y = x + j;
+        const uint64_t u = a[x], v = a[y];
+        if ((u > v) == ((x & k) == 0)) {
+          a[x] = v;
+          a[y] = u;
+        }
+      }
+      __syncthreads();
+    }
+}
+
 // ---- k2_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
+// WIDE: the single engine's wide windows.  Every record's rank in the dispatch order (ts, uid) is settled
+// here: the gen-0 records' ranks among themselves come from k2_handle's rank tiles (their keys are known
+// before the handlers run); a local record's uid is not known yet (its parent's child prefix + its child
+// index, assigned below), but its place is: after every gen-0 record of its ts (their uids are older), and
+// among the local records of one ts in their parents' order, then by child index (DefaultSimulatorImpl
+// gives uids in Schedule order).  Parents have smaller timestamps, so passes over the groups of equal ts
+// settle one more generation each.
+template <bool WIDE>
 __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   Ctl &C = *M.C;
-  constexpr int RPT = WCAP / SCAN_THREADS;
-  __shared__ uint32_t l_slot[WCAP], l_cnt[WCAP], l_rel[WCAP], gstart[WCAP];
+  // one thread per RPT records (dense order: the W gen-0 slots, then the local records region by region);
+  // the rank-ordered arrays hold NREC records.  Wide: the ranking's scratch (local keys, gen-0 rel ts by
+  // rank, final ranks, parents) shares the buffer, 144 KB of LDS.
+  constexpr int NREC = WIDE ? NMAX : WCAP;
+  constexpr int RPT = NREC / SCAN_THREADS;
+  constexpr int RPT0 = WCAP / SCAN_THREADS;  // (the gen-0 part, loaded speculatively at entry)
+  constexpr int SBUF = WIDE ? 4 * NMAX + WCAP : 4 * WCAP;
+  __shared__ uint32_t sbuf[SBUF];
+  uint32_t *l_slot = sbuf, *l_cnt = sbuf + NREC, *l_rel = sbuf + 2 * NREC, *gstart = sbuf + 3 * NREC;
+  __shared__ uint32_t pre[NLR + 1];
   PH_BEGIN();
   BLK_T0();
 #ifdef NSGPU_PHASE_PROF
@@ -1258,26 +1513,34 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   const int tid = threadIdx.x;
   // the run control and the window's slots (speculatively at base 0), all loaded at once
   const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run, c_wbase = C.wbase;
-  const uint32_t c_nhub = C.nhub;
-  const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
+  const uint32_t c_nhub = C.nhub, uid0 = C.uid;
+  const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush, c_lim = C.lim_rel, c_bound = C.bound,
+                 c_nbound = C.nbound;
   // the bookkeeping's run control as well (thread 0 writes it back at the end; loaded now, its trip
   // overlaps the slot loads instead of following the scan)
   struct Book {
-    uint64_t K, tmin, inline_lim, live, P_end, r0, rW, windows, max_window, max_windows, hts;
+    uint64_t K, tmin, inline_lim, live, P_end, r0, rW, windows, max_window, max_windows, hts, span_t;
     uint32_t uid, rt, stop_seen, hcap;
   } bk{};
   if (tid == 0)
     bk = Book{C.K, C.tmin, C.inline_lim, C.live, C.P_end, C.r0, C.rW, C.windows, C.max_window, C.max_windows, C.hts,
-              C.uid, C.rt, C.stop_seen, C.hcap};
-  uint32_t pr[RPT], pc[RPT], pctx[RPT];
-  uint64_t pkey[RPT];
+              C.span_t, C.uid, C.rt, C.stop_seen, C.hcap};
+  // per record: rank, child counts, record index, rel ts; a local record's parent (wpar), later the
+  // parent's rank | child index << 16
+  uint32_t pr[RPT], pc[RPT], prec[RPT], prel[RPT], ppx[RPT];
+  uint64_t gk[RPT0];
+  uint32_t gctx[RPT0];
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t i = tid + q * SCAN_THREADS;
-    pr[q] = M.wrank[i];
-    pc[q] = M.nchild[i] | (M.ninl[i] << 16);
-    pkey[q] = M.wkey[i];
-    pctx[q] = M.wctx[i];
+    prec[q] = i;
+    pr[q] = pc[q] = prel[q] = ppx[q] = 0;
+    if (q < RPT0) {
+      pr[q] = M.wrank[i];
+      pc[q] = M.nchild[i] | (M.ninl[i] << 16);
+      gk[q] = M.wkey[i];
+      gctx[q] = M.wctx[i];
+    }
   }
   if (c_done || c_mode >= MODE_SORT) return;
   const bool run = c_mode == MODE_RUN;
@@ -1307,51 +1570,183 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       C.pvalid = 0;
       C.refits++;
       C.force_run = 0;
+      // a widened window is trimmed back to its narrow bound before it runs (host step: the run's rule is
+      // that every child sorts after every run event), and the next ones start narrower
+      C.renarrow = c_nbound < c_bound ? 1u : 0u;
+      if (c_nbound < c_bound) C.span_t = ((c_bound >> 32) >> 1) + 1;
       C.mode = MODE_SORT;
     }
     return;
   }
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t i = tid + q * SCAN_THREADS;
-    if (run) pr[q] = i;
-    if (base != 0 && i < W) {
-      pkey[q] = M.wkey[base + i];
-      pctx[q] = M.wctx[base + i];
+  // ---- the local records (wide windows): dense positions W .. N-1
+  if constexpr (WIDE) local_prefix<SCAN_THREADS>(M, c_lim != 0 && !run, pre);
+  const uint32_t Lt = (WIDE && !run) ? pre[NLR] : 0u;
+  const uint32_t N = W + Lt;
+  if (N > (uint32_t)NREC) {  // (the adaptive span keeps windows well inside; a run that got here fails loudly)
+    if (tid == 0) {
+      atomicOr(M.error, 64u);
+      C.done = 1;
     }
-    if (i >= W) pkey[q] = pctx[q] = 0;  // (a run's last chunk ends before the array does)
+    return;
+  }
+  // the keys / contexts the next k2_pa appends with (a local record's uid comes after the ranking)
+#pragma unroll
+  for (int q = 0; q < RPT0; q++) {
+    const uint32_t i = tid + q * SCAN_THREADS;
+    if (base != 0 && i < W) {
+      gk[q] = M.wkey[base + i];
+      gctx[q] = M.wctx[base + i];
+    }
+    if (run) pr[q] = i;
+    if (i < W) {
+      M.pwctx[i] = gctx[q];
+      M.pwkey[i] = gk[q];
+      prel[q] = (uint32_t)(gk[q] >> 32);
+    }
+  }
+  if constexpr (WIDE) {
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+      const uint32_t i = tid + q * SCAN_THREADS;
+      if (i >= W && i < N) {  // a local record
+        const uint32_t r = dense_rec(i, W, pre);
+        prec[q] = r;
+        pc[q] = M.nchild[r] | (M.ninl[r] << 16);
+        prel[q] = (uint32_t)(M.wkey[r] >> 32);
+        M.pwctx[r] = M.wctx[r];
+        ppx[q] = M.wpar[r];
+      }
+    }
+    if (Lt) {  // ---- the ranking (see above)
+      uint64_t *keys = reinterpret_cast<uint64_t *>(sbuf);  // [P] local records: rel ts << 32 | local index
+      uint32_t *g0rel = sbuf + 2 * NMAX;                     // [W] gen-0 rel ts by gen-0 rank (ascending)
+      uint32_t *F = g0rel + WCAP;                            // [N] final rank by dense index
+      uint32_t *lpar = F + NMAX;                             // [Lt] parent's dense index | child index << 24
+      uint32_t P = 64;
+      while (P < Lt) P <<= 1;
+#pragma unroll
+      for (int q = 0; q < RPT; q++) {
+        const uint32_t i = tid + q * SCAN_THREADS;
+        if (i < W) {
+          g0rel[pr[q]] = prel[q];
+        } else if (i < N) {
+          const uint32_t k = i - W;
+          keys[k] = ((uint64_t)prel[q] << 32) | k;
+          lpar[k] = dense_of(ppx[q] & 0xffffffu, W, pre) | (ppx[q] & 0xff000000u);
+        }
+      }
+      for (uint32_t k = Lt + tid; k < P; k += SCAN_THREADS) keys[k] = ~0ull;
+      __syncthreads();
+      bitonic_lds64<SCAN_THREADS>(keys, P);
+      // a gen-0 record: its gen-0 rank + the local records of smaller ts
+#pragma unroll
+      for (int q = 0; q < RPT0; q++) {
+        const uint32_t i = tid + q * SCAN_THREADS;
+        if (i < W) {
+          pr[q] += lds_lower<uint64_t>(keys, Lt, (uint64_t)prel[q] << 32);
+          F[i] = pr[q];
+        }
+      }
+      // a local record (sorted position p): the gen-0 records up to its ts + the local records of smaller
+      // ts (its group's base) + its place in its group of equal ts
+      uint32_t glo[RPT], ghi[RPT], gbase[RPT];
+      bool multi = false, lpm = false;
+#pragma unroll
+      for (int u = 0; u < RPT; u++) {
+        const uint32_t p = tid + u * SCAN_THREADS;
+        glo[u] = ghi[u] = gbase[u] = 0;
+        if (p < Lt) {
+          const uint64_t key = keys[p];
+          const uint32_t rel = (uint32_t)(key >> 32), k = (uint32_t)key;
+          const uint32_t lo = lds_lower<uint64_t>(keys, Lt, (uint64_t)rel << 32);
+          const uint32_t hi = lds_lower<uint64_t>(keys, Lt, (uint64_t)(rel + 1) << 32);
+          const uint32_t b = lo + lds_lower<uint32_t>(g0rel, W, rel + 1);
+          glo[u] = lo;
+          ghi[u] = hi;
+          gbase[u] = b;
+          F[W + k] = b + (hi - lo == 1 ? 0u : p - lo);  // (a group of one is placed; others: a first guess)
+          if (hi - lo > 1) {
+            multi = true;
+            lpm |= (lpar[k] & 0xffffffu) >= W;  // (a local parent: its rank may move while this settles)
+          }
+        }
+      }
+      const bool any_multi = __syncthreads_or(multi);
+      if (any_multi) {
+        const bool iterate = __syncthreads_or(lpm);
+        for (int pass = 0;; pass++) {
+          uint32_t nv[RPT];
+          bool ch = false;
+#pragma unroll
+          for (int u = 0; u < RPT; u++) {
+            const uint32_t p = tid + u * SCAN_THREADS;
+            nv[u] = 0;
+            if (p < Lt && ghi[u] - glo[u] > 1) {
+              const uint32_t k = (uint32_t)keys[p], me = lpar[k];
+              const uint32_t pf = F[me & 0xffffffu], j = me >> 24;
+              uint32_t cnt = 0;
+              for (uint32_t m = glo[u]; m < ghi[u]; m++) {
+                const uint32_t o = lpar[(uint32_t)keys[m]];
+                const uint32_t pf2 = F[o & 0xffffffu], j2 = o >> 24;
+                cnt += pf2 < pf || (pf2 == pf && j2 < j);
+              }
+              nv[u] = gbase[u] + cnt;
+              ch |= nv[u] != F[W + k];
+            }
+          }
+          __syncthreads();
+#pragma unroll
+          for (int u = 0; u < RPT; u++) {
+            const uint32_t p = tid + u * SCAN_THREADS;
+            if (p < Lt && ghi[u] - glo[u] > 1) F[W + (uint32_t)keys[p]] = nv[u];
+          }
+          const bool again = __syncthreads_or(ch);
+          if (!iterate || !again) break;
+          if (pass == 64) {  // (a generation per pass: cannot happen within a window)
+            if (tid == 0) atomicOr(M.error, 64u);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < RPT; q++) {
+        const uint32_t i = tid + q * SCAN_THREADS;
+        if (i >= W && i < N) {
+          const uint32_t o = lpar[i - W];
+          pr[q] = F[i];
+          ppx[q] = F[o & 0xffffffu] | ((o >> 24) << 16);  // (the parent's rank < NMAX, child index)
+        }
+      }
+      __syncthreads();  // (the buffer holds the rank-ordered arrays next)
+    }
   }
   PH_MARK(16);
 #pragma unroll
-  for (int q = 0; q < RPT; q++) {  // slot order -> rank order; keys / contexts kept for the next k2_pa
+  for (int q = 0; q < RPT; q++) {  // record order -> rank order
     const uint32_t i = tid + q * SCAN_THREADS;
-    if (i < W) {
+    if (i < N) {
       const uint32_t r = pr[q];
-      if (!run) M.wrank[i] = 0;
-      M.pwkey[i] = pkey[q];
-      M.pwctx[i] = pctx[q];
-      l_slot[r] = i;
+      l_slot[r] = prec[q];
       l_cnt[r] = pc[q];
-      l_rel[r] = (uint32_t)(pkey[q] >> 32);
+      l_rel[r] = prel[q];
     }
   }
   __syncthreads();
   PH_MARK(17);
-  uint32_t nc[RPT], ni[RPT], hd[RPT];
   uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
-  uint32_t prev_rel = (tid * RPT < (int)W && tid > 0) ? l_rel[tid * RPT - 1] : 0;
+  {
+    uint32_t prev_rel = (tid * RPT < (int)N && tid > 0) ? l_rel[tid * RPT - 1] : 0;
 #pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    nc[q] = ni[q] = hd[q] = 0;
-    if (r < W) {
-      nc[q] = l_cnt[r] & 0xffffu;
-      ni[q] = l_cnt[r] >> 16;
-      const uint32_t rel = l_rel[r];
-      hd[q] = r == 0 || rel != prev_rel;
-      prev_rel = rel;
+    for (int q = 0; q < RPT; q++) {
+      const uint32_t r = tid * RPT + q;
+      if (r < N) {
+        const uint32_t c = l_cnt[r], rel = l_rel[r];
+        const uint32_t hd = r == 0 || rel != prev_rel;
+        prev_rel = rel;
+        sum += (uint64_t)(c & 0xffffu) | ((uint64_t)(c >> 16) << 21) | ((uint64_t)hd << 42);
+      }
     }
-    sum += (uint64_t)nc[q] | ((uint64_t)ni[q] << 21) | ((uint64_t)hd[q] << 42);
   }
   const int lane = tid & 63, wid = tid >> 6;
   uint64_t inc = sum;
@@ -1373,34 +1768,68 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
                  ng = (uint32_t)(tot >> 42);
   uint32_t bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu), bh = (uint32_t)(ex >> 42);
   uint32_t g[RPT], ipr[RPT], cpr[RPT];
+  {
+    uint32_t prev_rel = (tid * RPT < (int)N && tid > 0) ? l_rel[tid * RPT - 1] : 0;
 #pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    bh += hd[q];
-    g[q] = bh - 1;
-    cpr[q] = bc;
-    ipr[q] = bi;
-    if (r < W && hd[q]) gstart[g[q]] = r;
-    bc += nc[q];
-    bi += ni[q];
+    for (int q = 0; q < RPT; q++) {
+      const uint32_t r = tid * RPT + q;
+      uint32_t c = 0, hd = 0;
+      if (r < N) {
+        c = l_cnt[r];
+        const uint32_t rel = l_rel[r];
+        hd = r == 0 || rel != prev_rel;
+        prev_rel = rel;
+      }
+      bh += hd;
+      g[q] = bh - 1;
+      cpr[q] = bc;
+      ipr[q] = bi;
+      if (r < N && hd) gstart[g[q]] = r;
+      bc += c & 0xffffu;
+      bi += c >> 16;
+    }
   }
   __syncthreads();
   PH_MARK(18);
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
-    if (r < W) l_cnt[r] = ipr[q];
+    if (r < N) l_cnt[r] = ipr[q];
   }
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
-    if (r < W) {
+    if (r < N) {
       const uint32_t first = gstart[g[q]];
-      const uint32_t last = (g[q] + 1 < ng ? gstart[g[q] + 1] : W) - 1;
+      const uint32_t last = (g[q] + 1 < ng ? gstart[g[q] + 1] : N) - 1;
       M.sinfo[l_slot[r]] = make_uint4(r + (tinl ? l_cnt[first] : 0), last + 1 + ipr[q], cpr[q], ipr[q]);
     }
   }
+  if (WIDE && Lt) {
+    __syncthreads();  // (gstart is reused: the child prefix by rank, for the local records' uids)
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+      const uint32_t r = tid * RPT + q;
+      if (r < N) gstart[r] = cpr[q];
+    }
+    __syncthreads();
+  }
+  // the keys / contexts the next k2_pa appends with: a local record's uid is its parent's child prefix +
+  // its child index (DefaultSimulatorImpl::Schedule order); the local records' list; ranks cleared
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t i = tid + q * SCAN_THREADS;
+    if (i < N) {
+      const uint32_t r = prec[q];
+      if (WIDE && i >= W) {
+        M.pwkey[r] = ((uint64_t)prel[q] << 32) | (uint32_t)(uid0 + gstart[ppx[q] & 0xffffu] + (ppx[q] >> 16));
+        M.lrec[i - W] = r;
+      }
+      if (!run && i < W) M.wrank[r] = 0;
+    }
+  }
+  if (WIDE && Lt && tid < NLR) M.lcnt[tid] = 0;
   PH_MARK(19);
   if (tid == 0) {
     C.pK0 = bk.K;
@@ -1408,12 +1837,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     C.ptmin = bk.tmin;
     C.pinline_lim = bk.inline_lim;
     C.pW = W;
+    C.plt = Lt;
     C.pinl = tinl;
     C.pvalid = 1;
-    if (W) C.last_ts = bk.tmin + l_rel[W - 1];
-    C.K = bk.K + W + tinl;
+    if (N) C.last_ts = bk.tmin + l_rel[N - 1];
+    C.K = bk.K + N + tinl;
     C.uid = bk.uid + tc;
-    C.pchild = tc - tinl;
+    C.pchild = tc - tinl - Lt;  // (the local records' uids were consumed, they ran in the window)
+    if (M.trace && (uint64_t)bk.uid + tc >= (1ull << 31)) atomicOr(M.error, 128u);  // (LOCALBIT trace uids)
     C.nfree = nfree - consumed + npush;
     const uint64_t P_end = bk.P_end + (nF > nfree ? nF - nfree : 0);
     const uint64_t live = bk.live - npush + nF;
@@ -1431,17 +1862,22 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       C.r0 = r0;
       if (r0 >= bk.rW) mode = MODE_NORMAL;
       else flip = false;  // the run's chunks keep folding into the same reduction
+    } else if (WIDE) {  // wide windows: keep them inside the window capacity (WCAP gen-0, NMAX records)
+      const uint64_t span = c_bound >> 32;
+      if (N > (uint32_t)(7 * NMAX / 8) || W > (uint32_t)(7 * WCAP / 8)) C.span_t = span - span / 4;
+      else if (N < (uint32_t)(3 * NMAX / 4) && W < (uint32_t)(3 * WCAP / 4) && bk.span_t < (1ull << 40))
+        C.span_t = bk.span_t + bk.span_t / 8 + 1;
     }
     if (flip) {
       const uint32_t rt = bk.rt;
-      C.red[rt ^ 1].tmin = C.red[rt ^ 1].wend = C.red[rt ^ 1].stopts = ~0ull;  // consumed
+      C.red[rt ^ 1].tmin = C.red[rt ^ 1].wend = C.red[rt ^ 1].stopts = C.red[rt ^ 1].wendw = ~0ull;  // consumed
       C.rt = rt ^ 1;
     }
     const uint64_t windows = bk.windows + 1;
     C.windows = windows;
-    if (W > bk.max_window) C.max_window = W;
+    if (N > bk.max_window) C.max_window = N;
     C.W = 0;
-    const uint64_t pending = live + (tc - tinl) + (mode == MODE_RUN ? bk.rW - r0 : 0);
+    const uint64_t pending = live + (tc - tinl - Lt) + (mode == MODE_RUN ? bk.rW - r0 : 0);
     bool done = bk.stop_seen || (pending == 0 && bk.hts == ~0ull);
     if (P_end > M.pool_cap) {
       atomicOr(M.error, 1u);
@@ -1463,6 +1899,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   }
   PH_MARK(20);
   BLK_REC(2, c_win);
+}
+
+// ---- local records' trace uids (traced wide engines): records made by this window's handlers carry
+// LOCALBIT | record until k2_scan has assigned the record's uid
+__global__ __launch_bounds__(256) void k_tpatch(const P2PDev M) {
+  const Ctl &C = *M.C;
+  if (!M.trace || C.plt == 0) return;
+  const uint64_t t0 = C.tn0, tn = *M.trace_n;
+  const uint64_t t1 = tn < M.trace_cap ? tn : M.trace_cap;
+  for (uint64_t i = t0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < t1; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t u = M.trace[i].uid;
+    if (u & LOCALBIT) M.trace[i].uid = (uint32_t)M.pwkey[u & ~LOCALBIT];
+  }
 }
 
 // ================================ host-driven steps (rare) ================================
@@ -1591,10 +2040,67 @@ __global__ __launch_bounds__(256) void k_cmp(const P2PDev M, uint64_t P) {
   }
 }
 
+// A widened window that overflowed (sorted by k_rs_*): the records past its narrow bound go back to the
+// pool, so that the run is a narrow window (every child of a run event sorts after every run event); they
+// fold into the pending reduction the run's chunks accumulate, and a host cut waits for a later window.
+__global__ __launch_bounds__(1024) void k_renarrow(const P2PDev M) {
+  Ctl &C = *M.C;
+  const uint64_t n = C.rW, nb = C.nbound, tmin = C.tmin, P0 = C.P_end;
+  __shared__ uint64_t s_cut;
+  if (threadIdx.x == 0) {  // the first record past the narrow bound (the records are sorted by key)
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (M.wkey[mid] <= nb) lo = mid + 1;
+      else hi = mid;
+    }
+    s_cut = lo;
+  }
+  __syncthreads();
+  const uint64_t cut = s_cut, m = n - cut;
+  if (P0 + m > M.pool_cap) {
+    if (threadIdx.x == 0) atomicOr(M.error, 1u);
+    return;
+  }
+  Red &R = C.red[C.rt];
+  uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull;
+  for (uint64_t i = cut + threadIdx.x; i < n; i += 1024) {
+    const uint64_t key = M.wkey[i];
+    const uint64_t ts = tmin + (key >> 32);
+    const uint32_t kind = M.wkind[i];
+    const uint64_t d = P0 + (i - cut);
+    M.ev_ts[0][d] = ts;
+    M.ev_uid[0][d] = (uint32_t)key;
+    M.ev_ctx[0][d] = M.wctx[i];
+    M.ev_kind[0][d] = kind;
+    M.ev_a[0][d] = M.wa[i];
+    M.ev_pkt[0][d] = M.wpkt[i];
+    tmn = ts < tmn ? ts : tmn;
+    const uint64_t x = ts + (uint64_t)M.lookahead[kind & 0xffu], xw = ts + (uint64_t)M.lookw[kind & 0xffu];
+    wnd = x < wnd ? x : wnd;
+    wndw = xw < wndw ? xw : wndw;
+    if ((kind & 0xffu) == K_STOP) {
+      R.stopts = ts;
+      R.stopuid = (uint32_t)key;
+    }
+  }
+  publish_min<1024>(R, tmn, wnd, wndw);
+  if (threadIdx.x == 0) {
+    C.P_end = P0 + m;
+    C.live += m;
+    C.rW = cut;
+    C.renarrow = 0;
+    const uint64_t edge = nb >> 32;
+    C.hrel = C.hrel < edge ? C.hrel : edge;
+    if (m) C.hcap = 0;  // (the host event's key is past the trimmed run: a later window reaches it)
+  }
+}
+
 // Mode transitions the host makes after a host-driven step.
 __global__ void k_after_sort(const P2PDev M) {
   M.C->mode = MODE_RUN;
   M.C->r0 = 0;
+  M.C->lim_rel = 0;  // (a run has no local records)
 }
 __global__ void k_after_compact(const P2PDev M, uint64_t live) {
   M.C->P_end = live;
@@ -1636,8 +2142,12 @@ __global__ void k_inject(const P2PDev M, uint32_t a, uint64_t now, uint32_t cur,
   E.ch_a = M.f_a;
   E.ch_pkt = M.f_pkt;
   E.lookahead = M.lookahead;
+  E.lookw = M.lookw;
   E.tmn = ~0ull;
   E.wnd = ~0ull;
+  E.wndw = ~0ull;
+  E.lim_abs = 0;  // (no window is forming: the children are pending)
+  E.lj = -1;
   E.uid = cur;
   E.trseq = seq;
   E.demote = false;
@@ -1673,6 +2183,7 @@ __global__ void k_inject(const P2PDev M, uint32_t a, uint64_t now, uint32_t cur,
   Red &R = C.red[C.rt ^ 1];  // bounds the next window (k2_scan flipped rt)
   if (E.tmn < R.tmin) R.tmin = E.tmn;
   if (E.wnd < R.wend) R.wend = E.wnd;
+  if (E.wndw < R.wendw) R.wendw = E.wndw;
   C.uid = uid0 + E.n;
   out[0] = C.uid;
   out[1] = E.trseq;

@@ -127,6 +127,7 @@ SIGNATURES = {
     "nsgpu_sim_destroy_pending": (C.c_int, [_vp, _u64, _u64, _vp]),
     "nsgpu_sched_stats": (C.c_int, [_vp, _vp, _vp, _vp]),
     "nsgpu_p2p_pending": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "nsgpu_p2p_get_wide": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_setup_uid": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_advance": (C.c_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "nsgpu_p2p_inject_send": (C.c_int, [_vp, _u32, _u64, _u32, _u32, _vp, _vp, _vp]),

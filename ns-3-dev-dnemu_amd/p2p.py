@@ -521,6 +521,12 @@ class Engine:
     def launch(self):
         nsgpu.check(nsgpu.lib().nsgpu_p2p_run(self.h, self.stream))
 
+    def wide(self):
+        """Whether this engine runs wide windows (nsgpu_p2p_get_wide)."""
+        w = C.c_int()
+        nsgpu.check(nsgpu.lib().nsgpu_p2p_get_wide(self.h, C.byref(w)))
+        return bool(w.value)
+
     def set_eager(self, eager=True):
         nsgpu.check(nsgpu.lib().nsgpu_p2p_set_eager(self.h, int(eager)))
 
