@@ -165,6 +165,31 @@ int nsgpu_wifi_kernel_count(int *n);
 const char *nsgpu_wifi_kernel_name(int k);
 int nsgpu_wifi_profile(nsgpu_wifi *h, void *stream, double *ms);
 
+/* ---------------- closed-loop Wi-Fi PHY (config 3 with the MAC on the host) ----------------
+ * Replaces, for transmissions host closures start at run time (a MAC / DcfManager on the host that reads the
+ * PHY state), YansWifiPhy::SendPacket (yans-wifi-phy.cc:499-522) -> YansWifiChannel::Send
+ * (yans-wifi-channel.cc:77-115) -> StartReceivePacket (yans-wifi-phy.cc:399-496) -> EndReceive
+ * (yans-wifi-phy.cc:770-799) with InterferenceHelper (interference-helper.cc:129-367: NiChanges, GetEnergyDuration,
+ * CalculateSnrPer), the error-rate models (nist- / yans- / dsss-error-rate-model.cc) and WifiPhyStateHelper
+ * (wifi-phy-state-helper.cc:122-183, 254-322, 391-423).  The device keeps every phy's state in HBM; the host
+ * runtime (nsgpu_sim_attach_wifi) advances it to each host event's key.  Each EndReceive's (snr, per) comes
+ * back for the host's m_random draw (yans-wifi-phy.cc:783; the PHY state does not depend on it). */
+typedef struct nsgpu_wifil nsgpu_wifil;
+int nsgpu_wifil_create(const nsgpu_wifil_config *cfg, nsgpu_wifil **out);
+int nsgpu_wifil_destroy(nsgpu_wifil *h);
+int nsgpu_wifil_receivers(nsgpu_wifil *h, uint32_t phy, uint32_t *n);  /* uids one SendPacket of phy takes */
+/* SendPacket of phy from the closure running at `now`; its fan-out takes uids uid_base .. + receivers - 1 */
+int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base, uint32_t phy, uint32_t size, double dbm,
+                     uint32_t modclass, uint64_t rate, uint32_t bw, uint32_t preamble);
+/* every device event with a key below (bound_ts, bound_uid) (~0: all): ranks from *dispatched, the syncs'
+ * EndReceive uids from *uid, digest terms and log entries (at their ranks, below log_cap) added */
+int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t bound_uid, uint32_t *uid, uint64_t *dispatched,
+                        uint64_t *digest, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap);
+int nsgpu_wifil_get_state(nsgpu_wifil *h, uint32_t phy, uint64_t now, nsgpu_wifil_phy_state *out);
+int nsgpu_wifil_read_ends(nsgpu_wifil *h, nsgpu_wifil_end *out, uint64_t cap, uint64_t *n);  /* since last read */
+int nsgpu_wifil_read_phys(nsgpu_wifil *h, nsgpu_wifi_phy_counters *out);                    /* n_phy */
+int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_ts);
+
 /* ---------------- GPU-resident bench-simulator churn (config 1) ----------------
  * Runs utils/bench-simulator.cc's RunBench + Simulator::Run (bench-simulator.cc:79-127) over
  * MapScheduler order entirely on the device: n initial events Schedule (NanoSeconds (d[i])),
@@ -275,6 +300,12 @@ int nsgpu_sim_set_log(nsgpu_sim *s, uint64_t *ts, uint32_t *uid, uint32_t *ctx, 
  * OnOff applications send a datagram now (UdpSocket::Send from a host application) */
 int nsgpu_sim_attach_p2p(nsgpu_sim *s, nsgpu_p2p *h);
 int nsgpu_sim_p2p_send(nsgpu_sim *s, uint32_t app);
+/* the closed-loop Wi-Fi PHY: its events join this runtime's order (one host event per window after the
+ * PHY's events before it); a closure's SendPacket (now, the runtime's next uids) and GetState (now) */
+int nsgpu_sim_attach_wifi(nsgpu_sim *s, nsgpu_wifil *h);
+int nsgpu_sim_wifi_send(nsgpu_sim *s, uint32_t phy, uint32_t size, double dbm, uint32_t modclass, uint64_t rate,
+                        uint32_t bw, uint32_t preamble);
+int nsgpu_sim_wifi_state(nsgpu_sim *s, uint32_t phy, nsgpu_wifil_phy_state *out);
 
 /* ---------------- GPU-resident point-to-point subset (configs 2, 4) ----------------
  * Replaces, for a topology of PointToPointNetDevices, the handler chain

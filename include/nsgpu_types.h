@@ -350,6 +350,45 @@ NSGPU_HD static inline uint64_t nsgpu_wifi_term(uint64_t kind, uint64_t ts, uint
                      c * 0xd1b54a32d192ed03ULL);
 }
 
+/* ---- closed-loop Wi-Fi PHY (nsgpu_wifil_*, attached to nsgpu_sim: SendPacket from host closures) ---- */
+typedef struct nsgpu_wifil_config {
+  int64_t n_phy;                /* YansWifiChannel::m_phyList, in Add order */
+  const double *x, *y, *z;      /* ConstantPositionMobilityModel positions */
+  const uint32_t *channel;      /* GetChannelNumber () */
+  const uint32_t *node;         /* context of the Receive / EndReceive events */
+  nsgpu_loss_chain loss;
+  double speed;                 /* ConstantSpeedPropagationDelayModel Speed */
+  double rx_gain_db;            /* YansWifiPhy RxGain (default 1) */
+  double ed_threshold_dbm;      /* EnergyDetectionThreshold (default -96) */
+  double cca_threshold_dbm;     /* CcaMode1Threshold (default -99) */
+  double rx_noise_figure_db;    /* RxNoiseFigure (default 7): InterferenceHelper::SetNoiseFigure (DbToRatio) */
+  uint32_t error_model;         /* nsgpu_wifil_error_model */
+  uint32_t ni_cap;              /* NiChanges entries per phy (power of two); a longer list fails the run */
+  uint32_t rxq_cap;             /* pending Receive events per phy (power of two) */
+  uint32_t pad_;
+  uint64_t tx_cap;              /* SendPacket calls over the run */
+} nsgpu_wifil_config;
+enum nsgpu_wifil_error_model { NSGPU_WIFIL_NIST = 0, NSGPU_WIFIL_YANS = 1 };  /* (YansWifiPhyHelper::Default: Nist) */
+
+/* One EndReceive (yans-wifi-phy.cc:770-799): InterferenceHelper::CalculateSnrPer's result, for the host's
+ * m_random draw (a cancelled one carries no snr / per). */
+typedef struct nsgpu_wifil_end {
+  uint64_t ts;
+  uint32_t uid, phy;
+  double snr, per;
+  uint32_t tx;     /* the transmission (SendPacket call) it receives */
+  uint32_t flags;  /* NSGPU_WIFI_END_CANCELLED */
+} nsgpu_wifil_end;
+
+/* WifiPhyStateHelper of one phy at Now (wifi-phy-state-helper.cc:159-183). */
+enum nsgpu_wifil_state { NSGPU_WIFIL_IDLE = 0, NSGPU_WIFIL_RX = 1, NSGPU_WIFIL_TX = 2, NSGPU_WIFIL_CCA_BUSY = 3 };
+typedef struct nsgpu_wifil_phy_state {
+  uint32_t state;  /* nsgpu_wifil_state */
+  uint32_t rxing;
+  int64_t end_tx, end_rx, end_cca_busy;
+  int64_t delay_until_idle;  /* GetDelayUntilIdle (:122-151) */
+} nsgpu_wifil_phy_state;
+
 #ifdef __cplusplus
 }
 #endif

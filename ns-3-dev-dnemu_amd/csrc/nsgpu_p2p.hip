@@ -122,11 +122,29 @@ struct Ctl {
   uint64_t span_t;    // adaptive span target of wide windows (kept between the narrow and the wide bound)
   uint32_t plt;       // local records of the last scanned window (lrec)
   uint32_t renarrow;  // the overflowing window is wide: trim its sorted run to nbound (host step)
+  // ---- sorted runs: the chunk being dispatched ends at rnext; rtrim: the run ends after it (k_trim) ----
+  uint64_t rnext;
+  uint32_t rtrim, pad5;
 };
 
 static_assert(offsetof(Ctl, prep) == offsetof(Ctl, W) + 12 && offsetof(Ctl, W) % 16 == 0, "the X0 payload");
 
 // Device-resident model + engine state (all pointers are HBM).  Passed to the kernels by value.
+// A window record's place in the dispatch order, for the wide windows' ranking (k2_rank): the chain of
+// records from it up to its gen-0 ancestor (a local record is a same-node TransmitComplete run inside the
+// window; its parent is the event whose TransmitStart made it).  A gen-0 record is a chain of length 0.
+// Order (ts, uid): a local record's uid is its parent's child prefix + its child index, so among records of
+// one ts the gen-0 ones come first (older uids), and local ones follow their parents' order, then j.
+constexpr int LKD = 8;  // chain levels kept: a record and up to 7 local ancestors (create: Lx <= 8 tx_min)
+struct LKey {
+  uint32_t rel[LKD];  // rel[t]: rel ts of the chain's level-t record (level 0: this one)
+  uint32_t uid;       // the gen-0 ancestor's uid (level `depth`)
+  uint32_t depth;     // local records in the chain (0: a gen-0 record)
+  uint32_t pad[2];
+  uint8_t j[16];      // j[t]: the level-t local record's child index in its parent
+};
+static_assert(sizeof(LKey) == 64, "LKey: four 16-B loads");
+
 struct P2PDev {
   // scenario
   uint32_t n_nodes, n_devices, n_apps, n_dst, qcap, maxc;
@@ -220,6 +238,7 @@ struct P2PDev {
   uint32_t *wpar;         // local record: parent record | child index << 24
   uint32_t *lcnt;         // local records per region this window (one region per holder / hub block)
   uint32_t *lrec;         // the last scanned window's local records (dense list, C.plt of them)
+  LKey *lkey;             // [LCAP] the local records' chains (k2_rank)
 };
 
 // ---------------- wave / block helpers ----------------
@@ -1701,7 +1720,9 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     uint32_t dmax = 0;
     for (uint32_t d = 0; d < D; d++) dmax = std::max(dmax, ++deg[sc->dev_node[d]]);
     const char *nw = getenv("NSGPU_P2P_NARROW");
-    M.wide = (!owner && dmax <= (uint32_t)LQ && lx > tx_min && lx < INFL && !(nw && nw[0] == '1')) ? 1u : 0u;
+    // (a chain of same-node TransmitCompletes inside a window is shorter than Lx / tx_min: LKD levels)
+    M.wide = (!owner && dmax <= (uint32_t)LQ && lx > tx_min && lx <= (int64_t)LKD * tx_min && lx < INFL &&
+              !(nw && nw[0] == '1')) ? 1u : 0u;
   }
   // ---- scenario upload ----
   TRY(dupload(h, &M.dev_node, sc->dev_node, D));
@@ -1862,6 +1883,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   for (uint32_t **p : {&M.nchild, &M.ninl, &M.pwctx, &M.wrank, &M.wpar}) TRY(dalloc(h, p, WTOT));
   TRY(dalloc(h, &M.lcnt, NLR));
   TRY(dalloc(h, &M.lrec, NMAX));  // (k2_pa loads lrec[k] speculatively: zeroed, every entry stays < WTOT)
+  TRY(dalloc(h, &M.lkey, LCAP));
   if (hipMemset(M.lrec, 0, NMAX * sizeof(uint32_t)) != hipSuccess || hipMemset(M.lcnt, 0, NLR * sizeof(uint32_t)) != hipSuccess) {
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipMemset failed");
@@ -2041,12 +2063,13 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
 
 // The window pipeline, in launch order (graph capture, eager runs and the per-kernel profile).
 namespace {
-constexpr int NKERN = 4;
-const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_scan", "k_tpatch"};
+constexpr int NKERN = 5;
+const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_rank", "k2_scan", "k_tpatch"};
 // ev0 / ev1: optional HIP events the command processor records at the kernel's start and end
 // (hipExtLaunchKernelGGL: no separate marker packets between the pipeline's kernels).
-// Kernel k of the single engine's window (KERNEL_NAMES); a traced wide engine patches the local records'
-// trace uids (k_tpatch).  Returns whether kernel k is part of this engine's window.
+// Kernel k of the single engine's window (KERNEL_NAMES); a wide engine places its local records after
+// its handlers (k2_rank) and, traced, patches their trace uids (k_tpatch).  Returns
+// whether kernel k is part of this engine's window.
 bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   const bool wide = h->M.wide != 0;
   switch (k) {
@@ -2059,6 +2082,10 @@ bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr,
       else hipExtLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M);
       return true;
     case 2:
+      if (!wide) return false;
+      hipExtLaunchKernelGGL(k2_rank, dim3(RK_GRID), dim3(RKT), 0, s, ev0, ev1, 0, h->M);
+      return true;
+    case 3:
       if (wide) hipExtLaunchKernelGGL(k2_scan<true>, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
       else hipExtLaunchKernelGGL(k2_scan<false>, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
       return true;
@@ -2112,7 +2139,10 @@ static int host_step(nsgpu_p2p *h, const Ctl &c, hipStream_t s) {
       NSGPU_HIP(hipMemcpyAsync(M.wpkt, M.g_pkt, n * sizeof(Pkt), hipMemcpyDeviceToDevice, s));
     }
     if (c.renarrow) hipLaunchKernelGGL(k_renarrow, dim3(1), dim3(1024), 0, s, M);  // (a widened window)
-    hipLaunchKernelGGL(k_after_sort, dim3(1), dim3(1), 0, s, M);
+    hipLaunchKernelGGL(k_after_sort, dim3(1), dim3(1024), 0, s, M);
+    NSGPU_HIP(hipGetLastError());
+  } else if (c.mode == MODE_TRIM) {  // a run ends after a cut same-ts group: the rest goes back to the pool
+    hipLaunchKernelGGL(k_trim, dim3(1), dim3(1024), 0, s, M);
     NSGPU_HIP(hipGetLastError());
   } else if (c.mode == MODE_COMPACT) {
     NSGPU_HIP(hipMemsetAsync(M.cmp_cnt, 0, sizeof(uint64_t), s));

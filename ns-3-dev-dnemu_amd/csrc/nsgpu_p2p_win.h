@@ -23,7 +23,8 @@
 // run inline, which keeps its (ts, uid) position.  When the pool holds many tombstones the host
 // compacts it (k_cmp).
 
-enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3, MODE_HOST = 4, MODE_CUT = 5 };
+enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3, MODE_HOST = 4, MODE_CUT = 5,
+                  MODE_TRIM = 6 };
 constexpr uint64_t TOMB = ~0ull;        // ev_ts of a free pool slot
 constexpr uint32_t NOSRC = 0xffffffffu;
 constexpr int NHUB = 32;                // hub blocks of k2_handle
@@ -262,6 +263,45 @@ __device__ __forceinline__ void block_alloc2(Ctl &C, uint32_t nw, uint32_t nf, u
   __syncthreads();  // (s_w / s_base are reused by the next call)
 }
 
+// The end of the sorted-run chunk that starts at r0 (a run is dispatched in rank-order chunks of at most
+// WCAP).  A chunk does not end inside a same-ts group unless the group alone fills it: the chunk's
+// DoForwardUp leaves at a cut group's ts are queued (K_FWD_UP_D, their uids sort after the whole group), so
+// a chunk that continues a cut group ends with the group and the run ends there (*trim: the rest of the
+// run goes back to the pool, k_trim) — the queued leaves are then dispatched before any later event.
+// Every thread of the block calls it.
+template <int NT>
+__device__ void run_chunk_end(const P2PDev &M, uint64_t r0, uint64_t rW, uint64_t &r1_out, bool &trim_out) {
+  __shared__ unsigned long long s_r1;
+  __shared__ uint32_t s_trim;
+  const uint64_t r1 = r0 + (uint64_t)WCAP < rW ? r0 + (uint64_t)WCAP : rW;
+  const uint64_t t0 = M.wkey[r0] >> 32, tl = M.wkey[r1 - 1] >> 32;
+  const bool cont = r0 > 0 && (M.wkey[r0 - 1] >> 32) == t0;
+  const bool cut = r1 < rW && (M.wkey[r1] >> 32) == tl;
+  if (threadIdx.x == 0) {
+    s_r1 = r1;
+    s_trim = 0;
+  }
+  __syncthreads();
+  if (cont && tl != t0) {  // the continued group ends inside [r0, r1): the chunk ends with it
+    for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT)
+      if ((M.wkey[i] >> 32) > t0) {
+        atomicMin(&s_r1, (unsigned long long)i);
+        break;
+      }
+    if (threadIdx.x == 0) s_trim = 1;
+  } else if (!cont && cut) {  // back off to the start of the group the chunk would cut (unless it fills it)
+    for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT)
+      if ((M.wkey[i] >> 32) == tl) {
+        if (i > r0) atomicMin(&s_r1, (unsigned long long)i);
+        break;
+      }
+  }
+  __syncthreads();
+  r1_out = s_r1;
+  trim_out = s_trim != 0;
+  __syncthreads();
+}
+
 // ---- k2_pa ----
 // DIST: a partitioned rank's variant: children on other ranks' nodes are skipped (they travel through
 // X2), the remote events the last X2 brought are classified like children (a role of whole blocks
@@ -485,8 +525,8 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     }
   } else if (partition && run) {
     // ---- the next chunk of the sorted run: per-node slot tables, chunk bounds
-    const uint64_t r0 = C.r0, rW = C.rW;
-    const uint32_t Wc = (uint32_t)(rW - r0 < (uint64_t)WCAP ? rW - r0 : (uint64_t)WCAP);
+    const uint64_t r0 = C.r0, rW = C.rW, rn = C.rnext;
+    const uint32_t Wc = (uint32_t)(rn - r0);  // (run_chunk_end: at most WCAP)
     const uint64_t s = g - NSG;
     if (s == 0) {
       C.W = Wc;
@@ -556,6 +596,27 @@ __device__ __forceinline__ uint32_t local_record(const P2PDev &M, const Emit &E,
   M.wa[rec] = E.la;
   M.wpkt[rec] = Pkt{0, 0, 0, 0};
   M.wpar[rec] = par | ((uint32_t)E.lj << 24);
+  // its chain for k2_rank: the parent's, one level up
+  LKey x;
+  if (par < LBASE) {
+    const uint64_t pk = M.wkey[par];
+    x.rel[1] = (uint32_t)(pk >> 32);
+    x.uid = (uint32_t)pk;
+    x.depth = 1;
+  } else {
+    const LKey p = M.lkey[par - LBASE];
+#pragma unroll
+    for (int t = 0; t + 1 < LKD; t++) x.rel[t + 1] = p.rel[t];
+#pragma unroll
+    for (int t = 0; t + 1 < 16; t++) x.j[t + 1] = p.j[t];
+    x.uid = p.uid;
+    x.depth = p.depth + 1;
+    if (x.depth >= (uint32_t)LKD) atomicOr(M.error, 32u);  // (create keeps chains shorter: Lx <= LKD tx_min)
+  }
+  x.rel[0] = (uint32_t)(E.lts - tmin);
+  x.j[0] = (uint8_t)E.lj;
+  x.pad[0] = x.pad[1] = 0;
+  M.lkey[rec - LBASE] = x;
   return rec;
 }
 // A node's pending local records, sorted by rel ts (ties: creation order = the parents' order); head qh.
@@ -1350,8 +1411,7 @@ __device__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool ha
   }
 }
 
-// WIDE: the single engine's wide windows (local records; the rank tiles rank the gen-0 records among
-// themselves, k2_scan places the local records).
+// WIDE: the single engine's wide windows (local records: k2_rank places them after the handlers).
 template <bool WIDE>
 __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   __shared__ uint64_t lds64[(WIDE ? K2_LDS_WORDS_W : K2_LDS_WORDS) / 2];
@@ -1435,17 +1495,22 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   BLK_REC(1, c_win);
 }
 
-// The local regions' prefix (NLR + 1 entries) from M.lcnt, into LDS; every thread of the block calls it.
+// The local regions' prefix (NLR + 1 entries) into LDS from each thread's region count v (M.lcnt[thread],
+// 0 past NLR); every thread of the block calls it.
 template <int NT>
-__device__ __forceinline__ void local_prefix(const P2PDev &M, bool any, uint32_t *pre) {
-  static_assert(NT >= NLR, "one thread per region");
-  const uint32_t v = (any && threadIdx.x < (uint32_t)NLR) ? M.lcnt[threadIdx.x] : 0u;
-  if (threadIdx.x < (uint32_t)NLR) pre[threadIdx.x + 1] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    pre[0] = 0;
-    for (int r = 1; r <= NLR; r++) pre[r] += pre[r - 1];
+__device__ __forceinline__ void local_prefix(uint32_t v, uint32_t *pre) {
+  static_assert(NT >= NLR && NLR <= 128, "one thread per region, two waves");
+  __shared__ uint32_t s_w0;
+  const int lane = threadIdx.x & 63;
+  for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scan
+    const uint32_t x = __shfl_up(v, o);
+    if (lane >= o) v += x;
   }
+  if (threadIdx.x == 63) s_w0 = v;
+  __syncthreads();
+  if (threadIdx.x >= 64) v += s_w0;
+  if (threadIdx.x < (uint32_t)NLR) pre[threadIdx.x + 1] = v;
+  if (threadIdx.x == 0) pre[0] = 0;
   __syncthreads();
 }
 // Record index -> dense index (gen-0 slot, or W + its region's prefix + its offset in the region).
@@ -1456,52 +1521,143 @@ __device__ __forceinline__ uint32_t dense_of(uint32_t rec, uint32_t W, const uin
   const uint32_t o2 = off - (uint32_t)(NHB * LR);
   return W + pre[NHB + o2 / LRH] + o2 % LRH;
 }
-// First position of a sorted LDS array whose value is >= v.
-template <typename T>
-__device__ __forceinline__ uint32_t lds_lower(const T *a, uint32_t n, T v) {
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint32_t m = (lo + hi) >> 1;
-    if (a[m] < v) lo = m + 1;
-    else hi = m;
-  }
-  return lo;
+// ---- k2_rank (wide engines): every record's rank in the window's dispatch order, after the handlers ----
+// All pairs of the window's records (gen-0 and local) by their chains (LKey): compare level by level —
+// rel ts, then a gen-0 record before a local one, gen-0 ancestors by uid; chains that reach the same gen-0
+// ancestor are ordered by the child index just below the first level where they part.
+constexpr int RKT = 256;   // rows (threads) and columns per tile
+constexpr int RK_GRID = 1024;
+__device__ __forceinline__ LKey lkey_of(const P2PDev &M, uint32_t r) {
+  if (r >= LBASE) return M.lkey[r - LBASE];
+  const uint64_t k = M.wkey[r];
+  LKey x;
+  x.rel[0] = (uint32_t)(k >> 32);
+  x.uid = (uint32_t)k;
+  x.depth = 0;
+  return x;
 }
-// Ascending bitonic sort of n keys in LDS (n a power of two) by the whole block; ends synchronised.
-template <int NT>
-__device__ __forceinline__ void bitonic_lds64(uint64_t *a, uint32_t n) {
-  for (uint32_t k = 2; k <= n; k <<= 1)
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < n / 2; i += NT) {
-        const uint32_t x = ((i & ~(j - 1)) << 1) | (i & (j - 1)), y = x + j;
-        const uint64_t u = a[x], v = a[y];
-        if ((u > v) == ((x & k) == 0)) {
-          a[x] = v;
-          a[y] = u;
+// a before b (distinct records)
+__device__ __forceinline__ bool lk_before(const LKey &a, const LKey &b) {
+#pragma unroll
+  for (int t = 0; t < LKD; t++) {
+    if (a.rel[t] != b.rel[t]) return a.rel[t] < b.rel[t];
+    const bool ga = (uint32_t)t == a.depth, gb = (uint32_t)t == b.depth;
+    if (ga != gb) return ga;
+    if (ga) {
+      if (a.uid != b.uid) return a.uid < b.uid;
+      for (int u = t - 1; u >= 0; u--)
+        if (a.j[u] != b.j[u]) return a.j[u] < b.j[u];
+      return false;
+    }
+  }
+  return false;  // (deeper chains are refused at create)
+}
+// A local record's chain order packed into two words (lexicographic), the LKey compare only for a tie:
+// word 1 = rel ts, local, the parent's rel ts; word 2 = a gen-0 parent's uid and the child index (exact:
+// records tie only with themselves), or a local parent's: its parent's rel ts and class, and that one's
+// uid or parent rel ts (clamped: a tie falls back to the LKey compare).
+__device__ __forceinline__ uint64_t lk_word(const LKey &k) {
+  const uint32_t r1 = k.rel[1] < 0x7fffffffu ? k.rel[1] : 0x7fffffffu;
+  return ((uint64_t)k.rel[0] << 32) | 0x80000000u | r1;
+}
+__device__ __forceinline__ uint64_t lk_word2(const LKey &k) {
+  if (k.depth == 1) return ((uint64_t)k.uid << 8) | k.j[0];
+  const bool g2 = k.depth == 2;  // (the grandparent is the gen-0 ancestor)
+  const uint32_t r2 = k.rel[2] < 0x7fffffffu ? k.rel[2] : 0x7fffffffu;
+  const uint32_t nx = g2 ? k.uid : k.rel[3];
+  return (1ull << 63) | ((uint64_t)r2 << 31) | ((g2 ? 0ull : 1ull) << 30) | (nx < 0x3fffffffu ? nx : 0x3fffffffu);
+}
+// The gen-0 records' ranks among themselves come from k2_handle's rank tiles (keys known before the
+// handlers run); here, tiles of (all records x local records) add the local records before each record,
+// and tiles of (local records x gen-0 records) the gen-0 records before each local one (rel ts only: at
+// equal ts a gen-0 record comes first).
+__global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
+  Ctl &C = *M.C;
+  const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run;
+  const uint64_t lim = C.lim_rel;
+  if (c_done || c_mode >= MODE_SORT || c_mode == MODE_RUN || W > (uint32_t)WCAP || c_fr || lim == 0) return;
+  __shared__ uint32_t pre[NLR + 1];
+  __shared__ uint64_t cw[RKT], cw2[RKT];
+  __shared__ LKey ck[RKT];
+  local_prefix<RKT>(threadIdx.x < (uint32_t)NLR ? M.lcnt[threadIdx.x] : 0u, pre);
+  const uint32_t Lt = pre[NLR], N = W + Lt;
+  if (Lt == 0 || N > (uint32_t)NMAX) return;  // (N > NMAX: k2_scan fails the run, error 64)
+
+  const uint32_t nr = (N + RKT - 1) / RKT, nl = (Lt + RKT - 1) / RKT, ng = (W + RKT - 1) / RKT;
+  const uint32_t na = nr * nl;  // phase A tiles, then phase B (nl x ng)
+  for (uint32_t t = blockIdx.x; t < na + nl * ng; t += gridDim.x) {  // (uniform over the block)
+    uint32_t c = 0, rx = 0;
+    if (t < na) {  // rows: every record; columns: local records
+      const uint32_t ti = t / nl, tj = t % nl;
+      const uint32_t cy = tj * RKT + threadIdx.x, ix = ti * RKT + threadIdx.x;
+      if (cy < Lt) {
+        const LKey k = M.lkey[dense_rec(W + cy, W, pre) - LBASE];
+        ck[threadIdx.x] = k;
+        cw[threadIdx.x] = lk_word(k);
+        cw2[threadIdx.x] = lk_word2(k);
+      }
+      LKey kx;
+      uint64_t wx = 0, wx2 = 0;
+      const bool lx = ix >= W;
+      if (ix < N) {
+        rx = dense_rec(ix, W, pre);
+        if (lx) {
+          kx = M.lkey[rx - LBASE];
+          wx = lk_word(kx);
+          wx2 = lk_word2(kx);
+        } else {
+          wx = (M.wkey[rx] >> 32) << 32;  // (a local record of smaller rel ts comes first)
         }
       }
       __syncthreads();
+      const uint32_t jn = Lt - tj * RKT < (uint32_t)RKT ? Lt - tj * RKT : (uint32_t)RKT;
+      if (ix < N) {
+        if (lx) {
+          for (uint32_t y = 0; y < jn; y++) {
+            const uint64_t wy = cw[y];
+            if (wy != wx) {
+              c += wy < wx;
+            } else {
+              const uint64_t wy2 = cw2[y];
+              c += wy2 < wx2 || (wy2 == wx2 && W + tj * RKT + y != ix && lk_before(ck[y], kx));
+            }
+          }
+        } else {
+          for (uint32_t y = 0; y < jn; y++) c += cw[y] < wx;
+        }
+      }
+    } else {  // rows: local records; columns: gen-0 records (rel ts <= the row's)
+      const uint32_t u = t - na, ti = u / ng, tj = u % ng;
+      const uint32_t cy = tj * RKT + threadIdx.x, ix = ti * RKT + threadIdx.x;
+      if (cy < W) cw[threadIdx.x] = M.wkey[cy] >> 32;
+      uint64_t relx = 0;
+      if (ix < Lt) {
+        rx = dense_rec(W + ix, W, pre);
+        relx = M.wkey[rx] >> 32;
+      }
+      __syncthreads();
+      const uint32_t jn = W - tj * RKT < (uint32_t)RKT ? W - tj * RKT : (uint32_t)RKT;
+      if (ix < Lt)
+        for (uint32_t y = 0; y < jn; y++) c += cw[y] <= relx;
     }
+    if (c) atomicAdd(&M.wrank[rx], c);
+    __syncthreads();
+  }
 }
 
 // ---- k2_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
-// WIDE: the single engine's wide windows.  Every record's rank in the dispatch order (ts, uid) is settled
-// here: the gen-0 records' ranks among themselves come from k2_handle's rank tiles (their keys are known
-// before the handlers run); a local record's uid is not known yet (its parent's child prefix + its child
-// index, assigned below), but its place is: after every gen-0 record of its ts (their uids are older), and
-// among the local records of one ts in their parents' order, then by child index (DefaultSimulatorImpl
-// gives uids in Schedule order).  Parents have smaller timestamps, so passes over the groups of equal ts
-// settle one more generation each.
+// WIDE: the single engine's wide windows: the local records join the gen-0 ones (ranks from k2_rank), and
+// a local record's uid is its parent's child prefix + its child index (DefaultSimulatorImpl gives uids in
+// Schedule order).
 template <bool WIDE>
 __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   Ctl &C = *M.C;
   // one thread per RPT records (dense order: the W gen-0 slots, then the local records region by region);
-  // the rank-ordered arrays hold NREC records.  Wide: the ranking's scratch (local keys, gen-0 rel ts by
-  // rank, final ranks, parents) shares the buffer, 144 KB of LDS.
+  // the rank-ordered arrays hold NREC records (wide: 128 KB of LDS)
   constexpr int NREC = WIDE ? NMAX : WCAP;
   constexpr int RPT = NREC / SCAN_THREADS;
   constexpr int RPT0 = WCAP / SCAN_THREADS;  // (the gen-0 part, loaded speculatively at entry)
-  constexpr int SBUF = WIDE ? 4 * NMAX + WCAP : 4 * WCAP;
+  constexpr int SBUF = 4 * NREC;
   __shared__ uint32_t sbuf[SBUF];
   uint32_t *l_slot = sbuf, *l_cnt = sbuf + NREC, *l_rel = sbuf + 2 * NREC, *gstart = sbuf + 3 * NREC;
   __shared__ uint32_t pre[NLR + 1];
@@ -1515,7 +1671,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run, c_wbase = C.wbase;
   const uint32_t c_nhub = C.nhub, uid0 = C.uid;
   const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush, c_lim = C.lim_rel, c_bound = C.bound,
-                 c_nbound = C.nbound;
+                 c_nbound = C.nbound, c_r0 = C.r0, c_rW = C.rW;
+  const uint32_t c_rtrim = C.rtrim;
+  const uint32_t c_lcnt = (WIDE && tid < NLR) ? M.lcnt[tid] : 0u;  // (the local regions' counts, at once)
   // the bookkeeping's run control as well (thread 0 writes it back at the end; loaded now, its trip
   // overlaps the slot loads instead of following the scan)
   struct Book {
@@ -1579,7 +1737,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     return;
   }
   // ---- the local records (wide windows): dense positions W .. N-1
-  if constexpr (WIDE) local_prefix<SCAN_THREADS>(M, c_lim != 0 && !run, pre);
+  if constexpr (WIDE) local_prefix<SCAN_THREADS>(c_lim != 0 && !run ? c_lcnt : 0u, pre);
   const uint32_t Lt = (WIDE && !run) ? pre[NLR] : 0u;
   const uint32_t N = W + Lt;
   if (N > (uint32_t)NREC) {  // (the adaptive span keeps windows well inside; a run that got here fails loudly)
@@ -1611,112 +1769,25 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       if (i >= W && i < N) {  // a local record
         const uint32_t r = dense_rec(i, W, pre);
         prec[q] = r;
+        pr[q] = M.wrank[r];
         pc[q] = M.nchild[r] | (M.ninl[r] << 16);
         prel[q] = (uint32_t)(M.wkey[r] >> 32);
         M.pwctx[r] = M.wctx[r];
         ppx[q] = M.wpar[r];
       }
     }
-    if (Lt) {  // ---- the ranking (see above)
-      uint64_t *keys = reinterpret_cast<uint64_t *>(sbuf);  // [P] local records: rel ts << 32 | local index
-      uint32_t *g0rel = sbuf + 2 * NMAX;                     // [W] gen-0 rel ts by gen-0 rank (ascending)
-      uint32_t *F = g0rel + WCAP;                            // [N] final rank by dense index
-      uint32_t *lpar = F + NMAX;                             // [Lt] parent's dense index | child index << 24
-      uint32_t P = 64;
-      while (P < Lt) P <<= 1;
+    if (Lt) {  // a local record's parent's rank (its uid below is the parent's child prefix + j)
+      uint32_t *Fd = sbuf;  // [N] rank by dense index
 #pragma unroll
       for (int q = 0; q < RPT; q++) {
         const uint32_t i = tid + q * SCAN_THREADS;
-        if (i < W) {
-          g0rel[pr[q]] = prel[q];
-        } else if (i < N) {
-          const uint32_t k = i - W;
-          keys[k] = ((uint64_t)prel[q] << 32) | k;
-          lpar[k] = dense_of(ppx[q] & 0xffffffu, W, pre) | (ppx[q] & 0xff000000u);
-        }
-      }
-      for (uint32_t k = Lt + tid; k < P; k += SCAN_THREADS) keys[k] = ~0ull;
-      __syncthreads();
-      bitonic_lds64<SCAN_THREADS>(keys, P);
-      // a gen-0 record: its gen-0 rank + the local records of smaller ts
-#pragma unroll
-      for (int q = 0; q < RPT0; q++) {
-        const uint32_t i = tid + q * SCAN_THREADS;
-        if (i < W) {
-          pr[q] += lds_lower<uint64_t>(keys, Lt, (uint64_t)prel[q] << 32);
-          F[i] = pr[q];
-        }
-      }
-      // a local record (sorted position p): the gen-0 records up to its ts + the local records of smaller
-      // ts (its group's base) + its place in its group of equal ts
-      uint32_t glo[RPT], ghi[RPT], gbase[RPT];
-      bool multi = false, lpm = false;
-#pragma unroll
-      for (int u = 0; u < RPT; u++) {
-        const uint32_t p = tid + u * SCAN_THREADS;
-        glo[u] = ghi[u] = gbase[u] = 0;
-        if (p < Lt) {
-          const uint64_t key = keys[p];
-          const uint32_t rel = (uint32_t)(key >> 32), k = (uint32_t)key;
-          const uint32_t lo = lds_lower<uint64_t>(keys, Lt, (uint64_t)rel << 32);
-          const uint32_t hi = lds_lower<uint64_t>(keys, Lt, (uint64_t)(rel + 1) << 32);
-          const uint32_t b = lo + lds_lower<uint32_t>(g0rel, W, rel + 1);
-          glo[u] = lo;
-          ghi[u] = hi;
-          gbase[u] = b;
-          F[W + k] = b + (hi - lo == 1 ? 0u : p - lo);  // (a group of one is placed; others: a first guess)
-          if (hi - lo > 1) {
-            multi = true;
-            lpm |= (lpar[k] & 0xffffffu) >= W;  // (a local parent: its rank may move while this settles)
-          }
-        }
-      }
-      const bool any_multi = __syncthreads_or(multi);
-      if (any_multi) {
-        const bool iterate = __syncthreads_or(lpm);
-        for (int pass = 0;; pass++) {
-          uint32_t nv[RPT];
-          bool ch = false;
-#pragma unroll
-          for (int u = 0; u < RPT; u++) {
-            const uint32_t p = tid + u * SCAN_THREADS;
-            nv[u] = 0;
-            if (p < Lt && ghi[u] - glo[u] > 1) {
-              const uint32_t k = (uint32_t)keys[p], me = lpar[k];
-              const uint32_t pf = F[me & 0xffffffu], j = me >> 24;
-              uint32_t cnt = 0;
-              for (uint32_t m = glo[u]; m < ghi[u]; m++) {
-                const uint32_t o = lpar[(uint32_t)keys[m]];
-                const uint32_t pf2 = F[o & 0xffffffu], j2 = o >> 24;
-                cnt += pf2 < pf || (pf2 == pf && j2 < j);
-              }
-              nv[u] = gbase[u] + cnt;
-              ch |= nv[u] != F[W + k];
-            }
-          }
-          __syncthreads();
-#pragma unroll
-          for (int u = 0; u < RPT; u++) {
-            const uint32_t p = tid + u * SCAN_THREADS;
-            if (p < Lt && ghi[u] - glo[u] > 1) F[W + (uint32_t)keys[p]] = nv[u];
-          }
-          const bool again = __syncthreads_or(ch);
-          if (!iterate || !again) break;
-          if (pass == 64) {  // (a generation per pass: cannot happen within a window)
-            if (tid == 0) atomicOr(M.error, 64u);
-            break;
-          }
-        }
+        if (i < N) Fd[i] = pr[q];
       }
       __syncthreads();
 #pragma unroll
       for (int q = 0; q < RPT; q++) {
         const uint32_t i = tid + q * SCAN_THREADS;
-        if (i >= W && i < N) {
-          const uint32_t o = lpar[i - W];
-          pr[q] = F[i];
-          ppx[q] = F[o & 0xffffffu] | ((o >> 24) << 16);  // (the parent's rank < NMAX, child index)
-        }
+        if (i >= W && i < N) ppx[q] = Fd[dense_of(ppx[q] & 0xffffffu, W, pre)] | ((ppx[q] >> 24) << 16);
       }
       __syncthreads();  // (the buffer holds the rank-ordered arrays next)
     }
@@ -1826,10 +1897,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
         M.pwkey[r] = ((uint64_t)prel[q] << 32) | (uint32_t)(uid0 + gstart[ppx[q] & 0xffffu] + (ppx[q] >> 16));
         M.lrec[i - W] = r;
       }
-      if (!run && i < W) M.wrank[r] = 0;
+      if (!run) M.wrank[r] = 0;
     }
   }
   if (WIDE && Lt && tid < NLR) M.lcnt[tid] = 0;
+  // the next chunk of a sorted run (a block search over the run's keys: every thread calls it)
+  uint64_t rn1 = 0;
+  bool rtrim = false;
+  if (run && c_r0 + W < c_rW && !c_rtrim) run_chunk_end<SCAN_THREADS>(M, c_r0 + W, c_rW, rn1, rtrim);
   PH_MARK(19);
   if (tid == 0) {
     C.pK0 = bk.K;
@@ -1860,8 +1935,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     if (run) {
       r0 += W;
       C.r0 = r0;
-      if (r0 >= bk.rW) mode = MODE_NORMAL;
-      else flip = false;  // the run's chunks keep folding into the same reduction
+      if (r0 >= bk.rW) {
+        mode = MODE_NORMAL;
+      } else if (c_rtrim) {  // the chunk ended a cut same-ts group: the run ends, k_trim returns the rest
+        mode = MODE_TRIM;
+      } else {
+        flip = false;  // the run's chunks keep folding into the same reduction
+        C.rnext = rn1;
+        C.rtrim = rtrim ? 1u : 0u;
+      }
     } else if (WIDE) {  // wide windows: keep them inside the window capacity (WCAP gen-0, NMAX records)
       const uint64_t span = c_bound >> 32;
       if (N > (uint32_t)(7 * NMAX / 8) || W > (uint32_t)(7 * WCAP / 8)) C.span_t = span - span / 4;
@@ -1877,7 +1959,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     C.windows = windows;
     if (N > bk.max_window) C.max_window = N;
     C.W = 0;
-    const uint64_t pending = live + (tc - tinl - Lt) + (mode == MODE_RUN ? bk.rW - r0 : 0);
+    const uint64_t pending = live + (tc - tinl - Lt) + ((mode == MODE_RUN || mode == MODE_TRIM) ? bk.rW - r0 : 0);
     bool done = bk.stop_seen || (pending == 0 && bk.hts == ~0ull);
     if (P_end > M.pool_cap) {
       atomicOr(M.error, 1u);
@@ -1889,6 +1971,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     }
     if (done) {
       C.done = 1;
+      if (mode == MODE_TRIM) mode = MODE_NORMAL;  // (the final window is appended by the next k2_pa)
     } else if (mode == MODE_NORMAL && bk.hcap) {  // the window was cut at the next host closure: pause
       C.hcap = 0;
       mode = MODE_HOST;
@@ -2084,7 +2167,7 @@ __global__ __launch_bounds__(1024) void k_renarrow(const P2PDev M) {
       R.stopuid = (uint32_t)key;
     }
   }
-  publish_min<1024>(R, tmn, wnd, wndw);
+  publish_min<1024, true>(R, tmn, wnd, wndw);
   if (threadIdx.x == 0) {
     C.P_end = P0 + m;
     C.live += m;
@@ -2097,10 +2180,59 @@ __global__ __launch_bounds__(1024) void k_renarrow(const P2PDev M) {
 }
 
 // Mode transitions the host makes after a host-driven step.
-__global__ void k_after_sort(const P2PDev M) {
+__global__ __launch_bounds__(1024) void k_after_sort(const P2PDev M) {
+  const uint64_t rW = M.C->rW;
+  uint64_t r1 = 0;
+  bool trim = false;
+  if (rW) run_chunk_end<1024>(M, 0, rW, r1, trim);
+  if (threadIdx.x != 0) return;
   M.C->mode = MODE_RUN;
   M.C->r0 = 0;
+  M.C->rnext = r1;
+  M.C->rtrim = trim ? 1u : 0u;
   M.C->lim_rel = 0;  // (a run has no local records)
+}
+
+// A run that ended after a cut same-ts group (run_chunk_end): its records [r0, rW) go back to the pool and
+// fold into the reduction that bounds the next window (k2_scan flipped rt when it asked for the trim).
+__global__ __launch_bounds__(1024) void k_trim(const P2PDev M) {
+  Ctl &C = *M.C;
+  const uint64_t cut = C.r0, n = C.rW, tmin = C.tmin, P0 = C.P_end, m = n - cut;
+  if (P0 + m > M.pool_cap) {
+    if (threadIdx.x == 0) atomicOr(M.error, 1u);
+    return;
+  }
+  Red &R = C.red[C.rt ^ 1];
+  uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull;
+  for (uint64_t i = cut + threadIdx.x; i < n; i += 1024) {
+    const uint64_t key = M.wkey[i];
+    const uint64_t ts = tmin + (key >> 32);
+    const uint32_t kind = M.wkind[i];
+    const uint64_t d = P0 + (i - cut);
+    M.ev_ts[0][d] = ts;
+    M.ev_uid[0][d] = (uint32_t)key;
+    M.ev_ctx[0][d] = M.wctx[i];
+    M.ev_kind[0][d] = kind;
+    M.ev_a[0][d] = M.wa[i];
+    M.ev_pkt[0][d] = M.wpkt[i];
+    tmn = ts < tmn ? ts : tmn;
+    const uint64_t x = ts + (uint64_t)M.lookahead[kind & 0xffu], xw = ts + (uint64_t)M.lookw[kind & 0xffu];
+    wnd = x < wnd ? x : wnd;
+    wndw = xw < wndw ? xw : wndw;
+    if ((kind & 0xffu) == K_STOP) {
+      R.stopts = ts;
+      R.stopuid = (uint32_t)key;
+    }
+  }
+  publish_min<1024, true>(R, tmn, wnd, wndw);
+  if (threadIdx.x == 0) {
+    C.P_end = P0 + m;
+    C.live += m;
+    C.rW = cut;
+    C.rtrim = 0;
+    if (m) C.hcap = 0;  // (the host event's key is past these: a later window reaches it)
+    C.mode = MODE_NORMAL;
+  }
 }
 __global__ void k_after_compact(const P2PDev M, uint64_t live) {
   M.C->P_end = live;

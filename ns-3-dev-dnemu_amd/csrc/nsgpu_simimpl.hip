@@ -1,6 +1,7 @@
 // nsgpu_simimpl.hip — the host-closure runtime behind ns3::HipSimulatorImpl: events whose closures
 // stay on the host (EventImpl*), kept in the device-resident HipBatchScheduler (nsgpu_sched), dispatched
-// in WINDOWS, optionally interleaved with a GPU-resident p2p engine in one (ts, uid) order.
+// in WINDOWS, optionally interleaved with a GPU-resident p2p engine or the closed-loop Wi-Fi PHY
+// (nsgpu_wifil) in one (ts, uid) order.
 //
 // Contract (the reference semantics it keeps — default-simulator-impl.cc:49-353 — are listed so the
 // parity tests can cite them): uids from 4, ScheduleDestroy consumes one (:235-242); Now / Context / uid
@@ -44,6 +45,7 @@ constexpr uint64_t RAW = 1;  // handle tag: a caller-owned handle (nsgpu_sim_ins
 struct nsgpu_sim {
   nsgpu_sched *events = nullptr;
   nsgpu_p2p *p2p = nullptr;
+  nsgpu_wifil *wifi = nullptr;  // closed-loop Wi-Fi PHY (nsgpu_sim_attach_wifi)
   void *stream = nullptr;
   bool stop = false, ended = false, dev_stopped = false;
   uint32_t uid = 4;
@@ -116,6 +118,7 @@ struct nsgpu_sim {
   int device_pending(uint64_t *n, uint64_t *next_ts) {
     *n = 0;
     *next_ts = ~0ull;
+    if (wifi) return nsgpu_wifil_pending(wifi, n, next_ts);
     if (!p2p || ended) return NSGPU_OK;
     int stopped = 0;
     return nsgpu_p2p_pending(p2p, n, next_ts, &stopped, stream);
@@ -157,6 +160,15 @@ int nsgpu_sim_attach_p2p(nsgpu_sim *s, nsgpu_p2p *h) {
   if (rc) return rc;
   s->p2p = h;
   s->uid = u;
+  return NSGPU_OK;
+}
+
+// The closed-loop Wi-Fi PHY joins this runtime's order: its events are scheduled at run time only (the
+// host closures' SendPacket calls), so it takes no setup uids.
+int nsgpu_sim_attach_wifi(nsgpu_sim *s, nsgpu_wifil *h) {
+  if (!s || !h) return set_error(NSGPU_EINVAL, "nsgpu_sim_attach_wifi: null");
+  if (s->p2p || s->wifi) return set_error(NSGPU_ESTATE, "nsgpu_sim_attach_wifi: an engine is attached already");
+  s->wifi = h;
   return NSGPU_OK;
 }
 
@@ -307,6 +319,21 @@ static int pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n,
   int rc;
   nsgpu_event e;
   nsgpu_sched *q = s->events;
+  if (s->wifi) {  // the PHY's events below the next host event's key, then that host event (one per window)
+    bool have = false;
+    if (q->size) {
+      if (!nsgpu::sched_next(q, &e, false, &rc)) return rc ? rc : set_error(NSGPU_ESTATE, "pop_window: lost events");
+      have = true;
+    }
+    rc = nsgpu_wifil_advance(s->wifi, have ? e.ts : ~0ull, have ? e.uid : 0u, &s->uid, &s->dispatched, &s->digest,
+                             s->log_ts, s->log_uid, s->log_ctx, s->log_cap);
+    if (rc || !have) return rc;
+    if ((rc = nsgpu::sched_remove_next1(q, &e))) return rc;
+    out[0] = e;
+    s->win.push_back(e);
+    *n = 1;
+    return NSGPU_OK;
+  }
   if (s->p2p && !s->ended) {
     bool have = false;
     if (q->size) {
@@ -544,6 +571,26 @@ int nsgpu_sim_live_closures(nsgpu_sim *s, uint64_t *n) {
   if (!s || !n) return set_error(NSGPU_EINVAL, "nsgpu_sim_live_closures: null");
   *n = s->slab.size() - s->free_slots.size();
   return NSGPU_OK;
+}
+
+// A host closure's YansWifiPhy::SendPacket on `phy` of the attached Wi-Fi PHY (now; YansWifiChannel::Send's
+// receiver loop takes the runtime's next uids, one per receiver).
+int nsgpu_sim_wifi_send(nsgpu_sim *s, uint32_t phy, uint32_t size, double dbm, uint32_t modclass, uint64_t rate,
+                        uint32_t bw, uint32_t preamble) {
+  if (!s || !s->wifi) return set_error(NSGPU_ESTATE, "nsgpu_sim_wifi_send: no Wi-Fi PHY attached");
+  uint32_t n = 0;
+  int rc = nsgpu_wifil_receivers(s->wifi, phy, &n);
+  if (rc) return rc;
+  rc = nsgpu_wifil_send(s->wifi, s->cur_ts, s->uid, phy, size, dbm, modclass, rate, bw, preamble);
+  if (rc) return rc;
+  s->uid += n;
+  return NSGPU_OK;
+}
+
+// WifiPhyStateHelper::GetState of `phy` at Now (the device has run every event before the running closure).
+int nsgpu_sim_wifi_state(nsgpu_sim *s, uint32_t phy, nsgpu_wifil_phy_state *out) {
+  if (!s || !s->wifi) return set_error(NSGPU_ESTATE, "nsgpu_sim_wifi_state: no Wi-Fi PHY attached");
+  return nsgpu_wifil_get_state(s->wifi, phy, s->cur_ts, out);
 }
 
 // A host closure's UdpSocket::Send on application `app` of the attached engine (now, with the uid

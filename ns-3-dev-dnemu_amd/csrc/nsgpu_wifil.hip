@@ -1,0 +1,877 @@
+// nsgpu_wifil.hip — the closed-loop Wi-Fi PHY on the device (include/nsgpu.h: nsgpu_wifil_*, and
+// nsgpu_sim_attach_wifi / nsgpu_sim_wifi_send / nsgpu_sim_wifi_state in nsgpu_simimpl.hip).
+//
+// Replaces, for transmissions that host closures start at run time (a MAC on the host):
+// YansWifiPhy::SendPacket (yans-wifi-phy.cc:499-522) -> YansWifiChannel::Send (yans-wifi-channel.cc:77-115)
+// -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496) with InterferenceHelper::Add / AppendEvent /
+// GetEnergyDuration (interference-helper.cc:129-212), the WifiPhyStateHelper transitions
+// (wifi-phy-state-helper.cc:122-183, 254-322, 391-423), and YansWifiPhy::EndReceive (yans-wifi-phy.cc:770-799)
+// with InterferenceHelper::CalculateSnrPer (interference-helper.cc:215-353) and the error-rate models
+// (nist-error-rate-model.cc, yans-error-rate-model.cc, dsss-error-rate-model.cc).  EndReceive's m_random
+// draw (:783) is the host's: each EndReceive's (snr, per) goes back to it (nsgpu_wifil_read_ends).
+//
+// Epochs.  The host runtime (nsgpu_sim) owns the uid counter and the dispatch order; before it runs a host
+// closure with key (T, u) it advances the device to that key (nsgpu_wifil_advance): every phy's lane runs
+// its pending Receive / EndReceive events with keys below (T, u), in (ts, uid) order, then the epoch's
+// syncs get their EndReceive uids.  A host closure's SendPacket (nsgpu_wifil_send) applies the sender's
+// state switch at once and queues one Receive per receiver, with the uids the runtime hands out.
+// Order inside one phy needs no global rank: every Receive's uid is known when it is queued (the runtime's
+// counter at the SendPacket), and an EndReceive scheduled in the running epoch has a uid above every uid
+// handed out before the epoch — so it sorts after those at equal ts, and among themselves by their syncing
+// Receives' keys (uids follow the dispatch order of the events that schedule them).
+//
+// State per phy lives in HBM between epochs: the InterferenceHelper list as a time-sorted ring (the r02
+// RingNi layout of nsgpu_wifi.hip, with its eager prefix cursor), the state helper's end times, the pending
+// Receive queue (sorted by (arrival, uid)) and up to LPE_CAP pending EndReceive records.
+#include <algorithm>
+#include <vector>
+#include "nsgpu_device.h"
+#include "nsgpu_internal.h"
+
+namespace nsgpu {
+namespace {
+
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr int LPE_CAP = 8;  // pending EndReceive records of one phy (the live one + cancelled ones)
+constexpr uint32_t WE_TX_IN_TX = 1, WE_NICAP = 2, WE_RQCAP = 4, WE_PECAP = 8, WE_CAP = 16;
+constexpr int NB = 8;  // ring entries loaded per batch
+
+struct LNi {  // InterferenceHelper::NiChange (interference-helper.cc:91-110)
+  int64_t t;
+  double d;
+};
+struct LRx {  // a pending Receive: arrival, uid, transmission, rxPowerW (DbmToW of CalcRxPower + RxGain)
+  uint64_t at;
+  uint32_t uid, tx;
+  double w;
+};
+struct LPe {  // a pending EndReceive
+  uint64_t ts, sts;          // its ts; the syncing Receive's ts
+  uint32_t suid, euid;       // the syncing Receive's uid; its own uid (NONE: scheduled in the running epoch)
+  uint32_t tx, can, sslot, used;
+  double w;                  // rxPowerW
+};
+struct LTx {  // one SendPacket: duration and payload mode
+  uint64_t ts;
+  int64_t dur;
+  uint64_t rate;
+  uint32_t phy, mc, bw, preamble;
+};
+struct LPhy {  // a phy's state between epochs
+  double firstPower, cur_s;      // InterferenceHelper::m_firstPower; the ring's prefix-cursor sum
+  int64_t endTx, endRx, endCca;  // WifiPhyStateHelper m_endTx / m_endRx / m_endCcaBusy
+  uint32_t rxing, head, len, cur_n;
+  uint32_t rq_head, rq_len, live, ni_max;
+  nsgpu_wifi_phy_counters c;
+};
+struct LEv {  // one dispatched device event of the epoch
+  uint64_t ts;
+  uint32_t uid, ctx, sslot, pad;
+};
+struct LSync {  // one sync of the epoch (its EndReceive's uid comes from the sync order)
+  uint64_t sts;
+  uint32_t suid, euid;
+};
+
+struct WDev {
+  int64_t nphy;
+  const double *x, *y, *z;
+  const uint32_t *chan, *chan_rank, *node;
+  nsgpu_loss_chain loss;
+  double speed, rx_gain_db, edW, ccaW, nf;  // nf: the noise figure as a ratio (DbToRatio)
+  uint32_t model, ni_mask, rq_mask, pad;
+  uint64_t inv_hi, inv_lo;  // int64x64_t::Invert (1e9): Time::GetSeconds at NS resolution
+  LPhy *ps;
+  LNi *ni;
+  LRx *rq;
+  LPe *pe;
+  LTx *tx;
+  LSync *sync;
+  LEv *ev;
+  nsgpu_wifil_end *ends;
+  uint32_t *end_sslot;
+  uint32_t *cnt;  // [0] events, [1] syncs, [2] ends, [3] error bits
+  uint64_t sync_cap, ev_cap, end_cap;
+};
+
+// ---- WifiMode attributes (the CreateWifiMode calls of wifi-phy.cc:355-840; phyRate: wifi-mode.cc:140-155) ----
+struct Mode {
+  uint32_t mc, bw, phy_rate, cons, code;  // code: 0 undefined, 1: 1/2, 2: 2/3, 3: 3/4
+  uint64_t data_rate;
+};
+__host__ __device__ __forceinline__ Mode make_mode(uint32_t mc, uint64_t rate, uint32_t bw) {
+  Mode m{mc, mc == NSGPU_WIFI_DSSS ? 22000000u : bw, (uint32_t)rate, rate == 1000000 ? 2u : 4u, 0u, rate};
+  if (mc == NSGPU_WIFI_DSSS) return m;
+  switch (rate * 20000000ull / m.bw) {  // the 20 MHz OFDM ladder; 10 / 5 MHz channels run at 1/2, 1/4 the rates
+    case 6000000: m.cons = 2, m.code = 1; break;
+    case 9000000: m.cons = 2, m.code = 3; break;
+    case 12000000: m.cons = 4, m.code = 1; break;
+    case 18000000: m.cons = 4, m.code = 3; break;
+    case 24000000: m.cons = 16, m.code = 1; break;
+    case 36000000: m.cons = 16, m.code = 3; break;
+    case 48000000: m.cons = 64, m.code = 2; break;
+    default: m.cons = 64, m.code = 3; break;
+  }
+  const uint32_t dr = (uint32_t)rate;
+  m.phy_rate = m.code == 1 ? dr * 2 / 1 : m.code == 2 ? dr * 3 / 2 : dr * 4 / 3;
+  return m;
+}
+// WifiPhy::GetPlcpHeaderMode — wifi-phy.cc:99-139
+__device__ __forceinline__ Mode header_mode(const Mode &p, uint32_t preamble) {
+  if (p.mc == NSGPU_WIFI_OFDM)
+    return p.bw == 5000000 ? make_mode(NSGPU_WIFI_OFDM, 1500000, 5000000)
+           : p.bw == 10000000 ? make_mode(NSGPU_WIFI_OFDM, 3000000, 10000000)
+                              : make_mode(NSGPU_WIFI_OFDM, 6000000, 20000000);
+  if (p.mc == NSGPU_WIFI_ERP_OFDM) return make_mode(NSGPU_WIFI_ERP_OFDM, 6000000, 20000000);
+  return make_mode(NSGPU_WIFI_DSSS, preamble == NSGPU_WIFI_PREAMBLE_LONG ? 1000000 : 2000000, 22000000);
+}
+// WifiPhy::GetPlcpPreambleDurationMicroSeconds / GetPlcpHeaderDurationMicroSeconds — wifi-phy.cc:141-231
+__device__ __forceinline__ uint32_t preamble_us(uint32_t mc, uint32_t bw, uint32_t preamble) {
+  if (mc == NSGPU_WIFI_OFDM) return bw == 10000000 ? 32 : bw == 5000000 ? 64 : 16;
+  if (mc == NSGPU_WIFI_ERP_OFDM) return 4;
+  return preamble == NSGPU_WIFI_PREAMBLE_SHORT ? 72 : 144;
+}
+__device__ __forceinline__ uint32_t header_us(uint32_t mc, uint32_t bw, uint32_t preamble) {
+  if (mc == NSGPU_WIFI_OFDM) return bw == 10000000 ? 8 : bw == 5000000 ? 16 : 4;
+  if (mc == NSGPU_WIFI_ERP_OFDM) return 16;
+  return preamble == NSGPU_WIFI_PREAMBLE_SHORT ? 24 : 48;
+}
+
+// ---- error-rate models ----
+// DsssErrorRateModel — dsss-error-rate-model.cc:29-127, ENABLE_GSL unset (the CCK rates use the Matlab fits)
+__device__ double dsss_success(uint64_t rate, double sinr, uint32_t nbits) {
+  double ber;
+  switch (rate) {
+    case 1000000: {
+      double EbN0 = sinr * 22000000.0 / 1000000.0;
+      ber = 0.5 * exp(-EbN0);
+      break;
+    }
+    case 2000000: {
+      double x = sinr * 22000000.0 / 1000000.0 / 2.0;  // DqpskFunction (:29-35)
+      ber = ((sqrt(2.0) + 1.0) / sqrt(8.0 * 3.1415926 * sqrt(2.0))) * (1.0 / sqrt(x)) * exp(-(2.0 - sqrt(2.0)) * x);
+      break;
+    }
+    case 5500000:
+      if (sinr > 10.0) ber = 0.0;
+      else if (sinr < 0.1) ber = 0.5;
+      else ber = 5.3681634344056195e-001 * exp(-(pow((sinr - 3.3092430025608586e-003) / 4.1654372361004000e-001,
+                                                     1.0288981434358866e+000)));
+      break;
+    case 11000000:
+      if (sinr > 10.0) ber = 0.0;
+      else if (sinr < 0.1) ber = 0.5;
+      else {
+        const double a1 = 7.9056742265333456e-003, a2 = -1.8397449399176360e-001, a3 = 1.0740689468707241e+000,
+                     a4 = 1.0523316904502553e+000, a5 = 3.0552298746496687e-001, a6 = 2.2032715128698435e+000;
+        ber = (a1 * sinr * sinr + a2 * sinr + a3) / (sinr * sinr * sinr + a4 * sinr * sinr + a5 * sinr + a6);
+      }
+      break;
+    default:
+      return 0;
+  }
+  return pow((1.0 - ber), (double)nbits);
+}
+// NistErrorRateModel — nist-error-rate-model.cc:38-270 (YansWifiPhyHelper::Default's model)
+__device__ double nist_pe(double p, uint32_t b) {  // CalculatePe
+  const double D = sqrt(4.0 * p * (1.0 - p));
+  if (b == 1)
+    return 0.5 * (36.0 * pow(D, 10.0) + 211.0 * pow(D, 12.0) + 1404.0 * pow(D, 14.0) + 11633.0 * pow(D, 16.0) +
+                  77433.0 * pow(D, 18.0) + 502690.0 * pow(D, 20.0) + 3322763.0 * pow(D, 22.0) +
+                  21292910.0 * pow(D, 24.0) + 134365911.0 * pow(D, 26.0));
+  if (b == 2)
+    return 1.0 / (2.0 * b) *
+           (3.0 * pow(D, 6.0) + 70.0 * pow(D, 7.0) + 285.0 * pow(D, 8.0) + 1276.0 * pow(D, 9.0) + 6160.0 * pow(D, 10.0) +
+            27128.0 * pow(D, 11.0) + 117019.0 * pow(D, 12.0) + 498860.0 * pow(D, 13.0) + 2103891.0 * pow(D, 14.0) +
+            8784123.0 * pow(D, 15.0));
+  return 1.0 / (2.0 * b) *
+         (42.0 * pow(D, 5.0) + 201.0 * pow(D, 6.0) + 1492.0 * pow(D, 7.0) + 10469.0 * pow(D, 8.0) + 62935.0 * pow(D, 9.0) +
+          379644.0 * pow(D, 10.0) + 2253373.0 * pow(D, 11.0) + 13073811.0 * pow(D, 12.0) + 75152755.0 * pow(D, 13.0) +
+          428005675.0 * pow(D, 14.0));
+}
+__device__ double nist_success(const Mode &m, double snr, uint32_t nbits) {
+  if (m.mc == NSGPU_WIFI_DSSS) return dsss_success(m.data_rate, snr, nbits);
+  const uint32_t b = m.cons == 64 ? (m.code == 2 ? 2u : 3u) : (m.code == 1 ? 1u : 3u);
+  double ber;
+  switch (m.cons) {
+    case 2: ber = 0.5 * erfc(sqrt(snr)); break;                               // GetBpskBer
+    case 4: ber = 0.5 * erfc(sqrt(snr / 2.0)); break;                         // GetQpskBer
+    case 16: ber = 0.75 * 0.5 * erfc(sqrt(snr / (5.0 * 2.0))); break;         // Get16QamBer
+    default: ber = 7.0 / 12.0 * 0.5 * erfc(sqrt(snr / (21.0 * 2.0))); break;  // Get64QamBer
+  }
+  if (ber == 0.0) return 1.0;  // GetFec*Ber
+  double pe = nist_pe(ber, b);
+  pe = pe < 1.0 ? pe : 1.0;
+  return pow(1 - pe, (double)nbits);
+}
+// YansErrorRateModel — yans-error-rate-model.cc:45-300
+__device__ uint32_t yans_factorial(uint32_t k) {
+  uint32_t f = 1;
+  while (k > 0) f *= k--;
+  return f;
+}
+__device__ double yans_binomial(uint32_t k, double p, uint32_t n) {
+  return yans_factorial(n) / (yans_factorial(k) * yans_factorial(n - k)) * pow(p, (double)k) * pow(1 - p, (double)(n - k));
+}
+__device__ double yans_pd(double ber, uint32_t d) {  // CalculatePd (Odd / Even)
+  double pd = 0;
+  if ((d % 2) == 0) {
+    for (uint32_t i = d / 2 + 1; i < d; i++) pd += yans_binomial(i, ber, d);
+    pd += 0.5 * yans_binomial(d / 2, ber, d);
+  } else {
+    for (uint32_t i = (d + 1) / 2; i < d; i++) pd += yans_binomial(i, ber, d);
+  }
+  return pd;
+}
+__device__ double yans_success(const Mode &m, double snr, uint32_t nbits) {
+  if (m.mc == NSGPU_WIFI_DSSS) return dsss_success(m.data_rate, snr, nbits);
+  const double EbNo = snr * m.bw / m.phy_rate;
+  if (m.cons == 2) {  // GetFecBpskBer
+    const double ber = 0.5 * erfc(sqrt(EbNo));
+    const uint32_t dFree = m.code == 1 ? 10 : 5, adFree = m.code == 1 ? 11 : 8;
+    if (ber == 0.0) return 1.0;
+    double pmu = adFree * yans_pd(ber, dFree);
+    pmu = pmu < 1.0 ? pmu : 1.0;
+    return pow(1 - pmu, (double)nbits);
+  }
+  const unsigned int M = m.cons;  // GetQamBer + GetFecQamBer
+  const double z = sqrt((1.5 * (log((double)M) / log(2.0)) * EbNo) / (M - 1.0));
+  const double z1 = ((1.0 - 1.0 / sqrt((double)M)) * erfc(z));
+  const double z2 = 1 - pow((1 - z1), 2.0);
+  const double ber = z2 / (log((double)M) / log(2.0));
+  uint32_t dFree, adFree, adFree1;
+  if (M == 64) {
+    if (m.code == 2) dFree = 6, adFree = 1, adFree1 = 16;
+    else dFree = 5, adFree = 8, adFree1 = 31;
+  } else {
+    if (m.code == 1) dFree = 10, adFree = 11, adFree1 = 0;
+    else dFree = 5, adFree = 8, adFree1 = 31;
+  }
+  if (ber == 0.0) return 1.0;
+  double pmu = adFree * yans_pd(ber, dFree);
+  pmu += adFree1 * yans_pd(ber, dFree + 1);
+  pmu = pmu < 1.0 ? pmu : 1.0;
+  return pow(1 - pmu, (double)nbits);
+}
+
+// Time::GetSeconds at NS resolution: To (S) = MulByInvert (Invert (1e9)) then GetDouble
+// (nstime.h:398-431, int64x64-128.cc:94-118, int64x64-128.h:83-95).
+__device__ __forceinline__ double get_seconds(const WDev &D, int64_t ts) {
+  const bool neg = ts < 0;
+  const u128 a = (u128)(neg ? -ts : ts) << 64;
+  const u128 b = ((u128)D.inv_hi << 64) | D.inv_lo;
+  const u128 ah = a >> 64, bh = b >> 64, al = a & (u128)~0ull, bl = b & (u128)~0ull;
+  u128 mid = ah * bl + al * bh;
+  mid >>= 64;
+  const u128 r = ah * bh + mid;
+  const uint64_t hi = (uint64_t)(r >> 64), lo = (uint64_t)r;
+  double flo = (double)lo;
+  flo /= 18446744073709551615.0;
+  double v = (double)hi;
+  v += flo;
+  return neg ? -v : v;
+}
+// InterferenceHelper::CalculateChunkSuccessRate — interference-helper.cc:244-255
+__device__ double chunk(const WDev &D, double snir, int64_t duration, const Mode &m) {
+  if (duration == 0) return 1.0;
+  const uint32_t rate = m.phy_rate;
+  const uint64_t nbits = (uint64_t)(rate * get_seconds(D, duration));
+  return D.model == NSGPU_WIFIL_YANS ? yans_success(m, snir, (uint32_t)nbits) : nist_success(m, snir, (uint32_t)nbits);
+}
+// InterferenceHelper::CalculateSnr — interference-helper.cc:215-227
+__device__ __forceinline__ double snr_of(const WDev &D, double signal, double noiseInterference, const Mode &m) {
+  const double Nt = 1.3803e-23 * 290.0 * m.bw;  // BOLTZMANN
+  const double noiseFloor = D.nf * Nt;
+  const double noise = noiseFloor + noiseInterference;
+  return signal / noise;
+}
+
+// ---- the NiChanges ring of one phy (RingNi of nsgpu_wifi.hip: time-sorted, eager prefix cursor) ----
+__device__ __forceinline__ void ni_insert(LNi *ring, uint32_t head, uint32_t &len, uint32_t m, int64_t t, double d) {
+  uint32_t q = len;  // AddNiChangeEvent (interference-helper.cc:378-383): at upper_bound (time)
+  while (q > 0) {
+    const LNi e = ring[(head + q - 1) & m];
+    if (e.t <= t) break;
+    ring[(head + q) & m] = e;
+    q--;
+  }
+  ring[(head + q) & m] = LNi{t, d};
+  len++;
+}
+template <bool LE>
+__device__ __forceinline__ void cursor_advance(const LNi *ring, uint32_t head, uint32_t len, uint32_t m, int64_t lim,
+                                               uint32_t &cur_n, double &cur_s) {
+  while (cur_n < len) {
+    LNi e[NB];
+#pragma unroll
+    for (int u = 0; u < NB; u++) e[u] = ring[(head + cur_n + u) & m];
+#pragma unroll
+    for (int u = 0; u < NB; u++) {
+      if (cur_n >= len || (LE ? e[u].t > lim : e[u].t >= lim)) return;
+      cur_s += e[u].d;
+      cur_n++;
+    }
+  }
+}
+
+// EndReceive's order key against another pending EndReceive of the same phy (ts, then uid; a uid of the
+// running epoch is above every known one, and those order by their syncing Receives' keys).
+__device__ __forceinline__ bool pe_before(const LPe &a, const LPe &b) {
+  if (a.ts != b.ts) return a.ts < b.ts;
+  const bool ka = a.euid != NONE, kb = b.euid != NONE;
+  if (ka != kb) return ka;
+  if (ka) return a.euid < b.euid;
+  return a.sts != b.sts ? a.sts < b.sts : a.suid < b.suid;
+}
+
+// One phy's events of the epoch: every pending Receive / EndReceive with a key below (bts, buid).
+__global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint32_t buid) {
+  const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (j >= D.nphy) return;
+  LPhy P = D.ps[j];
+  LNi *ring = D.ni + (uint64_t)j * (D.ni_mask + 1);
+  LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
+  LPe *pe = D.pe + (uint64_t)j * LPE_CAP;
+  const uint32_t m = D.ni_mask, ctx = D.node[j];
+  uint32_t err = 0;
+  for (;;) {
+    // the next pending EndReceive and the next Receive
+    int e = -1;
+    LPe eb{};
+    for (int q = 0; q < LPE_CAP; q++) {
+      const LPe c = pe[q];
+      if (c.used && (e < 0 || pe_before(c, eb))) e = q, eb = c;
+    }
+    const bool hr = P.rq_len > 0;
+    LRx r{};
+    if (hr) r = rq[P.rq_head & D.rq_mask];
+    bool take_r;
+    if (hr && e >= 0) take_r = r.at < eb.ts || (r.at == eb.ts && (eb.euid == NONE || r.uid < eb.euid));
+    else if (hr) take_r = true;
+    else if (e >= 0) take_r = false;
+    else break;
+    if (take_r) {
+      if (!(r.at < bts || (r.at == bts && r.uid < buid))) break;
+    } else {
+      if (!(eb.ts < bts || (eb.ts == bts && eb.euid != NONE && eb.euid < buid))) break;
+    }
+    if (!take_r) {  // ---- YansWifiPhy::EndReceive (yans-wifi-phy.cc:770-799)
+      const int64_t nw = (int64_t)eb.ts;
+      nsgpu_wifil_end rec{eb.ts, eb.euid, (uint32_t)j, 0.0, 0.0, eb.tx, eb.can ? (uint32_t)NSGPU_WIFI_END_CANCELLED : 0u};
+      P.c.end++;
+      if (eb.can) {  // EventImpl::Invoke skips a cancelled event (event-impl.cc:40-46); still dispatched
+        P.c.end_cancelled++;
+      } else {
+        // InterferenceHelper::CalculateSnrPer (interference-helper.cc:336-353): ni = (start, m_firstPower), the
+        // list after the event's own start entry (the ring's head: no fold while receiving) up to its end
+        // entry, (end, 0) — CalculateNoiseInterferenceW (:229-243) — then CalculatePer's walk (:257-334)
+        const LTx t = D.tx[eb.tx];
+        const Mode pm = make_mode(t.mc, t.rate, t.bw), hm = header_mode(pm, t.preamble);
+        const double noise0 = P.firstPower;
+        rec.snr = snr_of(D, eb.w, noise0, pm);
+        const int64_t t0 = (int64_t)eb.sts;
+        const int64_t hdrStart = t0 + (int64_t)preamble_us(t.mc, pm.bw, t.preamble) * 1000;
+        const int64_t payStart = hdrStart + (int64_t)header_us(t.mc, pm.bw, t.preamble) * 1000;
+        double psr = 1.0, noiseW = noise0;
+        int64_t previous = t0;
+        uint32_t q = 1;
+        for (bool last = false; !last;) {
+          int64_t current;
+          double delta;
+          if (q < P.len) {
+            const LNi en = ring[(P.head + q) & m];
+            if (en.t == nw && eb.w == -en.d) {
+              current = nw, delta = 0.0, last = true;  // (the event's end entry: the closing (end, 0))
+            } else {
+              current = en.t, delta = en.d;
+            }
+            q++;
+          } else {
+            current = nw, delta = 0.0, last = true;
+          }
+          if (previous >= payStart) {
+            psr *= chunk(D, snr_of(D, eb.w, noiseW, pm), current - previous, pm);
+          } else if (previous >= hdrStart) {
+            if (current >= payStart) {
+              psr *= chunk(D, snr_of(D, eb.w, noiseW, hm), payStart - previous, hm);
+              psr *= chunk(D, snr_of(D, eb.w, noiseW, pm), current - payStart, pm);
+            } else {
+              psr *= chunk(D, snr_of(D, eb.w, noiseW, hm), current - previous, hm);
+            }
+          } else {
+            if (current >= payStart) {
+              psr *= chunk(D, snr_of(D, eb.w, noiseW, hm), payStart - hdrStart, hm);
+              psr *= chunk(D, snr_of(D, eb.w, noiseW, pm), current - payStart, pm);
+            } else if (current >= hdrStart) {
+              psr *= chunk(D, snr_of(D, eb.w, noiseW, hm), current - hdrStart, hm);
+            }
+          }
+          noiseW += delta;
+          previous = current;
+        }
+        rec.per = 1 - psr;
+        P.rxing = 0;  // NotifyRxEnd (); SwitchFromRxEndOk / Error -> DoSwitchFromRx (wifi-phy-state-helper.cc:391-402)
+      }
+      const uint32_t sl = eb.euid == NONE ? eb.sslot : NONE;
+      const uint32_t ei = atomicAdd(&D.cnt[2], 1u);
+      if (ei < D.end_cap) {
+        D.ends[ei] = rec;
+        D.end_sslot[ei] = sl;
+      } else {
+        err |= WE_CAP;
+      }
+      const uint32_t vi = atomicAdd(&D.cnt[0], 1u);
+      if (vi < D.ev_cap) D.ev[vi] = LEv{eb.ts, eb.euid, ctx, sl, 0};
+      else err |= WE_CAP;
+      pe[e].used = 0;
+      if (P.live == (uint32_t)e) P.live = NONE;
+      continue;
+    }
+    // ---- YansWifiChannel::Receive -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496)
+    P.rq_head++;
+    P.rq_len--;
+    const int64_t nw = (int64_t)r.at;
+    const int64_t endNew = nw + D.tx[r.tx].dur;
+    if (P.len + 2 > m + 1) {
+      err |= WE_NICAP;
+      break;
+    }
+    // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
+    if (!P.rxing) {  // fold the entries up to upper_bound (now) into m_firstPower; the new entry first
+      cursor_advance<true>(ring, P.head, P.len, m, nw, P.cur_n, P.cur_s);
+      P.head = (P.head + P.cur_n) & m;
+      P.len -= P.cur_n;
+      P.cur_n = 0;
+      P.head = (P.head - 1) & m;
+      ring[P.head] = LNi{nw, r.w};
+      P.len++;
+      P.firstPower = P.cur_s;
+    } else {
+      ni_insert(ring, P.head, P.len, m, nw, r.w);
+    }
+    ni_insert(ring, P.head, P.len, m, endNew, -r.w);
+    P.ni_max = P.len > P.ni_max ? P.len : P.ni_max;
+    const int st = P.endTx > nw ? 2 : P.rxing ? 1 : P.endCca > nw ? 3 : 0;  // GetState (:159-183)
+    bool maybe = false;
+    P.c.rx++;
+    if (st == 1 || st == 2) {  // drop; noise after the current Rx / Tx (:431-457)
+      if (st == 1) P.c.drop_rx++;
+      else P.c.drop_tx++;
+      int64_t until = (st == 1 ? P.endRx : P.endTx) - nw;  // GetDelayUntilIdle (:122-151)
+      until = until > 0 ? until : 0;
+      maybe = endNew > nw + until;
+    } else if (r.w > D.edW) {  // sync (:461-472): SwitchToRx, NotifyRxStart, Schedule (rxDuration, EndReceive)
+      int q = -1;
+      for (int k = 0; k < LPE_CAP; k++)
+        if (!pe[k].used) {
+          q = k;
+          break;
+        }
+      const uint32_t sl = atomicAdd(&D.cnt[1], 1u);
+      if (q < 0 || sl >= D.sync_cap) {
+        err |= q < 0 ? WE_PECAP : WE_CAP;
+        break;
+      }
+      D.sync[sl] = LSync{r.at, r.uid, NONE};
+      pe[q] = LPe{(uint64_t)endNew, r.at, r.uid, NONE, r.tx, 0, sl, 1, r.w};
+      P.live = (uint32_t)q;
+      P.rxing = 1;
+      P.endRx = endNew;
+      P.c.sync++;
+    } else {
+      P.c.drop_ed++;
+      maybe = true;
+    }
+    if (maybe) {  // maybeCcaBusy (:485-495): GetEnergyDuration (interference-helper.cc:171-190)
+      cursor_advance<false>(ring, P.head, P.len, m, nw, P.cur_n, P.cur_s);
+      double noise = P.cur_s;
+      int64_t end = nw;
+      for (uint32_t q = P.cur_n; q < P.len; q++) {
+        const LNi en = ring[(P.head + q) & m];
+        noise += en.d;
+        end = en.t;
+        if (noise < D.ccaW) break;
+      }
+      const int64_t cca = end > nw ? end - nw : 0;
+      if (cca != 0) {  // SwitchMaybeToCcaBusy (wifi-phy-state-helper.cc:404-423)
+        P.endCca = P.endCca > nw + cca ? P.endCca : nw + cca;
+        P.c.cca_switches++;
+      }
+    }
+    const uint32_t vi = atomicAdd(&D.cnt[0], 1u);
+    if (vi < D.ev_cap) D.ev[vi] = LEv{r.at, r.uid, ctx, NONE, 0};
+    else err |= WE_CAP;
+  }
+  D.ps[j] = P;
+  if (err) atomicOr(&D.cnt[3], err);
+}
+
+// The epoch's syncs in dispatch order (ts, uid of the syncing Receive): EndReceive uid = uid0 + rank.
+__global__ __launch_bounds__(256) void k_wl_rank(const WDev D, uint32_t uid0) {
+  const uint32_t n = D.cnt[1] < D.sync_cap ? D.cnt[1] : (uint32_t)D.sync_cap;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const LSync a = D.sync[i];
+    uint32_t r = 0;
+    for (uint32_t k = 0; k < n; k++) {
+      const LSync b = D.sync[k];
+      r += b.sts < a.sts || (b.sts == a.sts && b.suid < a.suid);
+    }
+    D.sync[i].euid = uid0 + r;
+  }
+}
+// The epoch's EndReceive uids into its dispatched events, its end records and the still pending records.
+__global__ __launch_bounds__(256) void k_wl_patch(const WDev D) {
+  const uint32_t nev = D.cnt[0] < D.ev_cap ? D.cnt[0] : (uint32_t)D.ev_cap;
+  const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
+  const uint64_t npe = (uint64_t)D.nphy * LPE_CAP;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nev + nend + npe; i += (uint64_t)gridDim.x * 256) {
+    if (i < nev) {
+      const uint32_t sl = D.ev[i].sslot;
+      if (sl != NONE) D.ev[i].uid = D.sync[sl].euid;
+    } else if (i < nev + nend) {
+      const uint32_t sl = D.end_sslot[i - nev];
+      if (sl != NONE) D.ends[i - nev].uid = D.sync[sl].euid;
+    } else {
+      LPe &p = D.pe[i - nev - nend];
+      if (p.used && p.euid == NONE) p.euid = D.sync[p.sslot].euid;
+    }
+  }
+}
+
+// SendPacket of phy s at (ts): the sender's state switch (thread s) and one Receive per receiver.
+__global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t, double dbm, uint32_t base) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j == 0) D.tx[k] = t;
+  if (j >= D.nphy) return;
+  const uint32_t s = t.phy;
+  if ((uint32_t)j == s) {  // YansWifiPhy::SendPacket (yans-wifi-phy.cc:499-522)
+    LPhy &P = D.ps[j];
+    if (P.endTx > (int64_t)t.ts) {  // NS_ASSERT (!IsStateTx ()); SwitchToTx from TX: NS_FATAL_ERROR (:285-287)
+      atomicOr(&D.cnt[3], WE_TX_IN_TX);
+      return;
+    }
+    if (P.rxing) {  // m_endRxEvent.Cancel (); NotifyRxEnd (); SwitchToTx's RX case (:263-268)
+      D.pe[(uint64_t)j * LPE_CAP + P.live].can = 1;
+      P.live = NONE;
+      P.rxing = 0;
+      P.endRx = (int64_t)t.ts;
+    }
+    P.endTx = (int64_t)t.ts + t.dur;
+    return;
+  }
+  if (D.chan[j] != D.chan[s]) return;  // YansWifiChannel::Send: other channels get nothing (:88-91)
+  const double dist = distance3(D.x[s], D.y[s], D.z[s], D.x[j], D.y[j], D.z[j]);
+  const uint64_t at = t.ts + (uint64_t)seconds_to_ts(dist / D.speed);  // ConstantSpeed delay (propagation-delay-model.cc:90-96)
+  const double dBm = calc_rx_power(D.loss, dbm, dist) + D.rx_gain_db;      // StartReceivePacket: rxPowerDbm += RxGain
+  const double w = pow(10.0, dBm / 10.0) / 1000.0;                         // DbmToW (yans-wifi-phy.cc:727-732)
+  const uint32_t uid = base + D.chan_rank[j] - (j > (int64_t)s ? 1u : 0u);  // the receiver loop's Schedule order
+  LPhy &P = D.ps[j];
+  LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
+  if (P.rq_len > D.rq_mask) {
+    atomicOr(&D.cnt[3], WE_RQCAP);
+    return;
+  }
+  uint32_t q = P.rq_len;  // sorted by (arrival, uid)
+  while (q > 0) {
+    const LRx e = rq[(P.rq_head + q - 1) & D.rq_mask];
+    if (e.at < at || (e.at == at && e.uid < uid)) break;
+    rq[(P.rq_head + q) & D.rq_mask] = e;
+    q--;
+  }
+  rq[(P.rq_head + q) & D.rq_mask] = LRx{at, uid, k, w};
+  P.rq_len++;
+}
+
+// Pending device events and the smallest ts among them (Next / IsFinished).
+__global__ __launch_bounds__(256) void k_wl_pending(const WDev D, unsigned long long *out) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= D.nphy) return;
+  const LPhy P = D.ps[j];
+  uint64_t n = P.rq_len, mt = P.rq_len ? D.rq[(uint64_t)j * (D.rq_mask + 1) + (P.rq_head & D.rq_mask)].at : ~0ull;
+  for (int q = 0; q < LPE_CAP; q++) {
+    const LPe &p = D.pe[(uint64_t)j * LPE_CAP + q];
+    if (p.used) n++, mt = p.ts < mt ? p.ts : mt;
+  }
+  if (n) {
+    atomicAdd(&out[0], (unsigned long long)n);
+    atomicMin(&out[1], (unsigned long long)mt);
+  }
+}
+
+// int64x64_t::Invert (int64x64-128.cc:119-134) with Divu (:70-92) and MulByInvert (:94-118), on the host.
+u128 umul_by_invert(u128 a, u128 b) {
+  const u128 ah = a >> 64, bh = b >> 64, al = a & (u128)~0ull, bl = b & (u128)~0ull;
+  u128 mid = ah * bl + al * bh;
+  mid >>= 64;
+  return ah * bh + mid;
+}
+u128 invert(uint64_t v) {
+  const u128 a = (u128)1 << 64;
+  u128 quo = a / v, rem = a % v;  // Divu (a, v)
+  u128 result = quo << 64;
+  u128 div;
+  if ((rem >> 64) == 0) rem <<= 64, div = v;
+  else div = (u128)v >> 64;
+  result += rem / div;
+  const u128 tmp = umul_by_invert((u128)v << 64, result);  // int64x64_t (v, false).MulByInvert (result)
+  if ((uint64_t)(tmp >> 64) != 1) result += 1;             // GetHigh () != 1
+  return result;
+}
+
+}  // namespace
+}  // namespace nsgpu
+
+using namespace nsgpu;
+
+struct nsgpu_wifil {
+  WDev D{};
+  hipStream_t s = nullptr;
+  std::vector<void *> allocs;
+  std::vector<uint32_t> recv;  // fan-out uids of one SendPacket per phy
+  uint64_t n_tx = 0, tx_cap = 0;
+  uint32_t *h_cnt = nullptr;  // pinned: the epoch counters
+  unsigned long long *d_pend = nullptr, *h_pend = nullptr;
+  std::vector<LEv> ev;
+  std::vector<nsgpu_wifil_end> ends, ends_epoch;
+};
+
+template <class T>
+static int wl_alloc(nsgpu_wifil *h, T **p, size_t n, const T *src = nullptr) {
+  void *v = nullptr;
+  NSGPU_HIP(hipMalloc(&v, std::max<size_t>(n, 1) * sizeof(T)));
+  h->allocs.push_back(v);
+  if (src && n) NSGPU_HIP(hipMemcpy(v, src, n * sizeof(T), hipMemcpyHostToDevice));
+  else NSGPU_HIP(hipMemset(v, 0, std::max<size_t>(n, 1) * sizeof(T)));
+  *p = (T *)v;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifil_destroy(nsgpu_wifil *h) {
+  if (!h) return NSGPU_OK;
+  if (h->s) {
+    (void)hipStreamSynchronize(h->s);
+    (void)hipStreamDestroy(h->s);
+  }
+  for (void *p : h->allocs) (void)hipFree(p);
+  if (h->h_cnt) (void)hipHostFree(h->h_cnt);
+  if (h->h_pend) (void)hipHostFree(h->h_pend);
+  delete h;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out) {
+  if (!c || !out || c->n_phy <= 0 || !c->x || !c->y || !c->z || !c->channel || !c->node)
+    return set_error(NSGPU_EINVAL, "nsgpu_wifil_create: bad config");
+  const auto pow2 = [](uint32_t v) { return v >= 2 && (v & (v - 1)) == 0; };
+  if (!pow2(c->ni_cap) || !pow2(c->rxq_cap) || c->tx_cap == 0 || c->tx_cap >= 0xffffffffull || c->loss.n < 0 ||
+      c->loss.n > NSGPU_MAX_LOSS_CHAIN || c->error_model > NSGPU_WIFIL_YANS)
+    return set_error(NSGPU_EINVAL, "nsgpu_wifil_create: ni_cap / rxq_cap must be powers of two >= 2, tx_cap in (0, 2^32)");
+  nsgpu_wifil *h = new nsgpu_wifil();
+  const int64_t N = c->n_phy;
+  WDev &D = h->D;
+  D.nphy = N;
+  D.loss = c->loss;
+  D.speed = c->speed;
+  D.rx_gain_db = c->rx_gain_db;
+  D.edW = pow(10.0, c->ed_threshold_dbm / 10.0) / 1000.0;   // SetEdThreshold (yans-wifi-phy.cc:228-232)
+  D.ccaW = pow(10.0, c->cca_threshold_dbm / 10.0) / 1000.0; // SetCcaMode1Threshold (:234-238)
+  D.nf = pow(10.0, c->rx_noise_figure_db / 10.0);           // SetRxNoiseFigure: DbToRatio (:192-197)
+  D.model = c->error_model;
+  D.ni_mask = c->ni_cap - 1;
+  D.rq_mask = c->rxq_cap - 1;
+  const u128 inv = invert(1000000000ull);
+  D.inv_hi = (uint64_t)(inv >> 64);
+  D.inv_lo = (uint64_t)inv;
+  // the receiver loop's order on each channel (m_phyList order)
+  std::vector<uint32_t> rank((size_t)N);
+  h->recv.resize((size_t)N);
+  {
+    std::vector<std::pair<uint32_t, uint32_t>> cnt;  // (channel, count so far)
+    for (int64_t j = 0; j < N; j++) {
+      auto it = std::find_if(cnt.begin(), cnt.end(), [&](const std::pair<uint32_t, uint32_t> &p) { return p.first == c->channel[j]; });
+      if (it == cnt.end()) cnt.emplace_back(c->channel[j], 0), it = cnt.end() - 1;
+      rank[j] = it->second++;
+    }
+    for (int64_t j = 0; j < N; j++)
+      for (auto &p : cnt)
+        if (p.first == c->channel[j]) h->recv[j] = p.second - 1;
+  }
+  const uint64_t ev_cap = (uint64_t)N * 64 + 4096, sync_cap = (uint64_t)N * LPE_CAP + 1024;
+  int rc;
+#define WL_TRY(x)                \
+  if ((rc = (x)) != NSGPU_OK) {  \
+    nsgpu_wifil_destroy(h);      \
+    return rc;                   \
+  }
+  WL_TRY(wl_alloc(h, (double **)&D.x, N, c->x));
+  WL_TRY(wl_alloc(h, (double **)&D.y, N, c->y));
+  WL_TRY(wl_alloc(h, (double **)&D.z, N, c->z));
+  WL_TRY(wl_alloc(h, (uint32_t **)&D.chan, N, c->channel));
+  WL_TRY(wl_alloc(h, (uint32_t **)&D.node, N, c->node));
+  WL_TRY(wl_alloc(h, (uint32_t **)&D.chan_rank, N, rank.data()));
+  std::vector<LPhy> ps((size_t)N);
+  for (auto &p : ps) p.live = NONE;
+  WL_TRY(wl_alloc(h, &D.ps, N, ps.data()));
+  WL_TRY(wl_alloc(h, &D.ni, (size_t)N * c->ni_cap));
+  WL_TRY(wl_alloc(h, &D.rq, (size_t)N * c->rxq_cap));
+  WL_TRY(wl_alloc(h, &D.pe, (size_t)N * LPE_CAP));
+  WL_TRY(wl_alloc(h, &D.tx, c->tx_cap));
+  WL_TRY(wl_alloc(h, &D.sync, sync_cap));
+  WL_TRY(wl_alloc(h, &D.ev, ev_cap));
+  WL_TRY(wl_alloc(h, &D.ends, sync_cap));
+  WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
+  WL_TRY(wl_alloc(h, &D.cnt, 4));
+  WL_TRY(wl_alloc(h, &h->d_pend, 2));
+#undef WL_TRY
+  D.sync_cap = sync_cap;
+  D.ev_cap = ev_cap;
+  D.end_cap = sync_cap;
+  h->tx_cap = c->tx_cap;
+  if (hipHostMalloc((void **)&h->h_cnt, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&h->h_pend, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
+    nsgpu_wifil_destroy(h);
+    return set_error(NSGPU_EHIP, "nsgpu_wifil_create: host buffers / stream");
+  }
+  *out = h;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifil_receivers(nsgpu_wifil *h, uint32_t phy, uint32_t *n) {
+  if (!h || !n || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_receivers: bad phy");
+  *n = h->recv[phy];
+  return NSGPU_OK;
+}
+
+static int wl_check(nsgpu_wifil *h, const char *what) {
+  const uint32_t e = h->h_cnt[3];
+  if (!e) return NSGPU_OK;
+  if (e & WE_TX_IN_TX)
+    return set_error(NSGPU_ESTATE, "%s: SendPacket while transmitting (yans-wifi-phy.cc:508 NS_ASSERT)", what);
+  return set_error(NSGPU_ENOMEM, "%s: capacity exceeded (bits %u: 2 NiChanges ring, 4 Receive queue, 8 pending "
+                                 "EndReceive records, 16 epoch lists)", what, e);
+}
+
+// YansWifiPhy::SendPacket of `phy` from the host closure running at (now, closure uid); its fan-out takes
+// the uids uid_base .. uid_base + receivers - 1 (nsgpu_wifil_receivers).
+extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base, uint32_t phy, uint32_t size, double dbm,
+                                uint32_t modclass, uint64_t rate, uint32_t bw, uint32_t preamble) {
+  if (!h || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_send: bad phy");
+  if (h->n_tx >= h->tx_cap) return set_error(NSGPU_ENOMEM, "nsgpu_wifil_send: tx_cap SendPacket calls");
+  int64_t dur = 0;
+  int rc = nsgpu_wifi_tx_duration_ns(size, modclass, rate, bw, preamble, &dur);  // CalculateTxDuration
+  if (rc) return rc;
+  LTx t{now, dur, rate, phy, modclass, bw, preamble};
+  const uint32_t k = (uint32_t)h->n_tx++;
+  hipLaunchKernelGGL(k_wl_send, dim3((unsigned)((h->D.nphy + 255) / 256)), dim3(256), 0, h->s, h->D, k, t, dbm, uid_base);
+  NSGPU_HIP(hipGetLastError());
+  NSGPU_HIP(hipMemcpyAsync(h->h_cnt, h->D.cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  return wl_check(h, "nsgpu_wifil_send");
+}
+
+// Every device event with a key below (bound_ts, bound_uid) (~0: all of them): dispatched in (ts, uid) order
+// from rank *dispatched on; the syncs' EndReceives take the uids from *uid on.  The dispatches are added to
+// the caller's digest (nsgpu_dispatch_digest_term) and log (at their ranks, below log_cap).
+extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t bound_uid, uint32_t *uid,
+                                   uint64_t *dispatched, uint64_t *digest, uint64_t *log_ts, uint32_t *log_uid,
+                                   uint32_t *log_ctx, uint64_t log_cap) {
+  if (!h || !uid || !dispatched || !digest) return set_error(NSGPU_EINVAL, "nsgpu_wifil_advance: null");
+  WDev &D = h->D;
+  NSGPU_HIP(hipMemsetAsync(D.cnt, 0, 4 * sizeof(uint32_t), h->s));
+  hipLaunchKernelGGL(k_wl_step, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
+  hipLaunchKernelGGL(k_wl_rank, dim3(64), dim3(256), 0, h->s, D, *uid);
+  hipLaunchKernelGGL(k_wl_patch, dim3(256), dim3(256), 0, h->s, D);
+  NSGPU_HIP(hipGetLastError());
+  NSGPU_HIP(hipMemcpyAsync(h->h_cnt, D.cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  int rc = wl_check(h, "nsgpu_wifil_advance");
+  if (rc) return rc;
+  const uint32_t nev = h->h_cnt[0], nsync = h->h_cnt[1], nend = h->h_cnt[2];
+  h->ev.resize(nev);
+  h->ends_epoch.resize(nend);
+  if (nev) NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.ev, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
+  if (nend) NSGPU_HIP(hipMemcpyAsync(h->ends_epoch.data(), D.ends, nend * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  // the epoch's dispatch order: (ts, uid) over every phy's events (one lane per phy ran them in order)
+  std::sort(h->ev.begin(), h->ev.end(), [](const LEv &a, const LEv &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
+  for (const LEv &e : h->ev) {
+    const uint64_t rank = (*dispatched)++;
+    *digest += nsgpu_dispatch_digest_term(rank, e.ts, e.uid);
+    if (rank < log_cap && log_ts && log_uid && log_ctx) {
+      log_ts[rank] = e.ts;
+      log_uid[rank] = e.uid;
+      log_ctx[rank] = e.ctx;
+    }
+  }
+  std::sort(h->ends_epoch.begin(), h->ends_epoch.end(),
+            [](const nsgpu_wifil_end &a, const nsgpu_wifil_end &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
+  h->ends.insert(h->ends.end(), h->ends_epoch.begin(), h->ends_epoch.end());
+  *uid += nsync;
+  return NSGPU_OK;
+}
+
+// WifiPhyStateHelper::GetState / GetDelayUntilIdle of `phy` at `now` (wifi-phy-state-helper.cc:122-183).
+extern "C" int nsgpu_wifil_get_state(nsgpu_wifil *h, uint32_t phy, uint64_t now, nsgpu_wifil_phy_state *out) {
+  if (!h || !out || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_get_state: bad phy");
+  LPhy P;
+  NSGPU_HIP(hipMemcpyAsync(&P, h->D.ps + phy, sizeof(LPhy), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  const int64_t nw = (int64_t)now;
+  out->state = P.endTx > nw ? NSGPU_WIFIL_TX : P.rxing ? NSGPU_WIFIL_RX : P.endCca > nw ? NSGPU_WIFIL_CCA_BUSY : NSGPU_WIFIL_IDLE;
+  out->rxing = P.rxing;
+  out->end_tx = P.endTx;
+  out->end_rx = P.endRx;
+  out->end_cca_busy = P.endCca;
+  int64_t r = 0;
+  if (out->state == NSGPU_WIFIL_RX) r = P.endRx - nw;
+  else if (out->state == NSGPU_WIFIL_TX) r = P.endTx - nw;
+  else if (out->state == NSGPU_WIFIL_CCA_BUSY) r = P.endCca - nw;
+  out->delay_until_idle = r > 0 ? r : 0;
+  return NSGPU_OK;
+}
+
+// The EndReceive records dispatched since the last call, in dispatch order (cap 0: count only, kept).
+extern "C" int nsgpu_wifil_read_ends(nsgpu_wifil *h, nsgpu_wifil_end *out, uint64_t cap, uint64_t *n) {
+  if (!h || !n) return set_error(NSGPU_EINVAL, "nsgpu_wifil_read_ends: null");
+  *n = h->ends.size();
+  if (!out || cap == 0) return NSGPU_OK;
+  const uint64_t k = std::min<uint64_t>(cap, h->ends.size());
+  std::copy(h->ends.begin(), h->ends.begin() + (ptrdiff_t)k, out);
+  h->ends.erase(h->ends.begin(), h->ends.begin() + (ptrdiff_t)k);
+  *n = k;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifil_read_phys(nsgpu_wifil *h, nsgpu_wifi_phy_counters *out) {
+  if (!h || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifil_read_phys: null");
+  std::vector<LPhy> ps((size_t)h->D.nphy);
+  NSGPU_HIP(hipMemcpyAsync(ps.data(), h->D.ps, ps.size() * sizeof(LPhy), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  for (size_t j = 0; j < ps.size(); j++) {
+    nsgpu_wifi_phy_counters c = ps[j].c;
+    c.ni_len = ps[j].len;
+    c.ni_max = ps[j].ni_max;
+    c.end_tx = ps[j].endTx;
+    c.end_rx = ps[j].endRx;
+    c.end_cca_busy = ps[j].endCca;
+    c.first_power = ps[j].firstPower;
+    c.rxing = ps[j].rxing;
+    out[j] = c;
+  }
+  return NSGPU_OK;
+}
+
+// Pending Receive / EndReceive events and the smallest ts among them (~0: none).
+extern "C" int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_ts) {
+  if (!h || !n || !next_ts) return set_error(NSGPU_EINVAL, "nsgpu_wifil_pending: null");
+  const unsigned long long init[2] = {0ull, ~0ull};
+  NSGPU_HIP(hipMemcpyAsync(h->d_pend, init, sizeof(init), hipMemcpyHostToDevice, h->s));
+  hipLaunchKernelGGL(k_wl_pending, dim3((unsigned)((h->D.nphy + 255) / 256)), dim3(256), 0, h->s, h->D, h->d_pend);
+  NSGPU_HIP(hipGetLastError());
+  NSGPU_HIP(hipMemcpyAsync(h->h_pend, h->d_pend, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));
+  *n = h->h_pend[0];
+  *next_ts = h->h_pend[1];
+  return NSGPU_OK;
+}

@@ -117,6 +117,18 @@ SIGNATURES = {
     "nsgpu_sim_set_log": (C.c_int, [_vp, _vp, _vp, _vp, _u64]),
     "nsgpu_sim_attach_p2p": (C.c_int, [_vp, _vp]),
     "nsgpu_sim_p2p_send": (C.c_int, [_vp, _u32]),
+    "nsgpu_sim_attach_wifi": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_wifi_send": (C.c_int, [_vp, _u32, _u32, C.c_double, _u32, _u64, _u32, _u32]),
+    "nsgpu_sim_wifi_state": (C.c_int, [_vp, _u32, _vp]),
+    "nsgpu_wifil_create": (C.c_int, [_vp, _vp]),
+    "nsgpu_wifil_destroy": (C.c_int, [_vp]),
+    "nsgpu_wifil_receivers": (C.c_int, [_vp, _u32, _vp]),
+    "nsgpu_wifil_send": (C.c_int, [_vp, _u64, _u32, _u32, _u32, C.c_double, _u32, _u64, _u32, _u32]),
+    "nsgpu_wifil_advance": (C.c_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u64]),
+    "nsgpu_wifil_get_state": (C.c_int, [_vp, _u32, _u64, _vp]),
+    "nsgpu_wifil_read_ends": (C.c_int, [_vp, _vp, _u64, _vp]),
+    "nsgpu_wifil_read_phys": (C.c_int, [_vp, _vp]),
+    "nsgpu_wifil_pending": (C.c_int, [_vp, _vp, _vp]),
     "nsgpu_sim_is_finished": (C.c_int, [_vp, _vp]),
     "nsgpu_sim_run_one": (C.c_int, [_vp]),
     "nsgpu_sim_pop_one": (C.c_int, [_vp, _vp, _vp]),
@@ -685,6 +697,22 @@ class Sim:
 
     def p2p_send(self, app):
         check(lib().nsgpu_sim_p2p_send(self.h, app))
+
+    def attach_wifi(self, phy):
+        """Attach a closed-loop Wi-Fi PHY (wifi.LoopPhy)."""
+        check(lib().nsgpu_sim_attach_wifi(self.h, phy.h))
+        self._engine = phy
+
+    def wifi_send(self, phy, size, dbm, mode, preamble):
+        """YansWifiPhy::SendPacket of `phy` now (mode = (modclass, rate, bandwidth))."""
+        check(lib().nsgpu_sim_wifi_send(self.h, phy, size, dbm, mode[0], mode[1], mode[2], preamble))
+
+    def wifi_state(self, phy):
+        """WifiPhyStateHelper::GetState of `phy` now: (state, delay until idle ns)."""
+        import wifi
+        st = wifi.WifilPhyState()
+        check(lib().nsgpu_sim_wifi_state(self.h, phy, C.byref(st)))
+        return st.state, st.delay_until_idle
 
     def set_log(self, cap):
         self.log = (np.zeros(cap, np.uint64), np.zeros(cap, np.uint32), np.zeros(cap, np.uint32))

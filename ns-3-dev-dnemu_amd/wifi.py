@@ -233,3 +233,106 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+
+# ---- closed-loop PHY (nsgpu_wifil_*: SendPacket from host closures on nsgpu_sim) ----
+NIST, YANS = 0, 1  # nsgpu_wifil_error_model
+IDLE, RX, TX, CCA_BUSY = 0, 1, 2, 3  # nsgpu_wifil_state
+WIFIL_END_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("phy", "<u4"), ("snr", "<f8"), ("per", "<f8"),
+                            ("tx", "<u4"), ("flags", "<u4")])
+
+
+class WifilConfigStruct(C.Structure):
+    _fields_ = [
+        ("n_phy", C.c_int64), ("x", C.c_void_p), ("y", C.c_void_p), ("z", C.c_void_p),
+        ("channel", C.c_void_p), ("node", C.c_void_p), ("loss", nsgpu.LossChain), ("speed", C.c_double),
+        ("rx_gain_db", C.c_double), ("ed_threshold_dbm", C.c_double), ("cca_threshold_dbm", C.c_double),
+        ("rx_noise_figure_db", C.c_double), ("error_model", C.c_uint32), ("ni_cap", C.c_uint32),
+        ("rxq_cap", C.c_uint32), ("pad_", C.c_uint32), ("tx_cap", C.c_uint64),
+    ]
+
+
+class WifilPhyState(C.Structure):
+    _fields_ = [("state", C.c_uint32), ("rxing", C.c_uint32), ("end_tx", C.c_int64), ("end_rx", C.c_int64),
+                ("end_cca_busy", C.c_int64), ("delay_until_idle", C.c_int64)]
+
+
+class LoopPhys:
+    """The phys of a closed-loop run (nsgpu_wifil_config): positions, channels, nodes and the PHY /
+    channel attributes (defaults as Scenario above; RxNoiseFigure 7 dB, NistErrorRateModel as
+    YansWifiPhyHelper::Default sets, yans-wifi-helper.cc:187)."""
+
+    def __init__(self, x, y, z, channel=None, node=None, loss=((nsgpu.LOSS_LOG_DISTANCE, 3.0, 1.0, 46.6777),),
+                 speed=300000000.0, rx_gain_db=1.0, ed_threshold_dbm=-96.0, cca_threshold_dbm=-99.0,
+                 noise_figure_db=7.0, error_model=NIST, ni_cap=256, rxq_cap=256, tx_cap=1 << 16):
+        n = len(x)
+        self.x = np.ascontiguousarray(x, np.float64)
+        self.y = np.ascontiguousarray(y, np.float64)
+        self.z = np.ascontiguousarray(z, np.float64)
+        self.channel = np.ascontiguousarray(np.ones(n, np.uint32) if channel is None else channel, np.uint32)
+        self.node = np.ascontiguousarray(np.arange(n, dtype=np.uint32) if node is None else node, np.uint32)
+        self.loss = loss
+        self.speed, self.rx_gain_db, self.ed, self.cca = speed, rx_gain_db, ed_threshold_dbm, cca_threshold_dbm
+        self.noise_figure_db, self.error_model = noise_figure_db, error_model
+        self.ni_cap, self.rxq_cap, self.tx_cap = ni_cap, rxq_cap, tx_cap
+
+    @property
+    def n_phy(self):
+        return len(self.x)
+
+    def receivers(self, phy):
+        """Fan-out uids one SendPacket of `phy` takes: the other phys on its channel."""
+        return int(np.count_nonzero(self.channel == self.channel[phy])) - 1
+
+    def c_struct(self):
+        s = WifilConfigStruct()
+        s.n_phy = self.n_phy
+        s.x, s.y, s.z = self.x.ctypes.data, self.y.ctypes.data, self.z.ctypes.data
+        s.channel, s.node = self.channel.ctypes.data, self.node.ctypes.data
+        s.loss = nsgpu.loss_chain(*self.loss)
+        s.speed, s.rx_gain_db = self.speed, self.rx_gain_db
+        s.ed_threshold_dbm, s.cca_threshold_dbm = self.ed, self.cca
+        s.rx_noise_figure_db, s.error_model = self.noise_figure_db, self.error_model
+        s.ni_cap, s.rxq_cap, s.tx_cap = self.ni_cap, self.rxq_cap, self.tx_cap
+        return s
+
+
+class LoopPhy:
+    """The closed-loop PHY on the device (nsgpu_wifil): attach it to a nsgpu.Sim, whose closures call
+    Sim.wifi_send / Sim.wifi_state; EndReceive records (snr, per) come back through read_ends."""
+
+    def __init__(self, phys):
+        self.phys = phys
+        self._cfg = phys.c_struct()
+        h = C.c_void_p()
+        nsgpu.check(nsgpu.lib().nsgpu_wifil_create(C.byref(self._cfg), C.byref(h)))
+        self.h = h.value
+
+    def read_ends(self):
+        n = C.c_uint64()
+        nsgpu.check(nsgpu.lib().nsgpu_wifil_read_ends(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, WIFIL_END_DTYPE)
+        if n.value:
+            nsgpu.check(nsgpu.lib().nsgpu_wifil_read_ends(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return out
+
+    def read_phys(self):
+        out = np.zeros(self.phys.n_phy, PHY_COUNTERS_DTYPE)
+        nsgpu.check(nsgpu.lib().nsgpu_wifil_read_phys(self.h, out.ctypes.data))
+        return out
+
+    def pending(self):
+        n, ts = C.c_uint64(), C.c_uint64()
+        nsgpu.check(nsgpu.lib().nsgpu_wifil_pending(self.h, C.byref(n), C.byref(ts)))
+        return n.value, ts.value
+
+    def close(self):
+        if self.h:
+            nsgpu.lib().nsgpu_wifil_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

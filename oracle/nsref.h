@@ -168,6 +168,26 @@ int nsref_wifi_run(const nsgpu_wifi_scenario *sc, nsgpu_wifi_stats *stats, nsgpu
                    uint32_t *tx_base, nsgpu_wifi_end_record *ends, uint64_t ends_cap, uint64_t *n_ends,
                    nsgpu_wifi_rx_log *rx_log);
 
+/* Closed-loop Wi-Fi (the engine behind nsgpu_wifil_* / nsgpu_sim_attach_wifi): SendPacket from host
+ * closures.  The host side is the tests' MAC stand-in (restated by the GPU tests on nsgpu_sim): setup
+ * Schedule (first[i], attempt i) for every phy i in order, then Simulator::Stop (stop_ts); attempt i at
+ * Now: if phy i's WifiPhyStateHelper state is IDLE, SendPacket (the packet below) and Schedule (period,
+ * attempt i), else Schedule (backoff[i], attempt i).  EndReceive computes InterferenceHelper::
+ * CalculateSnrPer (interference-helper.cc:216-367) with the configured error-rate model; the m_random draw
+ * is the caller's (ends[], in dispatch order).  out[]: dispatched, digest (nsgpu_dispatch_digest_term),
+ * next uid, final ts, SendPacket calls, attempts that found the phy busy. */
+typedef struct nsref_wifil_mac {
+  const uint64_t *first, *backoff;
+  uint64_t period, stop_ts, rate;
+  uint32_t size, modclass, bw, preamble;
+  double dbm;
+} nsref_wifil_mac;
+int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, uint64_t *log_ts, uint32_t *log_uid,
+                    uint32_t *log_ctx, uint64_t log_cap, nsgpu_wifil_end *ends, uint64_t ends_cap, uint64_t *n_ends,
+                    nsgpu_wifi_phy_counters *phys, uint64_t out[6]);
+/* InterferenceHelper::CalculateChunkSuccessRate's error-rate model call for one chunk (tests). */
+double nsref_wifil_chunk_success(uint32_t model, uint32_t modclass, uint64_t rate, uint32_t bw, double snr, uint32_t nbits);
+
 /* ---------------- Global routing (nsref_route.cc) ----------------
  * GlobalRouteManager::PopulateRoutingTables + Ipv4GlobalRouting::RouteInput/LookupGlobal over a
  * point-to-point topology: route_out[node * n_dst + k] = the device the node's first matching route

@@ -463,6 +463,51 @@ def wifi_run(scenario_struct, stats_struct, phys, tx_base, end_dtype, rx_log=Non
     return secs, np.sort(ends, order="uid")
 
 
+class WifilMacStruct(C.Structure):  # nsref_wifil_mac (nsref.h)
+    _fields_ = [("first", C.c_void_p), ("backoff", C.c_void_p), ("period", C.c_uint64), ("stop_ts", C.c_uint64),
+                ("rate", C.c_uint64), ("size", C.c_uint32), ("modclass", C.c_uint32), ("bw", C.c_uint32),
+                ("preamble", C.c_uint32), ("dbm", C.c_double)]
+
+
+def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble, dbm, n_phy, end_dtype,
+              phys_dtype, log_cap=1 << 20):
+    """The closed-loop oracle run (nsref_wifil_run): the MAC stand-in of nsref.h over the PHY.  Returns
+    (pop log (ts, uid, ctx), EndReceive records in dispatch order, per-phy counters, dict of totals)."""
+    f = lib().nsref_wifil_run
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                  C.c_void_p, C.c_void_p, C.c_void_p]
+    first = np.ascontiguousarray(first, np.uint64)
+    backoff = np.ascontiguousarray(backoff, np.uint64)
+    m = WifilMacStruct(first.ctypes.data, backoff.ctypes.data, period, stop_ts, mode[1], size, mode[0], mode[2],
+                       preamble, dbm)
+    lts = np.zeros(log_cap, np.uint64)
+    luid = np.zeros(log_cap, np.uint32)
+    lctx = np.zeros(log_cap, np.uint32)
+    phys = np.zeros(n_phy, phys_dtype)
+    out = np.zeros(6, np.uint64)
+    n = C.c_uint64()
+    args = lambda ends, cap: (C.byref(cfg_struct), C.byref(m), lts.ctypes.data, luid.ctypes.data, lctx.ctypes.data,
+                              log_cap, ends, cap, C.byref(n), phys.ctypes.data, out.ctypes.data)
+    rc = f(*args(None, 0))
+    if rc != 0:
+        raise RuntimeError(f"nsref_wifil_run: {rc}")
+    ends = np.zeros(n.value, end_dtype)
+    rc = f(*args(ends.ctypes.data, n.value))
+    if rc != 0:
+        raise RuntimeError(f"nsref_wifil_run: {rc}")
+    tot = dict(zip(("dispatched", "digest", "next_uid", "final_ts", "sends", "busy"), (int(v) for v in out)))
+    k = min(tot["dispatched"], log_cap)
+    return (lts[:k], luid[:k], lctx[:k]), ends, phys, tot
+
+
+def wifil_chunk_success(model, mode, snr, nbits):
+    f = lib().nsref_wifil_chunk_success
+    f.restype = C.c_double
+    f.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_double, C.c_uint32]
+    return f(model, mode[0], mode[1], mode[2], snr, nbits)
+
+
 def global_routes(dev_node, dev_peer, dev_addr, dev_mask, dev_ifindex, n_nodes, dst_addr):
     """GlobalRouteManager::PopulateRoutingTables + LookupGlobal restated (nsref_route.cc): uint32
     [n_nodes, n_dst] of output devices (0xfffffffe local delivery, 0xffffffff no route)."""

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3, session d: wide windows with the ranking in k2_scan — divergence diagnostic
 # (scripts/wide_debug.py), the wide tests, the partitioned 65,536-node dumbbell (X1 header padding), the
-# 128 x 128 grid test, then config 4's bench line wide and narrow.
+# 128 x 128 grid test, config 4's bench line wide and narrow, then the closed-loop Wi-Fi tests.
 export TMPDIR=/tmp
 O=gpurun_out/r03d
 mkdir -p $O
@@ -21,4 +21,5 @@ step hubs 300 $PYT tests/test_gpu_hubs.py -k "65536_nodes_eight"
 step p2p 400 $PYT tests/test_gpu_p2p.py
 step bench_wide 300 python bench.py --no-secondary --steps 5
 step bench_narrow 300 env NSGPU_P2P_NARROW=1 python bench.py --no-secondary --steps 5 --no-cpu-baseline
+step wifi_loop 400 $PYT tests/test_gpu_wifi_loop.py
 exit 0

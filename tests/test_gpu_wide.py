@@ -1,6 +1,7 @@
 """Wide windows of the single p2p engine: windows bounded by the cross-node lookahead,
-a node's same-node TransmitCompletes running inside the window as local records, placed in the dispatch
-order and given their uids from their parents' child prefixes by k2_scan.
+a node's same-node TransmitCompletes running inside the window as local records, ranked after the handlers
+(k2_rank, by their chains up to a gen-0 ancestor) and given their uids from their parents' child prefixes
+(k2_scan).
 
 Every run is compared with the oracle's sequential DefaultSimulatorImpl restatement — full (ts, uid,
 context) pop log, counters and trace records — and with the same engine forced narrow
@@ -29,7 +30,8 @@ def narrow_engine(sc, log_cap=0):
 def check_wide_and_narrow(sc, log_cap, trace_cap, expect_wide=True):
     o = oracle_full(sc, log_cap)
     eng = p2p.Engine(sc)
-    assert eng.wide() == expect_wide
+    if expect_wide is not None:  # (wide needs Lx <= 8 tx_min: chains of local records stay short)
+        assert eng.wide() == expect_wide
     eng.close()
     g = gpu_full(sc, log_cap, trace_cap)
     assert_same_run(sc, o, g)
@@ -63,12 +65,12 @@ def test_congested_grid_transmit_complete_chains():
 @pytest.mark.parametrize("seed", range(5))
 def test_random_topologies(seed):
     sc = p2p.random_topology(30, 60, 12, seed)
-    check_wide_and_narrow(sc, 300_000, 2_000_000)
+    check_wide_and_narrow(sc, 300_000, 2_000_000, expect_wide=None)
 
 
 def test_icmp_ttl_expiry_grid():
     sc = p2p.grid(10, 10, ttl=5, icmp=True, stop_ns=300_000_000, sim_stop_ns=350_000_000)
-    check_wide_and_narrow(sc, 300_000, 2_000_000)
+    check_wide_and_narrow(sc, 300_000, 2_000_000, expect_wide=None)  # (58-B errors: Lx > 8 tx_min, narrow)
 
 
 def test_start_burst_larger_than_a_window_is_trimmed_narrow():

@@ -1,0 +1,62 @@
+"""Closed-loop Wi-Fi (config 3 with the MAC on the host): host closures send only when the
+device reports the phy IDLE, EndReceive's (snr, per) go back to the host for its draw.  GPU = oracle on the
+full (ts, uid, context) pop log, the digest, the per-phy counters and state; SNR / PER within 1e-9
+relative (device libm vs glibc; the state machine does not depend on them).  SNR / PER are parity
+unpinned: the reference holds no CalculateSnrPer fixture (wifi-interference-test-suite.cc only compares
+PERs of its own runs)."""
+import numpy as np
+import pytest
+
+import wifi
+from wifi_loop_harness import draws, run_gpu, run_oracle, scenario
+
+pytestmark = pytest.mark.gpu
+
+PHY_FIELDS = ("rx", "sync", "drop_rx", "drop_tx", "drop_ed", "cca_switches", "end", "end_cancelled", "ni_len",
+              "end_tx", "end_rx", "end_cca_busy", "rxing")
+
+
+def check(sc):
+    olog, oends, ophys, otot = run_oracle(sc)
+    glog, gends, gphys, gtot, _keep = run_gpu(sc)
+    for f in ("dispatched", "digest", "next_uid", "final_ts", "sends", "busy"):
+        assert gtot[f] == otot[f], (f, gtot[f], otot[f])
+    for a, b in zip(glog, olog):
+        assert np.array_equal(a, b)
+    for f in PHY_FIELDS:
+        assert np.array_equal(gphys[f], ophys[f]), f
+    # m_firstPower: sums of +P / -P (DbmToW through the device's pow: within an ulp of glibc's, as in
+    # test_gpu_wifi.py) — the residual of cancelled terms, compared absolutely
+    np.testing.assert_allclose(gphys["first_power"], ophys["first_power"], rtol=1e-9, atol=1e-24)
+    assert len(gends) == len(oends)
+    for f in ("ts", "uid", "phy", "tx", "flags"):
+        assert np.array_equal(gends[f], oends[f]), f
+    np.testing.assert_allclose(gends["snr"], oends["snr"], rtol=1e-9, atol=0)
+    np.testing.assert_allclose(gends["per"], oends["per"], rtol=1e-9, atol=1e-15)
+    n = sc["phys"].n_phy
+    assert np.array_equal(draws(gends, n), draws(oends, n))
+    return otot, oends
+
+
+def test_grid_4x4_dsss_nist():
+    tot, ends = check(scenario())
+    assert tot["sends"] > 50 and tot["busy"] > 10 and len(ends) > 100
+    assert (ends["per"] > 0).any() and (ends["per"] < 1).all()
+
+
+def test_grid_6x6_dense_collisions_cca_busy():
+    """60 m spacing, 1 Mb/s 600-B frames every 12 ms: receptions overlap, CCA-busy phys back off."""
+    tot, ends = check(scenario(n_side=6, spacing=60.0, seed=3, period=12_000_000, stop_ns=150_000_000, size=600))
+    assert tot["busy"] > tot["sends"] // 4
+
+
+@pytest.mark.parametrize("mode", [(wifi.OFDM, 6000000, 20000000), (wifi.OFDM, 54000000, 20000000),
+                                  (wifi.ERP_OFDM, 24000000, 20000000), (wifi.DSSS, 11000000, 22000000)])
+def test_modes_nist(mode):
+    check(scenario(seed=5, mode=mode, size=400, stop_ns=120_000_000))
+
+
+def test_yans_error_model_and_short_preamble():
+    check(scenario(seed=7, mode=(wifi.DSSS, 2000000, 22000000), preamble=wifi.PREAMBLE_SHORT,
+                   error_model=wifi.YANS, stop_ns=120_000_000))
+    check(scenario(seed=8, mode=(wifi.OFDM, 36000000, 20000000), error_model=wifi.YANS, stop_ns=120_000_000))

@@ -1,0 +1,79 @@
+"""The closed-loop Wi-Fi tests' MAC stand-in, run on the oracle (nsref_wifil_run, which restates it in
+C++) and on the device PHY attached to the host runtime (nsgpu.Sim + wifi.LoopPhy, the closures below).
+
+The stand-in (nsref.h: nsref_wifil_mac): at setup, Schedule (first[i], attempt i) for every phy in order,
+then Simulator::Stop (stop_ts).  attempt i: if phy i's WifiPhyStateHelper state is IDLE, SendPacket and
+Schedule (period, attempt i); otherwise Schedule (backoff[i], attempt i).  The m_random draw of every
+EndReceive (yans-wifi-phy.cc:783) is made here, on both runs' records, with one fixed sequence per phy."""
+import numpy as np
+
+import nsref
+import wifi
+
+
+def scenario(n_side=4, spacing=100.0, seed=1, period=20_000_000, stop_ns=200_000_000, size=200,
+             mode=wifi.DSSS_1M, preamble=wifi.PREAMBLE_LONG, dbm=16.0206 + 1.0, **phy_kw):
+    x, y, z = wifi.grid(n_side, spacing)
+    phys = wifi.LoopPhys(x, y, z, **phy_kw)
+    rng = np.random.default_rng(seed)
+    n = phys.n_phy
+    first = rng.integers(0, period // 2, n).astype(np.uint64)
+    backoff = (100_000 + 37_000 * np.arange(n)).astype(np.uint64)
+    return dict(phys=phys, first=first, backoff=backoff, period=period, stop_ns=stop_ns, size=size, mode=mode,
+                preamble=preamble, dbm=dbm)
+
+
+def run_oracle(sc, log_cap=1 << 20):
+    ph = sc["phys"]
+    cfg = ph.c_struct()
+    log, ends, phys, tot = nsref.wifil_run(cfg, sc["first"], sc["backoff"], sc["period"], sc["stop_ns"], sc["size"],
+                                           sc["mode"], sc["preamble"], sc["dbm"], ph.n_phy, wifi.WIFIL_END_DTYPE,
+                                           wifi.PHY_COUNTERS_DTYPE, log_cap)
+    return log, ends, phys, tot
+
+
+def run_gpu(sc, log_cap=1 << 20):
+    import nsgpu
+    ph = sc["phys"]
+    sim = nsgpu.Sim()
+    lp = wifi.LoopPhy(ph)
+    sim.attach_wifi(lp)
+    sim.set_log(log_cap)
+    cnt = {"sends": 0, "busy": 0}
+
+    def attempt(i):
+        st, _ = sim.wifi_state(i)
+        if st != wifi.IDLE:
+            cnt["busy"] += 1
+            sim.schedule(int(sc["backoff"][i]), lambda: attempt(i))
+            return
+        sim.wifi_send(i, sc["size"], sc["dbm"], sc["mode"], sc["preamble"])
+        cnt["sends"] += 1
+        sim.schedule(sc["period"], lambda: attempt(i))
+
+    for i in range(ph.n_phy):
+        sim.schedule(int(sc["first"][i]), (lambda i=i: lambda: attempt(i))())
+    sim.stop(sc["stop_ns"])
+    sim.run()
+    _n, _c, digest = sim.host_stats()
+    k = min(sim.dispatched(), log_cap)
+    log = (sim.log[0][:k].copy(), sim.log[1][:k].copy(), sim.log[2][:k].copy())
+    ends = lp.read_ends()
+    phys = lp.read_phys()
+    tot = dict(dispatched=sim.dispatched(), digest=digest, next_uid=sim.next_uid(), final_ts=sim.now(), **cnt)
+    lp_keep = (sim, lp)
+    return log, ends, phys, tot, lp_keep
+
+
+def draws(ends, n_phy):
+    """EndReceive outcomes: m_random.GetValue () > per, with phy j's k-th draw a fixed value."""
+    k = np.zeros(n_phy, np.int64)
+    ok = np.zeros(n_phy, np.int64)
+    for e in ends:
+        if e["flags"] & wifi.END_CANCELLED:
+            continue
+        j = int(e["phy"])
+        u = ((k[j] + 1) * 0.6180339887498949 + j * 0.1) % 1.0
+        k[j] += 1
+        ok[j] += u > e["per"]
+    return ok
