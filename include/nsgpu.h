@@ -381,7 +381,9 @@ int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset);
  * 1327-1490) + Ipv4GlobalRouting::LookupGlobal (ipv4-global-routing.cc:136-242, RandomEcmpRouting off)
  * for point-to-point topologies with unit metrics: route_out[node * n_dst + k] (host memory) = the device
  * through which `node` forwards a datagram to any address of node dst_node[k]; 0xffffffff for the
- * destination itself and for unreachable nodes.  dev_addr / dev_ifindex: each device's IPv4 address and
+ * destination itself and for unreachable nodes — except that a node with exactly one device always
+ * forwards through it, reachable or not (GlobalRouter's stub-node default route, CheckForStubNode,
+ * global-route-manager-impl.cc:1245-1290,1363-1366).  dev_addr / dev_ifindex: each device's IPv4 address and
  * interface index (both NULL: the lowest device wins ties).  One GPU BFS per destination. */
 int nsgpu_route_global(uint32_t n_nodes, uint32_t n_devices, const uint32_t *dev_node, const uint32_t *dev_peer,
                        const uint32_t *dev_addr, const uint32_t *dev_ifindex, uint32_t n_dst, const uint32_t *dst_node,

@@ -238,7 +238,11 @@ struct P2PDev {
   uint32_t *wpar;         // local record: parent record | child index << 24
   uint32_t *lcnt;         // local records per region this window (one region per holder / hub block)
   uint32_t *lrec;         // the last scanned window's local records (dense list, C.plt of them)
-  LKey *lkey;             // [LCAP] the local records' chains (k2_rank)
+  LKey *lkey;             // [LCAP] the local records' chains (k2_rank: the rare exact compare)
+  ulonglong2 *lkw;        // [LCAP] their chain order packed into two words (lk_word, lk_word2)
+  uint4 *ldat;            // [LMAX] the window's local records in dense order (k2_rank -> k2_scan): record,
+                          // child counts (n | inline << 16), rel ts, parent (wpar)
+  uint32_t *lrank;        // [LMAX] their rank accumulators (k2_rank; 0 between windows)
 };
 
 // ---------------- wave / block helpers ----------------
@@ -1884,6 +1888,9 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.lcnt, NLR));
   TRY(dalloc(h, &M.lrec, NMAX));  // (k2_pa loads lrec[k] speculatively: zeroed, every entry stays < WTOT)
   TRY(dalloc(h, &M.lkey, LCAP));
+  TRY(dalloc(h, &M.lkw, LCAP));
+  TRY(dalloc(h, &M.ldat, LMAX));
+  TRY(dalloc(h, &M.lrank, LMAX));
   if (hipMemset(M.lrec, 0, NMAX * sizeof(uint32_t)) != hipSuccess || hipMemset(M.lcnt, 0, NLR * sizeof(uint32_t)) != hipSuccess) {
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipMemset failed");
@@ -2038,6 +2045,7 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
   NSGPU_HIP(hipMemsetAsync(M.node_tab, 0, (size_t)M.n_nodes * NTAB * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.wrank, 0, WTOT * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(M.lrank, 0, LMAX * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.lcnt, 0, NLR * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
   if (M.dist) {

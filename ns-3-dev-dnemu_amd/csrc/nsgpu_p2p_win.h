@@ -41,6 +41,7 @@ constexpr uint32_t LBASE = WCAP;         // local records live at [LBASE, LBASE 
 constexpr int LCAP = NHB * LR + NHUB * LRH;
 constexpr int WTOT = WCAP + LCAP;        // record index space (gen-0 slots + local regions)
 constexpr int NMAX = 8192;               // records of one window, gen-0 + local (k2_scan's LDS capacity)
+constexpr int LMAX = NMAX - WCAP;        // local records of one window
 constexpr int SLOTG = WCAP + NMAX;       // k2_pa's slot-role threads (single engine): gen-0 slots, then local
 static_assert(LCAP < (1 << 24) && WTOT < (1 << 24), "wpar packs a record index in 24 bits");
 __device__ __forceinline__ uint32_t region_base(uint32_t r) {
@@ -577,6 +578,21 @@ struct SlotPre {
   uint64_t key;
 };
 
+// A local record's chain order packed into two words (lexicographic), the LKey compare only for a tie:
+// word 1 = rel ts, local, the parent's rel ts; word 2 = a gen-0 parent's uid and the child index (exact:
+// records tie only with themselves), or a local parent's: its parent's rel ts and class, and that one's
+// uid or parent rel ts (clamped: a tie falls back to the LKey compare).
+__device__ __forceinline__ uint64_t lk_word(const LKey &k) {
+  const uint32_t r1 = k.rel[1] < 0x7fffffffu ? k.rel[1] : 0x7fffffffu;
+  return ((uint64_t)k.rel[0] << 32) | 0x80000000u | r1;
+}
+__device__ __forceinline__ uint64_t lk_word2(const LKey &k) {
+  if (k.depth == 1) return ((uint64_t)k.uid << 8) | k.j[0];
+  const bool g2 = k.depth == 2;  // (the grandparent is the gen-0 ancestor)
+  const uint32_t r2 = k.rel[2] < 0x7fffffffu ? k.rel[2] : 0x7fffffffu;
+  const uint32_t nx = g2 ? k.uid : k.rel[3];
+  return (1ull << 63) | ((uint64_t)r2 << 31) | ((g2 ? 0ull : 1ull) << 30) | (nx < 0x3fffffffu ? nx : 0x3fffffffu);
+}
 // The local record of child E.lj of record `par` (a same-node TransmitComplete inside a wide window, marked
 // LOCALBIT by Emit::child): slot k of the caller's region (counter *cnt: LDS, shared by a holder block's
 // threads, or a hub block's lane 0), written like a window record; its key holds the rel ts (its uid is
@@ -617,6 +633,7 @@ __device__ __forceinline__ uint32_t local_record(const P2PDev &M, const Emit &E,
   x.j[0] = (uint8_t)E.lj;
   x.pad[0] = x.pad[1] = 0;
   M.lkey[rec - LBASE] = x;
+  M.lkw[rec - LBASE] = make_ulonglong2(lk_word(x), lk_word2(x));
   return rec;
 }
 // A node's pending local records, sorted by rel ts (ties: creation order = the parents' order); head qh.
@@ -1527,15 +1544,6 @@ __device__ __forceinline__ uint32_t dense_of(uint32_t rec, uint32_t W, const uin
 // ancestor are ordered by the child index just below the first level where they part.
 constexpr int RKT = 256;   // rows (threads) and columns per tile
 constexpr int RK_GRID = 1024;
-__device__ __forceinline__ LKey lkey_of(const P2PDev &M, uint32_t r) {
-  if (r >= LBASE) return M.lkey[r - LBASE];
-  const uint64_t k = M.wkey[r];
-  LKey x;
-  x.rel[0] = (uint32_t)(k >> 32);
-  x.uid = (uint32_t)k;
-  x.depth = 0;
-  return x;
-}
 // a before b (distinct records)
 __device__ __forceinline__ bool lk_before(const LKey &a, const LKey &b) {
 #pragma unroll
@@ -1552,97 +1560,125 @@ __device__ __forceinline__ bool lk_before(const LKey &a, const LKey &b) {
   }
   return false;  // (deeper chains are refused at create)
 }
-// A local record's chain order packed into two words (lexicographic), the LKey compare only for a tie:
-// word 1 = rel ts, local, the parent's rel ts; word 2 = a gen-0 parent's uid and the child index (exact:
-// records tie only with themselves), or a local parent's: its parent's rel ts and class, and that one's
-// uid or parent rel ts (clamped: a tie falls back to the LKey compare).
-__device__ __forceinline__ uint64_t lk_word(const LKey &k) {
-  const uint32_t r1 = k.rel[1] < 0x7fffffffu ? k.rel[1] : 0x7fffffffu;
-  return ((uint64_t)k.rel[0] << 32) | 0x80000000u | r1;
-}
-__device__ __forceinline__ uint64_t lk_word2(const LKey &k) {
-  if (k.depth == 1) return ((uint64_t)k.uid << 8) | k.j[0];
-  const bool g2 = k.depth == 2;  // (the grandparent is the gen-0 ancestor)
-  const uint32_t r2 = k.rel[2] < 0x7fffffffu ? k.rel[2] : 0x7fffffffu;
-  const uint32_t nx = g2 ? k.uid : k.rel[3];
-  return (1ull << 63) | ((uint64_t)r2 << 31) | ((g2 ? 0ull : 1ull) << 30) | (nx < 0x3fffffffu ? nx : 0x3fffffffu);
-}
 // The gen-0 records' ranks among themselves come from k2_handle's rank tiles (keys known before the
 // handlers run); here, tiles of (all records x local records) add the local records before each record,
 // and tiles of (local records x gen-0 records) the gen-0 records before each local one (rel ts only: at
-// equal ts a gen-0 record comes first).
+// equal ts a gen-0 record comes first).  Each record's two order words are made once (local_record: lkw;
+// a gen-0 row: its rel ts, with a zero low word, sorts before every local record of its ts), so a column
+// costs one 16-B LDS load and two compares (64 columns a tile, unrolled: the loads pipeline); the exact
+// chain compare runs after the tile, only for rows whose words tie with a distinct record's (chains of 3+
+// levels with equal ts pairs).
+constexpr int RKC = 64;  // columns per tile
 __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
   Ctl &C = *M.C;
+  BLK_T0();
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t c_win = C.windows;
+  uint32_t n_tie = 0;
+#endif
   const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run;
   const uint64_t lim = C.lim_rel;
+  const uint32_t lc = threadIdx.x < (uint32_t)NLR ? M.lcnt[threadIdx.x] : 0u;  // (its trip overlaps the control's)
   if (c_done || c_mode >= MODE_SORT || c_mode == MODE_RUN || W > (uint32_t)WCAP || c_fr || lim == 0) return;
   __shared__ uint32_t pre[NLR + 1];
-  __shared__ uint64_t cw[RKT], cw2[RKT];
-  __shared__ LKey ck[RKT];
-  local_prefix<RKT>(threadIdx.x < (uint32_t)NLR ? M.lcnt[threadIdx.x] : 0u, pre);
+  __shared__ ulonglong2 cw[RKC];
+  local_prefix<RKT>(lc, pre);
   const uint32_t Lt = pre[NLR], N = W + Lt;
-  if (Lt == 0 || N > (uint32_t)NMAX) return;  // (N > NMAX: k2_scan fails the run, error 64)
-
-  const uint32_t nr = (N + RKT - 1) / RKT, nl = (Lt + RKT - 1) / RKT, ng = (W + RKT - 1) / RKT;
-  const uint32_t na = nr * nl;  // phase A tiles, then phase B (nl x ng)
-  for (uint32_t t = blockIdx.x; t < na + nl * ng; t += gridDim.x) {  // (uniform over the block)
-    uint32_t c = 0, rx = 0;
+  if (Lt == 0 || N > (uint32_t)NMAX || Lt > (uint32_t)LMAX) return;  // (too many: k2_scan fails the run, error 64)
+#ifdef NSGPU_PHASE_PROF
+  if (c_win == g_blk_win && blockIdx.x == 0 && threadIdx.x == 0) {
+    g_phase[57] = N;
+    g_phase[58] = Lt;
+  }
+#endif
+  BLK_MARK(48, c_win);
+  const uint32_t nr = (N + RKT - 1) / RKT, ncl = (Lt + RKC - 1) / RKC;  // phase A: rows x local columns
+  const uint32_t nl = (Lt + RKT - 1) / RKT, ncg = (W + RKC - 1) / RKC;  // phase B: local rows x gen-0 columns
+  const uint32_t na = nr * ncl;
+  for (uint32_t t = blockIdx.x; t < na + nl * ncg; t += gridDim.x) {  // (uniform over the block)
+    uint32_t c = 0, slot = 0;  // slot: the row's accumulator (wrank[dense] for gen-0, LBASE + k for local k)
     if (t < na) {  // rows: every record; columns: local records
-      const uint32_t ti = t / nl, tj = t % nl;
-      const uint32_t cy = tj * RKT + threadIdx.x, ix = ti * RKT + threadIdx.x;
-      if (cy < Lt) {
-        const LKey k = M.lkey[dense_rec(W + cy, W, pre) - LBASE];
-        ck[threadIdx.x] = k;
-        cw[threadIdx.x] = lk_word(k);
-        cw2[threadIdx.x] = lk_word2(k);
+      const uint32_t ti = t / ncl, tj = t % ncl;
+      const uint32_t ix = ti * RKT + threadIdx.x;
+      if (threadIdx.x < (uint32_t)RKC) {
+        const uint32_t cy = tj * RKC + threadIdx.x;
+        ulonglong2 w = make_ulonglong2(~0ull, ~0ull);  // (a padding column: after every row)
+        if (cy < Lt) {
+          const uint32_t r = dense_rec(W + cy, W, pre);
+          w = M.lkw[r - LBASE];
+          if (ti == 0) {  // the dense list k2_scan (ldat) and the next k2_pa (lrec) read; the local's context
+            M.ldat[cy] = make_uint4(r, M.nchild[r] | (M.ninl[r] << 16), (uint32_t)(w.x >> 32), M.wpar[r]);
+            M.lrec[cy] = r;
+            M.pwctx[r] = M.wctx[r];
+          }
+        }
+        cw[threadIdx.x] = w;
       }
-      LKey kx;
-      uint64_t wx = 0, wx2 = 0;
-      const bool lx = ix >= W;
+      uint64_t wx = ~0ull, wx2 = ~0ull;
+      uint32_t rx = 0;
       if (ix < N) {
         rx = dense_rec(ix, W, pre);
-        if (lx) {
-          kx = M.lkey[rx - LBASE];
-          wx = lk_word(kx);
-          wx2 = lk_word2(kx);
+        if (ix >= W) {
+          const ulonglong2 w = M.lkw[rx - LBASE];
+          wx = w.x;
+          wx2 = w.y;
         } else {
           wx = (M.wkey[rx] >> 32) << 32;  // (a local record of smaller rel ts comes first)
+          wx2 = 0;
         }
       }
       __syncthreads();
-      const uint32_t jn = Lt - tj * RKT < (uint32_t)RKT ? Lt - tj * RKT : (uint32_t)RKT;
-      if (ix < N) {
-        if (lx) {
-          for (uint32_t y = 0; y < jn; y++) {
-            const uint64_t wy = cw[y];
-            if (wy != wx) {
-              c += wy < wx;
-            } else {
-              const uint64_t wy2 = cw2[y];
-              c += wy2 < wx2 || (wy2 == wx2 && W + tj * RKT + y != ix && lk_before(ck[y], kx));
-            }
+      BLK_MARK(50, c_win);
+      bool tie = false;
+      const uint32_t self = ix - W - tj * RKC;  // (the row's own column, if it is one of this tile's)
+#pragma unroll 16
+      for (uint32_t y = 0; y < (uint32_t)RKC; y++) {
+        const ulonglong2 w = cw[y];
+        const bool eq = w.x == wx;
+        c += (w.x < wx) | (eq & (w.y < wx2));
+        tie |= eq & (w.y == wx2) & (y != self);
+      }
+      if (tie && ix < N) {  // (rare: deep chains)
+        const LKey kx = M.lkey[rx - LBASE];
+        for (uint32_t y = 0; y < (uint32_t)RKC; y++) {
+          const ulonglong2 w = cw[y];
+          const uint32_t cy = tj * RKC + y;
+          if (w.x == wx && w.y == wx2 && y != self && cy < Lt) {
+#ifdef NSGPU_PHASE_PROF
+            n_tie++;
+#endif
+            c += lk_before(M.lkey[dense_rec(W + cy, W, pre) - LBASE], kx);
           }
-        } else {
-          for (uint32_t y = 0; y < jn; y++) c += cw[y] < wx;
         }
       }
+      if (ix >= N) c = 0;
+      slot = ix >= W ? ix - W + LBASE : rx;
     } else {  // rows: local records; columns: gen-0 records (rel ts <= the row's)
-      const uint32_t u = t - na, ti = u / ng, tj = u % ng;
-      const uint32_t cy = tj * RKT + threadIdx.x, ix = ti * RKT + threadIdx.x;
-      if (cy < W) cw[threadIdx.x] = M.wkey[cy] >> 32;
-      uint64_t relx = 0;
-      if (ix < Lt) {
-        rx = dense_rec(W + ix, W, pre);
-        relx = M.wkey[rx] >> 32;
+      const uint32_t u = t - na, ti = u / ncg, tj = u % ncg;
+      const uint32_t ix = ti * RKT + threadIdx.x;
+      if (threadIdx.x < (uint32_t)RKC) {
+        const uint32_t cy = tj * RKC + threadIdx.x;
+        cw[threadIdx.x].x = cy < W ? M.wkey[cy] >> 32 : ~0ull;
       }
+      uint64_t relx = 0;
+      if (ix < Lt) relx = M.wkey[dense_rec(W + ix, W, pre)] >> 32;
       __syncthreads();
-      const uint32_t jn = W - tj * RKT < (uint32_t)RKT ? W - tj * RKT : (uint32_t)RKT;
-      if (ix < Lt)
-        for (uint32_t y = 0; y < jn; y++) c += cw[y] <= relx;
+#pragma unroll 16
+      for (uint32_t y = 0; y < (uint32_t)RKC; y++) c += cw[y].x <= relx;
+      if (ix >= Lt) c = 0;
+      slot = ix + LBASE;
     }
-    if (c) atomicAdd(&M.wrank[rx], c);
+    BLK_MARK(52, c_win);
+    if (c) atomicAdd(slot >= LBASE ? &M.lrank[slot - LBASE] : &M.wrank[slot], c);
     __syncthreads();
+    BLK_MARK(54, c_win);
   }
+#ifdef NSGPU_PHASE_PROF
+  if (c_win == g_blk_win) {
+    if (n_tie) atomicAdd((unsigned long long *)&g_phase[56], (unsigned long long)n_tie);
+    if (threadIdx.x == 0) atomicAdd((unsigned long long *)&g_phase[59], 1ull);
+  }
+#endif
 }
 
 // ---- k2_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
@@ -1685,6 +1721,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
               C.span_t, C.uid, C.rt, C.stop_seen, C.hcap};
   // per record: rank, child counts, record index, rel ts; a local record's parent (wpar), later the
   // parent's rank | child index << 16
+  // Slot q of a thread: q < RPT0 the gen-0 slot i = tid + q * SCAN_THREADS (dense index i), q >= RPT0 (wide)
+  // the local record k = i - WCAP of k2_rank's dense list (dense index W + k); both loaded speculatively.
   uint32_t pr[RPT], pc[RPT], prec[RPT], prel[RPT], ppx[RPT];
   uint64_t gk[RPT0];
   uint32_t gctx[RPT0];
@@ -1698,6 +1736,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       pc[q] = M.nchild[i] | (M.ninl[i] << 16);
       gk[q] = M.wkey[i];
       gctx[q] = M.wctx[i];
+    } else {
+      const uint4 d = M.ldat[i - WCAP];
+      prec[q] = d.x;
+      pc[q] = d.y;
+      prel[q] = d.z;
+      ppx[q] = d.w;
+      pr[q] = M.lrank[i - WCAP];
     }
   }
   if (c_done || c_mode >= MODE_SORT) return;
@@ -1740,7 +1785,16 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   if constexpr (WIDE) local_prefix<SCAN_THREADS>(c_lim != 0 && !run ? c_lcnt : 0u, pre);
   const uint32_t Lt = (WIDE && !run) ? pre[NLR] : 0u;
   const uint32_t N = W + Lt;
-  if (N > (uint32_t)NREC) {  // (the adaptive span keeps windows well inside; a run that got here fails loudly)
+  // dense index of slot q, and whether it holds a record of this window
+  auto dense_q = [&](int q) -> uint32_t {
+    const uint32_t i = tid + q * SCAN_THREADS;
+    return q < RPT0 ? i : W + (i - (uint32_t)WCAP);
+  };
+  auto valid_q = [&](int q) -> bool {
+    const uint32_t i = tid + q * SCAN_THREADS;
+    return q < RPT0 ? i < W : i - (uint32_t)WCAP < Lt;
+  };
+  if (N > (uint32_t)NREC || Lt > (uint32_t)LMAX) {  // (the adaptive span keeps windows well inside; a run that got here fails loudly)
     if (tid == 0) {
       atomicOr(M.error, 64u);
       C.done = 1;
@@ -1763,40 +1817,22 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     }
   }
   if constexpr (WIDE) {
-#pragma unroll
-    for (int q = 0; q < RPT; q++) {
-      const uint32_t i = tid + q * SCAN_THREADS;
-      if (i >= W && i < N) {  // a local record
-        const uint32_t r = dense_rec(i, W, pre);
-        prec[q] = r;
-        pr[q] = M.wrank[r];
-        pc[q] = M.nchild[r] | (M.ninl[r] << 16);
-        prel[q] = (uint32_t)(M.wkey[r] >> 32);
-        M.pwctx[r] = M.wctx[r];
-        ppx[q] = M.wpar[r];
-      }
-    }
     if (Lt) {  // a local record's parent's rank (its uid below is the parent's child prefix + j)
       uint32_t *Fd = sbuf;  // [N] rank by dense index
 #pragma unroll
-      for (int q = 0; q < RPT; q++) {
-        const uint32_t i = tid + q * SCAN_THREADS;
-        if (i < N) Fd[i] = pr[q];
-      }
+      for (int q = 0; q < RPT; q++)
+        if (valid_q(q)) Fd[dense_q(q)] = pr[q];
       __syncthreads();
 #pragma unroll
-      for (int q = 0; q < RPT; q++) {
-        const uint32_t i = tid + q * SCAN_THREADS;
-        if (i >= W && i < N) ppx[q] = Fd[dense_of(ppx[q] & 0xffffffu, W, pre)] | ((ppx[q] >> 24) << 16);
-      }
+      for (int q = RPT0; q < RPT; q++)
+        if (valid_q(q)) ppx[q] = Fd[dense_of(ppx[q] & 0xffffffu, W, pre)] | ((ppx[q] >> 24) << 16);
       __syncthreads();  // (the buffer holds the rank-ordered arrays next)
     }
   }
   PH_MARK(16);
 #pragma unroll
   for (int q = 0; q < RPT; q++) {  // record order -> rank order
-    const uint32_t i = tid + q * SCAN_THREADS;
-    if (i < N) {
+    if (valid_q(q)) {
       const uint32_t r = pr[q];
       l_slot[r] = prec[q];
       l_cnt[r] = pc[q];
@@ -1890,14 +1926,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   // its child index (DefaultSimulatorImpl::Schedule order); the local records' list; ranks cleared
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
-    const uint32_t i = tid + q * SCAN_THREADS;
-    if (i < N) {
+    if (valid_q(q)) {
       const uint32_t r = prec[q];
-      if (WIDE && i >= W) {
+      if (WIDE && q >= RPT0) {  // (k2_rank wrote the dense list lrec)
         M.pwkey[r] = ((uint64_t)prel[q] << 32) | (uint32_t)(uid0 + gstart[ppx[q] & 0xffffu] + (ppx[q] >> 16));
-        M.lrec[i - W] = r;
+        M.lrank[tid + q * SCAN_THREADS - WCAP] = 0;
+      } else if (!run) {
+        M.wrank[r] = 0;
       }
-      if (!run) M.wrank[r] = 0;
     }
   }
   if (WIDE && Lt && tid < NLR) M.lcnt[tid] = 0;
