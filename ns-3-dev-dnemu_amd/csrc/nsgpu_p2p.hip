@@ -51,6 +51,9 @@ constexpr int RTR = 1;           // window keys (rows) per thread of a rank tile
 constexpr int NRT = WCAP / (HB * RTR);  // rank tile rows
 constexpr int NRB = NRT * NJT;   // rank tile blocks (k2_handle)
 constexpr int GRID_POOL = 256;   // blocks of the pool sweep (grid-stride)
+#ifndef PA_SLOT_LANES
+#define PA_SLOT_LANES 256        // k2_pa (single engine): last-window records per slot block (diagnostic override)
+#endif
 constexpr int SCAN_THREADS = 1024;
 constexpr int CH = 16;           // events of one node a handler thread sorts in LDS
 constexpr int NSLOT = 7;         // per-node slot table entries
@@ -2082,8 +2085,8 @@ bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr,
   const bool wide = h->M.wide != 0;
   switch (k) {
     case 0:
-      if (wide) hipExtLaunchKernelGGL((k2_pa<false, true>), dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M);
-      else hipExtLaunchKernelGGL((k2_pa<false, false>), dim3(GRID_POOL), dim3(TB), 0, s, ev0, ev1, 0, h->M);
+      if (wide) hipExtLaunchKernelGGL((k2_pa<false, true>), dim3(pa_grid<true>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
+      else hipExtLaunchKernelGGL((k2_pa<false, false>), dim3(pa_grid<false>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
       return true;
     case 1:
       if (wide) hipExtLaunchKernelGGL(k2_handle<true>, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M);

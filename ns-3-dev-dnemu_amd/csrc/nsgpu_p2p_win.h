@@ -42,7 +42,7 @@ constexpr int LCAP = NHB * LR + NHUB * LRH;
 constexpr int WTOT = WCAP + LCAP;        // record index space (gen-0 slots + local regions)
 constexpr int NMAX = 8192;               // records of one window, gen-0 + local (k2_scan's LDS capacity)
 constexpr int LMAX = NMAX - WCAP;        // local records of one window
-constexpr int SLOTG = WCAP + NMAX;       // k2_pa's slot-role threads (single engine): gen-0 slots, then local
+constexpr int SLOTG = WCAP + LMAX;       // k2_pa's slot-role threads (single engine): gen-0 slots, then local
 static_assert(LCAP < (1 << 24) && WTOT < (1 << 24), "wpar packs a record index in 24 bits");
 __device__ __forceinline__ uint32_t region_base(uint32_t r) {
   return LBASE + (r < (uint32_t)NHB ? r * LR : NHB * LR + (r - NHB) * LRH);
@@ -309,6 +309,12 @@ __device__ void run_chunk_end(const P2PDev &M, uint64_t r0, uint64_t rW, uint64_
 // after the slot blocks), the rank's reduction goes to its X1 summary, and a window the host cut
 // (k_cut2: C.prep) is already formed.
 // WIDE: the single engine's wide windows (the last window's local records are appended too).
+// k2_pa's grid (single engine): the slot blocks, then as many blocks of the pool sweep as GRID_POOL leaves
+template <bool WIDE>
+constexpr int pa_grid() {
+  constexpr int nsg = WIDE ? SLOTG : WCAP;
+  return nsg / PA_SLOT_LANES + GRID_POOL - nsg / TB;
+}
 template <bool DIST, bool WIDE>
 __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   static_assert(!(DIST && WIDE), "wide windows are the single engine's");
@@ -318,13 +324,17 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 #ifdef NSGPU_PHASE_PROF
   const uint64_t c_win = C.windows;
 #endif
-  const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
   // slot role: one thread per record of the last window — its gen-0 slots, then (single engine) its local
-  // records (the dense list lrec); (roles are block-uniform)
+  // records (the dense list lrec), SL of them in each of the first NSGB blocks (roles are block-uniform:
+  // a slot block's lanes past SL take part in its barriers only)
   constexpr uint32_t NSG = WIDE ? (uint32_t)SLOTG : (uint32_t)WCAP;
-  const bool slot_role = g < (uint64_t)NSG;
+  constexpr uint32_t SL = DIST ? (uint32_t)TB : (uint32_t)PA_SLOT_LANES, NSGB = NSG / SL;
+  const bool slot_block = blockIdx.x < NSGB;
+  const bool slot_role = slot_block && threadIdx.x < SL;
+  const uint64_t g = slot_block ? (uint64_t)blockIdx.x * SL + threadIdx.x
+                                : NSG + (uint64_t)(blockIdx.x - NSGB) * TB + threadIdx.x;
   const uint32_t rrb = DIST ? (M.nranks * M.capx + TB - 1) / TB : 0u;  // remote-event blocks
-  const bool remote_role = DIST && !slot_role && blockIdx.x < NSG / TB + rrb;
+  const bool remote_role = DIST && !slot_block && blockIdx.x < NSGB + rrb;
   // Everything this kernel reads of the run control and of the last window's slot, loaded at once:
   // these lines were written by k2_scan on another XCD, so every dependent level is a trip to memory.
   // (The slot arrays are WCAP long: a slot past the last window's size is loaded and ignored.)
@@ -357,7 +367,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     if (C.prep) return;
   }
   if (c_done >= 2 || c_mode >= MODE_SORT) return;
-  if (slot_role) BLK_MARK(32, c_win);  // snapshot + slot loads issued (waits at first use)
+  if (slot_block) BLK_MARK(32, c_win);  // snapshot + slot loads issued (waits at first use)
   const bool run = c_mode == MODE_RUN;
   const bool partition = c_done == 0;
   Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[rt];
@@ -398,9 +408,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const uint32_t pW = c_pvalid ? c_pW : 0;
   PH_MARK(0);
   uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull, digest = 0;
-  if (slot_role) {
+  if (slot_block) {
     // ---- record `rec` of the last window: dispatch rank (log, digest), inline children, children -> pending
-    const bool vs = g < (uint64_t)WCAP ? g < pW : (c_pvalid && g - WCAP < c_plt);
+    const bool vs = slot_role && (g < (uint64_t)WCAP ? g < pW : (c_pvalid && g - WCAP < c_plt));
     const uint32_t s = rec;
     const uint64_t rel = spk >> 32;
     const uint64_t t = c_ptmin + rel;
@@ -489,7 +499,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     // blocks past the pool's end do nothing (no atomics).
     constexpr int PPT = 4;
     const uint64_t P = c_P;
-    const uint64_t pb = blockIdx.x - (uint64_t)(NSG / TB + rrb), npb = gridDim.x - (uint64_t)(NSG / TB + rrb);
+    const uint64_t pb = blockIdx.x - (uint64_t)(NSGB + rrb), npb = gridDim.x - (uint64_t)(NSGB + rrb);
     for (uint64_t c0 = pb * TB * PPT; c0 < P; c0 += npb * TB * PPT) {  // block-uniform trip count
       Ev ge[PPT];
       bool gin[PPT], gpk[PPT];
@@ -543,7 +553,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     }
   }
   PH_MARK(1);
-  if (slot_role) BLK_MARK(42, c_win);
+  if (slot_block) BLK_MARK(42, c_win);
   publish_min<TB, WIDE>(R, tmn, wnd, wndw);
   digest = wave_sum64(digest);
   {  // one digest atomic per block
@@ -557,7 +567,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     }
   }
   PH_MARK(2);
-  if (slot_role) BLK_MARK(44, c_win);  // publish_min, digest
+  if (slot_block) BLK_MARK(44, c_win);  // publish_min, digest
   BLK_REC(0, c_win);
 }
 
@@ -565,7 +575,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 // The roles of k2_handle's blocks share one LDS buffer (holders: per-thread sort lists; hub blocks:
 // the hub's list), so that every block of the launch is resident at once.
 constexpr int K2_LDS_WORDS = HB * CH * 3;                // holders: sort lists (12 KB; >= HUBL * 3)
-constexpr int K2_LDS_WORDS_W = K2_LDS_WORDS + HB * LQ * 2;  // wide engines: + local queues (20 KB)
+constexpr int K2_LDS_WORDS_W = K2_LDS_WORDS + HB * LQ * 4;  // wide engines: + local queues (28 KB)
 static_assert(HUBL * 3 <= K2_LDS_WORDS, "hub list does not fit the shared buffer");
 // Run control a window kernel reads, loaded once at its entry (all fields at once: one memory trip).
 struct HCtl {
@@ -637,13 +647,21 @@ __device__ __forceinline__ uint32_t local_record(const P2PDev &M, const Emit &E,
   return rec;
 }
 // A node's pending local records, sorted by rel ts (ties: creation order = the parents' order); head qh.
-__device__ __forceinline__ void lq_push(const P2PDev &M, uint32_t *qrel, uint32_t *qrec, uint32_t stride, uint32_t &qh,
-                                        uint32_t &nq, uint32_t rel, uint32_t rec) {
+// Each entry: rel ts, record, and the record's context and device (so running it reads no record field).
+struct LQ4 {
+  uint32_t *rel, *rec, *ctx, *dev;
+  uint32_t stride;
+  __device__ __forceinline__ void move(uint32_t to, uint32_t from) const {
+    rel[to * stride] = rel[from * stride];
+    rec[to * stride] = rec[from * stride];
+    ctx[to * stride] = ctx[from * stride];
+    dev[to * stride] = dev[from * stride];
+  }
+};
+__device__ __forceinline__ void lq_push(const P2PDev &M, const LQ4 &q, uint32_t &qh, uint32_t &nq, uint32_t rel,
+                                        uint32_t rec, uint32_t ctx, uint32_t dev) {
   if (nq == (uint32_t)LQ && qh > 0) {  // compact the consumed head away
-    for (uint32_t i = qh; i < nq; i++) {
-      qrel[(i - qh) * stride] = qrel[i * stride];
-      qrec[(i - qh) * stride] = qrec[i * stride];
-    }
+    for (uint32_t i = qh; i < nq; i++) q.move(i - qh, i);
     nq -= qh;
     qh = 0;
   }
@@ -652,174 +670,18 @@ __device__ __forceinline__ void lq_push(const P2PDev &M, uint32_t *qrel, uint32_
     return;
   }
   uint32_t p = nq;
-  while (p > qh && qrel[(p - 1) * stride] > rel) {
-    qrel[p * stride] = qrel[(p - 1) * stride];
-    qrec[p * stride] = qrec[(p - 1) * stride];
+  while (p > qh && q.rel[(p - 1) * q.stride] > rel) {
+    q.move(p, p - 1);
     p--;
   }
-  qrel[p * stride] = rel;
-  qrec[p * stride] = rec;
+  q.rel[p * q.stride] = rel;
+  q.rec[p * q.stride] = rec;
+  q.ctx[p * q.stride] = ctx;
+  q.dev[p * q.stride] = dev;
   nq++;
 }
 
-template <bool WIDE>
-__device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i0, uint32_t W, uint32_t base, Red &R,
-                                             uint32_t *lds, const HCtl &hc, SlotPre sp, uint32_t *lcnt_sh) {
-  uint32_t *chs = lds;
-  uint64_t *chk = reinterpret_cast<uint64_t *>(lds + HB * CH);
-  uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull;
-  HStat hs{0, 0, 0, 0, false};
-  if (base != 0 && i0 < W) {
-    sp.ctx = M.wctx[base + i0];
-    sp.kind = M.wkind[base + i0];
-    sp.a = M.wa[base + i0];
-    sp.key = M.wkey[base + i0];
-  }
-  X1Acc xa{0, 0, 0};
-  const uint32_t wi = i0 < W ? sp.widx : 1u;
-  if (wi == NOHOLD) slot_done(M, i0, sp.key, 0, 0, xa);  // NetDevice::Start: dispatched, no children
-  if (wi == 0) {  // the holder
-    const uint32_t c = lp_of(M, sp.ctx, sp.kind, sp.a);
-    uint32_t n = 1;
-    int32_t sink = -1;
-    if (c < M.n_nodes) {
-      n = M.node_tab[(uint64_t)c * NTAB];
-      sink = M.sink_of_node[c];
-    }
-    if (n <= (uint32_t)CH) {  // (a hub's events are its hub block's)
-      if (c < M.n_nodes) M.node_tab[(uint64_t)c * NTAB] = 0;
-      const uint64_t key0 = sp.key;
-      uint32_t *my = &chs[threadIdx.x * CH];
-      uint64_t *mk = &chk[threadIdx.x * CH];
-      my[0] = i0;
-      mk[0] = key0;
-      if (n > 1) {
-        const uint32_t ns = n < (uint32_t)NSLOT ? n : (uint32_t)NSLOT;
-        for (uint32_t j = 0; j < ns; j++) my[j] = M.node_tab[(uint64_t)c * NTAB + 1 + j];
-        if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
-          uint32_t m = NSLOT;
-          for (uint32_t x = 0; x < W && m < n; x++)
-            if (M.widx[x] >= (uint32_t)NSLOT && M.widx[x] != NOHOLD &&
-                lp_of(M, M.wctx[base + x], M.wkind[base + x], M.wa[base + x]) == c)
-              my[m++] = x;
-        }
-        for (uint32_t j = 0; j < n; j++) mk[j] = M.wkey[base + my[j]];
-        for (uint32_t a = 1; a < n; a++) {  // insertion sort by key
-          const uint32_t v = my[a];
-          const uint64_t kv = mk[a];
-          uint32_t bb = a;
-          while (bb > 0 && mk[bb - 1] > kv) {
-            my[bb] = my[bb - 1];
-            mk[bb] = mk[bb - 1];
-            bb--;
-          }
-          my[bb] = v;
-          mk[bb] = kv;
-        }
-      }
-      const uint64_t tmin = hc.tmin, inline_lim = hc.inline_lim, slo = hc.slo, shi = hc.shi;
-      Emit E;
-      E.ctx = c;
-      E.ch_ts = M.ch_ts;
-      E.ch_ctx = M.ch_ctx;
-      E.ch_kind = M.ch_kind;
-      E.ch_a = M.ch_a;
-      E.ch_pkt = M.ch_pkt;
-      E.lookahead = M.lookahead;
-      E.lookw = WIDE ? M.lookw : nullptr;
-      E.tmn = ~0ull;
-      E.wnd = ~0ull;
-      E.wndw = ~0ull;
-      E.lim_abs = WIDE && hc.lim ? tmin + hc.lim : 0;
-      // the node's events in key order: its gen-0 window events (sorted above) merged with the local records
-      // its own TransmitStarts make (a gen-0 event first at equal ts: its uid is older)
-      uint32_t *qrel = lds + HB * CH * 3 + threadIdx.x, *qrec = qrel + HB * LQ;
-      uint32_t qh = 0, nq = 0, it = 0, ts0_it = 0, pending = 0;
-      uint64_t cur_rel = 0;
-      bool started = false;
-      for (;;) {
-        const bool hg = it < n, hl = WIDE && qh < nq;
-        const uint64_t relg = hg ? (mk[it] >> 32) : ~0ull;
-        const bool take_l = hl && (uint64_t)qrel[qh * HB] < relg;
-        const uint64_t rel = take_l ? (uint64_t)qrel[qh * HB] : relg;
-        if (started && rel > cur_rel && pending) {
-          // flush the inline children of this node's gen-0 events at cur_rel (positions [ts0_it, it))
-          for (uint32_t jt = ts0_it; jt < it; jt++) {
-            const uint32_t xr = my[jt];
-            const uint32_t ncr = M.nchild[xr];
-            for (uint32_t j = 0; j < ncr; j++) {
-              const uint32_t sl = xr * M.maxc + j;
-              if ((E.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
-              const uint32_t sa = E.ch_a[sl];  // DoForwardUp -> PacketSink::HandleRead
-              if (M.app_flags[sa] & 2u) {
-                M.appc[sa].rx_packets++;
-                M.appc[sa].rx_bytes += E.ch_pkt[sl].size - 28;
-              }
-            }
-          }
-          pending = 0;
-        }
-        if (!hg && !hl) break;
-        if (!started || rel > cur_rel) {
-          ts0_it = it;
-          cur_rel = rel;
-          started = true;
-        }
-        uint32_t s, kw, a;
-        Pkt pk{0, 0, 0, 0};
-        uint64_t key = 0;
-        if (WIDE && take_l) {  // a local record: PointToPointNetDevice::TransmitComplete
-          s = qrec[qh * HB];
-          qh++;
-          E.ctx = M.wctx[s];
-          kw = K_TX_COMPLETE;
-          a = M.wa[s];
-          E.uid = LOCALBIT | s;
-          E.demote = false;
-        } else {
-          s = my[it];
-          key = mk[it];
-          it++;
-          E.ctx = M.wctx[base + s];  // (Schedule calls inherit the event's context)
-          kw = M.wkind[base + s];
-          a = M.wa[base + s];
-          pk = M.wpkt[base + s];
-          E.uid = (uint32_t)key;
-          E.demote = rel == slo || rel == shi;
-        }
-        E.now = tmin + rel;
-        E.slot0 = s * M.maxc;
-        E.n = 0;
-        E.trseq = 0;
-        E.lj = -1;
-        hs.cancelled += run_event(M, E, kw, a, pk, sink, hs);
-        uint32_t ni = 0;
-        if (rel < inline_lim)
-          for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
-        slot_done(M, s, key, E.n, ni, xa);
-        pending += ni;
-        if (WIDE && E.lj >= 0) {
-          const uint32_t r2 = local_record(M, E, s, tmin, blockIdx.x, lcnt_sh, true);
-          if (r2 != NOSRC) lq_push(M, qrel, qrec, HB, qh, nq, (uint32_t)(E.lts - tmin), r2);
-        }
-      }
-      tmn = E.tmn;
-      wnd = E.wnd;
-      wndw = E.wndw;
-    }
-  }
-  publish_min<HB, WIDE>(R, tmn, wnd, wndw);
-  x1_totals(M, xa);
-  if (hs.stop) C.stop_seen = 1;
-  if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
-  if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
-  if (hs.no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)hs.no_route);
-  if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
-  if (hs.icmp) atomicAdd((unsigned long long *)&C.icmp, (unsigned long long)hs.icmp);
-}
-
-// ---- k2_handle: hub blocks ----
-// Device state of the device a hub's serial device pass is on, in registers.
+// Device state of the device a holder's or a hub's serial device pass is on, in registers.
 struct DevCache {
   uint32_t d, busy, cnt, head, qmax, peer, peer_node;
   uint64_t bps;
@@ -913,6 +775,175 @@ __device__ __forceinline__ void device_act_cached(const P2PDev &M, Emit &E, cons
   }
 }
 
+template <bool WIDE>
+__device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i0, uint32_t W, uint32_t base, Red &R,
+                                             uint32_t *lds, const HCtl &hc, SlotPre sp, uint32_t *lcnt_sh) {
+  uint32_t *chs = lds;
+  uint64_t *chk = reinterpret_cast<uint64_t *>(lds + HB * CH);
+  uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull;
+  HStat hs{0, 0, 0, 0, false};
+  if (base != 0 && i0 < W) {
+    sp.ctx = M.wctx[base + i0];
+    sp.kind = M.wkind[base + i0];
+    sp.a = M.wa[base + i0];
+    sp.key = M.wkey[base + i0];
+  }
+  X1Acc xa{0, 0, 0};
+  const uint32_t wi = i0 < W ? sp.widx : 1u;
+  if (wi == NOHOLD) slot_done(M, i0, sp.key, 0, 0, xa);  // NetDevice::Start: dispatched, no children
+  if (wi == 0) {  // the holder
+    const uint32_t c = lp_of(M, sp.ctx, sp.kind, sp.a);
+    uint32_t n = 1;
+    int32_t sink = -1;
+    if (c < M.n_nodes) {
+      n = M.node_tab[(uint64_t)c * NTAB];
+      sink = M.sink_of_node[c];
+    }
+    if (n <= (uint32_t)CH) {  // (a hub's events are its hub block's)
+      if (c < M.n_nodes) M.node_tab[(uint64_t)c * NTAB] = 0;
+      const uint64_t key0 = sp.key;
+      uint32_t *my = &chs[threadIdx.x * CH];
+      uint64_t *mk = &chk[threadIdx.x * CH];
+      my[0] = i0;
+      mk[0] = key0;
+      if (n > 1) {
+        const uint32_t ns = n < (uint32_t)NSLOT ? n : (uint32_t)NSLOT;
+        for (uint32_t j = 0; j < ns; j++) my[j] = M.node_tab[(uint64_t)c * NTAB + 1 + j];
+        if (n > (uint32_t)NSLOT) {  // the rest: window entries of node c not in the table
+          uint32_t m = NSLOT;
+          for (uint32_t x = 0; x < W && m < n; x++)
+            if (M.widx[x] >= (uint32_t)NSLOT && M.widx[x] != NOHOLD &&
+                lp_of(M, M.wctx[base + x], M.wkind[base + x], M.wa[base + x]) == c)
+              my[m++] = x;
+        }
+        for (uint32_t j = 0; j < n; j++) mk[j] = M.wkey[base + my[j]];
+        for (uint32_t a = 1; a < n; a++) {  // insertion sort by key
+          const uint32_t v = my[a];
+          const uint64_t kv = mk[a];
+          uint32_t bb = a;
+          while (bb > 0 && mk[bb - 1] > kv) {
+            my[bb] = my[bb - 1];
+            mk[bb] = mk[bb - 1];
+            bb--;
+          }
+          my[bb] = v;
+          mk[bb] = kv;
+        }
+      }
+      const uint64_t tmin = hc.tmin, inline_lim = hc.inline_lim, slo = hc.slo, shi = hc.shi;
+      Emit E;
+      E.ctx = c;
+      E.ch_ts = M.ch_ts;
+      E.ch_ctx = M.ch_ctx;
+      E.ch_kind = M.ch_kind;
+      E.ch_a = M.ch_a;
+      E.ch_pkt = M.ch_pkt;
+      E.lookahead = M.lookahead;
+      E.lookw = WIDE ? M.lookw : nullptr;
+      E.tmn = ~0ull;
+      E.wnd = ~0ull;
+      E.wndw = ~0ull;
+      E.lim_abs = WIDE && hc.lim ? tmin + hc.lim : 0;
+      // the node's events in key order: its gen-0 window events (sorted above) merged with the local records
+      // its own TransmitStarts make (a gen-0 event first at equal ts: its uid is older)
+      uint32_t *qrel = lds + HB * CH * 3 + threadIdx.x;
+      const LQ4 lq{qrel, qrel + HB * LQ, qrel + 2 * HB * LQ, qrel + 3 * HB * LQ, (uint32_t)HB};
+      // the node's device state in registers across its events (every device step of a node's events is
+      // on one of its own devices; the Receive's rx counter is not cached)
+      DevCache D;
+      D.d = NOSRC;
+      uint32_t qh = 0, nq = 0, it = 0, ts0_it = 0, pending = 0;
+      uint64_t cur_rel = 0;
+      bool started = false;
+      for (;;) {
+        const bool hg = it < n, hl = WIDE && qh < nq;
+        const uint64_t relg = hg ? (mk[it] >> 32) : ~0ull;
+        const bool take_l = hl && (uint64_t)qrel[qh * HB] < relg;
+        const uint64_t rel = take_l ? (uint64_t)qrel[qh * HB] : relg;
+        if (started && rel > cur_rel && pending) {
+          // flush the inline children of this node's gen-0 events at cur_rel (positions [ts0_it, it))
+          for (uint32_t jt = ts0_it; jt < it; jt++) {
+            const uint32_t xr = my[jt];
+            const uint32_t ncr = M.nchild[xr];
+            for (uint32_t j = 0; j < ncr; j++) {
+              const uint32_t sl = xr * M.maxc + j;
+              if ((E.ch_kind[sl] & 0xffu) != K_FWD_UP) continue;
+              const uint32_t sa = E.ch_a[sl];  // DoForwardUp -> PacketSink::HandleRead
+              if (M.app_flags[sa] & 2u) {
+                M.appc[sa].rx_packets++;
+                M.appc[sa].rx_bytes += E.ch_pkt[sl].size - 28;
+              }
+            }
+          }
+          pending = 0;
+        }
+        if (!hg && !hl) break;
+        if (!started || rel > cur_rel) {
+          ts0_it = it;
+          cur_rel = rel;
+          started = true;
+        }
+        uint32_t s, kw, a;
+        Pkt pk{0, 0, 0, 0};
+        uint64_t key = 0;
+        if (WIDE && take_l) {  // a local record: PointToPointNetDevice::TransmitComplete
+          s = lq.rec[qh * HB];
+          E.ctx = lq.ctx[qh * HB];
+          a = lq.dev[qh * HB];
+          qh++;
+          kw = K_TX_COMPLETE;
+          E.uid = LOCALBIT | s;
+          E.demote = false;
+        } else {
+          s = my[it];
+          key = mk[it];
+          it++;
+          E.ctx = M.wctx[base + s];  // (Schedule calls inherit the event's context)
+          kw = M.wkind[base + s];
+          a = M.wa[base + s];
+          pk = M.wpkt[base + s];
+          E.uid = (uint32_t)key;
+          E.demote = rel == slo || rel == shi;
+        }
+        E.now = tmin + rel;
+        E.slot0 = s * M.maxc;
+        E.n = 0;
+        E.trseq = 0;
+        E.lj = -1;
+        {  // run_event with the device step on the cached state
+          const NodeOut o = node_part(M, E, kw, a, pk, sink, hs);
+          device_act_cached(M, E, o.act, D);
+          if (o.xdrop) trace_te_drop(M, E, o.xdrop - 1, o.act.p);
+          if (o.post.valid) E.child(o.post.delay, E.ctx, o.post.kind, o.post.a, Pkt{0, 0, 0, 0});
+          hs.cancelled += o.cancelled;
+        }
+        uint32_t ni = 0;
+        if (rel < inline_lim)
+          for (uint32_t j = 0; j < E.n; j++) ni += (E.ch_kind[E.slot0 + j] & 0xffu) == K_FWD_UP;
+        slot_done(M, s, key, E.n, ni, xa);
+        pending += ni;
+        if (WIDE && E.lj >= 0) {
+          const uint32_t r2 = local_record(M, E, s, tmin, blockIdx.x, lcnt_sh, true);
+          if (r2 != NOSRC) lq_push(M, lq, qh, nq, (uint32_t)(E.lts - tmin), r2, E.lctx, E.la);
+        }
+      }
+      D.flush(M);
+      tmn = E.tmn;
+      wnd = E.wnd;
+      wndw = E.wndw;
+    }
+  }
+  publish_min<HB, WIDE>(R, tmn, wnd, wndw);
+  x1_totals(M, xa);
+  if (hs.stop) C.stop_seen = 1;
+  if (hs.cancelled) atomicAdd((unsigned long long *)&C.cancelled, (unsigned long long)hs.cancelled);
+  if (hs.ttl_drops) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)hs.ttl_drops);
+  if (hs.no_route) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)hs.no_route);
+  if (hs.unreach) atomicAdd((unsigned long long *)&C.unreach, (unsigned long long)hs.unreach);
+  if (hs.icmp) atomicAdd((unsigned long long *)&C.icmp, (unsigned long long)hs.icmp);
+}
+
+// ---- k2_handle: hub blocks ----
 // Events whose node part touches no node state: TransmitComplete, and a Receive that IpForward
 // sends on (its node is not the datagram's destination).
 __device__ __forceinline__ bool stateless_event(const P2PDev &M, uint32_t c, uint32_t kind, const Pkt &p) {
@@ -1279,7 +1310,8 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     uint64_t cur_rel = 0;
     bool started = false;
     // local records (wide windows) of this hub, lane 0's queue: merged with the gen-0 events by rel ts
-    __shared__ uint32_t hq_rel[LQ], hq_rec[LQ];
+    __shared__ uint32_t hq_rel[LQ], hq_rec[LQ], hq_ctx[LQ], hq_dev[LQ];
+    const LQ4 hq{hq_rel, hq_rec, hq_ctx, hq_dev, 1u};
     uint32_t qh = 0, nq = 0;
     // the inline DoForwardUp leaves of this node's gen-0 events at cur_rel (positions [ts0_it, it)), before
     // anything at a later ts
@@ -1302,7 +1334,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     auto new_local = [&](uint32_t par) {
       if (!WIDE || E.lj < 0) return;
       const uint32_t r2 = local_record(M, E, par, tmin, NHB + hb, lcnt_sh, false);
-      if (r2 != NOSRC) lq_push(M, hq_rel, hq_rec, 1, qh, nq, (uint32_t)(E.lts - tmin), r2);
+      if (r2 != NOSRC) lq_push(M, hq, qh, nq, (uint32_t)(E.lts - tmin), r2, E.lctx, E.la);
     };
     // the local records due before rel (at equal ts the gen-0 event first); `it`: the next gen-0 position
     auto run_locals = [&](uint64_t rel, uint32_t it) {
@@ -1314,8 +1346,8 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           cur_rel = lrel;
           started = true;
         }
-        const uint32_t s = hq_rec[qh++];
-        E.ctx = M.wctx[s];
+        const uint32_t s = hq_rec[qh], la = hq_dev[qh];
+        E.ctx = hq_ctx[qh++];
         E.now = tmin + lrel;
         E.slot0 = s * M.maxc;
         E.n = 0;
@@ -1323,7 +1355,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
         E.trseq = 0;
         E.demote = false;
         E.lj = -1;
-        device_act_cached(M, E, Act{ACT_KICK, M.wa[s], Pkt{0, 0, 0, 0}}, D);  // TransmitComplete
+        device_act_cached(M, E, Act{ACT_KICK, la, Pkt{0, 0, 0, 0}}, D);  // TransmitComplete
         slot_done(M, s, 0, E.n, 0, xa);
         new_local(s);
       }
@@ -1841,13 +1873,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   }
   __syncthreads();
   PH_MARK(17);
+  // E consecutive ranks a thread (odd where it can be: a stride of E words is free of LDS bank conflicts)
+  uint32_t E = (N + SCAN_THREADS - 1) / SCAN_THREADS;
+  if (E % 2 == 0 && E < (uint32_t)RPT) E++;
   uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
   {
-    uint32_t prev_rel = (tid * RPT < (int)N && tid > 0) ? l_rel[tid * RPT - 1] : 0;
+    uint32_t prev_rel = (tid * E < N && tid > 0) ? l_rel[tid * E - 1] : 0;
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
-      const uint32_t r = tid * RPT + q;
-      if (r < N) {
+      const uint32_t r = tid * E + q;
+      const bool in = (uint32_t)q < E && r < N;
+      if (in) {
         const uint32_t c = l_cnt[r], rel = l_rel[r];
         const uint32_t hd = r == 0 || rel != prev_rel;
         prev_rel = rel;
@@ -1876,12 +1912,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   uint32_t bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu), bh = (uint32_t)(ex >> 42);
   uint32_t g[RPT], ipr[RPT], cpr[RPT];
   {
-    uint32_t prev_rel = (tid * RPT < (int)N && tid > 0) ? l_rel[tid * RPT - 1] : 0;
+    uint32_t prev_rel = (tid * E < N && tid > 0) ? l_rel[tid * E - 1] : 0;
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
-      const uint32_t r = tid * RPT + q;
+      const uint32_t r = tid * E + q;
+      const bool in = (uint32_t)q < E && r < N;
       uint32_t c = 0, hd = 0;
-      if (r < N) {
+      if (in) {
         c = l_cnt[r];
         const uint32_t rel = l_rel[r];
         hd = r == 0 || rel != prev_rel;
@@ -1891,7 +1928,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       g[q] = bh - 1;
       cpr[q] = bc;
       ipr[q] = bi;
-      if (r < N && hd) gstart[g[q]] = r;
+      if (in && hd) gstart[g[q]] = r;
       bc += c & 0xffffu;
       bi += c >> 16;
     }
@@ -1900,14 +1937,16 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   PH_MARK(18);
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    if (r < N) l_cnt[r] = ipr[q];
+    const uint32_t r = tid * E + q;
+      const bool in = (uint32_t)q < E && r < N;
+    if (in) l_cnt[r] = ipr[q];
   }
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    if (r < N) {
+    const uint32_t r = tid * E + q;
+      const bool in = (uint32_t)q < E && r < N;
+    if (in) {
       const uint32_t first = gstart[g[q]];
       const uint32_t last = (g[q] + 1 < ng ? gstart[g[q] + 1] : N) - 1;
       M.sinfo[l_slot[r]] = make_uint4(r + (tinl ? l_cnt[first] : 0), last + 1 + ipr[q], cpr[q], ipr[q]);
@@ -1917,8 +1956,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     __syncthreads();  // (gstart is reused: the child prefix by rank, for the local records' uids)
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
-      const uint32_t r = tid * RPT + q;
-      if (r < N) gstart[r] = cpr[q];
+      const uint32_t r = tid * E + q;
+      const bool in = (uint32_t)q < E && r < N;
+      if (in) gstart[r] = cpr[q];
     }
     __syncthreads();
   }

@@ -18,7 +18,8 @@ BLK = 2048
 buf = np.zeros(64 + 3 * BLK * 2, np.uint64)
 nsgpu.check(nsgpu.lib().nsgpu_p2p_phase_read(buf.ctypes.data, buf.size, 1))
 blk = buf[64:].reshape(3, BLK, 2).astype(np.int64)
-roles = {0: [("slot", 0, 16), ("pool", 16, 256)],
+nslot = (4096 + 4096) // 256 if eng.wide() else 16  # (wide: gen-0 slots + the local records' dense list)
+roles = {0: [("slot", 0, 16), ("lslot", 16, nslot), ("pool", nslot, 256)],
          1: [("holder", 0, 64), ("rank", 64, 1088), ("hub", 1088, 1120), ("maint", 1120, 1248)],
          2: [("scan", 0, 1)]}
 for k, name in enumerate(("k2_pa", "k2_handle", "k2_scan")):
