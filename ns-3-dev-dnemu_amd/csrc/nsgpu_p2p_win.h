@@ -1783,14 +1783,18 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   const uint32_t base = run ? c_wbase : 0;
   // ---- pool bookkeeping: the free stack loses the slots the fresh children took and gains the
   // window's; its pushed part is moved down over the popped hole
+  // (last in the kernel: a moving wave waits for its loads, and nothing here reads the stack)
   const uint64_t consumed = nF < nfree ? nF : nfree;
   const uint64_t mv = consumed < npush ? consumed : npush;
-  for (uint64_t i = tid; i < mv; i += SCAN_THREADS) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
-  if (handled) {
-    const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
-    for (uint32_t h = tid; h < nh; h += SCAN_THREADS) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
-  }
+  auto stack_and_hubs = [&]() {
+    for (uint64_t i = tid; i < mv; i += SCAN_THREADS) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
+    if (handled) {
+      const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
+      for (uint32_t h = tid; h < nh; h += SCAN_THREADS) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
+    }
+  };
   if (!handled) {  // the window overflowed WCAP: it becomes a sorted run (host radix sort), nothing dispatched yet
+    stack_and_hubs();
     __syncthreads();
     if (tid == 0) {
       C.nfree = nfree - consumed + npush;
@@ -1866,7 +1870,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   for (int q = 0; q < RPT; q++) {  // record order -> rank order
     if (valid_q(q)) {
       const uint32_t r = pr[q];
-      l_slot[r] = prec[q];
       l_cnt[r] = pc[q];
       l_rel[r] = prel[q];
     }
@@ -1933,46 +1936,38 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       bi += c >> 16;
     }
   }
+  const uint32_t last_rel = (tid == 0 && N) ? l_rel[N - 1] : 0u;  // (bookkeeping: the window's last ts)
   __syncthreads();
   PH_MARK(18);
+  // per rank: inline prefix (l_cnt), group (l_rel: read above, free now), child prefix (l_slot); then each
+  // thread writes its own records' sinfo (record order: coalesced for the gen-0 slots)
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * E + q;
-      const bool in = (uint32_t)q < E && r < N;
-    if (in) l_cnt[r] = ipr[q];
+    const bool in = (uint32_t)q < E && r < N;
+    if (in) {
+      l_cnt[r] = ipr[q];
+      l_rel[r] = g[q];
+      l_slot[r] = cpr[q];
+    }
   }
   __syncthreads();
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * E + q;
-      const bool in = (uint32_t)q < E && r < N;
-    if (in) {
-      const uint32_t first = gstart[g[q]];
-      const uint32_t last = (g[q] + 1 < ng ? gstart[g[q] + 1] : N) - 1;
-      M.sinfo[l_slot[r]] = make_uint4(r + (tinl ? l_cnt[first] : 0), last + 1 + ipr[q], cpr[q], ipr[q]);
-    }
-  }
-  if (WIDE && Lt) {
-    __syncthreads();  // (gstart is reused: the child prefix by rank, for the local records' uids)
-#pragma unroll
-    for (int q = 0; q < RPT; q++) {
-      const uint32_t r = tid * E + q;
-      const bool in = (uint32_t)q < E && r < N;
-      if (in) gstart[r] = cpr[q];
-    }
-    __syncthreads();
-  }
   // the keys / contexts the next k2_pa appends with: a local record's uid is its parent's child prefix +
-  // its child index (DefaultSimulatorImpl::Schedule order); the local records' list; ranks cleared
+  // its child index (DefaultSimulatorImpl::Schedule order); ranks cleared
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     if (valid_q(q)) {
-      const uint32_t r = prec[q];
+      const uint32_t r = pr[q], rc = prec[q];
+      const uint32_t gg = l_rel[r];
+      const uint32_t first = gstart[gg];
+      const uint32_t last = (gg + 1 < ng ? gstart[gg + 1] : N) - 1;
+      const uint32_t ip = l_cnt[r];
+      M.sinfo[rc] = make_uint4(r + (tinl ? l_cnt[first] : 0), last + 1 + ip, l_slot[r], ip);
       if (WIDE && q >= RPT0) {  // (k2_rank wrote the dense list lrec)
-        M.pwkey[r] = ((uint64_t)prel[q] << 32) | (uint32_t)(uid0 + gstart[ppx[q] & 0xffffu] + (ppx[q] >> 16));
+        M.pwkey[rc] = ((uint64_t)prel[q] << 32) | (uint32_t)(uid0 + l_slot[ppx[q] & 0xffffu] + (ppx[q] >> 16));
         M.lrank[tid + q * SCAN_THREADS - WCAP] = 0;
       } else if (!run) {
-        M.wrank[r] = 0;
+        M.wrank[rc] = 0;
       }
     }
   }
@@ -1981,6 +1976,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   uint64_t rn1 = 0;
   bool rtrim = false;
   if (run && c_r0 + W < c_rW && !c_rtrim) run_chunk_end<SCAN_THREADS>(M, c_r0 + W, c_rW, rn1, rtrim);
+  stack_and_hubs();
   PH_MARK(19);
   if (tid == 0) {
     C.pK0 = bk.K;
@@ -1991,7 +1987,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     C.plt = Lt;
     C.pinl = tinl;
     C.pvalid = 1;
-    if (N) C.last_ts = bk.tmin + l_rel[N - 1];
+    if (N) C.last_ts = bk.tmin + last_rel;
     C.K = bk.K + N + tinl;
     C.uid = bk.uid + tc;
     C.pchild = tc - tinl - Lt;  // (the local records' uids were consumed, they ran in the window)
