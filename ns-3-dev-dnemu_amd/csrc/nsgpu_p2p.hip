@@ -620,9 +620,8 @@ __device__ __forceinline__ Pkt icmp_error(const Pkt &p, bool unreach) {
              (p.ipid & 0xffffu) << 16, 56u, 64u | ((p.ttl & 0xffu) << 8) | (p.size << 16)};
 }
 
-// Ipv4 route lookup: the static next-hop device of node n towards the packet's destination.
-__device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const Pkt &p) {
-  const uint32_t slot = pkt_dst_slot(M, p);
+// Ipv4 route lookup: the static next-hop device of node n towards route-table slot `slot`.
+__device__ __forceinline__ uint32_t route_at(const P2PDev &M, uint32_t n, uint32_t slot) {
   if (slot == 0xffffffffu) return 0xffffffffu;
   if (M.route) return M.route[(uint64_t)n * M.n_dst + slot];
   // compressed: binary search of the node's exceptions (a dumbbell router holds one per leaf); a node
@@ -636,6 +635,10 @@ __device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const 
     else hi = mid;
   }
   return (lo < e1 && M.route_exc_slot[lo] == slot) ? M.route_exc_dev[lo] : M.route_def[n];
+}
+// ... towards the packet's destination.
+__device__ __forceinline__ uint32_t route_of(const P2PDev &M, uint32_t n, const Pkt &p) {
+  return route_at(M, n, pkt_dst_slot(M, p));
 }
 
 // Icmpv4L4Protocol::SendMessage (icmpv4-l4-protocol.cc:85-129): RouteOutput towards the error's
@@ -661,9 +664,16 @@ struct NodeOut {
   uint32_t xdrop;  // forwarding device + 1 of a TTL-expired datagram whose time-exceeded error is act:
                    // its Drop record follows the device step (0: none)
 };
-// rx_atomic: the device's rx counter is also added to by other lanes (hub blocks).
+// A Receive's addressing (pkt_dst_node, pkt_dst_slot), loaded ahead of the event by its caller.
+struct DstHint {
+  bool valid;
+  uint32_t node, slot;
+};
+// rx_atomic: the device's rx counter is added with an atomic (hub blocks: other lanes add to it too;
+// holders: a no-return atomic, so the event does not wait for the counter's line).
 __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t kind_word, uint32_t a,
-                                             const Pkt &pkt, int32_t sink, HStat &hs, bool rx_atomic = false) {
+                                             const Pkt &pkt, int32_t sink, HStat &hs, bool rx_atomic = false,
+                                             DstHint hint = DstHint{false, 0, 0}) {
   const uint32_t kind = kind_word & 0xffu;
   const uint32_t gen = kind_word >> 8;
   Act act{ACT_NONE, 0, Pkt{0, 0, 0, 0}};
@@ -681,7 +691,7 @@ __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t 
     const uint32_t n = E.ctx < M.n_nodes ? E.ctx : M.dev_node[a];
     const bool reply = (p.app & NSGPU_PKT_REPLY) != 0;
     const uint32_t fa = p.app & ~NSGPU_PKT_REPLY;
-    if (pkt_dst_node(M, p) == n) {
+    if ((hint.valid ? hint.node : pkt_dst_node(M, p)) == n) {
       // LocalDeliver -> UdpL4Protocol::Receive (udp-l4-protocol.cc:312-407): the bound endpoint is the
       // client's own socket for an echo reply, else the node's PacketSink / UdpEchoServer.  An ICMP error
       // ends in Icmpv4L4Protocol::Receive -> UdpL4Protocol::ReceiveIcmp (no event, no counter).
@@ -697,7 +707,7 @@ __device__ __forceinline__ NodeOut node_part(const P2PDev &M, Emit &E, uint32_t 
         E.child(0, E.ctx, q ? K_FWD_UP_Q : K_FWD_UP, (uint32_t)k, p);
       }
     } else {
-      const uint32_t out = route_of(M, n, p);
+      const uint32_t out = hint.valid ? route_at(M, n, hint.slot) : route_of(M, n, p);
       if (out == 0xffffffffu) {
         hs.no_route++;
         trace_ip_drop(M, E, a, p);  // DROP_NO_ROUTE

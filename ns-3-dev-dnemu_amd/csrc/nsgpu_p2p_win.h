@@ -586,6 +586,7 @@ struct HCtl {
 struct SlotPre {
   uint32_t widx, ctx, kind, a;
   uint64_t key;
+  Pkt pkt;
 };
 
 // A local record's chain order packed into two words (lexicographic), the LKey compare only for a tie:
@@ -608,7 +609,7 @@ __device__ __forceinline__ uint64_t lk_word2(const LKey &k) {
 // threads, or a hub block's lane 0), written like a window record; its key holds the rel ts (its uid is
 // assigned by k2_scan: uid0 + the parent's child prefix + j).  NOSRC: the region is full (error 32).
 __device__ __forceinline__ uint32_t local_record(const P2PDev &M, const Emit &E, uint32_t par, uint64_t tmin,
-                                                 uint32_t region, uint32_t *cnt, bool atomic) {
+                                                 uint32_t region, uint32_t *cnt, bool atomic, uint64_t par_key) {
   const uint32_t cap = region < (uint32_t)NHB ? (uint32_t)LR : (uint32_t)LRH;
   const uint32_t k = atomic ? atomicAdd(cnt, 1u) : (*cnt)++;
   if (k >= cap) {
@@ -624,8 +625,8 @@ __device__ __forceinline__ uint32_t local_record(const P2PDev &M, const Emit &E,
   M.wpar[rec] = par | ((uint32_t)E.lj << 24);
   // its chain for k2_rank: the parent's, one level up
   LKey x;
-  if (par < LBASE) {
-    const uint64_t pk = M.wkey[par];
+  if (par < LBASE) {  // (par_key: the gen-0 parent's window key, wkey[par])
+    const uint64_t pk = par_key;
     x.rel[1] = (uint32_t)(pk >> 32);
     x.uid = (uint32_t)pk;
     x.depth = 1;
@@ -787,12 +788,17 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
     sp.kind = M.wkind[base + i0];
     sp.a = M.wa[base + i0];
     sp.key = M.wkey[base + i0];
+    sp.pkt = M.wpkt[base + i0];
   }
   X1Acc xa{0, 0, 0};
   const uint32_t wi = i0 < W ? sp.widx : 1u;
   if (wi == NOHOLD) slot_done(M, i0, sp.key, 0, 0, xa);  // NetDevice::Start: dispatched, no children
   if (wi == 0) {  // the holder
     const uint32_t c = lp_of(M, sp.ctx, sp.kind, sp.a);
+    // its own event's addressing, if a Receive, loaded beside the node table (the node's only event, or
+    // one of them: used when it runs)
+    DstHint h0{false, 0, 0};
+    if ((sp.kind & 0xffu) == K_RECEIVE) h0 = DstHint{true, pkt_dst_node(M, sp.pkt), pkt_dst_slot(M, sp.pkt)};
     uint32_t n = 1;
     int32_t sink = -1;
     if (c < M.n_nodes) {
@@ -886,6 +892,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
         uint32_t s, kw, a;
         Pkt pk{0, 0, 0, 0};
         uint64_t key = 0;
+        DstHint hint{false, 0, 0};
         if (WIDE && take_l) {  // a local record: PointToPointNetDevice::TransmitComplete
           s = lq.rec[qh * HB];
           E.ctx = lq.ctx[qh * HB];
@@ -898,10 +905,18 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
           s = my[it];
           key = mk[it];
           it++;
-          E.ctx = M.wctx[base + s];  // (Schedule calls inherit the event's context)
-          kw = M.wkind[base + s];
-          a = M.wa[base + s];
-          pk = M.wpkt[base + s];
+          if (s == i0) {  // (the holder's own event: loaded at entry)
+            E.ctx = sp.ctx;
+            kw = sp.kind;
+            a = sp.a;
+            pk = sp.pkt;
+            hint = h0;
+          } else {
+            E.ctx = M.wctx[base + s];  // (Schedule calls inherit the event's context)
+            kw = M.wkind[base + s];
+            a = M.wa[base + s];
+            pk = M.wpkt[base + s];
+          }
           E.uid = (uint32_t)key;
           E.demote = rel == slo || rel == shi;
         }
@@ -911,7 +926,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
         E.trseq = 0;
         E.lj = -1;
         {  // run_event with the device step on the cached state
-          const NodeOut o = node_part(M, E, kw, a, pk, sink, hs);
+          const NodeOut o = node_part(M, E, kw, a, pk, sink, hs, true, hint);
           device_act_cached(M, E, o.act, D);
           if (o.xdrop) trace_te_drop(M, E, o.xdrop - 1, o.act.p);
           if (o.post.valid) E.child(o.post.delay, E.ctx, o.post.kind, o.post.a, Pkt{0, 0, 0, 0});
@@ -923,7 +938,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
         slot_done(M, s, key, E.n, ni, xa);
         pending += ni;
         if (WIDE && E.lj >= 0) {
-          const uint32_t r2 = local_record(M, E, s, tmin, blockIdx.x, lcnt_sh, true);
+          const uint32_t r2 = local_record(M, E, s, tmin, blockIdx.x, lcnt_sh, true, key);
           if (r2 != NOSRC) lq_push(M, lq, qh, nq, (uint32_t)(E.lts - tmin), r2, E.lctx, E.la);
         }
       }
@@ -1333,7 +1348,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     };
     auto new_local = [&](uint32_t par) {
       if (!WIDE || E.lj < 0) return;
-      const uint32_t r2 = local_record(M, E, par, tmin, NHB + hb, lcnt_sh, false);
+      const uint32_t r2 = local_record(M, E, par, tmin, NHB + hb, lcnt_sh, false, par < LBASE ? M.wkey[par] : 0ull);
       if (r2 != NOSRC) lq_push(M, hq, qh, nq, (uint32_t)(E.lts - tmin), r2, E.lctx, E.la);
     };
     // the local records due before rel (at equal ts the gen-0 event first); `it`: the next gen-0 position
@@ -1482,7 +1497,7 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   SlotPre sp{1u, 0, 0, 0, 0};
   if (bx < (uint32_t)NHB) {
     const uint32_t i0 = bx * HB + threadIdx.x;
-    sp = SlotPre{M.widx[i0], M.wctx[i0], M.wkind[i0], M.wa[i0], M.wkey[i0]};
+    sp = SlotPre{M.widx[i0], M.wctx[i0], M.wkind[i0], M.wa[i0], M.wkey[i0], M.wpkt[i0]};
   }
   // partitioned: every rank's X0 payload (window candidates, hub flag): a window some rank cannot hold
   // is cut by the host (k_refit2 / k_cut2) before anything of it runs, on every rank
