@@ -1056,7 +1056,10 @@ __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_
   const uint32_t r0 = ti * HB * RTR;
   if (r0 >= W || tj * RJ >= W) return;  // uniform over the block
 #pragma unroll
-  for (int q = 0; q < RJ / HB; q++) tk[q * HB + threadIdx.x] = M.wkey[tj * RJ + q * HB + threadIdx.x];
+  for (int q = 0; q < RJ / HB; q++) {  // (slots past W hold stale keys: padded with a key after every row's)
+    const uint32_t j = tj * RJ + q * HB + threadIdx.x;
+    tk[q * HB + threadIdx.x] = j < W ? M.wkey[j] : ~0ull;
+  }
   uint64_t x[RTR];
 #pragma unroll
   for (int r = 0; r < RTR; r++) {
@@ -1065,20 +1068,11 @@ __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_
   }
   __syncthreads();
   uint32_t c[RTR] = {};
-  const int jn = W - tj * RJ < (uint32_t)RJ ? (int)(W - tj * RJ) : RJ;  // (slots past W hold stale keys)
-  if (jn == RJ) {
-#pragma unroll 8
-    for (int y = 0; y < RJ; y++) {
-      const uint64_t k = tk[y];
+#pragma unroll 16
+  for (int y = 0; y < RJ; y++) {
+    const uint64_t k = tk[y];
 #pragma unroll
-      for (int r = 0; r < RTR; r++) c[r] += k < x[r];
-    }
-  } else {
-    for (int y = 0; y < jn; y++) {
-      const uint64_t k = tk[y];
-#pragma unroll
-      for (int r = 0; r < RTR; r++) c[r] += k < x[r];
-    }
+    for (int r = 0; r < RTR; r++) c[r] += k < x[r];
   }
 #pragma unroll
   for (int r = 0; r < RTR; r++) {
@@ -1316,9 +1310,9 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
     const uint32_t j0 = (tj - s_off[q]) * RJ;
     const uint32_t n = s_w[q] - j0 < (uint32_t)RJ ? s_w[q] - j0 : (uint32_t)RJ;
     const X1Ent *E = x1ent(M.x1_recv, q) + j0;
-    for (uint32_t k = threadIdx.x; k < n; k += HB) {
-      tk[k] = E[k].key;
-      tc[k] = E[k].cnt;
+    for (uint32_t k = threadIdx.x; k < (uint32_t)RJ; k += HB) {  // (padding: a key after every row's)
+      tk[k] = k < n ? E[k].key : ~0ull;
+      tc[k] = k < n ? E[k].cnt : 0u;
     }
     __syncthreads();
     const uint32_t i = ti * HB + threadIdx.x;
@@ -1326,7 +1320,9 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
       const uint64_t x = M.wkey[i];
       const uint64_t lo = x & 0xffffffff00000000ull, hi = lo + (1ull << 32);
       uint32_t gr = 0, cp = 0, ip = 0, ipf = 0, lp = 0;
-      for (uint32_t y = 0; y < n; y++) {
+      // (a fixed trip count, unrolled: the LDS loads pipeline instead of waiting one by one)
+#pragma unroll 16
+      for (uint32_t y = 0; y < (uint32_t)RJ; y++) {
         const uint64_t k = tk[y];
         const uint32_t c = tc[y];
         const uint32_t nc = c & 0xffffu, ni = c >> 16;
