@@ -1030,6 +1030,7 @@ struct X2Hdr {
 constexpr int CAPX_MAX = 1024;
 constexpr size_t X0B = 16;  // X0: one rank's largest fitting window bound (+ pad)
 constexpr int MAXR = 64;    // ranks
+static_assert(MAXR <= 64 && HB == 64, "per-rank summaries are read one lane per rank in one-wave blocks");
 static_assert((uint64_t)MAXR * WCAP < (1u << 21), "k_gtile's packed rank fields");
 __device__ __forceinline__ X1Hdr *x1hdr(uint8_t *b, uint32_t q) { return (X1Hdr *)(b + (size_t)q * X1B); }
 __device__ __forceinline__ X1Ent *x1ent(uint8_t *b, uint32_t q) {
@@ -1290,15 +1291,20 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
   __shared__ uint32_t tc[RJ];
   __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR];
   const uint32_t W = C.pW;
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (uint32_t q = 0; q < M.nranks; q++) {
-      const uint32_t wq = x1hdr(M.x1_recv, q)->W;
-      s_w[q] = wq;
-      s_off[q] = acc;
-      acc += (wq + RJ - 1) / RJ;
+  {  // every rank's window size at once, one lane per rank (HB = one wave), and the column tiles' prefix
+    const uint32_t q = threadIdx.x;
+    const uint32_t wq = q < M.nranks ? x1hdr(M.x1_recv, q)->W : 0u;
+    const uint32_t nt = (wq + RJ - 1) / RJ;
+    uint32_t inc = nt;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(inc, o);
+      if ((int)q >= o) inc += x;
     }
-    s_off[M.nranks] = acc;
+    if (q < M.nranks) {
+      s_w[q] = wq;
+      s_off[q] = inc - nt;
+    }
+    if (q == M.nranks - 1) s_off[M.nranks] = inc;
   }
   __syncthreads();
   const uint32_t njt = s_off[M.nranks];
@@ -1351,26 +1357,66 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   Ctl &C = *M.C;
   if (!C.hdl) return;
   const uint32_t W = C.pW;
-  uint32_t tinl_g = 0;
-  for (uint32_t q = 0; q < M.nranks; q++) tinl_g += x1hdr(M.x1_recv, q)->tinl;
+  // every rank's X1 header at once, one lane per rank (HB = one wave)
+  const uint32_t lq = threadIdx.x;
+  const X1Hdr *lh = x1hdr(M.x1_recv, lq < M.nranks ? lq : 0u);
+  const bool lv = lq < M.nranks;
+  const uint32_t tinl_q = lv ? lh->tinl : 0u;
+  // (block 0: the rest of the summaries and the run control, for the run bookkeeping, in the same trip)
+  struct Bk {
+    uint64_t nF, nfree, npush, pK0, ptmin, windows, P_end, live, inline_lim, max_windows, max_window;
+    uint32_t nhub, puid0, rt;
+  } bk{};
+  if (blockIdx.x == 0)
+    bk = Bk{C.nF, C.nfree, C.npush, C.pK0, C.ptmin, C.windows, C.P_end, C.live, C.inline_lim, C.max_windows,
+            C.max_window, C.nhub, C.puid0, C.rt};
+  uint32_t hW = 0, htc = 0, hneedc = 0, hsuid = 0;
+  uint64_t hlk = 0, htmin = ~0ull, hwend = ~0ull, hsts = ~0ull;
+  if (blockIdx.x == 0 && lv) {
+    hW = lh->W;
+    htc = lh->tc;
+    hneedc = lh->needc;
+    hlk = lh->lastkey;
+    htmin = lh->red.tmin;
+    hwend = lh->red.wend;
+    hsts = lh->red.stopts;
+    hsuid = lh->red.stopuid;
+  }
+  // the slot's accumulators, record and first children, all loaded before anything waits
   const uint32_t s = blockIdx.x * HB + threadIdx.x;
-  if (s < W) {
-    uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);
-    const uint64_t w0 = A[s], w1 = A[WCAP + s];
+  const bool vs = s < W;
+  uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);
+  uint64_t w0 = 0, w1 = 0, wk = 0;
+  uint32_t wc = 0, ncr = 0, ckw[PFC], cctx[PFC];
+  if (vs) {
+    w0 = A[s];
+    w1 = A[WCAP + s];
+    wk = M.wkey[s];
+    wc = M.wctx[s];
+    ncr = M.nchild[s];
+#pragma unroll
+    for (int j = 0; j < PFC; j++)
+      if ((uint32_t)j < M.maxc) {
+        ckw[j] = M.ch_kind[s * M.maxc + j];
+        cctx[j] = M.ch_ctx[s * M.maxc + j];
+      }
+  }
+  const uint32_t tinl_g = wave_sum32(tinl_q);
+  if (vs) {
     A[s] = 0;
     A[WCAP + s] = 0;
     const uint32_t gr = (uint32_t)(w0 & 0x1fffffu), lp = (uint32_t)((w0 >> 21) & 0x1fffffu),
                    ip = (uint32_t)(w0 >> 42), cp = (uint32_t)w1, ipf = (uint32_t)(w1 >> 32);
     // as k2_scan: (dispatch rank rel. K0, rank of the first inline child, child prefix, inline prefix)
     M.sinfo[s] = make_uint4(gr + (tinl_g ? ipf : 0), lp + ip, cp, ip);
-    M.pwkey[s] = M.wkey[s];
-    M.pwctx[s] = M.wctx[s];
-    const uint32_t ncr = M.nchild[s], uid0 = C.puid0;
+    M.pwkey[s] = wk;
+    M.pwctx[s] = wc;
+    const uint32_t uid0 = C.puid0;
     for (uint32_t j = 0; j < ncr; j++) {
       const uint32_t sl = s * M.maxc + j;
-      const uint32_t kw = M.ch_kind[sl];
+      const uint32_t kw = j < (uint32_t)PFC ? ckw[j] : M.ch_kind[sl];
       if ((kw & 0xffu) == K_FWD_UP) continue;
-      const uint32_t ctx = M.ch_ctx[sl];
+      const uint32_t ctx = j < (uint32_t)PFC ? cctx[j] : M.ch_ctx[sl];
       const uint32_t q = M.owner[ctx];
       if (q == M.rank) continue;
       const uint32_t pos = atomicAdd(&x2hdr(M, M.x2_send, q)->n, 1u);
@@ -1383,43 +1429,45 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   if (blockIdx.x != 0) return;
   // ---- pool bookkeeping (k2_scan's): the free stack loses the slots the fresh children took and gains
   // the window's; its pushed part is moved down over the popped hole; the hubs' slot tables are cleared
-  const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
+  const uint64_t nF = bk.nF, nfree = bk.nfree, npush = bk.npush;
   const uint64_t consumed = nF < nfree ? nF : nfree;
   const uint64_t mv = consumed < npush ? consumed : npush;
-  for (uint64_t i = threadIdx.x; i < mv; i += HB) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
-  const uint32_t nh = C.nhub < (uint32_t)MAXHUB ? C.nhub : (uint32_t)MAXHUB;
-  for (uint32_t h = threadIdx.x; h < nh; h += HB) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  uint32_t Wg = 0, tcg = 0, needc = 0;
-  uint64_t lk = 0;
+  const uint32_t nh = bk.nhub < (uint32_t)MAXHUB ? bk.nhub : (uint32_t)MAXHUB;
+  // the ranks' summaries, reduced across the lanes (rank q's in lane q)
+  const uint32_t Wg = wave_sum32(hW), tcg = wave_sum32(htc);
+  const uint32_t needc = __ballot(hneedc != 0) ? 1u : 0u;
+  const uint64_t lk = wave_max64(hW ? hlk : 0ull);
   Red rg{~0ull, ~0ull, ~0ull, 0, 0, ~0ull};
-  for (uint32_t q = 0; q < M.nranks; q++) {
-    const X1Hdr *h = x1hdr(M.x1_recv, q);
-    Wg += h->W;
-    tcg += h->tc;
-    needc |= h->needc;
-    if (h->W && h->lastkey > lk) lk = h->lastkey;
-    rg.tmin = h->red.tmin < rg.tmin ? h->red.tmin : rg.tmin;
-    rg.wend = h->red.wend < rg.wend ? h->red.wend : rg.wend;
-    if (h->red.stopts < rg.stopts) {
-      rg.stopts = h->red.stopts;
-      rg.stopuid = h->red.stopuid;
-    }
+  rg.tmin = wave_min64(htmin);
+  rg.wend = wave_min64(hwend);
+  {  // the pending Stop: the smallest stopts, the first rank holding it
+    rg.stopts = wave_min64(hsts);
+    const uint64_t m = __ballot(lv && hsts == rg.stopts && rg.stopts != ~0ull);
+    const int first = m ? __ffsll((unsigned long long)m) - 1 : 0;
+    rg.stopuid = __shfl(hsuid, first);
   }
-  C.K = C.pK0 + Wg + tinl_g;
-  C.uid = C.puid0 + tcg;
-  if (Wg) C.last_ts = C.ptmin + (lk >> 32);
-  const uint32_t rt = C.rt;
+  // (the free-stack move and the hubs' slot tables last: a moving lane waits for its loads)
+  auto stack_and_hubs = [&]() {
+    for (uint64_t i = threadIdx.x; i < mv; i += HB) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
+    for (uint32_t h = threadIdx.x; h < nh; h += HB) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
+  };
+  if (threadIdx.x != 0) {
+    stack_and_hubs();
+    return;
+  }
+  C.K = bk.pK0 + Wg + tinl_g;
+  C.uid = bk.puid0 + tcg;
+  if (Wg) C.last_ts = bk.ptmin + (lk >> 32);
+  const uint32_t rt = bk.rt;
   C.red[rt] = rg;  // bounds the next window (k2_pa reads red[rt ^ 1] after the flip)
   C.rt = rt ^ 1;
-  const uint64_t windows = C.windows + 1;
+  const uint64_t windows = bk.windows + 1;
   C.windows = windows;
-  if (Wg > C.max_window) C.max_window = Wg;
-  const uint64_t P_end = C.P_end + (nF > nfree ? nF - nfree : 0);
+  if (Wg > bk.max_window) C.max_window = Wg;
+  const uint64_t P_end = bk.P_end + (nF > nfree ? nF - nfree : 0);
   C.nfree = nfree - consumed + npush;
   C.P_end = P_end;
-  C.live = C.live - npush + nF;
+  C.live = bk.live - npush + nF;
   C.npush = 0;
   C.nF = 0;
   C.nhub = 0;
@@ -1428,12 +1476,12 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   C.prep = 0;
   // the window that held Simulator::Stop ends the run (every rank knows it from the bound), as does an
   // empty pending set on every rank
-  bool done = C.inline_lim != ~0ull || rg.tmin == ~0ull;
+  bool done = bk.inline_lim != ~0ull || rg.tmin == ~0ull;
   if (P_end > M.pool_cap) {
     atomicOr(M.error, 1u);
     done = true;
   }
-  if (windows >= C.max_windows && !done) {
+  if (windows >= bk.max_windows && !done) {
     atomicOr(M.error, 4u);
     done = true;
   }
@@ -1444,6 +1492,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   hs->lastkey = 0;
   hs->red.tmin = hs->red.wend = hs->red.stopts = hs->red.wendw = ~0ull;
   hs->red.stopuid = 0;
+  stack_and_hubs();
 }
 
 // Loopback transport (nsgpu_p2p_group_*: every partition on one device): one block per copy.

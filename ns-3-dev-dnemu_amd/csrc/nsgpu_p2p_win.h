@@ -1502,11 +1502,15 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   // partitioned: every rank's X0 payload (window candidates, hub flag): a window some rank cannot hold
   // is cut by the host (k_refit2 / k_cut2) before anything of it runs, on every rank
   bool ovf = false;
-  if (M.dist)
-    for (uint32_t q = 0; q < M.nranks; q++) {
+  if (M.dist) {  // (one lane per rank: HB = one wave)
+    const uint32_t q = threadIdx.x;
+    bool o = false;
+    if (q < M.nranks) {
       const uint4 x = reinterpret_cast<const uint4 *>(M.x0_recv)[q];
-      ovf |= x.x > (uint32_t)WCAP || x.z != 0;
+      o = x.x > (uint32_t)WCAP || x.z != 0;
     }
+    ovf = __ballot(o) != 0;
+  }
   if (c_done || c_mode >= MODE_SORT || ovf) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       if (c_done == 1) C.done = 2;  // the final window is appended
