@@ -153,26 +153,36 @@ __device__ __forceinline__ uint32_t lp_of(const P2PDev &M, uint32_t ctx, uint32_
 // Window record `slot` of node `ctx` -> the node's slot table (local slot index); the node that
 // reaches CH + 1 events becomes a hub.  NetDevice::Start is a no-op (the device was started by
 // Node::Start): it is dispatched (logged, uid-ranked) but no holder runs it — a dumbbell router has
-// one per leaf link at time 0.
-__device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t slot, uint32_t ctx, uint32_t kind) {
+// one per leaf link at time 0.  In two halves: the claim issues the count atomic, the finish (late in
+// the kernel, once the atomic's value is back) stores the slot, so a wave does not wait for the atomic.
+struct NtClaim {
+  uint32_t slot, c, idx;  // c == NOSRC: nothing to finish
+};
+__device__ __forceinline__ NtClaim node_table_claim(const P2PDev &M, uint32_t slot, uint32_t ctx, uint32_t kind) {
   if ((kind & 0xffu) == K_DEV_START) {  // (k2_handle writes its zero child counts: k2_pa still reads the
     M.widx[slot] = NOHOLD;               //  last window's counts of this slot)
-    return;
+    return NtClaim{slot, NOSRC, 0};
   }
-  uint32_t idx = 0;
-  if (ctx < M.n_nodes) {
-    idx = atomicAdd(&M.node_tab[(uint64_t)ctx * NTAB], 1u);
-    if (idx < (uint32_t)NSLOT) M.node_tab[(uint64_t)ctx * NTAB + 1 + idx] = slot;
-    if (idx == (uint32_t)CH) {
-      const uint32_t hh = atomicAdd(&C.nhub, 1u);
-      if (hh < (uint32_t)MAXHUB) M.hub_list[hh] = ctx;
-    }
-    if (idx == (uint32_t)HUBL) {  // too many for a hub block: a sorted run; partitioned: a cut (k_refit2)
-      if (M.dist) C.overflow = 1;
-      else C.force_run = 1;
-    }
+  if (ctx < M.n_nodes) return NtClaim{slot, ctx, atomicAdd(&M.node_tab[(uint64_t)ctx * NTAB], 1u)};
+  M.widx[slot] = 0;
+  return NtClaim{slot, NOSRC, 0};
+}
+__device__ __forceinline__ void node_table_finish(const P2PDev &M, Ctl &C, const NtClaim &p) {
+  if (p.c == NOSRC) return;
+  const uint32_t idx = p.idx;
+  if (idx < (uint32_t)NSLOT) M.node_tab[(uint64_t)p.c * NTAB + 1 + idx] = p.slot;
+  if (idx == (uint32_t)CH) {
+    const uint32_t hh = atomicAdd(&C.nhub, 1u);
+    if (hh < (uint32_t)MAXHUB) M.hub_list[hh] = p.c;
   }
-  M.widx[slot] = idx;
+  if (idx == (uint32_t)HUBL) {  // too many for a hub block: a sorted run; partitioned: a cut (k_refit2)
+    if (M.dist) C.overflow = 1;
+    else C.force_run = 1;
+  }
+  M.widx[p.slot] = idx;
+}
+__device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t slot, uint32_t ctx, uint32_t kind) {
+  node_table_finish(M, C, node_table_claim(M, slot, ctx, kind));
 }
 
 // A pending event against the window bound: window record (normal mode, key <= bound), else pending:
@@ -200,9 +210,11 @@ __device__ __forceinline__ void k2_classify(const P2PDev &M, const WinBound &b, 
   }
 }
 
-// Writes a classified event: window record `slot`, or fresh-buffer entry `fi` (a parked child).
-__device__ __forceinline__ void k2_write(const P2PDev &M, Ctl &C, const WinBound &b, const Ev &e, uint32_t src,
-                                         bool in, bool park, uint32_t slot, uint64_t fi) {
+// Writes a classified event: window record `slot`, or fresh-buffer entry `fi` (a parked child).  Returns
+// the window record's node-table claim (to finish later in the kernel).
+__device__ __forceinline__ NtClaim k2_write(const P2PDev &M, Ctl &C, const WinBound &b, const Ev &e, uint32_t src,
+                                            bool in, bool park, uint32_t slot, uint64_t fi) {
+  NtClaim cl{0, NOSRC, 0};
   if (in) {
     if (slot < M.runcap) {
       M.wkey[slot] = ((e.ts - b.tmin) << 32) | e.uid;
@@ -211,7 +223,7 @@ __device__ __forceinline__ void k2_write(const P2PDev &M, Ctl &C, const WinBound
       M.wa[slot] = e.a;
       M.wpkt[slot] = e.p;
       M.wsrc[slot] = src;
-      if (slot < (uint32_t)WCAP) node_table_add(M, C, slot, lp_of(M, e.ctx, e.kind, e.a), e.kind);
+      if (slot < (uint32_t)WCAP) cl = node_table_claim(M, slot, lp_of(M, e.ctx, e.kind, e.a), e.kind);
     } else {
       atomicOr(M.error, 1u);
     }
@@ -227,6 +239,7 @@ __device__ __forceinline__ void k2_write(const P2PDev &M, Ctl &C, const WinBound
       atomicOr(M.error, 1u);
     }
   }
+  return cl;
 }
 
 // Block-wide allocation of window slots (C.W) and fresh-buffer entries (C.nF): per-thread counts in,
@@ -347,6 +360,11 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   uint4 si = make_uint4(0, 0, 0, 0);
   uint32_t ncr = 0, sctx = 0;
   Ev ce[PFC];
+  constexpr int NPEND = 4;  // node-table claims a thread keeps pending (PFC children, or PPT pool entries)
+  static_assert(PFC <= NPEND, "pending claims");
+  NtClaim pend[NPEND];
+#pragma unroll
+  for (int q = 0; q < NPEND; q++) pend[q] = NtClaim{0, NOSRC, 0};
   // the record this slot-role thread appends: gen-0 slot g, or local record lrec[g - WCAP] (lrec holds
   // record indices from earlier windows past C.plt: loaded speculatively, always in range)
   const uint32_t rec = (WIDE && g >= (uint64_t)WCAP && slot_role) ? M.lrec[g - WCAP] : (uint32_t)g;
@@ -428,6 +446,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     const uint32_t nl = vs ? ncr : 0u;
     uint32_t ii = 0;
     for (uint32_t j0 = 0; __syncthreads_or(j0 < nl); j0 += PFC) {
+      if (j0) {  // (the last group's claims: finished now, their atomics had a block allocation's time)
+#pragma unroll
+        for (int q = 0; q < PFC; q++) node_table_finish(M, C, pend[q]);
+      }
       Ev ge[PFC];
       bool gin[PFC], gpk[PFC];
       uint32_t cw = 0, cf = 0;
@@ -472,7 +494,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       BLK_MARK(38, c_win);  // block allocation (atomics)
 #pragma unroll
       for (int q = 0; q < PFC; q++) {
-        k2_write(M, C, b, ge[q], NOSRC, gin[q], gpk[q], w0, f0);
+        pend[q] = k2_write(M, C, b, ge[q], NOSRC, gin[q], gpk[q], w0, f0);
         w0 += gin[q];
         f0 += gpk[q];
       }
@@ -491,7 +513,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       uint32_t w0;
       uint64_t f0;
       block_alloc2<TB>(C, gin, gpk, w0, f0);
-      k2_write(M, C, b, e, NOSRC, gin, gpk, w0, f0);
+      pend[0] = k2_write(M, C, b, e, NOSRC, gin, gpk, w0, f0);
     }
   } else if (partition && !run) {
     // ---- the pool, in place: read (ts, uid, kind) of every slot; window events are copied out.
@@ -500,7 +522,12 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     constexpr int PPT = 4;
     const uint64_t P = c_P;
     const uint64_t pb = blockIdx.x - (uint64_t)(NSGB + rrb), npb = gridDim.x - (uint64_t)(NSGB + rrb);
+    static_assert(PPT <= NPEND, "pending claims");
     for (uint64_t c0 = pb * TB * PPT; c0 < P; c0 += npb * TB * PPT) {  // block-uniform trip count
+#pragma unroll
+      for (int q = 0; q < PPT; q++) node_table_finish(M, C, pend[q]);  // (the last chunk's)
+#pragma unroll
+      for (int q = 0; q < PPT; q++) pend[q].c = NOSRC;
       Ev ge[PPT];
       bool gin[PPT], gpk[PPT];
       uint32_t cw = 0;
@@ -530,7 +557,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 #pragma unroll
       for (int q = 0; q < PPT; q++) {
         const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
-        k2_write(M, C, b, ge[q], (uint32_t)i, gin[q], false, w0, 0);
+        pend[q] = k2_write(M, C, b, ge[q], (uint32_t)i, gin[q], false, w0, 0);
         w0 += gin[q];
       }
     }
@@ -566,6 +593,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       if (dg) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)dg);
     }
   }
+  // the node-table claims still pending (their atomics overlapped the reductions above)
+#pragma unroll
+  for (int q = 0; q < NPEND; q++) node_table_finish(M, C, pend[q]);
   PH_MARK(2);
   if (slot_block) BLK_MARK(44, c_win);  // publish_min, digest
   BLK_REC(0, c_win);
