@@ -33,6 +33,7 @@ namespace {
 
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr int LPE_CAP = 8;  // pending EndReceive records of one phy (the live one + cancelled ones)
+constexpr uint32_t END_STAGE = 128;  // EndReceive records an epoch returns with its counters (more: a second copy)
 constexpr uint32_t WE_TX_IN_TX = 1, WE_NICAP = 2, WE_RQCAP = 4, WE_PECAP = 8, WE_CAP = 16;
 constexpr int NB = 8;  // ring entries loaded per batch
 
@@ -90,7 +91,10 @@ struct WDev {
   LEv *ev;
   nsgpu_wifil_end *ends;
   uint32_t *end_sslot;
-  uint32_t *cnt;  // [0] events, [1] syncs, [2] ends, [3] error bits
+  uint32_t *cnt;  // [0] events, [1] syncs, [2] ends, [3] error bits (sticky: a SendPacket's are seen at the
+                  // next advance)
+  uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_erank; 0 between epochs)
+  unsigned long long *edig;  // the epoch's digest terms, summed on the device (k_wl_edigest)
   uint64_t sync_cap, ev_cap, end_cap;
 };
 
@@ -538,6 +542,63 @@ __global__ __launch_bounds__(256) void k_wl_patch(const WDev D) {
   }
 }
 
+// The epoch's dispatch order on the device (epochs of at most ERANK_MAX events; larger ones are ordered by
+// the host): each event's rank = the number of the epoch's events with a smaller (ts, uid), by tiles of
+// 256 rows x 64 columns (one 16-B LDS load and a compare per column, unrolled); then the digest terms
+// nsgpu_dispatch_digest_term (K0 + rank, ts, uid), summed per block, one atomic each.
+constexpr uint32_t ERANK_MAX = 65536;
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+constexpr int ERT = 256, ERC = 64;
+__global__ __launch_bounds__(ERT) void k_wl_erank(const WDev D) {
+  const uint32_t nev = D.cnt[0] < D.ev_cap ? D.cnt[0] : (uint32_t)D.ev_cap;
+  if (nev == 0 || nev > ERANK_MAX) return;
+  __shared__ ulonglong2 ck[ERC];
+  const uint32_t nr = (nev + ERT - 1) / ERT, nc = (nev + ERC - 1) / ERC;
+  for (uint32_t t = blockIdx.x; t < nr * nc; t += gridDim.x) {  // (uniform over the block)
+    const uint32_t ti = t / nc, tj = t % nc;
+    if (threadIdx.x < (uint32_t)ERC) {
+      const uint32_t j = tj * ERC + threadIdx.x;
+      ck[threadIdx.x] = j < nev ? make_ulonglong2(D.ev[j].ts, D.ev[j].uid) : make_ulonglong2(~0ull, ~0ull);
+    }
+    const uint32_t i = ti * ERT + threadIdx.x;
+    uint64_t xts = ~0ull, xuid = ~0ull;
+    if (i < nev) {
+      xts = D.ev[i].ts;
+      xuid = D.ev[i].uid;
+    }
+    __syncthreads();
+    uint32_t c = 0;
+#pragma unroll 16
+    for (int y = 0; y < ERC; y++) {
+      const ulonglong2 k = ck[y];
+      c += (k.x < xts) | ((k.x == xts) & (k.y < xuid));
+    }
+    if (i < nev && c) atomicAdd(&D.erank[i], c);
+    __syncthreads();
+  }
+}
+__global__ __launch_bounds__(256) void k_wl_edigest(const WDev D, uint64_t K0, int keep) {
+  const uint32_t nev = D.cnt[0] < D.ev_cap ? D.cnt[0] : (uint32_t)D.ev_cap;
+  if (nev > ERANK_MAX) return;
+  uint64_t dg = 0;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nev; i += gridDim.x * 256) {
+    const uint32_t r = D.erank[i];
+    dg += digest_term(K0 + r, D.ev[i].ts, D.ev[i].uid);
+    if (!keep) D.erank[i] = 0;  // (kept: the host reads the ranks for its log, then clears them)
+  }
+  dg = wave_sum_u64(dg);
+  __shared__ uint64_t s_dg[4];
+  if ((threadIdx.x & 63) == 0) s_dg[threadIdx.x >> 6] = dg;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t b = s_dg[0] + s_dg[1] + s_dg[2] + s_dg[3];
+    if (b) atomicAdd(D.edig, (unsigned long long)b);
+  }
+}
+
 // SendPacket of phy s at (ts): the sender's state switch (thread s) and one Receive per receiver.
 __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t, double dbm, uint32_t base) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -630,6 +691,10 @@ struct nsgpu_wifil {
   std::vector<uint32_t> recv;  // fan-out uids of one SendPacket per phy
   uint64_t n_tx = 0, tx_cap = 0;
   uint32_t *h_cnt = nullptr;  // pinned: the epoch counters
+  unsigned long long *h_dig = nullptr;  // pinned: the epoch's digest sum
+  nsgpu_wifil_end *h_ends = nullptr;     // pinned: the epoch's first END_STAGE end records
+  LPhy *h_ps = nullptr;                  // pinned: one phy's state (nsgpu_wifil_get_state)
+  std::vector<uint32_t> erank;
   unsigned long long *d_pend = nullptr, *h_pend = nullptr;
   std::vector<LEv> ev;
   std::vector<nsgpu_wifil_end> ends, ends_epoch;
@@ -654,6 +719,9 @@ extern "C" int nsgpu_wifil_destroy(nsgpu_wifil *h) {
   }
   for (void *p : h->allocs) (void)hipFree(p);
   if (h->h_cnt) (void)hipHostFree(h->h_cnt);
+  if (h->h_dig) (void)hipHostFree(h->h_dig);
+  if (h->h_ends) (void)hipHostFree(h->h_ends);
+  if (h->h_ps) (void)hipHostFree(h->h_ps);
   if (h->h_pend) (void)hipHostFree(h->h_pend);
   delete h;
   return NSGPU_OK;
@@ -721,6 +789,8 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   WL_TRY(wl_alloc(h, &D.ends, sync_cap));
   WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
   WL_TRY(wl_alloc(h, &D.cnt, 4));
+  WL_TRY(wl_alloc(h, &D.erank, std::min<uint64_t>(ev_cap, ERANK_MAX)));
+  WL_TRY(wl_alloc(h, &D.edig, 1));
   WL_TRY(wl_alloc(h, &h->d_pend, 2));
 #undef WL_TRY
   D.sync_cap = sync_cap;
@@ -728,6 +798,9 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   D.end_cap = sync_cap;
   h->tx_cap = c->tx_cap;
   if (hipHostMalloc((void **)&h->h_cnt, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&h->h_dig, sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&h->h_ends, END_STAGE * sizeof(nsgpu_wifil_end), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&h->h_ps, sizeof(LPhy), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void **)&h->h_pend, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
       hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
     nsgpu_wifil_destroy(h);
@@ -765,9 +838,7 @@ extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base,
   const uint32_t k = (uint32_t)h->n_tx++;
   hipLaunchKernelGGL(k_wl_send, dim3((unsigned)((h->D.nphy + 255) / 256)), dim3(256), 0, h->s, h->D, k, t, dbm, uid_base);
   NSGPU_HIP(hipGetLastError());
-  NSGPU_HIP(hipMemcpyAsync(h->h_cnt, h->D.cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
-  NSGPU_HIP(hipStreamSynchronize(h->s));
-  return wl_check(h, "nsgpu_wifil_send");
+  return NSGPU_OK;  // (asynchronous: its error bits, if any, fail the next nsgpu_wifil_advance)
 }
 
 // Every device event with a key below (bound_ts, bound_uid) (~0: all of them): dispatched in (ts, uid) order
@@ -778,32 +849,68 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
                                    uint32_t *log_ctx, uint64_t log_cap) {
   if (!h || !uid || !dispatched || !digest) return set_error(NSGPU_EINVAL, "nsgpu_wifil_advance: null");
   WDev &D = h->D;
-  NSGPU_HIP(hipMemsetAsync(D.cnt, 0, 4 * sizeof(uint32_t), h->s));
+  NSGPU_HIP(hipMemsetAsync(D.cnt, 0, 3 * sizeof(uint32_t), h->s));  // (cnt[3]: sticky error bits)
+  NSGPU_HIP(hipMemsetAsync(D.edig, 0, sizeof(unsigned long long), h->s));
   hipLaunchKernelGGL(k_wl_step, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
   hipLaunchKernelGGL(k_wl_rank, dim3(64), dim3(256), 0, h->s, D, *uid);
   hipLaunchKernelGGL(k_wl_patch, dim3(256), dim3(256), 0, h->s, D);
+  const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
+  hipLaunchKernelGGL(k_wl_erank, dim3(1024), dim3(ERT), 0, h->s, D);
+  hipLaunchKernelGGL(k_wl_edigest, dim3(256), dim3(256), 0, h->s, D, *dispatched, logging ? 1 : 0);
   NSGPU_HIP(hipGetLastError());
+  // counters, the digest sum and the first end records in one trip
   NSGPU_HIP(hipMemcpyAsync(h->h_cnt, D.cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipMemcpyAsync(h->h_dig, D.edig, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipMemcpyAsync(h->h_ends, D.ends, END_STAGE * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipStreamSynchronize(h->s));
   int rc = wl_check(h, "nsgpu_wifil_advance");
   if (rc) return rc;
   const uint32_t nev = h->h_cnt[0], nsync = h->h_cnt[1], nend = h->h_cnt[2];
-  h->ev.resize(nev);
   h->ends_epoch.resize(nend);
-  if (nev) NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.ev, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
-  if (nend) NSGPU_HIP(hipMemcpyAsync(h->ends_epoch.data(), D.ends, nend * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
-  NSGPU_HIP(hipStreamSynchronize(h->s));
-  // the epoch's dispatch order: (ts, uid) over every phy's events (one lane per phy ran them in order)
-  std::sort(h->ev.begin(), h->ev.end(), [](const LEv &a, const LEv &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
-  for (const LEv &e : h->ev) {
-    const uint64_t rank = (*dispatched)++;
-    *digest += nsgpu_dispatch_digest_term(rank, e.ts, e.uid);
-    if (rank < log_cap && log_ts && log_uid && log_ctx) {
-      log_ts[rank] = e.ts;
-      log_uid[rank] = e.uid;
-      log_ctx[rank] = e.ctx;
-    }
+  if (nend > END_STAGE) {
+    NSGPU_HIP(hipMemcpyAsync(h->ends_epoch.data(), D.ends, nend * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
+  } else if (nend) {
+    std::copy(h->h_ends, h->h_ends + nend, h->ends_epoch.begin());
   }
+  if (nev > ERANK_MAX) {  // a large epoch: its order on the host
+    h->ev.resize(nev);
+    NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.ev, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
+    NSGPU_HIP(hipStreamSynchronize(h->s));
+    std::sort(h->ev.begin(), h->ev.end(), [](const LEv &a, const LEv &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
+    for (const LEv &e : h->ev) {
+      const uint64_t rank = (*dispatched)++;
+      *digest += nsgpu_dispatch_digest_term(rank, e.ts, e.uid);
+      if (rank < log_cap && log_ts && log_uid && log_ctx) {
+        log_ts[rank] = e.ts;
+        log_uid[rank] = e.uid;
+        log_ctx[rank] = e.ctx;
+      }
+    }
+  } else {
+    if (logging && nev) {  // the ranked events into the log (no host sort)
+      h->ev.resize(nev);
+      h->erank.resize(nev);
+      NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.ev, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
+      NSGPU_HIP(hipMemcpyAsync(h->erank.data(), D.erank, nev * sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
+      NSGPU_HIP(hipMemsetAsync(D.erank, 0, nev * sizeof(uint32_t), h->s));
+      NSGPU_HIP(hipStreamSynchronize(h->s));
+      for (uint32_t i = 0; i < nev; i++) {
+        const uint64_t rank = *dispatched + h->erank[i];
+        if (rank < log_cap) {
+          log_ts[rank] = h->ev[i].ts;
+          log_uid[rank] = h->ev[i].uid;
+          log_ctx[rank] = h->ev[i].ctx;
+        }
+      }
+    } else if (logging) {
+      // (nothing dispatched)
+    } else if (nend > END_STAGE) {
+      NSGPU_HIP(hipStreamSynchronize(h->s));
+    }
+    *digest += *h->h_dig;
+    *dispatched += nev;
+  }
+  if (nend > END_STAGE) NSGPU_HIP(hipStreamSynchronize(h->s));
   std::sort(h->ends_epoch.begin(), h->ends_epoch.end(),
             [](const nsgpu_wifil_end &a, const nsgpu_wifil_end &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
   h->ends.insert(h->ends.end(), h->ends_epoch.begin(), h->ends_epoch.end());
@@ -814,9 +921,9 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
 // WifiPhyStateHelper::GetState / GetDelayUntilIdle of `phy` at `now` (wifi-phy-state-helper.cc:122-183).
 extern "C" int nsgpu_wifil_get_state(nsgpu_wifil *h, uint32_t phy, uint64_t now, nsgpu_wifil_phy_state *out) {
   if (!h || !out || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_get_state: bad phy");
-  LPhy P;
-  NSGPU_HIP(hipMemcpyAsync(&P, h->D.ps + phy, sizeof(LPhy), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipMemcpyAsync(h->h_ps, h->D.ps + phy, sizeof(LPhy), hipMemcpyDeviceToHost, h->s));  // (pinned)
   NSGPU_HIP(hipStreamSynchronize(h->s));
+  const LPhy P = *h->h_ps;
   const int64_t nw = (int64_t)now;
   out->state = P.endTx > nw ? NSGPU_WIFIL_TX : P.rxing ? NSGPU_WIFIL_RX : P.endCca > nw ? NSGPU_WIFIL_CCA_BUSY : NSGPU_WIFIL_IDLE;
   out->rxing = P.rxing;
