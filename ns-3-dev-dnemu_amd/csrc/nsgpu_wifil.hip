@@ -290,6 +290,18 @@ __device__ __forceinline__ double snr_of(const WDev &D, double signal, double no
   return signal / noise;
 }
 
+// One index of counter *ctr per calling lane: the wave's active lanes share one atomic (every phy's lane
+// appending to the same epoch lists one atomic each serialized on the counter's line: ~11 ns apiece).
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t *ctr) {
+  const uint64_t m = __ballot(1);
+  const int lane = threadIdx.x & 63;
+  const int first = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == first) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+  base = __shfl(base, first);
+  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
 // ---- the NiChanges ring of one phy (RingNi of nsgpu_wifi.hip: time-sorted, eager prefix cursor) ----
 __device__ __forceinline__ void ni_insert(LNi *ring, uint32_t head, uint32_t &len, uint32_t m, int64_t t, double d) {
   uint32_t q = len;  // AddNiChangeEvent (interference-helper.cc:378-383): at upper_bound (time)
@@ -379,11 +391,18 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
         double psr = 1.0, noiseW = noise0;
         int64_t previous = t0;
         uint32_t q = 1;
+        LNi nb[NB];  // the ring read NB entries a trip (the walk itself stays one entry at a time)
+        uint32_t nbq = q - (uint32_t)NB;  // (q - nbq >= NB: the first entry loads a batch)
         for (bool last = false; !last;) {
           int64_t current;
           double delta;
           if (q < P.len) {
-            const LNi en = ring[(P.head + q) & m];
+            if (q - nbq >= (uint32_t)NB) {
+              nbq = q;
+#pragma unroll
+              for (int u = 0; u < NB; u++) nb[u] = ring[(P.head + q + u) & m];
+            }
+            const LNi en = nb[q - nbq];
             if (en.t == nw && eb.w == -en.d) {
               current = nw, delta = 0.0, last = true;  // (the event's end entry: the closing (end, 0))
             } else {
@@ -417,14 +436,14 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
         P.rxing = 0;  // NotifyRxEnd (); SwitchFromRxEndOk / Error -> DoSwitchFromRx (wifi-phy-state-helper.cc:391-402)
       }
       const uint32_t sl = eb.euid == NONE ? eb.sslot : NONE;
-      const uint32_t ei = atomicAdd(&D.cnt[2], 1u);
+      const uint32_t ei = wave_alloc(&D.cnt[2]);
       if (ei < D.end_cap) {
         D.ends[ei] = rec;
         D.end_sslot[ei] = sl;
       } else {
         err |= WE_CAP;
       }
-      const uint32_t vi = atomicAdd(&D.cnt[0], 1u);
+      const uint32_t vi = wave_alloc(&D.cnt[0]);
       if (vi < D.ev_cap) D.ev[vi] = LEv{eb.ts, eb.euid, ctx, sl, 0};
       else err |= WE_CAP;
       pe[e].used = 0;
@@ -471,7 +490,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
           q = k;
           break;
         }
-      const uint32_t sl = atomicAdd(&D.cnt[1], 1u);
+      const uint32_t sl = wave_alloc(&D.cnt[1]);
       if (q < 0 || sl >= D.sync_cap) {
         err |= q < 0 ? WE_PECAP : WE_CAP;
         break;
@@ -490,11 +509,22 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
       cursor_advance<false>(ring, P.head, P.len, m, nw, P.cur_n, P.cur_s);
       double noise = P.cur_s;
       int64_t end = nw;
-      for (uint32_t q = P.cur_n; q < P.len; q++) {
-        const LNi en = ring[(P.head + q) & m];
-        noise += en.d;
-        end = en.t;
-        if (noise < D.ccaW) break;
+      for (uint32_t q0 = P.cur_n; q0 < P.len; q0 += NB) {  // (NB entries a trip; the sums one at a time)
+        LNi en[NB];
+#pragma unroll
+        for (int u = 0; u < NB; u++) en[u] = ring[(P.head + q0 + u) & m];
+        bool stop = false;
+#pragma unroll
+        for (int u = 0; u < NB; u++) {
+          if (stop || q0 + u >= P.len) {
+            stop = true;
+            continue;
+          }
+          noise += en[u].d;
+          end = en[u].t;
+          if (noise < D.ccaW) stop = true;
+        }
+        if (stop) break;
       }
       const int64_t cca = end > nw ? end - nw : 0;
       if (cca != 0) {  // SwitchMaybeToCcaBusy (wifi-phy-state-helper.cc:404-423)
@@ -502,7 +532,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
         P.c.cca_switches++;
       }
     }
-    const uint32_t vi = atomicAdd(&D.cnt[0], 1u);
+    const uint32_t vi = wave_alloc(&D.cnt[0]);
     if (vi < D.ev_cap) D.ev[vi] = LEv{r.at, r.uid, ctx, NONE, 0};
     else err |= WE_CAP;
   }
