@@ -12,6 +12,8 @@ Workloads (--workload):
       on one GPU, whole simulation per step.
   wifi-grid: config 3 — 10,000 YansWifiPhys on a 100 x 100 grid, every phy broadcasting once a second,
       2 s: the whole SendPacket / Receive / EndReceive event chain on the device (nsgpu_wifi_run).
+  wifi-loop: config 3 with the MAC on the host — 10,000 phys on the device behind the host-closure runtime,
+      a MAC stand-in per phy sending when its PHY reports IDLE (nsgpu_wifil + nsgpu_sim), Stop 0.2 s.
   wifi-fanout: config 3's YansWifiChannel::Send receiver loop alone at 10,000 nodes, batched (receiver
       events/s; a measurement of the fan-out kernel).
   churn: config 1, utils/bench-simulator.cc — 10,000 pending, U[0,1) s delays, 5e6 holds,
@@ -411,8 +413,109 @@ class WifiGrid:
             f"passes timed: {secs:.2f} s); digest_match = that sample's GPU run has the oracle's digest and count")
 
 
+class WifiLoop:
+    """Config 3 as ns-3 runs it: the MAC on the host, the PHYs on the device (nsgpu_wifil behind the
+    host-closure runtime nsgpu_sim).  100 x 100 phys, 100 m, YansWifiPhy / channel defaults, NIST error
+    model; a MAC stand-in per phy (the same one tests/wifi_loop_harness.py and the oracle's
+    nsref_wifil_mac run): an attempt reads the PHY state (WifiPhyStateHelper::GetState), sends a 1000-B
+    DSSS 1 Mb/s frame when IDLE and tries again a period later, else backs off; first attempts from a
+    seeded random phase in [0, 0.5 s), period 1 s, Stop at --wifi-loop-stop s.  One step = the whole run
+    (host closures and device events in one (ts, uid) order; each EndReceive's (snr, per) back to the
+    host).  Bytes per event: the fan-out's 64 B per receiver; the step's kernels are launched per host
+    event on the PHY's own stream, so the roofline uses the step's wall time."""
+    bytes_per_event = 64
+    kernel = "nsgpu::k_wl_step"
+
+    def __init__(self, args, stream):
+        import numpy as np
+        import wifi
+        self.np, self.wifi = np, wifi
+        self.side, self.stop = args.wifi_side, args.wifi_loop_stop
+        self.sc = self.scenario(self.stop)
+        self.workload = (f"wifi-simple-adhoc-grid scaled to {self.side * self.side} nodes (config 3) with the MAC on the "
+                         f"host: {self.side}x{self.side} grid 100 m, LogDistance(3, 46.6777)+ConstantSpeed, NIST error "
+                         f"model; per phy a MAC stand-in sending 1000-B DSSS 1Mb/s frames when the PHY is IDLE (else "
+                         f"backing off), period 1 s from seeded phases, Stop {self.stop}s; PHYs on the GPU "
+                         f"(nsgpu_wifil), closures on the host (nsgpu_sim)")
+        self._last = None
+
+    def scenario(self, stop_s):
+        x, y, z = self.wifi.grid(self.side, 100.0)
+        phys = self.wifi.LoopPhys(x, y, z, tx_cap=1 << 20, rxq_cap=1024, ni_cap=1024)
+        rng = self.np.random.default_rng(11)
+        n, period = phys.n_phy, 1_000_000_000
+        return dict(phys=phys, first=rng.integers(0, period // 2, n).astype(self.np.uint64),
+                    backoff=(100_000 + 37_000 * self.np.arange(n)).astype(self.np.uint64), period=period,
+                    stop_ns=int(stop_s * 1e9), size=1000, mode=self.wifi.DSSS_1M, preamble=self.wifi.PREAMBLE_LONG,
+                    dbm=16.0206 + 1.0)
+
+    def run(self, sc):
+        import nsgpu
+        wifi = self.wifi
+        sim = nsgpu.Sim()
+        lp = wifi.LoopPhy(sc["phys"])
+        sim.attach_wifi(lp)
+        cnt = [0, 0]
+
+        def attempt(i):
+            st, _ = sim.wifi_state(i)
+            if st != wifi.IDLE:
+                cnt[1] += 1
+                sim.schedule(int(sc["backoff"][i]), lambda: attempt(i))
+                return
+            sim.wifi_send(i, sc["size"], sc["dbm"], sc["mode"], sc["preamble"])
+            cnt[0] += 1
+            sim.schedule(sc["period"], lambda: attempt(i))
+
+        for i in range(sc["phys"].n_phy):
+            sim.schedule(int(sc["first"][i]), (lambda i=i: lambda: attempt(i))())
+        sim.stop(sc["stop_ns"])
+        sim.run()
+        _n, _c, digest = sim.host_stats()
+        ends = lp.read_ends()
+        res = (int(sim.dispatched()), int(digest), {"sends": cnt[0], "busy_attempts": cnt[1],
+                                                   "end_receives": int(len(ends)), "next_uid": int(sim.next_uid())})
+        lp.close()
+        return res
+
+    def step(self):
+        self._last = self.run(self.sc)
+
+    def close(self):
+        pass
+
+    def roofline(self, step_kernel_ms, events_per_step):
+        return {"kernel": self.kernel + " (whole closed-loop run)", "kernel_ms": step_kernel_ms, "events_per_launch":
+                events_per_step, "launch_unit": "one whole run: k_wl_step / k_wl_rank / k_wl_patch / k_wl_erank / "
+                "k_wl_edigest per host event, k_wl_send per SendPacket"}
+
+    def result(self):
+        return self._last
+
+    def cpu_baseline(self):
+        import time
+        nsref = oracle()
+        wifi = self.wifi
+        sample_stop = min(self.stop, 0.05)
+        sc = self.scenario(sample_stop)
+        ph = sc["phys"]
+        t0 = time.perf_counter()
+        _log, _ends, _phys, tot = nsref.wifil_run(ph.c_struct(), sc["first"], sc["backoff"], sc["period"],
+                                                  sc["stop_ns"], sc["size"], sc["mode"], sc["preamble"], sc["dbm"],
+                                                  ph.n_phy, wifi.WIFIL_END_DTYPE, wifi.PHY_COUNTERS_DTYPE, 1)
+        secs = time.perf_counter() - t0
+        g = self.run(sc)
+        self._sample_match = g[0] == tot["dispatched"] and g[1] == tot["digest"]
+        return tot["dispatched"] / secs, "sample", (
+            f"the same workload cut at Stop {sample_stop}s ({tot['dispatched']} dispatches) through the oracle's "
+            f"sequential restatement of the closed loop (nsref_wifil_run: the MAC stand-in, DefaultSimulatorImpl "
+            f"order, YansWifiChannel::Send, StartReceivePacket / InterferenceHelper / CalculateSnrPer, g++ -O2, one "
+            f"core, {secs:.2f} s wall incl. its setup); digest_match = that sample's GPU run has the oracle's "
+            f"digest and count")
+
+
 WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid, "dumbbell": P2PDumbbell, "wifi-fanout": WifiFanout,
-             "wifi-grid": WifiGrid}
+             "wifi-grid": WifiGrid, "wifi-loop": WifiLoop}
 
 
 def main():
@@ -427,6 +530,7 @@ def main():
     ap.add_argument("--fanout-tx", type=int, default=1024, help="wifi-fanout: transmissions per step")
     ap.add_argument("--wifi-side", type=int, default=100, help="wifi-grid: phys per grid side")
     ap.add_argument("--wifi-stop", type=float, default=2.0, help="wifi-grid: Simulator::Stop (s)")
+    ap.add_argument("--wifi-loop-stop", type=float, default=0.2, help="wifi-loop: Simulator::Stop (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="p2p-grid: skip the wifi-grid / dumbbell entries of the `secondary` list")
@@ -545,7 +649,7 @@ def main():
         # whole run per step, digest-checked against the oracle like the primary
         secondary = []
         if world == 1 and not partitioned and args.workload == "p2p-grid" and not args.no_secondary:
-            for name in ("wifi-grid", "dumbbell"):
+            for name in ("wifi-grid", "wifi-loop", "dumbbell"):
                 wl2 = WORKLOADS[name](args, stream.handle)
                 el2, kms2 = measure(wl2, args.secondary_steps, 1)
                 ev2, dg2, ex2 = wl2.result()

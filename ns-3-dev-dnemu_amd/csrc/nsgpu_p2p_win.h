@@ -1755,6 +1755,7 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
     BLK_MARK(54, c_win);
   }
 #ifdef NSGPU_PHASE_PROF
+  if (n_tie) atomicAdd((unsigned long long *)&g_phase[61], (unsigned long long)n_tie);  // (every window)
   if (c_win == g_blk_win) {
     if (n_tie) atomicAdd((unsigned long long *)&g_phase[56], (unsigned long long)n_tie);
     if (threadIdx.x == 0) atomicAdd((unsigned long long *)&g_phase[59], 1ull);

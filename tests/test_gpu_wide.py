@@ -49,6 +49,17 @@ def test_config4_shape_wide_has_fewer_windows():
     assert gst.windows < nst.windows * 0.6, (gst.windows, nst.windows)
 
 
+def test_lockstep_deep_chains_tie_break():
+    """Two identical rows, each saturated by a flow along it (20 Mb/s offered to 10 Mb/s links): the sources'
+    TransmitComplete chains run up to 3 deep inside each window, in lockstep across the rows, so local records
+    of one ts whose parents and grandparents share their ts meet — their two order words tie and k2_rank falls
+    back to the exact chain compare (the gen-0 ancestors' uids decide)."""
+    cols = 8
+    sc = p2p.grid(2, cols, flows=[(0, cols - 1), (cols, 2 * cols - 1)], rate_bps=20_000_000, qmax=100,
+                  stop_ns=160_000_000, sim_stop_ns=180_000_000)
+    check_wide_and_narrow(sc, 400_000, 2_000_000)
+
+
 def test_congested_grid_transmit_complete_chains():
     """Every node of the top row sends 2 Mb/s to one bottom corner: the corner's column links saturate, the
     queues back up and drop, and TransmitComplete chains (a local record's TransmitStart making the next
