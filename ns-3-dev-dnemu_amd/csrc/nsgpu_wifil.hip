@@ -304,12 +304,24 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t *ctr) {
 
 // ---- the NiChanges ring of one phy (RingNi of nsgpu_wifi.hip: time-sorted, eager prefix cursor) ----
 __device__ __forceinline__ void ni_insert(LNi *ring, uint32_t head, uint32_t &len, uint32_t m, int64_t t, double d) {
-  uint32_t q = len;  // AddNiChangeEvent (interference-helper.cc:378-383): at upper_bound (time)
+  // AddNiChangeEvent (interference-helper.cc:378-383): at upper_bound (time).  The entries after it (a
+  // start while receiving passes every pending end: ~100 of them) move up one place, read NB at a time
+  // from the tail (one memory trip per NB, not per entry)
+  uint32_t q = len;
   while (q > 0) {
-    const LNi e = ring[(head + q - 1) & m];
-    if (e.t <= t) break;
-    ring[(head + q) & m] = e;
-    q--;
+    const uint32_t nb = q < (uint32_t)NB ? q : (uint32_t)NB;
+    LNi e[NB];
+#pragma unroll
+    for (int u = 0; u < NB; u++) e[u] = ring[(head + q - 1 - u) & m];  // (past the head: masked, unused)
+    uint32_t k = 0;  // the batch's entries after t: a run from the tail
+#pragma unroll
+    for (int u = 0; u < NB; u++)
+      if ((uint32_t)u < nb && k == (uint32_t)u && e[u].t > t) k++;
+#pragma unroll
+    for (int u = 0; u < NB; u++)
+      if ((uint32_t)u < k) ring[(head + q - u) & m] = e[u];
+    q -= k;
+    if (k < nb) break;
   }
   ring[(head + q) & m] = LNi{t, d};
   len++;
@@ -341,9 +353,19 @@ __device__ __forceinline__ bool pe_before(const LPe &a, const LPe &b) {
 }
 
 // One phy's events of the epoch: every pending Receive / EndReceive with a key below (bts, buid).
+#ifdef NSGPU_PHASE_PROF
+// diagnostic build: [0] sum over epochs of the slowest lane's time, [1] sum of lane times, [2] lanes, [3] events,
+// [4] sum over epochs of the most events one lane ran, [5] epochs, [6] max lane time, [7] its events
+__device__ unsigned long long g_wl_ph[8];
+__device__ unsigned long long g_wl_ep[2];  // the current epoch's slowest lane time / most events (reset by host)
+#endif
 __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint32_t buid) {
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (j >= D.nphy) return;
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t pt0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t pev = 0;
+#endif
   LPhy P = D.ps[j];
   LNi *ring = D.ni + (uint64_t)j * (D.ni_mask + 1);
   LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
@@ -448,6 +470,9 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
       else err |= WE_CAP;
       pe[e].used = 0;
       if (P.live == (uint32_t)e) P.live = NONE;
+#ifdef NSGPU_PHASE_PROF
+      pev++;
+#endif
       continue;
     }
     // ---- YansWifiChannel::Receive -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496)
@@ -535,10 +560,33 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
     const uint32_t vi = wave_alloc(&D.cnt[0]);
     if (vi < D.ev_cap) D.ev[vi] = LEv{r.at, r.uid, ctx, NONE, 0};
     else err |= WE_CAP;
+#ifdef NSGPU_PHASE_PROF
+    pev++;
+#endif
   }
   D.ps[j] = P;
   if (err) atomicOr(&D.cnt[3], err);
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t dt = __builtin_amdgcn_s_memrealtime() - pt0;
+  atomicAdd(&g_wl_ph[1], (unsigned long long)dt);
+  atomicAdd(&g_wl_ph[2], 1ull);
+  atomicAdd(&g_wl_ph[3], (unsigned long long)pev);
+  atomicMax(&g_wl_ep[0], (unsigned long long)dt);
+  atomicMax(&g_wl_ep[1], (unsigned long long)pev);
+  if (dt > g_wl_ph[6]) {
+    g_wl_ph[6] = dt;
+    g_wl_ph[7] = pev;
+  }
+#endif
 }
+#ifdef NSGPU_PHASE_PROF
+__global__ void k_wl_prof_epoch() {  // (one thread: fold the epoch's maxima, reset them)
+  g_wl_ph[0] += g_wl_ep[0];
+  g_wl_ph[4] += g_wl_ep[1];
+  g_wl_ph[5] += 1;
+  g_wl_ep[0] = g_wl_ep[1] = 0;
+}
+#endif
 
 // The epoch's syncs in dispatch order (ts, uid of the syncing Receive): EndReceive uid = uid0 + rank.
 __global__ __launch_bounds__(256) void k_wl_rank(const WDev D, uint32_t uid0) {
@@ -882,6 +930,9 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   NSGPU_HIP(hipMemsetAsync(D.cnt, 0, 3 * sizeof(uint32_t), h->s));  // (cnt[3]: sticky error bits)
   NSGPU_HIP(hipMemsetAsync(D.edig, 0, sizeof(unsigned long long), h->s));
   hipLaunchKernelGGL(k_wl_step, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
+#ifdef NSGPU_PHASE_PROF
+  hipLaunchKernelGGL(k_wl_prof_epoch, dim3(1), dim3(1), 0, h->s);
+#endif
   hipLaunchKernelGGL(k_wl_rank, dim3(64), dim3(256), 0, h->s, D, *uid);
   hipLaunchKernelGGL(k_wl_patch, dim3(256), dim3(256), 0, h->s, D);
   const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
@@ -1012,3 +1063,14 @@ extern "C" int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_t
   *next_ts = h->h_pend[1];
   return NSGPU_OK;
 }
+
+#ifdef NSGPU_PHASE_PROF
+// (diagnostic build only) the k_wl_step counters above, reset after the read
+extern "C" int nsgpu_wifil_prof_read(unsigned long long *out) {
+  NSGPU_HIP(hipDeviceSynchronize());
+  NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wl_ph), sizeof(unsigned long long) * 8));
+  unsigned long long z[8] = {};
+  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wl_ph), z, sizeof(z)));
+  return NSGPU_OK;
+}
+#endif
