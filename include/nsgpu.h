@@ -155,8 +155,12 @@ int nsgpu_wifi_destroy(nsgpu_wifi *h);
  * Independently, the receptions (arrival, rxPowerW of every receiver x transmission pair: the fan-out
  * arithmetic) are computed up front into an HBM table by one parallel kernel when n_phy x transmissions
  * x 16 B fits half of the free HBM at create; | NSGPU_WIFI_INLINE_RX computes them inside the per-phy
- * kernel instead (same values: the same expressions).
- * nsgpu_wifi_get_store reports the store the next run uses (| NSGPU_WIFI_INLINE_RX without the table),
+ * kernel instead (same values: the same expressions).  When every transmission's arrivals can interleave
+ * with at most 64 others' (arrivals lie within the grid's largest propagation delay of the send) and the
+ * table fits twice more (32 B a pair), each phy's row is also put in dispatch order (arrival, uid) so the
+ * per-phy chain reads its next Receive sequentially; | NSGPU_WIFI_UNSORTED_RX scans the unsorted row.
+ * nsgpu_wifi_get_store reports the store the next run uses (| NSGPU_WIFI_INLINE_RX without the table,
+ * | NSGPU_WIFI_UNSORTED_RX with the table but unsorted rows),
  * its phys per block and the end-queue (LDS) or ring (HBM) capacity. */
 int nsgpu_wifi_set_store(nsgpu_wifi *h, int store);
 int nsgpu_wifi_get_store(nsgpu_wifi *h, int *store, uint32_t *phys_per_block, uint32_t *e_cap);

@@ -262,7 +262,7 @@ NSGPU_HD static inline uint64_t nsgpu_dispatch_digest_term(uint64_t rank, uint64
  * (SURVEY H13).  Channel switching is not modelled (no SWITCHING state). */
 enum nsgpu_wifi_modclass { NSGPU_WIFI_DSSS = 0, NSGPU_WIFI_OFDM = 1, NSGPU_WIFI_ERP_OFDM = 2 };
 enum nsgpu_wifi_store { NSGPU_WIFI_STORE_AUTO = 0, NSGPU_WIFI_STORE_LDS = 1, NSGPU_WIFI_STORE_HBM = 2,
-                        NSGPU_WIFI_STORE_MASK = 3, NSGPU_WIFI_INLINE_RX = 4 };
+                        NSGPU_WIFI_STORE_MASK = 3, NSGPU_WIFI_INLINE_RX = 4, NSGPU_WIFI_UNSORTED_RX = 8 };
 enum nsgpu_wifi_preamble { NSGPU_WIFI_PREAMBLE_LONG = 0, NSGPU_WIFI_PREAMBLE_SHORT = 1 };
 
 typedef struct nsgpu_wifi_scenario {

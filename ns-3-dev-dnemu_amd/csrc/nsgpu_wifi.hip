@@ -130,6 +130,8 @@ struct WifiDev {
   nsgpu_wifi_end_record *ends;
   struct RxPre *pre;  // nullable: [nphy][ktx] receptions computed up front (k_wifi_rx)
   const struct TsDur *tsdur;  // [ktx] (ts, dur) of every transmission, packed for the per-phy scan
+  struct RxS *srt;            // nullable: [nphy][ktx] each row of `pre` in (arrival, transmission) order
+  const uint32_t *wlo, *whi;  // [ktx] the transmissions whose arrivals can interleave with k's (sorted rows)
 };
 
 // One (receiver, transmission) pair computed up front by k_wifi_rx: the Receive's arrival and its
@@ -144,6 +146,15 @@ struct TsDur {  // a TxDesc's (ts, dur) half-line
   int64_t dur;
 };
 static_assert(offsetof(TxDesc, dur) == offsetof(TxDesc, ts) + 8 && offsetof(TxDesc, ts) % 16 == 0, "TsDur view");
+// One entry of a sorted reception row (k_wifi_rx_sort): a phy's Receives in their dispatch order — (arrival,
+// then uid, i.e. transmission index) — with the markers of `pre` kept at their transmission's ts.
+struct RxS {
+  uint64_t at;   // arrival, or PRE_OWN / PRE_NONE
+  double w;      // rxPowerW
+  uint64_t tts;  // the transmission's ts
+  uint32_t k;    // the transmission
+  uint32_t dur;  // its duration (ns; < 2^32, checked at create)
+};
 
 // ConstantSpeedPropagationDelayModel::GetDelay + DefaultSimulatorImpl::ScheduleWithContext's m_currentTs +
 __device__ __forceinline__ uint64_t arrival(const WifiDev &D, uint32_t k, double px, double py, double pz,
@@ -507,15 +518,39 @@ __global__ __launch_bounds__(256) void k_wifi_rx(const WifiDev D) {
   }
 }
 
+// Each reception row in dispatch order: entry (j, k) goes to position #{k' : (a', k') < (a, k)} of row j, where
+// a is the arrival (a marker: its transmission's ts).  Every arrival lies in [ts, ts + dmax], so transmissions
+// before wlo[k] (ts' + dmax < ts) all come first and those after whi[k] (ts' > ts + dmax) all come later: only
+// the window [wlo[k], whi[k]] (at most WSORT_MAX, host-checked) is compared.
+__global__ __launch_bounds__(256) void k_wifi_rx_sort(const WifiDev D) {
+  const uint64_t K = D.ktx, n = (uint64_t)D.nphy * K;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t j = i / K, k = i - j * K;
+    const RxPre *row = D.pre + j * K;
+    const RxPre r = row[k];
+    const TsDur td = D.tsdur[k];
+    const uint64_t a = r.at >= PRE_OWN ? td.ts : r.at;
+    const uint32_t lo = D.wlo[k], hi = D.whi[k];
+    uint32_t pos = lo;
+    for (uint32_t q = lo; q <= hi; q++) {
+      const uint64_t b = row[q].at;
+      const uint64_t bq = b >= PRE_OWN ? D.tsdur[q].ts : b;
+      pos += (bq < a || (bq == a && q < k)) ? 1u : 0u;
+    }
+    D.srt[j * K + pos] = RxS{r.at, r.w, td.ts, (uint32_t)k, (uint32_t)td.dur};
+  }
+}
+
 // A phy's pending EndReceive events (the live one + cancelled ones), one record per lane in LDS.
 struct PeSlots {
   uint64_t ts[PE_CAP], sts[PE_CAP];
   uint32_t tx[PE_CAP], slot[PE_CAP], can[PE_CAP];
 };
 
-// One lane = one phy: its SendPacket / Receive / EndReceive sequence in (ts, uid) order.  PRE: the
-// receptions come from k_wifi_rx's table.
-template <bool PRE, class Ni>
+// One lane = one phy: its SendPacket / Receive / EndReceive sequence in (ts, uid) order.  MODE 0: receptions
+// computed here; 1: read from k_wifi_rx's table (each scan looks at the unconsumed transmissions in order);
+// 2: read in order from the sorted row (k_wifi_rx_sort), the next entry prefetched while an event runs.
+template <int MODE, class Ni>
 __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &ni, PeSlots *pe) {
   const double px = D.x[j], py = D.y[j], pz = D.z[j];
   const uint32_t ch = D.chan[j];
@@ -539,6 +574,11 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
   const uint32_t oe = D.own_off[j + 1];
   uint32_t ok = oc < oe ? D.own_idx[oc] : NONE;
   uint64_t ok_ts = ok != NONE ? D.txd[ok].ts : INF;
+  // MODE 2: sr = the row's next unconsumed entry, nx = that entry (loaded one event ahead)
+  const RxS *srow = MODE == 2 ? D.srt + (uint64_t)j * D.ktx : nullptr;
+  uint32_t sr = 0;
+  RxS nx{};
+  if (MODE == 2 && D.ktx) nx = srow[0];
   bool have_c = false;
   uint64_t c_ts = INF, c_tts = 0;
   uint32_t c_k = NONE;
@@ -554,7 +594,21 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
       c_ts = INF;
       c_k = NONE;
       uint32_t at = 64;  // where the scan stopped (64: it went through the whole window)
-      if (PRE) {
+      if (MODE == 2) {
+        for (;;) {
+          if (sr >= D.ktx) break;
+          const RxS r = nx;
+          if (r.at >= PRE_OWN) {  // our own SendPacket (taken from the own list) / another channel: no Receive
+            sr++;
+            if (sr < D.ktx) nx = srow[sr];
+            continue;
+          }
+          c_ts = r.at, c_k = r.k, c_w = r.w, c_tts = r.tts, c_dur = (int64_t)r.dur;
+          if (sr + 1 < D.ktx) nx = srow[sr + 1];  // (in flight while this Receive runs)
+          break;
+        }
+        at = 0;
+      } else if (MODE == 1) {
         const RxPre *row = D.pre + (uint64_t)j * D.ktx;
         for (uint32_t i0 = 0; i0 < 64 && at == 64; i0 += 2) {
           TsDur tp[2];  // two transmissions per memory trip (a scan usually reads the next two)
@@ -617,11 +671,13 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
         }
       }
       }
-      if (at == 64 && p + 64 < D.ktx && D.txd[p + 64].ts < c_ts) {
-        err |= ERR_WINDOW;
-        break;
+      if (MODE != 2) {
+        if (at == 64 && p + 64 < D.ktx && D.txd[p + 64].ts < c_ts) {
+          err |= ERR_WINDOW;
+          break;
+        }
+        while (done & 1ull) done >>= 1, p++;
       }
-      while (done & 1ull) done >>= 1, p++;
       have_c = true;
     }
     WPH(9);  // the scan for the next Receive (selection: the rest)
@@ -657,12 +713,14 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
         endRx = nw;
       }
       endTx = nw + D.txd[ok].dur;
-      if (ok - p >= 64) {
-        err |= ERR_WINDOW;
-        break;
+      if (MODE != 2) {
+        if (ok - p >= 64) {
+          err |= ERR_WINDOW;
+          break;
+        }
+        done |= 1ull << (ok - p);
+        while (done & 1ull) done >>= 1, p++;
       }
-      done |= 1ull << (ok - p);
-      while (done & 1ull) done >>= 1, p++;
       oc++;
       ok = oc < oe ? D.own_idx[oc] : NONE;
       ok_ts = ok != NONE ? D.txd[ok].ts : INF;
@@ -702,7 +760,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
 
     // YansWifiChannel::Receive -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496)
     const uint32_t k = c_k;
-    const double rxPowerW = PRE ? c_w : rx_power_w(D, c_dbm, c_dist);
+    const double rxPowerW = MODE != 0 ? c_w : rx_power_w(D, c_dbm, c_dist);
     const int64_t endNew = nw + c_dur;
     // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
     WPH(6);  // (kind decision, Receive operands)
@@ -782,8 +840,12 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
       l->flags = (uint8_t)flags;
       l->cca_ns = cca;
     }
-    done |= 1ull << (k - p);
-    while (done & 1ull) done >>= 1, p++;
+    if (MODE == 2) {
+      sr++;
+    } else {
+      done |= 1ull << (k - p);
+      while (done & 1ull) done >>= 1, p++;
+    }
     have_c = false;
     disp++;
     last_ts = now;
@@ -830,13 +892,13 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
 }
 
 // HBM ring store: 64 phys per block.
-template <bool PRE>
+template <int MODE>
 __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (j >= D.nphy) return;
   __shared__ PeSlots pes[64];
   RingNi ni{D.ni + (uint64_t)j * (D.ni_mask + 1), D.ni_mask, 0, 0, 0, 0.0};
-  phy_run<PRE>(D, j, ni, &pes[threadIdx.x]);
+  phy_run<MODE>(D, j, ni, &pes[threadIdx.x]);
 }
 
 // LDS split store: blockDim.x phys per block, each with its S ring (scap entries), E ring (ecap) and
@@ -844,7 +906,7 @@ __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
 __host__ __device__ constexpr size_t wifi_lds_per_phy(uint32_t scap, uint32_t ecap) {
   return (size_t)(scap + ecap) * 16 + (size_t)ecap * 8 + sizeof(PeSlots);
 }
-template <bool PRE>
+template <int MODE>
 __global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t scap, uint32_t ecap) {
   extern __shared__ uint64_t wlds[];
   const uint32_t P = blockDim.x, l = threadIdx.x;
@@ -857,7 +919,7 @@ __global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t s
              reinterpret_cast<double *>(b + 3 * ecap + scap), reinterpret_cast<double *>(b + ecap),
              reinterpret_cast<double *>(b + 2 * ecap), scap, ecap, D.ni_mask + 1, 0, 0, 0, 0, 0, 0.0, 0.0, 0,
              INT64_MAX, INT64_MAX, 0.0, 0.0, 0.0, INT64_MIN, 0.0};
-  phy_run<PRE>(D, j, ni, pe);
+  phy_run<MODE>(D, j, ni, pe);
 }
 
 // Syncs per bucket m = #transmissions with t_T <= ts (binary search over the schedule).
@@ -1003,7 +1065,10 @@ struct nsgpu_wifi {
   uint32_t lds_P = 0, lds_pmax = 0, lds_scap = 0, lds_ecap = 0;
   size_t lds_bytes = 0;
   bool use_pre = false;  // the run reads its receptions from D.pre (allocated when the table fits HBM)
+  bool use_sorted = false;  // ... in dispatch order from D.srt (allocated beside D.pre when the windows are short)
 };
+
+constexpr uint32_t WSORT_MAX = 64;  // the longest interleaving window k_wifi_rx_sort compares
 
 constexpr uint32_t SCAP_LDS = 8;  // S: starts at one instant (more: ERR_LDS, the run repeats on the ring)
 
@@ -1107,8 +1172,19 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   // i.e. to transmissions whose [ts, ts + max delay + duration] interval covers that instant: the largest
   // such overlap over the schedule bounds it (closed intervals; the sweep visits every start)
   uint32_t overlap = 0;
+  // the interleaving windows of the sorted reception rows: wlo[k] = the first k' with ts' + dmax >= ts_k,
+  // whi[k] = the last k' with ts' <= ts_k + dmax (arrivals lie in [ts, ts + dmax])
+  std::vector<uint32_t> wlo(std::max<uint32_t>(ktx, 1)), whi(std::max<uint32_t>(ktx, 1));
+  bool sortable = ktx > 0;
   if (ktx) {
     const int64_t dmax = (int64_t)ceil(diag / sc->speed * 1e9) + 2;
+    for (uint32_t k = 0, lo = 0, hi = 0; k < ktx; k++) {
+      while ((int64_t)sc->tx_ts[lo] + dmax < (int64_t)sc->tx_ts[k]) lo++;
+      if (hi < k) hi = k;
+      while (hi + 1 < ktx && (int64_t)sc->tx_ts[hi + 1] <= (int64_t)sc->tx_ts[k] + dmax) hi++;
+      wlo[k] = lo, whi[k] = hi;
+      if (hi - lo + 1 > WSORT_MAX || tx_dur[k] < 0 || tx_dur[k] > (int64_t)0xffffffffll) sortable = false;
+    }
     std::vector<int64_t> ends(ktx);
     for (uint32_t k = 0; k < ktx; k++) ends[k] = (int64_t)sc->tx_ts[k] + dmax + tx_dur[k];
     std::sort(ends.begin(), ends.end());
@@ -1204,6 +1280,8 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   TRY(dalloc(h, (uint64_t **)&D.fcum, fcum.size(), fcum.data()));
   TRY(dalloc(h, (uint32_t **)&D.own_off, own_off.size(), own_off.data()));
   TRY(dalloc(h, (uint32_t **)&D.own_idx, own_idx.size(), own_idx.data()));
+  TRY(dalloc(h, (uint32_t **)&D.wlo, wlo.size(), wlo.data()));
+  TRY(dalloc(h, (uint32_t **)&D.whi, whi.size(), whi.data()));
   TRY(dalloc(h, &D.ni, (size_t)N * cap));
   TRY(dalloc(h, &D.sync, sync_cap));
   TRY(dalloc(h, &D.n_sync, 1));
@@ -1220,11 +1298,16 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   TRY(dalloc(h, &D.ends, sync_cap));
   {  // the reception table (k_wifi_rx): n_phy x dispatched transmissions x 16 B, when half of free HBM holds it
     size_t fr = 0, tot = 0;
-    const uint64_t bytes = (uint64_t)N * ktx * sizeof(RxPre);
+    const uint64_t bytes = (uint64_t)N * ktx * sizeof(RxPre), sbytes = (uint64_t)N * ktx * sizeof(RxS);
     D.pre = nullptr;
+    D.srt = nullptr;
     if (ktx && hipMemGetInfo(&fr, &tot) == hipSuccess && bytes <= fr / 2) {
       TRY(dalloc(h, &D.pre, (size_t)N * ktx));
       h->use_pre = true;
+      if (sortable && bytes + sbytes <= fr / 2) {  // and its rows in dispatch order
+        TRY(dalloc(h, &D.srt, (size_t)N * ktx));
+        h->use_sorted = true;
+      }
     }
   }
 #undef TRY
@@ -1250,22 +1333,29 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
   if (ev) NSGPU_HIP(hipEventRecord(ev[0], s));
   WifiDev Dk = D;
   if (!h->use_pre) Dk.pre = nullptr;
+  if (!h->use_pre || !h->use_sorted) Dk.srt = nullptr;
+  const int mode = Dk.srt ? 2 : Dk.pre ? 1 : 0;
   if (Dk.pre) {
     const uint64_t n = (uint64_t)D.nphy * D.ktx;
-    if (n) hipLaunchKernelGGL(k_wifi_rx, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 16384)), dim3(256), 0, s, Dk);
+    const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 16384);
+    if (n) hipLaunchKernelGGL(k_wifi_rx, dim3(g), dim3(256), 0, s, Dk);
+    if (n && Dk.srt) hipLaunchKernelGGL(k_wifi_rx_sort, dim3(g), dim3(256), 0, s, Dk);
   }
   if (ev) NSGPU_HIP(hipEventRecord(ev[1], s));
   if (h->use_lds) {
-    const void *kf = Dk.pre ? (const void *)k_wifi_phy_lds<true> : (const void *)k_wifi_phy_lds<false>;
+    const void *kf = mode == 2 ? (const void *)k_wifi_phy_lds<2> : mode == 1 ? (const void *)k_wifi_phy_lds<1>
+                                                                             : (const void *)k_wifi_phy_lds<0>;
     if (h->lds_bytes > 65536)
       NSGPU_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes));
     const dim3 g((unsigned)((D.nphy + h->lds_P - 1) / h->lds_P)), b(h->lds_P);
-    if (Dk.pre) hipLaunchKernelGGL(k_wifi_phy_lds<true>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
-    else hipLaunchKernelGGL(k_wifi_phy_lds<false>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
+    if (mode == 2) hipLaunchKernelGGL(k_wifi_phy_lds<2>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
+    else if (mode == 1) hipLaunchKernelGGL(k_wifi_phy_lds<1>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
+    else hipLaunchKernelGGL(k_wifi_phy_lds<0>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
   } else {
     const dim3 g((unsigned)((D.nphy + 63) / 64)), b(64);
-    if (Dk.pre) hipLaunchKernelGGL(k_wifi_phy<true>, g, b, 0, s, Dk);
-    else hipLaunchKernelGGL(k_wifi_phy<false>, g, b, 0, s, Dk);
+    if (mode == 2) hipLaunchKernelGGL(k_wifi_phy<2>, g, b, 0, s, Dk);
+    else if (mode == 1) hipLaunchKernelGGL(k_wifi_phy<1>, g, b, 0, s, Dk);
+    else hipLaunchKernelGGL(k_wifi_phy<0>, g, b, 0, s, Dk);
   }
   if (ev) NSGPU_HIP(hipEventRecord(ev[2], s));
   hipLaunchKernelGGL(k_sync_hist, dim3(1024), dim3(256), 0, s, D);
@@ -1285,8 +1375,10 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
 
 extern "C" int nsgpu_wifi_set_store(nsgpu_wifi *h, int store) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: null");
-  if (store & ~(NSGPU_WIFI_STORE_MASK | NSGPU_WIFI_INLINE_RX)) return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: store %d", store);
+  if (store & ~(NSGPU_WIFI_STORE_MASK | NSGPU_WIFI_INLINE_RX | NSGPU_WIFI_UNSORTED_RX))
+    return set_error(NSGPU_EINVAL, "nsgpu_wifi_set_store: store %d", store);
   h->use_pre = h->D.pre != nullptr && !(store & NSGPU_WIFI_INLINE_RX);
+  h->use_sorted = h->D.srt != nullptr && !(store & NSGPU_WIFI_UNSORTED_RX);
   store &= NSGPU_WIFI_STORE_MASK;
   switch (store) {
     case NSGPU_WIFI_STORE_AUTO:
@@ -1308,7 +1400,8 @@ extern "C" int nsgpu_wifi_set_store(nsgpu_wifi *h, int store) {
 
 extern "C" int nsgpu_wifi_get_store(nsgpu_wifi *h, int *store, uint32_t *phys_per_block, uint32_t *e_cap) {
   if (!h || !store) return set_error(NSGPU_EINVAL, "nsgpu_wifi_get_store: null");
-  *store = (h->use_lds ? NSGPU_WIFI_STORE_LDS : NSGPU_WIFI_STORE_HBM) | (h->use_pre ? 0 : NSGPU_WIFI_INLINE_RX);
+  *store = (h->use_lds ? NSGPU_WIFI_STORE_LDS : NSGPU_WIFI_STORE_HBM) | (h->use_pre ? 0 : NSGPU_WIFI_INLINE_RX) |
+           (h->use_pre && !h->use_sorted ? NSGPU_WIFI_UNSORTED_RX : 0);
   if (phys_per_block) *phys_per_block = h->use_lds ? h->lds_P : 64;
   if (e_cap) *e_cap = h->use_lds ? h->lds_ecap : h->D.ni_mask + 1;
   return NSGPU_OK;

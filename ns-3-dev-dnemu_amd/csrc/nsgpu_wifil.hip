@@ -73,6 +73,14 @@ struct LSync {  // one sync of the epoch (its EndReceive's uid comes from the sy
   uint64_t sts;
   uint32_t suid, euid;
 };
+struct LCk {  // one chunk of an EndReceive's CalculatePer walk, evaluated by k_wl_per: the noise before it,
+  double noise;  // and (duration << 1) | (1: the PLCP header mode)
+  int64_t dm;
+};
+struct LEck {  // an end record's chunks: ck[start, start + n) (n = NONE: its PER was computed inline)
+  uint32_t start, n;
+  double w;  // rxPowerW
+};
 
 struct WDev {
   int64_t nphy;
@@ -92,10 +100,12 @@ struct WDev {
   nsgpu_wifil_end *ends;
   uint32_t *end_sslot;
   uint32_t *cnt;  // [0] events, [1] syncs, [2] ends, [3] error bits (sticky: a SendPacket's are seen at the
-                  // next advance)
+                  // next advance), [4] chunk slots claimed (zeroed by k_wl_patch)
+  LCk *ck;        // the epoch's deferred chunks (ck_cap; a walk that finds no room computes its PER inline)
+  LEck *eck;      // per end record
   uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_erank; 0 between epochs)
   unsigned long long *edig;  // the epoch's digest terms, summed on the device (k_wl_edigest)
-  uint64_t sync_cap, ev_cap, end_cap;
+  uint64_t sync_cap, ev_cap, end_cap, ck_cap;
 };
 
 // ---- WifiMode attributes (the CreateWifiMode calls of wifi-phy.cc:355-840; phyRate: wifi-mode.cc:140-155) ----
@@ -396,6 +406,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
     if (!take_r) {  // ---- YansWifiPhy::EndReceive (yans-wifi-phy.cc:770-799)
       const int64_t nw = (int64_t)eb.ts;
       nsgpu_wifil_end rec{eb.ts, eb.euid, (uint32_t)j, 0.0, 0.0, eb.tx, eb.can ? (uint32_t)NSGPU_WIFI_END_CANCELLED : 0u};
+      LEck eck{0, NONE, 0.0};
       P.c.end++;
       if (eb.can) {  // EventImpl::Invoke skips a cancelled event (event-impl.cc:40-46); still dispatched
         P.c.end_cancelled++;
@@ -410,7 +421,22 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
         const int64_t t0 = (int64_t)eb.sts;
         const int64_t hdrStart = t0 + (int64_t)preamble_us(t.mc, pm.bw, t.preamble) * 1000;
         const int64_t payStart = hdrStart + (int64_t)header_us(t.mc, pm.bw, t.preamble) * 1000;
+        // The walk's sequential part (the noise sums, the chunk bounds) runs here; the chunks' error-rate
+        // models (~10 pow / erfc calls each, ~100-200 chunks an EndReceive) run lane-parallel in k_wl_per,
+        // which multiplies them in this order.  A zero-length chunk is 1.0 (CalculateChunkSuccessRate) and
+        // is not recorded.  Without room in the chunk pool the product is formed here.
+        const uint32_t need = 2 * P.len + 2;
+        const uint32_t cs = atomicAdd(&D.cnt[4], need);
+        const bool defer = (uint64_t)cs + need <= D.ck_cap;
+        uint32_t cn = 0;
         double psr = 1.0, noiseW = noise0;
+        auto ck = [&](int64_t dur, bool hdr) {
+          if (defer) {
+            if (dur != 0) D.ck[cs + cn++] = LCk{noiseW, (int64_t)((uint64_t)dur << 1) | (hdr ? 1 : 0)};
+          } else {
+            psr *= hdr ? chunk(D, snr_of(D, eb.w, noiseW, hm), dur, hm) : chunk(D, snr_of(D, eb.w, noiseW, pm), dur, pm);
+          }
+        };
         int64_t previous = t0;
         uint32_t q = 1;
         LNi nb[NB];  // the ring read NB entries a trip (the walk itself stays one entry at a time)
@@ -435,26 +461,27 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
             current = nw, delta = 0.0, last = true;
           }
           if (previous >= payStart) {
-            psr *= chunk(D, snr_of(D, eb.w, noiseW, pm), current - previous, pm);
+            ck(current - previous, false);
           } else if (previous >= hdrStart) {
             if (current >= payStart) {
-              psr *= chunk(D, snr_of(D, eb.w, noiseW, hm), payStart - previous, hm);
-              psr *= chunk(D, snr_of(D, eb.w, noiseW, pm), current - payStart, pm);
+              ck(payStart - previous, true);
+              ck(current - payStart, false);
             } else {
-              psr *= chunk(D, snr_of(D, eb.w, noiseW, hm), current - previous, hm);
+              ck(current - previous, true);
             }
           } else {
             if (current >= payStart) {
-              psr *= chunk(D, snr_of(D, eb.w, noiseW, hm), payStart - hdrStart, hm);
-              psr *= chunk(D, snr_of(D, eb.w, noiseW, pm), current - payStart, pm);
+              ck(payStart - hdrStart, true);
+              ck(current - payStart, false);
             } else if (current >= hdrStart) {
-              psr *= chunk(D, snr_of(D, eb.w, noiseW, hm), current - hdrStart, hm);
+              ck(current - hdrStart, true);
             }
           }
           noiseW += delta;
           previous = current;
         }
-        rec.per = 1 - psr;
+        eck = LEck{cs, defer ? cn : NONE, eb.w};
+        rec.per = 1 - psr;  // (deferred: k_wl_per overwrites it)
         P.rxing = 0;  // NotifyRxEnd (); SwitchFromRxEndOk / Error -> DoSwitchFromRx (wifi-phy-state-helper.cc:391-402)
       }
       const uint32_t sl = eb.euid == NONE ? eb.sslot : NONE;
@@ -462,6 +489,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
       if (ei < D.end_cap) {
         D.ends[ei] = rec;
         D.end_sslot[ei] = sl;
+        D.eck[ei] = eck;
       } else {
         err |= WE_CAP;
       }
@@ -588,6 +616,32 @@ __global__ void k_wl_prof_epoch() {  // (one thread: fold the epoch's maxima, re
 }
 #endif
 
+// CalculatePer's chunk product for the epoch's deferred EndReceives (interference-helper.cc:257-334): one
+// wave per end record, a lane per chunk (CalculateChunkSuccessRate with the error-rate model), the
+// product taken in walk order (every lane forms the same product from the wave's values).
+__global__ __launch_bounds__(256) void k_wl_per(const WDev D) {
+  const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t ei = blockIdx.x * 4 + (threadIdx.x >> 6); ei < nend; ei += gridDim.x * 4) {
+    const LEck k = D.eck[ei];  // (uniform over the wave)
+    if (k.n == NONE) continue;
+    const LTx t = D.tx[D.ends[ei].tx];
+    const Mode pm = make_mode(t.mc, t.rate, t.bw), hm = header_mode(pm, t.preamble);
+    double psr = 1.0;
+    for (uint32_t b = 0; b < k.n; b += 64) {
+      double c = 1.0;
+      if (b + lane < k.n) {
+        const LCk x = D.ck[k.start + b + lane];
+        const int64_t dur = x.dm >> 1;
+        c = (x.dm & 1) ? chunk(D, snr_of(D, k.w, x.noise, hm), dur, hm) : chunk(D, snr_of(D, k.w, x.noise, pm), dur, pm);
+      }
+      const uint32_t mm = k.n - b < 64 ? k.n - b : 64;
+      for (uint32_t i = 0; i < mm; i++) psr *= __shfl(c, (int)i);
+    }
+    if (lane == 0) D.ends[ei].per = 1 - psr;
+  }
+}
+
 // The epoch's syncs in dispatch order (ts, uid of the syncing Receive): EndReceive uid = uid0 + rank.
 __global__ __launch_bounds__(256) void k_wl_rank(const WDev D, uint32_t uid0) {
   const uint32_t n = D.cnt[1] < D.sync_cap ? D.cnt[1] : (uint32_t)D.sync_cap;
@@ -606,6 +660,7 @@ __global__ __launch_bounds__(256) void k_wl_patch(const WDev D) {
   const uint32_t nev = D.cnt[0] < D.ev_cap ? D.cnt[0] : (uint32_t)D.ev_cap;
   const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
   const uint64_t npe = (uint64_t)D.nphy * LPE_CAP;
+  if (blockIdx.x == 0 && threadIdx.x == 0) D.cnt[4] = 0;  // (the chunk pool: k_wl_step is done with it)
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nev + nend + npe; i += (uint64_t)gridDim.x * 256) {
     if (i < nev) {
       const uint32_t sl = D.ev[i].sslot;
@@ -866,7 +921,10 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   WL_TRY(wl_alloc(h, &D.ev, ev_cap));
   WL_TRY(wl_alloc(h, &D.ends, sync_cap));
   WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
-  WL_TRY(wl_alloc(h, &D.cnt, 4));
+  WL_TRY(wl_alloc(h, &D.cnt, 5));
+  WL_TRY(wl_alloc(h, &D.eck, sync_cap));
+  D.ck_cap = 1u << 21;  // 32 MB of deferred chunks an epoch (~100-200 an EndReceive)
+  WL_TRY(wl_alloc(h, &D.ck, (size_t)D.ck_cap));
   WL_TRY(wl_alloc(h, &D.erank, std::min<uint64_t>(ev_cap, ERANK_MAX)));
   WL_TRY(wl_alloc(h, &D.edig, 1));
   WL_TRY(wl_alloc(h, &h->d_pend, 2));
@@ -933,6 +991,7 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
 #ifdef NSGPU_PHASE_PROF
   hipLaunchKernelGGL(k_wl_prof_epoch, dim3(1), dim3(1), 0, h->s);
 #endif
+  hipLaunchKernelGGL(k_wl_per, dim3(128), dim3(256), 0, h->s, D);
   hipLaunchKernelGGL(k_wl_rank, dim3(64), dim3(256), 0, h->s, D, *uid);
   hipLaunchKernelGGL(k_wl_patch, dim3(256), dim3(256), 0, h->s, D);
   const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;

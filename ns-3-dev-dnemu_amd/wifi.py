@@ -21,6 +21,7 @@ DSSS, OFDM, ERP_OFDM = 0, 1, 2
 PREAMBLE_LONG, PREAMBLE_SHORT = 0, 1
 STORE_AUTO, STORE_LDS, STORE_HBM = 0, 1, 2  # nsgpu_wifi_store: where each phy's NiChanges list lives
 INLINE_RX = 4  # | store: receptions computed inside the per-phy kernel (no up-front reception table)
+UNSORTED_RX = 8  # | store: the reception table's rows scanned unsorted (not put in dispatch order first)
 SYNC, DROP_RX, DROP_TX, DROP_ED, NOT_RUN = 0, 1, 2, 3, 255
 F_CCA_EVAL, F_CCA_SWITCH, F_NEAR_ED, F_NEAR_CCA = 1, 2, 4, 8
 END_CANCELLED, END_DISPATCHED = 1, 2

@@ -72,7 +72,9 @@ def test_micro_scenarios():
 
 STORES = [pytest.param(wifi.STORE_LDS, id="lds"), pytest.param(wifi.STORE_HBM, id="hbm"),
           pytest.param(wifi.STORE_LDS | wifi.INLINE_RX, id="lds-inline"),
-          pytest.param(wifi.STORE_HBM | wifi.INLINE_RX, id="hbm-inline")]
+          pytest.param(wifi.STORE_HBM | wifi.INLINE_RX, id="hbm-inline"),
+          pytest.param(wifi.STORE_LDS | wifi.UNSORTED_RX, id="lds-unsorted"),
+          pytest.param(wifi.STORE_HBM | wifi.UNSORTED_RX, id="hbm-unsorted")]
 
 
 @pytest.mark.parametrize("store", STORES)
@@ -90,6 +92,9 @@ def test_auto_store_is_lds_on_the_bench_grid():
     assert store == wifi.STORE_LDS and 1 <= per_block <= 64 and ecap < 512, (store, per_block, ecap)
     eng = wifi.Engine(wifi.wifi_grid(n_side=100, stop_s=0.15), store=wifi.STORE_HBM | wifi.INLINE_RX)
     assert eng.store()[0] == wifi.STORE_HBM | wifi.INLINE_RX
+    eng.close()
+    eng = wifi.Engine(wifi.wifi_grid(n_side=100, stop_s=0.15), store=wifi.STORE_LDS | wifi.UNSORTED_RX)
+    assert eng.store()[0] == wifi.STORE_LDS | wifi.UNSORTED_RX  # (the default store reads sorted rows)
     eng.close()
 
 
