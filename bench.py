@@ -22,8 +22,10 @@ Workloads (--workload):
 With --gpus N (one process per GPU under torch.distributed.run) p2p-grid runs ONE simulation of a
 grid weak-scaled to 128 x 128N, partitioned into N row bands with the partitioned engine (RCCL
 allgathers + all-to-all every window; `--partitioned` forces that engine on one rank); `value` is
-the run's events / the slowest rank's time.  churn is a single logical process: its ranks run
-independent replicas and their events add up.
+the run's events / the slowest rank's time.  wifi-grid with --gpus N splits the same 10,000-phy run by
+receiver over N ranks (strong scaling; the syncs all-gathered and the counters all-reduced over RCCL
+after the per-phy chains).  churn is a single logical process: its ranks run independent replicas and
+their events add up.
 
 roofline: dominant kernel = the churn's persistent kernel, or for p2p-grid the window-pipeline
 kernel with the largest average launch time (per-kernel HIP events in a separate bracketed run);
@@ -413,6 +415,39 @@ class WifiGrid:
             f"passes timed: {secs:.2f} s); digest_match = that sample's GPU run has the oracle's digest and count")
 
 
+class WifiGridDist(WifiGrid):
+    """Config 3's PHY harness (WifiGrid) split by receiver over N ranks, one GPU each (SURVEY 8(e)'s Wi-Fi
+    split): every rank holds the whole schedule (the Tx records) and runs a contiguous block of n/N receivers;
+    after the chains the ranks all-gather their sync records and all-reduce their counters / digest terms
+    over RCCL, and each hands out the same EndReceive uids (nsgpu_wifi_create_dist).  Strong scaling: the
+    run is one simulation of the same grid whatever N is."""
+    scaling = "strong"
+
+    def __init__(self, args, stream, rank, world, td):
+        import p2p
+        import wifi
+        self.wifi, self.world = wifi, world
+        self.side, self.stop = args.wifi_side, args.wifi_stop
+        self.scenario = wifi.wifi_grid(n_side=self.side, stop_s=self.stop)
+        uid = [p2p.Comm.unique_id() if rank == 0 else None]
+        if td is not None:
+            td.broadcast_object_list(uid, src=0)
+        self.comm = p2p.Comm(uid[0], world, rank)
+        self.part = wifi.partitions(self.scenario.n_phy, world)[rank]
+        self.engine = wifi.Engine(self.scenario, stream=stream, phys=self.part, comm=self.comm)
+        self.workload = (f"wifi-simple-adhoc-grid scaled to {self.side * self.side} nodes (config 3) as a YansWifiPhy "
+                         f"harness split by receiver over {world} rank(s) (RCCL all-gather of syncs, all-reduce of "
+                         f"counters after the chains): {self.side}x{self.side} grid 100 m, LogDistance(3, 46.6777)+"
+                         f"ConstantSpeed, every phy broadcasting 1064-B DSSS 1Mb/s frames once a second (seeded "
+                         f"phases), {len(self.scenario.tx)} SendPacket calls, Stop {self.stop}s")
+
+    def roofline(self, step_kernel_ms, events_per_step):
+        rl = super().roofline(step_kernel_ms, events_per_step)
+        rl["events_per_launch"] = events_per_step / self.world  # (this rank's receivers' share)
+        rl["receivers"] = list(self.part)
+        return rl
+
+
 class WifiLoop:
     """Config 3 as ns-3 runs it: the MAC on the host, the PHYs on the device (nsgpu_wifil behind the
     host-closure runtime nsgpu_sim).  100 x 100 phys, 100 m, YansWifiPhy / channel defaults, NIST error
@@ -536,7 +571,7 @@ def main():
                     help="p2p-grid: skip the wifi-grid / dumbbell entries of the `secondary` list")
     ap.add_argument("--secondary-steps", type=int, default=3, help="timed steps of each secondary workload")
     ap.add_argument("--partitioned", action="store_true",
-                    help="p2p-grid through the partitioned engine even on one rank (RCCL with one rank)")
+                    help="p2p-grid / wifi-grid through the partitioned engine even on one rank (RCCL with one rank)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -554,8 +589,10 @@ def main():
         td.init_process_group("gloo")  # env:// (MASTER_ADDR / MASTER_PORT / RANK / WORLD_SIZE)
         tdist = td
     stream = nsgpu.Stream()
-    partitioned = args.workload == "p2p-grid" and (world > 1 or args.partitioned)
-    if partitioned:
+    partitioned = args.workload in ("p2p-grid", "wifi-grid") and (world > 1 or args.partitioned)
+    if partitioned and args.workload == "wifi-grid":
+        wl = WifiGridDist(args, stream.handle, rank, world, tdist)
+    elif partitioned:
         wl = P2PGridDist(args, stream.handle, rank, world, tdist)
     else:
         wl = WORKLOADS[args.workload](args, stream.handle)
@@ -634,7 +671,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": getattr(wl, "scaling", "weak"),
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",

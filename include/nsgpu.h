@@ -163,6 +163,18 @@ int nsgpu_wifi_destroy(nsgpu_wifi *h);
  * | NSGPU_WIFI_UNSORTED_RX with the table but unsorted rows),
  * its phys per block and the end-queue (LDS) or ring (HBM) capacity. */
 int nsgpu_wifi_set_store(nsgpu_wifi *h, int store);
+/* Partitioned receive subset (the Wi-Fi split: every partition holds the transmissions — the
+ * gathered Tx records — and runs its own receivers [phy_begin, phy_end); no all-to-all).  After the
+ * receivers' chains the partitions' sync records are all-gathered and their counters and digest terms
+ * all-reduced (RCCL on `comm`: nsgpu_wifi_run, one rank per GPU, synchronous), so every partition then hands
+ * out the same EndReceive uids and reports the whole run's stats / ends / tx bases; nsgpu_wifi_read_phys and
+ * the rx log hold the partition's own receivers.  comm = NULL makes a loopback member, run with the others of
+ * its group on one device by nsgpu_wifi_group_run (tests).  Replaces no reference interface: the reference's
+ * YansWifiChannel is not distributed (DistributedSimulatorImpl carries p2p links only). */
+typedef struct nsgpu_comm nsgpu_comm;  /* RCCL communicator: nsgpu_comm_init below */
+int nsgpu_wifi_create_dist(const nsgpu_wifi_scenario *sc, int rx_log, int64_t phy_begin, int64_t phy_end,
+                           nsgpu_comm *comm, nsgpu_wifi **out);
+int nsgpu_wifi_group_run(nsgpu_wifi **members, int n, void *stream);
 int nsgpu_wifi_get_store(nsgpu_wifi *h, int *store, uint32_t *phys_per_block, uint32_t *e_cap);
 /* Diagnostics: the kernels of one run and a run with each bracketed by HIP events (ms[k], k < count). */
 int nsgpu_wifi_kernel_count(int *n);
@@ -404,7 +416,6 @@ int nsgpu_route_global(uint32_t n_nodes, uint32_t n_devices, const uint32_t *dev
  * of DistributedSimulatorImpl).  dispatched / final_ts / next_uid / windows in nsgpu_p2p_results are
  * run-global; digest and drop counters are this rank's share; counters are valid for owned nodes,
  * and the log holds the entries this rank dispatched (zeros elsewhere). */
-typedef struct nsgpu_comm nsgpu_comm;
 int nsgpu_comm_unique_id(uint8_t *id);   /* 128 bytes, rank 0; share it with every rank */
 int nsgpu_comm_init(const uint8_t *id, int nranks, int rank, nsgpu_comm **out);  /* on the rank's device */
 int nsgpu_comm_destroy(nsgpu_comm *c);

@@ -1520,17 +1520,7 @@ __global__ __launch_bounds__(256) void k_copies(const CopyDesc *__restrict__ d) 
 
 using namespace nsgpu;
 
-// ---- RCCL communicator of a partitioned run (one rank per GPU process) ----
-struct nsgpu_comm {
-  ncclComm_t comm = nullptr;
-  int nranks = 0, rank = 0;
-};
-
-#define NCCL_TRY(x)                                                                            \
-  do {                                                                                         \
-    ncclResult_t r_ = (x);                                                                     \
-    if (r_ != ncclSuccess) return set_error(NSGPU_EHIP, "%s: %s", #x, ncclGetErrorString(r_)); \
-  } while (0)
+// (nsgpu_comm, NCCL_TRY: nsgpu_internal.h)
 
 extern "C" int nsgpu_comm_unique_id(uint8_t *id) {
   if (!id) return set_error(NSGPU_EINVAL, "nsgpu_comm_unique_id: null");

@@ -103,6 +103,7 @@ struct TxDesc {  // one transmission, packed for the per-phy scan (64 B: four 16
 
 struct WifiDev {
   int64_t nphy;
+  int64_t j0, nown;  // the receivers this engine runs: phys [j0, j0 + nown) (a partition; all of them alone)
   uint32_t ktx;  // dispatched transmissions: those with a key below the Stop event's
   uint32_t uid_start;
   const double *x, *y, *z;
@@ -502,9 +503,9 @@ __device__ __forceinline__ double rx_power_w(const WifiDev &D, double tx_dbm, do
 // kernel's serial chain then reads 16 B per Receive instead of running the distance / delay / loss /
 // DbmToW chain itself): YansWifiChannel::Send's receiver loop (yans-wifi-channel.cc:77-115).
 __global__ __launch_bounds__(256) void k_wifi_rx(const WifiDev D) {
-  const uint64_t K = D.ktx, n = (uint64_t)D.nphy * K;
+  const uint64_t K = D.ktx, n = (uint64_t)D.nown * K;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-    const uint64_t j = i / K, k = i - j * K;
+    const uint64_t jl = i / K, k = i - jl * K, j = D.j0 + jl;  // (rows: the engine's own receivers)
     const TxDesc t = D.txd[k];
     RxPre r{PRE_NONE, 0.0};
     if (t.phy == (uint32_t)j) {
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(256) void k_wifi_rx(const WifiDev D) {
 // before wlo[k] (ts' + dmax < ts) all come first and those after whi[k] (ts' > ts + dmax) all come later: only
 // the window [wlo[k], whi[k]] (at most WSORT_MAX, host-checked) is compared.
 __global__ __launch_bounds__(256) void k_wifi_rx_sort(const WifiDev D) {
-  const uint64_t K = D.ktx, n = (uint64_t)D.nphy * K;
+  const uint64_t K = D.ktx, n = (uint64_t)D.nown * K;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     const uint64_t j = i / K, k = i - j * K;
     const RxPre *row = D.pre + j * K;
@@ -575,7 +576,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
   uint32_t ok = oc < oe ? D.own_idx[oc] : NONE;
   uint64_t ok_ts = ok != NONE ? D.txd[ok].ts : INF;
   // MODE 2: sr = the row's next unconsumed entry, nx = that entry (loaded one event ahead)
-  const RxS *srow = MODE == 2 ? D.srt + (uint64_t)j * D.ktx : nullptr;
+  const RxS *srow = MODE == 2 ? D.srt + (uint64_t)(j - D.j0) * D.ktx : nullptr;
   uint32_t sr = 0;
   RxS nx{};
   if (MODE == 2 && D.ktx) nx = srow[0];
@@ -609,7 +610,7 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
         }
         at = 0;
       } else if (MODE == 1) {
-        const RxPre *row = D.pre + (uint64_t)j * D.ktx;
+        const RxPre *row = D.pre + (uint64_t)(j - D.j0) * D.ktx;
         for (uint32_t i0 = 0; i0 < 64 && at == 64; i0 += 2) {
           TsDur tp[2];  // two transmissions per memory trip (a scan usually reads the next two)
           RxPre rp[2];
@@ -894,10 +895,11 @@ __device__ __forceinline__ void phy_run(const WifiDev &D, const int64_t j, Ni &n
 // HBM ring store: 64 phys per block.
 template <int MODE>
 __global__ __launch_bounds__(64) void k_wifi_phy(const WifiDev D) {
-  const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (j >= D.nphy) return;
+  const int64_t jl = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (jl >= D.nown) return;
+  const int64_t j = D.j0 + jl;
   __shared__ PeSlots pes[64];
-  RingNi ni{D.ni + (uint64_t)j * (D.ni_mask + 1), D.ni_mask, 0, 0, 0, 0.0};
+  RingNi ni{D.ni + (uint64_t)jl * (D.ni_mask + 1), D.ni_mask, 0, 0, 0, 0.0};
   phy_run<MODE>(D, j, ni, &pes[threadIdx.x]);
 }
 
@@ -910,8 +912,9 @@ template <int MODE>
 __global__ __launch_bounds__(64) void k_wifi_phy_lds(const WifiDev D, uint32_t scap, uint32_t ecap) {
   extern __shared__ uint64_t wlds[];
   const uint32_t P = blockDim.x, l = threadIdx.x;
-  const int64_t j = (int64_t)blockIdx.x * P + l;
-  if (j >= D.nphy) return;
+  const int64_t jl = (int64_t)blockIdx.x * P + l;
+  if (jl >= D.nown) return;
+  const int64_t j = D.j0 + jl;
   const size_t w = 2 * scap + 3 * ecap;  // words per phy: E times, deltas, running sums; S times, deltas
   uint64_t *b = wlds + (size_t)l * w;
   PeSlots *pe = reinterpret_cast<PeSlots *>(wlds + (size_t)P * w) + l;
@@ -1066,6 +1069,14 @@ struct nsgpu_wifi {
   size_t lds_bytes = 0;
   bool use_pre = false;  // the run reads its receptions from D.pre (allocated when the table fits HBM)
   bool use_sorted = false;  // ... in dispatch order from D.srt (allocated beside D.pre when the windows are short)
+  // partitioned runs: this engine runs receivers [D.j0, D.j0 + D.nown); the partitions' results
+  // are combined after the per-phy chains — RCCL (`comm`) or a loopback group on one device (`grouped`)
+  nsgpu_comm *comm = nullptr;
+  bool grouped = false;
+  SyncRec *xsync = nullptr;  // the gathered sync records (sync_cap)
+  unsigned long long *x_acc = nullptr;  // [2][A_N]: the accumulators' sums and maxima over the partitions
+  unsigned long long *x_cnt = nullptr;  // [nranks] sync counts
+  uint32_t *x_err = nullptr;            // [nranks] error bits
 };
 
 constexpr uint32_t WSORT_MAX = 64;  // the longest interleaving window k_wifi_rx_sort compares
@@ -1097,10 +1108,14 @@ static int dalloc(nsgpu_wifi *h, T **p, size_t n, const T *src = nullptr) {
   return NSGPU_OK;
 }
 
-extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgpu_wifi **out) {
+static int wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, int64_t j0, int64_t j1, nsgpu_comm *comm, int nranks,
+                       nsgpu_wifi **out) {
   if (!sc || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: null");
   *out = nullptr;
   const int64_t N = sc->n_phy, K = sc->n_tx;
+  if (j1 < 0) j1 = N;
+  if (j0 < 0 || j0 > j1 || j1 > N) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create_dist: phys [%lld, %lld) of %lld", (long long)j0, (long long)j1, (long long)N);
+  const int64_t NO = j1 - j0;  // the receivers this engine runs
   if (N < 1 || N > 0x7fffffff || K < 0 || K > 0x7fffffff) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: n_phy %lld n_tx %lld", (long long)N, (long long)K);
   if (!sc->x || !sc->y || !sc->z || !sc->channel || !sc->node) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: phy arrays");
   if (K && (!sc->tx_ts || !sc->tx_uid || !sc->tx_phy || !sc->tx_size || !sc->tx_dbm || !sc->tx_modclass ||
@@ -1209,6 +1224,8 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   h->has_stop = has_stop;
   WifiDev &D = h->D;
   D.nphy = N;
+  D.j0 = j0;
+  D.nown = NO;
   D.ktx = ktx;
   D.uid_start = sc->uid_start;
   D.loss = sc->loss;
@@ -1231,7 +1248,7 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
       // each, 4 per CU) rather than packing 64 into a wave.
       int ncu = 0;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
-      size_t P = (size_t)((N + 4 * (int64_t)ncu - 1) / (4 * (int64_t)ncu));
+      size_t P = (size_t)((std::max<int64_t>(NO, 1) + 4 * (int64_t)ncu - 1) / (4 * (int64_t)ncu));
       if (const char *e = getenv("NSGPU_WIFI_PHYS_PER_BLOCK")) P = (size_t)atoi(e);  // (diagnostic sweeps)
       P = std::max<size_t>(1, std::min(P, pmax));
       if (pmax >= 1) {
@@ -1282,10 +1299,19 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   TRY(dalloc(h, (uint32_t **)&D.own_idx, own_idx.size(), own_idx.data()));
   TRY(dalloc(h, (uint32_t **)&D.wlo, wlo.size(), wlo.data()));
   TRY(dalloc(h, (uint32_t **)&D.whi, whi.size(), whi.data()));
-  TRY(dalloc(h, &D.ni, (size_t)N * cap));
+  TRY(dalloc(h, &D.ni, (size_t)std::max<int64_t>(NO, 1) * cap));
   TRY(dalloc(h, &D.sync, sync_cap));
   TRY(dalloc(h, &D.n_sync, 1));
   TRY(dalloc(h, &D.pc, N));
+  NSGPU_HIP(hipMemset(D.pc, 0, (size_t)N * sizeof(*D.pc)));  // (a partition writes only its own phys')
+  if (comm || nranks > 1) {
+    const int R = comm ? comm->nranks : 1;
+    TRY(dalloc(h, &h->xsync, sync_cap));
+    TRY(dalloc(h, &h->x_acc, 2 * (size_t)A_N));
+    TRY(dalloc(h, &h->x_cnt, (size_t)R));
+    TRY(dalloc(h, &h->x_err, (size_t)R));
+    h->comm = comm;
+  }
   D.rx_log = nullptr;
   if (rx_log) TRY(dalloc(h, &D.rx_log, std::max<uint64_t>((uint64_t)ktx * (uint64_t)N, 1)));
   TRY(dalloc(h, &D.acc, A_N));
@@ -1298,14 +1324,14 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   TRY(dalloc(h, &D.ends, sync_cap));
   {  // the reception table (k_wifi_rx): n_phy x dispatched transmissions x 16 B, when half of free HBM holds it
     size_t fr = 0, tot = 0;
-    const uint64_t bytes = (uint64_t)N * ktx * sizeof(RxPre), sbytes = (uint64_t)N * ktx * sizeof(RxS);
+    const uint64_t bytes = (uint64_t)NO * ktx * sizeof(RxPre), sbytes = (uint64_t)NO * ktx * sizeof(RxS);
     D.pre = nullptr;
     D.srt = nullptr;
-    if (ktx && hipMemGetInfo(&fr, &tot) == hipSuccess && bytes <= fr / 2) {
-      TRY(dalloc(h, &D.pre, (size_t)N * ktx));
+    if (ktx && NO && hipMemGetInfo(&fr, &tot) == hipSuccess && bytes <= fr / 2) {
+      TRY(dalloc(h, &D.pre, (size_t)NO * ktx));
       h->use_pre = true;
       if (sortable && bytes + sbytes <= fr / 2) {  // and its rows in dispatch order
-        TRY(dalloc(h, &D.srt, (size_t)N * ktx));
+        TRY(dalloc(h, &D.srt, (size_t)NO * ktx));
         h->use_sorted = true;
       }
     }
@@ -1315,13 +1341,30 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
   return NSGPU_OK;
 }
 
+extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgpu_wifi **out) {
+  return wifi_create(sc, rx_log, 0, -1, nullptr, 1, out);
+}
+
+// A partition of the receivers (every partition knows the transmissions and runs its own
+// receivers); comm = the RCCL communicator of one rank per GPU, or null for a loopback group member
+// (nsgpu_wifi_group_run).
+extern "C" int nsgpu_wifi_create_dist(const nsgpu_wifi_scenario *sc, int rx_log, int64_t phy_begin, int64_t phy_end,
+                                      nsgpu_comm *comm, nsgpu_wifi **out) {
+  if (!sc || phy_end < phy_begin) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create_dist: bad arguments");
+  int rc = wifi_create(sc, rx_log, phy_begin, phy_end, comm, 2, out);
+  if (rc == NSGPU_OK && !comm) (*out)->grouped = true;
+  return rc;
+}
+
 // (k_wifi_rx: 0 ms when the run computes its receptions inline; k_wifi_phy: k_wifi_phy_lds with the LDS store)
 static const char *const WIFI_KERNELS[] = {"k_wifi_rx", "k_wifi_phy", "k_sync_hist", "k_tx_base", "k_sync_place",
                                            "k_sync_rank"};
 constexpr int WIFI_NK = 6;
 
-// One whole run on `s`; with `ev` (WIFI_NK + 1 events) each kernel of the chain is bracketed.
-static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
+// One whole run on `s`; with `ev` (WIFI_NK + 1 events) each kernel of the chain is bracketed.  The first part
+// (wifi_launch_phys) runs the receivers' chains, the second (wifi_launch_uids) hands out the EndReceive uids
+// from the syncs; a partitioned run combines the partitions' syncs and accumulators in between.
+static int wifi_launch_phys(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
   const WifiDev &D = h->D;
   NSGPU_HIP(hipMemsetAsync(D.n_sync, 0, sizeof(unsigned long long), s));
   NSGPU_HIP(hipMemsetAsync(D.acc, 0, A_N * sizeof(unsigned long long), s));
@@ -1336,8 +1379,8 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
   if (!h->use_pre || !h->use_sorted) Dk.srt = nullptr;
   const int mode = Dk.srt ? 2 : Dk.pre ? 1 : 0;
   if (Dk.pre) {
-    const uint64_t n = (uint64_t)D.nphy * D.ktx;
-    const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 16384);
+    const uint64_t n = (uint64_t)D.nown * D.ktx;
+    const unsigned g = (unsigned)std::max<uint64_t>(std::min<uint64_t>((n + 255) / 256, 16384), 1);
     if (n) hipLaunchKernelGGL(k_wifi_rx, dim3(g), dim3(256), 0, s, Dk);
     if (n && Dk.srt) hipLaunchKernelGGL(k_wifi_rx_sort, dim3(g), dim3(256), 0, s, Dk);
   }
@@ -1347,17 +1390,24 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
                                                                              : (const void *)k_wifi_phy_lds<0>;
     if (h->lds_bytes > 65536)
       NSGPU_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_bytes));
-    const dim3 g((unsigned)((D.nphy + h->lds_P - 1) / h->lds_P)), b(h->lds_P);
+    const dim3 g((unsigned)std::max<int64_t>((D.nown + h->lds_P - 1) / h->lds_P, 1)), b(h->lds_P);
     if (mode == 2) hipLaunchKernelGGL(k_wifi_phy_lds<2>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
     else if (mode == 1) hipLaunchKernelGGL(k_wifi_phy_lds<1>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
     else hipLaunchKernelGGL(k_wifi_phy_lds<0>, g, b, h->lds_bytes, s, Dk, h->lds_scap, h->lds_ecap);
   } else {
-    const dim3 g((unsigned)((D.nphy + 63) / 64)), b(64);
+    const dim3 g((unsigned)std::max<int64_t>((D.nown + 63) / 64, 1)), b(64);
     if (mode == 2) hipLaunchKernelGGL(k_wifi_phy<2>, g, b, 0, s, Dk);
     else if (mode == 1) hipLaunchKernelGGL(k_wifi_phy<1>, g, b, 0, s, Dk);
     else hipLaunchKernelGGL(k_wifi_phy<0>, g, b, 0, s, Dk);
   }
   if (ev) NSGPU_HIP(hipEventRecord(ev[2], s));
+  NSGPU_HIP(hipGetLastError());
+  h->last = s;
+  return NSGPU_OK;
+}
+static int wifi_launch_uids(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
+  const WifiDev &D = h->D;
+  const uint64_t nlog = (uint64_t)D.ktx * (uint64_t)D.nphy;
   hipLaunchKernelGGL(k_sync_hist, dim3(1024), dim3(256), 0, s, D);
   if (ev) NSGPU_HIP(hipEventRecord(ev[3], s));
   hipLaunchKernelGGL(k_tx_base, dim3(1), dim3(1024), 0, s, D);
@@ -1370,6 +1420,140 @@ static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
   NSGPU_HIP(hipGetLastError());
   h->last = s;
   h->ran = true;
+  return NSGPU_OK;
+}
+
+// The partitions' results into every partition (after their chains): the accumulators summed (the two
+// maxima maxed), the error bits or-ed, the sync records gathered in partition order (k_sync_rank ranks them
+// by key, so any order gives the same uids).  `cnt[q]`, `err[q]`, `acc[q]` were read back from partition q.
+static int wifi_combine_host(nsgpu_wifi *h, hipStream_t s, const std::vector<unsigned long long> &cnt,
+                             const std::vector<uint32_t> &err, const std::vector<std::vector<unsigned long long>> &acc,
+                             uint64_t *total) {
+  unsigned long long a[A_N] = {};
+  uint32_t e = 0;
+  uint64_t tot = 0;
+  for (size_t q = 0; q < cnt.size(); q++) {
+    for (int i = 0; i < A_N; i++)
+      a[i] = (i == A_NI_MAX || i == A_LAST_TS) ? std::max(a[i], acc[q][i]) : a[i] + acc[q][i];
+    e |= err[q];
+    tot += cnt[q];
+  }
+  if (tot > h->D.sync_cap) e |= ERR_SYNCCAP;
+  if (e & ERR_SYNCCAP) tot = 0;  // (the run fails at its readers; the uid kernels see no records)
+  NSGPU_HIP(hipMemcpyAsync(h->D.acc, a, sizeof(a), hipMemcpyHostToDevice, s));
+  NSGPU_HIP(hipMemcpyAsync(h->D.err, &e, sizeof(e), hipMemcpyHostToDevice, s));
+  const unsigned long long t = tot;
+  NSGPU_HIP(hipMemcpyAsync(h->D.n_sync, &t, sizeof(t), hipMemcpyHostToDevice, s));
+  NSGPU_HIP(hipStreamSynchronize(s));  // (the host sources above are on this stack frame)
+  *total = tot;
+  return NSGPU_OK;
+}
+
+// RCCL partition: counts, errors and accumulators gathered, then the sync records (padded to the largest
+// partition's count) — one host synchronisation per run.
+static int wifi_exchange_rccl(nsgpu_wifi *h, hipStream_t s, uint32_t *err_out) {
+  const WifiDev &D = h->D;
+  const int R = h->comm->nranks;
+  ncclComm_t c = h->comm->comm;
+  NCCL_TRY(ncclGroupStart());
+  NCCL_TRY(ncclAllGather(D.n_sync, h->x_cnt, 1, ncclUint64, c, s));
+  NCCL_TRY(ncclAllGather(D.err, h->x_err, 1, ncclUint32, c, s));
+  NCCL_TRY(ncclAllReduce(D.acc, h->x_acc, A_N, ncclUint64, ncclSum, c, s));
+  NCCL_TRY(ncclAllReduce(D.acc, h->x_acc + A_N, A_N, ncclUint64, ncclMax, c, s));
+  NCCL_TRY(ncclGroupEnd());
+  std::vector<unsigned long long> cnt(R), ac(2 * A_N);
+  std::vector<uint32_t> er(R);
+  NSGPU_HIP(hipMemcpyAsync(cnt.data(), h->x_cnt, R * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  NSGPU_HIP(hipMemcpyAsync(er.data(), h->x_err, R * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  NSGPU_HIP(hipMemcpyAsync(ac.data(), h->x_acc, 2 * A_N * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  NSGPU_HIP(hipStreamSynchronize(s));
+  uint64_t maxc = 0;
+  for (int q = 0; q < R; q++) maxc = std::max<uint64_t>(maxc, std::min<uint64_t>(cnt[q], D.sync_cap));
+  std::vector<std::vector<unsigned long long>> acc(1, std::vector<unsigned long long>(A_N));
+  for (int i = 0; i < A_N; i++) acc[0][i] = (i == A_NI_MAX || i == A_LAST_TS) ? ac[A_N + i] : ac[i];
+  uint32_t e = 0;
+  for (uint32_t x : er) e |= x;
+  uint64_t tot = 0;
+  for (int q = 0; q < R; q++) tot += cnt[q];
+  if (maxc && (uint64_t)R * maxc <= D.sync_cap && tot <= D.sync_cap) {
+    NCCL_TRY(ncclAllGather(D.sync, h->xsync, maxc * sizeof(SyncRec), ncclUint8, c, s));
+    uint64_t off = 0;
+    for (int q = 0; q < R; q++) {
+      if (cnt[q]) NSGPU_HIP(hipMemcpyAsync(D.sync + off, h->xsync + (uint64_t)q * maxc, cnt[q] * sizeof(SyncRec), hipMemcpyDeviceToDevice, s));
+      off += cnt[q];
+    }
+  } else if (maxc) {
+    e |= ERR_SYNCCAP;  // (the padded gather would not fit the sync capacity)
+  }
+  uint64_t t2 = 0;
+  int rc = wifi_combine_host(h, s, std::vector<unsigned long long>{tot}, std::vector<uint32_t>{e}, acc, &t2);
+  *err_out = e;
+  return rc;
+}
+
+// One run: the chains, the exchange of a partitioned (RCCL) run, the uids.  A partitioned run whose LDS
+// start queue overflowed repeats its chains on the HBM ring before the uids (every rank sees the or-ed bits).
+static int wifi_launch(nsgpu_wifi *h, hipStream_t s, hipEvent_t *ev) {
+  int rc = wifi_launch_phys(h, s, ev);
+  if (rc == NSGPU_OK && h->comm) {
+    uint32_t e = 0;
+    rc = wifi_exchange_rccl(h, s, &e);
+    if (rc == NSGPU_OK && (e & ERR_LDS) && !(e & (ERR_TX_IN_TX | ERR_NICAP)) && h->use_lds) {
+      h->use_lds = false;
+      rc = wifi_launch_phys(h, s, ev);
+      if (rc == NSGPU_OK) rc = wifi_exchange_rccl(h, s, &e);
+    }
+  }
+  if (rc == NSGPU_OK) rc = wifi_launch_uids(h, s, ev);
+  return rc;
+}
+
+// A loopback group (every partition on this device, in one process): the members' chains, their results
+// combined through the host, then every member's uids — each member then reads like a partitioned rank.
+extern "C" int nsgpu_wifi_group_run(nsgpu_wifi **m, int n, void *stream) {
+  if (!m || n < 1) return set_error(NSGPU_EINVAL, "nsgpu_wifi_group_run: no members");
+  for (int q = 0; q < n; q++)
+    if (!m[q] || !m[q]->grouped) return set_error(NSGPU_EINVAL, "nsgpu_wifi_group_run: member %d is not a loopback partition", q);
+  const hipStream_t s = (hipStream_t)stream;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    for (int q = 0; q < n; q++) {
+      int rc = wifi_launch_phys(m[q], s, nullptr);
+      if (rc) return rc;
+    }
+    std::vector<unsigned long long> cnt(n);
+    std::vector<uint32_t> er(n);
+    std::vector<std::vector<unsigned long long>> acc(n, std::vector<unsigned long long>(A_N));
+    for (int q = 0; q < n; q++) {
+      NSGPU_HIP(hipMemcpyAsync(&cnt[q], m[q]->D.n_sync, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+      NSGPU_HIP(hipMemcpyAsync(&er[q], m[q]->D.err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      NSGPU_HIP(hipMemcpyAsync(acc[q].data(), m[q]->D.acc, A_N * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    }
+    NSGPU_HIP(hipStreamSynchronize(s));
+    uint32_t e = 0;
+    for (uint32_t x : er) e |= x;
+    if ((e & ERR_LDS) && !(e & (ERR_TX_IN_TX | ERR_NICAP)) && attempt == 0) {
+      for (int q = 0; q < n; q++) m[q]->use_lds = false;
+      continue;
+    }
+    for (int q = 0; q < n; q++) cnt[q] = std::min<unsigned long long>(cnt[q], m[q]->D.sync_cap);
+    for (int r = 0; r < n; r++) {  // every member's syncs into member r's gather buffer, in member order
+      uint64_t off = 0;
+      for (int q = 0; q < n; q++) {
+        if (cnt[q] && off + cnt[q] <= m[r]->D.sync_cap)
+          NSGPU_HIP(hipMemcpyAsync(m[r]->xsync + off, m[q]->D.sync, cnt[q] * sizeof(SyncRec), hipMemcpyDeviceToDevice, s));
+        off += cnt[q];
+      }
+    }
+    for (int r = 0; r < n; r++) {
+      uint64_t tot = 0;
+      int rc = wifi_combine_host(m[r], s, cnt, er, acc, &tot);
+      if (rc) return rc;
+      if (tot) NSGPU_HIP(hipMemcpyAsync(m[r]->D.sync, m[r]->xsync, tot * sizeof(SyncRec), hipMemcpyDeviceToDevice, s));
+      rc = wifi_launch_uids(m[r], s, nullptr);
+      if (rc) return rc;
+    }
+    return NSGPU_OK;
+  }
   return NSGPU_OK;
 }
 
@@ -1409,6 +1593,7 @@ extern "C" int nsgpu_wifi_get_store(nsgpu_wifi *h, int *store, uint32_t *phys_pe
 
 extern "C" int nsgpu_wifi_run(nsgpu_wifi *h, void *stream) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_wifi_run: null");
+  if (h->grouped) return set_error(NSGPU_ESTATE, "nsgpu_wifi_run: a loopback partition runs with its group (nsgpu_wifi_group_run)");
   return wifi_launch(h, (hipStream_t)stream, nullptr);
 }
 
@@ -1434,6 +1619,7 @@ extern "C" const char *nsgpu_wifi_kernel_name(int k) { return k >= 0 && k < WIFI
 // One run with every kernel of the chain bracketed by HIP events on `stream`: ms[k] = kernel k's time.
 extern "C" int nsgpu_wifi_profile(nsgpu_wifi *h, void *stream, double *ms) {
   if (!h || !ms) return set_error(NSGPU_EINVAL, "nsgpu_wifi_profile: null");
+  if (h->grouped) return set_error(NSGPU_ESTATE, "nsgpu_wifi_profile: a loopback partition runs with its group");
   hipEvent_t ev[WIFI_NK + 1] = {};
   int rc = NSGPU_OK;
   for (auto &e : ev)
@@ -1457,7 +1643,7 @@ static int wifi_check(nsgpu_wifi *h, uint64_t *n_sync) {
   unsigned long long ns = 0;
   NSGPU_HIP(hipMemcpy(&err, h->D.err, sizeof(err), hipMemcpyDeviceToHost));
   NSGPU_HIP(hipMemcpy(&ns, h->D.n_sync, sizeof(ns), hipMemcpyDeviceToHost));
-  if ((err & ERR_LDS) && !(err & (ERR_TX_IN_TX | ERR_NICAP))) {
+  if ((err & ERR_LDS) && !(err & (ERR_TX_IN_TX | ERR_NICAP)) && !h->comm && !h->grouped) {
     // an S queue outgrew its LDS capacity (more starts at one instant than SCAP_LDS): the same run on
     // the HBM ring, and every later run of this handle too
     h->use_lds = false;

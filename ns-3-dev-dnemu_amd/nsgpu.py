@@ -169,6 +169,8 @@ SIGNATURES = {
     "nsgpu_hold_run": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _vp]),
     "nsgpu_wifi_tx_duration_ns": (C.c_int, [_u32, _u32, _u64, _u32, _u32, _vp]),
     "nsgpu_wifi_create": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p)]),
+    "nsgpu_wifi_create_dist": (C.c_int, [_vp, C.c_int, C.c_int64, C.c_int64, _vp, C.POINTER(C.c_void_p)]),
+    "nsgpu_wifi_group_run": (C.c_int, [_vp, C.c_int, _vp]),
     "nsgpu_wifi_run": (C.c_int, [_vp, _vp]),
     "nsgpu_wifi_get_stats": (C.c_int, [_vp, _vp]),
     "nsgpu_wifi_read_phys": (C.c_int, [_vp, _vp]),

@@ -165,13 +165,22 @@ def wifi_grid(n_side=100, spacing=100.0, period_s=1.0, stop_s=2.0, size=FRAME_10
 class Engine:
     """The device receive subset for one scenario (nsgpu_wifi_create / run / readers)."""
 
-    def __init__(self, scenario, rx_log=False, stream=None, store=STORE_AUTO):
+    def __init__(self, scenario, rx_log=False, stream=None, store=STORE_AUTO, phys=None, comm=None):
+        """phys=(begin, end): a partition running those receivers (nsgpu_wifi_create_dist) — on the RCCL
+        communicator `comm` (p2p.Comm), or, without one, a loopback member for group_run."""
         self.sc = scenario
         self.s = scenario.c_struct()
         self.stream = stream
         self.rx_log = rx_log
+        self.phys_range = (0, scenario.n_phy) if phys is None else (int(phys[0]), int(phys[1]))
+        self.comm = comm
         h = C.c_void_p()
-        nsgpu.check(nsgpu.lib().nsgpu_wifi_create(C.byref(self.s), int(rx_log), C.byref(h)))
+        if phys is None and comm is None:
+            nsgpu.check(nsgpu.lib().nsgpu_wifi_create(C.byref(self.s), int(rx_log), C.byref(h)))
+        else:
+            nsgpu.check(nsgpu.lib().nsgpu_wifi_create_dist(C.byref(self.s), int(rx_log), self.phys_range[0],
+                                                           self.phys_range[1], comm.h if comm else None,
+                                                           C.byref(h)))
         self.h = h.value
         nsgpu.check(nsgpu.lib().nsgpu_wifi_set_store(self.h, int(store)))
 
@@ -234,6 +243,18 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+
+def partitions(n_phy, parts):
+    """Contiguous receiver blocks [begin, end) of `parts` partitions (the row bands of a grid)."""
+    return [(n_phy * p // parts, n_phy * (p + 1) // parts) for p in range(parts)]
+
+
+def group_run(engines, stream=None):
+    """One run of a loopback group (nsgpu_wifi_group_run): the partitions' chains, then their combined
+    syncs and counters in every member."""
+    arr = (C.c_void_p * len(engines))(*[e.h for e in engines])
+    nsgpu.check(nsgpu.lib().nsgpu_wifi_group_run(arr, len(engines), stream))
 
 
 # ---- closed-loop PHY (nsgpu_wifil_*: SendPacket from host closures on nsgpu_sim) ----
