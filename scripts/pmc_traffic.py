@@ -4,7 +4,8 @@ profiles/traffic_<workload>.json: average HBM bytes per launch of each named ker
 Corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
 WRITE_SIZE are in KiB; FETCH_SIZE is doubled on gfx950 (128-B requests tallied at 64 B).
 Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <out.json> <kernel-substring>...
-(the first kernel's entry is also written at the top level, for older readers)
+(the first kernel's entry is also written at the top level, for older readers; a name ending in "(" matches
+that kernel only, not the kernels it prefixes — "k_wifi_rx(" against k_wifi_rx_sort — and is keyed without it)
 """
 import csv
 import glob
@@ -38,10 +39,10 @@ def main():
         write_kib, nw = per_dispatch(wdir, "WRITE_SIZE", k)
         rd = 2.0 * fetch_kib * 1024.0
         wr = write_kib * 1024.0
-        res["kernels"][k] = {"fetch_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+        res["kernels"][k.rstrip("(")] = {"fetch_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                              "hbm_bytes_per_launch": rd + wr, "dispatches": [nf, nw]}
-    first = res["kernels"][kernels[0]]
-    res.update({"kernel": kernels[0], **first})
+    first = res["kernels"][kernels[0].rstrip("(")]
+    res.update({"kernel": kernels[0].rstrip("("), **first})
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
