@@ -116,7 +116,8 @@ struct Ctl {
   uint32_t force_run, hcap;        // a hub too large to sort in a block: dispatch the window as a run;
                                    // the window is cut at the next host event (pause after it)
   uint64_t hts, hrel;              // next host event (nsgpu_p2p_advance): ts (~0: none); the rel ts of the
-  uint32_t huid, pad4;             //   window's last timestamp (W_end or the host event's); the host uid
+  uint32_t huid, x1arr;            //   window's last timestamp (W_end or the host event's); the host uid;
+                                   //   k_dfin2's blocks that have read the X1 headers
   uint64_t pchild;                 // children of the last scanned window that stay pending (not inline)
   // ---- wide windows (single engine, nsgpu_p2p_win.h): same-node TransmitCompletes run inside them ----
   uint64_t lim_rel;   // a TransmitComplete child with rel ts < lim_rel is a local record of this window
@@ -1382,6 +1383,20 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     hsts = lh->red.stopts;
     hsuid = lh->red.stopuid;
   }
+  // X1 is all-gathered in place (x1_send is this rank's slot of x1_recv): the last block to have read the
+  // headers resets this rank's for the next window — every block's header loads have returned before it
+  // arrives (one wave per block: the wave's wait covers every lane)
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  if (threadIdx.x == 0 && atomicAdd(&C.x1arr, 1u) == gridDim.x - 1) {
+    atomicExch(&C.x1arr, 0u);
+    X1Hdr *hs = x1hdr(M.x1_send, 0);
+    hs->W = hs->tc = hs->tinl = hs->needc = 0;
+    hs->lastkey = 0;
+    hs->red.tmin = hs->red.wend = hs->red.stopts = hs->red.wendw = ~0ull;
+    hs->red.stopuid = 0;
+  }
   // the slot's accumulators, record and first children, all loaded before anything waits
   const uint32_t s = blockIdx.x * HB + threadIdx.x;
   const bool vs = s < W;
@@ -1487,11 +1502,6 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   }
   if (done) C.done = 1;
   else if (needc) C.mode = MODE_COMPACT;  // (every rank: the pipelines stay in step)
-  X1Hdr *hs = x1hdr(M.x1_send, 0);
-  hs->W = hs->tc = hs->tinl = hs->needc = 0;
-  hs->lastkey = 0;
-  hs->red.tmin = hs->red.wend = hs->red.stopts = hs->red.wendw = ~0ull;
-  hs->red.stopuid = 0;
   stack_and_hubs();
 }
 
@@ -1968,8 +1978,8 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.x0_recv, 2 * (size_t)nranks));
     TRY(dalloc(h, &M.xk_send, 2));
     TRY(dalloc(h, &M.xk_recv, 2 * (size_t)nranks));
-    TRY(dalloc(h, &M.x1_send, X1B));
     TRY(dalloc(h, &M.x1_recv, X1B * nranks));
+    M.x1_send = M.x1_recv + (size_t)rank * X1B;  // (in place: NCCL moves only the other ranks' slots)
     if ((uint64_t)nranks * WCAP * M.maxc >= (1ull << 32))  // (k_gtile's packed child prefix)
       return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: %d ranks x %u children per event", nranks, M.maxc);
     {  // X2 capacity: the largest number of devices of one rank whose peer another rank owns
@@ -2101,9 +2111,8 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
     NSGPU_HIP(hipMemsetAsync(M.x0_recv, 0, X0B * R, s));
     NSGPU_HIP(hipMemsetAsync(M.xk_send, 0, 16, s));
     NSGPU_HIP(hipMemsetAsync(M.xk_recv, 0, 16 * R, s));
-    NSGPU_HIP(hipMemsetAsync(M.x1_send, 0, X1B, s));
-    NSGPU_HIP(hipMemcpyAsync(M.x1_send, &h->x1h0, sizeof(X1Hdr), hipMemcpyHostToDevice, s));
     NSGPU_HIP(hipMemsetAsync(M.x1_recv, 0, X1B * R, s));
+    NSGPU_HIP(hipMemcpyAsync(M.x1_send, &h->x1h0, sizeof(X1Hdr), hipMemcpyHostToDevice, s));  // (its own slot)
     NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, M.x2b * R, s));
     NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, M.x2b * R, s));
     NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 4 * WCAP * sizeof(uint32_t), s));
