@@ -881,9 +881,21 @@ __device__ uint64_t g_phase[64];
       ph_t_ = t_;                                                                       \
     }                                                                                   \
   } while (0)
+// hub blocks (k2_handle): thread 0 of every hub block adds its phase times into g_phase[24..27], calls in [28]
+#define HUB_T0() uint64_t hub_t_ = threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0
+#define HUB_MARK(i)                                                                     \
+  do {                                                                                  \
+    if (threadIdx.x == 0) {                                                             \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                             \
+      atomicAdd((unsigned long long *)&g_phase[i], (unsigned long long)(t_ - hub_t_));  \
+      hub_t_ = t_;                                                                      \
+    }                                                                                   \
+  } while (0)
 #else
 #define PH_BEGIN() (void)0
 #define PH_MARK(i) (void)0
+#define HUB_T0() (void)0
+#define HUB_MARK(i) (void)0
 #endif
 // Per-block start / end times (s_memrealtime) of the window kernels in one sampled window
 // (diagnostic build only): g_blk[kernel][block] = {start, end}, window g_blk_win.

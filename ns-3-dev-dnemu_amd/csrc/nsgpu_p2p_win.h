@@ -1196,6 +1196,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   const uint64_t below = (1ull << lane) - 1ull;
   uint64_t *gk = M.hub_key + (uint64_t)hb * WCAP;
   uint32_t *gs = M.hub_slot + (uint64_t)hb * WCAP;
+  HUB_T0();
   // 1. the node's window events, in slot order
   uint32_t n = 0;
   for (uint32_t x0 = 0; x0 < W; x0 += HB) {
@@ -1225,6 +1226,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     }
     __syncthreads();
   }
+  HUB_MARK(24);  // (the window scan and the sort)
   const uint64_t tmin = hc.tmin, inline_lim = hc.inline_lim, slo = hc.slo, shi = hc.shi;
   const int32_t sink = M.sink_of_node[c];
   Emit E;
@@ -1251,79 +1253,159 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   Pkt *b_pkt = reinterpret_cast<Pkt *>(lds + 7 * HB);     // [HB]
   HubEv *b_h = reinterpret_cast<HubEv *>(lds + 11 * HB);  // [HB]
   // 2. node parts: the stateless ones (TransmitComplete, NetDevice::Start, Receive -> IpForward: rx
-  //    counter, MacRx trace, route, TTL) by their own lane, the others serially by lane 0 in key order
-  for (uint32_t j0 = 0; j0 < n; j0 += HB) {
-    const uint32_t j = j0 + lane;
-    if (j < n) {
-      const uint32_t s = gs[j];
-      const uint64_t key = gk[j];
-      const uint32_t kw = M.wkind[base + s], a = M.wa[base + s], ctx = M.wctx[base + s];
-      Pkt p = M.wpkt[base + s];
-      const uint32_t kind = kw & 0xffu;
-      const bool sl = stateless_event(M, c, kind, p);
-      b_ctx[lane] = ctx;
-      b_s[lane] = s;
-      b_key[lane] = key;
-      b_kind[lane] = kw;
-      b_a[lane] = a;
-      b_pkt[lane] = p;
-      b_sl[lane] = sl;
-      if (sl) {
-        E.now = tmin + (key >> 32);
-        E.uid = (uint32_t)key;
-        E.trseq = 0;
-        HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, ctx, 0};
-        if (kind == K_TX_COMPLETE) {
-          h.op = ACT_KICK;
-          h.dev = a;
-        } else if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive -> IpForward
-          atomicAdd(&M.dev[a].c.rx_packets, 1u);
-          p.size -= 2;
-          trace_call(M, E, NSGPU_TR_RX, a, p);
-          trace_call(M, E, NSGPU_TR_IP_RX, a, p);
-          const uint32_t out = route_of(M, c, p);
-          if (out == 0xffffffffu) {
-            hs.no_route++;
-            trace_ip_drop(M, E, a, p);
-          } else {
-            p.ttl -= 1;
-            if (p.ttl == 0) {  // (ICMP off: stateless_event)
-              hs.ttl_drops++;
-              trace_ip_drop(M, E, out, Pkt{p.app, p.ipid, p.size, 1u});
+  //    counter, MacRx trace, route, TTL) by their own lane, the others serially by lane 0 in key order.
+  //    NBT batches of HB events per round: each dependent step (slot -> record -> destination -> route)
+  //    is one memory trip for all of them.
+  constexpr int NBT = WIDE ? 1 : 2;  // (the wide kernel has no registers to spare: its hubs stay one batch a round)
+  {
+    uint64_t *c_key = reinterpret_cast<uint64_t *>(lds);  // [HB * NBT]
+    uint32_t *c_s = lds + 2 * HB * NBT, *c_kind = lds + 3 * HB * NBT, *c_a = lds + 4 * HB * NBT,
+             *c_ctx = lds + 6 * HB * NBT;
+    Pkt *c_pkt = reinterpret_cast<Pkt *>(lds + 7 * HB * NBT);  // [HB * NBT]
+    static_assert(11 * HB * NBT <= K2_LDS_WORDS, "hub node-part batch does not fit the shared buffer");
+    for (uint32_t j0 = 0; j0 < n; j0 += HB * NBT) {
+      uint32_t s_[NBT], kw_[NBT], a_[NBT], ctx_[NBT], dn_[NBT], ds_[NBT], out_[NBT];
+      uint64_t key_[NBT];
+      Pkt p_[NBT];
+#pragma unroll
+      for (int u = 0; u < NBT; u++) {
+        const uint32_t j = j0 + (uint32_t)(u * HB) + lane;
+        if (j < n) {
+          s_[u] = gs[j];
+          key_[u] = gk[j];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NBT; u++) {
+        const uint32_t j = j0 + (uint32_t)(u * HB) + lane;
+        if (j < n) {
+          kw_[u] = M.wkind[base + s_[u]];
+          a_[u] = M.wa[base + s_[u]];
+          ctx_[u] = M.wctx[base + s_[u]];
+          p_[u] = M.wpkt[base + s_[u]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NBT; u++) {  // (stateless_event's and route_of's addressing)
+        const uint32_t j = j0 + (uint32_t)(u * HB) + lane;
+        dn_[u] = ds_[u] = 0;
+        if (j < n && (kw_[u] & 0xffu) == K_RECEIVE) {
+          dn_[u] = pkt_dst_node(M, p_[u]);
+          ds_[u] = pkt_dst_slot(M, p_[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NBT; u++) {
+        const uint32_t j = j0 + (uint32_t)(u * HB) + lane;
+        out_[u] = 0xffffffffu;
+        if (j < n && (kw_[u] & 0xffu) == K_RECEIVE && dn_[u] != c) out_[u] = route_at(M, c, ds_[u]);
+      }
+      // stateless_event, with the destination loaded above; the others' positions as wave masks (lane 0
+      // visits only those: a scan of every position's flag in LDS cost ~80 ns an event)
+      bool sl_[NBT];
+      uint64_t ser_[NBT];
+#pragma unroll
+      for (int u = 0; u < NBT; u++) {
+        const uint32_t j = j0 + (uint32_t)(u * HB) + lane;
+        const uint32_t kind = kw_[u] & 0xffu;
+        sl_[u] = j < n && (kind == K_TX_COMPLETE || kind == K_DEV_START ||
+                           (kind == K_RECEIVE && !(M.icmp && (p_[u].ttl & 0xffu) <= 1u) && dn_[u] != c));
+        ser_[u] = __ballot(j < n && !sl_[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < NBT; u++) {
+        const uint32_t j = j0 + (uint32_t)(u * HB) + lane;
+        if (j >= n) continue;
+        const uint32_t s = s_[u], kw = kw_[u], a = a_[u], ctx = ctx_[u], bq = (uint32_t)(u * HB) + lane;
+        const uint64_t key = key_[u];
+        Pkt p = p_[u];
+        const uint32_t kind = kw & 0xffu;
+        const bool sl = sl_[u];
+        c_ctx[bq] = ctx;
+        c_s[bq] = s;
+        c_key[bq] = key;
+        c_kind[bq] = kw;
+        c_a[bq] = a;
+        c_pkt[bq] = p;
+        if (sl) {
+          E.now = tmin + (key >> 32);
+          E.uid = (uint32_t)key;
+          E.trseq = 0;
+          HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, ctx, 0};
+          if (kind == K_TX_COMPLETE) {
+            h.op = ACT_KICK;
+            h.dev = a;
+          } else if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive -> IpForward
+            atomicAdd(&M.dev[a].c.rx_packets, 1u);
+            p.size -= 2;
+            trace_call(M, E, NSGPU_TR_RX, a, p);
+            trace_call(M, E, NSGPU_TR_IP_RX, a, p);
+            const uint32_t out = out_[u];
+            if (out == 0xffffffffu) {
+              hs.no_route++;
+              trace_ip_drop(M, E, a, p);
             } else {
-              h.op = ACT_SEND;
-              h.dev = out;
-              h.p = p;
+              p.ttl -= 1;
+              if (p.ttl == 0) {  // (ICMP off: stateless_event)
+                hs.ttl_drops++;
+                trace_ip_drop(M, E, out, Pkt{p.app, p.ipid, p.size, 1u});
+              } else {
+                h.op = ACT_SEND;
+                h.dev = out;
+                h.p = p;
+              }
             }
           }
+          h.seq = E.trseq;
+          M.hx[s] = h;
         }
-        h.seq = E.trseq;
-        M.hx[s] = h;
       }
-    }
-    __syncthreads();
-    if (lane == 0) {
-      const uint32_t nb = n - j0 < (uint32_t)HB ? n - j0 : (uint32_t)HB;
-      for (uint32_t q = 0; q < nb; q++) {
-        if (b_sl[q]) continue;
-        const uint32_t s = b_s[q];
-        const uint64_t rel = b_key[q] >> 32;
-        E.ctx = b_ctx[q];
-        E.now = tmin + rel;
-        E.slot0 = s * M.maxc;
-        E.n = 0;
-        E.uid = (uint32_t)b_key[q];
-        E.trseq = 0;
-        E.demote = rel == slo || rel == shi;
-        const NodeOut o = node_part(M, E, b_kind[q], b_a[q], b_pkt[q], sink, hs, true);
-        uint32_t ni = 0;
-        for (uint32_t jj = 0; jj < E.n; jj++) ni += (M.ch_kind[E.slot0 + jj] & 0xffu) == K_FWD_UP;
-        M.hx[s] = HubEv{o.act.op, o.act.dev, o.act.p, o.post.delay, o.post.valid ? o.post.kind : 0u, o.post.a, E.n,
-                        E.trseq, o.cancelled ? 1u : 0u, ni, b_ctx[q], o.xdrop};
+      __syncthreads();
+#ifdef NSGPU_PHASE_PROF
+      const uint64_t ser_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+      uint64_t any = 0;
+#pragma unroll
+      for (int u = 0; u < NBT; u++) any |= ser_[u];
+      if (lane == 0 && any) {
+#ifdef NSGPU_PHASE_PROF
+        atomicAdd((unsigned long long *)&g_phase[30], (unsigned long long)(n - j0 < (uint32_t)(HB * NBT) ? n - j0 : (uint32_t)(HB * NBT)));
+#endif
+#pragma unroll 1
+        for (int u = 0; u < NBT; u++) {
+          uint64_t m = 0;
+#pragma unroll
+          for (int k = 0; k < NBT; k++) m = k == u ? ser_[k] : m;  // (a select chain: no indexed registers)
+          while (m) {
+            const uint32_t q = (uint32_t)(u * HB) + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+            m &= m - 1;
+#ifdef NSGPU_PHASE_PROF
+            atomicAdd((unsigned long long *)&g_phase[29], 1ull);
+#endif
+            const uint32_t s = c_s[q];
+            const uint64_t rel = c_key[q] >> 32;
+            E.ctx = c_ctx[q];
+            E.now = tmin + rel;
+            E.slot0 = s * M.maxc;
+            E.n = 0;
+            E.uid = (uint32_t)c_key[q];
+            E.trseq = 0;
+            E.demote = rel == slo || rel == shi;
+            const NodeOut o = node_part(M, E, c_kind[q], c_a[q], c_pkt[q], sink, hs, true);
+            uint32_t ni = 0;
+            for (uint32_t jj = 0; jj < E.n; jj++) ni += (M.ch_kind[E.slot0 + jj] & 0xffu) == K_FWD_UP;
+            M.hx[s] = HubEv{o.act.op, o.act.dev, o.act.p, o.post.delay, o.post.valid ? o.post.kind : 0u, o.post.a, E.n,
+                            E.trseq, o.cancelled ? 1u : 0u, ni, c_ctx[q], o.xdrop};
+          }
+        }
       }
+      __syncthreads();
+#ifdef NSGPU_PHASE_PROF
+      if (lane == 0) atomicAdd((unsigned long long *)&g_phase[31], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - ser_t0));
+#endif
     }
-    __syncthreads();
   }
+  HUB_MARK(25);  // (node parts)
   // 3. device steps and trailing children.  When every device step of the hub is on one device and no
   //    event has inline children (a dumbbell router's burst), the steps are resolved in parallel
   //    (hub_device_scan); otherwise serially in key order with the device state in registers.
@@ -1453,6 +1535,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     }
     if (lane == 0) D.flush(M);
   }
+  HUB_MARK(26);  // (device steps: the parallel scan or the serial pass)
   publish_min<HB, WIDE>(R, E.tmn, E.wnd, E.wndw);
   x1_totals(M, xa);
   const uint64_t nr = wave_sum64(hs.no_route), td = wave_sum64(hs.ttl_drops), cn = wave_sum64(hs.cancelled),
@@ -1467,6 +1550,10 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     if (ic) atomicAdd((unsigned long long *)&C.icmp, (unsigned long long)ic);
   }
   __syncthreads();
+  HUB_MARK(27);  // (publish, totals)
+#ifdef NSGPU_PHASE_PROF
+  if (threadIdx.x == 0) atomicAdd((unsigned long long *)&g_phase[28], 1ull);
+#endif
 }
 
 // ---- k2_handle: pool maintenance (tombstones, free slots, fresh children -> pool) ----
