@@ -1041,9 +1041,10 @@ constexpr int32_t CBIG = 1 << 28;
 
 // Returns false (nothing done) when the batch would reuse a ring slot (more enqueues than the ring
 // holds beyond the queued packets): the serial pass runs instead.
+// hops[j]: the op of the list's event j (hub_node gathered the lane's segment into LDS).
 __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d, const uint32_t *gs,
                                 const uint64_t *gk, uint32_t n, uint32_t j0s, uint32_t j1s, uint64_t tmin, HStat &hs,
-                                X1Acc &xa) {
+                                X1Acc &xa, const uint8_t *hops) {
   const int lane = threadIdx.x;
   const DevRec dr = M.dev[d];
   const int32_t qmax = (int32_t)dr.qmax;
@@ -1056,9 +1057,9 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
   // pass A: the segment's composed map and its enqueue / dequeue counts
   CMap f{0, -CBIG, CBIG};
   for (uint32_t j = j0s; j < j1s; j++) {
-    const HubEv h = M.hx[gs[j]];
-    if (h.op == ACT_SEND) f = cmap_then(f, CMap{1, -CBIG, qmax});
-    else if (h.op == ACT_KICK) f = cmap_then(f, CMap{-1, -CBIG, CBIG});
+    const uint32_t op = hops[j];
+    if (op == ACT_SEND) f = cmap_then(f, CMap{1, -CBIG, qmax});
+    else if (op == ACT_KICK) f = cmap_then(f, CMap{-1, -CBIG, CBIG});
   }
   CMap inc = f;
   for (int o = 1; o < 64; o <<= 1) {
@@ -1073,7 +1074,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
   {
     int32_t x = cin;
     for (uint32_t j = j0s; j < j1s; j++) {
-      const uint32_t op = M.hx[gs[j]].op;
+      const uint32_t op = hops[j];
       if (op == ACT_SEND) {
         if (x < qmax) ne++;
         if (x == -1) nd++;
@@ -1092,16 +1093,16 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
     int32_t x = cin;
     uint32_t e = ebefore;
     for (uint32_t j = j0s; j < j1s; j++) {
-      const HubEv h = M.hx[gs[j]];
-      if (h.op == ACT_SEND) {
+      const uint32_t op = hops[j];
+      if (op == ACT_SEND) {
         if (x >= 0 && x < qmax) {
-          Pkt p = h.p;
+          Pkt p = M.hx[gs[j]].p;
           p.size += 2;
           qb[(head0 + cnt0 + e) % qcap] = p;
         }
         if (x < qmax) e++;
         x = x + 1 < qmax ? x + 1 : qmax;
-      } else if (h.op == ACT_KICK) {
+      } else if (op == ACT_KICK) {
         x -= 1;
       }
     }
@@ -1197,18 +1198,35 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   uint64_t *gk = M.hub_key + (uint64_t)hb * WCAP;
   uint32_t *gs = M.hub_slot + (uint64_t)hb * WCAP;
   HUB_T0();
-  // 1. the node's window events, in slot order
+  // 1. the node's window events, in slot order (HSB batches of HB window entries a memory trip; the wide
+  //    kernel has no registers to spare: one there)
+  constexpr int HSB = WIDE ? 1 : 4;
   uint32_t n = 0;
-  for (uint32_t x0 = 0; x0 < W; x0 += HB) {
-    const uint32_t x = x0 + lane;
-    const bool m = x < W && M.widx[x] != NOHOLD && lp_of(M, M.wctx[base + x], M.wkind[base + x], M.wa[base + x]) == c;
-    const uint64_t bm = __ballot(m);
-    if (m) {
-      const uint32_t p = n + (uint32_t)__popcll(bm & below);
-      gs[p] = x;
-      gk[p] = M.wkey[base + x];
+  for (uint32_t x0 = 0; x0 < W; x0 += HB * HSB) {
+    uint32_t bi[HSB], bc[HSB], bk[HSB], ba[HSB];
+#pragma unroll
+    for (int u = 0; u < HSB; u++) {
+      const uint32_t x = x0 + (uint32_t)(u * HB) + lane;
+      bi[u] = NOHOLD;
+      if (x < W) {
+        bi[u] = M.widx[x];
+        bc[u] = M.wctx[base + x];
+        bk[u] = M.wkind[base + x];
+        ba[u] = M.wa[base + x];
+      }
     }
-    n += (uint32_t)__popcll(bm);
+#pragma unroll
+    for (int u = 0; u < HSB; u++) {
+      const uint32_t x = x0 + (uint32_t)(u * HB) + lane;
+      const bool m = x < W && bi[u] != NOHOLD && lp_of(M, bc[u], bk[u], ba[u]) == c;
+      const uint64_t bm = __ballot(m);
+      if (m) {
+        const uint32_t p = n + (uint32_t)__popcll(bm & below);
+        gs[p] = x;
+        gk[p] = M.wkey[base + x];
+      }
+      n += (uint32_t)__popcll(bm);
+    }
   }
   __syncthreads();
   if (!sorted) {  // (n <= HUBL here: a larger hub makes its window a sorted run, k2_pa)
@@ -1411,13 +1429,34 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   //    (hub_device_scan); otherwise serially in key order with the device state in registers.
   const uint32_t mseg = (n + HB - 1) / HB, j0s = lane * mseg, j1s = j0s + mseg < n ? j0s + mseg : n;
   uint32_t dmin = NOSRC, dmax = 0, inl = 0;
-  for (uint32_t j = j0s; j < j1s; j++) {
-    const HubEv h = M.hx[gs[j]];
-    if (h.op != ACT_NONE) {
-      dmin = h.dev < dmin ? h.dev : dmin;
-      dmax = h.dev > dmax ? h.dev : dmax;
-    }
-    inl |= h.pad;
+  // the lane's segment: devices, inline flags, and its ops into LDS for the device scan (HSO events a
+  // memory trip; past the serial pass's batch arrays)
+  uint8_t *hops = reinterpret_cast<uint8_t *>(lds + 2048);
+  static_assert(2048 + WCAP / 4 <= K2_LDS_WORDS, "hub ops do not fit the shared buffer");
+  constexpr int HSO = WIDE ? 1 : 8;
+  for (uint32_t j = j0s; j < j1s; j += HSO) {
+    uint32_t sl[HSO], op[HSO], dv[HSO], pd[HSO];
+#pragma unroll
+    for (int u = 0; u < HSO; u++)
+      if (j + u < j1s) sl[u] = gs[j + u];
+#pragma unroll
+    for (int u = 0; u < HSO; u++)
+      if (j + u < j1s) {
+        const HubEv *hp = M.hx + sl[u];
+        op[u] = hp->op;
+        dv[u] = hp->dev;
+        pd[u] = hp->pad;
+      }
+#pragma unroll
+    for (int u = 0; u < HSO; u++)
+      if (j + u < j1s) {
+        hops[j + u] = (uint8_t)op[u];
+        if (op[u] != ACT_NONE) {
+          dmin = dv[u] < dmin ? dv[u] : dmin;
+          dmax = dv[u] > dmax ? dv[u] : dmax;
+        }
+        inl |= pd[u];
+      }
   }
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t x = __shfl_xor(dmin, o), y = __shfl_xor(dmax, o), z = __shfl_xor(inl, o);
@@ -1429,7 +1468,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && (!WIDE || hc.lim == 0) && M.dev[dmin].qmax >= 1 &&
               !(M.dev[dmin].busy == 0 && M.dev[dmin].cnt != 0);
   X1Acc xa{0, 0, 0};
-  if (fast) fast = hub_device_scan(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs, xa);
+  if (fast) fast = hub_device_scan(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs, xa, hops);
   if (!fast) {
     DevCache D;
     D.d = NOSRC;
