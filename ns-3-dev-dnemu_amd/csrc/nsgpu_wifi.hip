@@ -1108,7 +1108,9 @@ static int dalloc(nsgpu_wifi *h, T **p, size_t n, const T *src = nullptr) {
   return NSGPU_OK;
 }
 
-static int wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, int64_t j0, int64_t j1, nsgpu_comm *comm, int nranks,
+// dist: a partition (nsgpu_wifi_create_dist) — it gets the exchange buffers, sized for comm's ranks (a
+// loopback member, comm = NULL, combines through the host and needs one count / error slot).
+static int wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, int64_t j0, int64_t j1, nsgpu_comm *comm, bool dist,
                        nsgpu_wifi **out) {
   if (!sc || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create: null");
   *out = nullptr;
@@ -1304,7 +1306,7 @@ static int wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, int64_t j0, in
   TRY(dalloc(h, &D.n_sync, 1));
   TRY(dalloc(h, &D.pc, N));
   NSGPU_HIP(hipMemset(D.pc, 0, (size_t)N * sizeof(*D.pc)));  // (a partition writes only its own phys')
-  if (comm || nranks > 1) {
+  if (dist) {
     const int R = comm ? comm->nranks : 1;
     TRY(dalloc(h, &h->xsync, sync_cap));
     TRY(dalloc(h, &h->x_acc, 2 * (size_t)A_N));
@@ -1342,7 +1344,7 @@ static int wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, int64_t j0, in
 }
 
 extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgpu_wifi **out) {
-  return wifi_create(sc, rx_log, 0, -1, nullptr, 1, out);
+  return wifi_create(sc, rx_log, 0, -1, nullptr, false, out);
 }
 
 // A partition of the receivers (every partition knows the transmissions and runs its own
@@ -1351,7 +1353,7 @@ extern "C" int nsgpu_wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, nsgp
 extern "C" int nsgpu_wifi_create_dist(const nsgpu_wifi_scenario *sc, int rx_log, int64_t phy_begin, int64_t phy_end,
                                       nsgpu_comm *comm, nsgpu_wifi **out) {
   if (!sc || phy_end < phy_begin) return set_error(NSGPU_EINVAL, "nsgpu_wifi_create_dist: bad arguments");
-  int rc = wifi_create(sc, rx_log, phy_begin, phy_end, comm, 2, out);
+  int rc = wifi_create(sc, rx_log, phy_begin, phy_end, comm, true, out);
   if (rc == NSGPU_OK && !comm) (*out)->grouped = true;
   return rc;
 }

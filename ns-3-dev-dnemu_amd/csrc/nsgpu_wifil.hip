@@ -34,6 +34,8 @@ namespace {
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr int LPE_CAP = 8;  // pending EndReceive records of one phy (the live one + cancelled ones)
 constexpr uint32_t END_STAGE = 128;  // EndReceive records an epoch returns with its counters (more: a second copy)
+constexpr size_t STAT_HDR = 32;      // the status block's counters (5 x u32) and digest (at 24) before the ends
+static_assert(sizeof(nsgpu_wifil_end) % 8 == 0 && STAT_HDR % 8 == 0, "status block alignment");
 constexpr uint32_t WE_TX_IN_TX = 1, WE_NICAP = 2, WE_RQCAP = 4, WE_PECAP = 8, WE_CAP = 16;
 constexpr int NB = 8;  // ring entries loaded per batch
 
@@ -823,9 +825,12 @@ struct nsgpu_wifil {
   std::vector<void *> allocs;
   std::vector<uint32_t> recv;  // fan-out uids of one SendPacket per phy
   uint64_t n_tx = 0, tx_cap = 0;
-  uint32_t *h_cnt = nullptr;  // pinned: the epoch counters
-  unsigned long long *h_dig = nullptr;  // pinned: the epoch's digest sum
-  nsgpu_wifil_end *h_ends = nullptr;     // pinned: the epoch's first END_STAGE end records
+  // pinned: the epoch's status block as one copy — counters, digest sum, first END_STAGE end records (the
+  // device's D.cnt / D.edig / D.ends are laid out the same way in one allocation)
+  uint8_t *h_stat = nullptr;
+  uint32_t *h_cnt = nullptr;
+  unsigned long long *h_dig = nullptr;
+  nsgpu_wifil_end *h_ends = nullptr;
   LPhy *h_ps = nullptr;                  // pinned: one phy's state (nsgpu_wifil_get_state)
   std::vector<uint32_t> erank;
   unsigned long long *d_pend = nullptr, *h_pend = nullptr;
@@ -851,9 +856,7 @@ extern "C" int nsgpu_wifil_destroy(nsgpu_wifil *h) {
     (void)hipStreamDestroy(h->s);
   }
   for (void *p : h->allocs) (void)hipFree(p);
-  if (h->h_cnt) (void)hipHostFree(h->h_cnt);
-  if (h->h_dig) (void)hipHostFree(h->h_dig);
-  if (h->h_ends) (void)hipHostFree(h->h_ends);
+  if (h->h_stat) (void)hipHostFree(h->h_stat);
   if (h->h_ps) (void)hipHostFree(h->h_ps);
   if (h->h_pend) (void)hipHostFree(h->h_pend);
   delete h;
@@ -919,29 +922,32 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   WL_TRY(wl_alloc(h, &D.tx, c->tx_cap));
   WL_TRY(wl_alloc(h, &D.sync, sync_cap));
   WL_TRY(wl_alloc(h, &D.ev, ev_cap));
-  WL_TRY(wl_alloc(h, &D.ends, sync_cap));
+  uint8_t *stat = nullptr;  // [cnt x 5 | pad | edig | ends x sync_cap]
+  WL_TRY(wl_alloc(h, &stat, STAT_HDR + sync_cap * sizeof(nsgpu_wifil_end)));
+  D.cnt = reinterpret_cast<uint32_t *>(stat);
+  D.edig = reinterpret_cast<unsigned long long *>(stat + 24);
+  D.ends = reinterpret_cast<nsgpu_wifil_end *>(stat + STAT_HDR);
   WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
-  WL_TRY(wl_alloc(h, &D.cnt, 5));
   WL_TRY(wl_alloc(h, &D.eck, sync_cap));
   D.ck_cap = 1u << 21;  // 32 MB of deferred chunks an epoch (~100-200 an EndReceive)
   WL_TRY(wl_alloc(h, &D.ck, (size_t)D.ck_cap));
   WL_TRY(wl_alloc(h, &D.erank, std::min<uint64_t>(ev_cap, ERANK_MAX)));
-  WL_TRY(wl_alloc(h, &D.edig, 1));
   WL_TRY(wl_alloc(h, &h->d_pend, 2));
 #undef WL_TRY
   D.sync_cap = sync_cap;
   D.ev_cap = ev_cap;
   D.end_cap = sync_cap;
   h->tx_cap = c->tx_cap;
-  if (hipHostMalloc((void **)&h->h_cnt, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void **)&h->h_dig, sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void **)&h->h_ends, END_STAGE * sizeof(nsgpu_wifil_end), hipHostMallocDefault) != hipSuccess ||
+  if (hipHostMalloc((void **)&h->h_stat, STAT_HDR + END_STAGE * sizeof(nsgpu_wifil_end), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void **)&h->h_ps, sizeof(LPhy), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void **)&h->h_pend, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
       hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
     nsgpu_wifil_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_wifil_create: host buffers / stream");
   }
+  h->h_cnt = reinterpret_cast<uint32_t *>(h->h_stat);
+  h->h_dig = reinterpret_cast<unsigned long long *>(h->h_stat + 24);
+  h->h_ends = reinterpret_cast<nsgpu_wifil_end *>(h->h_stat + STAT_HDR);
   *out = h;
   return NSGPU_OK;
 }
@@ -999,9 +1005,7 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   hipLaunchKernelGGL(k_wl_edigest, dim3(256), dim3(256), 0, h->s, D, *dispatched, logging ? 1 : 0);
   NSGPU_HIP(hipGetLastError());
   // counters, the digest sum and the first end records in one trip
-  NSGPU_HIP(hipMemcpyAsync(h->h_cnt, D.cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
-  NSGPU_HIP(hipMemcpyAsync(h->h_dig, D.edig, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->s));
-  NSGPU_HIP(hipMemcpyAsync(h->h_ends, D.ends, END_STAGE * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipMemcpyAsync(h->h_stat, D.cnt, STAT_HDR + END_STAGE * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipStreamSynchronize(h->s));
   int rc = wl_check(h, "nsgpu_wifil_advance");
   if (rc) return rc;
