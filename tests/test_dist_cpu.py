@@ -113,3 +113,15 @@ def _worker(rank, world, port):
 def test_gloo_world2_orchestration():
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_wifi_receiver_partitions():
+    """The Wi-Fi split's receiver blocks (wifi.partitions, bench.py wifi-grid --gpus N): contiguous,
+    covering every phy once, balanced, empty blocks allowed when there are more partitions than phys."""
+    import wifi
+    for n, k in [(10_000, 1), (10_000, 2), (10_000, 8), (3, 5), (7, 3)]:
+        r = wifi.partitions(n, k)
+        assert len(r) == k and r[0][0] == 0 and r[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        sizes = [e - b for b, e in r]
+        assert min(sizes) >= 0 and max(sizes) - min(sizes) <= 1
