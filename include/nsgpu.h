@@ -310,6 +310,9 @@ int nsgpu_sim_destroy_pending(nsgpu_sim *s, uint64_t handle, uint64_t ts, int *p
 /* dispatch accounting of the host events (the engine accounts for the device ones): count, cancelled
  * ones, digest (sum of nsgpu_dispatch_digest_term over their global ranks); optional log at global ranks */
 int nsgpu_sim_host_stats(nsgpu_sim *s, uint64_t *host_dispatched, uint64_t *cancelled, uint64_t *digest);
+/* the runtime's host-closure queue (a HipBatchScheduler): refills of its front batch, events served from
+ * the front, time spent refilling (nsgpu_sched_stats) */
+int nsgpu_sim_sched_stats(nsgpu_sim *s, uint64_t *refills, uint64_t *front, double *refill_us);
 int nsgpu_sim_set_log(nsgpu_sim *s, uint64_t *ts, uint32_t *uid, uint32_t *ctx, uint64_t cap);
 /* mixed host / device runs: the engine's events join this runtime's order (attach before scheduling;
  * the runtime continues from the engine's post-setup uid); a closure may make one of the engine's

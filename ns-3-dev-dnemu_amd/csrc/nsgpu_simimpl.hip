@@ -319,6 +319,16 @@ static int pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n,
   int rc;
   nsgpu_event e;
   nsgpu_sched *q = s->events;
+  // RunOneEvent (ProcessOneEvent, :167-170) dispatches exactly one event; an attached engine dispatches its
+  // events in windows (one advance can run any number of them), so one-event steps are refused there
+  if (force && (s->wifi || (s->p2p && !s->ended)))
+    return set_error(NSGPU_ESTATE, "RunOneEvent: not supported while a GPU-resident engine is attached (it "
+                                   "dispatches its events in windows)");
+  // a Run after the Run that the device's Simulator::Stop ended: the reference resumes (:153-165), this
+  // engine cannot (its final window's children were not queued) — fail instead of dropping the host events
+  if (s->dev_stopped && !force && q->size)
+    return set_error(NSGPU_ESTATE, "Run: the attached engine dispatched Simulator::Stop; resuming with %llu host "
+                                   "event(s) pending is not supported", (unsigned long long)q->size);
   if (s->wifi) {  // the PHY's events below the next host event's key, then that host event (one per window)
     bool have = false;
     if (q->size) {
@@ -558,6 +568,11 @@ int nsgpu_sim_current_uid(nsgpu_sim *s, uint32_t *uid) {
   return NSGPU_OK;
 }
 
+int nsgpu_sim_sched_stats(nsgpu_sim *s, uint64_t *refills, uint64_t *front, double *refill_us) {
+  if (!s) return set_error(NSGPU_EINVAL, "nsgpu_sim_sched_stats: null");
+  return nsgpu_sched_stats(s->events, refills, front, refill_us);
+}
+
 int nsgpu_sim_host_stats(nsgpu_sim *s, uint64_t *host_dispatched, uint64_t *cancelled, uint64_t *digest) {
   if (!s) return set_error(NSGPU_EINVAL, "nsgpu_sim_host_stats: null");
   if (host_dispatched) *host_dispatched = s->host_dispatched;
@@ -597,6 +612,11 @@ int nsgpu_sim_wifi_state(nsgpu_sim *s, uint32_t phy, nsgpu_wifil_phy_state *out)
 // of the closure being dispatched; its Schedule calls take the runtime's next uids).
 int nsgpu_sim_p2p_send(nsgpu_sim *s, uint32_t app) {
   if (!s || !s->p2p) return set_error(NSGPU_ESTATE, "nsgpu_sim_p2p_send: no engine attached");
+  // (an engine that has run out — nothing pending on the device, or a device Stop — is not advanced
+  // again, so a datagram handed to it would never be dispatched)
+  if (s->ended)
+    return set_error(NSGPU_ESTATE, "nsgpu_sim_p2p_send: the attached engine has finished (no device event was "
+                                   "pending when a host event was next); the datagram would never be sent");
   uint32_t seq = s->p2p_seq_uid == s->cur_uid ? s->p2p_seq : 0;
   int rc = nsgpu_p2p_inject_send(s->p2p, app, s->cur_ts, s->cur_uid, s->cur_ctx, &s->uid, &seq, s->stream);
   s->p2p_seq_uid = s->cur_uid;

@@ -1073,7 +1073,7 @@ struct nsgpu_wifi {
   // are combined after the per-phy chains — RCCL (`comm`) or a loopback group on one device (`grouped`)
   nsgpu_comm *comm = nullptr;
   bool grouped = false;
-  SyncRec *xsync = nullptr;  // the gathered sync records (sync_cap)
+  SyncRec *xsync = nullptr;  // the gathered sync records (nranks x sync_cap: padded to the largest rank's count)
   unsigned long long *x_acc = nullptr;  // [2][A_N]: the accumulators' sums and maxima over the partitions
   unsigned long long *x_cnt = nullptr;  // [nranks] sync counts
   uint32_t *x_err = nullptr;            // [nranks] error bits
@@ -1308,7 +1308,7 @@ static int wifi_create(const nsgpu_wifi_scenario *sc, int rx_log, int64_t j0, in
   NSGPU_HIP(hipMemset(D.pc, 0, (size_t)N * sizeof(*D.pc)));  // (a partition writes only its own phys')
   if (dist) {
     const int R = comm ? comm->nranks : 1;
-    TRY(dalloc(h, &h->xsync, sync_cap));
+    TRY(dalloc(h, &h->xsync, (uint64_t)R * sync_cap));  // (the padded gather: every rank's records up to sync_cap)
     TRY(dalloc(h, &h->x_acc, 2 * (size_t)A_N));
     TRY(dalloc(h, &h->x_cnt, (size_t)R));
     TRY(dalloc(h, &h->x_err, (size_t)R));
@@ -1477,7 +1477,7 @@ static int wifi_exchange_rccl(nsgpu_wifi *h, hipStream_t s, uint32_t *err_out) {
   for (uint32_t x : er) e |= x;
   uint64_t tot = 0;
   for (int q = 0; q < R; q++) tot += cnt[q];
-  if (maxc && (uint64_t)R * maxc <= D.sync_cap && tot <= D.sync_cap) {
+  if (maxc && tot <= D.sync_cap) {  // (xsync holds R x sync_cap records: the padding always fits)
     NCCL_TRY(ncclAllGather(D.sync, h->xsync, maxc * sizeof(SyncRec), ncclUint8, c, s));
     uint64_t off = 0;
     for (int q = 0; q < R; q++) {
@@ -1485,7 +1485,7 @@ static int wifi_exchange_rccl(nsgpu_wifi *h, hipStream_t s, uint32_t *err_out) {
       off += cnt[q];
     }
   } else if (maxc) {
-    e |= ERR_SYNCCAP;  // (the padded gather would not fit the sync capacity)
+    e |= ERR_SYNCCAP;  // (the run's syncs exceed the capacity a single engine would have)
   }
   uint64_t t2 = 0;
   int rc = wifi_combine_host(h, s, std::vector<unsigned long long>{tot}, std::vector<uint32_t>{e}, acc, &t2);

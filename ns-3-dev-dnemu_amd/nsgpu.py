@@ -114,6 +114,7 @@ SIGNATURES = {
     "nsgpu_sim_remove_key": (C.c_int, [_vp, _u64, _u32, _u32, _u64]),
     "nsgpu_sim_key_expired": (C.c_int, [_vp, _u64, _u32, _vp]),
     "nsgpu_sim_host_stats": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "nsgpu_sim_sched_stats": (C.c_int, [_vp, _vp, _vp, _vp]),
     "nsgpu_sim_set_log": (C.c_int, [_vp, _vp, _vp, _vp, _u64]),
     "nsgpu_sim_attach_p2p": (C.c_int, [_vp, _vp]),
     "nsgpu_sim_p2p_send": (C.c_int, [_vp, _u32]),

@@ -132,3 +132,59 @@ def test_pull_windows_same_time_group_and_remove():
                 s.remove_key(*uids[8])
                 uids[12] = (10, s.insert_raw(10, 0, 12))
     assert order == [4, 6, 12, 10, 2]
+
+
+def test_run_after_device_stop_with_host_events_fails_loudly():
+    """ADVICE r03: a device-dispatched Simulator::Stop ends the Run; a later Run (the pull interface that
+    ns3::HipSimulatorImpl::Run uses) with host events still pending must fail, not return silently —
+    the reference would resume them (default-simulator-impl.cc:153-165), this engine cannot."""
+    sc = flows_grid()
+    eng = p2p.Engine(sc, log_cap=0)
+    eng.reset()
+    sim = nsgpu.Sim()
+    sim.attach_p2p(eng)
+    ran = []
+    sim.schedule(sc.sim_stop_ns + 10_000_000, lambda: ran.append(1))  # after the device's Stop
+    while len(sim.pop_window()):  # HipSimulatorImpl::Run: windows until an empty one
+        pass
+    assert ran == []
+    with pytest.raises(nsgpu.NsgpuError, match="Simulator::Stop"):
+        sim.pop_window()  # the next Run
+
+
+def test_run_one_with_engine_attached_is_refused():
+    """RunOneEvent dispatches ONE event (default-simulator-impl.cc:167-170); an attached engine
+    advances in windows, so the one-event step is refused rather than running many device events."""
+    sc = flows_grid()
+    eng = p2p.Engine(sc, log_cap=0)
+    eng.reset()
+    sim = nsgpu.Sim()
+    sim.attach_p2p(eng)
+    sim.schedule(1000, lambda: None)
+    with pytest.raises(nsgpu.NsgpuError, match="RunOneEvent"):
+        sim.pop_one()
+
+
+def test_send_after_engine_finished_is_refused():
+    """once the attached engine has run out of device events it is not advanced again, so a
+    later UdpSocket::Send through it is refused with a clear error instead of queueing a datagram that
+    would never be dispatched."""
+    sc = p2p.grid(2, 2, stop_ns=20_000_000, flows=[(0, 3)])
+    sc.setup = [x for x in sc.setup if x[0] != p2p.SETUP_STOP]  # no Simulator::Stop: the device drains
+    sc.stop_ns = -1
+    eng = p2p.Engine(sc, log_cap=0)
+    eng.reset()
+    sim = nsgpu.Sim()
+    sim.attach_p2p(eng)
+    app_send = [i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_ONOFF][0]
+    errs = []
+
+    def late():
+        try:
+            sim.p2p_send(app_send)
+        except nsgpu.NsgpuError as e:
+            errs.append(str(e))
+
+    sim.schedule(5_000_000_000, late)  # long after the flow's last device event
+    sim.run()
+    assert errs and "finished" in errs[0]
