@@ -433,6 +433,40 @@ int nsgpu_p2p_group_reset(nsgpu_p2p_group *g, void *stream);
 int nsgpu_p2p_group_run(nsgpu_p2p_group *g, void *stream);
 int nsgpu_p2p_group_destroy(nsgpu_p2p_group *g);
 
+/* ---- trace codec (replaces the default sinks' formatting for GPU-resident events) ----
+ * nsgpu_trace_record streams -> the bytes ns-3's default ascii / pcap sinks write:
+ * AsciiTraceHelper::Default{Enqueue,Dequeue,Drop,Receive}SinkWithContext (src/network/helper/trace-helper.cc:
+ * 303-390) through Packet::Print (src/network/model/packet.cc:427-476), InternetStackHelper's Ipv4 Tx / Rx /
+ * Drop lines (src/internet/helper/internet-stack-helper.cc:650-730), and the PromiscSniffer pcap records
+ * (src/point-to-point/helper/point-to-point-helper.cc:81-110 -> PcapFileWrapper::Write,
+ * src/network/utils/pcap-file.cc:300-381).  ns3::HipSimulatorImpl hands nsgpu_trace_line's text to the
+ * helper's OutputStreamWrapper and nsgpu_trace_packet's bytes to PcapFileWrapper::Write (Time, buffer,
+ * length).  Output functions: out == NULL only sets *len (the size); otherwise cap must hold *len bytes. */
+typedef struct nsgpu_trace_addressing {
+  const uint32_t *dev_addr;         /* n_devices: the IPv4 address of the device's interface (0: none) */
+  const uint32_t *dev_ip_ifindex;   /* n_devices: its Ipv4 interface index (loopback 0, then Assign order) */
+  const uint32_t *app_remote_addr;  /* n_apps: the Remote address of a sender (0: the destination node's first
+                                     * interface) */
+  const uint32_t *app_remote_port;  /* n_apps: the Remote port of a sender */
+} nsgpu_trace_addressing;
+typedef struct nsgpu_trace_codec nsgpu_trace_codec;
+int nsgpu_trace_codec_create(const nsgpu_p2p_scenario *sc, const nsgpu_trace_addressing *ad, nsgpu_trace_codec **out);
+int nsgpu_trace_codec_free(nsgpu_trace_codec *c);
+/* trace order: the dispatching event's (ts, uid), then the call order inside it (seq) */
+int nsgpu_trace_sort(nsgpu_trace_record *rec, uint64_t n);
+int nsgpu_trace_line(const nsgpu_trace_codec *c, const nsgpu_trace_record *r, char *out, uint64_t cap, uint64_t *len);
+int nsgpu_trace_packet(const nsgpu_trace_codec *c, const nsgpu_trace_record *r, uint8_t *out, uint64_t cap,
+                       uint64_t *len);  /* the serialized packet the sniffer sees (PPP header included) */
+int nsgpu_trace_ascii(const nsgpu_trace_codec *c, const nsgpu_trace_record *rec, uint64_t n, char *out, uint64_t cap,
+                      uint64_t *len);   /* every record's line (EnableAsciiAll / EnableAsciiIpv4All on one stream) */
+int nsgpu_trace_pcap(const nsgpu_trace_codec *c, const nsgpu_trace_record *rec, uint64_t n, uint32_t dev, uint8_t *out,
+                     uint64_t cap, uint64_t *len);  /* device dev's pcap file (EnablePcapAll) */
+/* PcapFile::Init + Write (src/network/utils/pcap-file.cc:300-381) of arbitrary packets: record i is
+ * data[off[i] .. off[i + 1]) with origLen orig_len[i] (inclLen = min (origLen, snaplen, its bytes)) */
+int nsgpu_pcap_file(uint32_t linktype, uint32_t snaplen, uint64_t n, const uint32_t *sec, const uint32_t *usec,
+                    const uint32_t *orig_len, const uint64_t *off, const uint8_t *data, uint8_t *out, uint64_t cap,
+                    uint64_t *len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -184,6 +184,15 @@ SIGNATURES = {
     "nsgpu_wifi_kernel_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nsgpu_wifi_kernel_name": (C.c_char_p, [C.c_int]),
     "nsgpu_wifi_profile": (C.c_int, [_vp, _vp, _vp]),
+    # trace codec (host code in libnsgpu: nsgpu_trace.cc)
+    "nsgpu_trace_codec_create": (C.c_int, [_vp, _vp, _vp]),
+    "nsgpu_trace_codec_free": (C.c_int, [_vp]),
+    "nsgpu_trace_sort": (C.c_int, [_vp, _u64]),
+    "nsgpu_trace_line": (C.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "nsgpu_trace_packet": (C.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "nsgpu_trace_ascii": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp]),
+    "nsgpu_trace_pcap": (C.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _vp]),
+    "nsgpu_pcap_file": (C.c_int, [_u32, _u32, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
 }
 
 _lib = None

@@ -737,3 +737,82 @@ class LoopbackGroup:
             nsgpu.lib().nsgpu_p2p_group_destroy(self.h)
         except Exception:
             pass
+
+
+class TraceAddressing(C.Structure):
+    """nsgpu_trace_addressing (include/nsgpu.h)."""
+    _fields_ = [("dev_addr", C.c_void_p), ("dev_ip_ifindex", C.c_void_p), ("app_remote_addr", C.c_void_p),
+                ("app_remote_port", C.c_void_p)]
+
+
+def _out_bytes(call):
+    """Runs a size query, then the call into a buffer of that size (the codec's output convention)."""
+    n = C.c_uint64(0)
+    nsgpu.check(call(None, 0, C.byref(n)))
+    buf = C.create_string_buffer(max(n.value, 1))
+    nsgpu.check(call(buf, n.value, C.byref(n)))
+    return buf.raw[:n.value]
+
+
+class TraceCodec:
+    """The product library's trace codec (nsgpu_trace_*, ns-3-dev-dnemu_amd/csrc/nsgpu_trace.cc) for a
+    scenario: the ascii / pcap bytes of ns-3's default sinks from nsgpu_trace_record streams."""
+
+    def __init__(self, sc):
+        self.sc = sc
+        self._s = sc.c_struct()
+        nd, na = len(sc.dev), len(sc.apps)
+        self._arrs = [np.array([sc.dev_addr.get(d, 0) for d in range(nd)], np.uint32),
+                      np.array([sc.dev_ifindex.get(d, 0) for d in range(nd)], np.uint32),
+                      np.array([a["remote_addr"] or 0 for a in sc.apps] or [0], np.uint32)[:max(na, 1)],
+                      np.array([a["remote_port"] for a in sc.apps] or [0], np.uint32)]
+        self._ad = TraceAddressing(*[a.ctypes.data for a in self._arrs])
+        h = C.c_void_p()
+        nsgpu.check(nsgpu.lib().nsgpu_trace_codec_create(C.byref(self._s), C.byref(self._ad), C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            nsgpu.lib().nsgpu_trace_codec_free(self.h)
+            self.h = None
+
+    @staticmethod
+    def sort(tr):
+        tr = np.ascontiguousarray(np.array(tr, dtype=TRACE_RECORD_DTYPE))
+        nsgpu.check(nsgpu.lib().nsgpu_trace_sort(tr.ctypes.data, len(tr)))
+        return tr
+
+    def ascii(self, tr):
+        tr = np.ascontiguousarray(tr, dtype=TRACE_RECORD_DTYPE)
+        return _out_bytes(lambda o, c, n: nsgpu.lib().nsgpu_trace_ascii(self.h, tr.ctypes.data, len(tr), o, c, n)).decode()
+
+    def line(self, rec):
+        r = np.ascontiguousarray(np.array([rec], dtype=TRACE_RECORD_DTYPE))
+        return _out_bytes(lambda o, c, n: nsgpu.lib().nsgpu_trace_line(self.h, r.ctypes.data, o, c, n)).decode()
+
+    def packet(self, rec):
+        r = np.ascontiguousarray(np.array([rec], dtype=TRACE_RECORD_DTYPE))
+        return _out_bytes(lambda o, c, n: nsgpu.lib().nsgpu_trace_packet(self.h, r.ctypes.data, o, c, n))
+
+    def pcap(self, tr, dev):
+        tr = np.ascontiguousarray(tr, dtype=TRACE_RECORD_DTYPE)
+        return _out_bytes(lambda o, c, n: nsgpu.lib().nsgpu_trace_pcap(self.h, tr.ctypes.data, len(tr), dev, o, c, n))
+
+    def pcaps(self, tr, ifindex):
+        """{(node, ifindex): file bytes} for every point-to-point device (EnablePcapAll)."""
+        return {(self.sc.dev[d][0], ifindex[d]): self.pcap(tr, d) for d in range(len(self.sc.dev))}
+
+
+def pcap_file(linktype, snaplen, records):
+    """PcapFile::Init + Write through the product library (nsgpu_pcap_file): records = [(sec, usec, data,
+    orig_len)]."""
+    n = len(records)
+    sec = np.array([r[0] for r in records] or [0], np.uint32)
+    usec = np.array([r[1] for r in records] or [0], np.uint32)
+    orig = np.array([r[3] for r in records] or [0], np.uint32)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum([len(r[2]) for r in records]) if n else []
+    data = np.frombuffer(b"".join(bytes(r[2]) for r in records) or b"\0", np.uint8).copy()
+    return _out_bytes(lambda o, c, k: nsgpu.lib().nsgpu_pcap_file(linktype, snaplen, n, sec.ctypes.data, usec.ctypes.data,
+                                                                  orig.ctypes.data, off.ctypes.data, data.ctypes.data,
+                                                                  o, c, k))
