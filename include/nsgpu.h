@@ -318,6 +318,12 @@ int nsgpu_sim_set_log(nsgpu_sim *s, uint64_t *ts, uint32_t *uid, uint32_t *ctx, 
  * the runtime continues from the engine's post-setup uid); a closure may make one of the engine's
  * OnOff applications send a datagram now (UdpSocket::Send from a host application) */
 int nsgpu_sim_attach_p2p(nsgpu_sim *s, nsgpu_p2p *h);
+/* the same after setup (ns3::HipSimulatorImpl::AdoptDeviceSubset): the program built its topology with the
+ * stock helpers, whose setup-time Schedule calls took uids 4.. in this runtime; the engine was created with
+ * a setup list mirroring them (NsgpuP2pScenario::FromNodeList) and the caller removed the host events the
+ * engine now dispatches (nsgpu_sim_remove_key).  Host events that remain (the program's own) keep their
+ * uids; nothing may have been dispatched yet, and the engine's post-setup uid must equal this runtime's. */
+int nsgpu_sim_adopt_p2p(nsgpu_sim *s, nsgpu_p2p *h);
 int nsgpu_sim_p2p_send(nsgpu_sim *s, uint32_t app);
 /* the closed-loop Wi-Fi PHY: its events join this runtime's order (one host event per window after the
  * PHY's events before it); a closure's SendPacket (now, the runtime's next uids) and GetState (now) */

@@ -90,6 +90,28 @@ struct Red {
   uint64_t wendw;  // the wide bound: min over pending of ts + lookw (cross-node lookahead; single engine)
 };
 
+// A deferred window's dispatch bases: what k2_sdef needs once the window's records are staged in rank order.
+struct WInfo {
+  uint64_t K0, tmin, ilim;  // dispatches before the window, its tmin and inline limit
+  uint32_t uid0, N, W, Lt;  // the uid its first child takes; records (gen-0 W + local Lt)
+};
+
+// A staged record of a deferred window, at its rank: key (rel ts << 32 | its uid, which may be provisional;
+// a local record's uid is its parent's child prefix + j, resolved by k2_sdef), context, child counts
+// (n | inline << 16), and for a local record its parent (wpar: record | child index << 24) with loc = 1.
+struct Stg {
+  uint64_t key;
+  uint32_t ctx, cnt, par, loc;
+};
+static_assert(sizeof(Stg) == 24, "Stg");
+// Provisional uids (deferred windows): child j of the record of rank r of window n, before window n's child
+// prefix is known, is PROV | (n & 1) << 30 | r << 8 | j — above every resolved uid (< UID_DF_LIMIT, checked), so
+// keys compare as the final uids do; resolved to uid0(n) + cpt[n & 1][r] + j.
+constexpr uint32_t PROV = 0x80000000u, PROV_MAXC = 256, UID_DF_LIMIT = 0x3fe00000u;
+__device__ __forceinline__ uint32_t prov_uid(uint64_t win, uint32_t r, uint32_t j) {
+  return PROV | ((uint32_t)(win & 1) << 30) | (r << 8) | j;
+}
+
 // Device-resident run control (one per engine).  Every field is written by one kernel of the
 // window pipeline and read by later ones, never read and written by different blocks of one kernel
 // except through atomics.  Window k: red[(k + 1) & 1] holds the pending set's reduction that bounds
@@ -129,6 +151,13 @@ struct Ctl {
   // ---- sorted runs: the chunk being dispatched ends at rnext; rtrim: the run ends after it (k_trim) ----
   uint64_t rnext;
   uint32_t rtrim, pad5;
+  // ---- deferred dispatch accounting (single wide engine, nsgpu_p2p_win.h "deferred windows") ----
+  uint64_t acc_tc, acc_tinl;  // this window's children / inline children (k2_handle accumulates)
+  uint32_t pdf;               // the window the next k2_pa appends is staged (1) or appended from sinfo (0)
+  uint32_t sflag;             // a staged window awaits k2_sdef: 1 | (its window index & 3) << 1
+  uint32_t rk_W, rk_go;       // k2_handle's snapshot for k2_rank (window size; it was handled, normally)
+  uint64_t rk_win, rk_lim;    //   (its window index, lim_rel): k2_rank's bookkeeping block rewrites C.W etc.
+  WInfo winfo[4];             // window n's dispatch bases (k2_rank's bookkeeping), at n & 3
 };
 
 static_assert(offsetof(Ctl, prep) == offsetof(Ctl, W) + 12 && offsetof(Ctl, W) % 16 == 0, "the X0 payload");
@@ -247,6 +276,11 @@ struct P2PDev {
   uint4 *ldat;            // [LMAX] the window's local records in dense order (k2_rank -> k2_scan): record,
                           // child counts (n | inline << 16), rel ts, parent (wpar)
   uint32_t *lrank;        // [LMAX] their rank accumulators (k2_rank; 0 between windows)
+  // ---- deferred windows (wrank / lrank are then 2 x WTOT / 2 x LMAX: by window parity) ----
+  struct Stg *stage;      // [2][NMAX] a window's records in rank order (k2_pa stages, k2_sdef reads)
+  uint2 *sleaf;           // [2][NMAX][maxc] their inline DoForwardUp leaves: (context, child index)
+  uint32_t *cpt;          // [2][NMAX] child prefix by rank (k2_sdef): provisional uids resolve through it
+  uint32_t *dmap;         // [LCAP] local record -> dense index of its window (k2_rank)
 };
 
 // ---------------- wave / block helpers ----------------
@@ -1058,10 +1092,12 @@ __device__ __forceinline__ Ev *x2rec(const P2PDev &M, uint8_t *b, uint32_t q) {
 
 constexpr int PFC = 4;  // children per slot k2_pa loads ahead
 
+
 // Rank tile t: rows [ti * HB * RTR, +HB * RTR) of the window (RTR keys per thread) against the RJ keys
 // of column tile tj: each row's count of smaller keys is added to its rank (keys are distinct: uids).
 // Wide rows: each column tile's keys are loaded by NRT blocks, not WCAP / HB.
-__device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_t t) {
+// (wr: the rank accumulators of the window's parity, wrank_of)
+__device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_t t, uint32_t *wr) {
   const uint32_t ti = t / NJT, tj = t % NJT;
   __shared__ uint64_t tk[RJ];
   // the window size first: a config-4 window fills ~1/4 of the WCAP x WCAP tiles, and the tiles past
@@ -1091,7 +1127,7 @@ __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_
 #pragma unroll
   for (int r = 0; r < RTR; r++) {
     const uint32_t i = r0 + r * HB + threadIdx.x;
-    if (i < W && c[r]) atomicAdd(&M.wrank[i], c[r]);
+    if (i < W && c[r]) atomicAdd(&wr[i], c[r]);
   }
 }
 
@@ -1585,6 +1621,7 @@ struct nsgpu_p2p {
   uint64_t max_windows = ~0ull;
   hipStream_t s = nullptr;  // engine stream (graph capture and replay)
   hipGraphExec_t gexec = nullptr;
+  hipGraphExec_t gexec_df = nullptr;  // the deferred pipeline's replay (single wide engine, untraced)
   hipEvent_t ev[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr;
   uint32_t *done_host = nullptr;  // pinned, 2 slots
   Ctl *snap = nullptr;            // pinned, 2 run-control snapshots (single engine)
@@ -1635,6 +1672,7 @@ extern "C" int nsgpu_p2p_destroy(nsgpu_p2p *h) {
   if (!h) return NSGPU_OK;
   if (h->s) (void)hipStreamSynchronize(h->s);
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  if (h->gexec_df) (void)hipGraphExecDestroy(h->gexec_df);
   for (hipEvent_t e : {h->ev[0], h->ev[1], h->t0, h->t1})
     if (e) (void)hipEventDestroy(e);
   if (h->done_host) (void)hipHostFree(h->done_host);
@@ -1954,13 +1992,21 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.pwkey, WTOT));
   TRY(dalloc(h, &M.sinfo, WTOT));
   TRY(dalloc(h, &M.widx, WCAP));
-  for (uint32_t **p : {&M.nchild, &M.ninl, &M.pwctx, &M.wrank, &M.wpar}) TRY(dalloc(h, p, WTOT));
+  for (uint32_t **p : {&M.nchild, &M.ninl, &M.pwctx, &M.wpar}) TRY(dalloc(h, p, WTOT));
+  TRY(dalloc(h, &M.wrank, 2 * (size_t)WTOT));  // (by window parity)
   TRY(dalloc(h, &M.lcnt, NLR));
   TRY(dalloc(h, &M.lrec, NMAX));  // (k2_pa loads lrec[k] speculatively: zeroed, every entry stays < WTOT)
   TRY(dalloc(h, &M.lkey, LCAP));
   TRY(dalloc(h, &M.lkw, LCAP));
   TRY(dalloc(h, &M.ldat, LMAX));
-  TRY(dalloc(h, &M.lrank, LMAX));
+  TRY(dalloc(h, &M.lrank, 2 * (size_t)LMAX));
+  // deferred windows (single wide engine): staged records, their leaves, child prefixes, dense map
+  if (M.wide) {
+    TRY(dalloc(h, &M.stage, 2 * (size_t)NMAX));
+    TRY(dalloc(h, &M.sleaf, 2 * (size_t)NMAX * M.maxc));
+    TRY(dalloc(h, &M.cpt, 2 * (size_t)NMAX));
+    TRY(dalloc(h, &M.dmap, LCAP));
+  }
   if (hipMemset(M.lrec, 0, NMAX * sizeof(uint32_t)) != hipSuccess || hipMemset(M.lcnt, 0, NLR * sizeof(uint32_t)) != hipSuccess) {
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipMemset failed");
@@ -2114,8 +2160,8 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.app_last_start, 0, A * sizeof(uint64_t), s));
   NSGPU_HIP(hipMemsetAsync(M.appc, 0, A * sizeof(nsgpu_app_counters), s));
   NSGPU_HIP(hipMemsetAsync(M.node_tab, 0, (size_t)M.n_nodes * NTAB * sizeof(uint32_t), s));
-  NSGPU_HIP(hipMemsetAsync(M.wrank, 0, WTOT * sizeof(uint32_t), s));
-  NSGPU_HIP(hipMemsetAsync(M.lrank, 0, LMAX * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(M.wrank, 0, 2 * WTOT * sizeof(uint32_t), s));
+  NSGPU_HIP(hipMemsetAsync(M.lrank, 0, 2 * LMAX * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.lcnt, 0, NLR * sizeof(uint32_t), s));
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
   if (M.dist) {
@@ -2140,18 +2186,19 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
 
 // The window pipeline, in launch order (graph capture, eager runs and the per-kernel profile).
 namespace {
-constexpr int NKERN = 5;
-const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_rank", "k2_scan", "k_tpatch"};
+constexpr int NKERN = 6;
+const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_rank", "k2_scan", "k_tpatch", "k2_sdef"};
 // ev0 / ev1: optional HIP events the command processor records at the kernel's start and end
 // (hipExtLaunchKernelGGL: no separate marker packets between the pipeline's kernels).
 // Kernel k of the single engine's window (KERNEL_NAMES); a wide engine places its local records after
 // its handlers (k2_rank) and, traced, patches their trace uids (k_tpatch).  Returns
 // whether kernel k is part of this engine's window.
-bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, bool df, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   const bool wide = h->M.wide != 0;
   switch (k) {
     case 0:
-      if (wide) hipExtLaunchKernelGGL((k2_pa<false, true>), dim3(pa_grid<true>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
+      if (df) hipExtLaunchKernelGGL((k2_pa<false, true, true>), dim3(pa_grid<true>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
+      else if (wide) hipExtLaunchKernelGGL((k2_pa<false, true>), dim3(pa_grid<true>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
       else hipExtLaunchKernelGGL((k2_pa<false, false>), dim3(pa_grid<false>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
       return true;
     case 1:
@@ -2160,21 +2207,44 @@ bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, hipEvent_t ev0 = nullptr,
       return true;
     case 2:
       if (!wide) return false;
-      hipExtLaunchKernelGGL(k2_rank, dim3(RK_GRID), dim3(RKT), 0, s, ev0, ev1, 0, h->M);
+      if (df) hipExtLaunchKernelGGL(k2_rank<true>, dim3(RK_GRID), dim3(RKT), 0, s, ev0, ev1, 0, h->M);
+      else hipExtLaunchKernelGGL(k2_rank<false>, dim3(RK_GRID), dim3(RKT), 0, s, ev0, ev1, 0, h->M);
       return true;
     case 3:
+      if (df) return false;  // (the deferred pipeline: df_book in k2_rank, the accounting in k2_sdef)
       if (wide) hipExtLaunchKernelGGL(k2_scan<true>, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
       else hipExtLaunchKernelGGL(k2_scan<false>, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
       return true;
-    default:
+    case 4:
       if (!(wide && h->M.trace)) return false;
       hipExtLaunchKernelGGL(k_tpatch, dim3(64), dim3(256), 0, s, ev0, ev1, 0, h->M);
       return true;
+    default:  // k2_sdef(n) after k2_rank(n + 1): window n was staged by k2_pa(n + 1)
+      if (!df) return false;
+      hipExtLaunchKernelGGL(k2_sdef, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
+      return true;
   }
 }
-void launch_windows(nsgpu_p2p *h, hipStream_t s) {
+void launch_windows(nsgpu_p2p *h, hipStream_t s, bool df) {
   for (int w = 0; w < NWIN; w++)
-    for (int k = 0; k < NKERN; k++) launch_kernel(h, k, s);
+    for (int k = 0; k < NKERN; k++) launch_kernel(h, k, s, df);
+}
+// The deferred pipeline is used for untraced single wide engines (NSGPU_P2P_NODEFER=1: never).
+bool df_usable(const nsgpu_p2p *h) {
+  static const bool off = [] {
+    const char *e = getenv("NSGPU_P2P_NODEFER");
+    return e && e[0] == '1';
+  }();
+  return h->M.wide && !h->M.dist && !h->M.trace && h->M.maxc <= PROV_MAXC && !off;
+}
+// When the deferred pipeline paused itself (a sorted run, a compaction, a host closure) after window n's
+// bookkeeping: window n's dispatch accounting from its records (k2_scan<true, true>: sinfo for the next
+// k2_pa), and every provisional uid still pending resolved (k_xlate); the other pipeline can take over.
+int df_flush(nsgpu_p2p *h, hipStream_t s) {
+  hipLaunchKernelGGL((k2_scan<true, true>), dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
+  hipLaunchKernelGGL(k_xlate, dim3(1024), dim3(256), 0, s, h->M);
+  NSGPU_HIP(hipGetLastError());
+  return NSGPU_OK;
 }
 }  // namespace
 
@@ -2279,14 +2349,15 @@ static int host_step_dist(const Ctl &c, hipStream_t s, X cut, P pass, const Ctl 
   }
 }
 
-static int build_graph(nsgpu_p2p *h) {
+static int build_graph(nsgpu_p2p *h, bool df = false) {
   // NWIN windows of the pipeline; kernels read every run-dependent value from the device (Ctl), so
   // one instantiated graph serves every run of this engine
+  hipGraphExec_t &gx = df ? h->gexec_df : h->gexec;
   hipGraph_t g = nullptr;
   NSGPU_HIP(hipStreamBeginCapture(h->s, h->M.dist ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal));
   int rc = NSGPU_OK;
   if (h->M.dist) rc = launch_windows_dist(h, h->s);
-  else launch_windows(h, h->s);
+  else launch_windows(h, h->s, df);
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (rc != NSGPU_OK || e != hipSuccess) {
     if (g) (void)hipGraphDestroy(g);
@@ -2294,10 +2365,10 @@ static int build_graph(nsgpu_p2p *h) {
     if (rc != NSGPU_OK) return rc;
     return set_error(NSGPU_EHIP, "nsgpu_p2p: graph capture: %s", hipGetErrorString(e));
   }
-  e = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
+  e = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   if (e != hipSuccess) {
-    h->gexec = nullptr;
+    gx = nullptr;
     return set_error(NSGPU_EHIP, "nsgpu_p2p: graph instantiate: %s", hipGetErrorString(e));
   }
   return NSGPU_OK;
@@ -2306,7 +2377,8 @@ static int build_graph(nsgpu_p2p *h) {
 // A run that set the engine's error word: capacity exceeded (the simulation is truncated).
 static int engine_error(uint32_t err) {
   return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, 4 = window limit, "
-                                 "8 = window cut, 16 = a window's remote events beyond the X2 capacity)", err);
+                                 "8 = window cut, 16 = a window's remote events beyond the X2 capacity, 256 = deferred "
+                                 "uid resolution (internal), 512 = uids beyond the deferred pipeline's range)", err);
 }
 
 // Replays the single engine's window pipeline until the run is over (done >= 2) or the pipeline paused
@@ -2317,13 +2389,23 @@ static int drive(nsgpu_p2p *h, bool *paused) {
   *paused = false;
   int cur = 0;
   bool have_prev = false;
+  // the deferred pipeline while the engine runs normal windows; after a pause (which it flushes) the other
+  // pipeline until a replay ends in a normal window
+  const bool dfu = df_usable(h);
+  bool df = dfu;
+  bool df_of[2] = {false, false};
+  if (df && !h->eager && !h->gexec_df) {
+    const int rc = build_graph(h, true);
+    if (rc) return rc;
+  }
   for (;;) {
     if (h->eager) {
-      launch_windows(h, h->s);
+      launch_windows(h, h->s, df);
       NSGPU_HIP(hipGetLastError());
     } else {
-      NSGPU_HIP(hipGraphLaunch(h->gexec, h->s));
+      NSGPU_HIP(hipGraphLaunch(df ? h->gexec_df : h->gexec, h->s));
     }
+    df_of[cur] = df;
     NSGPU_HIP(hipMemcpyAsync(&h->snap[cur], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
     NSGPU_HIP(hipEventRecord(h->ev[cur], h->s));
     if (have_prev) {
@@ -2332,6 +2414,15 @@ static int drive(nsgpu_p2p *h, bool *paused) {
       if (c.done >= 2) break;  // 2: the final window is appended
       if (c.mode >= MODE_SORT) {
         NSGPU_HIP(hipEventSynchronize(h->ev[cur]));
+        if (df_of[cur ^ 1]) {  // (the pause came from the deferred pipeline: its last window is not accounted yet)
+          int rc = df_flush(h, h->s);
+          if (!rc) {
+            NSGPU_HIP(hipMemcpyAsync(&h->snap[cur], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+            NSGPU_HIP(hipStreamSynchronize(h->s));
+          }
+          if (rc) return rc;
+        }
+        df = false;
         if (h->snap[cur].mode == MODE_HOST) {
           *paused = true;
           break;
@@ -2340,6 +2431,13 @@ static int drive(nsgpu_p2p *h, bool *paused) {
         if (rc) return rc;
         have_prev = false;
         continue;
+      }
+      if (!df && dfu) {  // a normal window ended the replay: back to the deferred pipeline
+        if (!h->eager && !h->gexec_df) {
+          const int rc = build_graph(h, true);
+          if (rc) return rc;
+        }
+        df = true;
       }
     }
     have_prev = true;
@@ -2575,6 +2673,10 @@ extern "C" int nsgpu_p2p_set_trace(nsgpu_p2p *h, uint64_t cap) {
     (void)hipGraphExecDestroy(h->gexec);
     h->gexec = nullptr;
   }
+  if (h->gexec_df) {  // (traced engines run the other pipeline)
+    (void)hipGraphExecDestroy(h->gexec_df);
+    h->gexec_df = nullptr;
+  }
   return NSGPU_OK;
 }
 
@@ -2651,13 +2753,15 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
     rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: stream join failed");
   int ns = 0;
   bool used[NKERN] = {};  // the engine's window launches kernel k (its events are recorded)
+  const bool dfu = df_usable(h);
+  bool df = dfu;
   // the run control is read after every window (so no sampled pass is a paused no-op and the
   // host-driven steps run as soon as the pipeline asks)
   for (uint64_t w = 0; rc == NSGPU_OK; w++) {
     const bool sample = (w % sample_every) == 0 && ns < NS;
     for (int k = 0; k < NKERN; k++) {
-      if (sample) used[k] = launch_kernel(h, k, h->s, ev[(2 * ns) * NKERN + k], ev[(2 * ns + 1) * NKERN + k]);
-      else launch_kernel(h, k, h->s);
+      if (sample) used[k] |= launch_kernel(h, k, h->s, df, ev[(2 * ns) * NKERN + k], ev[(2 * ns + 1) * NKERN + k]);
+      else launch_kernel(h, k, h->s, df);
     }
     if (sample) ns++;
     if (hipGetLastError() != hipSuccess) {
@@ -2670,7 +2774,18 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
       break;
     }
     if (h->snap[0].done >= 2) break;  // the final window is appended
-    if (h->snap[0].mode >= MODE_SORT) rc = host_step(h, h->snap[0], h->s);
+    if (h->snap[0].mode >= MODE_SORT) {
+      if (df) {  // (the deferred pipeline paused: flush its last window first)
+        rc = df_flush(h, h->s);
+        if (rc == NSGPU_OK && (hipMemcpyAsync(&h->snap[0], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s) != hipSuccess ||
+                               hipStreamSynchronize(h->s) != hipSuccess))
+          rc = set_error(NSGPU_EHIP, "nsgpu_p2p_profile: sync failed");
+        df = false;
+      }
+      if (rc == NSGPU_OK) rc = host_step(h, h->snap[0], h->s);
+    } else if (!df && dfu) {
+      df = true;
+    }
   }
   if (rc == NSGPU_OK) {
     for (int i = 0; i < ns; i++)

@@ -44,6 +44,11 @@ constexpr int NMAX = 8192;               // records of one window, gen-0 + local
 constexpr int LMAX = NMAX - WCAP;        // local records of one window
 constexpr int SLOTG = WCAP + LMAX;       // k2_pa's slot-role threads (single engine): gen-0 slots, then local
 static_assert(LCAP < (1 << 24) && WTOT < (1 << 24), "wpar packs a record index in 24 bits");
+// Rank accumulators of window `win` (by parity: a deferred window's ranks are read after the next window's
+// ranking has begun).  wrank: 2 x WTOT, lrank: 2 x LMAX.
+__device__ __forceinline__ uint32_t *wrank_of(const P2PDev &M, uint64_t win) { return M.wrank + (win & 1) * WTOT; }
+__device__ __forceinline__ uint32_t *lrank_of(const P2PDev &M, uint64_t win) { return M.lrank + (win & 1) * LMAX; }
+
 __device__ __forceinline__ uint32_t region_base(uint32_t r) {
   return LBASE + (r < (uint32_t)NHB ? r * LR : NHB * LR + (r - NHB) * LRH);
 }
@@ -83,16 +88,24 @@ __device__ __forceinline__ void slot_done(const P2PDev &M, uint32_t s, uint64_t 
                                           X1Acc &xa) {
   M.nchild[s] = n;
   M.ninl[s] = ni;
+  xa.tc += n;  // (the window's totals: a partitioned rank's X1 summary, the single engine's k2_rank bookkeeping)
+  xa.ti += ni;
   if (M.dist) {
     x1ent(M.x1_send, 0)[s] = X1Ent{key, n | (ni << 16), 0};
-    xa.tc += n;
-    xa.ti += ni;
     xa.lk = key > xa.lk ? key : xa.lk;
   }
 }
 // All lanes of the wave call it.
 __device__ __forceinline__ void x1_totals(const P2PDev &M, X1Acc xa) {
-  if (!M.dist) return;
+  if (!M.dist) {  // single engine: the window's child totals (the deferred bookkeeping advances uid / K by them)
+    xa.tc = wave_sum32(xa.tc);
+    xa.ti = wave_sum32(xa.ti);
+    if ((threadIdx.x & 63) == 0) {
+      if (xa.tc) atomicAdd((unsigned long long *)&M.C->acc_tc, (unsigned long long)xa.tc);
+      if (xa.ti) atomicAdd((unsigned long long *)&M.C->acc_tinl, (unsigned long long)xa.ti);
+    }
+    return;
+  }
   xa.tc = wave_sum32(xa.tc);
   xa.ti = wave_sum32(xa.ti);
   xa.lk = wave_max64(xa.lk);
@@ -328,9 +341,13 @@ constexpr int pa_grid() {
   constexpr int nsg = WIDE ? SLOTG : WCAP;
   return nsg / PA_SLOT_LANES + GRID_POOL - nsg / TB;
 }
-template <bool DIST, bool WIDE>
+// DF: the deferred pipeline's variant (single wide engine): when the last window is staged (C.pdf) its records
+// are written in rank order to the stage for k2_sdef and its children get provisional uids (no dispatch log
+// here); the pool's provisional uids of the window before it are resolved as the pool is read.
+template <bool DIST, bool WIDE, bool DF = false>
 __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   static_assert(!(DIST && WIDE), "wide windows are the single engine's");
+  static_assert(!DF || WIDE, "deferred windows are the wide engine's");
   PH_BEGIN();
   BLK_T0();
   Ctl &C = *M.C;
@@ -356,6 +373,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const Red red0 = C.red[0], red1 = C.red[1];
   const uint64_t hts = C.hts, c_ptmin = C.ptmin, K0 = C.pK0, ilim = C.pinline_lim, c_P = C.P_end;
   const uint64_t c_span_t = WIDE ? C.span_t : 0;
+  const uint32_t c_pdf = DF ? C.pdf : 0u;
+  const uint64_t c_wn = DF ? C.windows : 0;  // (this window's index: the last one is c_wn - 1)
+  const uint32_t xw_uid0 = DF ? C.winfo[(c_wn + 2) & 3].uid0 : 0u;  // (window c_wn - 2: the pool's provisional uids)
   uint64_t spk = 0;
   uint4 si = make_uint4(0, 0, 0, 0);
   uint32_t ncr = 0, sctx = 0;
@@ -366,14 +386,28 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 #pragma unroll
   for (int q = 0; q < NPEND; q++) pend[q] = NtClaim{0, NOSRC, 0};
   // the record this slot-role thread appends: gen-0 slot g, or local record lrec[g - WCAP] (lrec holds
-  // record indices from earlier windows past C.plt: loaded speculatively, always in range)
-  const uint32_t rec = (WIDE && g >= (uint64_t)WCAP && slot_role) ? M.lrec[g - WCAP] : (uint32_t)g;
+  // record indices from earlier windows past C.plt: loaded speculatively, always in range).  DF: the dense
+  // local entry ldat (record, child counts, rel ts, parent) instead, and both parities' rank accumulators
+  uint4 ldd = make_uint4((uint32_t)g, 0, 0, 0);
+  uint32_t rk2[2] = {0, 0}, ninl0 = 0;
+  if (DF && WIDE && g >= (uint64_t)WCAP && slot_role) ldd = M.ldat[g - WCAP];
+  const uint32_t rec = (WIDE && g >= (uint64_t)WCAP && slot_role) ? (DF ? ldd.x : M.lrec[g - WCAP]) : (uint32_t)g;
   if (slot_role) {  // the slot and its first children
     const uint32_t s = rec;
     spk = M.pwkey[s];
     si = M.sinfo[s];
     ncr = M.nchild[s];
     sctx = M.pwctx[s];
+    if (DF) {
+      if (g < (uint64_t)WCAP) {
+        rk2[0] = M.wrank[g];
+        rk2[1] = M.wrank[WTOT + g];
+        ninl0 = M.ninl[g];
+      } else {
+        rk2[0] = M.lrank[g - WCAP];
+        rk2[1] = M.lrank[LMAX + g - WCAP];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < PFC; j++) {
       const uint32_t sl = s * M.maxc + j;
@@ -411,6 +445,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       }
     }
   }
+  if (DF && g == 0 && c_pdf && c_pvalid && !run) C.sflag = 1u | (uint32_t)(((c_wn - 1) & 3) << 1);  // (k2_sdef's)
   if (!run && partition && g == 0) {
     publish_bound(C, b);
     if (WIDE && M.trace) C.tn0 = *M.trace_n;  // (the local records' trace uids are patched from here on)
@@ -430,10 +465,23 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     // ---- record `rec` of the last window: dispatch rank (log, digest), inline children, children -> pending
     const bool vs = slot_role && (g < (uint64_t)WCAP ? g < pW : (c_pvalid && g - WCAP < c_plt));
     const uint32_t s = rec;
-    const uint64_t rel = spk >> 32;
+    const bool loc = WIDE && g >= (uint64_t)WCAP;
+    const bool stg = DF && c_pdf;  // the last window is staged for k2_sdef (deferred dispatch accounting)
+    const uint64_t rel = (stg && loc) ? (uint64_t)ldd.z : spk >> 32;
     const uint64_t t = c_ptmin + rel;
+    const uint32_t pn = (uint32_t)((c_wn - 1) & 1);  // (DF: the last window's parity)
+    const uint32_t srank = rk2[pn];
     BLK_MARK(34, c_win);  // bound, publish_bound
-    if (vs) {
+    if (stg && vs && srank >= (uint32_t)NMAX) atomicOr(M.error, 256u);
+    if (stg && vs && srank < (uint32_t)NMAX) {  // the record at its rank (k2_sdef logs it and resolves its uid)
+      Stg st;
+      st.key = loc ? (rel << 32) : spk;
+      st.ctx = sctx;
+      st.cnt = loc ? ldd.y : (ncr | (ninl0 << 16));
+      st.par = loc ? ldd.w : 0u;
+      st.loc = loc ? 1u : 0u;
+      M.stage[(uint64_t)pn * NMAX + srank] = st;
+    } else if (vs) {
       const uint64_t rk = K0 + si.x;
       digest += digest_term(rk, t, (uint32_t)spk);
       if (rk < M.log_cap) {
@@ -466,9 +514,14 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
             const uint32_t sl = s * M.maxc + j;
             e = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
           }
-          e.uid = uid0 + si.z + j;
+          e.uid = stg ? prov_uid(c_wn - 1, srank, j) : uid0 + si.z + j;
           if ((e.kind & 0xffu) == K_FWD_UP) {  // leaf: dispatched inside its window (or never), not queued
-            if (rel < ilim) {
+            if (stg) {
+              if (rel < ilim && srank < (uint32_t)NMAX) {  // (k2_sdef logs it after its group)
+                M.sleaf[((uint64_t)pn * NMAX + srank) * M.maxc + ii] = make_uint2(e.ctx, j);
+                ii++;
+              }
+            } else if (rel < ilim) {
               const uint64_t crk = K0 + si.y + ii;
               digest += digest_term(crk, t, e.uid);
               if (crk < M.log_cap) {
@@ -539,6 +592,19 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
         // so the window entries' second load costs no window time, and the pool's other 24 B a slot
         // are not fetched for the rest)
         if (i < P) ge[q] = Ev{M.ev_ts[0][i], M.ev_uid[0][i], 0, M.ev_kind[0][i], 0, Pkt{0, 0, 0, 0}};
+      }
+      if (DF) {  // children the window before the last one parked: their uids resolve now (k2_sdef ran for it)
+#pragma unroll
+        for (int q = 0; q < PPT; q++) {
+          const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
+          const uint32_t u = ge[q].uid;
+          if (ge[q].ts != TOMB && (u & PROV)) {
+            const uint32_t tag = (u >> 30) & 1u;
+            if (tag != (uint32_t)(c_wn & 1)) atomicOr(M.error, 256u);
+            ge[q].uid = xw_uid0 + M.cpt[(uint64_t)tag * NMAX + ((u & 0x3fffffffu) >> 8) % NMAX] + (u & 0xffu);
+            M.ev_uid[0][i] = ge[q].uid;
+          }
+        }
       }
 #pragma unroll
       for (int q = 0; q < PPT; q++) {
@@ -631,7 +697,8 @@ __device__ __forceinline__ uint64_t lk_word2(const LKey &k) {
   if (k.depth == 1) return ((uint64_t)k.uid << 8) | k.j[0];
   const bool g2 = k.depth == 2;  // (the grandparent is the gen-0 ancestor)
   const uint32_t r2 = k.rel[2] < 0x7fffffffu ? k.rel[2] : 0x7fffffffu;
-  const uint32_t nx = g2 ? k.uid : k.rel[3];
+  // (a provisional uid, deferred windows: above every real one, squeezed into the field's top 2^21 values)
+  const uint32_t nx = g2 ? ((k.uid & PROV) ? 0x3fe00000u | (k.uid & 0x1fffffu) : k.uid) : k.rel[3];
   return (1ull << 63) | ((uint64_t)r2 << 31) | ((g2 ? 0ull : 1ull) << 30) | (nx < 0x3fffffffu ? nx : 0x3fffffffu);
 }
 // The local record of child E.lj of record `par` (a same-node TransmitComplete inside a wide window, marked
@@ -1646,6 +1713,7 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_wbase = C.wbase, c_fr = C.force_run, rt = C.rt,
                  c_nhub = C.nhub;
   const HCtl hc{C.tmin, C.inline_lim, C.split_lo, C.split_hi, C.lim_rel};
+  const uint64_t c_wn = C.windows;
   __shared__ uint32_t s_lcnt;  // local records this block made (its region's count, wide windows)
   if (threadIdx.x == 0) s_lcnt = 0;
   const uint64_t c_nfree = C.nfree, c_nF = C.nF, c_Pe = C.P_end;
@@ -1669,6 +1737,7 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   }
   if (c_done || c_mode >= MODE_SORT || ovf) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+      C.rk_go = 0;  // (k2_rank: nothing to rank or account)
       if (c_done == 1) C.done = 2;  // the final window is appended
       if (M.dist) {
         C.hdl = 0;  // (k_gtile / k_dfin2: nothing ran)
@@ -1693,6 +1762,12 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   const uint32_t base = run ? c_wbase : 0;
   const bool handle = run || (W <= (uint32_t)WCAP && !c_fr);
   Red &R = M.dist ? x1hdr(M.x1_send, 0)->red : C.red[rt];
+  if (WIDE && bx == 0 && threadIdx.x == 0) {  // what k2_rank ranks and accounts (its bookkeeping rewrites C.W ...)
+    C.rk_W = W;
+    C.rk_go = 2u | ((handle && !run) ? 1u : 0u);  // 2: a window was formed; 1: handled normally (ranked)
+    C.rk_win = c_wn;
+    C.rk_lim = hc.lim;
+  }
   PH_MARK(8);
   __syncthreads();  // (s_lcnt)
   if (bx < (uint32_t)NHB) {
@@ -1706,11 +1781,11 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   } else if (bx < (uint32_t)K2_GRID_W) {
     maintain(M, C, bx - (NHB + NHUB), run, handle, W, c_nfree, c_nF, c_Pe);
   } else {
-    if (!run && handle && !M.dist) rank_tile(M, C, bx - K2_GRID_W);  // (keys known before the handlers run)
+    if (!run && handle && !M.dist) rank_tile(M, C, bx - K2_GRID_W, wrank_of(M, c_wn));  // (keys known before the handlers run)
   }
-  if (WIDE && hc.lim && bx < (uint32_t)NLR) {  // this block's local region count (k2_scan reads it)
-    __syncthreads();
-    if (threadIdx.x == 0 && s_lcnt) {
+  if (WIDE && hc.lim && bx < (uint32_t)NLR) {  // this block's local region count (k2_rank / k2_scan read it;
+    __syncthreads();                               //  written even when 0: the deferred pipeline keeps no reset)
+    if (threadIdx.x == 0) {
       const uint32_t cap = bx < (uint32_t)NHB ? (uint32_t)LR : (uint32_t)LRH;
       M.lcnt[bx] = s_lcnt < cap ? s_lcnt : cap;
     }
@@ -1776,6 +1851,13 @@ __device__ __forceinline__ bool lk_before(const LKey &a, const LKey &b) {
 // chain compare runs after the tile, only for rows whose words tie with a distinct record's (chains of 3+
 // levels with equal ts pairs).
 constexpr int RKC = 64;  // columns per tile
+template <int NT>
+__device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32_t Lt, uint64_t wn);
+// DF: the deferred pipeline's variant: it reads k2_handle's snapshot (rk_*), always runs for a formed window,
+// copies the window's keys / contexts for the next k2_pa (pwkey / pwctx: k2_scan's job in the other
+// pipeline), and its block 0 does the window's bookkeeping (df_book); the dispatch accounting (log, digest,
+// uid resolution) is deferred to k2_sdef once the next k2_pa has staged the records in rank order.
+template <bool DF>
 __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
   Ctl &C = *M.C;
   BLK_T0();
@@ -1783,15 +1865,39 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
   const uint64_t c_win = C.windows;
   uint32_t n_tie = 0;
 #endif
-  const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run;
-  const uint64_t lim = C.lim_rel;
+  uint32_t c_done = 0, c_mode = 0, W, c_fr = 0, go = 3;
+  uint64_t lim, wn;
+  if (DF) {
+    go = C.rk_go, W = C.rk_W, lim = C.rk_lim, wn = C.rk_win;
+  } else {
+    c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run, lim = C.lim_rel, wn = C.windows;
+  }
   const uint32_t lc = threadIdx.x < (uint32_t)NLR ? M.lcnt[threadIdx.x] : 0u;  // (its trip overlaps the control's)
-  if (c_done || c_mode >= MODE_SORT || c_mode == MODE_RUN || W > (uint32_t)WCAP || c_fr || lim == 0) return;
+  if (DF) {
+    if (!(go & 2u)) return;  // (no window was formed: the run is over or paused)
+  } else if (c_done || c_mode >= MODE_SORT || c_mode == MODE_RUN || W > (uint32_t)WCAP || c_fr || lim == 0) {
+    return;
+  }
+  const bool ranked = (go & 1u) != 0;
   __shared__ uint32_t pre[NLR + 1];
   __shared__ ulonglong2 cw[RKC];
-  local_prefix<RKT>(lc, pre);
+  local_prefix<RKT>((ranked && lim) ? lc : 0u, pre);
   const uint32_t Lt = pre[NLR], N = W + Lt;
-  if (Lt == 0 || N > (uint32_t)NMAX || Lt > (uint32_t)LMAX) return;  // (too many: k2_scan fails the run, error 64)
+  uint32_t *const wr = wrank_of(M, wn), *const lr = lrank_of(M, wn);
+  uint32_t b0 = blockIdx.x, nb = gridDim.x;  // (DF: block 0 keeps the books, the others rank)
+  if (DF) {
+    if (blockIdx.x == 0) {
+      df_book<RKT>(M, C, ranked, W, Lt, wn);
+      return;
+    }
+    if (!ranked) return;
+    b0 -= 1, nb -= 1;
+    for (uint32_t i = b0 * RKT + threadIdx.x; i < W; i += nb * RKT) {  // (the next k2_pa rewrites wkey / wctx)
+      M.pwkey[i] = M.wkey[i];
+      M.pwctx[i] = M.wctx[i];
+    }
+  }
+  if (Lt == 0 || N > (uint32_t)NMAX || Lt > (uint32_t)LMAX) return;  // (too many: the bookkeeping fails the run, error 64)
 #ifdef NSGPU_PHASE_PROF
   if (c_win == g_blk_win && blockIdx.x == 0 && threadIdx.x == 0) {
     g_phase[57] = N;
@@ -1802,7 +1908,7 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
   const uint32_t nr = (N + RKT - 1) / RKT, ncl = (Lt + RKC - 1) / RKC;  // phase A: rows x local columns
   const uint32_t nl = (Lt + RKT - 1) / RKT, ncg = (W + RKC - 1) / RKC;  // phase B: local rows x gen-0 columns
   const uint32_t na = nr * ncl;
-  for (uint32_t t = blockIdx.x; t < na + nl * ncg; t += gridDim.x) {  // (uniform over the block)
+  for (uint32_t t = b0; t < na + nl * ncg; t += nb) {  // (uniform over the block)
     uint32_t c = 0, slot = 0;  // slot: the row's accumulator (wrank[dense] for gen-0, LBASE + k for local k)
     if (t < na) {  // rows: every record; columns: local records
       const uint32_t ti = t / ncl, tj = t % ncl;
@@ -1817,6 +1923,7 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
             M.ldat[cy] = make_uint4(r, M.nchild[r] | (M.ninl[r] << 16), (uint32_t)(w.x >> 32), M.wpar[r]);
             M.lrec[cy] = r;
             M.pwctx[r] = M.wctx[r];
+            if (DF) M.dmap[r - LBASE] = cy;  // (k2_sdef: a local parent's rank)
           }
         }
         cw[threadIdx.x] = w;
@@ -1876,7 +1983,7 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
       slot = ix + LBASE;
     }
     BLK_MARK(52, c_win);
-    if (c) atomicAdd(slot >= LBASE ? &M.lrank[slot - LBASE] : &M.wrank[slot], c);
+    if (c) atomicAdd(slot >= LBASE ? &lr[slot - LBASE] : &wr[slot], c);
     __syncthreads();
     BLK_MARK(54, c_win);
   }
@@ -1889,12 +1996,262 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
 #endif
 }
 
+// The deferred pipeline's window bookkeeping (k2_rank<true>'s block 0; NT threads): k2_scan's run
+// bookkeeping without its scan — the child totals come from k2_handle (acc_tc / acc_tinl), the dispatch
+// bases of the window go to winfo for k2_sdef, and the next k2_pa stages the window (pdf = 1).  The
+// free-stack move and the hub resets are the block's; the rest is thread 0's.
+template <int NT>
+__device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32_t Lt, uint64_t wn) {
+  const int tid = threadIdx.x;
+  const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
+  const uint32_t c_nhub = C.nhub;
+  const uint64_t consumed = nF < nfree ? nF : nfree;
+  const uint64_t mv = consumed < npush ? consumed : npush;
+  // the free stack loses the slots the fresh children took and gains the window's (disjoint ranges)
+  for (uint64_t i = tid; i < mv; i += NT) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
+  if (ranked) {
+    const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
+    for (uint32_t h = tid; h < nh; h += NT) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
+  }
+  if (tid != 0) return;
+  const uint64_t tc = C.acc_tc, tinl = C.acc_tinl;
+  C.acc_tc = 0;
+  C.acc_tinl = 0;
+  const uint64_t live = C.live, P_end = C.P_end;
+  C.nfree = nfree - consumed + npush;
+  const uint64_t P_end2 = P_end + (nF > nfree ? nF - nfree : 0);
+  const uint64_t live2 = live - npush + nF;
+  C.P_end = P_end2;
+  C.live = live2;
+  C.npush = 0;
+  C.nF = 0;
+  C.nhub = 0;
+  C.force_run = 0;
+  const uint64_t c_bound = C.bound, c_nbound = C.nbound;
+  if (!ranked) {  // the window overflowed: a sorted run (host radix sort), nothing dispatched (k2_scan's branch)
+    C.rW = W;
+    C.r0 = 0;
+    C.W = 0;
+    C.pvalid = 0;
+    C.refits++;
+    C.renarrow = c_nbound < c_bound ? 1u : 0u;
+    if (c_nbound < c_bound) C.span_t = ((c_bound >> 32) >> 1) + 1;
+    C.mode = MODE_SORT;
+    return;
+  }
+  const uint32_t N = W + Lt;
+  if (N > (uint32_t)NMAX || Lt > (uint32_t)LMAX) {  // (the adaptive span keeps windows well inside)
+    atomicOr(M.error, 64u);
+    C.done = 1;
+    return;
+  }
+  const uint64_t K = C.K, tmin = C.tmin, ilim = C.inline_lim, windows = C.windows, span_t = C.span_t;
+  const uint32_t uid = C.uid, rt = C.rt;
+  C.winfo[wn & 3] = WInfo{K, tmin, ilim, uid, N, W, Lt};
+  C.pK0 = K;
+  C.puid0 = uid;
+  C.ptmin = tmin;
+  C.pinline_lim = ilim;
+  C.pW = W;
+  C.plt = Lt;
+  C.pinl = (uint32_t)tinl;
+  C.pvalid = 1;
+  C.pdf = 1;
+  C.K = K + N + tinl;
+  C.uid = uid + (uint32_t)tc;
+  const uint64_t pchild = tc - tinl - Lt;  // (the local records' uids were consumed, they ran in the window)
+  C.pchild = pchild;
+  bool done = C.stop_seen || (live2 + pchild == 0 && C.hts == ~0ull);
+  if ((uint64_t)uid + tc >= (uint64_t)UID_DF_LIMIT) {  // (provisional uids must stay above every real one)
+    atomicOr(M.error, 512u);
+    done = true;
+  }
+  const uint64_t span = c_bound >> 32;  // wide windows: keep them inside the window capacity
+  if (N > (uint32_t)(7 * NMAX / 8) || W > (uint32_t)(7 * WCAP / 8)) C.span_t = span - span / 4;
+  else if (N < (uint32_t)(3 * NMAX / 4) && W < (uint32_t)(3 * WCAP / 4) && span_t < (1ull << 40))
+    C.span_t = span_t + span_t / 8 + 1;
+  C.red[rt ^ 1].tmin = C.red[rt ^ 1].wend = C.red[rt ^ 1].stopts = C.red[rt ^ 1].wendw = ~0ull;  // consumed
+  C.rt = rt ^ 1;
+  C.windows = windows + 1;
+  if (N > C.max_window) C.max_window = N;
+  C.W = 0;
+  if (P_end2 > M.pool_cap) {
+    atomicOr(M.error, 1u);
+    done = true;
+  }
+  if (windows + 1 >= C.max_windows && !done) {
+    atomicOr(M.error, 4u);
+    done = true;
+  }
+  if (done) {
+    C.done = 1;
+  } else if (C.hcap) {  // the window was cut at the next host closure: pause
+    C.hcap = 0;
+    C.mode = MODE_HOST;
+  } else if (P_end2 > 65536 && live2 * 4 < P_end2) {
+    C.mode = MODE_COMPACT;
+  }
+}
+
+// ---- k2_sdef: a deferred window's dispatch accounting (DF pipeline; one block) ----
+// Window n's records, staged in rank order by the next k2_pa: exclusive scans of (children, inline children,
+// same-ts group heads) give each record its dispatch rank (K0 + rank + the inline leaves of earlier ts groups)
+// and child prefix; a record's own uid resolves (a provisional one through window n-1's prefixes, a local
+// record's through its parent's rank and this window's prefixes); the log and digest get every record and
+// leaf; the child prefixes are kept (cpt) for the provisional uids of window n's children.  Afterwards the
+// window's rank accumulators are cleared (their parity is window n + 2's).
+__global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
+  Ctl &C = *M.C;
+  const uint32_t sf = C.sflag;
+  if (!(sf & 1u)) return;
+  const uint32_t wi = (sf >> 1) & 3u, pn = wi & 1u;  // window n & 3, its parity
+  const WInfo w = C.winfo[wi];
+  const uint32_t uidq = C.winfo[(wi + 3) & 3].uid0;  // window n - 1's uid base
+  const uint32_t N = w.N;
+  constexpr int RPT = NMAX / SCAN_THREADS;
+  __shared__ uint32_t s_cp[NMAX];   // child prefix by rank
+  __shared__ uint32_t s_ip[NMAX];   // inline prefix by rank
+  __shared__ uint32_t s_gs[NMAX];   // start rank of each ts group
+  __shared__ uint64_t wsum[SCAN_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const Stg *st = M.stage + (uint64_t)pn * NMAX;
+  // the scan's fields in registers (rel ts, counts); the rest is read again for the outputs (L2 hits)
+  uint32_t erel[RPT], ecnt[RPT];
+  uint32_t prev_rel = 0;
+  if (tid * RPT > 0 && (uint32_t)(tid * RPT) <= N) prev_rel = (uint32_t)(st[tid * RPT - 1].key >> 32);
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    erel[q] = ecnt[q] = 0;
+    if (r < N) {
+      erel[q] = (uint32_t)(st[r].key >> 32);
+      ecnt[q] = st[r].cnt;
+    }
+  }
+  uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
+  {
+    uint32_t pr = prev_rel;
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+      const uint32_t r = tid * RPT + q;
+      if (r < N) {
+        const uint32_t rel = erel[q];
+        const uint32_t hd = r == 0 || rel != pr;
+        pr = rel;
+        sum += (uint64_t)(ecnt[q] & 0xffffu) | ((uint64_t)(ecnt[q] >> 16) << 21) | ((uint64_t)hd << 42);
+      }
+    }
+  }
+  uint64_t inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t x = __shfl_up(inc, o);
+    if (lane >= o) inc += x;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+  for (int k = 0; k < SCAN_THREADS / 64; k++) {
+    const uint64_t x = wsum[k];
+    off += k < wid ? x : 0;
+    tot += x;
+  }
+  const uint64_t ex = off + inc - sum;
+  const uint32_t tinl = (uint32_t)((tot >> 21) & 0x1fffffu), ng = (uint32_t)(tot >> 42);
+  uint32_t bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu), bh = (uint32_t)(ex >> 42);
+  uint32_t cpr[RPT], ipr[RPT], grp[RPT];
+  {
+    uint32_t pr = prev_rel;
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+      const uint32_t r = tid * RPT + q;
+      uint32_t hd = 0;
+      if (r < N) {
+        const uint32_t rel = erel[q];
+        hd = r == 0 || rel != pr;
+        pr = rel;
+      }
+      bh += hd;
+      grp[q] = bh - 1;
+      cpr[q] = bc;
+      ipr[q] = bi;
+      if (r < N) {
+        s_cp[r] = bc;
+        s_ip[r] = bi;
+        if (hd) s_gs[bh - 1] = r;
+        M.cpt[(uint64_t)pn * NMAX + r] = bc;
+        bc += ecnt[q] & 0xffffu;
+        bi += ecnt[q] >> 16;
+      }
+    }
+  }
+  __syncthreads();
+  // own uids, log and digest (records at K0 + rank + the leaves of earlier groups; leaves after their group)
+  const uint32_t *const wr = M.wrank + (uint64_t)pn * WTOT, *const lr = M.lrank + (uint64_t)pn * LMAX;
+  const uint32_t *const cq = M.cpt + (uint64_t)(pn ^ 1u) * NMAX;
+  uint64_t digest = 0;
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    if (r >= N) continue;
+    const Stg e = st[r];
+    const uint32_t rel = erel[q];
+    const uint64_t t = w.tmin + rel;
+    uint32_t uid = (uint32_t)e.key;
+    if (e.loc) {  // a local record: its parent's child prefix + its child index
+      const uint32_t p = e.par & 0xffffffu, j = e.par >> 24;
+      uint32_t rp = p < LBASE ? wr[p] : (p - LBASE < (uint32_t)LCAP ? lr[M.dmap[p - LBASE] % LMAX] : ~0u);
+      if (rp >= N) {  // (cannot happen: the parent is a record of this window)
+        atomicOr(M.error, 256u);
+        rp = 0;
+      }
+      uid = w.uid0 + s_cp[rp] + j;
+    } else if (uid & PROV) {  // a child of window n - 1
+      if (((uid >> 30) & 1u) != (pn ^ 1u)) atomicOr(M.error, 256u);
+      uid = uidq + cq[((uid & 0x3fffffffu) >> 8) % NMAX] + (uid & 0xffu);
+    }
+    const uint32_t g = grp[q];
+    const uint32_t first = s_gs[g];
+    const uint32_t last = (g + 1 < ng ? s_gs[g + 1] : N) - 1;
+    const uint64_t rk = w.K0 + r + (tinl ? s_ip[first] : 0u);
+    digest += digest_term(rk, t, uid);
+    if (rk < M.log_cap) {
+      M.log_ts[rk] = t;
+      M.log_uid[rk] = uid;
+      M.log_ctx[rk] = e.ctx;
+    }
+    const uint32_t ni = ecnt[q] >> 16;
+    const uint2 *lf = M.sleaf + ((uint64_t)pn * NMAX + r) * M.maxc;
+    for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
+      const uint2 l = lf[k];
+      const uint64_t lk = w.K0 + last + 1 + ipr[q] + k;
+      const uint32_t lu = w.uid0 + cpr[q] + l.y;
+      digest += digest_term(lk, t, lu);
+      if (lk < M.log_cap) {
+        M.log_ts[lk] = t;
+        M.log_uid[lk] = lu;
+        M.log_ctx[lk] = l.x;
+      }
+    }
+    if (r == N - 1) C.last_ts = t;
+  }
+  digest = wave_sum64(digest);
+  __syncthreads();  // (every lookup of the rank accumulators is done: clear them for window n + 2)
+  if (lane == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
+  for (uint32_t i = tid; i < w.W; i += SCAN_THREADS) M.wrank[(uint64_t)pn * WTOT + i] = 0;
+  for (uint32_t i = tid; i < w.Lt; i += SCAN_THREADS) M.lrank[(uint64_t)pn * LMAX + i] = 0;
+  if (tid == 0) C.sflag = 0;
+}
+
 // ---- k2_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
 // WIDE: the single engine's wide windows: the local records join the gen-0 ones (ranks from k2_rank), and
 // a local record's uid is its parent's child prefix + its child index (DefaultSimulatorImpl gives uids in
 // Schedule order).
-template <bool WIDE>
+// FL: the flush of a deferred window (host step, when the deferred pipeline paused after window n's
+// bookkeeping): the same scan from the records, into sinfo / pwkey for the next k2_pa's appending, with
+// window n's bases from winfo and its provisional uids resolved; no run bookkeeping (df_book did it).
+template <bool WIDE, bool FL = false>
 __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
+  static_assert(!FL || WIDE, "flushes are the deferred pipeline's");
   Ctl &C = *M.C;
   // one thread per RPT records (dense order: the W gen-0 slots, then the local records region by region);
   // the rank-ordered arrays hold NREC records (wide: 128 KB of LDS)
@@ -1912,8 +2269,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
 #endif
   const int tid = threadIdx.x;
   // the run control and the window's slots (speculatively at base 0), all loaded at once
-  const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_fr = C.force_run, c_wbase = C.wbase;
-  const uint32_t c_nhub = C.nhub, uid0 = C.uid;
+  const uint64_t c_wn = C.windows;  // (FL: df_book counted window n already)
+  const uint32_t c_done = C.done, c_mode = C.mode, W = FL ? C.pW : C.W, c_fr = FL ? 0u : C.force_run,
+                 c_wbase = C.wbase;
+  const uint32_t c_nhub = C.nhub, c_pvalid = C.pvalid, c_pdf = C.pdf;
+  const WInfo wif = C.winfo[(c_wn + 3) & 3];  // (FL: window n = c_wn - 1)
+  const uint32_t uid0 = FL ? wif.uid0 : C.uid;
   const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush, c_lim = C.lim_rel, c_bound = C.bound,
                  c_nbound = C.nbound, c_r0 = C.r0, c_rW = C.rW;
   const uint32_t c_rtrim = C.rtrim;
@@ -1931,16 +2292,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   // parent's rank | child index << 16
   // Slot q of a thread: q < RPT0 the gen-0 slot i = tid + q * SCAN_THREADS (dense index i), q >= RPT0 (wide)
   // the local record k = i - WCAP of k2_rank's dense list (dense index W + k); both loaded speculatively.
-  uint32_t pr[RPT], pc[RPT], prec[RPT], prel[RPT], ppx[RPT];
+  uint32_t pr[RPT], pc[RPT], prec[RPT], prel[RPT], ppx[RPT], pr1[RPT];
   uint64_t gk[RPT0];
   uint32_t gctx[RPT0];
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t i = tid + q * SCAN_THREADS;
     prec[q] = i;
-    pr[q] = pc[q] = prel[q] = ppx[q] = 0;
-    if (q < RPT0) {
+    pr[q] = pc[q] = prel[q] = ppx[q] = pr1[q] = 0;
+    if (q < RPT0) {  // (both parities' rank accumulators: the window's is picked once C.windows is back)
       pr[q] = M.wrank[i];
+      pr1[q] = M.wrank[WTOT + i];
       pc[q] = M.nchild[i] | (M.ninl[i] << 16);
       gk[q] = M.wkey[i];
       gctx[q] = M.wctx[i];
@@ -1951,10 +2313,33 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       prel[q] = d.z;
       ppx[q] = d.w;
       pr[q] = M.lrank[i - WCAP];
+      pr1[q] = M.lrank[LMAX + i - WCAP];
     }
   }
-  if (c_done || c_mode >= MODE_SORT) return;
-  const bool run = c_mode == MODE_RUN;
+  if (FL) {
+    if (!(c_pvalid && c_pdf)) return;  // (the window was not handled: nothing to append)
+  } else if (c_done || c_mode >= MODE_SORT) {
+    return;
+  }
+  const uint64_t wn = FL ? c_wn - 1 : c_wn;  // the window scanned
+  if (wn & 1) {
+#pragma unroll
+    for (int q = 0; q < RPT; q++) pr[q] = pr1[q];
+  }
+  if (FL) {  // a record that is a child of window n - 1 has a provisional uid: resolve it
+    const uint32_t uq = C.winfo[(wn + 3) & 3].uid0;
+    const uint32_t *cq = M.cpt + (uint64_t)((wn + 1) & 1) * NMAX;
+#pragma unroll
+    for (int q = 0; q < RPT0; q++) {
+      const uint32_t u = (uint32_t)gk[q];
+      const uint32_t i = tid + q * SCAN_THREADS;
+      if (i < W && (u & PROV)) {
+        if (((u >> 30) & 1u) != (uint32_t)((wn + 1) & 1)) atomicOr(M.error, 256u);
+        gk[q] = (gk[q] & ~0xffffffffull) | (uint32_t)(uq + cq[((u & 0x3fffffffu) >> 8) % NMAX] + (u & 0xffu));
+      }
+    }
+  }
+  const bool run = !FL && c_mode == MODE_RUN;
   const bool handled = run || (W <= (uint32_t)WCAP && !c_fr);
   const uint32_t base = run ? c_wbase : 0;
   // ---- pool bookkeeping: the free stack loses the slots the fresh children took and gains the
@@ -1963,6 +2348,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   const uint64_t consumed = nF < nfree ? nF : nfree;
   const uint64_t mv = consumed < npush ? consumed : npush;
   auto stack_and_hubs = [&]() {
+    if (FL) return;  // (df_book did it)
     for (uint64_t i = tid; i < mv; i += SCAN_THREADS) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
     if (handled) {
       const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
@@ -1973,6 +2359,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     stack_and_hubs();
     __syncthreads();
     if (tid == 0) {
+      C.acc_tc = 0;  // (k2_handle's totals: this pipeline scans its own)
+      C.acc_tinl = 0;
+      C.pdf = 0;
       C.nfree = nfree - consumed + npush;
       C.P_end += nF > nfree ? nF - nfree : 0;
       C.live = C.live - npush + nF;
@@ -2141,9 +2530,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       M.sinfo[rc] = make_uint4(r + (tinl ? l_cnt[first] : 0), last + 1 + ip, l_slot[r], ip);
       if (WIDE && q >= RPT0) {  // (k2_rank wrote the dense list lrec)
         M.pwkey[rc] = ((uint64_t)prel[q] << 32) | (uint32_t)(uid0 + l_slot[ppx[q] & 0xffffu] + (ppx[q] >> 16));
-        M.lrank[tid + q * SCAN_THREADS - WCAP] = 0;
+        lrank_of(M, wn)[tid + q * SCAN_THREADS - WCAP] = 0;
       } else if (!run) {
-        M.wrank[rc] = 0;
+        wrank_of(M, wn)[rc] = 0;
       }
     }
   }
@@ -2154,7 +2543,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   if (run && c_r0 + W < c_rW && !c_rtrim) run_chunk_end<SCAN_THREADS>(M, c_r0 + W, c_rW, rn1, rtrim);
   stack_and_hubs();
   PH_MARK(19);
-  if (tid == 0) {
+  if (FL && tid == 0) {  // the next k2_pa appends window n from sinfo (df_book did the run bookkeeping)
+    C.pK0 = wif.K0;
+    C.puid0 = wif.uid0;
+    C.pinl = tinl;
+    C.pdf = 0;
+    if (N) C.last_ts = wif.tmin + last_rel;
+  }
+  if (!FL && tid == 0) {
+    C.acc_tc = 0;  // (k2_handle's totals: this pipeline scans its own)
+    C.acc_tinl = 0;
+    C.pdf = 0;
     C.pK0 = bk.K;
     C.puid0 = bk.uid;
     C.ptmin = bk.tmin;
@@ -2230,6 +2629,37 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   }
   PH_MARK(20);
   BLK_REC(2, c_win);
+}
+
+// ---- the deferred pipeline's flush, second part: every provisional uid still pending (children of window
+// n - 1 in the pool, and in the window records when window n became a sorted run) resolves; afterwards the
+// next k2_pa appends from sinfo (pdf = 0) and the other pipeline can take over.  (Grid-stride.)
+__global__ __launch_bounds__(256) void k_xlate(const P2PDev M) {
+  Ctl &C = *M.C;
+  const uint64_t wn = C.windows;  // n + 1 (df_book counted window n), or n when window n became a sorted run
+  const uint64_t P = C.P_end;
+  const bool sorted = C.mode == MODE_SORT;
+  const uint64_t nw = sorted ? C.rW : 0;
+  const uint64_t wq = sorted ? wn + 3 : wn + 2;  // window n - 1 (mod 4: its parity, its winfo slot)
+  const uint32_t uq = C.winfo[wq & 3].uid0;
+  const uint32_t *cq = M.cpt + (uint64_t)(wq & 1) * NMAX;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += stride) {
+    const uint32_t u = M.ev_uid[0][i];
+    if (M.ev_ts[0][i] != TOMB && (u & PROV)) {
+      if (((u >> 30) & 1u) != (uint32_t)(wq & 1)) atomicOr(M.error, 256u);
+      M.ev_uid[0][i] = uq + cq[((u & 0x3fffffffu) >> 8) % NMAX] + (u & 0xffu);
+    }
+  }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) {
+    const uint64_t k = M.wkey[i];
+    const uint32_t u = (uint32_t)k;
+    if (u & PROV) {
+      if (((u >> 30) & 1u) != (uint32_t)(wq & 1)) atomicOr(M.error, 256u);
+      M.wkey[i] = (k & ~0xffffffffull) | (uint32_t)(uq + cq[((u & 0x3fffffffu) >> 8) % NMAX] + (u & 0xffu));
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) C.pdf = 0;
 }
 
 // ---- local records' trace uids (traced wide engines): records made by this window's handlers carry

@@ -163,6 +163,20 @@ int nsgpu_sim_attach_p2p(nsgpu_sim *s, nsgpu_p2p *h) {
   return NSGPU_OK;
 }
 
+int nsgpu_sim_adopt_p2p(nsgpu_sim *s, nsgpu_p2p *h) {
+  if (!s || !h) return set_error(NSGPU_EINVAL, "nsgpu_sim_adopt_p2p: null");
+  if (s->p2p || s->wifi) return set_error(NSGPU_ESTATE, "nsgpu_sim_adopt_p2p: an engine is attached already");
+  if (s->dispatched) return set_error(NSGPU_ESTATE, "nsgpu_sim_adopt_p2p: events were dispatched already");
+  uint32_t u = 0;
+  int rc = nsgpu_p2p_setup_uid(h, &u);
+  if (rc) return rc;
+  if (u != s->uid)
+    return set_error(NSGPU_ESTATE, "nsgpu_sim_adopt_p2p: the engine's setup ends at uid %u, this runtime is at %u "
+                                   "(the setup list does not mirror the program's Schedule calls)", u, s->uid);
+  s->p2p = h;
+  return NSGPU_OK;
+}
+
 // The closed-loop Wi-Fi PHY joins this runtime's order: its events are scheduled at run time only (the
 // host closures' SendPacket calls), so it takes no setup uids.
 int nsgpu_sim_attach_wifi(nsgpu_sim *s, nsgpu_wifil *h) {

@@ -37,7 +37,9 @@ HipSimulatorImpl::GetTypeId (void)
 
 HipSimulatorImpl::HipSimulatorImpl ()
   : m_rt (0),
-    m_window (4096)
+    m_window (4096),
+    m_running (false),
+    m_nextStop (false)
 {
   // front size 0: adaptive (nsgpu_sched_host.h)
   NSGPU_RT (nsgpu_sim_create (0, 0, &m_rt));
@@ -69,6 +71,34 @@ void
 HipSimulatorImpl::AttachDeviceSubset (nsgpu_p2p *engine)
 {
   NSGPU_RT (nsgpu_sim_attach_p2p (m_rt, engine));
+}
+
+const std::vector<HipSimulatorImpl::SetupCall> &
+HipSimulatorImpl::GetSetupJournal (void) const
+{
+  return m_journal;
+}
+
+void
+HipSimulatorImpl::AdoptDeviceSubset (nsgpu_p2p *engine, const std::vector<uint32_t> &owned)
+{
+  if (m_running)
+    {
+      NS_FATAL_ERROR ("HipSimulatorImpl::AdoptDeviceSubset: call it before Run");
+    }
+  for (size_t i = 0; i < owned.size (); i++)
+    {
+      if (owned[i] >= m_journal.size () || m_journal[owned[i]].kind == SETUP_DESTROY)
+        {
+          NS_FATAL_ERROR ("HipSimulatorImpl::AdoptDeviceSubset: journal entry " << owned[i] << " is not a pending event");
+        }
+      const SetupCall &c = m_journal[owned[i]];
+      // the host closure leaves the queue (its uid stays consumed: the engine's copy of the event has it)
+      NSGPU_RT (nsgpu_sim_remove_key (m_rt, c.ts, c.uid, c.context, reinterpret_cast<uintptr_t> (c.event)));
+      c.event->Cancel ();
+      c.event->Unref ();  // the queue's reference
+    }
+  NSGPU_RT (nsgpu_sim_adopt_p2p (m_rt, engine));
 }
 
 uint64_t
@@ -149,6 +179,12 @@ HipSimulatorImpl::Enqueue (uint64_t ts, uint32_t context, EventImpl *event)
 {
   uint32_t uid = 0;
   NSGPU_RT (nsgpu_sim_insert (m_rt, ts, context, reinterpret_cast<uintptr_t> (event), &uid));
+  if (!m_running)
+    {
+      const SetupCall c = {m_nextStop ? (uint32_t) SETUP_STOP : (uint32_t) SETUP_CALL, context, uid, ts, event};
+      m_journal.push_back (c);
+    }
+  m_nextStop = false;
   return EventId (event, ts, context, uid);
 }
 
@@ -194,6 +230,8 @@ HipSimulatorImpl::Dispatch (uint32_t n)
 void
 HipSimulatorImpl::Run (void)
 {
+  m_running = true;
+  m_journal.clear ();
   NSGPU_RT (nsgpu_sim_set_stop (m_rt, 0));
   for (;;)
     {
@@ -229,6 +267,7 @@ HipSimulatorImpl::Stop (void)
 void
 HipSimulatorImpl::Stop (Time const &time)
 {
+  m_nextStop = true;  // (journaled as the Stop event: Simulator::Stop (Time) -> Schedule (time, &Simulator::Stop))
   Simulator::Schedule (time, &Simulator::Stop);
 }
 
@@ -263,6 +302,11 @@ HipSimulatorImpl::ScheduleDestroy (EventImpl *event)
   // Remove or DoDispose).
   uint64_t ts = 0;
   NSGPU_RT (nsgpu_sim_destroy_insert (m_rt, reinterpret_cast<uintptr_t> (event), &ts));
+  if (!m_running)
+    {
+      const SetupCall c = {(uint32_t) SETUP_DESTROY, 0xffffffffu, 2u, ts, event};
+      m_journal.push_back (c);
+    }
   event->Ref ();
   return EventId (Ptr<EventImpl> (event, false), ts, 0xffffffff, 2);
 }

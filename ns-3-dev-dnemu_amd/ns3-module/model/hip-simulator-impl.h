@@ -54,6 +54,23 @@ public:
   /* A GPU-resident point-to-point subset (nsgpu_p2p, e.g. from NsgpuP2pScenario) joins this
    * simulator's event order; call before anything is scheduled on it. */
   void AttachDeviceSubset (nsgpu_p2p *engine);
+
+  /* The setup journal: every Schedule* / ScheduleDestroy / Stop (Time) call made before the first Run, in
+   * call order (= uid order, from 4).  NsgpuP2pScenario::FromNodeList maps the stock helpers' calls
+   * (NodeListPriv::Add's Node::Start, Node::AddDevice's NetDevice::Start, Node::AddApplication's
+   * Application::Start, Simulator::Stop) to the engine's setup list. */
+  enum SetupKind { SETUP_CALL = 0, SETUP_DESTROY = 1, SETUP_STOP = 2 };
+  struct SetupCall
+  {
+    uint32_t kind, context, uid;
+    uint64_t ts;
+    EventImpl *event;
+  };
+  const std::vector<SetupCall> &GetSetupJournal (void) const;
+  /* The engine built from this program's own topology (NsgpuP2pScenario::FromNodeList) takes over the
+   * journal entries `owned`: their host events are removed (the engine dispatches them, with the same
+   * uids) and the engine joins the event order; the program's other events stay on the host. */
+  void AdoptDeviceSubset (nsgpu_p2p *engine, const std::vector<uint32_t> &owned);
   /* Dispatches so far (RemoveNext calls, cancelled events included: SURVEY H16), host and device. */
   uint64_t GetEventCount (void) const;
 
@@ -68,6 +85,9 @@ private:
 
   nsgpu_sim *m_rt;
   std::vector<nsgpu_event> m_window;
+  std::vector<SetupCall> m_journal;
+  bool m_running;    // Run was called (the journal is closed)
+  bool m_nextStop;   // Stop (Time) is scheduling Simulator::Stop
 };
 
 } // namespace ns3

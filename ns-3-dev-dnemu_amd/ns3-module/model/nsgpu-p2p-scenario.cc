@@ -1,9 +1,42 @@
 /* -*- Mode:C++; c-file-style:"gnu"; indent-tabs-mode:nil; -*- */
 #include "nsgpu-p2p-scenario.h"
 #include "ns3/fatal-error.h"
+#include "ns3/node-list.h"
+#include "ns3/node.h"
+#include "ns3/application.h"
+#include "ns3/point-to-point-net-device.h"
+#include "ns3/point-to-point-channel.h"
+#include "ns3/loopback-net-device.h"
+#include "ns3/drop-tail-queue.h"
+#include "ns3/ipv4.h"
+#include "ns3/ipv4-l3-protocol.h"
+#include "ns3/onoff-application.h"
+#include "ns3/packet-sink.h"
+#include "ns3/udp-echo-client.h"
+#include "ns3/udp-echo-server.h"
+#include "ns3/inet-socket-address.h"
+#include "ns3/address.h"
+#include "ns3/uinteger.h"
+#include "ns3/enum.h"
+#include "ns3/data-rate.h"
+#include "ns3/random-variable.h"
+#include "ns3/output-stream-wrapper.h"
+#include "ns3/pcap-file-wrapper.h"
+#include "ns3/trace-helper.h"
 #include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <sstream>
 
 namespace ns3 {
+
+#define NSGPU_TRY(call)                                                     \
+  do {                                                                      \
+      if ((call) != NSGPU_OK)                                               \
+        {                                                                   \
+          NS_FATAL_ERROR ("libnsgpu: " << nsgpu_last_error ());             \
+        }                                                                   \
+    } while (false)
 
 NsgpuP2pScenario::NsgpuP2pScenario ()
   : m_nodes (0),
@@ -11,12 +44,17 @@ NsgpuP2pScenario::NsgpuP2pScenario ()
     m_icmp (true),
     m_stop (-1),
     m_firstLink (true),
-    m_engine (0)
+    m_engine (0),
+    m_codec (0)
 {
 }
 
 NsgpuP2pScenario::~NsgpuP2pScenario ()
 {
+  if (m_codec != 0)
+    {
+      nsgpu_trace_codec_free (m_codec);
+    }
   if (m_engine != 0)
     {
       nsgpu_p2p_destroy (m_engine);
@@ -74,7 +112,7 @@ NsgpuP2pScenario::AddApp (const App &a)
 uint32_t
 NsgpuP2pScenario::AddPacketSink (uint32_t node, Time start, Time stop)
 {
-  App a = {NSGPU_APP_SINK, node, 0, 0, 0, 0, start.GetTimeStep (), stop.GetTimeStep (), 0, 0.0, 0.0};
+  App a = {NSGPU_APP_SINK, node, 0, 0, 0, 0, start.GetTimeStep (), stop.GetTimeStep (), 0, 0.0, 0.0, 0, 0, 0, 0};
   return AddApp (a);
 }
 
@@ -83,7 +121,7 @@ NsgpuP2pScenario::AddOnOff (uint32_t node, uint32_t dstNode, Time start, Time st
                             uint32_t packetSize, double onSeconds, double offSeconds, uint32_t maxBytes, uint32_t ttl)
 {
   App a = {NSGPU_APP_ONOFF, node, dstNode, packetSize, maxBytes, ttl, start.GetTimeStep (), stop.GetTimeStep (),
-           rateBps, onSeconds, offSeconds};
+           rateBps, onSeconds, offSeconds, 0, 0, 0, 9};
   return AddApp (a);
 }
 
@@ -112,6 +150,271 @@ NsgpuP2pScenario::SetIcmp (bool on)
   m_icmp = on;
 }
 
+namespace {
+/* ConstantVariable (v) prints as "Constant:v" (random-variable.cc:1931-1940); anything else draws from a
+ * random stream, which the GPU-resident OnOff cannot */
+double
+ConstantSeconds (const RandomVariable &v, const char *what, uint32_t node)
+{
+  std::ostringstream os;
+  os << v;
+  const std::string s = os.str ();
+  if (s.compare (0, 9, "Constant:") != 0)
+    {
+      NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << node << ": OnOffApplication " << what << " is " << s
+                      << ", not a ConstantVariable");
+    }
+  return std::strtod (s.c_str () + 9, 0);
+}
+
+Time
+TimeAttribute (Ptr<Object> o, const char *name)
+{
+  TimeValue v;
+  o->GetAttribute (name, v);
+  return v.Get ();
+}
+
+uint32_t
+UintAttribute (Ptr<Object> o, const char *name)
+{
+  UintegerValue v;
+  o->GetAttribute (name, v);
+  return (uint32_t) v.Get ();
+}
+} // anonymous namespace
+
+void
+NsgpuP2pScenario::FromNodeList (Ptr<HipSimulatorImpl> impl)
+{
+  if (m_nodes != 0 || !m_setup.empty ())
+    {
+      NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: the scenario is not empty");
+    }
+  const uint32_t N = NodeList::GetNNodes ();
+  m_nodes = N;
+  // ---- devices, in the setup order of their NetDevice::Start calls (engine index = that order) ----
+  // per node: (device or application object, its engine index) in AddDevice / AddApplication order
+  std::map<Ptr<NetDevice>, uint32_t> devIndex;
+  std::vector<std::vector<Ptr<NetDevice> > > nodeDevs (N);
+  std::vector<std::vector<Ptr<Application> > > nodeApps (N);
+  for (uint32_t n = 0; n < N; n++)
+    {
+      Ptr<Node> node = NodeList::GetNode (n);
+      for (uint32_t i = 0; i < node->GetNDevices (); i++)
+        {
+          nodeDevs[n].push_back (node->GetDevice (i));
+        }
+      for (uint32_t i = 0; i < node->GetNApplications (); i++)
+        {
+          nodeApps[n].push_back (node->GetApplication (i));
+        }
+    }
+  // ---- the setup list from the journal (uid order) ----
+  const std::vector<HipSimulatorImpl::SetupCall> &J = impl->GetSetupJournal ();
+  std::vector<uint32_t> seen (N, 0);
+  std::vector<Ptr<Application> > apps;  // engine application index -> object
+  std::vector<Ptr<NetDevice> > devs;    // engine device index -> object
+  for (uint32_t i = 0; i < J.size (); i++)
+    {
+      const HipSimulatorImpl::SetupCall &c = J[i];
+      if (c.kind == HipSimulatorImpl::SETUP_DESTROY)
+        {
+          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_UID, 0u));
+          continue;
+        }
+      if (c.kind == HipSimulatorImpl::SETUP_STOP)
+        {
+          if (m_stop >= 0)
+            {
+              NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: two Simulator::Stop calls");
+            }
+          m_stop = (int64_t) c.ts;
+          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_STOP, 0u));
+          m_owned.push_back (i);
+          continue;
+        }
+      const uint32_t n = c.context;
+      const uint32_t nd = n < N ? nodeDevs[n].size () : 0u, na = n < N ? nodeApps[n].size () : 0u;
+      if (c.ts != 0 || n >= N || seen[n] >= 1 + nd + na)
+        {
+          // the program's own event: it stays on the host, its uid is consumed
+          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_UID, 0u));
+          continue;
+        }
+      const uint32_t k = seen[n]++;
+      m_owned.push_back (i);
+      if (k == 0)  // NodeListPriv::Add -> ScheduleWithContext (node, 0, &Node::Start)
+        {
+          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_NODE, n));
+        }
+      else if (k <= nd)  // Node::AddDevice -> NetDevice::Start
+        {
+          Ptr<NetDevice> d = nodeDevs[n][k - 1];
+          if (DynamicCast<LoopbackNetDevice> (d) != 0)
+            {
+              m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_NOOP, n));
+            }
+          else if (DynamicCast<PointToPointNetDevice> (d) != 0)
+            {
+              devIndex[d] = devs.size ();
+              m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_DEVICE, (uint32_t) devs.size ()));
+              devs.push_back (d);
+              m_devObj.push_back (d);
+            }
+          else
+            {
+              NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << n << " device " << k - 1
+                              << " is not a PointToPointNetDevice (not in the GPU-resident subset)");
+            }
+        }
+      else  // Node::AddApplication -> Application::Start
+        {
+          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_APP, (uint32_t) apps.size ()));
+          apps.push_back (nodeApps[n][k - 1 - nd]);
+        }
+    }
+  for (uint32_t n = 0; n < N; n++)
+    {
+      if (seen[n] != 1 + nodeDevs[n].size () + nodeApps[n].size ())
+        {
+          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << n << ": " << seen[n]
+                          << " setup calls in the journal, " << 1 + nodeDevs[n].size () + nodeApps[n].size ()
+                          << " expected (build the topology under HipSimulatorImpl, before Run)");
+        }
+    }
+  // ---- device parameters ----
+  const uint32_t D = devs.size ();
+  m_dev.resize (D);
+  m_addr.assign (D, 0u);
+  m_ifindex.assign (D, 0u);
+  for (uint32_t d = 0; d < D; d++)
+    {
+      Ptr<PointToPointNetDevice> p = DynamicCast<PointToPointNetDevice> (devs[d]);
+      Ptr<PointToPointChannel> ch = DynamicCast<PointToPointChannel> (p->GetChannel ());
+      if (ch == 0 || ch->GetNDevices () != 2)
+        {
+          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: device " << d << " has no point-to-point channel");
+        }
+      Ptr<NetDevice> other = ch->GetDevice (0) == devs[d] ? ch->GetDevice (1) : ch->GetDevice (0);
+      if (devIndex.find (other) == devIndex.end ())
+        {
+          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: device " << d << "'s peer is not in the subset");
+        }
+      Ptr<DropTailQueue> q = DynamicCast<DropTailQueue> (p->GetQueue ());
+      if (q == 0)
+        {
+          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: device " << d << "'s TxQueue is not a DropTailQueue");
+        }
+      EnumValue mode;
+      q->GetAttribute ("Mode", mode);
+      if (mode.Get () != DropTailQueue::PACKETS)
+        {
+          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: device " << d << "'s DropTailQueue is not in PACKETS mode");
+        }
+      DataRateValue rate;
+      p->GetAttribute ("DataRate", rate);
+      Dev x = {devs[d]->GetNode ()->GetId (), devIndex[other], UintAttribute (q, "MaxPackets"), rate.Get ().GetBitRate (),
+               TimeAttribute (p, "InterframeGap").GetTimeStep (), TimeAttribute (ch, "Delay").GetTimeStep ()};
+      m_dev[d] = x;
+    }
+  // ---- Ipv4: interface addresses and indices, DefaultTtl ----
+  std::vector<uint32_t> ttl (N, 64);
+  std::map<uint32_t, uint32_t> nodeOfAddr;
+  for (uint32_t n = 0; n < N; n++)
+    {
+      Ptr<Ipv4> ip = NodeList::GetNode (n)->GetObject<Ipv4> ();
+      if (ip == 0)
+        {
+          continue;
+        }
+      for (uint32_t i = 0; i < ip->GetNInterfaces (); i++)
+        {
+          Ptr<NetDevice> nd = ip->GetNetDevice (i);
+          if (ip->GetNAddresses (i) == 0 || devIndex.find (nd) == devIndex.end ())
+            {
+              continue;
+            }
+          const uint32_t a = ip->GetAddress (i, 0).GetLocal ().Get ();
+          m_addr[devIndex[nd]] = a;
+          m_ifindex[devIndex[nd]] = i;
+          nodeOfAddr[a] = n;
+        }
+      Ptr<Ipv4L3Protocol> l3 = DynamicCast<Ipv4L3Protocol> (ip);
+      if (l3 != 0)
+        {
+          ttl[n] = UintAttribute (l3, "DefaultTtl");
+        }
+    }
+  // ---- applications ----
+  for (uint32_t a = 0; a < apps.size (); a++)
+    {
+      Ptr<Application> o = apps[a];
+      const uint32_t n = o->GetNode ()->GetId ();
+      App x = {0, n, 0, 0, 0, ttl[n], TimeAttribute (o, "StartTime").GetTimeStep (),
+               TimeAttribute (o, "StopTime").GetTimeStep (), 0, 0.0, 0.0, 0, 0, 0, 0};
+      uint32_t remote = 0;
+      if (DynamicCast<OnOffApplication> (o) != 0)
+        {
+          x.kind = NSGPU_APP_ONOFF;
+          DataRateValue rate;
+          o->GetAttribute ("DataRate", rate);
+          x.rate = rate.Get ().GetBitRate ();
+          x.size = UintAttribute (o, "PacketSize");
+          x.maxBytes = UintAttribute (o, "MaxBytes");
+          RandomVariableValue on, off;
+          o->GetAttribute ("OnTime", on);
+          o->GetAttribute ("OffTime", off);
+          x.on = ConstantSeconds (on.Get (), "OnTime", n);
+          x.off = ConstantSeconds (off.Get (), "OffTime", n);
+          AddressValue peer;
+          o->GetAttribute ("Remote", peer);
+          if (!InetSocketAddress::IsMatchingType (peer.Get ()))
+            {
+              NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: OnOffApplication on node " << n << ": Remote is not "
+                              "an InetSocketAddress");
+            }
+          const InetSocketAddress s = InetSocketAddress::ConvertFrom (peer.Get ());
+          remote = s.GetIpv4 ().Get ();
+          x.remotePort = s.GetPort ();
+        }
+      else if (DynamicCast<UdpEchoClient> (o) != 0)
+        {
+          x.kind = NSGPU_APP_ECHO_CLIENT;
+          x.size = UintAttribute (o, "PacketSize");
+          x.count = UintAttribute (o, "MaxPackets");
+          x.interval = TimeAttribute (o, "Interval").GetTimeStep ();
+          Ipv4AddressValue ra;
+          o->GetAttribute ("RemoteAddress", ra);
+          remote = ra.Get ().Get ();
+          x.remotePort = UintAttribute (o, "RemotePort");
+        }
+      else if (DynamicCast<UdpEchoServer> (o) != 0)
+        {
+          x.kind = NSGPU_APP_ECHO_SERVER;
+        }
+      else if (DynamicCast<PacketSink> (o) != 0)
+        {
+          x.kind = NSGPU_APP_SINK;
+        }
+      else
+        {
+          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << n << " application " << a
+                          << " is not OnOff / PacketSink / UdpEcho (not in the GPU-resident subset)");
+        }
+      if (x.kind == NSGPU_APP_ONOFF || x.kind == NSGPU_APP_ECHO_CLIENT)
+        {
+          if (nodeOfAddr.find (remote) == nodeOfAddr.end ())
+            {
+              NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << n << " sends to an address no node has");
+            }
+          x.dst = nodeOfAddr[remote];
+          x.remoteAddr = remote;
+        }
+      m_app.push_back (x);
+    }
+}
+
 void
 NsgpuP2pScenario::PopulateRoutingTables (void)
 {
@@ -119,12 +422,12 @@ NsgpuP2pScenario::PopulateRoutingTables (void)
   m_nDst = 0;
   for (size_t i = 0; i < m_app.size (); i++)
     {
-      if (m_app[i].kind == NSGPU_APP_ONOFF)
+      if (m_app[i].kind == NSGPU_APP_ONOFF || m_app[i].kind == NSGPU_APP_ECHO_CLIENT)
         {
           m_dstSlot[m_app[i].dst] = 0;  // mark; numbered below in node order
-          if (m_icmp)
+          if (m_icmp || m_app[i].kind == NSGPU_APP_ECHO_CLIENT)
             {
-              m_dstSlot[m_app[i].node] = 0;  // an ICMP error goes back to the sender
+              m_dstSlot[m_app[i].node] = 0;  // an ICMP error / an echo goes back to the sender
             }
         }
     }
@@ -153,62 +456,175 @@ NsgpuP2pScenario::PopulateRoutingTables (void)
     }
 }
 
-nsgpu_p2p *
-NsgpuP2pScenario::CreateEngine (uint64_t poolCap, uint64_t logCap)
+void
+NsgpuP2pScenario::Fill (void)
 {
   if (m_route.empty ())
     {
       RouteShortestPaths ();
     }
   const size_t D = m_dev.size (), A = m_app.size ();
-  std::vector<uint32_t> devNode (D), devPeer (D), devQmax (D);
-  std::vector<uint64_t> devBps (D);
-  std::vector<int64_t> devIfg (D), devDelay (D);
+  m_cDevNode.resize (D), m_cDevPeer.resize (D), m_cDevQmax.resize (D);
+  m_cDevBps.resize (D), m_cDevIfg.resize (D), m_cDevDelay.resize (D);
   for (size_t d = 0; d < D; d++)
     {
-      devNode[d] = m_dev[d].node, devPeer[d] = m_dev[d].peer, devQmax[d] = m_dev[d].qmax;
-      devBps[d] = m_dev[d].bps, devIfg[d] = m_dev[d].ifg, devDelay[d] = m_dev[d].delay;
+      m_cDevNode[d] = m_dev[d].node, m_cDevPeer[d] = m_dev[d].peer, m_cDevQmax[d] = m_dev[d].qmax;
+      m_cDevBps[d] = m_dev[d].bps, m_cDevIfg[d] = m_dev[d].ifg, m_cDevDelay[d] = m_dev[d].delay;
     }
-  std::vector<uint32_t> kind (A), node (A), dst (A), slot (A), src (A), size (A), maxb (A), ttl (A), zero (A, 0);
-  std::vector<int64_t> start (A), stop (A), ivl (A, 0);
-  std::vector<uint64_t> rate (A);
-  std::vector<double> on (A), off (A);
+  const size_t A1 = std::max (A, (size_t) 1);
+  m_cKind.assign (A1, 0), m_cNode.assign (A1, 0), m_cDst.assign (A1, 0), m_cSlot.assign (A1, 0);
+  m_cSrc.assign (A1, 0xffffffffu), m_cSize.assign (A1, 0), m_cMaxb.assign (A1, 0), m_cTtl.assign (A1, 0);
+  m_cCount.assign (A1, 0), m_cRaddr.assign (A1, 0), m_cRport.assign (A1, 0);
+  m_cStart.assign (A1, 0), m_cStop.assign (A1, 0), m_cIvl.assign (A1, 0), m_cRate.assign (A1, 0);
+  m_cOn.assign (A1, 0.0), m_cOff.assign (A1, 0.0);
   for (size_t i = 0; i < A; i++)
     {
       const App &a = m_app[i];
-      kind[i] = a.kind, node[i] = a.node, dst[i] = a.dst, size[i] = a.size, maxb[i] = a.maxBytes, ttl[i] = a.ttl;
-      slot[i] = a.kind == NSGPU_APP_ONOFF ? m_dstSlot[a.dst] : 0;
-      src[i] = a.kind == NSGPU_APP_ONOFF ? m_dstSlot[a.node] : 0xffffffffu;
-      start[i] = a.start, stop[i] = a.stop, rate[i] = a.rate, on[i] = a.on, off[i] = a.off;
+      const bool sender = a.kind == NSGPU_APP_ONOFF || a.kind == NSGPU_APP_ECHO_CLIENT;
+      m_cKind[i] = a.kind, m_cNode[i] = a.node, m_cDst[i] = a.dst, m_cSize[i] = a.size, m_cMaxb[i] = a.maxBytes;
+      m_cTtl[i] = a.ttl, m_cCount[i] = a.count, m_cIvl[i] = a.interval, m_cRaddr[i] = a.remoteAddr;
+      m_cRport[i] = a.remotePort;
+      m_cSlot[i] = sender ? m_dstSlot[a.dst] : 0;
+      m_cSrc[i] = sender ? m_dstSlot[a.node] : 0xffffffffu;
+      m_cStart[i] = a.start, m_cStop[i] = a.stop, m_cRate[i] = a.rate, m_cOn[i] = a.on, m_cOff[i] = a.off;
     }
-  std::vector<uint32_t> sk (m_setup.size ()), si (m_setup.size ());
+  m_cSk.resize (m_setup.size ()), m_cSi.resize (m_setup.size ());
   for (size_t i = 0; i < m_setup.size (); i++)
     {
-      sk[i] = m_setup[i].first, si[i] = m_setup[i].second;
+      m_cSk[i] = m_setup[i].first, m_cSi[i] = m_setup[i].second;
     }
-  nsgpu_p2p_scenario sc = nsgpu_p2p_scenario ();
+  nsgpu_p2p_scenario &sc = m_sc;
+  sc = nsgpu_p2p_scenario ();
   sc.n_nodes = m_nodes;
   sc.n_devices = D;
   sc.n_apps = A;
   sc.n_dst = std::max (m_nDst, 1u);
-  sc.dev_node = &devNode[0], sc.dev_peer = &devPeer[0], sc.dev_bps = &devBps[0];
-  sc.dev_ifg_ns = &devIfg[0], sc.dev_delay_ns = &devDelay[0], sc.dev_qmax = &devQmax[0];
+  sc.dev_node = &m_cDevNode[0], sc.dev_peer = &m_cDevPeer[0], sc.dev_bps = &m_cDevBps[0];
+  sc.dev_ifg_ns = &m_cDevIfg[0], sc.dev_delay_ns = &m_cDevDelay[0], sc.dev_qmax = &m_cDevQmax[0];
   sc.route = &m_route[0];
-  sc.app_kind = &kind[0], sc.app_node = &node[0], sc.app_start_ns = &start[0], sc.app_stop_ns = &stop[0];
-  sc.app_dst_node = &dst[0], sc.app_dst_slot = &slot[0], sc.app_rate_bps = &rate[0], sc.app_pkt_size = &size[0];
-  sc.app_on_s = &on[0], sc.app_off_s = &off[0], sc.app_max_bytes = &maxb[0], sc.app_ttl = &ttl[0];
-  sc.app_count = &zero[0], sc.app_interval_ns = &ivl[0], sc.app_src_slot = &src[0];
+  sc.app_kind = &m_cKind[0], sc.app_node = &m_cNode[0], sc.app_start_ns = &m_cStart[0], sc.app_stop_ns = &m_cStop[0];
+  sc.app_dst_node = &m_cDst[0], sc.app_dst_slot = &m_cSlot[0], sc.app_rate_bps = &m_cRate[0];
+  sc.app_pkt_size = &m_cSize[0], sc.app_on_s = &m_cOn[0], sc.app_off_s = &m_cOff[0], sc.app_max_bytes = &m_cMaxb[0];
+  sc.app_ttl = &m_cTtl[0], sc.app_count = &m_cCount[0], sc.app_interval_ns = &m_cIvl[0], sc.app_src_slot = &m_cSrc[0];
   sc.stop_ns = m_stop;
   sc.icmp = m_icmp ? 1u : 0u;
   sc.n_setup = m_setup.size ();
-  sc.setup_kind = &sk[0];
-  sc.setup_index = &si[0];
-  if (nsgpu_p2p_create (&sc, poolCap, logCap, &m_engine) != NSGPU_OK ||
+  sc.setup_kind = m_cSk.empty () ? 0 : &m_cSk[0];
+  sc.setup_index = m_cSi.empty () ? 0 : &m_cSi[0];
+}
+
+nsgpu_p2p *
+NsgpuP2pScenario::CreateEngine (uint64_t poolCap, uint64_t logCap)
+{
+  Fill ();
+  if (nsgpu_p2p_create (&m_sc, poolCap, logCap, &m_engine) != NSGPU_OK ||
       nsgpu_p2p_reset (m_engine, 0) != NSGPU_OK)
     {
       NS_FATAL_ERROR ("libnsgpu: " << nsgpu_last_error ());
     }
   return m_engine;
+}
+
+void
+NsgpuP2pScenario::AdoptInto (Ptr<HipSimulatorImpl> impl)
+{
+  if (m_engine == 0)
+    {
+      NS_FATAL_ERROR ("NsgpuP2pScenario::AdoptInto: CreateEngine first");
+    }
+  impl->AdoptDeviceSubset (m_engine, m_owned);
+}
+
+void
+NsgpuP2pScenario::EnableTraceRecords (uint64_t capacity)
+{
+  if (m_engine == 0)
+    {
+      NS_FATAL_ERROR ("NsgpuP2pScenario::EnableTraceRecords: CreateEngine first");
+    }
+  NSGPU_TRY (nsgpu_p2p_set_trace (m_engine, capacity));
+  NSGPU_TRY (nsgpu_p2p_reset (m_engine, 0));
+}
+
+void
+NsgpuP2pScenario::WriteTraces (Ptr<OutputStreamWrapper> ascii, std::string pcapPrefix)
+{
+  if (m_engine == 0)
+    {
+      NS_FATAL_ERROR ("NsgpuP2pScenario::WriteTraces: CreateEngine first");
+    }
+  if (m_codec == 0)
+    {
+      nsgpu_trace_addressing ad;
+      ad.dev_addr = m_addr.empty () ? 0 : &m_addr[0];
+      ad.dev_ip_ifindex = m_ifindex.empty () ? 0 : &m_ifindex[0];
+      ad.app_remote_addr = &m_cRaddr[0];
+      ad.app_remote_port = &m_cRport[0];
+      NSGPU_TRY (nsgpu_trace_codec_create (&m_sc, &ad, &m_codec));
+    }
+  uint64_t n = 0;
+  NSGPU_TRY (nsgpu_p2p_trace_read (m_engine, 0, 0, &n, 0));
+  std::vector<nsgpu_trace_record> rec (std::max (n, (uint64_t) 1));
+  NSGPU_TRY (nsgpu_p2p_trace_read (m_engine, &rec[0], n, &n, 0));
+  NSGPU_TRY (nsgpu_trace_sort (&rec[0], n));
+  std::vector<char> line (512);
+  std::vector<uint8_t> pkt (2048);
+  if (ascii != 0)
+    {
+      std::ostream *os = ascii->GetStream ();
+      for (uint64_t i = 0; i < n; i++)
+        {
+          uint64_t len = 0;
+          NSGPU_TRY (nsgpu_trace_line (m_codec, &rec[i], &line[0], line.size (), &len));
+          os->write (&line[0], (std::streamsize) len);
+        }
+    }
+  if (!pcapPrefix.empty ())
+    {
+      // PointToPointHelper::EnablePcapInternal (point-to-point-helper.cc:81-110): one file per device,
+      // PcapHelper::CreateFile (DLT_PPP), the PromiscSniffer's packets (after Dequeue, before MacRx)
+      PcapHelper helper;
+      // the device's NetDevice index on its node (Node::AddDevice order: the setup list's devices and loopbacks)
+      std::vector<uint32_t> nxt (m_nodes, 0), devid (m_dev.size (), 0);
+      for (size_t i = 0; i < m_setup.size (); i++)
+        {
+          if (m_setup[i].first == NSGPU_SETUP_DEVICE)
+            {
+              devid[m_setup[i].second] = nxt[m_dev[m_setup[i].second].node]++;
+            }
+          else if (m_setup[i].first == NSGPU_SETUP_NOOP)
+            {
+              nxt[m_setup[i].second]++;
+            }
+        }
+      std::vector<Ptr<PcapFileWrapper> > files (m_dev.size ());
+      for (uint32_t d = 0; d < m_dev.size (); d++)
+        {
+          // PcapHelper::GetFilenameFromDevice: <prefix>-<node id>-<device id>.pcap
+          std::string fn;
+          if (d < m_devObj.size () && m_devObj[d] != 0)
+            {
+              fn = helper.GetFilenameFromDevice (pcapPrefix, m_devObj[d]);
+            }
+          else
+            {
+              std::ostringstream name;
+              name << pcapPrefix << "-" << m_dev[d].node << "-" << devid[d] << ".pcap";
+              fn = name.str ();
+            }
+          files[d] = helper.CreateFile (fn, std::ios::out, PcapHelper::DLT_PPP);
+        }
+      for (uint64_t i = 0; i < n; i++)
+        {
+          if (rec[i].kind != NSGPU_TR_DEQUEUE && rec[i].kind != NSGPU_TR_RX)
+            {
+              continue;
+            }
+          uint64_t len = 0;
+          NSGPU_TRY (nsgpu_trace_packet (m_codec, &rec[i], &pkt[0], pkt.size (), &len));
+          files[rec[i].dev]->Write (TimeStep ((int64_t) rec[i].ts), &pkt[0], (uint32_t) len);
+        }
+    }
 }
 
 } // namespace ns3

@@ -117,6 +117,7 @@ SIGNATURES = {
     "nsgpu_sim_sched_stats": (C.c_int, [_vp, _vp, _vp, _vp]),
     "nsgpu_sim_set_log": (C.c_int, [_vp, _vp, _vp, _vp, _u64]),
     "nsgpu_sim_attach_p2p": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_adopt_p2p": (C.c_int, [_vp, _vp]),
     "nsgpu_sim_p2p_send": (C.c_int, [_vp, _u32]),
     "nsgpu_sim_attach_wifi": (C.c_int, [_vp, _vp]),
     "nsgpu_sim_wifi_send": (C.c_int, [_vp, _u32, _u32, C.c_double, _u32, _u64, _u32, _u32]),
@@ -705,6 +706,11 @@ class Sim:
     # ---- mixed host / device runs ----
     def attach_p2p(self, engine):
         check(lib().nsgpu_sim_attach_p2p(self.h, engine.h))
+        self._engine = engine
+
+    def adopt_p2p(self, engine):
+        """nsgpu_sim_adopt_p2p: the engine takes over after setup-time events were scheduled here."""
+        check(lib().nsgpu_sim_adopt_p2p(self.h, engine.h))
         self._engine = engine
 
     def p2p_send(self, app):

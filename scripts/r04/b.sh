@@ -1,0 +1,8 @@
+# r04 b: graph probe + deferred pipeline parity + default bench
+set -e
+O=gpurun_out/r04b; mkdir -p $O
+timeout -k 10 60 ./scripts/build/probe_graph 8 12 > $O/probe_graph_8_12.log 2>&1
+timeout -k 10 60 ./scripts/build/probe_graph 3 10 > $O/probe_graph_3_10.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_wide.py tests/test_gpu_p2p.py tests/test_gpu_mixed.py > $O/pytest_p2p.log 2>&1
+timeout -k 10 300 python -u bench.py > $O/bench_default.log 2>&1
+NSGPU_P2P_NODEFER=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-secondary > $O/bench_nodefer.log 2>&1

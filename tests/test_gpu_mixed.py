@@ -188,3 +188,78 @@ def test_send_after_engine_finished_is_refused():
     sim.schedule(5_000_000_000, late)  # long after the flow's last device event
     sim.run()
     assert errs and "finished" in errs[0]
+
+
+def adopt_run(sc, own_event_ts=None):
+    """ns3::HipSimulatorImpl + NsgpuP2pScenario::FromNodeList / AdoptInto, as the C++ module calls the C-ABI:
+    the program's setup-time Schedule calls go to the host runtime first (the journal: Node::Start,
+    NetDevice::Start, Application::Start, ScheduleDestroy, Simulator::Stop, in program order), then the
+    engine built from the same scenario takes them over (nsgpu_sim_remove_key, nsgpu_sim_adopt_p2p) and Run
+    pulls windows.  `own_event_ts`: one event of the program's own, scheduled between the setup calls, that
+    stays on the host."""
+    sim = nsgpu.Sim()
+    owned = []
+    handle = 2
+    own = None
+    for i, (kind, k) in enumerate(sc.setup):
+        if own_event_ts is not None and i == len(sc.setup) // 2:
+            handle += 2
+            own = (own_event_ts, sim.insert_raw(own_event_ts, 0xFFFFFFFF, handle), handle)
+        handle += 2
+        if kind == p2p.SETUP_UID:
+            sim.destroy_insert(handle)  # (NodeListPriv / ChannelListPriv's ScheduleDestroy)
+            continue
+        ts, ctx = 0, 0
+        if kind in (p2p.SETUP_NODE, p2p.SETUP_NOOP):
+            ctx = k
+        elif kind == p2p.SETUP_DEVICE:
+            ctx = sc.dev[k][0]
+        elif kind == p2p.SETUP_APP:
+            ctx = sc.apps[k]["node"]
+        elif kind == p2p.SETUP_STOP:
+            ts, ctx = sc.stop_ns, 0xFFFFFFFF
+        owned.append((ts, sim.insert_raw(ts, ctx, handle), ctx, handle))
+    if own is not None:  # the engine's setup list counts the program's own call as a consumed uid
+        j = len(sc.setup) // 2
+        sc.setup.insert(j, (p2p.SETUP_UID, 0))
+    eng = p2p.Engine(sc, log_cap=200000)
+    eng.reset()
+    for ts, uid, ctx, h in owned:
+        sim.remove_key(ts, uid, ctx, h)
+    sim.adopt_p2p(eng)
+    sim.set_log(200000)
+    host = []
+    while True:
+        w = sim.pop_window()
+        if len(w) == 0:
+            break
+        for ev in w:
+            if sim.begin(ev) == 0:
+                host.append(int(ev["handle"]) & ~1)
+    return sim, eng, host, own
+
+
+def test_adopt_after_setup_equals_attach_before():
+    """The engine adopted after the stock helpers scheduled the setup events dispatches exactly the run the
+    oracle (and the attach-before-setup path) makes: same pop log, digest, counters, next uid."""
+    sc = flows_grid()
+    o = run_oracle(sc, 0, 1, 0, 0, 0, 200000)
+    sim, eng, host, _own = adopt_run(sc)
+    assert host == []
+    st, devc, appc, (lts, luid, lctx) = eng.results(log_n=200000)
+    assert sim.dispatched() == o[0].dispatched and int(st.digest) == o[0].digest
+    assert sim.next_uid() == o[0].next_uid
+    assert np.array_equal(devc, o[1]) and np.array_equal(appc, o[2])
+    n = int(o[0].dispatched)
+    for a, b, name in zip((lts, luid, lctx), o[3], ("ts", "uid", "ctx")):
+        assert np.array_equal(a[:n], b[:n]), name
+
+
+def test_adopt_keeps_the_programs_own_setup_event():
+    """A Schedule call of the program's own among the setup calls stays a host event (its uid is consumed in
+    the engine's setup list): it runs at its time, between the device events."""
+    sc = flows_grid()
+    sim, eng, host, own = adopt_run(sc, own_event_ts=150_000_000)
+    assert host == [own[2]]
+    st = eng.results(log_n=0)[0]
+    assert sim.dispatched() == int(st.dispatched) + 1

@@ -2,8 +2,8 @@
 
 `ns-3-dev-dnemu_amd/ns3-module/model/*.cc` (ns3::HipSimulatorImpl, ns3::HipBatchScheduler,
 ns3::NsgpuP2pScenario) are compiled with g++ -std=gnu++98 -fsyntax-only (the reference is C++98,
-wscript:318-330) against /root/reference/src/core/model's headers, laid out as the ns3/ include
-directory a waf build makes.  Only the waf-generated ns3/core-config.h is written here (three
+wscript:318-330) against the reference's headers (core, network, point-to-point, internet, applications),
+laid out as the ns3/ include directory a waf build makes.  Only the waf-generated ns3/core-config.h is written here (three
 feature macros) — it configures the int64x64 implementation; no reference code
 is built or linked.  Skipped where the reference tree is absent (the GPU box)."""
 import glob
@@ -26,8 +26,14 @@ def ns3_include(tmp_path_factory):
     root = tmp_path_factory.mktemp("ns3inc")
     inc = root / "ns3"
     inc.mkdir()
-    for h in glob.glob(os.path.join(REF, "src", "core", "model", "*.h")):
-        os.symlink(h, inc / os.path.basename(h))
+    # the headers of the modules the sources include (core, and for NsgpuP2pScenario::FromNodeList / WriteTraces
+    # network, point-to-point, internet, applications), flattened into ns3/ as a waf build does
+    for mod in ("core", "network", "point-to-point", "internet", "applications"):
+        for sub in ("model", "helper", "utils"):
+            for h in glob.glob(os.path.join(REF, "src", mod, sub, "*.h")):
+                dst = inc / os.path.basename(h)
+                if not dst.exists():
+                    os.symlink(h, dst)
     (inc / "core-config.h").write_text("#define HAVE___UINT128_T 1\n#define INT64X64_USE_128 1\n#define HAVE_STDLIB_H 1\n")
     return str(root)
 
