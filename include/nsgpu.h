@@ -467,6 +467,34 @@ int nsgpu_trace_ascii(const nsgpu_trace_codec *c, const nsgpu_trace_record *rec,
                       uint64_t *len);   /* every record's line (EnableAsciiAll / EnableAsciiIpv4All on one stream) */
 int nsgpu_trace_pcap(const nsgpu_trace_codec *c, const nsgpu_trace_record *rec, uint64_t n, uint32_t dev, uint8_t *out,
                      uint64_t cap, uint64_t *len);  /* device dev's pcap file (EnablePcapAll) */
+/* ---- Wi-Fi sniffer records (YansWifiPhyHelper's sinks for the GPU-resident PHY) ----
+ * YansWifiPhy calls MonitorSnifferTx in SendPacket (src/wifi/model/yans-wifi-phy.cc:516-519) and
+ * MonitorSnifferRx after an EndReceive whose m_random draw passed (:783-790, signal / noise dBm from the
+ * event's rxPowerW and the SNR); the State Tx / RxOk traces fire at the same instants.  The frame bytes
+ * are the host MAC's (the device keeps sizes only): record tx's frame is frames[frame_off[tx] ..
+ * frame_off[tx + 1]), its printed text (Packet::Print, for the ascii sinks) text[text_off[tx] ..). */
+typedef struct nsgpu_wifi_sniff {
+  uint64_t ts;           /* Now () of the call (ns) */
+  uint32_t phy, tx;      /* the phy (YansWifiChannel index: its file / context) and the transmission */
+  uint32_t kind;         /* 0: MonitorSnifferTx (+ State Tx), 1: MonitorSnifferRx (+ State RxOk) */
+  uint32_t rate;         /* dataRate500KbpsUnits = the mode's GetDataRate () / 500000 */
+  uint32_t freq_mhz;     /* GetChannelFrequencyMhz () */
+  uint32_t short_preamble;
+  double signal_dbm, noise_dbm;  /* Rx: RatioToDb (rxPowerW) + 30, RatioToDb (rxPowerW / snr) - RxNoiseFigure + 30 */
+} nsgpu_wifi_sniff;
+/* an Ok EndReceive's signal / noise dBm (yans-wifi-phy.cc:788-789) from its nsgpu_wifil_end */
+int nsgpu_wifi_sniff_power(const nsgpu_wifil_end *e, double rx_noise_figure_db, double *signal_dbm, double *noise_dbm);
+/* phy's pcap file (YansWifiPhyHelper::EnablePcapInternal, yans-wifi-helper.cc:415-445): dlt 105
+ * (DLT_IEEE802_11: the frame as is) or 127 (DLT_IEEE802_11_RADIO: a RadiotapHeader first — TSFT = Now in us,
+ * flags FCS included | short preamble, rate, channel frequency and CCK / OFDM / 2 / 5 GHz flags, and for Rx
+ * the antenna signal / noise dBm; PcapSniffTxEvent / PcapSniffRxEvent, :244-392) */
+int nsgpu_wifi_pcap(uint32_t dlt, const nsgpu_wifi_sniff *rec, uint64_t n, uint32_t phy, const uint64_t *frame_off,
+                    const uint8_t *frames, uint8_t *out, uint64_t cap, uint64_t *len);
+/* EnableAsciiAll (stream) lines (AsciiPhyTransmitSinkWithContext / AsciiPhyReceiveSinkWithContext,
+ * yans-wifi-helper.cc:42-88, connected at /NodeList/<node>/DeviceList/<device>/$ns3::WifiNetDevice/Phy/State/
+ * Tx and .../RxOk, :529-535): "t|r <Now ().GetSeconds ()> <context> <packet>" */
+int nsgpu_wifi_ascii(const nsgpu_wifi_sniff *rec, uint64_t n, const uint32_t *phy_node, const uint32_t *phy_device,
+                     const uint64_t *text_off, const char *text, char *out, uint64_t cap, uint64_t *len);
 /* PcapFile::Init + Write (src/network/utils/pcap-file.cc:300-381) of arbitrary packets: record i is
  * data[off[i] .. off[i + 1]) with origLen orig_len[i] (inclLen = min (origLen, snaplen, its bytes)) */
 int nsgpu_pcap_file(uint32_t linktype, uint32_t snaplen, uint64_t n, const uint32_t *sec, const uint32_t *usec,

@@ -378,6 +378,8 @@ typedef struct nsgpu_wifil_end {
   double snr, per;
   uint32_t tx;     /* the transmission (SendPacket call) it receives */
   uint32_t flags;  /* NSGPU_WIFI_END_CANCELLED */
+  double rx_w;     /* the event's received power (InterferenceHelper::Event::GetRxPowerW): with snr, the
+                    * MonitorSnifferRx signal / noise dBm of an Ok reception (yans-wifi-phy.cc:788-789) */
 } nsgpu_wifil_end;
 
 /* WifiPhyStateHelper of one phy at Now (wifi-phy-state-helper.cc:159-183). */

@@ -21,6 +21,7 @@
 // scenario (devices, routes, applications) and its addressing (nsgpu_trace_addressing).  Pinned by the
 // reference's first.cc md5s and known.pcap (tests/test_trace_codec_cpu.py).
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -411,6 +412,89 @@ int nsgpu_trace_pcap(const nsgpu_trace_codec *c, const nsgpu_trace_record *rec, 
     const uint64_t us = r.ts / 1000;  // (Time::GetMicroSeconds, PcapFileWrapper::Write)
     pcap_rec(o, (uint32_t)(us / 1000000), (uint32_t)(us % 1000000), pk.data(), (uint32_t)pk.size(), (uint32_t)pk.size(),
              65535);
+  }
+  return copy_out(o.data(), o.size(), out, cap, len);
+}
+
+// ---- Wi-Fi sniffer records ----
+int nsgpu_wifi_sniff_power(const nsgpu_wifil_end *e, double rx_noise_figure_db, double *signal_dbm, double *noise_dbm) {
+  if (!e || !signal_dbm || !noise_dbm) return set_error(NSGPU_EINVAL, "nsgpu_wifi_sniff_power: null");
+  // yans-wifi-phy.cc:788-789 (RatioToDb: 10 log10, wifi-utils / yans-wifi-phy.cc)
+  *signal_dbm = 10.0 * std::log10(e->rx_w) + 30;
+  *noise_dbm = 10.0 * std::log10(e->rx_w / e->snr) - rx_noise_figure_db + 30;
+  return NSGPU_OK;
+}
+
+namespace {
+// RadiotapHeader as PcapSniffTxEvent / PcapSniffRxEvent build it (radiotap-header.cc:69-138: fields in bit
+// order, little-endian, after the 8-byte header; setters at :231-380)
+void radiotap(std::vector<uint8_t> &o, const nsgpu_wifi_sniff &r) {
+  const bool rx = r.kind == 1;
+  const uint32_t present = 0x1u | 0x2u | 0x4u | 0x8u | (rx ? 0x20u | 0x40u : 0u);
+  const uint16_t length = (uint16_t)(8 + 8 + 1 + 1 + 4 + (rx ? 2 : 0));
+  o.push_back(0), o.push_back(0);
+  o.push_back((uint8_t)length), o.push_back((uint8_t)(length >> 8));
+  le32(o, present);
+  const uint64_t tsft = r.ts / 1000;  // Simulator::Now ().GetMicroSeconds ()
+  for (int i = 0; i < 8; i++) o.push_back((uint8_t)(tsft >> (8 * i)));
+  o.push_back((uint8_t)(0x10u | (r.short_preamble ? 0x02u : 0u)));  // FCS included, short preamble
+  o.push_back((uint8_t)r.rate);
+  uint16_t cf = 0;
+  switch (r.rate) {
+    case 2: case 4: case 10: case 22: cf |= 0x0020; break;  // CCK (1, 2, 5.5, 11 Mb/s)
+    default: cf |= 0x0040; break;                           // OFDM
+  }
+  cf |= r.freq_mhz < 2500 ? 0x0080 : 0x0100;
+  o.push_back((uint8_t)r.freq_mhz), o.push_back((uint8_t)(r.freq_mhz >> 8));
+  o.push_back((uint8_t)cf), o.push_back((uint8_t)(cf >> 8));
+  if (rx) {
+    auto dbm8 = [](double v) -> uint8_t {
+      if (v > 127) return (uint8_t)127;
+      if (v < -128) return (uint8_t)(int8_t)-128;
+      return (uint8_t)(int8_t)std::floor(v + 0.5);
+    };
+    o.push_back(dbm8(r.signal_dbm));
+    o.push_back(dbm8(r.noise_dbm));
+  }
+}
+}  // namespace
+
+int nsgpu_wifi_pcap(uint32_t dlt, const nsgpu_wifi_sniff *rec, uint64_t n, uint32_t phy, const uint64_t *frame_off,
+                    const uint8_t *frames, uint8_t *out, uint64_t cap, uint64_t *len) {
+  if (!len || (n && (!rec || !frame_off || !frames))) return set_error(NSGPU_EINVAL, "nsgpu_wifi_pcap: null");
+  if (dlt != 105 && dlt != 127)
+    return set_error(NSGPU_EINVAL, "nsgpu_wifi_pcap: data link type %u (105: IEEE802_11, 127: radiotap)", dlt);
+  std::vector<uint8_t> o, pk;
+  pcap_header(o, dlt, 65535);
+  for (uint64_t i = 0; i < n; i++) {
+    const nsgpu_wifi_sniff &r = rec[i];
+    if (r.phy != phy) continue;
+    if (r.kind > 1 || frame_off[r.tx + 1] < frame_off[r.tx])
+      return set_error(NSGPU_EINVAL, "nsgpu_wifi_pcap: record %llu is malformed", (unsigned long long)i);
+    pk.clear();
+    if (dlt == 127) radiotap(pk, r);
+    pk.insert(pk.end(), frames + frame_off[r.tx], frames + frame_off[r.tx + 1]);
+    const uint64_t us = r.ts / 1000;
+    pcap_rec(o, (uint32_t)(us / 1000000), (uint32_t)(us % 1000000), pk.data(), (uint32_t)pk.size(),
+             (uint32_t)pk.size(), 65535);
+  }
+  return copy_out(o.data(), o.size(), out, cap, len);
+}
+
+int nsgpu_wifi_ascii(const nsgpu_wifi_sniff *rec, uint64_t n, const uint32_t *phy_node, const uint32_t *phy_device,
+                     const uint64_t *text_off, const char *text, char *out, uint64_t cap, uint64_t *len) {
+  if (!len || (n && (!rec || !phy_node || !phy_device || !text_off || !text)))
+    return set_error(NSGPU_EINVAL, "nsgpu_wifi_ascii: null");
+  std::string o;
+  char b[160];
+  for (uint64_t i = 0; i < n; i++) {
+    const nsgpu_wifi_sniff &r = rec[i];
+    if (r.kind > 1) return set_error(NSGPU_EINVAL, "nsgpu_wifi_ascii: record %llu is malformed", (unsigned long long)i);
+    std::snprintf(b, sizeof b, "%s %g /NodeList/%u/DeviceList/%u/$ns3::WifiNetDevice/Phy/State/%s ", r.kind ? "r" : "t",
+                  (double)r.ts / 1e9, phy_node[r.phy], phy_device[r.phy], r.kind ? "RxOk" : "Tx");
+    o += b;
+    o.append(text + text_off[r.tx], text + text_off[r.tx + 1]);
+    o += "\n";
   }
   return copy_out(o.data(), o.size(), out, cap, len);
 }

@@ -407,7 +407,8 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
     }
     if (!take_r) {  // ---- YansWifiPhy::EndReceive (yans-wifi-phy.cc:770-799)
       const int64_t nw = (int64_t)eb.ts;
-      nsgpu_wifil_end rec{eb.ts, eb.euid, (uint32_t)j, 0.0, 0.0, eb.tx, eb.can ? (uint32_t)NSGPU_WIFI_END_CANCELLED : 0u};
+      nsgpu_wifil_end rec{eb.ts, eb.euid, (uint32_t)j, 0.0, 0.0, eb.tx, eb.can ? (uint32_t)NSGPU_WIFI_END_CANCELLED : 0u,
+                          eb.can ? 0.0 : eb.w};
       LEck eck{0, NONE, 0.0};
       P.c.end++;
       if (eb.can) {  // EventImpl::Invoke skips a cancelled event (event-impl.cc:40-46); still dispatched

@@ -194,6 +194,9 @@ SIGNATURES = {
     "nsgpu_trace_ascii": (C.c_int, [_vp, _vp, _u64, _vp, _u64, _vp]),
     "nsgpu_trace_pcap": (C.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _vp]),
     "nsgpu_pcap_file": (C.c_int, [_u32, _u32, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
+    "nsgpu_wifi_sniff_power": (C.c_int, [_vp, C.c_double, _vp, _vp]),
+    "nsgpu_wifi_pcap": (C.c_int, [_u32, _vp, _u64, _u32, _vp, _vp, _vp, _u64, _vp]),
+    "nsgpu_wifi_ascii": (C.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
 }
 
 _lib = None
@@ -641,6 +644,12 @@ class Sim:
 
     def next_uid(self):
         return self._state()[3]
+
+    def current_uid(self):
+        """The uid of the event being dispatched (the closure now running)."""
+        u = C.c_uint32()
+        check(lib().nsgpu_sim_current_uid(self.h, C.byref(u)))
+        return u.value
 
     # ---- windows (the pull interface ns3::HipSimulatorImpl uses) ----
     def insert_raw(self, ts, ctx, handle):

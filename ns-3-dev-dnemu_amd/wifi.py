@@ -261,7 +261,71 @@ def group_run(engines, stream=None):
 NIST, YANS = 0, 1  # nsgpu_wifil_error_model
 IDLE, RX, TX, CCA_BUSY = 0, 1, 2, 3  # nsgpu_wifil_state
 WIFIL_END_DTYPE = np.dtype([("ts", "<u8"), ("uid", "<u4"), ("phy", "<u4"), ("snr", "<f8"), ("per", "<f8"),
-                            ("tx", "<u4"), ("flags", "<u4")])
+                            ("tx", "<u4"), ("flags", "<u4"), ("rx_w", "<f8")])
+
+
+# ---- sniffer records (YansWifiPhyHelper's pcap / ascii sinks; the codec is in libnsgpu: nsgpu_wifi_*) ----
+WIFI_SNIFF_DTYPE = np.dtype([("ts", "<u8"), ("phy", "<u4"), ("tx", "<u4"), ("kind", "<u4"), ("rate", "<u4"),
+                             ("freq_mhz", "<u4"), ("short_preamble", "<u4"), ("signal_dbm", "<f8"),
+                             ("noise_dbm", "<f8")])
+DLT_IEEE802_11, DLT_IEEE802_11_RADIO = 105, 127
+
+
+def sniff_power(end, noise_figure_db):
+    """An Ok EndReceive's MonitorSnifferRx signal / noise dBm (yans-wifi-phy.cc:788-789), through the library."""
+    e = np.ascontiguousarray(np.array([end], dtype=WIFIL_END_DTYPE))
+    sig, noi = C.c_double(), C.c_double()
+    nsgpu.check(nsgpu.lib().nsgpu_wifi_sniff_power(e.ctypes.data, noise_figure_db, C.byref(sig), C.byref(noi)))
+    return sig.value, noi.value
+
+
+def sniff_records(txs, ends, ok, mode, preamble, noise_figure_db, freq_mhz):
+    """The sniffer calls of a closed-loop run in dispatch order: MonitorSnifferTx for every SendPacket (txs:
+    (ts, closure uid, phy), transmission index = row) and MonitorSnifferRx for every EndReceive whose draw
+    passed (ok[i] for ends[i]; cancelled ones never), keyed by the calling event's (ts, uid)."""
+    rate = int(mode[1]) // 500000
+    short = 1 if preamble == PREAMBLE_SHORT else 0
+    rows, keys = [], []
+    for k, (ts, uid, phy) in enumerate(np.asarray(txs, np.uint64).reshape(-1, 3)):
+        rows.append((int(ts), int(phy), k, 0, rate, freq_mhz, short, 0.0, 0.0))
+        keys.append((int(ts), int(uid)))
+    for e, o in zip(ends, ok):
+        if not o or (int(e["flags"]) & END_CANCELLED):
+            continue
+        sig, noi = sniff_power(e, noise_figure_db)
+        rows.append((int(e["ts"]), int(e["phy"]), int(e["tx"]), 1, rate, freq_mhz, short, sig, noi))
+        keys.append((int(e["ts"]), int(e["uid"])))
+    order = sorted(range(len(rows)), key=lambda i: keys[i])
+    return np.array([rows[i] for i in order], dtype=WIFI_SNIFF_DTYPE)
+
+
+def _frames(frames):
+    off = np.zeros(len(frames) + 1, np.uint64)
+    off[1:] = np.cumsum([len(f) for f in frames]) if frames else []
+    data = np.frombuffer(b"".join(bytes(f) for f in frames) or b"\0", np.uint8).copy()
+    return off, data
+
+
+def sniff_pcap(dlt, recs, phy, frames):
+    """phy's pcap file (YansWifiPhyHelper::EnablePcap, DLT 105 or 127) from sniffer records; frames[tx] = the
+    transmission's frame bytes (the host MAC's)."""
+    import p2p
+    recs = np.ascontiguousarray(recs, dtype=WIFI_SNIFF_DTYPE)
+    off, data = _frames(frames)
+    return p2p._out_bytes(lambda o, c, n: nsgpu.lib().nsgpu_wifi_pcap(dlt, recs.ctypes.data, len(recs), phy,
+                                                                     off.ctypes.data, data.ctypes.data, o, c, n))
+
+
+def sniff_ascii(recs, phy_node, phy_device, texts):
+    """EnableAsciiAll (stream) lines of the sniffer records; texts[tx] = the frame's Packet::Print text."""
+    import p2p
+    recs = np.ascontiguousarray(recs, dtype=WIFI_SNIFF_DTYPE)
+    off, data = _frames([t.encode() for t in texts])
+    pn = np.ascontiguousarray(phy_node, np.uint32)
+    pd = np.ascontiguousarray(phy_device, np.uint32)
+    return p2p._out_bytes(lambda o, c, n: nsgpu.lib().nsgpu_wifi_ascii(recs.ctypes.data, len(recs), pn.ctypes.data,
+                                                                      pd.ctypes.data, off.ctypes.data, data.ctypes.data,
+                                                                      o, c, n)).decode()
 
 
 class WifilConfigStruct(C.Structure):

@@ -184,7 +184,21 @@ typedef struct nsref_wifil_mac {
 } nsref_wifil_mac;
 int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, uint64_t *log_ts, uint32_t *log_uid,
                     uint32_t *log_ctx, uint64_t log_cap, nsgpu_wifil_end *ends, uint64_t ends_cap, uint64_t *n_ends,
-                    nsgpu_wifi_phy_counters *phys, uint64_t out[6]);
+                    nsgpu_wifi_phy_counters *phys, uint64_t out[6], uint64_t *tx_out, uint64_t tx_cap);
+/* (tx_out: 3 words per SendPacket call — ts, the closure's uid, phy — up to tx_cap calls; may be NULL)
+ * A replayed transmission schedule (SendPacket of phy[k] with size[k] at ts[k], whatever the PHY state) on
+ * the closed-loop PHY, then Simulator::Stop (stop_ts). */
+typedef struct nsref_wifil_sends {
+  uint64_t n;
+  const uint64_t *ts;
+  const uint32_t *phy, *size;
+  uint32_t modclass, bw, preamble, pad_;
+  uint64_t rate, stop_ts;
+  double dbm;
+} nsref_wifil_sends;
+int nsref_wifil_replay(const nsgpu_wifil_config *cfg, const nsref_wifil_sends *sn, uint64_t *log_ts, uint32_t *log_uid,
+                       uint32_t *log_ctx, uint64_t log_cap, nsgpu_wifil_end *ends, uint64_t ends_cap, uint64_t *n_ends,
+                       nsgpu_wifi_phy_counters *phys, uint64_t out[6], uint64_t *tx_out, uint64_t tx_cap);
 /* InterferenceHelper::CalculateChunkSuccessRate's error-rate model call for one chunk (tests). */
 double nsref_wifil_chunk_success(uint32_t model, uint32_t modclass, uint64_t rate, uint32_t bw, double snr, uint32_t nbits);
 

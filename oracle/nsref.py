@@ -476,7 +476,7 @@ def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble,
     f = lib().nsref_wifil_run
     f.restype = C.c_int
     f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
-                  C.c_void_p, C.c_void_p, C.c_void_p]
+                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     first = np.ascontiguousarray(first, np.uint64)
     backoff = np.ascontiguousarray(backoff, np.uint64)
     m = WifilMacStruct(first.ctypes.data, backoff.ctypes.data, period, stop_ts, mode[1], size, mode[0], mode[2],
@@ -487,8 +487,10 @@ def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble,
     phys = np.zeros(n_phy, phys_dtype)
     out = np.zeros(6, np.uint64)
     n = C.c_uint64()
+    txo = np.zeros((1 << 20, 3), np.uint64)
     args = lambda ends, cap: (C.byref(cfg_struct), C.byref(m), lts.ctypes.data, luid.ctypes.data, lctx.ctypes.data,
-                              log_cap, ends, cap, C.byref(n), phys.ctypes.data, out.ctypes.data)
+                              log_cap, ends, cap, C.byref(n), phys.ctypes.data, out.ctypes.data, txo.ctypes.data,
+                              txo.shape[0])
     rc = f(*args(None, 0))
     if rc != 0:
         raise RuntimeError(f"nsref_wifil_run: {rc}")
@@ -497,6 +499,49 @@ def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble,
     if rc != 0:
         raise RuntimeError(f"nsref_wifil_run: {rc}")
     tot = dict(zip(("dispatched", "digest", "next_uid", "final_ts", "sends", "busy"), (int(v) for v in out)))
+    tot["txs"] = txo[:min(tot["sends"], txo.shape[0])].copy()  # (ts, closure uid, phy) per SendPacket
+    k = min(tot["dispatched"], log_cap)
+    return (lts[:k], luid[:k], lctx[:k]), ends, phys, tot
+
+
+class WifilSendsStruct(C.Structure):  # nsref_wifil_sends (nsref.h)
+    _fields_ = [("n", C.c_uint64), ("ts", C.c_void_p), ("phy", C.c_void_p), ("size", C.c_void_p),
+                ("modclass", C.c_uint32), ("bw", C.c_uint32), ("preamble", C.c_uint32), ("pad_", C.c_uint32),
+                ("rate", C.c_uint64), ("stop_ts", C.c_uint64), ("dbm", C.c_double)]
+
+
+def wifil_replay(cfg_struct, ts, phy, size, mode, preamble, dbm, stop_ts, n_phy, end_dtype, phys_dtype, log_cap=1 << 16):
+    """A replayed transmission schedule on the closed-loop oracle PHY (nsref_wifil_replay): SendPacket of phy[k]
+    (size[k] bytes) at ts[k], host closures scheduled at setup in send order, then Stop (stop_ts).  Returns as
+    wifil_run."""
+    f = lib().nsref_wifil_replay
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+    ts = np.ascontiguousarray(ts, np.uint64)
+    phy = np.ascontiguousarray(phy, np.uint32)
+    size = np.ascontiguousarray(size, np.uint32)
+    sn = WifilSendsStruct(len(ts), ts.ctypes.data, phy.ctypes.data, size.ctypes.data, mode[0], mode[2], preamble, 0,
+                          mode[1], stop_ts, dbm)
+    lts = np.zeros(log_cap, np.uint64)
+    luid = np.zeros(log_cap, np.uint32)
+    lctx = np.zeros(log_cap, np.uint32)
+    phys = np.zeros(n_phy, phys_dtype)
+    out = np.zeros(6, np.uint64)
+    n = C.c_uint64()
+    txo = np.zeros((len(ts) + 1, 3), np.uint64)
+    args = lambda ends, cap: (C.byref(cfg_struct), C.byref(sn), lts.ctypes.data, luid.ctypes.data, lctx.ctypes.data,
+                              log_cap, ends, cap, C.byref(n), phys.ctypes.data, out.ctypes.data, txo.ctypes.data,
+                              txo.shape[0])
+    rc = f(*args(None, 0))
+    if rc != 0:
+        raise RuntimeError(f"nsref_wifil_replay: {rc}")
+    ends = np.zeros(n.value, end_dtype)
+    rc = f(*args(ends.ctypes.data, n.value))
+    if rc != 0:
+        raise RuntimeError(f"nsref_wifil_replay: {rc}")
+    tot = dict(zip(("dispatched", "digest", "next_uid", "final_ts", "sends", "busy"), (int(v) for v in out)))
+    tot["txs"] = txo[:min(tot["sends"], txo.shape[0])].copy()  # (ts, closure uid, phy) per SendPacket
     k = min(tot["dispatched"], log_cap)
     return (lts[:k], luid[:k], lctx[:k]), ends, phys, tot
 

@@ -456,6 +456,7 @@ struct LoopTx {
   uint32_t phy;
   Mode mode;
   uint32_t preamble;
+  uint32_t uid;  // the SendPacket's closure (its sniffer record's place in the dispatch order)
 };
 struct LoopEnd {  // an EndReceive's event data
   uint32_t phy, tx, cancelled;
@@ -468,13 +469,13 @@ struct Loop {
   std::vector<Phy> phy;
   std::vector<LoopTx> txs;
   std::vector<LoopEnd> endv;
-  enum { ATTEMPT = 0, RX = 1, END = 2, STOP = 3 };
+  enum { ATTEMPT = 0, RX = 1, END = 2, STOP = 3, SEND = 4 };
   struct E {
     uint32_t kind, a, b, ctx;
     double rx_dbm;
   };
   std::map<std::pair<uint64_t, uint32_t>, E> q;
-  uint32_t uid = 4, ctx = 0xffffffffu;
+  uint32_t uid = 4, ctx = 0xffffffffu, cur_uid = 0;
   uint64_t now = 0, dispatched = 0, digest = 0, sends = 0, busy = 0;
   double edW, ccaW, noiseFigure;
   std::vector<nsgpu_wifil_end> ends;
@@ -600,6 +601,7 @@ struct Loop {
     t.phy = i;
     t.mode = make_mode(mac->modclass, mac->rate, mac->bw);
     t.preamble = mac->preamble;
+    t.uid = cur_uid;
     t.dur = nsref_wifi_tx_duration(mac->size, mac->modclass, mac->rate, mac->bw, mac->preamble);
     const uint32_t k = (uint32_t)txs.size();
     txs.push_back(t);
@@ -614,6 +616,39 @@ struct Loop {
       schedule(now + (uint64_t)delay, E{RX, k, (uint32_t)j, cfg->node[j], rx});
     }
     schedule(now + mac->period, E{ATTEMPT, i, 0, ctx, 0.0});
+    return 0;
+  }
+  // YansWifiPhy::SendPacket from a host closure whatever the state (a replayed transmission schedule):
+  // yans-wifi-phy.cc:499-522 — a reception in progress is abandoned (m_endRxEvent.Cancel, NotifyRxEnd;
+  // SwitchToTx's RX case, wifi-phy-state-helper.cc:263-268), then the channel's fan-out
+  int send_packet(uint32_t i, uint32_t size, uint32_t modclass, uint64_t rate, uint32_t bw, uint32_t preamble,
+                  double dbm) {
+    Phy &p = phy[i];
+    if (p.endTx > (int64_t)now) return -3;  // NS_ASSERT (!IsStateTx ())
+    if (p.rxing) {
+      endv[(size_t)p.endRxEvent].cancelled = 1;
+      p.rxing = false;
+      p.irxing = false;
+      p.endRx = (int64_t)now;
+    }
+    LoopTx t;
+    t.ts = now;
+    t.phy = i;
+    t.mode = make_mode(modclass, rate, bw);
+    t.preamble = preamble;
+    t.uid = cur_uid;
+    t.dur = nsref_wifi_tx_duration(size, modclass, rate, bw, preamble);
+    const uint32_t k = (uint32_t)txs.size();
+    txs.push_back(t);
+    p.endTx = (int64_t)now + t.dur;
+    sends++;
+    for (int64_t j = 0; j < cfg->n_phy; j++) {  // YansWifiChannel::Send — yans-wifi-channel.cc:77-115
+      if (j == (int64_t)i || cfg->channel[j] != cfg->channel[i]) continue;
+      double d = nsref_distance(cfg->x[i], cfg->y[i], cfg->z[i], cfg->x[j], cfg->y[j], cfg->z[j]);
+      int64_t delay = nsref_const_speed_delay(d, cfg->speed);
+      double rx = nsref_calc_rx_power(dbm, d, &cfg->loss);
+      schedule(now + (uint64_t)delay, E{RX, k, (uint32_t)j, cfg->node[j], rx});
+    }
     return 0;
   }
   // YansWifiPhy::StartReceivePacket — yans-wifi-phy.cc:399-496
@@ -662,7 +697,7 @@ struct Loop {
     LoopEnd &r = endv[e];
     Phy &p = phy[r.phy];
     p.c.end++;
-    nsgpu_wifil_end out{now, euid, r.phy, 0.0, 0.0, r.tx, 0u};
+    nsgpu_wifil_end out{now, euid, r.phy, 0.0, 0.0, r.tx, 0u, r.cancelled ? 0.0 : r.w};
     if (r.cancelled) {
       p.c.end_cancelled++;
       out.flags = NSGPU_WIFI_END_CANCELLED;
@@ -752,13 +787,77 @@ int nsref_wifi_run(const nsgpu_wifi_scenario *sc, nsgpu_wifi_stats *stats, nsgpu
 }
 
 
+// A replayed transmission schedule: host closures scheduled at setup in send order (Schedule (ts_k, SendPacket
+// of phy_k)), then Simulator::Stop (Time); the same PHY and run loop as nsref_wifil_run.
+int nsref_wifil_replay(const nsgpu_wifil_config *cfg, const nsref_wifil_sends *sn, uint64_t *log_ts, uint32_t *log_uid,
+                       uint32_t *log_ctx, uint64_t log_cap, nsgpu_wifil_end *ends, uint64_t ends_cap, uint64_t *n_ends,
+                       nsgpu_wifi_phy_counters *phys, uint64_t out[6], uint64_t *tx_out, uint64_t tx_cap) {
+  Loop L;
+  L.cfg = cfg;
+  L.mac = nullptr;
+  L.phy.resize((size_t)cfg->n_phy);
+  L.edW = Loop::DbmToW(cfg->ed_threshold_dbm);
+  L.ccaW = Loop::DbmToW(cfg->cca_threshold_dbm);
+  L.noiseFigure = pow(10.0, cfg->rx_noise_figure_db / 10.0);
+  for (uint64_t k = 0; k < sn->n; k++) {
+    if (sn->phy[k] >= (uint64_t)cfg->n_phy) return -4;
+    L.schedule(sn->ts[k], Loop::E{Loop::SEND, (uint32_t)k, 0, 0xffffffffu, 0.0});
+  }
+  L.schedule(sn->stop_ts, Loop::E{Loop::STOP, 0, 0, 0xffffffffu, 0.0});
+  while (!L.q.empty()) {
+    auto it = L.q.begin();
+    const Loop::E e = it->second;
+    L.now = it->first.first;
+    const uint32_t euid = it->first.second;
+    L.q.erase(it);
+    L.ctx = e.ctx;
+    L.cur_uid = euid;
+    const uint64_t rank = L.dispatched++;
+    L.digest += nsgpu_dispatch_digest_term(rank, L.now, euid);
+    if (rank < log_cap) {
+      log_ts[rank] = L.now;
+      log_uid[rank] = euid;
+      log_ctx[rank] = e.ctx;
+    }
+    if (e.kind == Loop::STOP) break;
+    if (e.kind == Loop::SEND) {
+      const int rc = L.send_packet(sn->phy[e.a], sn->size[e.a], sn->modclass, sn->rate, sn->bw, sn->preamble, sn->dbm);
+      if (rc) return rc;
+    } else if (e.kind == Loop::RX) {
+      L.start_receive(e.a, e.b, e.rx_dbm);
+    } else if (e.kind == Loop::END) {
+      L.end_receive(e.a, euid);
+    }
+  }
+  out[0] = L.dispatched;
+  out[1] = L.digest;
+  out[2] = L.uid;
+  out[3] = L.now;
+  out[4] = L.sends;
+  out[5] = L.busy;
+  if (tx_out)  // the SendPacket calls: (ts, closure uid, phy), in call order (= transmission index)
+    for (size_t k = 0; k < L.txs.size() && k < tx_cap; k++) {
+      tx_out[3 * k] = L.txs[k].ts;
+      tx_out[3 * k + 1] = L.txs[k].uid;
+      tx_out[3 * k + 2] = L.txs[k].phy;
+    }
+  if (n_ends) *n_ends = L.ends.size();
+  if (ends) {
+    if (L.ends.size() > ends_cap) return -2;
+    for (size_t i = 0; i < L.ends.size(); i++) ends[i] = L.ends[i];
+  }
+  if (phys)
+    for (int64_t j = 0; j < cfg->n_phy; j++) phys[j] = L.phy[(size_t)j].c;
+  return 0;
+}
+
 double nsref_wifil_chunk_success(uint32_t model, uint32_t modclass, uint64_t rate, uint32_t bw, double snr, uint32_t nbits) {
   return chunk_success(model, make_mode(modclass, rate, bw), snr, nbits);
 }
 
 int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, uint64_t *log_ts, uint32_t *log_uid,
                     uint32_t *log_ctx, uint64_t log_cap, nsgpu_wifil_end *ends, uint64_t ends_cap, uint64_t *n_ends,
-                    nsgpu_wifi_phy_counters *phys, uint64_t out[6]) {
+                    nsgpu_wifi_phy_counters *phys, uint64_t out[6], uint64_t *tx_out, uint64_t tx_cap) {
   Loop L;
   L.cfg = cfg;
   L.mac = mac;
@@ -776,6 +875,7 @@ int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, u
     const uint32_t euid = it->first.second;
     L.q.erase(it);
     L.ctx = e.ctx;
+    L.cur_uid = euid;
     const uint64_t rank = L.dispatched++;
     L.digest += nsgpu_dispatch_digest_term(rank, L.now, euid);
     if (rank < log_cap) {
@@ -794,6 +894,12 @@ int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, u
   out[3] = L.now;
   out[4] = L.sends;
   out[5] = L.busy;
+  if (tx_out)  // the SendPacket calls: (ts, closure uid, phy), in call order (= transmission index)
+    for (size_t k = 0; k < L.txs.size() && k < tx_cap; k++) {
+      tx_out[3 * k] = L.txs[k].ts;
+      tx_out[3 * k + 1] = L.txs[k].uid;
+      tx_out[3 * k + 2] = L.txs[k].phy;
+    }
   if (n_ends) *n_ends = L.ends.size();
   if (ends) {
     if (L.ends.size() > ends_cap) return -2;

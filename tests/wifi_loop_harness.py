@@ -40,6 +40,7 @@ def run_gpu(sc, log_cap=1 << 20):
     sim.attach_wifi(lp)
     sim.set_log(log_cap)
     cnt = {"sends": 0, "busy": 0}
+    txs = []  # (ts, closure uid, phy) per SendPacket: the MonitorSnifferTx records
 
     def attempt(i):
         st, _ = sim.wifi_state(i)
@@ -47,6 +48,7 @@ def run_gpu(sc, log_cap=1 << 20):
             cnt["busy"] += 1
             sim.schedule(int(sc["backoff"][i]), lambda: attempt(i))
             return
+        txs.append((sim.now(), sim.current_uid(), i))
         sim.wifi_send(i, sc["size"], sc["dbm"], sc["mode"], sc["preamble"])
         cnt["sends"] += 1
         sim.schedule(sc["period"], lambda: attempt(i))
@@ -61,6 +63,7 @@ def run_gpu(sc, log_cap=1 << 20):
     ends = lp.read_ends()
     phys = lp.read_phys()
     tot = dict(dispatched=sim.dispatched(), digest=digest, next_uid=sim.next_uid(), final_ts=sim.now(), **cnt)
+    tot["txs"] = np.array(txs, np.uint64).reshape(-1, 3)
     lp_keep = (sim, lp)
     return log, ends, phys, tot, lp_keep
 
