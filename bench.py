@@ -274,6 +274,38 @@ class P2PGridDist:
             "ranks": self.world}
 
 
+class P2PDumbbellDist(P2PGridDist):
+    """Config 5 as BASELINE names it: simple-distributed.cc's 1,000,000-node dumbbell (2 x 499,999 leaves)
+    partitioned by system id (Node (systemId), simple-distributed.cc:98-246: the left leaves and router 1 on
+    rank 0, router 2 and the right leaves on the others — with more than 2 ranks the right leaves in
+    contiguous blocks, p2p.dumbbell_owner), one partition per rank through the partitioned engine (RCCL X0 /
+    X1 allgathers + X2 all-to-all per window, the sequential (ts, uid) order).  The same simulation however
+    many ranks: strong scaling; `value` counts its events once.  On one rank (`--partitioned`) every node
+    is rank 0's."""
+    scaling = "strong"
+
+    def __init__(self, args, stream, rank, world, td):
+        import numpy as np
+        import p2p
+        self.p2p, self.rank, self.world, self.td = p2p, rank, world, td
+        n = args.dumbbell_leaves
+        self.scenario = p2p.dumbbell(n)
+        owner = (p2p.dumbbell_owner(n, world) if world > 1 else np.zeros(self.scenario.n_nodes, np.uint32))
+        uid = [p2p.Comm.unique_id() if rank == 0 else None]
+        if td is not None:
+            td.broadcast_object_list(uid, src=0)
+        self.comm = p2p.Comm(uid[0], world, rank)
+        self.engine = p2p.DistEngine(self.scenario, owner, rank, world, self.comm, stream=stream)
+        self.workload = (f"simple-distributed.cc dumbbell (config 5): {self.scenario.n_nodes} nodes (2 x {n} leaves), "
+                         f"routers 5Mb/s 5ms, leaves 1Mb/s 2ms, DropTail(100), {n} OnOff UDP flows 1Mb/s 512B "
+                         f"MaxBytes 512 left i -> right i, 1-5s, Stop 5s; partitioned by system id over {world} "
+                         f"rank(s) (simple-distributed.cc Node (sid)), RCCL X0/X1 allgather + X2 all-to-all per "
+                         f"window, sequential (ts, uid) order")
+
+    def cpu_baseline(self):
+        return P2PGrid.cpu_baseline(self)
+
+
 class WifiFanout:
     """Config 3's hot loop: YansWifiChannel::Send (yans-wifi-channel.cc:77-115) over the
     wifi-simple-adhoc-grid scaled to 10,000 nodes (100 x 100, 100 m spacing, one channel),
@@ -571,7 +603,8 @@ def main():
                     help="p2p-grid: skip the wifi-grid / dumbbell entries of the `secondary` list")
     ap.add_argument("--secondary-steps", type=int, default=3, help="timed steps of each secondary workload")
     ap.add_argument("--partitioned", action="store_true",
-                    help="p2p-grid / wifi-grid through the partitioned engine even on one rank (RCCL with one rank)")
+                    help="p2p-grid / wifi-grid / dumbbell through the partitioned engine even on one rank (RCCL "
+                         "with one rank)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -589,9 +622,11 @@ def main():
         td.init_process_group("gloo")  # env:// (MASTER_ADDR / MASTER_PORT / RANK / WORLD_SIZE)
         tdist = td
     stream = nsgpu.Stream()
-    partitioned = args.workload in ("p2p-grid", "wifi-grid") and (world > 1 or args.partitioned)
+    partitioned = args.workload in ("p2p-grid", "wifi-grid", "dumbbell") and (world > 1 or args.partitioned)
     if partitioned and args.workload == "wifi-grid":
         wl = WifiGridDist(args, stream.handle, rank, world, tdist)
+    elif partitioned and args.workload == "dumbbell":
+        wl = P2PDumbbellDist(args, stream.handle, rank, world, tdist)
     elif partitioned:
         wl = P2PGridDist(args, stream.handle, rank, world, tdist)
     else:
@@ -680,7 +715,7 @@ def main():
                                             "replicas" if world > 1 else "single")}, **extra),
             "roofline": roofline,
         }
-        if not args.no_cpu_baseline and world == 1 and not partitioned:
+        if not args.no_cpu_baseline and world == 1 and (not partitioned or hasattr(wl, "cpu_baseline")):
             out["cpu_baseline"], out["speedup_vs_cpu"] = cpu_baseline_of(wl, value, digest)
         # the north star's other GPU targets (configs 3 and 5) in the same line, on the same box: each a
         # whole run per step, digest-checked against the oracle like the primary

@@ -280,7 +280,9 @@ struct P2PDev {
   struct Stg *stage;      // [2][NMAX] a window's records in rank order (k2_pa stages, k2_sdef reads)
   uint2 *sleaf;           // [2][NMAX][maxc] their inline DoForwardUp leaves: (context, child index)
   uint32_t *cpt;          // [2][NMAX] child prefix by rank (k2_sdef): provisional uids resolve through it
-  uint32_t *dmap;         // [LCAP] local record -> dense index of its window (k2_rank)
+  uint32_t *dmap;         // [2][LCAP] local record -> dense index of its window (k2_rank; by window parity)
+  uint32_t *sip, *sgs;    // [NMAX] each: df_sdef's inline prefix by rank and same-ts group starts (scratch)
+  uint32_t sdef_fold;     // df_sdef runs as k2_rank's block 1 (1) or as its own kernel k2_sdef (0)
 };
 
 // ---------------- wave / block helpers ----------------
@@ -2005,7 +2007,11 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.stage, 2 * (size_t)NMAX));
     TRY(dalloc(h, &M.sleaf, 2 * (size_t)NMAX * M.maxc));
     TRY(dalloc(h, &M.cpt, 2 * (size_t)NMAX));
-    TRY(dalloc(h, &M.dmap, LCAP));
+    TRY(dalloc(h, &M.dmap, 2 * (size_t)LCAP));
+    TRY(dalloc(h, &M.sip, NMAX));
+    TRY(dalloc(h, &M.sgs, NMAX));
+    const char *e = getenv("NSGPU_P2P_SDEF_KERNEL");  // (diagnostic: the accounting as its own kernel)
+    M.sdef_fold = (e && e[0] == '1') ? 0u : 1u;
   }
   if (hipMemset(M.lrec, 0, NMAX * sizeof(uint32_t)) != hipSuccess || hipMemset(M.lcnt, 0, NLR * sizeof(uint32_t)) != hipSuccess) {
     nsgpu_p2p_destroy(h);
@@ -2207,7 +2213,7 @@ bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, bool df, hipEvent_t ev0 =
       return true;
     case 2:
       if (!wide) return false;
-      if (df) hipExtLaunchKernelGGL(k2_rank<true>, dim3(RK_GRID), dim3(RKT), 0, s, ev0, ev1, 0, h->M);
+      if (df) hipExtLaunchKernelGGL(k2_rank<true>, dim3(RK_GRID_DF), dim3(RKT_DF), 0, s, ev0, ev1, 0, h->M);
       else hipExtLaunchKernelGGL(k2_rank<false>, dim3(RK_GRID), dim3(RKT), 0, s, ev0, ev1, 0, h->M);
       return true;
     case 3:
@@ -2219,8 +2225,8 @@ bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, bool df, hipEvent_t ev0 =
       if (!(wide && h->M.trace)) return false;
       hipExtLaunchKernelGGL(k_tpatch, dim3(64), dim3(256), 0, s, ev0, ev1, 0, h->M);
       return true;
-    default:  // k2_sdef(n) after k2_rank(n + 1): window n was staged by k2_pa(n + 1)
-      if (!df) return false;
+    default:  // k2_sdef(n) after k2_rank(n + 1): window n was staged by k2_pa(n + 1) (folded: k2_rank's block 1)
+      if (!df || h->M.sdef_fold) return false;
       hipExtLaunchKernelGGL(k2_sdef, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
       return true;
   }
@@ -2432,7 +2438,8 @@ static int drive(nsgpu_p2p *h, bool *paused) {
         have_prev = false;
         continue;
       }
-      if (!df && dfu) {  // a normal window ended the replay: back to the deferred pipeline
+      if (!df && dfu && c.mode == MODE_NORMAL) {  // a normal window ended the replay: back to the deferred pipeline
+        // (not in a sorted run's chunks: those belong to the other pipeline until the run is over)
         if (!h->eager && !h->gexec_df) {
           const int rc = build_graph(h, true);
           if (rc) return rc;

@@ -1764,7 +1764,7 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   Red &R = M.dist ? x1hdr(M.x1_send, 0)->red : C.red[rt];
   if (WIDE && bx == 0 && threadIdx.x == 0) {  // what k2_rank ranks and accounts (its bookkeeping rewrites C.W ...)
     C.rk_W = W;
-    C.rk_go = 2u | ((handle && !run) ? 1u : 0u);  // 2: a window was formed; 1: handled normally (ranked)
+    C.rk_go = 2u | ((handle && !run) ? 1u : 0u) | (run ? 4u : 0u);  // 2: formed; 1: ranked; 4: a sorted run's chunk
     C.rk_win = c_wn;
     C.rk_lim = hc.lim;
   }
@@ -1857,14 +1857,24 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 // copies the window's keys / contexts for the next k2_pa (pwkey / pwctx: k2_scan's job in the other
 // pipeline), and its block 0 does the window's bookkeeping (df_book); the dispatch accounting (log, digest,
 // uid resolution) is deferred to k2_sdef once the next k2_pa has staged the records in rank order.
+template <int NT>
+__device__ void df_sdef(const P2PDev &M, Ctl &C);
+constexpr int RKT_DF = 1024;              // the deferred pipeline's k2_rank blocks: SUBS tiles at once
+constexpr int RK_GRID_DF = RK_GRID / (RKT_DF / RKT) + 2;
 template <bool DF>
-__global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
+__global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
+  constexpr int NT = DF ? RKT_DF : RKT, SUBS = NT / RKT;
   Ctl &C = *M.C;
   BLK_T0();
 #ifdef NSGPU_PHASE_PROF
   const uint64_t c_win = C.windows;
   uint32_t n_tie = 0;
 #endif
+  // DF: block 1 does the last window's dispatch accounting (k2_pa staged it) beside this window's ranking
+  if (DF && blockIdx.x == 1) {
+    if (M.sdef_fold) df_sdef<NT>(M, C);
+    return;
+  }
   uint32_t c_done = 0, c_mode = 0, W, c_fr = 0, go = 3;
   uint64_t lim, wn;
   if (DF) {
@@ -1875,24 +1885,31 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
   const uint32_t lc = threadIdx.x < (uint32_t)NLR ? M.lcnt[threadIdx.x] : 0u;  // (its trip overlaps the control's)
   if (DF) {
     if (!(go & 2u)) return;  // (no window was formed: the run is over or paused)
+    if (go & 4u) {  // (a sorted run's chunk: the host drives runs with the other pipeline — never here)
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicOr(M.error, 256u);
+        C.done = 1;
+      }
+      return;
+    }
   } else if (c_done || c_mode >= MODE_SORT || c_mode == MODE_RUN || W > (uint32_t)WCAP || c_fr || lim == 0) {
     return;
   }
   const bool ranked = (go & 1u) != 0;
   __shared__ uint32_t pre[NLR + 1];
-  __shared__ ulonglong2 cw[RKC];
-  local_prefix<RKT>((ranked && lim) ? lc : 0u, pre);
+  __shared__ ulonglong2 cws[SUBS][RKC];
+  local_prefix<NT>((ranked && lim) ? lc : 0u, pre);
   const uint32_t Lt = pre[NLR], N = W + Lt;
   uint32_t *const wr = wrank_of(M, wn), *const lr = lrank_of(M, wn);
-  uint32_t b0 = blockIdx.x, nb = gridDim.x;  // (DF: block 0 keeps the books, the others rank)
+  uint32_t b0 = blockIdx.x, nb = gridDim.x;  // (DF: block 0 keeps the books, block 1 accounts, the others rank)
   if (DF) {
     if (blockIdx.x == 0) {
-      df_book<RKT>(M, C, ranked, W, Lt, wn);
+      df_book<NT>(M, C, ranked, W, Lt, wn);
       return;
     }
     if (!ranked) return;
-    b0 -= 1, nb -= 1;
-    for (uint32_t i = b0 * RKT + threadIdx.x; i < W; i += nb * RKT) {  // (the next k2_pa rewrites wkey / wctx)
+    b0 -= 2, nb -= 2;
+    for (uint32_t i = b0 * NT + threadIdx.x; i < W; i += nb * NT) {  // (the next k2_pa rewrites wkey / wctx)
       M.pwkey[i] = M.wkey[i];
       M.pwctx[i] = M.wctx[i];
     }
@@ -1907,14 +1924,23 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
   BLK_MARK(48, c_win);
   const uint32_t nr = (N + RKT - 1) / RKT, ncl = (Lt + RKC - 1) / RKC;  // phase A: rows x local columns
   const uint32_t nl = (Lt + RKT - 1) / RKT, ncg = (W + RKC - 1) / RKC;  // phase B: local rows x gen-0 columns
-  const uint32_t na = nr * ncl;
-  for (uint32_t t = b0; t < na + nl * ncg; t += nb) {  // (uniform over the block)
+  const uint32_t na = nr * ncl, ntile = na + nl * ncg;
+  // SUBS tiles a block at once: sub-tile `sub` is RKT threads (whole waves) with its own column buffer
+  const uint32_t sub = threadIdx.x / RKT, lt = threadIdx.x % RKT;
+  ulonglong2 *const cw = cws[sub];
+  uint32_t *const dmap = DF ? M.dmap + (wn & 1) * (uint64_t)LCAP : nullptr;
+  for (uint32_t t0 = b0 * SUBS; t0 < ntile; t0 += nb * SUBS) {  // (uniform over the block)
+    const uint32_t t = t0 + sub;
+    const bool tA = t < na, tB = !tA && t < ntile;
     uint32_t c = 0, slot = 0;  // slot: the row's accumulator (wrank[dense] for gen-0, LBASE + k for local k)
-    if (t < na) {  // rows: every record; columns: local records
-      const uint32_t ti = t / ncl, tj = t % ncl;
-      const uint32_t ix = ti * RKT + threadIdx.x;
-      if (threadIdx.x < (uint32_t)RKC) {
-        const uint32_t cy = tj * RKC + threadIdx.x;
+    uint32_t ix = 0, rx = 0, tj = 0;
+    uint64_t wx = ~0ull, wx2 = ~0ull, relx = 0;
+    if (tA) {  // rows: every record; columns: local records
+      const uint32_t ti = t / ncl;
+      tj = t % ncl;
+      ix = ti * RKT + lt;
+      if (lt < (uint32_t)RKC) {
+        const uint32_t cy = tj * RKC + lt;
         ulonglong2 w = make_ulonglong2(~0ull, ~0ull);  // (a padding column: after every row)
         if (cy < Lt) {
           const uint32_t r = dense_rec(W + cy, W, pre);
@@ -1923,13 +1949,11 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
             M.ldat[cy] = make_uint4(r, M.nchild[r] | (M.ninl[r] << 16), (uint32_t)(w.x >> 32), M.wpar[r]);
             M.lrec[cy] = r;
             M.pwctx[r] = M.wctx[r];
-            if (DF) M.dmap[r - LBASE] = cy;  // (k2_sdef: a local parent's rank)
+            if (DF) dmap[r - LBASE] = cy;  // (df_sdef: a local parent's rank)
           }
         }
-        cw[threadIdx.x] = w;
+        cw[lt] = w;
       }
-      uint64_t wx = ~0ull, wx2 = ~0ull;
-      uint32_t rx = 0;
       if (ix < N) {
         rx = dense_rec(ix, W, pre);
         if (ix >= W) {
@@ -1941,8 +1965,19 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
           wx2 = 0;
         }
       }
-      __syncthreads();
-      BLK_MARK(50, c_win);
+    } else if (tB) {  // rows: local records; columns: gen-0 records (rel ts <= the row's)
+      const uint32_t u = t - na, ti = u / ncg;
+      tj = u % ncg;
+      ix = ti * RKT + lt;
+      if (lt < (uint32_t)RKC) {
+        const uint32_t cy = tj * RKC + lt;
+        cw[lt].x = cy < W ? M.wkey[cy] >> 32 : ~0ull;
+      }
+      if (ix < Lt) relx = M.wkey[dense_rec(W + ix, W, pre)] >> 32;
+    }
+    __syncthreads();
+    BLK_MARK(50, c_win);
+    if (tA) {
       bool tie = false;
       const uint32_t self = ix - W - tj * RKC;  // (the row's own column, if it is one of this tile's)
 #pragma unroll 16
@@ -1967,16 +2002,7 @@ __global__ __launch_bounds__(RKT) void k2_rank(const P2PDev M) {
       }
       if (ix >= N) c = 0;
       slot = ix >= W ? ix - W + LBASE : rx;
-    } else {  // rows: local records; columns: gen-0 records (rel ts <= the row's)
-      const uint32_t u = t - na, ti = u / ncg, tj = u % ncg;
-      const uint32_t ix = ti * RKT + threadIdx.x;
-      if (threadIdx.x < (uint32_t)RKC) {
-        const uint32_t cy = tj * RKC + threadIdx.x;
-        cw[threadIdx.x].x = cy < W ? M.wkey[cy] >> 32 : ~0ull;
-      }
-      uint64_t relx = 0;
-      if (ix < Lt) relx = M.wkey[dense_rec(W + ix, W, pre)] >> 32;
-      __syncthreads();
+    } else if (tB) {
 #pragma unroll 16
       for (uint32_t y = 0; y < (uint32_t)RKC; y++) c += cw[y].x <= relx;
       if (ix >= Lt) c = 0;
@@ -2100,21 +2126,22 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 // record's through its parent's rank and this window's prefixes); the log and digest get every record and
 // leaf; the child prefixes are kept (cpt) for the provisional uids of window n's children.  Afterwards the
 // window's rank accumulators are cleared (their parity is window n + 2's).
-__global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
-  Ctl &C = *M.C;
+// NT threads of one block (k2_rank<true>'s block 1, or the k2_sdef kernel); the prefixes by rank live in
+// global scratch (cpt, sip, sgs: L2-resident, read back by this block after its barrier).
+template <int NT>
+__device__ void df_sdef(const P2PDev &M, Ctl &C) {
   const uint32_t sf = C.sflag;
   if (!(sf & 1u)) return;
   const uint32_t wi = (sf >> 1) & 3u, pn = wi & 1u;  // window n & 3, its parity
   const WInfo w = C.winfo[wi];
   const uint32_t uidq = C.winfo[(wi + 3) & 3].uid0;  // window n - 1's uid base
   const uint32_t N = w.N;
-  constexpr int RPT = NMAX / SCAN_THREADS;
-  __shared__ uint32_t s_cp[NMAX];   // child prefix by rank
-  __shared__ uint32_t s_ip[NMAX];   // inline prefix by rank
-  __shared__ uint32_t s_gs[NMAX];   // start rank of each ts group
-  __shared__ uint64_t wsum[SCAN_THREADS / 64];
+  constexpr int RPT = NMAX / NT;
+  __shared__ uint64_t wsum[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const Stg *st = M.stage + (uint64_t)pn * NMAX;
+  uint32_t *const s_cp = M.cpt + (uint64_t)pn * NMAX;  // child prefix by rank (kept for window n's children)
+  uint32_t *const s_ip = M.sip, *const s_gs = M.sgs;   // inline prefix by rank, start rank of each ts group
   // the scan's fields in registers (rel ts, counts); the rest is read again for the outputs (L2 hits)
   uint32_t erel[RPT], ecnt[RPT];
   uint32_t prev_rel = 0;
@@ -2150,56 +2177,56 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
   if (lane == 63) wsum[wid] = inc;
   __syncthreads();
   uint64_t off = 0, tot = 0;
-  for (int k = 0; k < SCAN_THREADS / 64; k++) {
+  for (int k = 0; k < NT / 64; k++) {
     const uint64_t x = wsum[k];
     off += k < wid ? x : 0;
     tot += x;
   }
   const uint64_t ex = off + inc - sum;
   const uint32_t tinl = (uint32_t)((tot >> 21) & 0x1fffffu), ng = (uint32_t)(tot >> 42);
-  uint32_t bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu), bh = (uint32_t)(ex >> 42);
-  uint32_t cpr[RPT], ipr[RPT], grp[RPT];
+  const uint32_t bc0 = (uint32_t)(ex & 0x1fffffu), bi0 = (uint32_t)((ex >> 21) & 0x1fffffu), bh0 = (uint32_t)(ex >> 42);
   {
-    uint32_t pr = prev_rel;
+    uint32_t pr = prev_rel, bc = bc0, bi = bi0, bh = bh0;
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
       const uint32_t r = tid * RPT + q;
-      uint32_t hd = 0;
       if (r < N) {
         const uint32_t rel = erel[q];
-        hd = r == 0 || rel != pr;
+        const uint32_t hd = r == 0 || rel != pr;
         pr = rel;
-      }
-      bh += hd;
-      grp[q] = bh - 1;
-      cpr[q] = bc;
-      ipr[q] = bi;
-      if (r < N) {
+        bh += hd;
         s_cp[r] = bc;
         s_ip[r] = bi;
         if (hd) s_gs[bh - 1] = r;
-        M.cpt[(uint64_t)pn * NMAX + r] = bc;
         bc += ecnt[q] & 0xffffu;
         bi += ecnt[q] >> 16;
       }
     }
   }
-  __syncthreads();
+  __syncthreads();  // (workgroup scope: the block's global writes above are visible to its waves)
   // own uids, log and digest (records at K0 + rank + the leaves of earlier groups; leaves after their group)
   const uint32_t *const wr = M.wrank + (uint64_t)pn * WTOT, *const lr = M.lrank + (uint64_t)pn * LMAX;
   const uint32_t *const cq = M.cpt + (uint64_t)(pn ^ 1u) * NMAX;
+  const uint32_t *const dmap = M.dmap + (uint64_t)pn * LCAP;
   uint64_t digest = 0;
+  uint32_t pr = prev_rel, bc = bc0, bi = bi0, bh = bh0;
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
     if (r >= N) continue;
-    const Stg e = st[r];
-    const uint32_t rel = erel[q];
+    const Stg e = st[r];  // (rel ts and counts again from the record: the register copies are dead here)
+    const uint32_t rel = (uint32_t)(e.key >> 32), ecn = e.cnt;
+    const uint32_t hd = r == 0 || rel != pr;
+    pr = rel;
+    bh += hd;
+    const uint32_t cpr = bc, ipr = bi;
+    bc += ecn & 0xffffu;
+    bi += ecn >> 16;
     const uint64_t t = w.tmin + rel;
     uint32_t uid = (uint32_t)e.key;
     if (e.loc) {  // a local record: its parent's child prefix + its child index
       const uint32_t p = e.par & 0xffffffu, j = e.par >> 24;
-      uint32_t rp = p < LBASE ? wr[p] : (p - LBASE < (uint32_t)LCAP ? lr[M.dmap[p - LBASE] % LMAX] : ~0u);
+      uint32_t rp = p < LBASE ? wr[p] : (p - LBASE < (uint32_t)LCAP ? lr[dmap[p - LBASE] % LMAX] : ~0u);
       if (rp >= N) {  // (cannot happen: the parent is a record of this window)
         atomicOr(M.error, 256u);
         rp = 0;
@@ -2209,7 +2236,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
       if (((uid >> 30) & 1u) != (pn ^ 1u)) atomicOr(M.error, 256u);
       uid = uidq + cq[((uid & 0x3fffffffu) >> 8) % NMAX] + (uid & 0xffu);
     }
-    const uint32_t g = grp[q];
+    const uint32_t g = bh - 1;
     const uint32_t first = s_gs[g];
     const uint32_t last = (g + 1 < ng ? s_gs[g + 1] : N) - 1;
     const uint64_t rk = w.K0 + r + (tinl ? s_ip[first] : 0u);
@@ -2219,12 +2246,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
       M.log_uid[rk] = uid;
       M.log_ctx[rk] = e.ctx;
     }
-    const uint32_t ni = ecnt[q] >> 16;
+    const uint32_t ni = ecn >> 16;
     const uint2 *lf = M.sleaf + ((uint64_t)pn * NMAX + r) * M.maxc;
     for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
       const uint2 l = lf[k];
-      const uint64_t lk = w.K0 + last + 1 + ipr[q] + k;
-      const uint32_t lu = w.uid0 + cpr[q] + l.y;
+      const uint64_t lk = w.K0 + last + 1 + ipr + k;
+      const uint32_t lu = w.uid0 + cpr + l.y;
       digest += digest_term(lk, t, lu);
       if (lk < M.log_cap) {
         M.log_ts[lk] = t;
@@ -2237,10 +2264,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
   digest = wave_sum64(digest);
   __syncthreads();  // (every lookup of the rank accumulators is done: clear them for window n + 2)
   if (lane == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
-  for (uint32_t i = tid; i < w.W; i += SCAN_THREADS) M.wrank[(uint64_t)pn * WTOT + i] = 0;
-  for (uint32_t i = tid; i < w.Lt; i += SCAN_THREADS) M.lrank[(uint64_t)pn * LMAX + i] = 0;
+  for (uint32_t i = tid; i < w.W; i += NT) M.wrank[(uint64_t)pn * WTOT + i] = 0;
+  for (uint32_t i = tid; i < w.Lt; i += NT) M.lrank[(uint64_t)pn * LMAX + i] = 0;
   if (tid == 0) C.sflag = 0;
 }
+__global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) { df_sdef<SCAN_THREADS>(M, *M.C); }
 
 // ---- k2_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
 // WIDE: the single engine's wide windows: the local records join the gen-0 ones (ranks from k2_rank), and

@@ -4,7 +4,7 @@
 T=$1; LOG=$2; shift 2
 for i in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@" > "$LOG" 2>&1
-  if grep -q "status=transient" "$LOG" && grep -q "nothing was charged" "$LOG"; then
+  if grep -q "status=transient" "$LOG"; then
     sleep 90
     continue
   fi
