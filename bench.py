@@ -175,7 +175,27 @@ class P2PGrid:
                 "events_per_launch": events_per_step / windows,
                 "step_device_ms": step_kernel_ms, "windows_per_step": windows,
                 "pipeline_ms_per_window": {k: round(v[0] * 1e3, 3) for k, v in prof.items()},
-                "pipeline_unit": "us per launch (hipExtLaunchKernel start/stop events, sampled windows)"}
+                "pipeline_unit": "us per launch (hipExtLaunchKernel start/stop events, sampled windows)",
+                "latency": self.latency_roofline(prof, step_kernel_ms * 1e3 / windows)}
+
+    # dependent memory trips on each kernel's critical path (DESIGN.md §4.4 "latency roofline"): k2_pa reads
+    # the run control + slot records, (local slots) their children, allocates (block atomic), claims node-table
+    # entries (atomic), folds the bound (atomics); k2_handle reads control + slot, node table, the holder's
+    # device / route records, writes local records, ranks (tile loads + atomics); k2_rank reads control +
+    # region counts, chain words, adds ranks (atomics); k2_scan / k2_sdef read control + slots, scan, write.
+    TRIPS = {"k2_pa": 5, "k2_handle": 5, "k2_rank": 3, "k2_scan": 4, "k2_sdef": 3, "k_tpatch": 2}
+
+    def latency_roofline(self, prof, window_us):
+        import nsgpu
+        boundary_us, trip_us = nsgpu.probe_latency()
+        used = [k for k, v in prof.items() if v[1] > 0]
+        trips = sum(self.TRIPS.get(k, 3) for k in used)
+        bound = len(used) * boundary_us + trips * trip_us
+        return {"bound": "latency", "kernels_per_window": len(used), "boundary_us": boundary_us,
+                "trips_per_window": trips, "trip_us": trip_us, "bound_us_per_window": bound,
+                "achieved_us_per_window": window_us, "frac": bound / window_us if window_us else None,
+                "note": "speed of light of the window chain = kernels x boundary + dependent trips x trip latency "
+                        "(nsgpu_probe_latency measures both on this GPU); frac = bound / the graph replay's window"}
 
     def result(self):
         st, devc, appc, _ = self.engine.results()

@@ -381,6 +381,11 @@ const char *nsgpu_p2p_kernel_name(int k);
  * processor records at the kernel's own start and end (hipExtLaunchKernel); kernel_ms[k] and
  * launches[k] (nsgpu_p2p_kernel_count entries) accumulate the bracketed time and launch count. */
 int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_every, double *kernel_ms, uint64_t *launches);
+/* The latency constants of the window pipeline's roofline (diagnostic, not a reference interface): a
+ * kernel boundary (back-to-back launches of an empty 64-block kernel, graph-replayed: us per kernel) and
+ * one dependent global-memory trip (a pointer chase through lines the previous launch rewrote from other
+ * XCDs: us per level). */
+int nsgpu_probe_latency(void *stream, double *boundary_us, double *trip_us);
 /* Mixed host / device runs (driven by nsgpu_sim, see above): the uid the program's own Schedule calls
  * start from (after the setup-time ones); advance = dispatch every device event with a key below
  * (hts, huid) (hts = UINT64_MAX: all of them), with *uid / *dispatched the global uid counter and

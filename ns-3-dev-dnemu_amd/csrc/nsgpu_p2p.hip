@@ -2013,7 +2013,19 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     const char *e = getenv("NSGPU_P2P_SDEF_KERNEL");  // (diagnostic: the accounting as its own kernel)
     M.sdef_fold = (e && e[0] == '1') ? 0u : 1u;
   }
-  if (hipMemset(M.lrec, 0, NMAX * sizeof(uint32_t)) != hipSuccess || hipMemset(M.lcnt, 0, NLR * sizeof(uint32_t)) != hipSuccess) {
+  // (k2_pa loads lrec / ldat entries speculatively and follows their record index: zeroed, every entry
+  // stays < WTOT; the deferred pipeline's arrays start zeroed too, so a stale entry is always in range)
+  bool zok = hipMemset(M.lrec, 0, NMAX * sizeof(uint32_t)) == hipSuccess &&
+             hipMemset(M.lcnt, 0, NLR * sizeof(uint32_t)) == hipSuccess &&
+             hipMemset(M.ldat, 0, LMAX * sizeof(uint4)) == hipSuccess;
+  if (zok && M.wide)
+    zok = hipMemset(M.stage, 0, 2 * (size_t)NMAX * sizeof(Stg)) == hipSuccess &&
+          hipMemset(M.sleaf, 0, 2 * (size_t)NMAX * M.maxc * sizeof(uint2)) == hipSuccess &&
+          hipMemset(M.cpt, 0, 2 * (size_t)NMAX * sizeof(uint32_t)) == hipSuccess &&
+          hipMemset(M.dmap, 0, 2 * (size_t)LCAP * sizeof(uint32_t)) == hipSuccess &&
+          hipMemset(M.sip, 0, NMAX * sizeof(uint32_t)) == hipSuccess &&
+          hipMemset(M.sgs, 0, NMAX * sizeof(uint32_t)) == hipSuccess;
+  if (!zok) {
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipMemset failed");
   }
@@ -2199,41 +2211,156 @@ const char *const KERNEL_NAMES[NKERN] = {"k2_pa", "k2_handle", "k2_rank", "k2_sc
 // Kernel k of the single engine's window (KERNEL_NAMES); a wide engine places its local records after
 // its handlers (k2_rank) and, traced, patches their trace uids (k_tpatch).  Returns
 // whether kernel k is part of this engine's window.
+// (NSGPU_P2P_PLAIN_LAUNCH=1, diagnostic: plain launches instead of hipExtLaunchKernelGGL where no events are asked)
+bool plain_launch() {
+  static const bool p = [] {
+    const char *e = getenv("NSGPU_P2P_PLAIN_LAUNCH");
+    return e && e[0] == '1';
+  }();
+  return p;
+}
+#define NSGPU_KLAUNCH(K, G, B, S, E0, E1, ...)                         \
+  do {                                                                \
+    if (plain_launch() && !(E0)) hipLaunchKernelGGL(K, G, B, 0, S, __VA_ARGS__); \
+    else hipExtLaunchKernelGGL(K, G, B, 0, S, E0, E1, 0, __VA_ARGS__);  \
+  } while (0)
 bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, bool df, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   const bool wide = h->M.wide != 0;
   switch (k) {
     case 0:
-      if (df) hipExtLaunchKernelGGL((k2_pa<false, true, true>), dim3(pa_grid<true>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
-      else if (wide) hipExtLaunchKernelGGL((k2_pa<false, true>), dim3(pa_grid<true>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
-      else hipExtLaunchKernelGGL((k2_pa<false, false>), dim3(pa_grid<false>()), dim3(TB), 0, s, ev0, ev1, 0, h->M);
+      if (df) NSGPU_KLAUNCH((k2_pa<false, true, true>), dim3(pa_grid<true>()), dim3(TB), s, ev0, ev1, h->M);
+      else if (wide) NSGPU_KLAUNCH((k2_pa<false, true>), dim3(pa_grid<true>()), dim3(TB), s, ev0, ev1, h->M);
+      else NSGPU_KLAUNCH((k2_pa<false, false>), dim3(pa_grid<false>()), dim3(TB), s, ev0, ev1, h->M);
       return true;
     case 1:
-      if (wide) hipExtLaunchKernelGGL(k2_handle<true>, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M);
-      else hipExtLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, ev0, ev1, 0, h->M);
+      if (wide) NSGPU_KLAUNCH(k2_handle<true>, dim3(K2_GRID), dim3(HB), s, ev0, ev1, h->M);
+      else NSGPU_KLAUNCH(k2_handle<false>, dim3(K2_GRID), dim3(HB), s, ev0, ev1, h->M);
       return true;
     case 2:
       if (!wide) return false;
-      if (df) hipExtLaunchKernelGGL(k2_rank<true>, dim3(RK_GRID_DF), dim3(RKT_DF), 0, s, ev0, ev1, 0, h->M);
-      else hipExtLaunchKernelGGL(k2_rank<false>, dim3(RK_GRID), dim3(RKT), 0, s, ev0, ev1, 0, h->M);
+      if (df) NSGPU_KLAUNCH(k2_rank<true>, dim3(RK_GRID_DF), dim3(RKT_DF), s, ev0, ev1, h->M);
+      else NSGPU_KLAUNCH(k2_rank<false>, dim3(RK_GRID), dim3(RKT), s, ev0, ev1, h->M);
       return true;
     case 3:
       if (df) return false;  // (the deferred pipeline: df_book in k2_rank, the accounting in k2_sdef)
-      if (wide) hipExtLaunchKernelGGL(k2_scan<true>, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
-      else hipExtLaunchKernelGGL(k2_scan<false>, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
+      if (wide) NSGPU_KLAUNCH(k2_scan<true>, dim3(1), dim3(SCAN_THREADS), s, ev0, ev1, h->M);
+      else NSGPU_KLAUNCH(k2_scan<false>, dim3(1), dim3(SCAN_THREADS), s, ev0, ev1, h->M);
       return true;
     case 4:
       if (!(wide && h->M.trace)) return false;
-      hipExtLaunchKernelGGL(k_tpatch, dim3(64), dim3(256), 0, s, ev0, ev1, 0, h->M);
+      NSGPU_KLAUNCH(k_tpatch, dim3(64), dim3(256), s, ev0, ev1, h->M);
       return true;
     default:  // k2_sdef(n) after k2_rank(n + 1): window n was staged by k2_pa(n + 1) (folded: k2_rank's block 1)
       if (!df || h->M.sdef_fold) return false;
-      hipExtLaunchKernelGGL(k2_sdef, dim3(1), dim3(SCAN_THREADS), 0, s, ev0, ev1, 0, h->M);
+      NSGPU_KLAUNCH(k2_sdef, dim3(1), dim3(SCAN_THREADS), s, ev0, ev1, h->M);
       return true;
   }
 }
-void launch_windows(nsgpu_p2p *h, hipStream_t s, bool df) {
+// Diagnostic mode (eager launches with NSGPU_P2P_DEBUG=1): after every kernel the stream is drained (a
+// fault is reported with the kernel and window that raised it) and k_dbg checks the engine's invariants
+// (pool, free stack, fresh buffer, window records, children), so that a broken state is reported by the
+// kernel that made it instead of faulting a later one.
+// In graph mode (NSGPU_P2P_DEBUG=2) k_dbg runs after every kernel of the replay (`at`: window << 8 | kernel)
+// and a broken invariant also ends the run (done = 2, error 1024) so that the next kernels do nothing.
+__global__ __launch_bounds__(256) void k_dbg(const P2PDev M, unsigned long long *out, unsigned long long at = 0) {
+  Ctl &C = *M.C;
+  const uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, st = (uint64_t)gridDim.x * 256;
+  if (at && out[0]) return;  // (graph mode: the first violation is kept)
+  auto bad = [&](unsigned long long code, unsigned long long a, unsigned long long b) {
+    if (atomicCAS(&out[0], 0ull, code) == 0ull) {
+      out[1] = a;
+      out[2] = b;
+      out[3] = at | ((unsigned long long)C.windows << 32);
+      if (at) {
+        atomicOr(M.error, 1024u);
+        C.done = 2;
+      }
+    }
+  };
+  const uint64_t Pe = C.P_end, nfree = C.nfree, nF = C.nF, W = C.W;
+  if (i0 == 0) {
+    if (Pe > M.pool_cap) bad(1, Pe, M.pool_cap);
+    if (nfree + C.npush > M.pool_cap) bad(2, nfree, C.npush);
+    if (C.live > Pe + nF) bad(3, C.live, Pe);
+    if (nF > M.fcap) bad(4, nF, M.fcap);
+    if (W > M.runcap) bad(5, W, M.runcap);
+  }
+  const uint64_t P = Pe < M.pool_cap ? Pe : M.pool_cap;
+  for (uint64_t p = i0; p < P; p += st)
+    if (M.ev_ts[0][p] != TOMB && ((M.ev_ctx[0][p] >= M.n_nodes && M.ev_ctx[0][p] != ~0u) ||
+                                  (M.ev_kind[0][p] & 0xffu) >= (uint32_t)K_NKINDS))
+      bad(10, p, M.ev_ctx[0][p]);
+  const uint64_t F = nF < M.fcap ? nF : M.fcap;
+  for (uint64_t f = i0; f < F; f += st)
+    if (M.f_ctx[f] >= M.n_nodes && M.f_ctx[f] != ~0u) bad(30, f, M.f_ctx[f]);
+  const uint64_t NF = nfree < M.pool_cap ? nfree : M.pool_cap;
+  for (uint64_t j = i0; j < NF; j += st)
+    if (M.fstack[j] >= P) bad(40, j, M.fstack[j]);
+  const uint64_t Wm = W < (uint64_t)WCAP ? W : (uint64_t)WCAP;
+  if (C.mode != MODE_RUN)
+    for (uint64_t s = i0; s < Wm; s += st) {
+      if (M.wctx[s] >= M.n_nodes && M.wctx[s] != ~0u) bad(20, s, M.wctx[s]);
+      if (M.nchild[s] > M.maxc) bad(21, s, M.nchild[s]);
+    }
+}
+unsigned long long *g_dbg_out = nullptr;
+int dbg_alloc() {  // (before any capture)
+  if (!g_dbg_out) {
+    NSGPU_HIP(hipMalloc(&g_dbg_out, 4 * sizeof(unsigned long long)));
+    NSGPU_HIP(hipMemset(g_dbg_out, 0, 4 * sizeof(unsigned long long)));
+  }
+  return NSGPU_OK;
+}
+int launch_windows_dbg(nsgpu_p2p *h, hipStream_t s, bool df) {
+  if (const int rd = dbg_alloc()) return rd;
+  unsigned long long *dout = g_dbg_out;
+  if (!h->eager) {  // graph capture: checks as graph nodes
+    for (int w = 0; w < NWIN; w++)
+      for (int k = 0; k < NKERN; k++)
+        if (launch_kernel(h, k, s, df)) hipLaunchKernelGGL(k_dbg, dim3(256), dim3(256), 0, s, h->M, dout, (unsigned long long)(w << 8 | k | 0x80000000u));
+    return NSGPU_OK;
+  }
+  static int lines = 0;
+  static const bool trace_c = getenv("NSGPU_P2P_DEBUG_TRACE") != nullptr;
+  for (int w = 0; w < NWIN; w++) {
+    Ctl c{};
+    NSGPU_HIP(hipMemcpyAsync(&c, h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+    if (trace_c && (lines < 400 || c.windows % 10000 == 0) && lines < 2000) {
+      lines++;
+      fprintf(stderr, "[p2p dbg] df %d win %llu mode %u done %u live %llu P_end %llu nfree %llu pvalid %u pchild %llu "
+              "hts %llu hcap %u tmin %llu W %u K %llu uid %u stop %u\n", (int)df, (unsigned long long)c.windows, c.mode,
+              c.done, (unsigned long long)c.live, (unsigned long long)c.P_end, (unsigned long long)c.nfree, c.pvalid,
+              (unsigned long long)c.pchild, (unsigned long long)c.hts, c.hcap, (unsigned long long)c.tmin, c.W,
+              (unsigned long long)c.K, c.uid, c.stop_seen);
+    }
+    for (int k = 0; k < NKERN; k++) {
+      if (!launch_kernel(h, k, s, df)) continue;
+      hipError_t e = hipStreamSynchronize(s);
+      if (e != hipSuccess)
+        return set_error(NSGPU_EHIP, "nsgpu_p2p debug: %s faulted in window %llu (df %d, mode %u): %s", KERNEL_NAMES[k],
+                         (unsigned long long)c.windows, (int)df, c.mode, hipGetErrorString(e));
+      NSGPU_HIP(hipMemsetAsync(dout, 0, 4 * sizeof(unsigned long long), s));
+      hipLaunchKernelGGL(k_dbg, dim3(256), dim3(256), 0, s, h->M, dout);
+      unsigned long long o[4] = {};
+      NSGPU_HIP(hipMemcpyAsync(o, dout, sizeof(o), hipMemcpyDeviceToHost, s));
+      NSGPU_HIP(hipStreamSynchronize(s));
+      if (o[0])
+        return set_error(NSGPU_EHIP, "nsgpu_p2p debug: invariant %llu broken after %s in window %llu (df %d, mode %u): "
+                         "%llu %llu", o[0], KERNEL_NAMES[k], (unsigned long long)c.windows, (int)df, c.mode, o[1], o[2]);
+    }
+  }
+  return NSGPU_OK;
+}
+int launch_windows(nsgpu_p2p *h, hipStream_t s, bool df) {
+  static const int dbg = [] {
+    const char *e = getenv("NSGPU_P2P_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  if ((dbg == 1 && h->eager) || (dbg == 2 && !h->eager)) return launch_windows_dbg(h, s, df);
   for (int w = 0; w < NWIN; w++)
     for (int k = 0; k < NKERN; k++) launch_kernel(h, k, s, df);
+  return NSGPU_OK;
 }
 // The deferred pipeline is used for untraced single wide engines (NSGPU_P2P_NODEFER=1: never).
 bool df_usable(const nsgpu_p2p *h) {
@@ -2360,6 +2487,7 @@ static int build_graph(nsgpu_p2p *h, bool df = false) {
   // one instantiated graph serves every run of this engine
   hipGraphExec_t &gx = df ? h->gexec_df : h->gexec;
   hipGraph_t g = nullptr;
+  if (const int rd = dbg_alloc()) return rd;
   NSGPU_HIP(hipStreamBeginCapture(h->s, h->M.dist ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal));
   int rc = NSGPU_OK;
   if (h->M.dist) rc = launch_windows_dist(h, h->s);
@@ -2406,7 +2534,8 @@ static int drive(nsgpu_p2p *h, bool *paused) {
   }
   for (;;) {
     if (h->eager) {
-      launch_windows(h, h->s, df);
+      const int rc = launch_windows(h, h->s, df);
+      if (rc) return rc;
       NSGPU_HIP(hipGetLastError());
     } else {
       NSGPU_HIP(hipGraphLaunch(df ? h->gexec_df : h->gexec, h->s));
@@ -2635,6 +2764,13 @@ extern "C" int nsgpu_p2p_run(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipEventSynchronize(h->t1));
   NSGPU_HIP(hipStreamSynchronize(h->s));
   NSGPU_HIP(hipEventElapsedTime(&h->last_ms, h->t0, h->t1));
+  if (err & 1024u) {  // (debug mode 2: a graph-resident check stopped the run)
+    unsigned long long o[4] = {};
+    NSGPU_HIP(hipMemcpy(o, g_dbg_out, sizeof(o), hipMemcpyDeviceToHost));
+    return set_error(NSGPU_EHIP, "nsgpu_p2p debug (graph): invariant %llu broken after %s (window %llu of the replay, "
+                     "C.windows %llu): %llu %llu", o[0], KERNEL_NAMES[o[3] & 0xff], (o[3] >> 8) & 0xff, o[3] >> 32, o[1],
+                     o[2]);
+  }
   if (err) return engine_error(err);
   NSGPU_HIP(hipEventRecord(h->ev[0], h->s));
   NSGPU_HIP(hipStreamWaitEvent(cs, h->ev[0], 0));
@@ -2692,10 +2828,11 @@ extern "C" int nsgpu_p2p_set_trace_kinds(nsgpu_p2p *h, uint32_t mask) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_trace_kinds: null");
   if (mask & ~0x7fu) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_trace_kinds: unknown kind bits 0x%x", mask);
   h->M.trace_kinds = mask;
-  if (h->gexec) {
-    (void)hipGraphExecDestroy(h->gexec);
-    h->gexec = nullptr;
-  }
+  for (hipGraphExec_t *g : {&h->gexec, &h->gexec_df})
+    if (*g) {
+      (void)hipGraphExecDestroy(*g);
+      *g = nullptr;
+    }
   return NSGPU_OK;
 }
 

@@ -391,7 +391,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   uint4 ldd = make_uint4((uint32_t)g, 0, 0, 0);
   uint32_t rk2[2] = {0, 0}, ninl0 = 0;
   if (DF && WIDE && g >= (uint64_t)WCAP && slot_role) ldd = M.ldat[g - WCAP];
-  const uint32_t rec = (WIDE && g >= (uint64_t)WCAP && slot_role) ? (DF ? ldd.x : M.lrec[g - WCAP]) : (uint32_t)g;
+  // (a speculative entry past the last window's records is followed too: clamped into the record space)
+  const uint32_t rec =
+      (WIDE && g >= (uint64_t)WCAP && slot_role) ? min(DF ? ldd.x : M.lrec[g - WCAP], (uint32_t)WTOT - 1u) : (uint32_t)g;
   if (slot_role) {  // the slot and its first children
     const uint32_t s = rec;
     spk = M.pwkey[s];
@@ -2246,7 +2248,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C) {
       M.log_uid[rk] = uid;
       M.log_ctx[rk] = e.ctx;
     }
-    const uint32_t ni = ecn >> 16;
+    const uint32_t ni = min(ecn >> 16, M.maxc);  // (bounded: a staged record's leaves fit its row)
     const uint2 *lf = M.sleaf + ((uint64_t)pn * NMAX + r) * M.maxc;
     for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
       const uint2 l = lf[k];

@@ -1,0 +1,91 @@
+// nsgpu_probe.hip — the latency constants of the window pipeline's roofline (include/nsgpu.h
+// nsgpu_probe_latency).  The p2p window is a chain of small kernels, each a few dependent memory trips
+// long: its speed of light is (boundaries x boundary cost) + (dependent trips x trip latency), not HBM
+// bandwidth.  Both constants are measured here, the way the pipeline meets them:
+//  * boundary: an empty 64-block kernel replayed 64 times from a graph (us per kernel);
+//  * trip: 64 blocks chase a pointer chain through a 256-KB table that the previous launch rewrote from
+//    other blocks (other XCDs' L2s), so each level is a dependent load that misses the local L2.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "nsgpu.h"
+#include "nsgpu_internal.h"
+
+namespace nsgpu {
+namespace {
+constexpr int PN = 1 << 16;  // chain table entries (256 KB)
+constexpr int LV = 32;       // chase levels per launch
+
+__global__ __launch_bounds__(64) void k_probe_chase(uint32_t *buf, int levels, uint32_t salt) {
+  const uint32_t tid = blockIdx.x * 64 + threadIdx.x;
+  uint32_t x = (tid * 40503u + salt) % PN;
+  for (int l = 0; l < levels; l++) x = buf[x];
+  // rewrite lines for the next launch (a different block's, so other XCDs hold them dirty)
+  const uint32_t w = ((tid + 997u * salt) * 7919u) % PN;
+  buf[w] = (w * 40503u + 12345u) % PN;
+  if (x == 0xffffffffu) buf[0] = 1;  // (keeps the chain live)
+}
+}  // namespace
+}  // namespace nsgpu
+
+using namespace nsgpu;
+
+extern "C" int nsgpu_probe_latency(void *stream, double *boundary_us, double *trip_us) {
+  if (!boundary_us || !trip_us) return set_error(NSGPU_EINVAL, "nsgpu_probe_latency: null");
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t *buf = nullptr;
+  NSGPU_HIP(hipMalloc(&buf, PN * sizeof(uint32_t)));
+  std::vector<uint32_t> h(PN);
+  for (int i = 0; i < PN; i++) h[i] = (uint32_t)((i * 40503ull + 12345) % PN);
+  hipEvent_t a = nullptr, b = nullptr;
+  hipGraph_t g[2] = {nullptr, nullptr};
+  hipGraphExec_t ge[2] = {nullptr, nullptr};
+  float ms[2] = {0, 0};
+  constexpr int NK = 64, REPS = 20;
+  int rc = NSGPU_OK;
+  auto fail = [&](const char *what, hipError_t e) {
+    rc = set_error(NSGPU_EHIP, "nsgpu_probe_latency: %s: %s", what, hipGetErrorString(e));
+  };
+  hipError_t e = hipMemcpyAsync(buf, h.data(), PN * sizeof(uint32_t), hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) fail("copy", e);
+  if (!rc && (e = hipEventCreate(&a)) != hipSuccess) fail("event", e);
+  if (!rc && (e = hipEventCreate(&b)) != hipSuccess) fail("event", e);
+  for (int v = 0; v < 2 && !rc; v++) {  // v = 0: empty kernels (levels 0), v = 1: LV levels each
+    hipStream_t cs = nullptr;
+    if ((e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) {
+      fail("stream", e);
+      break;
+    }
+    (void)hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    for (int k = 0; k < NK; k++) hipLaunchKernelGGL(k_probe_chase, dim3(64), dim3(64), 0, cs, buf, v ? LV : 0, (uint32_t)k);
+    e = hipStreamEndCapture(cs, &g[v]);
+    (void)hipStreamDestroy(cs);
+    if (e != hipSuccess || (e = hipGraphInstantiate(&ge[v], g[v], nullptr, nullptr, 0)) != hipSuccess) {
+      fail("graph", e);
+      break;
+    }
+    for (int r = 0; r < 3; r++) (void)hipGraphLaunch(ge[v], s);
+    (void)hipEventRecord(a, s);
+    for (int r = 0; r < REPS; r++) (void)hipGraphLaunch(ge[v], s);
+    (void)hipEventRecord(b, s);
+    if ((e = hipEventSynchronize(b)) != hipSuccess) {
+      fail("run", e);
+      break;
+    }
+    (void)hipEventElapsedTime(&ms[v], a, b);
+  }
+  for (int v = 0; v < 2; v++) {
+    if (ge[v]) (void)hipGraphExecDestroy(ge[v]);
+    if (g[v]) (void)hipGraphDestroy(g[v]);
+  }
+  if (a) (void)hipEventDestroy(a);
+  if (b) (void)hipEventDestroy(b);
+  (void)hipFree(buf);
+  if (rc) return rc;
+  const double per0 = 1e3 * ms[0] / (NK * REPS), per1 = 1e3 * ms[1] / (NK * REPS);
+  *boundary_us = per0;
+  *trip_us = std::max(0.0, (per1 - per0) / LV);
+  return NSGPU_OK;
+}

@@ -159,6 +159,7 @@ SIGNATURES = {
     "nsgpu_p2p_phase_read": (C.c_int, [_vp, C.c_int, C.c_int]),
     "nsgpu_p2p_kernel_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nsgpu_p2p_kernel_name": (C.c_char_p, [C.c_int]),
+    "nsgpu_probe_latency": (C.c_int, [_vp, _vp, _vp]),
     "nsgpu_p2p_profile": (C.c_int, [_vp, _vp, _u32, _vp, _vp]),
     "nsgpu_comm_unique_id": (C.c_int, [_vp]),
     "nsgpu_comm_init": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
@@ -771,3 +772,10 @@ def route_global(dev_node, dev_peer, dev_addr, dev_ifindex, n_nodes, dst_node, s
     check(lib().nsgpu_route_global(n_nodes, arrs[0].size, *[a.ctypes.data for a in arrs], dst.size, dst.ctypes.data,
                                    out.ctypes.data, stream))
     return out
+
+
+def probe_latency(stream=None):
+    """(kernel boundary us, dependent memory trip us) measured on the current device (nsgpu_probe_latency)."""
+    b, t = C.c_double(), C.c_double()
+    check(lib().nsgpu_probe_latency(stream, C.byref(b), C.byref(t)))
+    return b.value, t.value

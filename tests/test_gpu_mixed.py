@@ -144,7 +144,7 @@ def test_run_after_device_stop_with_host_events_fails_loudly():
     sim = nsgpu.Sim()
     sim.attach_p2p(eng)
     ran = []
-    sim.schedule(sc.sim_stop_ns + 10_000_000, lambda: ran.append(1))  # after the device's Stop
+    sim.schedule(sc.stop_ns + 10_000_000, lambda: ran.append(1))  # after the device's Stop
     while len(sim.pop_window()):  # HipSimulatorImpl::Run: windows until an empty one
         pass
     assert ran == []
