@@ -557,11 +557,16 @@ class WifiLoop:
         for i in range(sc["phys"].n_phy):
             sim.schedule(int(sc["first"][i]), (lambda i=i: lambda: attempt(i))())
         sim.stop(sc["stop_ns"])
+        import time
+        t0 = time.perf_counter()
         sim.run()
-        _n, _c, digest = sim.host_stats()
+        secs = time.perf_counter() - t0
+        nh, _c, digest = sim.host_stats()
         ends = lp.read_ends()
+        # an epoch = one nsgpu_wifil_advance: the device runs up to the next host closure (one per closure)
         res = (int(sim.dispatched()), int(digest), {"sends": cnt[0], "busy_attempts": cnt[1],
-                                                   "end_receives": int(len(ends)), "next_uid": int(sim.next_uid())})
+                                                   "end_receives": int(len(ends)), "next_uid": int(sim.next_uid()),
+                                                   "epochs": int(nh), "us_per_epoch": secs * 1e6 / max(int(nh), 1)})
         lp.close()
         return res
 
@@ -573,8 +578,8 @@ class WifiLoop:
 
     def roofline(self, step_kernel_ms, events_per_step):
         return {"kernel": self.kernel + " (whole closed-loop run)", "kernel_ms": step_kernel_ms, "events_per_launch":
-                events_per_step, "launch_unit": "one whole run: k_wl_step / k_wl_rank / k_wl_patch / k_wl_erank / "
-                "k_wl_edigest per host event, k_wl_send per SendPacket"}
+                events_per_step, "launch_unit": "one whole run: k_wl_step / k_wl_mid / k_wl_order per host event "
+                "(an epoch), k_wl_send per SendPacket"}
 
     def result(self):
         return self._last

@@ -75,7 +75,7 @@ struct LSync {  // one sync of the epoch (its EndReceive's uid comes from the sy
   uint64_t sts;
   uint32_t suid, euid;
 };
-struct LCk {  // one chunk of an EndReceive's CalculatePer walk, evaluated by k_wl_per: the noise before it,
+struct LCk {  // one chunk of an EndReceive's CalculatePer walk, evaluated by k_wl_mid: the noise before it,
   double noise;  // and (duration << 1) | (1: the PLCP header mode)
   int64_t dm;
 };
@@ -102,10 +102,10 @@ struct WDev {
   nsgpu_wifil_end *ends;
   uint32_t *end_sslot;
   uint32_t *cnt;  // [0] events, [1] syncs, [2] ends, [3] error bits (sticky: a SendPacket's are seen at the
-                  // next advance), [4] chunk slots claimed (zeroed by k_wl_patch)
+                  // next advance), [4] chunk slots claimed (zeroed by k_wl_order)
   LCk *ck;        // the epoch's deferred chunks (ck_cap; a walk that finds no room computes its PER inline)
   LEck *eck;      // per end record
-  uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_erank; 0 between epochs)
+  uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_order, when logging)
   unsigned long long *edig;  // the epoch's digest terms, summed on the device (k_wl_edigest)
   uint64_t sync_cap, ev_cap, end_cap, ck_cap;
 };
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
         const int64_t hdrStart = t0 + (int64_t)preamble_us(t.mc, pm.bw, t.preamble) * 1000;
         const int64_t payStart = hdrStart + (int64_t)header_us(t.mc, pm.bw, t.preamble) * 1000;
         // The walk's sequential part (the noise sums, the chunk bounds) runs here; the chunks' error-rate
-        // models (~10 pow / erfc calls each, ~100-200 chunks an EndReceive) run lane-parallel in k_wl_per,
+        // models (~10 pow / erfc calls each, ~100-200 chunks an EndReceive) run lane-parallel in k_wl_mid,
         // which multiplies them in this order.  A zero-length chunk is 1.0 (CalculateChunkSuccessRate) and
         // is not recorded.  Without room in the chunk pool the product is formed here.
         const uint32_t need = 2 * P.len + 2;
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
           previous = current;
         }
         eck = LEck{cs, defer ? cn : NONE, eb.w};
-        rec.per = 1 - psr;  // (deferred: k_wl_per overwrites it)
+        rec.per = 1 - psr;  // (deferred: k_wl_mid overwrites it)
         P.rxing = 0;  // NotifyRxEnd (); SwitchFromRxEndOk / Error -> DoSwitchFromRx (wifi-phy-state-helper.cc:391-402)
       }
       const uint32_t sl = eb.euid == NONE ? eb.sslot : NONE;
@@ -622,10 +622,10 @@ __global__ void k_wl_prof_epoch() {  // (one thread: fold the epoch's maxima, re
 // CalculatePer's chunk product for the epoch's deferred EndReceives (interference-helper.cc:257-334): one
 // wave per end record, a lane per chunk (CalculateChunkSuccessRate with the error-rate model), the
 // product taken in walk order (every lane forms the same product from the wave's values).
-__global__ __launch_bounds__(256) void k_wl_per(const WDev D) {
+__device__ __forceinline__ void wl_per(const WDev &D, uint32_t bx, uint32_t nbx) {
   const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t ei = blockIdx.x * 4 + (threadIdx.x >> 6); ei < nend; ei += gridDim.x * 4) {
+  for (uint32_t ei = bx * 4 + (threadIdx.x >> 6); ei < nend; ei += nbx * 4) {
     const LEck k = D.eck[ei];  // (uniform over the wave)
     if (k.n == NONE) continue;
     const LTx t = D.tx[D.ends[ei].tx];
@@ -646,9 +646,9 @@ __global__ __launch_bounds__(256) void k_wl_per(const WDev D) {
 }
 
 // The epoch's syncs in dispatch order (ts, uid of the syncing Receive): EndReceive uid = uid0 + rank.
-__global__ __launch_bounds__(256) void k_wl_rank(const WDev D, uint32_t uid0) {
+__device__ __forceinline__ void wl_sync_rank(const WDev &D, uint32_t uid0, uint32_t bx, uint32_t nbx) {
   const uint32_t n = D.cnt[1] < D.sync_cap ? D.cnt[1] : (uint32_t)D.sync_cap;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  for (uint32_t i = bx * 256 + threadIdx.x; i < n; i += nbx * 256) {
     const LSync a = D.sync[i];
     uint32_t r = 0;
     for (uint32_t k = 0; k < n; k++) {
@@ -658,80 +658,93 @@ __global__ __launch_bounds__(256) void k_wl_rank(const WDev D, uint32_t uid0) {
     D.sync[i].euid = uid0 + r;
   }
 }
-// The epoch's EndReceive uids into its dispatched events, its end records and the still pending records.
-__global__ __launch_bounds__(256) void k_wl_patch(const WDev D) {
-  const uint32_t nev = D.cnt[0] < D.ev_cap ? D.cnt[0] : (uint32_t)D.ev_cap;
-  const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
-  const uint64_t npe = (uint64_t)D.nphy * LPE_CAP;
-  if (blockIdx.x == 0 && threadIdx.x == 0) D.cnt[4] = 0;  // (the chunk pool: k_wl_step is done with it)
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nev + nend + npe; i += (uint64_t)gridDim.x * 256) {
-    if (i < nev) {
-      const uint32_t sl = D.ev[i].sslot;
-      if (sl != NONE) D.ev[i].uid = D.sync[sl].euid;
-    } else if (i < nev + nend) {
-      const uint32_t sl = D.end_sslot[i - nev];
-      if (sl != NONE) D.ends[i - nev].uid = D.sync[sl].euid;
-    } else {
-      LPe &p = D.pe[i - nev - nend];
-      if (p.used && p.euid == NONE) p.euid = D.sync[p.sslot].euid;
-    }
-  }
+// The epoch's first tail kernel: the deferred PER products (blocks 0 .. MID_PER-1) and the syncs' ranks
+// (the rest) — independent, one launch.
+constexpr uint32_t MID_PER = 128, MID_RANK = 64;
+__global__ __launch_bounds__(256) void k_wl_mid(const WDev D, uint32_t uid0) {
+  if (blockIdx.x < MID_PER) wl_per(D, blockIdx.x, MID_PER);
+  else wl_sync_rank(D, uid0, blockIdx.x - MID_PER, MID_RANK);
 }
 
-// The epoch's dispatch order on the device (epochs of at most ERANK_MAX events; larger ones are ordered by
-// the host): each event's rank = the number of the epoch's events with a smaller (ts, uid), by tiles of
-// 256 rows x 64 columns (one 16-B LDS load and a compare per column, unrolled); then the digest terms
-// nsgpu_dispatch_digest_term (K0 + rank, ts, uid), summed per block, one atomic each.
-constexpr uint32_t ERANK_MAX = 65536;
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
-constexpr int ERT = 256, ERC = 64;
-__global__ __launch_bounds__(ERT) void k_wl_erank(const WDev D) {
+// The epoch's second tail kernel (epochs of at most ERANK_MAX events; larger ones are ordered by the host):
+// the EndReceive uids into the end records and the still pending records, then every event's rank in the
+// epoch's (ts, uid) order, its digest term and (logging) its rank.  A block ranks ORW rows; the epoch's
+// keys stream through LDS in chunks of OCAP (one chunk for the usual epoch), each wave counting a quarter
+// of a chunk for the block's rows.  A dispatched EndReceive's uid resolves through its sync as the keys are
+// loaded.  The other status block (the next epoch's) is zeroed here, so an epoch needs no fills.
+constexpr uint32_t OCAP = 8192, ORW = 64;  // keys per LDS chunk (96 KB); rows per block
+constexpr uint32_t ERANK_MAX = 65536;
+__global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int keep, uint32_t *zcnt,
+                                                  unsigned long long *zdig) {
   const uint32_t nev = D.cnt[0] < D.ev_cap ? D.cnt[0] : (uint32_t)D.ev_cap;
-  if (nev == 0 || nev > ERANK_MAX) return;
-  __shared__ ulonglong2 ck[ERC];
-  const uint32_t nr = (nev + ERT - 1) / ERT, nc = (nev + ERC - 1) / ERC;
-  for (uint32_t t = blockIdx.x; t < nr * nc; t += gridDim.x) {  // (uniform over the block)
-    const uint32_t ti = t / nc, tj = t % nc;
-    if (threadIdx.x < (uint32_t)ERC) {
-      const uint32_t j = tj * ERC + threadIdx.x;
-      ck[threadIdx.x] = j < nev ? make_ulonglong2(D.ev[j].ts, D.ev[j].uid) : make_ulonglong2(~0ull, ~0ull);
+  const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
+  const uint64_t npe = (uint64_t)D.nphy * LPE_CAP;
+  if (blockIdx.x == 0 && threadIdx.x < 3) zcnt[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 3) *zdig = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 4) D.cnt[4] = 0;  // (the chunk pool: k_wl_step is done with it)
+  const uint64_t gs = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nend + npe; i += gs) {
+    if (i < nend) {
+      const uint32_t sl = D.end_sslot[i];
+      if (sl != NONE) D.ends[i].uid = D.sync[sl].euid;
+    } else {
+      LPe &p = D.pe[i - nend];
+      if (p.used && p.euid == NONE) p.euid = D.sync[p.sslot].euid;
     }
-    const uint32_t i = ti * ERT + threadIdx.x;
-    uint64_t xts = ~0ull, xuid = ~0ull;
-    if (i < nev) {
-      xts = D.ev[i].ts;
-      xuid = D.ev[i].uid;
+  }
+  if (nev > ERANK_MAX) {  // (the host sorts a huge epoch: its events' uids resolved for it)
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nev; i += gs) {
+      const uint32_t sl = D.ev[i].sslot;
+      if (sl != NONE) D.ev[i].uid = D.sync[sl].euid;
+    }
+    return;
+  }
+  const uint32_t r0 = blockIdx.x * ORW;
+  if (r0 >= nev) return;  // (block-uniform)
+  __shared__ uint64_t s_ts[OCAP];
+  __shared__ uint32_t s_uid[OCAP];
+  __shared__ uint32_t s_part[4][ORW];
+  const uint32_t lane = threadIdx.x & 63, q = threadIdx.x >> 6, i = r0 + lane;
+  uint64_t xts = ~0ull;
+  uint32_t xuid = ~0u;
+  if (i < nev) {  // (the row's own key; its trip overlaps the first chunk's)
+    const LEv e = D.ev[i];
+    xts = e.ts;
+    xuid = e.sslot != NONE ? D.sync[e.sslot].euid : e.uid;
+  }
+  uint32_t c = 0;
+  for (uint32_t b0 = 0; b0 < nev; b0 += OCAP) {
+    const uint32_t bn = nev - b0 < OCAP ? nev - b0 : OCAP;
+    __syncthreads();  // (the last chunk's counting is done)
+    for (uint32_t j = threadIdx.x; j < bn; j += 256) {
+      const LEv e = D.ev[b0 + j];
+      s_ts[j] = e.ts;
+      s_uid[j] = e.sslot != NONE ? D.sync[e.sslot].euid : e.uid;
     }
     __syncthreads();
-    uint32_t c = 0;
-#pragma unroll 16
-    for (int y = 0; y < ERC; y++) {
-      const ulonglong2 k = ck[y];
-      c += (k.x < xts) | ((k.x == xts) & (k.y < xuid));
+    const uint32_t c0 = (uint32_t)((uint64_t)bn * q / 4), c1 = (uint32_t)((uint64_t)bn * (q + 1) / 4);
+#pragma unroll 8
+    for (uint32_t y = c0; y < c1; y++) {  // (every lane reads the same word: an LDS broadcast)
+      const uint64_t t = s_ts[y];
+      c += (t < xts) | ((t == xts) & (s_uid[y] < xuid));
     }
-    if (i < nev && c) atomicAdd(&D.erank[i], c);
-    __syncthreads();
   }
-}
-__global__ __launch_bounds__(256) void k_wl_edigest(const WDev D, uint64_t K0, int keep) {
-  const uint32_t nev = D.cnt[0] < D.ev_cap ? D.cnt[0] : (uint32_t)D.ev_cap;
-  if (nev > ERANK_MAX) return;
-  uint64_t dg = 0;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nev; i += gridDim.x * 256) {
-    const uint32_t r = D.erank[i];
-    dg += digest_term(K0 + r, D.ev[i].ts, D.ev[i].uid);
-    if (!keep) D.erank[i] = 0;  // (kept: the host reads the ranks for its log, then clears them)
-  }
-  dg = wave_sum_u64(dg);
-  __shared__ uint64_t s_dg[4];
-  if ((threadIdx.x & 63) == 0) s_dg[threadIdx.x >> 6] = dg;
+  s_part[q][lane] = c;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t b = s_dg[0] + s_dg[1] + s_dg[2] + s_dg[3];
-    if (b) atomicAdd(D.edig, (unsigned long long)b);
+  uint64_t dg = 0;
+  if (q == 0 && i < nev) {
+    const uint32_t r = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane];
+    dg = digest_term(K0 + r, xts, xuid);
+    D.ev[i].uid = xuid;
+    if (keep) D.erank[i] = r;
+  }
+  if (q == 0) {
+    dg = wave_sum_u64(dg);
+    if (lane == 0 && dg) atomicAdd(D.edig, (unsigned long long)dg);
   }
 }
 
@@ -829,6 +842,8 @@ struct nsgpu_wifil {
   // pinned: the epoch's status block as one copy — counters, digest sum, first END_STAGE end records (the
   // device's D.cnt / D.edig / D.ends are laid out the same way in one allocation)
   uint8_t *h_stat = nullptr;
+  uint8_t *stat[2] = {nullptr, nullptr};  // the device's status blocks, by epoch parity (the next one is zeroed
+  uint32_t par = 0;                       //   by the running epoch's k_wl_order: no fills between epochs)
   uint32_t *h_cnt = nullptr;
   unsigned long long *h_dig = nullptr;
   nsgpu_wifil_end *h_ends = nullptr;
@@ -838,6 +853,14 @@ struct nsgpu_wifil {
   std::vector<LEv> ev;
   std::vector<nsgpu_wifil_end> ends, ends_epoch;
 };
+
+// The epoch's status block (counters, digest, end records) is stat[b].
+static void wl_use_stat(nsgpu_wifil *h, uint32_t b) {
+  h->par = b;
+  h->D.cnt = reinterpret_cast<uint32_t *>(h->stat[b]);
+  h->D.edig = reinterpret_cast<unsigned long long *>(h->stat[b] + 24);
+  h->D.ends = reinterpret_cast<nsgpu_wifil_end *>(h->stat[b] + STAT_HDR);
+}
 
 template <class T>
 static int wl_alloc(nsgpu_wifil *h, T **p, size_t n, const T *src = nullptr) {
@@ -923,11 +946,9 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   WL_TRY(wl_alloc(h, &D.tx, c->tx_cap));
   WL_TRY(wl_alloc(h, &D.sync, sync_cap));
   WL_TRY(wl_alloc(h, &D.ev, ev_cap));
-  uint8_t *stat = nullptr;  // [cnt x 5 | pad | edig | ends x sync_cap]
-  WL_TRY(wl_alloc(h, &stat, STAT_HDR + sync_cap * sizeof(nsgpu_wifil_end)));
-  D.cnt = reinterpret_cast<uint32_t *>(stat);
-  D.edig = reinterpret_cast<unsigned long long *>(stat + 24);
-  D.ends = reinterpret_cast<nsgpu_wifil_end *>(stat + STAT_HDR);
+  for (int b = 0; b < 2; b++)  // [cnt x 5 | pad | edig | ends x sync_cap], two of them (epoch parity)
+    WL_TRY(wl_alloc(h, &h->stat[b], STAT_HDR + sync_cap * sizeof(nsgpu_wifil_end)));
+  wl_use_stat(h, 0);
   WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
   WL_TRY(wl_alloc(h, &D.eck, sync_cap));
   D.ck_cap = 1u << 21;  // 32 MB of deferred chunks an epoch (~100-200 an EndReceive)
@@ -991,23 +1012,22 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
                                    uint64_t *dispatched, uint64_t *digest, uint64_t *log_ts, uint32_t *log_uid,
                                    uint32_t *log_ctx, uint64_t log_cap) {
   if (!h || !uid || !dispatched || !digest) return set_error(NSGPU_EINVAL, "nsgpu_wifil_advance: null");
-  WDev &D = h->D;
-  NSGPU_HIP(hipMemsetAsync(D.cnt, 0, 3 * sizeof(uint32_t), h->s));  // (cnt[3]: sticky error bits)
-  NSGPU_HIP(hipMemsetAsync(D.edig, 0, sizeof(unsigned long long), h->s));
+  const WDev D = h->D;  // (this epoch's status block: stat[par]; its counters were zeroed by the last epoch)
+  uint8_t *const nxt = h->stat[h->par ^ 1];
+  // epoch: the phys' lanes, then the tail (PER products + sync ranks; patch + order + digest)
   hipLaunchKernelGGL(k_wl_step, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
 #ifdef NSGPU_PHASE_PROF
   hipLaunchKernelGGL(k_wl_prof_epoch, dim3(1), dim3(1), 0, h->s);
 #endif
-  hipLaunchKernelGGL(k_wl_per, dim3(128), dim3(256), 0, h->s, D);
-  hipLaunchKernelGGL(k_wl_rank, dim3(64), dim3(256), 0, h->s, D, *uid);
-  hipLaunchKernelGGL(k_wl_patch, dim3(256), dim3(256), 0, h->s, D);
+  hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, h->s, D, *uid);
   const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
-  hipLaunchKernelGGL(k_wl_erank, dim3(1024), dim3(ERT), 0, h->s, D);
-  hipLaunchKernelGGL(k_wl_edigest, dim3(256), dim3(256), 0, h->s, D, *dispatched, logging ? 1 : 0);
+  hipLaunchKernelGGL(k_wl_order, dim3(ERANK_MAX / ORW), dim3(256), 0, h->s, D, *dispatched, logging ? 1 : 0,
+                     reinterpret_cast<uint32_t *>(nxt), reinterpret_cast<unsigned long long *>(nxt + 24));
   NSGPU_HIP(hipGetLastError());
   // counters, the digest sum and the first end records in one trip
   NSGPU_HIP(hipMemcpyAsync(h->h_stat, D.cnt, STAT_HDR + END_STAGE * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipStreamSynchronize(h->s));
+  wl_use_stat(h, h->par ^ 1);  // (the next epoch's block; SendPackets until then report their errors there)
   int rc = wl_check(h, "nsgpu_wifil_advance");
   if (rc) return rc;
   const uint32_t nev = h->h_cnt[0], nsync = h->h_cnt[1], nend = h->h_cnt[2];
@@ -1037,7 +1057,6 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
       h->erank.resize(nev);
       NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.ev, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
       NSGPU_HIP(hipMemcpyAsync(h->erank.data(), D.erank, nev * sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
-      NSGPU_HIP(hipMemsetAsync(D.erank, 0, nev * sizeof(uint32_t), h->s));
       NSGPU_HIP(hipStreamSynchronize(h->s));
       for (uint32_t i = 0; i < nev; i++) {
         const uint64_t rank = *dispatched + h->erank[i];

@@ -16,9 +16,9 @@ PHY_FIELDS = ("rx", "sync", "drop_rx", "drop_tx", "drop_ed", "cca_switches", "en
               "end_tx", "end_rx", "end_cca_busy", "rxing")
 
 
-def check(sc):
-    olog, oends, ophys, otot = run_oracle(sc)
-    glog, gends, gphys, gtot, _keep = run_gpu(sc)
+def check(sc, log_cap=1 << 20):
+    olog, oends, ophys, otot = run_oracle(sc, log_cap)
+    glog, gends, gphys, gtot, _keep = run_gpu(sc, log_cap)
     for f in ("dispatched", "digest", "next_uid", "final_ts", "sends", "busy"):
         assert gtot[f] == otot[f], (f, gtot[f], otot[f])
     for a, b in zip(glog, olog):
@@ -60,3 +60,20 @@ def test_yans_error_model_and_short_preamble():
     check(scenario(seed=7, mode=(wifi.DSSS, 2000000, 22000000), preamble=wifi.PREAMBLE_SHORT,
                    error_model=wifi.YANS, stop_ns=120_000_000))
     check(scenario(seed=8, mode=(wifi.OFDM, 36000000, 20000000), error_model=wifi.YANS, stop_ns=120_000_000))
+
+
+def test_grid_100x100_short_stop_full_pop_log():
+    """The bench's closed-loop workload (10,000 phys 100 m apart, 1000-B DSSS 1 Mb/s frames, period 1 s from
+    seeded phases) cut at Stop 0.02 s (317 SendPackets, 3.17 M dispatches): every SendPacket fans out to
+    9,999 receivers, so epochs hold more events than one LDS chunk of k_wl_order (OCAP) and k_wl_order
+    streams several; the full pop log, digest, counters and end records equal the oracle's."""
+    import numpy as np
+    x, y, z = wifi.grid(100, 100.0)
+    phys = wifi.LoopPhys(x, y, z, tx_cap=1 << 20, rxq_cap=1024, ni_cap=1024)
+    rng = np.random.default_rng(11)
+    n, period = phys.n_phy, 1_000_000_000
+    sc = dict(phys=phys, first=rng.integers(0, period // 2, n).astype(np.uint64),
+              backoff=(100_000 + 37_000 * np.arange(n)).astype(np.uint64), period=period, stop_ns=20_000_000,
+              size=1000, mode=wifi.DSSS_1M, preamble=wifi.PREAMBLE_LONG, dbm=16.0206 + 1.0)
+    tot, ends = check(sc, log_cap=1 << 22)
+    assert tot["sends"] > 200 and tot["dispatched"] > 2_000_000 and len(ends) > 1000
