@@ -2927,7 +2927,7 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
         df = false;
       }
       if (rc == NSGPU_OK) rc = host_step(h, h->snap[0], h->s);
-    } else if (!df && dfu) {
+    } else if (!df && dfu && h->snap[0].mode == MODE_NORMAL) {  // (sorted-run chunks stay on the other pipeline)
       df = true;
     }
   }

@@ -18,13 +18,15 @@ namespace {
 constexpr int PN = 1 << 16;  // chain table entries (256 KB)
 constexpr int LV = 32;       // chase levels per launch
 
-__global__ __launch_bounds__(64) void k_probe_chase(uint32_t *buf, int levels, uint32_t salt) {
+__global__ __launch_bounds__(64) void k_probe_chase(uint32_t *buf, int levels, uint32_t salt, int rewrite) {
   const uint32_t tid = blockIdx.x * 64 + threadIdx.x;
   uint32_t x = (tid * 40503u + salt) % PN;
   for (int l = 0; l < levels; l++) x = buf[x];
-  // rewrite lines for the next launch (a different block's, so other XCDs hold them dirty)
-  const uint32_t w = ((tid + 997u * salt) * 7919u) % PN;
-  buf[w] = (w * 40503u + 12345u) % PN;
+  // rewrite the whole table for the next launch (the same chain values, other blocks' entries: most lines
+  // a level reads were last written on another XCD, so each level misses this XCD's L2)
+  const uint32_t nt = gridDim.x * 64;
+  if (rewrite)
+    for (uint32_t w = (tid + 997u * salt) % nt; w < (uint32_t)PN; w += nt) buf[w] = (w * 40503u + 12345u) % PN;
   if (x == 0xffffffffu) buf[0] = 1;  // (keeps the chain live)
 }
 }  // namespace
@@ -40,9 +42,9 @@ extern "C" int nsgpu_probe_latency(void *stream, double *boundary_us, double *tr
   std::vector<uint32_t> h(PN);
   for (int i = 0; i < PN; i++) h[i] = (uint32_t)((i * 40503ull + 12345) % PN);
   hipEvent_t a = nullptr, b = nullptr;
-  hipGraph_t g[2] = {nullptr, nullptr};
-  hipGraphExec_t ge[2] = {nullptr, nullptr};
-  float ms[2] = {0, 0};
+  hipGraph_t g[3] = {nullptr, nullptr, nullptr};
+  hipGraphExec_t ge[3] = {nullptr, nullptr, nullptr};
+  float ms[3] = {0, 0, 0};
   constexpr int NK = 64, REPS = 20;
   int rc = NSGPU_OK;
   auto fail = [&](const char *what, hipError_t e) {
@@ -52,14 +54,16 @@ extern "C" int nsgpu_probe_latency(void *stream, double *boundary_us, double *tr
   if (e != hipSuccess) fail("copy", e);
   if (!rc && (e = hipEventCreate(&a)) != hipSuccess) fail("event", e);
   if (!rc && (e = hipEventCreate(&b)) != hipSuccess) fail("event", e);
-  for (int v = 0; v < 2 && !rc; v++) {  // v = 0: empty kernels (levels 0), v = 1: LV levels each
+  // v = 0: empty kernels; v = 1: the table rewritten, no chase; v = 2: rewritten, LV levels each
+  for (int v = 0; v < 3 && !rc; v++) {
     hipStream_t cs = nullptr;
     if ((e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) {
       fail("stream", e);
       break;
     }
     (void)hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-    for (int k = 0; k < NK; k++) hipLaunchKernelGGL(k_probe_chase, dim3(64), dim3(64), 0, cs, buf, v ? LV : 0, (uint32_t)k);
+    for (int k = 0; k < NK; k++)
+      hipLaunchKernelGGL(k_probe_chase, dim3(64), dim3(64), 0, cs, buf, v == 2 ? LV : 0, (uint32_t)k, v ? 1 : 0);
     e = hipStreamEndCapture(cs, &g[v]);
     (void)hipStreamDestroy(cs);
     if (e != hipSuccess || (e = hipGraphInstantiate(&ge[v], g[v], nullptr, nullptr, 0)) != hipSuccess) {
@@ -76,7 +80,7 @@ extern "C" int nsgpu_probe_latency(void *stream, double *boundary_us, double *tr
     }
     (void)hipEventElapsedTime(&ms[v], a, b);
   }
-  for (int v = 0; v < 2; v++) {
+  for (int v = 0; v < 3; v++) {
     if (ge[v]) (void)hipGraphExecDestroy(ge[v]);
     if (g[v]) (void)hipGraphDestroy(g[v]);
   }
@@ -84,8 +88,8 @@ extern "C" int nsgpu_probe_latency(void *stream, double *boundary_us, double *tr
   if (b) (void)hipEventDestroy(b);
   (void)hipFree(buf);
   if (rc) return rc;
-  const double per0 = 1e3 * ms[0] / (NK * REPS), per1 = 1e3 * ms[1] / (NK * REPS);
+  const double per0 = 1e3 * ms[0] / (NK * REPS), per1 = 1e3 * ms[1] / (NK * REPS), per2 = 1e3 * ms[2] / (NK * REPS);
   *boundary_us = per0;
-  *trip_us = std::max(0.0, (per1 - per0) / LV);
+  *trip_us = std::max(0.0, (per2 - per1) / LV);
   return NSGPU_OK;
 }

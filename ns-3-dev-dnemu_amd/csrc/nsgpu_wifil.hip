@@ -677,6 +677,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 // of a chunk for the block's rows.  A dispatched EndReceive's uid resolves through its sync as the keys are
 // loaded.  The other status block (the next epoch's) is zeroed here, so an epoch needs no fills.
 constexpr uint32_t OCAP = 8192, ORW = 64;  // keys per LDS chunk (96 KB); rows per block
+constexpr int OLB = 8;                     // chunk entries a thread loads per memory trip
 constexpr uint32_t ERANK_MAX = 65536;
 __global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int keep, uint32_t *zcnt,
                                                   unsigned long long *zdig) {
@@ -720,10 +721,24 @@ __global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int
   for (uint32_t b0 = 0; b0 < nev; b0 += OCAP) {
     const uint32_t bn = nev - b0 < OCAP ? nev - b0 : OCAP;
     __syncthreads();  // (the last chunk's counting is done)
-    for (uint32_t j = threadIdx.x; j < bn; j += 256) {
-      const LEv e = D.ev[b0 + j];
-      s_ts[j] = e.ts;
-      s_uid[j] = e.sslot != NONE ? D.sync[e.sslot].euid : e.uid;
+    for (uint32_t j0 = 0; j0 < bn; j0 += 256 * OLB) {  // OLB entries a thread per trip: loads, then syncs
+      LEv e[OLB];
+      uint32_t u[OLB];
+#pragma unroll
+      for (int k = 0; k < OLB; k++) {
+        const uint32_t j = j0 + k * 256 + threadIdx.x;
+        e[k] = j < bn ? D.ev[b0 + j] : LEv{0, 0, 0, NONE, 0};
+      }
+#pragma unroll
+      for (int k = 0; k < OLB; k++) u[k] = e[k].sslot != NONE ? D.sync[e[k].sslot].euid : e[k].uid;
+#pragma unroll
+      for (int k = 0; k < OLB; k++) {
+        const uint32_t j = j0 + k * 256 + threadIdx.x;
+        if (j < bn) {
+          s_ts[j] = e[k].ts;
+          s_uid[j] = u[k];
+        }
+      }
     }
     __syncthreads();
     const uint32_t c0 = (uint32_t)((uint64_t)bn * q / 4), c1 = (uint32_t)((uint64_t)bn * (q + 1) / 4);

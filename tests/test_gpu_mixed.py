@@ -166,10 +166,10 @@ def test_run_one_with_engine_attached_is_refused():
 
 
 def test_send_after_engine_finished_is_refused():
-    """once the attached engine has run out of device events it is not advanced again, so a
-    later UdpSocket::Send through it is refused with a clear error instead of queueing a datagram that
-    would never be dispatched."""
-    sc = p2p.grid(2, 2, stop_ns=20_000_000, flows=[(0, 3)])
+    """once the attached engine has run out of device events (a Run with nothing pending on the
+    host either ends there) it is not advanced again, so a UdpSocket::Send through it from a later Run's
+    closure is refused with a clear error instead of queueing a datagram that would never be dispatched."""
+    sc = p2p.grid(2, 2, stop_ns=120_000_000, flows=[(0, 3)])  # (OnOff 0.1-0.12 s)
     sc.setup = [x for x in sc.setup if x[0] != p2p.SETUP_STOP]  # no Simulator::Stop: the device drains
     sc.stop_ns = -1
     eng = p2p.Engine(sc, log_cap=0)
@@ -177,6 +177,7 @@ def test_send_after_engine_finished_is_refused():
     sim = nsgpu.Sim()
     sim.attach_p2p(eng)
     app_send = [i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_ONOFF][0]
+    sim.run()  # the device drains; no host event: the Run ends and the engine is finished
     errs = []
 
     def late():
@@ -185,7 +186,7 @@ def test_send_after_engine_finished_is_refused():
         except nsgpu.NsgpuError as e:
             errs.append(str(e))
 
-    sim.schedule(5_000_000_000, late)  # long after the flow's last device event
+    sim.schedule(1_000_000_000, late)
     sim.run()
     assert errs and "finished" in errs[0]
 
@@ -262,4 +263,6 @@ def test_adopt_keeps_the_programs_own_setup_event():
     sim, eng, host, own = adopt_run(sc, own_event_ts=150_000_000)
     assert host == [own[2]]
     st = eng.results(log_n=0)[0]
-    assert sim.dispatched() == int(st.dispatched) + 1
+    assert sim.dispatched() == int(st.dispatched)  # (the engine counts the run's dispatches, host ones included)
+    ts = sim.log[0][:sim.dispatched()].astype(np.int64)
+    assert (np.diff(ts) >= 0).all() and own[0] in set(ts.tolist())
