@@ -1860,9 +1860,10 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 // pipeline), and its block 0 does the window's bookkeeping (df_book); the dispatch accounting (log, digest,
 // uid resolution) is deferred to k2_sdef once the next k2_pa has staged the records in rank order.
 template <int NT>
-__device__ void df_sdef(const P2PDev &M, Ctl &C);
+__device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb);
 constexpr int RKT_DF = 1024;              // the deferred pipeline's k2_rank blocks: SUBS tiles at once
-constexpr int RK_GRID_DF = RK_GRID / (RKT_DF / RKT) + 2;
+constexpr int NSDEF = 8;                  // blocks of the deferred accounting (df_sdef)
+constexpr int RK_GRID_DF = 256;             // one 1024-thread block per CU (~132 KB of LDS each): bookkeeping, accounting, tiles
 template <bool DF>
 __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   constexpr int NT = DF ? RKT_DF : RKT, SUBS = NT / RKT;
@@ -1872,9 +1873,10 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   const uint64_t c_win = C.windows;
   uint32_t n_tie = 0;
 #endif
-  // DF: block 1 does the last window's dispatch accounting (k2_pa staged it) beside this window's ranking
-  if (DF && blockIdx.x == 1) {
-    if (M.sdef_fold) df_sdef<NT>(M, C);
+  // DF: blocks 1 .. NSDEF do the last window's dispatch accounting (k2_pa staged it) beside this window's
+  // ranking
+  if (DF && blockIdx.x >= 1 && blockIdx.x <= (uint32_t)NSDEF) {
+    if (M.sdef_fold) df_sdef<NT>(M, C, blockIdx.x - 1, NSDEF);
     return;
   }
   uint32_t c_done = 0, c_mode = 0, W, c_fr = 0, go = 3;
@@ -1903,14 +1905,14 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   local_prefix<NT>((ranked && lim) ? lc : 0u, pre);
   const uint32_t Lt = pre[NLR], N = W + Lt;
   uint32_t *const wr = wrank_of(M, wn), *const lr = lrank_of(M, wn);
-  uint32_t b0 = blockIdx.x, nb = gridDim.x;  // (DF: block 0 keeps the books, block 1 accounts, the others rank)
+  uint32_t b0 = blockIdx.x, nb = gridDim.x;  // (DF: block 0 keeps the books, 1 .. NSDEF account, the others rank)
   if (DF) {
     if (blockIdx.x == 0) {
       df_book<NT>(M, C, ranked, W, Lt, wn);
       return;
     }
     if (!ranked) return;
-    b0 -= 2, nb -= 2;
+    b0 -= 1 + NSDEF, nb -= 1 + NSDEF;
     for (uint32_t i = b0 * NT + threadIdx.x; i < W; i += nb * NT) {  // (the next k2_pa rewrites wkey / wctx)
       M.pwkey[i] = M.wkey[i];
       M.pwctx[i] = M.wctx[i];
@@ -2128,23 +2130,26 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 // record's through its parent's rank and this window's prefixes); the log and digest get every record and
 // leaf; the child prefixes are kept (cpt) for the provisional uids of window n's children.  Afterwards the
 // window's rank accumulators are cleared (their parity is window n + 2's).
-// NT threads of one block (k2_rank<true>'s block 1, or the k2_sdef kernel); the prefixes by rank live in
-// global scratch (cpt, sip, sgs: L2-resident, read back by this block after its barrier).
+// nsb blocks of NT threads (k2_rank<true>'s blocks 1 .. NSDEF, or the k2_sdef kernel): every block scans
+// the whole window into LDS (child / inline prefixes, group of each rank, group starts) — the scan is one
+// load trip and a few LDS passes — and then resolves, logs and digests its share of the ranks, one a thread.
+// The last block to finish clears the window's rank accumulators and the flag.
 template <int NT>
-__device__ void df_sdef(const P2PDev &M, Ctl &C) {
-  const uint32_t sf = C.sflag;
+__device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb) {
+  const uint32_t sf = C.sflag;  // (cleared by the last block, after every block has read it)
   if (!(sf & 1u)) return;
   const uint32_t wi = (sf >> 1) & 3u, pn = wi & 1u;  // window n & 3, its parity
   const WInfo w = C.winfo[wi];
   const uint32_t uidq = C.winfo[(wi + 3) & 3].uid0;  // window n - 1's uid base
   const uint32_t N = w.N;
   constexpr int RPT = NMAX / NT;
+  __shared__ uint32_t s_cp[NMAX];   // child prefix by rank
+  __shared__ uint32_t s_ip[NMAX];   // inline prefix by rank
+  __shared__ uint32_t s_grp[NMAX];  // same-ts group of each rank
+  __shared__ uint32_t s_gs[NMAX];   // start rank of each group
   __shared__ uint64_t wsum[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const Stg *st = M.stage + (uint64_t)pn * NMAX;
-  uint32_t *const s_cp = M.cpt + (uint64_t)pn * NMAX;  // child prefix by rank (kept for window n's children)
-  uint32_t *const s_ip = M.sip, *const s_gs = M.sgs;   // inline prefix by rank, start rank of each ts group
-  // the scan's fields in registers (rel ts, counts); the rest is read again for the outputs (L2 hits)
   uint32_t erel[RPT], ecnt[RPT];
   uint32_t prev_rel = 0;
   if (tid * RPT > 0 && (uint32_t)(tid * RPT) <= N) prev_rel = (uint32_t)(st[tid * RPT - 1].key >> 32);
@@ -2164,9 +2169,8 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C) {
     for (int q = 0; q < RPT; q++) {
       const uint32_t r = tid * RPT + q;
       if (r < N) {
-        const uint32_t rel = erel[q];
-        const uint32_t hd = r == 0 || rel != pr;
-        pr = rel;
+        const uint32_t hd = r == 0 || erel[q] != pr;
+        pr = erel[q];
         sum += (uint64_t)(ecnt[q] & 0xffffu) | ((uint64_t)(ecnt[q] >> 16) << 21) | ((uint64_t)hd << 42);
       }
     }
@@ -2186,44 +2190,37 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C) {
   }
   const uint64_t ex = off + inc - sum;
   const uint32_t tinl = (uint32_t)((tot >> 21) & 0x1fffffu), ng = (uint32_t)(tot >> 42);
-  const uint32_t bc0 = (uint32_t)(ex & 0x1fffffu), bi0 = (uint32_t)((ex >> 21) & 0x1fffffu), bh0 = (uint32_t)(ex >> 42);
   {
-    uint32_t pr = prev_rel, bc = bc0, bi = bi0, bh = bh0;
+    uint32_t pr = prev_rel, bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu),
+             bh = (uint32_t)(ex >> 42);
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
       const uint32_t r = tid * RPT + q;
       if (r < N) {
-        const uint32_t rel = erel[q];
-        const uint32_t hd = r == 0 || rel != pr;
-        pr = rel;
+        const uint32_t hd = r == 0 || erel[q] != pr;
+        pr = erel[q];
         bh += hd;
         s_cp[r] = bc;
         s_ip[r] = bi;
+        s_grp[r] = bh - 1;
         if (hd) s_gs[bh - 1] = r;
+        if (b == 0) M.cpt[(uint64_t)pn * NMAX + r] = bc;  // (kept: window n's children resolve through it)
         bc += ecnt[q] & 0xffffu;
         bi += ecnt[q] >> 16;
       }
     }
   }
-  __syncthreads();  // (workgroup scope: the block's global writes above are visible to its waves)
-  // own uids, log and digest (records at K0 + rank + the leaves of earlier groups; leaves after their group)
+  __syncthreads();
+  // this block's ranks: own uids, log and digest (records at K0 + rank + the leaves of earlier groups;
+  // leaves after their group)
   const uint32_t *const wr = M.wrank + (uint64_t)pn * WTOT, *const lr = M.lrank + (uint64_t)pn * LMAX;
   const uint32_t *const cq = M.cpt + (uint64_t)(pn ^ 1u) * NMAX;
   const uint32_t *const dmap = M.dmap + (uint64_t)pn * LCAP;
+  const uint32_t r0 = (uint32_t)((uint64_t)N * b / nsb), r1 = (uint32_t)((uint64_t)N * (b + 1) / nsb);
   uint64_t digest = 0;
-  uint32_t pr = prev_rel, bc = bc0, bi = bi0, bh = bh0;
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    if (r >= N) continue;
-    const Stg e = st[r];  // (rel ts and counts again from the record: the register copies are dead here)
-    const uint32_t rel = (uint32_t)(e.key >> 32), ecn = e.cnt;
-    const uint32_t hd = r == 0 || rel != pr;
-    pr = rel;
-    bh += hd;
-    const uint32_t cpr = bc, ipr = bi;
-    bc += ecn & 0xffffu;
-    bi += ecn >> 16;
+  for (uint32_t r = r0 + tid; r < r1; r += NT) {
+    const Stg e = st[r];
+    const uint32_t rel = (uint32_t)(e.key >> 32);
     const uint64_t t = w.tmin + rel;
     uint32_t uid = (uint32_t)e.key;
     if (e.loc) {  // a local record: its parent's child prefix + its child index
@@ -2238,7 +2235,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C) {
       if (((uid >> 30) & 1u) != (pn ^ 1u)) atomicOr(M.error, 256u);
       uid = uidq + cq[((uid & 0x3fffffffu) >> 8) % NMAX] + (uid & 0xffu);
     }
-    const uint32_t g = bh - 1;
+    const uint32_t g = s_grp[r];
     const uint32_t first = s_gs[g];
     const uint32_t last = (g + 1 < ng ? s_gs[g + 1] : N) - 1;
     const uint64_t rk = w.K0 + r + (tinl ? s_ip[first] : 0u);
@@ -2248,7 +2245,8 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C) {
       M.log_uid[rk] = uid;
       M.log_ctx[rk] = e.ctx;
     }
-    const uint32_t ni = min(ecn >> 16, M.maxc);  // (bounded: a staged record's leaves fit its row)
+    const uint32_t ni = min(e.cnt >> 16, M.maxc);  // (bounded: a staged record's leaves fit its row)
+    const uint32_t cpr = s_cp[r], ipr = s_ip[r];
     const uint2 *lf = M.sleaf + ((uint64_t)pn * NMAX + r) * M.maxc;
     for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
       const uint2 l = lf[k];
@@ -2264,13 +2262,28 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C) {
     if (r == N - 1) C.last_ts = t;
   }
   digest = wave_sum64(digest);
-  __syncthreads();  // (every lookup of the rank accumulators is done: clear them for window n + 2)
   if (lane == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
+  // the last block: every block's lookups of the rank accumulators are done — clear them (their parity is
+  // window n + 2's) and the flag
+  __shared__ uint32_t s_last;
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    s_last = atomicAdd(&C.sdone, 1u) == nsb - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
   for (uint32_t i = tid; i < w.W; i += NT) M.wrank[(uint64_t)pn * WTOT + i] = 0;
   for (uint32_t i = tid; i < w.Lt; i += NT) M.lrank[(uint64_t)pn * LMAX + i] = 0;
-  if (tid == 0) C.sflag = 0;
+  if (tid == 0) {
+    C.sdone = 0;
+    C.sflag = 0;
+  }
 }
-__global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) { df_sdef<SCAN_THREADS>(M, *M.C); }
+__global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
+  df_sdef<SCAN_THREADS>(M, *M.C, blockIdx.x, gridDim.x);
+}
 
 // ---- k2_scan: rank order; child / inline prefixes, same-ts groups, run bookkeeping ----
 // WIDE: the single engine's wide windows: the local records join the gen-0 ones (ranks from k2_rank), and

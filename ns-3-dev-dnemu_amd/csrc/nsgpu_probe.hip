@@ -38,56 +38,53 @@ extern "C" int nsgpu_probe_latency(void *stream, double *boundary_us, double *tr
   if (!boundary_us || !trip_us) return set_error(NSGPU_EINVAL, "nsgpu_probe_latency: null");
   hipStream_t s = (hipStream_t)stream;
   uint32_t *buf = nullptr;
-  NSGPU_HIP(hipMalloc(&buf, PN * sizeof(uint32_t)));
-  std::vector<uint32_t> h(PN);
-  for (int i = 0; i < PN; i++) h[i] = (uint32_t)((i * 40503ull + 12345) % PN);
+  hipStream_t cs = nullptr;
   hipEvent_t a = nullptr, b = nullptr;
   hipGraph_t g[3] = {nullptr, nullptr, nullptr};
   hipGraphExec_t ge[3] = {nullptr, nullptr, nullptr};
   float ms[3] = {0, 0, 0};
   constexpr int NK = 64, REPS = 20;
-  int rc = NSGPU_OK;
-  auto fail = [&](const char *what, hipError_t e) {
-    rc = set_error(NSGPU_EHIP, "nsgpu_probe_latency: %s: %s", what, hipGetErrorString(e));
-  };
-  hipError_t e = hipMemcpyAsync(buf, h.data(), PN * sizeof(uint32_t), hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) fail("copy", e);
-  if (!rc && (e = hipEventCreate(&a)) != hipSuccess) fail("event", e);
-  if (!rc && (e = hipEventCreate(&b)) != hipSuccess) fail("event", e);
+  std::vector<uint32_t> h(PN);
+  for (int i = 0; i < PN; i++) h[i] = (uint32_t)((i * 40503ull + 12345) % PN);
+  hipError_t e = hipSuccess;
+  const char *what = "";
+#define PROBE(x, w)                  \
+  if (e == hipSuccess) {             \
+    e = (x);                         \
+    if (e != hipSuccess) what = (w); \
+  }
+  PROBE(hipMalloc(&buf, PN * sizeof(uint32_t)), "hipMalloc");
+  PROBE(hipMemcpy(buf, h.data(), PN * sizeof(uint32_t), hipMemcpyHostToDevice), "copy");
+  PROBE(hipEventCreate(&a), "event");
+  PROBE(hipEventCreate(&b), "event");
+  PROBE(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
   // v = 0: empty kernels; v = 1: the table rewritten, no chase; v = 2: rewritten, LV levels each
-  for (int v = 0; v < 3 && !rc; v++) {
-    hipStream_t cs = nullptr;
-    if ((e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) {
-      fail("stream", e);
-      break;
-    }
-    (void)hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+  for (int v = 0; v < 3 && e == hipSuccess; v++) {
+    PROBE(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "capture");
+    if (e != hipSuccess) break;
     for (int k = 0; k < NK; k++)
       hipLaunchKernelGGL(k_probe_chase, dim3(64), dim3(64), 0, cs, buf, v == 2 ? LV : 0, (uint32_t)k, v ? 1 : 0);
-    e = hipStreamEndCapture(cs, &g[v]);
-    (void)hipStreamDestroy(cs);
-    if (e != hipSuccess || (e = hipGraphInstantiate(&ge[v], g[v], nullptr, nullptr, 0)) != hipSuccess) {
-      fail("graph", e);
-      break;
-    }
-    for (int r = 0; r < 3; r++) (void)hipGraphLaunch(ge[v], s);
-    (void)hipEventRecord(a, s);
-    for (int r = 0; r < REPS; r++) (void)hipGraphLaunch(ge[v], s);
-    (void)hipEventRecord(b, s);
-    if ((e = hipEventSynchronize(b)) != hipSuccess) {
-      fail("run", e);
-      break;
-    }
-    (void)hipEventElapsedTime(&ms[v], a, b);
+    hipError_t ec = hipStreamEndCapture(cs, &g[v]);
+    PROBE(ec, "capture end");
+    PROBE(hipGraphInstantiate(&ge[v], g[v], nullptr, nullptr, 0), "instantiate");
+    for (int r = 0; r < 3; r++) PROBE(hipGraphLaunch(ge[v], s), "launch");
+    PROBE(hipEventRecord(a, s), "record");
+    for (int r = 0; r < REPS; r++) PROBE(hipGraphLaunch(ge[v], s), "launch");
+    PROBE(hipEventRecord(b, s), "record");
+    PROBE(hipEventSynchronize(b), "run");
+    PROBE(hipEventElapsedTime(&ms[v], a, b), "elapsed");
   }
+#undef PROBE
   for (int v = 0; v < 3; v++) {
     if (ge[v]) (void)hipGraphExecDestroy(ge[v]);
     if (g[v]) (void)hipGraphDestroy(g[v]);
   }
   if (a) (void)hipEventDestroy(a);
   if (b) (void)hipEventDestroy(b);
-  (void)hipFree(buf);
-  if (rc) return rc;
+  if (cs) (void)hipStreamDestroy(cs);
+  if (buf) (void)hipFree(buf);
+  (void)hipGetLastError();  // (nothing of the probe's is left as the thread's last error)
+  if (e != hipSuccess) return set_error(NSGPU_EHIP, "nsgpu_probe_latency: %s: %s", what, hipGetErrorString(e));
   const double per0 = 1e3 * ms[0] / (NK * REPS), per1 = 1e3 * ms[1] / (NK * REPS), per2 = 1e3 * ms[2] / (NK * REPS);
   *boundary_us = per0;
   *trip_us = std::max(0.0, (per2 - per1) / LV);

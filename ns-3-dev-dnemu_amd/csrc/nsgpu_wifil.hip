@@ -36,7 +36,7 @@ constexpr int LPE_CAP = 8;  // pending EndReceive records of one phy (the live o
 constexpr uint32_t END_STAGE = 128;  // EndReceive records an epoch returns with its counters (more: a second copy)
 constexpr size_t STAT_HDR = 32;      // the status block's counters (5 x u32) and digest (at 24) before the ends
 static_assert(sizeof(nsgpu_wifil_end) % 8 == 0 && STAT_HDR % 8 == 0, "status block alignment");
-constexpr uint32_t WE_TX_IN_TX = 1, WE_NICAP = 2, WE_RQCAP = 4, WE_PECAP = 8, WE_CAP = 16;
+constexpr uint32_t WE_TX_IN_TX = 1, WE_NICAP = 2, WE_RQCAP = 4, WE_PECAP = 8, WE_CAP = 16, WE_CKCAP = 32;
 constexpr int NB = 8;  // ring entries loaded per batch
 
 struct LNi {  // InterferenceHelper::NiChange (interference-helper.cc:91-110)
@@ -105,10 +105,16 @@ struct WDev {
                   // next advance), [4] chunk slots claimed (zeroed by k_wl_order)
   LCk *ck;        // the epoch's deferred chunks (ck_cap; a walk that finds no room computes its PER inline)
   LEck *eck;      // per end record
+  uint32_t *evc;             // the epoch's event-list stripes: EV_STRIPES counters, EV_STRIDE words apart
+  LEv *evd;                  // the epoch's events in k_wl_order's dense order, uids resolved (the host's copy)
   uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_order, when logging)
   unsigned long long *edig;  // the epoch's digest terms, summed on the device (k_wl_edigest)
   uint64_t sync_cap, ev_cap, end_cap, ck_cap;
+  uint64_t ev_scap;  // events per stripe (stripe s holds ev[s * ev_scap, s * ev_scap + evc[s * EV_STRIDE]))
 };
+// The epoch's dispatched events are appended to EV_STRIPES lists (phy j's to stripe j % EV_STRIPES): one
+// counter a phy's event would serialize ~10^4 atomics an epoch on one line.
+constexpr int EV_STRIPES = 64, EV_STRIDE = 32;
 
 // ---- WifiMode attributes (the CreateWifiMode calls of wifi-phy.cc:355-840; phyRate: wifi-mode.cc:140-155) ----
 struct Mode {
@@ -496,8 +502,8 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
       } else {
         err |= WE_CAP;
       }
-      const uint32_t vi = wave_alloc(&D.cnt[0]);
-      if (vi < D.ev_cap) D.ev[vi] = LEv{eb.ts, eb.euid, ctx, sl, 0};
+      const uint32_t vi = wave_alloc(D.evc + (blockIdx.x % EV_STRIPES) * EV_STRIDE);
+      if (vi < D.ev_scap) D.ev[(blockIdx.x % EV_STRIPES) * D.ev_scap + vi] = LEv{eb.ts, eb.euid, ctx, sl, 0};
       else err |= WE_CAP;
       pe[e].used = 0;
       if (P.live == (uint32_t)e) P.live = NONE;
@@ -588,8 +594,8 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
         P.c.cca_switches++;
       }
     }
-    const uint32_t vi = wave_alloc(&D.cnt[0]);
-    if (vi < D.ev_cap) D.ev[vi] = LEv{r.at, r.uid, ctx, NONE, 0};
+    const uint32_t vi = wave_alloc(D.evc + (blockIdx.x % EV_STRIPES) * EV_STRIDE);
+    if (vi < D.ev_scap) D.ev[(blockIdx.x % EV_STRIPES) * D.ev_scap + vi] = LEv{r.at, r.uid, ctx, NONE, 0};
     else err |= WE_CAP;
 #ifdef NSGPU_PHASE_PROF
     pev++;
@@ -610,6 +616,318 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
   }
 #endif
 }
+// ---- the epoch with one wave per phy (the default; NSGPU_WIFIL_LANE=1: the lane-per-phy k_wl_step above) ----
+// k_wl_step's lanes spend their time in the NiChanges ring: a start inserted while receiving shifts every
+// pending end (100-300 entries at 10^4 phys), and the cursor and the CCA energy walk read the ring entry by
+// entry, 8 a memory trip.  Here the 64 lanes of a wave serve ONE phy: the ring is read 64 entries a trip, an
+// insertion shifts 64 entries a trip, and the sums whose order matters (the cursor's prefix, the energy
+// walk, CalculatePer's walk) run over the loaded entries lane by lane with readlane — no memory trip.  The
+// same operations in the same order as k_wl_step (bit-exact).  Every decision is wave-uniform; lane 0
+// makes the stores of uniform values.
+__device__ __forceinline__ uint32_t lead_run(uint64_t bm) { return ~bm ? (uint32_t)__builtin_ctzll(~bm) : 64u; }
+__device__ __forceinline__ int64_t rl_i64(int64_t v, int u) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), u);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double rl_d(double v, int u) { return __longlong_as_double(rl_i64(__double_as_longlong(v), u)); }
+__device__ __forceinline__ uint32_t rl_u32(uint32_t v, int u) { return (uint32_t)__builtin_amdgcn_readlane((int)v, u); }
+
+__device__ __forceinline__ LPe rl_pe(const LPe &a, int u) {
+  LPe b;
+  b.ts = (uint64_t)rl_i64((int64_t)a.ts, u);
+  b.sts = (uint64_t)rl_i64((int64_t)a.sts, u);
+  b.suid = rl_u32(a.suid, u);
+  b.euid = rl_u32(a.euid, u);
+  b.tx = rl_u32(a.tx, u);
+  b.can = rl_u32(a.can, u);
+  b.sslot = rl_u32(a.sslot, u);
+  b.used = rl_u32(a.used, u);
+  b.w = rl_d(a.w, u);
+  return b;
+}
+template <bool LE>
+__device__ __forceinline__ void w_cursor_advance(const LNi *ring, uint32_t head, uint32_t len, uint32_t m, int64_t lim,
+                                                 uint32_t &cur_n, double &cur_s) {
+  const uint32_t lane = threadIdx.x & 63;
+  while (cur_n < len) {
+    const uint32_t idx = cur_n + lane;
+    LNi e{0, 0.0};
+    bool in = false;
+    if (idx < len) {
+      e = ring[(head + idx) & m];
+      in = LE ? e.t <= lim : e.t < lim;
+    }
+    const uint32_t k = lead_run(__ballot(in));  // (sorted: the entries up to lim are the chunk's head)
+    for (uint32_t u = 0; u < k; u++) cur_s += rl_d(e.d, (int)u);
+    cur_n += k;
+    if (k < 64) return;
+  }
+}
+// AddNiChangeEvent (interference-helper.cc:378-383) at upper_bound (t): the entries after it move up one
+// place, 64 a trip from the tail.
+__device__ __forceinline__ void w_ni_insert(LNi *ring, uint32_t head, uint32_t &len, uint32_t m, int64_t t, double d) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t q = len;
+  while (q > 0) {
+    const uint32_t c0 = q > 64 ? q - 64 : 0, n = q - c0;
+    LNi e{0, 0.0};
+    bool gt = false;
+    if (lane < n) {
+      e = ring[(head + c0 + lane) & m];
+      gt = e.t > t;
+    }
+    const uint32_t k = (uint32_t)__popcll(__ballot(gt));  // (sorted: the entries after t are the chunk's tail)
+    if (gt) ring[(head + c0 + lane + 1) & m] = e;
+    q -= k;
+    if (k < n) break;
+  }
+  if (lane == 0) ring[(head + q) & m] = LNi{t, d};
+  len++;
+}
+
+__global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uint32_t buid) {
+  const int64_t j = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  if (j >= D.nphy) return;
+  LPhy P = D.ps[j];
+  LNi *ring = D.ni + (uint64_t)j * (D.ni_mask + 1);
+  LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
+  LPe *pe = D.pe + (uint64_t)j * LPE_CAP;
+  const uint32_t m = D.ni_mask, ctx = D.node[j];
+  uint32_t *const evc = D.evc + (uint32_t)(j % EV_STRIPES) * EV_STRIDE;
+  LEv *const evs = D.ev + (uint64_t)(j % EV_STRIPES) * D.ev_scap;
+  uint32_t err = 0;
+  for (;;) {
+    // the next pending EndReceive (lane q < LPE_CAP loads record q; the selection reads them lane by lane)
+    LPe mine{};
+    if (lane < (uint32_t)LPE_CAP) mine = pe[lane];
+    const uint64_t used = __ballot(lane < (uint32_t)LPE_CAP && mine.used);
+    int e = -1;
+    LPe eb{};
+    for (int q = 0; q < LPE_CAP; q++) {
+      if (!((used >> q) & 1ull)) continue;
+      const LPe c = rl_pe(mine, q);
+      if (e < 0 || pe_before(c, eb)) e = q, eb = c;
+    }
+    const bool hr = P.rq_len > 0;
+    LRx r{};
+    if (hr) r = rq[P.rq_head & D.rq_mask];
+    bool take_r;
+    if (hr && e >= 0) take_r = r.at < eb.ts || (r.at == eb.ts && (eb.euid == NONE || r.uid < eb.euid));
+    else if (hr) take_r = true;
+    else if (e >= 0) take_r = false;
+    else break;
+    if (take_r) {
+      if (!(r.at < bts || (r.at == bts && r.uid < buid))) break;
+    } else {
+      if (!(eb.ts < bts || (eb.ts == bts && eb.euid != NONE && eb.euid < buid))) break;
+    }
+    if (!take_r) {  // ---- YansWifiPhy::EndReceive (yans-wifi-phy.cc:770-799)
+      const int64_t nw = (int64_t)eb.ts;
+      nsgpu_wifil_end rec{eb.ts, eb.euid, (uint32_t)j, 0.0, 0.0, eb.tx, eb.can ? (uint32_t)NSGPU_WIFI_END_CANCELLED : 0u,
+                          eb.can ? 0.0 : eb.w};
+      LEck eck{0, NONE, 0.0};
+      P.c.end++;
+      if (eb.can) {  // EventImpl::Invoke skips a cancelled event (event-impl.cc:40-46); still dispatched
+        P.c.end_cancelled++;
+      } else {
+        // InterferenceHelper::CalculateSnrPer (interference-helper.cc:336-353), as k_wl_step: the walk's
+        // sequential part here (64 ring entries a trip, then lane by lane), the chunks' models in k_wl_mid
+        const LTx t = D.tx[eb.tx];
+        const Mode pm = make_mode(t.mc, t.rate, t.bw);
+        const double noise0 = P.firstPower;
+        rec.snr = snr_of(D, eb.w, noise0, pm);
+        const int64_t t0 = (int64_t)eb.sts;
+        const int64_t hdrStart = t0 + (int64_t)preamble_us(t.mc, pm.bw, t.preamble) * 1000;
+        const int64_t payStart = hdrStart + (int64_t)header_us(t.mc, pm.bw, t.preamble) * 1000;
+        const uint32_t need = 2 * P.len + 2;
+        uint32_t cs = 0;
+        if (lane == 0) cs = atomicAdd(&D.cnt[4], need);
+        cs = rl_u32(cs, 0);
+        const bool defer = (uint64_t)cs + need <= D.ck_cap;
+        if (!defer) err |= WE_CKCAP;  // (the run fails: no inline fallback here)
+        uint32_t cn = 0;
+        double noiseW = noise0;
+        auto ck = [&](int64_t dur, bool hdr) {
+          if (defer && dur != 0) {
+            if (lane == 0) D.ck[cs + cn] = LCk{noiseW, (int64_t)((uint64_t)dur << 1) | (hdr ? 1 : 0)};
+            cn++;
+          }
+        };
+        int64_t previous = t0;
+        uint32_t q = 1;
+        LNi cb{0, 0.0};
+        uint32_t cq0 = 0;
+        bool have = false;
+        for (bool last = false; !last;) {
+          int64_t current;
+          double delta;
+          if (q < P.len) {
+            if (!have || q - cq0 >= 64) {
+              cq0 = q;
+              have = true;
+              cb = q + lane < P.len ? ring[(P.head + q + lane) & m] : LNi{0, 0.0};
+            }
+            const int u = (int)(q - cq0);
+            const int64_t et = rl_i64(cb.t, u);
+            const double ed = rl_d(cb.d, u);
+            if (et == nw && eb.w == -ed) {
+              current = nw, delta = 0.0, last = true;  // (the event's end entry: the closing (end, 0))
+            } else {
+              current = et, delta = ed;
+            }
+            q++;
+          } else {
+            current = nw, delta = 0.0, last = true;
+          }
+          if (previous >= payStart) {
+            ck(current - previous, false);
+          } else if (previous >= hdrStart) {
+            if (current >= payStart) {
+              ck(payStart - previous, true);
+              ck(current - payStart, false);
+            } else {
+              ck(current - previous, true);
+            }
+          } else {
+            if (current >= payStart) {
+              ck(payStart - hdrStart, true);
+              ck(current - payStart, false);
+            } else if (current >= hdrStart) {
+              ck(current - hdrStart, true);
+            }
+          }
+          noiseW += delta;
+          previous = current;
+        }
+        eck = LEck{cs, defer ? cn : NONE, eb.w};
+        rec.per = 0.0;  // (k_wl_mid writes the product)
+        P.rxing = 0;  // NotifyRxEnd (); SwitchFromRxEndOk / Error -> DoSwitchFromRx (wifi-phy-state-helper.cc:391-402)
+      }
+      const uint32_t sl = eb.euid == NONE ? eb.sslot : NONE;
+      uint32_t ei = 0, vi = 0;
+      if (lane == 0) {
+        ei = atomicAdd(&D.cnt[2], 1u);
+        vi = atomicAdd(evc, 1u);
+      }
+      ei = rl_u32(ei, 0);
+      vi = rl_u32(vi, 0);
+      if (ei < D.end_cap) {
+        if (lane == 0) {
+          D.ends[ei] = rec;
+          D.end_sslot[ei] = sl;
+          D.eck[ei] = eck;
+        }
+      } else {
+        err |= WE_CAP;
+      }
+      if (vi < D.ev_scap) {
+        if (lane == 0) evs[vi] = LEv{eb.ts, eb.euid, ctx, sl, 0};
+      } else {
+        err |= WE_CAP;
+      }
+      if (lane == 0) pe[e].used = 0;
+      if (P.live == (uint32_t)e) P.live = NONE;
+      continue;
+    }
+    // ---- YansWifiChannel::Receive -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496)
+    P.rq_head++;
+    P.rq_len--;
+    const int64_t nw = (int64_t)r.at;
+    const int64_t endNew = nw + D.tx[r.tx].dur;
+    if (P.len + 2 > m + 1) {
+      err |= WE_NICAP;
+      break;
+    }
+    // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
+    if (!P.rxing) {  // fold the entries up to upper_bound (now) into m_firstPower; the new entry first
+      w_cursor_advance<true>(ring, P.head, P.len, m, nw, P.cur_n, P.cur_s);
+      P.head = (P.head + P.cur_n) & m;
+      P.len -= P.cur_n;
+      P.cur_n = 0;
+      P.head = (P.head - 1) & m;
+      if (lane == 0) ring[P.head] = LNi{nw, r.w};
+      P.len++;
+      P.firstPower = P.cur_s;
+    } else {
+      w_ni_insert(ring, P.head, P.len, m, nw, r.w);
+    }
+    w_ni_insert(ring, P.head, P.len, m, endNew, -r.w);
+    P.ni_max = P.len > P.ni_max ? P.len : P.ni_max;
+    const int st = P.endTx > nw ? 2 : P.rxing ? 1 : P.endCca > nw ? 3 : 0;  // GetState (:159-183)
+    bool maybe = false;
+    P.c.rx++;
+    if (st == 1 || st == 2) {  // drop; noise after the current Rx / Tx (:431-457)
+      if (st == 1) P.c.drop_rx++;
+      else P.c.drop_tx++;
+      int64_t until = (st == 1 ? P.endRx : P.endTx) - nw;  // GetDelayUntilIdle (:122-151)
+      until = until > 0 ? until : 0;
+      maybe = endNew > nw + until;
+    } else if (r.w > D.edW) {  // sync (:461-472): SwitchToRx, NotifyRxStart, Schedule (rxDuration, EndReceive)
+      int q = -1;
+      for (int k = 0; k < LPE_CAP; k++)
+        if (!pe[k].used) {
+          q = k;
+          break;
+        }
+      uint32_t sl = 0;
+      if (lane == 0) sl = atomicAdd(&D.cnt[1], 1u);
+      sl = rl_u32(sl, 0);
+      if (q < 0 || sl >= D.sync_cap) {
+        err |= q < 0 ? WE_PECAP : WE_CAP;
+        break;
+      }
+      if (lane == 0) {
+        D.sync[sl] = LSync{r.at, r.uid, NONE};
+        pe[q] = LPe{(uint64_t)endNew, r.at, r.uid, NONE, r.tx, 0, sl, 1, r.w};
+      }
+      P.live = (uint32_t)q;
+      P.rxing = 1;
+      P.endRx = endNew;
+      P.c.sync++;
+    } else {
+      P.c.drop_ed++;
+      maybe = true;
+    }
+    if (maybe) {  // maybeCcaBusy (:485-495): GetEnergyDuration (interference-helper.cc:171-190)
+      w_cursor_advance<false>(ring, P.head, P.len, m, nw, P.cur_n, P.cur_s);
+      double noise = P.cur_s;
+      int64_t end = nw;
+      bool stop = false;
+      for (uint32_t q0 = P.cur_n; q0 < P.len && !stop; q0 += 64) {  // (64 entries a trip; the sums one at a time)
+        const LNi en = q0 + lane < P.len ? ring[(P.head + q0 + lane) & m] : LNi{0, 0.0};
+        const uint32_t n = P.len - q0 < 64 ? P.len - q0 : 64;
+        for (uint32_t u = 0; u < n; u++) {
+          noise += rl_d(en.d, (int)u);
+          end = rl_i64(en.t, (int)u);
+          if (noise < D.ccaW) {
+            stop = true;
+            break;
+          }
+        }
+      }
+      const int64_t cca = end > nw ? end - nw : 0;
+      if (cca != 0) {  // SwitchMaybeToCcaBusy (wifi-phy-state-helper.cc:404-423)
+        P.endCca = P.endCca > nw + cca ? P.endCca : nw + cca;
+        P.c.cca_switches++;
+      }
+    }
+    uint32_t vi = 0;
+    if (lane == 0) vi = atomicAdd(evc, 1u);
+    vi = rl_u32(vi, 0);
+    if (vi < D.ev_scap) {
+      if (lane == 0) evs[vi] = LEv{r.at, r.uid, ctx, NONE, 0};
+    } else {
+      err |= WE_CAP;
+    }
+  }
+  if (lane == 0) {
+    D.ps[j] = P;
+    if (err) atomicOr(&D.cnt[3], err);
+  }
+}
+
 #ifdef NSGPU_PHASE_PROF
 __global__ void k_wl_prof_epoch() {  // (one thread: fold the epoch's maxima, reset them)
   g_wl_ph[0] += g_wl_ep[0];
@@ -680,13 +998,36 @@ constexpr uint32_t OCAP = 8192, ORW = 64;  // keys per LDS chunk (96 KB); rows p
 constexpr int OLB = 8;                     // chunk entries a thread loads per memory trip
 constexpr uint32_t ERANK_MAX = 65536;
 __global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int keep, uint32_t *zcnt,
-                                                  unsigned long long *zdig) {
-  const uint32_t nev = D.cnt[0] < D.ev_cap ? D.cnt[0] : (uint32_t)D.ev_cap;
+                                                  unsigned long long *zdig, uint32_t *zevc) {
+  __shared__ uint32_t s_pre[EV_STRIPES + 1];  // the stripes' prefix: dense index -> stripe
+  if (threadIdx.x < (uint32_t)EV_STRIPES) {
+    const uint32_t c = D.evc[threadIdx.x * EV_STRIDE];
+    s_pre[threadIdx.x + 1] = c < D.ev_scap ? c : (uint32_t)D.ev_scap;
+  }
+  if (threadIdx.x == 0) s_pre[0] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 1; k <= EV_STRIPES; k++) s_pre[k] += s_pre[k - 1];  // (64 adds, LDS)
+  __syncthreads();
+  const uint32_t nev = s_pre[EV_STRIPES];
+  auto addr = [&](uint32_t i) -> uint64_t {  // dense index -> the event's slot
+    uint32_t lo = 0, hi = EV_STRIPES;  // s_pre[lo] <= i < s_pre[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_pre[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    return (uint64_t)lo * D.ev_scap + (i - s_pre[lo]);
+  };
   const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
   const uint64_t npe = (uint64_t)D.nphy * LPE_CAP;
-  if (blockIdx.x == 0 && threadIdx.x < 3) zcnt[threadIdx.x] = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 3) *zdig = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 4) D.cnt[4] = 0;  // (the chunk pool: k_wl_step is done with it)
+  if (blockIdx.x == 0) {  // the next epoch's counters (its status block, its stripes); this epoch's total
+    if (threadIdx.x < 3) zcnt[threadIdx.x] = 0;
+    if (threadIdx.x == 3) *zdig = 0;
+    if (threadIdx.x == 4) D.cnt[4] = 0;  // (the chunk pool: k_wl_step is done with it)
+    if (threadIdx.x == 5) D.cnt[0] = nev;
+    if (threadIdx.x < (uint32_t)EV_STRIPES) zevc[threadIdx.x * EV_STRIDE] = 0;
+  }
   const uint64_t gs = (uint64_t)gridDim.x * 256;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nend + npe; i += gs) {
     if (i < nend) {
@@ -697,10 +1038,11 @@ __global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int
       if (p.used && p.euid == NONE) p.euid = D.sync[p.sslot].euid;
     }
   }
-  if (nev > ERANK_MAX) {  // (the host sorts a huge epoch: its events' uids resolved for it)
+  if (nev > ERANK_MAX) {  // (the host sorts a huge epoch: its events dense, uids resolved)
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nev; i += gs) {
-      const uint32_t sl = D.ev[i].sslot;
-      if (sl != NONE) D.ev[i].uid = D.sync[sl].euid;
+      LEv e = D.ev[addr((uint32_t)i)];
+      if (e.sslot != NONE) e.uid = D.sync[e.sslot].euid;
+      D.evd[i] = e;
     }
     return;
   }
@@ -711,10 +1053,11 @@ __global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int
   __shared__ uint32_t s_part[4][ORW];
   const uint32_t lane = threadIdx.x & 63, q = threadIdx.x >> 6, i = r0 + lane;
   uint64_t xts = ~0ull;
-  uint32_t xuid = ~0u;
+  uint32_t xuid = ~0u, xctx = 0;
   if (i < nev) {  // (the row's own key; its trip overlaps the first chunk's)
-    const LEv e = D.ev[i];
+    const LEv e = D.ev[addr(i)];
     xts = e.ts;
+    xctx = e.ctx;
     xuid = e.sslot != NONE ? D.sync[e.sslot].euid : e.uid;
   }
   uint32_t c = 0;
@@ -727,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int
 #pragma unroll
       for (int k = 0; k < OLB; k++) {
         const uint32_t j = j0 + k * 256 + threadIdx.x;
-        e[k] = j < bn ? D.ev[b0 + j] : LEv{0, 0, 0, NONE, 0};
+        e[k] = j < bn ? D.ev[addr(b0 + j)] : LEv{0, 0, 0, NONE, 0};
       }
 #pragma unroll
       for (int k = 0; k < OLB; k++) u[k] = e[k].sslot != NONE ? D.sync[e[k].sslot].euid : e[k].uid;
@@ -754,8 +1097,10 @@ __global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int
   if (q == 0 && i < nev) {
     const uint32_t r = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane];
     dg = digest_term(K0 + r, xts, xuid);
-    D.ev[i].uid = xuid;
-    if (keep) D.erank[i] = r;
+    if (keep) {
+      D.erank[i] = r;
+      D.evd[i] = LEv{xts, xuid, xctx, NONE, 0};
+    }
   }
   if (q == 0) {
     dg = wave_sum_u64(dg);
@@ -859,6 +1204,7 @@ struct nsgpu_wifil {
   uint8_t *h_stat = nullptr;
   uint8_t *stat[2] = {nullptr, nullptr};  // the device's status blocks, by epoch parity (the next one is zeroed
   uint32_t par = 0;                       //   by the running epoch's k_wl_order: no fills between epochs)
+  uint32_t *evc[2] = {nullptr, nullptr};  // the event-list stripe counters, by epoch parity (likewise)
   uint32_t *h_cnt = nullptr;
   unsigned long long *h_dig = nullptr;
   nsgpu_wifil_end *h_ends = nullptr;
@@ -875,6 +1221,7 @@ static void wl_use_stat(nsgpu_wifil *h, uint32_t b) {
   h->D.cnt = reinterpret_cast<uint32_t *>(h->stat[b]);
   h->D.edig = reinterpret_cast<unsigned long long *>(h->stat[b] + 24);
   h->D.ends = reinterpret_cast<nsgpu_wifil_end *>(h->stat[b] + STAT_HDR);
+  h->D.evc = h->evc[b];
 }
 
 template <class T>
@@ -961,12 +1308,19 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   WL_TRY(wl_alloc(h, &D.tx, c->tx_cap));
   WL_TRY(wl_alloc(h, &D.sync, sync_cap));
   WL_TRY(wl_alloc(h, &D.ev, ev_cap));
-  for (int b = 0; b < 2; b++)  // [cnt x 5 | pad | edig | ends x sync_cap], two of them (epoch parity)
+  for (int b = 0; b < 2; b++) {  // [cnt x 5 | pad | edig | ends x sync_cap], two of them (epoch parity)
     WL_TRY(wl_alloc(h, &h->stat[b], STAT_HDR + sync_cap * sizeof(nsgpu_wifil_end)));
+    WL_TRY(wl_alloc(h, &h->evc[b], (size_t)EV_STRIPES * EV_STRIDE));
+  }
+  WL_TRY(wl_alloc(h, &D.evd, ev_cap));
+  D.ev_scap = ev_cap / EV_STRIPES;
   wl_use_stat(h, 0);
   WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
   WL_TRY(wl_alloc(h, &D.eck, sync_cap));
-  D.ck_cap = 1u << 21;  // 32 MB of deferred chunks an epoch (~100-200 an EndReceive)
+  // deferred chunks an epoch (~100-600 an EndReceive): 64 MB, or 512 a phy (k_wl_stepw has no inline
+  // fallback — its error-rate models would take ~130 more VGPRs and scratch from every lane: a full pool
+  // fails the run, WE_CKCAP)
+  D.ck_cap = std::max<uint64_t>(1ull << 22, (uint64_t)N * 512);
   WL_TRY(wl_alloc(h, &D.ck, (size_t)D.ck_cap));
   WL_TRY(wl_alloc(h, &D.erank, std::min<uint64_t>(ev_cap, ERANK_MAX)));
   WL_TRY(wl_alloc(h, &h->d_pend, 2));
@@ -1001,7 +1355,7 @@ static int wl_check(nsgpu_wifil *h, const char *what) {
   if (e & WE_TX_IN_TX)
     return set_error(NSGPU_ESTATE, "%s: SendPacket while transmitting (yans-wifi-phy.cc:508 NS_ASSERT)", what);
   return set_error(NSGPU_ENOMEM, "%s: capacity exceeded (bits %u: 2 NiChanges ring, 4 Receive queue, 8 pending "
-                                 "EndReceive records, 16 epoch lists)", what, e);
+                                 "EndReceive records, 16 epoch lists, 32 CalculatePer chunk pool)", what, e);
 }
 
 // YansWifiPhy::SendPacket of `phy` from the host closure running at (now, closure uid); its fan-out takes
@@ -1029,15 +1383,23 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   if (!h || !uid || !dispatched || !digest) return set_error(NSGPU_EINVAL, "nsgpu_wifil_advance: null");
   const WDev D = h->D;  // (this epoch's status block: stat[par]; its counters were zeroed by the last epoch)
   uint8_t *const nxt = h->stat[h->par ^ 1];
+  uint32_t *const nxt_evc = h->evc[h->par ^ 1];
   // epoch: the phys' lanes, then the tail (PER products + sync ranks; patch + order + digest)
-  hipLaunchKernelGGL(k_wl_step, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
+  static const bool lane_step = [] {  // (NSGPU_WIFIL_LANE=1: the lane-per-phy step kernel)
+    const char *e = getenv("NSGPU_WIFIL_LANE");
+    return e && e[0] == '1';
+  }();
+  if (lane_step)
+    hipLaunchKernelGGL(k_wl_step, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
+  else
+    hipLaunchKernelGGL(k_wl_stepw, dim3((unsigned)D.nphy), dim3(64), 0, h->s, D, bound_ts, bound_uid);
 #ifdef NSGPU_PHASE_PROF
   hipLaunchKernelGGL(k_wl_prof_epoch, dim3(1), dim3(1), 0, h->s);
 #endif
   hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, h->s, D, *uid);
   const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
   hipLaunchKernelGGL(k_wl_order, dim3(ERANK_MAX / ORW), dim3(256), 0, h->s, D, *dispatched, logging ? 1 : 0,
-                     reinterpret_cast<uint32_t *>(nxt), reinterpret_cast<unsigned long long *>(nxt + 24));
+                     reinterpret_cast<uint32_t *>(nxt), reinterpret_cast<unsigned long long *>(nxt + 24), nxt_evc);
   NSGPU_HIP(hipGetLastError());
   // counters, the digest sum and the first end records in one trip
   NSGPU_HIP(hipMemcpyAsync(h->h_stat, D.cnt, STAT_HDR + END_STAGE * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
@@ -1054,7 +1416,7 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   }
   if (nev > ERANK_MAX) {  // a large epoch: its order on the host
     h->ev.resize(nev);
-    NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.ev, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
+    NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.evd, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
     NSGPU_HIP(hipStreamSynchronize(h->s));
     std::sort(h->ev.begin(), h->ev.end(), [](const LEv &a, const LEv &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
     for (const LEv &e : h->ev) {
@@ -1070,7 +1432,7 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
     if (logging && nev) {  // the ranked events into the log (no host sort)
       h->ev.resize(nev);
       h->erank.resize(nev);
-      NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.ev, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
+      NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.evd, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
       NSGPU_HIP(hipMemcpyAsync(h->erank.data(), D.erank, nev * sizeof(uint32_t), hipMemcpyDeviceToHost, h->s));
       NSGPU_HIP(hipStreamSynchronize(h->s));
       for (uint32_t i = 0; i < nev; i++) {
