@@ -2441,20 +2441,39 @@ static int host_step(nsgpu_p2p *h, const Ctl &c, hipStream_t s) {
   return NSGPU_OK;
 }
 
+// The exchanges of a partitioned window.  A one-rank job has nothing to exchange: its "all-gather" and
+// "all-to-all" are a device copy of its own slot (no RCCL call, so the window graph is all kernels and copies).
+static int x_allgather(nsgpu_p2p *h, const void *send, void *recv, size_t bytes, hipStream_t s) {
+  if (h->M.nranks == 1) {
+    if (send != recv) NSGPU_HIP(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+    return NSGPU_OK;
+  }
+  NCCL_TRY(ncclAllGather(send, recv, bytes, ncclUint8, h->comm->comm, s));
+  return NSGPU_OK;
+}
+static int x_alltoall(nsgpu_p2p *h, const void *send, void *recv, size_t bytes, hipStream_t s) {
+  if (h->M.nranks == 1) {
+    if (send != recv && bytes) NSGPU_HIP(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+    return NSGPU_OK;
+  }
+  NCCL_TRY(ncclAllToAll(send, recv, bytes, ncclUint8, h->comm->comm, s));
+  return NSGPU_OK;
+}
+
 // The partitioned window (one RCCL member): 4 kernels and 3 collectives, on stream s.
 static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s, int nwin = NWIN) {
-  ncclComm_t comm = h->comm->comm;
   const P2PDev &M = h->M;
-  for (int w = 0; w < nwin; w++) {
+  int rc = NSGPU_OK;
+  for (int w = 0; w < nwin && !rc; w++) {
     hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL), dim3(TB), 0, s, M);
-    NCCL_TRY(ncclAllGather(M.x0_send, M.x0_recv, X0B, ncclUint8, comm, s));
+    rc = x_allgather(h, M.x0_send, M.x0_recv, X0B, s);
     hipLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, M);
-    NCCL_TRY(ncclAllGather(M.x1_send, M.x1_recv, X1B, ncclUint8, comm, s));
+    if (!rc) rc = x_allgather(h, M.x1_send, M.x1_recv, X1B, s);
     hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, M);
     hipLaunchKernelGGL(k_dfin2, dim3(NHB), dim3(HB), 0, s, M);
-    NCCL_TRY(ncclAllToAll(M.x2_send, M.x2_recv, M.x2b, ncclUint8, comm, s));
+    if (!rc) rc = x_alltoall(h, M.x2_send, M.x2_recv, M.x2b, s);
   }
-  return NSGPU_OK;
+  return rc;
 }
 
 // The partitioned engine's host-driven steps (every rank makes the same ones: the pause that asks
@@ -2587,7 +2606,8 @@ static int drive_dist(nsgpu_p2p *h) {
   bool have_prev = false;
   auto cut = [h]() -> int {
     hipLaunchKernelGGL(k_refit2, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->M);
-    NCCL_TRY(ncclAllGather(h->M.xk_send, h->M.xk_recv, 16, ncclUint8, h->comm->comm, h->s));
+    const int rx = x_allgather(h, h->M.xk_send, h->M.xk_recv, 16, h->s);
+    if (rx) return rx;
     hipLaunchKernelGGL(k_cut2, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->M);
     NSGPU_HIP(hipGetLastError());
     return NSGPU_OK;

@@ -15,7 +15,9 @@ step bench_default 500 python bench.py
 step bench_nodefer 300 env NSGPU_P2P_NODEFER=1 python bench.py --no-cpu-baseline --no-secondary
 step bench_sdefk 300 env NSGPU_P2P_SDEF_KERNEL=1 python bench.py --no-cpu-baseline --no-secondary
 step bench_wifil_lane 300 env NSGPU_WIFIL_LANE=1 python bench.py --workload wifi-loop --no-cpu-baseline
+step bench_dumbbell_part 300 python bench.py --workload dumbbell --partitioned --steps 2 --warmup 1
 cd /tmp
 step rocprof_p2p 240 env NSGPU_P2P_EAGER=1 rocprofv3 --kernel-trace --stats -d $O/rocprof_p2p -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary
 step rocprof_wifil 240 rocprofv3 --kernel-trace --stats -d $O/rocprof_wifil -o run --output-format csv -- python3 $R/bench.py --workload wifi-loop --steps 1 --warmup 0 --no-cpu-baseline
+step rocprof_dumbbell_part 240 env NSGPU_P2P_EAGER=1 rocprofv3 --kernel-trace --stats -d $O/rocprof_dumbbell_part -o run --output-format csv -- python3 $R/bench.py --workload dumbbell --partitioned --steps 1 --warmup 0 --no-cpu-baseline
 exit 0
