@@ -155,7 +155,6 @@ struct Ctl {
   uint64_t acc_tc, acc_tinl;  // this window's children / inline children (k2_handle accumulates)
   uint32_t pdf;               // the window the next k2_pa appends is staged (1) or appended from sinfo (0)
   uint32_t sflag;             // a staged window awaits k2_sdef: 1 | (its window index & 3) << 1
-  uint32_t sdone, pad_sd;     // df_sdef blocks finished with it (the last one clears sflag and the ranks)
   uint32_t rk_W, rk_go;       // k2_handle's snapshot for k2_rank (window size; it was handled, normally)
   uint64_t rk_win, rk_lim;    //   (its window index, lim_rel): k2_rank's bookkeeping block rewrites C.W etc.
   WInfo winfo[4];             // window n's dispatch bases (k2_rank's bookkeeping), at n & 3
@@ -281,7 +280,7 @@ struct P2PDev {
   struct Stg *stage;      // [2][NMAX] a window's records in rank order (k2_pa stages, k2_sdef reads)
   uint2 *sleaf;           // [2][NMAX][maxc] their inline DoForwardUp leaves: (context, child index)
   uint32_t *cpt;          // [2][NMAX] child prefix by rank (k2_sdef): provisional uids resolve through it
-  uint32_t *dmap;         // [2][LCAP] local record -> dense index of its window (k2_rank; by window parity)
+  uint32_t *rmap;         // [2][WTOT] a staged window's record -> its rank (k2_pa; by window parity)
   uint32_t sdef_fold;     // df_sdef runs as k2_rank's block 1 (1) or as its own kernel k2_sdef (0)
 };
 
@@ -2007,7 +2006,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.stage, 2 * (size_t)NMAX));
     TRY(dalloc(h, &M.sleaf, 2 * (size_t)NMAX * M.maxc));
     TRY(dalloc(h, &M.cpt, 2 * (size_t)NMAX));
-    TRY(dalloc(h, &M.dmap, 2 * (size_t)LCAP));
+    TRY(dalloc(h, &M.rmap, 2 * (size_t)WTOT));
     const char *e = getenv("NSGPU_P2P_SDEF_KERNEL");  // (diagnostic: the accounting as its own kernel)
     M.sdef_fold = (e && e[0] == '1') ? 0u : 1u;
   }
@@ -2020,7 +2019,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     zok = hipMemset(M.stage, 0, 2 * (size_t)NMAX * sizeof(Stg)) == hipSuccess &&
           hipMemset(M.sleaf, 0, 2 * (size_t)NMAX * M.maxc * sizeof(uint2)) == hipSuccess &&
           hipMemset(M.cpt, 0, 2 * (size_t)NMAX * sizeof(uint32_t)) == hipSuccess &&
-          hipMemset(M.dmap, 0, 2 * (size_t)LCAP * sizeof(uint32_t)) == hipSuccess;
+          hipMemset(M.rmap, 0, 2 * (size_t)WTOT * sizeof(uint32_t)) == hipSuccess;
   if (!zok) {
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipMemset failed");

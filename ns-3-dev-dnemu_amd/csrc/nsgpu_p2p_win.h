@@ -483,6 +483,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       st.par = loc ? ldd.w : 0u;
       st.loc = loc ? 1u : 0u;
       M.stage[(uint64_t)pn * NMAX + srank] = st;
+      M.rmap[(uint64_t)pn * WTOT + s] = srank;  // (df_sdef: a local record's parent's rank)
     } else if (vs) {
       const uint64_t rk = K0 + si.x;
       digest += digest_term(rk, t, (uint32_t)spk);
@@ -1862,7 +1863,7 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 template <int NT>
 __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb);
 constexpr int RKT_DF = 1024;              // the deferred pipeline's k2_rank blocks: SUBS tiles at once
-constexpr int NSDEF = 8;                  // blocks of the deferred accounting (df_sdef)
+constexpr int NSDEF = 1;                  // blocks of the deferred accounting (df_sdef)
 constexpr int RK_GRID_DF = 256;             // one 1024-thread block per CU (~132 KB of LDS each): bookkeeping, accounting, tiles
 template <bool DF>
 __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
@@ -1932,7 +1933,6 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   // SUBS tiles a block at once: sub-tile `sub` is RKT threads (whole waves) with its own column buffer
   const uint32_t sub = threadIdx.x / RKT, lt = threadIdx.x % RKT;
   ulonglong2 *const cw = cws[sub];
-  uint32_t *const dmap = DF ? M.dmap + (wn & 1) * (uint64_t)LCAP : nullptr;
   for (uint32_t t0 = b0 * SUBS; t0 < ntile; t0 += nb * SUBS) {  // (uniform over the block)
     const uint32_t t = t0 + sub;
     const bool tA = t < na, tB = !tA && t < ntile;
@@ -1953,7 +1953,6 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
             M.ldat[cy] = make_uint4(r, M.nchild[r] | (M.ninl[r] << 16), (uint32_t)(w.x >> 32), M.wpar[r]);
             M.lrec[cy] = r;
             M.pwctx[r] = M.wctx[r];
-            if (DF) dmap[r - LBASE] = cy;  // (df_sdef: a local parent's rank)
           }
         }
         cw[lt] = w;
@@ -2130,38 +2129,56 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 // record's through its parent's rank and this window's prefixes); the log and digest get every record and
 // leaf; the child prefixes are kept (cpt) for the provisional uids of window n's children.  Afterwards the
 // window's rank accumulators are cleared (their parity is window n + 2's).
-// nsb blocks of NT threads (k2_rank<true>'s blocks 1 .. NSDEF, or the k2_sdef kernel): every block scans
-// the whole window into LDS (child / inline prefixes, group of each rank, group starts) — the scan is one
-// load trip and a few LDS passes — and then resolves, logs and digests its share of the ranks, one a thread.
-// The last block to finish clears the window's rank accumulators and the flag.
+// One block of NT threads (k2_rank<true>'s block 1, or the k2_sdef kernel).  Every record is loaded once, into
+// registers (RPT consecutive ranks a thread); the scan's per-rank results go to LDS (child / inline prefixes,
+// the group of each rank, group starts); each thread then resolves, logs and digests its own records with
+// their lookups (a local record's parent's rank through rmap, a provisional uid through window n-1's
+// prefixes, the inline leaves) issued together.  The staged window's parity is known from k2_handle's
+// snapshot (rk_win), so the records are loaded in the same trip as the flag.
 template <int NT>
-__device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb) {
-  const uint32_t sf = C.sflag;  // (cleared by the last block, after every block has read it)
+__device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
+  const uint32_t sf = C.sflag;
+  const uint64_t wn1 = C.rk_win - 1;  // (speculative: the window k2_pa staged is the last one)
+  constexpr int RPT = NMAX / NT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t pn = (uint32_t)(wn1 & 1);
+  // per record: key, counts, parent (a local record's key has uid 0: gen-0 uids start at 4; its context is
+  // read again only when logging)
+  uint64_t ek[RPT];
+  uint32_t ec[RPT], ep[RPT];
+  uint32_t prev_rel = 0;
+  {
+    const Stg *st = M.stage + (uint64_t)pn * NMAX;
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {  // (NMAX entries: in range, ignored past N)
+      ek[q] = st[tid * RPT + q].key;
+      ec[q] = st[tid * RPT + q].cnt;
+      ep[q] = st[tid * RPT + q].par;
+    }
+    if (tid > 0) prev_rel = (uint32_t)(st[tid * RPT - 1].key >> 32);
+  }
   if (!(sf & 1u)) return;
-  const uint32_t wi = (sf >> 1) & 3u, pn = wi & 1u;  // window n & 3, its parity
+  const uint32_t wi = (sf >> 1) & 3u;  // window n & 3
+  if ((wi & 1u) != pn) {  // (the snapshot was not the staged window's successor: reload by the flag's parity)
+    pn = wi & 1u;
+    const Stg *st = M.stage + (uint64_t)pn * NMAX;
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+      ek[q] = st[tid * RPT + q].key;
+      ec[q] = st[tid * RPT + q].cnt;
+      ep[q] = st[tid * RPT + q].par;
+    }
+    prev_rel = tid > 0 ? (uint32_t)(st[tid * RPT - 1].key >> 32) : 0u;
+  }
   const WInfo w = C.winfo[wi];
   const uint32_t uidq = C.winfo[(wi + 3) & 3].uid0;  // window n - 1's uid base
   const uint32_t N = w.N;
-  constexpr int RPT = NMAX / NT;
   __shared__ uint32_t s_cp[NMAX];   // child prefix by rank
   __shared__ uint32_t s_ip[NMAX];   // inline prefix by rank
   __shared__ uint32_t s_grp[NMAX];  // same-ts group of each rank
   __shared__ uint32_t s_gs[NMAX];   // start rank of each group
   __shared__ uint64_t wsum[NT / 64];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const Stg *st = M.stage + (uint64_t)pn * NMAX;
-  uint32_t erel[RPT], ecnt[RPT];
-  uint32_t prev_rel = 0;
-  if (tid * RPT > 0 && (uint32_t)(tid * RPT) <= N) prev_rel = (uint32_t)(st[tid * RPT - 1].key >> 32);
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    erel[q] = ecnt[q] = 0;
-    if (r < N) {
-      erel[q] = (uint32_t)(st[r].key >> 32);
-      ecnt[q] = st[r].cnt;
-    }
-  }
+  if ((uint32_t)(tid * RPT) > N) prev_rel = 0;
   uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
   {
     uint32_t pr = prev_rel;
@@ -2169,9 +2186,10 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb) {
     for (int q = 0; q < RPT; q++) {
       const uint32_t r = tid * RPT + q;
       if (r < N) {
-        const uint32_t hd = r == 0 || erel[q] != pr;
-        pr = erel[q];
-        sum += (uint64_t)(ecnt[q] & 0xffffu) | ((uint64_t)(ecnt[q] >> 16) << 21) | ((uint64_t)hd << 42);
+        const uint32_t rel = (uint32_t)(ek[q] >> 32);
+        const uint32_t hd = r == 0 || rel != pr;
+        pr = rel;
+        sum += (uint64_t)(ec[q] & 0xffffu) | ((uint64_t)(ec[q] >> 16) << 21) | ((uint64_t)hd << 42);
       }
     }
   }
@@ -2197,43 +2215,53 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb) {
     for (int q = 0; q < RPT; q++) {
       const uint32_t r = tid * RPT + q;
       if (r < N) {
-        const uint32_t hd = r == 0 || erel[q] != pr;
-        pr = erel[q];
+        const uint32_t rel = (uint32_t)(ek[q] >> 32);
+        const uint32_t hd = r == 0 || rel != pr;
+        pr = rel;
         bh += hd;
         s_cp[r] = bc;
         s_ip[r] = bi;
         s_grp[r] = bh - 1;
         if (hd) s_gs[bh - 1] = r;
-        if (b == 0) M.cpt[(uint64_t)pn * NMAX + r] = bc;  // (kept: window n's children resolve through it)
-        bc += ecnt[q] & 0xffffu;
-        bi += ecnt[q] >> 16;
+        M.cpt[(uint64_t)pn * NMAX + r] = bc;  // (kept: window n's children resolve through it)
+        bc += ec[q] & 0xffffu;
+        bi += ec[q] >> 16;
       }
     }
   }
-  __syncthreads();
-  // this block's ranks: own uids, log and digest (records at K0 + rank + the leaves of earlier groups;
-  // leaves after their group)
-  const uint32_t *const wr = M.wrank + (uint64_t)pn * WTOT, *const lr = M.lrank + (uint64_t)pn * LMAX;
+  // the lookups of this thread's records, all issued before the barrier's wait
+  const uint32_t *const rm = M.rmap + (uint64_t)pn * WTOT;
   const uint32_t *const cq = M.cpt + (uint64_t)(pn ^ 1u) * NMAX;
-  const uint32_t *const dmap = M.dmap + (uint64_t)pn * LCAP;
-  const uint32_t r0 = (uint32_t)((uint64_t)N * b / nsb), r1 = (uint32_t)((uint64_t)N * (b + 1) / nsb);
+  uint32_t look[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    look[q] = 0;
+    if (r < N) {
+      const uint32_t u = (uint32_t)ek[q];
+      if (((uint32_t)ek[q] == 0u)) look[q] = rm[(ep[q] & 0xffffffu) % WTOT];            // the parent's rank
+      else if (u & PROV) look[q] = cq[((u & 0x3fffffffu) >> 8) % NMAX];   // window n-1's child prefix
+    }
+  }
+  __syncthreads();
   uint64_t digest = 0;
-  for (uint32_t r = r0 + tid; r < r1; r += NT) {
-    const Stg e = st[r];
-    const uint32_t rel = (uint32_t)(e.key >> 32);
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    const uint32_t r = tid * RPT + q;
+    if (r >= N) continue;
+    const uint32_t rel = (uint32_t)(ek[q] >> 32);
     const uint64_t t = w.tmin + rel;
-    uint32_t uid = (uint32_t)e.key;
-    if (e.loc) {  // a local record: its parent's child prefix + its child index
-      const uint32_t p = e.par & 0xffffffu, j = e.par >> 24;
-      uint32_t rp = p < LBASE ? wr[p] : (p - LBASE < (uint32_t)LCAP ? lr[dmap[p - LBASE] % LMAX] : ~0u);
+    uint32_t uid = (uint32_t)ek[q];
+    if (((uint32_t)ek[q] == 0u)) {  // a local record: its parent's child prefix + its child index
+      uint32_t rp = look[q];
       if (rp >= N) {  // (cannot happen: the parent is a record of this window)
         atomicOr(M.error, 256u);
         rp = 0;
       }
-      uid = w.uid0 + s_cp[rp] + j;
+      uid = w.uid0 + s_cp[rp] + (ep[q] >> 24);
     } else if (uid & PROV) {  // a child of window n - 1
       if (((uid >> 30) & 1u) != (pn ^ 1u)) atomicOr(M.error, 256u);
-      uid = uidq + cq[((uid & 0x3fffffffu) >> 8) % NMAX] + (uid & 0xffu);
+      uid = uidq + look[q] + (uid & 0xffu);
     }
     const uint32_t g = s_grp[r];
     const uint32_t first = s_gs[g];
@@ -2243,11 +2271,11 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb) {
     if (rk < M.log_cap) {
       M.log_ts[rk] = t;
       M.log_uid[rk] = uid;
-      M.log_ctx[rk] = e.ctx;
+      M.log_ctx[rk] = M.stage[(uint64_t)pn * NMAX + r].ctx;
     }
-    const uint32_t ni = min(e.cnt >> 16, M.maxc);  // (bounded: a staged record's leaves fit its row)
-    const uint32_t cpr = s_cp[r], ipr = s_ip[r];
+    const uint32_t ni = min(ec[q] >> 16, M.maxc);  // (bounded: a staged record's leaves fit its row)
     const uint2 *lf = M.sleaf + ((uint64_t)pn * NMAX + r) * M.maxc;
+    const uint32_t cpr = s_cp[r], ipr = s_ip[r];
     for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
       const uint2 l = lf[k];
       const uint64_t lk = w.K0 + last + 1 + ipr + k;
@@ -2263,23 +2291,10 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb) {
   }
   digest = wave_sum64(digest);
   if (lane == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
-  // the last block: every block's lookups of the rank accumulators are done — clear them (their parity is
-  // window n + 2's) and the flag
-  __shared__ uint32_t s_last;
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    s_last = atomicAdd(&C.sdone, 1u) == nsb - 1 ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
+  __syncthreads();  // (every lookup of the rank accumulators is done: clear them for window n + 2)
   for (uint32_t i = tid; i < w.W; i += NT) M.wrank[(uint64_t)pn * WTOT + i] = 0;
   for (uint32_t i = tid; i < w.Lt; i += NT) M.lrank[(uint64_t)pn * LMAX + i] = 0;
-  if (tid == 0) {
-    C.sdone = 0;
-    C.sflag = 0;
-  }
+  if (tid == 0) C.sflag = 0;
 }
 __global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
   df_sdef<SCAN_THREADS>(M, *M.C, blockIdx.x, gridDim.x);

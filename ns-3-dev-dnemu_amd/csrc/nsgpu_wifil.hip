@@ -102,11 +102,12 @@ struct WDev {
   nsgpu_wifil_end *ends;
   uint32_t *end_sslot;
   uint32_t *cnt;  // [0] events, [1] syncs, [2] ends, [3] error bits (sticky: a SendPacket's are seen at the
-                  // next advance), [4] chunk slots claimed (zeroed by k_wl_order)
+                  // next advance), [4] chunk slots claimed (zeroed by k_wl_resolve)
   LCk *ck;        // the epoch's deferred chunks (ck_cap; a walk that finds no room computes its PER inline)
   LEck *eck;      // per end record
   uint32_t *evc;             // the epoch's event-list stripes: EV_STRIPES counters, EV_STRIDE words apart
-  LEv *evd;                  // the epoch's events in k_wl_order's dense order, uids resolved (the host's copy)
+  LEv *evd;                  // the epoch's events in dense order, uids resolved (the host's copy)
+  ulonglong2 *evk;           // the epoch's events' keys (ts, resolved uid) in dense order (k_wl_resolve)
   uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_order, when logging)
   unsigned long long *edig;  // the epoch's digest terms, summed on the device (k_wl_edigest)
   uint64_t sync_cap, ev_cap, end_cap, ck_cap;
@@ -988,118 +989,102 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
-// The epoch's second tail kernel (epochs of at most ERANK_MAX events; larger ones are ordered by the host):
-// the EndReceive uids into the end records and the still pending records, then every event's rank in the
-// epoch's (ts, uid) order, its digest term and (logging) its rank.  A block ranks ORW rows; the epoch's
-// keys stream through LDS in chunks of OCAP (one chunk for the usual epoch), each wave counting a quarter
-// of a chunk for the block's rows.  A dispatched EndReceive's uid resolves through its sync as the keys are
-// loaded.  The other status block (the next epoch's) is zeroed here, so an epoch needs no fills.
-constexpr uint32_t OCAP = 8192, ORW = 64;  // keys per LDS chunk (96 KB); rows per block
-constexpr int OLB = 8;                     // chunk entries a thread loads per memory trip
+// The epoch's tail, second and third kernels (epochs of at most ERANK_MAX events; larger ones are ordered by
+// the host).  k_wl_resolve: the EndReceive uids into the end records and the still pending records, and the
+// epoch's events from their stripes into a dense key array (ts, resolved uid) and, for the host, a dense
+// event array.  k_wl_order: every event's rank in the epoch's (ts, uid) order — a block ranks ORW rows, the
+// keys stream through LDS in chunks of OCAP (one chunk for the usual epoch), its 16 waves counting a slice of
+// a chunk each — then its digest term and (logging) its rank.  The next epoch's counters (status block,
+// stripes) are zeroed here, so an epoch needs no fills.
+constexpr uint32_t OCAP = 8192, ORW = 64;  // keys per LDS chunk (128 KB); rows per block
+constexpr int OWV = 16;                    // waves of a k_wl_order block (column slices)
 constexpr uint32_t ERANK_MAX = 65536;
-__global__ __launch_bounds__(256) void k_wl_order(const WDev D, uint64_t K0, int keep, uint32_t *zcnt,
-                                                  unsigned long long *zdig, uint32_t *zevc) {
-  __shared__ uint32_t s_pre[EV_STRIPES + 1];  // the stripes' prefix: dense index -> stripe
+struct StripeMap {  // dense index -> stripe slot (the stripes' prefix in LDS)
+  uint32_t pre[EV_STRIPES + 1];
+};
+__device__ __forceinline__ uint32_t load_stripes(const WDev &D, StripeMap &sm) {
   if (threadIdx.x < (uint32_t)EV_STRIPES) {
     const uint32_t c = D.evc[threadIdx.x * EV_STRIDE];
-    s_pre[threadIdx.x + 1] = c < D.ev_scap ? c : (uint32_t)D.ev_scap;
+    sm.pre[threadIdx.x + 1] = c < D.ev_scap ? c : (uint32_t)D.ev_scap;
   }
-  if (threadIdx.x == 0) s_pre[0] = 0;
+  if (threadIdx.x == 0) sm.pre[0] = 0;
   __syncthreads();
   if (threadIdx.x == 0)
-    for (int k = 1; k <= EV_STRIPES; k++) s_pre[k] += s_pre[k - 1];  // (64 adds, LDS)
+    for (int k = 1; k <= EV_STRIPES; k++) sm.pre[k] += sm.pre[k - 1];  // (64 adds, LDS)
   __syncthreads();
-  const uint32_t nev = s_pre[EV_STRIPES];
-  auto addr = [&](uint32_t i) -> uint64_t {  // dense index -> the event's slot
-    uint32_t lo = 0, hi = EV_STRIPES;  // s_pre[lo] <= i < s_pre[hi]
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_pre[mid] <= i) lo = mid;
-      else hi = mid;
-    }
-    return (uint64_t)lo * D.ev_scap + (i - s_pre[lo]);
-  };
+  return sm.pre[EV_STRIPES];
+}
+__device__ __forceinline__ uint64_t stripe_slot(const WDev &D, const StripeMap &sm, uint32_t i) {
+  uint32_t lo = 0, hi = EV_STRIPES;  // pre[lo] <= i < pre[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sm.pre[mid] <= i) lo = mid;
+    else hi = mid;
+  }
+  return (uint64_t)lo * D.ev_scap + (i - sm.pre[lo]);
+}
+__global__ __launch_bounds__(256) void k_wl_resolve(const WDev D, int keep, uint32_t *zcnt, unsigned long long *zdig,
+                                                    uint32_t *zevc) {
+  __shared__ StripeMap sm;
+  const uint32_t nev = load_stripes(D, sm);
   const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
   const uint64_t npe = (uint64_t)D.nphy * LPE_CAP;
   if (blockIdx.x == 0) {  // the next epoch's counters (its status block, its stripes); this epoch's total
     if (threadIdx.x < 3) zcnt[threadIdx.x] = 0;
     if (threadIdx.x == 3) *zdig = 0;
-    if (threadIdx.x == 4) D.cnt[4] = 0;  // (the chunk pool: k_wl_step is done with it)
+    if (threadIdx.x == 4) D.cnt[4] = 0;  // (the chunk pool: k_wl_stepw is done with it)
     if (threadIdx.x == 5) D.cnt[0] = nev;
     if (threadIdx.x < (uint32_t)EV_STRIPES) zevc[threadIdx.x * EV_STRIDE] = 0;
   }
   const uint64_t gs = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nend + npe; i += gs) {
+  const bool dense = keep || nev > ERANK_MAX;  // (the host reads the dense events)
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nend + npe + nev; i += gs) {
     if (i < nend) {
       const uint32_t sl = D.end_sslot[i];
       if (sl != NONE) D.ends[i].uid = D.sync[sl].euid;
-    } else {
+    } else if (i < nend + npe) {
       LPe &p = D.pe[i - nend];
       if (p.used && p.euid == NONE) p.euid = D.sync[p.sslot].euid;
-    }
-  }
-  if (nev > ERANK_MAX) {  // (the host sorts a huge epoch: its events dense, uids resolved)
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nev; i += gs) {
-      LEv e = D.ev[addr((uint32_t)i)];
+    } else {
+      const uint32_t k = (uint32_t)(i - nend - npe);
+      LEv e = D.ev[stripe_slot(D, sm, k)];
       if (e.sslot != NONE) e.uid = D.sync[e.sslot].euid;
-      D.evd[i] = e;
-    }
-    return;
-  }
-  const uint32_t r0 = blockIdx.x * ORW;
-  if (r0 >= nev) return;  // (block-uniform)
-  __shared__ uint64_t s_ts[OCAP];
-  __shared__ uint32_t s_uid[OCAP];
-  __shared__ uint32_t s_part[4][ORW];
-  const uint32_t lane = threadIdx.x & 63, q = threadIdx.x >> 6, i = r0 + lane;
-  uint64_t xts = ~0ull;
-  uint32_t xuid = ~0u, xctx = 0;
-  if (i < nev) {  // (the row's own key; its trip overlaps the first chunk's)
-    const LEv e = D.ev[addr(i)];
-    xts = e.ts;
-    xctx = e.ctx;
-    xuid = e.sslot != NONE ? D.sync[e.sslot].euid : e.uid;
-  }
-  uint32_t c = 0;
-  for (uint32_t b0 = 0; b0 < nev; b0 += OCAP) {
-    const uint32_t bn = nev - b0 < OCAP ? nev - b0 : OCAP;
-    __syncthreads();  // (the last chunk's counting is done)
-    for (uint32_t j0 = 0; j0 < bn; j0 += 256 * OLB) {  // OLB entries a thread per trip: loads, then syncs
-      LEv e[OLB];
-      uint32_t u[OLB];
-#pragma unroll
-      for (int k = 0; k < OLB; k++) {
-        const uint32_t j = j0 + k * 256 + threadIdx.x;
-        e[k] = j < bn ? D.ev[addr(b0 + j)] : LEv{0, 0, 0, NONE, 0};
-      }
-#pragma unroll
-      for (int k = 0; k < OLB; k++) u[k] = e[k].sslot != NONE ? D.sync[e[k].sslot].euid : e[k].uid;
-#pragma unroll
-      for (int k = 0; k < OLB; k++) {
-        const uint32_t j = j0 + k * 256 + threadIdx.x;
-        if (j < bn) {
-          s_ts[j] = e[k].ts;
-          s_uid[j] = u[k];
-        }
-      }
-    }
-    __syncthreads();
-    const uint32_t c0 = (uint32_t)((uint64_t)bn * q / 4), c1 = (uint32_t)((uint64_t)bn * (q + 1) / 4);
-#pragma unroll 8
-    for (uint32_t y = c0; y < c1; y++) {  // (every lane reads the same word: an LDS broadcast)
-      const uint64_t t = s_ts[y];
-      c += (t < xts) | ((t == xts) & (s_uid[y] < xuid));
+      D.evk[k] = make_ulonglong2(e.ts, e.uid);
+      if (dense) D.evd[k] = e;
     }
   }
-  s_part[q][lane] = c;
-  __syncthreads();
+}
+__global__ __launch_bounds__(OWV * 64) void k_wl_order(const WDev D, uint64_t K0, int keep) {
+  const uint32_t nev = D.cnt[0];
+  if (nev > ERANK_MAX) return;  // (the host sorts a huge epoch)
+  __shared__ ulonglong2 s_k[OCAP];
+  __shared__ uint32_t s_part[OWV][ORW];
+  const uint32_t lane = threadIdx.x & 63, q = threadIdx.x >> 6;
   uint64_t dg = 0;
-  if (q == 0 && i < nev) {
-    const uint32_t r = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane];
-    dg = digest_term(K0 + r, xts, xuid);
-    if (keep) {
-      D.erank[i] = r;
-      D.evd[i] = LEv{xts, xuid, xctx, NONE, 0};
+  for (uint32_t r0 = blockIdx.x * ORW; r0 < nev; r0 += gridDim.x * ORW) {  // (block-uniform)
+    const uint32_t i = r0 + lane;
+    const ulonglong2 x = i < nev ? D.evk[i] : make_ulonglong2(~0ull, ~0ull);
+    uint32_t c = 0;
+    for (uint32_t b0 = 0; b0 < nev; b0 += OCAP) {
+      const uint32_t bn = nev - b0 < OCAP ? nev - b0 : OCAP;
+      __syncthreads();  // (the last chunk's counting is done)
+      for (uint32_t j = threadIdx.x; j < bn; j += OWV * 64) s_k[j] = D.evk[b0 + j];
+      __syncthreads();
+      const uint32_t c0 = (uint32_t)((uint64_t)bn * q / OWV), c1 = (uint32_t)((uint64_t)bn * (q + 1) / OWV);
+#pragma unroll 8
+      for (uint32_t y = c0; y < c1; y++) {  // (every lane reads the same entry: an LDS broadcast)
+        const ulonglong2 k = s_k[y];
+        c += (k.x < x.x) | ((k.x == x.x) & (k.y < x.y));
+      }
+    }
+    s_part[q][lane] = c;
+    __syncthreads();
+    if (q == 0 && i < nev) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int k = 0; k < OWV; k++) r += s_part[k][lane];
+      dg += digest_term(K0 + r, x.x, (uint32_t)x.y);
+      if (keep) D.erank[i] = r;
     }
   }
   if (q == 0) {
@@ -1203,7 +1188,7 @@ struct nsgpu_wifil {
   // device's D.cnt / D.edig / D.ends are laid out the same way in one allocation)
   uint8_t *h_stat = nullptr;
   uint8_t *stat[2] = {nullptr, nullptr};  // the device's status blocks, by epoch parity (the next one is zeroed
-  uint32_t par = 0;                       //   by the running epoch's k_wl_order: no fills between epochs)
+  uint32_t par = 0;                       //   by the running epoch's k_wl_resolve: no fills between epochs)
   uint32_t *evc[2] = {nullptr, nullptr};  // the event-list stripe counters, by epoch parity (likewise)
   uint32_t *h_cnt = nullptr;
   unsigned long long *h_dig = nullptr;
@@ -1313,6 +1298,7 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
     WL_TRY(wl_alloc(h, &h->evc[b], (size_t)EV_STRIPES * EV_STRIDE));
   }
   WL_TRY(wl_alloc(h, &D.evd, ev_cap));
+  WL_TRY(wl_alloc(h, &D.evk, ev_cap));
   D.ev_scap = ev_cap / EV_STRIPES;
   wl_use_stat(h, 0);
   WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
@@ -1398,8 +1384,9 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
 #endif
   hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, h->s, D, *uid);
   const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
-  hipLaunchKernelGGL(k_wl_order, dim3(ERANK_MAX / ORW), dim3(256), 0, h->s, D, *dispatched, logging ? 1 : 0,
-                     reinterpret_cast<uint32_t *>(nxt), reinterpret_cast<unsigned long long *>(nxt + 24), nxt_evc);
+  hipLaunchKernelGGL(k_wl_resolve, dim3(512), dim3(256), 0, h->s, D, logging ? 1 : 0, reinterpret_cast<uint32_t *>(nxt),
+                     reinterpret_cast<unsigned long long *>(nxt + 24), nxt_evc);
+  hipLaunchKernelGGL(k_wl_order, dim3(256), dim3(OWV * 64), 0, h->s, D, *dispatched, logging ? 1 : 0);
   NSGPU_HIP(hipGetLastError());
   // counters, the digest sum and the first end records in one trip
   NSGPU_HIP(hipMemcpyAsync(h->h_stat, D.cnt, STAT_HDR + END_STAGE * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
