@@ -2032,8 +2032,19 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
 template <int NT>
 __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32_t Lt, uint64_t wn) {
   const int tid = threadIdx.x;
+  // every run-control field the bookkeeping reads, loaded at once (one memory trip: a load issued after a
+  // branch on another loaded value would wait for that value first)
   const uint64_t nF = C.nF, nfree = C.nfree, npush = C.npush;
   const uint32_t c_nhub = C.nhub;
+  uint64_t tc = 0, tinl = 0, live = 0, P_end = 0, c_bound = 0, c_nbound = 0, K = 0, tmin = 0, ilim = 0, windows = 0,
+           span_t = 0, hts = 0, max_window = 0, max_windows = 0, refits = 0;
+  uint32_t uid = 0, rt = 0, stop_seen = 0, hcap = 0;
+  if (tid == 0) {
+    tc = C.acc_tc, tinl = C.acc_tinl, live = C.live, P_end = C.P_end, c_bound = C.bound, c_nbound = C.nbound;
+    K = C.K, tmin = C.tmin, ilim = C.inline_lim, windows = C.windows, span_t = C.span_t, hts = C.hts;
+    max_window = C.max_window, max_windows = C.max_windows, refits = C.refits;
+    uid = C.uid, rt = C.rt, stop_seen = C.stop_seen, hcap = C.hcap;
+  }
   const uint64_t consumed = nF < nfree ? nF : nfree;
   const uint64_t mv = consumed < npush ? consumed : npush;
   // the free stack loses the slots the fresh children took and gains the window's (disjoint ranges)
@@ -2043,10 +2054,8 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
     for (uint32_t h = tid; h < nh; h += NT) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
   }
   if (tid != 0) return;
-  const uint64_t tc = C.acc_tc, tinl = C.acc_tinl;
   C.acc_tc = 0;
   C.acc_tinl = 0;
-  const uint64_t live = C.live, P_end = C.P_end;
   C.nfree = nfree - consumed + npush;
   const uint64_t P_end2 = P_end + (nF > nfree ? nF - nfree : 0);
   const uint64_t live2 = live - npush + nF;
@@ -2056,13 +2065,12 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
   C.nF = 0;
   C.nhub = 0;
   C.force_run = 0;
-  const uint64_t c_bound = C.bound, c_nbound = C.nbound;
   if (!ranked) {  // the window overflowed: a sorted run (host radix sort), nothing dispatched (k2_scan's branch)
     C.rW = W;
     C.r0 = 0;
     C.W = 0;
     C.pvalid = 0;
-    C.refits++;
+    C.refits = refits + 1;
     C.renarrow = c_nbound < c_bound ? 1u : 0u;
     if (c_nbound < c_bound) C.span_t = ((c_bound >> 32) >> 1) + 1;
     C.mode = MODE_SORT;
@@ -2074,8 +2082,6 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
     C.done = 1;
     return;
   }
-  const uint64_t K = C.K, tmin = C.tmin, ilim = C.inline_lim, windows = C.windows, span_t = C.span_t;
-  const uint32_t uid = C.uid, rt = C.rt;
   C.winfo[wn & 3] = WInfo{K, tmin, ilim, uid, N, W, Lt};
   C.pK0 = K;
   C.puid0 = uid;
@@ -2090,7 +2096,7 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
   C.uid = uid + (uint32_t)tc;
   const uint64_t pchild = tc - tinl - Lt;  // (the local records' uids were consumed, they ran in the window)
   C.pchild = pchild;
-  bool done = C.stop_seen || (live2 + pchild == 0 && C.hts == ~0ull);
+  bool done = stop_seen || (live2 + pchild == 0 && hts == ~0ull);
   if ((uint64_t)uid + tc >= (uint64_t)UID_DF_LIMIT) {  // (provisional uids must stay above every real one)
     atomicOr(M.error, 512u);
     done = true;
@@ -2102,19 +2108,19 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
   C.red[rt ^ 1].tmin = C.red[rt ^ 1].wend = C.red[rt ^ 1].stopts = C.red[rt ^ 1].wendw = ~0ull;  // consumed
   C.rt = rt ^ 1;
   C.windows = windows + 1;
-  if (N > C.max_window) C.max_window = N;
+  if (N > max_window) C.max_window = N;
   C.W = 0;
   if (P_end2 > M.pool_cap) {
     atomicOr(M.error, 1u);
     done = true;
   }
-  if (windows + 1 >= C.max_windows && !done) {
+  if (windows + 1 >= max_windows && !done) {
     atomicOr(M.error, 4u);
     done = true;
   }
   if (done) {
     C.done = 1;
-  } else if (C.hcap) {  // the window was cut at the next host closure: pause
+  } else if (hcap) {  // the window was cut at the next host closure: pause
     C.hcap = 0;
     C.mode = MODE_HOST;
   } else if (P_end2 > 65536 && live2 * 4 < P_end2) {
@@ -2139,6 +2145,9 @@ template <int NT>
 __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   const uint32_t sf = C.sflag;
   const uint64_t wn1 = C.rk_win - 1;  // (speculative: the window k2_pa staged is the last one)
+  WInfo wa[4];  // (all four: loaded with the flag, picked by it)
+#pragma unroll
+  for (int k = 0; k < 4; k++) wa[k] = C.winfo[k];
   constexpr int RPT = NMAX / NT;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint32_t pn = (uint32_t)(wn1 & 1);
@@ -2170,8 +2179,11 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     }
     prev_rel = tid > 0 ? (uint32_t)(st[tid * RPT - 1].key >> 32) : 0u;
   }
-  const WInfo w = C.winfo[wi];
-  const uint32_t uidq = C.winfo[(wi + 3) & 3].uid0;  // window n - 1's uid base
+  WInfo w = wa[0];
+  uint32_t uidq = wa[3].uid0;  // window n - 1's uid base
+#pragma unroll
+  for (int k = 1; k < 4; k++)
+    if ((uint32_t)k == wi) w = wa[k], uidq = wa[k - 1].uid0;
   const uint32_t N = w.N;
   __shared__ uint32_t s_cp[NMAX];   // child prefix by rank
   __shared__ uint32_t s_ip[NMAX];   // inline prefix by rank

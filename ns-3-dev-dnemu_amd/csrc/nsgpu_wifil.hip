@@ -43,10 +43,11 @@ struct LNi {  // InterferenceHelper::NiChange (interference-helper.cc:91-110)
   int64_t t;
   double d;
 };
-struct LRx {  // a pending Receive: arrival, uid, transmission, rxPowerW (DbmToW of CalcRxPower + RxGain)
-  uint64_t at;
+struct LRx {  // a pending Receive: arrival, uid, transmission, rxPowerW (DbmToW of CalcRxPower + RxGain), and
+  uint64_t at;  // the transmission's duration (so a Receive needs no second load)
   uint32_t uid, tx;
   double w;
+  int64_t dur;
 };
 struct LPe {  // a pending EndReceive
   uint64_t ts, sts;          // its ts; the syncing Receive's ts
@@ -699,10 +700,15 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
   uint32_t *const evc = D.evc + (uint32_t)(j % EV_STRIPES) * EV_STRIDE;
   LEv *const evs = D.ev + (uint64_t)(j % EV_STRIPES) * D.ev_scap;
   uint32_t err = 0;
+  // the pending EndReceive records: lane q < LPE_CAP holds record q for the whole epoch (the kernel's own
+  // changes are made to both copies); the Receive queue: lane l holds entry head + rq0 + l, 64 a trip
+  LPe mine{};
+  if (lane < (uint32_t)LPE_CAP) mine = pe[lane];
+  uint32_t rq0 = ~0u;  // (queue offset of the loaded chunk; ~0: none)
+  LRx rqc{};
+  uint32_t rqn = 0;    // Receives taken this epoch
   for (;;) {
-    // the next pending EndReceive (lane q < LPE_CAP loads record q; the selection reads them lane by lane)
-    LPe mine{};
-    if (lane < (uint32_t)LPE_CAP) mine = pe[lane];
+    // the next pending EndReceive (the selection reads the records lane by lane)
     const uint64_t used = __ballot(lane < (uint32_t)LPE_CAP && mine.used);
     int e = -1;
     LPe eb{};
@@ -713,7 +719,18 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
     }
     const bool hr = P.rq_len > 0;
     LRx r{};
-    if (hr) r = rq[P.rq_head & D.rq_mask];
+    if (hr) {
+      if (rq0 == ~0u || rqn - rq0 >= 64) {  // (the next 64 queued Receives, one trip)
+        rq0 = rqn;
+        rqc = lane < P.rq_len ? rq[(P.rq_head + lane) & D.rq_mask] : LRx{};
+      }
+      const int u = (int)(rqn - rq0);
+      r.at = (uint64_t)rl_i64((int64_t)rqc.at, u);
+      r.uid = rl_u32(rqc.uid, u);
+      r.tx = rl_u32(rqc.tx, u);
+      r.w = rl_d(rqc.w, u);
+      r.dur = rl_i64(rqc.dur, u);
+    }
     bool take_r;
     if (hr && e >= 0) take_r = r.at < eb.ts || (r.at == eb.ts && (eb.euid == NONE || r.uid < eb.euid));
     else if (hr) take_r = true;
@@ -829,14 +846,16 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
         err |= WE_CAP;
       }
       if (lane == 0) pe[e].used = 0;
+      if (lane == (uint32_t)e) mine.used = 0;
       if (P.live == (uint32_t)e) P.live = NONE;
       continue;
     }
     // ---- YansWifiChannel::Receive -> YansWifiPhy::StartReceivePacket (yans-wifi-phy.cc:399-496)
     P.rq_head++;
     P.rq_len--;
+    rqn++;
     const int64_t nw = (int64_t)r.at;
-    const int64_t endNew = nw + D.tx[r.tx].dur;
+    const int64_t endNew = nw + r.dur;
     if (P.len + 2 > m + 1) {
       err |= WE_NICAP;
       break;
@@ -866,12 +885,8 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
       until = until > 0 ? until : 0;
       maybe = endNew > nw + until;
     } else if (r.w > D.edW) {  // sync (:461-472): SwitchToRx, NotifyRxStart, Schedule (rxDuration, EndReceive)
-      int q = -1;
-      for (int k = 0; k < LPE_CAP; k++)
-        if (!pe[k].used) {
-          q = k;
-          break;
-        }
+      const uint64_t fr = __ballot(lane < (uint32_t)LPE_CAP && !mine.used);  // (the first free record)
+      const int q = fr ? __builtin_ctzll(fr) : -1;
       uint32_t sl = 0;
       if (lane == 0) sl = atomicAdd(&D.cnt[1], 1u);
       sl = rl_u32(sl, 0);
@@ -879,10 +894,12 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
         err |= q < 0 ? WE_PECAP : WE_CAP;
         break;
       }
+      const LPe np{(uint64_t)endNew, r.at, r.uid, NONE, r.tx, 0, sl, 1, r.w};
       if (lane == 0) {
         D.sync[sl] = LSync{r.at, r.uid, NONE};
-        pe[q] = LPe{(uint64_t)endNew, r.at, r.uid, NONE, r.tx, 0, sl, 1, r.w};
+        pe[q] = np;
       }
+      if (lane == (uint32_t)q) mine = np;
       P.live = (uint32_t)q;
       P.rxing = 1;
       P.endRx = endNew;
@@ -1133,7 +1150,7 @@ __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t
     rq[(P.rq_head + q) & D.rq_mask] = e;
     q--;
   }
-  rq[(P.rq_head + q) & D.rq_mask] = LRx{at, uid, k, w};
+  rq[(P.rq_head + q) & D.rq_mask] = LRx{at, uid, k, w, t.dur};
   P.rq_len++;
 }
 
