@@ -2245,14 +2245,17 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   const uint32_t *const rm = M.rmap + (uint64_t)pn * WTOT;
   const uint32_t *const cq = M.cpt + (uint64_t)(pn ^ 1u) * NMAX;
   uint32_t look[RPT];
+  uint2 lf0[RPT];  // each record's first inline leaf (most have at most one: the rest are loaded in the loop)
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
     look[q] = 0;
+    lf0[q] = make_uint2(0, 0);
     if (r < N) {
       const uint32_t u = (uint32_t)ek[q];
       if (((uint32_t)ek[q] == 0u)) look[q] = rm[(ep[q] & 0xffffffu) % WTOT];            // the parent's rank
       else if (u & PROV) look[q] = cq[((u & 0x3fffffffu) >> 8) % NMAX];   // window n-1's child prefix
+      if (ec[q] >> 16) lf0[q] = M.sleaf[((uint64_t)pn * NMAX + r) * M.maxc];
     }
   }
   __syncthreads();
@@ -2289,7 +2292,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     const uint2 *lf = M.sleaf + ((uint64_t)pn * NMAX + r) * M.maxc;
     const uint32_t cpr = s_cp[r], ipr = s_ip[r];
     for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
-      const uint2 l = lf[k];
+      const uint2 l = k ? lf[k] : lf0[q];
       const uint64_t lk = w.K0 + last + 1 + ipr + k;
       const uint32_t lu = w.uid0 + cpr + l.y;
       digest += digest_term(lk, t, lu);
