@@ -277,10 +277,10 @@ struct P2PDev {
                           // child counts (n | inline << 16), rel ts, parent (wpar)
   uint32_t *lrank;        // [LMAX] their rank accumulators (k2_rank; 0 between windows)
   // ---- deferred windows (wrank / lrank are then 2 x WTOT / 2 x LMAX: by window parity) ----
-  struct Stg *stage;      // [2][NMAX] a window's records in rank order (k2_pa stages, k2_sdef reads)
-  uint2 *sleaf;           // [2][NMAX][maxc] their inline DoForwardUp leaves: (context, child index)
+  struct Stg *stage;      // [NMAX] a window's records in rank order (k2_pa stages, k2_sdef reads)
+  uint2 *sleaf;           // [NMAX][maxc] their inline DoForwardUp leaves: (context, child index)
   uint32_t *cpt;          // [2][NMAX] child prefix by rank (k2_sdef): provisional uids resolve through it
-  uint32_t *rmap;         // [2][WTOT] a staged window's record -> its rank (k2_pa; by window parity)
+  uint32_t *rmap;         // [WTOT] the staged window's record -> its rank (k2_pa)
   uint32_t sdef_fold;     // df_sdef runs as k2_rank's block 1 (1) or as its own kernel k2_sdef (0)
 };
 
@@ -2003,10 +2003,10 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.lrank, 2 * (size_t)LMAX));
   // deferred windows (single wide engine): staged records, their leaves, child prefixes, dense map
   if (M.wide) {
-    TRY(dalloc(h, &M.stage, 2 * (size_t)NMAX));
-    TRY(dalloc(h, &M.sleaf, 2 * (size_t)NMAX * M.maxc));
+    TRY(dalloc(h, &M.stage, NMAX));
+    TRY(dalloc(h, &M.sleaf, (size_t)NMAX * M.maxc));
     TRY(dalloc(h, &M.cpt, 2 * (size_t)NMAX));
-    TRY(dalloc(h, &M.rmap, 2 * (size_t)WTOT));
+    TRY(dalloc(h, &M.rmap, WTOT));
     const char *e = getenv("NSGPU_P2P_SDEF_KERNEL");  // (diagnostic: the accounting as its own kernel)
     M.sdef_fold = (e && e[0] == '1') ? 0u : 1u;
   }
@@ -2016,10 +2016,10 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
              hipMemset(M.lcnt, 0, NLR * sizeof(uint32_t)) == hipSuccess &&
              hipMemset(M.ldat, 0, LMAX * sizeof(uint4)) == hipSuccess;
   if (zok && M.wide)
-    zok = hipMemset(M.stage, 0, 2 * (size_t)NMAX * sizeof(Stg)) == hipSuccess &&
-          hipMemset(M.sleaf, 0, 2 * (size_t)NMAX * M.maxc * sizeof(uint2)) == hipSuccess &&
+    zok = hipMemset(M.stage, 0, (size_t)NMAX * sizeof(Stg)) == hipSuccess &&
+          hipMemset(M.sleaf, 0, (size_t)NMAX * M.maxc * sizeof(uint2)) == hipSuccess &&
           hipMemset(M.cpt, 0, 2 * (size_t)NMAX * sizeof(uint32_t)) == hipSuccess &&
-          hipMemset(M.rmap, 0, 2 * (size_t)WTOT * sizeof(uint32_t)) == hipSuccess;
+          hipMemset(M.rmap, 0, (size_t)WTOT * sizeof(uint32_t)) == hipSuccess;
   if (!zok) {
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipMemset failed");

@@ -482,8 +482,8 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       st.cnt = loc ? ldd.y : (ncr | (ninl0 << 16));
       st.par = loc ? ldd.w : 0u;
       st.loc = loc ? 1u : 0u;
-      M.stage[(uint64_t)pn * NMAX + srank] = st;
-      M.rmap[(uint64_t)pn * WTOT + s] = srank;  // (df_sdef: a local record's parent's rank)
+      M.stage[srank] = st;  // (one stage: df_sdef(n - 1) is done with it before k2_pa(n + 1) writes)
+      M.rmap[s] = srank;     // (df_sdef: a local record's parent's rank)
     } else if (vs) {
       const uint64_t rk = K0 + si.x;
       digest += digest_term(rk, t, (uint32_t)spk);
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
           if ((e.kind & 0xffu) == K_FWD_UP) {  // leaf: dispatched inside its window (or never), not queued
             if (stg) {
               if (rel < ilim && srank < (uint32_t)NMAX) {  // (k2_sdef logs it after its group)
-                M.sleaf[((uint64_t)pn * NMAX + srank) * M.maxc + ii] = make_uint2(e.ctx, j);
+                M.sleaf[(uint64_t)srank * M.maxc + ii] = make_uint2(e.ctx, j);
                 ii++;
               }
             } else if (rel < ilim) {
@@ -2144,20 +2144,18 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 template <int NT>
 __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   const uint32_t sf = C.sflag;
-  const uint64_t wn1 = C.rk_win - 1;  // (speculative: the window k2_pa staged is the last one)
   WInfo wa[4];  // (all four: loaded with the flag, picked by it)
 #pragma unroll
   for (int k = 0; k < 4; k++) wa[k] = C.winfo[k];
   constexpr int RPT = NMAX / NT;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  uint32_t pn = (uint32_t)(wn1 & 1);
   // per record: key, counts, parent (a local record's key has uid 0: gen-0 uids start at 4; its context is
-  // read again only when logging)
+  // read again only when logging) — one stage (the window k2_pa staged), loaded with the run control
   uint64_t ek[RPT];
   uint32_t ec[RPT], ep[RPT];
   uint32_t prev_rel = 0;
   {
-    const Stg *st = M.stage + (uint64_t)pn * NMAX;
+    const Stg *st = M.stage;
 #pragma unroll
     for (int q = 0; q < RPT; q++) {  // (NMAX entries: in range, ignored past N)
       ek[q] = st[tid * RPT + q].key;
@@ -2167,18 +2165,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     if (tid > 0) prev_rel = (uint32_t)(st[tid * RPT - 1].key >> 32);
   }
   if (!(sf & 1u)) return;
-  const uint32_t wi = (sf >> 1) & 3u;  // window n & 3
-  if ((wi & 1u) != pn) {  // (the snapshot was not the staged window's successor: reload by the flag's parity)
-    pn = wi & 1u;
-    const Stg *st = M.stage + (uint64_t)pn * NMAX;
-#pragma unroll
-    for (int q = 0; q < RPT; q++) {
-      ek[q] = st[tid * RPT + q].key;
-      ec[q] = st[tid * RPT + q].cnt;
-      ep[q] = st[tid * RPT + q].par;
-    }
-    prev_rel = tid > 0 ? (uint32_t)(st[tid * RPT - 1].key >> 32) : 0u;
-  }
+  const uint32_t wi = (sf >> 1) & 3u, pn = wi & 1u;  // window n & 3, its parity (its child prefixes' buffer)
   WInfo w = wa[0];
   uint32_t uidq = wa[3].uid0;  // window n - 1's uid base
 #pragma unroll
@@ -2242,7 +2229,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     }
   }
   // the lookups of this thread's records, all issued before the barrier's wait
-  const uint32_t *const rm = M.rmap + (uint64_t)pn * WTOT;
+  const uint32_t *const rm = M.rmap;
   const uint32_t *const cq = M.cpt + (uint64_t)(pn ^ 1u) * NMAX;
   uint32_t look[RPT];
   uint2 lf0[RPT];  // each record's first inline leaf (most have at most one: the rest are loaded in the loop)
@@ -2255,7 +2242,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
       const uint32_t u = (uint32_t)ek[q];
       if (((uint32_t)ek[q] == 0u)) look[q] = rm[(ep[q] & 0xffffffu) % WTOT];            // the parent's rank
       else if (u & PROV) look[q] = cq[((u & 0x3fffffffu) >> 8) % NMAX];   // window n-1's child prefix
-      if (ec[q] >> 16) lf0[q] = M.sleaf[((uint64_t)pn * NMAX + r) * M.maxc];
+      if (ec[q] >> 16) lf0[q] = M.sleaf[(uint64_t)r * M.maxc];
     }
   }
   __syncthreads();
@@ -2286,10 +2273,10 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     if (rk < M.log_cap) {
       M.log_ts[rk] = t;
       M.log_uid[rk] = uid;
-      M.log_ctx[rk] = M.stage[(uint64_t)pn * NMAX + r].ctx;
+      M.log_ctx[rk] = M.stage[r].ctx;
     }
     const uint32_t ni = min(ec[q] >> 16, M.maxc);  // (bounded: a staged record's leaves fit its row)
-    const uint2 *lf = M.sleaf + ((uint64_t)pn * NMAX + r) * M.maxc;
+    const uint2 *lf = M.sleaf + (uint64_t)r * M.maxc;
     const uint32_t cpr = s_cp[r], ipr = s_ip[r];
     for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
       const uint2 l = k ? lf[k] : lf0[q];
