@@ -97,13 +97,17 @@ struct WInfo {
 };
 
 // A staged record of a deferred window, at its rank: key (rel ts << 32 | its uid, which may be provisional;
-// a local record's uid is its parent's child prefix + j, resolved by k2_sdef), context, child counts
-// (n | inline << 16), and for a local record its parent (wpar: record | child index << 24) with loc = 1.
+// a local record's uid is its parent's child prefix + j, resolved by k2_sdef, and its key's uid is 0), child
+// counts (n | inline << 16), and for a local record its parent (wpar: record | child index << 24).  Its
+// context and first inline leaf are kept beside it (stx, slf0).  Stage arrays (and the child prefixes cpt) are
+// indexed by stg_pos(rank): k2_sdef's thread t owns the 8 consecutive ranks 8t..8t+7 and loads its q-th one
+// from q * 1024 + t, so every load and store of a wave is coalesced.
 struct Stg {
   uint64_t key;
-  uint32_t ctx, cnt, par, loc;
+  uint32_t cnt, par;
 };
-static_assert(sizeof(Stg) == 24, "Stg");
+static_assert(sizeof(Stg) == 16, "Stg");
+constexpr uint32_t STG_NT = 1024;  // k2_sdef's threads (its rank slices)
 // Provisional uids (deferred windows): child j of the record of rank r of window n, before window n's child
 // prefix is known, is PROV | (n & 1) << 30 | r << 8 | j — above every resolved uid (< UID_DF_LIMIT, checked), so
 // keys compare as the final uids do; resolved to uid0(n) + cpt[n & 1][r] + j.
@@ -277,11 +281,14 @@ struct P2PDev {
                           // child counts (n | inline << 16), rel ts, parent (wpar)
   uint32_t *lrank;        // [LMAX] their rank accumulators (k2_rank; 0 between windows)
   // ---- deferred windows (wrank / lrank are then 2 x WTOT / 2 x LMAX: by window parity) ----
-  struct Stg *stage;      // [NMAX] a window's records in rank order (k2_pa stages, k2_sdef reads)
-  uint2 *sleaf;           // [NMAX][maxc] their inline DoForwardUp leaves: (context, child index)
+  struct Stg *stage;      // [NMAX] a window's records by stg_pos(rank) (k2_pa stages, k2_sdef reads)
+  uint32_t *stx;          // [NMAX] their contexts (stg_pos)
+  uint2 *slf0;            // [NMAX] their first inline DoForwardUp leaf: (context, child index) (stg_pos)
+  uint2 *sleaf;           // [NMAX][maxc] their further inline leaves (by rank, entry 0 unused)
   uint32_t *cpt;          // [2][NMAX] child prefix by rank (k2_sdef): provisional uids resolve through it
   uint32_t *rmap;         // [WTOT] the staged window's record -> its rank (k2_pa)
   uint32_t sdef_fold;     // df_sdef runs as k2_rank's block 1 (1) or as its own kernel k2_sdef (0)
+  uint32_t sdef_abl;      // (diagnostic ablation, NSGPU_P2P_SDEF_ABL: 1 no lookups, 2 no resolve pass, 4 no prefix stores)
 };
 
 // ---------------- wave / block helpers ----------------
@@ -2005,10 +2012,14 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   if (M.wide) {
     TRY(dalloc(h, &M.stage, NMAX));
     TRY(dalloc(h, &M.sleaf, (size_t)NMAX * M.maxc));
+    TRY(dalloc(h, &M.stx, NMAX));
+    TRY(dalloc(h, &M.slf0, NMAX));
     TRY(dalloc(h, &M.cpt, 2 * (size_t)NMAX));
     TRY(dalloc(h, &M.rmap, WTOT));
     const char *e = getenv("NSGPU_P2P_SDEF_KERNEL");  // (diagnostic: the accounting as its own kernel)
     M.sdef_fold = (e && e[0] == '1') ? 0u : 1u;
+    const char *ab = getenv("NSGPU_P2P_SDEF_ABL");
+    M.sdef_abl = ab ? (uint32_t)atoi(ab) : 0u;
   }
   // (k2_pa loads lrec / ldat entries speculatively and follows their record index: zeroed, every entry
   // stays < WTOT; the deferred pipeline's arrays start zeroed too, so a stale entry is always in range)
@@ -2018,6 +2029,8 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   if (zok && M.wide)
     zok = hipMemset(M.stage, 0, (size_t)NMAX * sizeof(Stg)) == hipSuccess &&
           hipMemset(M.sleaf, 0, (size_t)NMAX * M.maxc * sizeof(uint2)) == hipSuccess &&
+          hipMemset(M.stx, 0, (size_t)NMAX * sizeof(uint32_t)) == hipSuccess &&
+          hipMemset(M.slf0, 0, (size_t)NMAX * sizeof(uint2)) == hipSuccess &&
           hipMemset(M.cpt, 0, 2 * (size_t)NMAX * sizeof(uint32_t)) == hipSuccess &&
           hipMemset(M.rmap, 0, (size_t)WTOT * sizeof(uint32_t)) == hipSuccess;
   if (!zok) {

@@ -41,6 +41,13 @@ constexpr uint32_t LBASE = WCAP;         // local records live at [LBASE, LBASE 
 constexpr int LCAP = NHB * LR + NHUB * LRH;
 constexpr int WTOT = WCAP + LCAP;        // record index space (gen-0 slots + local regions)
 constexpr int NMAX = 8192;               // records of one window, gen-0 + local (k2_scan's LDS capacity)
+static_assert(NMAX == 8 * STG_NT, "stage slices");
+// a staged rank's position in the stage arrays and cpt (k2_sdef's thread r / 8 loads it as its (r % 8)-th)
+__device__ __forceinline__ uint32_t stg_pos(uint32_t r) { return (r & 7u) * STG_NT + (r >> 3); }
+// a rank's word in k2_sdef's per-rank LDS arrays: one pad word per 64, so a wave's 8-strided accesses
+// (lane l, rank 8l + q) fall in 64 different banks
+__device__ __forceinline__ uint32_t lds_pad(uint32_t r) { return r + (r >> 6); }
+constexpr int NMAX_PAD = NMAX + NMAX / 64;
 constexpr int LMAX = NMAX - WCAP;        // local records of one window
 constexpr int SLOTG = WCAP + LMAX;       // k2_pa's slot-role threads (single engine): gen-0 slots, then local
 static_assert(LCAP < (1 << 24) && WTOT < (1 << 24), "wpar packs a record index in 24 bits");
@@ -478,11 +485,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     if (stg && vs && srank < (uint32_t)NMAX) {  // the record at its rank (k2_sdef logs it and resolves its uid)
       Stg st;
       st.key = loc ? (rel << 32) : spk;
-      st.ctx = sctx;
       st.cnt = loc ? ldd.y : (ncr | (ninl0 << 16));
       st.par = loc ? ldd.w : 0u;
-      st.loc = loc ? 1u : 0u;
-      M.stage[srank] = st;  // (one stage: df_sdef(n - 1) is done with it before k2_pa(n + 1) writes)
+      M.stage[stg_pos(srank)] = st;  // (one stage: df_sdef(n - 1) is done with it before k2_pa(n + 1) writes)
+      M.stx[stg_pos(srank)] = sctx;
       M.rmap[s] = srank;     // (df_sdef: a local record's parent's rank)
     } else if (vs) {
       const uint64_t rk = K0 + si.x;
@@ -521,7 +527,8 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
           if ((e.kind & 0xffu) == K_FWD_UP) {  // leaf: dispatched inside its window (or never), not queued
             if (stg) {
               if (rel < ilim && srank < (uint32_t)NMAX) {  // (k2_sdef logs it after its group)
-                M.sleaf[(uint64_t)srank * M.maxc + ii] = make_uint2(e.ctx, j);
+                if (ii) M.sleaf[(uint64_t)srank * M.maxc + ii] = make_uint2(e.ctx, j);
+                else M.slf0[stg_pos(srank)] = make_uint2(e.ctx, j);
                 ii++;
               }
             } else if (rel < ilim) {
@@ -604,7 +611,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
           if (ge[q].ts != TOMB && (u & PROV)) {
             const uint32_t tag = (u >> 30) & 1u;
             if (tag != (uint32_t)(c_wn & 1)) atomicOr(M.error, 256u);
-            ge[q].uid = xw_uid0 + M.cpt[(uint64_t)tag * NMAX + ((u & 0x3fffffffu) >> 8) % NMAX] + (u & 0xffu);
+            ge[q].uid = xw_uid0 + M.cpt[(uint64_t)tag * NMAX + stg_pos(((u & 0x3fffffffu) >> 8) % NMAX)] + (u & 0xffu);
             M.ev_uid[0][i] = ge[q].uid;
           }
         }
@@ -1876,9 +1883,11 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
 #endif
   // DF: blocks 1 .. NSDEF do the last window's dispatch accounting (k2_pa staged it) beside this window's
   // ranking
-  if (DF && blockIdx.x >= 1 && blockIdx.x <= (uint32_t)NSDEF) {
-    if (M.sdef_fold) df_sdef<NT>(M, C, blockIdx.x - 1, NSDEF);
-    return;
+  if constexpr (DF) {
+    if (blockIdx.x >= 1 && blockIdx.x <= (uint32_t)NSDEF) {
+      if (M.sdef_fold) df_sdef<NT>(M, C, blockIdx.x - 1, NSDEF);
+      return;
+    }
   }
   uint32_t c_done = 0, c_mode = 0, W, c_fr = 0, go = 3;
   uint64_t lim, wn;
@@ -2144,13 +2153,19 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 template <int NT>
 __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   const uint32_t sf = C.sflag;
+  BLK_T0();
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t c_win = C.rk_win - 1;  // (diagnostic build: phase marks 16..22 in the sampled window)
+#endif
   WInfo wa[4];  // (all four: loaded with the flag, picked by it)
 #pragma unroll
   for (int k = 0; k < 4; k++) wa[k] = C.winfo[k];
+  static_assert(NT == (int)STG_NT, "k2_sdef's rank slices are the stage layout's");
   constexpr int RPT = NMAX / NT;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // per record: key, counts, parent (a local record's key has uid 0: gen-0 uids start at 4; its context is
-  // read again only when logging) — one stage (the window k2_pa staged), loaded with the run control
+  // read only when logging) — one stage (the window k2_pa staged), loaded with the run control; record
+  // 8 tid + q is at q * NT + tid (stg_pos), so each load of a wave reads 1 KB of consecutive entries
   uint64_t ek[RPT];
   uint32_t ec[RPT], ep[RPT];
   uint32_t prev_rel = 0;
@@ -2158,11 +2173,12 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     const Stg *st = M.stage;
 #pragma unroll
     for (int q = 0; q < RPT; q++) {  // (NMAX entries: in range, ignored past N)
-      ek[q] = st[tid * RPT + q].key;
-      ec[q] = st[tid * RPT + q].cnt;
-      ep[q] = st[tid * RPT + q].par;
+      const Stg x = st[q * NT + tid];
+      ek[q] = x.key;
+      ec[q] = x.cnt;
+      ep[q] = x.par;
     }
-    if (tid > 0) prev_rel = (uint32_t)(st[tid * RPT - 1].key >> 32);
+    if (tid > 0) prev_rel = (uint32_t)(st[(RPT - 1) * NT + tid - 1].key >> 32);
   }
   if (!(sf & 1u)) return;
   const uint32_t wi = (sf >> 1) & 3u, pn = wi & 1u;  // window n & 3, its parity (its child prefixes' buffer)
@@ -2172,10 +2188,10 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   for (int k = 1; k < 4; k++)
     if ((uint32_t)k == wi) w = wa[k], uidq = wa[k - 1].uid0;
   const uint32_t N = w.N;
-  __shared__ uint32_t s_cp[NMAX];   // child prefix by rank
-  __shared__ uint32_t s_ip[NMAX];   // inline prefix by rank
-  __shared__ uint32_t s_grp[NMAX];  // same-ts group of each rank
-  __shared__ uint32_t s_gs[NMAX];   // start rank of each group
+  __shared__ uint32_t s_cp[NMAX_PAD];   // child prefix by rank (lds_pad)
+  __shared__ uint32_t s_ip[NMAX_PAD];   // inline prefix by rank
+  __shared__ uint32_t s_grp[NMAX_PAD];  // same-ts group of each rank
+  __shared__ uint32_t s_gs[NMAX_PAD];   // start rank of each group (by group: lds_pad)
   __shared__ uint64_t wsum[NT / 64];
   if ((uint32_t)(tid * RPT) > N) prev_rel = 0;
   uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
@@ -2192,6 +2208,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
       }
     }
   }
+  BLK_MARK(16, c_win);  // the records arrived (the first scan pass used them)
   uint64_t inc = sum;
   for (int o = 1; o < 64; o <<= 1) {
     const uint64_t x = __shfl_up(inc, o);
@@ -2207,6 +2224,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   }
   const uint64_t ex = off + inc - sum;
   const uint32_t tinl = (uint32_t)((tot >> 21) & 0x1fffffu), ng = (uint32_t)(tot >> 42);
+  BLK_MARK(18, c_win);  // the block scan
   {
     uint32_t pr = prev_rel, bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu),
              bh = (uint32_t)(ex >> 42);
@@ -2218,11 +2236,11 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
         const uint32_t hd = r == 0 || rel != pr;
         pr = rel;
         bh += hd;
-        s_cp[r] = bc;
-        s_ip[r] = bi;
-        s_grp[r] = bh - 1;
-        if (hd) s_gs[bh - 1] = r;
-        M.cpt[(uint64_t)pn * NMAX + r] = bc;  // (kept: window n's children resolve through it)
+        s_cp[lds_pad(r)] = bc;
+        s_ip[lds_pad(r)] = bi;
+        s_grp[lds_pad(r)] = bh - 1;
+        if (hd) s_gs[lds_pad(bh - 1)] = r;
+        if (!(M.sdef_abl & 4u)) M.cpt[(uint64_t)pn * NMAX + q * NT + tid] = bc;  // (stg_pos(r): window n's children resolve through it)
         bc += ec[q] & 0xffffu;
         bi += ec[q] >> 16;
       }
@@ -2238,19 +2256,20 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     const uint32_t r = tid * RPT + q;
     look[q] = 0;
     lf0[q] = make_uint2(0, 0);
-    if (r < N) {
+    if (r < N && !(M.sdef_abl & 1u)) {
       const uint32_t u = (uint32_t)ek[q];
       if (((uint32_t)ek[q] == 0u)) look[q] = rm[(ep[q] & 0xffffffu) % WTOT];            // the parent's rank
-      else if (u & PROV) look[q] = cq[((u & 0x3fffffffu) >> 8) % NMAX];   // window n-1's child prefix
-      if (ec[q] >> 16) lf0[q] = M.sleaf[(uint64_t)r * M.maxc];
+      else if (u & PROV) look[q] = cq[stg_pos(((u & 0x3fffffffu) >> 8) % NMAX)];   // window n-1's child prefix
+      if (ec[q] >> 16) lf0[q] = M.slf0[q * NT + tid];
     }
   }
   __syncthreads();
+  BLK_MARK(20, c_win);  // per-rank arrays written, lookups issued, barrier
   uint64_t digest = 0;
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
-    if (r >= N) continue;
+    if (r >= N || (M.sdef_abl & 2u)) continue;
     const uint32_t rel = (uint32_t)(ek[q] >> 32);
     const uint64_t t = w.tmin + rel;
     uint32_t uid = (uint32_t)ek[q];
@@ -2260,24 +2279,24 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
         atomicOr(M.error, 256u);
         rp = 0;
       }
-      uid = w.uid0 + s_cp[rp] + (ep[q] >> 24);
+      uid = w.uid0 + s_cp[lds_pad(rp)] + (ep[q] >> 24);
     } else if (uid & PROV) {  // a child of window n - 1
       if (((uid >> 30) & 1u) != (pn ^ 1u)) atomicOr(M.error, 256u);
       uid = uidq + look[q] + (uid & 0xffu);
     }
-    const uint32_t g = s_grp[r];
-    const uint32_t first = s_gs[g];
-    const uint32_t last = (g + 1 < ng ? s_gs[g + 1] : N) - 1;
-    const uint64_t rk = w.K0 + r + (tinl ? s_ip[first] : 0u);
+    const uint32_t g = s_grp[lds_pad(r)];
+    const uint32_t first = s_gs[lds_pad(g)];
+    const uint32_t last = (g + 1 < ng ? s_gs[lds_pad(g + 1)] : N) - 1;
+    const uint64_t rk = w.K0 + r + (tinl ? s_ip[lds_pad(first)] : 0u);
     digest += digest_term(rk, t, uid);
     if (rk < M.log_cap) {
       M.log_ts[rk] = t;
       M.log_uid[rk] = uid;
-      M.log_ctx[rk] = M.stage[r].ctx;
+      M.log_ctx[rk] = M.stx[q * NT + tid];
     }
     const uint32_t ni = min(ec[q] >> 16, M.maxc);  // (bounded: a staged record's leaves fit its row)
     const uint2 *lf = M.sleaf + (uint64_t)r * M.maxc;
-    const uint32_t cpr = s_cp[r], ipr = s_ip[r];
+    const uint32_t cpr = s_cp[lds_pad(r)], ipr = s_ip[lds_pad(r)];
     for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
       const uint2 l = k ? lf[k] : lf0[q];
       const uint64_t lk = w.K0 + last + 1 + ipr + k;
@@ -2292,6 +2311,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     if (r == N - 1) C.last_ts = t;
   }
   digest = wave_sum64(digest);
+  BLK_MARK(22, c_win);  // resolve, log, digest (lookups and leaves arrived)
   if (lane == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
   __syncthreads();  // (every lookup of the rank accumulators is done: clear them for window n + 2)
   for (uint32_t i = tid; i < w.W; i += NT) M.wrank[(uint64_t)pn * WTOT + i] = 0;
@@ -2395,7 +2415,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       const uint32_t i = tid + q * SCAN_THREADS;
       if (i < W && (u & PROV)) {
         if (((u >> 30) & 1u) != (uint32_t)((wn + 1) & 1)) atomicOr(M.error, 256u);
-        gk[q] = (gk[q] & ~0xffffffffull) | (uint32_t)(uq + cq[((u & 0x3fffffffu) >> 8) % NMAX] + (u & 0xffu));
+        gk[q] = (gk[q] & ~0xffffffffull) | (uint32_t)(uq + cq[stg_pos(((u & 0x3fffffffu) >> 8) % NMAX)] + (u & 0xffu));
       }
     }
   }
@@ -2708,7 +2728,7 @@ __global__ __launch_bounds__(256) void k_xlate(const P2PDev M) {
     const uint32_t u = M.ev_uid[0][i];
     if (M.ev_ts[0][i] != TOMB && (u & PROV)) {
       if (((u >> 30) & 1u) != (uint32_t)(wq & 1)) atomicOr(M.error, 256u);
-      M.ev_uid[0][i] = uq + cq[((u & 0x3fffffffu) >> 8) % NMAX] + (u & 0xffu);
+      M.ev_uid[0][i] = uq + cq[stg_pos(((u & 0x3fffffffu) >> 8) % NMAX)] + (u & 0xffu);
     }
   }
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) {
@@ -2716,7 +2736,7 @@ __global__ __launch_bounds__(256) void k_xlate(const P2PDev M) {
     const uint32_t u = (uint32_t)k;
     if (u & PROV) {
       if (((u >> 30) & 1u) != (uint32_t)(wq & 1)) atomicOr(M.error, 256u);
-      M.wkey[i] = (k & ~0xffffffffull) | (uint32_t)(uq + cq[((u & 0x3fffffffu) >> 8) % NMAX] + (u & 0xffu));
+      M.wkey[i] = (k & ~0xffffffffull) | (uint32_t)(uq + cq[stg_pos(((u & 0x3fffffffu) >> 8) % NMAX)] + (u & 0xffu));
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) C.pdf = 0;
