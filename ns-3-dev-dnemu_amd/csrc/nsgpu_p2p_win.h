@@ -42,6 +42,16 @@ constexpr int LCAP = NHB * LR + NHUB * LRH;
 constexpr int WTOT = WCAP + LCAP;        // record index space (gen-0 slots + local regions)
 constexpr int NMAX = 8192;               // records of one window, gen-0 + local (k2_scan's LDS capacity)
 static_assert(NMAX == 8 * STG_NT, "stage slices");
+// The run control through the vector memory path.  A kernel's first reads of Ctl come from lines another XCD
+// wrote (one memory trip).  As scalar loads they hold back every later scalar load (a scalar wait cannot
+// single out one load), so the kernel-argument pointers of the slot loads wait for the run control and the
+// slot loads go out one trip late; as vector loads they are in flight together.
+__device__ __forceinline__ Ctl *vec_ctl(Ctl *p) {
+  typedef __attribute__((address_space(1))) Ctl GCtl;
+  GCtl *g = (GCtl *)p;
+  asm volatile("" : "+v"(g));
+  return (Ctl *)g;  // (a global pointer: global, not flat, loads)
+}
 // a staged rank's position in the stage arrays and cpt (k2_sdef's thread r / 8 loads it as its (r % 8)-th)
 __device__ __forceinline__ uint32_t stg_pos(uint32_t r) { return (r & 7u) * STG_NT + (r >> 3); }
 // a rank's word in k2_sdef's per-rank LDS arrays: one pad word per 64, so a wave's 8-strided accesses
@@ -357,7 +367,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   static_assert(!DF || WIDE, "deferred windows are the wide engine's");
   PH_BEGIN();
   BLK_T0();
-  Ctl &C = *M.C;
+  Ctl &C = *vec_ctl(M.C);
 #ifdef NSGPU_PHASE_PROF
   const uint64_t c_win = C.windows;
 #endif
@@ -382,11 +392,19 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const uint64_t c_span_t = WIDE ? C.span_t : 0;
   const uint32_t c_pdf = DF ? C.pdf : 0u;
   const uint64_t c_wn = DF ? C.windows : 0;  // (this window's index: the last one is c_wn - 1)
-  const uint32_t xw_uid0 = DF ? C.winfo[(c_wn + 2) & 3].uid0 : 0u;  // (window c_wn - 2: the pool's provisional uids)
+  uint32_t xw_u[4] = {0, 0, 0, 0};  // (window c_wn - 2's uid base: the pool's provisional uids; all four
+  if (DF) {                          //  loaded with the run control, picked once C.windows is back)
+#pragma unroll
+    for (int k = 0; k < 4; k++) xw_u[k] = C.winfo[k].uid0;
+  }
   uint64_t spk = 0;
   uint4 si = make_uint4(0, 0, 0, 0);
   uint32_t ncr = 0, sctx = 0;
-  Ev ce[PFC];
+  // the first PFC children, field by field (an Ev array here was kept in scratch, and each child's scratch
+  // store waited for its loads: one memory trip per child)
+  uint64_t cts[PFC];
+  uint32_t cctx[PFC], ckind[PFC], ca[PFC];
+  uint4 cpk[PFC];
   constexpr int NPEND = 4;  // node-table claims a thread keeps pending (PFC children, or PPT pool entries)
   static_assert(PFC <= NPEND, "pending claims");
   NtClaim pend[NPEND];
@@ -407,20 +425,21 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     si = M.sinfo[s];
     ncr = M.nchild[s];
     sctx = M.pwctx[s];
-    if (DF) {
-      if (g < (uint64_t)WCAP) {
-        rk2[0] = M.wrank[g];
-        rk2[1] = M.wrank[WTOT + g];
-        ninl0 = M.ninl[g];
-      } else {
-        rk2[0] = M.lrank[g - WCAP];
-        rk2[1] = M.lrank[LMAX + g - WCAP];
-      }
+    if (DF) {  // (branch-free: a branch here made the wave wait for these before issuing the child loads)
+      const bool gz = g < (uint64_t)WCAP;
+      const uint32_t *wr = gz ? M.wrank + g : M.lrank + (g - WCAP);
+      rk2[0] = wr[0];
+      rk2[1] = wr[gz ? (uint32_t)WTOT : (uint32_t)LMAX];
+      ninl0 = M.ninl[gz ? (uint32_t)g : 0u];  // (a local record's is not used)
     }
 #pragma unroll
-    for (int j = 0; j < PFC; j++) {
-      const uint32_t sl = s * M.maxc + j;
-      if ((uint32_t)j < M.maxc) ce[j] = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
+    for (int j = 0; j < PFC; j++) {  // (a child index past maxc loads the slot's last one: in range, ignored)
+      const uint32_t sl = s * M.maxc + min((uint32_t)j, M.maxc - 1u);
+      cts[j] = M.ch_ts[sl];
+      cctx[j] = M.ch_ctx[sl];
+      ckind[j] = M.ch_kind[sl];
+      ca[j] = M.ch_a[sl];
+      cpk[j] = *(const uint4 *)&M.ch_pkt[sl];
     }
   }
   if (DIST) {
@@ -479,7 +498,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     const uint64_t rel = (stg && loc) ? (uint64_t)ldd.z : spk >> 32;
     const uint64_t t = c_ptmin + rel;
     const uint32_t pn = (uint32_t)((c_wn - 1) & 1);  // (DF: the last window's parity)
-    const uint32_t srank = rk2[pn];
+    const uint32_t srank = pn ? rk2[1] : rk2[0];
     BLK_MARK(34, c_win);  // bound, publish_bound
     if (stg && vs && srank >= (uint32_t)NMAX) atomicOr(M.error, 256u);
     if (stg && vs && srank < (uint32_t)NMAX) {  // the record at its rank (k2_sdef logs it and resolves its uid)
@@ -518,7 +537,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
         bool valid = false;
         if (has) {
           if (j0 == 0) {
-            e = ce[q];
+            e = Ev{cts[q], 0, cctx[q], ckind[q], ca[q], Pkt{cpk[q].x, cpk[q].y, cpk[q].z, cpk[q].w}};
           } else {
             const uint32_t sl = s * M.maxc + j;
             e = Ev{M.ch_ts[sl], 0, M.ch_ctx[sl], M.ch_kind[sl], M.ch_a[sl], M.ch_pkt[sl]};
@@ -604,6 +623,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
         if (i < P) ge[q] = Ev{M.ev_ts[0][i], M.ev_uid[0][i], 0, M.ev_kind[0][i], 0, Pkt{0, 0, 0, 0}};
       }
       if (DF) {  // children the window before the last one parked: their uids resolve now (k2_sdef ran for it)
+        uint32_t xw_uid0 = xw_u[0];
+#pragma unroll
+        for (int k = 1; k < 4; k++)
+          if ((uint64_t)k == ((c_wn + 2) & 3)) xw_uid0 = xw_u[k];
 #pragma unroll
         for (int q = 0; q < PPT; q++) {
           const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
