@@ -1737,7 +1737,7 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   __shared__ uint64_t lds64[(WIDE ? K2_LDS_WORDS_W : K2_LDS_WORDS) / 2];
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds64);
   PH_BEGIN();
-  Ctl &C = *M.C;
+  Ctl &C = *vec_ctl(M.C);
   BLK_T0();
 #ifdef NSGPU_PHASE_PROF
   const uint64_t c_win = C.windows;
