@@ -96,12 +96,13 @@ struct WInfo {
   uint32_t uid0, N, W, Lt;  // the uid its first child takes; records (gen-0 W + local Lt)
 };
 
-// A staged record of a deferred window, at its rank: key (rel ts << 32 | its uid, which may be provisional;
-// a local record's uid is its parent's child prefix + j, resolved by k2_sdef, and its key's uid is 0), child
-// counts (n | inline << 16), and for a local record its parent (wpar: record | child index << 24).  Its
-// context and first inline leaf are kept beside it (stx, slf0).  Stage arrays (and the child prefixes cpt) are
-// indexed by stg_pos(rank): k2_sdef's thread t owns the 8 consecutive ranks 8t..8t+7 and loads its q-th one
-// from q * 1024 + t, so every load and store of a wave is coalesced.
+// A staged record of a deferred window, at its rank: key (rel ts << 32 | its uid — resolved at staging when it
+// was provisional; a local record's key has uid 0: its uid is its parent's child prefix + j, resolved by
+// k2_sdef), counts (children | inline children << 9 | the record's dense index << 18), and for a local record
+// its parent (the parent's dense index | child index << 24), for a gen-0 record its first inline leaf (its
+// context | child index << 24; a local record has none).  Its context is kept beside it (stx).  Stage arrays (and the child prefixes cpt) are indexed by stg_pos(rank): k2_sdef's
+// thread t owns the 8 consecutive ranks 8t..8t+7 and loads its q-th one from q * 1024 + t, so every load and
+// store of a wave is coalesced.
 struct Stg {
   uint64_t key;
   uint32_t cnt, par;
@@ -283,12 +284,10 @@ struct P2PDev {
   // ---- deferred windows (wrank / lrank are then 2 x WTOT / 2 x LMAX: by window parity) ----
   struct Stg *stage;      // [NMAX] a window's records by stg_pos(rank) (k2_pa stages, k2_sdef reads)
   uint32_t *stx;          // [NMAX] their contexts (stg_pos)
-  uint2 *slf0;            // [NMAX] their first inline DoForwardUp leaf: (context, child index) (stg_pos)
-  uint2 *sleaf;           // [NMAX][maxc] their further inline leaves (by rank, entry 0 unused)
+  uint2 *sleaf;           // [NMAX][maxc] their further inline leaves: (context, child index) (by rank, entry 0 unused)
   uint32_t *cpt;          // [2][NMAX] child prefix by rank (k2_sdef): provisional uids resolve through it
-  uint32_t *rmap;         // [WTOT] the staged window's record -> its rank (k2_pa)
+  uint32_t *ldpd;         // [LMAX] the dense list's parents as dense indices | child index << 24 (k2_rank -> k2_pa)
   uint32_t sdef_fold;     // df_sdef runs as k2_rank's block 1 (1) or as its own kernel k2_sdef (0)
-  uint32_t sdef_abl;      // (diagnostic ablation, NSGPU_P2P_SDEF_ABL: 1 no lookups, 2 no resolve pass, 4 no prefix stores)
 };
 
 // ---------------- wave / block helpers ----------------
@@ -2013,13 +2012,10 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.stage, NMAX));
     TRY(dalloc(h, &M.sleaf, (size_t)NMAX * M.maxc));
     TRY(dalloc(h, &M.stx, NMAX));
-    TRY(dalloc(h, &M.slf0, NMAX));
     TRY(dalloc(h, &M.cpt, 2 * (size_t)NMAX));
-    TRY(dalloc(h, &M.rmap, WTOT));
+    TRY(dalloc(h, &M.ldpd, LMAX));
     const char *e = getenv("NSGPU_P2P_SDEF_KERNEL");  // (diagnostic: the accounting as its own kernel)
     M.sdef_fold = (e && e[0] == '1') ? 0u : 1u;
-    const char *ab = getenv("NSGPU_P2P_SDEF_ABL");
-    M.sdef_abl = ab ? (uint32_t)atoi(ab) : 0u;
   }
   // (k2_pa loads lrec / ldat entries speculatively and follows their record index: zeroed, every entry
   // stays < WTOT; the deferred pipeline's arrays start zeroed too, so a stale entry is always in range)
@@ -2030,9 +2026,8 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     zok = hipMemset(M.stage, 0, (size_t)NMAX * sizeof(Stg)) == hipSuccess &&
           hipMemset(M.sleaf, 0, (size_t)NMAX * M.maxc * sizeof(uint2)) == hipSuccess &&
           hipMemset(M.stx, 0, (size_t)NMAX * sizeof(uint32_t)) == hipSuccess &&
-          hipMemset(M.slf0, 0, (size_t)NMAX * sizeof(uint2)) == hipSuccess &&
           hipMemset(M.cpt, 0, 2 * (size_t)NMAX * sizeof(uint32_t)) == hipSuccess &&
-          hipMemset(M.rmap, 0, (size_t)WTOT * sizeof(uint32_t)) == hipSuccess;
+          hipMemset(M.ldpd, 0, (size_t)LMAX * sizeof(uint32_t)) == hipSuccess;
   if (!zok) {
     nsgpu_p2p_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_p2p_create: hipMemset failed");
@@ -2376,7 +2371,7 @@ bool df_usable(const nsgpu_p2p *h) {
     const char *e = getenv("NSGPU_P2P_NODEFER");
     return e && e[0] == '1';
   }();
-  return h->M.wide && !h->M.dist && !h->M.trace && h->M.maxc <= PROV_MAXC && !off;
+  return h->M.wide && !h->M.dist && !h->M.trace && h->M.maxc <= PROV_MAXC && h->M.n_nodes < (1u << 24) && !off;
 }
 // When the deferred pipeline paused itself (a sorted run, a compaction, a host closure) after window n's
 // bookkeeping: window n's dispatch accounting from its records (k2_scan<true, true>: sinfo for the next

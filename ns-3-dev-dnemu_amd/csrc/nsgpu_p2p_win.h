@@ -414,8 +414,11 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   // record indices from earlier windows past C.plt: loaded speculatively, always in range).  DF: the dense
   // local entry ldat (record, child counts, rel ts, parent) instead, and both parities' rank accumulators
   uint4 ldd = make_uint4((uint32_t)g, 0, 0, 0);
-  uint32_t rk2[2] = {0, 0}, ninl0 = 0;
-  if (DF && WIDE && g >= (uint64_t)WCAP && slot_role) ldd = M.ldat[g - WCAP];
+  uint32_t rk2[2] = {0, 0}, ninl0 = 0, lpd = 0;
+  if (DF && WIDE && g >= (uint64_t)WCAP && slot_role) {
+    ldd = M.ldat[g - WCAP];
+    lpd = M.ldpd[g - WCAP];  // (its parent as a dense index: k2_sdef finds the parent's rank in LDS)
+  }
   // (a speculative entry past the last window's records is followed too: clamped into the record space)
   const uint32_t rec =
       (WIDE && g >= (uint64_t)WCAP && slot_role) ? min(DF ? ldd.x : M.lrec[g - WCAP], (uint32_t)WTOT - 1u) : (uint32_t)g;
@@ -489,6 +492,11 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const uint32_t pW = c_pvalid ? c_pW : 0;
   PH_MARK(0);
   uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull, digest = 0;
+  uint32_t xw_uid0 = xw_u[0];  // (window c_wn - 2's uid base: its provisional uids resolve in this kernel)
+#pragma unroll
+  for (int k = 1; k < 4; k++)
+    if ((uint64_t)k == ((c_wn + 2) & 3)) xw_uid0 = xw_u[k];
+  Stg st_pending{0, 0, 0};
   if (slot_block) {
     // ---- record `rec` of the last window: dispatch rank (log, digest), inline children, children -> pending
     const bool vs = slot_role && (g < (uint64_t)WCAP ? g < pW : (c_pvalid && g - WCAP < c_plt));
@@ -501,14 +509,21 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     const uint32_t srank = pn ? rk2[1] : rk2[0];
     BLK_MARK(34, c_win);  // bound, publish_bound
     if (stg && vs && srank >= (uint32_t)NMAX) atomicOr(M.error, 256u);
-    if (stg && vs && srank < (uint32_t)NMAX) {  // the record at its rank (k2_sdef logs it and resolves its uid)
-      Stg st;
-      st.key = loc ? (rel << 32) : spk;
-      st.cnt = loc ? ldd.y : (ncr | (ninl0 << 16));
-      st.par = loc ? ldd.w : 0u;
-      M.stage[stg_pos(srank)] = st;  // (one stage: df_sdef(n - 1) is done with it before k2_pa(n + 1) writes)
+    const bool sw = stg && vs && srank < (uint32_t)NMAX;  // the record is staged at its rank (k2_sdef logs it)
+    if (sw) {
+      // a provisional uid (a child of the window before) resolves now: k2_sdef ran for that window.  The
+      // prefix's load is issued here and the stage is written after the children, so its trip overlaps theirs
+      uint32_t ku = (uint32_t)spk;
+      if (!loc && (ku & PROV)) {
+        const uint32_t tag = (ku >> 30) & 1u;
+        if (tag != (uint32_t)(c_wn & 1)) atomicOr(M.error, 256u);
+        ku = xw_uid0 + M.cpt[(uint64_t)tag * NMAX + stg_pos(((ku & 0x3fffffffu) >> 8) % NMAX)] + (ku & 0xffu);
+      }
+      const uint32_t cc = loc ? ldd.y : (ncr | (ninl0 << 16));
+      const uint32_t dn = loc ? pW + (uint32_t)(g - WCAP) : (uint32_t)g;  // (its dense index)
+      st_pending = Stg{loc ? (rel << 32) : ((spk >> 32) << 32 | ku), (cc & 0x1ffu) | ((cc >> 16) << 9) | (dn << 18),
+                       loc ? lpd : 0u};
       M.stx[stg_pos(srank)] = sctx;
-      M.rmap[s] = srank;     // (df_sdef: a local record's parent's rank)
     } else if (vs) {
       const uint64_t rk = K0 + si.x;
       digest += digest_term(rk, t, (uint32_t)spk);
@@ -547,7 +562,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
             if (stg) {
               if (rel < ilim && srank < (uint32_t)NMAX) {  // (k2_sdef logs it after its group)
                 if (ii) M.sleaf[(uint64_t)srank * M.maxc + ii] = make_uint2(e.ctx, j);
-                else M.slf0[stg_pos(srank)] = make_uint2(e.ctx, j);
+                else st_pending.par = e.ctx | (j << 24);  // (a gen-0 record's: local records have no leaves)
                 ii++;
               }
             } else if (rel < ilim) {
@@ -582,6 +597,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       }
       BLK_MARK(40, c_win);  // writes (node-table atomics)
     }
+    if (sw) M.stage[stg_pos(srank)] = st_pending;  // (one stage: df_sdef(n - 1) was done with it before k2_pa(n + 1))
   } else if (DIST && remote_role) {
     // ---- remote events the last X2 brought (partitioned): record idx % capx from rank idx / capx
     if (partition) {
@@ -623,10 +639,6 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
         if (i < P) ge[q] = Ev{M.ev_ts[0][i], M.ev_uid[0][i], 0, M.ev_kind[0][i], 0, Pkt{0, 0, 0, 0}};
       }
       if (DF) {  // children the window before the last one parked: their uids resolve now (k2_sdef ran for it)
-        uint32_t xw_uid0 = xw_u[0];
-#pragma unroll
-        for (int k = 1; k < 4; k++)
-          if ((uint64_t)k == ((c_wn + 2) & 3)) xw_uid0 = xw_u[k];
 #pragma unroll
         for (int q = 0; q < PPT; q++) {
           const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
@@ -1982,7 +1994,9 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
           const uint32_t r = dense_rec(W + cy, W, pre);
           w = M.lkw[r - LBASE];
           if (ti == 0) {  // the dense list k2_scan (ldat) and the next k2_pa (lrec) read; the local's context
-            M.ldat[cy] = make_uint4(r, M.nchild[r] | (M.ninl[r] << 16), (uint32_t)(w.x >> 32), M.wpar[r]);
+            const uint32_t wp = M.wpar[r];
+            M.ldat[cy] = make_uint4(r, M.nchild[r] | (M.ninl[r] << 16), (uint32_t)(w.x >> 32), wp);
+            if (DF) M.ldpd[cy] = dense_of(wp & 0xffffffu, W, pre) | (wp & 0xff000000u);
             M.lrec[cy] = r;
             M.pwctx[r] = M.wctx[r];
           }
@@ -2163,32 +2177,27 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 // ---- k2_sdef: a deferred window's dispatch accounting (DF pipeline; one block) ----
 // Window n's records, staged in rank order by the next k2_pa: exclusive scans of (children, inline children,
 // same-ts group heads) give each record its dispatch rank (K0 + rank + the inline leaves of earlier ts groups)
-// and child prefix; a record's own uid resolves (a provisional one through window n-1's prefixes, a local
-// record's through its parent's rank and this window's prefixes); the log and digest get every record and
-// leaf; the child prefixes are kept (cpt) for the provisional uids of window n's children.  Afterwards the
-// window's rank accumulators are cleared (their parity is window n + 2's).
+// and child prefix; a local record's uid resolves through its parent's rank and this window's prefixes (k2_pa
+// resolved the provisional ones at staging); the log and digest get every record and leaf; the child prefixes
+// are kept (cpt) for the provisional uids of window n's children.  Afterwards the window's rank accumulators
+// are cleared (their parity is window n + 2's).
 // One block of NT threads (k2_rank<true>'s block 1, or the k2_sdef kernel).  Every record is loaded once, into
-// registers (RPT consecutive ranks a thread); the scan's per-rank results go to LDS (child / inline prefixes,
-// the group of each rank, group starts); each thread then resolves, logs and digests its own records with
-// their lookups (a local record's parent's rank through rmap, a provisional uid through window n-1's
-// prefixes, the inline leaves) issued together.  The staged window's parity is known from k2_handle's
-// snapshot (rk_win), so the records are loaded in the same trip as the flag.
+// registers (RPT consecutive ranks a thread), in the same memory trip as the run control; the scan's per-rank
+// results go to LDS (child / inline prefixes, the group of each rank, group starts, and the rank of each dense
+// index, through which a local record finds its parent's), so after the loads the kernel reads LDS only.
 template <int NT>
 __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   const uint32_t sf = C.sflag;
   BLK_T0();
-#ifdef NSGPU_PHASE_PROF
-  const uint64_t c_win = C.rk_win - 1;  // (diagnostic build: phase marks 16..22 in the sampled window)
-#endif
-  WInfo wa[4];  // (all four: loaded with the flag, picked by it)
-#pragma unroll
-  for (int k = 0; k < 4; k++) wa[k] = C.winfo[k];
   static_assert(NT == (int)STG_NT, "k2_sdef's rank slices are the stage layout's");
   constexpr int RPT = NMAX / NT;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // per record: key, counts, parent (a local record's key has uid 0: gen-0 uids start at 4; its context is
-  // read only when logging) — one stage (the window k2_pa staged), loaded with the run control; record
-  // 8 tid + q is at q * NT + tid (stg_pos), so each load of a wave reads 1 KB of consecutive entries
+  WInfo wa[4];  // (all four: loaded with the flag, picked by it)
+#pragma unroll
+  for (int k = 0; k < 4; k++) wa[k] = C.winfo[k];
+  // per record: key, counts, parent or first inline leaf (a local record's key has uid 0: gen-0 uids start
+  // at 4) — one stage (the window k2_pa staged), loaded with the run control; record 8 tid + q is at
+  // q * NT + tid (stg_pos), so each load of a wave reads consecutive entries
   uint64_t ek[RPT];
   uint32_t ec[RPT], ep[RPT];
   uint32_t prev_rel = 0;
@@ -2203,18 +2212,23 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     }
     if (tid > 0) prev_rel = (uint32_t)(st[(RPT - 1) * NT + tid - 1].key >> 32);
   }
+  // (the window records in registers before the flag's test: otherwise the compiler sinks their loads past it,
+  // a second trip)
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    asm volatile("" ::"s"(wa[k].K0), "s"(wa[k].tmin), "s"(wa[k].uid0), "s"(wa[k].N), "s"(wa[k].W), "s"(wa[k].Lt));
   if (!(sf & 1u)) return;
   const uint32_t wi = (sf >> 1) & 3u, pn = wi & 1u;  // window n & 3, its parity (its child prefixes' buffer)
   WInfo w = wa[0];
-  uint32_t uidq = wa[3].uid0;  // window n - 1's uid base
 #pragma unroll
   for (int k = 1; k < 4; k++)
-    if ((uint32_t)k == wi) w = wa[k], uidq = wa[k - 1].uid0;
+    if ((uint32_t)k == wi) w = wa[k];
   const uint32_t N = w.N;
   __shared__ uint32_t s_cp[NMAX_PAD];   // child prefix by rank (lds_pad)
   __shared__ uint32_t s_ip[NMAX_PAD];   // inline prefix by rank
   __shared__ uint32_t s_grp[NMAX_PAD];  // same-ts group of each rank
   __shared__ uint32_t s_gs[NMAX_PAD];   // start rank of each group (by group: lds_pad)
+  __shared__ uint16_t s_rk[NMAX];       // rank of each dense index (local records' parents)
   __shared__ uint64_t wsum[NT / 64];
   if ((uint32_t)(tid * RPT) > N) prev_rel = 0;
   uint64_t sum = 0;  // packed (children, inline children, group heads), 21 bits each
@@ -2227,11 +2241,10 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
         const uint32_t rel = (uint32_t)(ek[q] >> 32);
         const uint32_t hd = r == 0 || rel != pr;
         pr = rel;
-        sum += (uint64_t)(ec[q] & 0xffffu) | ((uint64_t)(ec[q] >> 16) << 21) | ((uint64_t)hd << 42);
+        sum += (uint64_t)(ec[q] & 0x1ffu) | ((uint64_t)((ec[q] >> 9) & 0x1ffu) << 21) | ((uint64_t)hd << 42);
       }
     }
   }
-  BLK_MARK(16, c_win);  // the records arrived (the first scan pass used them)
   uint64_t inc = sum;
   for (int o = 1; o < 64; o <<= 1) {
     const uint64_t x = __shfl_up(inc, o);
@@ -2247,7 +2260,6 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   }
   const uint64_t ex = off + inc - sum;
   const uint32_t tinl = (uint32_t)((tot >> 21) & 0x1fffffu), ng = (uint32_t)(tot >> 42);
-  BLK_MARK(18, c_win);  // the block scan
   {
     uint32_t pr = prev_rel, bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu),
              bh = (uint32_t)(ex >> 42);
@@ -2263,49 +2275,31 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
         s_ip[lds_pad(r)] = bi;
         s_grp[lds_pad(r)] = bh - 1;
         if (hd) s_gs[lds_pad(bh - 1)] = r;
-        if (!(M.sdef_abl & 4u)) M.cpt[(uint64_t)pn * NMAX + q * NT + tid] = bc;  // (stg_pos(r): window n's children resolve through it)
-        bc += ec[q] & 0xffffu;
-        bi += ec[q] >> 16;
+        s_rk[(ec[q] >> 18) % NMAX] = (uint16_t)r;
+        M.cpt[(uint64_t)pn * NMAX + q * NT + tid] = bc;  // (stg_pos(r): window n's children resolve through it)
+        bc += ec[q] & 0x1ffu;
+        bi += (ec[q] >> 9) & 0x1ffu;
       }
     }
   }
-  // the lookups of this thread's records, all issued before the barrier's wait
-  const uint32_t *const rm = M.rmap;
-  const uint32_t *const cq = M.cpt + (uint64_t)(pn ^ 1u) * NMAX;
-  uint32_t look[RPT];
-  uint2 lf0[RPT];  // each record's first inline leaf (most have at most one: the rest are loaded in the loop)
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const uint32_t r = tid * RPT + q;
-    look[q] = 0;
-    lf0[q] = make_uint2(0, 0);
-    if (r < N && !(M.sdef_abl & 1u)) {
-      const uint32_t u = (uint32_t)ek[q];
-      if (((uint32_t)ek[q] == 0u)) look[q] = rm[(ep[q] & 0xffffffu) % WTOT];            // the parent's rank
-      else if (u & PROV) look[q] = cq[stg_pos(((u & 0x3fffffffu) >> 8) % NMAX)];   // window n-1's child prefix
-      if (ec[q] >> 16) lf0[q] = M.slf0[q * NT + tid];
-    }
-  }
   __syncthreads();
-  BLK_MARK(20, c_win);  // per-rank arrays written, lookups issued, barrier
   uint64_t digest = 0;
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
-    if (r >= N || (M.sdef_abl & 2u)) continue;
+    if (r >= N) continue;
     const uint32_t rel = (uint32_t)(ek[q] >> 32);
     const uint64_t t = w.tmin + rel;
     uint32_t uid = (uint32_t)ek[q];
-    if (((uint32_t)ek[q] == 0u)) {  // a local record: its parent's child prefix + its child index
-      uint32_t rp = look[q];
+    if (uid == 0u) {  // a local record: its parent's child prefix + its child index
+      uint32_t rp = s_rk[(ep[q] & 0xffffffu) % NMAX];
       if (rp >= N) {  // (cannot happen: the parent is a record of this window)
         atomicOr(M.error, 256u);
         rp = 0;
       }
       uid = w.uid0 + s_cp[lds_pad(rp)] + (ep[q] >> 24);
-    } else if (uid & PROV) {  // a child of window n - 1
-      if (((uid >> 30) & 1u) != (pn ^ 1u)) atomicOr(M.error, 256u);
-      uid = uidq + look[q] + (uid & 0xffu);
+    } else if (uid & PROV) {  // (k2_pa resolves these at staging)
+      atomicOr(M.error, 256u);
     }
     const uint32_t g = s_grp[lds_pad(r)];
     const uint32_t first = s_gs[lds_pad(g)];
@@ -2317,11 +2311,11 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
       M.log_uid[rk] = uid;
       M.log_ctx[rk] = M.stx[q * NT + tid];
     }
-    const uint32_t ni = min(ec[q] >> 16, M.maxc);  // (bounded: a staged record's leaves fit its row)
+    const uint32_t ni = min((ec[q] >> 9) & 0x1ffu, M.maxc);  // (bounded: a staged record's leaves fit its row)
     const uint2 *lf = M.sleaf + (uint64_t)r * M.maxc;
     const uint32_t cpr = s_cp[lds_pad(r)], ipr = s_ip[lds_pad(r)];
     for (uint32_t k = 0; k < ni; k++) {  // its inline DoForwardUp leaves, in Schedule order
-      const uint2 l = k ? lf[k] : lf0[q];
+      const uint2 l = k ? lf[k] : make_uint2(ep[q] & 0xffffffu, ep[q] >> 24);
       const uint64_t lk = w.K0 + last + 1 + ipr + k;
       const uint32_t lu = w.uid0 + cpr + l.y;
       digest += digest_term(lk, t, lu);
@@ -2334,7 +2328,6 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     if (r == N - 1) C.last_ts = t;
   }
   digest = wave_sum64(digest);
-  BLK_MARK(22, c_win);  // resolve, log, digest (lookups and leaves arrived)
   if (lane == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
   __syncthreads();  // (every lookup of the rank accumulators is done: clear them for window n + 2)
   for (uint32_t i = tid; i < w.W; i += NT) M.wrank[(uint64_t)pn * WTOT + i] = 0;
