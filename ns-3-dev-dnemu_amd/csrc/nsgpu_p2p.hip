@@ -159,7 +159,8 @@ struct Ctl {
   // ---- deferred dispatch accounting (single wide engine, nsgpu_p2p_win.h "deferred windows") ----
   uint64_t acc_tc, acc_tinl;  // this window's children / inline children (k2_handle accumulates)
   uint32_t pdf;               // the window the next k2_pa appends is staged (1) or appended from sinfo (0)
-  uint32_t sflag;             // a staged window awaits k2_sdef: 1 | (its window index & 3) << 1
+  uint32_t sflag;             // k2_pa staged a window for k2_sdef: 1 | (its window index & 3) << 1 (k2_pa writes
+                              // it every window; k2_sdef's blocks only read it)
   uint32_t rk_W, rk_go;       // k2_handle's snapshot for k2_rank (window size; it was handled, normally)
   uint64_t rk_win, rk_lim;    //   (its window index, lim_rel): k2_rank's bookkeeping block rewrites C.W etc.
   WInfo winfo[4];             // window n's dispatch bases (k2_rank's bookkeeping), at n & 3

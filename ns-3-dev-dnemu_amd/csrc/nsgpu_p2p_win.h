@@ -449,6 +449,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     if (blockIdx.x == 0 && threadIdx.x < M.nranks) x2hdr(M, M.x2_send, threadIdx.x)->n = 0;  // (X2 has sent them)
     if (C.prep) return;
   }
+  // k2_sdef's flag, every window (its blocks only read it: a block may start after another finished)
+  if (DF && g == 0)
+    C.sflag = (c_done < 2 && c_mode < MODE_SORT && c_mode != MODE_RUN && c_pdf && c_pvalid)
+                  ? 1u | (uint32_t)(((c_wn - 1) & 3) << 1) : 0u;
   if (c_done >= 2 || c_mode >= MODE_SORT) return;
   if (slot_block) BLK_MARK(32, c_win);  // snapshot + slot loads issued (waits at first use)
   const bool run = c_mode == MODE_RUN;
@@ -476,7 +480,6 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       }
     }
   }
-  if (DF && g == 0 && c_pdf && c_pvalid && !run) C.sflag = 1u | (uint32_t)(((c_wn - 1) & 3) << 1);  // (k2_sdef's)
   if (!run && partition && g == 0) {
     publish_bound(C, b);
     if (WIDE && M.trace) C.tn0 = *M.trace_n;  // (the local records' trace uids are patched from here on)
@@ -1905,7 +1908,8 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 template <int NT>
 __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb);
 constexpr int RKT_DF = 1024;              // the deferred pipeline's k2_rank blocks: SUBS tiles at once
-constexpr int NSDEF = 1;                  // blocks of the deferred accounting (df_sdef)
+constexpr int NSDEF = 4;                  // blocks of the deferred accounting (df_sdef: each scans the whole
+                                          // window, then resolves / logs / digests a quarter of its records)
 constexpr int RK_GRID_DF = 256;             // one 1024-thread block per CU (~132 KB of LDS each): bookkeeping, accounting, tiles
 template <bool DF>
 __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
@@ -1913,7 +1917,7 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   Ctl &C = *M.C;
   BLK_T0();
 #ifdef NSGPU_PHASE_PROF
-  const uint64_t c_win = C.windows;
+  const uint64_t c_win = DF ? C.rk_win : C.windows;  // (DF: block 0's bookkeeping advances C.windows)
   uint32_t n_tie = 0;
 #endif
   // DF: blocks 1 .. NSDEF do the last window's dispatch accounting (k2_pa staged it) beside this window's
@@ -1921,6 +1925,7 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   if constexpr (DF) {
     if (blockIdx.x >= 1 && blockIdx.x <= (uint32_t)NSDEF) {
       if (M.sdef_fold) df_sdef<NT>(M, C, blockIdx.x - 1, NSDEF);
+      BLK_REC(2, c_win);  // (diagnostic build: k2_scan's per-block slot, unused by the deferred pipeline)
       return;
     }
   }
@@ -1954,6 +1959,7 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   if (DF) {
     if (blockIdx.x == 0) {
       df_book<NT>(M, C, ranked, W, Lt, wn);
+      BLK_REC(2, c_win);
       return;
     }
     if (!ranked) return;
@@ -2062,6 +2068,7 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
     __syncthreads();
     BLK_MARK(54, c_win);
   }
+  BLK_REC(2, c_win);
 #ifdef NSGPU_PHASE_PROF
   if (n_tie) atomicAdd((unsigned long long *)&g_phase[61], (unsigned long long)n_tie);  // (every window)
   if (c_win == g_blk_win) {
@@ -2186,9 +2193,12 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 // results go to LDS (child / inline prefixes, the group of each rank, group starts, and the rank of each dense
 // index, through which a local record finds its parent's), so after the loads the kernel reads LDS only.
 template <int NT>
-__device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
+__device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb) {
   const uint32_t sf = C.sflag;
   BLK_T0();
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t c_win = C.rk_win - 1;  // (diagnostic build: marks 22..30 in the sampled window)
+#endif
   static_assert(NT == (int)STG_NT, "k2_sdef's rank slices are the stage layout's");
   constexpr int RPT = NMAX / NT;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -2245,6 +2255,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
       }
     }
   }
+  BLK_MARK(22, c_win);  // the records arrived
   uint64_t inc = sum;
   for (int o = 1; o < 64; o <<= 1) {
     const uint64_t x = __shfl_up(inc, o);
@@ -2260,6 +2271,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
   }
   const uint64_t ex = off + inc - sum;
   const uint32_t tinl = (uint32_t)((tot >> 21) & 0x1fffffu), ng = (uint32_t)(tot >> 42);
+  BLK_MARK(24, c_win);  // block scan
   {
     uint32_t pr = prev_rel, bc = (uint32_t)(ex & 0x1fffffu), bi = (uint32_t)((ex >> 21) & 0x1fffffu),
              bh = (uint32_t)(ex >> 42);
@@ -2276,18 +2288,19 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
         s_grp[lds_pad(r)] = bh - 1;
         if (hd) s_gs[lds_pad(bh - 1)] = r;
         s_rk[(ec[q] >> 18) % NMAX] = (uint16_t)r;
-        M.cpt[(uint64_t)pn * NMAX + q * NT + tid] = bc;  // (stg_pos(r): window n's children resolve through it)
+        if ((uint32_t)q % nsb == b) M.cpt[(uint64_t)pn * NMAX + q * NT + tid] = bc;  // (stg_pos(r): window n's children resolve through it)
         bc += ec[q] & 0x1ffu;
         bi += (ec[q] >> 9) & 0x1ffu;
       }
     }
   }
   __syncthreads();
+  BLK_MARK(26, c_win);  // per-rank LDS arrays, prefixes stored
   uint64_t digest = 0;
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     const uint32_t r = tid * RPT + q;
-    if (r >= N) continue;
+    if (r >= N || (uint32_t)q % nsb != b) continue;  // (this block's share of the records)
     const uint32_t rel = (uint32_t)(ek[q] >> 32);
     const uint64_t t = w.tmin + rel;
     uint32_t uid = (uint32_t)ek[q];
@@ -2328,11 +2341,13 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t, uint32_t) {
     if (r == N - 1) C.last_ts = t;
   }
   digest = wave_sum64(digest);
+  BLK_MARK(28, c_win);  // resolve, log, digest
   if (lane == 0 && digest) atomicAdd((unsigned long long *)&C.digest, (unsigned long long)digest);
-  __syncthreads();  // (every lookup of the rank accumulators is done: clear them for window n + 2)
-  for (uint32_t i = tid; i < w.W; i += NT) M.wrank[(uint64_t)pn * WTOT + i] = 0;
-  for (uint32_t i = tid; i < w.Lt; i += NT) M.lrank[(uint64_t)pn * LMAX + i] = 0;
-  if (tid == 0) C.sflag = 0;
+  // the window's rank accumulators, cleared for window n + 2 (k2_pa read them; nothing here does)
+  for (uint32_t i = b * NT + tid; i < w.W; i += nsb * NT) M.wrank[(uint64_t)pn * WTOT + i] = 0;
+  for (uint32_t i = b * NT + tid; i < w.Lt; i += nsb * NT) M.lrank[(uint64_t)pn * LMAX + i] = 0;
+
+  BLK_MARK(30, c_win);  // clears
 }
 __global__ __launch_bounds__(SCAN_THREADS) void k2_sdef(const P2PDev M) {
   df_sdef<SCAN_THREADS>(M, *M.C, blockIdx.x, gridDim.x);
