@@ -178,17 +178,19 @@ class P2PGrid:
                 "pipeline_unit": "us per launch (hipExtLaunchKernel start/stop events, sampled windows)",
                 "latency": self.latency_roofline(prof, step_kernel_ms * 1e3 / windows)}
 
-    # dependent memory trips on each kernel's critical path (DESIGN.md §4.4 "latency roofline"): k2_pa reads
-    # the run control + slot records, (local slots) their children, allocates (block atomic), claims node-table
-    # entries (atomic), folds the bound (atomics); k2_handle reads control + slot, node table, the holder's
-    # device / route records, writes local records, ranks (tile loads + atomics); k2_rank reads control +
-    # region counts, chain words, adds ranks (atomics); k2_scan / k2_sdef read control + slots, scan, write.
-    TRIPS = {"k2_pa": 5, "k2_handle": 5, "k2_rank": 3, "k2_scan": 4, "k2_sdef": 3, "k_tpatch": 2}
+    # dependent memory trips on each kernel's critical path (DESIGN.md §4.4 "latency roofline"): k2_pa reads a
+    # local slot's dense entry, then the run control + slot records + first children (one trip), allocates
+    # (block atomic), claims node-table entries (atomic); k2_handle reads control + slot, node table, the
+    # node's other slots, the holder's device / route records, the queue ring; k2_rank reads control + region
+    # counts, then chain words (its accounting blocks: the staged records, with the control); k2_scan (the
+    # scanning pipeline) reads control + slots, scans, resolves, writes.
+    TRIPS = {"k2_pa": 4, "k2_handle": 5, "k2_rank": 2, "k2_scan": 4, "k2_sdef": 1, "k_tpatch": 2}
 
     def latency_roofline(self, prof, window_us):
         import nsgpu
         boundary_us, trip_us = nsgpu.probe_latency()
-        used = [k for k, v in prof.items() if v[1] > 0]
+        top = max((v[1] for v in prof.values()), default=0)
+        used = [k for k, v in prof.items() if v[1] > 0 and v[1] * 2 >= top]  # (the per-window chain, not pauses)
         trips = sum(self.TRIPS.get(k, 3) for k in used)
         bound = len(used) * boundary_us + trips * trip_us
         return {"bound": "latency", "kernels_per_window": len(used), "boundary_us": boundary_us,

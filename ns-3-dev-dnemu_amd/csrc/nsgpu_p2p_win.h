@@ -219,7 +219,7 @@ __device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t
 // a child (src == NOSRC) is parked in the fresh buffer, a pool entry stays where it is; both fold
 // into the next window's reduction.
 template <bool WIDE>
-__device__ __forceinline__ void k2_classify(const P2PDev &M, const WinBound &b, bool run, bool valid, const Ev &e,
+__device__ __forceinline__ void k2_classify(const int64_t *look, const WinBound &b, bool run, bool valid, const Ev &e,
                                             uint32_t src, Red &R, uint64_t &tmn, uint64_t &wnd, uint64_t &wndw,
                                             bool &in, bool &park) {
   const uint64_t pk = ((e.ts - b.tmin) << 32) | e.uid;
@@ -227,10 +227,11 @@ __device__ __forceinline__ void k2_classify(const P2PDev &M, const WinBound &b, 
   park = valid && !in && src == NOSRC;
   if (valid && !in) {
     tmn = e.ts < tmn ? e.ts : tmn;
-    const uint64_t x = e.ts + (uint64_t)M.lookahead[e.kind & 0xffu];
+    const uint32_t kd = (e.kind & 0xffu) % K_NKINDS;
+    const uint64_t x = e.ts + (uint64_t)look[kd];
     wnd = x < wnd ? x : wnd;
     if constexpr (WIDE) {
-      const uint64_t xw = e.ts + (uint64_t)M.lookw[e.kind & 0xffu];
+      const uint64_t xw = e.ts + (uint64_t)look[K_NKINDS + kd];
       wndw = xw < wndw ? xw : wndw;
     }
     if ((e.kind & 0xffu) == K_STOP) {  // at most one Stop event is pending
@@ -392,6 +393,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const uint64_t c_span_t = WIDE ? C.span_t : 0;
   const uint32_t c_pdf = DF ? C.pdf : 0u;
   const uint64_t c_wn = DF ? C.windows : 0;  // (this window's index: the last one is c_wn - 1)
+  const int64_t look_mine = threadIdx.x < K_NKINDS       ? M.lookahead[threadIdx.x]
+                            : threadIdx.x < 2 * K_NKINDS ? (WIDE ? M.lookw[threadIdx.x - K_NKINDS] : 0)
+                                                         : 0;
   uint32_t xw_u[4] = {0, 0, 0, 0};  // (window c_wn - 2's uid base: the pool's provisional uids; all four
   if (DF) {                          //  loaded with the run control, picked once C.windows is back)
 #pragma unroll
@@ -422,19 +426,8 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   // (a speculative entry past the last window's records is followed too: clamped into the record space)
   const uint32_t rec =
       (WIDE && g >= (uint64_t)WCAP && slot_role) ? min(DF ? ldd.x : M.lrec[g - WCAP], (uint32_t)WTOT - 1u) : (uint32_t)g;
-  if (slot_role) {  // the slot and its first children
-    const uint32_t s = rec;
-    spk = M.pwkey[s];
-    si = M.sinfo[s];
-    ncr = M.nchild[s];
-    sctx = M.pwctx[s];
-    if (DF) {  // (branch-free: a branch here made the wave wait for these before issuing the child loads)
-      const bool gz = g < (uint64_t)WCAP;
-      const uint32_t *wr = gz ? M.wrank + g : M.lrank + (g - WCAP);
-      rk2[0] = wr[0];
-      rk2[1] = wr[gz ? (uint32_t)WTOT : (uint32_t)LMAX];
-      ninl0 = M.ninl[gz ? (uint32_t)g : 0u];  // (a local record's is not used)
-    }
+  if (slot_role) {  // the slot and its first children (the children first: a register copy of an early-arriving
+    const uint32_t s = rec;  // slot field made the wave wait for it before the later loads were issued)
 #pragma unroll
     for (int j = 0; j < PFC; j++) {  // (a child index past maxc loads the slot's last one: in range, ignored)
       const uint32_t sl = s * M.maxc + min((uint32_t)j, M.maxc - 1u);
@@ -444,6 +437,17 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       ca[j] = M.ch_a[sl];
       cpk[j] = *(const uint4 *)&M.ch_pkt[sl];
     }
+    if (DF) {  // (branch-free: a branch here made the wave wait for these before issuing the child loads)
+      const bool gz = g < (uint64_t)WCAP;
+      const uint32_t *wr = (gz ? M.wrank : M.lrank - WCAP) + g;
+      rk2[0] = wr[0];
+      rk2[1] = wr[gz ? (uint32_t)WTOT : (uint32_t)LMAX];
+      ninl0 = M.ninl[gz ? (uint32_t)g : 0u];  // (a local record's is not used)
+    }
+    spk = M.pwkey[s];
+    si = M.sinfo[s];
+    ncr = M.nchild[s];
+    sctx = M.pwctx[s];
   }
   if (DIST) {
     if (blockIdx.x == 0 && threadIdx.x < M.nranks) x2hdr(M, M.x2_send, threadIdx.x)->n = 0;  // (X2 has sent them)
@@ -454,6 +458,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     C.sflag = (c_done < 2 && c_mode < MODE_SORT && c_mode != MODE_RUN && c_pdf && c_pvalid)
                   ? 1u | (uint32_t)(((c_wn - 1) & 3) << 1) : 0u;
   if (c_done >= 2 || c_mode >= MODE_SORT) return;
+  // the kinds' lookaheads in LDS (a per-child lookup of the kernel-argument table was a memory trip each)
+  __shared__ int64_t s_look[2 * K_NKINDS];
+  if (threadIdx.x < 2 * K_NKINDS) s_look[threadIdx.x] = look_mine;
+  __syncthreads();
   if (slot_block) BLK_MARK(32, c_win);  // snapshot + slot loads issued (waits at first use)
   const bool run = c_mode == MODE_RUN;
   const bool partition = c_done == 0;
@@ -582,7 +590,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
             valid = partition && (!DIST || M.owner[e.ctx] == M.rank);
           }  // (a local record's child ran in the last window itself)
         }
-        k2_classify<WIDE>(M, b, run, valid, e, NOSRC, R, tmn, wnd, wndw, gin[q], gpk[q]);
+        k2_classify<WIDE>(s_look, b, run, valid, e, NOSRC, R, tmn, wnd, wndw, gin[q], gpk[q]);
         ge[q] = e;
         cw += gin[q];
         cf += gpk[q];
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
       if (valid) e = x2rec(M, M.x2_recv, q)[rec];
       bool gin, gpk;
-      k2_classify<WIDE>(M, b, false, valid, e, NOSRC, R, tmn, wnd, wndw, gin, gpk);
+      k2_classify<WIDE>(s_look, b, false, valid, e, NOSRC, R, tmn, wnd, wndw, gin, gpk);
       uint32_t w0;
       uint64_t f0;
       block_alloc2<TB>(C, gin, gpk, w0, f0);
@@ -657,7 +665,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 #pragma unroll
       for (int q = 0; q < PPT; q++) {
         const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
-        k2_classify<WIDE>(M, b, false, ge[q].ts != TOMB, ge[q], (uint32_t)i, R, tmn, wnd, wndw, gin[q], gpk[q]);
+        k2_classify<WIDE>(s_look, b, false, ge[q].ts != TOMB, ge[q], (uint32_t)i, R, tmn, wnd, wndw, gin[q], gpk[q]);
         cw += gin[q];
         if (gin[q]) {  // the window entry's record (its loads overlap the block allocation below)
           ge[q].ctx = M.ev_ctx[0][i];

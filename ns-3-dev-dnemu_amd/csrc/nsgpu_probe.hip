@@ -3,8 +3,8 @@
 // long: its speed of light is (boundaries x boundary cost) + (dependent trips x trip latency), not HBM
 // bandwidth.  Both constants are measured here, the way the pipeline meets them:
 //  * boundary: an empty 64-block kernel replayed 64 times from a graph (us per kernel);
-//  * trip: 64 blocks chase a pointer chain through a 256-KB table that the previous launch rewrote from
-//    other blocks (other XCDs' L2s), so each level is a dependent load that misses the local L2.
+//  * trip: 64 blocks chase pointers through a 128-MB table (random jumps: every level is a line no L2 holds,
+//    served from the Infinity Cache or HBM, as the window kernels' reads of the previous kernel's writes are).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -15,18 +15,13 @@
 
 namespace nsgpu {
 namespace {
-constexpr int PN = 1 << 16;  // chain table entries (256 KB)
+constexpr int PN = 1 << 25;  // chain table entries (128 MB: 32x the L2s)
 constexpr int LV = 32;       // chase levels per launch
 
-__global__ __launch_bounds__(64) void k_probe_chase(uint32_t *buf, int levels, uint32_t salt, int rewrite) {
+__global__ __launch_bounds__(64) void k_probe_chase(uint32_t *buf, int levels, uint32_t salt) {
   const uint32_t tid = blockIdx.x * 64 + threadIdx.x;
-  uint32_t x = (tid * 40503u + salt) % PN;
+  uint32_t x = (uint32_t)(((uint64_t)(tid + 1) * 0x9e3779b97f4a7c15ull + salt * 0x632be59bd9b4e019ull) >> 39) % PN;
   for (int l = 0; l < levels; l++) x = buf[x];
-  // rewrite the whole table for the next launch (the same chain values, other blocks' entries: most lines
-  // a level reads were last written on another XCD, so each level misses this XCD's L2)
-  const uint32_t nt = gridDim.x * 64;
-  if (rewrite)
-    for (uint32_t w = (tid + 997u * salt) % nt; w < (uint32_t)PN; w += nt) buf[w] = (w * 40503u + 12345u) % PN;
   if (x == 0xffffffffu) buf[0] = 1;  // (keeps the chain live)
 }
 }  // namespace
@@ -45,7 +40,11 @@ extern "C" int nsgpu_probe_latency(void *stream, double *boundary_us, double *tr
   float ms[3] = {0, 0, 0};
   constexpr int NK = 64, REPS = 20;
   std::vector<uint32_t> h(PN);
-  for (int i = 0; i < PN; i++) h[i] = (uint32_t)((i * 40503ull + 12345) % PN);
+  for (int i = 0; i < PN; i++) {  // a random jump per entry
+    uint64_t z = (uint64_t)i * 0x9e3779b97f4a7c15ull + 0x2545f4914f6cdd1dull;
+    z = (z ^ (z >> 31)) * 0xbf58476d1ce4e5b9ull;
+    h[i] = (uint32_t)((z ^ (z >> 29)) % PN);
+  }
   hipError_t e = hipSuccess;
   const char *what = "";
 #define PROBE(x, w)                  \
@@ -58,12 +57,12 @@ extern "C" int nsgpu_probe_latency(void *stream, double *boundary_us, double *tr
   PROBE(hipEventCreate(&a), "event");
   PROBE(hipEventCreate(&b), "event");
   PROBE(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
-  // v = 0: empty kernels; v = 1: the table rewritten, no chase; v = 2: rewritten, LV levels each
+  // v = 0: empty kernels; v = 1: the same (the chase's baseline); v = 2: LV levels each
   for (int v = 0; v < 3 && e == hipSuccess; v++) {
     PROBE(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "capture");
     if (e != hipSuccess) break;
     for (int k = 0; k < NK; k++)
-      hipLaunchKernelGGL(k_probe_chase, dim3(64), dim3(64), 0, cs, buf, v == 2 ? LV : 0, (uint32_t)k, v ? 1 : 0);
+      hipLaunchKernelGGL(k_probe_chase, dim3(64), dim3(64), 0, cs, buf, v == 2 ? LV : 0, (uint32_t)k);
     hipError_t ec = hipStreamEndCapture(cs, &g[v]);
     PROBE(ec, "capture end");
     PROBE(hipGraphInstantiate(&ge[v], g[v], nullptr, nullptr, 0), "instantiate");
