@@ -166,11 +166,13 @@ class P2PGrid:
         # the window pipeline is 3 kernels per window; a separate eager run launches each kernel of
         # every 8th window with start/stop HIP events recorded by the command processor at the
         # kernel's own start and end (hipExtLaunchKernel), and the kernel with the largest average
-        # time is the dominant one (events per launch = the average window)
+        # time among the per-window ones (not the pauses' flush kernels) is the dominant one (events per
+        # launch = the average window)
         prof = self.engine.profile(sample_every=8)
         st, _, _, _ = self.engine.results()
         windows = max(int(st.windows), 1)
-        name = max(prof, key=lambda k: prof[k][0])
+        top = max((v[1] for v in prof.values()), default=0)
+        name = max((k for k, v in prof.items() if v[1] * 2 >= top), key=lambda k: prof[k][0])
         return {"kernel": "nsgpu::" + name, "kernel_ms": prof[name][0],
                 "events_per_launch": events_per_step / windows,
                 "step_device_ms": step_kernel_ms, "windows_per_step": windows,

@@ -2196,11 +2196,12 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
     NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, M.x2b * R, s));
     NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, M.x2b * R, s));
     NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 4 * WCAP * sizeof(uint32_t), s));
-    if (M.log_cap) {  // every rank writes only the entries it dispatches: the union is the log
-      NSGPU_HIP(hipMemsetAsync(M.log_ts, 0, M.log_cap * 8, s));
-      NSGPU_HIP(hipMemsetAsync(M.log_uid, 0, M.log_cap * 4, s));
-      NSGPU_HIP(hipMemsetAsync(M.log_ctx, 0, M.log_cap * 4, s));
-    }
+  }
+  if (M.log_cap) {  // (partitioned: every rank writes only the entries it dispatches, the union is the log;
+                    //  mixed runs: the ranks of host dispatches stay unwritten)
+    NSGPU_HIP(hipMemsetAsync(M.log_ts, 0, M.log_cap * 8, s));
+    NSGPU_HIP(hipMemsetAsync(M.log_uid, 0, M.log_cap * 4, s));
+    NSGPU_HIP(hipMemsetAsync(M.log_ctx, 0, M.log_cap * 4, s));
   }
   NSGPU_HIP(hipMemcpyAsync(M.C, &h->C0, sizeof(Ctl), hipMemcpyHostToDevice, s));
   return NSGPU_OK;
