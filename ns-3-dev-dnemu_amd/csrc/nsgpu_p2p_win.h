@@ -732,7 +732,9 @@ static_assert(HUBL * 3 <= K2_LDS_WORDS, "hub list does not fit the shared buffer
 // Run control a window kernel reads, loaded once at its entry (all fields at once: one memory trip).
 struct HCtl {
   uint64_t tmin, inline_lim, slo, shi;
-  uint64_t lim;  // wide window: a TransmitComplete child with rel ts < lim is a local record (0: none)
+  uint64_t lim;         // wide window: a TransmitComplete child with rel ts < lim is a local record (0: none)
+  const int64_t *look;  // the kinds' lookaheads, then (wide) their wide lookaheads, in LDS (a child's lookup of
+                        // the kernel-argument table was a dependent memory load each)
 };
 // Slot i0's window record, loaded ahead (speculatively at base 0; reloaded for a run chunk).
 struct SlotPre {
@@ -997,8 +999,8 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
       E.ch_kind = M.ch_kind;
       E.ch_a = M.ch_a;
       E.ch_pkt = M.ch_pkt;
-      E.lookahead = M.lookahead;
-      E.lookw = WIDE ? M.lookw : nullptr;
+      E.lookahead = hc.look;
+      E.lookw = WIDE ? hc.look + K_NKINDS : nullptr;
       E.tmn = ~0ull;
       E.wnd = ~0ull;
       E.wndw = ~0ull;
@@ -1377,8 +1379,8 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   E.ch_kind = M.ch_kind;
   E.ch_a = M.ch_a;
   E.ch_pkt = M.ch_pkt;
-  E.lookahead = M.lookahead;
-  E.lookw = WIDE ? M.lookw : nullptr;
+  E.lookahead = hc.look;
+  E.lookw = WIDE ? hc.look + K_NKINDS : nullptr;
   E.tmn = ~0ull;
   E.wnd = ~0ull;
   E.wndw = ~0ull;
@@ -1768,7 +1770,10 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   // the run control and (holder blocks) the slot's record, all loaded at once
   const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_wbase = C.wbase, c_fr = C.force_run, rt = C.rt,
                  c_nhub = C.nhub;
-  const HCtl hc{C.tmin, C.inline_lim, C.split_lo, C.split_hi, C.lim_rel};
+  __shared__ int64_t s_look[2 * K_NKINDS];
+  const HCtl hc{C.tmin, C.inline_lim, C.split_lo, C.split_hi, C.lim_rel, s_look};
+  const uint32_t lt_ = threadIdx.x;  // (loaded now, stored in LDS just before the block's first barrier)
+  const int64_t look_mine = lt_ < K_NKINDS ? M.lookahead[lt_] : (WIDE && lt_ < 2 * K_NKINDS ? M.lookw[lt_ - K_NKINDS] : 0);
   const uint64_t c_wn = C.windows;
   __shared__ uint32_t s_lcnt;  // local records this block made (its region's count, wide windows)
   if (threadIdx.x == 0) s_lcnt = 0;
@@ -1825,7 +1830,8 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
     C.rk_lim = hc.lim;
   }
   PH_MARK(8);
-  __syncthreads();  // (s_lcnt)
+  if (lt_ < 2 * K_NKINDS) s_look[lt_] = look_mine;
+  __syncthreads();  // (s_lcnt, s_look)
   if (bx < (uint32_t)NHB) {
     if (handle) handle_node2<WIDE>(M, C, bx * HB + threadIdx.x, W, base, R, lds, hc, sp, &s_lcnt);
   } else if (bx < (uint32_t)(NHB + NHUB)) {
