@@ -1084,8 +1084,20 @@ __global__ __launch_bounds__(OWV * 64) void k_wl_order(const WDev D, uint64_t K0
     uint32_t c = 0;
     for (uint32_t b0 = 0; b0 < nev; b0 += OCAP) {
       const uint32_t bn = nev - b0 < OCAP ? nev - b0 : OCAP;
+      // the chunk's keys: every load issued before any is stored (a load-store loop waited a trip per entry)
+      constexpr uint32_t PT = OCAP / (OWV * 64);
+      ulonglong2 v[PT];
+#pragma unroll
+      for (uint32_t t = 0; t < PT; t++) {
+        const uint32_t j = threadIdx.x + t * OWV * 64;
+        v[t] = j < bn ? D.evk[b0 + j] : make_ulonglong2(0, 0);
+      }
       __syncthreads();  // (the last chunk's counting is done)
-      for (uint32_t j = threadIdx.x; j < bn; j += OWV * 64) s_k[j] = D.evk[b0 + j];
+#pragma unroll
+      for (uint32_t t = 0; t < PT; t++) {
+        const uint32_t j = threadIdx.x + t * OWV * 64;
+        if (j < bn) s_k[j] = v[t];
+      }
       __syncthreads();
       const uint32_t c0 = (uint32_t)((uint64_t)bn * q / OWV), c1 = (uint32_t)((uint64_t)bn * (q + 1) / OWV);
 #pragma unroll 8
