@@ -383,8 +383,8 @@ const char *nsgpu_p2p_kernel_name(int k);
 int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_every, double *kernel_ms, uint64_t *launches);
 /* The latency constants of the window pipeline's roofline (diagnostic, not a reference interface): a
  * kernel boundary (back-to-back launches of an empty 64-block kernel, graph-replayed: us per kernel) and
- * one dependent global-memory trip (a pointer chase through lines the previous launch rewrote from other
- * XCDs: us per level). */
+ * one dependent global-memory trip (a pointer chase with random jumps through a 128-MB table, every level a
+ * line no L2 holds: us per level). */
 int nsgpu_probe_latency(void *stream, double *boundary_us, double *trip_us);
 /* Mixed host / device runs (driven by nsgpu_sim, see above): the uid the program's own Schedule calls
  * start from (after the setup-time ones); advance = dispatch every device event with a key below
