@@ -288,7 +288,7 @@ struct P2PDev {
   uint2 *sleaf;           // [NMAX][maxc] their further inline leaves: (context, child index) (by rank, entry 0 unused)
   uint32_t *cpt;          // [2][NMAX] child prefix by rank (k2_sdef): provisional uids resolve through it
   uint32_t *ldpd;         // [LMAX] the dense list's parents as dense indices | child index << 24 (k2_rank -> k2_pa)
-  uint32_t sdef_fold;     // df_sdef runs as k2_rank's block 1 (1) or as its own kernel k2_sdef (0)
+  uint32_t sdef_fold;     // df_sdef runs as k2_rank's blocks 1 .. NSDEF (1) or as its own kernel k2_sdef (0)
 };
 
 // ---------------- wave / block helpers ----------------
@@ -2255,7 +2255,7 @@ bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, bool df, hipEvent_t ev0 =
       if (!(wide && h->M.trace)) return false;
       NSGPU_KLAUNCH(k_tpatch, dim3(64), dim3(256), s, ev0, ev1, h->M);
       return true;
-    default:  // k2_sdef(n) after k2_rank(n + 1): window n was staged by k2_pa(n + 1) (folded: k2_rank's block 1)
+    default:  // k2_sdef(n) after k2_rank(n + 1): window n was staged by k2_pa(n + 1) (folded: k2_rank's blocks 1 .. NSDEF)
       if (!df || h->M.sdef_fold) return false;
       NSGPU_KLAUNCH(k2_sdef, dim3(NSDEF), dim3(SCAN_THREADS), s, ev0, ev1, h->M);
       return true;

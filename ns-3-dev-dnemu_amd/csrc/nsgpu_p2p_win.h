@@ -1924,7 +1924,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb);
 constexpr int RKT_DF = 1024;              // the deferred pipeline's k2_rank blocks: SUBS tiles at once
 constexpr int NSDEF = 4;                  // blocks of the deferred accounting (df_sdef: each scans the whole
                                           // window, then resolves / logs / digests a quarter of its records)
-constexpr int RK_GRID_DF = 256;             // one 1024-thread block per CU (~132 KB of LDS each): bookkeeping, accounting, tiles
+constexpr int RK_GRID_DF = 256;             // one 1024-thread block per CU (~150 KB of LDS each): bookkeeping, accounting, tiles
 template <bool DF>
 __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   constexpr int NT = DF ? RKT_DF : RKT, SUBS = NT / RKT;
@@ -2202,7 +2202,8 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 // resolved the provisional ones at staging); the log and digest get every record and leaf; the child prefixes
 // are kept (cpt) for the provisional uids of window n's children.  Afterwards the window's rank accumulators
 // are cleared (their parity is window n + 2's).
-// One block of NT threads (k2_rank<true>'s block 1, or the k2_sdef kernel).  Every record is loaded once, into
+// NSDEF blocks of NT threads (k2_rank<true>'s blocks 1 .. NSDEF, or the k2_sdef kernel): each scans the whole
+// window and resolves / logs / digests its share (every NSDEF-th record of a thread).  Every record is loaded once, into
 // registers (RPT consecutive ranks a thread), in the same memory trip as the run control; the scan's per-rank
 // results go to LDS (child / inline prefixes, the group of each rank, group starts, and the rank of each dense
 // index, through which a local record finds its parent's), so after the loads the kernel reads LDS only.
