@@ -1913,6 +1913,12 @@ __device__ __forceinline__ bool lk_before(const LKey &a, const LKey &b) {
 // chain compare runs after the tile, only for rows whose words tie with a distinct record's (chains of 3+
 // levels with equal ts pairs).
 constexpr int RKC = 64;  // columns per tile
+// (diagnostic build: the tiles' phase marks only with NSGPU_TILE_MARKS — their atomics distort the per-block times)
+#ifdef NSGPU_TILE_MARKS
+#define TILE_MARK(i, win) BLK_MARK(i, win)
+#else
+#define TILE_MARK(i, win) (void)0
+#endif
 template <int NT>
 __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32_t Lt, uint64_t wn);
 // DF: the deferred pipeline's variant: it reads k2_handle's snapshot (rk_*), always runs for a formed window,
@@ -1990,7 +1996,7 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
     g_phase[58] = Lt;
   }
 #endif
-  BLK_MARK(48, c_win);
+  TILE_MARK(48, c_win);
   const uint32_t nr = (N + RKT - 1) / RKT, ncl = (Lt + RKC - 1) / RKC;  // phase A: rows x local columns
   const uint32_t nl = (Lt + RKT - 1) / RKT, ncg = (W + RKC - 1) / RKC;  // phase B: local rows x gen-0 columns
   const uint32_t na = nr * ncl, ntile = na + nl * ncg;
@@ -2045,7 +2051,7 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
       if (ix < Lt) relx = M.wkey[dense_rec(W + ix, W, pre)] >> 32;
     }
     __syncthreads();
-    BLK_MARK(50, c_win);
+    TILE_MARK(50, c_win);
     if (tA) {
       bool tie = false;
       const uint32_t self = ix - W - tj * RKC;  // (the row's own column, if it is one of this tile's)
@@ -2077,10 +2083,10 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
       if (ix >= Lt) c = 0;
       slot = ix + LBASE;
     }
-    BLK_MARK(52, c_win);
+    TILE_MARK(52, c_win);
     if (c) atomicAdd(slot >= LBASE ? &lr[slot - LBASE] : &wr[slot], c);
     __syncthreads();
-    BLK_MARK(54, c_win);
+    TILE_MARK(54, c_win);
   }
   BLK_REC(2, c_win);
 #ifdef NSGPU_PHASE_PROF

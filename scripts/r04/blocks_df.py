@@ -45,6 +45,7 @@ for rep in range(2):
             print("  book (0), accounting (1):", " ".join(f"{i}:{(b[i, 0] - t0) * 0.01:.1f}-{(b[i, 1] - t0) * 0.01:.1f}"
                                                       for i in (0, 1)))
     ph = buf[:64]
+    print(f"  rank-tile ties (chain compares) over the run: {int(ph[61])}")
     for i in range(22, 64, 2):
         if ph[i + 1]:
             nm = SDEF.get(i, "")
