@@ -2003,16 +2003,20 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   // SUBS tiles a block at once: sub-tile `sub` is RKT threads (whole waves) with its own column buffer
   const uint32_t sub = threadIdx.x / RKT, lt = threadIdx.x % RKT;
   ulonglong2 *const cw = cws[sub];
-  for (uint32_t t0 = b0 * SUBS; t0 < ntile; t0 += nb * SUBS) {  // (uniform over the block)
-    const uint32_t t = t0 + sub;
+  // a block's sub-tiles are spread over the tile space (sub-tile `sub` of block b0 takes tile base + sub x nb +
+  // b0), so each block gets a mix of the costly tiles (rows with local records) and the cheap ones
+  for (uint32_t t0 = 0; t0 < ntile; t0 += nb * SUBS) {  // (uniform over the block)
+    const uint32_t t = t0 + sub * nb + b0;
     const bool tA = t < na, tB = !tA && t < ntile;
     uint32_t c = 0, slot = 0;  // slot: the row's accumulator (wrank[dense] for gen-0, LBASE + k for local k)
     uint32_t ix = 0, rx = 0, tj = 0;
+    bool g0rows = false;  // (tA: every row is a gen-0 record)
     uint64_t wx = ~0ull, wx2 = ~0ull, relx = 0;
     if (tA) {  // rows: every record; columns: local records
       const uint32_t ti = t / ncl;
       tj = t % ncl;
       ix = ti * RKT + lt;
+      g0rows = ti * RKT + RKT <= W;
       if (lt < (uint32_t)RKC) {
         const uint32_t cy = tj * RKC + lt;
         ulonglong2 w = make_ulonglong2(~0ull, ~0ull);  // (a padding column: after every row)
@@ -2052,7 +2056,11 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
     }
     __syncthreads();
     TILE_MARK(50, c_win);
-    if (tA) {
+    if (tA && g0rows) {  // a local column precedes a gen-0 row iff its rel ts is smaller: one compare
+#pragma unroll 16
+      for (uint32_t y = 0; y < (uint32_t)RKC; y++) c += cw[y].x < wx;
+      slot = rx;
+    } else if (tA) {
       bool tie = false;
       const uint32_t self = ix - W - tj * RKC;  // (the row's own column, if it is one of this tile's)
 #pragma unroll 16
