@@ -463,6 +463,9 @@ typedef struct nsgpu_trace_addressing {
 typedef struct nsgpu_trace_codec nsgpu_trace_codec;
 int nsgpu_trace_codec_create(const nsgpu_p2p_scenario *sc, const nsgpu_trace_addressing *ad, nsgpu_trace_codec **out);
 int nsgpu_trace_codec_free(nsgpu_trace_codec *c);
+/* Time::GetSeconds () of ts ns (the ascii sinks' timestamp): int64x64_t MulByInvert (Invert (1e9)) then
+ * GetDouble, src/core/model/nstime.h:419-431, int64x64-128.cc:94-134, int64x64-128.h:83-95 — not ts / 1e9 */
+double nsgpu_time_get_seconds(int64_t ts);
 /* trace order: the dispatching event's (ts, uid), then the call order inside it (seq) */
 int nsgpu_trace_sort(nsgpu_trace_record *rec, uint64_t n);
 int nsgpu_trace_line(const nsgpu_trace_codec *c, const nsgpu_trace_record *r, char *out, uint64_t cap, uint64_t *len);

@@ -118,6 +118,52 @@ IcmpF icmp_fields(const nsgpu_trace_codec &c, const nsgpu_trace_record &r) {
   return f;
 }
 
+// Time::GetSeconds () at the default NS resolution, as ns-3 computes it (not ts / 1e9): ToDouble (S) = To (S)
+// .GetDouble () (nstime.h:419-431); To (S) with toMul false is int64x64_t (ts).MulByInvert (Invert (1e9))
+// (int64x64-128.cc:94-134), then the two-rounding GetDouble (int64x64-128.h:83-95).  ts / 1e9 differs at
+// half-way timestamps: 840,877,500 ns is 0.8408774999999999 here and prints 0.840877, not 0.840878.
+typedef unsigned __int128 u128;
+u128 divu128(u128 a, u128 b) {  // int64x64_t::Divu (int64x64-128.cc:67-92)
+  u128 quo = a / b, rem = a % b;
+  u128 result = quo << 64;
+  u128 div;
+  if ((rem >> 64) == 0) {
+    rem <<= 64;
+    div = b;
+  } else {
+    div = b >> 64;
+  }
+  return result + rem / div;
+}
+u128 umul_by_invert(u128 a, u128 b) {  // int64x64_t::UmulByInvert (int64x64-128.cc:103-118)
+  const u128 lo = ~(u128)0 >> 64;
+  const u128 ah = a >> 64, bh = b >> 64, al = a & lo, bl = b & lo;
+  return ah * bh + ((ah * bl + al * bh) >> 64);
+}
+u128 invert_1e9() {  // int64x64_t::Invert (1e9) (int64x64-128.cc:119-134)
+  const uint64_t v = 1000000000ULL;
+  u128 r = divu128((u128)1 << 64, v);
+  const u128 t = umul_by_invert((u128)v << 64, r);
+  if ((uint64_t)(t >> 64) != 1) r += 1;
+  return r;
+}
+}  // namespace
+
+extern "C" double nsgpu_time_get_seconds(int64_t ts) {
+  static const u128 inv = invert_1e9();
+  const bool neg = ts < 0;
+  const u128 a = (u128)(neg ? -(__int128)ts : (__int128)ts) << 64;
+  const u128 v = umul_by_invert(a, inv);  // MulByInvert: the magnitude, sign restored below
+  const uint64_t hi = (uint64_t)(v >> 64), lo = (uint64_t)v;
+  double flo = (double)lo;
+  flo /= 18446744073709551615.0;  // HP128_MAX_64
+  double r = (double)hi;
+  r += flo;
+  return neg ? -r : r;
+}
+
+namespace {
+
 void dotted(std::string &o, uint32_t a) {
   char b[20];
   std::snprintf(b, sizeof b, "%u.%u.%u.%u", a >> 24, (a >> 16) & 255, (a >> 8) & 255, a & 255);
@@ -170,7 +216,7 @@ void line(const nsgpu_trace_codec &c, const nsgpu_trace_record &r, std::string &
   const uint32_t k = r.kind, d = r.dev;
   char b[128];
   o += kChar[k];
-  std::snprintf(b, sizeof b, " %g ", (double)r.ts / 1e9);  // std::ostream << double: precision 6, %g
+  std::snprintf(b, sizeof b, " %g ", nsgpu_time_get_seconds(r.ts));  // std::ostream << double: precision 6, %g
   o += b;
   if (k >= NSGPU_TR_IP_TX)
     std::snprintf(b, sizeof b, "/NodeList/%u/$ns3::Ipv4L3Protocol/%s(%u) ", c.dev_node[d], kSource[k], c.dev_ipif[d]);
@@ -491,7 +537,7 @@ int nsgpu_wifi_ascii(const nsgpu_wifi_sniff *rec, uint64_t n, const uint32_t *ph
     const nsgpu_wifi_sniff &r = rec[i];
     if (r.kind > 1) return set_error(NSGPU_EINVAL, "nsgpu_wifi_ascii: record %llu is malformed", (unsigned long long)i);
     std::snprintf(b, sizeof b, "%s %g /NodeList/%u/DeviceList/%u/$ns3::WifiNetDevice/Phy/State/%s ", r.kind ? "r" : "t",
-                  (double)r.ts / 1e9, phy_node[r.phy], phy_device[r.phy], r.kind ? "RxOk" : "Tx");
+                  nsgpu_time_get_seconds(r.ts), phy_node[r.phy], phy_device[r.phy], r.kind ? "RxOk" : "Tx");
     o += b;
     o.append(text + text_off[r.tx], text + text_off[r.tx + 1]);
     o += "\n";

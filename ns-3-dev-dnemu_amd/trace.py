@@ -98,9 +98,45 @@ def pcap_diff(a, b, snaplen=65535):
     return False, sec, usec
 
 
+_M64 = (1 << 64) - 1
+
+
+def _umul_by_invert(a, b):
+    """int64x64_t::UmulByInvert (int64x64-128.cc:103-118): hi = ah * bh is NOT shifted back."""
+    ah, al, bh, bl = a >> 64, a & _M64, b >> 64, b & _M64
+    return (ah * bh + (((ah * bl + al * bh) & ((1 << 128) - 1)) >> 64)) & ((1 << 128) - 1)
+
+
+def _invert(v):
+    """int64x64_t::Invert (int64x64-128.cc:119-134) via Divu (:67-92)."""
+    a = 1 << 64
+    quo, rem = divmod(a, v)
+    r = quo << 64
+    if rem >> 64 == 0:
+        r += (rem << 64) // v
+    else:
+        r += rem // (v >> 64)
+    if _umul_by_invert(v << 64, r) >> 64 != 1:
+        r += 1
+    return r
+
+
+_INV_1E9 = _invert(1_000_000_000)
+
+
+def get_seconds(ts_ns):
+    """Time::GetSeconds () at NS resolution: To (S) = int64x64_t (ts).MulByInvert (Invert (1e9)), then the
+    two-rounding GetDouble (nstime.h:419-431, int64x64-128.cc:94-134, int64x64-128.h:83-95) — not ts / 1e9,
+    which differs at half-way timestamps (840,877,500 ns: 0.8408774999999999 in ns-3)."""
+    ts = int(ts_ns)
+    v = _umul_by_invert(abs(ts) << 64, _INV_1E9)
+    r = float(v >> 64) + float(v & _M64) / 18446744073709551615.0
+    return -r if ts < 0 else r
+
+
 def seconds_text(ts_ns):
     """std::ostream << double (precision 6, %g) of Time::GetSeconds ()."""
-    return "%g" % (ts_ns / 1e9)
+    return "%g" % get_seconds(ts_ns)
 
 
 class Codec:

@@ -188,3 +188,32 @@ def test_echo_grid_partitioned(nranks):
     grp = p2p.LoopbackGroup(g, nranks, trace_cap=len(otr) + 16)
     grp.run()
     assert_same_trace(g, otr, trace.sort_records(grp.trace()))
+
+
+def halfway_link():
+    """Two nodes, 10 Mb/s, delay 1,991,400 ns, a 4.096 Mb/s CBR OnOff from 1.1 s to 1.9 s: sends every 1 ms,
+    Receive / MacRx at ... 5,000 ns (transmission 433,600 + delay) — GetSeconds () of those lies half-way
+    between two 6-digit decimals, where ns-3's int64x64 path and ts / 1e9 round apart on ~6 % of them
+    (trace-helper.cc:306-390, nstime.h:419-431)."""
+    sc = p2p.Scenario(2)
+    da, db = sc.link(0, 1, 10_000_000, 1_991_400)
+    sc.install_stack()
+    sc.assign_link(da, db, p2p.ip("10.1.1.0"))
+    sc.add_sink(1, 0, 2_500_000_000)
+    sc.add_onoff(0, 1, 1_100_000_000, 1_900_000_000, rate_bps=4_096_000, on_s=1e9, off_s=0.0,
+                 remote_addr=sc.dev_addr[db])
+    sc.route_bfs()
+    return sc
+
+
+def test_halfway_timestamps_gpu_equals_oracle_line_for_line():
+    sc = halfway_link()
+    o = oracle_full(sc, 4096)
+    g = gpu_full(sc, 4096, 8192)
+    assert_same_run(sc, o, g)
+    gtr = g[4]
+    naive = ["%g" % (int(t) / 1e9) for t in gtr["ts"]]
+    ns3 = [trace.seconds_text(int(t)) for t in gtr["ts"]]
+    assert sum(a != b for a, b in zip(naive, ns3)) > 0  # the run does land on half-way timestamps
+    cc = p2p.TraceCodec(sc)
+    assert cc.ascii(gtr) == trace.Codec(sc).ascii(o[4])

@@ -126,3 +126,59 @@ def test_malformed_records_are_refused():
     import nsgpu
     with pytest.raises(nsgpu.NsgpuError):
         cc.ascii(r)
+
+
+def halfway_timestamps(n, seed=7):
+    """Timestamps whose GetSeconds () lies half-way between two 6-significant-digit decimals (where ts / 1e9
+    and ns-3's int64x64 path can round apart): k * 10^(e-5) + 10^(e-5) / 2 ns for ts in [10^(e+3), 10^(e+4))
+    ns, over 1 ms .. 100 s, plus the two values the round-4 review found by hand."""
+    rng = np.random.default_rng(seed)
+    out = [840_877_500, 236_789_500]
+    per = n // 5
+    for e in range(2, 7):  # ts in [10^(e+3), 10^(e+4)) ns: the 6th digit is 10^(e-2) ns, half of it 10^(e-2)/2
+        step = 10 ** (e - 2)
+        k = rng.integers(10 ** 5, 10 ** 6, per)
+        out.extend((k * step + step // 2).tolist())
+    return np.array(out, dtype=np.int64)
+
+
+def test_ascii_seconds_are_ns3_get_seconds():
+    """trace-helper.cc:306-390 print Simulator::Now ().GetSeconds () (int64x64 MulByInvert + GetDouble,
+    nstime.h:419-431), not ts / 1e9: the product codec, the Python codec and the oracle's restatement
+    (nsref_get_seconds) agree on 10^6 half-way timestamps, and ts / 1e9 would differ on some of them."""
+    import nsgpu
+    ts = halfway_timestamps(1_000_000)
+    L = nsgpu.lib()
+    prod = np.fromiter((L.nsgpu_time_get_seconds(int(t)) for t in ts), np.float64, len(ts))
+    ref = np.fromiter((nsref.get_seconds(int(t)) for t in ts), np.float64, len(ts))
+    assert np.array_equal(prod, ref)
+    assert "%g" % prod[0] == "0.840877" and "%g" % prod[1] == "0.236789"
+    sample = ts[::10]
+    assert all(trace.get_seconds(int(t)) == r for t, r in zip(sample, ref[::10]))
+    naive = ts / 1e9
+    assert (naive != ref).sum() > 1000  # the cases the old ts / 1e9 printing got wrong exist in this set
+    # the codec's ascii lines carry exactly those texts: one record per timestamp through nsgpu_trace_ascii
+    sc = p2p.first_cc()
+    _st, tr = oracle_records(sc)
+    cc = p2p.TraceCodec(sc)
+    recs = np.repeat(tr[:1], len(ts))
+    recs["ts"] = ts.astype(np.uint64)
+    for lo in range(0, len(ts), 250_000):
+        lines = cc.ascii(recs[lo:lo + 250_000]).splitlines()
+        got = [ln.split(" ", 2)[1] for ln in lines]
+        assert got == ["%g" % x for x in ref[lo:lo + 250_000]]
+    py = trace.Codec(sc)
+    assert py.ascii(recs[:2000]) == cc.ascii(recs[:2000])
+
+
+def test_halfway_run_codec_same_as_python():
+    """The oracle's records of a run whose Receives land on half-way timestamps (test_gpu_trace.halfway_link):
+    both codecs print ns-3's GetSeconds (), which differs from ts / 1e9 on some of its lines."""
+    from test_gpu_trace import halfway_link
+    sc = halfway_link()
+    _st, tr = oracle_records(sc)
+    tr = same_as_python(sc, tr)
+    text = p2p.TraceCodec(sc).ascii(tr)
+    got = [ln.split(" ", 2)[1] for ln in text.splitlines()]
+    assert got == [trace.seconds_text(int(t)) for t in tr["ts"]]
+    assert sum(g != "%g" % (int(t) / 1e9) for g, t in zip(got, tr["ts"])) > 100
