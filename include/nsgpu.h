@@ -444,6 +444,51 @@ int nsgpu_p2p_group_reset(nsgpu_p2p_group *g, void *stream);
 int nsgpu_p2p_group_run(nsgpu_p2p_group *g, void *stream);
 int nsgpu_p2p_group_destroy(nsgpu_p2p_group *g);
 
+/* ---- setup journal -> setup list (NsgpuP2pScenario::FromNodeList's uid-critical part) ----
+ * Every Schedule* / ScheduleDestroy / Stop (t) call a program makes before Run consumes one uid
+ * (default-simulator-impl.cc:188-242), so the engine's setup list (nsgpu_p2p_scenario.setup_kind / setup_index)
+ * must hold one entry per call, in call order.  HipSimulatorImpl journals each call, classified when it is
+ * made: the stock start calls (NodeListPriv::Add -> Node::Start, src/network/model/node-list.cc:124-131;
+ * Node::AddDevice -> NetDevice::Start and Node::AddApplication -> Application::Start, node.cc:111-145, each
+ * with the index the object got on its node) are told apart from the program's own events by the closure's
+ * type, so an application added before a later link, or a program's own ts-0 event with a node context, maps
+ * to the right object.  This function checks the journal against the node list (each node started once
+ * before its devices and applications, their indices in AddDevice / AddApplication order, every one started)
+ * and returns the setup list, the journal entries the engine takes over, and which node-local device /
+ * application each engine device / application is.  Anything inconsistent is NSGPU_EINVAL, never a shifted
+ * uid. */
+enum nsgpu_journal_kind {
+  NSGPU_J_CALL = 0,          /* any other Schedule* (the program's own event): a consumed uid, kept on the host */
+  NSGPU_J_DESTROY = 1,       /* ScheduleDestroy */
+  NSGPU_J_STOP = 2,          /* Simulator::Stop (t): Schedule (t, &Simulator::Stop), simulator.cc:168-172 */
+  NSGPU_J_NODE_START = 3,    /* ScheduleWithContext (k, 0, &Node::Start, node) */
+  NSGPU_J_DEVICE_START = 4,  /* ScheduleWithContext (node, 0, &NetDevice::Start, device) */
+  NSGPU_J_APP_START = 5      /* ScheduleWithContext (node, 0, &Application::Start, application) */
+};
+typedef struct nsgpu_journal_entry {
+  uint64_t ts;       /* the event's timestamp (ns) */
+  uint32_t context;  /* its context (0xffffffff: none) */
+  uint32_t kind;     /* nsgpu_journal_kind */
+  uint32_t local;    /* DEVICE_START: the node's GetNDevices () - 1 at the call; APP_START: GetNApplications () - 1 */
+  uint32_t pad_;
+} nsgpu_journal_entry;  /* 24 bytes */
+enum nsgpu_node_device_kind { NSGPU_NDEV_P2P = 0, NSGPU_NDEV_LOOPBACK = 1, NSGPU_NDEV_OTHER = 2 };
+typedef struct nsgpu_setup_map {
+  /* caller-allocated outputs */
+  uint32_t *setup_kind, *setup_index;  /* n (one per journal entry): the engine's setup list */
+  uint32_t *owned;                     /* n: the journal entries the engine dispatches (the rest stay on the host) */
+  uint32_t *dev_node, *dev_local;      /* node_dev_off[n_nodes]: engine device d is dev_node[d]'s device dev_local[d] */
+  uint32_t *app_node, *app_local;      /* sum of node_n_apps: engine application a likewise */
+  uint64_t n_owned;
+  uint32_t n_devices, n_apps;          /* engine devices (point-to-point) and applications */
+  int64_t stop_ns;                     /* Simulator::Stop's time, -1: none */
+} nsgpu_setup_map;
+/* node_dev_off[n_nodes + 1]: CSR of each node's devices in AddDevice order; node_dev_kind: their
+ * nsgpu_node_device_kind (NSGPU_NDEV_OTHER fails: not in the GPU-resident subset); node_n_apps: each node's
+ * GetNApplications () */
+int nsgpu_setup_from_journal(const nsgpu_journal_entry *j, uint64_t n, uint32_t n_nodes, const uint64_t *node_dev_off,
+                             const uint32_t *node_dev_kind, const uint32_t *node_n_apps, nsgpu_setup_map *out);
+
 /* ---- trace codec (replaces the default sinks' formatting for GPU-resident events) ----
  * nsgpu_trace_record streams -> the bytes ns-3's default ascii / pcap sinks write:
  * AsciiTraceHelper::Default{Enqueue,Dequeue,Drop,Receive}SinkWithContext (src/network/helper/trace-helper.cc:

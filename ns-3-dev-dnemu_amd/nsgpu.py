@@ -190,6 +190,7 @@ SIGNATURES = {
     "nsgpu_trace_codec_create": (C.c_int, [_vp, _vp, _vp]),
     "nsgpu_trace_codec_free": (C.c_int, [_vp]),
     "nsgpu_time_get_seconds": (C.c_double, [_i64]),
+    "nsgpu_setup_from_journal": (C.c_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "nsgpu_trace_sort": (C.c_int, [_vp, _u64]),
     "nsgpu_trace_line": (C.c_int, [_vp, _vp, _vp, _u64, _vp]),
     "nsgpu_trace_packet": (C.c_int, [_vp, _vp, _vp, _u64, _vp]),

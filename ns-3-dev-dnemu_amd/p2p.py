@@ -816,3 +816,66 @@ def pcap_file(linktype, snaplen, records):
     return _out_bytes(lambda o, c, k: nsgpu.lib().nsgpu_pcap_file(linktype, snaplen, n, sec.ctypes.data, usec.ctypes.data,
                                                                   orig.ctypes.data, off.ctypes.data, data.ctypes.data,
                                                                   o, c, k))
+
+
+# ---------------- setup journal (HipSimulatorImpl's) -> setup list (nsgpu_setup_from_journal) ----------------
+J_CALL, J_DESTROY, J_STOP, J_NODE_START, J_DEVICE_START, J_APP_START = 0, 1, 2, 3, 4, 5
+NDEV_P2P, NDEV_LOOPBACK, NDEV_OTHER = 0, 1, 2
+JOURNAL_DTYPE = np.dtype([("ts", "<u8"), ("context", "<u4"), ("kind", "<u4"), ("local", "<u4"), ("pad_", "<u4")])
+
+
+class SetupMap(C.Structure):
+    """nsgpu_setup_map (include/nsgpu.h)."""
+    _fields_ = [("setup_kind", C.c_void_p), ("setup_index", C.c_void_p), ("owned", C.c_void_p),
+                ("dev_node", C.c_void_p), ("dev_local", C.c_void_p), ("app_node", C.c_void_p),
+                ("app_local", C.c_void_p), ("n_owned", C.c_uint64), ("n_devices", C.c_uint32),
+                ("n_apps", C.c_uint32), ("stop_ns", C.c_int64)]
+
+
+def scenario_journal(sc):
+    """What HipSimulatorImpl journals while a program builds scenario `sc` with the stock helpers, and the node
+    list it then sees: (journal entries, per-node device kinds in AddDevice order, per-node application counts).
+    A setup UID entry is the singletons' ScheduleDestroy; NOOP the loopback device's start."""
+    j = np.zeros(len(sc.setup), JOURNAL_DTYPE)
+    devs = [[] for _ in range(sc.n_nodes)]
+    napp = [0] * sc.n_nodes
+    for i, (kind, k) in enumerate(sc.setup):
+        e = j[i]
+        e["context"] = 0xFFFFFFFF
+        if kind == SETUP_UID:
+            e["kind"] = J_DESTROY
+        elif kind == SETUP_STOP:
+            e["kind"], e["ts"] = J_STOP, sc.stop_ns
+        elif kind == SETUP_NODE:
+            e["kind"], e["context"] = J_NODE_START, k
+        elif kind in (SETUP_DEVICE, SETUP_NOOP):
+            n = sc.dev[k][0] if kind == SETUP_DEVICE else k
+            e["kind"], e["context"], e["local"] = J_DEVICE_START, n, len(devs[n])
+            devs[n].append(NDEV_P2P if kind == SETUP_DEVICE else NDEV_LOOPBACK)
+        elif kind == SETUP_APP:
+            n = sc.apps[k]["node"]
+            e["kind"], e["context"], e["local"] = J_APP_START, n, napp[n]
+            napp[n] += 1
+    return j, devs, napp
+
+
+def setup_from_journal(journal, node_devs, node_n_apps):
+    """nsgpu_setup_from_journal: (setup list [(kind, index)], owned journal indices, engine device -> (node,
+    local), engine application -> (node, local), stop_ns).  Raises NsgpuError on an inconsistent journal."""
+    j = np.ascontiguousarray(journal, dtype=JOURNAL_DTYPE)
+    n, nn = len(j), len(node_devs)
+    off = np.zeros(nn + 1, np.uint64)
+    off[1:] = np.cumsum([len(d) for d in node_devs]) if nn else []
+    kinds = np.array([k for d in node_devs for k in d] or [0], np.uint32)
+    napp = np.array(list(node_n_apps) or [0], np.uint32)
+    nd, na = int(off[-1]), int(napp[:nn].sum()) if nn else 0
+    sk, si, ow = (np.zeros(max(n, 1), np.uint32) for _ in range(3))
+    dn, dl = np.zeros(max(nd, 1), np.uint32), np.zeros(max(nd, 1), np.uint32)
+    an, al = np.zeros(max(na, 1), np.uint32), np.zeros(max(na, 1), np.uint32)
+    m = SetupMap(sk.ctypes.data, si.ctypes.data, ow.ctypes.data, dn.ctypes.data, dl.ctypes.data, an.ctypes.data,
+                 al.ctypes.data, 0, 0, 0, -1)
+    nsgpu.check(nsgpu.lib().nsgpu_setup_from_journal(j.ctypes.data if n else None, n, nn, off.ctypes.data,
+                                                     kinds.ctypes.data, napp.ctypes.data, C.byref(m)))
+    setup = [(int(a), int(b)) for a, b in zip(sk[:n], si[:n])]
+    return (setup, ow[:m.n_owned].tolist(), list(zip(dn[:m.n_devices].tolist(), dl[:m.n_devices].tolist())),
+            list(zip(an[:m.n_apps].tolist(), al[:m.n_apps].tolist())), m.stop_ns)

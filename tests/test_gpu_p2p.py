@@ -81,3 +81,17 @@ def test_grid_128x128_counters_digest():
     """The bench workload itself (config 4): every counter, the digest, final time and next uid."""
     o, g = both(p2p.grid(128, 128))
     assert_same(o, g, log=False)
+
+
+def test_setup_list_from_journal_app_before_a_device():
+    """A program that installs an application on a node before one more link (its journal has an
+    Application::Start between two NetDevice::Starts): the setup list nsgpu_setup_from_journal derives from
+    the classified journal runs on the engine exactly as on the oracle, full pop order."""
+    from test_setup_journal_cpu import app_before_link
+    sc = app_before_link()
+    j, devs, napp = p2p.scenario_journal(sc)
+    setup, _owned, _dmap, _amap, _stop = p2p.setup_from_journal(j, devs, napp)
+    sc.setup = setup
+    o, g = both(sc, log_cap=20000)
+    assert o[2]["rx_packets"][0] > 0
+    assert_same(o, g)
