@@ -320,7 +320,8 @@ extern "C" {
 int nsgpu_trace_codec_create(const nsgpu_p2p_scenario *sc, const nsgpu_trace_addressing *ad, nsgpu_trace_codec **out) {
   if (!sc || !ad || !out) return set_error(NSGPU_EINVAL, "nsgpu_trace_codec_create: null");
   if (!sc->dev_node || !sc->dev_peer || !ad->dev_addr || !ad->dev_ip_ifindex || (sc->n_apps && (!ad->app_remote_addr ||
-      !ad->app_remote_port || !sc->app_kind || !sc->app_node || !sc->app_dst_node || !sc->app_dst_slot || !sc->app_ttl)))
+      !ad->app_remote_port || !sc->app_kind || !sc->app_node || !sc->app_dst_node || !sc->app_dst_slot || !sc->app_ttl ||
+      !sc->app_start_ns)) || (sc->n_setup && (!sc->setup_kind || !sc->setup_index)))
     return set_error(NSGPU_EINVAL, "nsgpu_trace_codec_create: missing scenario / addressing arrays");
   if (!sc->route && !(sc->route_default && sc->route_exc_off && sc->route_exc_slot && sc->route_exc_dev))
     return set_error(NSGPU_EINVAL, "nsgpu_trace_codec_create: no route table");

@@ -3,6 +3,12 @@
 #include "ns3/simulator.h"
 #include "ns3/fatal-error.h"
 #include "ns3/object-factory.h"
+#include "ns3/make-event.h"
+#include "ns3/node-list.h"
+#include "ns3/node.h"
+#include "ns3/net-device.h"
+#include "ns3/application.h"
+#include <typeinfo>
 
 namespace ns3 {
 
@@ -22,6 +28,24 @@ EventImpl *
 HandleToEvent (uint64_t handle)
 {
   return reinterpret_cast<EventImpl *> (static_cast<uintptr_t> (handle & ~static_cast<uint64_t> (1)));
+}
+
+/* The closure class MakeEvent instantiates for ScheduleWithContext (ctx, t, &T::Start, Ptr<T>) — the stock
+ * start calls of NodeListPriv::Add (T = Node), Node::AddDevice (NetDevice) and Node::AddApplication
+ * (Application) (node-list.cc:124-131, node.cc:111-145; &T::Start is &Object::Start, so the object's
+ * pointer type is what tells them apart) */
+template <typename T>
+const std::type_info &
+StartEventType (void)
+{
+  static const std::type_info *type = 0;
+  if (type == 0)
+    {
+      EventImpl *e = MakeEvent (&T::Start, Ptr<T> ());
+      type = &typeid (*e);
+      e->Unref ();
+    }
+  return *type;
 }
 } // anonymous namespace
 
@@ -181,7 +205,26 @@ HipSimulatorImpl::Enqueue (uint64_t ts, uint32_t context, EventImpl *event)
   NSGPU_RT (nsgpu_sim_insert (m_rt, ts, context, reinterpret_cast<uintptr_t> (event), &uid));
   if (!m_running)
     {
-      const SetupCall c = {m_nextStop ? (uint32_t) SETUP_STOP : (uint32_t) SETUP_CALL, context, uid, ts, event};
+      SetupCall c = {m_nextStop ? (uint32_t) SETUP_STOP : (uint32_t) SETUP_CALL, context, uid, ts, event, 0};
+      if (!m_nextStop && context != 0xffffffffu)
+        {
+          const std::type_info &t = typeid (*event);
+          if (t == StartEventType<Node> ())
+            {
+              c.kind = SETUP_NODE_START;
+            }
+          else if (t == StartEventType<NetDevice> () && context < NodeList::GetNNodes ())
+            {
+              // Node::AddDevice pushed the device before scheduling its start
+              c.kind = SETUP_DEVICE_START;
+              c.local = NodeList::GetNode (context)->GetNDevices () - 1;
+            }
+          else if (t == StartEventType<Application> () && context < NodeList::GetNNodes ())
+            {
+              c.kind = SETUP_APP_START;
+              c.local = NodeList::GetNode (context)->GetNApplications () - 1;
+            }
+        }
       m_journal.push_back (c);
     }
   m_nextStop = false;
@@ -304,7 +347,7 @@ HipSimulatorImpl::ScheduleDestroy (EventImpl *event)
   NSGPU_RT (nsgpu_sim_destroy_insert (m_rt, reinterpret_cast<uintptr_t> (event), &ts));
   if (!m_running)
     {
-      const SetupCall c = {(uint32_t) SETUP_DESTROY, 0xffffffffu, 2u, ts, event};
+      const SetupCall c = {(uint32_t) SETUP_DESTROY, 0xffffffffu, 2u, ts, event, 0};
       m_journal.push_back (c);
     }
   event->Ref ();

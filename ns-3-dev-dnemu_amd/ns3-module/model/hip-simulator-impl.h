@@ -56,15 +56,27 @@ public:
   void AttachDeviceSubset (nsgpu_p2p *engine);
 
   /* The setup journal: every Schedule* / ScheduleDestroy / Stop (Time) call made before the first Run, in
-   * call order (= uid order, from 4).  NsgpuP2pScenario::FromNodeList maps the stock helpers' calls
+   * call order (= uid order, from 4), classified when it is made: the stock helpers' start calls
    * (NodeListPriv::Add's Node::Start, Node::AddDevice's NetDevice::Start, Node::AddApplication's
-   * Application::Start, Simulator::Stop) to the engine's setup list. */
-  enum SetupKind { SETUP_CALL = 0, SETUP_DESTROY = 1, SETUP_STOP = 2 };
+   * Application::Start, node-list.cc:124-131, node.cc:111-145) are told apart from the program's own events
+   * by the closure's type (MakeEvent's class for (&Object::Start, Ptr<Node | NetDevice | Application>)), and
+   * carry the index the device / application got on its node.  NsgpuP2pScenario::FromNodeList hands the
+   * journal to nsgpu_setup_from_journal (include/nsgpu.h), which maps it to the engine's setup list. */
+  enum SetupKind
+  {
+    SETUP_CALL = NSGPU_J_CALL,
+    SETUP_DESTROY = NSGPU_J_DESTROY,
+    SETUP_STOP = NSGPU_J_STOP,
+    SETUP_NODE_START = NSGPU_J_NODE_START,
+    SETUP_DEVICE_START = NSGPU_J_DEVICE_START,
+    SETUP_APP_START = NSGPU_J_APP_START
+  };
   struct SetupCall
   {
     uint32_t kind, context, uid;
     uint64_t ts;
     EventImpl *event;
+    uint32_t local;  // SETUP_DEVICE_START / SETUP_APP_START: the object's index on its node
   };
   const std::vector<SetupCall> &GetSetupJournal (void) const;
   /* The engine built from this program's own topology (NsgpuP2pScenario::FromNodeList) takes over the

@@ -10,6 +10,10 @@
 #include "ns3/drop-tail-queue.h"
 #include "ns3/ipv4.h"
 #include "ns3/ipv4-l3-protocol.h"
+#include "ns3/ipv4-list-routing.h"
+#include "ns3/ipv4-static-routing.h"
+#include "ns3/ipv4-global-routing.h"
+#include "ns3/ipv4-routing-table-entry.h"
 #include "ns3/onoff-application.h"
 #include "ns3/packet-sink.h"
 #include "ns3/udp-echo-client.h"
@@ -182,6 +186,51 @@ UintAttribute (Ptr<Object> o, const char *name)
   o->GetAttribute (name, v);
   return (uint32_t) v.Get ();
 }
+/* The engine forwards along global routing's choices (PopulateRoutingTables + LookupGlobal, computed by
+ * nsgpu_route_global): a node's Ipv4 must route through an Ipv4GlobalRouting in its Ipv4ListRouting (the
+ * InternetStackHelper default, static priority 0 + global -10), with no static route of its own beyond the
+ * interfaces' directly connected networks (Ipv4StaticRouting::NotifyInterfaceUp adds those; any other static
+ * route would win over global routing) */
+void
+CheckGlobalRouting (Ptr<Ipv4> ip, uint32_t node)
+{
+  Ptr<Ipv4ListRouting> list = DynamicCast<Ipv4ListRouting> (ip->GetRoutingProtocol ());
+  if (list == 0)
+    {
+      NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << node << "'s Ipv4 routing is not an Ipv4ListRouting "
+                      "(the engine models global routing)");
+    }
+  bool global = false;
+  for (uint32_t i = 0; i < list->GetNRoutingProtocols (); i++)
+    {
+      int16_t priority;
+      Ptr<Ipv4RoutingProtocol> rp = list->GetRoutingProtocol (i, priority);
+      if (DynamicCast<Ipv4GlobalRouting> (rp) != 0)
+        {
+          global = true;
+          continue;
+        }
+      Ptr<Ipv4StaticRouting> st = DynamicCast<Ipv4StaticRouting> (rp);
+      if (st == 0)
+        {
+          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << node << " runs a routing protocol other than "
+                          "static / global routing (not in the GPU-resident subset)");
+        }
+      for (uint32_t r = 0; r < st->GetNRoutes (); r++)
+        {
+          Ipv4RoutingTableEntry e = st->GetRoute (r);
+          if (e.GetGateway () != Ipv4Address::GetZero () || e.IsDefault ())
+            {
+              NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << node << " holds the static route " << e
+                              << " (the engine models global routing only)");
+            }
+        }
+    }
+  if (!global)
+    {
+      NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << node << " has no Ipv4GlobalRouting");
+    }
+}
 } // anonymous namespace
 
 void
@@ -193,95 +242,66 @@ NsgpuP2pScenario::FromNodeList (Ptr<HipSimulatorImpl> impl)
     }
   const uint32_t N = NodeList::GetNNodes ();
   m_nodes = N;
-  // ---- devices, in the setup order of their NetDevice::Start calls (engine index = that order) ----
-  // per node: (device or application object, its engine index) in AddDevice / AddApplication order
-  std::map<Ptr<NetDevice>, uint32_t> devIndex;
-  std::vector<std::vector<Ptr<NetDevice> > > nodeDevs (N);
-  std::vector<std::vector<Ptr<Application> > > nodeApps (N);
+  // ---- the node list: each node's devices (in AddDevice order) and application count ----
+  std::vector<uint64_t> devOff (N + 1, 0);
+  std::vector<uint32_t> devKind, nApps (N, 0);
   for (uint32_t n = 0; n < N; n++)
     {
       Ptr<Node> node = NodeList::GetNode (n);
       for (uint32_t i = 0; i < node->GetNDevices (); i++)
         {
-          nodeDevs[n].push_back (node->GetDevice (i));
+          Ptr<NetDevice> d = node->GetDevice (i);
+          devKind.push_back (DynamicCast<PointToPointNetDevice> (d) != 0 ? (uint32_t) NSGPU_NDEV_P2P
+                             : DynamicCast<LoopbackNetDevice> (d) != 0 ? (uint32_t) NSGPU_NDEV_LOOPBACK
+                             : (uint32_t) NSGPU_NDEV_OTHER);
         }
-      for (uint32_t i = 0; i < node->GetNApplications (); i++)
-        {
-          nodeApps[n].push_back (node->GetApplication (i));
-        }
+      devOff[n + 1] = devKind.size ();
+      nApps[n] = node->GetNApplications ();
     }
-  // ---- the setup list from the journal (uid order) ----
+  // ---- the setup list from the journal (uid order; classified by HipSimulatorImpl when each call was made) ----
   const std::vector<HipSimulatorImpl::SetupCall> &J = impl->GetSetupJournal ();
-  std::vector<uint32_t> seen (N, 0);
-  std::vector<Ptr<Application> > apps;  // engine application index -> object
-  std::vector<Ptr<NetDevice> > devs;    // engine device index -> object
-  for (uint32_t i = 0; i < J.size (); i++)
+  const size_t nj = J.size ();
+  std::vector<nsgpu_journal_entry> journal (std::max (nj, (size_t) 1));
+  for (size_t i = 0; i < nj; i++)
     {
-      const HipSimulatorImpl::SetupCall &c = J[i];
-      if (c.kind == HipSimulatorImpl::SETUP_DESTROY)
-        {
-          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_UID, 0u));
-          continue;
-        }
-      if (c.kind == HipSimulatorImpl::SETUP_STOP)
-        {
-          if (m_stop >= 0)
-            {
-              NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: two Simulator::Stop calls");
-            }
-          m_stop = (int64_t) c.ts;
-          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_STOP, 0u));
-          m_owned.push_back (i);
-          continue;
-        }
-      const uint32_t n = c.context;
-      const uint32_t nd = n < N ? nodeDevs[n].size () : 0u, na = n < N ? nodeApps[n].size () : 0u;
-      if (c.ts != 0 || n >= N || seen[n] >= 1 + nd + na)
-        {
-          // the program's own event: it stays on the host, its uid is consumed
-          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_UID, 0u));
-          continue;
-        }
-      const uint32_t k = seen[n]++;
-      m_owned.push_back (i);
-      if (k == 0)  // NodeListPriv::Add -> ScheduleWithContext (node, 0, &Node::Start)
-        {
-          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_NODE, n));
-        }
-      else if (k <= nd)  // Node::AddDevice -> NetDevice::Start
-        {
-          Ptr<NetDevice> d = nodeDevs[n][k - 1];
-          if (DynamicCast<LoopbackNetDevice> (d) != 0)
-            {
-              m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_NOOP, n));
-            }
-          else if (DynamicCast<PointToPointNetDevice> (d) != 0)
-            {
-              devIndex[d] = devs.size ();
-              m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_DEVICE, (uint32_t) devs.size ()));
-              devs.push_back (d);
-              m_devObj.push_back (d);
-            }
-          else
-            {
-              NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << n << " device " << k - 1
-                              << " is not a PointToPointNetDevice (not in the GPU-resident subset)");
-            }
-        }
-      else  // Node::AddApplication -> Application::Start
-        {
-          m_setup.push_back (std::make_pair ((uint32_t) NSGPU_SETUP_APP, (uint32_t) apps.size ()));
-          apps.push_back (nodeApps[n][k - 1 - nd]);
-        }
+      journal[i].ts = J[i].ts;
+      journal[i].context = J[i].context;
+      journal[i].kind = J[i].kind;
+      journal[i].local = J[i].local;
+      journal[i].pad_ = 0;
     }
+  size_t nApp = 0;
   for (uint32_t n = 0; n < N; n++)
     {
-      if (seen[n] != 1 + nodeDevs[n].size () + nodeApps[n].size ())
-        {
-          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << n << ": " << seen[n]
-                          << " setup calls in the journal, " << 1 + nodeDevs[n].size () + nodeApps[n].size ()
-                          << " expected (build the topology under HipSimulatorImpl, before Run)");
-        }
+      nApp += nApps[n];
+    }
+  std::vector<uint32_t> sk (journal.size ()), si (journal.size ()), owned (journal.size ());
+  std::vector<uint32_t> dNode (std::max (devKind.size (), (size_t) 1)), dLocal (dNode.size ());
+  std::vector<uint32_t> aNode (std::max (nApp, (size_t) 1)), aLocal (aNode.size ());
+  nsgpu_setup_map map;
+  map.setup_kind = &sk[0], map.setup_index = &si[0], map.owned = &owned[0];
+  map.dev_node = &dNode[0], map.dev_local = &dLocal[0], map.app_node = &aNode[0], map.app_local = &aLocal[0];
+  map.n_owned = 0, map.n_devices = 0, map.n_apps = 0, map.stop_ns = -1;
+  NSGPU_TRY (nsgpu_setup_from_journal (&journal[0], nj, N, &devOff[0], devKind.empty () ? 0 : &devKind[0], N ? &nApps[0] : 0,
+                                       &map));
+  for (size_t i = 0; i < nj; i++)
+    {
+      m_setup.push_back (std::make_pair (sk[i], si[i]));
+    }
+  m_owned.assign (owned.begin (), owned.begin () + map.n_owned);
+  m_stop = map.stop_ns;
+  std::map<Ptr<NetDevice>, uint32_t> devIndex;
+  std::vector<Ptr<NetDevice> > devs;    // engine device index -> object
+  std::vector<Ptr<Application> > apps;  // engine application index -> object
+  for (uint32_t d = 0; d < map.n_devices; d++)
+    {
+      devs.push_back (NodeList::GetNode (dNode[d])->GetDevice (dLocal[d]));
+      devIndex[devs[d]] = d;
+      m_devObj.push_back (devs[d]);
+    }
+  for (uint32_t a = 0; a < map.n_apps; a++)
+    {
+      apps.push_back (NodeList::GetNode (aNode[a])->GetApplication (aLocal[a]));
     }
   // ---- device parameters ----
   const uint32_t D = devs.size ();
@@ -312,6 +332,12 @@ NsgpuP2pScenario::FromNodeList (Ptr<HipSimulatorImpl> impl)
         {
           NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: device " << d << "'s DropTailQueue is not in PACKETS mode");
         }
+      if (UintAttribute (p, "Mtu") != 1500)
+        {
+          // the engine forwards whole datagrams up to 1500 bytes (no Ipv4L3Protocol fragmentation, ipv4-l3-protocol.cc:722)
+          NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: device " << d << "'s Mtu is " << UintAttribute (p, "Mtu")
+                          << ", not 1500");
+        }
       DataRateValue rate;
       p->GetAttribute ("DataRate", rate);
       Dev x = {devs[d]->GetNode ()->GetId (), devIndex[other], UintAttribute (q, "MaxPackets"), rate.Get ().GetBitRate (),
@@ -340,6 +366,7 @@ NsgpuP2pScenario::FromNodeList (Ptr<HipSimulatorImpl> impl)
           m_ifindex[devIndex[nd]] = i;
           nodeOfAddr[a] = n;
         }
+      CheckGlobalRouting (ip, n);
       Ptr<Ipv4L3Protocol> l3 = DynamicCast<Ipv4L3Protocol> (ip);
       if (l3 != 0)
         {
@@ -575,6 +602,11 @@ NsgpuP2pScenario::WriteTraces (Ptr<OutputStreamWrapper> ascii, std::string pcapP
       for (uint64_t i = 0; i < n; i++)
         {
           uint64_t len = 0;
+          NSGPU_TRY (nsgpu_trace_line (m_codec, &rec[i], 0, 0, &len));  // the size first (an ICMP line can exceed 512 B)
+          if (len > line.size ())
+            {
+              line.resize (len);
+            }
           NSGPU_TRY (nsgpu_trace_line (m_codec, &rec[i], &line[0], line.size (), &len));
           os->write (&line[0], (std::streamsize) len);
         }
@@ -621,6 +653,11 @@ NsgpuP2pScenario::WriteTraces (Ptr<OutputStreamWrapper> ascii, std::string pcapP
               continue;
             }
           uint64_t len = 0;
+          NSGPU_TRY (nsgpu_trace_packet (m_codec, &rec[i], 0, 0, &len));
+          if (len > pkt.size ())
+            {
+              pkt.resize (len);
+            }
           NSGPU_TRY (nsgpu_trace_packet (m_codec, &rec[i], &pkt[0], pkt.size (), &len));
           files[rec[i].dev]->Write (TimeStep ((int64_t) rec[i].ts), &pkt[0], (uint32_t) len);
         }

@@ -182,3 +182,16 @@ def test_halfway_run_codec_same_as_python():
     got = [ln.split(" ", 2)[1] for ln in text.splitlines()]
     assert got == [trace.seconds_text(int(t)) for t in tr["ts"]]
     assert sum(g != "%g" % (int(t) / 1e9) for g, t in zip(got, tr["ts"])) > 100
+
+
+def test_codec_create_refuses_missing_arrays():
+    """nsgpu_trace_codec_create checks every array it reads (app_start_ns, setup_kind / setup_index included)."""
+    import ctypes as C
+    import nsgpu
+    sc = p2p.first_cc()
+    for field in ("app_start_ns", "setup_kind", "setup_index"):
+        cc = p2p.TraceCodec(sc)  # the addressing arrays
+        s = sc.c_struct()
+        setattr(s, field, None)
+        h = C.c_void_p()
+        assert nsgpu.lib().nsgpu_trace_codec_create(C.byref(s), C.byref(cc._ad), C.byref(h)) != 0
