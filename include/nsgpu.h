@@ -27,7 +27,10 @@ enum {
   NSGPU_EINVAL = 1,   /* bad argument (shape, null pointer, capacity) */
   NSGPU_EHIP = 2,     /* HIP runtime error */
   NSGPU_ENOMEM = 3,   /* device allocation or fixed capacity exhausted */
-  NSGPU_ESTATE = 4    /* call not valid in the current state (e.g. empty queue) */
+  NSGPU_ESTATE = 4,   /* call not valid in the current state (e.g. empty queue) */
+  NSGPU_ERANGE = 5    /* the uid counter would pass 0xfffffffe: DefaultSimulatorImpl's uint32 m_uid wraps to 0 after
+                       * 0xffffffff (default-simulator-impl.cc:52-56,188-219), which no engine replicates;
+                       * the run fails before an event with such a uid is dispatched */
 };
 
 /* ---------------- library / device plumbing ---------------- */
@@ -277,6 +280,10 @@ int nsgpu_sim_stop_at(nsgpu_sim *s, int64_t delay);
 int nsgpu_sim_destroy(nsgpu_sim *s);
 int nsgpu_sim_state(nsgpu_sim *s, uint64_t *now, uint32_t *context, uint64_t *dispatched, uint32_t *next_uid);
 int nsgpu_sim_current_uid(nsgpu_sim *s, uint32_t *uid);
+/* m_uid before anything is scheduled (default 4, default-simulator-impl.cc:52-56): the uids below it count as
+ * consumed by Schedule calls this runtime did not see.  Every Schedule* / ScheduleDestroy that would take uid
+ * 0xffffffff (or a wrapped one) fails with NSGPU_ERANGE, as do the attached engines' allocations. */
+int nsgpu_sim_set_next_uid(nsgpu_sim *s, uint32_t uid);
 int nsgpu_sim_next(nsgpu_sim *s, uint64_t *ts, int *empty);          /* Next (): host and device events */
 int nsgpu_sim_is_finished(nsgpu_sim *s, int *finished);              /* IsFinished (): empty || stopped */
 int nsgpu_sim_set_stop(nsgpu_sim *s, int stop);                      /* Stop (); Run clears it */

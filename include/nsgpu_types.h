@@ -161,6 +161,10 @@ typedef struct nsgpu_p2p_scenario {
   const uint64_t *route_exc_off;   /* n_nodes + 1 */
   const uint32_t *route_exc_slot;
   const uint32_t *route_exc_dev;
+  /* DefaultSimulatorImpl::m_uid before the first setup call (0: 4, the reference's start, :52-56) — a program
+   * whose earlier Schedule calls consumed uids; the engine refuses to pass 0xfffffffe (NSGPU_ERANGE) */
+  uint32_t uid_first;
+  uint32_t pad_uid_;
 } nsgpu_p2p_scenario;
 
 /* Packet descriptor flags (the descriptor {app, ipid, size, ttl} of a datagram): an echo reply

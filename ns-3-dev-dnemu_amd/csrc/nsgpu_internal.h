@@ -11,6 +11,16 @@ namespace nsgpu {
 // Sets the thread-local last-error string returned by nsgpu_last_error() and returns `code`.
 int set_error(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// DefaultSimulatorImpl's m_uid is a uint32 that wraps to 0 after 0xffffffff (default-simulator-impl.cc:52-56,
+// 188-219).  No engine replicates the wrap: a Schedule call that would take uid 0xffffffff (the
+// engines' "none" marker) or a wrapped one fails with NSGPU_ERANGE before any such event is dispatched.  The
+// counter (the next uid) may reach UID_NEXT_MAX; every uid handed out stays below it.
+constexpr uint64_t UID_NEXT_MAX = 0xffffffffull;
+inline int uid_range_error(const char *where) {
+  return set_error(NSGPU_ERANGE, "%s: the uid counter would pass 0xfffffffe (DefaultSimulatorImpl's uint32 m_uid "
+                                 "wraps there, which the engines do not replicate)", where);
+}
+
 }  // namespace nsgpu
 
 #define NSGPU_HIP(call)                                                                              \

@@ -113,6 +113,16 @@ constexpr uint32_t STG_NT = 1024;  // k2_sdef's threads (its rank slices)
 // prefix is known, is PROV | (n & 1) << 30 | r << 8 | j — above every resolved uid (< UID_DF_LIMIT, checked), so
 // keys compare as the final uids do; resolved to uid0(n) + cpt[n & 1][r] + j.
 constexpr uint32_t PROV = 0x80000000u, PROV_MAXC = 256, UID_DF_LIMIT = 0x3fe00000u;
+// A window's children take at most NMAX x PROV_MAXC = 2^21 uids, so a deferred window that starts below
+// UID_DF_SOFT ends below UID_DF_LIMIT; the window that reaches UID_DF_SOFT pauses the deferred pipeline
+// (MODE_UIDX) and the scanning pipeline runs the rest of the run (df_usable is false from there on).
+constexpr uint32_t UID_DF_SOFT = UID_DF_LIMIT - (1u << 22);
+// DefaultSimulatorImpl's m_uid is a uint32 that wraps to 0 after 0xffffffff (default-simulator-impl.cc:52-56,
+// 188-219); the wrapped uids would sort before every earlier one at equal ts and uid 2 would read as a
+// ScheduleDestroy id.  The engines do not replicate that: a window whose children would take uid 0xffffffff
+// or a wrapped one fails the run (error 2048) before any of them runs.  (0xffffffff itself is kept free: it is
+// the "none" marker of several engine records.)
+constexpr uint64_t UID_MAX_NEXT = nsgpu::UID_NEXT_MAX;
 __device__ __forceinline__ uint32_t prov_uid(uint64_t win, uint32_t r, uint32_t j) {
   return PROV | ((uint32_t)(win & 1) << 30) | (r << 8) | j;
 }
@@ -354,7 +364,8 @@ struct Emit {
   const int64_t *lookahead, *lookw;
   uint64_t tmn, wnd, wndw;
   uint64_t lim_abs;  // wide window: a TransmitComplete child before it is a local record (0: none)
-  uint32_t uid;      // uid of the event being run (its trace records; LOCALBIT | record: a local record's)
+  uint32_t uid;      // uid of the event being run (its trace records; a local record's: its record index, tloc)
+  bool tloc = false; // the event is a local record whose uid k2_scan assigns later (k_tpatch resolves its records)
   uint32_t trseq;    // trace sink calls made by it so far
   bool demote;       // the event's ts group is cut by a run chunk: its DoForwardUp leaves are queued
   int32_t lj;        // the local child this event made (an event makes at most one TransmitComplete): its
@@ -415,7 +426,7 @@ __device__ __forceinline__ void trace_call(const P2PDev &M, Emit &E, uint32_t ki
   r.uid = E.uid;
   r.seq = (uint16_t)E.trseq++;
   r.kind = (uint8_t)kind;
-  r.pad_ = 0;
+  r.pad_ = E.tloc ? 1 : 0;  // (k_tpatch replaces a local record's index by its uid and clears the flag)
   r.dev = d;
   r.app = p.app;
   r.ipid = p.ipid;
@@ -1556,6 +1567,10 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     atomicOr(M.error, 4u);
     done = true;
   }
+  if ((uint64_t)bk.puid0 + tcg > UID_MAX_NEXT) {  // (every rank: tcg is the merged window's)
+    atomicOr(M.error, 2048u);
+    done = true;
+  }
   if (done) C.done = 1;
   else if (needc) C.mode = MODE_COMPACT;  // (every rank: the pipelines stay in step)
   stack_and_hubs();
@@ -1626,6 +1641,7 @@ struct nsgpu_p2p {
   std::vector<uint32_t> app_kind;
   std::vector<void *> allocs;
   Ctl C0{};               // run control after reset
+  uint32_t uid_hint = 4;  // the run control's uid as last seen by the host (the deferred pipeline starts below UID_DF_SOFT)
   uint64_t max_windows = ~0ull;
   hipStream_t s = nullptr;  // engine stream (graph capture and replay)
   hipGraphExec_t gexec = nullptr;
@@ -1919,7 +1935,11 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   // ---- setup-time events (node-list.cc:124-131, node.cc:111-145, default-simulator-impl.cc:179-183) ----
   std::vector<uint64_t> its;
   std::vector<uint32_t> iuid, ictx, ikind, ia;
-  uint32_t uid = 4;
+  uint32_t uid = sc->uid_first ? sc->uid_first : 4u;  // (DefaultSimulatorImpl: m_uid (4), :52-56)
+  if ((uint64_t)uid + sc->n_setup > UID_MAX_NEXT) {
+    nsgpu_p2p_destroy(h);
+    return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: the setup calls' uids would pass 0xfffffffe");
+  }
   for (uint32_t i = 0; i < sc->n_setup; i++) {
     const uint32_t k = sc->setup_index[i];
     switch (sc->setup_kind[i]) {
@@ -2204,6 +2224,7 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
     NSGPU_HIP(hipMemsetAsync(M.log_ctx, 0, M.log_cap * 4, s));
   }
   NSGPU_HIP(hipMemcpyAsync(M.C, &h->C0, sizeof(Ctl), hipMemcpyHostToDevice, s));
+  h->uid_hint = h->C0.uid;
   return NSGPU_OK;
 }
 
@@ -2426,6 +2447,9 @@ static int host_step(nsgpu_p2p *h, const Ctl &c, hipStream_t s) {
     if (c.renarrow) hipLaunchKernelGGL(k_renarrow, dim3(1), dim3(1024), 0, s, M);  // (a widened window)
     hipLaunchKernelGGL(k_after_sort, dim3(1), dim3(1024), 0, s, M);
     NSGPU_HIP(hipGetLastError());
+  } else if (c.mode == MODE_UIDX) {  // (the deferred pipeline handed over: nothing to do on the host)
+    hipLaunchKernelGGL(k_after_uidx, dim3(1), dim3(1), 0, s, M);
+    NSGPU_HIP(hipGetLastError());
   } else if (c.mode == MODE_TRIM) {  // a run ends after a cut same-ts group: the rest goes back to the pool
     hipLaunchKernelGGL(k_trim, dim3(1), dim3(1024), 0, s, M);
     NSGPU_HIP(hipGetLastError());
@@ -2534,9 +2558,12 @@ static int build_graph(nsgpu_p2p *h, bool df = false) {
 
 // A run that set the engine's error word: capacity exceeded (the simulation is truncated).
 static int engine_error(uint32_t err) {
-  return set_error(NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, 4 = window limit, "
-                                 "8 = window cut, 16 = a window's remote events beyond the X2 capacity, 256 = deferred "
-                                 "uid resolution (internal), 512 = uids beyond the deferred pipeline's range)", err);
+  return set_error((err & 2048u) ? NSGPU_ERANGE : NSGPU_ENOMEM, "nsgpu_p2p: engine capacity exceeded (code %u: 1 = event pool, 4 = window limit, "
+                                 "8 = window cut, 16 = a window's remote events beyond the X2 capacity, 32 = local "
+                                 "records, 64 = window records, 256 = deferred uid resolution (internal), 512 = uids "
+                                 "beyond the deferred pipeline's range (internal), 2048 = the uid counter would pass "
+                                 "0xfffffffe: DefaultSimulatorImpl's uint32 m_uid wraps there, which the engine does "
+                                 "not replicate)", err);
 }
 
 // Replays the single engine's window pipeline until the run is over (done >= 2) or the pipeline paused
@@ -2550,7 +2577,7 @@ static int drive(nsgpu_p2p *h, bool *paused) {
   // the deferred pipeline while the engine runs normal windows; after a pause (which it flushes) the other
   // pipeline until a replay ends in a normal window
   const bool dfu = df_usable(h);
-  bool df = dfu;
+  bool df = dfu && h->uid_hint < UID_DF_SOFT;
   bool df_of[2] = {false, false};
   if (df && !h->eager && !h->gexec_df) {
     const int rc = build_graph(h, true);
@@ -2591,7 +2618,8 @@ static int drive(nsgpu_p2p *h, bool *paused) {
         have_prev = false;
         continue;
       }
-      if (!df && dfu && c.mode == MODE_NORMAL) {  // a normal window ended the replay: back to the deferred pipeline
+      if (!df && dfu && c.mode == MODE_NORMAL && c.uid < UID_DF_SOFT) {  // a normal window ended the replay: back
+                                                                        // to the deferred pipeline
         // (not in a sorted run's chunks: those belong to the other pipeline until the run is over)
         if (!h->eager && !h->gexec_df) {
           const int rc = build_graph(h, true);
@@ -2683,6 +2711,7 @@ extern "C" int nsgpu_p2p_advance(nsgpu_p2p *h, uint64_t hts, uint32_t huid, uint
   }
   hipLaunchKernelGGL(k_host_resume, dim3(1), dim3(1), 0, h->s, h->M, hts, huid, *uid, *dispatched);
   NSGPU_HIP(hipGetLastError());
+  h->uid_hint = *uid;
   bool paused = false;
   const int rc = drive(h, &paused);
   if (rc) return rc;
@@ -2692,6 +2721,7 @@ extern "C" int nsgpu_p2p_advance(nsgpu_p2p *h, uint64_t hts, uint32_t huid, uint
   NSGPU_HIP(hipStreamSynchronize(h->s));
   if (err) return engine_error(err);
   *uid = h->snap[0].uid;
+  h->uid_hint = *uid;
   *dispatched = h->snap[0].K;
   *ended = paused ? 0 : 1;
   NSGPU_HIP(hipEventRecord(h->ev[0], h->s));
@@ -2740,6 +2770,7 @@ extern "C" int nsgpu_p2p_inject_send(nsgpu_p2p *h, uint32_t app, uint64_t now, u
   uint32_t outv[2];
   NSGPU_HIP(hipMemcpyAsync(outv, h->M.s_val, sizeof(outv), hipMemcpyDeviceToHost, s));
   NSGPU_HIP(hipStreamSynchronize(s));
+  if ((uint64_t)*uid + (uint32_t)(outv[0] - *uid) > UID_MAX_NEXT) return nsgpu::uid_range_error("nsgpu_p2p_inject_send");
   *uid = outv[0];
   *trace_seq = outv[1];
   return NSGPU_OK;
@@ -2923,7 +2954,7 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
   int ns = 0;
   bool used[NKERN] = {};  // the engine's window launches kernel k (its events are recorded)
   const bool dfu = df_usable(h);
-  bool df = dfu;
+  bool df = dfu && h->uid_hint < UID_DF_SOFT;
   // the run control is read after every window (so no sampled pass is a paused no-op and the
   // host-driven steps run as soon as the pipeline asks)
   for (uint64_t w = 0; rc == NSGPU_OK; w++) {
@@ -2952,7 +2983,8 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
         df = false;
       }
       if (rc == NSGPU_OK) rc = host_step(h, h->snap[0], h->s);
-    } else if (!df && dfu && h->snap[0].mode == MODE_NORMAL) {  // (sorted-run chunks stay on the other pipeline)
+    } else if (!df && dfu && h->snap[0].mode == MODE_NORMAL && h->snap[0].uid < UID_DF_SOFT) {  // (sorted-run
+                                                                                             //  chunks stay on the other pipeline)
       df = true;
     }
   }
@@ -3189,5 +3221,12 @@ extern "C" int nsgpu_p2p_group_run(nsgpu_p2p_group *g, void *stream) {
   NSGPU_HIP(hipEventRecord(g->ev[0], g->s));
   NSGPU_HIP(hipEventSynchronize(g->ev[0]));
   NSGPU_HIP(hipStreamWaitEvent(cs, g->ev[0], 0));
+  uint32_t err = 0;
+  for (nsgpu_p2p *m : g->m) {  // (as nsgpu_p2p_run: a member's error word fails the run)
+    uint32_t e = 0;
+    NSGPU_HIP(hipMemcpy(&e, m->M.error, 4, hipMemcpyDeviceToHost));
+    err |= e;
+  }
+  if (err) return engine_error(err);
   return NSGPU_OK;
 }

@@ -24,7 +24,7 @@
 // compacts it (k_cmp).
 
 enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3, MODE_HOST = 4, MODE_CUT = 5,
-                  MODE_TRIM = 6 };
+                  MODE_TRIM = 6, MODE_UIDX = 7 };  // UIDX: the deferred pipeline hands over (uids near UID_DF_SOFT)
 constexpr uint64_t TOMB = ~0ull;        // ev_ts of a free pool slot
 constexpr uint32_t NOSRC = 0xffffffffu;
 constexpr int NHUB = 32;                // hub blocks of k2_handle
@@ -1054,7 +1054,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
           a = lq.dev[qh * HB];
           qh++;
           kw = K_TX_COMPLETE;
-          E.uid = LOCALBIT | s;
+          E.uid = s, E.tloc = true;
           E.demote = false;
         } else {
           s = my[it];
@@ -1072,7 +1072,7 @@ __device__ __forceinline__ void handle_node2(const P2PDev &M, Ctl &C, uint32_t i
             a = M.wa[base + s];
             pk = M.wpkt[base + s];
           }
-          E.uid = (uint32_t)key;
+          E.uid = (uint32_t)key, E.tloc = false;
           E.demote = rel == slo || rel == shi;
         }
         E.now = tmin + rel;
@@ -1246,7 +1246,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
       E.now = tmin + (key >> 32);
       E.slot0 = s * M.maxc;
       E.n = h.n;
-      E.uid = (uint32_t)key;
+      E.uid = (uint32_t)key, E.tloc = false;
       E.trseq = h.seq;
       E.demote = false;
       hs.cancelled += h.cancelled;
@@ -1472,7 +1472,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
         c_pkt[bq] = p;
         if (sl) {
           E.now = tmin + (key >> 32);
-          E.uid = (uint32_t)key;
+          E.uid = (uint32_t)key, E.tloc = false;
           E.trseq = 0;
           HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, ctx, 0};
           if (kind == K_TX_COMPLETE) {
@@ -1531,7 +1531,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
             E.now = tmin + rel;
             E.slot0 = s * M.maxc;
             E.n = 0;
-            E.uid = (uint32_t)c_key[q];
+            E.uid = (uint32_t)c_key[q], E.tloc = false;
             E.trseq = 0;
             E.demote = rel == slo || rel == shi;
             const NodeOut o = node_part(M, E, c_kind[q], c_a[q], c_pkt[q], sink, hs, true);
@@ -1642,7 +1642,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
         E.now = tmin + lrel;
         E.slot0 = s * M.maxc;
         E.n = 0;
-        E.uid = LOCALBIT | s;
+        E.uid = s, E.tloc = true;
         E.trseq = 0;
         E.demote = false;
         E.lj = -1;
@@ -1681,7 +1681,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
           E.now = tmin + rel;
           E.slot0 = s * M.maxc;
           E.n = h.n;
-          E.uid = (uint32_t)key;
+          E.uid = (uint32_t)key, E.tloc = false;
           E.trseq = h.seq;
           E.demote = rel == slo || rel == shi;
           E.lj = -1;
@@ -2178,8 +2178,8 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
   const uint64_t pchild = tc - tinl - Lt;  // (the local records' uids were consumed, they ran in the window)
   C.pchild = pchild;
   bool done = stop_seen || (live2 + pchild == 0 && hts == ~0ull);
-  if ((uint64_t)uid + tc >= (uint64_t)UID_DF_LIMIT) {  // (provisional uids must stay above every real one)
-    atomicOr(M.error, 512u);
+  if ((uint64_t)uid + tc >= (uint64_t)UID_DF_LIMIT) {  // (provisional uids must stay above every real one;
+    atomicOr(M.error, 512u);                           //  unreachable: the pause below hands over first)
     done = true;
   }
   const uint64_t span = c_bound >> 32;  // wide windows: keep them inside the window capacity
@@ -2206,6 +2206,8 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
     C.mode = MODE_HOST;
   } else if (P_end2 > 65536 && live2 * 4 < P_end2) {
     C.mode = MODE_COMPACT;
+  } else if ((uint64_t)uid + tc >= (uint64_t)UID_DF_SOFT) {  // uids near the provisional range: the scanning
+    C.mode = MODE_UIDX;                                        // pipeline takes over for the rest of the run
   }
 }
 
@@ -2706,7 +2708,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
     C.K = bk.K + N + tinl;
     C.uid = bk.uid + tc;
     C.pchild = tc - tinl - Lt;  // (the local records' uids were consumed, they ran in the window)
-    if (M.trace && (uint64_t)bk.uid + tc >= (1ull << 31)) atomicOr(M.error, 128u);  // (LOCALBIT trace uids)
     C.nfree = nfree - consumed + npush;
     const uint64_t P_end = bk.P_end + (nF > nfree ? nF - nfree : 0);
     const uint64_t live = bk.live - npush + nF;
@@ -2756,6 +2757,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
       atomicOr(M.error, 4u);
       done = true;
     }
+    if ((uint64_t)bk.uid + tc > (uint64_t)UID_MAX_NEXT) {  // (fails before any child with a wrapped uid runs)
+      atomicOr(M.error, 2048u);
+      done = true;
+    }
     if (done) {
       C.done = 1;
       if (mode == MODE_TRIM) mode = MODE_NORMAL;  // (the final window is appended by the next k2_pa)
@@ -2803,15 +2808,17 @@ __global__ __launch_bounds__(256) void k_xlate(const P2PDev M) {
 }
 
 // ---- local records' trace uids (traced wide engines): records made by this window's handlers carry
-// LOCALBIT | record until k2_scan has assigned the record's uid
+// their record index (flagged in pad_) until k2_scan has assigned the record's uid
 __global__ __launch_bounds__(256) void k_tpatch(const P2PDev M) {
   const Ctl &C = *M.C;
   if (!M.trace || C.plt == 0) return;
   const uint64_t t0 = C.tn0, tn = *M.trace_n;
   const uint64_t t1 = tn < M.trace_cap ? tn : M.trace_cap;
   for (uint64_t i = t0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < t1; i += (uint64_t)gridDim.x * 256) {
-    const uint32_t u = M.trace[i].uid;
-    if (u & LOCALBIT) M.trace[i].uid = (uint32_t)M.pwkey[u & ~LOCALBIT];
+    if (M.trace[i].pad_) {  // a local record's: uid holds its record index
+      M.trace[i].uid = (uint32_t)M.pwkey[M.trace[i].uid];
+      M.trace[i].pad_ = 0;
+    }
   }
 }
 
@@ -3052,6 +3059,9 @@ __global__ __launch_bounds__(1024) void k_trim(const P2PDev M) {
     C.mode = MODE_NORMAL;
   }
 }
+__global__ void k_after_uidx(const P2PDev M) {
+  if (M.C->mode == MODE_UIDX) M.C->mode = MODE_NORMAL;
+}
 __global__ void k_after_compact(const P2PDev M, uint64_t live) {
   M.C->P_end = live;
   M.C->live = live;
@@ -3098,7 +3108,7 @@ __global__ void k_inject(const P2PDev M, uint32_t a, uint64_t now, uint32_t cur,
   E.wndw = ~0ull;
   E.lim_abs = 0;  // (no window is forming: the children are pending)
   E.lj = -1;
-  E.uid = cur;
+  E.uid = cur, E.tloc = false;
   E.trseq = seq;
   E.demote = false;
   const uint32_t sz = M.app_pkt_size[a];

@@ -49,6 +49,8 @@ struct nsgpu_sim {
   void *stream = nullptr;
   bool stop = false, ended = false, dev_stopped = false;
   uint32_t uid = 4;
+  uint32_t uid_first = 4;  // m_uid before the program's first Schedule call (nsgpu_sim_set_next_uid)
+  bool uid_spent = false;  // a Schedule call hit the uid limit (a closure's call fails; the run then fails too)
   uint32_t cur_uid = 0;
   uint64_t cur_ts = 0;
   uint32_t cur_ctx = 0xffffffffu;
@@ -91,7 +93,12 @@ struct nsgpu_sim {
     e->gen++;
     free_slots.push_back((uint32_t)(handle >> 1));
   }
+  int spent(const char *where) {
+    uid_spent = true;
+    return nsgpu::uid_range_error(where);
+  }
   int insert(uint64_t ts, uint32_t ctx, uint64_t handle, uint32_t *out_uid) {
+    if (uid >= nsgpu::UID_NEXT_MAX) return spent("nsgpu_sim: Schedule");
     const nsgpu_event ev{ts, uid, ctx, handle};
     if (out_uid) *out_uid = uid;
     uid++;
@@ -153,7 +160,7 @@ int nsgpu_sim_free(nsgpu_sim *s) {
 // Schedule calls precede the program's), so the runtime continues from the engine's post-setup uid.
 int nsgpu_sim_attach_p2p(nsgpu_sim *s, nsgpu_p2p *h) {
   if (!s || !h) return set_error(NSGPU_EINVAL, "nsgpu_sim_attach_p2p: null");
-  if (s->events->size || s->dispatched || s->uid != 4)
+  if (s->events->size || s->dispatched || s->uid != s->uid_first)
     return set_error(NSGPU_ESTATE, "nsgpu_sim_attach_p2p: attach before scheduling");
   uint32_t u = 0;
   int rc = nsgpu_p2p_setup_uid(h, &u);
@@ -254,8 +261,20 @@ int nsgpu_sim_insert(nsgpu_sim *s, uint64_t ts, uint32_t ctx, uint64_t handle, u
   return s->insert(ts, ctx, handle | RAW, uid);
 }
 
+// m_uid before anything is scheduled: the uids below `uid` count as consumed by Schedule calls this runtime did
+// not see (default-simulator-impl.cc:52-56 starts at 4).  Only on a fresh runtime.
+int nsgpu_sim_set_next_uid(nsgpu_sim *s, uint32_t uid) {
+  if (!s) return set_error(NSGPU_EINVAL, "nsgpu_sim_set_next_uid: null");
+  if (s->events->size || s->dispatched || s->uid != s->uid_first || !s->destroy_events.empty() || s->p2p || s->wifi)
+    return set_error(NSGPU_ESTATE, "nsgpu_sim_set_next_uid: the runtime has scheduled or attached something already");
+  if (uid < 4) return set_error(NSGPU_EINVAL, "nsgpu_sim_set_next_uid: uids 0, 1, 2 (and 3) are reserved");
+  s->uid = s->uid_first = uid;
+  return NSGPU_OK;
+}
+
 int nsgpu_sim_consume_uid(nsgpu_sim *s, uint32_t *uid) {  // ScheduleDestroy's uid (:235-242)
   if (!s) return set_error(NSGPU_EINVAL, "nsgpu_sim_consume_uid: null");
+  if (s->uid >= nsgpu::UID_NEXT_MAX) return s->spent("nsgpu_sim_consume_uid");
   if (uid) *uid = s->uid;
   s->uid++;
   return NSGPU_OK;
@@ -265,6 +284,7 @@ int nsgpu_sim_consume_uid(nsgpu_sim *s, uint32_t *uid) {  // ScheduleDestroy's u
 // :306-322): the runtime keeps the list, the caller keeps the reference each entry holds.
 int nsgpu_sim_destroy_insert(nsgpu_sim *s, uint64_t handle, uint64_t *ts) {  // ScheduleDestroy
   if (!s || (handle & RAW)) return set_error(NSGPU_EINVAL, "nsgpu_sim_destroy_insert: null runtime or odd handle");
+  if (s->uid >= nsgpu::UID_NEXT_MAX) return s->spent("nsgpu_sim_destroy_insert");
   s->destroy_events.push_back(DestroyEv{handle | RAW, s->cur_ts});
   s->uid++;
   if (ts) *ts = s->cur_ts;
@@ -326,6 +346,7 @@ int nsgpu_sim_remove_key(nsgpu_sim *s, uint64_t ts, uint32_t uid, uint32_t ctx, 
 // (RunOneEvent).
 static int pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n, bool force) {
   *n = 0;
+  if (s->uid_spent) return nsgpu::uid_range_error("nsgpu_sim: Run after a Schedule call failed at the uid limit");
   s->win.clear();
   s->win_next = 0;
   if (!s->win_removed.empty()) s->win_removed.clear();
@@ -610,6 +631,7 @@ int nsgpu_sim_wifi_send(nsgpu_sim *s, uint32_t phy, uint32_t size, double dbm, u
   uint32_t n = 0;
   int rc = nsgpu_wifil_receivers(s->wifi, phy, &n);
   if (rc) return rc;
+  if ((uint64_t)s->uid + n > nsgpu::UID_NEXT_MAX) return s->spent("nsgpu_sim_wifi_send");
   rc = nsgpu_wifil_send(s->wifi, s->cur_ts, s->uid, phy, size, dbm, modclass, rate, bw, preamble);
   if (rc) return rc;
   s->uid += n;

@@ -1379,6 +1379,10 @@ extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base,
                                 uint32_t modclass, uint64_t rate, uint32_t bw, uint32_t preamble) {
   if (!h || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_send: bad phy");
   if (h->n_tx >= h->tx_cap) return set_error(NSGPU_ENOMEM, "nsgpu_wifil_send: tx_cap SendPacket calls");
+  uint32_t nrx = 0;
+  int rc0 = nsgpu_wifil_receivers(h, phy, &nrx);
+  if (rc0) return rc0;
+  if ((uint64_t)uid_base + nrx > nsgpu::UID_NEXT_MAX) return nsgpu::uid_range_error("nsgpu_wifil_send");
   int64_t dur = 0;
   int rc = nsgpu_wifi_tx_duration_ns(size, modclass, rate, bw, preamble, &dur);  // CalculateTxDuration
   if (rc) return rc;
@@ -1471,6 +1475,8 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   std::sort(h->ends_epoch.begin(), h->ends_epoch.end(),
             [](const nsgpu_wifil_end &a, const nsgpu_wifil_end &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
   h->ends.insert(h->ends.end(), h->ends_epoch.begin(), h->ends_epoch.end());
+  if ((uint64_t)*uid + nsync > nsgpu::UID_NEXT_MAX)  // (the epoch's EndReceives are queued, none dispatched yet)
+    return nsgpu::uid_range_error("nsgpu_wifil_advance");
   *uid += nsync;
   return NSGPU_OK;
 }

@@ -104,6 +104,7 @@ SIGNATURES = {
     "nsgpu_sim_destroy": (C.c_int, [_vp]),
     "nsgpu_sim_state": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "nsgpu_sim_current_uid": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_set_next_uid": (C.c_int, [_vp, _u32]),
     "nsgpu_sim_next": (C.c_int, [_vp, _vp, _vp]),
     "nsgpu_sim_set_stop": (C.c_int, [_vp, C.c_int]),
     "nsgpu_sim_drain": (C.c_int, [_vp, _vp, _u32, _vp]),
@@ -653,6 +654,10 @@ class Sim:
         u = C.c_uint32()
         check(lib().nsgpu_sim_current_uid(self.h, C.byref(u)))
         return u.value
+
+    def set_next_uid(self, uid):
+        """m_uid before anything is scheduled (the uids below it were consumed by calls this runtime did not see)."""
+        check(lib().nsgpu_sim_set_next_uid(self.h, uid))
 
     # ---- windows (the pull interface ns3::HipSimulatorImpl uses) ----
     def insert_raw(self, ts, ctx, handle):

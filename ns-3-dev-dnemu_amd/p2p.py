@@ -44,7 +44,7 @@ class ScenarioStruct(C.Structure):
         ("setup_kind", C.c_void_p), ("setup_index", C.c_void_p),
         ("app_count", C.c_void_p), ("app_interval_ns", C.c_void_p), ("app_src_slot", C.c_void_p),
         ("route_default", C.c_void_p), ("route_exc_off", C.c_void_p), ("route_exc_slot", C.c_void_p),
-        ("route_exc_dev", C.c_void_p),
+        ("route_exc_dev", C.c_void_p), ("uid_first", C.c_uint32), ("pad_uid_", C.c_uint32),
     ]
 
 
@@ -67,6 +67,7 @@ class Scenario:
 
     def __init__(self, n_nodes, icmp=False):
         self.icmp = icmp  # ICMP errors generated and routed back to senders (nsgpu_p2p_scenario.icmp)
+        self.uid_first = 0  # m_uid before the first setup call (0: 4, DefaultSimulatorImpl's start)
         self.n_nodes = 0
         self.dev = []     # (node, peer, bps, ifg, delay, qmax)
         self.apps = []    # dicts
@@ -270,6 +271,7 @@ class Scenario:
         s.stop_ns = self.stop_ns
         s.n_setup = len(self.setup)
         s.icmp = 1 if self.icmp else 0
+        s.uid_first = self.uid_first
         s._keep = arrays  # keep the arrays alive with the struct
         return s
 

@@ -91,6 +91,7 @@ typedef struct nsref_sim nsref_sim;
 
 nsref_sim *nsref_sim_new(int scheduler);
 void       nsref_sim_free(nsref_sim *s);
+void       nsref_sim_set_uid(nsref_sim *s, uint32_t uid);  /* m_uid (a uint32: it wraps like the reference's) */
 nsgpu_event_id nsref_sim_schedule(nsref_sim *s, int64_t delay, nsref_fn fn, void *user, uint64_t arg);
 void       nsref_sim_schedule_with_context(nsref_sim *s, uint32_t ctx, int64_t delay, nsref_fn fn, void *user, uint64_t arg);
 nsgpu_event_id nsref_sim_schedule_now(nsref_sim *s, nsref_fn fn, void *user, uint64_t arg);
@@ -181,6 +182,7 @@ typedef struct nsref_wifil_mac {
   uint64_t period, stop_ts, rate;
   uint32_t size, modclass, bw, preamble;
   double dbm;
+  uint32_t uid_first, pad_;  /* m_uid before the setup calls (0: 4) */
 } nsref_wifil_mac;
 int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, uint64_t *log_ts, uint32_t *log_uid,
                     uint32_t *log_ctx, uint64_t log_cap, nsgpu_wifil_end *ends, uint64_t ends_cap, uint64_t *n_ends,

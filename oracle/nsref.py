@@ -100,6 +100,7 @@ def lib():
         L.nsref_sim_new.argtypes = [C.c_int]
         L.nsref_sim_new.restype = C.c_void_p
         L.nsref_sim_free.argtypes = [C.c_void_p]
+        L.nsref_sim_set_uid.argtypes = [C.c_void_p, C.c_uint32]
         L.nsref_sim_schedule.argtypes = [C.c_void_p, C.c_int64, EVENT_FN, C.c_void_p, C.c_uint64]
         L.nsref_sim_schedule.restype = EventId
         L.nsref_sim_schedule_with_context.argtypes = [C.c_void_p, C.c_uint32, C.c_int64, EVENT_FN, C.c_void_p,
@@ -353,6 +354,9 @@ class Sim:
     def next_uid(self):
         return self.L.nsref_sim_next_uid(self.h)
 
+    def set_next_uid(self, uid):
+        self.L.nsref_sim_set_uid(self.h, uid)
+
     def close(self):
         if self.h:
             self.L.nsref_sim_free(self.h)
@@ -466,11 +470,11 @@ def wifi_run(scenario_struct, stats_struct, phys, tx_base, end_dtype, rx_log=Non
 class WifilMacStruct(C.Structure):  # nsref_wifil_mac (nsref.h)
     _fields_ = [("first", C.c_void_p), ("backoff", C.c_void_p), ("period", C.c_uint64), ("stop_ts", C.c_uint64),
                 ("rate", C.c_uint64), ("size", C.c_uint32), ("modclass", C.c_uint32), ("bw", C.c_uint32),
-                ("preamble", C.c_uint32), ("dbm", C.c_double)]
+                ("preamble", C.c_uint32), ("dbm", C.c_double), ("uid_first", C.c_uint32), ("pad_", C.c_uint32)]
 
 
 def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble, dbm, n_phy, end_dtype,
-              phys_dtype, log_cap=1 << 20):
+              phys_dtype, log_cap=1 << 20, uid_first=0):
     """The closed-loop oracle run (nsref_wifil_run): the MAC stand-in of nsref.h over the PHY.  Returns
     (pop log (ts, uid, ctx), EndReceive records in dispatch order, per-phy counters, dict of totals)."""
     f = lib().nsref_wifil_run
@@ -480,7 +484,7 @@ def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble,
     first = np.ascontiguousarray(first, np.uint64)
     backoff = np.ascontiguousarray(backoff, np.uint64)
     m = WifilMacStruct(first.ctypes.data, backoff.ctypes.data, period, stop_ts, mode[1], size, mode[0], mode[2],
-                       preamble, dbm)
+                       preamble, dbm, uid_first, 0)
     lts = np.zeros(log_cap, np.uint64)
     luid = np.zeros(log_cap, np.uint32)
     lctx = np.zeros(log_cap, np.uint32)

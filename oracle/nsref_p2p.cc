@@ -390,6 +390,7 @@ struct Model {
     for (uint32_t a : node_apps[n]) app_object_start(a);
   }
   void setup() {
+    if (s.uid_first) sim.m_uid = s.uid_first;  // the program's earlier Schedule calls consumed the uids below it
     dev.resize(s.n_devices);
     app.resize(s.n_apps);
     node_apps.assign(s.n_nodes, {});

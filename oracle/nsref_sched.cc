@@ -26,6 +26,7 @@ extern "C" {
 
 nsref_sim *nsref_sim_new(int scheduler) { return new nsref_sim(scheduler); }
 void nsref_sim_free(nsref_sim *s) { delete s; }
+void nsref_sim_set_uid(nsref_sim *s, uint32_t uid) { s->m_uid = uid; }
 nsgpu_event_id nsref_sim_schedule(nsref_sim *s, int64_t delay, nsref_fn fn, void *user, uint64_t arg) {
   EventImpl *e = new CEvent(fn, user, arg);
   s->pin(e);

@@ -865,6 +865,7 @@ int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, u
   L.edW = Loop::DbmToW(cfg->ed_threshold_dbm);
   L.ccaW = Loop::DbmToW(cfg->cca_threshold_dbm);
   L.noiseFigure = pow(10.0, cfg->rx_noise_figure_db / 10.0);  // DbToRatio (SetRxNoiseFigure, yans-wifi-phy.cc:192-197)
+  if (mac->uid_first) L.uid = mac->uid_first;  // (a uint32: it wraps after 0xffffffff as the reference's m_uid does)
   // setup: the attempts in phy order, then Stop (Time)
   for (int64_t i = 0; i < cfg->n_phy; i++) L.schedule(mac->first[i], Loop::E{Loop::ATTEMPT, (uint32_t)i, 0, 0xffffffffu, 0.0});
   L.schedule(mac->stop_ts, Loop::E{Loop::STOP, 0, 0, 0xffffffffu, 0.0});

@@ -16,9 +16,9 @@ PHY_FIELDS = ("rx", "sync", "drop_rx", "drop_tx", "drop_ed", "cca_switches", "en
               "end_tx", "end_rx", "end_cca_busy", "rxing")
 
 
-def check(sc, log_cap=1 << 20):
-    olog, oends, ophys, otot = run_oracle(sc, log_cap)
-    glog, gends, gphys, gtot, _keep = run_gpu(sc, log_cap)
+def check(sc, log_cap=1 << 20, uid_first=0):
+    olog, oends, ophys, otot = run_oracle(sc, log_cap, uid_first=uid_first)
+    glog, gends, gphys, gtot, _keep = run_gpu(sc, log_cap, uid_first=uid_first)
     for f in ("dispatched", "digest", "next_uid", "final_ts", "sends", "busy"):
         assert gtot[f] == otot[f], (f, gtot[f], otot[f])
     for a, b in zip(glog, olog):

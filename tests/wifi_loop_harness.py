@@ -23,19 +23,22 @@ def scenario(n_side=4, spacing=100.0, seed=1, period=20_000_000, stop_ns=200_000
                 preamble=preamble, dbm=dbm)
 
 
-def run_oracle(sc, log_cap=1 << 20):
+def run_oracle(sc, log_cap=1 << 20, uid_first=0):
     ph = sc["phys"]
     cfg = ph.c_struct()
     log, ends, phys, tot = nsref.wifil_run(cfg, sc["first"], sc["backoff"], sc["period"], sc["stop_ns"], sc["size"],
                                            sc["mode"], sc["preamble"], sc["dbm"], ph.n_phy, wifi.WIFIL_END_DTYPE,
-                                           wifi.PHY_COUNTERS_DTYPE, log_cap)
+                                           wifi.PHY_COUNTERS_DTYPE, log_cap, uid_first=uid_first)
     return log, ends, phys, tot
 
 
-def run_gpu(sc, log_cap=1 << 20):
+def run_gpu(sc, log_cap=1 << 20, uid_first=0):
+    """uid_first: m_uid before the setup calls (nsgpu_sim_set_next_uid; 0: the reference's 4)."""
     import nsgpu
     ph = sc["phys"]
     sim = nsgpu.Sim()
+    if uid_first:
+        sim.set_next_uid(uid_first)
     lp = wifi.LoopPhy(ph)
     sim.attach_wifi(lp)
     sim.set_log(log_cap)
