@@ -204,15 +204,22 @@ int nsgpu_sim_schedule(nsgpu_sim *s, int64_t delay, nsgpu_event_fn fn, void *use
   const int64_t t = delay + (int64_t)s->cur_ts;
   if (t < 0 || t < (int64_t)s->cur_ts) return set_error(NSGPU_EINVAL, "Schedule: negative absolute time");
   const uint64_t h = s->make(fn, user, arg);
-  uint32_t u;
+  uint32_t u = 0;
   const int rc = s->insert((uint64_t)t, s->cur_ctx, h, &u);
+  if (rc) {
+    s->release(h);
+    return rc;
+  }
   if (id) *id = nsgpu_event_id{h, (uint64_t)t, s->cur_ctx, u};
   return rc;
 }
 
 int nsgpu_sim_schedule_with_context(nsgpu_sim *s, uint32_t ctx, int64_t delay, nsgpu_event_fn fn, void *user,
                                     uint64_t arg) {  // :206-219
-  return s->insert(s->cur_ts + (uint64_t)delay, ctx, s->make(fn, user, arg), nullptr);
+  const uint64_t h = s->make(fn, user, arg);
+  const int rc = s->insert(s->cur_ts + (uint64_t)delay, ctx, h, nullptr);
+  if (rc) s->release(h);
+  return rc;
 }
 
 int nsgpu_sim_schedule_now(nsgpu_sim *s, nsgpu_event_fn fn, void *user, uint64_t arg, nsgpu_event_id *id) {
@@ -220,6 +227,7 @@ int nsgpu_sim_schedule_now(nsgpu_sim *s, nsgpu_event_fn fn, void *user, uint64_t
 }
 
 int nsgpu_sim_schedule_destroy(nsgpu_sim *s, nsgpu_event_fn fn, void *user, uint64_t arg, nsgpu_event_id *id) {
+  if (s->uid >= nsgpu::UID_NEXT_MAX) return s->spent("nsgpu_sim_schedule_destroy");
   const uint64_t h = s->make(fn, user, arg);  // :235-242
   s->destroy_events.push_back(DestroyEv{h, s->cur_ts});
   s->uid++;
