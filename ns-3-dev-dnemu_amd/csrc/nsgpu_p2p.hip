@@ -1651,6 +1651,12 @@ struct nsgpu_p2p {
   Ctl *snap = nullptr;            // pinned, 2 run-control snapshots (single engine)
   float last_ms = 0.f;
   bool eager = getenv("NSGPU_P2P_EAGER") != nullptr;  // kernels one by one instead of graph replays
+  // NSGPU_P2P_POISON=1: every device array is filled with 0xa5 bytes when allocated, before create initialises
+  // it (a deterministic stand-in for device memory a previous engine dirtied: create must zero what it reads)
+  bool poison = [] {
+    const char *e = getenv("NSGPU_P2P_POISON");
+    return e && e[0] == '1';
+  }();
   // pristine initial pool (device) for resets
   uint64_t *init_ts = nullptr;
   uint32_t *init_uid = nullptr, *init_ctx = nullptr, *init_kind = nullptr, *init_a = nullptr;
@@ -1669,6 +1675,7 @@ int dalloc(nsgpu_p2p *h, T **p, size_t n) {
   if (e != hipSuccess) return set_error(NSGPU_ENOMEM, "nsgpu_p2p: hipMalloc(%zu): %s", n * sizeof(T),
                                         hipGetErrorString(e));
   h->allocs.push_back(q);
+  if (h->poison) NSGPU_HIP(hipMemset(q, 0xa5, (n ? n : 1) * sizeof(T)));
   *p = (T *)q;
   return NSGPU_OK;
 }

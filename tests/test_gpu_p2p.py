@@ -95,3 +95,49 @@ def test_setup_list_from_journal_app_before_a_device():
     o, g = both(sc, log_cap=20000)
     assert o[2]["rx_packets"][0] > 0
     assert_same(o, g)
+
+
+def test_stop_before_start_bounded_by_a_far_stop():
+    """r04c's scenario (OnOff StartTime 0.1 s, StopTime 0.02 s: the flow never stops, application.cc:87-95) with
+    an explicit Simulator::Stop at 3 s: full pop log = the oracle's (without the Stop the run is unbounded in ns-3
+    too; tests/test_p2p_oracle.py pins the semantics)."""
+    sc = p2p.grid(2, 2, start_ns=100_000_000, stop_ns=20_000_000, sim_stop_ns=3_000_000_000, flows=[(0, 3)])
+    o, g = both(sc, log_cap=20_000)
+    assert o[2]["tx_packets"].sum() > 300
+    assert_same(o, g)
+
+
+@pytest.mark.parametrize("which", ["grid", "random", "dumbbell_hubs", "partitioned", "traced"])
+def test_poisoned_device_memory(which, monkeypatch):
+    """r04b: the fault came from device memory a previous engine had dirtied (create did not zero the deferred
+    pipeline's arrays).  NSGPU_P2P_POISON=1 fills every array with 0xa5 bytes when it is allocated, before create
+    initialises it: each pipeline (deferred, hub blocks, partitioned, traced) must still equal the oracle."""
+    monkeypatch.setenv("NSGPU_P2P_POISON", "1")
+    if which == "grid":
+        sc = p2p.grid(12, 12)
+        eng = p2p.Engine(sc, log_cap=60_000)
+        assert eng.wide()
+        o = both(sc, log_cap=60_000)[0]
+        assert_same(o, eng.run(log_n=60_000))
+    elif which == "random":
+        o, g = both(p2p.random_topology(15, 25, 8, 3), log_cap=300_000)
+        assert_same(o, g)
+    elif which == "dumbbell_hubs":
+        o, g = both(p2p.dumbbell(2000), log_cap=0)
+        assert_same(o, g, log=False)
+    elif which == "partitioned":
+        sc = p2p.grid(6, 6)
+        o = both(sc, log_cap=0)[0]
+        st = p2p.LoopbackGroup(sc, 3).run()[0]
+        assert (st.dispatched, st.digest, st.next_uid) == (o[0].dispatched, o[0].digest, o[0].next_uid)
+    else:
+        from test_gpu_trace import assert_same_trace, oracle_trace
+        import trace
+        g = p2p.grid(4, 4, qmax=3, rate_bps=4_000_000, stop_ns=300_000_000, sim_stop_ns=400_000_000,
+                     flows=[(0, 15), (1, 15), (4, 15), (5, 15)])
+        _ost, odevc, otr = oracle_trace(g)
+        eng = p2p.Engine(g)
+        eng.set_trace(len(otr) + 16)
+        _st, gdevc, _appc, _log = eng.run()
+        assert np.array_equal(gdevc, odevc)
+        assert_same_trace(g, otr, trace.sort_records(eng.trace()))

@@ -57,3 +57,25 @@ def test_random_topology_queue_conservation():
         n = int(min(st.dispatched, 200000))
         key = lts[:n].astype(object) * (1 << 32) + luid[:n].astype(object)
         assert all(key[i] < key[i + 1] for i in range(n - 1))
+
+
+def test_stop_application_before_start_leaves_the_flow_running():
+    """Application::DoStart (src/network/model/application.cc:87-95) schedules StartApplication at StartTime and,
+    when StopTime != 0, StopApplication at StopTime — with StopTime < StartTime the stop runs first (it cancels
+    nothing yet) and the flow then runs until Simulator::Stop: the same packets as a flow that never stops.
+    (Round 4's r04c GPU run used this scenario without a Simulator::Stop: unbounded in ns-3 as well.)"""
+    def run(app_stop):
+        sc = p2p.grid(2, 2, start_ns=100_000_000, stop_ns=app_stop, sim_stop_ns=1_000_000_000, flows=[(0, 3)])
+        s = sc.c_struct()
+        st = p2p.P2PStats()
+        devc = np.zeros(s.n_devices, p2p.DEV_COUNTERS_DTYPE)
+        appc = np.zeros(s.n_apps, p2p.APP_COUNTERS_DTYPE)
+        nsref.p2p_run(s, st, devc, appc, 0)
+        onoff = [i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_ONOFF][0]
+        return st, appc, onoff
+    st_early, appc_early, a = run(20_000_000)
+    st_never, appc_never, _ = run(0)
+    assert appc_early["tx_packets"][a] == appc_never["tx_packets"][a] > 100  # (0.9 s / 8.192 ms)
+    assert st_early.final_ts == 1_000_000_000
+    # the stop event is one more dispatch (and one more uid) than the never-stopping flow's run
+    assert st_early.dispatched == st_never.dispatched + 1
