@@ -155,6 +155,13 @@ int nsref_p2p_run_probe(const nsgpu_p2p_scenario *sc, int64_t t0, int64_t period
                         uint32_t *log_ctx, uint64_t log_cap, nsgpu_trace_record *trace, uint64_t trace_cap,
                         uint64_t *trace_n);
 
+/* The same run with host datagrams: after setup, Schedule (ts[k], UdpSocket::Send of one datagram of app[k]'s
+ * flow) for k in order (a replay of a reference pcap's sends). */
+int nsref_p2p_run_sends(const nsgpu_p2p_scenario *sc, uint64_t n, const int64_t *ts, const uint32_t *app,
+                        nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc, nsgpu_app_counters *appc, uint64_t *log_ts,
+                        uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap, nsgpu_trace_record *trace,
+                        uint64_t trace_cap, uint64_t *trace_n);
+
 /* bench-simulator ReadDistribution: (uint64_t)(data * 1000000000)  (bench-simulator.cc:66) */
 uint64_t nsref_distribution_ns(double seconds);
 

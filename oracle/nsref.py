@@ -140,6 +140,8 @@ def lib():
         L.nsref_p2p_run_probe.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_uint32, C.c_uint32, C.c_uint32] + \
             [C.c_void_p] * 7 + [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
         L.nsref_p2p_run_trace.restype = C.c_int
+        L.nsref_p2p_run_sends.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p] + [C.c_void_p] * 6 + \
+            [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
         L.nsref_p2p_set_trace_kinds.argtypes = [C.c_uint32]
         L.nsref_p2p_set_trace_kinds.restype = None
         L.nsref_distribution_ns.argtypes = [C.c_double]
@@ -433,6 +435,26 @@ def p2p_run_probe(scenario_struct, stats_struct, devc, appc, t0, period, count, 
     lib().nsref_p2p_run_probe(*args, tr.ctypes.data, n.value, C.byref(n))
     lib().nsref_p2p_set_trace_kinds(TRACE_DEVICE_KINDS)
     return (lts, luid, lctx), tr, samples
+
+
+def p2p_run_sends(scenario_struct, stats_struct, devc, appc, ts, apps, log_cap=0, kinds=TRACE_DEVICE_KINDS):
+    """p2p run with host datagrams (nsref_p2p_run_sends: Schedule (ts[k], send of app[k]) after setup); returns
+    (log, trace)."""
+    lib().nsref_p2p_set_trace_kinds(kinds)
+    ts = np.ascontiguousarray(ts, np.int64)
+    apps = np.ascontiguousarray(apps, np.uint32)
+    lts = np.zeros(log_cap, np.uint64)
+    luid = np.zeros(log_cap, np.uint32)
+    lctx = np.zeros(log_cap, np.uint32)
+    n = C.c_uint64()
+    args = [C.byref(scenario_struct), len(ts), ts.ctypes.data, apps.ctypes.data, C.byref(stats_struct),
+            devc.ctypes.data, appc.ctypes.data, lts.ctypes.data if log_cap else None,
+            luid.ctypes.data if log_cap else None, lctx.ctypes.data if log_cap else None, log_cap]
+    lib().nsref_p2p_run_sends(*args, None, 0, C.byref(n))
+    tr = np.zeros(n.value, TRACE_RECORD_DTYPE)
+    lib().nsref_p2p_run_sends(*args, tr.ctypes.data, n.value, C.byref(n))
+    lib().nsref_p2p_set_trace_kinds(TRACE_DEVICE_KINDS)
+    return (lts, luid, lctx), tr
 
 
 def wifi_tx_duration(size, modclass, rate_bps, bw_hz, preamble):

@@ -529,6 +529,56 @@ extern "C" int nsref_p2p_run_probe(const nsgpu_p2p_scenario *sc, int64_t t0, int
   return 0;
 }
 
+// A host application's datagrams at given times: right after setup, Simulator::Schedule (ts[k], send k) for k in
+// order; send k is UdpSocket::Send of one datagram of application app[k]'s flow (as the probe's send above).  The
+// replay of a reference pcap's sends (tests/olsr_replay.py: OLSR HELLOs over point-to-point).
+extern "C" int nsref_p2p_run_sends(const nsgpu_p2p_scenario *sc, uint64_t n, const int64_t *ts, const uint32_t *app,
+                                   nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc, nsgpu_app_counters *appc,
+                                   uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap,
+                                   nsgpu_trace_record *trace, uint64_t trace_cap, uint64_t *trace_n) {
+  Model *m = new Model();
+  std::vector<nsgpu_trace_record> tv;
+  if (trace_n) m->trace = &tv;
+  m->tr_kinds = g_trace_kinds;
+  m->s = *sc;
+  m->sim.want_digest = true;
+  m->sim.log_ts = log_ts;
+  m->sim.log_uid = log_uid;
+  m->sim.log_ctx = log_ctx;
+  m->sim.log_cap = log_ts ? log_cap : 0;
+  m->setup();
+  for (uint64_t k = 0; k < n; k++) {
+    const uint32_t a = app[k];
+    m->schedule(ts[k], [m, sc, a]() {
+      App &A = m->app[a];
+      A.c.tx_packets++;
+      A.c.tx_bytes += sc->app_pkt_size[a];
+      m->ip_send(sc->app_node[a], Pkt{a, 0, sc->app_pkt_size[a] + 8 + 20, sc->app_ttl[a]});
+    });
+  }
+  m->sim.Run();
+  memset(stats, 0, sizeof(*stats));
+  stats->dispatched = m->sim.m_dispatched;
+  stats->cancelled = m->sim.m_cancelled;
+  stats->digest = m->sim.m_digest;
+  stats->final_ts = m->sim.m_currentTs;
+  stats->next_uid = m->sim.m_uid;
+  stats->ttl_drops = m->ttl_drops;
+  stats->no_route_drops = m->no_route_drops;
+  stats->unreach_drops = m->unreach_drops;
+  stats->icmp_sent = m->icmp_sent;
+  if (devc)
+    for (uint32_t d = 0; d < sc->n_devices; d++) devc[d] = m->dev[d].c;
+  if (appc)
+    for (uint32_t a = 0; a < sc->n_apps; a++) appc[a] = m->app[a].c;
+  if (trace_n) {
+    *trace_n = tv.size();
+    for (uint64_t i = 0; i < tv.size() && i < trace_cap; i++) trace[i] = tv[i];
+  }
+  delete m;
+  return 0;
+}
+
 extern "C" int nsref_p2p_run(const nsgpu_p2p_scenario *sc, nsgpu_p2p_stats *stats, nsgpu_dev_counters *devc,
                              nsgpu_app_counters *appc, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx,
                              uint64_t log_cap, double *run_seconds) {
