@@ -205,6 +205,9 @@ int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base, uint32_t p
 int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t bound_uid, uint32_t *uid, uint64_t *dispatched,
                         uint64_t *digest, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap);
 int nsgpu_wifil_get_state(nsgpu_wifil *h, uint32_t phy, uint64_t now, nsgpu_wifil_phy_state *out);
+/* MobilityModel::SetPosition of phy's node (src/mobility/model/mobility-model.cc): the later SendPackets'
+ * YansWifiChannel::Send fan-outs (yans-wifi-channel.cc:92-96) read the new position */
+int nsgpu_wifil_set_position(nsgpu_wifil *h, uint32_t phy, double x, double y, double z);
 int nsgpu_wifil_read_ends(nsgpu_wifil *h, nsgpu_wifil_end *out, uint64_t cap, uint64_t *n);  /* since last read */
 int nsgpu_wifil_read_phys(nsgpu_wifil *h, nsgpu_wifi_phy_counters *out);                    /* n_phy */
 int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_ts);
@@ -338,6 +341,8 @@ int nsgpu_sim_attach_wifi(nsgpu_sim *s, nsgpu_wifil *h);
 int nsgpu_sim_wifi_send(nsgpu_sim *s, uint32_t phy, uint32_t size, double dbm, uint32_t modclass, uint64_t rate,
                         uint32_t bw, uint32_t preamble);
 int nsgpu_sim_wifi_state(nsgpu_sim *s, uint32_t phy, nsgpu_wifil_phy_state *out);
+/* a host closure's MobilityModel::SetPosition of phy's node (nsgpu_wifil_set_position on the attached PHY) */
+int nsgpu_sim_wifi_set_position(nsgpu_sim *s, uint32_t phy, double x, double y, double z);
 
 /* ---------------- GPU-resident point-to-point subset (configs 2, 4) ----------------
  * Replaces, for a topology of PointToPointNetDevices, the handler chain

@@ -646,6 +646,12 @@ int nsgpu_sim_wifi_send(nsgpu_sim *s, uint32_t phy, uint32_t size, double dbm, u
   return NSGPU_OK;
 }
 
+// MobilityModel::SetPosition of `phy`'s node from the running closure: the later SendPackets' fan-outs see it.
+int nsgpu_sim_wifi_set_position(nsgpu_sim *s, uint32_t phy, double x, double y, double z) {
+  if (!s || !s->wifi) return set_error(NSGPU_ESTATE, "nsgpu_sim_wifi_set_position: no Wi-Fi PHY attached");
+  return nsgpu_wifil_set_position(s->wifi, phy, x, y, z);
+}
+
 // WifiPhyStateHelper::GetState of `phy` at Now (the device has run every event before the running closure).
 int nsgpu_sim_wifi_state(nsgpu_sim *s, uint32_t phy, nsgpu_wifil_phy_state *out) {
   if (!s || !s->wifi) return set_error(NSGPU_ESTATE, "nsgpu_sim_wifi_state: no Wi-Fi PHY attached");

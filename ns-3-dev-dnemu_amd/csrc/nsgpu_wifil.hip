@@ -1481,6 +1481,20 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   return NSGPU_OK;
 }
 
+// MobilityModel::SetPosition of `phy`'s node (mobility-model.cc SetPosition -> DoSetPosition; e.g. a host closure
+// at run time): YansWifiChannel::Send reads the positions at each send (yans-wifi-channel.cc:92-96), so the
+// later sends' fan-outs see it; receptions already scheduled keep their delay and power.  In stream order with
+// the sends.
+extern "C" int nsgpu_wifil_set_position(nsgpu_wifil *h, uint32_t phy, double x, double y, double z) {
+  if (!h || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_set_position: bad phy");
+  const double v[3] = {x, y, z};
+  double *dst[3] = {const_cast<double *>(h->D.x), const_cast<double *>(h->D.y), const_cast<double *>(h->D.z)};
+  for (int c = 0; c < 3; c++)
+    NSGPU_HIP(hipMemcpyAsync(dst[c] + phy, &v[c], sizeof(double), hipMemcpyHostToDevice, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));  // (v is on this stack)
+  return NSGPU_OK;
+}
+
 // WifiPhyStateHelper::GetState / GetDelayUntilIdle of `phy` at `now` (wifi-phy-state-helper.cc:122-183).
 extern "C" int nsgpu_wifil_get_state(nsgpu_wifil *h, uint32_t phy, uint64_t now, nsgpu_wifil_phy_state *out) {
   if (!h || !out || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_get_state: bad phy");

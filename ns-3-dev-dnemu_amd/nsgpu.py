@@ -123,6 +123,8 @@ SIGNATURES = {
     "nsgpu_sim_attach_wifi": (C.c_int, [_vp, _vp]),
     "nsgpu_sim_wifi_send": (C.c_int, [_vp, _u32, _u32, C.c_double, _u32, _u64, _u32, _u32]),
     "nsgpu_sim_wifi_state": (C.c_int, [_vp, _u32, _vp]),
+    "nsgpu_sim_wifi_set_position": (C.c_int, [_vp, _u32, _d, _d, _d]),
+    "nsgpu_wifil_set_position": (C.c_int, [_vp, _u32, _d, _d, _d]),
     "nsgpu_wifil_create": (C.c_int, [_vp, _vp]),
     "nsgpu_wifil_destroy": (C.c_int, [_vp]),
     "nsgpu_wifil_receivers": (C.c_int, [_vp, _u32, _vp]),
@@ -737,6 +739,10 @@ class Sim:
         """Attach a closed-loop Wi-Fi PHY (wifi.LoopPhy)."""
         check(lib().nsgpu_sim_attach_wifi(self.h, phy.h))
         self._engine = phy
+
+    def wifi_set_position(self, phy, x, y, z):
+        """MobilityModel::SetPosition of `phy`'s node from the running closure."""
+        check(lib().nsgpu_sim_wifi_set_position(self.h, phy, x, y, z))
 
     def wifi_send(self, phy, size, dbm, mode, preamble):
         """YansWifiPhy::SendPacket of `phy` now (mode = (modclass, rate, bandwidth))."""

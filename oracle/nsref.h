@@ -204,6 +204,12 @@ typedef struct nsref_wifil_sends {
   uint32_t modclass, bw, preamble, pad_;
   uint64_t rate, stop_ts;
   double dbm;
+  /* MobilityModel::SetPosition of move_phy[k] to move_xyz[3k..3k+2] at move_ts[k] (host closures scheduled after
+   * the sends, before the Stop) */
+  uint64_t n_moves;
+  const uint64_t *move_ts;
+  const uint32_t *move_phy;
+  const double *move_xyz;
 } nsref_wifil_sends;
 int nsref_wifil_replay(const nsgpu_wifil_config *cfg, const nsref_wifil_sends *sn, uint64_t *log_ts, uint32_t *log_uid,
                        uint32_t *log_ctx, uint64_t log_cap, nsgpu_wifil_end *ends, uint64_t ends_cap, uint64_t *n_ends,

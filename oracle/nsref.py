@@ -533,10 +533,13 @@ def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble,
 class WifilSendsStruct(C.Structure):  # nsref_wifil_sends (nsref.h)
     _fields_ = [("n", C.c_uint64), ("ts", C.c_void_p), ("phy", C.c_void_p), ("size", C.c_void_p),
                 ("modclass", C.c_uint32), ("bw", C.c_uint32), ("preamble", C.c_uint32), ("pad_", C.c_uint32),
-                ("rate", C.c_uint64), ("stop_ts", C.c_uint64), ("dbm", C.c_double)]
+                ("rate", C.c_uint64), ("stop_ts", C.c_uint64), ("dbm", C.c_double), ("n_moves", C.c_uint64),
+                ("move_ts", C.c_void_p), ("move_phy", C.c_void_p), ("move_xyz", C.c_void_p)]
 
 
-def wifil_replay(cfg_struct, ts, phy, size, mode, preamble, dbm, stop_ts, n_phy, end_dtype, phys_dtype, log_cap=1 << 16):
+def wifil_replay(cfg_struct, ts, phy, size, mode, preamble, dbm, stop_ts, n_phy, end_dtype, phys_dtype, log_cap=1 << 16,
+                 moves=()):
+    """moves: [(ts, phy, (x, y, z))] — MobilityModel::SetPosition host closures scheduled after the sends."""
     """A replayed transmission schedule on the closed-loop oracle PHY (nsref_wifil_replay): SendPacket of phy[k]
     (size[k] bytes) at ts[k], host closures scheduled at setup in send order, then Stop (stop_ts).  Returns as
     wifil_run."""
@@ -547,8 +550,11 @@ def wifil_replay(cfg_struct, ts, phy, size, mode, preamble, dbm, stop_ts, n_phy,
     ts = np.ascontiguousarray(ts, np.uint64)
     phy = np.ascontiguousarray(phy, np.uint32)
     size = np.ascontiguousarray(size, np.uint32)
+    mts = np.array([m[0] for m in moves] or [0], np.uint64)
+    mph = np.array([m[1] for m in moves] or [0], np.uint32)
+    mxyz = np.array([c for m in moves for c in m[2]] or [0.0], np.float64)
     sn = WifilSendsStruct(len(ts), ts.ctypes.data, phy.ctypes.data, size.ctypes.data, mode[0], mode[2], preamble, 0,
-                          mode[1], stop_ts, dbm)
+                          mode[1], stop_ts, dbm, len(moves), mts.ctypes.data, mph.ctypes.data, mxyz.ctypes.data)
     lts = np.zeros(log_cap, np.uint64)
     luid = np.zeros(log_cap, np.uint32)
     lctx = np.zeros(log_cap, np.uint32)

@@ -469,7 +469,15 @@ struct Loop {
   std::vector<Phy> phy;
   std::vector<LoopTx> txs;
   std::vector<LoopEnd> endv;
-  enum { ATTEMPT = 0, RX = 1, END = 2, STOP = 3, SEND = 4 };
+  enum { ATTEMPT = 0, RX = 1, END = 2, STOP = 3, SEND = 4, MOVE = 5 };
+  // current positions (MobilityModel::SetPosition from a host closure moves a phy; YansWifiChannel::Send reads
+  // them at each send, yans-wifi-channel.cc:92-96)
+  std::vector<double> px, py, pz;
+  void init_positions() {
+    px.assign(cfg->x, cfg->x + cfg->n_phy);
+    py.assign(cfg->y, cfg->y + cfg->n_phy);
+    pz.assign(cfg->z, cfg->z + cfg->n_phy);
+  }
   struct E {
     uint32_t kind, a, b, ctx;
     double rx_dbm;
@@ -610,7 +618,7 @@ struct Loop {
     // YansWifiChannel::Send — yans-wifi-channel.cc:77-115
     for (int64_t j = 0; j < cfg->n_phy; j++) {
       if (j == (int64_t)i || cfg->channel[j] != cfg->channel[i]) continue;
-      double d = nsref_distance(cfg->x[i], cfg->y[i], cfg->z[i], cfg->x[j], cfg->y[j], cfg->z[j]);
+      double d = nsref_distance(px[i], py[i], pz[i], px[j], py[j], pz[j]);
       int64_t delay = nsref_const_speed_delay(d, cfg->speed);
       double rx = nsref_calc_rx_power(mac->dbm, d, &cfg->loss);
       schedule(now + (uint64_t)delay, E{RX, k, (uint32_t)j, cfg->node[j], rx});
@@ -644,7 +652,7 @@ struct Loop {
     sends++;
     for (int64_t j = 0; j < cfg->n_phy; j++) {  // YansWifiChannel::Send — yans-wifi-channel.cc:77-115
       if (j == (int64_t)i || cfg->channel[j] != cfg->channel[i]) continue;
-      double d = nsref_distance(cfg->x[i], cfg->y[i], cfg->z[i], cfg->x[j], cfg->y[j], cfg->z[j]);
+      double d = nsref_distance(px[i], py[i], pz[i], px[j], py[j], pz[j]);
       int64_t delay = nsref_const_speed_delay(d, cfg->speed);
       double rx = nsref_calc_rx_power(dbm, d, &cfg->loss);
       schedule(now + (uint64_t)delay, E{RX, k, (uint32_t)j, cfg->node[j], rx});
@@ -796,12 +804,17 @@ int nsref_wifil_replay(const nsgpu_wifil_config *cfg, const nsref_wifil_sends *s
   L.cfg = cfg;
   L.mac = nullptr;
   L.phy.resize((size_t)cfg->n_phy);
+  L.init_positions();
   L.edW = Loop::DbmToW(cfg->ed_threshold_dbm);
   L.ccaW = Loop::DbmToW(cfg->cca_threshold_dbm);
   L.noiseFigure = pow(10.0, cfg->rx_noise_figure_db / 10.0);
   for (uint64_t k = 0; k < sn->n; k++) {
     if (sn->phy[k] >= (uint64_t)cfg->n_phy) return -4;
     L.schedule(sn->ts[k], Loop::E{Loop::SEND, (uint32_t)k, 0, 0xffffffffu, 0.0});
+  }
+  for (uint64_t k = 0; k < sn->n_moves; k++) {  // Simulator::Schedule (t, &MobilityModel::SetPosition, ...)
+    if (sn->move_phy[k] >= (uint64_t)cfg->n_phy) return -4;
+    L.schedule(sn->move_ts[k], Loop::E{Loop::MOVE, (uint32_t)k, 0, 0xffffffffu, 0.0});
   }
   L.schedule(sn->stop_ts, Loop::E{Loop::STOP, 0, 0, 0xffffffffu, 0.0});
   while (!L.q.empty()) {
@@ -823,6 +836,9 @@ int nsref_wifil_replay(const nsgpu_wifil_config *cfg, const nsref_wifil_sends *s
     if (e.kind == Loop::SEND) {
       const int rc = L.send_packet(sn->phy[e.a], sn->size[e.a], sn->modclass, sn->rate, sn->bw, sn->preamble, sn->dbm);
       if (rc) return rc;
+    } else if (e.kind == Loop::MOVE) {
+      const uint32_t j = sn->move_phy[e.a];
+      L.px[j] = sn->move_xyz[3 * e.a], L.py[j] = sn->move_xyz[3 * e.a + 1], L.pz[j] = sn->move_xyz[3 * e.a + 2];
     } else if (e.kind == Loop::RX) {
       L.start_receive(e.a, e.b, e.rx_dbm);
     } else if (e.kind == Loop::END) {
@@ -862,6 +878,7 @@ int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, u
   L.cfg = cfg;
   L.mac = mac;
   L.phy.resize((size_t)cfg->n_phy);
+  L.init_positions();
   L.edW = Loop::DbmToW(cfg->ed_threshold_dbm);
   L.ccaW = Loop::DbmToW(cfg->cca_threshold_dbm);
   L.noiseFigure = pow(10.0, cfg->rx_noise_figure_db / 10.0);  // DbToRatio (SetRxNoiseFigure, yans-wifi-phy.cc:192-197)

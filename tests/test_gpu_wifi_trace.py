@@ -72,3 +72,21 @@ def test_closed_loop_grid_sniffer_traces_equal_the_oracle():
     texts = [f"ns3::WifiMacHeader (DATA, tx {k}) Payload (size={sc['size']})" for k in range(len(frames))]
     nodes, devs = np.arange(n), np.ones(n)
     assert wifi.sniff_ascii(grecs, nodes, devs, texts) == wifi.sniff_ascii(orecs, nodes, devs, texts)
+
+
+@pytest.mark.parametrize("prefix", ["aodv-chain-regression-test", "bug-606-test"])
+def test_aodv_chain_with_a_moving_node_on_the_device(prefix):
+    """ChainRegressionTest's sends replayed on the device PHY with the central node moved by a host closure at
+    m_time / 3 (nsgpu_sim_wifi_set_position): pop log, EndReceive records and the reference files byte for byte."""
+    import aodv_replay as aodv
+    files, _recs, sends, _rx = aodv.golden(prefix)
+    olog, oends, _ophys, otot = aodv.oracle_replay(prefix)
+    glog, gends, _gphys, gtot, _keep = aodv.gpu_replay(prefix)
+    assert gtot["dispatched"] == otot["dispatched"] and gtot["next_uid"] == otot["next_uid"]
+    for a, b in zip(glog, olog):
+        assert np.array_equal(a, b)
+    same_ends(gends, oends)
+    assert np.array_equal(gtot["txs"], otot["txs"])
+    out = aodv.pcaps(prefix, gends, gtot["txs"], [f for _t, _i, f in sends])
+    for i in range(len(files)):
+        assert out[i] == files[i], i
