@@ -174,6 +174,16 @@ struct Ctl {
   uint32_t rk_W, rk_go;       // k2_handle's snapshot for k2_rank (window size; it was handled, normally)
   uint64_t rk_win, rk_lim;    //   (its window index, lim_rel): k2_rank's bookkeeping block rewrites C.W etc.
   WInfo winfo[4];             // window n's dispatch bases (k2_rank's bookkeeping), at n & 3
+  // ---- partitioned sorted runs (a window some rank cannot hold: every rank sorts its candidates once and the
+  // run is dispatched in chunks cut at a common key; k_drun_*, k2_pa's chunk role, k_dfin2) ----
+  uint32_t drun, drpad;       // a run is being dispatched (every rank alike)
+  uint64_t dr0, drW, dr1;     // this rank's run: next entry, length (rn_* arrays); past the chunk being formed
+  uint64_t drg;               // the next chunk's cut key (from the ranks' fitting and head keys, k_dfin2)
+  uint64_t drlo;              // the next chunk continues the same-ts group the last one cut: its rel ts (~0: no)
+  uint32_t drtrim, dtrim;     // the next chunk ends that group and the run after it; the run ended so: the next
+                              // k2_pa returns this rank's entries left that are not in the pool to pending
+  uint64_t drn_tmin, drn_wend;  // the reduction of this rank's run entries outside the pool (k_drun_red)
+  uint64_t drb_tmin, drb_span, drb_bound, drb_stop, drb_nbound, drb_lim;  // the run window's bound (WinBound)
 };
 
 static_assert(offsetof(Ctl, prep) == offsetof(Ctl, W) + 12 && offsetof(Ctl, W) % 16 == 0, "the X0 payload");
@@ -299,6 +309,10 @@ struct P2PDev {
   uint32_t *cpt;          // [2][NMAX] child prefix by rank (k2_sdef): provisional uids resolve through it
   uint32_t *ldpd;         // [LMAX] the dense list's parents as dense indices | child index << 24 (k2_rank -> k2_pa)
   uint32_t sdef_fold;     // df_sdef runs as k2_rank's blocks 1 .. NSDEF (1) or as its own kernel k2_sdef (0)
+  // ---- partitioned sorted runs: this rank's candidates of the run window, in key order (runcap each) ----
+  uint64_t *rn_key;
+  uint32_t *rn_ctx, *rn_kind, *rn_a, *rn_src;
+  Pkt *rn_pkt;
 };
 
 // ---------------- wave / block helpers ----------------
@@ -1075,7 +1089,9 @@ struct X1Hdr {
   uint32_t W, tc, tinl, needc;  // window events, their children, their inline children; pool compaction wanted
   uint64_t pad0, lastkey;     // largest window key
   Red red;                    // reduction of this rank's pending set after the window (next LBTS)
-  uint64_t pad2[7];
+  uint64_t rkey, rrem, rhead; // sorted run: this rank's fitting key for the next chunk (~0: the rest fits), entries
+                              // left, the first one's key (~0: none)
+  uint64_t pad2[4];
 };
 static_assert(sizeof(X1Hdr) == 128, "X1 records: the loopback transport copies 16-byte words");
 struct X1Ent {  // one window event: key and child counts (children | inline children << 16)
@@ -1163,9 +1179,9 @@ __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_
 //   k2_pa<true>  as single-GPU (in-place pool), plus the remote events of the last X2;
 //   X0           allgather of every rank's window size and hub flag (16 B, straight from Ctl);
 //   k2_handle    holders and hub blocks (no rank tiles), writing this rank's X1 summary and entries —
-//                unless some rank's window does not fit: then nothing runs and the host cuts the
-//                window on every rank at the smallest of their largest fitting keys (k_refit2,
-//                allgather, k_cut2; a key prefix of a safe window is safe);
+//                unless some rank's window does not fit: then nothing runs and the window becomes a
+//                partitioned sorted run (every rank sorts its candidates once; chunks cut at the smallest
+//                of the ranks' fitting keys, nsgpu_p2p_win.h);
 //   X1           allgather of the summaries;
 //   k_gtile      per own event, over the merged windows: # smaller keys (global dispatch rank) and the
 //                child / inline-child sums below it and below its same-ts group (uid prefixes);
@@ -1174,179 +1190,97 @@ __device__ __forceinline__ void rank_tile(const P2PDev &M, const Ctl &C, uint32_
 //                window's bound), `done`, a compaction every rank makes;
 //   X2           all-to-all of remote events.
 
-// The largest key lo with at most T of the window's n candidates <= lo (256-way radix bisection over
-// (0, bound]; count (<= bound) > T).  All SCAN_THREADS threads of the block call it.
-__device__ uint64_t window_bisect(const P2PDev &M, uint64_t n, uint64_t bound, uint32_t T) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint64_t s_lo, s_hi;
-  __shared__ uint32_t s_clo;
-  if (threadIdx.x == 0) {
-    s_lo = 0;  // (every key is >= 4: uids start at 4)
-    s_hi = bound;
-    s_clo = 0;
-  }
-  __syncthreads();
-  while (s_hi - s_lo > 1) {
-    const uint64_t lo = s_lo, hi = s_hi;
-    const uint64_t range = hi - lo;  // keys in (lo, hi]: bucket (k - lo - 1) >> sh in [0, 256)
-    int sh = 0;
-    while (((range - 1) >> sh) >= 256) sh++;
-    for (int j = threadIdx.x; j < 256; j += SCAN_THREADS) hist[j] = 0;
-    __syncthreads();
-    for (uint64_t i = threadIdx.x; i < n; i += SCAN_THREADS) {
-      const uint64_t k = M.wkey[i];
-      if (k > lo && k <= hi) atomicAdd(&hist[(uint32_t)((k - lo - 1) >> sh)], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t c = s_clo;
-      int j = -1;
-      while (j + 1 < 256 && c + hist[j + 1] <= T) c += hist[++j];
-      // keys <= lo + (j + 1) << sh: c <= T; keys <= lo + (j + 2) << sh: > T
-      const uint64_t nlo = lo + ((uint64_t)(j + 1) << sh);
-      const uint64_t nhi = lo + ((uint64_t)(j + 2) << sh);
-      s_lo = nlo;
-      s_clo = c;
-      s_hi = nhi < hi ? nhi : hi;
-    }
-    __syncthreads();
-  }
-  const uint64_t r = s_lo;
-  __syncthreads();
-  return r;
-}
-
-// Host-driven cut, step 1 (one block): this rank's largest fitting key -> xk_send.  A rank holds WCAP
-// window events, HUBL when a hub is too large for a block (Ctl::overflow).
-__global__ __launch_bounds__(SCAN_THREADS) void k_refit2(const P2PDev M) {
-  Ctl &C = *M.C;
-  const uint64_t bound = C.bound;
-  const uint32_t W = C.W;
-  const uint32_t T = C.overflow ? (uint32_t)HUBL : (uint32_t)WCAP;
-  const uint64_t n = W < M.runcap ? W : M.runcap;
-  uint64_t lb = bound;
-  if (W > T || C.overflow) lb = window_bisect(M, n, bound, T);
-  if (threadIdx.x == 0) {
-    M.xk_send[0] = lb;
-    M.xk_send[1] = 0;
-  }
-}
-
-// Host-driven cut, step 2 (one block, after the allgather of the keys): the window becomes its
-// candidates with key <= g (the smallest fitting key of all ranks), compacted in place with fresh slot
-// tables; the others become pending again (a pool entry stays where it is, a child or a remote event
-// is parked in the fresh buffer) and fold into this rank's reduction.  The next k2_pa finds the window
-// formed (C.prep).
-__global__ __launch_bounds__(SCAN_THREADS) void k_cut2(const P2PDev M) {
-  Ctl &C = *M.C;
-  __shared__ uint32_t s_nw, s_nf;
-  __shared__ uint32_t wsum[2][SCAN_THREADS / 64];
-  uint64_t g = ~0ull;
-  for (uint32_t q = 0; q < M.nranks; q++) g = M.xk_recv[2 * q] < g ? M.xk_recv[2 * q] : g;
-  const uint64_t bound = C.bound, tmin = C.tmin;
-  const uint32_t W = C.W;
-  const uint64_t n = W < M.runcap ? W : M.runcap;
-  const uint64_t nF0 = C.nF;
-  // the slot tables of the candidate slots (rebuilt below for the ones kept)
-  const uint64_t nt = n < (uint64_t)WCAP ? n : (uint64_t)WCAP;
-  for (uint64_t s = threadIdx.x; s < nt; s += SCAN_THREADS) {
+// ---- partitioned sorted runs: the host step that starts one (nsgpu_p2p_win.h, "partitioned sorted runs") ----
+// The window that did not fit (C.W candidates in the window records, relative to its tmin) is sorted by key into
+// rn_* (k_rs_*), after its node-table entries are cleared (k_drun_clear: the chunks claim them again); k_drun_start
+// keeps the window's bound and sends this rank's fitting key (its WCAP-th entry's key; ~0 when all fit) and size,
+// and after their all-gather k_drun_first moves the first chunk in.  The candidates that came from the pool stay
+// there until their chunk runs (its maintenance tombstones them); the others live in the run only.
+__global__ __launch_bounds__(256) void k_drun_clear(const P2PDev M) {
+  const Ctl &C = *M.C;
+  const uint64_t W = C.W;
+  const uint64_t nt = W < (uint64_t)WCAP ? W : (uint64_t)WCAP;  // (k2_write claims slots below WCAP only)
+  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < nt; s += (uint64_t)gridDim.x * 256) {
     const uint32_t c = lp_of(M, M.wctx[s], M.wkind[s], M.wa[s]);
     if (c < M.n_nodes) M.node_tab[(uint64_t)c * NTAB] = 0;
   }
-  if (threadIdx.x == 0) {
-    s_nw = 0;
-    s_nf = 0;
-    C.nhub = 0;
-    C.overflow = 0;
-  }
-  __syncthreads();
-  Red &R = x1hdr(M.x1_send, 0)->red;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint64_t below = (1ull << lane) - 1ull;
+}
+__global__ void k_drun_start(const P2PDev M, uint64_t n) {
+  Ctl &C = *M.C;
+  const WinBound b = window_bound(C.rt ? C.red[0] : C.red[1]);  // (the bound k2_pa formed the window with)
+  C.drb_tmin = b.tmin;
+  C.drb_span = b.span;
+  C.drb_bound = b.bound;
+  C.drb_stop = b.stop_packed;
+  C.drb_nbound = b.nbound;
+  C.drb_lim = b.lim;
+  C.dr0 = C.dr1 = 0;
+  C.drW = n;
+  C.W = 0;
+  C.nhub = 0;
+  C.overflow = 0;
+  C.drlo = ~0ull;
+  C.drtrim = 0;
+  C.dtrim = 0;
+  C.drn_tmin = C.drn_wend = ~0ull;
+  M.xk_send[0] = n > (uint64_t)WCAP ? M.rn_key[WCAP - 1] : ~0ull;  // (this rank's fitting key)
+  M.xk_send[1] = n ? M.rn_key[0] : ~0ull;                           // (its head key)
+}
+// The run's entries that are not in the pool (children and remote events of the window before) stay pending
+// outside it until their chunk: their reduction is folded into every chunk's (conservatively: all of them).
+__global__ __launch_bounds__(256) void k_drun_red(const P2PDev M, uint64_t n) {
+  Ctl &C = *M.C;
+  const uint64_t tmin = C.drb_tmin;
   uint64_t tmn = ~0ull, wnd = ~0ull;
-  for (uint64_t c0 = 0; c0 < n; c0 += SCAN_THREADS) {
-    const uint64_t i = c0 + threadIdx.x;
-    const bool valid = i < n;
-    uint64_t key = 0;
-    uint32_t ctx = 0, kind = 0, a = 0, src = NOSRC;
-    Pkt p{0, 0, 0, 0};
-    if (valid) {
-      key = M.wkey[i];
-      ctx = M.wctx[i];
-      kind = M.wkind[i];
-      a = M.wa[i];
-      p = M.wpkt[i];
-      src = M.wsrc[i];
-    }
-    const bool keep = valid && key <= g;
-    const bool park = valid && !keep && src == NOSRC;
-    const uint64_t bk = __ballot(keep), bp = __ballot(park);
-    if (lane == 0) {
-      wsum[0][wid] = (uint32_t)__popcll(bk);
-      wsum[1][wid] = (uint32_t)__popcll(bp);
-    }
-    __syncthreads();  // (also: every read of this chunk is done; kept records only move down)
-    uint32_t ok = s_nw, of = s_nf, tk = 0, tf = 0;
-    for (int w = 0; w < SCAN_THREADS / 64; w++) {
-      ok += w < wid ? wsum[0][w] : 0;
-      of += w < wid ? wsum[1][w] : 0;
-      tk += wsum[0][w];
-      tf += wsum[1][w];
-    }
-    if (keep) {
-      const uint64_t o = ok + (uint32_t)__popcll(bk & below);
-      M.wkey[o] = key;
-      M.wctx[o] = ctx;
-      M.wkind[o] = kind;
-      M.wa[o] = a;
-      M.wpkt[o] = p;
-      M.wsrc[o] = src;
-    } else if (valid) {
-      const uint64_t ts = tmin + (key >> 32);
-      tmn = ts < tmn ? ts : tmn;
-      const uint64_t x = ts + (uint64_t)M.lookahead[kind & 0xffu];
-      wnd = x < wnd ? x : wnd;
-      if ((kind & 0xffu) == K_STOP) {
-        R.stopts = ts;
-        R.stopuid = (uint32_t)key;
-      }
-      if (park) {
-        const uint64_t fi = nF0 + of + (uint32_t)__popcll(bp & below);
-        if (fi < M.fcap) {
-          M.f_ts[fi] = ts;
-          M.f_uid[fi] = (uint32_t)key;
-          M.f_ctx[fi] = ctx;
-          M.f_kind[fi] = kind;
-          M.f_a[fi] = a;
-          M.f_pkt[fi] = p;
-        } else {
-          atomicOr(M.error, 1u);
-        }
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      s_nw += tk;
-      s_nf += tf;
-    }
-    __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    if (M.rn_src[i] != NOSRC) continue;
+    const uint64_t ts = tmin + (M.rn_key[i] >> 32);
+    const uint64_t x = ts + (uint64_t)M.lookahead[(M.rn_kind[i] & 0xffu) % K_NKINDS];
+    tmn = ts < tmn ? ts : tmn;
+    wnd = x < wnd ? x : wnd;
   }
-  publish_min<SCAN_THREADS>(R, tmn, wnd);
-  __syncthreads();
-  const uint32_t Wk = s_nw;
-  for (uint32_t s = threadIdx.x; s < Wk && s < (uint32_t)WCAP; s += SCAN_THREADS)
-    node_table_add(M, C, s, lp_of(M, M.wctx[s], M.wkind[s], M.wa[s]), M.wkind[s]);
-  if (threadIdx.x == 0) {
-    WinBound b = window_bound(C.rt ? C.red[0] : C.red[1]);  // (the window's own reduction)
-    b.bound = g < b.bound ? g : b.bound;
+  tmn = wave_min64(tmn);
+  wnd = wave_min64(wnd);
+  if ((threadIdx.x & 63) == 0) {
+    if (tmn != ~0ull) atomicMin((unsigned long long *)&C.drn_tmin, (unsigned long long)tmn);
+    if (wnd != ~0ull) atomicMin((unsigned long long *)&C.drn_wend, (unsigned long long)wnd);
+  }
+}
+// The next chunk's cut key from the ranks' smallest fitting key fk and smallest head key hk (every rank computes
+// the same): a chunk that continues the same-ts group the last one cut (gp: the last chunk's key) takes more of
+// that group, and when the rest of the group fits, exactly the rest — and the run ends after it (its queued
+// DoForwardUp leaves at that ts are pending: they sort before every later run entry); otherwise the chunk backs
+// off to the start of the group its fitting key would cut, unless that group alone fills it.
+struct DrunCut {
+  uint64_t g, lo;
+  uint32_t trim;
+};
+__device__ __forceinline__ DrunCut drun_cut(uint64_t fk, uint64_t hk, uint64_t gp) {
+  const uint64_t T0 = hk >> 32, gend = (T0 << 32) | 0xffffffffull;
+  if (gp != ~0ull && (uint32_t)gp != 0xffffffffu && (gp >> 32) == T0)  // (a real key's uid is below 0xffffffff)
+    return fk >= gend ? DrunCut{gend, T0, 1u} : DrunCut{fk, T0, 0u};
+  if (fk != ~0ull && (fk >> 32) > T0) return DrunCut{((fk >> 32) << 32) - 1, ~0ull, 0u};
+  return DrunCut{fk, ~0ull, 0u};
+}
+__global__ __launch_bounds__(TB) void k_drun_first(const P2PDev M) {
+  Ctl &C = *M.C;
+  uint64_t fk = ~0ull, hk = ~0ull;
+  for (uint32_t q = 0; q < M.nranks; q++) {
+    fk = M.xk_recv[2 * q] < fk ? M.xk_recv[2 * q] : fk;
+    hk = M.xk_recv[2 * q + 1] < hk ? M.xk_recv[2 * q + 1] : hk;
+  }
+  const uint64_t g = drun_cut(fk, hk, ~0ull).g;
+  drun_chunk<TB>(M, C, (uint64_t)blockIdx.x * TB + threadIdx.x, 0, C.drW, g);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const WinBound b = drun_bound(C, g);
     publish_bound(C, b);
-    C.split_lo = ~0ull;
-    // leaves at the cut's timestamp are queued: pending events of that timestamp sort before them
-    C.split_hi = g < bound ? (g >> 32) : b.span;
-    if (g < bound) C.refits++;
-    C.W = Wk;
-    C.nF = nF0 + s_nf;
-    C.prep = 1;
+    C.split_lo = ~0ull;  // (leaves at a cut group's ts are queued: pending events of that ts sort before them)
+    C.split_hi = drun_cuts_group(g, C.drb_bound) ? (g >> 32) : b.span;
+    C.hrel = C.split_hi;
+    C.hcap = 0;
+    C.drun = 1;
+    C.drg = g;
+    C.prep = 1;  // (the next k2_pa finds the window formed: it appended the last window already)
     C.mode = MODE_NORMAL;
   }
 }
@@ -1432,14 +1366,14 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   const uint32_t tinl_q = lv ? lh->tinl : 0u;
   // (block 0: the rest of the summaries and the run control, for the run bookkeeping, in the same trip)
   struct Bk {
-    uint64_t nF, nfree, npush, pK0, ptmin, windows, P_end, live, inline_lim, max_windows, max_window;
-    uint32_t nhub, puid0, rt;
+    uint64_t nF, nfree, npush, pK0, ptmin, windows, P_end, live, inline_lim, max_windows, max_window, drg, dr1;
+    uint32_t nhub, puid0, rt, drtrim;
   } bk{};
   if (blockIdx.x == 0)
     bk = Bk{C.nF, C.nfree, C.npush, C.pK0, C.ptmin, C.windows, C.P_end, C.live, C.inline_lim, C.max_windows,
-            C.max_window, C.nhub, C.puid0, C.rt};
+            C.max_window, C.drg, C.dr1, C.nhub, C.puid0, C.rt, C.drtrim};
   uint32_t hW = 0, htc = 0, hneedc = 0, hsuid = 0;
-  uint64_t hlk = 0, htmin = ~0ull, hwend = ~0ull, hsts = ~0ull;
+  uint64_t hlk = 0, htmin = ~0ull, hwend = ~0ull, hsts = ~0ull, hrkey = ~0ull, hrrem = 0, hrhead = ~0ull;
   if (blockIdx.x == 0 && lv) {
     hW = lh->W;
     htc = lh->tc;
@@ -1449,6 +1383,9 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     hwend = lh->red.wend;
     hsts = lh->red.stopts;
     hsuid = lh->red.stopuid;
+    hrkey = lh->rkey;
+    hrrem = lh->rrem;
+    hrhead = lh->rhead;
   }
   // X1 is all-gathered in place (x1_send is this rank's slot of x1_recv): the last block to have read the
   // headers resets this rank's for the next window — every block's header loads have returned before it
@@ -1463,6 +1400,8 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     hs->lastkey = 0;
     hs->red.tmin = hs->red.wend = hs->red.stopts = hs->red.wendw = ~0ull;
     hs->red.stopuid = 0;
+    hs->rkey = ~0ull;
+    hs->rrem = 0;
   }
   // the slot's accumulators, record and first children, all loaded before anything waits
   const uint32_t s = blockIdx.x * HB + threadIdx.x;
@@ -1518,6 +1457,10 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   // the ranks' summaries, reduced across the lanes (rank q's in lane q)
   const uint32_t Wg = wave_sum32(hW), tcg = wave_sum32(htc);
   const uint32_t needc = __ballot(hneedc != 0) ? 1u : 0u;
+  // a partitioned sorted run: entries left on some rank -> the next chunk (drun_cut), unless the chunk just
+  // run ended the run (it ended a cut same-ts group)
+  const bool drun_more = __ballot(hrrem != 0) != 0;
+  const uint64_t drfk = wave_min64(hrrem != 0 ? hrkey : ~0ull), drhk = wave_min64(hrrem != 0 ? hrhead : ~0ull);
   const uint64_t lk = wave_max64(hW ? hlk : 0ull);
   Red rg{~0ull, ~0ull, ~0ull, 0, 0, ~0ull};
   rg.tmin = wave_min64(htmin);
@@ -1556,9 +1499,19 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   C.W = 0;
   C.overflow = 0;
   C.prep = 0;
+  {
+    const bool go = drun_more && !bk.drtrim;
+    const DrunCut dc = go ? drun_cut(drfk, drhk, bk.drg) : DrunCut{~0ull, ~0ull, 0u};
+    C.drun = go ? 1u : 0u;
+    C.dr0 = bk.dr1;  // (the chunk just run ended there; k2_pa reads dr0 at its start)
+    C.drg = dc.g;
+    C.drlo = dc.lo;
+    C.drtrim = dc.trim;
+    C.dtrim = drun_more && bk.drtrim ? 1u : 0u;  // (the next k2_pa returns the run's entries left to pending)
+  }
   // the window that held Simulator::Stop ends the run (every rank knows it from the bound), as does an
-  // empty pending set on every rank
-  bool done = bk.inline_lim != ~0ull || rg.tmin == ~0ull;
+  // empty pending set on every rank (a run's entries from the fresh buffer are pending outside the pool)
+  bool done = bk.inline_lim != ~0ull || (rg.tmin == ~0ull && !drun_more);
   if (P_end > M.pool_cap) {
     atomicOr(M.error, 1u);
     done = true;
@@ -1572,7 +1525,8 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     done = true;
   }
   if (done) C.done = 1;
-  else if (needc) C.mode = MODE_COMPACT;  // (every rank: the pipelines stay in step)
+  else if (needc && !drun_more) C.mode = MODE_COMPACT;  // (every rank: the pipelines stay in step; a run's
+                                                         //  pool entries keep their slots until it ends)
   stack_and_hubs();
 }
 
@@ -1734,8 +1688,9 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   }
   if (owner) {
     if (nranks < 1 || nranks > MAXR || rank < 0 || rank >= nranks ||
-        (uint64_t)nranks * CAPX_MAX + TB + WCAP >= (uint64_t)GRID_POOL * TB)
-      return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: rank %d of %d (at most %d ranks)", rank, nranks, MAXR);
+        (uint64_t)nranks * CAPX_MAX + TB + 2 * WCAP >= (uint64_t)GRID_POOL * TB)  // (k2_pa: slot, remote, chunk blocks)
+      return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: rank %d of %d (at most %d ranks)", rank, nranks,
+                       (int)(((uint64_t)GRID_POOL * TB - TB - 2 * WCAP - 1) / CAPX_MAX));
     for (uint32_t n = 0; n < N; n++)
       if (owner[n] >= (uint32_t)nranks) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: node %u: owner %u", n, owner[n]);
   }
@@ -2071,13 +2026,19 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.hub_key, (size_t)NHUB * WCAP));
   TRY(dalloc(h, &M.hub_slot, (size_t)NHUB * WCAP));
   TRY(dalloc(h, &M.cmp_cnt, 1));
-  if (!owner) {
+  {  // radix sort scratch: the single engine's sorted runs, a partitioned rank's run (sorted once per run)
     TRY(dalloc(h, &M.s_key2, M.runcap));
-    for (uint32_t **p : {&M.s_val, &M.s_val2, &M.g_u32}) TRY(dalloc(h, p, M.runcap));
+    for (uint32_t **p : {&M.s_val, &M.s_val2}) TRY(dalloc(h, p, M.runcap));
     TRY(dalloc(h, &M.s_hist, 256 * ((M.runcap + RS_TILE - 1) / RS_TILE)));
-    TRY(dalloc(h, &M.g_pkt, M.runcap));
+    if (!owner) {  // (the single engine gathers in place through these; a partitioned rank into rn_*)
+      TRY(dalloc(h, &M.g_u32, M.runcap));
+      TRY(dalloc(h, &M.g_pkt, M.runcap));
+    }
   }
   if (owner) {
+    TRY(dalloc(h, &M.rn_key, M.runcap));
+    for (uint32_t **p : {&M.rn_ctx, &M.rn_kind, &M.rn_a, &M.rn_src}) TRY(dalloc(h, p, M.runcap));
+    TRY(dalloc(h, &M.rn_pkt, M.runcap));
     M.dist = 1;
     M.rank = (uint32_t)rank;
     M.nranks = (uint32_t)nranks;
@@ -2106,6 +2067,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     h->comm = comm;
     memset(&h->x1h0, 0, sizeof(X1Hdr));
     h->x1h0.red.tmin = h->x1h0.red.wend = h->x1h0.red.stopts = h->x1h0.red.wendw = ~0ull;
+    h->x1h0.rkey = ~0ull;
   }
   TRY(dalloc(h, &M.C, 1));
   if (owner) M.x0_send = reinterpret_cast<uint64_t *>(&M.C->W);  // X0 sends (W, nxtP, overflow, prep)
@@ -2516,25 +2478,60 @@ static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s, int nwin = NWIN) {
   return rc;
 }
 
-// The partitioned engine's host-driven steps (every rank makes the same ones: the pause that asks
-// for them is decided from exchanged data): the pool compaction, and the window cut — k_refit2, an
-// allgather of the keys (`cut`'s), k_cut2 — after which the cut window and the next one run as single
-// passes (`pass`), cut again while the next window does not fit either (the setup burst at t = 0: one
-// host step, not a paused graph replay per cut).  `snap`: pinned run-control snapshot of `C`.
+// The partitioned engine's host-driven steps (every rank makes the same ones: the pause that asks for them is
+// decided from exchanged data): the pool compaction, and the start of a partitioned sorted run — a window some
+// rank cannot hold (MODE_CUT): every rank sorts its candidates (drun_sort), the ranks' fitting keys are
+// all-gathered (`gather`) and every rank moves the first chunk in (k_drun_first); the later chunks are formed
+// by the window pipeline itself.
 static int host_step(nsgpu_p2p *h, const Ctl &c, hipStream_t s);
-template <class X, class P>
-static int host_step_dist(const Ctl &c, hipStream_t s, X cut, P pass, const Ctl *C, Ctl *snap,
-                          nsgpu_p2p *h) {
-  if (c.mode != MODE_CUT) return host_step(h, c, s);
-  for (;;) {
-    int rc = cut();
-    if (!rc) rc = pass();  // the cut window
-    if (!rc) rc = pass();  // the next one (MODE_CUT again if it does not fit)
-    if (rc) return rc;
-    NSGPU_HIP(hipMemcpyAsync(snap, C, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+static int drun_sort(nsgpu_p2p *h, uint64_t W, hipStream_t s) {
+  const P2PDev &M = h->M;
+  const uint64_t n = W < M.runcap ? W : M.runcap;
+  hipLaunchKernelGGL(k_drun_clear, dim3(64), dim3(256), 0, s, M);
+  if (n) {  // LSD radix sort of the keys (as host_step's MODE_SORT), the records gathered into rn_*
+    NSGPU_HIP(hipMemsetAsync(M.cmp_cnt, 0, sizeof(uint64_t), s));
+    hipLaunchKernelGGL(k_rs_or, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 2048)), dim3(256), 0, s, M.wkey, n,
+                       (unsigned long long *)M.cmp_cnt);
+    uint64_t kor = 0;
+    NSGPU_HIP(hipMemcpyAsync(&kor, M.cmp_cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     NSGPU_HIP(hipStreamSynchronize(s));
-    if (snap->mode != MODE_CUT || snap->done >= 2) return NSGPU_OK;
+    const int bits = kor ? 64 - __builtin_clzll(kor) : 1;
+    const int passes = (bits + 7) / 8;
+    const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    const uint64_t *kin = M.wkey;
+    uint64_t *kout = (passes & 1) ? M.rn_key : M.s_key2;  // (alternating so that the last pass writes rn_key)
+    uint32_t *vin = nullptr, *vout = M.s_val;
+    for (int p = 0; p < passes; p++) {
+      hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_T), 0, s, kin, n, 8 * p, M.s_hist, ntiles);
+      hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), 0, s, M.s_hist, (uint64_t)256 * ntiles);
+      hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_T), 0, s, kin, vin, kout, vout, n, 8 * p, M.s_hist,
+                         ntiles);
+      kin = kout;
+      kout = kout == M.rn_key ? M.s_key2 : M.rn_key;
+      vin = vout;
+      vout = vin == M.s_val ? M.s_val2 : M.s_val;
+    }
+    const uint32_t gg = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_rs_gather<uint32_t>, dim3(gg), dim3(256), 0, s, vin, M.wctx, M.rn_ctx, n);
+    hipLaunchKernelGGL(k_rs_gather<uint32_t>, dim3(gg), dim3(256), 0, s, vin, M.wkind, M.rn_kind, n);
+    hipLaunchKernelGGL(k_rs_gather<uint32_t>, dim3(gg), dim3(256), 0, s, vin, M.wa, M.rn_a, n);
+    hipLaunchKernelGGL(k_rs_gather<uint32_t>, dim3(gg), dim3(256), 0, s, vin, M.wsrc, M.rn_src, n);
+    hipLaunchKernelGGL(k_rs_gather<Pkt>, dim3(gg), dim3(256), 0, s, vin, M.wpkt, M.rn_pkt, n);
   }
+  hipLaunchKernelGGL(k_drun_start, dim3(1), dim3(1), 0, s, M, n);
+  if (n) hipLaunchKernelGGL(k_drun_red, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256), 0, s, M, n);
+  NSGPU_HIP(hipGetLastError());
+  return NSGPU_OK;
+}
+template <class G>
+static int host_step_dist(const Ctl &c, hipStream_t s, G gather, nsgpu_p2p *h) {
+  if (c.mode != MODE_CUT) return host_step(h, c, s);
+  int rc = drun_sort(h, c.W, s);
+  if (!rc) rc = gather();
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_drun_first, dim3(WCAP / TB), dim3(TB), 0, s, h->M);
+  NSGPU_HIP(hipGetLastError());
+  return NSGPU_OK;
 }
 
 static int build_graph(nsgpu_p2p *h, bool df = false) {
@@ -2648,20 +2645,7 @@ static int drive(nsgpu_p2p *h, bool *paused) {
 static int drive_dist(nsgpu_p2p *h) {
   int cur = 0;
   bool have_prev = false;
-  auto cut = [h]() -> int {
-    hipLaunchKernelGGL(k_refit2, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->M);
-    const int rx = x_allgather(h, h->M.xk_send, h->M.xk_recv, 16, h->s);
-    if (rx) return rx;
-    hipLaunchKernelGGL(k_cut2, dim3(1), dim3(SCAN_THREADS), 0, h->s, h->M);
-    NSGPU_HIP(hipGetLastError());
-    return NSGPU_OK;
-  };
-  auto pass = [h]() -> int {
-    const int rc = launch_windows_dist(h, h->s, 1);
-    if (rc) return rc;
-    NSGPU_HIP(hipGetLastError());
-    return NSGPU_OK;
-  };
+  auto gather = [h]() -> int { return x_allgather(h, h->M.xk_send, h->M.xk_recv, 16, h->s); };
   for (;;) {
     if (h->eager) {
       const int rc = launch_windows_dist(h, h->s);
@@ -2678,7 +2662,7 @@ static int drive_dist(nsgpu_p2p *h) {
       if (c.done >= 2) break;  // 2: the final window is appended
       if (c.mode >= MODE_SORT) {
         NSGPU_HIP(hipEventSynchronize(h->ev[cur]));
-        const int rc = host_step_dist(h->snap[cur], h->s, cut, pass, h->M.C, &h->snap[cur ^ 1], h);
+        const int rc = host_step_dist(h->snap[cur], h->s, gather, h);
         if (rc) return rc;
         have_prev = false;
         continue;
@@ -3157,21 +3141,19 @@ extern "C" int nsgpu_p2p_group_reset(nsgpu_p2p_group *g, void *stream) {
 // The host-driven steps of a group (host_step_dist's, every member): the cut's keys go through k_copies.
 static int group_host_step(nsgpu_p2p_group *g, const Ctl &c0) {
   hipStream_t s = g->s;
-  if (c0.mode == MODE_CUT) {
-    auto cut = [g, s]() -> int {
-      for (auto *h : g->m) hipLaunchKernelGGL(k_refit2, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
-      const unsigned n = (unsigned)g->m.size();
-      hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[3]);
-      for (auto *h : g->m) hipLaunchKernelGGL(k_cut2, dim3(1), dim3(SCAN_THREADS), 0, s, h->M);
-      NSGPU_HIP(hipGetLastError());
-      return NSGPU_OK;
-    };
-    auto pass = [g, s]() -> int {
-      launch_windows_group(g, s, 1);
-      NSGPU_HIP(hipGetLastError());
-      return NSGPU_OK;
-    };
-    return host_step_dist(c0, s, cut, pass, g->m[0]->M.C, &g->snap[0], g->m[0]);
+  if (c0.mode == MODE_CUT) {  // a partitioned sorted run (host_step_dist's steps, every member)
+    for (auto *h : g->m) {
+      Ctl c;
+      NSGPU_HIP(hipMemcpyAsync(&c, h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+      NSGPU_HIP(hipStreamSynchronize(s));
+      const int rc = drun_sort(h, c.W, s);
+      if (rc) return rc;
+    }
+    const unsigned n = (unsigned)g->m.size();
+    hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[3]);
+    for (auto *h : g->m) hipLaunchKernelGGL(k_drun_first, dim3(WCAP / TB), dim3(TB), 0, s, h->M);
+    NSGPU_HIP(hipGetLastError());
+    return NSGPU_OK;
   }
   for (auto *h : g->m) {
     Ctl c;

@@ -197,7 +197,8 @@ __device__ __forceinline__ NtClaim node_table_claim(const P2PDev &M, uint32_t sl
   M.widx[slot] = 0;
   return NtClaim{slot, NOSRC, 0};
 }
-__device__ __forceinline__ void node_table_finish(const P2PDev &M, Ctl &C, const NtClaim &p) {
+// sorted: a partitioned run's chunk (key order: its hub blocks take a hub's events in slot order, no HUBL limit)
+__device__ __forceinline__ void node_table_finish(const P2PDev &M, Ctl &C, const NtClaim &p, bool sorted = false) {
   if (p.c == NOSRC) return;
   const uint32_t idx = p.idx;
   if (idx < (uint32_t)NSLOT) M.node_tab[(uint64_t)p.c * NTAB + 1 + idx] = p.slot;
@@ -205,7 +206,7 @@ __device__ __forceinline__ void node_table_finish(const P2PDev &M, Ctl &C, const
     const uint32_t hh = atomicAdd(&C.nhub, 1u);
     if (hh < (uint32_t)MAXHUB) M.hub_list[hh] = p.c;
   }
-  if (idx == (uint32_t)HUBL) {  // too many for a hub block: a sorted run; partitioned: a cut (k_refit2)
+  if (idx == (uint32_t)HUBL && !sorted) {  // too many for a hub block: a sorted run (single engine or partitioned)
     if (M.dist) C.overflow = 1;
     else C.force_run = 1;
   }
@@ -347,11 +348,73 @@ __device__ void run_chunk_end(const P2PDev &M, uint64_t r0, uint64_t rW, uint64_
   __syncthreads();
 }
 
+// ---- partitioned sorted runs (DIST) ----
+// A window some rank cannot hold (more than WCAP candidates, or a hub beyond HUBL) becomes a sorted run: every
+// rank sorts its candidates once (host step: k_drun_clear, k_rs_*, k_drun_start; the run lives in rn_*), and the
+// run is dispatched in chunks — chunk k is every rank's run entries with key <= g_k, g_k the smallest of the
+// ranks' fitting keys (the key of a rank's WCAP-th remaining entry; none when the rest fits).  A key prefix of a
+// safe window is safe, and every child of a run event sorts after the whole run (the run window was bounded by
+// the pending set's lookahead), so the chunks are the sequential order's windows; their children stay pending
+// until the run ends.  The first chunk is formed after the exchange of the fitting keys (k_drun_first), every
+// later one by k2_pa with g from the last window's X1 summaries (k_dfin2): no host step per chunk.
+
+// A chunk cut at g ends inside a same-ts group (g is a real key: its uid part is below 0xffffffff; a back-off or
+// group-end cut is ((ts << 32) | 0xffffffff)): its DoForwardUp leaves at that ts are queued.
+__device__ __forceinline__ bool drun_cuts_group(uint64_t g, uint64_t bound) {
+  return g < bound && (uint32_t)g != 0xffffffffu;
+}
+// The chunk's bound: the run window's, capped at the cut key g.
+__device__ __forceinline__ WinBound drun_bound(const Ctl &C, uint64_t g) {
+  WinBound b;
+  b.tmin = C.drb_tmin;
+  b.span = C.drb_span;
+  b.bound = C.drb_bound < g ? C.drb_bound : g;
+  b.stop_packed = C.drb_stop;
+  b.nbound = C.drb_nbound;
+  b.lim = C.drb_lim;
+  return b;
+}
+// Thread t (< WCAP, NT per block, every thread of the block calls it): run entry r0 + t, if its key is <= g,
+// becomes window record t (the entries <= g are a prefix: the run is sorted); the block's count goes to C.W.
+// The thread of the chunk's last entry (thread 0 when the chunk is empty) advances the run and puts this rank's
+// fitting key for the next chunk and its entries left into the rank's X1 summary.
+template <int NT>
+__device__ void drun_chunk(const P2PDev &M, Ctl &C, uint64_t t, uint64_t r0, uint64_t rW, uint64_t g) {
+  const uint64_t i = r0 + t;
+  const bool take = t < (uint64_t)WCAP && i < rW && M.rn_key[i] <= g;
+  const bool next = t + 1 < (uint64_t)WCAP && i + 1 < rW && M.rn_key[i + 1] <= g;
+  NtClaim cl{0, NOSRC, 0};
+  if (take) {
+    const uint64_t key = M.rn_key[i];
+    const uint32_t ctx = M.rn_ctx[i], kind = M.rn_kind[i], a = M.rn_a[i];
+    M.wkey[t] = key;
+    M.wctx[t] = ctx;
+    M.wkind[t] = kind;
+    M.wa[t] = a;
+    M.wpkt[t] = M.rn_pkt[i];
+    M.wsrc[t] = M.rn_src[i];
+    cl = node_table_claim(M, (uint32_t)t, lp_of(M, ctx, kind, a), kind);
+  }
+  const uint32_t nb = (uint32_t)__syncthreads_count(take);
+  if (threadIdx.x == 0 && nb) atomicAdd(&C.W, nb);
+  node_table_finish(M, C, cl, true);
+  if ((take && !next) || (t == 0 && !take)) {
+    const uint64_t r1 = take ? i + 1 : r0;
+    C.dr1 = r1;  // (k_dfin2 advances dr0: this kernel's other blocks may still be loading it)
+    X1Hdr *hs = x1hdr(M.x1_send, 0);
+    hs->rrem = rW - r1;
+    hs->rkey = rW - r1 > (uint64_t)WCAP ? M.rn_key[r1 + WCAP - 1] : ~0ull;
+    hs->rhead = rW > r1 ? M.rn_key[r1] : ~0ull;
+    if (g < C.drb_bound) C.refits++;
+  }
+}
+
 // ---- k2_pa ----
 // DIST: a partitioned rank's variant: children on other ranks' nodes are skipped (they travel through
 // X2), the remote events the last X2 brought are classified like children (a role of whole blocks
 // after the slot blocks), the rank's reduction goes to its X1 summary, and a window the host cut
-// (k_cut2: C.prep) is already formed.
+// (the first chunk of a partitioned sorted run, k_drun_first: C.prep) is already formed; during such a run
+// (C.drun) every k2_pa moves the run's next chunk in, and children, remote events and the pool stay pending.
 // WIDE: the single engine's wide windows (the last window's local records are appended too).
 // k2_pa's grid (single engine): the slot blocks, then as many blocks of the pool sweep as GRID_POOL leaves
 template <bool WIDE>
@@ -392,6 +455,11 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const uint64_t hts = C.hts, c_ptmin = C.ptmin, K0 = C.pK0, ilim = C.pinline_lim, c_P = C.P_end;
   const uint64_t c_span_t = WIDE ? C.span_t : 0;
   const uint32_t c_pdf = DF ? C.pdf : 0u;
+  // partitioned sorted run: this window is a chunk (children, remote events and the pool stay pending)
+  const bool drun = DIST && C.drun != 0;
+  const uint64_t c_dr0 = DIST ? C.dr0 : 0, c_drW = DIST ? C.drW : 0, c_drg = DIST ? C.drg : 0;
+  const uint64_t c_drlo = DIST ? C.drlo : ~0ull;
+  const bool dtrim = DIST && C.dtrim != 0;  // a run ended after a cut group: its entries left outside the pool
   const uint64_t c_wn = DF ? C.windows : 0;  // (this window's index: the last one is c_wn - 1)
   const int64_t look_mine = threadIdx.x < K_NKINDS       ? M.lookahead[threadIdx.x]
                             : threadIdx.x < 2 * K_NKINDS ? (WIDE ? M.lookw[threadIdx.x - K_NKINDS] : 0)
@@ -466,7 +534,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const bool run = c_mode == MODE_RUN;
   const bool partition = c_done == 0;
   Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[rt];
-  WinBound b = window_bound(rt ? red0 : red1, WIDE && !run, c_span_t);
+  WinBound b = drun ? drun_bound(C, c_drg) : window_bound(rt ? red0 : red1, WIDE && !run, c_span_t);
   // a pending host closure (nsgpu_p2p_advance) cuts the window at its key, like Simulator::Stop: the
   // window holds the device events before it, and the pipeline pauses for the host after the window
   bool hcap = false;
@@ -494,8 +562,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     // the window's last timestamp (W_end, or the host event's): other children of this window can land
     // there with smaller uids than a DoForwardUp leaf its events schedule, so those leaves are queued
     // (K_FWD_UP_D), not run inline; a leaf of an earlier timestamp has every same-time event in the window
-    const uint64_t edge = hcap ? hrel : b.span;
-    C.split_lo = ~0ull;
+    // (a run chunk cut inside a same-ts group: that group's ts)
+    const uint64_t edge = hcap ? hrel : (drun && drun_cuts_group(c_drg, C.drb_bound)) ? (c_drg >> 32) : b.span;
+    C.split_lo = drun ? c_drlo : ~0ull;  // (a chunk continuing a cut group queues that group's leaves too)
     C.split_hi = edge;
     C.hrel = edge;
     C.hcap = hcap;
@@ -590,7 +659,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
             valid = partition && (!DIST || M.owner[e.ctx] == M.rank);
           }  // (a local record's child ran in the last window itself)
         }
-        k2_classify<WIDE>(s_look, b, run, valid, e, NOSRC, R, tmn, wnd, wndw, gin[q], gpk[q]);
+        k2_classify<WIDE>(s_look, b, run || drun, valid, e, NOSRC, R, tmn, wnd, wndw, gin[q], gpk[q]);
         ge[q] = e;
         cw += gin[q];
         cf += gpk[q];
@@ -618,7 +687,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
       if (valid) e = x2rec(M, M.x2_recv, q)[rec];
       bool gin, gpk;
-      k2_classify<WIDE>(s_look, b, false, valid, e, NOSRC, R, tmn, wnd, wndw, gin, gpk);
+      k2_classify<WIDE>(s_look, b, drun, valid, e, NOSRC, R, tmn, wnd, wndw, gin, gpk);
       uint32_t w0;
       uint64_t f0;
       block_alloc2<TB>(C, gin, gpk, w0, f0);
@@ -632,6 +701,27 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     const uint64_t P = c_P;
     const uint64_t pb = blockIdx.x - (uint64_t)(NSGB + rrb), npb = gridDim.x - (uint64_t)(NSGB + rrb);
     static_assert(PPT <= NPEND, "pending claims");
+    // a partitioned run's chunk: the first WCAP / TB of these blocks move it in (then they sweep the pool too);
+    // after a run that ended at a cut group, they return its entries left that are not in the pool (children /
+    // remote events of the run's window) to pending: window records or parked, as the children above
+    if (DIST && drun && pb < (uint64_t)(WCAP / TB)) drun_chunk<TB>(M, C, pb * TB + threadIdx.x, c_dr0, c_drW, c_drg);
+    if (DIST && dtrim && pb < (uint64_t)(WCAP / TB)) {
+      for (uint64_t c0 = c_dr0 + pb * TB; __syncthreads_or(c0 < c_drW); c0 += (uint64_t)(WCAP / TB) * TB) {
+        const uint64_t i = c0 + threadIdx.x;
+        const bool valid = i < c_drW && M.rn_src[i] == NOSRC;
+        Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
+        if (valid) {
+          const uint64_t k = M.rn_key[i];
+          e = Ev{C.drb_tmin + (k >> 32), (uint32_t)k, M.rn_ctx[i], M.rn_kind[i], M.rn_a[i], M.rn_pkt[i]};
+        }
+        bool gin, gpk;
+        k2_classify<WIDE>(s_look, b, false, valid, e, NOSRC, R, tmn, wnd, wndw, gin, gpk);
+        uint32_t w0;
+        uint64_t f0;
+        block_alloc2<TB>(C, gin, gpk, w0, f0);
+        node_table_finish(M, C, k2_write(M, C, b, e, NOSRC, gin, gpk, w0, f0));
+      }
+    }
     for (uint64_t c0 = pb * TB * PPT; c0 < P; c0 += npb * TB * PPT) {  // block-uniform trip count
 #pragma unroll
       for (int q = 0; q < PPT; q++) node_table_finish(M, C, pend[q]);  // (the last chunk's)
@@ -665,7 +755,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 #pragma unroll
       for (int q = 0; q < PPT; q++) {
         const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
-        k2_classify<WIDE>(s_look, b, false, ge[q].ts != TOMB, ge[q], (uint32_t)i, R, tmn, wnd, wndw, gin[q], gpk[q]);
+        k2_classify<WIDE>(s_look, b, drun, ge[q].ts != TOMB, ge[q], (uint32_t)i, R, tmn, wnd, wndw, gin[q], gpk[q]);
         cw += gin[q];
         if (gin[q]) {  // the window entry's record (its loads overlap the block allocation below)
           ge[q].ctx = M.ev_ctx[0][i];
@@ -703,6 +793,11 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   }
   PH_MARK(1);
   if (slot_block) BLK_MARK(42, c_win);
+  if (drun && g == 0) {  // the run's entries outside the pool are pending too (k_drun_red)
+    const uint64_t a = C.drn_tmin, w = C.drn_wend;
+    tmn = a < tmn ? a : tmn;
+    wnd = w < wnd ? w : wnd;
+  }
   publish_min<TB, WIDE>(R, tmn, wnd, wndw);
   digest = wave_sum64(digest);
   {  // one digest atomic per block
@@ -1770,6 +1865,7 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   // the run control and (holder blocks) the slot's record, all loaded at once
   const uint32_t c_done = C.done, c_mode = C.mode, W = C.W, c_wbase = C.wbase, c_fr = C.force_run, rt = C.rt,
                  c_nhub = C.nhub;
+  const uint32_t c_drun = M.dist ? C.drun : 0u;  // a partitioned run's chunk: key order, hubs in slot order
   __shared__ int64_t s_look[2 * K_NKINDS];
   const HCtl hc{C.tmin, C.inline_lim, C.split_lo, C.split_hi, C.lim_rel, s_look};
   const uint32_t lt_ = threadIdx.x;  // (loaded now, stored in LDS just before the block's first barrier)
@@ -1784,8 +1880,9 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
     const uint32_t i0 = bx * HB + threadIdx.x;
     sp = SlotPre{M.widx[i0], M.wctx[i0], M.wkind[i0], M.wa[i0], M.wkey[i0], M.wpkt[i0]};
   }
+  if (M.dist && bx == 0 && threadIdx.x == 0) C.dtrim = 0;  // (k2_pa returned a trimmed run's rest to pending)
   // partitioned: every rank's X0 payload (window candidates, hub flag): a window some rank cannot hold
-  // is cut by the host (k_refit2 / k_cut2) before anything of it runs, on every rank
+  // becomes a partitioned sorted run (the host's drun_sort, k_drun_first) before anything of it runs, on every rank
   bool ovf = false;
   if (M.dist) {  // (one lane per rank: HB = one wave)
     const uint32_t q = threadIdx.x;
@@ -1838,7 +1935,8 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
     if (handle) {
       const uint32_t hb = bx - NHB;
       const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
-      for (uint32_t h = hb; h < nh; h += NHUB) hub_node<WIDE>(M, C, M.hub_list[h], W, base, run, R, hb, lds, hc, &s_lcnt);
+      for (uint32_t h = hb; h < nh; h += NHUB)
+        hub_node<WIDE>(M, C, M.hub_list[h], W, base, run || c_drun != 0, R, hb, lds, hc, &s_lcnt);
     }
   } else if (bx < (uint32_t)K2_GRID_W) {
     maintain(M, C, bx - (NHB + NHUB), run, handle, W, c_nfree, c_nF, c_Pe);
