@@ -87,18 +87,17 @@ def test_rccl_single_rank():
     assert_same(o, g2)
 
 
-@pytest.mark.parametrize("nranks,interleaved", [(2, False), (3, True)])
-def test_incast_sorted_run_cuts_a_same_ts_group(nranks, interleaved):
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_incast_sorted_run_cuts_a_same_ts_group(nranks):
     """A partitioned sorted run (nsgpu_p2p_win.h): 5,000 leaves send to one hub at the same instant, so its
     windows hold 5,000 same-ts Receives whose DoForwardUp leaves are zero-delay children: more than a rank's
     WCAP, so the window becomes a run sorted once per rank and dispatched in chunks; chunks cut that same-ts group
-    (its leaves queued), the chunk that ends it ends the run, and the rest returns to pending.  Full pop log."""
+    (its leaves queued), the chunk that ends it ends the run, and the rest returns to pending.  The hub and 4,000
+    leaves on rank 0, the last 1,000 leaves over the other ranks (X2 holds at most 1,024 remote events a peer a
+    window).  Full pop log."""
     sc = p2p.incast(5000, stop_ns=1_020_000_000, sim_stop_ns=1_040_000_000)
-    if interleaved:
-        owner = (np.arange(sc.n_nodes) % nranks).astype(np.uint32)
-    else:
-        owner = np.zeros(sc.n_nodes, np.uint32)
-        owner[1 + (sc.n_nodes - 1) // 2:] = 1
+    owner = np.zeros(sc.n_nodes, np.uint32)
+    owner[4001:] = 1 + (np.arange(1000) * (nranks - 1)) // 1000
     o = oracle(sc, 400000)
     g = p2p.LoopbackGroup(sc, nranks, owner=owner, log_cap=400000).run(log_n=400000)
     assert g[0].refits > 0
