@@ -182,7 +182,9 @@ struct Ctl {
   uint64_t drlo;              // the next chunk continues the same-ts group the last one cut: its rel ts (~0: no)
   uint32_t drtrim, dtrim;     // the next chunk ends that group and the run after it; the run ended so: the next
                               // k2_pa returns this rank's entries left that are not in the pool to pending
-  uint64_t drn_tmin, drn_wend;  // the reduction of this rank's run entries outside the pool (k_drun_red)
+  uint64_t drn_tmin, drn_wend;  // the pending set's reduction at the run's start, its own entries included (k2_pa
+  uint64_t drn_stopts;          // folds it into every chunk's instead of sweeping the pool)
+  uint32_t drn_stopuid, drpad2;
   uint64_t drb_tmin, drb_span, drb_bound, drb_stop, drb_nbound, drb_lim;  // the run window's bound (WinBound)
 };
 
@@ -1222,18 +1224,24 @@ __global__ void k_drun_start(const P2PDev M, uint64_t n) {
   C.drlo = ~0ull;
   C.drtrim = 0;
   C.dtrim = 0;
-  C.drn_tmin = C.drn_wend = ~0ull;
+  {  // the pending set outside the run, as the overflowing window's k2_pa reduced it (the run's entries: k_drun_red)
+    const Red r = x1hdr(M.x1_send, 0)->red;
+    C.drn_tmin = r.tmin;
+    C.drn_wend = r.wend;
+    C.drn_stopts = r.stopts;
+    C.drn_stopuid = r.stopuid;
+  }
   M.xk_send[0] = n > (uint64_t)WCAP ? M.rn_key[WCAP - 1] : ~0ull;  // (this rank's fitting key)
   M.xk_send[1] = n ? M.rn_key[0] : ~0ull;                           // (its head key)
 }
-// The run's entries that are not in the pool (children and remote events of the window before) stay pending
-// outside it until their chunk: their reduction is folded into every chunk's (conservatively: all of them).
+// During the run the pool is not swept: the pending set's reduction at its start (k_drun_start) and the run's
+// entries' (all of them: conservative, some are dispatched before the run ends) are folded into every chunk's; the
+// chunks' children fold in as they are parked.  So the first window after the run is bounded safely.
 __global__ __launch_bounds__(256) void k_drun_red(const P2PDev M, uint64_t n) {
   Ctl &C = *M.C;
   const uint64_t tmin = C.drb_tmin;
   uint64_t tmn = ~0ull, wnd = ~0ull;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-    if (M.rn_src[i] != NOSRC) continue;
     const uint64_t ts = tmin + (M.rn_key[i] >> 32);
     const uint64_t x = ts + (uint64_t)M.lookahead[(M.rn_kind[i] & 0xffu) % K_NKINDS];
     tmn = ts < tmn ? ts : tmn;
@@ -2071,6 +2079,10 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   }
   TRY(dalloc(h, &M.C, 1));
   if (owner) M.x0_send = reinterpret_cast<uint64_t *>(&M.C->W);  // X0 sends (W, nxtP, overflow, prep)
+  if (owner && nranks == 1) {  // one rank: its exchanges are its own payloads in place (no copies in the window)
+    M.x0_recv = M.x0_send;
+    M.x2_recv = M.x2_send;  // (with one rank no child is remote: X2 stays empty)
+  }
   TRY(dalloc(h, &M.error, 4));
   M.log_cap = log_cap;
   TRY(dalloc(h, &M.log_ts, log_cap));
@@ -2177,13 +2189,13 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
   NSGPU_HIP(hipMemsetAsync(M.error, 0, 4 * sizeof(uint32_t), s));
   if (M.dist) {
     const size_t R = M.nranks;
-    NSGPU_HIP(hipMemsetAsync(M.x0_recv, 0, X0B * R, s));
+    if (M.x0_recv != M.x0_send) NSGPU_HIP(hipMemsetAsync(M.x0_recv, 0, X0B * R, s));
     NSGPU_HIP(hipMemsetAsync(M.xk_send, 0, 16, s));
     NSGPU_HIP(hipMemsetAsync(M.xk_recv, 0, 16 * R, s));
     NSGPU_HIP(hipMemsetAsync(M.x1_recv, 0, X1B * R, s));
     NSGPU_HIP(hipMemcpyAsync(M.x1_send, &h->x1h0, sizeof(X1Hdr), hipMemcpyHostToDevice, s));  // (its own slot)
     NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, M.x2b * R, s));
-    NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, M.x2b * R, s));
+    if (M.x2_recv != M.x2_send) NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, M.x2b * R, s));
     NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 4 * WCAP * sizeof(uint32_t), s));
   }
   if (M.log_cap) {  // (partitioned: every rank writes only the entries it dispatches, the union is the log;

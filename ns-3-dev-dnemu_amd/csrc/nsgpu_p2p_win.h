@@ -693,6 +693,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       block_alloc2<TB>(C, gin, gpk, w0, f0);
       pend[0] = k2_write(M, C, b, e, NOSRC, gin, gpk, w0, f0);
     }
+  } else if (partition && !run && drun) {
+    // ---- a partitioned run's chunk (the pool is not swept during the run: its reduction is folded below)
+    const uint64_t pb = blockIdx.x - (uint64_t)(NSGB + rrb);
+    if (pb < (uint64_t)(WCAP / TB)) drun_chunk<TB>(M, C, pb * TB + threadIdx.x, c_dr0, c_drW, c_drg);
   } else if (partition && !run) {
     // ---- the pool, in place: read (ts, uid, kind) of every slot; window events are copied out.
     // Chunks of PPT x TB entries per block (loads of a chunk all in flight), one allocation per chunk;
@@ -701,10 +705,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     const uint64_t P = c_P;
     const uint64_t pb = blockIdx.x - (uint64_t)(NSGB + rrb), npb = gridDim.x - (uint64_t)(NSGB + rrb);
     static_assert(PPT <= NPEND, "pending claims");
-    // a partitioned run's chunk: the first WCAP / TB of these blocks move it in (then they sweep the pool too);
-    // after a run that ended at a cut group, they return its entries left that are not in the pool (children /
-    // remote events of the run's window) to pending: window records or parked, as the children above
-    if (DIST && drun && pb < (uint64_t)(WCAP / TB)) drun_chunk<TB>(M, C, pb * TB + threadIdx.x, c_dr0, c_drW, c_drg);
+    // after a partitioned run that ended at a cut group, the first WCAP / TB of these blocks return its entries
+    // left that are not in the pool (children / remote events of the run's window) to pending: window records or
+    // parked, as the children above (then they sweep the pool too)
     if (DIST && dtrim && pb < (uint64_t)(WCAP / TB)) {
       for (uint64_t c0 = c_dr0 + pb * TB; __syncthreads_or(c0 < c_drW); c0 += (uint64_t)(WCAP / TB) * TB) {
         const uint64_t i = c0 + threadIdx.x;
@@ -793,10 +796,14 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   }
   PH_MARK(1);
   if (slot_block) BLK_MARK(42, c_win);
-  if (drun && g == 0) {  // the run's entries outside the pool are pending too (k_drun_red)
-    const uint64_t a = C.drn_tmin, w = C.drn_wend;
+  if (drun && g == 0) {  // the pending set of the run's start and the run's entries (k_drun_start, k_drun_red)
+    const uint64_t a = C.drn_tmin, w = C.drn_wend, st = C.drn_stopts;
     tmn = a < tmn ? a : tmn;
     wnd = w < wnd ? w : wnd;
+    if (st != ~0ull) {
+      R.stopts = st;
+      R.stopuid = C.drn_stopuid;
+    }
   }
   publish_min<TB, WIDE>(R, tmn, wnd, wndw);
   digest = wave_sum64(digest);
