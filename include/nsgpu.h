@@ -201,9 +201,12 @@ int nsgpu_wifil_receivers(nsgpu_wifil *h, uint32_t phy, uint32_t *n);  /* uids o
 int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base, uint32_t phy, uint32_t size, double dbm,
                      uint32_t modclass, uint64_t rate, uint32_t bw, uint32_t preamble);
 /* every device event with a key below (bound_ts, bound_uid) (~0: all): ranks from *dispatched, the syncs'
- * EndReceive uids from *uid, digest terms and log entries (at their ranks, below log_cap) added */
+ * EndReceive uids from *uid, log entries (at their ranks, below log_cap) written.  The epoch's digest terms
+ * are summed by kernels that run behind the next epochs (the order is not on the PHY's critical path): each
+ * call adds to *digest the terms summed so far; nsgpu_wifil_flush adds the rest. */
 int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t bound_uid, uint32_t *uid, uint64_t *dispatched,
                         uint64_t *digest, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap);
+int nsgpu_wifil_flush(nsgpu_wifil *h, uint64_t *digest);  /* waits for every epoch's order; adds its digest terms */
 int nsgpu_wifil_get_state(nsgpu_wifil *h, uint32_t phy, uint64_t now, nsgpu_wifil_phy_state *out);
 /* MobilityModel::SetPosition of phy's node (src/mobility/model/mobility-model.cc): the later SendPackets'
  * YansWifiChannel::Send fan-outs (yans-wifi-channel.cc:92-96) read the new position */

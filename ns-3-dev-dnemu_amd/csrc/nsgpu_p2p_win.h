@@ -1492,10 +1492,9 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   HStat hs{0, 0, 0, 0, false};
   // the passes go through the list 64 events at a time: every lane loads one event's record into
   // LDS (one memory round trip per batch), then the serial work reads LDS
+  // (LDS words: key [0, 2 HB), slot [2 HB, 3 HB), then the hub events at 11 HB)
   uint64_t *b_key = reinterpret_cast<uint64_t *>(lds);  // [HB]
-  uint32_t *b_s = lds + 2 * HB, *b_kind = lds + 3 * HB, *b_a = lds + 4 * HB, *b_sl = lds + 5 * HB;
-  uint32_t *b_ctx = lds + 6 * HB;
-  Pkt *b_pkt = reinterpret_cast<Pkt *>(lds + 7 * HB);     // [HB]
+  uint32_t *b_s = lds + 2 * HB;
   HubEv *b_h = reinterpret_cast<HubEv *>(lds + 11 * HB);  // [HB]
   // 2. node parts: the stateless ones (TransmitComplete, NetDevice::Start, Receive -> IpForward: rx
   //    counter, MacRx trace, route, TTL) by their own lane, the others serially by lane 0 in key order.

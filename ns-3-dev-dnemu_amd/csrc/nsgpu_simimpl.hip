@@ -511,7 +511,7 @@ int nsgpu_sim_run(nsgpu_sim *s) {  // Run (:153-165): windows of closures (and d
     if (n == 0) break;
     if ((rc = run_window(s, w.data(), n))) return rc;
   }
-  return NSGPU_OK;
+  return s->wifi ? nsgpu_wifil_flush(s->wifi, &s->digest) : NSGPU_OK;  // (the epochs' digest terms still summing)
 }
 
 int nsgpu_sim_run_one(nsgpu_sim *s) {  // RunOneEvent (:167-170)
@@ -620,6 +620,10 @@ int nsgpu_sim_host_stats(nsgpu_sim *s, uint64_t *host_dispatched, uint64_t *canc
   if (!s) return set_error(NSGPU_EINVAL, "nsgpu_sim_host_stats: null");
   if (host_dispatched) *host_dispatched = s->host_dispatched;
   if (cancelled) *cancelled = s->cancelled;
+  if (s->wifi) {
+    int rc = nsgpu_wifil_flush(s->wifi, &s->digest);
+    if (rc) return rc;
+  }
   if (digest) *digest = s->digest;
   return NSGPU_OK;
 }

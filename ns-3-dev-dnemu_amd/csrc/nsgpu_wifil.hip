@@ -24,6 +24,7 @@
 // RingNi layout of nsgpu_wifi.hip, with its eager prefix cursor), the state helper's end times, the pending
 // Receive queue (sorted by (arrival, uid)) and up to LPE_CAP pending EndReceive records.
 #include <algorithm>
+#include <cstring>
 #include <vector>
 #include "nsgpu_device.h"
 #include "nsgpu_internal.h"
@@ -68,6 +69,10 @@ struct LPhy {  // a phy's state between epochs
   uint32_t rq_head, rq_len, live, ni_max;
   nsgpu_wifi_phy_counters c;
 };
+struct WMir {  // a phy's state helper fields in pinned host memory: GetState reads them with no device trip
+  int64_t endTx, endRx, endCca;
+  uint32_t rxing, pad;
+};
 struct LEv {  // one dispatched device event of the epoch
   uint64_t ts;
   uint32_t uid, ctx, sslot, pad;
@@ -75,6 +80,7 @@ struct LEv {  // one dispatched device event of the epoch
 struct LSync {  // one sync of the epoch (its EndReceive's uid comes from the sync order)
   uint64_t sts;
   uint32_t suid, euid;
+  uint32_t loc, pad;  // its pending EndReceive record: pe[loc]
 };
 struct LCk {  // one chunk of an EndReceive's CalculatePer walk, evaluated by k_wl_mid: the noise before it,
   double noise;  // and (duration << 1) | (1: the PLCP header mode)
@@ -103,14 +109,16 @@ struct WDev {
   nsgpu_wifil_end *ends;
   uint32_t *end_sslot;
   uint32_t *cnt;  // [0] events, [1] syncs, [2] ends, [3] error bits (sticky: a SendPacket's are seen at the
-                  // next advance), [4] chunk slots claimed (zeroed by k_wl_resolve)
+                  // next advance), [4] chunk slots claimed (zeroed by k_wl_tsort)
   LCk *ck;        // the epoch's deferred chunks (ck_cap; a walk that finds no room computes its PER inline)
   LEck *eck;      // per end record
   uint32_t *evc;             // the epoch's event-list stripes: EV_STRIPES counters, EV_STRIDE words apart
   LEv *evd;                  // the epoch's events in dense order, uids resolved (the host's copy)
-  ulonglong2 *evk;           // the epoch's events' keys (ts, resolved uid) in dense order (k_wl_resolve)
-  uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_order, when logging)
-  unsigned long long *edig;  // the epoch's digest terms, summed on the device (k_wl_edigest)
+  uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_rank, when logging)
+  ulonglong2 *evg;           // the epoch's keys (ts, uid << 32 | dense index), sorted by tiles (k_wl_tsort)
+  uint32_t *ticket;          // k_wl_rank's blocks done (its last block writes the status block; reset there)
+  WMir *mir;                 // (mapped host memory) each phy's state fields: a lane whose phy changed writes them
+  unsigned long long *edig;  // every ordered epoch's digest terms, summed on the device (k_wl_rank)
   uint64_t sync_cap, ev_cap, end_cap, ck_cap;
   uint64_t ev_scap;  // events per stripe (stripe s holds ev[s * ev_scap, s * ev_scap + evc[s * EV_STRIDE]))
 };
@@ -322,6 +330,29 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t *ctr) {
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
+// YansWifiChannel::Send's delivery of transmission t (index k, from the closure's uid base) to phy j (not the
+// sender): its Receive — ConstantSpeed delay, the loss chain + RxGain, DbmToW, the receiver loop's uid.
+__device__ __forceinline__ bool reception(const WDev &D, int64_t j, const LTx &t, uint32_t k, double dbm, uint32_t base,
+                                          LRx &out) {
+  const uint32_t s = t.phy;
+  if (D.chan[j] != D.chan[s]) return false;  // other channels get nothing (yans-wifi-channel.cc:88-91)
+  const double dist = distance3(D.x[s], D.y[s], D.z[s], D.x[j], D.y[j], D.z[j]);
+  const uint64_t at = t.ts + (uint64_t)seconds_to_ts(dist / D.speed);  // ConstantSpeed delay (propagation-delay-model.cc:90-96)
+  const double dBm = calc_rx_power(D.loss, dbm, dist) + D.rx_gain_db;      // StartReceivePacket: rxPowerDbm += RxGain
+  const double w = pow(10.0, dBm / 10.0) / 1000.0;                         // DbmToW (yans-wifi-phy.cc:727-732)
+  out = LRx{at, base + D.chan_rank[j] - (j > (int64_t)s ? 1u : 0u), k, w, t.dur};  // the receiver loop's Schedule order
+  return true;
+}
+// The SendPackets one host closure made since the last epoch, applied by the next epoch launch (more than
+// NSEND: the earlier ones by k_wl_send launches).
+constexpr uint32_t NSEND = 8;
+struct SendBatch {
+  uint32_t n, k0;  // SendPackets; the first one's transmission index (they are k0 .. k0 + n - 1)
+  LTx t[NSEND];
+  double dbm[NSEND];
+  uint32_t base[NSEND];
+};
+
 // ---- the NiChanges ring of one phy (RingNi of nsgpu_wifi.hip: time-sorted, eager prefix cursor) ----
 __device__ __forceinline__ void ni_insert(LNi *ring, uint32_t head, uint32_t &len, uint32_t m, int64_t t, double d) {
   // AddNiChangeEvent (interference-helper.cc:378-383): at upper_bound (time).  The entries after it (a
@@ -372,12 +403,23 @@ __device__ __forceinline__ bool pe_before(const LPe &a, const LPe &b) {
   return a.sts != b.sts ? a.sts < b.sts : a.suid < b.suid;
 }
 
+__device__ __forceinline__ WMir mir_of(const LPhy &P) { return WMir{P.endTx, P.endRx, P.endCca, P.rxing, 0}; }
+__device__ __forceinline__ void mir_put(const WDev &D, int64_t j, const WMir &m0, const LPhy &P) {
+  if (P.endTx != m0.endTx || P.endRx != m0.endRx || P.endCca != m0.endCca || P.rxing != m0.rxing) D.mir[j] = mir_of(P);
+}
+
 // One phy's events of the epoch: every pending Receive / EndReceive with a key below (bts, buid).
 #ifdef NSGPU_PHASE_PROF
 // diagnostic build: [0] sum over epochs of the slowest lane's time, [1] sum of lane times, [2] lanes, [3] events,
 // [4] sum over epochs of the most events one lane ran, [5] epochs, [6] max lane time, [7] its events
 __device__ unsigned long long g_wl_ph[8];
 __device__ unsigned long long g_wl_ep[2];  // the current epoch's slowest lane time / most events (reset by host)
+// k_wl_stepw's waves: [0..4] waves with 0, 1, 2, 3, 4+ events, [5..9] their summed lifetimes (s_memtime),
+// [10] the longest lifetime, [11] its events, [12] summed epoch spans (last end - first start), [13] / [14]
+// the running epoch's first start / last end, [15] summed epoch dispatch spreads (last start - first start);
+// g_sw2: [0] the running epoch's last start, [1..3] summed sections (loads, event loop, flush + write-backs)
+__device__ unsigned long long g_sw[16];
+__device__ unsigned long long g_sw2[4];
 #endif
 __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint32_t buid) {
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -387,6 +429,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
   uint32_t pev = 0;
 #endif
   LPhy P = D.ps[j];
+  const WMir m0 = mir_of(P);
   LNi *ring = D.ni + (uint64_t)j * (D.ni_mask + 1);
   LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
   LPe *pe = D.pe + (uint64_t)j * LPE_CAP;
@@ -559,7 +602,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
         err |= q < 0 ? WE_PECAP : WE_CAP;
         break;
       }
-      D.sync[sl] = LSync{r.at, r.uid, NONE};
+      D.sync[sl] = LSync{r.at, r.uid, NONE, (uint32_t)(j * LPE_CAP + q), 0};
       pe[q] = LPe{(uint64_t)endNew, r.at, r.uid, NONE, r.tx, 0, sl, 1, r.w};
       P.live = (uint32_t)q;
       P.rxing = 1;
@@ -604,6 +647,7 @@ __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint
 #endif
   }
   D.ps[j] = P;
+  mir_put(D, j, m0, P);
   if (err) atomicOr(&D.cnt[3], err);
 #ifdef NSGPU_PHASE_PROF
   const uint64_t dt = __builtin_amdgcn_s_memrealtime() - pt0;
@@ -688,25 +732,196 @@ __device__ __forceinline__ void w_ni_insert(LNi *ring, uint32_t head, uint32_t &
   len++;
 }
 
-__global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uint32_t buid) {
+// The epoch kernel's per-wave staging (r05): the ring of NiChanges in LDS (RL entries; a longer ring stays
+// in HBM), the Receive queue in the wave's registers (64 entries; more: HBM, 64 a trip), and the epoch's
+// appends — dispatched events, end records, syncs — staged in LDS and claimed with one atomic per list
+// per wave (the r04 kernel waited one atomic round trip per event).  A staged sync's slot is LOCAL | index
+// until the claim; the staged events, end records and pending records that name it are patched then.
+constexpr uint32_t RL = 256;
+constexpr uint32_t EVB = 64, ENB = 8, SYB = 8;
+constexpr uint32_t LOCAL = 0x80000000u;
+struct LEnd {  // a staged end record
+  nsgpu_wifil_end rec;
+  LEck eck;
+  uint32_t sl, pad;
+};
+__device__ __forceinline__ LRx rl_rx(const LRx &a, int u) {
+  return LRx{(uint64_t)rl_i64((int64_t)a.at, u), rl_u32(a.uid, u), rl_u32(a.tx, u), rl_d(a.w, u), rl_i64(a.dur, u)};
+}
+__device__ __forceinline__ LRx shfl_up_rx(const LRx &a) {
+  LRx b;
+  b.at = (uint64_t)__shfl_up((long long)a.at, 1);
+  b.uid = (uint32_t)__shfl_up((int)a.uid, 1);
+  b.tx = (uint32_t)__shfl_up((int)a.tx, 1);
+  b.w = __shfl_up(a.w, 1);
+  b.dur = (int64_t)__shfl_up((long long)a.dur, 1);
+  return b;
+}
+
+// One epoch of every phy, a wave each: first the SendPackets the last host closure made (nsgpu_wifil_send
+// batches up to NSEND of them into this launch: the sender's switch and this phy's Receive of each, what
+// k_wl_send does — they precede every event of the epoch), then every pending Receive / EndReceive with a
+// key below (bts, buid), in (ts, uid) order.
+__global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uint32_t buid, const SendBatch sb) {
   const int64_t j = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   if (j >= D.nphy) return;
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+  uint64_t pt1 = pt0, pt2 = pt0;
+  uint32_t pev = 0;
+#endif
+  __shared__ LNi s_ring[RL];
+  __shared__ LEv s_ev[EVB];
+  __shared__ LEnd s_end[ENB];
+  __shared__ LSync s_sy[SYB];
   LPhy P = D.ps[j];
-  LNi *ring = D.ni + (uint64_t)j * (D.ni_mask + 1);
+  const WMir m0 = mir_of(P);
+  LNi *const gring = D.ni + (uint64_t)j * (D.ni_mask + 1);
   LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
   LPe *pe = D.pe + (uint64_t)j * LPE_CAP;
-  const uint32_t m = D.ni_mask, ctx = D.node[j];
+  const uint32_t gm = D.ni_mask, ctx = D.node[j];
   uint32_t *const evc = D.evc + (uint32_t)(j % EV_STRIPES) * EV_STRIDE;
   LEv *const evs = D.ev + (uint64_t)(j % EV_STRIPES) * D.ev_scap;
   uint32_t err = 0;
-  // the pending EndReceive records: lane q < LPE_CAP holds record q for the whole epoch (the kernel's own
-  // changes are made to both copies); the Receive queue: lane l holds entry head + rq0 + l, 64 a trip
+#pragma unroll
+  for (uint32_t u = 0; u < NSEND; u++)  // (constant indices into the batch: no scratch copy of it)
+    if (j == 0 && lane == u && u < sb.n) D.tx[sb.k0 + u] = sb.t[u];
+  // the pending EndReceive records: lane q < LPE_CAP holds record q for the whole epoch (written back at the
+  // end when changed)
   LPe mine{};
   if (lane < (uint32_t)LPE_CAP) mine = pe[lane];
+  bool pe_dirty = false, changed = false;
+  // ---- the batched SendPackets: lane i computes this phy's Receive of send i (YansWifiChannel::Send)
+  LRx my{};
+  bool ok = false;
+  {
+    LTx t{};
+    double dbm = 0.0;
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < NSEND; u++)
+      if (lane == u) t = sb.t[u], dbm = sb.dbm[u], base = sb.base[u];
+    if (lane < sb.n && t.phy != (uint32_t)j) ok = reception(D, j, t, sb.k0 + lane, dbm, base, my);
+  }
+  const uint64_t okm = __ballot(ok);
+  const uint32_t nins = (uint32_t)__popcll(okm);
+#pragma unroll
+  for (uint32_t i = 0; i < NSEND; i++) {  // the sender's switch (YansWifiPhy::SendPacket, yans-wifi-phy.cc:499-522)
+    if (i >= sb.n) break;
+    if (sb.t[i].phy != (uint32_t)j) continue;
+    const LTx &t = sb.t[i];
+    changed = true;
+    if (P.endTx > (int64_t)t.ts) {  // NS_ASSERT (!IsStateTx ()); SwitchToTx from TX: NS_FATAL_ERROR (:285-287)
+      err |= WE_TX_IN_TX;
+      continue;
+    }
+    if (P.rxing) {  // m_endRxEvent.Cancel (); NotifyRxEnd (); SwitchToTx's RX case (:263-268)
+      if (lane == P.live) mine.can = 1;
+      pe_dirty = true;
+      P.live = NONE;
+      P.rxing = 0;
+      P.endRx = (int64_t)t.ts;
+    }
+    P.endTx = (int64_t)t.ts + t.dur;
+  }
+  // ---- the Receive queue and the ring: registers and LDS when they fit
+  const bool fast = P.rq_len + nins <= 64 && P.len + 2 * (P.rq_len + nins) + 2 <= RL;
   uint32_t rq0 = ~0u;  // (queue offset of the loaded chunk; ~0: none)
   LRx rqc{};
-  uint32_t rqn = 0;    // Receives taken this epoch
+  uint32_t qn = 0;     // (fast: entries in rqc)
+  if (nins) changed = true;
+  if (fast) {
+    rq0 = 0;
+    qn = P.rq_len;
+    if (lane < qn) rqc = rq[(P.rq_head + lane) & D.rq_mask];
+#pragma unroll
+    for (uint32_t u = 0; u < RL / 64; u++) {
+      const uint32_t i = u * 64 + lane;
+      if (i < P.len) s_ring[(P.head + i) & (RL - 1)] = gring[(P.head + i) & gm];
+    }
+    for (uint32_t i = 0; i < sb.n; i++) {  // (sorted by (arrival, uid): an insertion in registers)
+      if (!((okm >> i) & 1ull)) continue;
+      const LRx e = rl_rx(my, (int)i);
+      const bool lt = lane < qn && (rqc.at < e.at || (rqc.at == e.at && rqc.uid < e.uid));
+      const uint32_t pos = (uint32_t)__popcll(__ballot(lt));
+      const LRx up = shfl_up_rx(rqc);
+      if (lane > pos && lane <= qn) rqc = up;
+      if (lane == pos) rqc = e;
+      qn++;
+    }
+    P.rq_len = qn;
+    __syncthreads();
+  } else if (nins) {  // (k_wl_send's insertion into the HBM queue, in send order)
+    for (uint32_t i = 0; i < sb.n; i++) {
+      if (!((okm >> i) & 1ull)) continue;
+      const LRx e = rl_rx(my, (int)i);
+      if (P.rq_len > D.rq_mask) {
+        err |= WE_RQCAP;
+        continue;
+      }
+      if (lane == 0) {
+        uint32_t q = P.rq_len;
+        while (q > 0) {
+          const LRx x = rq[(P.rq_head + q - 1) & D.rq_mask];
+          if (x.at < e.at || (x.at == e.at && x.uid < e.uid)) break;
+          rq[(P.rq_head + q) & D.rq_mask] = x;
+          q--;
+        }
+        rq[(P.rq_head + q) & D.rq_mask] = e;
+      }
+      P.rq_len++;
+    }
+    __syncthreads();
+  }
+  LNi *const ring = fast ? s_ring : gring;
+  const uint32_t m = fast ? RL - 1 : gm;
+#ifdef NSGPU_PHASE_PROF
+  pt1 = __builtin_amdgcn_s_memtime();
+#endif
+  // ---- staged appends
+  uint32_t ns = 0, ne = 0, nv = 0;
+  auto flush = [&]() {  // claim the staged syncs, end records and events (one atomic each), patch, store
+    __syncthreads();
+    uint32_t bs = 0, be = 0, bv = 0;
+    if (lane == 0) {
+      if (ns) bs = atomicAdd(&D.cnt[1], ns);
+      if (ne) be = atomicAdd(&D.cnt[2], ne);
+      if (nv) bv = atomicAdd(evc, nv);
+    }
+    bs = rl_u32(bs, 0);
+    be = rl_u32(be, 0);
+    bv = rl_u32(bv, 0);
+    const auto fix = [&](uint32_t sl) { return sl != NONE && (sl & LOCAL) ? bs + (sl & ~LOCAL) : sl; };
+    if (ns) {
+      if ((uint64_t)bs + ns > D.sync_cap) err |= WE_CAP;
+      else if (lane < ns) D.sync[bs + lane] = s_sy[lane];
+      if (lane < (uint32_t)LPE_CAP) mine.sslot = fix(mine.sslot);
+    }
+    if (ne) {
+      if ((uint64_t)be + ne > D.end_cap) {
+        err |= WE_CAP;
+      } else if (lane < ne) {
+        const LEnd x = s_end[lane];
+        D.ends[be + lane] = x.rec;
+        D.end_sslot[be + lane] = fix(x.sl);
+        D.eck[be + lane] = x.eck;
+      }
+    }
+    if (nv) {
+      if ((uint64_t)bv + nv > D.ev_scap) {
+        err |= WE_CAP;
+      } else if (lane < nv) {
+        LEv v = s_ev[lane];
+        v.sslot = fix(v.sslot);
+        evs[bv + lane] = v;
+      }
+    }
+    ns = ne = nv = 0;
+    __syncthreads();
+  };
+  uint32_t rqn = 0;  // Receives taken this epoch
+  bool ring_dirty = false;
   for (;;) {
     // the next pending EndReceive (the selection reads the records lane by lane)
     const uint64_t used = __ballot(lane < (uint32_t)LPE_CAP && mine.used);
@@ -720,16 +935,11 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
     const bool hr = P.rq_len > 0;
     LRx r{};
     if (hr) {
-      if (rq0 == ~0u || rqn - rq0 >= 64) {  // (the next 64 queued Receives, one trip)
+      if (rq0 == ~0u || rqn - rq0 >= 64) {  // (HBM queue: the next 64 queued Receives, one trip)
         rq0 = rqn;
         rqc = lane < P.rq_len ? rq[(P.rq_head + lane) & D.rq_mask] : LRx{};
       }
-      const int u = (int)(rqn - rq0);
-      r.at = (uint64_t)rl_i64((int64_t)rqc.at, u);
-      r.uid = rl_u32(rqc.uid, u);
-      r.tx = rl_u32(rqc.tx, u);
-      r.w = rl_d(rqc.w, u);
-      r.dur = rl_i64(rqc.dur, u);
+      r = rl_rx(rqc, (int)(rqn - rq0));
     }
     bool take_r;
     if (hr && e >= 0) take_r = r.at < eb.ts || (r.at == eb.ts && (eb.euid == NONE || r.uid < eb.euid));
@@ -741,6 +951,10 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
     } else {
       if (!(eb.ts < bts || (eb.ts == bts && eb.euid != NONE && eb.euid < buid))) break;
     }
+    changed = true;
+#ifdef NSGPU_PHASE_PROF
+    pev++;
+#endif
     if (!take_r) {  // ---- YansWifiPhy::EndReceive (yans-wifi-phy.cc:770-799)
       const int64_t nw = (int64_t)eb.ts;
       nsgpu_wifil_end rec{eb.ts, eb.euid, (uint32_t)j, 0.0, 0.0, eb.tx, eb.can ? (uint32_t)NSGPU_WIFI_END_CANCELLED : 0u,
@@ -752,7 +966,15 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
       } else {
         // InterferenceHelper::CalculateSnrPer (interference-helper.cc:336-353), as k_wl_step: the walk's
         // sequential part here (64 ring entries a trip, then lane by lane), the chunks' models in k_wl_mid
-        const LTx t = D.tx[eb.tx];
+        const uint32_t bi = eb.tx - sb.k0;  // (a transmission of this launch's batch: D.tx is being written)
+        LTx t{};
+        if (bi < sb.n) {
+#pragma unroll
+          for (uint32_t u = 0; u < NSEND; u++)
+            if (bi == u) t = sb.t[u];
+        } else {
+          t = D.tx[eb.tx];
+        }
         const Mode pm = make_mode(t.mc, t.rate, t.bw);
         const double noise0 = P.firstPower;
         rec.snr = snr_of(D, eb.w, noise0, pm);
@@ -823,30 +1045,16 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
         rec.per = 0.0;  // (k_wl_mid writes the product)
         P.rxing = 0;  // NotifyRxEnd (); SwitchFromRxEndOk / Error -> DoSwitchFromRx (wifi-phy-state-helper.cc:391-402)
       }
-      const uint32_t sl = eb.euid == NONE ? eb.sslot : NONE;
-      uint32_t ei = 0, vi = 0;
+      if (ne == ENB || nv == EVB) flush();
+      const uint32_t sl = eb.euid == NONE ? rl_u32(mine.sslot, e) : NONE;  // (after a flush: its patched slot)
       if (lane == 0) {
-        ei = atomicAdd(&D.cnt[2], 1u);
-        vi = atomicAdd(evc, 1u);
+        s_end[ne] = LEnd{rec, eck, sl, 0};
+        s_ev[nv] = LEv{eb.ts, eb.euid, ctx, sl, 0};
       }
-      ei = rl_u32(ei, 0);
-      vi = rl_u32(vi, 0);
-      if (ei < D.end_cap) {
-        if (lane == 0) {
-          D.ends[ei] = rec;
-          D.end_sslot[ei] = sl;
-          D.eck[ei] = eck;
-        }
-      } else {
-        err |= WE_CAP;
-      }
-      if (vi < D.ev_scap) {
-        if (lane == 0) evs[vi] = LEv{eb.ts, eb.euid, ctx, sl, 0};
-      } else {
-        err |= WE_CAP;
-      }
-      if (lane == 0) pe[e].used = 0;
+      ne++;
+      nv++;
       if (lane == (uint32_t)e) mine.used = 0;
+      pe_dirty = true;
       if (P.live == (uint32_t)e) P.live = NONE;
       continue;
     }
@@ -856,10 +1064,11 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
     rqn++;
     const int64_t nw = (int64_t)r.at;
     const int64_t endNew = nw + r.dur;
-    if (P.len + 2 > m + 1) {
+    if (P.len + 2 > gm + 1) {
       err |= WE_NICAP;
       break;
     }
+    ring_dirty = true;
     // InterferenceHelper::AppendEvent (interference-helper.cc:192-212)
     if (!P.rxing) {  // fold the entries up to upper_bound (now) into m_firstPower; the new entry first
       w_cursor_advance<true>(ring, P.head, P.len, m, nw, P.cur_n, P.cur_s);
@@ -887,19 +1096,16 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
     } else if (r.w > D.edW) {  // sync (:461-472): SwitchToRx, NotifyRxStart, Schedule (rxDuration, EndReceive)
       const uint64_t fr = __ballot(lane < (uint32_t)LPE_CAP && !mine.used);  // (the first free record)
       const int q = fr ? __builtin_ctzll(fr) : -1;
-      uint32_t sl = 0;
-      if (lane == 0) sl = atomicAdd(&D.cnt[1], 1u);
-      sl = rl_u32(sl, 0);
-      if (q < 0 || sl >= D.sync_cap) {
-        err |= q < 0 ? WE_PECAP : WE_CAP;
+      if (q < 0) {
+        err |= WE_PECAP;
         break;
       }
-      const LPe np{(uint64_t)endNew, r.at, r.uid, NONE, r.tx, 0, sl, 1, r.w};
-      if (lane == 0) {
-        D.sync[sl] = LSync{r.at, r.uid, NONE};
-        pe[q] = np;
-      }
+      if (ns == SYB) flush();
+      if (lane == 0) s_sy[ns] = LSync{r.at, r.uid, NONE, (uint32_t)(j * LPE_CAP + q), 0};
+      const LPe np{(uint64_t)endNew, r.at, r.uid, NONE, r.tx, 0, LOCAL | ns, 1, r.w};
+      ns++;
       if (lane == (uint32_t)q) mine = np;
+      pe_dirty = true;
       P.live = (uint32_t)q;
       P.rxing = 1;
       P.endRx = endNew;
@@ -931,19 +1137,43 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
         P.c.cca_switches++;
       }
     }
-    uint32_t vi = 0;
-    if (lane == 0) vi = atomicAdd(evc, 1u);
-    vi = rl_u32(vi, 0);
-    if (vi < D.ev_scap) {
-      if (lane == 0) evs[vi] = LEv{r.at, r.uid, ctx, NONE, 0};
-    } else {
-      err |= WE_CAP;
+    if (nv == EVB) flush();
+    if (lane == 0) s_ev[nv] = LEv{r.at, r.uid, ctx, NONE, 0};
+    nv++;
+  }
+#ifdef NSGPU_PHASE_PROF
+  pt2 = __builtin_amdgcn_s_memtime();
+#endif
+  if (ns | ne | nv) flush();
+  // ---- write-backs: the pending records, the queue's rest (fast, after insertions), the ring (fast), the state
+  if (pe_dirty && lane < (uint32_t)LPE_CAP) pe[lane] = mine;
+  if (fast && nins && lane >= rqn && lane < qn) rq[(P.rq_head + (lane - rqn)) & D.rq_mask] = rqc;
+  if (fast && ring_dirty) {
+#pragma unroll
+    for (uint32_t u = 0; u < RL / 64; u++) {
+      const uint32_t i = u * 64 + lane;
+      if (i < P.len) gring[(P.head + i) & gm] = s_ring[(P.head + i) & (RL - 1)];
     }
   }
   if (lane == 0) {
-    D.ps[j] = P;
+    if (changed) D.ps[j] = P;
+    mir_put(D, j, m0, P);
     if (err) atomicOr(&D.cnt[3], err);
   }
+#ifdef NSGPU_PHASE_PROF
+  if (lane == 0) {
+    const uint64_t pt3 = __builtin_amdgcn_s_memtime(), dt = pt3 - pt0, c = pev < 4 ? pev : 4;
+    atomicAdd(&g_sw[c], 1ull);
+    atomicAdd(&g_sw[5 + c], dt);
+    if (dt > atomicMax(&g_sw[10], dt)) g_sw[11] = pev;
+    atomicMin(&g_sw[13], pt0);
+    atomicMax(&g_sw[14], pt3);
+    atomicMax(&g_sw2[0], pt0);
+    atomicAdd(&g_sw2[1], pt1 - pt0);
+    atomicAdd(&g_sw2[2], pt2 - pt1);
+    atomicAdd(&g_sw2[3], pt3 - pt2);
+  }
+#endif
 }
 
 #ifdef NSGPU_PHASE_PROF
@@ -952,32 +1182,44 @@ __global__ void k_wl_prof_epoch() {  // (one thread: fold the epoch's maxima, re
   g_wl_ph[4] += g_wl_ep[1];
   g_wl_ph[5] += 1;
   g_wl_ep[0] = g_wl_ep[1] = 0;
+  if (g_sw[14]) {
+    g_sw[12] += g_sw[14] - g_sw[13];
+    g_sw[15] += g_sw2[0] - g_sw[13];
+  }
+  g_sw[13] = ~0ull;
+  g_sw[14] = 0;
+  g_sw2[0] = 0;
 }
 #endif
 
 // CalculatePer's chunk product for the epoch's deferred EndReceives (interference-helper.cc:257-334): one
-// wave per end record, a lane per chunk (CalculateChunkSuccessRate with the error-rate model), the
-// product taken in walk order (every lane forms the same product from the wave's values).
-__device__ __forceinline__ void wl_per(const WDev &D, uint32_t bx, uint32_t nbx) {
+// block per end record, a thread per chunk (CalculateChunkSuccessRate with the error-rate model, every
+// chunk's model evaluated at once), then the product in walk order by one thread from LDS (its order is
+// the reference's: a float product is not reassociated).
+constexpr uint32_t PER_SEG = 4096;  // chunks a block holds in LDS at once (32 KB)
+__device__ __forceinline__ void wl_per(const WDev &D, uint32_t bx, uint32_t nbx, double *s_c) {
   const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t ei = bx * 4 + (threadIdx.x >> 6); ei < nend; ei += nbx * 4) {
-    const LEck k = D.eck[ei];  // (uniform over the wave)
+  for (uint32_t ei = bx; ei < nend; ei += nbx) {  // (block-uniform)
+    const LEck k = D.eck[ei];
     if (k.n == NONE) continue;
     const LTx t = D.tx[D.ends[ei].tx];
     const Mode pm = make_mode(t.mc, t.rate, t.bw), hm = header_mode(pm, t.preamble);
     double psr = 1.0;
-    for (uint32_t b = 0; b < k.n; b += 64) {
-      double c = 1.0;
-      if (b + lane < k.n) {
-        const LCk x = D.ck[k.start + b + lane];
+    for (uint32_t b = 0; b < k.n; b += PER_SEG) {
+      const uint32_t mm = k.n - b < PER_SEG ? k.n - b : PER_SEG;
+      for (uint32_t u = threadIdx.x; u < mm; u += 256) {
+        const LCk x = D.ck[k.start + b + u];
         const int64_t dur = x.dm >> 1;
-        c = (x.dm & 1) ? chunk(D, snr_of(D, k.w, x.noise, hm), dur, hm) : chunk(D, snr_of(D, k.w, x.noise, pm), dur, pm);
+        s_c[u] = (x.dm & 1) ? chunk(D, snr_of(D, k.w, x.noise, hm), dur, hm) : chunk(D, snr_of(D, k.w, x.noise, pm), dur, pm);
       }
-      const uint32_t mm = k.n - b < 64 ? k.n - b : 64;
-      for (uint32_t i = 0; i < mm; i++) psr *= __shfl(c, (int)i);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+#pragma unroll 16
+        for (uint32_t i = 0; i < mm; i++) psr *= s_c[i];
+      }
+      __syncthreads();
     }
-    if (lane == 0) D.ends[ei].per = 1 - psr;
+    if (threadIdx.x == 0) D.ends[ei].per = 1 - psr;
   }
 }
 
@@ -998,7 +1240,8 @@ __device__ __forceinline__ void wl_sync_rank(const WDev &D, uint32_t uid0, uint3
 // (the rest) — independent, one launch.
 constexpr uint32_t MID_PER = 128, MID_RANK = 64;
 __global__ __launch_bounds__(256) void k_wl_mid(const WDev D, uint32_t uid0) {
-  if (blockIdx.x < MID_PER) wl_per(D, blockIdx.x, MID_PER);
+  __shared__ double s_c[PER_SEG];
+  if (blockIdx.x < MID_PER) wl_per(D, blockIdx.x, MID_PER, s_c);
   else wl_sync_rank(D, uid0, blockIdx.x - MID_PER, MID_RANK);
 }
 
@@ -1006,16 +1249,26 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
-// The epoch's tail, second and third kernels (epochs of at most ERANK_MAX events; larger ones are ordered by
-// the host).  k_wl_resolve: the EndReceive uids into the end records and the still pending records, and the
-// epoch's events from their stripes into a dense key array (ts, resolved uid) and, for the host, a dense
-// event array.  k_wl_order: every event's rank in the epoch's (ts, uid) order — a block ranks ORW rows, the
-// keys stream through LDS in chunks of OCAP (one chunk for the usual epoch), its 16 waves counting a slice of
-// a chunk each — then its digest term and (logging) its rank.  The next epoch's counters (status block,
-// stripes) are zeroed here, so an epoch needs no fills.
-constexpr uint32_t OCAP = 8192, ORW = 64;  // keys per LDS chunk (128 KB); rows per block
-constexpr int OWV = 16;                    // waves of a k_wl_order block (column slices)
-constexpr uint32_t ERANK_MAX = 65536;
+// The epoch's tail after k_wl_mid, on the critical path: k_wl_fin (one block) — the EndReceive uids (the
+// sync order's) into the epoch's end records and its syncs' pending records, the status block (counters,
+// the first END_STAGE end records) straight into the host's mapped copy (no copy), the next epoch's counters
+// zeroed (no fills).
+// The epoch's order, behind it on a second stream (nothing the PHY or the host closures do depends on it;
+// only the digest and the log): a merge-rank sort over tiles of TS keys (ts, uid << 32 | dense index) —
+//   k_wl_tsort: a block per tile resolves its events' EndReceive uids from their stripes, writes the dense
+//     events (when the host reads them) and sorts the tile in LDS (bitonic);
+//   k_wl_rank: an event's rank = its place in its tile + its lower bound in every other tile (each tile
+//     read once into LDS, the searches in LDS), then its digest term and (logging) its rank; the block that
+//     finishes last writes the running digest sum into the host's mapped copy.
+// The event lists and syncs are kept per epoch parity, and an epoch's k_wl_fin waits for the order of the
+// epoch before it (whose lists, syncs and status block it is about to reuse): the order runs one epoch
+// behind.  Epochs above ERANK_MAX events are ordered by the host from the dense events.  (The r04 all-pairs
+// count, k_wl_order, was quadratic: 384 us at 6.5 x 10^4 events, and on the critical path.)
+constexpr uint32_t TS = 2048, TS_T = 1024;  // keys a tile; threads a block (two keys each)
+constexpr uint32_t ERANK_MAX = 65536, NTILE = ERANK_MAX / TS;
+__device__ __forceinline__ bool key_lt(const ulonglong2 &a, const ulonglong2 &b) {
+  return a.x < b.x || (a.x == b.x && a.y < b.y);
+}
 struct StripeMap {  // dense index -> stripe slot (the stripes' prefix in LDS)
   uint32_t pre[EV_STRIPES + 1];
 };
@@ -1040,85 +1293,142 @@ __device__ __forceinline__ uint64_t stripe_slot(const WDev &D, const StripeMap &
   }
   return (uint64_t)lo * D.ev_scap + (i - sm.pre[lo]);
 }
-__global__ __launch_bounds__(256) void k_wl_resolve(const WDev D, int keep, uint32_t *zcnt, unsigned long long *zdig,
-                                                    uint32_t *zevc) {
+__device__ __forceinline__ LEv resolved(const WDev &D, const StripeMap &sm, uint32_t k) {
+  LEv e = D.ev[stripe_slot(D, sm, k)];
+  if (e.sslot != NONE) e.uid = D.sync[e.sslot].euid;
+  return e;
+}
+__global__ __launch_bounds__(256) void k_wl_fin(const WDev D, uint32_t *zcnt, uint32_t *zevc, uint8_t *hst) {
   __shared__ StripeMap sm;
+  const uint32_t tid = threadIdx.x;
   const uint32_t nev = load_stripes(D, sm);
   const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
-  const uint64_t npe = (uint64_t)D.nphy * LPE_CAP;
-  if (blockIdx.x == 0) {  // the next epoch's counters (its status block, its stripes); this epoch's total
-    if (threadIdx.x < 3) zcnt[threadIdx.x] = 0;
-    if (threadIdx.x == 3) *zdig = 0;
-    if (threadIdx.x == 4) D.cnt[4] = 0;  // (the chunk pool: k_wl_stepw is done with it)
-    if (threadIdx.x == 5) D.cnt[0] = nev;
-    if (threadIdx.x < (uint32_t)EV_STRIPES) zevc[threadIdx.x * EV_STRIDE] = 0;
+  const uint32_t nsync = D.cnt[1] < D.sync_cap ? D.cnt[1] : (uint32_t)D.sync_cap;
+  for (uint32_t i = tid; i < nend; i += 256) {  // the end records' EndReceive uids
+    const uint32_t sl = D.end_sslot[i];
+    if (sl != NONE) D.ends[i].uid = D.sync[sl].euid;
   }
-  const uint64_t gs = (uint64_t)gridDim.x * 256;
-  const bool dense = keep || nev > ERANK_MAX;  // (the host reads the dense events)
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nend + npe + nev; i += gs) {
-    if (i < nend) {
-      const uint32_t sl = D.end_sslot[i];
-      if (sl != NONE) D.ends[i].uid = D.sync[sl].euid;
-    } else if (i < nend + npe) {
-      LPe &p = D.pe[i - nend];
-      if (p.used && p.euid == NONE) p.euid = D.sync[p.sslot].euid;
-    } else {
-      const uint32_t k = (uint32_t)(i - nend - npe);
-      LEv e = D.ev[stripe_slot(D, sm, k)];
-      if (e.sslot != NONE) e.uid = D.sync[e.sslot].euid;
-      D.evk[k] = make_ulonglong2(e.ts, e.uid);
-      if (dense) D.evd[k] = e;
-    }
+  for (uint32_t i = tid; i < nsync; i += 256) {  // (a record taken again this epoch: a later sync's)
+    const LSync y = D.sync[i];
+    LPe &p = D.pe[y.loc];
+    if (p.used && p.euid == NONE && p.sslot == i) p.euid = y.euid;
   }
+  __syncthreads();
+  nsgpu_wifil_end *he = reinterpret_cast<nsgpu_wifil_end *>(hst + STAT_HDR);
+  for (uint32_t i = tid; i < nend && i < END_STAGE; i += 256) he[i] = D.ends[i];
+  if (tid == 0) {
+    uint32_t *hc = reinterpret_cast<uint32_t *>(hst);
+    hc[0] = nev;
+    hc[1] = D.cnt[1];
+    hc[2] = D.cnt[2];
+    hc[3] = D.cnt[3];
+    D.cnt[0] = nev;
+    D.cnt[4] = 0;  // (the chunk pool: k_wl_stepw and k_wl_mid are done with it)
+  }
+  if (tid < 3) zcnt[tid] = 0;
+  if (tid < (uint32_t)EV_STRIPES) zevc[tid * EV_STRIDE] = 0;
 }
-__global__ __launch_bounds__(OWV * 64) void k_wl_order(const WDev D, uint64_t K0, int keep) {
-  const uint32_t nev = D.cnt[0];
-  if (nev > ERANK_MAX) return;  // (the host sorts a huge epoch)
-  __shared__ ulonglong2 s_k[OCAP];
-  __shared__ uint32_t s_part[OWV][ORW];
-  const uint32_t lane = threadIdx.x & 63, q = threadIdx.x >> 6;
-  uint64_t dg = 0;
-  for (uint32_t r0 = blockIdx.x * ORW; r0 < nev; r0 += gridDim.x * ORW) {  // (block-uniform)
-    const uint32_t i = r0 + lane;
-    const ulonglong2 x = i < nev ? D.evk[i] : make_ulonglong2(~0ull, ~0ull);
-    uint32_t c = 0;
-    for (uint32_t b0 = 0; b0 < nev; b0 += OCAP) {
-      const uint32_t bn = nev - b0 < OCAP ? nev - b0 : OCAP;
-      // the chunk's keys: every load issued before any is stored (a load-store loop waited a trip per entry)
-      constexpr uint32_t PT = OCAP / (OWV * 64);
-      ulonglong2 v[PT];
+__global__ __launch_bounds__(TS_T) void k_wl_tsort(const WDev D, int keep) {
+  __shared__ StripeMap sm;
+  __shared__ ulonglong2 s_t[TS];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nev = load_stripes(D, sm);
+  const bool big = nev > ERANK_MAX, dense = keep || big;
+  if (big) {  // (the host orders it: the dense events only)
+    for (uint32_t k = blockIdx.x * TS_T + tid; k < nev; k += gridDim.x * TS_T) D.evd[k] = resolved(D, sm, k);
+    return;
+  }
+  const uint32_t base = blockIdx.x * TS;
+  if (base >= nev) return;  // (block-uniform)
+  LEv e[2];
 #pragma unroll
-      for (uint32_t t = 0; t < PT; t++) {
-        const uint32_t j = threadIdx.x + t * OWV * 64;
-        v[t] = j < bn ? D.evk[b0 + j] : make_ulonglong2(0, 0);
-      }
-      __syncthreads();  // (the last chunk's counting is done)
+  for (uint32_t u = 0; u < 2; u++) {  // (both loads in flight)
+    const uint32_t k = base + u * TS_T + tid;
+    e[u] = k < nev ? D.ev[stripe_slot(D, sm, k)] : LEv{~0ull, NONE, 0, NONE, 0};
+  }
+  uint32_t eu[2];
 #pragma unroll
-      for (uint32_t t = 0; t < PT; t++) {
-        const uint32_t j = threadIdx.x + t * OWV * 64;
-        if (j < bn) s_k[j] = v[t];
+  for (uint32_t u = 0; u < 2; u++) eu[u] = e[u].sslot != NONE ? D.sync[e[u].sslot].euid : e[u].uid;
+#pragma unroll
+  for (uint32_t u = 0; u < 2; u++) {
+    const uint32_t k = base + u * TS_T + tid;
+    e[u].uid = eu[u];
+    if (k < nev && dense) D.evd[k] = e[u];
+    s_t[u * TS_T + tid] = k < nev ? make_ulonglong2(e[u].ts, (uint64_t)e[u].uid << 32 | k) : make_ulonglong2(~0ull, ~0ull);
+  }
+  __syncthreads();
+  for (uint32_t kk = 2; kk <= TS; kk <<= 1) {  // bitonic: TS_T compare-exchanges a stage
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+      const uint32_t i = 2 * j * (tid / j) + (tid % j), l = i + j;
+      const ulonglong2 a = s_t[i], b = s_t[l];
+      if (key_lt(b, a) == ((i & kk) == 0)) {
+        s_t[i] = b;
+        s_t[l] = a;
       }
       __syncthreads();
-      const uint32_t c0 = (uint32_t)((uint64_t)bn * q / OWV), c1 = (uint32_t)((uint64_t)bn * (q + 1) / OWV);
-#pragma unroll 8
-      for (uint32_t y = c0; y < c1; y++) {  // (every lane reads the same entry: an LDS broadcast)
-        const ulonglong2 k = s_k[y];
-        c += (k.x < x.x) | ((k.x == x.x) & (k.y < x.y));
-      }
-    }
-    s_part[q][lane] = c;
-    __syncthreads();
-    if (q == 0 && i < nev) {
-      uint32_t r = 0;
-#pragma unroll
-      for (int k = 0; k < OWV; k++) r += s_part[k][lane];
-      dg += digest_term(K0 + r, x.x, (uint32_t)x.y);
-      if (keep) D.erank[i] = r;
     }
   }
-  if (q == 0) {
-    dg = wave_sum_u64(dg);
-    if (lane == 0 && dg) atomicAdd(D.edig, (unsigned long long)dg);
+  const uint32_t n = nev - base < TS ? nev - base : TS;
+  for (uint32_t i = tid; i < n; i += TS_T) D.evg[base + i] = s_t[i];
+}
+__global__ __launch_bounds__(TS_T) void k_wl_rank(const WDev D, uint64_t K0, int keep, unsigned long long *hdig) {
+  __shared__ ulonglong2 s_o[TS];
+  __shared__ unsigned long long s_dg[TS_T / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t nev = D.cnt[0];
+  const uint32_t nt = (nev + TS - 1) / TS;
+  uint64_t dg = 0;
+  if (nev <= ERANK_MAX && blockIdx.x < nt) {  // (block-uniform)
+    const uint32_t t = blockIdx.x, n = nev - t * TS < TS ? nev - t * TS : TS;
+    ulonglong2 x[2];
+    uint32_t r[2];
+#pragma unroll
+    for (uint32_t u = 0; u < 2; u++) {
+      const uint32_t p = u * TS_T + tid;
+      x[u] = p < n ? D.evg[t * TS + p] : make_ulonglong2(~0ull, ~0ull);
+      r[u] = p;  // (its place in its own tile)
+    }
+    for (uint32_t t2 = 0; t2 < nt; t2++) {
+      if (t2 == t) continue;
+      const uint32_t n2 = nev - t2 * TS < TS ? nev - t2 * TS : TS;
+#pragma unroll
+      for (uint32_t u = 0; u < 2; u++) {
+        const uint32_t p = u * TS_T + tid;
+        if (p < n2) s_o[p] = D.evg[t2 * TS + p];
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t u = 0; u < 2; u++) {  // lower bound: the tile's keys below x
+        uint32_t lo = 0, c = n2;
+        while (c > 0) {
+          const uint32_t h = c >> 1;
+          if (key_lt(s_o[lo + h], x[u])) lo += h + 1, c -= h + 1;
+          else c = h;
+        }
+        r[u] += lo;
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 2; u++) {
+      if (u * TS_T + tid >= n) break;
+      dg += digest_term(K0 + r[u], x[u].x, (uint32_t)(x[u].y >> 32));
+      if (keep) D.erank[(uint32_t)x[u].y] = r[u];
+    }
+  }
+  dg = wave_sum_u64(dg);
+  if (lane == 0) s_dg[wv] = dg;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (uint32_t w = 0; w < TS_T / 64; w++) t += s_dg[w];
+    if (t) atomicAdd(D.edig, t);
+    __threadfence();
+    if (atomicAdd(D.ticket, 1u) == gridDim.x - 1) {  // the last block: the running sum for the host
+      __threadfence();
+      *hdig = atomicAdd(D.edig, 0ull);
+      atomicExch(D.ticket, 0u);
+    }
   }
 }
 
@@ -1143,12 +1453,10 @@ __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t
     P.endTx = (int64_t)t.ts + t.dur;
     return;
   }
-  if (D.chan[j] != D.chan[s]) return;  // YansWifiChannel::Send: other channels get nothing (:88-91)
-  const double dist = distance3(D.x[s], D.y[s], D.z[s], D.x[j], D.y[j], D.z[j]);
-  const uint64_t at = t.ts + (uint64_t)seconds_to_ts(dist / D.speed);  // ConstantSpeed delay (propagation-delay-model.cc:90-96)
-  const double dBm = calc_rx_power(D.loss, dbm, dist) + D.rx_gain_db;      // StartReceivePacket: rxPowerDbm += RxGain
-  const double w = pow(10.0, dBm / 10.0) / 1000.0;                         // DbmToW (yans-wifi-phy.cc:727-732)
-  const uint32_t uid = base + D.chan_rank[j] - (j > (int64_t)s ? 1u : 0u);  // the receiver loop's Schedule order
+  LRx e;
+  if (!reception(D, j, t, k, dbm, base, e)) return;
+  const uint64_t at = e.at;
+  const uint32_t uid = e.uid;
   LPhy &P = D.ps[j];
   LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
   if (P.rq_len > D.rq_mask) {
@@ -1162,7 +1470,7 @@ __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t
     rq[(P.rq_head + q) & D.rq_mask] = e;
     q--;
   }
-  rq[(P.rq_head + q) & D.rq_mask] = LRx{at, uid, k, w, t.dur};
+  rq[(P.rq_head + q) & D.rq_mask] = e;
   P.rq_len++;
 }
 
@@ -1213,16 +1521,23 @@ struct nsgpu_wifil {
   std::vector<void *> allocs;
   std::vector<uint32_t> recv;  // fan-out uids of one SendPacket per phy
   uint64_t n_tx = 0, tx_cap = 0;
-  // pinned: the epoch's status block as one copy — counters, digest sum, first END_STAGE end records (the
-  // device's D.cnt / D.edig / D.ends are laid out the same way in one allocation)
-  uint8_t *h_stat = nullptr;
+  SendBatch sb{};  // SendPackets not yet applied (the next epoch launch applies them; k_wl_send past NSEND)
+  // mapped host memory: the epoch's status block — counters, digest sum, first END_STAGE end records (the
+  // device's D.cnt / D.edig / D.ends are laid out the same way in one allocation) — k_wl_rank writes it
+  uint8_t *h_stat = nullptr, *d_stat = nullptr;  // (mapped: k_wl_rank writes it; d_stat is its device address)
   uint8_t *stat[2] = {nullptr, nullptr};  // the device's status blocks, by epoch parity (the next one is zeroed
-  uint32_t par = 0;                       //   by the running epoch's k_wl_resolve: no fills between epochs)
+  uint32_t par = 0;                       //   by the running epoch's k_wl_tsort: no fills between epochs)
   uint32_t *evc[2] = {nullptr, nullptr};  // the event-list stripe counters, by epoch parity (likewise)
   uint32_t *h_cnt = nullptr;
-  unsigned long long *h_dig = nullptr;
+  LEv *evb[2] = {nullptr, nullptr};      // the event lists, by epoch parity (the order reads them an epoch behind)
+  LSync *syncb[2] = {nullptr, nullptr};  // the syncs, by epoch parity (likewise)
+  hipStream_t s2 = nullptr;              // the epochs' order (k_wl_tsort / k_wl_rank)
+  hipEvent_t ev_fin[2] = {nullptr, nullptr}, ev_ord[2] = {nullptr, nullptr};
+  bool ord_pending[2] = {false, false};  // an order of this parity's epoch was launched and not yet waited for
+  unsigned long long *h_digtot = nullptr, *d_digtot = nullptr;  // (mapped) the ordered epochs' digest sum
+  uint64_t dig_added = 0;                // the part of it already added to a caller's digest
   nsgpu_wifil_end *h_ends = nullptr;
-  LPhy *h_ps = nullptr;                  // pinned: one phy's state (nsgpu_wifil_get_state)
+  WMir *h_mir = nullptr;                 // mapped host memory: every phy's state fields (D.mir; GetState)
   std::vector<uint32_t> erank;
   unsigned long long *d_pend = nullptr, *h_pend = nullptr;
   std::vector<LEv> ev;
@@ -1233,7 +1548,8 @@ struct nsgpu_wifil {
 static void wl_use_stat(nsgpu_wifil *h, uint32_t b) {
   h->par = b;
   h->D.cnt = reinterpret_cast<uint32_t *>(h->stat[b]);
-  h->D.edig = reinterpret_cast<unsigned long long *>(h->stat[b] + 24);
+  h->D.ev = h->evb[b];
+  h->D.sync = h->syncb[b];
   h->D.ends = reinterpret_cast<nsgpu_wifil_end *>(h->stat[b] + STAT_HDR);
   h->D.evc = h->evc[b];
 }
@@ -1251,13 +1567,19 @@ static int wl_alloc(nsgpu_wifil *h, T **p, size_t n, const T *src = nullptr) {
 
 extern "C" int nsgpu_wifil_destroy(nsgpu_wifil *h) {
   if (!h) return NSGPU_OK;
-  if (h->s) {
-    (void)hipStreamSynchronize(h->s);
-    (void)hipStreamDestroy(h->s);
+  for (hipStream_t q : {h->s, h->s2})
+    if (q) {
+      (void)hipStreamSynchronize(q);
+      (void)hipStreamDestroy(q);
+    }
+  for (int b = 0; b < 2; b++) {
+    if (h->ev_fin[b]) (void)hipEventDestroy(h->ev_fin[b]);
+    if (h->ev_ord[b]) (void)hipEventDestroy(h->ev_ord[b]);
   }
+  if (h->h_digtot) (void)hipHostFree(h->h_digtot);
   for (void *p : h->allocs) (void)hipFree(p);
   if (h->h_stat) (void)hipHostFree(h->h_stat);
-  if (h->h_ps) (void)hipHostFree(h->h_ps);
+  if (h->h_mir) (void)hipHostFree(h->h_mir);
   if (h->h_pend) (void)hipHostFree(h->h_pend);
   delete h;
   return NSGPU_OK;
@@ -1320,14 +1642,14 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   WL_TRY(wl_alloc(h, &D.rq, (size_t)N * c->rxq_cap));
   WL_TRY(wl_alloc(h, &D.pe, (size_t)N * LPE_CAP));
   WL_TRY(wl_alloc(h, &D.tx, c->tx_cap));
-  WL_TRY(wl_alloc(h, &D.sync, sync_cap));
-  WL_TRY(wl_alloc(h, &D.ev, ev_cap));
+  WL_TRY(wl_alloc(h, &D.edig, 1));
   for (int b = 0; b < 2; b++) {  // [cnt x 5 | pad | edig | ends x sync_cap], two of them (epoch parity)
     WL_TRY(wl_alloc(h, &h->stat[b], STAT_HDR + sync_cap * sizeof(nsgpu_wifil_end)));
     WL_TRY(wl_alloc(h, &h->evc[b], (size_t)EV_STRIPES * EV_STRIDE));
+    WL_TRY(wl_alloc(h, &h->evb[b], ev_cap));
+    WL_TRY(wl_alloc(h, &h->syncb[b], sync_cap));
   }
   WL_TRY(wl_alloc(h, &D.evd, ev_cap));
-  WL_TRY(wl_alloc(h, &D.evk, ev_cap));
   D.ev_scap = ev_cap / EV_STRIPES;
   wl_use_stat(h, 0);
   WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
@@ -1338,22 +1660,35 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   D.ck_cap = std::max<uint64_t>(1ull << 22, (uint64_t)N * 512);
   WL_TRY(wl_alloc(h, &D.ck, (size_t)D.ck_cap));
   WL_TRY(wl_alloc(h, &D.erank, std::min<uint64_t>(ev_cap, ERANK_MAX)));
+  WL_TRY(wl_alloc(h, &D.ticket, 1));
+  WL_TRY(wl_alloc(h, &D.evg, std::min<uint64_t>(ev_cap, ERANK_MAX)));
   WL_TRY(wl_alloc(h, &h->d_pend, 2));
 #undef WL_TRY
   D.sync_cap = sync_cap;
   D.ev_cap = ev_cap;
   D.end_cap = sync_cap;
   h->tx_cap = c->tx_cap;
-  if (hipHostMalloc((void **)&h->h_stat, STAT_HDR + END_STAGE * sizeof(nsgpu_wifil_end), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void **)&h->h_ps, sizeof(LPhy), hipHostMallocDefault) != hipSuccess ||
+  if (hipHostMalloc((void **)&h->h_stat, STAT_HDR + END_STAGE * sizeof(nsgpu_wifil_end),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&h->d_stat, h->h_stat, 0) != hipSuccess ||
+      hipHostMalloc((void **)&h->h_mir, (size_t)N * sizeof(WMir), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&D.mir, h->h_mir, 0) != hipSuccess ||
       hipHostMalloc((void **)&h->h_pend, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
+      hipHostMalloc((void **)&h->h_digtot, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&h->d_digtot, h->h_digtot, 0) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->s2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_fin[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_fin[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_ord[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_ord[1], hipEventDisableTiming) != hipSuccess) {
     nsgpu_wifil_destroy(h);
     return set_error(NSGPU_EHIP, "nsgpu_wifil_create: host buffers / stream");
   }
   h->h_cnt = reinterpret_cast<uint32_t *>(h->h_stat);
-  h->h_dig = reinterpret_cast<unsigned long long *>(h->h_stat + 24);
   h->h_ends = reinterpret_cast<nsgpu_wifil_end *>(h->h_stat + STAT_HDR);
+  *h->h_digtot = 0;
+  std::memset(h->h_mir, 0, (size_t)N * sizeof(WMir));  // (the phys' initial state: every end time 0, not receiving)
   *out = h;
   return NSGPU_OK;
 }
@@ -1373,6 +1708,16 @@ static int wl_check(nsgpu_wifil *h, const char *what) {
                                  "EndReceive records, 16 epoch lists, 32 CalculatePer chunk pool)", what, e);
 }
 
+// The batched SendPackets as k_wl_send launches (before anything that reads the phys or moves one).
+static int wl_flush_sends(nsgpu_wifil *h) {
+  const unsigned g = (unsigned)((h->D.nphy + 255) / 256);
+  for (uint32_t i = 0; i < h->sb.n; i++)
+    hipLaunchKernelGGL(k_wl_send, dim3(g), dim3(256), 0, h->s, h->D, h->sb.k0 + i, h->sb.t[i], h->sb.dbm[i], h->sb.base[i]);
+  h->sb.n = 0;
+  NSGPU_HIP(hipGetLastError());
+  return NSGPU_OK;
+}
+
 // YansWifiPhy::SendPacket of `phy` from the host closure running at (now, closure uid); its fan-out takes
 // the uids uid_base .. uid_base + receivers - 1 (nsgpu_wifil_receivers).
 extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base, uint32_t phy, uint32_t size, double dbm,
@@ -1387,10 +1732,22 @@ extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base,
   int rc = nsgpu_wifi_tx_duration_ns(size, modclass, rate, bw, preamble, &dur);  // CalculateTxDuration
   if (rc) return rc;
   LTx t{now, dur, rate, phy, modclass, bw, preamble};
+  if (h->sb.n == NSEND) {
+    int rcf = wl_flush_sends(h);
+    if (rcf) return rcf;
+  }
   const uint32_t k = (uint32_t)h->n_tx++;
-  hipLaunchKernelGGL(k_wl_send, dim3((unsigned)((h->D.nphy + 255) / 256)), dim3(256), 0, h->s, h->D, k, t, dbm, uid_base);
-  NSGPU_HIP(hipGetLastError());
-  return NSGPU_OK;  // (asynchronous: its error bits, if any, fail the next nsgpu_wifil_advance)
+  WMir &mr = h->h_mir[phy];  // the sender's switch (k_wl_send's), in the host's copy of its state fields
+  if (!(mr.endTx > (int64_t)now)) {
+    if (mr.rxing) mr.rxing = 0, mr.endRx = (int64_t)now;
+    mr.endTx = (int64_t)now + dur;
+  }
+  if (h->sb.n == 0) h->sb.k0 = k;
+  h->sb.t[h->sb.n] = t;
+  h->sb.dbm[h->sb.n] = dbm;
+  h->sb.base[h->sb.n] = uid_base;
+  h->sb.n++;
+  return NSGPU_OK;  // (applied by the next epoch launch: its error bits, if any, fail that nsgpu_wifil_advance)
 }
 
 // Every device event with a key below (bound_ts, bound_uid) (~0: all of them): dispatched in (ts, uid) order
@@ -1408,23 +1765,35 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
     const char *e = getenv("NSGPU_WIFIL_LANE");
     return e && e[0] == '1';
   }();
-  if (lane_step)
+  if (lane_step) {
+    int rcf = wl_flush_sends(h);
+    if (rcf) return rcf;
     hipLaunchKernelGGL(k_wl_step, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
-  else
-    hipLaunchKernelGGL(k_wl_stepw, dim3((unsigned)D.nphy), dim3(64), 0, h->s, D, bound_ts, bound_uid);
+  } else {
+    hipLaunchKernelGGL(k_wl_stepw, dim3((unsigned)D.nphy), dim3(64), 0, h->s, D, bound_ts, bound_uid, h->sb);
+    h->sb.n = 0;
+  }
 #ifdef NSGPU_PHASE_PROF
   hipLaunchKernelGGL(k_wl_prof_epoch, dim3(1), dim3(1), 0, h->s);
 #endif
   hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, h->s, D, *uid);
   const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
-  hipLaunchKernelGGL(k_wl_resolve, dim3(512), dim3(256), 0, h->s, D, logging ? 1 : 0, reinterpret_cast<uint32_t *>(nxt),
-                     reinterpret_cast<unsigned long long *>(nxt + 24), nxt_evc);
-  hipLaunchKernelGGL(k_wl_order, dim3(256), dim3(OWV * 64), 0, h->s, D, *dispatched, logging ? 1 : 0);
+  const uint32_t b = h->par;
+  if (h->ord_pending[b ^ 1]) {  // (k_wl_fin reuses the last epoch's status block, lists and syncs)
+    NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev_ord[b ^ 1], 0));
+    h->ord_pending[b ^ 1] = false;
+  }
+  hipLaunchKernelGGL(k_wl_fin, dim3(1), dim3(256), 0, h->s, D, reinterpret_cast<uint32_t *>(nxt), nxt_evc, h->d_stat);
   NSGPU_HIP(hipGetLastError());
-  // counters, the digest sum and the first end records in one trip
-  NSGPU_HIP(hipMemcpyAsync(h->h_stat, D.cnt, STAT_HDR + END_STAGE * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipEventRecord(h->ev_fin[b], h->s));
+  NSGPU_HIP(hipStreamWaitEvent(h->s2, h->ev_fin[b], 0));
+  hipLaunchKernelGGL(k_wl_tsort, dim3(NTILE), dim3(TS_T), 0, h->s2, D, logging ? 1 : 0);
+  hipLaunchKernelGGL(k_wl_rank, dim3(NTILE), dim3(TS_T), 0, h->s2, D, *dispatched, logging ? 1 : 0, h->d_digtot);
+  NSGPU_HIP(hipGetLastError());
+  NSGPU_HIP(hipEventRecord(h->ev_ord[b], h->s2));
+  h->ord_pending[b] = true;
   NSGPU_HIP(hipStreamSynchronize(h->s));
-  wl_use_stat(h, h->par ^ 1);  // (the next epoch's block; SendPackets until then report their errors there)
+  wl_use_stat(h, b ^ 1);  // (the next epoch's block; SendPackets until then report their errors there)
   int rc = wl_check(h, "nsgpu_wifil_advance");
   if (rc) return rc;
   const uint32_t nev = h->h_cnt[0], nsync = h->h_cnt[1], nend = h->h_cnt[2];
@@ -1434,6 +1803,7 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   } else if (nend) {
     std::copy(h->h_ends, h->h_ends + nend, h->ends_epoch.begin());
   }
+  if (nev > ERANK_MAX || (logging && nev)) NSGPU_HIP(hipStreamSynchronize(h->s2));  // (the dense events / ranks)
   if (nev > ERANK_MAX) {  // a large epoch: its order on the host
     h->ev.resize(nev);
     NSGPU_HIP(hipMemcpyAsync(h->ev.data(), D.evd, nev * sizeof(LEv), hipMemcpyDeviceToHost, h->s));
@@ -1463,14 +1833,12 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
           log_ctx[rank] = h->ev[i].ctx;
         }
       }
-    } else if (logging) {
-      // (nothing dispatched)
-    } else if (nend > END_STAGE) {
-      NSGPU_HIP(hipStreamSynchronize(h->s));
     }
-    *digest += *h->h_dig;
     *dispatched += nev;
   }
+  const uint64_t tot = *h->h_digtot;  // (the ordered epochs' terms so far: one aligned 8-byte store's value)
+  *digest += tot - h->dig_added;
+  h->dig_added = tot;
   if (nend > END_STAGE) NSGPU_HIP(hipStreamSynchronize(h->s));
   std::sort(h->ends_epoch.begin(), h->ends_epoch.end(),
             [](const nsgpu_wifil_end &a, const nsgpu_wifil_end &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
@@ -1481,12 +1849,24 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   return NSGPU_OK;
 }
 
+// Waits for the epochs' order behind the PHY (k_wl_tsort / k_wl_rank on the second stream) and adds the
+// digest terms it summed since the last advance / flush.
+extern "C" int nsgpu_wifil_flush(nsgpu_wifil *h, uint64_t *digest) {
+  if (!h || !digest) return set_error(NSGPU_EINVAL, "nsgpu_wifil_flush: null");
+  NSGPU_HIP(hipStreamSynchronize(h->s2));
+  const uint64_t tot = *h->h_digtot;
+  *digest += tot - h->dig_added;
+  h->dig_added = tot;
+  return NSGPU_OK;
+}
+
 // MobilityModel::SetPosition of `phy`'s node (mobility-model.cc SetPosition -> DoSetPosition; e.g. a host closure
 // at run time): YansWifiChannel::Send reads the positions at each send (yans-wifi-channel.cc:92-96), so the
 // later sends' fan-outs see it; receptions already scheduled keep their delay and power.  In stream order with
 // the sends.
 extern "C" int nsgpu_wifil_set_position(nsgpu_wifil *h, uint32_t phy, double x, double y, double z) {
   if (!h || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_set_position: bad phy");
+  if (int rcf = wl_flush_sends(h)) return rcf;  // (the sends so far see the positions they were made with)
   const double v[3] = {x, y, z};
   double *dst[3] = {const_cast<double *>(h->D.x), const_cast<double *>(h->D.y), const_cast<double *>(h->D.z)};
   for (int c = 0; c < 3; c++)
@@ -1498,9 +1878,9 @@ extern "C" int nsgpu_wifil_set_position(nsgpu_wifil *h, uint32_t phy, double x, 
 // WifiPhyStateHelper::GetState / GetDelayUntilIdle of `phy` at `now` (wifi-phy-state-helper.cc:122-183).
 extern "C" int nsgpu_wifil_get_state(nsgpu_wifil *h, uint32_t phy, uint64_t now, nsgpu_wifil_phy_state *out) {
   if (!h || !out || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_get_state: bad phy");
-  NSGPU_HIP(hipMemcpyAsync(h->h_ps, h->D.ps + phy, sizeof(LPhy), hipMemcpyDeviceToHost, h->s));  // (pinned)
-  NSGPU_HIP(hipStreamSynchronize(h->s));
-  const LPhy P = *h->h_ps;
+  // the state fields as the last epoch's kernels (their lanes write a changed phy's) and the host's SendPackets
+  // left them: every event before `now` has run (the runtime advanced the device to the running closure)
+  const WMir P = h->h_mir[phy];
   const int64_t nw = (int64_t)now;
   out->state = P.endTx > nw ? NSGPU_WIFIL_TX : P.rxing ? NSGPU_WIFIL_RX : P.endCca > nw ? NSGPU_WIFIL_CCA_BUSY : NSGPU_WIFIL_IDLE;
   out->rxing = P.rxing;
@@ -1529,6 +1909,7 @@ extern "C" int nsgpu_wifil_read_ends(nsgpu_wifil *h, nsgpu_wifil_end *out, uint6
 
 extern "C" int nsgpu_wifil_read_phys(nsgpu_wifil *h, nsgpu_wifi_phy_counters *out) {
   if (!h || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifil_read_phys: null");
+  if (int rcf = wl_flush_sends(h)) return rcf;
   std::vector<LPhy> ps((size_t)h->D.nphy);
   NSGPU_HIP(hipMemcpyAsync(ps.data(), h->D.ps, ps.size() * sizeof(LPhy), hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipStreamSynchronize(h->s));
@@ -1549,6 +1930,7 @@ extern "C" int nsgpu_wifil_read_phys(nsgpu_wifil *h, nsgpu_wifi_phy_counters *ou
 // Pending Receive / EndReceive events and the smallest ts among them (~0: none).
 extern "C" int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_ts) {
   if (!h || !n || !next_ts) return set_error(NSGPU_EINVAL, "nsgpu_wifil_pending: null");
+  if (int rcf = wl_flush_sends(h)) return rcf;
   const unsigned long long init[2] = {0ull, ~0ull};
   NSGPU_HIP(hipMemcpyAsync(h->d_pend, init, sizeof(init), hipMemcpyHostToDevice, h->s));
   hipLaunchKernelGGL(k_wl_pending, dim3((unsigned)((h->D.nphy + 255) / 256)), dim3(256), 0, h->s, h->D, h->d_pend);
@@ -1561,12 +1943,19 @@ extern "C" int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_t
 }
 
 #ifdef NSGPU_PHASE_PROF
-// (diagnostic build only) the k_wl_step counters above, reset after the read
+// (diagnostic build only) the k_wl_step counters above (out[0..8)), k_wl_stepw's (out[8..24) g_sw, out[24..28)
+// g_sw2), reset after the read
 extern "C" int nsgpu_wifil_prof_read(unsigned long long *out) {
   NSGPU_HIP(hipDeviceSynchronize());
   NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wl_ph), sizeof(unsigned long long) * 8));
-  unsigned long long z[8] = {};
-  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wl_ph), z, sizeof(z)));
+  NSGPU_HIP(hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_sw), sizeof(unsigned long long) * 16));
+  NSGPU_HIP(hipMemcpyFromSymbol(out + 24, HIP_SYMBOL(g_sw2), sizeof(unsigned long long) * 4));
+  unsigned long long z[16] = {};
+  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wl_ph), z, sizeof(unsigned long long) * 8));
+  z[13] = ~0ull;  // (the running epoch's first start: a minimum)
+  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sw), z, sizeof(z)));
+  z[13] = 0;
+  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sw2), z, sizeof(unsigned long long) * 4));
   return NSGPU_OK;
 }
 #endif

@@ -130,6 +130,7 @@ SIGNATURES = {
     "nsgpu_wifil_receivers": (C.c_int, [_vp, _u32, _vp]),
     "nsgpu_wifil_send": (C.c_int, [_vp, _u64, _u32, _u32, _u32, C.c_double, _u32, _u64, _u32, _u32]),
     "nsgpu_wifil_advance": (C.c_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u64]),
+    "nsgpu_wifil_flush": (C.c_int, [_vp, _vp]),
     "nsgpu_wifil_get_state": (C.c_int, [_vp, _u32, _u64, _vp]),
     "nsgpu_wifil_read_ends": (C.c_int, [_vp, _vp, _u64, _vp]),
     "nsgpu_wifil_read_phys": (C.c_int, [_vp, _vp]),

@@ -65,8 +65,7 @@ def test_yans_error_model_and_short_preamble():
 def test_grid_100x100_short_stop_full_pop_log():
     """The bench's closed-loop workload (10,000 phys 100 m apart, 1000-B DSSS 1 Mb/s frames, period 1 s from
     seeded phases) cut at Stop 0.02 s (317 SendPackets, 3.17 M dispatches): every SendPacket fans out to
-    9,999 receivers, so epochs hold more events than one LDS chunk of k_wl_order (OCAP) and k_wl_order
-    streams several; the full pop log, digest, counters and end records equal the oracle's."""
+    9,999 receivers, so epochs hold ~10^4 events (k_wl_tail's sample sort, keys in LDS); the full pop log, digest, counters and end records equal the oracle's."""
     import numpy as np
     x, y, z = wifi.grid(100, 100.0)
     phys = wifi.LoopPhys(x, y, z, tx_cap=1 << 20, rxq_cap=1024, ni_cap=1024)
@@ -77,3 +76,42 @@ def test_grid_100x100_short_stop_full_pop_log():
               size=1000, mode=wifi.DSSS_1M, preamble=wifi.PREAMBLE_LONG, dbm=16.0206 + 1.0)
     tot, ends = check(sc, log_cap=1 << 22)
     assert tot["sends"] > 200 and tot["dispatched"] > 2_000_000 and len(ends) > 1000
+
+
+def test_epoch_order_paths_lds_hbm_host():
+    """One SendPacket at 1 us, two at 1 ms, seven at 2 ms on the 100x100 grid (host closures scheduled in
+    send order): the epochs that end at the next sends hold ~10^4 events (k_wl_tail's keys in LDS), ~2x10^4
+    (more than LDS_EV: keys in HBM) and, in the last epoch, ~7x10^4 receptions plus every EndReceive (more
+    than ERANK_MAX: the host orders it).  Pop log, digest, end records and counters = the oracle's replay."""
+    import nsgpu
+    import nsref
+    x, y, z = wifi.grid(100, 100.0)
+    ph = wifi.LoopPhys(x, y, z, tx_cap=64, rxq_cap=1024, ni_cap=1024)
+    n = ph.n_phy
+    sends = [(1_000, 5050), (1_000_000, 0), (1_000_000, 9999)] + [(2_000_000, p) for p in range(101, 808, 101)]
+    ts = np.array([t for t, _p in sends], np.uint64)
+    phy = np.array([p for _t, p in sends], np.uint32)
+    size = np.full(len(sends), 1000, np.uint32)
+    dbm, stop, cap = 16.0206 + 1.0, 30_000_000, 1 << 18
+    olog, oends, ophys, otot = nsref.wifil_replay(ph.c_struct(), ts, phy, size, wifi.DSSS_1M, wifi.PREAMBLE_LONG, dbm,
+                                                  stop, n, wifi.WIFIL_END_DTYPE, wifi.PHY_COUNTERS_DTYPE, log_cap=cap)
+    assert otot["dispatched"] > 100_000
+    sim = nsgpu.Sim()
+    lp = wifi.LoopPhy(ph)
+    sim.attach_wifi(lp)
+    sim.set_log(cap)
+    for t, p in sends:
+        sim.schedule(t, (lambda p=p: lambda: sim.wifi_send(p, 1000, dbm, wifi.DSSS_1M, wifi.PREAMBLE_LONG))())
+    sim.stop(stop)
+    sim.run()
+    assert sim.dispatched() == otot["dispatched"] and sim.next_uid() == otot["next_uid"]
+    k = min(sim.dispatched(), cap)
+    for a, b in zip((sim.log[0][:k], sim.log[1][:k], sim.log[2][:k]), olog):
+        assert np.array_equal(a, b)
+    gends, gphys = lp.read_ends(), lp.read_phys()
+    for f in ("ts", "uid", "phy", "tx", "flags"):
+        assert np.array_equal(gends[f], oends[f]), f
+    np.testing.assert_allclose(gends["per"], oends["per"], rtol=1e-9, atol=1e-15)
+    for f in PHY_FIELDS[:8]:  # (the replay's oracle returns the counters only: nsref_wifil_replay)
+        assert np.array_equal(gphys[f], ophys[f]), f
+    lp.close()
