@@ -24,6 +24,8 @@
 // RingNi layout of nsgpu_wifi.hip, with its eager prefix cursor), the state helper's end times, the pending
 // Receive queue (sorted by (arrival, uid)) and up to LPE_CAP pending EndReceive records.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 #include "nsgpu_device.h"
@@ -109,15 +111,23 @@ struct WDev {
   nsgpu_wifil_end *ends;
   uint32_t *end_sslot;
   uint32_t *cnt;  // [0] events, [1] syncs, [2] ends, [3] error bits (sticky: a SendPacket's are seen at the
-                  // next advance), [4] chunk slots claimed (zeroed by k_wl_tsort)
+                  // next advance), [4] chunk slots claimed ([0..2], [4] zeroed by the order's
+                  // k_wl_rank, for the epoch two on)
   LCk *ck;        // the epoch's deferred chunks (ck_cap; a walk that finds no room computes its PER inline)
   LEck *eck;      // per end record
   uint32_t *evc;             // the epoch's event-list stripes: EV_STRIPES counters, EV_STRIDE words apart
-  LEv *evd;                  // the epoch's events in dense order, uids resolved (the host's copy)
+  LEv *evd;                  // the epoch's events in dense order, uids resolved (k_wl_gather; the host's copy)
+  LEv *evp;                  // a phy's events of the epoch in its own EVB slots (k_wl_stepw, no claim); by parity
+  uint32_t *evn;             // their counts (zeroed by k_wl_gather once read); by parity
+  uint32_t *evt;             // their total, EV_STRIPES counters EV_STRIDE words apart (one would serialize 10^4
+                             //   adds on one line); by parity, zeroed by k_wl_rank for the epoch two on
+  uint32_t *gtot;            // k_wl_gather's claims (reset by k_wl_tsort)
   uint32_t *erank;           // the epoch's events: rank in its (ts, uid) order (k_wl_rank, when logging)
   ulonglong2 *evg;           // the epoch's keys (ts, uid << 32 | dense index), sorted by tiles (k_wl_tsort)
-  uint32_t *ticket;          // k_wl_rank's blocks done (its last block writes the status block; reset there)
+  uint32_t *ticket;          // k_wl_rank's blocks done (its last block: the digest sum, the counters' zeroing)
+  uint32_t *mticket;         // k_wl_mid's blocks done (its last block closes the epoch: wl_fin)
   WMir *mir;                 // (mapped host memory) each phy's state fields: a lane whose phy changed writes them
+  LRx *rxb;                  // the batched SendPackets' Receives, NSEND x nphy (k_wl_rx; at = ~0: none for that phy)
   unsigned long long *edig;  // every ordered epoch's digest terms, summed on the device (k_wl_rank)
   uint64_t sync_cap, ev_cap, end_cap, ck_cap;
   uint64_t ev_scap;  // events per stripe (stripe s holds ev[s * ev_scap, s * ev_scap + evc[s * EV_STRIDE]))
@@ -414,12 +424,12 @@ __device__ __forceinline__ void mir_put(const WDev &D, int64_t j, const WMir &m0
 // [4] sum over epochs of the most events one lane ran, [5] epochs, [6] max lane time, [7] its events
 __device__ unsigned long long g_wl_ph[8];
 __device__ unsigned long long g_wl_ep[2];  // the current epoch's slowest lane time / most events (reset by host)
-// k_wl_stepw's waves: [0..4] waves with 0, 1, 2, 3, 4+ events, [5..9] their summed lifetimes (s_memtime),
-// [10] the longest lifetime, [11] its events, [12] summed epoch spans (last end - first start), [13] / [14]
-// the running epoch's first start / last end, [15] summed epoch dispatch spreads (last start - first start);
-// g_sw2: [0] the running epoch's last start, [1..3] summed sections (loads, event loop, flush + write-backs)
-__device__ unsigned long long g_sw[16];
-__device__ unsigned long long g_sw2[4];
+// k_wl_stepw's waves, recorded without atomics for WREC_E epochs from epoch g_wtarget on (the epoch counter
+// g_wepoch counts k_wl_prof_epoch launches): per wave (start, loads done, loop done, end) s_memtime stamps and
+// its events
+constexpr uint32_t WREC_E = 8, WREC_P = 16384;
+__device__ unsigned long long g_wrec[WREC_E][WREC_P][5];
+__device__ uint32_t g_wepoch, g_wtarget;
 #endif
 __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint32_t buid) {
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -762,7 +772,8 @@ __device__ __forceinline__ LRx shfl_up_rx(const LRx &a) {
 // batches up to NSEND of them into this launch: the sender's switch and this phy's Receive of each, what
 // k_wl_send does — they precede every event of the epoch), then every pending Receive / EndReceive with a
 // key below (bts, buid), in (ts, uid) order.
-__global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uint32_t buid, const SendBatch sb) {
+__global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uint32_t buid,
+                                                                                   const SendBatch sb) {
   const int64_t j = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   if (j >= D.nphy) return;
@@ -776,6 +787,10 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
   __shared__ LEnd s_end[ENB];
   __shared__ LSync s_sy[SYB];
   LPhy P = D.ps[j];
+  // (issued with the state: the ring's first 64 entries and the queue's first 8 at their compact places — a
+  // fast epoch leaves them there, head 0 — used when the state says they are the ones)
+  const LNi rg = lane <= D.ni_mask ? D.ni[(uint64_t)j * (D.ni_mask + 1) + lane] : LNi{0, 0.0};
+  const LRx q8 = lane < 8 && lane <= D.rq_mask ? D.rq[(uint64_t)j * (D.rq_mask + 1) + lane] : LRx{};
   const WMir m0 = mir_of(P);
   LNi *const gring = D.ni + (uint64_t)j * (D.ni_mask + 1);
   LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
@@ -784,9 +799,6 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
   uint32_t *const evc = D.evc + (uint32_t)(j % EV_STRIPES) * EV_STRIDE;
   LEv *const evs = D.ev + (uint64_t)(j % EV_STRIPES) * D.ev_scap;
   uint32_t err = 0;
-#pragma unroll
-  for (uint32_t u = 0; u < NSEND; u++)  // (constant indices into the batch: no scratch copy of it)
-    if (j == 0 && lane == u && u < sb.n) D.tx[sb.k0 + u] = sb.t[u];
   // the pending EndReceive records: lane q < LPE_CAP holds record q for the whole epoch (written back at the
   // end when changed)
   LPe mine{};
@@ -795,14 +807,9 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
   // ---- the batched SendPackets: lane i computes this phy's Receive of send i (YansWifiChannel::Send)
   LRx my{};
   bool ok = false;
-  {
-    LTx t{};
-    double dbm = 0.0;
-    uint32_t base = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < NSEND; u++)
-      if (lane == u) t = sb.t[u], dbm = sb.dbm[u], base = sb.base[u];
-    if (lane < sb.n && t.phy != (uint32_t)j) ok = reception(D, j, t, sb.k0 + lane, dbm, base, my);
+  if (lane < sb.n) {  // (computed by k_wl_rx when the closure sent: off the epoch's critical path)
+    my = D.rxb[(uint64_t)lane * D.nphy + j];
+    ok = my.at != ~0ull;
   }
   const uint64_t okm = __ballot(ok);
   const uint32_t nins = (uint32_t)__popcll(okm);
@@ -834,14 +841,19 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
   if (fast) {
     rq0 = 0;
     qn = P.rq_len;
-    if (lane < qn) rqc = rq[(P.rq_head + lane) & D.rq_mask];
+    const bool qc = (P.rq_head & D.rq_mask) == 0 && qn <= 8, h0 = (P.head & gm) == 0;
+    if (lane < qn) rqc = qc ? q8 : rq[(P.rq_head + lane) & D.rq_mask];
 #pragma unroll
     for (uint32_t u = 0; u < RL / 64; u++) {
       const uint32_t i = u * 64 + lane;
-      if (i < P.len) s_ring[(P.head + i) & (RL - 1)] = gring[(P.head + i) & gm];
+      if (i < P.len) s_ring[(P.head + i) & (RL - 1)] = h0 && u == 0 ? rg : gring[(P.head + i) & gm];
     }
     for (uint32_t i = 0; i < sb.n; i++) {  // (sorted by (arrival, uid): an insertion in registers)
       if (!((okm >> i) & 1ull)) continue;
+      if (qn > D.rq_mask) {  // (k_wl_send's capacity check)
+        err |= WE_RQCAP;
+        continue;
+      }
       const LRx e = rl_rx(my, (int)i);
       const bool lt = lane < qn && (rqc.at < e.at || (rqc.at == e.at && rqc.uid < e.uid));
       const uint32_t pos = (uint32_t)__popcll(__ballot(lt));
@@ -881,13 +893,14 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
 #endif
   // ---- staged appends
   uint32_t ns = 0, ne = 0, nv = 0;
+  bool slotted = false;  // (the phy's own event slots are written: further events go to the stripes)
   auto flush = [&]() {  // claim the staged syncs, end records and events (one atomic each), patch, store
     __syncthreads();
     uint32_t bs = 0, be = 0, bv = 0;
     if (lane == 0) {
       if (ns) bs = atomicAdd(&D.cnt[1], ns);
       if (ne) be = atomicAdd(&D.cnt[2], ne);
-      if (nv) bv = atomicAdd(evc, nv);
+      if (nv && slotted) bv = atomicAdd(evc, nv);
     }
     bs = rl_u32(bs, 0);
     be = rl_u32(be, 0);
@@ -908,7 +921,18 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
         D.eck[be + lane] = x.eck;
       }
     }
-    if (nv) {
+    if (nv && !slotted) {  // the epoch's first EVB events: the phy's own slots (a count, no claim)
+      if (lane < nv) {
+        LEv v = s_ev[lane];
+        v.sslot = fix(v.sslot);
+        D.evp[(uint64_t)j * EVB + lane] = v;
+      }
+      if (lane == 0) {
+        D.evn[j] = nv;
+        atomicAdd(&D.evt[(uint32_t)(j % EV_STRIPES) * EV_STRIDE], nv);  // (its result unused: no wait)
+      }
+      slotted = true;
+    } else if (nv) {  // (more: the stripes, claimed)
       if ((uint64_t)bv + nv > D.ev_scap) {
         err |= WE_CAP;
       } else if (lane < nv) {
@@ -966,15 +990,7 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
       } else {
         // InterferenceHelper::CalculateSnrPer (interference-helper.cc:336-353), as k_wl_step: the walk's
         // sequential part here (64 ring entries a trip, then lane by lane), the chunks' models in k_wl_mid
-        const uint32_t bi = eb.tx - sb.k0;  // (a transmission of this launch's batch: D.tx is being written)
-        LTx t{};
-        if (bi < sb.n) {
-#pragma unroll
-          for (uint32_t u = 0; u < NSEND; u++)
-            if (bi == u) t = sb.t[u];
-        } else {
-          t = D.tx[eb.tx];
-        }
+        const LTx t = D.tx[eb.tx];
         const Mode pm = make_mode(t.mc, t.rate, t.bw);
         const double noise0 = P.firstPower;
         rec.snr = snr_of(D, eb.w, noise0, pm);
@@ -987,59 +1003,67 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
         cs = rl_u32(cs, 0);
         const bool defer = (uint64_t)cs + need <= D.ck_cap;
         if (!defer) err |= WE_CKCAP;  // (the run fails: no inline fallback here)
+        // the walk, 64 ring entries a batch, a lane per step: step k's (previous, current) interval gives its
+        // chunks (CalculatePer's cases, interference-helper.cc:270-330); only the noise before each step — a
+        // running double sum, whose order is the reference's — is formed lane by lane
         uint32_t cn = 0;
         double noiseW = noise0;
-        auto ck = [&](int64_t dur, bool hdr) {
-          if (defer && dur != 0) {
-            if (lane == 0) D.ck[cs + cn] = LCk{noiseW, (int64_t)((uint64_t)dur << 1) | (hdr ? 1 : 0)};
-            cn++;
-          }
-        };
         int64_t previous = t0;
-        uint32_t q = 1;
-        LNi cb{0, 0.0};
-        uint32_t cq0 = 0;
-        bool have = false;
-        for (bool last = false; !last;) {
-          int64_t current;
-          double delta;
-          if (q < P.len) {
-            if (!have || q - cq0 >= 64) {
-              cq0 = q;
-              have = true;
-              cb = q + lane < P.len ? ring[(P.head + q + lane) & m] : LNi{0, 0.0};
-            }
-            const int u = (int)(q - cq0);
-            const int64_t et = rl_i64(cb.t, u);
-            const double ed = rl_d(cb.d, u);
-            if (et == nw && eb.w == -ed) {
-              current = nw, delta = 0.0, last = true;  // (the event's end entry: the closing (end, 0))
-            } else {
-              current = et, delta = ed;
-            }
-            q++;
-          } else {
-            current = nw, delta = 0.0, last = true;
+        for (uint32_t q0 = 1, last = 0; !last; q0 += 64) {
+          const uint32_t q = q0 + lane;
+          LNi c{0, 0.0};
+          if (q < P.len) c = ring[(P.head + q) & m];
+          const uint64_t em = __ballot(q < P.len && c.t == nw && eb.w == -c.d);  // (the event's end entry)
+          const uint32_t nin = P.len > q0 ? (P.len - q0 < 64 ? P.len - q0 : 64) : 0;
+          uint32_t nstep = 64, close = 64;  // steps of the batch; the lane of the closing (nw, 0) step
+          if (em) {
+            nstep = (uint32_t)__builtin_ctzll(em) + 1, close = nstep - 1, last = 1;
+          } else if (nin < 64) {
+            nstep = nin + 1, close = nin, last = 1;  // (the list ends: the closing step after it)
           }
-          if (previous >= payStart) {
-            ck(current - previous, false);
-          } else if (previous >= hdrStart) {
-            if (current >= payStart) {
-              ck(payStart - previous, true);
-              ck(current - payStart, false);
-            } else {
-              ck(current - previous, true);
-            }
-          } else {
-            if (current >= payStart) {
-              ck(payStart - hdrStart, true);
-              ck(current - payStart, false);
-            } else if (current >= hdrStart) {
-              ck(current - hdrStart, true);
+          const int64_t cur = lane == close ? nw : c.t;
+          const double dl = lane == close ? 0.0 : c.d;
+          int64_t prv = __shfl_up((long long)cur, 1);
+          if (lane == 0) prv = previous;
+          double nz = 0.0;  // the noise before step `lane`
+          double acc = noiseW;
+          for (uint32_t k = 0; k < nstep; k++) {
+            if (lane == k) nz = acc;
+            acc += rl_d(dl, (int)k);
+          }
+          int64_t d1 = 0, d2 = 0;
+          bool h1 = false;
+          if (lane < nstep) {
+            if (prv >= payStart) {
+              d1 = cur - prv;
+            } else if (prv >= hdrStart) {
+              h1 = true;
+              if (cur >= payStart) d1 = payStart - prv, d2 = cur - payStart;
+              else d1 = cur - prv;
+            } else if (cur >= payStart) {
+              h1 = true;
+              d1 = payStart - hdrStart, d2 = cur - payStart;
+            } else if (cur >= hdrStart) {
+              h1 = true;
+              d1 = cur - hdrStart;
             }
           }
-          noiseW += delta;
-          previous = current;
+          // (a zero-length chunk is skipped: ck (dur != 0)); the chunks' places by a wave prefix count
+          const uint32_t n1 = d1 != 0, n2 = d2 != 0, nc = n1 + n2;
+          uint32_t pre = nc;
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)pre, d);
+            if (lane >= (uint32_t)d) pre += y;
+          }
+          const uint32_t tot = rl_u32(pre, 63), at = cn + pre - nc;
+          if (defer) {
+            if (n1) D.ck[cs + at] = LCk{nz, (int64_t)((uint64_t)d1 << 1) | (h1 ? 1 : 0)};
+            if (n2) D.ck[cs + at + n1] = LCk{nz, (int64_t)((uint64_t)d2 << 1)};
+            cn += tot;
+          }
+          previous = rl_i64(cur, (int)(nstep - 1));
+          noiseW = acc;
         }
         eck = LEck{cs, defer ? cn : NONE, eb.w};
         rec.per = 0.0;  // (k_wl_mid writes the product)
@@ -1147,13 +1171,17 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
   if (ns | ne | nv) flush();
   // ---- write-backs: the pending records, the queue's rest (fast, after insertions), the ring (fast), the state
   if (pe_dirty && lane < (uint32_t)LPE_CAP) pe[lane] = mine;
-  if (fast && nins && lane >= rqn && lane < qn) rq[(P.rq_head + (lane - rqn)) & D.rq_mask] = rqc;
-  if (fast && ring_dirty) {
+  if (fast && (nins || rqn)) {  // (the queue's rest at its compact place: head 0)
+    if (lane >= rqn && lane < qn) rq[lane - rqn] = rqc;
+    P.rq_head = 0;
+  }
+  if (fast && ring_dirty) {  // (the ring at its compact place: head 0)
 #pragma unroll
     for (uint32_t u = 0; u < RL / 64; u++) {
       const uint32_t i = u * 64 + lane;
-      if (i < P.len) gring[(P.head + i) & gm] = s_ring[(P.head + i) & (RL - 1)];
+      if (i < P.len) gring[i] = s_ring[(P.head + i) & (RL - 1)];
     }
+    P.head = 0;
   }
   if (lane == 0) {
     if (changed) D.ps[j] = P;
@@ -1161,17 +1189,14 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
     if (err) atomicOr(&D.cnt[3], err);
   }
 #ifdef NSGPU_PHASE_PROF
-  if (lane == 0) {
-    const uint64_t pt3 = __builtin_amdgcn_s_memtime(), dt = pt3 - pt0, c = pev < 4 ? pev : 4;
-    atomicAdd(&g_sw[c], 1ull);
-    atomicAdd(&g_sw[5 + c], dt);
-    if (dt > atomicMax(&g_sw[10], dt)) g_sw[11] = pev;
-    atomicMin(&g_sw[13], pt0);
-    atomicMax(&g_sw[14], pt3);
-    atomicMax(&g_sw2[0], pt0);
-    atomicAdd(&g_sw2[1], pt1 - pt0);
-    atomicAdd(&g_sw2[2], pt2 - pt1);
-    atomicAdd(&g_sw2[3], pt3 - pt2);
+  const uint32_t we = g_wepoch - g_wtarget;
+  if (lane == 0 && we < WREC_E && j < (int64_t)WREC_P) {
+    unsigned long long *w = g_wrec[we][j];
+    w[0] = pt0;
+    w[1] = pt1;
+    w[2] = pt2;
+    w[3] = __builtin_amdgcn_s_memtime();
+    w[4] = pev;
   }
 #endif
 }
@@ -1182,13 +1207,7 @@ __global__ void k_wl_prof_epoch() {  // (one thread: fold the epoch's maxima, re
   g_wl_ph[4] += g_wl_ep[1];
   g_wl_ph[5] += 1;
   g_wl_ep[0] = g_wl_ep[1] = 0;
-  if (g_sw[14]) {
-    g_sw[12] += g_sw[14] - g_sw[13];
-    g_sw[15] += g_sw2[0] - g_sw[13];
-  }
-  g_sw[13] = ~0ull;
-  g_sw[14] = 0;
-  g_sw2[0] = 0;
+  g_wepoch++;
 }
 #endif
 
@@ -1239,31 +1258,27 @@ __device__ __forceinline__ void wl_sync_rank(const WDev &D, uint32_t uid0, uint3
 // The epoch's first tail kernel: the deferred PER products (blocks 0 .. MID_PER-1) and the syncs' ranks
 // (the rest) — independent, one launch.
 constexpr uint32_t MID_PER = 128, MID_RANK = 64;
-__global__ __launch_bounds__(256) void k_wl_mid(const WDev D, uint32_t uid0) {
-  __shared__ double s_c[PER_SEG];
-  if (blockIdx.x < MID_PER) wl_per(D, blockIdx.x, MID_PER, s_c);
-  else wl_sync_rank(D, uid0, blockIdx.x - MID_PER, MID_RANK);
-}
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
-// The epoch's tail after k_wl_mid, on the critical path: k_wl_fin (one block) — the EndReceive uids (the
-// sync order's) into the epoch's end records and its syncs' pending records, the status block (counters,
-// the first END_STAGE end records) straight into the host's mapped copy (no copy), the next epoch's counters
-// zeroed (no fills).
+// The epoch's close, on the critical path: k_wl_mid's last block (wl_fin) — the EndReceive uids (the sync
+// order's) into the epoch's end records and its syncs' pending records, the status block (counters, the
+// first END_STAGE end records) straight into the host's mapped copy (no copy).
 // The epoch's order, behind it on a second stream (nothing the PHY or the host closures do depends on it;
-// only the digest and the log): a merge-rank sort over tiles of TS keys (ts, uid << 32 | dense index) —
-//   k_wl_tsort: a block per tile resolves its events' EndReceive uids from their stripes, writes the dense
-//     events (when the host reads them) and sorts the tile in LDS (bitonic);
-//   k_wl_rank: an event's rank = its place in its tile + its lower bound in every other tile (each tile
-//     read once into LDS, the searches in LDS), then its digest term and (logging) its rank; the block that
-//     finishes last writes the running digest sum into the host's mapped copy.
-// The event lists and syncs are kept per epoch parity, and an epoch's k_wl_fin waits for the order of the
-// epoch before it (whose lists, syncs and status block it is about to reuse): the order runs one epoch
-// behind.  Epochs above ERANK_MAX events are ordered by the host from the dense events.  (The r04 all-pairs
-// count, k_wl_order, was quadratic: 384 us at 6.5 x 10^4 events, and on the critical path.)
+// only the digest and the log):
+//   k_wl_gather: the events from the phys' own slots (and the stripes' overflow) into one dense array, the
+//     EndReceive uids resolved;
+//   k_wl_tsort: a block per tile of TS keys (ts, uid << 32 | dense index) sorts it in LDS (bitonic);
+//   k_wl_rank: an event's rank = its place in its tile + its lower bound in every other tile (each tile read
+//     once into LDS, the searches in LDS), then its digest term and (logging) its rank; the block that
+//     finishes last writes the running digest sum into the host's mapped copy and zeroes the epoch's
+//     counters for the epoch two on.
+// The status blocks, event lists, syncs and counters are kept per epoch parity; an epoch's k_wl_stepw waits
+// for the order of the epoch two back (their last reader), which had a whole epoch to finish.  Epochs above
+// ERANK_MAX events are ordered by the host from the dense events.  (The r04 all-pairs count, k_wl_order, was
+// quadratic — 384 us at 6.5 x 10^4 events — and on the critical path.)
 constexpr uint32_t TS = 2048, TS_T = 1024;  // keys a tile; threads a block (two keys each)
 constexpr uint32_t ERANK_MAX = 65536, NTILE = ERANK_MAX / TS;
 __device__ __forceinline__ bool key_lt(const ulonglong2 &a, const ulonglong2 &b) {
@@ -1298,10 +1313,18 @@ __device__ __forceinline__ LEv resolved(const WDev &D, const StripeMap &sm, uint
   if (e.sslot != NONE) e.uid = D.sync[e.sslot].euid;
   return e;
 }
-__global__ __launch_bounds__(256) void k_wl_fin(const WDev D, uint32_t *zcnt, uint32_t *zevc, uint8_t *hst) {
+// The epoch's close (k_wl_mid's last block): the EndReceive uids (the sync order's) into the end records and
+// the syncs' pending records, the status block straight into the host's mapped copy.
+__device__ __forceinline__ void wl_fin(const WDev &D, uint8_t *hst) {
   __shared__ StripeMap sm;
+  __shared__ uint32_t s_nt;
   const uint32_t tid = threadIdx.x;
-  const uint32_t nev = load_stripes(D, sm);
+  if (tid < 64) {  // the events in the phys' own slots (their striped total), then the stripes' overflow
+    uint32_t c = D.evt[tid * EV_STRIDE];
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    if (tid == 0) s_nt = c;
+  }
+  const uint32_t nev = load_stripes(D, sm) + s_nt;  // (load_stripes's barriers order s_nt)
   const uint32_t nend = D.cnt[2] < D.end_cap ? D.cnt[2] : (uint32_t)D.end_cap;
   const uint32_t nsync = D.cnt[1] < D.sync_cap ? D.cnt[1] : (uint32_t)D.sync_cap;
   for (uint32_t i = tid; i < nend; i += 256) {  // the end records' EndReceive uids
@@ -1323,37 +1346,79 @@ __global__ __launch_bounds__(256) void k_wl_fin(const WDev D, uint32_t *zcnt, ui
     hc[2] = D.cnt[2];
     hc[3] = D.cnt[3];
     D.cnt[0] = nev;
-    D.cnt[4] = 0;  // (the chunk pool: k_wl_stepw and k_wl_mid are done with it)
   }
-  if (tid < 3) zcnt[tid] = 0;
-  if (tid < (uint32_t)EV_STRIPES) zevc[tid * EV_STRIDE] = 0;
 }
-__global__ __launch_bounds__(TS_T) void k_wl_tsort(const WDev D, int keep) {
+// The epoch's tail kernel: the deferred PER products (blocks 0 .. MID_PER-1), the syncs' ranks (the rest),
+// then — the block that finishes last — the epoch's close (wl_fin).
+__global__ __launch_bounds__(256) void k_wl_mid(const WDev D, uint32_t uid0, uint8_t *hst) {
+  __shared__ double s_c[PER_SEG];
+  __shared__ uint32_t s_last;
+  if (blockIdx.x < MID_PER) wl_per(D, blockIdx.x, MID_PER, s_c);
+  else wl_sync_rank(D, uid0, blockIdx.x - MID_PER, MID_RANK);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(D.mticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  wl_fin(D, hst);
+  if (threadIdx.x == 0) atomicExch(D.mticket, 0u);
+}
+// The epoch's events into one dense array, uids resolved (off the critical path): a block of 256 phys claims
+// its slots' events' places with one atomic (the dense order is the claims' order: the ranks do not depend
+// on it — keys are unique — and erank / evd agree), block 0 also the stripes' overflow events.
+__global__ __launch_bounds__(256) void k_wl_gather(const WDev D) {
   __shared__ StripeMap sm;
+  __shared__ uint32_t s_wt[4], s_base, s_sbase;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t nstr = blockIdx.x == 0 ? load_stripes(D, sm) : 0u;
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + tid;
+  const uint32_t n = j < (uint64_t)D.nphy ? D.evn[j] : 0u;
+  if (n) D.evn[j] = 0;  // (for the epoch two on, which reuses this parity)
+  uint32_t x = n;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) s_wt[wv] = x;
+  __syncthreads();
+  uint32_t off = x - n, tot = 0;
+  for (uint32_t w = 0; w < 4; w++) {
+    off += w < wv ? s_wt[w] : 0u;
+    tot += s_wt[w];
+  }
+  if (tid == 0) {
+    s_base = tot ? atomicAdd(D.gtot, tot) : 0u;
+    s_sbase = nstr ? atomicAdd(D.gtot, nstr) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t u = 0; u < n; u++) {
+    LEv e = D.evp[j * EVB + u];
+    if (e.sslot != NONE) e.uid = D.sync[e.sslot].euid;
+    D.evd[s_base + off + u] = e;
+  }
+  for (uint32_t k = tid; k < nstr; k += 256) D.evd[s_sbase + k] = resolved(D, sm, k);
+}
+__global__ __launch_bounds__(TS_T) void k_wl_tsort(const WDev D) {
   __shared__ ulonglong2 s_t[TS];
   const uint32_t tid = threadIdx.x;
-  const uint32_t nev = load_stripes(D, sm);
-  const bool big = nev > ERANK_MAX, dense = keep || big;
-  if (big) {  // (the host orders it: the dense events only)
-    for (uint32_t k = blockIdx.x * TS_T + tid; k < nev; k += gridDim.x * TS_T) D.evd[k] = resolved(D, sm, k);
-    return;
-  }
+  const uint32_t nev = D.cnt[0];
+  if (blockIdx.x == 0 && tid == 0) *D.gtot = 0;  // (k_wl_gather is done with its claims)
+  if (nev > ERANK_MAX) return;  // (the host orders it from the dense events)
   const uint32_t base = blockIdx.x * TS;
   if (base >= nev) return;  // (block-uniform)
   LEv e[2];
 #pragma unroll
   for (uint32_t u = 0; u < 2; u++) {  // (both loads in flight)
     const uint32_t k = base + u * TS_T + tid;
-    e[u] = k < nev ? D.ev[stripe_slot(D, sm, k)] : LEv{~0ull, NONE, 0, NONE, 0};
+    e[u] = k < nev ? D.evd[k] : LEv{~0ull, NONE, 0, NONE, 0};
   }
-  uint32_t eu[2];
-#pragma unroll
-  for (uint32_t u = 0; u < 2; u++) eu[u] = e[u].sslot != NONE ? D.sync[e[u].sslot].euid : e[u].uid;
 #pragma unroll
   for (uint32_t u = 0; u < 2; u++) {
     const uint32_t k = base + u * TS_T + tid;
-    e[u].uid = eu[u];
-    if (k < nev && dense) D.evd[k] = e[u];
     s_t[u * TS_T + tid] = k < nev ? make_ulonglong2(e[u].ts, (uint64_t)e[u].uid << 32 | k) : make_ulonglong2(~0ull, ~0ull);
   }
   __syncthreads();
@@ -1374,6 +1439,7 @@ __global__ __launch_bounds__(TS_T) void k_wl_tsort(const WDev D, int keep) {
 __global__ __launch_bounds__(TS_T) void k_wl_rank(const WDev D, uint64_t K0, int keep, unsigned long long *hdig) {
   __shared__ ulonglong2 s_o[TS];
   __shared__ unsigned long long s_dg[TS_T / 64];
+  __shared__ uint32_t s_last;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t nev = D.cnt[0];
   const uint32_t nt = (nev + TS - 1) / TS;
@@ -1424,12 +1490,19 @@ __global__ __launch_bounds__(TS_T) void k_wl_rank(const WDev D, uint64_t K0, int
     for (uint32_t w = 0; w < TS_T / 64; w++) t += s_dg[w];
     if (t) atomicAdd(D.edig, t);
     __threadfence();
-    if (atomicAdd(D.ticket, 1u) == gridDim.x - 1) {  // the last block: the running sum for the host
-      __threadfence();
-      *hdig = atomicAdd(D.edig, 0ull);
-      atomicExch(D.ticket, 0u);
-    }
+    s_last = atomicAdd(D.ticket, 1u) == gridDim.x - 1;
   }
+  __syncthreads();
+  if (!s_last) return;
+  // the last block: the running digest sum for the host; this parity's counters zeroed for the epoch two on
+  // (the order is their last reader; that epoch's k_wl_stepw waits for this kernel)
+  __threadfence();
+  if (tid == 0) {
+    *hdig = atomicAdd(D.edig, 0ull);
+    atomicExch(D.ticket, 0u);
+  }
+  if (tid < 3 || tid == 4) D.cnt[tid] = 0;  // (events, syncs, ends; the chunk pool)
+  if (tid < (uint32_t)EV_STRIPES) D.evc[tid * EV_STRIDE] = 0, D.evt[tid * EV_STRIDE] = 0;
 }
 
 // SendPacket of phy s at (ts): the sender's state switch (thread s) and one Receive per receiver.
@@ -1472,6 +1545,18 @@ __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t
   }
   rq[(P.rq_head + q) & D.rq_mask] = e;
   P.rq_len++;
+}
+
+// The Receives of one SendPacket (YansWifiChannel::Send's loop), computed when the closure sends — while the
+// host goes on — into the batch's row of D.rxb; the next epoch's k_wl_stepw queues them.  Thread 0 records
+// the transmission.
+__global__ __launch_bounds__(256) void k_wl_rx(const WDev D, LRx *row, LTx t, uint32_t k, double dbm, uint32_t base) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j == 0) D.tx[k] = t;
+  if (j >= D.nphy) return;
+  LRx e{};
+  if (j == (int64_t)t.phy || !reception(D, j, t, k, dbm, base, e)) e.at = ~0ull;
+  row[j] = e;
 }
 
 // Pending device events and the smallest ts among them (Next / IsFinished).
@@ -1530,12 +1615,20 @@ struct nsgpu_wifil {
   uint32_t *evc[2] = {nullptr, nullptr};  // the event-list stripe counters, by epoch parity (likewise)
   uint32_t *h_cnt = nullptr;
   LEv *evb[2] = {nullptr, nullptr};      // the event lists, by epoch parity (the order reads them an epoch behind)
+  LEv *evpb[2] = {nullptr, nullptr};     // the phys' own event slots, by epoch parity (likewise)
+  uint32_t *evnb[2] = {nullptr, nullptr};
+  uint32_t *evtb[2] = {nullptr, nullptr};  // their striped totals, by epoch parity
   LSync *syncb[2] = {nullptr, nullptr};  // the syncs, by epoch parity (likewise)
   hipStream_t s2 = nullptr;              // the epochs' order (k_wl_tsort / k_wl_rank)
   hipEvent_t ev_fin[2] = {nullptr, nullptr}, ev_ord[2] = {nullptr, nullptr};
   bool ord_pending[2] = {false, false};  // an order of this parity's epoch was launched and not yet waited for
   unsigned long long *h_digtot = nullptr, *d_digtot = nullptr;  // (mapped) the ordered epochs' digest sum
   uint64_t dig_added = 0;                // the part of it already added to a caller's digest
+  // host-side timing (NSGPU_WIFIL_HOSTPROF=1, printed at destroy): launches, the wait, the rest of an advance,
+  // and the time between advances (the host closure and the runtime), in ns summed over epochs
+  bool hprof = false;
+  uint64_t hp_n = 0, hp_launch = 0, hp_wait = 0, hp_post = 0, hp_out = 0;
+  std::chrono::steady_clock::time_point hp_last{};
   nsgpu_wifil_end *h_ends = nullptr;
   WMir *h_mir = nullptr;                 // mapped host memory: every phy's state fields (D.mir; GetState)
   std::vector<uint32_t> erank;
@@ -1549,6 +1642,9 @@ static void wl_use_stat(nsgpu_wifil *h, uint32_t b) {
   h->par = b;
   h->D.cnt = reinterpret_cast<uint32_t *>(h->stat[b]);
   h->D.ev = h->evb[b];
+  h->D.evp = h->evpb[b];
+  h->D.evn = h->evnb[b];
+  h->D.evt = h->evtb[b];
   h->D.sync = h->syncb[b];
   h->D.ends = reinterpret_cast<nsgpu_wifil_end *>(h->stat[b] + STAT_HDR);
   h->D.evc = h->evc[b];
@@ -1567,6 +1663,10 @@ static int wl_alloc(nsgpu_wifil *h, T **p, size_t n, const T *src = nullptr) {
 
 extern "C" int nsgpu_wifil_destroy(nsgpu_wifil *h) {
   if (!h) return NSGPU_OK;
+  if (h->hprof && h->hp_n)
+    fprintf(stderr, "nsgpu_wifil host: %llu epochs, per epoch (us): launches %.2f, wait %.2f, rest of advance %.2f, "
+            "between advances %.2f\n", (unsigned long long)h->hp_n, h->hp_launch / 1e3 / h->hp_n, h->hp_wait / 1e3 / h->hp_n,
+            h->hp_post / 1e3 / h->hp_n, h->hp_out / 1e3 / (h->hp_n > 1 ? h->hp_n - 1 : 1));
   for (hipStream_t q : {h->s, h->s2})
     if (q) {
       (void)hipStreamSynchronize(q);
@@ -1593,6 +1693,10 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
       c->loss.n > NSGPU_MAX_LOSS_CHAIN || c->error_model > NSGPU_WIFIL_YANS)
     return set_error(NSGPU_EINVAL, "nsgpu_wifil_create: ni_cap / rxq_cap must be powers of two >= 2, tx_cap in (0, 2^32)");
   nsgpu_wifil *h = new nsgpu_wifil();
+  {
+    const char *e = getenv("NSGPU_WIFIL_HOSTPROF");
+    h->hprof = e && e[0] == '1';
+  }
   const int64_t N = c->n_phy;
   WDev &D = h->D;
   D.nphy = N;
@@ -1647,9 +1751,12 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
     WL_TRY(wl_alloc(h, &h->stat[b], STAT_HDR + sync_cap * sizeof(nsgpu_wifil_end)));
     WL_TRY(wl_alloc(h, &h->evc[b], (size_t)EV_STRIPES * EV_STRIDE));
     WL_TRY(wl_alloc(h, &h->evb[b], ev_cap));
+    WL_TRY(wl_alloc(h, &h->evpb[b], (size_t)N * EVB));
+    WL_TRY(wl_alloc(h, &h->evnb[b], (size_t)N));
+    WL_TRY(wl_alloc(h, &h->evtb[b], (size_t)EV_STRIPES * EV_STRIDE));
     WL_TRY(wl_alloc(h, &h->syncb[b], sync_cap));
   }
-  WL_TRY(wl_alloc(h, &D.evd, ev_cap));
+  WL_TRY(wl_alloc(h, &D.evd, (size_t)N * EVB + ev_cap));  // (the slots' events, then the stripes')
   D.ev_scap = ev_cap / EV_STRIPES;
   wl_use_stat(h, 0);
   WL_TRY(wl_alloc(h, &D.end_sslot, sync_cap));
@@ -1661,6 +1768,9 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   WL_TRY(wl_alloc(h, &D.ck, (size_t)D.ck_cap));
   WL_TRY(wl_alloc(h, &D.erank, std::min<uint64_t>(ev_cap, ERANK_MAX)));
   WL_TRY(wl_alloc(h, &D.ticket, 1));
+  WL_TRY(wl_alloc(h, &D.mticket, 1));
+  WL_TRY(wl_alloc(h, &D.gtot, 1));
+  WL_TRY(wl_alloc(h, &D.rxb, (size_t)NSEND * N));
   WL_TRY(wl_alloc(h, &D.evg, std::min<uint64_t>(ev_cap, ERANK_MAX)));
   WL_TRY(wl_alloc(h, &h->d_pend, 2));
 #undef WL_TRY
@@ -1743,6 +1853,9 @@ extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base,
     mr.endTx = (int64_t)now + dur;
   }
   if (h->sb.n == 0) h->sb.k0 = k;
+  hipLaunchKernelGGL(k_wl_rx, dim3((unsigned)((h->D.nphy + 255) / 256)), dim3(256), 0, h->s, h->D,
+                     h->D.rxb + (uint64_t)h->sb.n * h->D.nphy, t, k, dbm, uid_base);
+  NSGPU_HIP(hipGetLastError());
   h->sb.t[h->sb.n] = t;
   h->sb.dbm[h->sb.n] = dbm;
   h->sb.base[h->sb.n] = uid_base;
@@ -1757,10 +1870,16 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
                                    uint64_t *dispatched, uint64_t *digest, uint64_t *log_ts, uint32_t *log_uid,
                                    uint32_t *log_ctx, uint64_t log_cap) {
   if (!h || !uid || !dispatched || !digest) return set_error(NSGPU_EINVAL, "nsgpu_wifil_advance: null");
-  const WDev D = h->D;  // (this epoch's status block: stat[par]; its counters were zeroed by the last epoch)
-  uint8_t *const nxt = h->stat[h->par ^ 1];
-  uint32_t *const nxt_evc = h->evc[h->par ^ 1];
-  // epoch: the phys' lanes, then the tail (PER products + sync ranks; patch + order + digest)
+  using clk = std::chrono::steady_clock;
+  const clk::time_point hp0 = h->hprof ? clk::now() : clk::time_point{};
+  if (h->hprof && h->hp_n) h->hp_out += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(hp0 - h->hp_last).count();
+  const WDev D = h->D;  // (this epoch's parity: its status block, lists, syncs; zeroed by the order two epochs back)
+  const uint32_t b = h->par;
+  if (h->ord_pending[b]) {  // (that order is their last reader)
+    NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev_ord[b], 0));
+    h->ord_pending[b] = false;
+  }
+  // epoch: the phys' waves, then the tail (PER products + sync ranks + the close), then the order behind it
   static const bool lane_step = [] {  // (NSGPU_WIFIL_LANE=1: the lane-per-phy step kernel)
     const char *e = getenv("NSGPU_WIFIL_LANE");
     return e && e[0] == '1';
@@ -1776,23 +1895,20 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
 #ifdef NSGPU_PHASE_PROF
   hipLaunchKernelGGL(k_wl_prof_epoch, dim3(1), dim3(1), 0, h->s);
 #endif
-  hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, h->s, D, *uid);
-  const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
-  const uint32_t b = h->par;
-  if (h->ord_pending[b ^ 1]) {  // (k_wl_fin reuses the last epoch's status block, lists and syncs)
-    NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev_ord[b ^ 1], 0));
-    h->ord_pending[b ^ 1] = false;
-  }
-  hipLaunchKernelGGL(k_wl_fin, dim3(1), dim3(256), 0, h->s, D, reinterpret_cast<uint32_t *>(nxt), nxt_evc, h->d_stat);
+  hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, h->s, D, *uid, h->d_stat);
   NSGPU_HIP(hipGetLastError());
+  const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
   NSGPU_HIP(hipEventRecord(h->ev_fin[b], h->s));
   NSGPU_HIP(hipStreamWaitEvent(h->s2, h->ev_fin[b], 0));
-  hipLaunchKernelGGL(k_wl_tsort, dim3(NTILE), dim3(TS_T), 0, h->s2, D, logging ? 1 : 0);
+  hipLaunchKernelGGL(k_wl_gather, dim3((unsigned)((D.nphy + 255) / 256)), dim3(256), 0, h->s2, D);
+  hipLaunchKernelGGL(k_wl_tsort, dim3(NTILE), dim3(TS_T), 0, h->s2, D);
   hipLaunchKernelGGL(k_wl_rank, dim3(NTILE), dim3(TS_T), 0, h->s2, D, *dispatched, logging ? 1 : 0, h->d_digtot);
   NSGPU_HIP(hipGetLastError());
   NSGPU_HIP(hipEventRecord(h->ev_ord[b], h->s2));
   h->ord_pending[b] = true;
+  const clk::time_point hp1 = h->hprof ? clk::now() : clk::time_point{};
   NSGPU_HIP(hipStreamSynchronize(h->s));
+  const clk::time_point hp2 = h->hprof ? clk::now() : clk::time_point{};
   wl_use_stat(h, b ^ 1);  // (the next epoch's block; SendPackets until then report their errors there)
   int rc = wl_check(h, "nsgpu_wifil_advance");
   if (rc) return rc;
@@ -1839,6 +1955,17 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   const uint64_t tot = *h->h_digtot;  // (the ordered epochs' terms so far: one aligned 8-byte store's value)
   *digest += tot - h->dig_added;
   h->dig_added = tot;
+  if (h->hprof) {
+    const clk::time_point hp3 = clk::now();
+    const auto ns = [](clk::time_point a, clk::time_point b) {
+      return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+    };
+    h->hp_launch += ns(hp0, hp1);
+    h->hp_wait += ns(hp1, hp2);
+    h->hp_post += ns(hp2, hp3);
+    h->hp_n++;
+    h->hp_last = hp3;
+  }
   if (nend > END_STAGE) NSGPU_HIP(hipStreamSynchronize(h->s));
   std::sort(h->ends_epoch.begin(), h->ends_epoch.end(),
             [](const nsgpu_wifil_end &a, const nsgpu_wifil_end &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
@@ -1943,19 +2070,25 @@ extern "C" int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_t
 }
 
 #ifdef NSGPU_PHASE_PROF
-// (diagnostic build only) the k_wl_step counters above (out[0..8)), k_wl_stepw's (out[8..24) g_sw, out[24..28)
-// g_sw2), reset after the read
+// (diagnostic build only) the k_wl_step counters above, reset after the read
 extern "C" int nsgpu_wifil_prof_read(unsigned long long *out) {
   NSGPU_HIP(hipDeviceSynchronize());
   NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wl_ph), sizeof(unsigned long long) * 8));
-  NSGPU_HIP(hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_sw), sizeof(unsigned long long) * 16));
-  NSGPU_HIP(hipMemcpyFromSymbol(out + 24, HIP_SYMBOL(g_sw2), sizeof(unsigned long long) * 4));
-  unsigned long long z[16] = {};
-  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wl_ph), z, sizeof(unsigned long long) * 8));
-  z[13] = ~0ull;  // (the running epoch's first start: a minimum)
-  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sw), z, sizeof(z)));
-  z[13] = 0;
-  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sw2), z, sizeof(unsigned long long) * 4));
+  unsigned long long z[8] = {};
+  NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wl_ph), z, sizeof(z)));
+  return NSGPU_OK;
+}
+// (diagnostic build only) k_wl_stepw's wave records: arm for WREC_E epochs from `target` on (out null), or read
+// them (out: WREC_E x WREC_P x 5 words)
+extern "C" int nsgpu_wifil_prof_waves(uint32_t target, unsigned long long *out) {
+  NSGPU_HIP(hipDeviceSynchronize());
+  if (!out) {
+    const uint32_t z = 0;
+    NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wepoch), &z, sizeof(z)));
+    NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wtarget), &target, sizeof(target)));
+    return NSGPU_OK;
+  }
+  NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wrec), sizeof(unsigned long long) * WREC_E * WREC_P * 5));
   return NSGPU_OK;
 }
 #endif
