@@ -195,11 +195,18 @@ class P2PGrid:
         used = [k for k, v in prof.items() if v[1] > 0 and v[1] * 2 >= top]  # (the per-window chain, not pauses)
         trips = sum(self.TRIPS.get(k, 3) for k in used)
         bound = len(used) * boundary_us + trips * trip_us
+        # each kernel's measured time in trips: (its live per-launch time - one boundary) / the probed trip
+        # latency, beside the trips counted from the code (TRIPS)
+        per = {k: {"counted": self.TRIPS.get(k, 3), "us_per_launch": round(prof[k][0] * 1e3, 3),
+                   "equivalent": round(max(prof[k][0] * 1e3 - boundary_us, 0.0) / trip_us, 1) if trip_us else None}
+               for k in used}
         return {"bound": "latency", "kernels_per_window": len(used), "boundary_us": boundary_us,
                 "trips_per_window": trips, "trip_us": trip_us, "bound_us_per_window": bound,
                 "achieved_us_per_window": window_us, "frac": bound / window_us if window_us else None,
+                "trips_per_kernel": per,
                 "note": "speed of light of the window chain = kernels x boundary + dependent trips x trip latency "
-                        "(nsgpu_probe_latency measures both on this GPU); frac = bound / the graph replay's window"}
+                        "(nsgpu_probe_latency measures both on this GPU); frac = bound / the graph replay's window; "
+                        "trips_per_kernel: counted from the code vs the live time expressed in unloaded trips"}
 
     def result(self):
         st, devc, appc, _ = self.engine.results()

@@ -11,7 +11,9 @@
 #   rocprof_p2p      rocprofv3 kernel stats of the default bench (eager launches: the tracer cannot follow graphs)
 #   rocprof_wifil    rocprofv3 kernel stats of the closed-loop Wi-Fi line
 #   rocprof_dumbbell rocprofv3 kernel stats of the partitioned dumbbell line
+#   rocprof_grid_part rocprofv3 kernel stats of the partitioned grid line (one rank)
 #   pmc_p2p          config-4 HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes -> traffic_p2p-grid.json
+#   pmc_lines        config-4 L2 / L1 request counters (TCC hit / miss / requests, TCP requests) per kernel
 #   py:<script>      python scripts/<script> (diagnostics), output to OUT/<script>.log
 set -e
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -52,6 +54,10 @@ for st in "$@"; do
       cd /tmp
       step rocprof_wifil 240 rocprofv3 --kernel-trace --stats -d $O/rocprof_wifil -o run --output-format csv -- python3 $R/bench.py --workload wifi-loop --steps 1 --warmup 0 --no-cpu-baseline
       cd $R ;;
+    rocprof_grid_part)
+      cd /tmp
+      NSGPU_P2P_EAGER=1 step rocprof_grid_part 240 rocprofv3 --kernel-trace --stats -d $O/rocprof_grid_part -o run --output-format csv -- python3 $R/bench.py --partitioned --steps 1 --warmup 0 --no-cpu-baseline
+      cd $R ;;
     rocprof_dumbbell)
       cd /tmp
       NSGPU_P2P_EAGER=1 step rocprof_dumbbell 240 rocprofv3 --kernel-trace --stats -d $O/rocprof_dumbbell -o run --output-format csv -- python3 $R/bench.py --workload dumbbell --partitioned --steps 1 --warmup 0 --no-cpu-baseline
@@ -62,6 +68,11 @@ for st in "$@"; do
       NSGPU_P2P_EAGER=1 step pmc_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_grid -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-secondary
       cd $R
       python scripts/pmc_traffic.py $O/pmc_fetch_grid $O/pmc_write_grid $O/traffic_p2p-grid.json k2_pa k2_handle k2_rank > $O/traffic_grid.log 2>&1 ;;
+    pmc_lines)
+      cd /tmp
+      NSGPU_P2P_EAGER=1 step pmc_tcc 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum --output-format csv -d $O/pmc_tcc -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-secondary
+      NSGPU_P2P_EAGER=1 step pmc_tcp 200 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d $O/pmc_tcp -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-secondary
+      cd $R ;;
     py:*) s=${st#py:}; step ${s%%.py*} 600 python scripts/${s//,/ } ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
