@@ -61,6 +61,10 @@ constexpr int NTAB = NSLOT + 1;  // words per node table record (count + slots)
 constexpr int NWIN = 32;         // windows per graph replay
 constexpr uint32_t NOCTX = 0xffffffffu;
 constexpr uint32_t LOCALBIT = 0x80000000u;  // child record kind: run inside the window as a local record
+// a Receive whose node another rank owns (partitioned engines; set by the device step from its record, so
+// that k2_pa and k_dfin2 need no owner lookup per child; only K_RECEIVE kind words carry it: their upper bits
+// hold no generation)
+constexpr uint32_t REMOTEBIT = 0x40000000u;
 
 // Packet descriptor: flow (sending app), IPv4 identification (Ipv4L3Protocol::m_identification of
 // the originating node), size in bytes with the headers added so far, IPv4 TTL.
@@ -74,8 +78,8 @@ struct Pkt {
 // from another XCD's writes: measured 2.8 -> 1.6 MB HBM fetch per k2_handle launch on config 4).
 struct DevRec {
   uint32_t busy, cnt, head, qmax;  // PointToPointNetDevice m_txMachineState, DropTail count / ring head, MaxPackets
-  uint32_t peer, peer_node, pad0, pad1;
-  uint64_t bps;                    // DataRate
+  uint32_t peer, peer_node, rkind, pad1;  // rkind: the Receive child's kind word (K_RECEIVE | REMOTEBIT when
+  uint64_t bps;                            //   another rank owns the peer's node)
   int64_t ifg, delay;              // InterframeGap, channel Delay
   uint64_t pad2;
   nsgpu_dev_counters c;            // (copied out strided by nsgpu_p2p_results / _counters)
@@ -530,7 +534,7 @@ __device__ __forceinline__ void device_act(const P2PDev &M, Emit &E, const Act &
     // Seconds (m_bps.CalculateTxTime (size)): static_cast<double>(bytes)*8/m_bps (data-rate.cc:224-227)
     const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)bps);
     E.child(txTime + ifg, E.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
-    E.child(txTime + delay, peer_node, K_RECEIVE, peer, tx);
+    E.child(txTime + delay, peer_node, dr.rkind, peer, tx);
   }
   if (nbusy != busy) M.dev[d].busy = nbusy;
   if (ncnt != cnt) M.dev[d].cnt = ncnt;
@@ -1445,9 +1449,9 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
       const uint32_t sl = s * M.maxc + j;
       const uint32_t kw = j < (uint32_t)PFC ? ckw[j] : M.ch_kind[sl];
       if ((kw & 0xffu) == K_FWD_UP) continue;
+      if (!(kw & REMOTEBIT)) continue;  // (a Receive on another rank's node: the device step marked it)
       const uint32_t ctx = j < (uint32_t)PFC ? cctx[j] : M.ch_ctx[sl];
       const uint32_t q = M.owner[ctx];
-      if (q == M.rank) continue;
       const uint32_t pos = atomicAdd(&x2hdr(M, M.x2_send, q)->n, 1u);
       if (pos < M.capx)
         x2rec(M, M.x2_send, q)[pos] = Ev{M.ch_ts[sl], uid0 + cp + j, ctx, kw, M.ch_a[sl], M.ch_pkt[sl]};
@@ -1882,6 +1886,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
       r.qmax = sc->dev_qmax[d];
       r.peer = sc->dev_peer[d];
       r.peer_node = sc->dev_node[sc->dev_peer[d]];
+      r.rkind = K_RECEIVE | ((owner && owner[r.peer_node] != (uint32_t)rank) ? REMOTEBIT : 0u);
       r.bps = sc->dev_bps[d];
       r.ifg = sc->dev_ifg_ns[d];
       r.delay = sc->dev_delay_ns[d];

@@ -656,7 +656,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
               ii++;
             }
           } else if (!WIDE || !(e.kind & LOCALBIT)) {  // (partitioned: a child on another rank's node goes there through X2)
-            valid = partition && (!DIST || M.owner[e.ctx] == M.rank);
+            valid = partition && (!DIST || !(e.kind & REMOTEBIT));  // (remote Receives go through X2)
           }  // (a local record's child ran in the last window itself)
         }
         k2_classify<WIDE>(s_look, b, run || drun, valid, e, NOSRC, R, tmn, wnd, wndw, gin[q], gpk[q]);
@@ -685,7 +685,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       const uint32_t q = (uint32_t)(idx / M.capx), rec = (uint32_t)(idx % M.capx);
       const bool valid = q < M.nranks && rec < x2hdr(M, M.x2_recv, q)->n;
       Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-      if (valid) e = x2rec(M, M.x2_recv, q)[rec];
+      if (valid) {
+        e = x2rec(M, M.x2_recv, q)[rec];
+        e.kind &= ~REMOTEBIT;  // (its sender's mark: this rank owns it)
+      }
       bool gin, gpk;
       k2_classify<WIDE>(s_look, b, drun, valid, e, NOSRC, R, tmn, wnd, wndw, gin, gpk);
       uint32_t w0;
@@ -941,7 +944,7 @@ __device__ __forceinline__ void lq_push(const P2PDev &M, const LQ4 &q, uint32_t 
 
 // Device state of the device a holder's or a hub's serial device pass is on, in registers.
 struct DevCache {
-  uint32_t d, busy, cnt, head, qmax, peer, peer_node;
+  uint32_t d, busy, cnt, head, qmax, peer, peer_node, rkind;
   uint64_t bps;
   int64_t ifg, delay;
   uint32_t q[6];  // enq_packets, enq_bytes, drop_packets, drop_bytes, deq_packets, tx_packets
@@ -966,6 +969,7 @@ struct DevCache {
     delay = dr.delay;
     peer = dr.peer;
     peer_node = dr.peer_node;
+    rkind = dr.rkind;
     const uint32_t *w = reinterpret_cast<const uint32_t *>(&M.dev[d].c);
     const uint4 a = *reinterpret_cast<const uint4 *>(w);
     const uint2 b2 = *reinterpret_cast<const uint2 *>(w + 4);
@@ -1029,7 +1033,7 @@ __device__ __forceinline__ void device_act_cached(const P2PDev &M, Emit &E, cons
     D.q[5]++;
     const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)D.bps);
     E.child(txTime + D.ifg, E.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
-    E.child(txTime + D.delay, D.peer_node, K_RECEIVE, D.peer, tx);
+    E.child(txTime + D.delay, D.peer_node, D.rkind, D.peer, tx);
   }
 }
 
@@ -1279,7 +1283,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
   const int32_t c0 = busy0 ? (int32_t)cnt0 : -1;
   const uint64_t bps = dr.bps;
   const int64_t ifg = dr.ifg, delay = dr.delay;
-  const uint32_t peer = dr.peer, peer_node = dr.peer_node;
+  const uint32_t peer = dr.peer, peer_node = dr.peer_node, rkind = dr.rkind;
   Pkt *qb = M.q_buf + (uint64_t)d * qcap;
   // pass A: the segment's composed map and its enqueue / dequeue counts
   CMap f{0, -CBIG, CBIG};
@@ -1389,7 +1393,7 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
         q5++;
         const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)bps);
         E.child(txTime + ifg, h.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
-        E.child(txTime + delay, peer_node, K_RECEIVE, peer, tx);
+        E.child(txTime + delay, peer_node, rkind, peer, tx);
       }
       if (h.xdrop) trace_te_drop(M, E, h.xdrop - 1, h.p);
       if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
