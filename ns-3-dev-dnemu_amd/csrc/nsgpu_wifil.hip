@@ -748,6 +748,7 @@ __device__ __forceinline__ void w_ni_insert(LNi *ring, uint32_t head, uint32_t &
 // per wave (the r04 kernel waited one atomic round trip per event).  A staged sync's slot is LOCAL | index
 // until the claim; the staged events, end records and pending records that name it are patched then.
 constexpr uint32_t RL = 256;
+constexpr uint32_t RSPEC = 32, QSPEC = 4;  // ring / queue entries loaded with the state (speculatively)
 constexpr uint32_t EVB = 64, ENB = 8, SYB = 8;
 constexpr uint32_t LOCAL = 0x80000000u;
 struct LEnd {  // a staged end record
@@ -787,10 +788,11 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
   __shared__ LEnd s_end[ENB];
   __shared__ LSync s_sy[SYB];
   LPhy P = D.ps[j];
-  // (issued with the state: the ring's first 64 entries and the queue's first 8 at their compact places — a
-  // fast epoch leaves them there, head 0 — used when the state says they are the ones)
-  const LNi rg = lane <= D.ni_mask ? D.ni[(uint64_t)j * (D.ni_mask + 1) + lane] : LNi{0, 0.0};
-  const LRx q8 = lane < 8 && lane <= D.rq_mask ? D.rq[(uint64_t)j * (D.rq_mask + 1) + lane] : LRx{};
+  // (issued with the state: the ring's first RSPEC entries and the queue's first QSPEC at their compact places
+  // — a fast epoch leaves them there, head 0 — used when the state says they are the ones; the first trip moves
+  // ~1 KB a wave, 10^4 waves at once)
+  const LNi rg = lane < RSPEC && lane <= D.ni_mask ? D.ni[(uint64_t)j * (D.ni_mask + 1) + lane] : LNi{0, 0.0};
+  const LRx q8 = lane < QSPEC && lane <= D.rq_mask ? D.rq[(uint64_t)j * (D.rq_mask + 1) + lane] : LRx{};
   const WMir m0 = mir_of(P);
   LNi *const gring = D.ni + (uint64_t)j * (D.ni_mask + 1);
   LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
@@ -841,12 +843,12 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
   if (fast) {
     rq0 = 0;
     qn = P.rq_len;
-    const bool qc = (P.rq_head & D.rq_mask) == 0 && qn <= 8, h0 = (P.head & gm) == 0;
+    const bool qc = (P.rq_head & D.rq_mask) == 0 && qn <= QSPEC, h0 = (P.head & gm) == 0;
     if (lane < qn) rqc = qc ? q8 : rq[(P.rq_head + lane) & D.rq_mask];
 #pragma unroll
     for (uint32_t u = 0; u < RL / 64; u++) {
       const uint32_t i = u * 64 + lane;
-      if (i < P.len) s_ring[(P.head + i) & (RL - 1)] = h0 && u == 0 ? rg : gring[(P.head + i) & gm];
+      if (i < P.len) s_ring[(P.head + i) & (RL - 1)] = h0 && i < RSPEC ? rg : gring[(P.head + i) & gm];
     }
     for (uint32_t i = 0; i < sb.n; i++) {  // (sorted by (arrival, uid): an insertion in registers)
       if (!((okm >> i) & 1ull)) continue;
