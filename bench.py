@@ -529,12 +529,17 @@ class WifiLoop:
         import wifi
         self.np, self.wifi = np, wifi
         self.side, self.stop = args.wifi_side, args.wifi_loop_stop
+        self.mac = getattr(args, "wifi_mac", "python")
+        if self.mac == "native" and os.environ.get("NSGPU_LIB"):
+            self.mac = "python"  # (the stand-in library links lib/libnsgpu.so: not another build of it)
         self.sc = self.scenario(self.stop)
         self.workload = (f"wifi-simple-adhoc-grid scaled to {self.side * self.side} nodes (config 3) with the MAC on the "
                          f"host: {self.side}x{self.side} grid 100 m, LogDistance(3, 46.6777)+ConstantSpeed, NIST error "
                          f"model; per phy a MAC stand-in sending 1000-B DSSS 1Mb/s frames when the PHY is IDLE (else "
                          f"backing off), period 1 s from seeded phases, Stop {self.stop}s; PHYs on the GPU "
-                         f"(nsgpu_wifil), closures on the host (nsgpu_sim)")
+                         f"(nsgpu_wifil), closures on the host (nsgpu_sim); the MAC stand-in as "
+                         + ("C callbacks (scripts/macstub.cc, as ns-3's C++ MAC)" if self.mac == "native"
+                            else "Python closures"))
         self._last = None
 
     def scenario(self, stop_s):
@@ -554,6 +559,8 @@ class WifiLoop:
         lp = wifi.LoopPhy(sc["phys"])
         sim.attach_wifi(lp)
         cnt = [0, 0]
+        if self.mac == "native":
+            return self.run_native(sc, sim, lp)
 
         def attempt(i):
             st, _ = sim.wifi_state(i)
@@ -578,6 +585,44 @@ class WifiLoop:
         res = (int(sim.dispatched()), int(digest), {"sends": cnt[0], "busy_attempts": cnt[1],
                                                    "end_receives": int(len(ends)), "next_uid": int(sim.next_uid()),
                                                    "epochs": int(nh), "us_per_epoch": secs * 1e6 / max(int(nh), 1)})
+        lp.close()
+        return res
+
+    def run_native(self, sc, sim, lp):
+        import ctypes as C
+        import time
+        import nsgpu
+        np = self.np
+        so = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(nsgpu.__file__)), "lib", "libnsgpu_macstub.so"))
+        so.nsgpu_macstub_install.restype = C.c_int
+        so.nsgpu_macstub_install.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                             C.c_double, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                             C.POINTER(C.c_void_p)]
+        so.nsgpu_macstub_counts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                            C.POINTER(C.c_int)]
+        so.nsgpu_macstub_destroy.argtypes = [C.c_void_p]
+        first = np.ascontiguousarray(sc["first"], np.uint64)
+        backoff = np.ascontiguousarray(sc["backoff"], np.uint64)
+        mode = sc["mode"]
+        h = C.c_void_p()
+        nsgpu.check(so.nsgpu_macstub_install(C.c_void_p(sim.h), sc["phys"].n_phy, first.ctypes.data, backoff.ctypes.data,
+                                             sc["period"], sc["size"], sc["dbm"], mode[0], mode[1], mode[2],
+                                             sc["preamble"], C.byref(h)))
+        sim.stop(sc["stop_ns"])
+        t0 = time.perf_counter()
+        sim.run()
+        secs = time.perf_counter() - t0
+        sends, busy, err = C.c_uint64(), C.c_uint64(), C.c_int()
+        so.nsgpu_macstub_counts(h, C.byref(sends), C.byref(busy), C.byref(err))
+        so.nsgpu_macstub_destroy(h)
+        if err.value:
+            raise RuntimeError(f"MAC stand-in: runtime call failed with {err.value}")
+        nh, _c, digest = sim.host_stats()
+        ends = lp.read_ends()
+        res = (int(sim.dispatched()), int(digest), {"sends": int(sends.value), "busy_attempts": int(busy.value),
+                                                    "end_receives": int(len(ends)), "next_uid": int(sim.next_uid()),
+                                                    "epochs": int(nh), "us_per_epoch": secs * 1e6 / max(int(nh), 1),
+                                                    "mac": "C callbacks (scripts/macstub.cc)"})
         lp.close()
         return res
 
@@ -634,6 +679,8 @@ def main():
     ap.add_argument("--wifi-side", type=int, default=100, help="wifi-grid: phys per grid side")
     ap.add_argument("--wifi-stop", type=float, default=2.0, help="wifi-grid: Simulator::Stop (s)")
     ap.add_argument("--wifi-loop-stop", type=float, default=0.2, help="wifi-loop: Simulator::Stop (s)")
+    ap.add_argument("--wifi-mac", choices=("native", "python"), default="native",
+                    help="wifi-loop: the MAC stand-in as C callbacks (lib/libnsgpu_macstub.so) or Python closures")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="p2p-grid: skip the wifi-grid / dumbbell entries of the `secondary` list")

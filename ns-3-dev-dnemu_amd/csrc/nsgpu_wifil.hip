@@ -24,6 +24,7 @@
 // RingNi layout of nsgpu_wifi.hip, with its eager prefix cursor), the state helper's end times, the pending
 // Receive queue (sorted by (arrival, uid)) and up to LPE_CAP pending EndReceive records.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -37,7 +38,7 @@ namespace {
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr int LPE_CAP = 8;  // pending EndReceive records of one phy (the live one + cancelled ones)
 constexpr uint32_t END_STAGE = 128;  // EndReceive records an epoch returns with its counters (more: a second copy)
-constexpr size_t STAT_HDR = 32;      // the status block's counters (5 x u32) and digest (at 24) before the ends
+constexpr size_t STAT_HDR = 32;      // the status block: counters (5 x u32), the epoch flag (word 6), then the ends
 static_assert(sizeof(nsgpu_wifil_end) % 8 == 0 && STAT_HDR % 8 == 0, "status block alignment");
 constexpr uint32_t WE_TX_IN_TX = 1, WE_NICAP = 2, WE_RQCAP = 4, WE_PECAP = 8, WE_CAP = 16, WE_CKCAP = 32;
 constexpr int NB = 8;  // ring entries loaded per batch
@@ -1317,7 +1318,7 @@ __device__ __forceinline__ LEv resolved(const WDev &D, const StripeMap &sm, uint
 }
 // The epoch's close (k_wl_mid's last block): the EndReceive uids (the sync order's) into the end records and
 // the syncs' pending records, the status block straight into the host's mapped copy.
-__device__ __forceinline__ void wl_fin(const WDev &D, uint8_t *hst) {
+__device__ __forceinline__ void wl_fin(const WDev &D, uint8_t *hst, uint32_t seq) {
   __shared__ StripeMap sm;
   __shared__ uint32_t s_nt;
   const uint32_t tid = threadIdx.x;
@@ -1341,18 +1342,21 @@ __device__ __forceinline__ void wl_fin(const WDev &D, uint8_t *hst) {
   __syncthreads();
   nsgpu_wifil_end *he = reinterpret_cast<nsgpu_wifil_end *>(hst + STAT_HDR);
   for (uint32_t i = tid; i < nend && i < END_STAGE; i += 256) he[i] = D.ends[i];
+  uint32_t *hc = reinterpret_cast<uint32_t *>(hst);
   if (tid == 0) {
-    uint32_t *hc = reinterpret_cast<uint32_t *>(hst);
     hc[0] = nev;
     hc[1] = D.cnt[1];
     hc[2] = D.cnt[2];
     hc[3] = D.cnt[3];
     D.cnt[0] = nev;
   }
+  __threadfence_system();  // (the block's writes to the host's copy land before the epoch's flag)
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(&hc[6], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // The epoch's tail kernel: the deferred PER products (blocks 0 .. MID_PER-1), the syncs' ranks (the rest),
 // then — the block that finishes last — the epoch's close (wl_fin).
-__global__ __launch_bounds__(256) void k_wl_mid(const WDev D, uint32_t uid0, uint8_t *hst) {
+__global__ __launch_bounds__(256) void k_wl_mid(const WDev D, uint32_t uid0, uint8_t *hst, uint32_t seq) {
   __shared__ double s_c[PER_SEG];
   __shared__ uint32_t s_last;
   if (blockIdx.x < MID_PER) wl_per(D, blockIdx.x, MID_PER, s_c);
@@ -1365,7 +1369,7 @@ __global__ __launch_bounds__(256) void k_wl_mid(const WDev D, uint32_t uid0, uin
   __syncthreads();
   if (!s_last) return;
   __threadfence();
-  wl_fin(D, hst);
+  wl_fin(D, hst, seq);
   if (threadIdx.x == 0) atomicExch(D.mticket, 0u);
 }
 // The epoch's events into one dense array, uids resolved (off the critical path): a block of 256 phys claims
@@ -1507,6 +1511,13 @@ __global__ __launch_bounds__(TS_T) void k_wl_rank(const WDev D, uint64_t K0, int
   if (tid < (uint32_t)EV_STRIPES) D.evc[tid * EV_STRIDE] = 0, D.evt[tid * EV_STRIDE] = 0;
 }
 
+// (diagnostic, NSGPU_WIFIL_NOORDER=1) what k_wl_rank's last block zeroes, without the order
+__global__ void k_wl_zero(const WDev D) {
+  const uint32_t tid = threadIdx.x;
+  if (tid < 3 || tid == 4) D.cnt[tid] = 0;
+  if (tid < (uint32_t)EV_STRIPES) D.evc[tid * EV_STRIDE] = 0, D.evt[tid * EV_STRIDE] = 0;
+}
+
 // SendPacket of phy s at (ts): the sender's state switch (thread s) and one Receive per receiver.
 __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t, double dbm, uint32_t base) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1626,6 +1637,7 @@ struct nsgpu_wifil {
   bool ord_pending[2] = {false, false};  // an order of this parity's epoch was launched and not yet waited for
   unsigned long long *h_digtot = nullptr, *d_digtot = nullptr;  // (mapped) the ordered epochs' digest sum
   uint64_t dig_added = 0;                // the part of it already added to a caller's digest
+  uint32_t seq = 0;                      // epochs launched (the close's flag)
   // host-side timing (NSGPU_WIFIL_HOSTPROF=1, printed at destroy): launches, the wait, the rest of an advance,
   // and the time between advances (the host closure and the runtime), in ns summed over epochs
   bool hprof = false;
@@ -1865,6 +1877,21 @@ extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base,
   return NSGPU_OK;  // (applied by the next epoch launch: its error bits, if any, fail that nsgpu_wifil_advance)
 }
 
+// The dispatch order of an epoch (gather, tile sort, rank) on the second stream behind the epoch's close; the
+// event lets the epoch two on (same parity) wait for it.  Launched before the host waits for the close: the
+// launches' API time overlaps the epoch's kernels.
+static int wl_launch_order(nsgpu_wifil *h, const WDev &D, uint32_t b, uint64_t K0, int keep) {
+  NSGPU_HIP(hipEventRecord(h->ev_fin[b], h->s));
+  NSGPU_HIP(hipStreamWaitEvent(h->s2, h->ev_fin[b], 0));
+  hipLaunchKernelGGL(k_wl_gather, dim3((unsigned)((D.nphy + 255) / 256)), dim3(256), 0, h->s2, D);
+  hipLaunchKernelGGL(k_wl_tsort, dim3(NTILE), dim3(TS_T), 0, h->s2, D);
+  hipLaunchKernelGGL(k_wl_rank, dim3(NTILE), dim3(TS_T), 0, h->s2, D, K0, keep, h->d_digtot);
+  NSGPU_HIP(hipGetLastError());
+  NSGPU_HIP(hipEventRecord(h->ev_ord[b], h->s2));
+  h->ord_pending[b] = true;
+  return NSGPU_OK;
+}
+
 // Every device event with a key below (bound_ts, bound_uid) (~0: all of them): dispatched in (ts, uid) order
 // from rank *dispatched on; the syncs' EndReceives take the uids from *uid on.  The dispatches are added to
 // the caller's digest (nsgpu_dispatch_digest_term) and log (at their ranks, below log_cap).
@@ -1877,8 +1904,10 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   if (h->hprof && h->hp_n) h->hp_out += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(hp0 - h->hp_last).count();
   const WDev D = h->D;  // (this epoch's parity: its status block, lists, syncs; zeroed by the order two epochs back)
   const uint32_t b = h->par;
-  if (h->ord_pending[b]) {  // (that order is their last reader)
-    NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev_ord[b], 0));
+  if (h->ord_pending[b]) {  // (that order is their last reader; it has had a whole epoch: usually done, then the
+    const hipError_t q = hipEventQuery(h->ev_ord[b]);  //  stream needs no wait packet before this epoch's kernels)
+    if (q == hipErrorNotReady) NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev_ord[b], 0));
+    else NSGPU_HIP(q);
     h->ord_pending[b] = false;
   }
   // epoch: the phys' waves, then the tail (PER products + sync ranks + the close), then the order behind it
@@ -1897,19 +1926,33 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
 #ifdef NSGPU_PHASE_PROF
   hipLaunchKernelGGL(k_wl_prof_epoch, dim3(1), dim3(1), 0, h->s);
 #endif
-  hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, h->s, D, *uid, h->d_stat);
+  const uint32_t seq = ++h->seq;  // (the close writes it into the host's status block last: the epoch's flag)
+  hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, h->s, D, *uid, h->d_stat, seq);
   NSGPU_HIP(hipGetLastError());
   const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
-  NSGPU_HIP(hipEventRecord(h->ev_fin[b], h->s));
-  NSGPU_HIP(hipStreamWaitEvent(h->s2, h->ev_fin[b], 0));
-  hipLaunchKernelGGL(k_wl_gather, dim3((unsigned)((D.nphy + 255) / 256)), dim3(256), 0, h->s2, D);
-  hipLaunchKernelGGL(k_wl_tsort, dim3(NTILE), dim3(TS_T), 0, h->s2, D);
-  hipLaunchKernelGGL(k_wl_rank, dim3(NTILE), dim3(TS_T), 0, h->s2, D, *dispatched, logging ? 1 : 0, h->d_digtot);
-  NSGPU_HIP(hipGetLastError());
-  NSGPU_HIP(hipEventRecord(h->ev_ord[b], h->s2));
-  h->ord_pending[b] = true;
+  static const bool no_order = [] {  // (diagnostic: NSGPU_WIFIL_NOORDER=1 skips the order — digest and log wrong)
+    const char *e = getenv("NSGPU_WIFIL_NOORDER");
+    return e && e[0] == '1';
+  }();
+  if (no_order) {  // (the counters the order would zero for the epoch two on)
+    hipLaunchKernelGGL(k_wl_zero, dim3(1), dim3(64), 0, h->s, D);
+  } else if (int rco = wl_launch_order(h, D, b, *dispatched, logging ? 1 : 0)) {
+    return rco;
+  }
   const clk::time_point hp1 = h->hprof ? clk::now() : clk::time_point{};
-  NSGPU_HIP(hipStreamSynchronize(h->s));
+  {  // the epoch's flag in the mapped status block (a spin: a stream synchronize's wake-up took microseconds);
+     // the stream is queried now and then, so a failed kernel (no flag) ends the wait with its error
+    volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(h->h_stat) + 6;
+    for (uint64_t n = 1; *flag != seq; n++) {
+      if ((n & 1023) == 0) {
+        const hipError_t q = hipStreamQuery(h->s);
+        if (q == hipErrorNotReady) continue;
+        NSGPU_HIP(q);
+        if (*flag != seq) return set_error(NSGPU_EHIP, "nsgpu_wifil_advance: the epoch's kernels ended without its flag");
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
   const clk::time_point hp2 = h->hprof ? clk::now() : clk::time_point{};
   wl_use_stat(h, b ^ 1);  // (the next epoch's block; SendPackets until then report their errors there)
   int rc = wl_check(h, "nsgpu_wifil_advance");

@@ -115,3 +115,27 @@ def test_epoch_order_paths_lds_hbm_host():
     for f in PHY_FIELDS[:8]:  # (the replay's oracle returns the counters only: nsref_wifil_replay)
         assert np.array_equal(gphys[f], ophys[f]), f
     lp.close()
+
+
+def test_bench_native_mac_stand_in_equals_the_oracle():
+    """bench.py's wifi-loop MAC stand-in as C callbacks (scripts/macstub.cc, lib/libnsgpu_macstub.so): on the
+    6x6 dense grid its run's dispatch count, digest, next uid, sends and busy attempts equal the oracle's
+    (nsref_wifil_run restates the same stand-in)."""
+    import os
+    import sys
+    import types
+    import nsgpu
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from wifi_loop_harness import run_oracle
+    sc = scenario(n_side=6, spacing=60.0, seed=3, period=12_000_000, stop_ns=150_000_000, size=600)
+    otot = run_oracle(sc)[3]
+    w = bench.WifiLoop(types.SimpleNamespace(wifi_side=6, wifi_loop_stop=0.15, wifi_mac="native"), None)
+    assert w.mac == "native"
+    sim = nsgpu.Sim()
+    lp = wifi.LoopPhy(sc["phys"])
+    sim.attach_wifi(lp)
+    disp, digest, info = w.run_native(sc, sim, lp)
+    assert (disp, digest, info["next_uid"]) == (otot["dispatched"], otot["digest"], otot["next_uid"])
+    assert (info["sends"], info["busy_attempts"]) == (otot["sends"], otot["busy"])
+    assert otot["busy"] > 0
