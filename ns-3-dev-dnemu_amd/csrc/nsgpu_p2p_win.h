@@ -451,6 +451,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   // (The slot arrays are WCAP long: a slot past the last window's size is loaded and ignored.)
   const uint32_t c_done = C.done, c_mode = C.mode, rt = C.rt, c_pvalid = C.pvalid, c_pW = C.pW, c_huid = C.huid;
   const uint32_t uid0 = C.puid0, c_plt = WIDE ? C.plt : 0u;
+  const uint32_t c_prep = DIST ? C.prep : 0u;  // (with the rest: its test after the slot loads cost a second trip)
   const Red red0 = C.red[0], red1 = C.red[1];
   const uint64_t hts = C.hts, c_ptmin = C.ptmin, K0 = C.pK0, ilim = C.pinline_lim, c_P = C.P_end;
   const uint64_t c_span_t = WIDE ? C.span_t : 0;
@@ -519,7 +520,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   }
   if (DIST) {
     if (blockIdx.x == 0 && threadIdx.x < M.nranks) x2hdr(M, M.x2_send, threadIdx.x)->n = 0;  // (X2 has sent them)
-    if (C.prep) return;
+    if (c_prep) return;
   }
   // k2_sdef's flag, every window (its blocks only read it: a block may start after another finished)
   if (DF && g == 0)
@@ -683,12 +684,13 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     if (partition) {
       const uint64_t idx = g - WCAP;
       const uint32_t q = (uint32_t)(idx / M.capx), rec = (uint32_t)(idx % M.capx);
-      const bool valid = q < M.nranks && rec < x2hdr(M, M.x2_recv, q)->n;
-      Ev e{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-      if (valid) {
-        e = x2rec(M, M.x2_recv, q)[rec];
-        e.kind &= ~REMOTEBIT;  // (its sender's mark: this rank owns it)
-      }
+      // the record and its peer's count in one trip (the record loaded whether or not it is valid: in range)
+      const uint32_t qc = q < M.nranks ? q : 0u;
+      const uint32_t nq = x2hdr(M, M.x2_recv, qc)->n;
+      Ev e = x2rec(M, M.x2_recv, qc)[rec];
+      const bool valid = q < M.nranks && rec < nq;
+      if (valid) e.kind &= ~REMOTEBIT;  // (its sender's mark: this rank owns it)
+      else e = Ev{0, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
       bool gin, gpk;
       k2_classify<WIDE>(s_look, b, drun, valid, e, NOSRC, R, tmn, wnd, wndw, gin, gpk);
       uint32_t w0;
