@@ -190,6 +190,8 @@ struct Ctl {
   uint64_t drn_stopts;          // folds it into every chunk's instead of sweeping the pool)
   uint32_t drn_stopuid, drpad2;
   uint64_t drb_tmin, drb_span, drb_bound, drb_stop, drb_nbound, drb_lim;  // the run window's bound (WinBound)
+  uint64_t drn_wendw;  // (wide partitioned engines) the wide bound's part of drn_*
+  uint64_t drcut;      // (wide partitioned engines) the run's candidates up to the narrow bound (k_drun_trim)
 };
 
 static_assert(offsetof(Ctl, prep) == offsetof(Ctl, W) + 12 && offsetof(Ctl, W) % 16 == 0, "the X0 payload");
@@ -269,7 +271,8 @@ struct P2PDev {
   uint8_t *x2_send, *x2_recv;   // X2: x2b bytes per peer
   uint32_t capx, pad_x;         // X2 records per peer per window (the run's largest cut between two ranks)
   uint64_t x2b;                 // X2 bytes per peer
-  uint32_t *gacc;               // k_gtile's accumulators: 2 x WCAP packed 64-bit words
+  uint32_t *gacc;               // k_gtile's accumulators: 2 x NACC packed 64-bit words
+  uint32_t *lxk;                // wide partitioned: a local record's compact index in this rank's X1Loc list
   // run control / outputs
   uint32_t n_init;    // initial pending count (pool 0)
   uint32_t uid_init;  // m_uid after setup
@@ -1093,7 +1096,8 @@ struct Ev {
 // rx/tx counts, smallest next time) is played by the pending-set reduction `red` and the counts.
 struct X1Hdr {
   uint32_t W, tc, tinl, needc;  // window events, their children, their inline children; pool compaction wanted
-  uint64_t pad0, lastkey;     // largest window key
+  uint32_t L, pad1;           // wide windows: this rank's local records (X1Loc entries)
+  uint64_t lastkey;           // largest window key
   Red red;                    // reduction of this rank's pending set after the window (next LBTS)
   uint64_t rkey, rrem, rhead; // sorted run: this rank's fitting key for the next chunk (~0: the rest fits), entries
                               // left, the first one's key (~0: none)
@@ -1104,7 +1108,20 @@ struct X1Ent {  // one window event: key and child counts (children | inline chi
   uint64_t key;
   uint32_t cnt, pad;
 };
-constexpr size_t X1B = sizeof(X1Hdr) + sizeof(X1Ent) * WCAP;
+// Wide windows: one rank's local records (same-node TransmitCompletes run inside the window), compacted by
+// k2_handle.  Their order words (lkw) decide every pair from different gen-0 ancestors exactly once the chain
+// depth is at most 2 (the partitioned wide span is kept below 3 tx_min, nsgpu_p2p_create_dist), except a
+// depth-2 word's clamped ancestor uid: `anc` holds it whole.  Records of one ancestor are on one rank, where
+// their exact chains are (lkey[rec]).
+struct X1Loc {
+  uint64_t w1, w2;     // lkw: (rel ts, local, parent rel ts), (ancestor uid, child index / ...)
+  uint32_t cnt, rec;   // children | inline children << 16; the record on its rank
+  uint32_t anc, pad;   // the gen-0 ancestor's uid
+};
+static_assert(sizeof(X1Loc) == 32, "X1Loc");
+constexpr int XLCAP = 4096;  // local records of one rank's window (LMAX)
+constexpr int NACC = WCAP + XLCAP;  // k_gtile's accumulator rows: gen-0 slots, then local records (compact order)
+constexpr size_t X1B = sizeof(X1Hdr) + sizeof(X1Ent) * WCAP + sizeof(X1Loc) * XLCAP;
 static_assert(X1B % 16 == 0, "k_copies moves 16-byte words");
 // X2: remote events for one peer (children whose node another rank owns), all-to-all; the record is
 // the pending event itself, uid included (mpi-interface.cc:414-506 sends {rx ns, node, dev, packet}).
@@ -1119,10 +1136,13 @@ constexpr int CAPX_MAX = 1024;
 constexpr size_t X0B = 16;  // X0: one rank's largest fitting window bound (+ pad)
 constexpr int MAXR = 64;    // ranks
 static_assert(MAXR <= 64 && HB == 64, "per-rank summaries are read one lane per rank in one-wave blocks");
-static_assert((uint64_t)MAXR * WCAP < (1u << 21), "k_gtile's packed rank fields");
+static_assert((uint64_t)MAXR * NACC <= (1u << 21), "k_gtile's packed rank fields");
 __device__ __forceinline__ X1Hdr *x1hdr(uint8_t *b, uint32_t q) { return (X1Hdr *)(b + (size_t)q * X1B); }
 __device__ __forceinline__ X1Ent *x1ent(uint8_t *b, uint32_t q) {
   return (X1Ent *)(b + (size_t)q * X1B + sizeof(X1Hdr));
+}
+__device__ __forceinline__ X1Loc *x1loc(uint8_t *b, uint32_t q) {
+  return (X1Loc *)(b + (size_t)q * X1B + sizeof(X1Hdr) + sizeof(X1Ent) * WCAP);
 }
 __device__ __forceinline__ X2Hdr *x2hdr(const P2PDev &M, uint8_t *b, uint32_t q) {
   return (X2Hdr *)(b + (size_t)q * M.x2b);
@@ -1213,6 +1233,7 @@ __global__ __launch_bounds__(256) void k_drun_clear(const P2PDev M) {
 }
 __global__ void k_drun_start(const P2PDev M, uint64_t n) {
   Ctl &C = *M.C;
+  if (M.wide) n = C.drcut < n ? C.drcut : n;  // (k_drun_trim: the run is the window's narrow part)
   const WinBound b = window_bound(C.rt ? C.red[0] : C.red[1]);  // (the bound k2_pa formed the window with)
   C.drb_tmin = b.tmin;
   C.drb_span = b.span;
@@ -1234,6 +1255,7 @@ __global__ void k_drun_start(const P2PDev M, uint64_t n) {
     C.drn_wend = r.wend;
     C.drn_stopts = r.stopts;
     C.drn_stopuid = r.stopuid;
+    C.drn_wendw = r.wendw;
   }
   M.xk_send[0] = n > (uint64_t)WCAP ? M.rn_key[WCAP - 1] : ~0ull;  // (this rank's fitting key)
   M.xk_send[1] = n ? M.rn_key[0] : ~0ull;                           // (its head key)
@@ -1244,19 +1266,59 @@ __global__ void k_drun_start(const P2PDev M, uint64_t n) {
 __global__ __launch_bounds__(256) void k_drun_red(const P2PDev M, uint64_t n) {
   Ctl &C = *M.C;
   const uint64_t tmin = C.drb_tmin;
-  uint64_t tmn = ~0ull, wnd = ~0ull;
+  uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     const uint64_t ts = tmin + (M.rn_key[i] >> 32);
-    const uint64_t x = ts + (uint64_t)M.lookahead[(M.rn_kind[i] & 0xffu) % K_NKINDS];
+    const uint32_t kd = (M.rn_kind[i] & 0xffu) % K_NKINDS;
+    const uint64_t x = ts + (uint64_t)M.lookahead[kd], xw = ts + (uint64_t)M.lookw[kd];
     tmn = ts < tmn ? ts : tmn;
     wnd = x < wnd ? x : wnd;
+    wndw = xw < wndw ? xw : wndw;
   }
   tmn = wave_min64(tmn);
   wnd = wave_min64(wnd);
+  wndw = wave_min64(wndw);
   if ((threadIdx.x & 63) == 0) {
     if (tmn != ~0ull) atomicMin((unsigned long long *)&C.drn_tmin, (unsigned long long)tmn);
     if (wnd != ~0ull) atomicMin((unsigned long long *)&C.drn_wend, (unsigned long long)wnd);
+    if (M.wide && wndw != ~0ull) atomicMin((unsigned long long *)&C.drn_wendw, (unsigned long long)wndw);
   }
+}
+// A widened window some rank cannot hold (wide partitioned engines): the run must be a narrow window (every child
+// of a run event sorts after every run event), so the sorted candidates past the window's narrow bound leave it —
+// those from the pool stay there, the others (children, remote events) are parked in the fresh buffer, which the
+// next handled window's maintenance moves into the pool; k_drun_red folds every candidate into the reduction.
+__global__ __launch_bounds__(1024) void k_drun_trim(const P2PDev M, uint64_t n) {
+  Ctl &C = *M.C;
+  const uint64_t nb = C.nbound, tmin = C.tmin;
+  __shared__ uint64_t s_cut;
+  if (threadIdx.x == 0) {  // the first candidate past the narrow bound (rn_key is sorted)
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (M.rn_key[mid] <= nb) lo = mid + 1;
+      else hi = mid;
+    }
+    s_cut = lo;
+  }
+  __syncthreads();
+  const uint64_t cut = s_cut;
+  for (uint64_t i = cut + threadIdx.x; i < n; i += 1024) {
+    if (M.rn_src[i] != NOSRC) continue;  // (still in the pool)
+    const uint64_t fi = atomicAdd((unsigned long long *)&C.nF, 1ull);
+    if (fi >= M.fcap) {
+      atomicOr(M.error, 1u);
+      continue;
+    }
+    const uint64_t k = M.rn_key[i];
+    M.f_ts[fi] = tmin + (k >> 32);
+    M.f_uid[fi] = (uint32_t)k;
+    M.f_ctx[fi] = M.rn_ctx[i];
+    M.f_kind[fi] = M.rn_kind[i];
+    M.f_a[fi] = M.rn_a[i];
+    M.f_pkt[fi] = M.rn_pkt[i];
+  }
+  if (threadIdx.x == 0) C.drcut = cut;
 }
 // The next chunk's cut key from the ranks' smallest fitting key fk and smallest head key hk (every rank computes
 // the same): a chunk that continues the same-ts group the last one cut (gp: the last chunk's key) takes more of
@@ -1298,17 +1360,27 @@ __global__ __launch_bounds__(TB) void k_drun_first(const P2PDev M) {
 }
 
 constexpr int GTB = 1024;  // blocks of k_gtile (grid-stride over tiles)
+// Rows: this rank's window records — its W gen-0 slots, then (WIDE) its L local records in X1Loc order; columns:
+// every rank's, in column tiles of RJ (a rank's gen-0 tiles, then its local tiles).  Per row, over the merged
+// window: the records before it (its global rank), those of a smaller ts, those of ts <= its own (its same-ts
+// group's end), and the children / inline children of the records before it and before its group (uid and
+// dispatch prefixes).  A gen-0 record precedes a local one of equal ts; two local records compare by their order
+// words, a tie by the ancestor uid, then (same ancestor: same node, this rank) by their exact chains.
+template <bool WIDE>
 __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
   Ctl &C = *M.C;
   if (!C.hdl) return;  // (k2_handle ran nothing: a cut, a pause, the end)
-  __shared__ uint64_t tk[RJ];
-  __shared__ uint32_t tc[RJ];
-  __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR];
+  __shared__ uint64_t tk[RJ], tk2[WIDE ? RJ : 1];
+  __shared__ uint32_t tc[RJ], tu[WIDE ? RJ : 1], tr[WIDE ? RJ : 1];
+  __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR], s_l[MAXR], s_g[MAXR];
   const uint32_t W = C.pW;
+  uint32_t L = 0;
   {  // every rank's window size at once, one lane per rank (HB = one wave), and the column tiles' prefix
     const uint32_t q = threadIdx.x;
-    const uint32_t wq = q < M.nranks ? x1hdr(M.x1_recv, q)->W : 0u;
-    const uint32_t nt = (wq + RJ - 1) / RJ;
+    const X1Hdr *hq = x1hdr(M.x1_recv, q < M.nranks ? q : 0u);
+    const uint32_t wq = q < M.nranks ? hq->W : 0u;
+    const uint32_t lq = (WIDE && q < M.nranks) ? hq->L : 0u;
+    const uint32_t ng = (wq + RJ - 1) / RJ, nt = ng + (lq + RJ - 1) / RJ;
     uint32_t inc = nt;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t x = __shfl_up(inc, o);
@@ -1316,57 +1388,141 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
     }
     if (q < M.nranks) {
       s_w[q] = wq;
+      s_l[q] = lq;
+      s_g[q] = ng;
       s_off[q] = inc - nt;
     }
     if (q == M.nranks - 1) s_off[M.nranks] = inc;
+    if (WIDE) L = __shfl(lq, (int)M.rank);
   }
   __syncthreads();
-  const uint32_t njt = s_off[M.nranks];
-  const uint64_t T = (uint64_t)((W + HB - 1) / HB) * njt;
+  const uint32_t njt = s_off[M.nranks], NR = W + L;
+  const uint64_t T = (uint64_t)((NR + HB - 1) / HB) * njt;
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {  // (uniform over the block)
     const uint32_t ti = (uint32_t)(t / njt), tj = (uint32_t)(t % njt);
     uint32_t q = 0;
     while (tj >= s_off[q + 1]) q++;
-    const uint32_t j0 = (tj - s_off[q]) * RJ;
-    const uint32_t n = s_w[q] - j0 < (uint32_t)RJ ? s_w[q] - j0 : (uint32_t)RJ;
-    const X1Ent *E = x1ent(M.x1_recv, q) + j0;
-    for (uint32_t k = threadIdx.x; k < (uint32_t)RJ; k += HB) {  // (padding: a key after every row's)
-      tk[k] = k < n ? E[k].key : ~0ull;
-      tc[k] = k < n ? E[k].cnt : 0u;
+    const uint32_t jt = tj - s_off[q];
+    const bool ltile = WIDE && jt >= s_g[q];  // a tile of rank q's local records
+    const uint32_t j0 = (ltile ? jt - s_g[q] : jt) * RJ, nq = ltile ? s_l[q] : s_w[q];
+    const uint32_t n = nq - j0 < (uint32_t)RJ ? nq - j0 : (uint32_t)RJ;
+    if (ltile) {
+      const X1Loc *E = x1loc(M.x1_recv, q) + j0;
+      for (uint32_t k = threadIdx.x; k < (uint32_t)RJ; k += HB) {  // (padding: after every row)
+        const bool in = k < n;
+        tk[k] = in ? E[k].w1 : ~0ull;
+        tk2[k] = in ? E[k].w2 : ~0ull;
+        tc[k] = in ? E[k].cnt : 0u;
+        tu[k] = in ? E[k].anc : 0u;
+        tr[k] = in ? E[k].rec : 0u;
+      }
+    } else {
+      const X1Ent *E = x1ent(M.x1_recv, q) + j0;
+      for (uint32_t k = threadIdx.x; k < (uint32_t)RJ; k += HB) {  // (padding: a key after every row's)
+        tk[k] = k < n ? E[k].key : ~0ull;
+        tc[k] = k < n ? E[k].cnt : 0u;
+      }
     }
     __syncthreads();
     const uint32_t i = ti * HB + threadIdx.x;
-    if (i < W) {
-      const uint64_t x = M.wkey[i];
+    if (i < NR) {
+      const bool lrow = WIDE && i >= W;
+      uint64_t x, x2 = 0;
+      uint32_t xu = 0, xrec = 0;
+      if (lrow) {
+        const X1Loc e = x1loc(M.x1_send, 0)[i - W];
+        x = e.w1, x2 = e.w2, xu = e.anc, xrec = e.rec;
+      } else {
+        x = M.wkey[i];
+      }
       const uint64_t lo = x & 0xffffffff00000000ull, hi = lo + (1ull << 32);
       uint32_t gr = 0, cp = 0, ip = 0, ipf = 0, lp = 0;
-      // (a fixed trip count, unrolled: the LDS loads pipeline instead of waiting one by one)
+      if (!ltile && !lrow) {
+        // (a fixed trip count, unrolled: the LDS loads pipeline instead of waiting one by one)
 #pragma unroll 16
-      for (uint32_t y = 0; y < (uint32_t)RJ; y++) {
-        const uint64_t k = tk[y];
-        const uint32_t c = tc[y];
-        const uint32_t nc = c & 0xffffu, ni = c >> 16;
-        const bool lt = k < x, blo = k < lo;
-        gr += lt;
-        cp += lt ? nc : 0u;
-        ip += lt ? ni : 0u;
-        ipf += blo ? ni : 0u;
-        lp += k < hi;
+        for (uint32_t y = 0; y < (uint32_t)RJ; y++) {
+          const uint64_t k = tk[y];
+          const uint32_t c = tc[y];
+          const uint32_t nc = c & 0xffffu, ni = c >> 16;
+          const bool lt = k < x, blo = k < lo;
+          gr += lt;
+          cp += lt ? nc : 0u;
+          ip += lt ? ni : 0u;
+          ipf += blo ? ni : 0u;
+          lp += k < hi;
+        }
+      } else if (!lrow || !ltile) {  // gen-0 x local: by ts only (at equal ts the gen-0 record first)
+        // a column before the row: local column of a smaller ts (gen-0 row) / gen-0 column of ts <= (local row)
+        const uint64_t cut = lrow ? hi : lo;
+#pragma unroll 16
+        for (uint32_t y = 0; y < (uint32_t)RJ; y++) {
+          const uint64_t k = tk[y] & 0xffffffff00000000ull;  // (the column's ts; padding: ~0)
+          const uint32_t c = tc[y];
+          const uint32_t nc = c & 0xffffu, ni = c >> 16;
+          const bool lt = k < cut, blo = k < lo;
+          gr += lt;
+          cp += lt ? nc : 0u;
+          ip += lt ? ni : 0u;
+          ipf += blo ? ni : 0u;
+          lp += k < hi;
+        }
+      } else {  // local x local: the order words
+        const int self = (q == M.rank && i - W >= j0 && i - W < j0 + n) ? (int)(i - W - j0) : -1;
+        bool tie = false;
+#pragma unroll 8
+        for (uint32_t y = 0; y < (uint32_t)RJ; y++) {
+          const uint64_t w1 = tk[y], w2 = tk2[y];
+          const uint32_t c = tc[y];
+          const uint32_t nc = c & 0xffffu, ni = c >> 16;
+          const bool eq = w1 == x;
+          const bool lt = (w1 < x) | (eq & (w2 < x2));
+          const uint64_t k = w1 & 0xffffffff00000000ull;
+          const bool blo = k < lo;
+          tie |= eq & (w2 == x2) & ((int)y != self);
+          gr += lt;
+          cp += lt ? nc : 0u;
+          ip += lt ? ni : 0u;
+          ipf += blo ? ni : 0u;
+          lp += k < hi;
+        }
+        if (tie) {  // (rare: equal words — a clamped ancestor uid, or one ancestor's chains)
+          for (uint32_t y = 0; y < n; y++) {
+            if (tk[y] != x || tk2[y] != x2 || (int)y == self) continue;
+            bool lt;
+            if (tu[y] != xu) {
+              lt = tu[y] < xu;
+            } else if (q == M.rank) {
+              lt = lk_before(M.lkey[tr[y] - LBASE], M.lkey[xrec - LBASE]);
+            } else {  // (one ancestor on two ranks: impossible — a node's chains are on its rank)
+              atomicOr(M.error, 64u);
+              lt = false;
+            }
+            if (lt) {
+              const uint32_t c = tc[y];
+              gr++;
+              cp += c & 0xffffu;
+              ip += c >> 16;
+            }
+          }
+        }
       }
       // two packed 64-bit accumulators instead of five words: (rank, group end, inline prefix: each at
-      // most MAXR x WCAP < 2^21) and (child prefix < 2^32, the group's inline prefix)
+      // most MAXR x NACC < 2^21) and (child prefix < 2^32, the group's inline prefix)
       unsigned long long *A = reinterpret_cast<unsigned long long *>(M.gacc);
+      const uint32_t row = lrow ? (uint32_t)WCAP + (i - W) : i;
       const uint64_t w0 = (uint64_t)gr | ((uint64_t)lp << 21) | ((uint64_t)ip << 42);
       const uint64_t w1 = (uint64_t)cp | ((uint64_t)ipf << 32);
-      if (w0) atomicAdd(&A[i], (unsigned long long)w0);
-      if (w1) atomicAdd(&A[WCAP + i], (unsigned long long)w1);
+      if (w0) atomicAdd(&A[row], (unsigned long long)w0);
+      if (w1) atomicAdd(&A[NACC + row], (unsigned long long)w1);
     }
     __syncthreads();
   }
 }
 
 // Block 0 also does the pool bookkeeping (k2_scan's) and, last, the run bookkeeping; the other blocks
-// read only fields block 0 leaves alone (pW, puid0, hdl, done < 2).
+// read only fields block 0 leaves alone (pW, puid0, hdl, done < 2).  WIDE: threads WCAP.. take this rank's local
+// records (X1Loc order): a local record's uid is its parent's child prefix + its child index.
+template <bool WIDE>
 __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   Ctl &C = *M.C;
   if (!C.hdl) return;
@@ -1376,16 +1532,20 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   const X1Hdr *lh = x1hdr(M.x1_recv, lq < M.nranks ? lq : 0u);
   const bool lv = lq < M.nranks;
   const uint32_t tinl_q = lv ? lh->tinl : 0u;
+  const uint32_t l_q = (WIDE && lv) ? lh->L : 0u;  // (the ranks' local records)
   // (block 0: the rest of the summaries and the run control, for the run bookkeeping, in the same trip)
   struct Bk {
     uint64_t nF, nfree, npush, pK0, ptmin, windows, P_end, live, inline_lim, max_windows, max_window, drg, dr1;
-    uint32_t nhub, puid0, rt, drtrim;
+    uint64_t bound, span_t;
+    uint32_t nhub, puid0, rt, drtrim, drun;
   } bk{};
   if (blockIdx.x == 0)
     bk = Bk{C.nF, C.nfree, C.npush, C.pK0, C.ptmin, C.windows, C.P_end, C.live, C.inline_lim, C.max_windows,
-            C.max_window, C.drg, C.dr1, C.nhub, C.puid0, C.rt, C.drtrim};
+            C.max_window, C.drg, C.dr1, WIDE ? C.bound : 0, WIDE ? C.span_t : 0, C.nhub, C.puid0, C.rt, C.drtrim,
+            C.drun};
   uint32_t hW = 0, htc = 0, hneedc = 0, hsuid = 0;
-  uint64_t hlk = 0, htmin = ~0ull, hwend = ~0ull, hsts = ~0ull, hrkey = ~0ull, hrrem = 0, hrhead = ~0ull;
+  uint64_t hlk = 0, htmin = ~0ull, hwend = ~0ull, hwendw = ~0ull, hsts = ~0ull, hrkey = ~0ull, hrrem = 0,
+           hrhead = ~0ull;
   if (blockIdx.x == 0 && lv) {
     hW = lh->W;
     htc = lh->tc;
@@ -1393,6 +1553,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     hlk = lh->lastkey;
     htmin = lh->red.tmin;
     hwend = lh->red.wend;
+    hwendw = lh->red.wendw;
     hsts = lh->red.stopts;
     hsuid = lh->red.stopuid;
     hrkey = lh->rkey;
@@ -1409,22 +1570,34 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     atomicExch(&C.x1arr, 0u);
     X1Hdr *hs = x1hdr(M.x1_send, 0);
     hs->W = hs->tc = hs->tinl = hs->needc = 0;
+    hs->L = 0;
     hs->lastkey = 0;
     hs->red.tmin = hs->red.wend = hs->red.stopts = hs->red.wendw = ~0ull;
     hs->red.stopuid = 0;
     hs->rkey = ~0ull;
     hs->rrem = 0;
   }
-  // the slot's accumulators, record and first children, all loaded before anything waits
-  const uint32_t s = blockIdx.x * HB + threadIdx.x;
-  const bool vs = s < W;
+  // the record's accumulators, record and first children, all loaded before anything waits (WIDE: thread
+  // WCAP + k takes local record k of this rank, its record index from the X1Loc list; its parent's child prefix
+  // needs the parent's accumulator, one more trip)
+  const uint32_t ti = blockIdx.x * HB + threadIdx.x;
+  const bool loc = WIDE && ti >= (uint32_t)WCAP;
+  const uint32_t Lown = WIDE ? __shfl(l_q, (int)M.rank) : 0u;
+  const bool vs = loc ? ti - (uint32_t)WCAP < Lown : ti < W;
   uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);
   uint64_t w0 = 0, w1 = 0, wk = 0;
-  uint32_t wc = 0, ncr = 0, ckw[PFC], cctx[PFC];
+  uint32_t s = ti, wc = 0, ncr = 0, ckw[PFC], cctx[PFC], wpar = 0;
   if (vs) {
-    w0 = A[s];
-    w1 = A[WCAP + s];
-    wk = M.wkey[s];
+    uint64_t lw1 = 0;
+    if (loc) {
+      const X1Loc e = x1loc(M.x1_send, 0)[ti - WCAP];
+      s = e.rec;
+      lw1 = e.w1;
+      wpar = M.wpar[s];
+    }
+    w0 = A[ti];
+    w1 = A[NACC + ti];
+    wk = loc ? lw1 : M.wkey[s];
     wc = M.wctx[s];
     ncr = M.nchild[s];
 #pragma unroll
@@ -1436,13 +1609,23 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   }
   const uint32_t tinl_g = wave_sum32(tinl_q);
   if (vs) {
-    A[s] = 0;
-    A[WCAP + s] = 0;
+    if (!WIDE) {  // (wide: k2_handle zeroes them — a local record reads its parent's below)
+      A[ti] = 0;
+      A[NACC + ti] = 0;
+    }
     const uint32_t gr = (uint32_t)(w0 & 0x1fffffu), lp = (uint32_t)((w0 >> 21) & 0x1fffffu),
                    ip = (uint32_t)(w0 >> 42), cp = (uint32_t)w1, ipf = (uint32_t)(w1 >> 32);
     // as k2_scan: (dispatch rank rel. K0, rank of the first inline child, child prefix, inline prefix)
     M.sinfo[s] = make_uint4(gr + (tinl_g ? ipf : 0), lp + ip, cp, ip);
-    M.pwkey[s] = wk;
+    if (loc) {  // uid = the parent's child prefix + the child index (DefaultSimulatorImpl::Schedule order)
+      const uint32_t p = wpar & 0xffffffu;
+      const uint32_t prow = p < (uint32_t)LBASE ? p : (uint32_t)WCAP + M.lxk[p - LBASE];
+      const uint32_t pcp = (uint32_t)A[NACC + prow];
+      M.pwkey[s] = ((wk >> 32) << 32) | (uint32_t)(C.puid0 + pcp + (wpar >> 24));
+      M.lrec[ti - WCAP] = s;
+    } else {
+      M.pwkey[s] = wk;
+    }
     M.pwctx[s] = wc;
     const uint32_t uid0 = C.puid0;
     for (uint32_t j = 0; j < ncr; j++) {
@@ -1467,7 +1650,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   const uint64_t mv = consumed < npush ? consumed : npush;
   const uint32_t nh = bk.nhub < (uint32_t)MAXHUB ? bk.nhub : (uint32_t)MAXHUB;
   // the ranks' summaries, reduced across the lanes (rank q's in lane q)
-  const uint32_t Wg = wave_sum32(hW), tcg = wave_sum32(htc);
+  const uint32_t Wg = wave_sum32(hW), tcg = wave_sum32(htc), Lg = WIDE ? wave_sum32(l_q) : 0u;
   const uint32_t needc = __ballot(hneedc != 0) ? 1u : 0u;
   // a partitioned sorted run: entries left on some rank -> the next chunk (drun_cut), unless the chunk just
   // run ended the run (it ended a cut same-ts group)
@@ -1477,6 +1660,10 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   Red rg{~0ull, ~0ull, ~0ull, 0, 0, ~0ull};
   rg.tmin = wave_min64(htmin);
   rg.wend = wave_min64(hwend);
+  if (WIDE) rg.wendw = wave_min64(hwendw);
+  // wide windows: the adaptive span keeps every rank's window inside its capacity (WCAP gen-0, NMAX records;
+  // k2_scan's rule, from the largest rank's counts so that every rank forms the same bound)
+  const uint64_t mxW = WIDE ? wave_max64(hW) : 0, mxN = WIDE ? wave_max64((uint64_t)hW + l_q) : 0;
   {  // the pending Stop: the smallest stopts, the first rank holding it
     rg.stopts = wave_min64(hsts);
     const uint64_t m = __ballot(lv && hsts == rg.stopts && rg.stopts != ~0ull);
@@ -1492,7 +1679,16 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     stack_and_hubs();
     return;
   }
-  C.K = bk.pK0 + Wg + tinl_g;
+  C.K = bk.pK0 + Wg + Lg + tinl_g;
+  if (WIDE) {
+    C.plt = Lown;  // (the next k2_pa appends them from lrec)
+    if (!bk.drun) {  // (a run's chunks are narrow)
+      const uint64_t span = bk.bound >> 32;
+      if (mxN > (uint64_t)(7 * NMAX / 8) || mxW > (uint64_t)(7 * WCAP / 8)) C.span_t = span - span / 4;
+      else if (mxN < (uint64_t)(3 * NMAX / 4) && mxW < (uint64_t)(3 * WCAP / 4) && bk.span_t < (1ull << 40))
+        C.span_t = bk.span_t + bk.span_t / 8 + 1;
+    }
+  }
   C.uid = bk.puid0 + tcg;
   if (Wg) C.last_ts = bk.ptmin + (lk >> 32);
   const uint32_t rt = bk.rt;
@@ -1500,7 +1696,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   C.rt = rt ^ 1;
   const uint64_t windows = bk.windows + 1;
   C.windows = windows;
-  if (Wg > bk.max_window) C.max_window = Wg;
+  if (Wg + Lg > bk.max_window) C.max_window = Wg + Lg;
   const uint64_t P_end = bk.P_end + (nF > nfree ? nF - nfree : 0);
   C.nfree = nfree - consumed + npush;
   C.P_end = P_end;
@@ -1831,8 +2027,13 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     for (uint32_t d = 0; d < D; d++) dmax = std::max(dmax, ++deg[sc->dev_node[d]]);
     const char *nw = getenv("NSGPU_P2P_NARROW");
     // (a chain of same-node TransmitCompletes inside a window is shorter than Lx / tx_min: LKD levels)
-    M.wide = (!owner && dmax <= (uint32_t)LQ && lx > tx_min && lx <= (int64_t)LKD * tx_min && lx < INFL &&
+    M.wide = (dmax <= (uint32_t)LQ && lx > tx_min && lx <= (int64_t)LKD * tx_min && lx < INFL &&
               !(nw && nw[0] == '1')) ? 1u : 0u;
+    // partitioned: the ranks order each other's local records by their two order words (k_gtile), which are
+    // exact for chains of at most 2 levels below a gen-0 event (the ancestor uid in X1Loc): the wide span is
+    // kept below 3 tx_min, so a third level (3 transmissions after its gen-0 event) never falls in a window
+    if (owner && M.wide)
+      for (int k = 0; k < K_NKINDS; k++) M.lookw[k] = std::min<int64_t>(M.lookw[k], 3 * tx_min - 1);
   }
   // ---- scenario upload ----
   TRY(dupload(h, &M.dev_node, sc->dev_node, D));
@@ -2071,12 +2272,14 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
       }
       uint32_t mx = 1;
       for (uint32_t c : cut) mx = std::max(mx, c);
+      if (M.wide) mx *= 3;  // (wide: a device's gen-0 TransmitStart and up to two local ones, chain depth <= 2)
       M.capx = std::min<uint32_t>((mx + 15) / 16 * 16, CAPX_MAX);
       M.x2b = sizeof(X2Hdr) + sizeof(Ev) * (uint64_t)M.capx;
     }
     TRY(dalloc(h, &M.x2_send, M.x2b * nranks));
     TRY(dalloc(h, &M.x2_recv, M.x2b * nranks));
-    TRY(dalloc(h, &M.gacc, 4 * (size_t)WCAP));
+    TRY(dalloc(h, &M.gacc, 4 * (size_t)NACC));
+    TRY(dalloc(h, &M.lxk, LCAP));
     h->comm = comm;
     memset(&h->x1h0, 0, sizeof(X1Hdr));
     h->x1h0.red.tmin = h->x1h0.red.wend = h->x1h0.red.stopts = h->x1h0.red.wendw = ~0ull;
@@ -2201,7 +2404,7 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
     NSGPU_HIP(hipMemcpyAsync(M.x1_send, &h->x1h0, sizeof(X1Hdr), hipMemcpyHostToDevice, s));  // (its own slot)
     NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, M.x2b * R, s));
     if (M.x2_recv != M.x2_send) NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, M.x2b * R, s));
-    NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 4 * WCAP * sizeof(uint32_t), s));
+    NSGPU_HIP(hipMemsetAsync(M.gacc, 0, 4 * NACC * sizeof(uint32_t), s));
   }
   if (M.log_cap) {  // (partitioned: every rank writes only the entries it dispatches, the union is the log;
                     //  mixed runs: the ranks of host dispatches stay unwritten)
@@ -2479,17 +2682,34 @@ static int x_alltoall(nsgpu_p2p *h, const void *send, void *recv, size_t bytes, 
   return NSGPU_OK;
 }
 
+// The partitioned window's kernels (narrow, or wide: local records ranked across the ranks through X1Loc).
+static void dist_pa(const P2PDev &M, hipStream_t s) {
+  if (M.wide) hipLaunchKernelGGL((k2_pa<true, true>), dim3(GRID_POOL), dim3(TB), 0, s, M);
+  else hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL), dim3(TB), 0, s, M);
+}
+static void dist_handle(const P2PDev &M, hipStream_t s) {
+  if (M.wide) hipLaunchKernelGGL(k2_handle<true>, dim3(K2_GRID_W), dim3(HB), 0, s, M);
+  else hipLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, M);
+}
+static void dist_rank_fin(const P2PDev &M, hipStream_t s) {
+  if (M.wide) {
+    hipLaunchKernelGGL(k_gtile<true>, dim3(GTB), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k_dfin2<true>, dim3(NACC / HB), dim3(HB), 0, s, M);
+  } else {
+    hipLaunchKernelGGL(k_gtile<false>, dim3(GTB), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k_dfin2<false>, dim3(NHB), dim3(HB), 0, s, M);
+  }
+}
 // The partitioned window (one RCCL member): 4 kernels and 3 collectives, on stream s.
 static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s, int nwin = NWIN) {
   const P2PDev &M = h->M;
   int rc = NSGPU_OK;
   for (int w = 0; w < nwin && !rc; w++) {
-    hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL), dim3(TB), 0, s, M);
+    dist_pa(M, s);
     rc = x_allgather(h, M.x0_send, M.x0_recv, X0B, s);
-    hipLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, M);
+    dist_handle(M, s);
     if (!rc) rc = x_allgather(h, M.x1_send, M.x1_recv, X1B, s);
-    hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, M);
-    hipLaunchKernelGGL(k_dfin2, dim3(NHB), dim3(HB), 0, s, M);
+    dist_rank_fin(M, s);
     if (!rc) rc = x_alltoall(h, M.x2_send, M.x2_recv, M.x2b, s);
   }
   return rc;
@@ -2535,6 +2755,7 @@ static int drun_sort(nsgpu_p2p *h, uint64_t W, hipStream_t s) {
     hipLaunchKernelGGL(k_rs_gather<uint32_t>, dim3(gg), dim3(256), 0, s, vin, M.wsrc, M.rn_src, n);
     hipLaunchKernelGGL(k_rs_gather<Pkt>, dim3(gg), dim3(256), 0, s, vin, M.wpkt, M.rn_pkt, n);
   }
+  if (n && M.wide) hipLaunchKernelGGL(k_drun_trim, dim3(1), dim3(1024), 0, s, M, n);
   hipLaunchKernelGGL(k_drun_start, dim3(1), dim3(1), 0, s, M, n);
   if (n) hipLaunchKernelGGL(k_drun_red, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256), 0, s, M, n);
   NSGPU_HIP(hipGetLastError());
@@ -2874,6 +3095,8 @@ extern "C" int nsgpu_p2p_set_trace(nsgpu_p2p *h, uint64_t cap) {
   if (rc) return rc;
   h->M.trace = tb;
   h->M.trace_n = tn;
+  if (h->M.dist) h->M.wide = 0;  // (a traced partitioned engine runs narrow windows: its local records' trace
+                                 //  uids would need the single engine's patch pass)
   NSGPU_HIP(hipMemset(h->M.trace_n, 0, sizeof(unsigned long long)));
   h->M.trace_cap = cap;
   if (h->gexec) {
@@ -3083,12 +3306,18 @@ struct nsgpu_p2p_group {
 static void launch_windows_group(nsgpu_p2p_group *g, hipStream_t s, int nwin = NWIN) {
   const unsigned n = (unsigned)g->m.size();
   for (int w = 0; w < nwin; w++) {
-    for (auto *h : g->m) hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL), dim3(TB), 0, s, h->M);
+    for (auto *h : g->m) dist_pa(h->M, s);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[0]);
-    for (auto *h : g->m) hipLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, h->M);
+    for (auto *h : g->m) dist_handle(h->M, s);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[1]);
-    for (auto *h : g->m) hipLaunchKernelGGL(k_gtile, dim3(GTB), dim3(HB), 0, s, h->M);
-    for (auto *h : g->m) hipLaunchKernelGGL(k_dfin2, dim3(NHB), dim3(HB), 0, s, h->M);
+    for (auto *h : g->m) {
+      if (h->M.wide) hipLaunchKernelGGL(k_gtile<true>, dim3(GTB), dim3(HB), 0, s, h->M);
+      else hipLaunchKernelGGL(k_gtile<false>, dim3(GTB), dim3(HB), 0, s, h->M);
+    }
+    for (auto *h : g->m) {
+      if (h->M.wide) hipLaunchKernelGGL(k_dfin2<true>, dim3(NACC / HB), dim3(HB), 0, s, h->M);
+      else hipLaunchKernelGGL(k_dfin2<false>, dim3(NHB), dim3(HB), 0, s, h->M);
+    }
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[2]);
   }
 }

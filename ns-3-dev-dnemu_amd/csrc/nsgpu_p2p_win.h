@@ -59,6 +59,7 @@ __device__ __forceinline__ uint32_t stg_pos(uint32_t r) { return (r & 7u) * STG_
 __device__ __forceinline__ uint32_t lds_pad(uint32_t r) { return r + (r >> 6); }
 constexpr int NMAX_PAD = NMAX + NMAX / 64;
 constexpr int LMAX = NMAX - WCAP;        // local records of one window
+static_assert(LMAX == XLCAP, "a partitioned rank's X1Loc list holds its window's local records");
 constexpr int SLOTG = WCAP + LMAX;       // k2_pa's slot-role threads (single engine): gen-0 slots, then local
 static_assert(LCAP < (1 << 24) && WTOT < (1 << 24), "wpar packs a record index in 24 bits");
 // Rank accumulators of window `win` (by parity: a deferred window's ranks are read after the next window's
@@ -107,7 +108,7 @@ __device__ __forceinline__ void slot_done(const P2PDev &M, uint32_t s, uint64_t 
   M.ninl[s] = ni;
   xa.tc += n;  // (the window's totals: a partitioned rank's X1 summary, the single engine's k2_rank bookkeeping)
   xa.ti += ni;
-  if (M.dist) {
+  if (M.dist && s < (uint32_t)WCAP) {  // (a local record's entry: X1Loc, compacted at its block's end)
     x1ent(M.x1_send, 0)[s] = X1Ent{key, n | (ni << 16), 0};
     xa.lk = key > xa.lk ? key : xa.lk;
   }
@@ -415,7 +416,8 @@ __device__ void drun_chunk(const P2PDev &M, Ctl &C, uint64_t t, uint64_t r0, uin
 // after the slot blocks), the rank's reduction goes to its X1 summary, and a window the host cut
 // (the first chunk of a partitioned sorted run, k_drun_first: C.prep) is already formed; during such a run
 // (C.drun) every k2_pa moves the run's next chunk in, and children, remote events and the pool stay pending.
-// WIDE: the single engine's wide windows (the last window's local records are appended too).
+// WIDE: wide windows (the last window's local records are appended too; partitioned: their sinfo / pwkey /
+// lrec come from k_dfin2).
 // k2_pa's grid (single engine): the slot blocks, then as many blocks of the pool sweep as GRID_POOL leaves
 template <bool WIDE>
 constexpr int pa_grid() {
@@ -427,7 +429,6 @@ constexpr int pa_grid() {
 // here); the pool's provisional uids of the window before it are resolved as the pool is read.
 template <bool DIST, bool WIDE, bool DF = false>
 __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
-  static_assert(!(DIST && WIDE), "wide windows are the single engine's");
   static_assert(!DF || WIDE, "deferred windows are the wide engine's");
   PH_BEGIN();
   BLK_T0();
@@ -682,7 +683,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   } else if (DIST && remote_role) {
     // ---- remote events the last X2 brought (partitioned): record idx % capx from rank idx / capx
     if (partition) {
-      const uint64_t idx = g - WCAP;
+      const uint64_t idx = g - NSG;
       const uint32_t q = (uint32_t)(idx / M.capx), rec = (uint32_t)(idx % M.capx);
       // the record and its peer's count in one trip (the record loaded whether or not it is valid: in range)
       const uint32_t qc = q < M.nranks ? q : 0u;
@@ -805,6 +806,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     const uint64_t a = C.drn_tmin, w = C.drn_wend, st = C.drn_stopts;
     tmn = a < tmn ? a : tmn;
     wnd = w < wnd ? w : wnd;
+    if (WIDE) {
+      const uint64_t ww = C.drn_wendw;
+      wndw = ww < wndw ? ww : wndw;
+    }
     if (st != ~0ull) {
       R.stopts = st;
       R.stopuid = C.drn_stopuid;
@@ -1951,15 +1956,40 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
         hub_node<WIDE>(M, C, M.hub_list[h], W, base, run || c_drun != 0, R, hb, lds, hc, &s_lcnt);
     }
   } else if (bx < (uint32_t)K2_GRID_W) {
+    if (WIDE && M.dist) {  // k_gtile's accumulators for this window (k_dfin2 read the last window's: local
+      uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);  // records' uids take their parents' child prefixes)
+      for (uint32_t i = (bx - (NHB + NHUB)) * HB + threadIdx.x; i < 2u * (uint32_t)NACC; i += NMB * HB) A[i] = 0;
+    }
     maintain(M, C, bx - (NHB + NHUB), run, handle, W, c_nfree, c_nF, c_Pe);
   } else {
     if (!run && handle && !M.dist) rank_tile(M, C, bx - K2_GRID_W, wrank_of(M, c_wn));  // (keys known before the handlers run)
   }
   if (WIDE && hc.lim && bx < (uint32_t)NLR) {  // this block's local region count (k2_rank / k2_scan read it;
     __syncthreads();                               //  written even when 0: the deferred pipeline keeps no reset)
-    if (threadIdx.x == 0) {
-      const uint32_t cap = bx < (uint32_t)NHB ? (uint32_t)LR : (uint32_t)LRH;
-      M.lcnt[bx] = s_lcnt < cap ? s_lcnt : cap;
+    const uint32_t cap = bx < (uint32_t)NHB ? (uint32_t)LR : (uint32_t)LRH;
+    const uint32_t cnt = s_lcnt < cap ? s_lcnt : cap;
+    if (threadIdx.x == 0) M.lcnt[bx] = cnt;
+    if (M.dist && cnt) {  // partitioned: the region's records (run by this block's holders) into this rank's
+      __shared__ uint32_t s_lb;  // X1Loc list, compacted: one allocation per block
+      if (threadIdx.x == 0) s_lb = atomicAdd(&x1hdr(M.x1_send, 0)->L, cnt);
+      __syncthreads();
+      const uint32_t lb = s_lb, rb = region_base(bx);
+      X1Loc *xl = x1loc(M.x1_send, 0);
+      uint64_t lts = 0;  // (the largest rel ts: the window's last dispatch time may be a local record's)
+      for (uint32_t k = threadIdx.x; k < cnt; k += HB) {
+        const uint32_t rec = rb + k;
+        if (lb + k >= (uint32_t)XLCAP) {
+          atomicOr(M.error, 64u);
+          continue;
+        }
+        const ulonglong2 w = M.lkw[rec - LBASE];
+        xl[lb + k] = X1Loc{w.x, w.y, M.nchild[rec] | (M.ninl[rec] << 16), rec, M.lkey[rec - LBASE].uid, 0u};
+        M.lxk[rec - LBASE] = lb + k;
+        const uint64_t t = w.x & 0xffffffff00000000ull;
+        lts = t > lts ? t : lts;
+      }
+      lts = wave_max64(lts);
+      if (threadIdx.x == 0 && lts) atomicMax((unsigned long long *)&x1hdr(M.x1_send, 0)->lastkey, (unsigned long long)lts);
     }
   }
   PH_MARK(9);

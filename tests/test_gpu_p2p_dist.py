@@ -28,8 +28,40 @@ def oracle(sc, log_cap=0):
 def test_grid_full_pop_order(nranks):
     sc = p2p.grid(8, 8)
     o = oracle(sc, 60000)
-    g = p2p.LoopbackGroup(sc, nranks, log_cap=60000).run(log_n=60000)
+    grp = p2p.LoopbackGroup(sc, nranks, log_cap=60000)
+    assert all(m.wide() for m in grp.members)  # (wide windows: local records ranked across the ranks)
+    g = grp.run(log_n=60000)
     assert_same(o, g)
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_wide_and_narrow_partitioned_windows_agree(nranks, monkeypatch):
+    """The same 24x24 grid through wide partitioned windows (same-node TransmitCompletes run inside the window as
+    local records, ordered across ranks by their chain words in X1Loc) and through narrow ones
+    (NSGPU_P2P_NARROW=1): both equal the oracle's full pop log, and the wide run takes fewer windows."""
+    sc = p2p.grid(24, 24)
+    o = oracle(sc, 400000)
+    wide = p2p.LoopbackGroup(sc, nranks, log_cap=400000)
+    assert all(m.wide() for m in wide.members)
+    gw = wide.run(log_n=400000)
+    assert_same(o, gw)
+    monkeypatch.setenv("NSGPU_P2P_NARROW", "1")
+    narrow = p2p.LoopbackGroup(sc, nranks, log_cap=400000)
+    assert not any(m.wide() for m in narrow.members)
+    gn = narrow.run(log_n=400000)
+    assert_same(o, gn)
+    assert gw[0].windows < gn[0].windows, (gw[0].windows, gn[0].windows)
+
+
+def test_config4_grid_partitioned_rccl_counters_digest():
+    """The partitioned bench line's workload on one RCCL rank (128x128, wide windows): every counter, the digest,
+    final time and next uid equal the oracle's."""
+    sc = p2p.grid(128, 128)
+    o = oracle(sc)
+    comm = p2p.Comm(p2p.Comm.unique_id(), 1, 0)
+    eng = p2p.DistEngine(sc, np.zeros(sc.n_nodes, np.uint32), 0, 1, comm)
+    assert eng.wide()
+    assert_same(o, eng.run(), log=False)
 
 
 @pytest.mark.parametrize("seed", range(3))
