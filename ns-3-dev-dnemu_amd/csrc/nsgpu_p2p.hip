@@ -91,7 +91,7 @@ static_assert(sizeof(DevRec) == 128 && offsetof(DevRec, c) == 64, "DevRec is one
 struct Red {
   uint64_t tmin, wend, stopts;
   uint32_t stopuid, pad;
-  uint64_t wendw;  // the wide bound: min over pending of ts + lookw (cross-node lookahead; single engine)
+  uint64_t wendw;  // the wide bound: min over pending of ts + lookw (cross-node lookahead; wide engines)
 };
 
 // A deferred window's dispatch bases: what k2_sdef needs once the window's records are staged in rank order.
@@ -160,7 +160,7 @@ struct Ctl {
   uint32_t huid, x1arr;            //   window's last timestamp (W_end or the host event's); the host uid;
                                    //   k_dfin2's blocks that have read the X1 headers
   uint64_t pchild;                 // children of the last scanned window that stay pending (not inline)
-  // ---- wide windows (single engine, nsgpu_p2p_win.h): same-node TransmitCompletes run inside them ----
+  // ---- wide windows (nsgpu_p2p_win.h; partitioned: k_gtile / k_dfin2): same-node TransmitCompletes run inside ----
   uint64_t lim_rel;   // a TransmitComplete child with rel ts < lim_rel is a local record of this window
   uint64_t nbound;    // the narrow bound of the forming window (an overflowing wide window is trimmed to it)
   uint64_t tn0;       // trace records before this window's handlers (the local records' uid patch)
@@ -230,7 +230,7 @@ struct P2PDev {
   uint32_t icmp;                                  // ICMP errors are generated (scenario icmp)
   int64_t lookahead[K_NKINDS];
   int64_t lookw[K_NKINDS];  // wide windows: the smallest delay of a child that does not run in the window
-  uint32_t wide, pad_w;     // wide windows on (single engine)
+  uint32_t wide, pad_w;     // wide windows on
   // model state
   DevRec *dev;  // per-device tx state + transmit parameters (one record per device)
   Pkt *q_buf;
@@ -1010,7 +1010,7 @@ struct WinBound {
   uint64_t nbound;  // the narrow bound (span = the narrow lookahead's)
   uint64_t lim;     // local records: a TransmitComplete child with rel ts < lim runs in the window (0: none)
 };
-// wide: the single engine's wide windows — the span is span_t clamped between the narrow bound (min over
+// wide: wide windows — the span is span_t clamped between the narrow bound (min over
 // pending of ts + lookahead) and the wide one (ts + lookw, nsgpu_p2p_create); a same-node TransmitComplete
 // before the window's end then runs inside it (local record).
 __device__ __forceinline__ WinBound window_bound(const Red &R, bool wide = false, uint64_t span_t = 0) {
@@ -1128,10 +1128,11 @@ static_assert(X1B % 16 == 0, "k_copies moves 16-byte words");
 struct X2Hdr {
   uint32_t n, pad[3];
 };
-// X2 records per peer: a device starts at most one transmission per window (its TransmitComplete is a
-// child, and children sort after the window), and Receive is the only child scheduled on another
-// node, so rank p sends rank q at most as many records per window as p has devices whose peer q owns
-// (nsgpu_p2p_create_dist sizes X2 to the largest such cut, rounded up to 16; at most CAPX_MAX).
+// X2 records per peer: a device starts at most one transmission per narrow window (its TransmitComplete is a
+// child, and children sort after the window) — three per wide one (its local TransmitCompletes start the next
+// ones: chain depth <= 2) — and Receive is the only child scheduled on another node, so rank p sends rank q at
+// most that many records per window per device of p whose peer q owns (nsgpu_p2p_create_dist sizes X2 to the
+// largest such cut, rounded up to 16; at most CAPX_MAX).
 constexpr int CAPX_MAX = 1024;
 constexpr size_t X0B = 16;  // X0: one rank's largest fitting window bound (+ pad)
 constexpr int MAXR = 64;    // ranks
@@ -1359,7 +1360,14 @@ __global__ __launch_bounds__(TB) void k_drun_first(const P2PDev M) {
   }
 }
 
-constexpr int GTB = 1024;  // blocks of k_gtile (grid-stride over tiles)
+#ifndef GT_CT
+#define GT_CT 1  // column tiles of one k_gtile work item (more: fewer atomics, but the compares bound it)
+#endif
+#ifndef GT_GJ
+#define GT_GJ 128  // columns of one k_gtile tile (smaller tiles: more waves a SIMD to interleave)
+#endif
+constexpr int GJ = GT_GJ;
+constexpr int GTB = 4096;  // blocks of k_gtile (grid-stride over tiles: a wide window's ~1,400 tiles in one round, several waves a SIMD)
 // Rows: this rank's window records — its W gen-0 slots, then (WIDE) its L local records in X1Loc order; columns:
 // every rank's, in column tiles of RJ (a rank's gen-0 tiles, then its local tiles).  Per row, over the merged
 // window: the records before it (its global rank), those of a smaller ts, those of ts <= its own (its same-ts
@@ -1370,8 +1378,11 @@ template <bool WIDE>
 __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
   Ctl &C = *M.C;
   if (!C.hdl) return;  // (k2_handle ran nothing: a cut, a pause, the end)
-  __shared__ uint64_t tk[RJ], tk2[WIDE ? RJ : 1];
-  __shared__ uint32_t tc[RJ], tu[WIDE ? RJ : 1], tr[WIDE ? RJ : 1];
+  // a column tile in LDS: its rel ts (the common test), child counts, and the fine key an equal ts needs — a
+  // gen-0 record's uid; a local record's order words' low part and second word (ties: ancestor uid, record)
+  __shared__ uint32_t tts[GJ], tc[GJ], tfa[GJ];
+  __shared__ uint64_t tfb[WIDE ? GJ : 1];
+  __shared__ uint32_t tu[WIDE ? GJ : 1], tr[WIDE ? GJ : 1];
   __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR], s_l[MAXR], s_g[MAXR];
   const uint32_t W = C.pW;
   uint32_t L = 0;
@@ -1380,7 +1391,7 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
     const X1Hdr *hq = x1hdr(M.x1_recv, q < M.nranks ? q : 0u);
     const uint32_t wq = q < M.nranks ? hq->W : 0u;
     const uint32_t lq = (WIDE && q < M.nranks) ? hq->L : 0u;
-    const uint32_t ng = (wq + RJ - 1) / RJ, nt = ng + (lq + RJ - 1) / RJ;
+    const uint32_t ng = (wq + GJ - 1) / GJ, nt = ng + (lq + GJ - 1) / GJ;
     uint32_t inc = nt;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t x = __shfl_up(inc, o);
@@ -1397,97 +1408,105 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
   }
   __syncthreads();
   const uint32_t njt = s_off[M.nranks], NR = W + L;
-  const uint64_t T = (uint64_t)((NR + HB - 1) / HB) * njt;
+  // a work item: one row tile against GT_CT consecutive column tiles, summed in registers (one pair of atomics per
+  // row and item: the accumulators' atomics, not the compares, bound the kernel)
+  const uint32_t nseg = (njt + GT_CT - 1) / GT_CT;
+  const uint64_t T = (uint64_t)((NR + HB - 1) / HB) * nseg;
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {  // (uniform over the block)
-    const uint32_t ti = (uint32_t)(t / njt), tj = (uint32_t)(t % njt);
+   const uint32_t ti = (uint32_t)(t / nseg), sg = (uint32_t)(t % nseg);
+   const uint32_t i = ti * HB + threadIdx.x;
+   const bool lrow = WIDE && i >= W;
+   uint32_t tx = 0, fax = 0, xu = 0, xrec = 0;
+   uint64_t fbx = 0;
+   if (i < NR) {
+     if (lrow) {
+       const X1Loc e = x1loc(M.x1_send, 0)[i - W];
+       tx = (uint32_t)(e.w1 >> 32), fax = (uint32_t)e.w1, fbx = e.w2, xu = e.anc, xrec = e.rec;
+     } else {
+       const uint64_t key = M.wkey[i];
+       tx = (uint32_t)(key >> 32), fax = (uint32_t)key;
+     }
+   }
+   uint32_t gr = 0, cp = 0, ip = 0, ipf = 0, lp = 0;
+   const uint32_t tj1 = (sg + 1) * GT_CT < njt ? (sg + 1) * GT_CT : njt;
+   for (uint32_t tj = sg * GT_CT; tj < tj1; tj++) {
     uint32_t q = 0;
     while (tj >= s_off[q + 1]) q++;
     const uint32_t jt = tj - s_off[q];
     const bool ltile = WIDE && jt >= s_g[q];  // a tile of rank q's local records
-    const uint32_t j0 = (ltile ? jt - s_g[q] : jt) * RJ, nq = ltile ? s_l[q] : s_w[q];
-    const uint32_t n = nq - j0 < (uint32_t)RJ ? nq - j0 : (uint32_t)RJ;
+    const uint32_t j0 = (ltile ? jt - s_g[q] : jt) * GJ, nq = ltile ? s_l[q] : s_w[q];
+    const uint32_t n = nq - j0 < (uint32_t)GJ ? nq - j0 : (uint32_t)GJ;
     if (ltile) {
       const X1Loc *E = x1loc(M.x1_recv, q) + j0;
-      for (uint32_t k = threadIdx.x; k < (uint32_t)RJ; k += HB) {  // (padding: after every row)
+      for (uint32_t k = threadIdx.x; k < (uint32_t)GJ; k += HB) {  // (padding: a ts after every row's)
         const bool in = k < n;
-        tk[k] = in ? E[k].w1 : ~0ull;
-        tk2[k] = in ? E[k].w2 : ~0ull;
+        const uint64_t w1 = in ? E[k].w1 : ~0ull;
+        tts[k] = (uint32_t)(w1 >> 32);
+        tfa[k] = (uint32_t)w1;
+        tfb[k] = in ? E[k].w2 : ~0ull;
         tc[k] = in ? E[k].cnt : 0u;
         tu[k] = in ? E[k].anc : 0u;
         tr[k] = in ? E[k].rec : 0u;
       }
     } else {
       const X1Ent *E = x1ent(M.x1_recv, q) + j0;
-      for (uint32_t k = threadIdx.x; k < (uint32_t)RJ; k += HB) {  // (padding: a key after every row's)
-        tk[k] = k < n ? E[k].key : ~0ull;
+      for (uint32_t k = threadIdx.x; k < (uint32_t)GJ; k += HB) {
+        const uint64_t key = k < n ? E[k].key : ~0ull;
+        tts[k] = (uint32_t)(key >> 32);
+        tfa[k] = (uint32_t)key;
         tc[k] = k < n ? E[k].cnt : 0u;
       }
     }
     __syncthreads();
-    const uint32_t i = ti * HB + threadIdx.x;
     if (i < NR) {
-      const bool lrow = WIDE && i >= W;
-      uint64_t x, x2 = 0;
-      uint32_t xu = 0, xrec = 0;
-      if (lrow) {
-        const X1Loc e = x1loc(M.x1_send, 0)[i - W];
-        x = e.w1, x2 = e.w2, xu = e.anc, xrec = e.rec;
-      } else {
-        x = M.wkey[i];
-      }
-      const uint64_t lo = x & 0xffffffff00000000ull, hi = lo + (1ull << 32);
-      uint32_t gr = 0, cp = 0, ip = 0, ipf = 0, lp = 0;
+      // per column: earlier ts -> before (and in ipf); equal ts -> the fine key: gen-0 x gen-0 by uid, a gen-0
+      // record before a local one, local x local by the order words (their ties after the loop)
+      auto acc = [&](uint32_t y, bool bef, bool lt, bool le) {
+        const uint32_t c = tc[y];
+        const uint32_t nc = c & 0xffffu, ni = c >> 16;
+        gr += bef;
+        lp += le;
+        cp += bef ? nc : 0u;
+        ip += bef ? ni : 0u;
+        ipf += lt ? ni : 0u;
+      };
       if (!ltile && !lrow) {
-        // (a fixed trip count, unrolled: the LDS loads pipeline instead of waiting one by one)
 #pragma unroll 16
-        for (uint32_t y = 0; y < (uint32_t)RJ; y++) {
-          const uint64_t k = tk[y];
-          const uint32_t c = tc[y];
-          const uint32_t nc = c & 0xffffu, ni = c >> 16;
-          const bool lt = k < x, blo = k < lo;
-          gr += lt;
-          cp += lt ? nc : 0u;
-          ip += lt ? ni : 0u;
-          ipf += blo ? ni : 0u;
-          lp += k < hi;
+        for (uint32_t y = 0; y < (uint32_t)GJ; y++) {
+          const uint32_t ty = tts[y];
+          const bool lt = ty < tx, eq = ty == tx;
+          acc(y, lt | (eq & (tfa[y] < fax)), lt, lt | eq);
         }
-      } else if (!lrow || !ltile) {  // gen-0 x local: by ts only (at equal ts the gen-0 record first)
-        // a column before the row: local column of a smaller ts (gen-0 row) / gen-0 column of ts <= (local row)
-        const uint64_t cut = lrow ? hi : lo;
+      } else if (!lrow) {  // gen-0 row, local columns: before iff an earlier ts
 #pragma unroll 16
-        for (uint32_t y = 0; y < (uint32_t)RJ; y++) {
-          const uint64_t k = tk[y] & 0xffffffff00000000ull;  // (the column's ts; padding: ~0)
-          const uint32_t c = tc[y];
-          const uint32_t nc = c & 0xffffu, ni = c >> 16;
-          const bool lt = k < cut, blo = k < lo;
-          gr += lt;
-          cp += lt ? nc : 0u;
-          ip += lt ? ni : 0u;
-          ipf += blo ? ni : 0u;
-          lp += k < hi;
+        for (uint32_t y = 0; y < (uint32_t)GJ; y++) {
+          const uint32_t ty = tts[y];
+          const bool lt = ty < tx;
+          acc(y, lt, lt, ty <= tx);
         }
-      } else {  // local x local: the order words
+      } else if (!ltile) {  // local row, gen-0 columns: before iff ts <= the row's
+#pragma unroll 16
+        for (uint32_t y = 0; y < (uint32_t)GJ; y++) {
+          const uint32_t ty = tts[y];
+          const bool le = ty <= tx;
+          acc(y, le, ty < tx, le);
+        }
+      } else {  // local x local
         const int self = (q == M.rank && i - W >= j0 && i - W < j0 + n) ? (int)(i - W - j0) : -1;
         bool tie = false;
 #pragma unroll 8
-        for (uint32_t y = 0; y < (uint32_t)RJ; y++) {
-          const uint64_t w1 = tk[y], w2 = tk2[y];
-          const uint32_t c = tc[y];
-          const uint32_t nc = c & 0xffffu, ni = c >> 16;
-          const bool eq = w1 == x;
-          const bool lt = (w1 < x) | (eq & (w2 < x2));
-          const uint64_t k = w1 & 0xffffffff00000000ull;
-          const bool blo = k < lo;
-          tie |= eq & (w2 == x2) & ((int)y != self);
-          gr += lt;
-          cp += lt ? nc : 0u;
-          ip += lt ? ni : 0u;
-          ipf += blo ? ni : 0u;
-          lp += k < hi;
+        for (uint32_t y = 0; y < (uint32_t)GJ; y++) {
+          const uint32_t ty = tts[y];
+          const bool lt = ty < tx, eq = ty == tx;
+          const uint32_t fa = tfa[y];
+          const uint64_t fb = tfb[y];
+          const bool ea = eq & (fa == fax);
+          tie |= ea & (fb == fbx) & ((int)y != self);
+          acc(y, lt | (eq & (fa < fax)) | (ea & (fb < fbx)), lt, lt | eq);
         }
         if (tie) {  // (rare: equal words — a clamped ancestor uid, or one ancestor's chains)
           for (uint32_t y = 0; y < n; y++) {
-            if (tk[y] != x || tk2[y] != x2 || (int)y == self) continue;
+            if (tts[y] != tx || tfa[y] != fax || tfb[y] != fbx || (int)y == self) continue;
             bool lt;
             if (tu[y] != xu) {
               lt = tu[y] < xu;
@@ -1506,16 +1525,19 @@ __global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
           }
         }
       }
-      // two packed 64-bit accumulators instead of five words: (rank, group end, inline prefix: each at
-      // most MAXR x NACC < 2^21) and (child prefix < 2^32, the group's inline prefix)
-      unsigned long long *A = reinterpret_cast<unsigned long long *>(M.gacc);
-      const uint32_t row = lrow ? (uint32_t)WCAP + (i - W) : i;
-      const uint64_t w0 = (uint64_t)gr | ((uint64_t)lp << 21) | ((uint64_t)ip << 42);
-      const uint64_t w1 = (uint64_t)cp | ((uint64_t)ipf << 32);
-      if (w0) atomicAdd(&A[row], (unsigned long long)w0);
-      if (w1) atomicAdd(&A[NACC + row], (unsigned long long)w1);
     }
     __syncthreads();
+   }
+   if (i < NR) {
+     // two packed 64-bit accumulators instead of five words: (rank, group end, inline prefix: each at
+     // most MAXR x NACC < 2^21) and (child prefix < 2^32, the group's inline prefix)
+     unsigned long long *A = reinterpret_cast<unsigned long long *>(M.gacc);
+     const uint32_t row = lrow ? (uint32_t)WCAP + (i - W) : i;
+     const uint64_t w0 = (uint64_t)gr | ((uint64_t)lp << 21) | ((uint64_t)ip << 42);
+     const uint64_t w1 = (uint64_t)cp | ((uint64_t)ipf << 32);
+     if (w0) atomicAdd(&A[row], (unsigned long long)w0);
+     if (w1) atomicAdd(&A[NACC + row], (unsigned long long)w1);
+   }
   }
 }
 
@@ -2005,7 +2027,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   // schedules): the window must then end at the delivering Receive's time, so that the DoForwardUp is
   // the next window's first event at that time.
   if (has_echo) M.lookahead[K_RECEIVE] = 0;
-  // Wide windows (single engine, nsgpu_p2p_win.h): an event on another node is at least one transmission
+  // Wide windows (nsgpu_p2p_win.h): an event on another node is at least one transmission
   // plus its channel delay away — Lx = min over devices of (smallest frame's tx time + delay) — and a
   // same-node TransmitComplete before the window's end runs inside the window (a local record), so only
   // the children that are neither bound the window: lookw = lookahead with tx_min replaced by Lx.
@@ -3236,7 +3258,8 @@ extern "C" int nsgpu_p2p_profile(nsgpu_p2p *h, void *stream, uint32_t sample_eve
   return rc;
 }
 
-// Whether the engine runs wide windows (single engine, node degree <= LQ, not NSGPU_P2P_NARROW=1).
+// Whether the engine runs wide windows (node degree <= LQ, not NSGPU_P2P_NARROW=1; a traced partitioned engine
+// runs narrow ones).
 extern "C" int nsgpu_p2p_get_wide(nsgpu_p2p *h, int *wide) {
   if (!h || !wide) return set_error(NSGPU_EINVAL, "nsgpu_p2p_get_wide: null");
   *wide = h->M.wide ? 1 : 0;
