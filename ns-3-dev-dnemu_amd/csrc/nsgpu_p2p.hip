@@ -1364,10 +1364,11 @@ __global__ __launch_bounds__(TB) void k_drun_first(const P2PDev M) {
 #define GT_CT 1  // column tiles of one k_gtile work item (more: fewer atomics, but the compares bound it)
 #endif
 #ifndef GT_GJ
-#define GT_GJ 128  // columns of one k_gtile tile (smaller tiles: more waves a SIMD to interleave)
+#define GT_GJ 64  // columns of one k_gtile tile (smaller tiles, more waves a SIMD to interleave: 256 -> 64 columns
+                   // took a wide window's k_gtile from 25 to 17 us)
 #endif
 constexpr int GJ = GT_GJ;
-constexpr int GTB = 4096;  // blocks of k_gtile (grid-stride over tiles: a wide window's ~1,400 tiles in one round, several waves a SIMD)
+constexpr int GTB = 8192;  // blocks of k_gtile (grid-stride over tiles: a wide window's ~5,600 tiles in one round)
 // Rows: this rank's window records — its W gen-0 slots, then (WIDE) its L local records in X1Loc order; columns:
 // every rank's, in column tiles of RJ (a rank's gen-0 tiles, then its local tiles).  Per row, over the merged
 // window: the records before it (its global rank), those of a smaller ts, those of ts <= its own (its same-ts
