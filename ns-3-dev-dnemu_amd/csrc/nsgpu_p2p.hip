@@ -2711,7 +2711,10 @@ static void dist_pa(const P2PDev &M, hipStream_t s) {
   else hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL), dim3(TB), 0, s, M);
 }
 static void dist_handle(const P2PDev &M, hipStream_t s) {
-  if (M.wide) hipLaunchKernelGGL(k2_handle<true>, dim3(K2_GRID_W), dim3(HB), 0, s, M);
+  if (M.wide) {
+    hipLaunchKernelGGL((k2_handle<true, true>), dim3(K2_GRID_W), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k_xlcompact, dim3(NLR), dim3(HB), 0, s, M);
+  }
   else hipLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, M);
 }
 static void dist_rank_fin(const P2PDev &M, hipStream_t s) {

@@ -1869,7 +1869,39 @@ __device__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool ha
 }
 
 // WIDE: the single engine's wide windows (local records: k2_rank places them after the handlers).
-template <bool WIDE>
+// Partitioned wide windows, after k2_handle: region bx's local records (its count in lcnt) into this rank's X1Loc
+// list, compacted with one allocation per region.  (Inside k2_handle this code made the kernel spill 1.3 KB of
+// scratch a lane: 20 instead of ~11 us.)
+__global__ __launch_bounds__(HB) void k_xlcompact(const P2PDev M) {
+  const Ctl &C = *M.C;
+  const uint32_t hdl = C.hdl, cnt = M.lcnt[blockIdx.x];
+  const uint64_t lim = C.lim_rel;
+  if (!hdl || !lim || !cnt) return;  // (uniform over the block)
+  __shared__ uint32_t s_lb;
+  if (threadIdx.x == 0) s_lb = atomicAdd(&x1hdr(M.x1_send, 0)->L, cnt);
+  __syncthreads();
+  const uint32_t lb = s_lb, rb = region_base(blockIdx.x);
+  X1Loc *xl = x1loc(M.x1_send, 0);
+  uint64_t lts = 0;  // (the largest rel ts: the window's last dispatch time may be a local record's)
+  for (uint32_t k = threadIdx.x; k < cnt; k += HB) {
+    const uint32_t rec = rb + k;
+    if (lb + k >= (uint32_t)XLCAP) {
+      atomicOr(M.error, 64u);
+      continue;
+    }
+    const ulonglong2 w = M.lkw[rec - LBASE];
+    xl[lb + k] = X1Loc{w.x, w.y, M.nchild[rec] | (M.ninl[rec] << 16), rec, M.lkey[rec - LBASE].uid, 0u};
+    M.lxk[rec - LBASE] = lb + k;
+    const uint64_t t = w.x & 0xffffffff00000000ull;
+    lts = t > lts ? t : lts;
+  }
+  lts = wave_max64(lts);
+  if (threadIdx.x == 0 && lts) atomicMax((unsigned long long *)&x1hdr(M.x1_send, 0)->lastkey, (unsigned long long)lts);
+}
+
+// XL: the partitioned wide engine's variant (k_gtile's accumulators zeroed; every region count written, for
+// k_xlcompact): a separate instantiation, so that the single engine's kernel has none of that code.
+template <bool WIDE, bool XL = false>
 __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   __shared__ uint64_t lds64[(WIDE ? K2_LDS_WORDS_W : K2_LDS_WORDS) / 2];
   uint32_t *lds = reinterpret_cast<uint32_t *>(lds64);
@@ -1956,7 +1988,7 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
         hub_node<WIDE>(M, C, M.hub_list[h], W, base, run || c_drun != 0, R, hb, lds, hc, &s_lcnt);
     }
   } else if (bx < (uint32_t)K2_GRID_W) {
-    if (WIDE && M.dist) {  // k_gtile's accumulators for this window (k_dfin2 read the last window's: local
+    if constexpr (XL) {  // k_gtile's accumulators for this window (k_dfin2 read the last window's: local
       uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);  // records' uids take their parents' child prefixes)
       for (uint32_t i = (bx - (NHB + NHUB)) * HB + threadIdx.x; i < 2u * (uint32_t)NACC; i += NMB * HB) A[i] = 0;
     }
@@ -1964,33 +1996,11 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   } else {
     if (!run && handle && !M.dist) rank_tile(M, C, bx - K2_GRID_W, wrank_of(M, c_wn));  // (keys known before the handlers run)
   }
-  if (WIDE && hc.lim && bx < (uint32_t)NLR) {  // this block's local region count (k2_rank / k2_scan read it;
-    __syncthreads();                               //  written even when 0: the deferred pipeline keeps no reset)
-    const uint32_t cap = bx < (uint32_t)NHB ? (uint32_t)LR : (uint32_t)LRH;
+  if (WIDE && (hc.lim || XL) && bx < (uint32_t)NLR) {  // this block's local region count (k2_rank / k2_scan /
+    __syncthreads();                                       //  k_xlcompact read it; written even when 0: the
+    const uint32_t cap = bx < (uint32_t)NHB ? (uint32_t)LR : (uint32_t)LRH;  // deferred pipeline keeps no reset)
     const uint32_t cnt = s_lcnt < cap ? s_lcnt : cap;
     if (threadIdx.x == 0) M.lcnt[bx] = cnt;
-    if (M.dist && cnt) {  // partitioned: the region's records (run by this block's holders) into this rank's
-      __shared__ uint32_t s_lb;  // X1Loc list, compacted: one allocation per block
-      if (threadIdx.x == 0) s_lb = atomicAdd(&x1hdr(M.x1_send, 0)->L, cnt);
-      __syncthreads();
-      const uint32_t lb = s_lb, rb = region_base(bx);
-      X1Loc *xl = x1loc(M.x1_send, 0);
-      uint64_t lts = 0;  // (the largest rel ts: the window's last dispatch time may be a local record's)
-      for (uint32_t k = threadIdx.x; k < cnt; k += HB) {
-        const uint32_t rec = rb + k;
-        if (lb + k >= (uint32_t)XLCAP) {
-          atomicOr(M.error, 64u);
-          continue;
-        }
-        const ulonglong2 w = M.lkw[rec - LBASE];
-        xl[lb + k] = X1Loc{w.x, w.y, M.nchild[rec] | (M.ninl[rec] << 16), rec, M.lkey[rec - LBASE].uid, 0u};
-        M.lxk[rec - LBASE] = lb + k;
-        const uint64_t t = w.x & 0xffffffff00000000ull;
-        lts = t > lts ? t : lts;
-      }
-      lts = wave_max64(lts);
-      if (threadIdx.x == 0 && lts) atomicMax((unsigned long long *)&x1hdr(M.x1_send, 0)->lastkey, (unsigned long long)lts);
-    }
   }
   PH_MARK(9);
   BLK_REC(1, c_win);
