@@ -18,7 +18,10 @@ nsgpu.check(nsgpu.lib().nsgpu_p2p_phase_read(buf.ctypes.data, 64, 1))
 grp.run()
 nsgpu.check(nsgpu.lib().nsgpu_p2p_phase_read(buf.ctypes.data, buf.size, 0))
 blk = buf[64:].reshape(3, BLK, 2).astype(np.int64)
-roles = {0: [("slot", 0, 16), ("remote", 16, 32), ("pool", 32, 256)], 1: [("all", 0, 2048)]}
+wide = grp.members[0].wide()
+nslot = (4096 + 4096) // 256 if wide else 16  # (wide: gen-0 slots, then the local records' dense list)
+roles = {0: [("slot", 0, 16), ("lslot", 16, nslot), ("remote", nslot, nslot + 1), ("pool", nslot + 1, 256)],
+         1: [("holder", 0, 64), ("hub", 64, 96), ("maint", 96, 224)]}
 for k, name in ((0, "k2_pa<DIST>"), (1, "k2_handle")):
     b = blk[k]
     ok = b[:, 1] > 0
