@@ -533,6 +533,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   if (threadIdx.x < 2 * K_NKINDS) s_look[threadIdx.x] = look_mine;
   __syncthreads();
   if (slot_block) BLK_MARK(32, c_win);  // snapshot + slot loads issued (waits at first use)
+  if (!slot_block && !remote_role) BLK_MARK(52, c_win);  // (pool blocks: the run control, the barrier)
   const bool run = c_mode == MODE_RUN;
   const bool partition = c_done == 0;
   Red &R = DIST ? x1hdr(M.x1_send, 0)->red : C.red[rt];
@@ -572,6 +573,13 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     C.hcap = hcap;
   }
   const uint32_t pW = c_pvalid ? c_pW : 0;
+#ifdef NSGPU_PHASE_PROF
+  if (c_win == g_blk_win && blockIdx.x == 0 && threadIdx.x == 0) {  // (diagnostic: the window's inputs)
+    g_phase[46] = c_P;
+    g_phase[47] = pW;
+    g_phase[48] = c_plt;
+  }
+#endif
   PH_MARK(0);
   uint64_t tmn = ~0ull, wnd = ~0ull, wndw = ~0ull, digest = 0;
   uint32_t xw_uid0 = xw_u[0];  // (window c_wn - 2's uid base: its provisional uids resolve in this kernel)
@@ -775,6 +783,12 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       uint32_t w0;
       uint64_t f0;
       block_alloc2<TB>(C, cw, 0u, w0, f0);
+#ifdef NSGPU_PHASE_PROF
+      if (c_win == g_blk_win) {  // (diagnostic: pool entries taken, pool chunks swept)
+        if (cw) atomicAdd((unsigned long long *)&g_phase[49], (unsigned long long)cw);
+        if (threadIdx.x == 0) atomicAdd((unsigned long long *)&g_phase[50], 1ull);
+      }
+#endif
 #pragma unroll
       for (int q = 0; q < PPT; q++) {
         const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
@@ -802,6 +816,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   }
   PH_MARK(1);
   if (slot_block) BLK_MARK(42, c_win);
+  if (!slot_block && !remote_role) BLK_MARK(54, c_win);  // (pool blocks: the sweep)
   if (drun && g == 0) {  // the pending set of the run's start and the run's entries (k_drun_start, k_drun_red)
     const uint64_t a = C.drn_tmin, w = C.drn_wend, st = C.drn_stopts;
     tmn = a < tmn ? a : tmn;
@@ -832,6 +847,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   for (int q = 0; q < NPEND; q++) node_table_finish(M, C, pend[q]);
   PH_MARK(2);
   if (slot_block) BLK_MARK(44, c_win);  // publish_min, digest
+  if (!slot_block && !remote_role) BLK_MARK(62, c_win);  // (pool blocks: publish_min, digest)
   BLK_REC(0, c_win);
 }
 

@@ -46,3 +46,9 @@ print("k2_pa slot blocks, mean per block (sampled window):")
 for i, nm in marks.items():
     c = max(int(ph[i + 1]), 1)
     print(f"  {nm:40s} {ph[i] * 0.01 / c:6.2f} us  (n={int(ph[i + 1])})")
+print(f"k2_pa inputs (sampled window): pool end {int(buf[46])}, last window gen-0 {int(buf[47])}, local {int(buf[48])}; "
+      f"pool entries taken {int(buf[49])}, pool chunks swept {int(buf[50])}")
+print("k2_pa pool blocks, mean per block (sampled window):")
+for i, nm in ((52, "run control + barrier"), (54, "pool sweep"), (62, "publish_min + digest")):
+    c = max(int(buf[i + 1]), 1)
+    print(f"  {nm:40s} {buf[i] * 0.01 / c:6.2f} us  (n={int(buf[i + 1])})")
