@@ -573,6 +573,13 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     C.hcap = hcap;
   }
   const uint32_t pW = c_pvalid ? c_pW : 0;
+  constexpr int PPT = 4;  // (pool entries a thread reads a chunk)
+  {  // a pool block past the pool's end (most of them: the pool holds a few thousand entries) has nothing to do
+    const uint64_t pb = blockIdx.x - (uint64_t)(NSGB + rrb);
+    if (!slot_block && !remote_role && partition && !run && !drun && !(DIST && dtrim && pb < (uint64_t)(WCAP / TB)) &&
+        pb * TB * PPT >= c_P)
+      return;
+  }
 #ifdef NSGPU_PHASE_PROF
   if (c_win == g_blk_win && blockIdx.x == 0 && threadIdx.x == 0) {  // (diagnostic: the window's inputs)
     g_phase[46] = c_P;
@@ -714,8 +721,7 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   } else if (partition && !run) {
     // ---- the pool, in place: read (ts, uid, kind) of every slot; window events are copied out.
     // Chunks of PPT x TB entries per block (loads of a chunk all in flight), one allocation per chunk;
-    // blocks past the pool's end do nothing (no atomics).
-    constexpr int PPT = 4;
+    // blocks past the pool's end returned above.
     const uint64_t P = c_P;
     const uint64_t pb = blockIdx.x - (uint64_t)(NSGB + rrb), npb = gridDim.x - (uint64_t)(NSGB + rrb);
     static_assert(PPT <= NPEND, "pending claims");
