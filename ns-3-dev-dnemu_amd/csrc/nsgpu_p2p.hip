@@ -1583,6 +1583,34 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     hrrem = lh->rrem;
     hrhead = lh->rhead;
   }
+  // the record's accumulators, record and first children, all loaded before anything waits — with the headers,
+  // before the arrival's wait (WIDE: thread WCAP + k takes local record k of this rank, its record index from
+  // the X1Loc list: one more trip; its parent's child prefix needs the parent's accumulator, one more)
+  const uint32_t ti = blockIdx.x * HB + threadIdx.x;
+  const bool loc = WIDE && ti >= (uint32_t)WCAP;
+  uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);
+  uint64_t w0, w1, wk;
+  uint32_t s = ti, wc, ncr, ckw[PFC], cctx[PFC], wpar = 0;
+  {  // (speculative: every thread loads, whether or not its record exists — the indices stay in range)
+    uint64_t lw1 = 0;
+    if (loc) {
+      const X1Loc e = x1loc(M.x1_send, 0)[ti - WCAP];
+      s = e.rec < (uint32_t)WTOT ? e.rec : (uint32_t)WTOT - 1u;
+      lw1 = e.w1;
+      wpar = M.wpar[s];
+    }
+    w0 = A[ti];
+    w1 = A[NACC + ti];
+    wk = loc ? lw1 : M.wkey[s];
+    wc = M.wctx[s];
+    ncr = M.nchild[s];
+#pragma unroll
+    for (int j = 0; j < PFC; j++) {  // (a child index past maxc loads the slot's last one: in range, ignored)
+      const uint32_t sl = s * M.maxc + min((uint32_t)j, M.maxc - 1u);
+      ckw[j] = M.ch_kind[sl];
+      cctx[j] = M.ch_ctx[sl];
+    }
+  }
   // X1 is all-gathered in place (x1_send is this rank's slot of x1_recv): the last block to have read the
   // headers resets this rank's for the next window — every block's header loads have returned before it
   // arrives (one wave per block: the wave's wait covers every lane)
@@ -1600,36 +1628,8 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     hs->rkey = ~0ull;
     hs->rrem = 0;
   }
-  // the record's accumulators, record and first children, all loaded before anything waits (WIDE: thread
-  // WCAP + k takes local record k of this rank, its record index from the X1Loc list; its parent's child prefix
-  // needs the parent's accumulator, one more trip)
-  const uint32_t ti = blockIdx.x * HB + threadIdx.x;
-  const bool loc = WIDE && ti >= (uint32_t)WCAP;
   const uint32_t Lown = WIDE ? __shfl(l_q, (int)M.rank) : 0u;
   const bool vs = loc ? ti - (uint32_t)WCAP < Lown : ti < W;
-  uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);
-  uint64_t w0 = 0, w1 = 0, wk = 0;
-  uint32_t s = ti, wc = 0, ncr = 0, ckw[PFC], cctx[PFC], wpar = 0;
-  if (vs) {
-    uint64_t lw1 = 0;
-    if (loc) {
-      const X1Loc e = x1loc(M.x1_send, 0)[ti - WCAP];
-      s = e.rec;
-      lw1 = e.w1;
-      wpar = M.wpar[s];
-    }
-    w0 = A[ti];
-    w1 = A[NACC + ti];
-    wk = loc ? lw1 : M.wkey[s];
-    wc = M.wctx[s];
-    ncr = M.nchild[s];
-#pragma unroll
-    for (int j = 0; j < PFC; j++)
-      if ((uint32_t)j < M.maxc) {
-        ckw[j] = M.ch_kind[s * M.maxc + j];
-        cctx[j] = M.ch_ctx[s * M.maxc + j];
-      }
-  }
   const uint32_t tinl_g = wave_sum32(tinl_q);
   if (vs) {
     if (!WIDE) {  // (wide: k2_handle zeroes them — a local record reads its parent's below)
@@ -1694,8 +1694,21 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     rg.stopuid = __shfl(hsuid, first);
   }
   // (the free-stack move and the hubs' slot tables last: a moving lane waits for its loads)
-  auto stack_and_hubs = [&]() {
-    for (uint64_t i = threadIdx.x; i < mv; i += HB) M.fstack[nfree - consumed + i] = M.fstack[nfree + npush - mv + i];
+  auto stack_and_hubs = [&]() {  // (the two ranges are disjoint: eight loads in flight a lane, then the stores)
+    constexpr int SB = 8;
+    for (uint64_t i0 = threadIdx.x; i0 < mv; i0 += (uint64_t)HB * SB) {
+      uint32_t v[SB];
+#pragma unroll
+      for (int k = 0; k < SB; k++) {
+        const uint64_t i = i0 + (uint64_t)k * HB;
+        v[k] = i < mv ? M.fstack[nfree + npush - mv + i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < SB; k++) {
+        const uint64_t i = i0 + (uint64_t)k * HB;
+        if (i < mv) M.fstack[nfree - consumed + i] = v[k];
+      }
+    }
     for (uint32_t h = threadIdx.x; h < nh; h += HB) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
   };
   if (threadIdx.x != 0) {
