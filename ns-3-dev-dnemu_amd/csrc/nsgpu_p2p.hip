@@ -1376,7 +1376,7 @@ constexpr int GTB = 8192;  // blocks of k_gtile (grid-stride over tiles: a wide 
 // dispatch prefixes).  A gen-0 record precedes a local one of equal ts; two local records compare by their order
 // words, a tie by the ancestor uid, then (same ancestor: same node, this rank) by their exact chains.
 template <bool WIDE>
-__global__ __launch_bounds__(HB) void k_gtile(const P2PDev M) {
+__global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves a SIMD: 73 VGPRs; 8 spilled)
   Ctl &C = *M.C;
   if (!C.hdl) return;  // (k2_handle ran nothing: a cut, a pause, the end)
   // a column tile in LDS: its rel ts (the common test), child counts, and the fine key an equal ts needs — a
