@@ -990,6 +990,10 @@ __device__ uint64_t g_blk_win = 1000;
       btm_ = t_;                                                                                 \
     }                                                                                            \
   } while (0)
+// k_gtile's per-block stamps in the sampled window: g_gt[block] = {start, prologue done, first tile in LDS,
+// first tile compared, end (after its atomics returned)}
+constexpr int GT_BLK_MAX = 8192;
+__device__ uint64_t g_gt[GT_BLK_MAX][8];
 #define BLK_REC(k, win)                                                                          \
   do {                                                                                           \
     if (threadIdx.x == 0 && (win) == g_blk_win && blockIdx.x < (uint32_t)BLK_MAX) {              \
@@ -1368,7 +1372,11 @@ __global__ __launch_bounds__(TB) void k_drun_first(const P2PDev M) {
                    // took a wide window's k_gtile from 25 to 17 us)
 #endif
 constexpr int GJ = GT_GJ;
-constexpr int GTB = 8192;  // blocks of k_gtile (grid-stride over tiles: a wide window's ~5,600 tiles in one round)
+static_assert(GJ <= 64, "k_gtile's packed column counts (7-bit count field)");
+#ifndef GT_GTB
+#define GT_GTB 8192
+#endif
+constexpr int GTB = GT_GTB;  // blocks of k_gtile (grid-stride over tiles: a wide window's ~5,600 tiles in one round)
 // Rows: this rank's window records — its W gen-0 slots, then (WIDE) its L local records in X1Loc order; columns:
 // every rank's, in column tiles of RJ (a rank's gen-0 tiles, then its local tiles).  Per row, over the merged
 // window: the records before it (its global rank), those of a smaller ts, those of ts <= its own (its same-ts
@@ -1378,20 +1386,37 @@ constexpr int GTB = 8192;  // blocks of k_gtile (grid-stride over tiles: a wide 
 template <bool WIDE>
 __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves a SIMD: 73 VGPRs; 8 spilled)
   Ctl &C = *M.C;
-  if (!C.hdl) return;  // (k2_handle ran nothing: a cut, a pause, the end)
+  // the run control and every rank's window size in one trip (the sizes loaded before the test: a load after a
+  // branch on C.hdl waited for it)
+  const uint32_t hdl = C.hdl, W = C.pW;
+  const uint32_t q = threadIdx.x;
+  const X1Hdr *hq = x1hdr(M.x1_recv, q < M.nranks ? q : 0u);
+  const uint32_t wq0 = hq->W, lq0 = WIDE ? hq->L : 0u;
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t gt_t0 = __builtin_amdgcn_s_memrealtime();
+  const bool gt_rec = C.windows == g_blk_win && blockIdx.x < (uint32_t)GT_BLK_MAX;
+  uint64_t gt_t[4] = {0, 0, 0, 0}, gt_kind = 0;
+#define GT_MARK(k)                                                       \
+  do {                                                                   \
+    if (gt_rec && !gt_t[k]) gt_t[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define GT_MARK(k) (void)0
+#endif
+  if (!hdl) return;  // (k2_handle ran nothing: a cut, a pause, the end)
   // a column tile in LDS: its rel ts (the common test), child counts, and the fine key an equal ts needs — a
   // gen-0 record's uid; a local record's order words' low part and second word (ties: ancestor uid, record)
-  __shared__ uint32_t tts[GJ], tc[GJ], tfa[GJ];
-  __shared__ uint64_t tfb[WIDE ? GJ : 1];
+  // a column's child counts packed for the row's before-sum (tpb: 1 | children << 7 | inline children << 29 — over
+  // one tile of GJ <= 64 columns the three fields stay within 7, 22 and 22 bits) and its inline children alone
+  // (read four columns at a time as 16-B vectors)
+  __shared__ __align__(16) uint32_t tts[GJ], tni[GJ], tfa[GJ];
+  __shared__ __align__(16) uint64_t tpb[GJ], tfb[WIDE ? GJ : 2];
   __shared__ uint32_t tu[WIDE ? GJ : 1], tr[WIDE ? GJ : 1];
   __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR], s_l[MAXR], s_g[MAXR];
-  const uint32_t W = C.pW;
   uint32_t L = 0;
   {  // every rank's window size at once, one lane per rank (HB = one wave), and the column tiles' prefix
-    const uint32_t q = threadIdx.x;
-    const X1Hdr *hq = x1hdr(M.x1_recv, q < M.nranks ? q : 0u);
-    const uint32_t wq = q < M.nranks ? hq->W : 0u;
-    const uint32_t lq = (WIDE && q < M.nranks) ? hq->L : 0u;
+    const uint32_t wq = q < M.nranks ? wq0 : 0u;
+    const uint32_t lq = (WIDE && q < M.nranks) ? lq0 : 0u;
     const uint32_t ng = (wq + GJ - 1) / GJ, nt = ng + (lq + GJ - 1) / GJ;
     uint32_t inc = nt;
     for (int o = 1; o < 64; o <<= 1) {
@@ -1408,13 +1433,17 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
     if (WIDE) L = __shfl(lq, (int)M.rank);
   }
   __syncthreads();
+  GT_MARK(0);
   const uint32_t njt = s_off[M.nranks], NR = W + L;
   // a work item: one row tile against GT_CT consecutive column tiles, summed in registers (one pair of atomics per
   // row and item: the accumulators' atomics, not the compares, bound the kernel)
   const uint32_t nseg = (njt + GT_CT - 1) / GT_CT;
-  const uint64_t T = (uint64_t)((NR + HB - 1) / HB) * nseg;
+  const uint32_t nrt = (NR + HB - 1) / HB;
+  const uint64_t T = (uint64_t)nrt * nseg;
   for (uint64_t t = blockIdx.x; t < T; t += gridDim.x) {  // (uniform over the block)
-   const uint32_t ti = (uint32_t)(t / nseg), sg = (uint32_t)(t % nseg);
+   // the local rows' tiles first (the last row tiles): their loads and compares take about twice a gen-0
+   // tile's, and the blocks dispatched first start first
+   const uint32_t ti = nrt - 1u - (uint32_t)(t / nseg), sg = (uint32_t)(t % nseg);
    const uint32_t i = ti * HB + threadIdx.x;
    const bool lrow = WIDE && i >= W;
    uint32_t tx = 0, fax = 0, xu = 0, xrec = 0;
@@ -1445,7 +1474,9 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
         tts[k] = (uint32_t)(w1 >> 32);
         tfa[k] = (uint32_t)w1;
         tfb[k] = in ? E[k].w2 : ~0ull;
-        tc[k] = in ? E[k].cnt : 0u;
+        const uint32_t c = in ? E[k].cnt : 0u;
+        tpb[k] = 1ull | (uint64_t)(c & 0xffffu) << 7 | (uint64_t)(c >> 16) << 29;
+        tni[k] = c >> 16;
         tu[k] = in ? E[k].anc : 0u;
         tr[k] = in ? E[k].rec : 0u;
       }
@@ -1455,56 +1486,100 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
         const uint64_t key = k < n ? E[k].key : ~0ull;
         tts[k] = (uint32_t)(key >> 32);
         tfa[k] = (uint32_t)key;
-        tc[k] = k < n ? E[k].cnt : 0u;
+        const uint32_t c = k < n ? E[k].cnt : 0u;
+        tpb[k] = 1ull | (uint64_t)(c & 0xffffu) << 7 | (uint64_t)(c >> 16) << 29;
+        tni[k] = c >> 16;
       }
     }
     __syncthreads();
+    GT_MARK(1);
+#ifdef NSGPU_PHASE_PROF
+    gt_kind |= (ltile ? 1u : 0u) | (__any(lrow) ? 2u : 0u) | (__any(i < NR) ? 8u : 0u);
+#endif
     if (i < NR) {
       // per column: earlier ts -> before (and in ipf); equal ts -> the fine key: gen-0 x gen-0 by uid, a gen-0
       // record before a local one, local x local by the order words (their ties after the loop)
-      auto acc = [&](uint32_t y, bool bef, bool lt, bool le) {
-        const uint32_t c = tc[y];
-        const uint32_t nc = c & 0xffffu, ni = c >> 16;
-        gr += bef;
+      // (the compares bound the kernel: one 64-bit add of the packed counts a column instead of three selects)
+      uint64_t ab = 0;
+      // columns y0..y0+3: rel ts, inline children, packed counts (and, FA / FB, the fine key's parts)
+      struct Col4 {
+        uint32_t ts[4], ni[4], fa[4];
+        uint64_t pb[4], fb[4];
+      };
+      auto col4 = [&](uint32_t y0, bool FA, bool FB) {
+        Col4 c;
+        const uint4 a = *(const uint4 *)&tts[y0], b = *(const uint4 *)&tni[y0];
+        const ulonglong2 p0 = *(const ulonglong2 *)&tpb[y0], p1 = *(const ulonglong2 *)&tpb[y0 + 2];
+        c.ts[0] = a.x, c.ts[1] = a.y, c.ts[2] = a.z, c.ts[3] = a.w;
+        c.ni[0] = b.x, c.ni[1] = b.y, c.ni[2] = b.z, c.ni[3] = b.w;
+        c.pb[0] = p0.x, c.pb[1] = p0.y, c.pb[2] = p1.x, c.pb[3] = p1.y;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {  // (opaque: else the selects below become a masked load each, and a wait)
+          asm("" : "+v"(c.pb[k]));
+          asm("" : "+v"(c.ni[k]));
+        }
+        if (FA) {
+          const uint4 f = *(const uint4 *)&tfa[y0];
+          c.fa[0] = f.x, c.fa[1] = f.y, c.fa[2] = f.z, c.fa[3] = f.w;
+        }
+        if (FB) {
+          const ulonglong2 f0 = *(const ulonglong2 *)&tfb[y0], f1 = *(const ulonglong2 *)&tfb[y0 + 2];
+          c.fb[0] = f0.x, c.fb[1] = f0.y, c.fb[2] = f1.x, c.fb[3] = f1.y;
+        }
+        return c;
+      };
+      auto acc = [&](const Col4 &c, int k, bool bef, bool lt, bool le) {
+        ab += bef ? c.pb[k] : 0ull;
         lp += le;
-        cp += bef ? nc : 0u;
-        ip += bef ? ni : 0u;
-        ipf += lt ? ni : 0u;
+        ipf += lt ? c.ni[k] : 0u;
       };
       if (!ltile && !lrow) {
-#pragma unroll 16
-        for (uint32_t y = 0; y < (uint32_t)GJ; y++) {
-          const uint32_t ty = tts[y];
-          const bool lt = ty < tx, eq = ty == tx;
-          acc(y, lt | (eq & (tfa[y] < fax)), lt, lt | eq);
+#pragma unroll 4
+        for (uint32_t y0 = 0; y0 < (uint32_t)GJ; y0 += 4) {
+          const Col4 c = col4(y0, true, false);
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const bool lt = c.ts[k] < tx, eq = c.ts[k] == tx;
+            acc(c, k, lt | (eq & (c.fa[k] < fax)), lt, lt | eq);
+          }
         }
       } else if (!lrow) {  // gen-0 row, local columns: before iff an earlier ts
-#pragma unroll 16
-        for (uint32_t y = 0; y < (uint32_t)GJ; y++) {
-          const uint32_t ty = tts[y];
-          const bool lt = ty < tx;
-          acc(y, lt, lt, ty <= tx);
+#pragma unroll 4
+        for (uint32_t y0 = 0; y0 < (uint32_t)GJ; y0 += 4) {
+          const Col4 c = col4(y0, false, false);
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const bool lt = c.ts[k] < tx;
+            acc(c, k, lt, lt, c.ts[k] <= tx);
+          }
         }
       } else if (!ltile) {  // local row, gen-0 columns: before iff ts <= the row's
-#pragma unroll 16
-        for (uint32_t y = 0; y < (uint32_t)GJ; y++) {
-          const uint32_t ty = tts[y];
-          const bool le = ty <= tx;
-          acc(y, le, ty < tx, le);
+#pragma unroll 4
+        for (uint32_t y0 = 0; y0 < (uint32_t)GJ; y0 += 4) {
+          const Col4 c = col4(y0, false, false);
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const bool le = c.ts[k] <= tx;
+            acc(c, k, le, c.ts[k] < tx, le);
+          }
         }
       } else {  // local x local
         const int self = (q == M.rank && i - W >= j0 && i - W < j0 + n) ? (int)(i - W - j0) : -1;
         bool tie = false;
-#pragma unroll 8
-        for (uint32_t y = 0; y < (uint32_t)GJ; y++) {
-          const uint32_t ty = tts[y];
-          const bool lt = ty < tx, eq = ty == tx;
-          const uint32_t fa = tfa[y];
-          const uint64_t fb = tfb[y];
-          const bool ea = eq & (fa == fax);
-          tie |= ea & (fb == fbx) & ((int)y != self);
-          acc(y, lt | (eq & (fa < fax)) | (ea & (fb < fbx)), lt, lt | eq);
+#pragma unroll 2
+        for (uint32_t y0 = 0; y0 < (uint32_t)GJ; y0 += 4) {
+          const Col4 c = col4(y0, true, true);
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const bool lt = c.ts[k] < tx, eq = c.ts[k] == tx;
+            const bool ea = eq & (c.fa[k] == fax);
+            tie |= ea & (c.fb[k] == fbx) & ((int)(y0 + k) != self);
+            acc(c, k, lt | (eq & (c.fa[k] < fax)) | (ea & (c.fb[k] < fbx)), lt, lt | eq);
+          }
         }
+#ifdef NSGPU_PHASE_PROF
+        gt_kind |= __any(tie) ? 4u : 0u;
+#endif
         if (tie) {  // (rare: equal words — a clamped ancestor uid, or one ancestor's chains)
           for (uint32_t y = 0; y < n; y++) {
             if (tts[y] != tx || tfa[y] != fax || tfb[y] != fbx || (int)y == self) continue;
@@ -1517,16 +1592,15 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
               atomicOr(M.error, 64u);
               lt = false;
             }
-            if (lt) {
-              const uint32_t c = tc[y];
-              gr++;
-              cp += c & 0xffffu;
-              ip += c >> 16;
-            }
+            if (lt) ab += tpb[y];
           }
         }
       }
+      gr += (uint32_t)(ab & 0x7fu);
+      cp += (uint32_t)((ab >> 7) & 0x3fffffu);
+      ip += (uint32_t)((ab >> 29) & 0x3fffffu);
     }
+    GT_MARK(2);
     __syncthreads();
    }
    if (i < NR) {
@@ -1540,6 +1614,19 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
      if (w1) atomicAdd(&A[NACC + row], (unsigned long long)w1);
    }
   }
+#ifdef NSGPU_PHASE_PROF
+  __builtin_amdgcn_s_waitcnt(0);
+  if (gt_rec && threadIdx.x == 0) {
+    g_gt[blockIdx.x][0] = gt_t0;
+    for (int k = 0; k < 3; k++) g_gt[blockIdx.x][1 + k] = gt_t[k];
+    g_gt[blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    g_gt[blockIdx.x][5] = xcc;
+    g_gt[blockIdx.x][6] = gt_kind;
+  }
+#endif
+#undef GT_MARK
 }
 
 // Block 0 also does the pool bookkeeping (k2_scan's) and, last, the run bookkeeping; the other blocks
@@ -1548,8 +1635,7 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
 template <bool WIDE>
 __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   Ctl &C = *M.C;
-  if (!C.hdl) return;
-  const uint32_t W = C.pW;
+  const uint32_t hdl = C.hdl, W = C.pW;  // (tested after the loads below: a load after a branch on it waited for it)
   // every rank's X1 header at once, one lane per rank (HB = one wave)
   const uint32_t lq = threadIdx.x;
   const X1Hdr *lh = x1hdr(M.x1_recv, lq < M.nranks ? lq : 0u);
@@ -1611,6 +1697,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
       cctx[j] = M.ch_ctx[sl];
     }
   }
+  if (!hdl) return;  // (k2_handle ran nothing: a cut, a pause, the end)
   // X1 is all-gathered in place (x1_send is this rank's slot of x1_recv): the last block to have read the
   // headers resets this rank's for the next window — every block's header loads have returned before it
   // arrives (one wave per block: the wave's wait covers every lane)
@@ -3107,6 +3194,8 @@ extern "C" int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset) {
   if (n > 64) {  // the rest: the per-block times of the sampled window (g_blk)
     const int nb = std::min(n - 64, 3 * BLK_MAX * 2);
     NSGPU_HIP(hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_blk), nb * sizeof(uint64_t)));
+    const int ng = std::min(n - 64 - 3 * BLK_MAX * 2, GT_BLK_MAX * 8);  // (then k_gtile's stamps)
+    if (ng > 0) NSGPU_HIP(hipMemcpyFromSymbol(out + 64 + 3 * BLK_MAX * 2, HIP_SYMBOL(g_gt), ng * sizeof(uint64_t)));
     n = 64;
   }
   NSGPU_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), n * sizeof(uint64_t)));

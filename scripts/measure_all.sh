@@ -14,6 +14,7 @@
 #   rocprof_grid_part rocprofv3 kernel stats of the partitioned grid line (one rank)
 #   pmc_p2p          config-4 HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes -> traffic_p2p-grid.json
 #   pmc_lines        config-4 L2 / L1 request counters (TCC hit / miss / requests, TCP requests) per kernel
+#   pmc_sq_part      wave-state counters (SQ busy / wait / VALU / LDS) of the partitioned grid's kernels
 #   py:<script>      python scripts/<script> (diagnostics), output to OUT/<script>.log
 set -e
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -72,6 +73,11 @@ for st in "$@"; do
       cd /tmp
       NSGPU_P2P_EAGER=1 step pmc_tcc 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum --output-format csv -d $O/pmc_tcc -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-secondary
       NSGPU_P2P_EAGER=1 step pmc_tcp 200 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d $O/pmc_tcp -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-secondary
+      cd $R ;;
+    pmc_sq_part)  # wave-state counters of the partitioned grid's kernels (one pass: 8 SQ + 1 GRBM counters)
+      cd /tmp
+      rocprofv3 -L > $O/avail_counters.txt 2>&1 || true
+      NSGPU_P2P_EAGER=1 step pmc_sq_part 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq_part -o pmc -- python3 $R/bench.py --partitioned --steps 1 --warmup 0 --no-cpu-baseline
       cd $R ;;
     py:*) s=${st#py:}; step ${s%%.py*} 600 python scripts/${s//,/ } ;;
     *) echo "unknown stage $st"; exit 2 ;;
