@@ -272,7 +272,6 @@ struct P2PDev {
   uint32_t capx, pad_x;         // X2 records per peer per window (the run's largest cut between two ranks)
   uint64_t x2b;                 // X2 bytes per peer
   uint32_t *gacc;               // k_gtile's accumulators: 2 x NACC packed 64-bit words
-  uint32_t *lxk;                // wide partitioned: a local record's compact index in this rank's X1Loc list
   // run control / outputs
   uint32_t n_init;    // initial pending count (pool 0)
   uint32_t uid_init;  // m_uid after setup
@@ -1120,7 +1119,7 @@ struct X1Ent {  // one window event: key and child counts (children | inline chi
 struct X1Loc {
   uint64_t w1, w2;     // lkw: (rel ts, local, parent rel ts), (ancestor uid, child index / ...)
   uint32_t cnt, rec;   // children | inline children << 16; the record on its rank
-  uint32_t anc, pad;   // the gen-0 ancestor's uid
+  uint32_t anc, par;   // the gen-0 ancestor's uid; the parent's accumulator row | child index << 24 (k_dfin2)
 };
 static_assert(sizeof(X1Loc) == 32, "X1Loc");
 constexpr int XLCAP = 4096;  // local records of one rank's window (LMAX)
@@ -1683,7 +1682,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
       const X1Loc e = x1loc(M.x1_send, 0)[ti - WCAP];
       s = e.rec < (uint32_t)WTOT ? e.rec : (uint32_t)WTOT - 1u;
       lw1 = e.w1;
-      wpar = M.wpar[s];
+      wpar = e.par;
     }
     w0 = A[ti];
     w1 = A[NACC + ti];
@@ -1728,9 +1727,8 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     // as k2_scan: (dispatch rank rel. K0, rank of the first inline child, child prefix, inline prefix)
     M.sinfo[s] = make_uint4(gr + (tinl_g ? ipf : 0), lp + ip, cp, ip);
     if (loc) {  // uid = the parent's child prefix + the child index (DefaultSimulatorImpl::Schedule order)
-      const uint32_t p = wpar & 0xffffffu;
-      const uint32_t prow = p < (uint32_t)LBASE ? p : (uint32_t)WCAP + M.lxk[p - LBASE];
-      const uint32_t pcp = (uint32_t)A[NACC + prow];
+      const uint32_t prow = wpar & 0xffffffu;  // (k_xlcompact: the parent's row, gen-0 slot or WCAP + compact index)
+      const uint32_t pcp = (uint32_t)A[NACC + (prow < (uint32_t)NACC ? prow : 0u)];
       M.pwkey[s] = ((wk >> 32) << 32) | (uint32_t)(C.puid0 + pcp + (wpar >> 24));
       M.lrec[ti - WCAP] = s;
     } else {
@@ -2402,7 +2400,6 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.x2_send, M.x2b * nranks));
     TRY(dalloc(h, &M.x2_recv, M.x2b * nranks));
     TRY(dalloc(h, &M.gacc, 4 * (size_t)NACC));
-    TRY(dalloc(h, &M.lxk, LCAP));
     h->comm = comm;
     memset(&h->x1h0, 0, sizeof(X1Hdr));
     h->x1h0.red.tmin = h->x1h0.red.wend = h->x1h0.red.stopts = h->x1h0.red.wendw = ~0ull;

@@ -1901,7 +1901,17 @@ __global__ __launch_bounds__(HB) void k_xlcompact(const P2PDev M) {
   const uint64_t lim = C.lim_rel;
   const uint32_t a0 = M.lcnt[tid], a1 = tid + HB < (uint32_t)NLR ? M.lcnt[tid + HB] : 0u;
   if (!hdl || !lim) return;  // (uniform over the block)
-  const uint32_t lb = wave_sum32((tid < bx ? a0 : 0u) + (tid + HB < bx ? a1 : 0u));
+  // every region's compact base (exclusive prefix of the counts: region tid in e0, region tid + HB in e1), for
+  // this block's records and their local parents' rows
+  uint32_t e0 = a0, e1 = a1;
+  for (int o = 1; o < HB; o <<= 1) {
+    const uint32_t x0 = __shfl_up(e0, o), x1 = __shfl_up(e1, o);
+    if ((int)tid >= o) e0 += x0, e1 += x1;
+  }
+  e1 += __shfl(e0, HB - 1);
+  e0 -= a0;
+  e1 -= a1;
+  const uint32_t lb = bx < (uint32_t)HB ? __shfl(e0, (int)bx) : __shfl(e1, (int)(bx - HB));
   const uint32_t cnt = bx < (uint32_t)HB ? __shfl(a0, (int)bx) : __shfl(a1, (int)(bx - HB));
   if (bx == 0) {
     const uint32_t tot = wave_sum32(a0 + a1);
@@ -1914,13 +1924,29 @@ __global__ __launch_bounds__(HB) void k_xlcompact(const P2PDev M) {
   const uint32_t rb = region_base(bx);
   X1Loc *xl = x1loc(M.x1_send, 0);
   uint64_t lts = 0;  // (the largest rel ts: the window's last dispatch time may be a local record's)
-  for (uint32_t k = tid; k < cnt && lb + k < (uint32_t)XLCAP; k += HB) {
-    const uint32_t rec = rb + k;
+  for (uint32_t k0 = 0; k0 < cnt; k0 += HB) {  // (block-uniform: the parents' bases come by shuffles)
+    const uint32_t k = k0 + tid;
+    const bool in = k < cnt && lb + k < (uint32_t)XLCAP;
+    const uint32_t rec = rb + (k < cnt ? k : 0u);
     const ulonglong2 w = M.lkw[rec - LBASE];
-    xl[lb + k] = X1Loc{w.x, w.y, M.nchild[rec] | (M.ninl[rec] << 16), rec, M.lkey[rec - LBASE].uid, 0u};
-    M.lxk[rec - LBASE] = lb + k;
-    const uint64_t t = w.x & 0xffffffff00000000ull;
-    lts = t > lts ? t : lts;
+    const uint32_t nc = M.nchild[rec] | (M.ninl[rec] << 16), anc = M.lkey[rec - LBASE].uid, wp = M.wpar[rec];
+    // the parent's accumulator row for k_dfin2 (a gen-0 slot, or WCAP + a local parent's compact index: its
+    // region's base + its place in the region), with the child index of wpar
+    const uint32_t p = wp & 0xffffffu;
+    uint32_t prow = p;
+    if (p >= (uint32_t)LBASE) {
+      const uint32_t off = p - LBASE;
+      const uint32_t r = off < (uint32_t)(NHB * LR) ? off / LR : NHB + (off - NHB * LR) / LRH;
+      const uint32_t pb = r < (uint32_t)HB ? __shfl(e0, (int)r) : __shfl(e1, (int)(r - HB));
+      prow = (uint32_t)WCAP + pb + (p - region_base(r));
+    } else {
+      (void)__shfl(e0, 0);  // (the shuffles are wave-wide: every lane takes part)
+    }
+    if (in) {
+      xl[lb + k] = X1Loc{w.x, w.y, nc, rec, anc, prow | (wp & 0xff000000u)};
+      const uint64_t t = w.x & 0xffffffff00000000ull;
+      lts = t > lts ? t : lts;
+    }
   }
   lts = wave_max64(lts);
   if (tid == 0 && lts) atomicMax((unsigned long long *)&x1hdr(M.x1_send, 0)->lastkey, (unsigned long long)lts);
