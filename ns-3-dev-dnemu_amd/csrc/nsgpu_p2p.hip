@@ -1409,7 +1409,7 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
   // one tile of GJ <= 64 columns the three fields stay within 7, 22 and 22 bits) and its inline children alone
   // (read four columns at a time as 16-B vectors)
   __shared__ __align__(16) uint32_t tts[GJ], tni[GJ], tfa[GJ];
-  __shared__ __align__(16) uint64_t tpb[GJ], tfb[WIDE ? GJ : 2];
+  __shared__ __align__(16) uint64_t tpb[GJ], tfb[GJ];  // (tfb: a gen-0 column's whole key, a local one's w2)
   __shared__ uint32_t tu[WIDE ? GJ : 1], tr[WIDE ? GJ : 1];
   __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR], s_l[MAXR], s_g[MAXR];
   uint32_t L = 0;
@@ -1485,6 +1485,7 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
         const uint64_t key = k < n ? E[k].key : ~0ull;
         tts[k] = (uint32_t)(key >> 32);
         tfa[k] = (uint32_t)key;
+        tfb[k] = key;
         const uint32_t c = k < n ? E[k].cnt : 0u;
         tpb[k] = 1ull | (uint64_t)(c & 0xffffu) << 7 | (uint64_t)(c >> 16) << 29;
         tni[k] = c >> 16;
@@ -1532,15 +1533,13 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
         lp += le;
         ipf += lt ? c.ni[k] : 0u;
       };
-      if (!ltile && !lrow) {
-#pragma unroll 4
+      if (!ltile && !lrow) {  // (the whole keys in one 64-bit compare)
+        const uint64_t kx = (uint64_t)tx << 32 | fax;
+#pragma unroll 2
         for (uint32_t y0 = 0; y0 < (uint32_t)GJ; y0 += 4) {
-          const Col4 c = col4(y0, true, false);
+          const Col4 c = col4(y0, false, true);
 #pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const bool lt = c.ts[k] < tx, eq = c.ts[k] == tx;
-            acc(c, k, lt | (eq & (c.fa[k] < fax)), lt, lt | eq);
-          }
+          for (int k = 0; k < 4; k++) acc(c, k, c.fb[k] < kx, c.ts[k] < tx, c.ts[k] <= tx);
         }
       } else if (!lrow) {  // gen-0 row, local columns: before iff an earlier ts
 #pragma unroll 4
