@@ -1900,6 +1900,12 @@ __global__ __launch_bounds__(HB) void k_xlcompact(const P2PDev M) {
   const uint32_t hdl = C.hdl, tid = threadIdx.x, bx = blockIdx.x;
   const uint64_t lim = C.lim_rel;
   const uint32_t a0 = M.lcnt[tid], a1 = tid + HB < (uint32_t)NLR ? M.lcnt[tid + HB] : 0u;
+  // the region's first HB records, loaded with the counts (speculatively: a region holds at least HB, so the
+  // indices are in range; the counts decide which are written)
+  static_assert(LR >= HB && LRH >= HB, "a region's first HB records");
+  const uint32_t rb = region_base(bx);
+  ulonglong2 w = M.lkw[rb + tid - LBASE];
+  uint32_t nc = M.nchild[rb + tid] | (M.ninl[rb + tid] << 16), anc = M.lkey[rb + tid - LBASE].uid, wp = M.wpar[rb + tid];
   if (!hdl || !lim) return;  // (uniform over the block)
   // every region's compact base (exclusive prefix of the counts: region tid in e0, region tid + HB in e1), for
   // this block's records and their local parents' rows
@@ -1921,27 +1927,25 @@ __global__ __launch_bounds__(HB) void k_xlcompact(const P2PDev M) {
     }
   }
   if (!cnt) return;
-  const uint32_t rb = region_base(bx);
   X1Loc *xl = x1loc(M.x1_send, 0);
   uint64_t lts = 0;  // (the largest rel ts: the window's last dispatch time may be a local record's)
   for (uint32_t k0 = 0; k0 < cnt; k0 += HB) {  // (block-uniform: the parents' bases come by shuffles)
     const uint32_t k = k0 + tid;
     const bool in = k < cnt && lb + k < (uint32_t)XLCAP;
-    const uint32_t rec = rb + (k < cnt ? k : 0u);
-    const ulonglong2 w = M.lkw[rec - LBASE];
-    const uint32_t nc = M.nchild[rec] | (M.ninl[rec] << 16), anc = M.lkey[rec - LBASE].uid, wp = M.wpar[rec];
-    // the parent's accumulator row for k_dfin2 (a gen-0 slot, or WCAP + a local parent's compact index: its
-    // region's base + its place in the region), with the child index of wpar
-    const uint32_t p = wp & 0xffffffu;
-    uint32_t prow = p;
-    if (p >= (uint32_t)LBASE) {
-      const uint32_t off = p - LBASE;
-      const uint32_t r = off < (uint32_t)(NHB * LR) ? off / LR : NHB + (off - NHB * LR) / LRH;
-      const uint32_t pb = r < (uint32_t)HB ? __shfl(e0, (int)r) : __shfl(e1, (int)(r - HB));
-      prow = (uint32_t)WCAP + pb + (p - region_base(r));
-    } else {
-      (void)__shfl(e0, 0);  // (the shuffles are wave-wide: every lane takes part)
+    const uint32_t rec = rb + (k < cnt ? k : tid);
+    if (k0) {  // (past the region's first HB: loaded here)
+      w = M.lkw[rec - LBASE];
+      nc = M.nchild[rec] | (M.ninl[rec] << 16), anc = M.lkey[rec - LBASE].uid, wp = M.wpar[rec];
     }
+    // the parent's accumulator row for k_dfin2 (a gen-0 slot, or WCAP + a local parent's compact index: its
+    // region's base + its place in the region), with the child index of wpar.  (The shuffles run on every
+    // lane: a lane shuffling from one that is off would read zero.)
+    const uint32_t p = wp & 0xffffffu;
+    const bool lpar = p >= (uint32_t)LBASE && p < (uint32_t)WTOT;
+    const uint32_t off = lpar ? p - LBASE : 0u;
+    const uint32_t r = off < (uint32_t)(NHB * LR) ? off / LR : NHB + (off - NHB * LR) / LRH;
+    const uint32_t pe0 = __shfl(e0, (int)(r & (HB - 1))), pe1 = __shfl(e1, (int)(r & (HB - 1)));
+    const uint32_t prow = lpar ? (uint32_t)WCAP + (r < (uint32_t)HB ? pe0 : pe1) + (p - region_base(r)) : p;
     if (in) {
       xl[lb + k] = X1Loc{w.x, w.y, nc, rec, anc, prow | (wp & 0xff000000u)};
       const uint64_t t = w.x & 0xffffffff00000000ull;
