@@ -157,8 +157,9 @@ struct Ctl {
   uint32_t force_run, hcap;        // a hub too large to sort in a block: dispatch the window as a run;
                                    // the window is cut at the next host event (pause after it)
   uint64_t hts, hrel;              // next host event (nsgpu_p2p_advance): ts (~0: none); the rel ts of the
-  uint32_t huid, x1arr;            //   window's last timestamp (W_end or the host event's); the host uid;
-                                   //   k_dfin2's blocks that have read the X1 headers
+  uint32_t huid, gt_tinl;          //   window's last timestamp (W_end or the host event's); the host uid;
+  uint32_t gt_lown, gt_pad;        //   k_gtile -> k_dfin2: the merged window's inline children, this rank's
+                                   //   local records (from the X1 headers: k_dfin2's record blocks read none)
   uint64_t pchild;                 // children of the last scanned window that stay pending (not inline)
   // ---- wide windows (nsgpu_p2p_win.h; partitioned: k_gtile / k_dfin2): same-node TransmitCompletes run inside ----
   uint64_t lim_rel;   // a TransmitComplete child with rel ts < lim_rel is a local record of this window
@@ -1390,7 +1391,7 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
   const uint32_t hdl = C.hdl, W = C.pW;
   const uint32_t q = threadIdx.x;
   const X1Hdr *hq = x1hdr(M.x1_recv, q < M.nranks ? q : 0u);
-  const uint32_t wq0 = hq->W, lq0 = WIDE ? hq->L : 0u;
+  const uint32_t wq0 = hq->W, lq0 = WIDE ? hq->L : 0u, tq0 = hq->tinl;
 #ifdef NSGPU_PHASE_PROF
   const uint64_t gt_t0 = __builtin_amdgcn_s_memrealtime();
   const bool gt_rec = C.windows == g_blk_win && blockIdx.x < (uint32_t)GT_BLK_MAX;
@@ -1430,6 +1431,13 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
     }
     if (q == M.nranks - 1) s_off[M.nranks] = inc;
     if (WIDE) L = __shfl(lq, (int)M.rank);
+    if (blockIdx.x == 0) {  // (for k_dfin2: its record blocks then read no X1 header, and its block 0, the only
+      const uint32_t tg = wave_sum32(q < M.nranks ? tq0 : 0u);  //  reader left, resets this rank's header)
+      if (q == 0) {
+        C.gt_tinl = tg;
+        C.gt_lown = L;
+      }
+    }
   }
   __syncthreads();
   GT_MARK(0);
@@ -1630,23 +1638,28 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
 // Block 0 also does the pool bookkeeping (k2_scan's) and, last, the run bookkeeping; the other blocks
 // read only fields block 0 leaves alone (pW, puid0, hdl, done < 2).  WIDE: threads WCAP.. take this rank's local
 // records (X1Loc order): a local record's uid is its parent's child prefix + its child index.
+constexpr int DF2_FB = 2;  // k_dfin2's blocks before the record blocks (the books, the free-stack move)
 template <bool WIDE>
 __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   Ctl &C = *M.C;
+  BLK_T0();
+#ifdef NSGPU_PHASE_PROF
+  const uint64_t c_win = C.windows;  // (diagnostic: block stamps in g_blk[2], the partitioned path runs no k2_scan)
+#endif
   const uint32_t hdl = C.hdl, W = C.pW;  // (tested after the loads below: a load after a branch on it waited for it)
-  // every rank's X1 header at once, one lane per rank (HB = one wave)
+  const uint32_t tinl_g = C.gt_tinl, Lown = WIDE ? C.gt_lown : 0u;  // (k_gtile's, from the X1 headers)
+  // block 0: every rank's X1 header at once, one lane per rank (HB = one wave)
   const uint32_t lq = threadIdx.x;
   const X1Hdr *lh = x1hdr(M.x1_recv, lq < M.nranks ? lq : 0u);
   const bool lv = lq < M.nranks;
-  const uint32_t tinl_q = lv ? lh->tinl : 0u;
-  const uint32_t l_q = (WIDE && lv) ? lh->L : 0u;  // (the ranks' local records)
+  const uint32_t l_q = (WIDE && lv && blockIdx.x == 0) ? lh->L : 0u;  // (the ranks' local records)
   // (block 0: the rest of the summaries and the run control, for the run bookkeeping, in the same trip)
   struct Bk {
     uint64_t nF, nfree, npush, pK0, ptmin, windows, P_end, live, inline_lim, max_windows, max_window, drg, dr1;
     uint64_t bound, span_t;
     uint32_t nhub, puid0, rt, drtrim, drun;
   } bk{};
-  if (blockIdx.x == 0)
+  if (blockIdx.x <= 1)  // (block 1: the free-stack move and the hubs' tables, beside block 0's bookkeeping)
     bk = Bk{C.nF, C.nfree, C.npush, C.pK0, C.ptmin, C.windows, C.P_end, C.live, C.inline_lim, C.max_windows,
             C.max_window, C.drg, C.dr1, WIDE ? C.bound : 0, WIDE ? C.span_t : 0, C.nhub, C.puid0, C.rt, C.drtrim,
             C.drun};
@@ -1670,7 +1683,10 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   // the record's accumulators, record and first children, all loaded before anything waits — with the headers,
   // before the arrival's wait (WIDE: thread WCAP + k takes local record k of this rank, its record index from
   // the X1Loc list: one more trip; its parent's child prefix needs the parent's accumulator, one more)
-  const uint32_t ti = blockIdx.x * HB + threadIdx.x;
+  // (block 0 keeps the books, block 1 moves the free stack: the records are the next blocks' — block 0 was the
+  //  kernel's tail with the books after its own records, block 1 with the stack move after its records)
+  const bool rec_block = blockIdx.x >= (uint32_t)DF2_FB;
+  const uint32_t ti = (rec_block ? blockIdx.x - (uint32_t)DF2_FB : 0u) * HB + threadIdx.x;
   const bool loc = WIDE && ti >= (uint32_t)WCAP;
   uint64_t *A = reinterpret_cast<uint64_t *>(M.gacc);
   uint64_t w0, w1, wk;
@@ -1696,14 +1712,15 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     }
   }
   if (!hdl) return;  // (k2_handle ran nothing: a cut, a pause, the end)
-  // X1 is all-gathered in place (x1_send is this rank's slot of x1_recv): the last block to have read the
-  // headers resets this rank's for the next window — every block's header loads have returned before it
-  // arrives (one wave per block: the wave's wait covers every lane)
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __builtin_amdgcn_s_waitcnt(0);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  if (threadIdx.x == 0 && atomicAdd(&C.x1arr, 1u) == gridDim.x - 1) {
-    atomicExch(&C.x1arr, 0u);
+  // X1 is all-gathered in place (x1_send is this rank's slot of x1_recv): block 0, the kernel's only reader of the
+  // headers (k_gtile's reads ended with its launch), resets this rank's for the next window once its loads have
+  // returned (one wave: the wave's wait covers every lane)
+  if (blockIdx.x == 0) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     X1Hdr *hs = x1hdr(M.x1_send, 0);
     hs->W = hs->tc = hs->tinl = hs->needc = 0;
     hs->L = 0;
@@ -1713,9 +1730,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     hs->rkey = ~0ull;
     hs->rrem = 0;
   }
-  const uint32_t Lown = WIDE ? __shfl(l_q, (int)M.rank) : 0u;
-  const bool vs = loc ? ti - (uint32_t)WCAP < Lown : ti < W;
-  const uint32_t tinl_g = wave_sum32(tinl_q);
+  const bool vs = rec_block && (loc ? ti - (uint32_t)WCAP < Lown : ti < W);
   if (vs) {
     if (!WIDE) {  // (wide: k2_handle zeroes them — a local record reads its parent's below)
       A[ti] = 0;
@@ -1735,27 +1750,60 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     }
     M.pwctx[s] = wc;
     const uint32_t uid0 = C.puid0;
-    for (uint32_t j = 0; j < ncr; j++) {
-      const uint32_t sl = s * M.maxc + j;
-      const uint32_t kw = j < (uint32_t)PFC ? ckw[j] : M.ch_kind[sl];
-      if ((kw & 0xffu) == K_FWD_UP) continue;
-      if (!(kw & REMOTEBIT)) continue;  // (a Receive on another rank's node: the device step marked it)
-      const uint32_t ctx = j < (uint32_t)PFC ? cctx[j] : M.ch_ctx[sl];
-      const uint32_t q = M.owner[ctx];
-      const uint32_t pos = atomicAdd(&x2hdr(M, M.x2_send, q)->n, 1u);
-      if (pos < M.capx)
-        x2rec(M, M.x2_send, q)[pos] = Ev{M.ch_ts[sl], uid0 + cp + j, ctx, kw, M.ch_a[sl], M.ch_pkt[sl]};
-      else
-        atomicOr(M.error, 16u);
+    // the record's children on other ranks' nodes -> X2 (one rank: none).  Their kinds eight at a time (one
+    // dependent load a child past the first PFC held a record with many children ~10 us: the kernel's tail)
+    constexpr int KB = 8;
+    static_assert(PFC <= KB, "the preloaded kinds fit the first batch");
+    for (uint32_t j0 = 0; M.nranks > 1 && j0 < ncr; j0 += KB) {
+      uint32_t kwv[KB];
+#pragma unroll
+      for (int q = 0; q < KB; q++) {
+        const uint32_t j = j0 + q;
+        kwv[q] = (j0 == 0 && q < PFC) ? ckw[q < PFC ? q : 0] : j < ncr ? M.ch_kind[s * M.maxc + j] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < KB; q++) {
+        const uint32_t j = j0 + q, kw = kwv[q];
+        if (j >= ncr || (kw & 0xffu) == K_FWD_UP) continue;
+        if (!(kw & REMOTEBIT)) continue;  // (a Receive on another rank's node: the device step marked it)
+        const uint32_t sl = s * M.maxc + j;
+        const uint32_t ctx = (j0 == 0 && q < PFC) ? cctx[q < PFC ? q : 0] : M.ch_ctx[sl];
+        const uint32_t qr = M.owner[ctx];
+        const uint32_t pos = atomicAdd(&x2hdr(M, M.x2_send, qr)->n, 1u);
+        if (pos < M.capx)
+          x2rec(M, M.x2_send, qr)[pos] = Ev{M.ch_ts[sl], uid0 + cp + j, ctx, kw, M.ch_a[sl], M.ch_pkt[sl]};
+        else
+          atomicOr(M.error, 16u);
+      }
     }
   }
-  if (blockIdx.x != 0) return;
   // ---- pool bookkeeping (k2_scan's): the free stack loses the slots the fresh children took and gains
   // the window's; its pushed part is moved down over the popped hole; the hubs' slot tables are cleared
   const uint64_t nF = bk.nF, nfree = bk.nfree, npush = bk.npush;
   const uint64_t consumed = nF < nfree ? nF : nfree;
   const uint64_t mv = consumed < npush ? consumed : npush;
   const uint32_t nh = bk.nhub < (uint32_t)MAXHUB ? bk.nhub : (uint32_t)MAXHUB;
+  if (blockIdx.x == 1) {  // the free-stack move and the hubs' slot tables (the two ranges are disjoint: eight
+    constexpr int SB = 8;  // loads in flight a lane, then the stores)
+    for (uint64_t i0 = threadIdx.x; i0 < mv; i0 += (uint64_t)HB * SB) {
+      uint32_t v[SB];
+#pragma unroll
+      for (int k = 0; k < SB; k++) {
+        const uint64_t i = i0 + (uint64_t)k * HB;
+        v[k] = i < mv ? M.fstack[nfree + npush - mv + i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < SB; k++) {
+        const uint64_t i = i0 + (uint64_t)k * HB;
+        if (i < mv) M.fstack[nfree - consumed + i] = v[k];
+      }
+    }
+    for (uint32_t h = threadIdx.x; h < nh; h += HB) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
+  }
+  if (blockIdx.x != 0) {
+    BLK_REC(2, c_win);
+    return;
+  }
   // the ranks' summaries, reduced across the lanes (rank q's in lane q)
   const uint32_t Wg = wave_sum32(hW), tcg = wave_sum32(htc), Lg = WIDE ? wave_sum32(l_q) : 0u;
   const uint32_t needc = __ballot(hneedc != 0) ? 1u : 0u;
@@ -1777,28 +1825,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
     const int first = m ? __ffsll((unsigned long long)m) - 1 : 0;
     rg.stopuid = __shfl(hsuid, first);
   }
-  // (the free-stack move and the hubs' slot tables last: a moving lane waits for its loads)
-  auto stack_and_hubs = [&]() {  // (the two ranges are disjoint: eight loads in flight a lane, then the stores)
-    constexpr int SB = 8;
-    for (uint64_t i0 = threadIdx.x; i0 < mv; i0 += (uint64_t)HB * SB) {
-      uint32_t v[SB];
-#pragma unroll
-      for (int k = 0; k < SB; k++) {
-        const uint64_t i = i0 + (uint64_t)k * HB;
-        v[k] = i < mv ? M.fstack[nfree + npush - mv + i] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < SB; k++) {
-        const uint64_t i = i0 + (uint64_t)k * HB;
-        if (i < mv) M.fstack[nfree - consumed + i] = v[k];
-      }
-    }
-    for (uint32_t h = threadIdx.x; h < nh; h += HB) M.node_tab[(uint64_t)M.hub_list[h] * NTAB] = 0;
-  };
-  if (threadIdx.x != 0) {
-    stack_and_hubs();
-    return;
-  }
+  if (threadIdx.x != 0) return;  // (the reductions above took the whole wave)
   C.K = bk.pK0 + Wg + Lg + tinl_g;
   if (WIDE) {
     C.plt = Lown;  // (the next k2_pa appends them from lrec)
@@ -1855,7 +1882,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   if (done) C.done = 1;
   else if (needc && !drun_more) C.mode = MODE_COMPACT;  // (every rank: the pipelines stay in step; a run's
                                                          //  pool entries keep their slots until it ends)
-  stack_and_hubs();
+  BLK_REC(2, c_win);
 }
 
 // Loopback transport (nsgpu_p2p_group_*: every partition on one device): one block per copy.
@@ -2816,10 +2843,10 @@ static void dist_handle(const P2PDev &M, hipStream_t s) {
 static void dist_rank_fin(const P2PDev &M, hipStream_t s) {
   if (M.wide) {
     hipLaunchKernelGGL(k_gtile<true>, dim3(GTB), dim3(HB), 0, s, M);
-    hipLaunchKernelGGL(k_dfin2<true>, dim3(NACC / HB), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k_dfin2<true>, dim3(DF2_FB + NACC / HB), dim3(HB), 0, s, M);
   } else {
     hipLaunchKernelGGL(k_gtile<false>, dim3(GTB), dim3(HB), 0, s, M);
-    hipLaunchKernelGGL(k_dfin2<false>, dim3(NHB), dim3(HB), 0, s, M);
+    hipLaunchKernelGGL(k_dfin2<false>, dim3(DF2_FB + NHB), dim3(HB), 0, s, M);
   }
 }
 // The partitioned window (one RCCL member): 4 kernels and 3 collectives, on stream s.
@@ -3440,8 +3467,8 @@ static void launch_windows_group(nsgpu_p2p_group *g, hipStream_t s, int nwin = N
       else hipLaunchKernelGGL(k_gtile<false>, dim3(GTB), dim3(HB), 0, s, h->M);
     }
     for (auto *h : g->m) {
-      if (h->M.wide) hipLaunchKernelGGL(k_dfin2<true>, dim3(NACC / HB), dim3(HB), 0, s, h->M);
-      else hipLaunchKernelGGL(k_dfin2<false>, dim3(NHB), dim3(HB), 0, s, h->M);
+      if (h->M.wide) hipLaunchKernelGGL(k_dfin2<true>, dim3(DF2_FB + NACC / HB), dim3(HB), 0, s, h->M);
+      else hipLaunchKernelGGL(k_dfin2<false>, dim3(DF2_FB + NHB), dim3(HB), 0, s, h->M);
     }
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[2]);
   }

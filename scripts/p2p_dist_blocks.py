@@ -21,8 +21,9 @@ blk = buf[64:].reshape(3, BLK, 2).astype(np.int64)
 wide = grp.members[0].wide()
 nslot = (4096 + 4096) // 256 if wide else 16  # (wide: gen-0 slots, then the local records' dense list)
 roles = {0: [("slot", 0, 16), ("lslot", 16, nslot), ("remote", nslot, nslot + 1), ("pool", nslot + 1, 256)],
-         1: [("holder", 0, 64), ("hub", 64, 96), ("maint", 96, 224)]}
-for k, name in ((0, "k2_pa<DIST>"), (1, "k2_handle")):
+         1: [("holder", 0, 64), ("hub", 64, 96), ("maint", 96, 224)],
+         2: [("book", 0, 1), ("stack", 1, 2), ("gen0", 2, 66), ("local", 66, 130)]}
+for k, name in ((0, "k2_pa<DIST>"), (1, "k2_handle"), (2, "k_dfin2")):
     b = blk[k]
     ok = b[:, 1] > 0
     if not ok.any():
