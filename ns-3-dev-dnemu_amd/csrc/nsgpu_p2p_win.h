@@ -573,7 +573,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
     C.hcap = hcap;
   }
   const uint32_t pW = c_pvalid ? c_pW : 0;
-  constexpr int PPT = 4;  // (pool entries a thread reads a chunk)
+#ifndef PA_PPT
+#define PA_PPT 2  // (4: config 4 149.5 M ev/s, 2: 153 M — twice the pool blocks, each half the claims and writes)
+#endif
+  constexpr int PPT = PA_PPT;  // (pool entries a thread reads a chunk)
   {  // a pool block past the pool's end (most of them: the pool holds a few thousand entries) has nothing to do
     const uint64_t pb = blockIdx.x - (uint64_t)(NSGB + rrb);
     if (!slot_block && !remote_role && partition && !run && !drun && !(DIST && dtrim && pb < (uint64_t)(WCAP / TB)) &&
