@@ -203,7 +203,10 @@ int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base, uint32_t p
 /* every device event with a key below (bound_ts, bound_uid) (~0: all): ranks from *dispatched, the syncs'
  * EndReceive uids from *uid, log entries (at their ranks, below log_cap) written.  The epoch's digest terms
  * are summed by kernels that run behind the next epochs (the order is not on the PHY's critical path): each
- * call adds to *digest the terms summed so far; nsgpu_wifil_flush adds the rest. */
+ * call adds to *digest the terms summed so far; nsgpu_wifil_flush adds the rest.  A direct caller MUST call
+ * nsgpu_wifil_flush before reading the digest (until then it is partial, with no error); nsgpu_sim_run and
+ * nsgpu_sim_host_stats flush by themselves.  NSGPU_ERANGE (the epoch's EndReceives would pass uid 0xfffffffe)
+ * is returned before the epoch's ends, dispatch count or digest are published; the runtime makes it sticky. */
 int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t bound_uid, uint32_t *uid, uint64_t *dispatched,
                         uint64_t *digest, uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap);
 int nsgpu_wifil_flush(nsgpu_wifil *h, uint64_t *digest);  /* waits for every epoch's order; adds its digest terms */

@@ -21,6 +21,12 @@ inline int uid_range_error(const char *where) {
                                  "wraps there, which the engines do not replicate)", where);
 }
 
+// The attached p2p engine's first setup uid (its scenario's uid_first, or 4): nsgpu_sim_attach_p2p checks it
+// against a start set with nsgpu_sim_set_next_uid.
+}  // namespace nsgpu
+struct nsgpu_p2p;
+namespace nsgpu {
+uint32_t p2p_first_uid(const nsgpu_p2p *h);
 }  // namespace nsgpu
 
 #define NSGPU_HIP(call)                                                                              \

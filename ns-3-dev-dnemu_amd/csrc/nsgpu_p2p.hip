@@ -3063,6 +3063,8 @@ static int drive_dist(nsgpu_p2p *h) {
 }
 
 // ---- mixed host / device runs: the host-closure runtime (nsgpu_sim) drives the engine ----
+uint32_t nsgpu::p2p_first_uid(const nsgpu_p2p *h) { return h->sc.uid_first ? h->sc.uid_first : 4u; }
+
 extern "C" int nsgpu_p2p_setup_uid(nsgpu_p2p *h, uint32_t *uid) {
   if (!h || !uid) return set_error(NSGPU_EINVAL, "nsgpu_p2p_setup_uid: null");
   *uid = h->C0.uid;
@@ -3081,8 +3083,11 @@ extern "C" int nsgpu_p2p_advance(nsgpu_p2p *h, uint64_t hts, uint32_t huid, uint
   hipStream_t cs = (hipStream_t)stream;
   NSGPU_HIP(hipEventRecord(h->ev[0], cs));
   NSGPU_HIP(hipStreamWaitEvent(h->s, h->ev[0], 0));
+  uint32_t err0 = 0;
   NSGPU_HIP(hipMemcpyAsync(&h->snap[0], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipMemcpyAsync(&err0, h->M.error, 4, hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipStreamSynchronize(h->s));
+  if (err0) return engine_error(err0);  // (sticky: e.g. a refused inject_send at the uid limit)
   if (h->snap[0].done >= 2) {
     *ended = 1;
     return NSGPU_OK;
@@ -3143,12 +3148,15 @@ extern "C" int nsgpu_p2p_inject_send(nsgpu_p2p *h, uint32_t app, uint64_t now, u
   NSGPU_HIP(hipStreamSynchronize(s));
   if (h->snap[0].mode != MODE_HOST) return set_error(NSGPU_ESTATE, "nsgpu_p2p_inject_send: the engine is not paused for a host closure");
   hipLaunchKernelGGL(k_set_uid, dim3(1), dim3(1), 0, s, h->M, *uid);  // (the host closures' Schedule calls)
-  hipLaunchKernelGGL(k_inject, dim3(1), dim3(1), 0, s, h->M, app, now, cur_uid, cur_ctx, *trace_seq, h->M.s_val);
+  // (the room is checked on the device before any child is written: a refused send leaves the sticky uid error)
+  if ((uint64_t)*uid > UID_MAX_NEXT) return nsgpu::uid_range_error("nsgpu_p2p_inject_send");
+  hipLaunchKernelGGL(k_inject, dim3(1), dim3(1), 0, s, h->M, app, now, cur_uid, cur_ctx, *trace_seq,
+                     (uint64_t)(UID_MAX_NEXT - *uid), h->M.s_val);
   NSGPU_HIP(hipGetLastError());
-  uint32_t outv[2];
+  uint32_t outv[3];
   NSGPU_HIP(hipMemcpyAsync(outv, h->M.s_val, sizeof(outv), hipMemcpyDeviceToHost, s));
   NSGPU_HIP(hipStreamSynchronize(s));
-  if ((uint64_t)*uid + (uint32_t)(outv[0] - *uid) > UID_MAX_NEXT) return nsgpu::uid_range_error("nsgpu_p2p_inject_send");
+  if (outv[2]) return nsgpu::uid_range_error("nsgpu_p2p_inject_send");
   *uid = outv[0];
   *trace_seq = outv[1];
   return NSGPU_OK;

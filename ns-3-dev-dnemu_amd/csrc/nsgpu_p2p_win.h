@@ -3298,8 +3298,10 @@ __global__ void k_set_uid(const P2PDev M, uint32_t uid) { M.C->uid = uid; }
 // (onoff-application.cc:226-236 -> udp-socket-impl.cc DoSendTo -> Ipv4L3Protocol::Send -> the device),
 // its Schedule calls taking uids from uid0.  The children become pending in place and fold into the
 // reduction that bounds the next window.
+// `room`: the uids left below UID_MAX_NEXT; a send whose Schedule calls would need more writes no child, sets the
+// sticky uid error (2048) and reports out[2] = 1 (DefaultSimulatorImpl's m_uid would wrap there).
 __global__ void k_inject(const P2PDev M, uint32_t a, uint64_t now, uint32_t cur, uint32_t ctx, uint32_t seq,
-                         uint32_t *out) {
+                         uint64_t room, uint32_t *out) {
   Ctl &C = *M.C;
   Emit E;
   E.now = now;
@@ -3334,6 +3336,14 @@ __global__ void k_inject(const P2PDev M, uint32_t a, uint64_t now, uint32_t cur,
     device_act(M, E, Act{ACT_SEND, o, p});
   }
   const uint32_t uid0 = C.uid;
+  out[2] = 0;
+  if ((uint64_t)E.n > room) {
+    atomicOr(M.error, 2048u);
+    out[0] = uid0;
+    out[1] = E.trseq;
+    out[2] = 1;
+    return;
+  }
   for (uint32_t j = 0; j < E.n; j++) {
     uint64_t dst;
     if (C.nfree) dst = M.fstack[--C.nfree];

@@ -50,6 +50,7 @@ struct nsgpu_sim {
   bool stop = false, ended = false, dev_stopped = false;
   uint32_t uid = 4;
   uint32_t uid_first = 4;  // m_uid before the program's first Schedule call (nsgpu_sim_set_next_uid)
+  bool uid_set = false;    // uid_first was set explicitly (an attached engine must start there too)
   bool uid_spent = false;  // a Schedule call hit the uid limit (a closure's call fails; the run then fails too)
   uint32_t cur_uid = 0;
   uint64_t cur_ts = 0;
@@ -162,6 +163,9 @@ int nsgpu_sim_attach_p2p(nsgpu_sim *s, nsgpu_p2p *h) {
   if (!s || !h) return set_error(NSGPU_EINVAL, "nsgpu_sim_attach_p2p: null");
   if (s->events->size || s->dispatched || s->uid != s->uid_first)
     return set_error(NSGPU_ESTATE, "nsgpu_sim_attach_p2p: attach before scheduling");
+  if (s->uid_set && nsgpu::p2p_first_uid(h) != s->uid_first)  // (two starts that disagree)
+    return set_error(NSGPU_ESTATE, "nsgpu_sim_attach_p2p: the engine's setup starts at uid %u, this runtime was set "
+                                   "to start at %u", nsgpu::p2p_first_uid(h), s->uid_first);
   uint32_t u = 0;
   int rc = nsgpu_p2p_setup_uid(h, &u);
   if (rc) return rc;
@@ -277,6 +281,7 @@ int nsgpu_sim_set_next_uid(nsgpu_sim *s, uint32_t uid) {
     return set_error(NSGPU_ESTATE, "nsgpu_sim_set_next_uid: the runtime has scheduled or attached something already");
   if (uid < 4) return set_error(NSGPU_EINVAL, "nsgpu_sim_set_next_uid: uids 0, 1, 2 (and 3) are reserved");
   s->uid = s->uid_first = uid;
+  s->uid_set = true;
   return NSGPU_OK;
 }
 
@@ -380,6 +385,7 @@ static int pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n,
     }
     rc = nsgpu_wifil_advance(s->wifi, have ? e.ts : ~0ull, have ? e.uid : 0u, &s->uid, &s->dispatched, &s->digest,
                              s->log_ts, s->log_uid, s->log_ctx, s->log_cap);
+    if (rc == NSGPU_ERANGE) s->uid_spent = true;  // (sticky: the epoch's EndReceives would take wrapped uids)
     if (rc || !have) return rc;
     if ((rc = nsgpu::sched_remove_next1(q, &e))) return rc;
     out[0] = e;
@@ -395,6 +401,7 @@ static int pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n,
     }
     int ended = 0;
     rc = nsgpu_p2p_advance(s->p2p, have ? e.ts : ~0ull, have ? e.uid : 0u, &s->uid, &s->dispatched, &ended, s->stream);
+    if (rc == NSGPU_ERANGE) s->uid_spent = true;
     if (rc) return rc;
     if (ended) {  // the device dispatched Simulator::Stop, or nothing is pending on the device
       uint64_t pn = 0, pts = 0;
@@ -673,6 +680,7 @@ int nsgpu_sim_p2p_send(nsgpu_sim *s, uint32_t app) {
                                    "pending when a host event was next); the datagram would never be sent");
   uint32_t seq = s->p2p_seq_uid == s->cur_uid ? s->p2p_seq : 0;
   int rc = nsgpu_p2p_inject_send(s->p2p, app, s->cur_ts, s->cur_uid, s->cur_ctx, &s->uid, &seq, s->stream);
+  if (rc == NSGPU_ERANGE) return s->spent("nsgpu_sim_p2p_send");
   s->p2p_seq_uid = s->cur_uid;
   s->p2p_seq = seq;
   return rc;

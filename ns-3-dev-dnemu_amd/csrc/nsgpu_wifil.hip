@@ -1958,6 +1958,14 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   int rc = wl_check(h, "nsgpu_wifil_advance");
   if (rc) return rc;
   const uint32_t nev = h->h_cnt[0], nsync = h->h_cnt[1], nend = h->h_cnt[2];
+  // (r05z4n: a diagnostic build that skipped the order also skipped its zeroing of the epoch counters, so nev
+  // grew epoch by epoch past the dense array — a count beyond it is an engine fault, reported as one)
+  if ((uint64_t)nev > (uint64_t)D.nphy * EVB + D.ev_cap || nend > D.end_cap || nsync > D.sync_cap)
+    return set_error(NSGPU_ESTATE, "nsgpu_wifil_advance: epoch counts beyond the engine's arrays (events %u, syncs "
+                                   "%u, ends %u): the epoch counters were not reset", nev, nsync, nend);
+  //  the uid range before anything of the epoch is published (ends, dispatch count, digest): the
+  // epoch's EndReceives are queued, none dispatched; the caller makes the error sticky (nsgpu_sim: uid_spent)
+  if ((uint64_t)*uid + nsync > nsgpu::UID_NEXT_MAX) return nsgpu::uid_range_error("nsgpu_wifil_advance");
   h->ends_epoch.resize(nend);
   if (nend > END_STAGE) {
     NSGPU_HIP(hipMemcpyAsync(h->ends_epoch.data(), D.ends, nend * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, h->s));
@@ -2015,8 +2023,6 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   std::sort(h->ends_epoch.begin(), h->ends_epoch.end(),
             [](const nsgpu_wifil_end &a, const nsgpu_wifil_end &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
   h->ends.insert(h->ends.end(), h->ends_epoch.begin(), h->ends_epoch.end());
-  if ((uint64_t)*uid + nsync > nsgpu::UID_NEXT_MAX)  // (the epoch's EndReceives are queued, none dispatched yet)
-    return nsgpu::uid_range_error("nsgpu_wifil_advance");
   *uid += nsync;
   return NSGPU_OK;
 }

@@ -219,7 +219,21 @@ CheckGlobalRouting (Ptr<Ipv4> ip, uint32_t node)
       for (uint32_t r = 0; r < st->GetNRoutes (); r++)
         {
           Ipv4RoutingTableEntry e = st->GetRoute (r);
-          if (e.GetGateway () != Ipv4Address::GetZero () || e.IsDefault ())
+          // the routes Ipv4StaticRouting adds by itself (ipv4-static-routing.cc NotifyInterfaceUp /
+          // NotifyAddAddress): each interface address's own network on that interface, gateway-less.  Any other
+          // route, gateway-less ones included (AddHostRouteTo (dst, if), AddNetworkRouteTo (net, mask, if)), is
+          // consulted before global routing (priority 0 > -10) and would override the paths the engine models.
+          bool own = false;
+          if (e.GetGateway () == Ipv4Address::GetZero () && !e.IsDefault () && e.GetInterface () < ip->GetNInterfaces ())
+            {
+              for (uint32_t a = 0; a < ip->GetNAddresses (e.GetInterface ()) && !own; a++)
+                {
+                  Ipv4InterfaceAddress ia = ip->GetAddress (e.GetInterface (), a);
+                  own = e.GetDestNetworkMask () == ia.GetMask ()
+                        && e.GetDestNetwork () == ia.GetLocal ().CombineMask (ia.GetMask ());
+                }
+            }
+          if (!own)
             {
               NS_FATAL_ERROR ("NsgpuP2pScenario::FromNodeList: node " << node << " holds the static route " << e
                               << " (the engine models global routing only)");

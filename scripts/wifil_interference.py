@@ -1,0 +1,73 @@
+"""Diagnostic: the closed-loop Wi-Fi line measured 75 us an epoch alone and 111 us as the
+p2p-grid bench's secondary.  This runs the wifi-loop workload (bench.WifiLoop) in one process after each of the
+steps the bench takes before it and prints its us per epoch, so the step that slows it shows up.
+Usage (GPU box): python scripts/wifil_interference.py [stages...]"""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "ns-3-dev-dnemu_amd"))
+
+import bench  # noqa: E402
+import nsgpu  # noqa: E402
+
+
+def args_ns():
+    return argparse.Namespace(grid=128, holds=5_000_000, dumbbell_leaves=499_999, fanout_tx=1024, wifi_side=100,
+                              wifi_stop=2.0, wifi_loop_stop=0.2, wifi_mac="native")
+
+
+def loop(tag, args, stream, reps=3):
+    wl = bench.WifiLoop(args, stream.handle)
+    wl.step()
+    us = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        wl.step()
+        us.append(round(wl.result()[2]["us_per_epoch"], 1))
+    wl.close()
+    print(f"{tag:40s} us/epoch {us}", flush=True)
+
+
+def main():
+    nsgpu.check(nsgpu.lib().nsgpu_set_device(0))
+    args = args_ns()
+    stream = nsgpu.Stream()
+    stages = sys.argv[1:] or ["fresh", "p2p", "profile", "close_p2p", "wifi_grid", "dumbbell"]
+    g = None
+    for st in stages:
+        if st == "fresh":
+            pass
+        elif st == "p2p":
+            g = bench.P2PGrid(args, stream.handle)
+            g.step()
+            stream.sync()
+        elif st == "profile":
+            g.roofline(50.0, 7_599_361)
+        elif st == "close_p2p":
+            g.close()
+            g = None
+        elif st == "wifi_grid":
+            w = bench.WifiGrid(args, stream.handle)
+            w.step()
+            stream.sync()
+            w.close()
+        elif st == "wifi_grid_open":
+            w = bench.WifiGrid(args, stream.handle)
+            w.step()
+            stream.sync()
+        elif st == "dumbbell":
+            d = bench.P2PDumbbell(args, stream.handle)
+            d.step()
+            stream.sync()
+            d.close()
+        elif st == "probe":
+            print("probe", nsgpu.probe_latency(), flush=True)
+        loop(f"after {st}", args, stream)
+
+
+if __name__ == "__main__":
+    main()

@@ -148,3 +148,59 @@ def test_wifi_loop_uid_limit():
     assert run_oracle(sc, uid_first=first + 1)[3]["next_uid"] == 0
     with pytest.raises(nsgpu.NsgpuError, match="error 5"):
         run_gpu(sc, uid_first=first + 1)
+
+
+# ---------------------------------------------------------------- a host closure's send on the attached p2p engine
+def _probe_run(sc, t0, period, count, app_send):
+    """Host closures every `period` from t0 sending one datagram of `app_send` (nsgpu_sim_p2p_send); returns each
+    call's (uid counter before, after or the error) and how the run ended."""
+    eng = p2p.Engine(sc)
+    eng.reset()
+    sim = nsgpu.Sim()
+    sim.attach_p2p(eng)
+    calls = []
+
+    def probe():
+        before = sim.next_uid()
+        try:
+            sim.p2p_send(app_send)
+            calls.append((before, sim.next_uid()))
+        except nsgpu.NsgpuError as e:
+            calls.append((before, str(e)))
+            return
+        if len(calls) < count:
+            sim.schedule(period, probe)
+
+    sim.schedule(t0, probe)
+    try:
+        sim.run()
+        ended = "ok"
+    except nsgpu.NsgpuError as e:
+        ended = str(e)
+    return calls, ended
+
+
+def test_p2p_inject_send_refused_at_the_uid_limit_before_any_child():
+    """nsgpu_sim_p2p_send with fewer uids left than the send's Schedule calls need.  The send is
+    refused on the device before any child is written (no wrapped uid enters the pool), the error is sticky
+    (the engine's advance and the runtime's Run both fail with NSGPU_ERANGE), and a send with exactly enough
+    room still succeeds (its last uid is 0xfffffffe)."""
+    from test_gpu_mixed import flows_grid
+    sc = flows_grid()
+    app_send = [i for i, a in enumerate(sc.apps) if a["kind"] == p2p.APP_ONOFF][1]
+    calls, ended = _probe_run(sc, 150_000_000, 7_300_001, 4, app_send)
+    assert ended == "ok" and len(calls) == 4
+    before, after = calls[2]
+    need = after - before
+    assert need >= 1
+    base = sc.uid_first or 4  # (0: DefaultSimulatorImpl's start, 4)
+    # exactly enough room at the third send: its children end at 0xfffffffe, the counter at 0xffffffff
+    sc.uid_first = base + (U32 - need - before)
+    calls, ended = _probe_run(sc, 150_000_000, 7_300_001, 3, app_send)
+    assert all(isinstance(c[1], int) for c in calls[:2])  # (the run itself then ends at the limit)
+    assert calls[2] == (U32 - need, U32)
+    # one uid less: the third send is refused, and the run ends with the uid error
+    sc.uid_first = base + (U32 - need - before) + 1
+    calls, ended = _probe_run(sc, 150_000_000, 7_300_001, 3, app_send)
+    assert calls[2][0] == U32 - need + 1 and "error 5" in calls[2][1]
+    assert "error 5" in ended
