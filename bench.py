@@ -249,6 +249,36 @@ class P2PDumbbell(P2PGrid):
                          f"routes; whole run GPU-resident on one GPU")
 
 
+def dist_scenario(args, workload, rank, world):
+    """The scenario and node -> rank map every rank of a partitioned p2p run builds (p2p-grid: the grid
+    weak-scaled to 128 x 128N in N row bands; dumbbell: simple-distributed.cc's system-id partition)."""
+    import numpy as np
+    import p2p
+    if workload == "dumbbell":
+        n = args.dumbbell_leaves
+        sc = p2p.dumbbell(n)
+        owner = p2p.dumbbell_owner(n, world) if world > 1 else np.zeros(sc.n_nodes, np.uint32)
+    else:
+        sc = p2p.grid(args.grid, args.grid * world)
+        owner = p2p.owner_blocks(sc.n_nodes, world)
+    return sc, owner
+
+
+def check_plans(sc, owner, rank, world, td):
+    """Every rank's engine plan (nsgpu_p2p_dist_plan: exchange sizes, window capacities, lookaheads) all-gathered
+    over gloo and compared BEFORE any RCCL call: ranks that disagree would call collectives of different sizes
+    and hang; here they fail with the fields that differ.  Returns this rank's plan."""
+    import p2p
+    plan = p2p.dist_plan(sc, owner, rank, world)
+    if td is not None:
+        plans = [None] * world
+        td.all_gather_object(plans, plan)
+        bad = p2p.plan_mismatch(plans)
+        if bad:
+            raise RuntimeError(f"partitioned run: the ranks' engine plans differ: {bad}")
+    return plan
+
+
 class P2PGridDist:
     """Config 4 weak-scaled over N ranks (one GPU each): PointToPointGridHelper 128 x 128N, one OnOff
     flow per column from row 0 to row 127, node ids (creation order) split into N contiguous row bands
@@ -262,8 +292,8 @@ class P2PGridDist:
         import p2p
         self.p2p, self.rank, self.world, self.td = p2p, rank, world, td
         n = args.grid
-        self.scenario = p2p.grid(n, n * world)
-        owner = p2p.owner_blocks(self.scenario.n_nodes, world)
+        self.scenario, owner = dist_scenario(args, "p2p-grid", rank, world)
+        self.plan = check_plans(self.scenario, owner, rank, world, td)
         uid = [p2p.Comm.unique_id() if rank == 0 else None]
         if td is not None:
             td.broadcast_object_list(uid, src=0)
@@ -320,8 +350,8 @@ class P2PDumbbellDist(P2PGridDist):
         import p2p
         self.p2p, self.rank, self.world, self.td = p2p, rank, world, td
         n = args.dumbbell_leaves
-        self.scenario = p2p.dumbbell(n)
-        owner = (p2p.dumbbell_owner(n, world) if world > 1 else np.zeros(self.scenario.n_nodes, np.uint32))
+        self.scenario, owner = dist_scenario(args, "dumbbell", rank, world)
+        self.plan = check_plans(self.scenario, owner, rank, world, td)
         uid = [p2p.Comm.unique_id() if rank == 0 else None]
         if td is not None:
             td.broadcast_object_list(uid, src=0)
@@ -666,7 +696,7 @@ WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid, "dumbbell": P2PDumbbell, "wifi
              "wifi-grid": WifiGrid, "wifi-loop": WifiLoop}
 
 
-def main():
+def parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -688,7 +718,11 @@ def main():
     ap.add_argument("--partitioned", action="store_true",
                     help="p2p-grid / wifi-grid / dumbbell through the partitioned engine even on one rank (RCCL "
                          "with one rank)")
-    args = ap.parse_args()
+    return ap
+
+
+def main():
+    args = parser().parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

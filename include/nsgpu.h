@@ -454,6 +454,33 @@ int nsgpu_comm_destroy(nsgpu_comm *c);
 /* comm == NULL: a loopback member (all partitions in one process on one device, see below). */
 int nsgpu_p2p_create_dist(const nsgpu_p2p_scenario *sc, const uint32_t *node_owner, int rank, int nranks,
                           nsgpu_comm *comm, uint64_t pool_cap, uint64_t log_cap, nsgpu_p2p **out);
+/* The constants a rank's partitioned engine is built from, computed on the host (no device, no communicator):
+ * what nsgpu_p2p_create_dist derives from the scenario and the owner map (the same code: create_engine runs it
+ * first).  Every field except n_init and pool_cap must be equal on every rank — the exchanges' sizes (X0 / X1 /
+ * X2 bytes, X2 records per peer), the window capacities and the lookaheads that bound every window; ranks that
+ * disagree would call collectives of different sizes, an RCCL hang no single process can see (the reference
+ * sizes its LBTS messages and per-peer buffers the same way on every rank: distributed-simulator-impl.cc:146-216,
+ * mpi-interface.cc:385-445).  node_owner == NULL: the single engine's plan (the exchange fields are 0). */
+typedef struct nsgpu_p2p_plan {
+  uint32_t wide;                /* wide windows (same-node TransmitCompletes inside the window) */
+  uint32_t maxc;                /* children per event record */
+  uint32_t wcap, xlcap;         /* gen-0 window records / local records of one rank's window */
+  uint64_t x0_bytes;            /* X0 all-gather: bytes per rank */
+  uint64_t x1_bytes;            /* X1 all-gather: bytes per rank */
+  uint64_t x2_bytes;            /* X2 all-to-all: bytes per peer */
+  uint32_t x2_records;          /* X2 event records per peer per window */
+  uint32_t n_kinds;             /* entries of lookahead / lookw in use */
+  int64_t lookahead[16];        /* narrow lookahead per event kind (ns) */
+  int64_t lookw[16];            /* wide lookahead per event kind (ns; partitioned: capped below 3 tx_min) */
+  int64_t tx_min, lx;           /* smallest transmission time; smallest cross-node delay (tx + channel) */
+  uint64_t red0_tmin, red0_wend, red0_wendw;  /* window 0's bound: the whole setup's reduction */
+  uint64_t stop_ts;             /* Simulator::Stop's time (~0: none) */
+  uint32_t stop_uid, uid_init;  /* Stop's uid; m_uid after setup */
+  uint32_t n_init, pad;         /* this rank's setup events (per rank) */
+  uint64_t pool_cap;            /* this rank's pending pool (per rank: follows n_init unless given) */
+} nsgpu_p2p_plan;
+int nsgpu_p2p_dist_plan(const nsgpu_p2p_scenario *sc, const uint32_t *node_owner, int rank, int nranks,
+                        uint64_t pool_cap, nsgpu_p2p_plan *out);
 /* Loopback group: partitions 0..n-1 (created with comm == NULL) run on this device with the
  * collectives replaced by device-to-device copies — the partitioned algorithm on one GPU. */
 typedef struct nsgpu_p2p_group nsgpu_p2p_group;

@@ -2023,16 +2023,35 @@ extern "C" int nsgpu_p2p_destroy(nsgpu_p2p *h) {
   return NSGPU_OK;
 }
 
-// owner == null: the whole scenario on this device; otherwise the partition `rank` of `nranks`
-// (node n belongs to rank owner[n]).
-static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, int rank, int nranks,
-                         nsgpu_comm *comm, uint64_t pool_cap, uint64_t log_cap, nsgpu_p2p **out) {
-  if (!sc || !out) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: null");
-  *out = nullptr;
+// What a rank's engine is built from, computed on the host before any device allocation (create_engine) and
+// exposed as nsgpu_p2p_dist_plan: every rank of a partitioned run must get the same lookaheads, window capacities
+// and exchange sizes — a mismatch would be a collective of different sizes (an RCCL hang), which the multi-process
+// CPU tests check (tests/test_dist_cpu.py).
+struct EnginePlan {
+  uint32_t qcap = 1, maxapps = 0, maxc = 3, wide = 0;
+  bool has_echo = false;
+  std::vector<uint32_t> napps, node_list;
+  std::vector<int32_t> sink;
+  int64_t tx_min = 0, lx = 0, send_ivl = 0;
+  int64_t lookahead[K_NKINDS], lookw[K_NKINDS];
+  // the setup-time events (this rank's, partitioned) and the bound of window 0 (the whole setup: every rank)
+  std::vector<uint64_t> its;
+  std::vector<uint32_t> iuid, ictx, ikind, ia;
+  Red red0{};
+  uint32_t n_init = 0, uid_init = 0;
+  uint64_t pool_cap = 0;
+  uint32_t capx = 0;  // partitioned: X2 records per peer per window
+  uint64_t x2b = 0;   // partitioned: X2 bytes per peer
+};
+
+static int plan_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, int rank, int nranks, uint64_t pool_cap,
+                       EnginePlan &P) {
+  if (!sc) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: null");
   const uint32_t N = sc->n_nodes, D = sc->n_devices, A = sc->n_apps;
   if (N == 0 || !sc->setup_kind || !sc->setup_index) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: empty");
   // ---- validation (host arrays) ----
-  uint32_t qcap = 1;
+  uint32_t &qcap = P.qcap;
+  qcap = 1;
   for (uint32_t d = 0; d < D; d++) {
     if (sc->dev_node[d] >= N || sc->dev_peer[d] >= D || sc->dev_peer[sc->dev_peer[d]] != d)
       return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: device %u: bad node/peer", d);
@@ -2065,10 +2084,13 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
                            (unsigned long long)j);
     }
   }
-  std::vector<uint32_t> napps(N + 1, 0);
-  std::vector<int32_t> sink(N, -1);
+  std::vector<uint32_t> &napps = P.napps;
+  std::vector<int32_t> &sink = P.sink;
+  napps.assign(N + 1, 0);
+  sink.assign(N, -1);
   uint32_t min_pkt = 0xffffffffu;
-  bool has_echo = false;
+  bool &has_echo = P.has_echo;
+  has_echo = false;
   int64_t echo_ivl = (int64_t)1 << 61;
   for (uint32_t a = 0; a < A; a++) {
     if (sc->app_node[a] >= N) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: app %u: bad node", a);
@@ -2108,10 +2130,12 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     }
     if (A > NSGPU_PKT_APP) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: more than 2^28 applications");
   }
-  uint32_t maxapps = 0;
+  uint32_t &maxapps = P.maxapps;
+  maxapps = 0;
   for (uint32_t n = 0; n < N; n++) maxapps = std::max(maxapps, napps[n + 1]);
   for (uint32_t n = 0; n < N; n++) napps[n + 1] += napps[n];
-  std::vector<uint32_t> node_list(A), fill(napps.begin(), napps.end() - 1);
+  std::vector<uint32_t> &node_list = P.node_list, fill(napps.begin(), napps.end() - 1);
+  node_list.assign(A, 0);
   for (uint32_t a = 0; a < A; a++) node_list[fill[sc->app_node[a]]++] = a;
   // ---- lookahead per event kind: the smallest delay a child of that kind can get ----
   const int64_t INFL = (int64_t)1 << 61;
@@ -2126,32 +2150,23 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   for (uint32_t a = 0; a < A; a++)
     if (sc->app_kind[a] == NSGPU_APP_ONOFF)
       send_ivl = std::min(send_ivl, seconds_to_ts((sc->app_pkt_size[a] * 8) / static_cast<double>(sc->app_rate_bps[a])));
-  nsgpu_p2p *h = new nsgpu_p2p();
-  h->sc = *sc;
-  h->app_kind.assign(sc->app_kind, sc->app_kind + A);
-  h->n_apps = A;
-  P2PDev &M = h->M;
-  memset(&M, 0, sizeof(M));
-  M.n_nodes = N;
-  M.n_devices = D;
-  M.n_apps = A;
-  M.n_dst = sc->n_dst;
-  M.qcap = qcap;
-  M.maxc = std::max(3u, 2 * maxapps);
-  for (int k = 0; k < K_NKINDS; k++) M.lookahead[k] = INFL;
-  M.lookahead[K_NODE_START] = 0;     // children at app start/stop times (may be 0)
-  M.lookahead[K_APPOBJ_START] = 0;
-  M.lookahead[K_APP_START] = 0;      // StartSending after OffTime (may be 0)
-  M.lookahead[K_START_SENDING] = 0;  // first send after residual-shortened interval
-  M.lookahead[K_STOP_SENDING] = 0;   // StartSending after OffTime
-  M.lookahead[K_SEND] = std::min(std::min(tx_min, send_ivl), echo_ivl);
-  M.lookahead[K_TX_COMPLETE] = tx_min;
-  M.lookahead[K_RECEIVE] = tx_min;
-  M.lookahead[K_FWD_UP_Q] = tx_min;  // UdpEchoServer reply: device children
+  P.tx_min = tx_min;
+  P.send_ivl = send_ivl;
+  P.maxc = std::max(3u, 2 * maxapps);
+  for (int k = 0; k < K_NKINDS; k++) P.lookahead[k] = INFL;
+  P.lookahead[K_NODE_START] = 0;     // children at app start/stop times (may be 0)
+  P.lookahead[K_APPOBJ_START] = 0;
+  P.lookahead[K_APP_START] = 0;      // StartSending after OffTime (may be 0)
+  P.lookahead[K_START_SENDING] = 0;  // first send after residual-shortened interval
+  P.lookahead[K_STOP_SENDING] = 0;   // StartSending after OffTime
+  P.lookahead[K_SEND] = std::min(std::min(tx_min, send_ivl), echo_ivl);
+  P.lookahead[K_TX_COMPLETE] = tx_min;
+  P.lookahead[K_RECEIVE] = tx_min;
+  P.lookahead[K_FWD_UP_Q] = tx_min;  // UdpEchoServer reply: device children
   // A datagram for a UDP echo endpoint is delivered by a queued zero-delay DoForwardUp (its handler
   // schedules): the window must then end at the delivering Receive's time, so that the DoForwardUp is
   // the next window's first event at that time.
-  if (has_echo) M.lookahead[K_RECEIVE] = 0;
+  if (has_echo) P.lookahead[K_RECEIVE] = 0;
   // Wide windows (nsgpu_p2p_win.h): an event on another node is at least one transmission
   // plus its channel delay away — Lx = min over devices of (smallest frame's tx time + delay) — and a
   // same-node TransmitComplete before the window's end runs inside the window (a local record), so only
@@ -2163,25 +2178,130 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
       if (sc->icmp) t = std::min(t, seconds_to_ts(static_cast<double>(56 + 2) * 8 / (double)sc->dev_bps[d]));
       lx = std::min(lx, t + sc->dev_delay_ns[d]);
     }
-  for (int k = 0; k < K_NKINDS; k++) M.lookw[k] = M.lookahead[k];
-  M.lookw[K_SEND] = std::min(std::min(lx, send_ivl), echo_ivl);
-  M.lookw[K_TX_COMPLETE] = lx;
-  M.lookw[K_RECEIVE] = has_echo ? 0 : lx;
-  M.lookw[K_FWD_UP_Q] = lx;
+  for (int k = 0; k < K_NKINDS; k++) P.lookw[k] = P.lookahead[k];
+  P.lookw[K_SEND] = std::min(std::min(lx, send_ivl), echo_ivl);
+  P.lookw[K_TX_COMPLETE] = lx;
+  P.lookw[K_RECEIVE] = has_echo ? 0 : lx;
+  P.lookw[K_FWD_UP_Q] = lx;
   {  // a node's pending local records are its busy devices' TransmitCompletes: at most its degree
     std::vector<uint32_t> deg(N, 0);
     uint32_t dmax = 0;
     for (uint32_t d = 0; d < D; d++) dmax = std::max(dmax, ++deg[sc->dev_node[d]]);
     const char *nw = getenv("NSGPU_P2P_NARROW");
     // (a chain of same-node TransmitCompletes inside a window is shorter than Lx / tx_min: LKD levels)
-    M.wide = (dmax <= (uint32_t)LQ && lx > tx_min && lx <= (int64_t)LKD * tx_min && lx < INFL &&
+    P.wide = (dmax <= (uint32_t)LQ && lx > tx_min && lx <= (int64_t)LKD * tx_min && lx < INFL &&
               !(nw && nw[0] == '1')) ? 1u : 0u;
     // partitioned: the ranks order each other's local records by their two order words (k_gtile), which are
     // exact for chains of at most 2 levels below a gen-0 event (the ancestor uid in X1Loc): the wide span is
     // kept below 3 tx_min, so a third level (3 transmissions after its gen-0 event) never falls in a window
-    if (owner && M.wide)
-      for (int k = 0; k < K_NKINDS; k++) M.lookw[k] = std::min<int64_t>(M.lookw[k], 3 * tx_min - 1);
+    if (owner && P.wide)
+      for (int k = 0; k < K_NKINDS; k++) P.lookw[k] = std::min<int64_t>(P.lookw[k], 3 * tx_min - 1);
   }
+  P.lx = lx;
+  // ---- setup-time events (node-list.cc:124-131, node.cc:111-145, default-simulator-impl.cc:179-183) ----
+  std::vector<uint64_t> &its = P.its;
+  std::vector<uint32_t> &iuid = P.iuid, &ictx = P.ictx, &ikind = P.ikind, &ia = P.ia;
+  uint32_t uid = sc->uid_first ? sc->uid_first : 4u;  // (DefaultSimulatorImpl: m_uid (4), :52-56)
+  if ((uint64_t)uid + sc->n_setup > UID_MAX_NEXT) {
+    return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: the setup calls' uids would pass 0xfffffffe");
+  }
+  for (uint32_t i = 0; i < sc->n_setup; i++) {
+    const uint32_t k = sc->setup_index[i];
+    switch (sc->setup_kind[i]) {
+      case NSGPU_SETUP_NODE:
+        if (k >= N) { return set_error(NSGPU_EINVAL, "setup: node %u", k); }
+        its.push_back(0); iuid.push_back(uid); ictx.push_back(k); ikind.push_back(K_NODE_START); ia.push_back(k);
+        break;
+      case NSGPU_SETUP_DEVICE:
+        if (k >= D) { return set_error(NSGPU_EINVAL, "setup: device %u", k); }
+        its.push_back(0); iuid.push_back(uid); ictx.push_back(sc->dev_node[k]); ikind.push_back(K_DEV_START); ia.push_back(k);
+        break;
+      case NSGPU_SETUP_APP:
+        if (k >= A) { return set_error(NSGPU_EINVAL, "setup: app %u", k); }
+        its.push_back(0); iuid.push_back(uid); ictx.push_back(sc->app_node[k]); ikind.push_back(K_APPOBJ_START); ia.push_back(k);
+        break;
+      case NSGPU_SETUP_NOOP:
+        if (k >= N) { return set_error(NSGPU_EINVAL, "setup: noop node %u", k); }
+        its.push_back(0); iuid.push_back(uid); ictx.push_back(k); ikind.push_back(K_DEV_START); ia.push_back(k);
+        break;
+      case NSGPU_SETUP_STOP:
+        if (sc->stop_ns < 0) { return set_error(NSGPU_EINVAL, "setup: negative stop"); }
+        its.push_back((uint64_t)sc->stop_ns); iuid.push_back(uid); ictx.push_back(NOCTX); ikind.push_back(K_STOP); ia.push_back(0);
+        break;
+      default:
+        break;  // consumes a uid, no event
+    }
+    uid++;
+  }
+  // reduction of the whole initial pending set: window 0 is bounded by red[1] on every rank
+  Red &red0 = P.red0;
+  red0 = Red{~0ull, ~0ull, ~0ull, 0, 0, ~0ull};
+  for (size_t i = 0; i < its.size(); i++) {
+    red0.tmin = std::min<uint64_t>(red0.tmin, its[i]);
+    red0.wend = std::min<uint64_t>(red0.wend, its[i] + (uint64_t)P.lookahead[ikind[i] & 0xffu]);
+    red0.wendw = std::min<uint64_t>(red0.wendw, its[i] + (uint64_t)P.lookw[ikind[i] & 0xffu]);
+    if ((ikind[i] & 0xffu) == K_STOP) {
+      red0.stopts = its[i];
+      red0.stopuid = iuid[i];
+    }
+  }
+  if (owner) {  // this rank's initial events (Simulator::Stop: rank 0)
+    size_t k = 0;
+    for (size_t i = 0; i < its.size(); i++) {
+      const bool mine = ictx[i] == NOCTX ? rank == 0 : owner[ictx[i]] == (uint32_t)rank;
+      if (!mine) continue;
+      its[k] = its[i], iuid[k] = iuid[i], ictx[k] = ictx[i], ikind[k] = ikind[i], ia[k] = ia[i];
+      k++;
+    }
+    its.resize(k), iuid.resize(k), ictx.resize(k), ikind.resize(k), ia.resize(k);
+  }
+  P.n_init = (uint32_t)its.size();
+  P.uid_init = uid;
+  P.pool_cap = pool_cap ? pool_cap : std::max<uint64_t>(4ull * P.n_init + 65536, 1ull << 20);
+  if (P.n_init > P.pool_cap) { return set_error(NSGPU_EINVAL, "pool_cap < setup events"); }
+  if (owner) {
+    {  // X2 capacity: the largest number of devices of one rank whose peer another rank owns
+      std::vector<uint32_t> cut((size_t)nranks * nranks, 0);
+      for (uint32_t d = 0; d < D; d++) {
+        const uint32_t p = owner[sc->dev_node[d]], q = owner[sc->dev_node[sc->dev_peer[d]]];
+        if (p != q) cut[(size_t)p * nranks + q]++;
+      }
+      uint32_t mx = 1;
+      for (uint32_t c : cut) mx = std::max(mx, c);
+      if (P.wide) mx *= 3;  // (wide: a device's gen-0 TransmitStart and up to two local ones, chain depth <= 2)
+      P.capx = std::min<uint32_t>((mx + 15) / 16 * 16, CAPX_MAX);
+      P.x2b = sizeof(X2Hdr) + sizeof(Ev) * (uint64_t)P.capx;
+    }
+  }
+  return NSGPU_OK;
+}
+
+// owner == null: the whole scenario on this device; otherwise the partition `rank` of `nranks`
+// (node n belongs to rank owner[n]).
+static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, int rank, int nranks,
+                         nsgpu_comm *comm, uint64_t pool_cap, uint64_t log_cap, nsgpu_p2p **out) {
+  if (!out) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: null");
+  *out = nullptr;
+  EnginePlan P;
+  if (int rcp = plan_engine(sc, owner, rank, nranks, pool_cap, P)) return rcp;
+  const uint32_t N = sc->n_nodes, D = sc->n_devices, A = sc->n_apps;
+  const uint32_t qcap = P.qcap;
+  const std::vector<uint32_t> &napps = P.napps, &node_list = P.node_list;
+  const std::vector<int32_t> &sink = P.sink;
+  nsgpu_p2p *h = new nsgpu_p2p();
+  h->sc = *sc;
+  h->app_kind.assign(sc->app_kind, sc->app_kind + A);
+  h->n_apps = A;
+  P2PDev &M = h->M;
+  memset(&M, 0, sizeof(M));
+  M.n_nodes = N;
+  M.n_devices = D;
+  M.n_apps = A;
+  M.n_dst = sc->n_dst;
+  M.qcap = qcap;
+  M.maxc = P.maxc;
+  for (int k = 0; k < K_NKINDS; k++) M.lookahead[k] = P.lookahead[k], M.lookw[k] = P.lookw[k];
+  M.wide = P.wide;
   // ---- scenario upload ----
   TRY(dupload(h, &M.dev_node, sc->dev_node, D));
   if (sc->route) {
@@ -2255,67 +2375,13 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.app_last_start, A));
   TRY(dalloc(h, &M.appc, A));
   TRY(dalloc(h, &M.node_tab, (size_t)N * NTAB));
-  // ---- setup-time events (node-list.cc:124-131, node.cc:111-145, default-simulator-impl.cc:179-183) ----
-  std::vector<uint64_t> its;
-  std::vector<uint32_t> iuid, ictx, ikind, ia;
-  uint32_t uid = sc->uid_first ? sc->uid_first : 4u;  // (DefaultSimulatorImpl: m_uid (4), :52-56)
-  if ((uint64_t)uid + sc->n_setup > UID_MAX_NEXT) {
-    nsgpu_p2p_destroy(h);
-    return set_error(NSGPU_EINVAL, "nsgpu_p2p_create: the setup calls' uids would pass 0xfffffffe");
-  }
-  for (uint32_t i = 0; i < sc->n_setup; i++) {
-    const uint32_t k = sc->setup_index[i];
-    switch (sc->setup_kind[i]) {
-      case NSGPU_SETUP_NODE:
-        if (k >= N) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "setup: node %u", k); }
-        its.push_back(0); iuid.push_back(uid); ictx.push_back(k); ikind.push_back(K_NODE_START); ia.push_back(k);
-        break;
-      case NSGPU_SETUP_DEVICE:
-        if (k >= D) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "setup: device %u", k); }
-        its.push_back(0); iuid.push_back(uid); ictx.push_back(sc->dev_node[k]); ikind.push_back(K_DEV_START); ia.push_back(k);
-        break;
-      case NSGPU_SETUP_APP:
-        if (k >= A) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "setup: app %u", k); }
-        its.push_back(0); iuid.push_back(uid); ictx.push_back(sc->app_node[k]); ikind.push_back(K_APPOBJ_START); ia.push_back(k);
-        break;
-      case NSGPU_SETUP_NOOP:
-        if (k >= N) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "setup: noop node %u", k); }
-        its.push_back(0); iuid.push_back(uid); ictx.push_back(k); ikind.push_back(K_DEV_START); ia.push_back(k);
-        break;
-      case NSGPU_SETUP_STOP:
-        if (sc->stop_ns < 0) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "setup: negative stop"); }
-        its.push_back((uint64_t)sc->stop_ns); iuid.push_back(uid); ictx.push_back(NOCTX); ikind.push_back(K_STOP); ia.push_back(0);
-        break;
-      default:
-        break;  // consumes a uid, no event
-    }
-    uid++;
-  }
-  // reduction of the whole initial pending set: window 0 is bounded by red[1] on every rank
-  Red red0{~0ull, ~0ull, ~0ull, 0, 0, ~0ull};
-  for (size_t i = 0; i < its.size(); i++) {
-    red0.tmin = std::min<uint64_t>(red0.tmin, its[i]);
-    red0.wend = std::min<uint64_t>(red0.wend, its[i] + (uint64_t)M.lookahead[ikind[i] & 0xffu]);
-    red0.wendw = std::min<uint64_t>(red0.wendw, its[i] + (uint64_t)M.lookw[ikind[i] & 0xffu]);
-    if ((ikind[i] & 0xffu) == K_STOP) {
-      red0.stopts = its[i];
-      red0.stopuid = iuid[i];
-    }
-  }
-  if (owner) {  // this rank's initial events (Simulator::Stop: rank 0)
-    size_t k = 0;
-    for (size_t i = 0; i < its.size(); i++) {
-      const bool mine = ictx[i] == NOCTX ? rank == 0 : owner[ictx[i]] == (uint32_t)rank;
-      if (!mine) continue;
-      its[k] = its[i], iuid[k] = iuid[i], ictx[k] = ictx[i], ikind[k] = ikind[i], ia[k] = ia[i];
-      k++;
-    }
-    its.resize(k), iuid.resize(k), ictx.resize(k), ikind.resize(k), ia.resize(k);
-  }
-  M.n_init = (uint32_t)its.size();
-  M.uid_init = uid;
-  M.pool_cap = pool_cap ? pool_cap : std::max<uint64_t>(4ull * M.n_init + 65536, 1ull << 20);
-  if (M.n_init > M.pool_cap) { nsgpu_p2p_destroy(h); return set_error(NSGPU_EINVAL, "pool_cap < setup events"); }
+  const std::vector<uint64_t> &its = P.its;
+  const std::vector<uint32_t> &iuid = P.iuid, &ictx = P.ictx, &ikind = P.ikind, &ia = P.ia;
+  const uint32_t uid = P.uid_init;
+  const Red red0 = P.red0;
+  M.n_init = P.n_init;
+  M.uid_init = P.uid_init;
+  M.pool_cap = P.pool_cap;
   for (int b = 0; b < 2; b++) {
     TRY(dalloc(h, &M.ev_ts[b], M.pool_cap));
     TRY(dalloc(h, &M.ev_uid[b], M.pool_cap));
@@ -2411,18 +2477,8 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     M.x1_send = M.x1_recv + (size_t)rank * X1B;  // (in place: NCCL moves only the other ranks' slots)
     if ((uint64_t)nranks * WCAP * M.maxc >= (1ull << 32))  // (k_gtile's packed child prefix)
       return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: %d ranks x %u children per event", nranks, M.maxc);
-    {  // X2 capacity: the largest number of devices of one rank whose peer another rank owns
-      std::vector<uint32_t> cut((size_t)nranks * nranks, 0);
-      for (uint32_t d = 0; d < D; d++) {
-        const uint32_t p = owner[sc->dev_node[d]], q = owner[sc->dev_node[sc->dev_peer[d]]];
-        if (p != q) cut[(size_t)p * nranks + q]++;
-      }
-      uint32_t mx = 1;
-      for (uint32_t c : cut) mx = std::max(mx, c);
-      if (M.wide) mx *= 3;  // (wide: a device's gen-0 TransmitStart and up to two local ones, chain depth <= 2)
-      M.capx = std::min<uint32_t>((mx + 15) / 16 * 16, CAPX_MAX);
-      M.x2b = sizeof(X2Hdr) + sizeof(Ev) * (uint64_t)M.capx;
-    }
+    M.capx = P.capx;
+    M.x2b = P.x2b;
     TRY(dalloc(h, &M.x2_send, M.x2b * nranks));
     TRY(dalloc(h, &M.x2_recv, M.x2b * nranks));
     TRY(dalloc(h, &M.gacc, 4 * (size_t)NACC));
@@ -2513,6 +2569,38 @@ extern "C" int nsgpu_p2p_create_dist(const nsgpu_p2p_scenario *sc, const uint32_
   if (comm && (comm->nranks != nranks || comm->rank != rank))
     return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: communicator is rank %d of %d", comm->rank, comm->nranks);
   return create_engine(sc, node_owner, rank, nranks, comm, pool_cap, log_cap, out);
+}
+
+extern "C" int nsgpu_p2p_dist_plan(const nsgpu_p2p_scenario *sc, const uint32_t *node_owner, int rank, int nranks,
+                                   uint64_t pool_cap, nsgpu_p2p_plan *out) {
+  if (!sc || !out) return set_error(NSGPU_EINVAL, "nsgpu_p2p_dist_plan: null");
+  static_assert(K_NKINDS <= 16, "nsgpu_p2p_plan holds 16 kinds");
+  EnginePlan P;
+  if (int rc = plan_engine(sc, node_owner, rank, nranks, pool_cap, P)) return rc;
+  memset(out, 0, sizeof(*out));
+  out->wide = P.wide;
+  out->maxc = P.maxc;
+  out->wcap = WCAP;
+  out->xlcap = XLCAP;
+  if (node_owner) {
+    out->x0_bytes = X0B;
+    out->x1_bytes = X1B;
+    out->x2_bytes = P.x2b;
+    out->x2_records = P.capx;
+  }
+  out->n_kinds = K_NKINDS;
+  for (int k = 0; k < K_NKINDS; k++) out->lookahead[k] = P.lookahead[k], out->lookw[k] = P.lookw[k];
+  out->tx_min = P.tx_min;
+  out->lx = P.lx;
+  out->red0_tmin = P.red0.tmin;
+  out->red0_wend = P.red0.wend;
+  out->red0_wendw = P.red0.wendw;
+  out->stop_ts = P.red0.stopts;
+  out->stop_uid = P.red0.stopuid;
+  out->uid_init = P.uid_init;
+  out->n_init = P.n_init;
+  out->pool_cap = P.pool_cap;
+  return NSGPU_OK;
 }
 
 // Restores the initial (post-setup) state on the device, asynchronously.

@@ -169,6 +169,7 @@ SIGNATURES = {
     "nsgpu_comm_init": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "nsgpu_comm_destroy": (C.c_int, [_vp]),
     "nsgpu_p2p_create_dist": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _vp, _u64, _u64, C.POINTER(C.c_void_p)]),
+    "nsgpu_p2p_dist_plan": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _u64, _vp]),
     "nsgpu_p2p_group_create": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p)]),
     "nsgpu_p2p_group_reset": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_group_run": (C.c_int, [_vp, _vp]),

@@ -677,6 +677,53 @@ class Comm:
             pass
 
 
+class Plan(C.Structure):
+    """nsgpu_p2p_plan (include/nsgpu.h): the constants a rank's partitioned engine is built from."""
+    _fields_ = [("wide", C.c_uint32), ("maxc", C.c_uint32), ("wcap", C.c_uint32), ("xlcap", C.c_uint32),
+                ("x0_bytes", C.c_uint64), ("x1_bytes", C.c_uint64), ("x2_bytes", C.c_uint64),
+                ("x2_records", C.c_uint32), ("n_kinds", C.c_uint32),
+                ("lookahead", C.c_int64 * 16), ("lookw", C.c_int64 * 16), ("tx_min", C.c_int64), ("lx", C.c_int64),
+                ("red0_tmin", C.c_uint64), ("red0_wend", C.c_uint64), ("red0_wendw", C.c_uint64),
+                ("stop_ts", C.c_uint64), ("stop_uid", C.c_uint32), ("uid_init", C.c_uint32),
+                ("n_init", C.c_uint32), ("pad", C.c_uint32), ("pool_cap", C.c_uint64)]
+
+
+# the plan's fields that may differ between ranks (each rank's own setup events and pool)
+PLAN_PER_RANK = ("n_init", "pool_cap", "pad")
+
+
+def dist_plan(scenario, owner, rank, nranks, pool_cap=0):
+    """nsgpu_p2p_dist_plan (host only, no device): the sizes and constants rank `rank`'s engine feeds its
+    collectives — X0 / X1 / X2 bytes, X2 records per peer, window capacities, lookaheads, window 0's bound —
+    as a dict (arrays as lists).  owner None: the single engine's plan."""
+    s = scenario.c_struct()
+    own = None
+    if owner is not None:
+        own = np.ascontiguousarray(owner, dtype=np.uint32)
+        if len(own) != s.n_nodes:
+            raise ValueError("owner: one rank per node")
+    pl = Plan()
+    nsgpu.check(nsgpu.lib().nsgpu_p2p_dist_plan(C.byref(s), own.ctypes.data if own is not None else None, rank,
+                                                 nranks, pool_cap, C.byref(pl)))
+    out = {}
+    for f, _t in Plan._fields_:
+        v = getattr(pl, f)
+        out[f] = list(v)[:pl.n_kinds] if f in ("lookahead", "lookw") else int(v)
+    return out
+
+
+def plan_mismatch(plans):
+    """The collective-shaping fields on which a list of per-rank plans disagree ({} when all agree)."""
+    bad = {}
+    for f in plans[0]:
+        if f in PLAN_PER_RANK:
+            continue
+        vals = [p[f] for p in plans]
+        if any(v != vals[0] for v in vals[1:]):
+            bad[f] = vals
+    return bad
+
+
 class DistEngine(Engine):
     """Partition `rank` of `nranks` of a scenario (nsgpu_p2p_create_dist): the nodes with
     owner[n] == rank.  With a Comm it runs on its own (one process per GPU, RCCL collectives);

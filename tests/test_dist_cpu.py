@@ -115,6 +115,72 @@ def test_gloo_world2_orchestration():
     mp.spawn(_worker, args=(2, _free_port()), nprocs=2, join=True)
 
 
+# ---------------------------------------------------------------- the ranks' engine plans, one process each
+def _plan_worker(rank, world, port, workload, leaves, skew):
+    """One rank of a partitioned run's bootstrap as bench.py does it (bench.dist_scenario + bench.check_plans, the
+    RCCL id broadcast), minus the GPU calls: every rank builds its scenario and owner map itself and computes its
+    engine plan (nsgpu_p2p_dist_plan, the host half of nsgpu_p2p_create_dist).  skew: rank 1 builds a different
+    grid (a rank whose plan disagrees must make every rank fail before any collective)."""
+    import sys
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if repo not in sys.path:
+        sys.path.insert(0, repo)
+    import torch.distributed as td
+    import bench
+    td.init_process_group("gloo")
+    try:
+        args = bench.parser().parse_args(["--workload", workload, "--dumbbell-leaves", str(leaves)])
+        if skew and rank == 1:
+            args.grid = 64
+        sc, owner = bench.dist_scenario(args, workload, rank, world)
+        try:
+            plan = bench.check_plans(sc, owner, rank, world, td)
+        except RuntimeError as e:
+            assert skew and "plans differ" in str(e), e
+            return
+        assert not skew, "a skewed rank went unnoticed"
+        uid = [os.urandom(128) if rank == 0 else None]  # (bench: rank 0's RCCL unique id to every rank)
+        td.broadcast_object_list(uid, src=0)
+        plans = [None] * world
+        td.all_gather_object(plans, plan)
+        assert p2p.plan_mismatch(plans) == {}
+        # what the collectives carry: X0 16 B, X1 the fixed summary, X2 at least the largest cut between two
+        # ranks (x3 for wide windows) per peer, at most CAPX_MAX records
+        s = sc.c_struct()
+        dn, dp = s._keep["dev_node"], s._keep["dev_peer"]
+        po, qo = owner[dn], owner[dn[dp]]
+        cut = np.zeros((world, world), np.int64)
+        np.add.at(cut, (po[po != qo], qo[po != qo]), 1)
+        need = int(cut.max()) * (3 if plan["wide"] else 1)
+        assert plan["x0_bytes"] == 16 and plan["x1_bytes"] > 0
+        assert plan["x2_records"] == min((need + 15) // 16 * 16, 1024)
+        assert plan["x2_bytes"] == 16 + 40 * plan["x2_records"]  # (X2Hdr + 40-B event records)
+        # every setup event is exactly one rank's (Simulator::Stop rank 0's), window 0's bound the whole setup's
+        whole = p2p.dist_plan(sc, None, 0, 1)
+        assert sum(p["n_init"] for p in plans) == whole["n_init"]
+        for f in ("red0_tmin", "red0_wend", "stop_ts", "uid_init", "lookahead"):
+            assert plan[f] == whole[f], f
+        td.barrier()
+    finally:
+        td.destroy_process_group()
+
+
+@pytest.mark.parametrize("workload,world,leaves,skew", [
+    ("p2p-grid", 2, 0, False),       # config 4 weak-scaled: 128 x 256 in 2 row bands
+    ("p2p-grid", 4, 0, False),       # 128 x 512 in 4
+    ("dumbbell", 4, 499_999, False),  # config 5 at BASELINE size: 1,000,000 nodes, simple-distributed.cc's owners
+    ("dumbbell", 2, 20_000, False),
+    ("p2p-grid", 2, 0, True),        # rank 1 builds another grid: both ranks fail before any collective
+])
+def test_gloo_ranks_build_equal_plans(workload, world, leaves, skew):
+    """a per-rank size mismatch is an RCCL hang at N > 1 that no single-process test sees.
+    Each gloo process builds the partitioned scenario on its own, and the ranks' plans must agree field for field
+    (except each rank's own setup events and pool)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_plan_worker, args=(world, _free_port(), workload, leaves or 499_999, skew), nprocs=world, join=True)
+
+
 def test_wifi_receiver_partitions():
     """The Wi-Fi split's receiver blocks (wifi.partitions, bench.py wifi-grid --gpus N): contiguous,
     covering every phy once, balanced, empty blocks allowed when there are more partitions than phys."""
