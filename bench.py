@@ -838,7 +838,10 @@ def main():
         # whole run per step, digest-checked against the oracle like the primary
         secondary = []
         if world == 1 and not partitioned and args.workload == "p2p-grid" and not args.no_secondary:
-            for name in ("wifi-grid", "wifi-loop", "dumbbell"):
+            names = os.environ.get("NSGPU_BENCH_SECONDARIES", "wifi-grid,wifi-loop,dumbbell").split(",")
+            if os.environ.get("NSGPU_BENCH_PRIMARY_CLOSE") == "1":  # (diagnostic)
+                wl.close()
+            for name in names:
                 wl2 = WORKLOADS[name](args, stream.handle)
                 el2, kms2 = measure(wl2, args.secondary_steps, 1)
                 ev2, dg2, ex2 = wl2.result()

@@ -1699,6 +1699,13 @@ extern "C" int nsgpu_wifil_destroy(nsgpu_wifil *h) {
   return NSGPU_OK;
 }
 
+// (hipDeviceGetStreamPriorityRange: greatest = the most urgent, a smaller number)
+static int wl_prio(bool high) {
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+  return high ? greatest : least;
+}
+
 extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out) {
   if (!c || !out || c->n_phy <= 0 || !c->x || !c->y || !c->z || !c->channel || !c->node)
     return set_error(NSGPU_EINVAL, "nsgpu_wifil_create: bad config");
@@ -1800,8 +1807,12 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
       hipHostMalloc((void **)&h->h_pend, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void **)&h->h_digtot, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&h->d_digtot, h->h_digtot, 0) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->s2, hipStreamNonBlocking) != hipSuccess ||
+      // the PHY's epochs on a high-priority stream, the order behind them on a low-priority one: streams of
+      // different priorities never share a hardware queue (with GPU_MAX_HW_QUEUES = 4 and other engines' streams
+      // alive, two normal streams could land on one queue, and the order's ~55 us would then run in line with
+      // the next epoch: 75 -> 112 us an epoch, VERDICT r05 item 2, scripts/wifil_interference.py)
+      hipStreamCreateWithPriority(&h->s, hipStreamNonBlocking, wl_prio(true)) != hipSuccess ||
+      hipStreamCreateWithPriority(&h->s2, hipStreamNonBlocking, wl_prio(false)) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_fin[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_fin[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_ord[0], hipEventDisableTiming) != hipSuccess ||

@@ -37,6 +37,8 @@ def main():
     args = args_ns()
     stream = nsgpu.Stream()
     stages = sys.argv[1:] or ["fresh", "p2p", "profile", "close_p2p", "wifi_grid", "dumbbell"]
+    if stages[0] == "nofresh":  # (the first loop only after the next stage: stream creation order as in bench.py)
+        stages = stages[1:]
     g = None
     for st in stages:
         if st == "fresh":
@@ -44,6 +46,13 @@ def main():
         elif st == "p2p":
             g = bench.P2PGrid(args, stream.handle)
             g.step()
+            stream.sync()
+        elif st == "p2p_norun":  # created, never run
+            g = bench.P2PGrid(args, stream.handle)
+        elif st == "p2p6":  # the bench primary's warmup + 5 timed steps
+            g = bench.P2PGrid(args, stream.handle)
+            for _ in range(6):
+                g.step()
             stream.sync()
         elif st == "profile":
             g.roofline(50.0, 7_599_361)
@@ -64,6 +73,23 @@ def main():
             d.step()
             stream.sync()
             d.close()
+        elif st == "cpu_p2p":  # the p2p-grid line's CPU baseline (the oracle's full run, one host core)
+            g = g or bench.P2PGrid(args, stream.handle)
+            g.cpu_baseline()
+        elif st == "cpu_wifi":  # the wifi-grid secondary's CPU baseline (oracle sample + a GPU sample engine)
+            w = bench.WifiGrid(args, stream.handle)
+            w.step()
+            stream.sync()
+            w.cpu_baseline()
+            w.close()
+        elif st == "cpu_oracle_wifi":  # only its oracle part
+            import wifi
+            import numpy as np
+            nsref = bench.oracle()
+            sc = wifi.wifi_grid(n_side=100, stop_s=0.1)
+            stt = wifi.WifiStats()
+            nsref.wifi_run(sc.c_struct(), stt, np.zeros(sc.n_phy, wifi.PHY_COUNTERS_DTYPE),
+                           np.zeros(len(sc.tx), np.uint32), wifi.END_RECORD_DTYPE)
         elif st == "probe":
             print("probe", nsgpu.probe_latency(), flush=True)
         loop(f"after {st}", args, stream)
