@@ -217,6 +217,23 @@ int nsgpu_wifil_set_position(nsgpu_wifil *h, uint32_t phy, double x, double y, d
 int nsgpu_wifil_read_ends(nsgpu_wifil *h, nsgpu_wifil_end *out, uint64_t cap, uint64_t *n);  /* since last read */
 int nsgpu_wifil_read_phys(nsgpu_wifil *h, nsgpu_wifi_phy_counters *out);                    /* n_phy */
 int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_ts);
+/* The EndReceive hand-back (see nsgpu_sim_wifi_set_end_handler): phys whose EndReceives the host takes back, and
+ * between advances the next one among them — a pending EndReceive that is not cancelled (found: its key and phy)
+ * and ts_potential, the earliest time an EndReceive not yet scheduled could fall: a pending Receive strong enough
+ * to sync (rxPowerW > the ED threshold, yans-wifi-phy.cc:461-471) ends at its arrival + duration (~0: none). */
+typedef struct nsgpu_wifil_next {
+  uint64_t ts;
+  uint32_t uid, phy;
+  int32_t found, pad_;
+  uint64_t ts_potential;
+} nsgpu_wifil_next;
+int nsgpu_wifil_listen(nsgpu_wifil *h, uint32_t phy, int on);
+/* YansWifiChannel::Send's ScheduleWithContext calls for one SendPacket of `sender` (yans-wifi-channel.cc:77-115),
+ * host only: the receivers (every other phy on the sender's channel number, in m_phyList order), their Receive uids
+ * (uid_base + place) and contexts (their device's node); *n = the count (entries past cap are not written). */
+int nsgpu_wifil_send_plan(const nsgpu_wifil_config *cfg, uint32_t sender, uint32_t uid_base, uint32_t *rx_phy,
+                          uint32_t *rx_uid, uint32_t *rx_ctx, uint64_t cap, uint64_t *n);
+int nsgpu_wifil_next_end(nsgpu_wifil *h, nsgpu_wifil_next *out);
 
 /* ---------------- GPU-resident bench-simulator churn (config 1) ----------------
  * Runs utils/bench-simulator.cc's RunBench + Simulator::Run (bench-simulator.cc:79-127) over
@@ -349,6 +366,18 @@ int nsgpu_sim_wifi_send(nsgpu_sim *s, uint32_t phy, uint32_t size, double dbm, u
 int nsgpu_sim_wifi_state(nsgpu_sim *s, uint32_t phy, nsgpu_wifil_phy_state *out);
 /* a host closure's MobilityModel::SetPosition of phy's node (nsgpu_wifil_set_position on the attached PHY) */
 int nsgpu_sim_wifi_set_position(nsgpu_sim *s, uint32_t phy, double x, double y, double z);
+/* EndReceive hand-back (YansWifiPhy::EndReceive, yans-wifi-phy.cc:770-799): for every phy marked with
+ * nsgpu_sim_wifi_listen, the runtime stops the device AT each of the phy's EndReceives (the event itself runs on
+ * the device: CalculateSnrPer, the state switch) and calls fn (user, &end) right there in the (ts, uid) order,
+ * with Now () = its time, the current uid = its uid and the context = the phy's node — where the reference makes
+ * its m_random draw (:783) and calls the MAC (SwitchFromRxEndOk / Error -> the receive callbacks), so the
+ * callback's Schedule / SendPacket calls take the uids and times the reference's would.  A cancelled EndReceive
+ * (a SendPacket during RX, :504-508) is dispatched without a call, as the reference's cancelled EventImpl.  An
+ * EndReceive scheduled inside an epoch is caught too: the runtime never advances past the earliest time a pending
+ * Receive of a listened phy could end (nsgpu_wifil_next_end's ts_potential) before it knows whether it synced. */
+typedef void (*nsgpu_wifi_end_fn)(void *user, const nsgpu_wifil_end *end);
+int nsgpu_sim_wifi_set_end_handler(nsgpu_sim *s, nsgpu_wifi_end_fn fn, void *user);
+int nsgpu_sim_wifi_listen(nsgpu_sim *s, uint32_t phy, int on);
 
 /* ---------------- GPU-resident point-to-point subset (configs 2, 4) ----------------
  * Replaces, for a topology of PointToPointNetDevices, the handler chain

@@ -25,8 +25,14 @@ inline int uid_range_error(const char *where) {
 // against a start set with nsgpu_sim_set_next_uid.
 }  // namespace nsgpu
 struct nsgpu_p2p;
+struct nsgpu_wifil;
+struct nsgpu_wifil_end;
 namespace nsgpu {
 uint32_t p2p_first_uid(const nsgpu_p2p *h);
+// The closed-loop PHY's last epoch's EndReceive with this uid (false: none), and a phy's node (the runtime's
+// EndReceive hand-back, nsgpu_sim_wifi_set_end_handler).
+bool wifil_epoch_end(const nsgpu_wifil *h, uint32_t uid, nsgpu_wifil_end *out);
+uint32_t wifil_node(const nsgpu_wifil *h, uint32_t phy);
 }  // namespace nsgpu
 
 #define NSGPU_HIP(call)                                                                              \

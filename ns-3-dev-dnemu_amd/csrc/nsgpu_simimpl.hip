@@ -51,6 +51,10 @@ struct nsgpu_sim {
   uint32_t uid = 4;
   uint32_t uid_first = 4;  // m_uid before the program's first Schedule call (nsgpu_sim_set_next_uid)
   bool uid_set = false;    // uid_first was set explicitly (an attached engine must start there too)
+  nsgpu_wifi_end_fn wifi_end_fn = nullptr;  // the EndReceive hand-back (nsgpu_sim_wifi_set_end_handler)
+  void *wifi_end_user = nullptr;
+  uint64_t wifi_listen_n = 0;                // phys listened to
+  std::vector<uint8_t> lis_on;
   bool uid_spent = false;  // a Schedule call hit the uid limit (a closure's call fails; the run then fails too)
   uint32_t cur_uid = 0;
   uint64_t cur_ts = 0;
@@ -378,20 +382,58 @@ static int pop_window(nsgpu_sim *s, nsgpu_event *out, uint32_t cap, uint32_t *n,
     return set_error(NSGPU_ESTATE, "Run: the attached engine dispatched Simulator::Stop; resuming with %llu host "
                                    "event(s) pending is not supported", (unsigned long long)q->size);
   if (s->wifi) {  // the PHY's events below the next host event's key, then that host event (one per window)
-    bool have = false;
-    if (q->size) {
-      if (!nsgpu::sched_next(q, &e, false, &rc)) return rc ? rc : set_error(NSGPU_ESTATE, "pop_window: lost events");
-      have = true;
+    for (;;) {
+      bool have = false;
+      if (q->size) {
+        if (!nsgpu::sched_next(q, &e, false, &rc)) return rc ? rc : set_error(NSGPU_ESTATE, "pop_window: lost events");
+        have = true;
+      }
+      uint64_t bts = have ? e.ts : ~0ull;
+      uint32_t buid = have ? e.uid : 0u;
+      // the EndReceive hand-back: a listened phy's next EndReceive before the host event runs inside the order
+      // (its own epoch, through its key), and the device never runs past a time where one not yet scheduled could
+      // fall (a pending Receive that may sync) before that Receive has run
+      bool handback = false, partial = false;
+      nsgpu_wifil_next nx;
+      if (s->wifi_end_fn && s->wifi_listen_n) {
+        if ((rc = nsgpu_wifil_next_end(s->wifi, &nx))) return rc;
+        const bool before_host = !have || nx.ts < e.ts || (nx.ts == e.ts && nx.uid < e.uid);
+        if (nx.found && before_host && nx.ts <= nx.ts_potential) {  // (a later sync's uid is larger: at an equal ts
+          bts = nx.ts;                                              //  the known one is first)
+          buid = nx.uid + 1u;
+          handback = true;
+        } else if (nx.ts_potential != ~0ull && (!have || nx.ts_potential < e.ts) &&
+                   (!nx.found || nx.ts_potential < nx.ts)) {  // (a host event at that ts was scheduled before the sync)
+          bts = nx.ts_potential;
+          buid = 0u;
+          partial = true;
+        }
+      }
+      rc = nsgpu_wifil_advance(s->wifi, bts, buid, &s->uid, &s->dispatched, &s->digest, s->log_ts, s->log_uid,
+                               s->log_ctx, s->log_cap);
+      if (rc == NSGPU_ERANGE) s->uid_spent = true;  // (sticky: the epoch's EndReceives would take wrapped uids)
+      if (rc) return rc;
+      if (handback) {
+        nsgpu_wifil_end end;
+        if (!nsgpu::wifil_epoch_end(s->wifi, nx.uid, &end))
+          return set_error(NSGPU_ESTATE, "EndReceive hand-back: EndReceive %u of phy %u was not dispatched", nx.uid, nx.phy);
+        if (!(end.flags & NSGPU_WIFI_END_CANCELLED)) {
+          s->cur_ts = end.ts;  // (YansWifiPhy::EndReceive's Now (), its EventImpl's uid and context)
+          s->cur_uid = end.uid;
+          s->cur_ctx = nsgpu::wifil_node(s->wifi, end.phy);
+          s->wifi_end_fn(s->wifi_end_user, &end);
+          if (s->uid_spent) return nsgpu::uid_range_error("nsgpu_sim: EndReceive hand-back");
+        }
+        continue;
+      }
+      if (partial) continue;
+      if (!have) return NSGPU_OK;
+      if ((rc = nsgpu::sched_remove_next1(q, &e))) return rc;
+      out[0] = e;
+      s->win.push_back(e);
+      *n = 1;
+      return NSGPU_OK;
     }
-    rc = nsgpu_wifil_advance(s->wifi, have ? e.ts : ~0ull, have ? e.uid : 0u, &s->uid, &s->dispatched, &s->digest,
-                             s->log_ts, s->log_uid, s->log_ctx, s->log_cap);
-    if (rc == NSGPU_ERANGE) s->uid_spent = true;  // (sticky: the epoch's EndReceives would take wrapped uids)
-    if (rc || !have) return rc;
-    if ((rc = nsgpu::sched_remove_next1(q, &e))) return rc;
-    out[0] = e;
-    s->win.push_back(e);
-    *n = 1;
-    return NSGPU_OK;
   }
   if (s->p2p && !s->ended) {
     bool have = false;
@@ -654,6 +696,26 @@ int nsgpu_sim_wifi_send(nsgpu_sim *s, uint32_t phy, uint32_t size, double dbm, u
   rc = nsgpu_wifil_send(s->wifi, s->cur_ts, s->uid, phy, size, dbm, modclass, rate, bw, preamble);
   if (rc) return rc;
   s->uid += n;
+  return NSGPU_OK;
+}
+
+int nsgpu_sim_wifi_set_end_handler(nsgpu_sim *s, nsgpu_wifi_end_fn fn, void *user) {
+  if (!s) return set_error(NSGPU_EINVAL, "nsgpu_sim_wifi_set_end_handler: null");
+  s->wifi_end_fn = fn;
+  s->wifi_end_user = user;
+  return NSGPU_OK;
+}
+
+int nsgpu_sim_wifi_listen(nsgpu_sim *s, uint32_t phy, int on) {
+  if (!s || !s->wifi) return set_error(NSGPU_ESTATE, "nsgpu_sim_wifi_listen: no Wi-Fi PHY attached");
+  if (s->lis_on.size() <= phy) s->lis_on.resize((size_t)phy + 1, 0);
+  const uint8_t v = on ? 1 : 0;
+  int rc = nsgpu_wifil_listen(s->wifi, phy, on);
+  if (rc) return rc;
+  if (s->lis_on[phy] != v) {
+    s->wifi_listen_n += v ? 1 : (uint64_t)-1;
+    s->lis_on[phy] = v;
+  }
   return NSGPU_OK;
 }
 

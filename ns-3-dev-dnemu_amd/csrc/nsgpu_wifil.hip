@@ -132,6 +132,8 @@ struct WDev {
   unsigned long long *edig;  // every ordered epoch's digest terms, summed on the device (k_wl_rank)
   uint64_t sync_cap, ev_cap, end_cap, ck_cap;
   uint64_t ev_scap;  // events per stripe (stripe s holds ev[s * ev_scap, s * ev_scap + evc[s * EV_STRIDE]))
+  const uint32_t *lis;  // the phys whose EndReceives the host takes back (nsgpu_wifil_listen), nlis of them
+  uint32_t nlis, pad_lis;
 };
 // The epoch's dispatched events are appended to EV_STRIPES lists (phy j's to stripe j % EV_STRIPES): one
 // counter a phy's event would serialize ~10^4 atomics an epoch on one line.
@@ -1588,6 +1590,56 @@ __global__ __launch_bounds__(256) void k_wl_pending(const WDev D, unsigned long 
   }
 }
 
+// The EndReceive hand-back (nsgpu_wifil_next_end): over the listened phys, the smallest key of a pending EndReceive
+// that is not cancelled (its uid assigned: every epoch's close gives the syncs theirs), and the earliest time at
+// which one not yet scheduled could fall — a pending Receive (queued, or a staged SendPacket's) strong enough to
+// sync (rxPowerW > the ED threshold, yans-wifi-phy.cc:461) ends its EndReceive at arrival + duration (:466-471).
+// One block; out: [0] ts, [1] uid | phy << 32 (~0: none), [2] the potential ts (~0: none).
+__global__ __launch_bounds__(256) void k_wl_nextend(const WDev D, uint32_t nsend, unsigned long long *out) {
+  __shared__ uint64_t s_ts[256], s_tp[256];
+  __shared__ uint32_t s_uid[256], s_phy[256];
+  const uint32_t tid = threadIdx.x;
+  uint64_t bts = ~0ull, tp = ~0ull;
+  uint32_t buid = NONE, bphy = NONE;
+  for (uint32_t i = tid; i < D.nlis; i += 256) {
+    const uint32_t j = D.lis[i];
+    for (int q = 0; q < LPE_CAP; q++) {
+      const LPe &p = D.pe[(uint64_t)j * LPE_CAP + q];
+      if (p.used && !p.can && p.euid != NONE && (p.ts < bts || (p.ts == bts && p.euid < buid))) {
+        bts = p.ts;
+        buid = p.euid;
+        bphy = j;
+      }
+    }
+    const LPhy P = D.ps[j];
+    const LRx *rq = D.rq + (uint64_t)j * (D.rq_mask + 1);
+    for (uint32_t k = 0; k < P.rq_len; k++) {
+      const LRx r = rq[(P.rq_head + k) & D.rq_mask];
+      if (r.w > D.edW && r.at + (uint64_t)r.dur < tp) tp = r.at + (uint64_t)r.dur;
+    }
+    for (uint32_t k = 0; k < nsend; k++) {
+      const LRx r = D.rxb[(uint64_t)k * D.nphy + j];
+      if (r.at != ~0ull && r.w > D.edW && r.at + (uint64_t)r.dur < tp) tp = r.at + (uint64_t)r.dur;
+    }
+  }
+  s_ts[tid] = bts, s_uid[tid] = buid, s_phy[tid] = bphy, s_tp[tid] = tp;
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      const uint32_t u = tid + o;
+      if (s_ts[u] < s_ts[tid] || (s_ts[u] == s_ts[tid] && s_uid[u] < s_uid[tid]))
+        s_ts[tid] = s_ts[u], s_uid[tid] = s_uid[u], s_phy[tid] = s_phy[u];
+      if (s_tp[u] < s_tp[tid]) s_tp[tid] = s_tp[u];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    out[0] = s_ts[0];
+    out[1] = s_uid[0] == NONE ? ~0ull : ((unsigned long long)s_phy[0] << 32) | s_uid[0];
+    out[2] = s_tp[0];
+  }
+}
+
 // int64x64_t::Invert (int64x64-128.cc:119-134) with Divu (:70-92) and MulByInvert (:94-118), on the host.
 u128 umul_by_invert(u128 a, u128 b) {
   const u128 ah = a >> 64, bh = b >> 64, al = a & (u128)~0ull, bl = b & (u128)~0ull;
@@ -1649,6 +1701,12 @@ struct nsgpu_wifil {
   unsigned long long *d_pend = nullptr, *h_pend = nullptr;
   std::vector<LEv> ev;
   std::vector<nsgpu_wifil_end> ends, ends_epoch;
+  // the EndReceive hand-back: listened phys (a flag each, and the list the device scans), each phy's node
+  std::vector<uint8_t> lis_on;
+  std::vector<uint32_t> lis_list, node_h;
+  bool lis_dirty = false;
+  uint32_t *d_lis = nullptr;
+  unsigned long long *d_next = nullptr, *h_next = nullptr;
 };
 
 // The epoch's status block (counters, digest, end records) is stat[b].
@@ -1695,6 +1753,7 @@ extern "C" int nsgpu_wifil_destroy(nsgpu_wifil *h) {
   if (h->h_stat) (void)hipHostFree(h->h_stat);
   if (h->h_mir) (void)hipHostFree(h->h_mir);
   if (h->h_pend) (void)hipHostFree(h->h_pend);
+  if (h->h_next) (void)hipHostFree(h->h_next);
   delete h;
   return NSGPU_OK;
 }
@@ -1794,6 +1853,12 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   WL_TRY(wl_alloc(h, &D.rxb, (size_t)NSEND * N));
   WL_TRY(wl_alloc(h, &D.evg, std::min<uint64_t>(ev_cap, ERANK_MAX)));
   WL_TRY(wl_alloc(h, &h->d_pend, 2));
+  WL_TRY(wl_alloc(h, &h->d_next, 4));
+  WL_TRY(wl_alloc(h, &h->d_lis, (size_t)N));
+  D.lis = h->d_lis;
+  D.nlis = 0;
+  h->lis_on.assign((size_t)N, 0);
+  h->node_h.assign(c->node, c->node + N);
 #undef WL_TRY
   D.sync_cap = sync_cap;
   D.ev_cap = ev_cap;
@@ -1805,6 +1870,7 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
       hipHostMalloc((void **)&h->h_mir, (size_t)N * sizeof(WMir), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&D.mir, h->h_mir, 0) != hipSuccess ||
       hipHostMalloc((void **)&h->h_pend, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&h->h_next, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void **)&h->h_digtot, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&h->d_digtot, h->h_digtot, 0) != hipSuccess ||
       // the PHY's epochs on a high-priority stream, the order behind them on a low-priority one: streams of
@@ -1831,6 +1897,29 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
 extern "C" int nsgpu_wifil_receivers(nsgpu_wifil *h, uint32_t phy, uint32_t *n) {
   if (!h || !n || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_receivers: bad phy");
   *n = h->recv[phy];
+  return NSGPU_OK;
+}
+
+// YansWifiChannel::Send's ScheduleWithContext calls for one SendPacket of `sender` (yans-wifi-channel.cc:77-115),
+// on the host: every other phy of m_phyList on the sender's channel number, in list order, gets the Receive with
+// uid uid_base + its place and the context of its device's node (0xffffffff: a phy without a device).  This is the
+// uid-critical half of a binding's Send (nsgpu_sim_wifi_send hands out the same block); no device is touched.
+extern "C" int nsgpu_wifil_send_plan(const nsgpu_wifil_config *c, uint32_t sender, uint32_t uid_base, uint32_t *rx_phy,
+                                     uint32_t *rx_uid, uint32_t *rx_ctx, uint64_t cap, uint64_t *n) {
+  if (!c || !n || !c->channel || !c->node || (int64_t)sender >= c->n_phy)
+    return set_error(NSGPU_EINVAL, "nsgpu_wifil_send_plan: bad config / sender");
+  uint64_t k = 0;
+  for (int64_t j = 0; j < c->n_phy; j++) {
+    if ((uint32_t)j == sender || c->channel[j] != c->channel[sender]) continue;  // (:86-91)
+    if ((uint64_t)uid_base + k >= nsgpu::UID_NEXT_MAX) return nsgpu::uid_range_error("nsgpu_wifil_send_plan");
+    if (k < cap) {
+      if (rx_phy) rx_phy[k] = (uint32_t)j;
+      if (rx_uid) rx_uid[k] = uid_base + (uint32_t)k;
+      if (rx_ctx) rx_ctx[k] = c->node[j];  // dstNode (:101-110)
+    }
+    k++;
+  }
+  *n = k;
   return NSGPU_OK;
 }
 
@@ -2114,6 +2203,61 @@ extern "C" int nsgpu_wifil_read_phys(nsgpu_wifil *h, nsgpu_wifi_phy_counters *ou
     out[j] = c;
   }
   return NSGPU_OK;
+}
+
+// The EndReceive hand-back: the host takes phy's EndReceives back (on = 1) or not.
+extern "C" int nsgpu_wifil_listen(nsgpu_wifil *h, uint32_t phy, int on) {
+  if (!h || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_listen: bad phy");
+  const uint8_t v = on ? 1 : 0;
+  if (h->lis_on[phy] != v) {
+    h->lis_on[phy] = v;
+    h->lis_dirty = true;
+  }
+  return NSGPU_OK;
+}
+
+// The next EndReceive of a listened phy (k_wl_nextend): a pending one (not cancelled) and the earliest time a
+// sync not yet made could put one (see the kernel).  Valid between advances.
+extern "C" int nsgpu_wifil_next_end(nsgpu_wifil *h, nsgpu_wifil_next *out) {
+  if (!h || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifil_next_end: null");
+  if (h->lis_dirty) {
+    h->lis_list.clear();
+    for (size_t j = 0; j < h->lis_on.size(); j++)
+      if (h->lis_on[j]) h->lis_list.push_back((uint32_t)j);
+    if (!h->lis_list.empty())
+      NSGPU_HIP(hipMemcpyAsync(h->d_lis, h->lis_list.data(), h->lis_list.size() * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, h->s));
+    h->D.nlis = (uint32_t)h->lis_list.size();
+    h->lis_dirty = false;
+  }
+  memset(out, 0, sizeof(*out));
+  out->ts = out->ts_potential = ~0ull;
+  if (h->D.nlis == 0) return NSGPU_OK;
+  hipLaunchKernelGGL(k_wl_nextend, dim3(1), dim3(256), 0, h->s, h->D, h->sb.n, h->d_next);
+  NSGPU_HIP(hipGetLastError());
+  NSGPU_HIP(hipMemcpyAsync(h->h_next, h->d_next, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->s));
+  NSGPU_HIP(hipStreamSynchronize(h->s));  // (lis_list stays alive until here)
+  if (h->h_next[1] != ~0ull) {
+    out->found = 1;
+    out->ts = h->h_next[0];
+    out->uid = (uint32_t)h->h_next[1];
+    out->phy = (uint32_t)(h->h_next[1] >> 32);
+  }
+  out->ts_potential = h->h_next[2];
+  return NSGPU_OK;
+}
+
+// (runtime) The last epoch's EndReceive with this uid, and a phy's node (the hand-back's context).
+bool nsgpu::wifil_epoch_end(const nsgpu_wifil *h, uint32_t uid, nsgpu_wifil_end *out) {
+  for (const nsgpu_wifil_end &e : h->ends_epoch)
+    if (e.uid == uid) {
+      *out = e;
+      return true;
+    }
+  return false;
+}
+uint32_t nsgpu::wifil_node(const nsgpu_wifil *h, uint32_t phy) {
+  return phy < h->node_h.size() ? h->node_h[phy] : 0xffffffffu;
 }
 
 // Pending Receive / EndReceive events and the smallest ts among them (~0: none).

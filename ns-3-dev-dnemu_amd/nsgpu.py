@@ -170,6 +170,11 @@ SIGNATURES = {
     "nsgpu_comm_destroy": (C.c_int, [_vp]),
     "nsgpu_p2p_create_dist": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _vp, _u64, _u64, C.POINTER(C.c_void_p)]),
     "nsgpu_p2p_dist_plan": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _u64, _vp]),
+    "nsgpu_wifil_listen": (C.c_int, [_vp, _u32, C.c_int]),
+    "nsgpu_wifil_send_plan": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, C.POINTER(C.c_uint64)]),
+    "nsgpu_wifil_next_end": (C.c_int, [_vp, _vp]),
+    "nsgpu_sim_wifi_set_end_handler": (C.c_int, [_vp, _vp, _vp]),
+    "nsgpu_sim_wifi_listen": (C.c_int, [_vp, _u32, C.c_int]),
     "nsgpu_p2p_group_create": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p)]),
     "nsgpu_p2p_group_reset": (C.c_int, [_vp, _vp]),
     "nsgpu_p2p_group_run": (C.c_int, [_vp, _vp]),
@@ -517,6 +522,7 @@ class EventId(C.Structure):  # nsgpu_event_id
 
 
 EVENT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)
+WIFI_END_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p)  # nsgpu_wifi_end_fn (user, const nsgpu_wifil_end *)
 
 
 class Sched:
@@ -749,6 +755,27 @@ class Sim:
     def wifi_send(self, phy, size, dbm, mode, preamble):
         """YansWifiPhy::SendPacket of `phy` now (mode = (modclass, rate, bandwidth))."""
         check(lib().nsgpu_sim_wifi_send(self.h, phy, size, dbm, mode[0], mode[1], mode[2], preamble))
+
+    def wifi_set_end_handler(self, fn):
+        """EndReceive hand-back (nsgpu_sim_wifi_set_end_handler): fn(end) — a wifi.WIFIL_END_DTYPE record — runs at
+        each EndReceive of a listened phy, in the order, as YansWifiPhy::EndReceive's host part (its m_random draw
+        and the MAC callbacks); fn None: none."""
+        import wifi
+        if fn is None:
+            check(lib().nsgpu_sim_wifi_set_end_handler(self.h, None, None))
+            self._end_cb = None
+            return
+        size = wifi.WIFIL_END_DTYPE.itemsize
+
+        def tramp(user, p):
+            fn(np.frombuffer(C.string_at(p, size), wifi.WIFIL_END_DTYPE)[0])
+
+        self._end_cb = WIFI_END_FN(tramp)
+        check(lib().nsgpu_sim_wifi_set_end_handler(self.h, C.cast(self._end_cb, C.c_void_p), None))
+
+    def wifi_listen(self, phy, on=True):
+        """The hand-back for `phy`'s EndReceives on (or off)."""
+        check(lib().nsgpu_sim_wifi_listen(self.h, phy, 1 if on else 0))
 
     def wifi_state(self, phy):
         """WifiPhyStateHelper::GetState of `phy` now: (state, delay until idle ns)."""

@@ -370,6 +370,17 @@ class LoopPhys:
         """Fan-out uids one SendPacket of `phy` takes: the other phys on its channel."""
         return int(np.count_nonzero(self.channel == self.channel[phy])) - 1
 
+    def send_plan(self, sender, uid_base):
+        """nsgpu_wifil_send_plan (host only): YansWifiChannel::Send's Receive calls for one SendPacket of `sender` —
+        (receiver phys, their uids, their contexts) in schedule order."""
+        n = self.n_phy
+        phy, uid, ctx = (np.zeros(max(n, 1), np.uint32) for _ in range(3))
+        k = C.c_uint64()
+        s = self.c_struct()
+        nsgpu.check(nsgpu.lib().nsgpu_wifil_send_plan(C.byref(s), sender, uid_base, phy.ctypes.data, uid.ctypes.data,
+                                                      ctx.ctypes.data, n, C.byref(k)))
+        return phy[:k.value], uid[:k.value], ctx[:k.value]
+
     def c_struct(self):
         s = WifilConfigStruct()
         s.n_phy = self.n_phy

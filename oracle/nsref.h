@@ -190,6 +190,12 @@ typedef struct nsref_wifil_mac {
   uint32_t size, modclass, bw, preamble;
   double dbm;
   uint32_t uid_first, pad_;  /* m_uid before the setup calls (0: 4) */
+  /* the EndReceive hand-back (YansWifiPhy::EndReceive -> the MAC's receive callback, yans-wifi-phy.cc:783-791):
+   * reply_on = 1: an EndReceive that is not cancelled and whose m_random draw (0.5 here) exceeds its per
+   * Schedules (reply_delay, reply of its phy) in the EndReceive's context; the reply sends a frame when the phy is
+   * IDLE (else counts as busy) and schedules nothing else */
+  uint64_t reply_delay;
+  uint32_t reply_on, pad2_;
 } nsref_wifil_mac;
 int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, uint64_t *log_ts, uint32_t *log_uid,
                     uint32_t *log_ctx, uint64_t log_cap, nsgpu_wifil_end *ends, uint64_t ends_cap, uint64_t *n_ends,

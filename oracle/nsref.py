@@ -492,13 +492,15 @@ def wifi_run(scenario_struct, stats_struct, phys, tx_base, end_dtype, rx_log=Non
 class WifilMacStruct(C.Structure):  # nsref_wifil_mac (nsref.h)
     _fields_ = [("first", C.c_void_p), ("backoff", C.c_void_p), ("period", C.c_uint64), ("stop_ts", C.c_uint64),
                 ("rate", C.c_uint64), ("size", C.c_uint32), ("modclass", C.c_uint32), ("bw", C.c_uint32),
-                ("preamble", C.c_uint32), ("dbm", C.c_double), ("uid_first", C.c_uint32), ("pad_", C.c_uint32)]
+                ("preamble", C.c_uint32), ("dbm", C.c_double), ("uid_first", C.c_uint32), ("pad_", C.c_uint32),
+                ("reply_delay", C.c_uint64), ("reply_on", C.c_uint32), ("pad2_", C.c_uint32)]
 
 
 def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble, dbm, n_phy, end_dtype,
-              phys_dtype, log_cap=1 << 20, uid_first=0):
+              phys_dtype, log_cap=1 << 20, uid_first=0, reply_delay=None):
     """The closed-loop oracle run (nsref_wifil_run): the MAC stand-in of nsref.h over the PHY.  Returns
-    (pop log (ts, uid, ctx), EndReceive records in dispatch order, per-phy counters, dict of totals)."""
+    (pop log (ts, uid, ctx), EndReceive records in dispatch order, per-phy counters, dict of totals).
+    reply_delay (ns): the EndReceive hand-back's reply (nsref.h), None: off."""
     f = lib().nsref_wifil_run
     f.restype = C.c_int
     f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
@@ -506,7 +508,7 @@ def wifil_run(cfg_struct, first, backoff, period, stop_ts, size, mode, preamble,
     first = np.ascontiguousarray(first, np.uint64)
     backoff = np.ascontiguousarray(backoff, np.uint64)
     m = WifilMacStruct(first.ctypes.data, backoff.ctypes.data, period, stop_ts, mode[1], size, mode[0], mode[2],
-                       preamble, dbm, uid_first, 0)
+                       preamble, dbm, uid_first, 0, reply_delay or 0, 0 if reply_delay is None else 1, 0)
     lts = np.zeros(log_cap, np.uint64)
     luid = np.zeros(log_cap, np.uint32)
     lctx = np.zeros(log_cap, np.uint32)

@@ -469,7 +469,7 @@ struct Loop {
   std::vector<Phy> phy;
   std::vector<LoopTx> txs;
   std::vector<LoopEnd> endv;
-  enum { ATTEMPT = 0, RX = 1, END = 2, STOP = 3, SEND = 4, MOVE = 5 };
+  enum { ATTEMPT = 0, RX = 1, END = 2, STOP = 3, SEND = 4, MOVE = 5, REPLY = 6 };
   // current positions (MobilityModel::SetPosition from a host closure moves a phy; YansWifiChannel::Send reads
   // them at each send, yans-wifi-channel.cc:92-96)
   std::vector<double> px, py, pz;
@@ -595,12 +595,12 @@ struct Loop {
     per = 1 - psr;
   }
 
-  // the MAC stand-in's attempt (see nsref.h)
-  int attempt(uint32_t i) {
+  // the MAC stand-in's attempt (see nsref.h); reply: the hand-back's reply (no retry, nothing rescheduled)
+  int attempt(uint32_t i, bool reply = false) {
     Phy &p = phy[i];
     if (state(p) != NSGPU_WIFIL_IDLE) {
       busy++;
-      schedule(now + mac->backoff[i], E{ATTEMPT, i, 0, ctx, 0.0});
+      if (!reply) schedule(now + mac->backoff[i], E{ATTEMPT, i, 0, ctx, 0.0});
       return 0;
     }
     // YansWifiPhy::SendPacket — yans-wifi-phy.cc:499-522 (IDLE: no reception to cancel)
@@ -623,7 +623,7 @@ struct Loop {
       double rx = nsref_calc_rx_power(mac->dbm, d, &cfg->loss);
       schedule(now + (uint64_t)delay, E{RX, k, (uint32_t)j, cfg->node[j], rx});
     }
-    schedule(now + mac->period, E{ATTEMPT, i, 0, ctx, 0.0});
+    if (!reply) schedule(now + mac->period, E{ATTEMPT, i, 0, ctx, 0.0});
     return 0;
   }
   // YansWifiPhy::SendPacket from a host closure whatever the state (a replayed transmission schedule):
@@ -903,8 +903,14 @@ int nsref_wifil_run(const nsgpu_wifil_config *cfg, const nsref_wifil_mac *mac, u
     }
     if (e.kind == Loop::STOP) break;
     if (e.kind == Loop::ATTEMPT) L.attempt(e.a);
+    else if (e.kind == Loop::REPLY) L.attempt(e.a, true);
     else if (e.kind == Loop::RX) L.start_receive(e.a, e.b, e.rx_dbm);
-    else L.end_receive(e.a, euid);
+    else {
+      L.end_receive(e.a, euid);
+      const nsgpu_wifil_end &r = L.ends.back();  // the hand-back: the host's draw, then the MAC's callback
+      if (mac->reply_on && !(r.flags & NSGPU_WIFI_END_CANCELLED) && 0.5 > r.per)
+        L.schedule(L.now + mac->reply_delay, Loop::E{Loop::REPLY, r.phy, 0, L.ctx, 0.0});
+    }
   }
   out[0] = L.dispatched;
   out[1] = L.digest;

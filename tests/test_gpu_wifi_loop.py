@@ -145,3 +145,53 @@ def test_bench_native_mac_stand_in_equals_the_oracle():
     assert (disp, digest, info["next_uid"]) == (otot["dispatched"], otot["digest"], otot["next_uid"])
     assert (info["sends"], info["busy_attempts"]) == (otot["sends"], otot["busy"])
     assert otot["busy"] > 0
+
+
+# ---------------------------------------------------------------- the EndReceive hand-back (nsgpu_sim_wifi_set_end_handler)
+@pytest.mark.parametrize("reply_delay", [10_000, 0])
+@pytest.mark.parametrize("dense", [False, True])
+def test_end_handback_mac_replies_equal_the_oracle(reply_delay, dense):
+    """YansWifiPhy::EndReceive's host part in the order (yans-wifi-phy.cc:770-799): every phy is handed back; at each
+    EndReceive that is not cancelled and whose draw passes, the MAC stand-in schedules a reply (after a SIFS-like
+    10 us, or Schedule (0): same time, a later uid) which sends if the phy is IDLE.  The replies' Schedule calls take
+    their uids at the EndReceive's place (the runtime stops the device there, and never advances past a time where a
+    pending Receive could still sync and end), so the full pop log, digest, end records, counters and sends equal
+    the oracle's restatement with the same MAC (nsref_wifil_mac.reply_on)."""
+    if dense:
+        sc = scenario(n_side=6, spacing=60.0, seed=3, period=12_000_000, stop_ns=80_000_000, size=600)
+    else:
+        sc = scenario(stop_ns=120_000_000)
+    sc["reply_delay"] = reply_delay
+    olog, oends, ophys, otot = run_oracle(sc)
+    glog, gends, gphys, gtot, _keep = run_gpu(sc)
+    for f in ("dispatched", "digest", "next_uid", "final_ts", "sends", "busy"):
+        assert gtot[f] == otot[f], (f, gtot[f], otot[f])
+    for a, b in zip(glog, olog):
+        assert np.array_equal(a, b)
+    for f in PHY_FIELDS:
+        assert np.array_equal(gphys[f], ophys[f]), f
+    for f in ("ts", "uid", "phy", "tx", "flags"):
+        assert np.array_equal(gends[f], oends[f]), f
+    np.testing.assert_allclose(gends["per"], oends["per"], rtol=1e-9, atol=1e-15)
+    live = int(np.count_nonzero((oends["flags"] & wifi.END_CANCELLED) == 0))
+    assert gtot["handbacks"] == live > 20
+    replies = int(np.count_nonzero(((oends["flags"] & wifi.END_CANCELLED) == 0) & (oends["per"] < 0.5)))
+    assert replies > 10  # (the replies are part of the sends and busy counts compared above)
+
+
+def test_end_handback_listening_alone_changes_nothing():
+    """Every phy handed back to a handler that schedules nothing: the epochs the hand-back cuts (at every EndReceive,
+    and before every time a pending Receive could end) leave the run identical to the plain one — the oracle's."""
+    sc = scenario(n_side=6, spacing=60.0, seed=3, period=12_000_000, stop_ns=60_000_000, size=600)
+    olog, oends, ophys, otot = run_oracle(sc)
+    sc["reply_delay"] = 1 << 62  # (replies far past Stop: never dispatched; the handler still runs and schedules)
+    glog, gends, _gphys, gtot, _keep = run_gpu(sc)
+    # (the handler's Schedule calls take uids: compare against the oracle run with the same far replies)
+    olog2, oends2, _ophys2, otot2 = run_oracle(sc)
+    for f in ("dispatched", "digest", "next_uid", "sends", "busy"):
+        assert gtot[f] == otot2[f], f
+    for a, b in zip(glog, olog2):
+        assert np.array_equal(a, b)
+    # and before the first reply-uid the runs agree with the plain one: same events, same end records
+    assert np.array_equal(gends["ts"], oends["ts"]) and np.array_equal(gends["phy"], oends["phy"])
+    assert otot2["dispatched"] == otot["dispatched"] and gtot["handbacks"] > 20

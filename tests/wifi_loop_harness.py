@@ -28,12 +28,16 @@ def run_oracle(sc, log_cap=1 << 20, uid_first=0):
     cfg = ph.c_struct()
     log, ends, phys, tot = nsref.wifil_run(cfg, sc["first"], sc["backoff"], sc["period"], sc["stop_ns"], sc["size"],
                                            sc["mode"], sc["preamble"], sc["dbm"], ph.n_phy, wifi.WIFIL_END_DTYPE,
-                                           wifi.PHY_COUNTERS_DTYPE, log_cap, uid_first=uid_first)
+                                           wifi.PHY_COUNTERS_DTYPE, log_cap, uid_first=uid_first,
+                                           reply_delay=sc.get("reply_delay"))
     return log, ends, phys, tot
 
 
-def run_gpu(sc, log_cap=1 << 20, uid_first=0):
-    """uid_first: m_uid before the setup calls (nsgpu_sim_set_next_uid; 0: the reference's 4)."""
+def run_gpu(sc, log_cap=1 << 20, uid_first=0, listen=None):
+    """uid_first: m_uid before the setup calls (nsgpu_sim_set_next_uid; 0: the reference's 4).
+    sc["reply_delay"] (ns, optional): the EndReceive hand-back (nsgpu_sim_wifi_set_end_handler) — at each EndReceive
+    that is not cancelled and whose draw (0.5) exceeds its per, the MAC stand-in schedules a reply of that phy
+    (nsref.h: nsref_wifil_mac.reply_on).  listen: the phys handed back (default: every phy when replying)."""
     import nsgpu
     ph = sc["phys"]
     sim = nsgpu.Sim()
@@ -42,19 +46,33 @@ def run_gpu(sc, log_cap=1 << 20, uid_first=0):
     lp = wifi.LoopPhy(ph)
     sim.attach_wifi(lp)
     sim.set_log(log_cap)
-    cnt = {"sends": 0, "busy": 0}
+    cnt = {"sends": 0, "busy": 0, "handbacks": 0}
     txs = []  # (ts, closure uid, phy) per SendPacket: the MonitorSnifferTx records
 
-    def attempt(i):
+    def attempt(i, reply=False):
         st, _ = sim.wifi_state(i)
         if st != wifi.IDLE:
             cnt["busy"] += 1
-            sim.schedule(int(sc["backoff"][i]), lambda: attempt(i))
+            if not reply:
+                sim.schedule(int(sc["backoff"][i]), lambda: attempt(i))
             return
         txs.append((sim.now(), sim.current_uid(), i))
         sim.wifi_send(i, sc["size"], sc["dbm"], sc["mode"], sc["preamble"])
         cnt["sends"] += 1
-        sim.schedule(sc["period"], lambda: attempt(i))
+        if not reply:
+            sim.schedule(sc["period"], lambda: attempt(i))
+
+    rd = sc.get("reply_delay")
+    if rd is not None:
+        def end_receive(e):  # YansWifiPhy::EndReceive's host part: the draw, then the MAC's receive callback
+            cnt["handbacks"] += 1
+            assert sim.now() == int(e["ts"]) and sim.current_uid() == int(e["uid"])
+            if 0.5 > e["per"]:
+                i = int(e["phy"])
+                sim.schedule(rd, lambda: attempt(i, True))
+        sim.wifi_set_end_handler(end_receive)
+        for i in (range(ph.n_phy) if listen is None else listen):
+            sim.wifi_listen(i)
 
     for i in range(ph.n_phy):
         sim.schedule(int(sc["first"][i]), (lambda i=i: lambda: attempt(i))())
