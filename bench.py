@@ -839,8 +839,7 @@ def main():
         secondary = []
         if world == 1 and not partitioned and args.workload == "p2p-grid" and not args.no_secondary:
             names = os.environ.get("NSGPU_BENCH_SECONDARIES", "wifi-grid,wifi-loop,dumbbell").split(",")
-            if os.environ.get("NSGPU_BENCH_PRIMARY_CLOSE") == "1":  # (diagnostic)
-                wl.close()
+            wl.close()  # (each workload closed before the next: its streams and HBM released)
             for name in names:
                 wl2 = WORKLOADS[name](args, stream.handle)
                 el2, kms2 = measure(wl2, args.secondary_steps, 1)

@@ -133,6 +133,12 @@ HipSimulatorImpl::NowTs (void) const
   return now;
 }
 
+nsgpu_sim *
+HipSimulatorImpl::GetRuntime (void) const
+{
+  return m_rt;
+}
+
 uint64_t
 HipSimulatorImpl::GetEventCount (void) const
 {

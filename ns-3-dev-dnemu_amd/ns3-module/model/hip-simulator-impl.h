@@ -85,6 +85,8 @@ public:
   void AdoptDeviceSubset (nsgpu_p2p *engine, const std::vector<uint32_t> &owned);
   /* Dispatches so far (RemoveNext calls, cancelled events included: SURVEY H16), host and device. */
   uint64_t GetEventCount (void) const;
+  /* The libnsgpu runtime behind this simulator (a device engine attaches to it: HipWifiBinding::Attach). */
+  nsgpu_sim *GetRuntime (void) const;
 
 private:
   virtual void DoDispose (void);

@@ -1,8 +1,8 @@
 """The ns-3 side of the boundary compiles against the reference's own headers.
 
 `ns-3-dev-dnemu_amd/ns3-module/model/*.cc` (ns3::HipSimulatorImpl, ns3::HipBatchScheduler,
-ns3::NsgpuP2pScenario) are compiled with g++ -std=gnu++98 -fsyntax-only (the reference is C++98,
-wscript:318-330) against the reference's headers (core, network, point-to-point, internet, applications),
+ns3::NsgpuP2pScenario, ns3::HipYansWifiPhy / HipYansWifiPhyHelper / HipWifiBinding) are compiled with g++ -std=gnu++98 -fsyntax-only (the reference is C++98,
+wscript:318-330) against the reference's headers (core, network, point-to-point, internet, applications, wifi, mobility, propagation),
 laid out as the ns3/ include directory a waf build makes.  Only the waf-generated ns3/core-config.h is written here (three
 feature macros) — it configures the int64x64 implementation; no reference code
 is built or linked.  Skipped where the reference tree is absent (the GPU box)."""
@@ -28,7 +28,7 @@ def ns3_include(tmp_path_factory):
     inc.mkdir()
     # the headers of the modules the sources include (core, and for NsgpuP2pScenario::FromNodeList / WriteTraces
     # network, point-to-point, internet, applications), flattened into ns3/ as a waf build does
-    for mod in ("core", "network", "point-to-point", "internet", "applications"):
+    for mod in ("core", "network", "point-to-point", "internet", "applications", "wifi", "mobility", "propagation"):
         for sub in ("model", "helper", "utils"):
             for h in glob.glob(os.path.join(REF, "src", mod, sub, "*.h")):
                 dst = inc / os.path.basename(h)
