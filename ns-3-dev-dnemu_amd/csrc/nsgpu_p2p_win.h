@@ -463,9 +463,13 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
   const uint64_t c_drlo = DIST ? C.drlo : ~0ull;
   const bool dtrim = DIST && C.dtrim != 0;  // a run ended after a cut group: its entries left outside the pool
   const uint64_t c_wn = DF ? C.windows : 0;  // (this window's index: the last one is c_wn - 1)
-  const int64_t look_mine = threadIdx.x < K_NKINDS       ? M.lookahead[threadIdx.x]
-                            : threadIdx.x < 2 * K_NKINDS ? (WIDE ? M.lookw[threadIdx.x - K_NKINDS] : 0)
-                                                         : 0;
+  // (branch-free, two loads into two registers: as one select of two branch loads the compiler reused one register,
+  // and the second branch's address write waited for the first branch's load — s_waitcnt vmcnt(0) — so wave 0 sat a
+  // whole trip on the run control before it issued the slot loads below)
+  const int64_t look_a = M.lookahead[threadIdx.x < K_NKINDS ? threadIdx.x : 0u];
+  const int64_t look_w = WIDE ? M.lookw[threadIdx.x >= K_NKINDS && threadIdx.x < 2 * K_NKINDS ? threadIdx.x - K_NKINDS : 0u]
+                              : 0;
+  const int64_t look_mine = threadIdx.x < K_NKINDS ? look_a : threadIdx.x < 2 * K_NKINDS ? look_w : 0;
   uint32_t xw_u[4] = {0, 0, 0, 0};  // (window c_wn - 2's uid base: the pool's provisional uids; all four
   if (DF) {                          //  loaded with the run control, picked once C.windows is back)
 #pragma unroll
