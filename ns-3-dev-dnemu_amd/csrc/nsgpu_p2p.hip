@@ -193,6 +193,9 @@ struct Ctl {
   uint64_t drb_tmin, drb_span, drb_bound, drb_stop, drb_nbound, drb_lim;  // the run window's bound (WinBound)
   uint64_t drn_wendw;  // (wide partitioned engines) the wide bound's part of drn_*
   uint64_t drcut;      // (wide partitioned engines) the run's candidates up to the narrow bound (k_drun_trim)
+  // ---- hub windows of the narrow engines: the hub events' stateless node parts by their slots' threads ----
+  uint32_t hub_rdy;    // holder blocks done with them (k2_pa zeroes it; the hub blocks wait for NHB)
+  uint32_t hub_ser;    // some hub event's node part touches node state (its hub block runs those serially)
 };
 
 static_assert(offsetof(Ctl, prep) == offsetof(Ctl, W) + 12 && offsetof(Ctl, W) % 16 == 0, "the X0 payload");
@@ -297,7 +300,8 @@ struct P2PDev {
   uint32_t *hub_list;     // nodes with more than CH window events (hub blocks)
   struct HubEv *hx;       // hub blocks: per-slot node-part results
   uint64_t *hub_key;      // hub blocks: the hub's events in key order (NHUB x WCAP)
-  uint32_t *hub_slot;
+  uint32_t *hub_slot;     // (then WCAP more: hub_mark.  P2PDev is passed by value: one more pointer here made the
+                          //  compiler copy the whole struct into scratch, 1.4 KB a lane, in k2_handle)
   uint64_t *s_key2;       // radix sort / compaction scratch
   uint32_t *s_val, *s_val2, *s_hist, *g_u32;
   Pkt *g_pkt;
@@ -2451,7 +2455,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
   TRY(dalloc(h, &M.hub_list, MAXHUB));
   TRY(dalloc(h, &M.hx, WCAP));
   TRY(dalloc(h, &M.hub_key, (size_t)NHUB * WCAP));
-  TRY(dalloc(h, &M.hub_slot, (size_t)NHUB * WCAP));
+  TRY(dalloc(h, &M.hub_slot, (size_t)(NHUB + 1) * WCAP));  // (+ hub_mark's WCAP)
   TRY(dalloc(h, &M.cmp_cnt, 1));
   {  // radix sort scratch: the single engine's sorted runs, a partitioned rank's run (sorted once per run)
     TRY(dalloc(h, &M.s_key2, M.runcap));

@@ -436,6 +436,10 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
 #ifdef NSGPU_PHASE_PROF
   const uint64_t c_win = C.windows;
 #endif
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // (k2_handle's hub-window handshake: this window's)
+    C.hub_rdy = 0;
+    C.hub_ser = 0;
+  }
   // slot role: one thread per record of the last window — its gen-0 slots, then (single engine) its local
   // records (the dense list lrec), SL of them in each of the first NSGB blocks (roles are block-uniform:
   // a slot block's lanes past SL take part in its barriers only)
@@ -1308,10 +1312,11 @@ constexpr int32_t CBIG = 1 << 28;
 
 // Returns false (nothing done) when the batch would reuse a ring slot (more enqueues than the ring
 // holds beyond the queued packets): the serial pass runs instead.
-// hops[j]: the op of the list's event j (hub_node gathered the lane's segment into LDS).
-__device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d, const uint32_t *gs,
+// hops[j], hsl[j]: the op and the slot of the list's event j (hub_node gathered the lane's segment into LDS).
+template <bool WIDE>
+__device__ __forceinline__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d, const uint32_t *gs,
                                 const uint64_t *gk, uint32_t n, uint32_t j0s, uint32_t j1s, uint64_t tmin, HStat &hs,
-                                X1Acc &xa, const uint8_t *hops) {
+                                X1Acc &xa, const uint8_t *hops, const uint16_t *hsl) {
   const int lane = threadIdx.x;
   const DevRec dr = M.dev[d];
   const int32_t qmax = (int32_t)dr.qmax;
@@ -1355,85 +1360,144 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
   const uint32_t ebefore = wave_exscan32(ne, lane), dbefore = wave_exscan32(nd, lane);
   const uint32_t dtot = __shfl(dbefore + nd, 63), etot = __shfl(ebefore + ne, 63);
   if (cnt0 + etot > qcap) return false;
-  // pass B1: enqueued packets into the ring (before any TransmitComplete reads one)
+  // pass B1: enqueued packets into the ring (before any TransmitComplete reads one).  The lane's segment in
+  // batches: the slots from LDS (hsl), the batch's packets loaded at once (one memory trip a batch, not one an
+  // event: the loop's ring stores kept the next event's loads behind them)
+  constexpr int B1B = WIDE ? 1 : 8;  // (the wide kernel has no registers to spare)
   {
     int32_t x = cin;
     uint32_t e = ebefore;
-    for (uint32_t j = j0s; j < j1s; j++) {
-      const uint32_t op = hops[j];
-      if (op == ACT_SEND) {
-        if (x >= 0 && x < qmax) {
-          Pkt p = M.hx[gs[j]].p;
-          p.size += 2;
-          qb[(head0 + cnt0 + e) % qcap] = p;
+    for (uint32_t jb = j0s; jb < j1s; jb += B1B) {
+      Pkt pb[B1B];
+      uint32_t qi[B1B];
+#pragma unroll
+      for (int u = 0; u < B1B; u++) {  // (the state walk over the batch's ops: which enqueue, where)
+        const uint32_t j = jb + (uint32_t)u;
+        qi[u] = NOSRC;
+        if (j < j1s) {
+          const uint32_t op = hops[j];
+          if (op == ACT_SEND) {
+            if (x >= 0 && x < qmax) qi[u] = (head0 + cnt0 + e) % qcap;
+            if (x < qmax) e++;
+            x = x + 1 < qmax ? x + 1 : qmax;
+          } else if (op == ACT_KICK) {
+            x -= 1;
+          }
         }
-        if (x < qmax) e++;
-        x = x + 1 < qmax ? x + 1 : qmax;
-      } else if (op == ACT_KICK) {
-        x -= 1;
       }
+#pragma unroll
+      for (int u = 0; u < B1B; u++)
+        if (qi[u] != NOSRC) pb[u] = M.hx[hsl[jb + u]].p;
+#pragma unroll
+      for (int u = 0; u < B1B; u++)
+        if (qi[u] != NOSRC) {
+          Pkt p = pb[u];
+          p.size += 2;
+          qb[qi[u]] = p;
+        }
     }
   }
   __syncthreads();
-  // pass B2: traces, counters, TransmitStart children, trailing children
+  // pass B2: traces, counters, TransmitStart children, trailing children (B2B events a batch: their records and
+  // ring reads in one memory trip)
+  constexpr int B2B = WIDE ? 1 : 4;
   uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0, q5 = 0;
   {
     int32_t x = cin;
     uint32_t dq = dbefore;
-    for (uint32_t j = j0s; j < j1s; j++) {
-      const uint32_t s = gs[j];
-      const uint64_t key = gk[j];
-      const HubEv h = M.hx[s];
-      E.ctx = h.ctx;
-      E.now = tmin + (key >> 32);
-      E.slot0 = s * M.maxc;
-      E.n = h.n;
-      E.uid = (uint32_t)key, E.tloc = false;
-      E.trseq = h.seq;
-      E.demote = false;
-      hs.cancelled += h.cancelled;
-      bool go = false;
-      Pkt tx{0, 0, 0, 0};
-      if (h.op == ACT_SEND) {
-        trace_call(M, E, NSGPU_TR_IP_TX, d, h.p);
-        Pkt p = h.p;
-        p.size += 2;  // PppHeader
-        if (x >= qmax) {
-          trace_call(M, E, NSGPU_TR_DROP, d, p);
-          q2++;
-          q3 += p.size;
-        } else {
-          trace_call(M, E, NSGPU_TR_ENQUEUE, d, p);
-          q0++;
-          q1 += p.size;
-          if (x == -1) {  // Enqueue + Dequeue: the packet leaves at once
-            tx = p;
+    for (uint32_t jb = j0s; jb < j1s; jb += B2B) {
+      uint32_t sb[B2B], ri[B2B];
+      uint64_t kb[B2B];
+      HubEv hb[B2B];
+      Pkt tq[B2B];
+      {
+        int32_t xx = x;
+        uint32_t dd = dq;
+#pragma unroll
+        for (int u = 0; u < B2B; u++) {  // (each TransmitComplete's dequeue position, from the ops)
+          const uint32_t j = jb + (uint32_t)u;
+          ri[u] = NOSRC;
+          sb[u] = 0;
+          if (j < j1s) {
+            sb[u] = hsl[j];
+            const uint32_t op = hops[j];
+            if (op == ACT_SEND) {
+              if (xx == -1) dd++;
+              xx = xx + 1 < qmax ? xx + 1 : qmax;
+            } else if (op == ACT_KICK) {
+              if (xx >= 1) ri[u] = (head0 + dd++) % qcap;
+              xx -= 1;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < B2B; u++) {
+        const uint32_t j = jb + (uint32_t)u;
+        if (j < j1s) {
+          kb[u] = gk[j];
+          hb[u] = M.hx[sb[u]];
+        }
+        if (ri[u] != NOSRC) tq[u] = qb[ri[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < B2B; u++) {
+        const uint32_t j = jb + (uint32_t)u;
+        if (j >= j1s) break;
+        const uint32_t s = sb[u];
+        const uint64_t key = kb[u];
+        const HubEv &h = hb[u];
+        E.ctx = h.ctx;
+        E.now = tmin + (key >> 32);
+        E.slot0 = s * M.maxc;
+        E.n = h.n;
+        E.uid = (uint32_t)key, E.tloc = false;
+        E.trseq = h.seq;
+        E.demote = false;
+        hs.cancelled += h.cancelled;
+        bool go = false;
+        Pkt tx{0, 0, 0, 0};
+        if (h.op == ACT_SEND) {
+          trace_call(M, E, NSGPU_TR_IP_TX, d, h.p);
+          Pkt p = h.p;
+          p.size += 2;  // PppHeader
+          if (x >= qmax) {
+            trace_call(M, E, NSGPU_TR_DROP, d, p);
+            q2++;
+            q3 += p.size;
+          } else {
+            trace_call(M, E, NSGPU_TR_ENQUEUE, d, p);
+            q0++;
+            q1 += p.size;
+            if (x == -1) {  // Enqueue + Dequeue: the packet leaves at once
+              tx = p;
+              trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);
+              q4++;
+              dq++;
+              go = true;
+            }
+          }
+          x = x + 1 < qmax ? x + 1 : qmax;
+        } else if (h.op == ACT_KICK) {
+          if (x >= 1) {
+            tx = tq[u];
             trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);
             q4++;
             dq++;
             go = true;
           }
+          x -= 1;
         }
-        x = x + 1 < qmax ? x + 1 : qmax;
-      } else if (h.op == ACT_KICK) {
-        if (x >= 1) {
-          tx = qb[(head0 + dq) % qcap];
-          trace_call(M, E, NSGPU_TR_DEQUEUE, d, tx);
-          q4++;
-          dq++;
-          go = true;
+        if (go) {
+          q5++;
+          const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)bps);
+          E.child(txTime + ifg, h.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
+          E.child(txTime + delay, peer_node, rkind, peer, tx);
         }
-        x -= 1;
+        if (h.xdrop) trace_te_drop(M, E, h.xdrop - 1, h.p);
+        if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
+        slot_done(M, s, key, E.n, 0, xa);
       }
-      if (go) {
-        q5++;
-        const int64_t txTime = seconds_to_ts(static_cast<double>(tx.size) * 8 / (double)bps);
-        E.child(txTime + ifg, h.ctx, K_TX_COMPLETE, d, Pkt{0, 0, 0, 0});
-        E.child(txTime + delay, peer_node, rkind, peer, tx);
-      }
-      if (h.xdrop) trace_te_drop(M, E, h.xdrop - 1, h.p);
-      if (h.pkind) E.child(h.pdelay, h.ctx, h.pkind, h.pa, Pkt{0, 0, 0, 0});
-      slot_done(M, s, key, E.n, 0, xa);
     }
   }
   q0 = wave_sum32(q0), q1 = wave_sum32(q1), q2 = wave_sum32(q2), q3 = wave_sum32(q3), q4 = wave_sum32(q4),
@@ -1451,6 +1515,94 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
   return true;
 }
 
+// ---- hub windows of the narrow engines: the stateless node parts by the slots' own threads ----
+// A hub block is one wave; its pass over the hub's node parts took 64 events a round, each round a chain of
+// four dependent memory trips (slot -> record -> destination -> route): ~160 us for a run chunk of 4,000 events
+// at a dumbbell router.  Those node parts touch no node state, so in a window with hubs every slot's own thread
+// of the holder blocks runs its event's, if it is a hub's (the same steps as hub_node's lanes), into hx, and marks
+// the slot's hub (hub_mark: the hub block's list is then one array's scan); a node part that touches node state is
+// left to the hub block (HOP_SER, hub_ser), which runs those serially in key order as before.  Each holder block
+// then signals the hub blocks (hub_rdy), which wait for all NHB before they read hx / hub_mark (lower block indices
+// are dispatched first: the holder blocks are running or done when a hub block waits).
+constexpr uint32_t HOP_SER = 0xffu;  // hx[s].op: the node part is the hub block's (serial, node state)
+__device__ __forceinline__ uint32_t *hub_mark(const P2PDev &M) { return M.hub_slot + (uint64_t)NHUB * WCAP; }
+__device__ __forceinline__ void hub_help(const P2PDev &M, Ctl &C, uint32_t i0, uint32_t W, uint32_t base,
+                                         const HCtl &hc, SlotPre &sp) {
+  uint32_t mark = NOSRC;
+  bool ser = false;
+  HStat hs{0, 0, 0, 0, false};
+  if (i0 < W) {
+    if (base != 0) {  // (a run chunk's records: handle_node2 reloads them too)
+      sp.ctx = M.wctx[base + i0];
+      sp.kind = M.wkind[base + i0];
+      sp.a = M.wa[base + i0];
+      sp.key = M.wkey[base + i0];
+      sp.pkt = M.wpkt[base + i0];
+    }
+    const uint32_t kind = sp.kind & 0xffu;
+    if (sp.widx != NOHOLD) {
+      const uint32_t c = lp_of(M, sp.ctx, sp.kind, sp.a);
+      uint32_t dn = 0, ds = 0;  // (a Receive's addressing, loaded with the node's count)
+      if (kind == K_RECEIVE) {
+        dn = pkt_dst_node(M, sp.pkt);
+        ds = pkt_dst_slot(M, sp.pkt);
+      }
+      if (c < M.n_nodes && M.node_tab[(uint64_t)c * NTAB] > (uint32_t)CH) {
+        mark = c;
+        const bool sl = kind == K_TX_COMPLETE || kind == K_DEV_START ||
+                        (kind == K_RECEIVE && !(M.icmp && (sp.pkt.ttl & 0xffu) <= 1u) && dn != c);
+        if (!sl) {
+          ser = true;
+          M.hx[i0].op = HOP_SER;
+        } else {
+          Emit E;
+          E.now = hc.tmin + (sp.key >> 32);
+          E.uid = (uint32_t)sp.key, E.tloc = false;
+          E.trseq = 0;
+          HubEv h{ACT_NONE, 0, Pkt{0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, sp.ctx, 0};
+          if (kind == K_TX_COMPLETE) {
+            h.op = ACT_KICK;
+            h.dev = sp.a;
+          } else if (kind == K_RECEIVE) {  // PointToPointNetDevice::Receive -> Ipv4L3Protocol::Receive -> IpForward
+            const uint32_t out = route_at(M, c, ds);
+            atomicAdd(&M.dev[sp.a].c.rx_packets, 1u);
+            Pkt p = sp.pkt;
+            p.size -= 2;
+            trace_call(M, E, NSGPU_TR_RX, sp.a, p);
+            trace_call(M, E, NSGPU_TR_IP_RX, sp.a, p);
+            if (out == 0xffffffffu) {
+              hs.no_route++;
+              trace_ip_drop(M, E, sp.a, p);
+            } else {
+              p.ttl -= 1;
+              if (p.ttl == 0) {  // (ICMP off: a stateless event)
+                hs.ttl_drops++;
+                trace_ip_drop(M, E, out, Pkt{p.app, p.ipid, p.size, 1u});
+              } else {
+                h.op = ACT_SEND;
+                h.dev = out;
+                h.p = p;
+              }
+            }
+          }
+          h.seq = E.trseq;
+          M.hx[i0] = h;
+        }
+      }
+    }
+    hub_mark(M)[i0] = mark;
+  }
+  const uint64_t nr = wave_sum64(hs.no_route), td = wave_sum64(hs.ttl_drops);
+  const bool anyser = __ballot(ser) != 0;
+  if (threadIdx.x == 0) {
+    if (nr) atomicAdd((unsigned long long *)&C.no_route, (unsigned long long)nr);
+    if (td) atomicAdd((unsigned long long *)&C.ttl_drops, (unsigned long long)td);
+    if (anyser) atomicOr(&C.hub_ser, 1u);
+    __threadfence();  // (HB = one wave: the block's writes, released before the signal)
+    atomicAdd(&C.hub_rdy, 1u);
+  }
+}
+
 // A hub node's window events, by one block: (1) its events in key order (slot order in a sorted run
 // chunk; otherwise at most HUBL of them, bitonic-sorted in LDS) into the block's global scratch list;
 // (2a) node parts without node state (TransmitComplete; Receive -> IpForward) in parallel; (2b) the
@@ -1458,18 +1610,53 @@ __device__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32_t c, uint32_t d
 // order, the device state in registers.  Node parts never read device state and device steps never
 // read node state (node_part), so this is the sequential order's result.
 template <bool WIDE>
-__device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32_t base, bool sorted, Red &R,
-                         uint32_t hb, uint32_t *lds, const HCtl &hc, uint32_t *lcnt_sh) {
+__device__ __forceinline__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32_t base, bool sorted, Red &R,
+                         uint32_t hb, uint32_t *lds, const HCtl &hc, uint32_t *lcnt_sh, bool helped) {
   const int lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1ull;
   uint64_t *gk = M.hub_key + (uint64_t)hb * WCAP;
   uint32_t *gs = M.hub_slot + (uint64_t)hb * WCAP;
   HUB_T0();
+  uint32_t ser = 1;  // (helped: some hub event's node part is left to its hub block)
+  if (!WIDE && helped) {  // the holder blocks ran the stateless node parts (hub_help): wait for all of them
+    if (lane == 0)
+      while (__hip_atomic_load(&C.hub_rdy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)NHB)
+        __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
+    __threadfence();
+    ser = __hip_atomic_load(&C.hub_ser, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    HUB_MARK(22);  // (the wait for the holder blocks)
+  }
   // 1. the node's window events, in slot order (HSB batches of HB window entries a memory trip; the wide
-  //    kernel has no registers to spare: one there)
+  //    kernel has no registers to spare: one there).  helped: the slots marked with this hub, HMB batches a trip
   constexpr int HSB = WIDE ? 1 : 4;
+  constexpr int HMB = 8;
   uint32_t n = 0;
-  for (uint32_t x0 = 0; x0 < W; x0 += HB * HSB) {
+  if (!WIDE && helped) {
+    for (uint32_t x0 = 0; x0 < W; x0 += HB * HMB) {
+      uint32_t hm[HMB];
+      uint64_t hk[HMB];
+#pragma unroll
+      for (int u = 0; u < HMB; u++) {  // (the keys loaded with the marks: in range, used for this hub's)
+        const uint32_t x = x0 + (uint32_t)(u * HB) + lane;
+        hm[u] = x < W ? hub_mark(M)[x] : NOSRC;
+        hk[u] = M.wkey[base + (x < W ? x : 0u)];
+      }
+#pragma unroll
+      for (int u = 0; u < HMB; u++) {
+        const uint32_t x = x0 + (uint32_t)(u * HB) + lane;
+        const bool m = hm[u] == c;
+        const uint64_t bm = __ballot(m);
+        if (m) {
+          const uint32_t p = n + (uint32_t)__popcll(bm & below);
+          gs[p] = x;
+          gk[p] = hk[u];
+        }
+        n += (uint32_t)__popcll(bm);
+      }
+    }
+  }
+  for (uint32_t x0 = 0; x0 < ((!WIDE && helped) ? 0u : W); x0 += HB * HSB) {
     uint32_t bi[HSB], bc[HSB], bk[HSB], ba[HSB];
 #pragma unroll
     for (int u = 0; u < HSB; u++) {
@@ -1541,7 +1728,38 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   //    NBT batches of HB events per round: each dependent step (slot -> record -> destination -> route)
   //    is one memory trip for all of them.
   constexpr int NBT = WIDE ? 1 : 2;  // (the wide kernel has no registers to spare: its hubs stay one batch a round)
-  {
+  if (!WIDE && helped) {
+    // the holder blocks ran the stateless ones (hub_help); the rest (HOP_SER), serially by lane 0 in key order
+    for (uint32_t j0 = 0; ser && j0 < n; j0 += HB) {
+      const uint32_t j = j0 + lane;
+      uint32_t op = 0;
+      if (j < n) op = M.hx[gs[j]].op;
+      uint64_t m = __ballot(j < n && op == HOP_SER);
+      if (lane == 0) {
+        while (m) {
+          const uint32_t q = j0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+          m &= m - 1;
+          const uint32_t s = gs[q];
+          const uint64_t key = gk[q], rel = key >> 32;
+          const uint32_t kw = M.wkind[base + s], a = M.wa[base + s], ctx = M.wctx[base + s];
+          const Pkt pk = M.wpkt[base + s];
+          E.ctx = ctx;
+          E.now = tmin + rel;
+          E.slot0 = s * M.maxc;
+          E.n = 0;
+          E.uid = (uint32_t)key, E.tloc = false;
+          E.trseq = 0;
+          E.demote = rel == slo || rel == shi;
+          const NodeOut o = node_part(M, E, kw, a, pk, sink, hs, true);
+          uint32_t ni = 0;
+          for (uint32_t jj = 0; jj < E.n; jj++) ni += (M.ch_kind[E.slot0 + jj] & 0xffu) == K_FWD_UP;
+          M.hx[s] = HubEv{o.act.op, o.act.dev, o.act.p, o.post.delay, o.post.valid ? o.post.kind : 0u, o.post.a, E.n,
+                          E.trseq, o.cancelled ? 1u : 0u, ni, ctx, o.xdrop};
+        }
+      }
+      __syncthreads();
+    }
+  } else {
     uint64_t *c_key = reinterpret_cast<uint64_t *>(lds);  // [HB * NBT]
     uint32_t *c_s = lds + 2 * HB * NBT, *c_kind = lds + 3 * HB * NBT, *c_a = lds + 4 * HB * NBT,
              *c_ctx = lds + 6 * HB * NBT;
@@ -1698,7 +1916,8 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   // the lane's segment: devices, inline flags, and its ops into LDS for the device scan (HSO events a
   // memory trip; past the serial pass's batch arrays)
   uint8_t *hops = reinterpret_cast<uint8_t *>(lds + 2048);
-  static_assert(2048 + WCAP / 4 <= K2_LDS_WORDS, "hub ops do not fit the shared buffer");
+  uint16_t *hsl = reinterpret_cast<uint16_t *>(lds);  // (the slots, for the device scan's batches)
+  static_assert(2048 + WCAP / 4 <= K2_LDS_WORDS && WCAP <= 4096, "hub ops / slots do not fit the shared buffer");
   constexpr int HSO = WIDE ? 1 : 8;
   for (uint32_t j = j0s; j < j1s; j += HSO) {
     uint32_t sl[HSO], op[HSO], dv[HSO], pd[HSO];
@@ -1717,6 +1936,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
     for (int u = 0; u < HSO; u++)
       if (j + u < j1s) {
         hops[j + u] = (uint8_t)op[u];
+        hsl[j + u] = (uint16_t)sl[u];
         if (op[u] != ACT_NONE) {
           dmin = dv[u] < dmin ? dv[u] : dmin;
           dmax = dv[u] > dmax ? dv[u] : dmax;
@@ -1724,6 +1944,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
         inl |= pd[u];
       }
   }
+  HUB_MARK(23);  // (the segments' ops into LDS)
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t x = __shfl_xor(dmin, o), y = __shfl_xor(dmax, o), z = __shfl_xor(inl, o);
     dmin = x < dmin ? x : dmin;
@@ -1734,7 +1955,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
   bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && (!WIDE || hc.lim == 0) && M.dev[dmin].qmax >= 1 &&
               !(M.dev[dmin].busy == 0 && M.dev[dmin].cnt != 0);
   X1Acc xa{0, 0, 0};
-  if (fast) fast = hub_device_scan(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs, xa, hops);
+  if (fast) fast = hub_device_scan<WIDE>(M, E, c, dmin, gs, gk, n, j0s, j1s, tmin, hs, xa, hops, hsl);
   if (!fast) {
     DevCache D;
     D.d = NOSRC;
@@ -1862,7 +2083,7 @@ __device__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, uint32_t W, uint32
 }
 
 // ---- k2_handle: pool maintenance (tombstones, free slots, fresh children -> pool) ----
-__device__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool handle, uint32_t W, uint64_t nfree,
+__device__ __forceinline__ void maintain(const P2PDev &M, Ctl &C, uint32_t mb, bool run, bool handle, uint32_t W, uint64_t nfree,
                          uint64_t nF, uint64_t Pe) {
   const uint64_t tstride = (uint64_t)NMB * HB;
   if (!run) {
@@ -2042,14 +2263,18 @@ __global__ __launch_bounds__(HB) void k2_handle(const P2PDev M) {
   PH_MARK(8);
   if (lt_ < 2 * K_NKINDS) s_look[lt_] = look_mine;
   __syncthreads();  // (s_lcnt, s_look)
+  const bool helped = !WIDE && c_nhub != 0;  // (a window with hubs: the holder blocks help the hub blocks first)
   if (bx < (uint32_t)NHB) {
-    if (handle) handle_node2<WIDE>(M, C, bx * HB + threadIdx.x, W, base, R, lds, hc, sp, &s_lcnt);
+    if (handle) {
+      if (helped) hub_help(M, C, bx * HB + threadIdx.x, W, base, hc, sp);
+      handle_node2<WIDE>(M, C, bx * HB + threadIdx.x, W, base, R, lds, hc, sp, &s_lcnt);
+    }
   } else if (bx < (uint32_t)(NHB + NHUB)) {
     if (handle) {
       const uint32_t hb = bx - NHB;
       const uint32_t nh = c_nhub < (uint32_t)MAXHUB ? c_nhub : (uint32_t)MAXHUB;
       for (uint32_t h = hb; h < nh; h += NHUB)
-        hub_node<WIDE>(M, C, M.hub_list[h], W, base, run || c_drun != 0, R, hb, lds, hc, &s_lcnt);
+        hub_node<WIDE>(M, C, M.hub_list[h], W, base, run || c_drun != 0, R, hb, lds, hc, &s_lcnt, helped);
     }
   } else if (bx < (uint32_t)K2_GRID_W) {
     if constexpr (XL) {  // k_gtile's accumulators for this window (k_dfin2 read the last window's: local

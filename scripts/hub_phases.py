@@ -21,7 +21,8 @@ nsgpu.check(nsgpu.lib().nsgpu_p2p_phase_read(buf.ctypes.data, 64, 1))
 w = max(int(st.windows), 1)
 calls = max(int(buf[28]), 1)
 print(f"dumbbell {leaves} leaves: {st.dispatched} events, {w} windows, {calls} hub-block calls ({calls / w:.2f} a window)")
-for i, nm in ((24, "window scan + sort"), (25, "node parts"), (26, "device steps"), (27, "publish / totals")):
+for i, nm in ((22, "wait for the holders"), (24, "window scan + sort"), (25, "node parts"), (23, "segment ops -> LDS"),
+              (26, "device steps"), (27, "publish / totals")):
     print(f"  {nm:20s} {buf[i] * 10.0 / calls / 1e3:8.3f} us per hub call")
 print(f"  events in hub calls {int(buf[30])} ({int(buf[30]) / calls:.0f} a call), of them serial node parts {int(buf[29])}; "
       f"serial loop time {buf[31] * 10.0 / calls / 1e3:.3f} us per hub call")

@@ -11,10 +11,12 @@
 #   rocprof_p2p      rocprofv3 kernel stats of the default bench (eager launches: the tracer cannot follow graphs)
 #   rocprof_wifil    rocprofv3 kernel stats of the closed-loop Wi-Fi line
 #   rocprof_dumbbell rocprofv3 kernel stats of the partitioned dumbbell line
+#   rocprof_dumbbell1 rocprofv3 kernel trace + stats of the single engine's dumbbell line
 #   rocprof_grid_part rocprofv3 kernel stats of the partitioned grid line (one rank)
 #   pmc_p2p          config-4 HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes -> traffic_p2p-grid.json
 #   pmc_lines        config-4 L2 / L1 request counters (TCC hit / miss / requests, TCP requests) per kernel
 #   pmc_sq_part      wave-state counters (SQ busy / wait / VALU / LDS) of the partitioned grid's kernels
+#   pmc_sq_p2p       wave-state counters (SQ wait / active / VMEM instructions) of config 4's kernels
 #   py:<script>      python scripts/<script> (diagnostics), output to OUT/<script>.log
 set -e
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -63,6 +65,10 @@ for st in "$@"; do
       cd /tmp
       NSGPU_P2P_EAGER=1 step rocprof_dumbbell 240 rocprofv3 --kernel-trace --stats -d $O/rocprof_dumbbell -o run --output-format csv -- python3 $R/bench.py --workload dumbbell --partitioned --steps 1 --warmup 0 --no-cpu-baseline
       cd $R ;;
+    rocprof_dumbbell1)  # the single engine's dumbbell: every dispatch (kernel_trace.csv) and the stats
+      cd /tmp
+      NSGPU_P2P_EAGER=1 step rocprof_dumbbell1 240 rocprofv3 --kernel-trace --stats -d $O/rocprof_dumbbell1 -o run --output-format csv -- python3 $R/bench.py --workload dumbbell --steps 1 --warmup 0 --no-cpu-baseline --no-secondary
+      cd $R ;;
     pmc_p2p)
       cd /tmp
       NSGPU_P2P_EAGER=1 step pmc_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_grid -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-secondary
@@ -78,6 +84,11 @@ for st in "$@"; do
       cd /tmp
       rocprofv3 -L > $O/avail_counters.txt 2>&1 || true
       NSGPU_P2P_EAGER=1 step pmc_sq_part 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq_part -o pmc -- python3 $R/bench.py --partitioned --steps 1 --warmup 0 --no-cpu-baseline
+      cd $R ;;
+    pmc_sq_p2p)  # wave-state counters of config 4's kernels (eager launches; one pass: 8 SQ counters)
+      cd /tmp
+      rocprofv3 -L > $O/avail_counters.txt 2>&1 || true
+      NSGPU_P2P_EAGER=1 step pmc_sq_p2p 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM --output-format csv -d $O/pmc_sq_p2p -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-secondary
       cd $R ;;
     py:*) s=${st#py:}; step ${s%%.py*} 600 python scripts/${s//,/ } ;;
     *) echo "unknown stage $st"; exit 2 ;;
