@@ -3326,6 +3326,12 @@ extern "C" int nsgpu_p2p_phase_read(uint64_t *out, int n, int reset) {
     uint64_t z[64] = {0};
     NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
   }
+  if (reset < 0) {  // (-w: the window the per-block stamps sample from now on; its old stamps cleared)
+    const uint64_t w = (uint64_t)(-(int64_t)reset);
+    NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_blk_win), &w, sizeof(w)));
+    std::vector<uint64_t> zb(3 * BLK_MAX * 2, 0);
+    NSGPU_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_blk), zb.data(), zb.size() * sizeof(uint64_t)));
+  }
   return NSGPU_OK;
 #else
   (void)out, (void)n, (void)reset;

@@ -216,6 +216,34 @@ __device__ __forceinline__ void node_table_finish(const P2PDev &M, Ctl &C, const
 __device__ __forceinline__ void node_table_add(const P2PDev &M, Ctl &C, uint32_t slot, uint32_t ctx, uint32_t kind) {
   node_table_finish(M, C, node_table_claim(M, slot, ctx, kind));
 }
+// node_table_claim for the wave's lanes with `on` (every lane of the wave calls it), the lanes whose node is the
+// first such lane's claimed with ONE atomic: a sorted run's chunk holds a hub's thousands of events, and their
+// count atomics on one word serialised (~10 ns each: k2_pa 51 us a chunk at a dumbbell router).  Which of a node's
+// slots gets which index does not matter (the holder sorts its node's events by key; a hub's block scans them).
+__device__ __forceinline__ NtClaim node_table_claim_wave(const P2PDev &M, uint32_t slot, uint32_t ctx, uint32_t kind,
+                                                         bool on) {
+  const bool dev_start = (kind & 0xffu) == K_DEV_START;
+  const bool nd = on && !dev_start && ctx < M.n_nodes;  // (a node's count claim)
+  const uint64_t mn = __ballot(nd);
+  NtClaim cl{slot, NOSRC, 0};
+  bool done = false;
+  if (mn) {
+    const int lead = __ffsll((unsigned long long)mn) - 1;
+    const uint32_t c0 = __shfl(ctx, lead);
+    const bool same = nd && ctx == c0;
+    const uint64_t ms = __ballot(same);
+    const int lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(&M.node_tab[(uint64_t)c0 * NTAB], (uint32_t)__popcll(ms));
+    base = __shfl(base, lead);
+    if (same) {
+      cl = NtClaim{slot, ctx, base + (uint32_t)__popcll(ms & ((1ull << lane) - 1ull))};
+      done = true;
+    }
+  }
+  if (on && !done) cl = node_table_claim(M, slot, ctx, kind);
+  return cl;
+}
 
 // A pending event against the window bound: window record (normal mode, key <= bound), else pending:
 // a child (src == NOSRC) is parked in the fresh buffer, a pool entry stays where it is; both fold
@@ -384,7 +412,7 @@ __device__ void drun_chunk(const P2PDev &M, Ctl &C, uint64_t t, uint64_t r0, uin
   const uint64_t i = r0 + t;
   const bool take = t < (uint64_t)WCAP && i < rW && M.rn_key[i] <= g;
   const bool next = t + 1 < (uint64_t)WCAP && i + 1 < rW && M.rn_key[i + 1] <= g;
-  NtClaim cl{0, NOSRC, 0};
+  uint32_t cc = NOSRC, ck = 0;
   if (take) {
     const uint64_t key = M.rn_key[i];
     const uint32_t ctx = M.rn_ctx[i], kind = M.rn_kind[i], a = M.rn_a[i];
@@ -394,8 +422,10 @@ __device__ void drun_chunk(const P2PDev &M, Ctl &C, uint64_t t, uint64_t r0, uin
     M.wa[t] = a;
     M.wpkt[t] = M.rn_pkt[i];
     M.wsrc[t] = M.rn_src[i];
-    cl = node_table_claim(M, (uint32_t)t, lp_of(M, ctx, kind, a), kind);
+    cc = lp_of(M, ctx, kind, a);
+    ck = kind;
   }
+  const NtClaim cl = node_table_claim_wave(M, (uint32_t)t, cc, ck, take);  // (a hub's claims aggregated)
   const uint32_t nb = (uint32_t)__syncthreads_count(take);
   if (threadIdx.x == 0 && nb) atomicAdd(&C.W, nb);
   node_table_finish(M, C, cl, true);
@@ -756,6 +786,18 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
         node_table_finish(M, C, k2_write(M, C, b, e, NOSRC, gin, gpk, w0, f0));
       }
     }
+    // the key fields only: most pool entries stay pending (the window entries' second load overlaps the block
+    // allocation, and the pool's other 24 B a slot are not fetched for the rest).  A large pool takes several
+    // chunks a block: the next chunk's keys are loaded before this one is classified (its trip overlaps this
+    // chunk's allocation and writes)
+    uint64_t nts[PPT];
+    uint32_t nuid[PPT], nkind[PPT];
+#pragma unroll
+    for (int q = 0; q < PPT; q++) {
+      const uint64_t i = pb * TB * PPT + (uint64_t)q * TB + threadIdx.x;
+      nts[q] = TOMB;
+      if (i < P) nts[q] = M.ev_ts[0][i], nuid[q] = M.ev_uid[0][i], nkind[q] = M.ev_kind[0][i];
+    }
     for (uint64_t c0 = pb * TB * PPT; c0 < P; c0 += npb * TB * PPT) {  // block-uniform trip count
 #pragma unroll
       for (int q = 0; q < PPT; q++) node_table_finish(M, C, pend[q]);  // (the last chunk's)
@@ -765,13 +807,12 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       bool gin[PPT], gpk[PPT];
       uint32_t cw = 0;
 #pragma unroll
-      for (int q = 0; q < PPT; q++) {
-        const uint64_t i = c0 + (uint64_t)q * TB + threadIdx.x;
-        ge[q] = Ev{TOMB, 0, 0, 0, 0, Pkt{0, 0, 0, 0}};
-        // the key fields only: most pool entries stay pending (these blocks are off the critical path,
-        // so the window entries' second load costs no window time, and the pool's other 24 B a slot
-        // are not fetched for the rest)
-        if (i < P) ge[q] = Ev{M.ev_ts[0][i], M.ev_uid[0][i], 0, M.ev_kind[0][i], 0, Pkt{0, 0, 0, 0}};
+      for (int q = 0; q < PPT; q++) ge[q] = Ev{nts[q], nuid[q], 0, nkind[q], 0, Pkt{0, 0, 0, 0}};
+#pragma unroll
+      for (int q = 0; q < PPT; q++) {  // (the next chunk's keys)
+        const uint64_t i = c0 + npb * TB * PPT + (uint64_t)q * TB + threadIdx.x;
+        nts[q] = TOMB;
+        if (i < P) nts[q] = M.ev_ts[0][i], nuid[q] = M.ev_uid[0][i], nkind[q] = M.ev_kind[0][i];
       }
       if (DF) {  // children the window before the last one parked: their uids resolve now (k2_sdef ran for it)
 #pragma unroll
@@ -797,9 +838,9 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
           ge[q].p = M.ev_pkt[0][i];
         }
       }
-      uint32_t w0;
-      uint64_t f0;
-      block_alloc2<TB>(C, cw, 0u, w0, f0);
+      uint32_t w0 = 0;
+      uint64_t f0 = 0;
+      if (__syncthreads_or(cw != 0)) block_alloc2<TB>(C, cw, 0u, w0, f0);  // (most chunks of a large pool: none)
 #ifdef NSGPU_PHASE_PROF
       if (c_win == g_blk_win) {  // (diagnostic: pool entries taken, pool chunks swept)
         if (cw) atomicAdd((unsigned long long *)&g_phase[49], (unsigned long long)cw);
@@ -826,9 +867,11 @@ __global__ __launch_bounds__(TB) void k2_pa(const P2PDev M) {
       C.split_lo = (r0 > 0 && (M.wkey[r0 - 1] >> 32) == klo) ? klo : ~0ull;
       C.split_hi = (r1 < rW && (M.wkey[r1] >> 32) == khi) ? khi : C.hrel;
     }
-    if (s < Wc) {
-      const uint32_t kw = M.wkind[r0 + s];
-      node_table_add(M, C, (uint32_t)s, lp_of(M, M.wctx[r0 + s], kw, M.wa[r0 + s]), kw);
+    {  // (every lane: the claims of one node are aggregated over the wave)
+      const bool on = s < Wc;
+      const uint32_t kw = on ? M.wkind[r0 + s] : 0u;
+      const uint32_t c = on ? lp_of(M, M.wctx[r0 + s], kw, M.wa[r0 + s]) : NOSRC;
+      node_table_finish(M, C, node_table_claim_wave(M, (uint32_t)s, c, kw, on));
     }
   }
   PH_MARK(1);
