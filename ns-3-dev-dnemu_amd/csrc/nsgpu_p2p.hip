@@ -50,7 +50,11 @@ constexpr int NJT = WCAP / RJ;   // rank tile columns
 constexpr int RTR = 1;           // window keys (rows) per thread of a rank tile (4: same traffic, slower)
 constexpr int NRT = WCAP / (HB * RTR);  // rank tile rows
 constexpr int NRB = NRT * NJT;   // rank tile blocks (k2_handle)
-constexpr int GRID_POOL = 256;   // blocks of the pool sweep (grid-stride)
+#ifndef GRID_POOL_N
+#define GRID_POOL_N 256
+#endif
+constexpr int GRID_POOL = GRID_POOL_N;   // blocks of the pool sweep (grid-stride; r06: 1,024 measured slower on
+                                         // config 4 and on the dumbbell's 5 M-entry pool: per-block reductions)
 #ifndef PA_SLOT_LANES
 #define PA_SLOT_LANES 256        // k2_pa (single engine): last-window records per slot block (diagnostic override)
 #endif
