@@ -578,15 +578,27 @@ __device__ __forceinline__ u128 divu(u128 a, u128 b) {
   quo = rem / div;
   return result + quo;
 }
+// Invert (1e9) (int64x64-128.cc:119-134): the same steps, evaluated at compile time (per call, its 128-bit
+// divisions took thousands of instructions a lane; a wave of OnOff StopApplications paid them in every window)
+constexpr u128 c_umul_by_invert(u128 a, u128 b) {
+  const u128 LO = (((u128)1) << 64) - 1;
+  return (a >> 64) * (b >> 64) + (((a >> 64) * (b & LO) + (a & LO) * (b >> 64)) >> 64);
+}
+constexpr u128 c_divu(u128 a, u128 b) {
+  const u128 quo = a / b, rem = a % b;
+  const bool small = (rem >> 64) == 0;
+  return (quo << 64) + (small ? (rem << 64) / b : rem / (b >> 64));
+}
+constexpr i128 c_invert_1e9() {
+  i128 inv = (i128)c_divu(((u128)1) << 64, (u128)1000000000ull);
+  const u128 r = c_umul_by_invert((u128)(((i128)1000000000ll) << 64), (u128)inv);
+  if ((int64_t)(r >> 64) != 1) inv += 1;
+  return inv;
+}
 __device__ __noinline__ int64_t residual_bits(int64_t delta_ns, uint64_t rate) {
-  // Invert (1e9) (int64x64-128.cc:119-134)
-  u128 one = ((u128)1) << 64;
-  i128 inv = (i128)divu(one, (u128)1000000000ull);
-  {
-    i128 tmp = ((i128)1000000000ll) << 64;
-    u128 r = umul_by_invert((u128)tmp, (u128)inv);
-    if ((int64_t)(r >> 64) != 1) inv += 1;
-  }
+  constexpr i128 inv = c_invert_1e9();
+  static_assert((uint64_t)((u128)inv >> 64) == 0x44b82fa09ull && (uint64_t)(u128)inv == 0xb5a52cb98b405448ull,
+                "Invert (1e9)");
   // MulByInvert (delta)
   i128 v = ((i128)delta_ns) << 64;
   bool neg = v < 0;

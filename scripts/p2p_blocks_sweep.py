@@ -1,7 +1,7 @@
 """Diagnostic: per-block spans of the window kernels at sampled windows across one scenario's run
-(lib/libnsgpu_prof.so).  Usage: python scripts/p2p_blocks_sweep.py dumbbell|grid [step] [n]
+(lib/libnsgpu_prof.so).  Usage: python scripts/p2p_blocks_sweep.py dumbbell|grid [step] [n] [first] [count]
 Each sample re-runs the engine with the per-block stamps aimed at window w (nsgpu_p2p_phase_read(-w)) and
-prints, per kernel, the span and each role's latest end (us), with the window's size from the phase words."""
+prints, per kernel, the span and each role's median / latest block end (us), with the window's size from the phase words."""
 import os
 import sys
 
@@ -28,9 +28,11 @@ wide = eng.wide()
 nslot = (4096 + 4096) // 256 if wide else 16
 roles = {0: [("slot", 0, nslot), ("pool", nslot, 256)],
          1: [("holder", 0, 64), ("hub", 64, 96), ("maint", 96, 224), ("rank", 224, 1248)],
-         2: [("scan", 0, 4)]}
+         2: [("book", 0, 1), ("sdef", 1, 5), ("tiles", 5, 256)] if wide else [("scan", 0, 1)]}
 names = ("k2_pa", "k2_handle", "k2_rank" if wide else "k2_scan")
-for w in range(1, W, step):
+first = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+count = int(sys.argv[5]) if len(sys.argv) > 5 else W
+for w in list(range(first, W, step))[:count]:
     nsgpu.check(nsgpu.lib().nsgpu_p2p_phase_read(buf.ctypes.data, 64, -w))
     eng.run()
     nsgpu.check(nsgpu.lib().nsgpu_p2p_phase_read(buf.ctypes.data, buf.size, 0))
@@ -47,6 +49,7 @@ for w in range(1, W, step):
         for rn, lo, hi in roles[k]:
             r = b[lo:hi][ok[lo:hi]]
             if len(r):
-                rs.append(f"{rn} {(r[:, 1].max() - t0) * 0.01:.1f}")
+                en = (r[:, 1] - t0) * 0.01
+                rs.append(f"{rn} {np.median(en):.1f}/{en.max():.1f}")
         parts.append(f"{name} {(b[ok, 1].max() - t0) * 0.01:.1f} ({', '.join(rs)})")
     print(f"w {w:5d}: pool end {int(buf[46]):8d} gen0 {int(buf[47]):5d} | " + " | ".join(parts), flush=True)
