@@ -234,6 +234,19 @@ int nsgpu_wifil_listen(nsgpu_wifil *h, uint32_t phy, int on);
 int nsgpu_wifil_send_plan(const nsgpu_wifil_config *cfg, uint32_t sender, uint32_t uid_base, uint32_t *rx_phy,
                           uint32_t *rx_uid, uint32_t *rx_ctx, uint64_t cap, uint64_t *n);
 int nsgpu_wifil_next_end(nsgpu_wifil *h, nsgpu_wifil_next *out);
+/* Partitioned closed-loop PHY (YansWifiChannel::Send, yans-wifi-channel.cc:77-115, fans a SendPacket out to
+ * every receiver; the receivers are split over GPUs).  Every rank runs the same host program (MAC closures, uids,
+ * GetState) over the returned handle, which takes every nsgpu_wifil_* call above; the device work of phys
+ * [phy_begin, phy_end) — their Receives, InterferenceHelper, state machine, EndReceive — runs on this rank.  Per epoch
+ * the ranks all-gather (RCCL on comm, one rank per GPU) the syncs (EndReceive uids = ranks among every rank's syncs),
+ * the counters, end records and phy state fields, and the dispatched events (ordered once for digest and log): every
+ * rank then returns what the single engine returns.  The ranks' ranges must tile [0, n_phy) in rank order.  A loopback
+ * group (nsgpu_wifil_create_group: partitions [bounds[q], bounds[q+1]), q < n, all on this device, exchanging through
+ * device copies) is the same split in one process (tests).  Replaces no reference interface: YansWifiChannel is not
+ * distributed in the reference (DistributedSimulatorImpl carries p2p links only). */
+int nsgpu_wifil_create_dist(const nsgpu_wifil_config *cfg, int64_t phy_begin, int64_t phy_end, nsgpu_comm *comm,
+                            nsgpu_wifil **out);
+int nsgpu_wifil_create_group(const nsgpu_wifil_config *cfg, const int64_t *bounds, int n, nsgpu_wifil **out);
 
 /* ---------------- GPU-resident bench-simulator churn (config 1) ----------------
  * Runs utils/bench-simulator.cc's RunBench + Simulator::Run (bench-simulator.cc:79-127) over

@@ -134,6 +134,13 @@ struct WDev {
   uint64_t ev_scap;  // events per stripe (stripe s holds ev[s * ev_scap, s * ev_scap + evc[s * EV_STRIDE]))
   const uint32_t *lis;  // the phys whose EndReceives the host takes back (nsgpu_wifil_listen), nlis of them
   uint32_t nlis, pad_lis;
+  // a partition of the phys (nsgpu_wifil_create_dist / _group): this engine runs phys [j0, j0 + nown) — their
+  // waves, Receives, pending records — while every array stays indexed by the global phy; a single engine has
+  // j0 = 0, nown = nphy.  xsync: every partition's syncs of the epoch (xn of them) the sync order ranks this
+  // partition's against (null: its own, the single engine).
+  int64_t j0, nown;
+  const LSync *xsync;
+  uint32_t xn, pad_x;
 };
 // The epoch's dispatched events are appended to EV_STRIPES lists (phy j's to stripe j % EV_STRIPES): one
 // counter a phy's event would serialize ~10^4 atomics an epoch on one line.
@@ -435,8 +442,8 @@ __device__ unsigned long long g_wrec[WREC_E][WREC_P][5];
 __device__ uint32_t g_wepoch, g_wtarget;
 #endif
 __global__ __launch_bounds__(64) void k_wl_step(const WDev D, uint64_t bts, uint32_t buid) {
-  const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (j >= D.nphy) return;
+  const int64_t j = D.j0 + (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (j >= D.j0 + D.nown) return;
 #ifdef NSGPU_PHASE_PROF
   const uint64_t pt0 = __builtin_amdgcn_s_memrealtime();
   uint32_t pev = 0;
@@ -778,9 +785,9 @@ __device__ __forceinline__ LRx shfl_up_rx(const LRx &a) {
 // key below (bts, buid), in (ts, uid) order.
 __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uint32_t buid,
                                                                                    const SendBatch sb) {
-  const int64_t j = blockIdx.x;
+  const int64_t j = D.j0 + blockIdx.x;
   const uint32_t lane = threadIdx.x;
-  if (j >= D.nphy) return;
+  if (j >= D.j0 + D.nown) return;
 #ifdef NSGPU_PHASE_PROF
   const uint64_t pt0 = __builtin_amdgcn_s_memtime();
   uint64_t pt1 = pt0, pt2 = pt0;
@@ -1247,14 +1254,18 @@ __device__ __forceinline__ void wl_per(const WDev &D, uint32_t bx, uint32_t nbx,
   }
 }
 
-// The epoch's syncs in dispatch order (ts, uid of the syncing Receive): EndReceive uid = uid0 + rank.
+// The epoch's syncs in dispatch order (ts, uid of the syncing Receive): EndReceive uid = uid0 + rank.  A
+// partition ranks its own syncs among every partition's (D.xsync: keys are unique, so the order of the gather
+// does not matter).
 __device__ __forceinline__ void wl_sync_rank(const WDev &D, uint32_t uid0, uint32_t bx, uint32_t nbx) {
   const uint32_t n = D.cnt[1] < D.sync_cap ? D.cnt[1] : (uint32_t)D.sync_cap;
+  const LSync *const X = D.xsync ? D.xsync : D.sync;
+  const uint32_t nx = D.xsync ? D.xn : n;
   for (uint32_t i = bx * 256 + threadIdx.x; i < n; i += nbx * 256) {
     const LSync a = D.sync[i];
     uint32_t r = 0;
-    for (uint32_t k = 0; k < n; k++) {
-      const LSync b = D.sync[k];
+    for (uint32_t k = 0; k < nx; k++) {
+      const LSync b = X[k];
       r += b.sts < a.sts || (b.sts == a.sts && b.suid < a.suid);
     }
     D.sync[i].euid = uid0 + r;
@@ -1382,8 +1393,8 @@ __global__ __launch_bounds__(256) void k_wl_gather(const WDev D) {
   __shared__ uint32_t s_wt[4], s_base, s_sbase;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t nstr = blockIdx.x == 0 ? load_stripes(D, sm) : 0u;
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + tid;
-  const uint32_t n = j < (uint64_t)D.nphy ? D.evn[j] : 0u;
+  const uint64_t j = (uint64_t)D.j0 + (uint64_t)blockIdx.x * 256 + tid;
+  const uint32_t n = j < (uint64_t)(D.j0 + D.nown) ? D.evn[j] : 0u;
   if (n) D.evn[j] = 0;  // (for the epoch two on, which reuses this parity)
   uint32_t x = n;
 #pragma unroll
@@ -1513,18 +1524,21 @@ __global__ __launch_bounds__(TS_T) void k_wl_rank(const WDev D, uint64_t K0, int
   if (tid < (uint32_t)EV_STRIPES) D.evc[tid * EV_STRIDE] = 0, D.evt[tid * EV_STRIDE] = 0;
 }
 
-// (diagnostic, NSGPU_WIFIL_NOORDER=1) what k_wl_rank's last block zeroes, without the order
+// (diagnostic, NSGPU_WIFIL_NOORDER=1) what k_wl_rank's last block zeroes, without the order; and (partitions,
+// whose epochs are ordered over every partition's gathered events) the partition's own lists once gathered
 __global__ void k_wl_zero(const WDev D) {
   const uint32_t tid = threadIdx.x;
   if (tid < 3 || tid == 4) D.cnt[tid] = 0;
   if (tid < (uint32_t)EV_STRIPES) D.evc[tid * EV_STRIDE] = 0, D.evt[tid * EV_STRIDE] = 0;
+  if (tid == 5 && D.gtot) *D.gtot = 0;
 }
+__global__ void k_wl_set(uint32_t *p, uint32_t v) { *p = v; }
 
 // SendPacket of phy s at (ts): the sender's state switch (thread s) and one Receive per receiver.
 __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t, double dbm, uint32_t base) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j == 0) D.tx[k] = t;
-  if (j >= D.nphy) return;
+  const int64_t j = D.j0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) D.tx[k] = t;  // (every partition holds every transmission)
+  if (j >= D.j0 + D.nown) return;
   const uint32_t s = t.phy;
   if ((uint32_t)j == s) {  // YansWifiPhy::SendPacket (yans-wifi-phy.cc:499-522)
     LPhy &P = D.ps[j];
@@ -1539,6 +1553,7 @@ __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t
       P.endRx = (int64_t)t.ts;
     }
     P.endTx = (int64_t)t.ts + t.dur;
+    D.mir[j] = mir_of(P);  // (the host applied the same switch to its copy; a partition's mirror is gathered)
     return;
   }
   LRx e;
@@ -1566,9 +1581,9 @@ __global__ __launch_bounds__(256) void k_wl_send(const WDev D, uint32_t k, LTx t
 // host goes on — into the batch's row of D.rxb; the next epoch's k_wl_stepw queues them.  Thread 0 records
 // the transmission.
 __global__ __launch_bounds__(256) void k_wl_rx(const WDev D, LRx *row, LTx t, uint32_t k, double dbm, uint32_t base) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j == 0) D.tx[k] = t;
-  if (j >= D.nphy) return;
+  const int64_t j = D.j0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) D.tx[k] = t;
+  if (j >= D.j0 + D.nown) return;
   LRx e{};
   if (j == (int64_t)t.phy || !reception(D, j, t, k, dbm, base, e)) e.at = ~0ull;
   row[j] = e;
@@ -1576,8 +1591,8 @@ __global__ __launch_bounds__(256) void k_wl_rx(const WDev D, LRx *row, LTx t, ui
 
 // Pending device events and the smallest ts among them (Next / IsFinished).
 __global__ __launch_bounds__(256) void k_wl_pending(const WDev D, unsigned long long *out) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= D.nphy) return;
+  const int64_t j = D.j0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= D.j0 + D.nown) return;
   const LPhy P = D.ps[j];
   uint64_t n = P.rq_len, mt = P.rq_len ? D.rq[(uint64_t)j * (D.rq_mask + 1) + (P.rq_head & D.rq_mask)].at : ~0ull;
   for (int q = 0; q < LPE_CAP; q++) {
@@ -1707,7 +1722,29 @@ struct nsgpu_wifil {
   bool lis_dirty = false;
   uint32_t *d_lis = nullptr;
   unsigned long long *d_next = nullptr, *h_next = nullptr;
+  // ---- a partitioned PHY (nsgpu_wifil_create_dist / nsgpu_wifil_create_group): this handle is the host side
+  // every rank replicates (the MAC's closures, the uids, GetState, the ends); `mem` are the partitions it runs —
+  // one (RCCL: `comm`, the others on other GPUs) or all of them (a loopback group on this device) — each an engine
+  // over its phys [lo, hi) with every array indexed by the global phy, launched on this handle's stream.
+  std::vector<nsgpu_wifil *> mem;
+  nsgpu_comm *comm = nullptr;
+  std::vector<int64_t> plo, phi;  // every partition's phys (RCCL: gathered at create)
+  int64_t pmax = 0;               // the largest partition (the gathers' padding)
+  WDev U{};                       // the order over every partition's events (k_wl_tsort / k_wl_rank)
+  LSync *xsync = nullptr;         // every partition's syncs of the epoch
+  LSync *xsr = nullptr;           // (RCCL) their gather, padded
+  LEv *xev = nullptr;             // (RCCL) the events' gather, padded
+  nsgpu_wifil_end *uend = nullptr, *xend = nullptr;  // every partition's end records; (RCCL) their gather, padded
+  WMir *xmir = nullptr, *dmir = nullptr, *smir = nullptr;  // (RCCL) mirror: gather, the partition's, send staging
+  uint8_t *xps = nullptr, *sps = nullptr;                  // (RCCL) phy states for read_phys: gather, staging
+  unsigned long long *xsm = nullptr;                       // (RCCL) small per-rank words: gather
+  unsigned long long *ssm = nullptr;                       // (RCCL) small per-rank words: send
+  uint64_t u_evcap = 0, g_sync_cap = 0, g_end_cap = 0;
 };
+
+// Blocks of b threads over n phys (at least one: a partition with no phys still records a transmission, and
+// its kernels return at once).
+static unsigned wl_grid(int64_t n, int b) { return (unsigned)std::max<int64_t>((n + b - 1) / b, 1); }
 
 // The epoch's status block (counters, digest, end records) is stat[b].
 static void wl_use_stat(nsgpu_wifil *h, uint32_t b) {
@@ -1735,6 +1772,12 @@ static int wl_alloc(nsgpu_wifil *h, T **p, size_t n, const T *src = nullptr) {
 
 extern "C" int nsgpu_wifil_destroy(nsgpu_wifil *h) {
   if (!h) return NSGPU_OK;
+  if (h->s) (void)hipStreamSynchronize(h->s);
+  for (nsgpu_wifil *m : h->mem) {  // (a partition runs on this handle's stream)
+    m->s = nullptr;
+    nsgpu_wifil_destroy(m);
+  }
+  h->mem.clear();
   if (h->hprof && h->hp_n)
     fprintf(stderr, "nsgpu_wifil host: %llu epochs, per epoch (us): launches %.2f, wait %.2f, rest of advance %.2f, "
             "between advances %.2f\n", (unsigned long long)h->hp_n, h->hp_launch / 1e3 / h->hp_n, h->hp_wait / 1e3 / h->hp_n,
@@ -1765,7 +1808,26 @@ static int wl_prio(bool high) {
   return high ? greatest : least;
 }
 
-extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out) {
+// Each phy's place among the phys of its channel (YansWifiChannel::Send's receiver loop, m_phyList order) and the
+// Receives one SendPacket of it schedules (the other phys of its channel).
+static void wl_channel_ranks(const nsgpu_wifil_config *c, std::vector<uint32_t> &rank, std::vector<uint32_t> &recv) {
+  const int64_t N = c->n_phy;
+  rank.assign((size_t)N, 0);
+  recv.assign((size_t)N, 0);
+  std::vector<std::pair<uint32_t, uint32_t>> cnt;  // (channel, count so far)
+  for (int64_t j = 0; j < N; j++) {
+    auto it = std::find_if(cnt.begin(), cnt.end(), [&](const std::pair<uint32_t, uint32_t> &p) { return p.first == c->channel[j]; });
+    if (it == cnt.end()) cnt.emplace_back(c->channel[j], 0), it = cnt.end() - 1;
+    rank[j] = it->second++;
+  }
+  for (int64_t j = 0; j < N; j++)
+    for (auto &p : cnt)
+      if (p.first == c->channel[j]) recv[j] = p.second - 1;
+}
+
+// An engine over phys [j0, j0 + nown) of the config (the single engine: all of them); its epoch lists are sized
+// for capn phys (a partition: the largest partition's, so that every rank's lists hold a gather's padding).
+static int wl_create(const nsgpu_wifil_config *c, int64_t j0, int64_t nown, int64_t capn, nsgpu_wifil **out) {
   if (!c || !out || c->n_phy <= 0 || !c->x || !c->y || !c->z || !c->channel || !c->node)
     return set_error(NSGPU_EINVAL, "nsgpu_wifil_create: bad config");
   const auto pow2 = [](uint32_t v) { return v >= 2 && (v & (v - 1)) == 0; };
@@ -1780,6 +1842,8 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   const int64_t N = c->n_phy;
   WDev &D = h->D;
   D.nphy = N;
+  D.j0 = j0;
+  D.nown = nown;
   D.loss = c->loss;
   D.speed = c->speed;
   D.rx_gain_db = c->rx_gain_db;
@@ -1793,20 +1857,9 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   D.inv_hi = (uint64_t)(inv >> 64);
   D.inv_lo = (uint64_t)inv;
   // the receiver loop's order on each channel (m_phyList order)
-  std::vector<uint32_t> rank((size_t)N);
-  h->recv.resize((size_t)N);
-  {
-    std::vector<std::pair<uint32_t, uint32_t>> cnt;  // (channel, count so far)
-    for (int64_t j = 0; j < N; j++) {
-      auto it = std::find_if(cnt.begin(), cnt.end(), [&](const std::pair<uint32_t, uint32_t> &p) { return p.first == c->channel[j]; });
-      if (it == cnt.end()) cnt.emplace_back(c->channel[j], 0), it = cnt.end() - 1;
-      rank[j] = it->second++;
-    }
-    for (int64_t j = 0; j < N; j++)
-      for (auto &p : cnt)
-        if (p.first == c->channel[j]) h->recv[j] = p.second - 1;
-  }
-  const uint64_t ev_cap = (uint64_t)N * 64 + 4096, sync_cap = (uint64_t)N * LPE_CAP + 1024;
+  std::vector<uint32_t> rank;
+  wl_channel_ranks(c, rank, h->recv);
+  const uint64_t ev_cap = (uint64_t)capn * 64 + 4096, sync_cap = (uint64_t)capn * LPE_CAP + 1024;
   int rc;
 #define WL_TRY(x)                \
   if ((rc = (x)) != NSGPU_OK) {  \
@@ -1844,7 +1897,7 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   // deferred chunks an epoch (~100-600 an EndReceive): 64 MB, or 512 a phy (k_wl_stepw has no inline
   // fallback — its error-rate models would take ~130 more VGPRs and scratch from every lane: a full pool
   // fails the run, WE_CKCAP)
-  D.ck_cap = std::max<uint64_t>(1ull << 22, (uint64_t)N * 512);
+  D.ck_cap = std::max<uint64_t>(1ull << 22, (uint64_t)capn * 512);
   WL_TRY(wl_alloc(h, &D.ck, (size_t)D.ck_cap));
   WL_TRY(wl_alloc(h, &D.erank, std::min<uint64_t>(ev_cap, ERANK_MAX)));
   WL_TRY(wl_alloc(h, &D.ticket, 1));
@@ -1894,6 +1947,11 @@ extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out
   return NSGPU_OK;
 }
 
+extern "C" int nsgpu_wifil_create(const nsgpu_wifil_config *c, nsgpu_wifil **out) {
+  if (!c || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifil_create: bad config");
+  return wl_create(c, 0, c->n_phy, c->n_phy, out);
+}
+
 extern "C" int nsgpu_wifil_receivers(nsgpu_wifil *h, uint32_t phy, uint32_t *n) {
   if (!h || !n || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_receivers: bad phy");
   *n = h->recv[phy];
@@ -1923,24 +1981,26 @@ extern "C" int nsgpu_wifil_send_plan(const nsgpu_wifil_config *c, uint32_t sende
   return NSGPU_OK;
 }
 
-static int wl_check(nsgpu_wifil *h, const char *what) {
-  const uint32_t e = h->h_cnt[3];
+static int wl_check_bits(uint32_t e, const char *what) {
   if (!e) return NSGPU_OK;
   if (e & WE_TX_IN_TX)
     return set_error(NSGPU_ESTATE, "%s: SendPacket while transmitting (yans-wifi-phy.cc:508 NS_ASSERT)", what);
   return set_error(NSGPU_ENOMEM, "%s: capacity exceeded (bits %u: 2 NiChanges ring, 4 Receive queue, 8 pending "
                                  "EndReceive records, 16 epoch lists, 32 CalculatePer chunk pool)", what, e);
 }
+static int wl_check(nsgpu_wifil *h, const char *what) { return wl_check_bits(h->h_cnt[3], what); }
 
 // The batched SendPackets as k_wl_send launches (before anything that reads the phys or moves one).
 static int wl_flush_sends(nsgpu_wifil *h) {
-  const unsigned g = (unsigned)((h->D.nphy + 255) / 256);
+  const unsigned g = wl_grid(h->D.nown, 256);
   for (uint32_t i = 0; i < h->sb.n; i++)
     hipLaunchKernelGGL(k_wl_send, dim3(g), dim3(256), 0, h->s, h->D, h->sb.k0 + i, h->sb.t[i], h->sb.dbm[i], h->sb.base[i]);
   h->sb.n = 0;
   NSGPU_HIP(hipGetLastError());
   return NSGPU_OK;
 }
+
+static int wl_queue_send(nsgpu_wifil *h, const LTx &t, double dbm, uint32_t uid_base);
 
 // YansWifiPhy::SendPacket of `phy` from the host closure running at (now, closure uid); its fan-out takes
 // the uids uid_base .. uid_base + receivers - 1 (nsgpu_wifil_receivers).
@@ -1955,19 +2015,28 @@ extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base,
   int64_t dur = 0;
   int rc = nsgpu_wifi_tx_duration_ns(size, modclass, rate, bw, preamble, &dur);  // CalculateTxDuration
   if (rc) return rc;
-  LTx t{now, dur, rate, phy, modclass, bw, preamble};
-  if (h->sb.n == NSEND) {
-    int rcf = wl_flush_sends(h);
-    if (rcf) return rcf;
-  }
-  const uint32_t k = (uint32_t)h->n_tx++;
+  const LTx t{now, dur, rate, phy, modclass, bw, preamble};
   WMir &mr = h->h_mir[phy];  // the sender's switch (k_wl_send's), in the host's copy of its state fields
   if (!(mr.endTx > (int64_t)now)) {
     if (mr.rxing) mr.rxing = 0, mr.endRx = (int64_t)now;
     mr.endTx = (int64_t)now + dur;
   }
+  if (h->mem.empty()) return wl_queue_send(h, t, dbm, uid_base);
+  h->n_tx++;
+  for (nsgpu_wifil *m : h->mem)  // (every partition records the transmission; its receivers take their Receives)
+    if (int rcm = wl_queue_send(m, t, dbm, uid_base)) return rcm;
+  return NSGPU_OK;
+}
+
+// A SendPacket into the engine's batch (applied by its next epoch launch), its Receives computed now (k_wl_rx).
+static int wl_queue_send(nsgpu_wifil *h, const LTx &t, double dbm, uint32_t uid_base) {
+  if (h->sb.n == NSEND) {
+    int rcf = wl_flush_sends(h);
+    if (rcf) return rcf;
+  }
+  const uint32_t k = (uint32_t)h->n_tx++;
   if (h->sb.n == 0) h->sb.k0 = k;
-  hipLaunchKernelGGL(k_wl_rx, dim3((unsigned)((h->D.nphy + 255) / 256)), dim3(256), 0, h->s, h->D,
+  hipLaunchKernelGGL(k_wl_rx, dim3(wl_grid(h->D.nown, 256)), dim3(256), 0, h->s, h->D,
                      h->D.rxb + (uint64_t)h->sb.n * h->D.nphy, t, k, dbm, uid_base);
   NSGPU_HIP(hipGetLastError());
   h->sb.t[h->sb.n] = t;
@@ -1983,7 +2052,7 @@ extern "C" int nsgpu_wifil_send(nsgpu_wifil *h, uint64_t now, uint32_t uid_base,
 static int wl_launch_order(nsgpu_wifil *h, const WDev &D, uint32_t b, uint64_t K0, int keep) {
   NSGPU_HIP(hipEventRecord(h->ev_fin[b], h->s));
   NSGPU_HIP(hipStreamWaitEvent(h->s2, h->ev_fin[b], 0));
-  hipLaunchKernelGGL(k_wl_gather, dim3((unsigned)((D.nphy + 255) / 256)), dim3(256), 0, h->s2, D);
+  hipLaunchKernelGGL(k_wl_gather, dim3(wl_grid(D.nown, 256)), dim3(256), 0, h->s2, D);
   hipLaunchKernelGGL(k_wl_tsort, dim3(NTILE), dim3(TS_T), 0, h->s2, D);
   hipLaunchKernelGGL(k_wl_rank, dim3(NTILE), dim3(TS_T), 0, h->s2, D, K0, keep, h->d_digtot);
   NSGPU_HIP(hipGetLastError());
@@ -1992,6 +2061,11 @@ static int wl_launch_order(nsgpu_wifil *h, const WDev &D, uint32_t b, uint64_t K
   return NSGPU_OK;
 }
 
+static int wlg_advance(nsgpu_wifil *G, uint64_t bts, uint32_t buid, uint32_t *uid, uint64_t *dispatched, uint64_t *digest,
+                       uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap);
+static int wlg_pending(nsgpu_wifil *G, uint64_t *n, uint64_t *next_ts);
+static int wlg_next_end(nsgpu_wifil *G, nsgpu_wifil_next *out);
+
 // Every device event with a key below (bound_ts, bound_uid) (~0: all of them): dispatched in (ts, uid) order
 // from rank *dispatched on; the syncs' EndReceives take the uids from *uid on.  The dispatches are added to
 // the caller's digest (nsgpu_dispatch_digest_term) and log (at their ranks, below log_cap).
@@ -1999,6 +2073,7 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
                                    uint64_t *dispatched, uint64_t *digest, uint64_t *log_ts, uint32_t *log_uid,
                                    uint32_t *log_ctx, uint64_t log_cap) {
   if (!h || !uid || !dispatched || !digest) return set_error(NSGPU_EINVAL, "nsgpu_wifil_advance: null");
+  if (!h->mem.empty()) return wlg_advance(h, bound_ts, bound_uid, uid, dispatched, digest, log_ts, log_uid, log_ctx, log_cap);
   using clk = std::chrono::steady_clock;
   const clk::time_point hp0 = h->hprof ? clk::now() : clk::time_point{};
   if (h->hprof && h->hp_n) h->hp_out += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(hp0 - h->hp_last).count();
@@ -2018,9 +2093,9 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
   if (lane_step) {
     int rcf = wl_flush_sends(h);
     if (rcf) return rcf;
-    hipLaunchKernelGGL(k_wl_step, dim3((unsigned)((D.nphy + 63) / 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
+    hipLaunchKernelGGL(k_wl_step, dim3(wl_grid(D.nown, 64)), dim3(64), 0, h->s, D, bound_ts, bound_uid);
   } else {
-    hipLaunchKernelGGL(k_wl_stepw, dim3((unsigned)D.nphy), dim3(64), 0, h->s, D, bound_ts, bound_uid, h->sb);
+    hipLaunchKernelGGL(k_wl_stepw, dim3(wl_grid(D.nown, 1)), dim3(64), 0, h->s, D, bound_ts, bound_uid, h->sb);
     h->sb.n = 0;
   }
 #ifdef NSGPU_PHASE_PROF
@@ -2131,7 +2206,7 @@ extern "C" int nsgpu_wifil_advance(nsgpu_wifil *h, uint64_t bound_ts, uint32_t b
 // digest terms it summed since the last advance / flush.
 extern "C" int nsgpu_wifil_flush(nsgpu_wifil *h, uint64_t *digest) {
   if (!h || !digest) return set_error(NSGPU_EINVAL, "nsgpu_wifil_flush: null");
-  NSGPU_HIP(hipStreamSynchronize(h->s2));
+  NSGPU_HIP(hipStreamSynchronize(h->mem.empty() ? h->s2 : h->s));  // (a partitioned PHY orders every epoch at once)
   const uint64_t tot = *h->h_digtot;
   *digest += tot - h->dig_added;
   h->dig_added = tot;
@@ -2144,6 +2219,11 @@ extern "C" int nsgpu_wifil_flush(nsgpu_wifil *h, uint64_t *digest) {
 // the sends.
 extern "C" int nsgpu_wifil_set_position(nsgpu_wifil *h, uint32_t phy, double x, double y, double z) {
   if (!h || phy >= h->D.nphy) return set_error(NSGPU_EINVAL, "nsgpu_wifil_set_position: bad phy");
+  if (!h->mem.empty()) {  // (every partition holds every position)
+    for (nsgpu_wifil *m : h->mem)
+      if (int rcm = nsgpu_wifil_set_position(m, phy, x, y, z)) return rcm;
+    return NSGPU_OK;
+  }
   if (int rcf = wl_flush_sends(h)) return rcf;  // (the sends so far see the positions they were made with)
   const double v[3] = {x, y, z};
   double *dst[3] = {const_cast<double *>(h->D.x), const_cast<double *>(h->D.y), const_cast<double *>(h->D.z)};
@@ -2185,23 +2265,27 @@ extern "C" int nsgpu_wifil_read_ends(nsgpu_wifil *h, nsgpu_wifil_end *out, uint6
   return NSGPU_OK;
 }
 
+static nsgpu_wifi_phy_counters wl_counters(const LPhy &p) {
+  nsgpu_wifi_phy_counters c = p.c;
+  c.ni_len = p.len;
+  c.ni_max = p.ni_max;
+  c.end_tx = p.endTx;
+  c.end_rx = p.endRx;
+  c.end_cca_busy = p.endCca;
+  c.first_power = p.firstPower;
+  c.rxing = p.rxing;
+  return c;
+}
+static int wlg_read_phys(nsgpu_wifil *G, nsgpu_wifi_phy_counters *out);
+
 extern "C" int nsgpu_wifil_read_phys(nsgpu_wifil *h, nsgpu_wifi_phy_counters *out) {
   if (!h || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifil_read_phys: null");
+  if (!h->mem.empty()) return wlg_read_phys(h, out);
   if (int rcf = wl_flush_sends(h)) return rcf;
   std::vector<LPhy> ps((size_t)h->D.nphy);
   NSGPU_HIP(hipMemcpyAsync(ps.data(), h->D.ps, ps.size() * sizeof(LPhy), hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipStreamSynchronize(h->s));
-  for (size_t j = 0; j < ps.size(); j++) {
-    nsgpu_wifi_phy_counters c = ps[j].c;
-    c.ni_len = ps[j].len;
-    c.ni_max = ps[j].ni_max;
-    c.end_tx = ps[j].endTx;
-    c.end_rx = ps[j].endRx;
-    c.end_cca_busy = ps[j].endCca;
-    c.first_power = ps[j].firstPower;
-    c.rxing = ps[j].rxing;
-    out[j] = c;
-  }
+  for (size_t j = 0; j < ps.size(); j++) out[j] = wl_counters(ps[j]);
   return NSGPU_OK;
 }
 
@@ -2220,6 +2304,7 @@ extern "C" int nsgpu_wifil_listen(nsgpu_wifil *h, uint32_t phy, int on) {
 // sync not yet made could put one (see the kernel).  Valid between advances.
 extern "C" int nsgpu_wifil_next_end(nsgpu_wifil *h, nsgpu_wifil_next *out) {
   if (!h || !out) return set_error(NSGPU_EINVAL, "nsgpu_wifil_next_end: null");
+  if (!h->mem.empty()) return wlg_next_end(h, out);
   if (h->lis_dirty) {
     h->lis_list.clear();
     for (size_t j = 0; j < h->lis_on.size(); j++)
@@ -2263,16 +2348,426 @@ uint32_t nsgpu::wifil_node(const nsgpu_wifil *h, uint32_t phy) {
 // Pending Receive / EndReceive events and the smallest ts among them (~0: none).
 extern "C" int nsgpu_wifil_pending(nsgpu_wifil *h, uint64_t *n, uint64_t *next_ts) {
   if (!h || !n || !next_ts) return set_error(NSGPU_EINVAL, "nsgpu_wifil_pending: null");
+  if (!h->mem.empty()) return wlg_pending(h, n, next_ts);
   if (int rcf = wl_flush_sends(h)) return rcf;
   const unsigned long long init[2] = {0ull, ~0ull};
   NSGPU_HIP(hipMemcpyAsync(h->d_pend, init, sizeof(init), hipMemcpyHostToDevice, h->s));
-  hipLaunchKernelGGL(k_wl_pending, dim3((unsigned)((h->D.nphy + 255) / 256)), dim3(256), 0, h->s, h->D, h->d_pend);
+  hipLaunchKernelGGL(k_wl_pending, dim3(wl_grid(h->D.nown, 256)), dim3(256), 0, h->s, h->D, h->d_pend);
   NSGPU_HIP(hipGetLastError());
   NSGPU_HIP(hipMemcpyAsync(h->h_pend, h->d_pend, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->s));
   NSGPU_HIP(hipStreamSynchronize(h->s));
   *n = h->h_pend[0];
   *next_ts = h->h_pend[1];
   return NSGPU_OK;
+}
+
+// ---------------- the partitioned PHY (SURVEY 8(e) for the closed loop: YansWifiChannel::Send's receivers
+// split over GPUs) ----------------
+// Every rank runs the same host program — the MAC's closures, the runtime's uids and order, GetState — over a
+// replicated host handle (the one these functions take); the device work of a phy (its Receives,
+// InterferenceHelper, state machine, EndReceive walks and PER chunks) runs on the partition that owns it.  A phy's
+// chain needs no other phy's state, so the partitions exchange only per epoch: (1) the epoch's syncs — an
+// EndReceive's uid is its sync's rank among every partition's syncs; (2) the counters, the end records (the
+// host's m_random draws and hand-backs) and the phys' state fields (GetState, DcfManager's CCA queries); (3) the
+// dispatched events, ordered over all partitions for the digest and the log.  The epochs run on one stream and
+// the host waits for each exchange (no order behind the epoch: every partition's events are needed first).
+// RCCL (nsgpu_wifil_create_dist): this rank's partition, the exchanges as all-gathers padded to the largest
+// partition's count (every rank's lists are sized for the largest partition); loopback (nsgpu_wifil_create_group):
+// every partition on this device, the exchanges as device copies.
+
+// k words of every partition (partition order): loopback from each member, RCCL this rank's all-gathered.
+template <class F>
+static int wlg_words(nsgpu_wifil *G, int k, F fn, std::vector<unsigned long long> &out) {
+  const int P = (int)G->plo.size();
+  out.assign((size_t)P * k, 0ull);
+  if (!G->comm) {
+    for (int q = 0; q < P; q++)
+      if (int rc = fn(G->mem[q], &out[(size_t)q * k])) return rc;
+    return NSGPU_OK;
+  }
+  std::vector<unsigned long long> mine((size_t)k, 0ull);
+  if (int rc = fn(G->mem[0], mine.data())) return rc;
+  NSGPU_HIP(hipMemcpyAsync(G->ssm, mine.data(), (size_t)k * 8, hipMemcpyHostToDevice, G->s));
+  NCCL_TRY(ncclAllGather(G->ssm, G->xsm, (size_t)k, ncclUint64, G->comm->comm, G->s));
+  NSGPU_HIP(hipMemcpyAsync(out.data(), G->xsm, (size_t)P * k * 8, hipMemcpyDeviceToHost, G->s));
+  NSGPU_HIP(hipStreamSynchronize(G->s));
+  return NSGPU_OK;
+}
+
+// Every partition's first cnt[q] elements (esz bytes) of a device array, concatenated in partition order into
+// dst: loopback from each member's array src(m), RCCL from this rank's, all-gathered padded to the largest count
+// through xbuf (P x that count; every partition's array holds it: equal capacities).
+template <class S>
+static int wlg_cat(nsgpu_wifil *G, const std::vector<uint64_t> &cnt, size_t esz, S src, void *xbuf, void *dst) {
+  const hipStream_t s = G->s;
+  const int P = (int)cnt.size();
+  uint64_t off = 0;
+  if (!G->comm) {
+    for (int q = 0; q < P; q++) {
+      if (cnt[q])
+        NSGPU_HIP(hipMemcpyAsync((uint8_t *)dst + off * esz, src(G->mem[q]), cnt[q] * esz, hipMemcpyDeviceToDevice, s));
+      off += cnt[q];
+    }
+    return NSGPU_OK;
+  }
+  uint64_t maxc = 0;
+  for (uint64_t c : cnt) maxc = std::max(maxc, c);
+  if (!maxc) return NSGPU_OK;
+  NCCL_TRY(ncclAllGather(src(G->mem[0]), xbuf, maxc * esz, ncclUint8, G->comm->comm, s));
+  for (int q = 0; q < P; q++) {
+    if (cnt[q])
+      NSGPU_HIP(hipMemcpyAsync((uint8_t *)dst + off * esz, (const uint8_t *)xbuf + (uint64_t)q * maxc * esz, cnt[q] * esz,
+                               hipMemcpyDeviceToDevice, s));
+    off += cnt[q];
+  }
+  return NSGPU_OK;
+}
+
+// The phys' state fields of every partition into the host's copy (RCCL; a loopback group's partitions write the
+// one mapped copy themselves).
+static int wlg_mirror(nsgpu_wifil *G) {
+  if (!G->comm) return NSGPU_OK;
+  const hipStream_t s = G->s;
+  const int P = (int)G->plo.size(), r = G->comm->rank;
+  const int64_t lo = G->plo[r], n = G->phi[r] - G->plo[r];
+  if (n) NSGPU_HIP(hipMemcpyAsync(G->smir, G->dmir + lo, (size_t)n * sizeof(WMir), hipMemcpyDeviceToDevice, s));
+  NCCL_TRY(ncclAllGather(G->smir, G->xmir, (size_t)G->pmax * sizeof(WMir), ncclUint8, G->comm->comm, s));
+  for (int q = 0; q < P; q++) {
+    const int64_t nq = G->phi[q] - G->plo[q];
+    if (nq)
+      NSGPU_HIP(hipMemcpyAsync(G->h_mir + G->plo[q], G->xmir + (uint64_t)q * G->pmax, (size_t)nq * sizeof(WMir),
+                               hipMemcpyDeviceToHost, s));
+  }
+  NSGPU_HIP(hipStreamSynchronize(s));
+  return NSGPU_OK;
+}
+
+static int wlg_advance(nsgpu_wifil *G, uint64_t bts, uint32_t buid, uint32_t *uid, uint64_t *dispatched, uint64_t *digest,
+                       uint64_t *log_ts, uint32_t *log_uid, uint32_t *log_ctx, uint64_t log_cap) {
+  const hipStream_t s = G->s;
+  const int P = (int)G->plo.size();
+  // (1) every partition's epoch: the batched SendPackets, then its phys' events below the bound
+  for (nsgpu_wifil *m : G->mem) {
+    if (m->D.nown) hipLaunchKernelGGL(k_wl_stepw, dim3((unsigned)m->D.nown), dim3(64), 0, s, m->D, bts, buid, m->sb);
+    m->sb.n = 0;
+  }
+  NSGPU_HIP(hipGetLastError());
+  // (2) the syncs of every partition
+  std::vector<unsigned long long> w;
+  int rc = wlg_words(G, 1, [&](nsgpu_wifil *m, unsigned long long *o) -> int {
+    uint32_t c = 0;
+    NSGPU_HIP(hipMemcpyAsync(&c, m->D.cnt + 1, sizeof(c), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+    o[0] = std::min<uint64_t>(c, m->D.sync_cap);
+    return NSGPU_OK;
+  }, w);
+  if (rc) return rc;
+  std::vector<uint64_t> cnt((size_t)P);
+  uint64_t tsy = 0;
+  for (int q = 0; q < P; q++) cnt[q] = w[q], tsy += w[q];
+  uint32_t xerr = 0;
+  if (tsy > G->g_sync_cap) {  // (the single engine's capacity: the run fails as it would there)
+    xerr |= WE_CAP;
+    tsy = 0;
+  } else if ((rc = wlg_cat(G, cnt, sizeof(LSync), [](nsgpu_wifil *m) { return (const void *)m->D.sync; }, G->xsr, G->xsync))) {
+    return rc;
+  }
+  // (3) each partition's tail: PER products, its syncs' EndReceive uids (ranks among all), the close
+  for (nsgpu_wifil *m : G->mem) {
+    WDev Dm = m->D;
+    Dm.xsync = G->xsync;
+    Dm.xn = (uint32_t)tsy;
+    hipLaunchKernelGGL(k_wl_mid, dim3(MID_PER + MID_RANK), dim3(256), 0, s, Dm, *uid, m->d_stat, ++m->seq);
+  }
+  NSGPU_HIP(hipGetLastError());
+  NSGPU_HIP(hipStreamSynchronize(s));
+  // (4) every partition's counters (the close's status block), then the checks before anything is published
+  if ((rc = wlg_words(G, 4, [&](nsgpu_wifil *m, unsigned long long *o) -> int {
+         for (int i = 0; i < 4; i++) o[i] = m->h_cnt[i];
+         return NSGPU_OK;
+       }, w)))
+    return rc;
+  std::vector<uint64_t> nevq((size_t)P), nendq((size_t)P);
+  uint64_t nev = 0, nend = 0, nsync = 0;
+  uint32_t err = xerr;
+  const nsgpu_wifil *m0 = G->mem[0];
+  for (int q = 0; q < P; q++) {
+    nevq[q] = w[(size_t)q * 4], nsync += w[(size_t)q * 4 + 1], nendq[q] = w[(size_t)q * 4 + 2];
+    err |= (uint32_t)w[(size_t)q * 4 + 3];
+    if (nevq[q] > (uint64_t)m0->D.nphy * EVB + m0->D.ev_cap || nendq[q] > m0->D.end_cap)
+      return set_error(NSGPU_ESTATE, "nsgpu_wifil_advance: partition %d's epoch counts beyond its arrays (events %llu, "
+                                     "ends %llu)", q, (unsigned long long)nevq[q], (unsigned long long)nendq[q]);
+    nev += nevq[q], nend += nendq[q];
+  }
+  if ((rc = wl_check_bits(err, "nsgpu_wifil_advance"))) return rc;
+  if (nsync != tsy) return set_error(NSGPU_ESTATE, "nsgpu_wifil_advance: sync counts changed in the close");
+  if ((uint64_t)*uid + nsync > nsgpu::UID_NEXT_MAX) return nsgpu::uid_range_error("nsgpu_wifil_advance");
+  // the end records (EndReceive uids patched by the closes) and the state fields
+  if ((rc = wlg_cat(G, nendq, sizeof(nsgpu_wifil_end), [](nsgpu_wifil *m) { return (const void *)m->D.ends; }, G->xend,
+                    G->uend)))
+    return rc;
+  G->ends_epoch.resize(nend);
+  if (nend) NSGPU_HIP(hipMemcpyAsync(G->ends_epoch.data(), G->uend, nend * sizeof(nsgpu_wifil_end), hipMemcpyDeviceToHost, s));
+  if ((rc = wlg_mirror(G))) return rc;
+  // (5) the order over every partition's events: each gathers its own (uids resolved), the union is ranked once
+  for (nsgpu_wifil *m : G->mem)
+    if (m->D.nown) hipLaunchKernelGGL(k_wl_gather, dim3(wl_grid(m->D.nown, 256)), dim3(256), 0, s, m->D);
+  if ((rc = wlg_cat(G, nevq, sizeof(LEv), [](nsgpu_wifil *m) { return (const void *)m->D.evd; }, G->xev, G->U.evd))) return rc;
+  for (nsgpu_wifil *m : G->mem) hipLaunchKernelGGL(k_wl_zero, dim3(1), dim3(64), 0, s, m->D);
+  const bool logging = log_ts && log_uid && log_ctx && *dispatched < log_cap;
+  hipLaunchKernelGGL(k_wl_set, dim3(1), dim3(1), 0, s, G->U.cnt, (uint32_t)nev);
+  hipLaunchKernelGGL(k_wl_tsort, dim3(NTILE), dim3(TS_T), 0, s, G->U);
+  hipLaunchKernelGGL(k_wl_rank, dim3(NTILE), dim3(TS_T), 0, s, G->U, *dispatched, logging ? 1 : 0, G->d_digtot);
+  NSGPU_HIP(hipGetLastError());
+  NSGPU_HIP(hipStreamSynchronize(s));
+  if (nev > ERANK_MAX || (logging && nev)) {
+    G->ev.resize(nev);
+    NSGPU_HIP(hipMemcpyAsync(G->ev.data(), G->U.evd, nev * sizeof(LEv), hipMemcpyDeviceToHost, s));
+    if (nev <= ERANK_MAX) {
+      G->erank.resize(nev);
+      NSGPU_HIP(hipMemcpyAsync(G->erank.data(), G->U.erank, nev * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    }
+    NSGPU_HIP(hipStreamSynchronize(s));
+  }
+  if (nev > ERANK_MAX) {  // a large epoch: its order on the host
+    std::sort(G->ev.begin(), G->ev.end(), [](const LEv &a, const LEv &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
+    for (const LEv &e : G->ev) {
+      const uint64_t rank = (*dispatched)++;
+      *digest += nsgpu_dispatch_digest_term(rank, e.ts, e.uid);
+      if (logging && rank < log_cap) log_ts[rank] = e.ts, log_uid[rank] = e.uid, log_ctx[rank] = e.ctx;
+    }
+  } else {
+    if (logging)
+      for (uint64_t i = 0; i < nev; i++) {
+        const uint64_t rank = *dispatched + G->erank[i];
+        if (rank < log_cap) log_ts[rank] = G->ev[i].ts, log_uid[rank] = G->ev[i].uid, log_ctx[rank] = G->ev[i].ctx;
+      }
+    *dispatched += nev;
+  }
+  const uint64_t tot = *G->h_digtot;
+  *digest += tot - G->dig_added;
+  G->dig_added = tot;
+  std::sort(G->ends_epoch.begin(), G->ends_epoch.end(),
+            [](const nsgpu_wifil_end &a, const nsgpu_wifil_end &b) { return a.ts != b.ts ? a.ts < b.ts : a.uid < b.uid; });
+  G->ends.insert(G->ends.end(), G->ends_epoch.begin(), G->ends_epoch.end());
+  *uid += (uint32_t)nsync;
+  return NSGPU_OK;
+}
+
+static int wlg_pending(nsgpu_wifil *G, uint64_t *n, uint64_t *next_ts) {
+  const hipStream_t s = G->s;
+  std::vector<unsigned long long> w;
+  int rc = wlg_words(G, 2, [&](nsgpu_wifil *m, unsigned long long *o) -> int {
+    if (int rcf = wl_flush_sends(m)) return rcf;
+    const unsigned long long init[2] = {0ull, ~0ull};
+    NSGPU_HIP(hipMemcpyAsync(m->d_pend, init, sizeof(init), hipMemcpyHostToDevice, s));
+    if (m->D.nown) hipLaunchKernelGGL(k_wl_pending, dim3(wl_grid(m->D.nown, 256)), dim3(256), 0, s, m->D, m->d_pend);
+    NSGPU_HIP(hipGetLastError());
+    NSGPU_HIP(hipMemcpyAsync(m->h_pend, m->d_pend, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+    o[0] = m->h_pend[0], o[1] = m->h_pend[1];
+    return NSGPU_OK;
+  }, w);
+  if (rc) return rc;
+  *n = 0;
+  *next_ts = ~0ull;
+  for (size_t q = 0; q < w.size() / 2; q++) *n += w[2 * q], *next_ts = std::min<uint64_t>(*next_ts, w[2 * q + 1]);
+  return NSGPU_OK;
+}
+
+static int wlg_next_end(nsgpu_wifil *G, nsgpu_wifil_next *out) {
+  const hipStream_t s = G->s;
+  if (G->lis_dirty) {  // (each partition scans its own listened phys)
+    G->lis_list.clear();
+    for (size_t j = 0; j < G->lis_on.size(); j++)
+      if (G->lis_on[j]) G->lis_list.push_back((uint32_t)j);
+    for (nsgpu_wifil *m : G->mem) {
+      m->lis_list.clear();
+      for (uint32_t j : G->lis_list)
+        if ((int64_t)j >= m->D.j0 && (int64_t)j < m->D.j0 + m->D.nown) m->lis_list.push_back(j);
+      if (!m->lis_list.empty())
+        NSGPU_HIP(hipMemcpyAsync(m->d_lis, m->lis_list.data(), m->lis_list.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+      m->D.nlis = (uint32_t)m->lis_list.size();
+    }
+    G->D.nlis = (uint32_t)G->lis_list.size();
+    G->lis_dirty = false;
+  }
+  memset(out, 0, sizeof(*out));
+  out->ts = out->ts_potential = ~0ull;
+  if (G->D.nlis == 0) return NSGPU_OK;
+  std::vector<unsigned long long> w;
+  int rc = wlg_words(G, 3, [&](nsgpu_wifil *m, unsigned long long *o) -> int {
+    hipLaunchKernelGGL(k_wl_nextend, dim3(1), dim3(256), 0, s, m->D, m->sb.n, m->d_next);
+    NSGPU_HIP(hipGetLastError());
+    NSGPU_HIP(hipMemcpyAsync(m->h_next, m->d_next, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    NSGPU_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < 3; i++) o[i] = m->h_next[i];
+    return NSGPU_OK;
+  }, w);
+  if (rc) return rc;
+  uint64_t bts = ~0ull, bkey = ~0ull, tp = ~0ull;
+  for (size_t q = 0; q < w.size() / 3; q++) {
+    const uint64_t ts = w[3 * q], key = w[3 * q + 1];
+    if (key != ~0ull && (ts < bts || (ts == bts && (uint32_t)key < (uint32_t)bkey))) bts = ts, bkey = key;
+    tp = std::min<uint64_t>(tp, w[3 * q + 2]);
+  }
+  if (bkey != ~0ull) {
+    out->found = 1;
+    out->ts = bts;
+    out->uid = (uint32_t)bkey;
+    out->phy = (uint32_t)(bkey >> 32);
+  }
+  out->ts_potential = tp;
+  return NSGPU_OK;
+}
+
+static int wlg_read_phys(nsgpu_wifil *G, nsgpu_wifi_phy_counters *out) {
+  const hipStream_t s = G->s;
+  for (nsgpu_wifil *m : G->mem)
+    if (int rcf = wl_flush_sends(m)) return rcf;
+  const int P = (int)G->plo.size();
+  std::vector<LPhy> ps;
+  if (!G->comm) {
+    for (nsgpu_wifil *m : G->mem) {
+      ps.resize((size_t)m->D.nown);
+      if (m->D.nown)
+        NSGPU_HIP(hipMemcpyAsync(ps.data(), m->D.ps + m->D.j0, ps.size() * sizeof(LPhy), hipMemcpyDeviceToHost, s));
+      NSGPU_HIP(hipStreamSynchronize(s));
+      for (int64_t i = 0; i < m->D.nown; i++) out[m->D.j0 + i] = wl_counters(ps[(size_t)i]);
+    }
+    return NSGPU_OK;
+  }
+  const nsgpu_wifil *m = G->mem[0];
+  if (m->D.nown)
+    NSGPU_HIP(hipMemcpyAsync(G->sps, m->D.ps + m->D.j0, (size_t)m->D.nown * sizeof(LPhy), hipMemcpyDeviceToDevice, s));
+  NCCL_TRY(ncclAllGather(G->sps, G->xps, (size_t)G->pmax * sizeof(LPhy), ncclUint8, G->comm->comm, s));
+  ps.resize((size_t)P * G->pmax);
+  NSGPU_HIP(hipMemcpyAsync(ps.data(), G->xps, ps.size() * sizeof(LPhy), hipMemcpyDeviceToHost, s));
+  NSGPU_HIP(hipStreamSynchronize(s));
+  for (int q = 0; q < P; q++)
+    for (int64_t i = 0; i < G->phi[q] - G->plo[q]; i++) out[G->plo[q] + i] = wl_counters(ps[(size_t)q * G->pmax + i]);
+  return NSGPU_OK;
+}
+
+// The replicated host handle over partitions lo[q] .. hi[q] (contiguous, covering every phy): every partition on
+// this device (comm null), or this rank's (comm).
+static int wlg_make(const nsgpu_wifil_config *c, const std::vector<int64_t> &lo, const std::vector<int64_t> &hi,
+                    nsgpu_comm *comm, nsgpu_wifil **out) {
+  const int P = (int)lo.size();
+  const int64_t N = c->n_phy;
+  for (int q = 0; q < P; q++)
+    if (lo[q] > hi[q] || (q == 0 ? lo[q] != 0 : lo[q] != hi[q - 1]) || (q == P - 1 && hi[q] != N))
+      return set_error(NSGPU_EINVAL, "nsgpu_wifil partitions: [%lld, %lld) of partition %d does not continue the ones "
+                                     "before it over [0, %lld)", (long long)lo[q], (long long)hi[q], q, (long long)N);
+  nsgpu_wifil *G = new nsgpu_wifil();
+  int rc;
+#define WG_TRY(x)                \
+  if ((rc = (x)) != NSGPU_OK) {  \
+    nsgpu_wifil_destroy(G);      \
+    return rc;                   \
+  }
+  G->comm = comm;
+  G->plo = lo;
+  G->phi = hi;
+  for (int q = 0; q < P; q++) G->pmax = std::max<int64_t>(G->pmax, hi[q] - lo[q]);
+  G->D.nphy = N;
+  G->D.j0 = 0;
+  G->D.nown = 0;  // (the handle runs no phy itself)
+  std::vector<uint32_t> rank;
+  wl_channel_ranks(c, rank, G->recv);
+  G->node_h.assign(c->node, c->node + N);
+  G->lis_on.assign((size_t)N, 0);
+  G->tx_cap = c->tx_cap;
+  if (hipStreamCreateWithPriority(&G->s, hipStreamNonBlocking, wl_prio(true)) != hipSuccess ||
+      hipHostMalloc((void **)&G->h_mir, (size_t)N * sizeof(WMir), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostMalloc((void **)&G->h_digtot, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&G->d_digtot, G->h_digtot, 0) != hipSuccess) {
+    nsgpu_wifil_destroy(G);
+    return set_error(NSGPU_EHIP, "nsgpu_wifil partitions: host buffers / stream");
+  }
+  std::memset(G->h_mir, 0, (size_t)N * sizeof(WMir));
+  *G->h_digtot = 0;
+  WMir *mir_dev = nullptr;  // (loopback: the partitions' lanes write the host's mapped copy)
+  if (!comm && hipHostGetDevicePointer((void **)&mir_dev, G->h_mir, 0) != hipSuccess) {
+    nsgpu_wifil_destroy(G);
+    return set_error(NSGPU_EHIP, "nsgpu_wifil partitions: mapped mirror");
+  }
+  for (int q = 0; q < P; q++) {
+    if (comm && q != comm->rank) continue;
+    nsgpu_wifil *m = nullptr;
+    WG_TRY(wl_create(c, lo[q], hi[q] - lo[q], G->pmax, &m));
+    (void)hipStreamSynchronize(m->s);
+    (void)hipStreamDestroy(m->s);
+    m->s = G->s;  // (every partition's kernels and copies in one order)
+    G->mem.push_back(m);
+  }
+  if (comm) {
+    WG_TRY(wl_alloc(G, &G->dmir, (size_t)N));
+    mir_dev = G->dmir;
+  }
+  for (nsgpu_wifil *m : G->mem) m->D.mir = mir_dev;
+  const nsgpu_wifil *m0 = G->mem[0];
+  G->g_sync_cap = (uint64_t)N * LPE_CAP + 1024;  // (the single engine's)
+  const uint64_t ev_per = (uint64_t)m0->D.nphy * EVB + m0->D.ev_cap;  // (a partition's dense events at most)
+  G->u_evcap = (uint64_t)P * ev_per;
+  WG_TRY(wl_alloc(G, &G->xsync, (size_t)G->g_sync_cap));
+  WG_TRY(wl_alloc(G, &G->uend, (size_t)P * m0->D.end_cap));
+  WDev &U = G->U;
+  WG_TRY(wl_alloc(G, &U.evd, (size_t)G->u_evcap));
+  WG_TRY(wl_alloc(G, &U.evg, (size_t)std::min<uint64_t>(G->u_evcap, ERANK_MAX)));
+  WG_TRY(wl_alloc(G, &U.erank, (size_t)std::min<uint64_t>(G->u_evcap, ERANK_MAX)));
+  WG_TRY(wl_alloc(G, &U.cnt, 8));
+  WG_TRY(wl_alloc(G, &U.ticket, 1));
+  WG_TRY(wl_alloc(G, &U.edig, 1));
+  WG_TRY(wl_alloc(G, &U.gtot, 1));
+  WG_TRY(wl_alloc(G, &U.evc, (size_t)EV_STRIPES * EV_STRIDE));
+  WG_TRY(wl_alloc(G, &U.evt, (size_t)EV_STRIPES * EV_STRIDE));
+  if (comm) {
+    WG_TRY(wl_alloc(G, &G->xsr, (size_t)P * m0->D.sync_cap));
+    WG_TRY(wl_alloc(G, &G->xev, (size_t)P * ev_per));
+    WG_TRY(wl_alloc(G, &G->xend, (size_t)P * m0->D.end_cap));
+    WG_TRY(wl_alloc(G, &G->smir, (size_t)std::max<int64_t>(G->pmax, 1)));
+    WG_TRY(wl_alloc(G, &G->xmir, (size_t)P * std::max<int64_t>(G->pmax, 1)));
+    WG_TRY(wl_alloc(G, &G->sps, (size_t)std::max<int64_t>(G->pmax, 1) * sizeof(LPhy)));
+    WG_TRY(wl_alloc(G, &G->xps, (size_t)P * std::max<int64_t>(G->pmax, 1) * sizeof(LPhy)));
+    WG_TRY(wl_alloc(G, &G->ssm, 8));
+    WG_TRY(wl_alloc(G, &G->xsm, (size_t)P * 8));
+  }
+#undef WG_TRY
+  *out = G;
+  return NSGPU_OK;
+}
+
+extern "C" int nsgpu_wifil_create_group(const nsgpu_wifil_config *c, const int64_t *bounds, int n, nsgpu_wifil **out) {
+  if (!c || !out || !bounds || n < 1 || c->n_phy <= 0) return set_error(NSGPU_EINVAL, "nsgpu_wifil_create_group: bad arguments");
+  std::vector<int64_t> lo((size_t)n), hi((size_t)n);
+  for (int q = 0; q < n; q++) lo[q] = bounds[q], hi[q] = bounds[q + 1];
+  return wlg_make(c, lo, hi, nullptr, out);
+}
+
+extern "C" int nsgpu_wifil_create_dist(const nsgpu_wifil_config *c, int64_t phy_begin, int64_t phy_end, nsgpu_comm *comm,
+                                       nsgpu_wifil **out) {
+  if (!c || !out || !comm || c->n_phy <= 0) return set_error(NSGPU_EINVAL, "nsgpu_wifil_create_dist: bad arguments");
+  // every rank's partition, gathered (each rank checks the same list: all fail or none)
+  const int R = comm->nranks;
+  unsigned long long *d = nullptr;
+  std::vector<unsigned long long> all((size_t)2 * R);
+  const unsigned long long mine[2] = {(unsigned long long)phy_begin, (unsigned long long)phy_end};
+  hipStream_t s = nullptr;
+  NSGPU_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipError_t e = hipMalloc((void **)&d, (size_t)(2 + 2 * R) * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyAsync(d, mine, sizeof(mine), hipMemcpyHostToDevice, s);
+  ncclResult_t nr = ncclSuccess;
+  if (e == hipSuccess) nr = ncclAllGather(d, d + 2, 2, ncclUint64, comm->comm, s);
+  if (e == hipSuccess && nr == ncclSuccess) e = hipMemcpyAsync(all.data(), d + 2, all.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (d) (void)hipFree(d);
+  (void)hipStreamDestroy(s);
+  if (e != hipSuccess) return set_error(NSGPU_EHIP, "nsgpu_wifil_create_dist: %s", hipGetErrorString(e));
+  if (nr != ncclSuccess) return set_error(NSGPU_EHIP, "nsgpu_wifil_create_dist: %s", ncclGetErrorString(nr));
+  std::vector<int64_t> lo((size_t)R), hi((size_t)R);
+  for (int q = 0; q < R; q++) lo[q] = (int64_t)all[2 * q], hi[q] = (int64_t)all[2 * q + 1];
+  return wlg_make(c, lo, hi, comm, out);
 }
 
 #ifdef NSGPU_PHASE_PROF

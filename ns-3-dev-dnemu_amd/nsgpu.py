@@ -173,6 +173,8 @@ SIGNATURES = {
     "nsgpu_wifil_listen": (C.c_int, [_vp, _u32, C.c_int]),
     "nsgpu_wifil_send_plan": (C.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _u64, C.POINTER(C.c_uint64)]),
     "nsgpu_wifil_next_end": (C.c_int, [_vp, _vp]),
+    "nsgpu_wifil_create_dist": (C.c_int, [_vp, C.c_int64, C.c_int64, _vp, C.POINTER(C.c_void_p)]),
+    "nsgpu_wifil_create_group": (C.c_int, [_vp, _vp, C.c_int, C.POINTER(C.c_void_p)]),
     "nsgpu_sim_wifi_set_end_handler": (C.c_int, [_vp, _vp, _vp]),
     "nsgpu_sim_wifi_listen": (C.c_int, [_vp, _u32, C.c_int]),
     "nsgpu_p2p_group_create": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p)]),

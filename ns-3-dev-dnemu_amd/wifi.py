@@ -398,11 +398,23 @@ class LoopPhy:
     """The closed-loop PHY on the device (nsgpu_wifil): attach it to a nsgpu.Sim, whose closures call
     Sim.wifi_send / Sim.wifi_state; EndReceive records (snr, per) come back through read_ends."""
 
-    def __init__(self, phys):
+    def __init__(self, phys, bounds=None, part=None, comm=None):
+        """bounds=[0, b1, ..., n_phy]: a loopback group whose partitions [bounds[q], bounds[q+1]) run on this device
+        (nsgpu_wifil_create_group); part=(begin, end) with comm (p2p.Comm): this rank's partition of an RCCL split
+        (nsgpu_wifil_create_dist).  Either way the handle answers every call as the single engine would."""
         self.phys = phys
         self._cfg = phys.c_struct()
         h = C.c_void_p()
-        nsgpu.check(nsgpu.lib().nsgpu_wifil_create(C.byref(self._cfg), C.byref(h)))
+        if bounds is not None:
+            self._bounds = np.ascontiguousarray(bounds, np.int64)
+            nsgpu.check(nsgpu.lib().nsgpu_wifil_create_group(C.byref(self._cfg), self._bounds.ctypes.data,
+                                                             len(self._bounds) - 1, C.byref(h)))
+        elif part is not None:
+            self._comm = comm
+            nsgpu.check(nsgpu.lib().nsgpu_wifil_create_dist(C.byref(self._cfg), int(part[0]), int(part[1]),
+                                                            comm.h, C.byref(h)))
+        else:
+            nsgpu.check(nsgpu.lib().nsgpu_wifil_create(C.byref(self._cfg), C.byref(h)))
         self.h = h.value
 
     def read_ends(self):

@@ -33,7 +33,7 @@ def run_oracle(sc, log_cap=1 << 20, uid_first=0):
     return log, ends, phys, tot
 
 
-def run_gpu(sc, log_cap=1 << 20, uid_first=0, listen=None):
+def run_gpu(sc, log_cap=1 << 20, uid_first=0, listen=None, bounds=None, part=None, comm=None):
     """uid_first: m_uid before the setup calls (nsgpu_sim_set_next_uid; 0: the reference's 4).
     sc["reply_delay"] (ns, optional): the EndReceive hand-back (nsgpu_sim_wifi_set_end_handler) — at each EndReceive
     that is not cancelled and whose draw (0.5) exceeds its per, the MAC stand-in schedules a reply of that phy
@@ -43,7 +43,7 @@ def run_gpu(sc, log_cap=1 << 20, uid_first=0, listen=None):
     sim = nsgpu.Sim()
     if uid_first:
         sim.set_next_uid(uid_first)
-    lp = wifi.LoopPhy(ph)
+    lp = wifi.LoopPhy(ph, bounds=bounds, part=part, comm=comm)
     sim.attach_wifi(lp)
     sim.set_log(log_cap)
     cnt = {"sends": 0, "busy": 0, "handbacks": 0}
