@@ -582,11 +582,14 @@ class WifiLoop:
                     stop_ns=int(stop_s * 1e9), size=1000, mode=self.wifi.DSSS_1M, preamble=self.wifi.PREAMBLE_LONG,
                     dbm=16.0206 + 1.0)
 
+    def loop_phy(self, phys):
+        return self.wifi.LoopPhy(phys)
+
     def run(self, sc):
         import nsgpu
         wifi = self.wifi
         sim = nsgpu.Sim()
-        lp = wifi.LoopPhy(sc["phys"])
+        lp = self.loop_phy(sc["phys"])
         sim.attach_wifi(lp)
         cnt = [0, 0]
         if self.mac == "native":
@@ -692,6 +695,37 @@ class WifiLoop:
             f"digest and count")
 
 
+class WifiLoopDist(WifiLoop):
+    """The closed loop split by receiver over N ranks, one GPU each (nsgpu_wifil_create_dist): every
+    rank runs the same host program (the MAC stand-in's closures, the runtime's uids, GetState) and its own block of
+    n/N phys' Receives / InterferenceHelper / state machine / EndReceive walks; per epoch the ranks all-gather the
+    syncs, counters, end records, state fields and dispatched events over RCCL.  Strong scaling: one simulation of
+    the same grid whatever N is.  On one rank (--partitioned) it is digest-checked against the oracle like the
+    single engine."""
+    scaling = "strong"
+
+    def __init__(self, args, stream, rank, world, td):
+        import p2p
+        super().__init__(args, stream)
+        self.world = world
+        uid = [p2p.Comm.unique_id() if rank == 0 else None]
+        if td is not None:
+            td.broadcast_object_list(uid, src=0)
+        self.comm = p2p.Comm(uid[0], world, rank)
+        n = self.sc["phys"].n_phy
+        self.part = (n * rank // world, n * (rank + 1) // world)
+        self.workload += (f"; split by receiver over {world} rank(s) (RCCL all-gathers of syncs, counters, end "
+                          f"records, state fields and events each epoch)")
+
+    def loop_phy(self, phys):
+        return self.wifi.LoopPhy(phys, part=self.part, comm=self.comm)
+
+    def roofline(self, step_kernel_ms, events_per_step):
+        rl = super().roofline(step_kernel_ms, events_per_step)
+        rl["receivers"] = list(self.part)
+        return rl
+
+
 WORKLOADS = {"churn": Churn, "p2p-grid": P2PGrid, "dumbbell": P2PDumbbell, "wifi-fanout": WifiFanout,
              "wifi-grid": WifiGrid, "wifi-loop": WifiLoop}
 
@@ -716,7 +750,7 @@ def parser():
                     help="p2p-grid: skip the wifi-grid / dumbbell entries of the `secondary` list")
     ap.add_argument("--secondary-steps", type=int, default=3, help="timed steps of each secondary workload")
     ap.add_argument("--partitioned", action="store_true",
-                    help="p2p-grid / wifi-grid / dumbbell through the partitioned engine even on one rank (RCCL "
+                    help="p2p-grid / wifi-grid / dumbbell / wifi-loop through the partitioned engine even on one rank (RCCL "
                          "with one rank)")
     return ap
 
@@ -739,8 +773,10 @@ def main():
         td.init_process_group("gloo")  # env:// (MASTER_ADDR / MASTER_PORT / RANK / WORLD_SIZE)
         tdist = td
     stream = nsgpu.Stream()
-    partitioned = args.workload in ("p2p-grid", "wifi-grid", "dumbbell") and (world > 1 or args.partitioned)
-    if partitioned and args.workload == "wifi-grid":
+    partitioned = args.workload in ("p2p-grid", "wifi-grid", "dumbbell", "wifi-loop") and (world > 1 or args.partitioned)
+    if partitioned and args.workload == "wifi-loop":
+        wl = WifiLoopDist(args, stream.handle, rank, world, tdist)
+    elif partitioned and args.workload == "wifi-grid":
         wl = WifiGridDist(args, stream.handle, rank, world, tdist)
     elif partitioned and args.workload == "dumbbell":
         wl = P2PDumbbellDist(args, stream.handle, rank, world, tdist)
