@@ -275,7 +275,8 @@ struct P2PDev {
   const uint32_t *owner;
   uint64_t *x0_send, *x0_recv;  // X0: 16 B per rank (x0_send points at the run control's X0 payload)
   uint64_t *xk_send, *xk_recv;  // the cut's exchange (host-driven): one rank's largest fitting key (16 B)
-  uint8_t *x1_send, *x1_recv;   // X1: X1B bytes per rank
+  uint8_t *x1_send, *x1_recv;   // X1: X1B bytes per rank (header, the rank's records in dispatch order: SEnt)
+  uint8_t *x1_own;              // this rank's window lists, not exchanged: X1Ent x WCAP, then X1Loc x XLCAP
   uint8_t *x2_send, *x2_recv;   // X2: x2b bytes per peer
   uint32_t capx, pad_x;         // X2 records per peer per window (the run's largest cut between two ranks)
   uint64_t x2b;                 // X2 bytes per peer
@@ -1145,7 +1146,20 @@ struct X1Loc {
 static_assert(sizeof(X1Loc) == 32, "X1Loc");
 constexpr int XLCAP = 4096;  // local records of one rank's window (LMAX)
 constexpr int NACC = WCAP + XLCAP;  // k_gtile's accumulator rows: gen-0 slots, then local records (compact order)
-constexpr size_t X1B = sizeof(X1Hdr) + sizeof(X1Ent) * WCAP + sizeof(X1Loc) * XLCAP;
+// One record of a rank's window in that rank's dispatch order (k_gsort), as another rank's k_gsearch compares its
+// own records with it: the order key (rel ts, gen-0 before local, then a gen-0 record's uid / a local record's
+// order words and ancestor uid: records of different ranks never tie on it) and the exclusive prefixes of its
+// rank's children / inline children before it.  Entry n (n = the rank's records) is a sentinel with the totals.
+struct SEnt {
+  uint64_t k0;  // rel ts << 32 | (gen-0: uid; local: the low word of its first order word)
+  uint64_t b;   // local: its second order word (gen-0: 0)
+  uint32_t c, L;  // local: the gen-0 ancestor's uid, 1 (gen-0: 0, 0)
+  uint32_t cp, ip;
+};
+static_assert(sizeof(SEnt) == 32, "SEnt");
+// X1 (all-gathered): the header and the sorted records; the rank's own lists stay in x1_own.
+constexpr size_t X1B = sizeof(X1Hdr) + sizeof(SEnt) * (NACC + 1);
+constexpr size_t X1OWN = sizeof(X1Ent) * WCAP + sizeof(X1Loc) * XLCAP;
 static_assert(X1B % 16 == 0, "k_copies moves 16-byte words");
 // X2: remote events for one peer (children whose node another rank owns), all-to-all; the record is
 // the pending event itself, uid included (mpi-interface.cc:414-506 sends {rx ns, node, dev, packet}).
@@ -1163,12 +1177,9 @@ constexpr int MAXR = 64;    // ranks
 static_assert(MAXR <= 64 && HB == 64, "per-rank summaries are read one lane per rank in one-wave blocks");
 static_assert((uint64_t)MAXR * NACC <= (1u << 21), "k_gtile's packed rank fields");
 __device__ __forceinline__ X1Hdr *x1hdr(uint8_t *b, uint32_t q) { return (X1Hdr *)(b + (size_t)q * X1B); }
-__device__ __forceinline__ X1Ent *x1ent(uint8_t *b, uint32_t q) {
-  return (X1Ent *)(b + (size_t)q * X1B + sizeof(X1Hdr));
-}
-__device__ __forceinline__ X1Loc *x1loc(uint8_t *b, uint32_t q) {
-  return (X1Loc *)(b + (size_t)q * X1B + sizeof(X1Hdr) + sizeof(X1Ent) * WCAP);
-}
+__device__ __forceinline__ SEnt *x1srt(uint8_t *b, uint32_t q) { return (SEnt *)(b + (size_t)q * X1B + sizeof(X1Hdr)); }
+__device__ __forceinline__ X1Ent *x1ent(const P2PDev &M) { return (X1Ent *)M.x1_own; }
+__device__ __forceinline__ X1Loc *x1loc(const P2PDev &M) { return (X1Loc *)(M.x1_own + sizeof(X1Ent) * WCAP); }
 __device__ __forceinline__ X2Hdr *x2hdr(const P2PDev &M, uint8_t *b, uint32_t q) {
   return (X2Hdr *)(b + (size_t)q * M.x2b);
 }
@@ -1397,21 +1408,28 @@ static_assert(GJ <= 64, "k_gtile's packed column counts (7-bit count field)");
 #define GT_GTB 8192
 #endif
 constexpr int GTB = GT_GTB;  // blocks of k_gtile (grid-stride over tiles: a wide window's ~5,600 tiles in one round)
+// The partitioned window's dispatch order, in three steps (r06; before, k_gtile compared every row with every
+// rank's records, so its work grew with the ranks: 12.6 / 19.6 / 40.6 / 52.8 us a window at 1 / 2 / 4 / 8
+// loopback partitions, profiles/r06/gtile_scale/):
+//   k_gtile (before the X1 exchange): this rank's records among themselves, all pairs in tiles;
+//   k_gsort (more than one rank): each record into the rank's X1 at its rank there (SEnt: its order key and the
+//     exclusive prefixes of the children / inline children before it, a sentinel with the totals after them);
+//   k_gsearch (after the exchange): a record's place among another rank's records is a binary search of that
+//     rank's sorted list (records of different ranks never tie), its counts and prefixes read at that place.
 // Rows: this rank's window records — its W gen-0 slots, then (WIDE) its L local records in X1Loc order; columns:
-// every rank's, in column tiles of RJ (a rank's gen-0 tiles, then its local tiles).  Per row, over the merged
-// window: the records before it (its global rank), those of a smaller ts, those of ts <= its own (its same-ts
-// group's end), and the children / inline children of the records before it and before its group (uid and
-// dispatch prefixes).  A gen-0 record precedes a local one of equal ts; two local records compare by their order
-// words, a tie by the ancestor uid, then (same ancestor: same node, this rank) by their exact chains.
+// this rank's, in column tiles of GJ (its gen-0 tiles, then its local tiles).  Per row, over the rank's window: the
+// records before it (its rank), those of a smaller ts, those of ts <= its own (its same-ts group's end), and the
+// children / inline children of the records before it and before its group (uid and dispatch prefixes).  A gen-0
+// record precedes a local one of equal ts; two local records compare by their order words, a tie by the ancestor
+// uid, then (same ancestor: same node, this rank) by their exact chains.
 template <bool WIDE>
 __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves a SIMD: 73 VGPRs; 8 spilled)
   Ctl &C = *M.C;
   // the run control and every rank's window size in one trip (the sizes loaded before the test: a load after a
   // branch on C.hdl waited for it)
   const uint32_t hdl = C.hdl, W = C.pW;
-  const uint32_t q = threadIdx.x;
-  const X1Hdr *hq = x1hdr(M.x1_recv, q < M.nranks ? q : 0u);
-  const uint32_t wq0 = hq->W, lq0 = WIDE ? hq->L : 0u, tq0 = hq->tinl;
+  const X1Hdr *hs = x1hdr(M.x1_send, 0);  // (this rank's summary: the tiles rank its records among themselves)
+  const uint32_t L0 = WIDE ? hs->L : 0u, tq0 = hs->tinl;
 #ifdef NSGPU_PHASE_PROF
   const uint64_t gt_t0 = __builtin_amdgcn_s_memrealtime();
   const bool gt_rec = C.windows == g_blk_win && blockIdx.x < (uint32_t)GT_BLK_MAX;
@@ -1432,36 +1450,14 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
   __shared__ __align__(16) uint32_t tts[GJ], tni[GJ], tfa[GJ];
   __shared__ __align__(16) uint64_t tpb[GJ], tfb[GJ];  // (tfb: a gen-0 column's whole key, a local one's w2)
   __shared__ uint32_t tu[WIDE ? GJ : 1], tr[WIDE ? GJ : 1];
-  __shared__ uint32_t s_off[MAXR + 1], s_w[MAXR], s_l[MAXR], s_g[MAXR];
-  uint32_t L = 0;
-  {  // every rank's window size at once, one lane per rank (HB = one wave), and the column tiles' prefix
-    const uint32_t wq = q < M.nranks ? wq0 : 0u;
-    const uint32_t lq = (WIDE && q < M.nranks) ? lq0 : 0u;
-    const uint32_t ng = (wq + GJ - 1) / GJ, nt = ng + (lq + GJ - 1) / GJ;
-    uint32_t inc = nt;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t x = __shfl_up(inc, o);
-      if ((int)q >= o) inc += x;
-    }
-    if (q < M.nranks) {
-      s_w[q] = wq;
-      s_l[q] = lq;
-      s_g[q] = ng;
-      s_off[q] = inc - nt;
-    }
-    if (q == M.nranks - 1) s_off[M.nranks] = inc;
-    if (WIDE) L = __shfl(lq, (int)M.rank);
-    if (blockIdx.x == 0) {  // (for k_dfin2: its record blocks then read no X1 header, and its block 0, the only
-      const uint32_t tg = wave_sum32(q < M.nranks ? tq0 : 0u);  //  reader left, resets this rank's header)
-      if (q == 0) {
-        C.gt_tinl = tg;
-        C.gt_lown = L;
-      }
-    }
+  const uint32_t L = L0;
+  const uint32_t ng = (W + GJ - 1) / GJ;  // (column tiles: the gen-0 records', then the local records')
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // (for k_dfin2: its record blocks then read no X1 header, and its
+    C.gt_tinl = tq0;                          //  block 0, the only reader left, resets this rank's header; more
+    C.gt_lown = L;                            //  ranks: k_gsearch sums every rank's inline children)
   }
-  __syncthreads();
   GT_MARK(0);
-  const uint32_t njt = s_off[M.nranks], NR = W + L;
+  const uint32_t njt = ng + (L + GJ - 1) / GJ, NR = W + L;
   // a work item: one row tile against GT_CT consecutive column tiles, summed in registers (one pair of atomics per
   // row and item: the accumulators' atomics, not the compares, bound the kernel)
   const uint32_t nseg = (njt + GT_CT - 1) / GT_CT;
@@ -1477,7 +1473,7 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
    uint64_t fbx = 0;
    if (i < NR) {
      if (lrow) {
-       const X1Loc e = x1loc(M.x1_send, 0)[i - W];
+       const X1Loc e = x1loc(M)[i - W];
        tx = (uint32_t)(e.w1 >> 32), fax = (uint32_t)e.w1, fbx = e.w2, xu = e.anc, xrec = e.rec;
      } else {
        const uint64_t key = M.wkey[i];
@@ -1487,14 +1483,11 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
    uint32_t gr = 0, cp = 0, ip = 0, ipf = 0, lp = 0;
    const uint32_t tj1 = (sg + 1) * GT_CT < njt ? (sg + 1) * GT_CT : njt;
    for (uint32_t tj = sg * GT_CT; tj < tj1; tj++) {
-    uint32_t q = 0;
-    while (tj >= s_off[q + 1]) q++;
-    const uint32_t jt = tj - s_off[q];
-    const bool ltile = WIDE && jt >= s_g[q];  // a tile of rank q's local records
-    const uint32_t j0 = (ltile ? jt - s_g[q] : jt) * GJ, nq = ltile ? s_l[q] : s_w[q];
+    const bool ltile = WIDE && tj >= ng;  // a tile of the local records
+    const uint32_t j0 = (ltile ? tj - ng : tj) * GJ, nq = ltile ? L : W;
     const uint32_t n = nq - j0 < (uint32_t)GJ ? nq - j0 : (uint32_t)GJ;
     if (ltile) {
-      const X1Loc *E = x1loc(M.x1_recv, q) + j0;
+      const X1Loc *E = x1loc(M) + j0;
       for (uint32_t k = threadIdx.x; k < (uint32_t)GJ; k += HB) {  // (padding: a ts after every row's)
         const bool in = k < n;
         const uint64_t w1 = in ? E[k].w1 : ~0ull;
@@ -1508,7 +1501,7 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
         tr[k] = in ? E[k].rec : 0u;
       }
     } else {
-      const X1Ent *E = x1ent(M.x1_recv, q) + j0;
+      const X1Ent *E = x1ent(M) + j0;
       for (uint32_t k = threadIdx.x; k < (uint32_t)GJ; k += HB) {
         const uint64_t key = k < n ? E[k].key : ~0ull;
         tts[k] = (uint32_t)(key >> 32);
@@ -1590,7 +1583,7 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
           }
         }
       } else {  // local x local
-        const int self = (q == M.rank && i - W >= j0 && i - W < j0 + n) ? (int)(i - W - j0) : -1;
+        const int self = (i - W >= j0 && i - W < j0 + n) ? (int)(i - W - j0) : -1;
         bool tie = false;
 #pragma unroll 2
         for (uint32_t y0 = 0; y0 < (uint32_t)GJ; y0 += 4) {
@@ -1609,15 +1602,7 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
         if (tie) {  // (rare: equal words — a clamped ancestor uid, or one ancestor's chains)
           for (uint32_t y = 0; y < n; y++) {
             if (tts[y] != tx || tfa[y] != fax || tfb[y] != fbx || (int)y == self) continue;
-            bool lt;
-            if (tu[y] != xu) {
-              lt = tu[y] < xu;
-            } else if (q == M.rank) {
-              lt = lk_before(M.lkey[tr[y] - LBASE], M.lkey[xrec - LBASE]);
-            } else {  // (one ancestor on two ranks: impossible — a node's chains are on its rank)
-              atomicOr(M.error, 64u);
-              lt = false;
-            }
+            const bool lt = tu[y] != xu ? tu[y] < xu : lk_before(M.lkey[tr[y] - LBASE], M.lkey[xrec - LBASE]);
             if (lt) ab += tpb[y];
           }
         }
@@ -1653,6 +1638,152 @@ __global__ __launch_bounds__(HB, 6) void k_gtile(const P2PDev M) {  // (6 waves 
   }
 #endif
 #undef GT_MARK
+}
+
+// k_gsort: this rank's records into its X1 list at their ranks among themselves (k_gtile's accumulators hold only
+// this rank's contributions until k_gsearch), with the prefixes before each and the totals after the last.
+template <bool WIDE>
+__global__ __launch_bounds__(256) void k_gsort(const P2PDev M) {
+  const Ctl &C = *M.C;
+  const uint32_t hdl = C.hdl, W = C.pW;
+  const uint32_t L = WIDE ? x1hdr(M.x1_send, 0)->L : 0u;
+  if (!hdl) return;
+  const uint32_t NR = W + L, i = blockIdx.x * 256 + threadIdx.x;
+  SEnt *S = x1srt(M.x1_send, 0);
+  if (NR == 0) {
+    if (i == 0) S[0] = SEnt{~0ull, ~0ull, ~0u, 1u, 0u, 0u};
+    return;
+  }
+  if (i >= NR) return;
+  const uint64_t *A = reinterpret_cast<const uint64_t *>(M.gacc);
+  const bool lrow = WIDE && i >= W;
+  const uint32_t row = lrow ? (uint32_t)WCAP + (i - W) : i;
+  const uint64_t w0 = A[row], w1 = A[NACC + row];
+  SEnt e;
+  uint32_t cnt;
+  if (lrow) {
+    const X1Loc x = x1loc(M)[i - W];
+    e = SEnt{x.w1, x.w2, x.anc, 1u, 0u, 0u};
+    cnt = x.cnt;
+  } else {
+    const X1Ent x = x1ent(M)[i];
+    e = SEnt{x.key, 0ull, 0u, 0u, 0u, 0u};
+    cnt = x.cnt;
+  }
+  const uint32_t gr = (uint32_t)(w0 & 0x1fffffu);
+  e.cp = (uint32_t)w1;
+  e.ip = (uint32_t)(w0 >> 42);
+  if (gr < NR) S[gr] = e;
+  else atomicOr(M.error, 64u);  // (ranks among the rank's own records are a permutation)
+  if (gr == NR - 1) S[NR] = SEnt{~0ull, ~0ull, ~0u, 1u, e.cp + (cnt & 0xffffu), e.ip + (cnt >> 16)};
+}
+
+// Record e of another rank before this rank's record x, in the merged dispatch order: earlier rel ts, then a gen-0
+// record before a local one, then (gen-0) the uid, (local) the order words and the ancestor uid.
+__device__ __forceinline__ bool sent_before(uint64_t ek0, uint32_t eL, uint64_t eb, uint32_t ec, uint64_t xk0, uint32_t xL,
+                                            uint64_t xb, uint32_t xc) {
+  if ((ek0 >> 32) != (xk0 >> 32)) return (ek0 >> 32) < (xk0 >> 32);
+  if (eL != xL) return eL < xL;
+  if ((uint32_t)ek0 != (uint32_t)xk0) return (uint32_t)ek0 < (uint32_t)xk0;
+  if (eb != xb) return eb < xb;
+  return ec < xc;
+}
+constexpr int GS_T = 256;             // k_gsearch: rows a block (one peer rank per blockIdx.y)
+constexpr int GS_STEP = 32;           // every GS_STEP-th record of the peer's list sampled into LDS
+constexpr int GS_NS = NACC / GS_STEP + 1;
+// k_gsearch: this rank's records against each other rank's sorted list — three searches a (row, peer): the
+// records before the row, those of a smaller ts, those of ts <= its own — first over the list's samples in LDS,
+// then within GS_STEP entries in the list (five trips); the counts and the prefixes found there are added to the
+// row's accumulators (k_gtile's packing).  Block (0, 0) also sums every rank's inline children for k_dfin2.
+template <bool WIDE>
+__global__ __launch_bounds__(GS_T) void k_gsearch(const P2PDev M) {
+  Ctl &C = *M.C;
+  const uint32_t hdl = C.hdl, W = C.pW;
+  const uint32_t L = WIDE ? x1hdr(M.x1_send, 0)->L : 0u;
+  const uint32_t q = blockIdx.y < M.rank ? blockIdx.y : blockIdx.y + 1u;  // (the peer)
+  const X1Hdr *hq = x1hdr(M.x1_recv, q);
+  const uint32_t nq = hq->W + (WIDE ? hq->L : 0u);
+  const uint32_t tq = threadIdx.x < M.nranks ? x1hdr(M.x1_recv, threadIdx.x)->tinl : 0u;
+  if (!hdl) return;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {  // (wave 0: one lane per rank)
+    const uint32_t tg = wave_sum32(tq);
+    if (threadIdx.x == 0) C.gt_tinl = tg;
+  }
+  const uint32_t NR = W + L, i = blockIdx.x * GS_T + threadIdx.x;
+  if (blockIdx.x * GS_T >= NR) return;  // (block-uniform)
+  const SEnt *S = x1srt(M.x1_recv, q);
+  __shared__ uint64_t s_k0[GS_NS], s_b[GS_NS];
+  __shared__ uint32_t s_c[GS_NS], s_L[GS_NS];
+  const uint32_t ns = (nq + GS_STEP - 1) / GS_STEP;
+  for (uint32_t k = threadIdx.x; k < ns; k += GS_T) {
+    const SEnt e = S[k * GS_STEP];
+    s_k0[k] = e.k0, s_b[k] = e.b, s_c[k] = e.c, s_L[k] = e.L;
+  }
+  __syncthreads();
+  if (i >= NR) return;
+  const bool lrow = WIDE && i >= W;
+  uint64_t xk0, xb = 0;
+  uint32_t xc = 0, xL = 0;
+  if (lrow) {
+    const X1Loc x = x1loc(M)[i - W];
+    xk0 = x.w1, xb = x.w2, xc = x.anc, xL = 1u;
+  } else {
+    xk0 = x1ent(M)[i].key;
+  }
+  const uint32_t xts = (uint32_t)(xk0 >> 32);
+  // the samples: how many satisfy each predicate (a prefix of them: the list is sorted)
+  uint32_t lo[3] = {0, 0, 0}, cn[3] = {ns, ns, ns};
+  while (cn[0] | cn[1] | cn[2]) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (!cn[k]) continue;
+      const uint32_t h = cn[k] >> 1, m = lo[k] + h;
+      const uint32_t ets = (uint32_t)(s_k0[m] >> 32);
+      const bool p = k == 0 ? sent_before(s_k0[m], s_L[m], s_b[m], s_c[m], xk0, xL, xb, xc) : k == 1 ? ets < xts : ets <= xts;
+      if (p) lo[k] = m + 1, cn[k] -= h + 1;
+      else cn[k] = h;
+    }
+  }
+  // within the list: entries ((c - 1) * STEP, min (c * STEP, nq)) after the last satisfying sample c - 1
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t c = lo[k];
+    if (c == 0) {
+      cn[k] = 0;
+    } else {
+      lo[k] = (c - 1) * GS_STEP + 1;
+      const uint32_t hi = c * GS_STEP < nq ? c * GS_STEP : nq;
+      cn[k] = hi > lo[k] ? hi - lo[k] : 0u;
+    }
+  }
+  while (cn[0] | cn[1] | cn[2]) {  // (the three searches' loads in flight together)
+    uint32_t m[3];
+    uint64_t ek0[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) m[k] = lo[k] + (cn[k] >> 1);
+    const SEnt e0 = S[m[0]];
+    ek0[0] = e0.k0;
+    ek0[1] = S[m[1]].k0;
+    ek0[2] = S[m[2]].k0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (!cn[k]) continue;
+      const uint32_t h = cn[k] >> 1, ets = (uint32_t)(ek0[k] >> 32);
+      const bool p = k == 0 ? sent_before(e0.k0, e0.L, e0.b, e0.c, xk0, xL, xb, xc) : k == 1 ? ets < xts : ets <= xts;
+      if (p) lo[k] = m[k] + 1, cn[k] -= h + 1;
+      else cn[k] = h;
+    }
+  }
+  const uint32_t p = lo[0], plt = lo[1], ple = lo[2];  // (<= nq: entry nq is the sentinel)
+  const SEnt ep = S[p];
+  const uint32_t ipf = S[plt].ip;
+  if (p < nq && ep.k0 == xk0 && ep.L == xL && ep.b == xb && ep.c == xc) atomicOr(M.error, 64u);  // (a tie: impossible)
+  unsigned long long *A = reinterpret_cast<unsigned long long *>(M.gacc);
+  const uint32_t row = lrow ? (uint32_t)WCAP + (i - W) : i;
+  const uint64_t w0 = (uint64_t)p | ((uint64_t)ple << 21) | ((uint64_t)ep.ip << 42);
+  const uint64_t w1 = (uint64_t)ep.cp | ((uint64_t)ipf << 32);
+  if (w0) atomicAdd(&A[row], (unsigned long long)w0);
+  if (w1) atomicAdd(&A[NACC + row], (unsigned long long)w1);
 }
 
 // Block 0 also does the pool bookkeeping (k2_scan's) and, last, the run bookkeeping; the other blocks
@@ -1714,7 +1845,7 @@ __global__ __launch_bounds__(HB) void k_dfin2(const P2PDev M) {
   {  // (speculative: every thread loads, whether or not its record exists — the indices stay in range)
     uint64_t lw1 = 0;
     if (loc) {
-      const X1Loc e = x1loc(M.x1_send, 0)[ti - WCAP];
+      const X1Loc e = x1loc(M)[ti - WCAP];
       s = e.rec < (uint32_t)WTOT ? e.rec : (uint32_t)WTOT - 1u;
       lw1 = e.w1;
       wpar = e.par;
@@ -2494,6 +2625,7 @@ static int create_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, in
     TRY(dalloc(h, &M.xk_send, 2));
     TRY(dalloc(h, &M.xk_recv, 2 * (size_t)nranks));
     TRY(dalloc(h, &M.x1_recv, X1B * nranks));
+    TRY(dalloc(h, &M.x1_own, X1OWN));
     M.x1_send = M.x1_recv + (size_t)rank * X1B;  // (in place: NCCL moves only the other ranks' slots)
     if ((uint64_t)nranks * WCAP * M.maxc >= (1ull << 32))  // (k_gtile's packed child prefix)
       return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: %d ranks x %u children per event", nranks, M.maxc);
@@ -2655,6 +2787,7 @@ extern "C" int nsgpu_p2p_reset(nsgpu_p2p *h, void *stream) {
     NSGPU_HIP(hipMemsetAsync(M.xk_send, 0, 16, s));
     NSGPU_HIP(hipMemsetAsync(M.xk_recv, 0, 16 * R, s));
     NSGPU_HIP(hipMemsetAsync(M.x1_recv, 0, X1B * R, s));
+    NSGPU_HIP(hipMemsetAsync(M.x1_own, 0, X1OWN, s));
     NSGPU_HIP(hipMemcpyAsync(M.x1_send, &h->x1h0, sizeof(X1Hdr), hipMemcpyHostToDevice, s));  // (its own slot)
     NSGPU_HIP(hipMemsetAsync(M.x2_send, 0, M.x2b * R, s));
     if (M.x2_recv != M.x2_send) NSGPU_HIP(hipMemsetAsync(M.x2_recv, 0, M.x2b * R, s));
@@ -2948,14 +3081,24 @@ static void dist_handle(const P2PDev &M, hipStream_t s) {
   }
   else hipLaunchKernelGGL(k2_handle<false>, dim3(K2_GRID), dim3(HB), 0, s, M);
 }
-static void dist_rank_fin(const P2PDev &M, hipStream_t s) {
-  if (M.wide) {
-    hipLaunchKernelGGL(k_gtile<true>, dim3(GTB), dim3(HB), 0, s, M);
-    hipLaunchKernelGGL(k_dfin2<true>, dim3(DF2_FB + NACC / HB), dim3(HB), 0, s, M);
-  } else {
-    hipLaunchKernelGGL(k_gtile<false>, dim3(GTB), dim3(HB), 0, s, M);
-    hipLaunchKernelGGL(k_dfin2<false>, dim3(DF2_FB + NHB), dim3(HB), 0, s, M);
+// Before the X1 exchange: this rank's records ranked among themselves and, with more ranks, sorted into its X1.
+static void dist_rank(const P2PDev &M, hipStream_t s) {
+  if (M.wide) hipLaunchKernelGGL(k_gtile<true>, dim3(GTB), dim3(HB), 0, s, M);
+  else hipLaunchKernelGGL(k_gtile<false>, dim3(GTB), dim3(HB), 0, s, M);
+  if (M.nranks > 1) {
+    if (M.wide) hipLaunchKernelGGL(k_gsort<true>, dim3(NACC / 256), dim3(256), 0, s, M);
+    else hipLaunchKernelGGL(k_gsort<false>, dim3(NACC / 256), dim3(256), 0, s, M);
   }
+}
+// After it: the other ranks' records before each of this rank's (binary searches), then the window's books.
+static void dist_rank_fin(const P2PDev &M, hipStream_t s) {
+  if (M.nranks > 1) {
+    const dim3 g(NACC / GS_T, M.nranks - 1);
+    if (M.wide) hipLaunchKernelGGL(k_gsearch<true>, g, dim3(GS_T), 0, s, M);
+    else hipLaunchKernelGGL(k_gsearch<false>, g, dim3(GS_T), 0, s, M);
+  }
+  if (M.wide) hipLaunchKernelGGL(k_dfin2<true>, dim3(DF2_FB + NACC / HB), dim3(HB), 0, s, M);
+  else hipLaunchKernelGGL(k_dfin2<false>, dim3(DF2_FB + NHB), dim3(HB), 0, s, M);
 }
 // The partitioned window (one RCCL member): 4 kernels and 3 collectives, on stream s.
 static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s, int nwin = NWIN) {
@@ -2965,6 +3108,7 @@ static int launch_windows_dist(nsgpu_p2p *h, hipStream_t s, int nwin = NWIN) {
     dist_pa(M, s);
     rc = x_allgather(h, M.x0_send, M.x0_recv, X0B, s);
     dist_handle(M, s);
+    dist_rank(M, s);
     if (!rc) rc = x_allgather(h, M.x1_send, M.x1_recv, X1B, s);
     dist_rank_fin(M, s);
     if (!rc) rc = x_alltoall(h, M.x2_send, M.x2_recv, M.x2b, s);
@@ -3583,15 +3727,9 @@ static void launch_windows_group(nsgpu_p2p_group *g, hipStream_t s, int nwin = N
     for (auto *h : g->m) dist_pa(h->M, s);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[0]);
     for (auto *h : g->m) dist_handle(h->M, s);
+    for (auto *h : g->m) dist_rank(h->M, s);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[1]);
-    for (auto *h : g->m) {
-      if (h->M.wide) hipLaunchKernelGGL(k_gtile<true>, dim3(GTB), dim3(HB), 0, s, h->M);
-      else hipLaunchKernelGGL(k_gtile<false>, dim3(GTB), dim3(HB), 0, s, h->M);
-    }
-    for (auto *h : g->m) {
-      if (h->M.wide) hipLaunchKernelGGL(k_dfin2<true>, dim3(DF2_FB + NACC / HB), dim3(HB), 0, s, h->M);
-      else hipLaunchKernelGGL(k_dfin2<false>, dim3(DF2_FB + NHB), dim3(HB), 0, s, h->M);
-    }
+    for (auto *h : g->m) dist_rank_fin(h->M, s);
     hipLaunchKernelGGL(k_copies, dim3(n * n), dim3(256), 0, s, (const CopyDesc *)g->d_x[2]);
   }
 }
@@ -3688,7 +3826,9 @@ static int group_host_step(nsgpu_p2p_group *g, const Ctl &c0) {
 // Runs every partition to the end of the simulation (blocking), like nsgpu_p2p_run.
 extern "C" int nsgpu_p2p_group_run(nsgpu_p2p_group *g, void *stream) {
   if (!g) return set_error(NSGPU_EINVAL, "nsgpu_p2p_group_run: null");
-  if (!g->gexec) {
+  // NSGPU_P2P_EAGER: the replays' kernels launched one by one (rocprofv3's kernel tracer does not follow graphs)
+  static const bool eager = getenv("NSGPU_P2P_EAGER") != nullptr;
+  if (!eager && !g->gexec) {
     hipGraph_t gr = nullptr;
     NSGPU_HIP(hipStreamBeginCapture(g->s, hipStreamCaptureModeThreadLocal));
     launch_windows_group(g, g->s);
@@ -3709,7 +3849,9 @@ extern "C" int nsgpu_p2p_group_run(nsgpu_p2p_group *g, void *stream) {
   int cur = 0;
   bool have_prev = false;
   for (;;) {
-    NSGPU_HIP(hipGraphLaunch(g->gexec, g->s));
+    if (eager) launch_windows_group(g, g->s);
+    else NSGPU_HIP(hipGraphLaunch(g->gexec, g->s));
+    NSGPU_HIP(hipGetLastError());
     NSGPU_HIP(hipMemcpyAsync(&g->snap[cur], C0, sizeof(Ctl), hipMemcpyDeviceToHost, g->s));
     NSGPU_HIP(hipEventRecord(g->ev[cur], g->s));
     if (have_prev) {

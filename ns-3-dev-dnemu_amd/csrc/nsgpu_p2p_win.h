@@ -109,7 +109,7 @@ __device__ __forceinline__ void slot_done(const P2PDev &M, uint32_t s, uint64_t 
   xa.tc += n;  // (the window's totals: a partitioned rank's X1 summary, the single engine's k2_rank bookkeeping)
   xa.ti += ni;
   if (M.dist && s < (uint32_t)WCAP) {  // (a local record's entry: X1Loc, compacted at its block's end)
-    x1ent(M.x1_send, 0)[s] = X1Ent{key, n | (ni << 16), 0};
+    x1ent(M)[s] = X1Ent{key, n | (ni << 16), 0};
     xa.lk = key > xa.lk ? key : xa.lk;
   }
 }
@@ -2204,7 +2204,7 @@ __global__ __launch_bounds__(HB) void k_xlcompact(const P2PDev M) {
     }
   }
   if (!cnt) return;
-  X1Loc *xl = x1loc(M.x1_send, 0);
+  X1Loc *xl = x1loc(M);
   uint64_t lts = 0;  // (the largest rel ts: the window's last dispatch time may be a local record's)
   for (uint32_t k0 = 0; k0 < cnt; k0 += HB) {  // (block-uniform: the parents' bases come by shuffles)
     const uint32_t k = k0 + tid;
