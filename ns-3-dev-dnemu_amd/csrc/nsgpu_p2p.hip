@@ -334,27 +334,55 @@ struct P2PDev {
 };
 
 // ---------------- wave / block helpers ----------------
+// Wave reductions (every lane of the wave active; the result in every lane): within each row of 16 lanes by DPP
+// moves — quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: each step pairs a lane with one of the other
+// half of its group, so after four steps every lane holds its row's value — then the four rows' values read into
+// scalars (v_readlane).  (The __shfl_xor butterflies were 6 dependent ds_bpermute rounds, LDS-latency each: the
+// holders' five counter sums alone cost config 4 ~0.5 us a window.)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  return ((uint64_t)dpp32<CTRL>((uint32_t)(v >> 32)) << 32) | dpp32<CTRL>((uint32_t)v);
+}
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) { return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l); }
+constexpr int DPP_X1 = 0xB1, DPP_X2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
 __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t w = __shfl_xor(v, o);
-    v = w < v ? w : v;
-  }
-  return v;
+  uint64_t w;
+  w = dpp64<DPP_X1>(v), v = w < v ? w : v;
+  w = dpp64<DPP_X2>(v), v = w < v ? w : v;
+  w = dpp64<DPP_HMIRROR>(v), v = w < v ? w : v;
+  w = dpp64<DPP_MIRROR>(v), v = w < v ? w : v;
+  const uint64_t a = rl64(v, 0), b = rl64(v, 16), c = rl64(v, 32), d = rl64(v, 48);
+  const uint64_t x = a < b ? a : b, y = c < d ? c : d;
+  return x < y ? x : y;
 }
 __device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t w = __shfl_xor(v, o);
-    v = w > v ? w : v;
-  }
-  return v;
+  uint64_t w;
+  w = dpp64<DPP_X1>(v), v = w > v ? w : v;
+  w = dpp64<DPP_X2>(v), v = w > v ? w : v;
+  w = dpp64<DPP_HMIRROR>(v), v = w > v ? w : v;
+  w = dpp64<DPP_MIRROR>(v), v = w > v ? w : v;
+  const uint64_t a = rl64(v, 0), b = rl64(v, 16), c = rl64(v, 32), d = rl64(v, 48);
+  const uint64_t x = a > b ? a : b, y = c > d ? c : d;
+  return x > y ? x : y;
 }
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dpp32<DPP_X1>(v);
+  v += dpp32<DPP_X2>(v);
+  v += dpp32<DPP_HMIRROR>(v);
+  v += dpp32<DPP_MIRROR>(v);
+  return rl32(v, 0) + rl32(v, 16) + rl32(v, 32) + rl32(v, 48);
 }
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dpp64<DPP_X1>(v);
+  v += dpp64<DPP_X2>(v);
+  v += dpp64<DPP_HMIRROR>(v);
+  v += dpp64<DPP_MIRROR>(v);
+  return rl64(v, 0) + rl64(v, 16) + rl64(v, 32) + rl64(v, 48);
 }
 __device__ __forceinline__ uint32_t wave_exscan32(uint32_t v, int lane) {
   uint32_t inc = v;
