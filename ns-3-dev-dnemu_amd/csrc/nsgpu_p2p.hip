@@ -384,13 +384,38 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   v += dpp64<DPP_MIRROR>(v);
   return rl64(v, 0) + rl64(v, 16) + rl64(v, 32) + rl64(v, 48);
 }
+// Inclusive wave scans by DPP (every lane active): row_shr 1 / 2 / 4 / 8 within each row of 16 (a lane without a
+// source adds 0), then row_bcast:15 (rows 1 and 3 add the previous row's last lane) and row_bcast:31 (rows 2 and 3
+// add lane 31) — six DPP steps instead of six ds_bpermute rounds.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dppm32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint64_t dppm64(uint64_t v) {
+  return ((uint64_t)dppm32<CTRL, ROWS>((uint32_t)(v >> 32)) << 32) | dppm32<CTRL, ROWS>((uint32_t)v);
+}
+__device__ __forceinline__ uint32_t wave_incscan32(uint32_t v) {
+  v += dppm32<0x111>(v);
+  v += dppm32<0x112>(v);
+  v += dppm32<0x114>(v);
+  v += dppm32<0x118>(v);
+  v += dppm32<0x142, 0xa>(v);
+  v += dppm32<0x143, 0xc>(v);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_incscan64(uint64_t v) {
+  v += dppm64<0x111>(v);
+  v += dppm64<0x112>(v);
+  v += dppm64<0x114>(v);
+  v += dppm64<0x118>(v);
+  v += dppm64<0x142, 0xa>(v);
+  v += dppm64<0x143, 0xc>(v);
+  return v;
+}
 __device__ __forceinline__ uint32_t wave_exscan32(uint32_t v, int lane) {
-  uint32_t inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t w = __shfl_up(inc, o);
-    if (lane >= o) inc += w;
-  }
-  return inc - v;
+  (void)lane;
+  return wave_incscan32(v) - v;
 }
 // Block exclusive scan of one value per thread (NTH threads); *total = block sum.
 template <int NTH>

@@ -313,11 +313,7 @@ __device__ __forceinline__ void block_alloc2(Ctl &C, uint32_t nw, uint32_t nf, u
   __shared__ uint64_t s_base[2];
   const uint64_t v = (uint64_t)nw | ((uint64_t)nf << 32);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint64_t inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t x = __shfl_up(inc, o);
-    if (lane >= o) inc += x;
-  }
+  const uint64_t inc = wave_incscan64(v);
   if (lane == 63) s_w[wid] = inc;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -2191,10 +2187,8 @@ __global__ __launch_bounds__(HB) void k_xlcompact(const P2PDev M) {
   // every region's compact base (exclusive prefix of the counts: region tid in e0, region tid + HB in e1), for
   // this block's records and their local parents' rows
   uint32_t e0 = a0, e1 = a1;
-  for (int o = 1; o < HB; o <<= 1) {
-    const uint32_t x0 = __shfl_up(e0, o), x1 = __shfl_up(e1, o);
-    if ((int)tid >= o) e0 += x0, e1 += x1;
-  }
+  e0 = wave_incscan32(e0);  // (HB = one wave)
+  e1 = wave_incscan32(e1);
   e1 += __shfl(e0, HB - 1);
   e0 -= a0;
   e1 -= a1;
@@ -2354,11 +2348,7 @@ template <int NT>
 __device__ __forceinline__ void local_prefix(uint32_t v, uint32_t *pre) {
   static_assert(NT >= NLR && NLR <= 128, "one thread per region, two waves");
   __shared__ uint32_t s_w0;
-  const int lane = threadIdx.x & 63;
-  for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scan
-    const uint32_t x = __shfl_up(v, o);
-    if (lane >= o) v += x;
-  }
+  v = wave_incscan32(v);  // (inclusive wave scan)
   if (threadIdx.x == 63) s_w0 = v;
   __syncthreads();
   if (threadIdx.x >= 64) v += s_w0;
@@ -2780,10 +2770,7 @@ __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb) {
   }
   BLK_MARK(22, c_win);  // the records arrived
   uint64_t inc = sum;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t x = __shfl_up(inc, o);
-    if (lane >= o) inc += x;
-  }
+  inc = wave_incscan64(inc);
   if (lane == 63) wsum[wid] = inc;
   __syncthreads();
   uint64_t off = 0, tot = 0;
@@ -3095,10 +3082,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k2_scan(const P2PDev M) {
   }
   const int lane = tid & 63, wid = tid >> 6;
   uint64_t inc = sum;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t w = __shfl_up(inc, o);
-    if (lane >= o) inc += w;
-  }
+  inc = wave_incscan64(inc);
   __shared__ uint64_t wsum64[SCAN_THREADS / 64];
   if (lane == 63) wsum64[wid] = inc;
   __syncthreads();
