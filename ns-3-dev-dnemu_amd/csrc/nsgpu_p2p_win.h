@@ -143,7 +143,7 @@ __device__ __forceinline__ uint32_t wave_alloc32(uint32_t *ctr, bool want) {
   if (m) {
     const int first = __ffsll((unsigned long long)m) - 1;
     if (lane == first) base = atomicAdd(ctr, (uint32_t)__popcll(m));
-    base = __shfl(base, first);
+    base = rl32(base, first);  // (first is uniform: a readlane, not a ds_bpermute)
   }
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
@@ -154,7 +154,7 @@ __device__ __forceinline__ uint64_t wave_alloc64(uint64_t *ctr, bool want) {
   if (m) {
     const int first = __ffsll((unsigned long long)m) - 1;
     if (lane == first) base = atomicAdd((unsigned long long *)ctr, (unsigned long long)__popcll(m));
-    base = __shfl(base, first);
+    base = rl64(base, first);
   }
   return (uint64_t)base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
 }
@@ -229,13 +229,13 @@ __device__ __forceinline__ NtClaim node_table_claim_wave(const P2PDev &M, uint32
   bool done = false;
   if (mn) {
     const int lead = __ffsll((unsigned long long)mn) - 1;
-    const uint32_t c0 = __shfl(ctx, lead);
+    const uint32_t c0 = rl32(ctx, lead);  // (lead is uniform)
     const bool same = nd && ctx == c0;
     const uint64_t ms = __ballot(same);
     const int lane = threadIdx.x & 63;
     uint32_t base = 0;
     if (lane == lead) base = atomicAdd(&M.node_tab[(uint64_t)c0 * NTAB], (uint32_t)__popcll(ms));
-    base = __shfl(base, lead);
+    base = rl32(base, lead);
     if (same) {
       cl = NtClaim{slot, ctx, base + (uint32_t)__popcll(ms & ((1ull << lane) - 1ull))};
       done = true;
@@ -1390,7 +1390,7 @@ __device__ __forceinline__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32
   CMap ex{__shfl_up(inc.a, 1), __shfl_up(inc.lo, 1), __shfl_up(inc.hi, 1)};
   if (lane == 0) ex = CMap{0, -CBIG, CBIG};
   const int32_t cin = clampi(c0 + ex.a, ex.lo, ex.hi);
-  const int32_t cfin = clampi(c0 + __shfl(inc.a, 63), __shfl(inc.lo, 63), __shfl(inc.hi, 63));
+  const int32_t cfin = clampi(c0 + (int32_t)rl32((uint32_t)inc.a, 63), (int32_t)rl32((uint32_t)inc.lo, 63), (int32_t)rl32((uint32_t)inc.hi, 63));
   uint32_t ne = 0, nd = 0;
   {
     int32_t x = cin;
@@ -1407,7 +1407,7 @@ __device__ __forceinline__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32
     }
   }
   const uint32_t ebefore = wave_exscan32(ne, lane), dbefore = wave_exscan32(nd, lane);
-  const uint32_t dtot = __shfl(dbefore + nd, 63), etot = __shfl(ebefore + ne, 63);
+  const uint32_t dtot = rl32(dbefore + nd, 63), etot = rl32(ebefore + ne, 63);
   if (cnt0 + etot > qcap) return false;
   // pass B1: enqueued packets into the ring (before any TransmitComplete reads one).  The lane's segment in
   // batches: the slots from LDS (hsl), the batch's packets loaded at once (one memory trip a batch, not one an
@@ -2189,7 +2189,7 @@ __global__ __launch_bounds__(HB) void k_xlcompact(const P2PDev M) {
   uint32_t e0 = a0, e1 = a1;
   e0 = wave_incscan32(e0);  // (HB = one wave)
   e1 = wave_incscan32(e1);
-  e1 += __shfl(e0, HB - 1);
+  e1 += rl32(e0, HB - 1);
   e0 -= a0;
   e1 -= a1;
   const uint32_t lb = bx < (uint32_t)HB ? __shfl(e0, (int)bx) : __shfl(e1, (int)(bx - HB));
