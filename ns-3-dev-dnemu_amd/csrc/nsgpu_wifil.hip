@@ -338,6 +338,26 @@ __device__ __forceinline__ double snr_of(const WDev &D, double signal, double no
   return signal / noise;
 }
 
+// Cross-lane moves by DPP instead of ds_bpermute (an LDS round trip each): the previous lane's value (wave_shr:1;
+// lane 0 gets 0) and an inclusive wave scan (row_shr 1 / 2 / 4 / 8, then row_bcast 15 / 31); every lane active.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t wdpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ uint32_t prev_lane32(uint32_t v) { return wdpp32<0x138>(v); }
+__device__ __forceinline__ uint64_t prev_lane64(uint64_t v) {
+  return ((uint64_t)prev_lane32((uint32_t)(v >> 32)) << 32) | prev_lane32((uint32_t)v);
+}
+__device__ __forceinline__ uint32_t wave_incscan32(uint32_t v) {
+  v += wdpp32<0x111>(v);
+  v += wdpp32<0x112>(v);
+  v += wdpp32<0x114>(v);
+  v += wdpp32<0x118>(v);
+  v += wdpp32<0x142, 0xa>(v);
+  v += wdpp32<0x143, 0xc>(v);
+  return v;
+}
+
 // One index of counter *ctr per calling lane: the wave's active lanes share one atomic (every phy's lane
 // appending to the same epoch lists one atomic each serialized on the counter's line: ~11 ns apiece).
 __device__ __forceinline__ uint32_t wave_alloc(uint32_t *ctr) {
@@ -346,7 +366,7 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t *ctr) {
   const int first = __ffsll((unsigned long long)m) - 1;
   uint32_t base = 0;
   if (lane == first) base = atomicAdd(ctr, (uint32_t)__popcll(m));
-  base = __shfl(base, first);
+  base = (uint32_t)__builtin_amdgcn_readlane((int)base, first);  // (first is uniform)
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
@@ -771,11 +791,11 @@ __device__ __forceinline__ LRx rl_rx(const LRx &a, int u) {
 }
 __device__ __forceinline__ LRx shfl_up_rx(const LRx &a) {
   LRx b;
-  b.at = (uint64_t)__shfl_up((long long)a.at, 1);
-  b.uid = (uint32_t)__shfl_up((int)a.uid, 1);
-  b.tx = (uint32_t)__shfl_up((int)a.tx, 1);
-  b.w = __shfl_up(a.w, 1);
-  b.dur = (int64_t)__shfl_up((long long)a.dur, 1);
+  b.at = prev_lane64(a.at);  // (lane 0's is not used)
+  b.uid = prev_lane32(a.uid);
+  b.tx = prev_lane32(a.tx);
+  b.w = __longlong_as_double((long long)prev_lane64((uint64_t)__double_as_longlong(a.w)));
+  b.dur = (int64_t)prev_lane64((uint64_t)a.dur);
   return b;
 }
 
@@ -1035,7 +1055,7 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
           }
           const int64_t cur = lane == close ? nw : c.t;
           const double dl = lane == close ? 0.0 : c.d;
-          int64_t prv = __shfl_up((long long)cur, 1);
+          int64_t prv = (int64_t)prev_lane64((uint64_t)cur);
           if (lane == 0) prv = previous;
           double nz = 0.0;  // the noise before step `lane`
           double acc = noiseW;
@@ -1062,12 +1082,7 @@ __global__ __launch_bounds__(64) void k_wl_stepw(const WDev D, uint64_t bts, uin
           }
           // (a zero-length chunk is skipped: ck (dur != 0)); the chunks' places by a wave prefix count
           const uint32_t n1 = d1 != 0, n2 = d2 != 0, nc = n1 + n2;
-          uint32_t pre = nc;
-#pragma unroll
-          for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)pre, d);
-            if (lane >= (uint32_t)d) pre += y;
-          }
+          const uint32_t pre = wave_incscan32(nc);
           const uint32_t tot = rl_u32(pre, 63), at = cn + pre - nc;
           if (defer) {
             if (n1) D.ck[cs + at] = LCk{nz, (int64_t)((uint64_t)d1 << 1) | (h1 ? 1 : 0)};

@@ -6,6 +6,6 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 R=$(pwd); O=$R/gpurun_out/$1; REPS=$2; shift 2; mkdir -p $O
 for r in $(seq 1 $REPS); do
   for d in "$@"; do
-    (cd $R/$d && timeout -k 10 200 python bench.py --no-secondary --no-cpu-baseline > $O/${d//\//_}_$r.json 2> $O/${d//\//_}_$r.err)
+    (cd $R/$d && timeout -k 10 200 python bench.py --no-secondary --no-cpu-baseline $BENCH_ARGS > $O/${d//\//_}_$r.json 2> $O/${d//\//_}_$r.err)
   done
 done
