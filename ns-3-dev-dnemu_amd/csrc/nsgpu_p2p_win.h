@@ -1354,10 +1354,16 @@ struct CMap {
   int32_t a, lo, hi;
 };
 __device__ __forceinline__ int32_t clampi(int32_t x, int32_t l, int32_t h) { return x < l ? l : (x > h ? h : x); }
+constexpr int32_t CBIG = 1 << 28;
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ CMap cmap_dpp(const CMap &x) {  // (rows / lanes without a source: the identity map)
+  return CMap{__builtin_amdgcn_update_dpp(0, x.a, CTRL, ROWS, 0xf, false),
+              __builtin_amdgcn_update_dpp(-CBIG, x.lo, CTRL, ROWS, 0xf, false),
+              __builtin_amdgcn_update_dpp(CBIG, x.hi, CTRL, ROWS, 0xf, false)};
+}
 __device__ __forceinline__ CMap cmap_then(const CMap &f, const CMap &g) {  // g after f
   return CMap{f.a + g.a, clampi(f.lo + g.a, g.lo, g.hi), clampi(f.hi + g.a, g.lo, g.hi)};
 }
-constexpr int32_t CBIG = 1 << 28;
 
 // Returns false (nothing done) when the batch would reuse a ring slot (more enqueues than the ring
 // holds beyond the queued packets): the serial pass runs instead.
@@ -1382,13 +1388,15 @@ __device__ __forceinline__ bool hub_device_scan(const P2PDev &M, Emit &E, uint32
     if (op == ACT_SEND) f = cmap_then(f, CMap{1, -CBIG, qmax});
     else if (op == ACT_KICK) f = cmap_then(f, CMap{-1, -CBIG, CBIG});
   }
+  // the lanes' inclusive composition by DPP (a lane without a source composes with the identity map)
   CMap inc = f;
-  for (int o = 1; o < 64; o <<= 1) {
-    const CMap g{__shfl_up(inc.a, o), __shfl_up(inc.lo, o), __shfl_up(inc.hi, o)};
-    if (lane >= o) inc = cmap_then(g, inc);
-  }
-  CMap ex{__shfl_up(inc.a, 1), __shfl_up(inc.lo, 1), __shfl_up(inc.hi, 1)};
-  if (lane == 0) ex = CMap{0, -CBIG, CBIG};
+  inc = cmap_then(cmap_dpp<0x111>(inc), inc);
+  inc = cmap_then(cmap_dpp<0x112>(inc), inc);
+  inc = cmap_then(cmap_dpp<0x114>(inc), inc);
+  inc = cmap_then(cmap_dpp<0x118>(inc), inc);
+  inc = cmap_then(cmap_dpp<0x142, 0xa>(inc), inc);
+  inc = cmap_then(cmap_dpp<0x143, 0xc>(inc), inc);
+  const CMap ex = cmap_dpp<0x138>(inc);  // (wave_shr:1: the exclusive one; lane 0 the identity)
   const int32_t cin = clampi(c0 + ex.a, ex.lo, ex.hi);
   const int32_t cfin = clampi(c0 + (int32_t)rl32((uint32_t)inc.a, 63), (int32_t)rl32((uint32_t)inc.lo, 63), (int32_t)rl32((uint32_t)inc.hi, 63));
   uint32_t ne = 0, nd = 0;
@@ -1994,12 +2002,9 @@ __device__ __forceinline__ void hub_node(const P2PDev &M, Ctl &C, uint32_t c, ui
       }
   }
   HUB_MARK(23);  // (the segments' ops into LDS)
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t x = __shfl_xor(dmin, o), y = __shfl_xor(dmax, o), z = __shfl_xor(inl, o);
-    dmin = x < dmin ? x : dmin;
-    dmax = y > dmax ? y : dmax;
-    inl |= z;
-  }
+  dmin = (uint32_t)wave_min64(dmin);
+  dmax = (uint32_t)wave_max64(dmax);
+  inl = (uint32_t)wave_sum32(inl != 0 ? 1u : 0u) != 0 ? 1u : 0u;
   // (not in a wide window: a TransmitStart there makes a local record the scan cannot place)
   bool fast = dmin != NOSRC && dmin == dmax && inl == 0 && (!WIDE || hc.lim == 0) && M.dev[dmin].qmax >= 1 &&
               !(M.dev[dmin].busy == 0 && M.dev[dmin].cnt != 0);
