@@ -487,7 +487,7 @@ struct Emit {
 
 // Run statistics of one handler thread.
 struct HStat {
-  uint64_t cancelled, ttl_drops, no_route, unreach, icmp;
+  uint32_t cancelled, ttl_drops, no_route, unreach, icmp;  // (one holder's window: 32 bits; 64-bit fields were spilled to scratch)
   bool stop;
 };
 
