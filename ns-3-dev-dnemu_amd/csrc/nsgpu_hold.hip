@@ -71,23 +71,42 @@ struct HoldLds {
   uint32_t p;                 // committed prefix this round
 };
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t w = __shfl_xor(v, o);
-    v = w < v ? w : v;
-  }
+// Cross-lane moves by DPP (every lane of the wave active): a lane without a source reads the identity `id` (~0 for
+// min, 0 for sums).  row_shr 1 / 2 / 4 / 8 then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) make an
+// inclusive scan; wave_shr:1 the exclusive one; quad_perm / mirrors + readlanes a reduction.  (The __shfl butterflies
+// were ds_bpermute rounds, an LDS round trip each, on the one workgroup's critical path every round.)
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint64_t hdpp64(uint64_t v, uint64_t id) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)id, (int)(uint32_t)v, CTRL, ROWS, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(id >> 32), (int)(uint32_t)(v >> 32), CTRL, ROWS, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t min64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t wave_incscan_min_u64(uint64_t v) {
+  v = min64(v, hdpp64<0x111>(v, ~0ull));
+  v = min64(v, hdpp64<0x112>(v, ~0ull));
+  v = min64(v, hdpp64<0x114>(v, ~0ull));
+  v = min64(v, hdpp64<0x118>(v, ~0ull));
+  v = min64(v, hdpp64<0x142, 0xa>(v, ~0ull));
+  v = min64(v, hdpp64<0x143, 0xc>(v, ~0ull));
   return v;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  v = min64(v, hdpp64<0xB1>(v, ~0ull));
+  v = min64(v, hdpp64<0x4E>(v, ~0ull));
+  v = min64(v, hdpp64<0x141>(v, ~0ull));
+  v = min64(v, hdpp64<0x140>(v, ~0ull));
+  const auto rl = [](uint64_t x, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  };
+  return min64(min64(rl(v, 0), rl(v, 16)), min64(rl(v, 32), rl(v, 48)));
 }
 
 // Exclusive prefix-min across the 64 lanes of a wave.
 __device__ __forceinline__ uint64_t wave_exscan_min_u64(uint64_t v, int lane) {
-  uint64_t inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    uint64_t w = __shfl_up(inc, o);
-    if (lane >= o) inc = w < inc ? w : inc;
-  }
-  uint64_t ex = __shfl_up(inc, 1);
-  return lane == 0 ? ~0ull : ex;
+  (void)lane;
+  return hdpp64<0x138>(wave_incscan_min_u64(v), ~0ull);  // (wave_shr:1; lane 0: ~0)
 }
 
 // lower_bound over a sorted (ts, uid) range in LDS: number of elements < (kts, kuid).
@@ -282,11 +301,14 @@ struct HoldPackedLds {
 };
 
 __device__ __forceinline__ uint32_t wave_exscan_add_u32(uint32_t v, int lane) {
+  (void)lane;
   uint32_t inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t w = __shfl_up(inc, o);
-    if (lane >= o) inc += w;
-  }
+  inc += (uint32_t)hdpp64<0x111>(inc, 0);
+  inc += (uint32_t)hdpp64<0x112>(inc, 0);
+  inc += (uint32_t)hdpp64<0x114>(inc, 0);
+  inc += (uint32_t)hdpp64<0x118>(inc, 0);
+  inc += (uint32_t)hdpp64<0x142, 0xa>(inc, 0);
+  inc += (uint32_t)hdpp64<0x143, 0xc>(inc, 0);
   return inc - v;
 }
 
@@ -365,12 +387,8 @@ __global__ __launch_bounds__(HOLD_THREADS) void hold_run_packed(const uint32_t *
     }
     if (tid < HOLD_BATCH) L.Rk[tid] = 0;
     // ---- B ----
-    uint64_t inc = child;
-    for (int o = 1; o < 64; o <<= 1) {
-      uint64_t w = __shfl_up(inc, o);
-      if (lane >= o) inc = w < inc ? w : inc;
-    }
-    uint64_t ex = __shfl_up(inc, 1);
+    const uint64_t inc = wave_incscan_min_u64(child);
+    uint64_t ex = hdpp64<0x138>(inc, ~0ull);  // (wave_shr:1)
     if (lane == 0) ex = INF;
     if (lane == 63) L.Wmin[wid] = inc;
     __syncthreads();

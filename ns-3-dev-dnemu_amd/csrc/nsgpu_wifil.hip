@@ -1290,9 +1290,21 @@ __device__ __forceinline__ void wl_sync_rank(const WDev &D, uint32_t uid0, uint3
 // (the rest) — independent, one launch.
 constexpr uint32_t MID_PER = 128, MID_RANK = 64;
 
+template <int CTRL>
+__device__ __forceinline__ uint64_t wdpp64t(uint64_t v) {
+  return ((uint64_t)wdpp32<CTRL>((uint32_t)(v >> 32)) << 32) | wdpp32<CTRL>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t wrl64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+// (every lane active) quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror, then the four rows' sums
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += wdpp64t<0xB1>(v);
+  v += wdpp64t<0x4E>(v);
+  v += wdpp64t<0x141>(v);
+  v += wdpp64t<0x140>(v);
+  return wrl64(v, 0) + wrl64(v, 16) + wrl64(v, 32) + wrl64(v, 48);
 }
 // The epoch's close, on the critical path: k_wl_mid's last block (wl_fin) — the EndReceive uids (the sync
 // order's) into the epoch's end records and its syncs' pending records, the status block (counters, the
@@ -1351,8 +1363,7 @@ __device__ __forceinline__ void wl_fin(const WDev &D, uint8_t *hst, uint32_t seq
   __shared__ uint32_t s_nt;
   const uint32_t tid = threadIdx.x;
   if (tid < 64) {  // the events in the phys' own slots (their striped total), then the stripes' overflow
-    uint32_t c = D.evt[tid * EV_STRIDE];
-    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    const uint32_t c = (uint32_t)wave_sum_u64(D.evt[tid * EV_STRIDE]);  // (wave 0, every lane)
     if (tid == 0) s_nt = c;
   }
   const uint32_t nev = load_stripes(D, sm) + s_nt;  // (load_stripes's barriers order s_nt)
@@ -1411,12 +1422,7 @@ __global__ __launch_bounds__(256) void k_wl_gather(const WDev D) {
   const uint64_t j = (uint64_t)D.j0 + (uint64_t)blockIdx.x * 256 + tid;
   const uint32_t n = j < (uint64_t)(D.j0 + D.nown) ? D.evn[j] : 0u;
   if (n) D.evn[j] = 0;  // (for the epoch two on, which reuses this parity)
-  uint32_t x = n;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-    if (lane >= (uint32_t)d) x += y;
-  }
+  const uint32_t x = wave_incscan32(n);
   if (lane == 63) s_wt[wv] = x;
   __syncthreads();
   uint32_t off = x - n, tot = 0;
