@@ -62,7 +62,10 @@ constexpr int SCAN_THREADS = 1024;
 constexpr int CH = 16;           // events of one node a handler thread sorts in LDS
 constexpr int NSLOT = 7;         // per-node slot table entries
 constexpr int NTAB = NSLOT + 1;  // words per node table record (count + slots)
-constexpr int NWIN = 32;         // windows per graph replay
+#ifndef NWIN_N
+#define NWIN_N 32
+#endif
+constexpr int NWIN = NWIN_N;     // windows per graph replay
 constexpr uint32_t NOCTX = 0xffffffffu;
 constexpr uint32_t LOCALBIT = 0x80000000u;  // child record kind: run inside the window as a local record
 // a Receive whose node another rank owns (partitioned engines; set by the device step from its record, so
@@ -3262,6 +3265,18 @@ static int engine_error(uint32_t err) {
                                  "not replicate)", err);
 }
 
+// The run control into a pinned snapshot after a replay: a copy-engine transfer (hipMemcpyAsync), or with
+// NSGPU_P2P_SNAPK=1 one wave of k_snap on the same queue (no hand-over to the copy engine between replays).
+static hipError_t snapshot(const Ctl *c, Ctl *out, hipStream_t s) {
+  static const bool kern = [] {
+    const char *e = getenv("NSGPU_P2P_SNAPK");
+    return e && e[0] == '1';
+  }();
+  if (!kern) return hipMemcpyAsync(out, c, sizeof(Ctl), hipMemcpyDeviceToHost, s);
+  hipLaunchKernelGGL(k_snap, dim3(1), dim3(64), 0, s, c, out);
+  return hipGetLastError();
+}
+
 // Replays the single engine's window pipeline until the run is over (done >= 2) or the pipeline paused
 // for a host closure (*paused).  Two replays in flight: replay i+1 is queued before the run control
 // after replay i is examined; a pipeline that paused itself (host-driven sort or compaction, a host
@@ -3288,7 +3303,7 @@ static int drive(nsgpu_p2p *h, bool *paused) {
       NSGPU_HIP(hipGraphLaunch(df ? h->gexec_df : h->gexec, h->s));
     }
     df_of[cur] = df;
-    NSGPU_HIP(hipMemcpyAsync(&h->snap[cur], h->M.C, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+    NSGPU_HIP(snapshot(h->M.C, &h->snap[cur], h->s));
     NSGPU_HIP(hipEventRecord(h->ev[cur], h->s));
     if (have_prev) {
       NSGPU_HIP(hipEventSynchronize(h->ev[cur ^ 1]));

@@ -2415,9 +2415,16 @@ __device__ void df_book(const P2PDev &M, Ctl &C, bool ranked, uint32_t W, uint32
 template <int NT>
 __device__ void df_sdef(const P2PDev &M, Ctl &C, uint32_t b, uint32_t nsb);
 constexpr int RKT_DF = 1024;              // the deferred pipeline's k2_rank blocks: SUBS tiles at once
-constexpr int NSDEF = 4;                  // blocks of the deferred accounting (df_sdef: each scans the whole
+#ifndef NSDEF_N
+#define NSDEF_N 4
+#endif
+#ifndef RK_GRID_DF_N
+#define RK_GRID_DF_N 256
+#endif
+constexpr int NSDEF = NSDEF_N;            // blocks of the deferred accounting (df_sdef: each scans the whole
                                           // window, then resolves / logs / digests a quarter of its records)
-constexpr int RK_GRID_DF = 256;             // one 1024-thread block per CU (~150 KB of LDS each): bookkeeping, accounting, tiles
+static_assert(NSDEF == 1 || NSDEF == 2 || NSDEF == 4 || NSDEF == 8, "a thread's NMAX / NT records split evenly");
+constexpr int RK_GRID_DF = RK_GRID_DF_N;    // one 1024-thread block per CU (~150 KB of LDS each): bookkeeping, accounting, tiles
 template <bool DF>
 __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   constexpr int NT = DF ? RKT_DF : RKT, SUBS = NT / RKT;
@@ -3563,6 +3570,14 @@ __global__ void k_host_resume(const P2PDev M, uint64_t hts, uint32_t huid, uint3
 }
 
 __global__ void k_set_uid(const P2PDev M, uint32_t uid) { M.C->uid = uid; }
+// The run control copied into a pinned host snapshot by one wave on the engine's stream (drive's per-replay
+// check without a copy-engine transfer between two graph replays; the event after it publishes the stores)
+static_assert(sizeof(Ctl) % 4 == 0, "Ctl in words");
+__global__ __launch_bounds__(64) void k_snap(const Ctl *__restrict__ c, Ctl *__restrict__ out) {
+  const uint32_t *s = reinterpret_cast<const uint32_t *>(c);
+  uint32_t *d = reinterpret_cast<uint32_t *>(out);
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(Ctl) / 4); i += 64) d[i] = s[i];
+}
 
 // A host application's UdpSocket::Send of one datagram of application `a`'s flow, made by the host
 // closure running now (uid `cur`): the same steps as OnOffApplication::SendPacket's send
