@@ -56,7 +56,8 @@ constexpr int NRB = NRT * NJT;   // rank tile blocks (k2_handle)
 constexpr int GRID_POOL = GRID_POOL_N;   // blocks of the pool sweep (grid-stride; r06: 1,024 measured slower on
                                          // config 4 and on the dumbbell's 5 M-entry pool: per-block reductions)
 #ifndef PA_SLOT_LANES
-#define PA_SLOT_LANES 256        // k2_pa (single engine): last-window records per slot block (diagnostic override)
+#define PA_SLOT_LANES 128        // k2_pa (single engine): last-window records per slot block (r06: 128 against 256,
+                                 // config 4 +0.7 %, k2_pa ~10.3 -> ~9.8 us; profiles/r06/ab/p2p_tail_replays_slot_lanes.log)
 #endif
 constexpr int SCAN_THREADS = 1024;
 constexpr int CH = 16;           // events of one node a handler thread sorts in LDS
@@ -65,7 +66,11 @@ constexpr int NTAB = NSLOT + 1;  // words per node table record (count + slots)
 #ifndef NWIN_N
 #define NWIN_N 32
 #endif
+#ifndef NWIN_TAIL_N
+#define NWIN_TAIL_N 2  // (2 / 4 / 8 / none: 160.4 / 159.9 / 160.3 / 159.5 M ev/s on config 4, interleaved)
+#endif
 constexpr int NWIN = NWIN_N;     // windows per graph replay
+constexpr int NWIN_TAIL = NWIN_TAIL_N;  // ... near the end of a run (drive)
 constexpr uint32_t NOCTX = 0xffffffffu;
 constexpr uint32_t LOCALBIT = 0x80000000u;  // child record kind: run inside the window as a local record
 // a Receive whose node another rank owns (partitioned engines; set by the device step from its record, so
@@ -2162,6 +2167,7 @@ struct nsgpu_p2p {
   hipStream_t s = nullptr;  // engine stream (graph capture and replay)
   hipGraphExec_t gexec = nullptr;
   hipGraphExec_t gexec_df = nullptr;  // the deferred pipeline's replay (single wide engine, untraced)
+  hipGraphExec_t gtail[2] = {nullptr, nullptr};  // NWIN_TAIL-window replays (plain, deferred): a run's last windows
   hipEvent_t ev[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr;
   uint32_t *done_host = nullptr;  // pinned, 2 slots
   Ctl *snap = nullptr;            // pinned, 2 run-control snapshots (single engine)
@@ -2220,6 +2226,8 @@ extern "C" int nsgpu_p2p_destroy(nsgpu_p2p *h) {
   if (h->s) (void)hipStreamSynchronize(h->s);
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   if (h->gexec_df) (void)hipGraphExecDestroy(h->gexec_df);
+  for (hipGraphExec_t g : h->gtail)
+    if (g) (void)hipGraphExecDestroy(g);
   for (hipEvent_t e : {h->ev[0], h->ev[1], h->t0, h->t1})
     if (e) (void)hipEventDestroy(e);
   if (h->done_host) (void)hipHostFree(h->done_host);
@@ -3010,13 +3018,13 @@ int launch_windows_dbg(nsgpu_p2p *h, hipStream_t s, bool df) {
   }
   return NSGPU_OK;
 }
-int launch_windows(nsgpu_p2p *h, hipStream_t s, bool df) {
+int launch_windows(nsgpu_p2p *h, hipStream_t s, bool df, int nwin = NWIN) {
   static const int dbg = [] {
     const char *e = getenv("NSGPU_P2P_DEBUG");
     return e ? atoi(e) : 0;
   }();
   if ((dbg == 1 && h->eager) || (dbg == 2 && !h->eager)) return launch_windows_dbg(h, s, df);
-  for (int w = 0; w < NWIN; w++)
+  for (int w = 0; w < nwin; w++)
     for (int k = 0; k < NKERN; k++) launch_kernel(h, k, s, df);
   return NSGPU_OK;
 }
@@ -3229,16 +3237,16 @@ static int host_step_dist(const Ctl &c, hipStream_t s, G gather, nsgpu_p2p *h) {
   return NSGPU_OK;
 }
 
-static int build_graph(nsgpu_p2p *h, bool df = false) {
-  // NWIN windows of the pipeline; kernels read every run-dependent value from the device (Ctl), so
-  // one instantiated graph serves every run of this engine
-  hipGraphExec_t &gx = df ? h->gexec_df : h->gexec;
+static int build_graph(nsgpu_p2p *h, bool df = false, bool tail = false) {
+  // NWIN windows of the pipeline (tail: NWIN_TAIL, single engine); kernels read every run-dependent value from the
+  // device (Ctl), so one instantiated graph serves every run of this engine
+  hipGraphExec_t &gx = tail ? h->gtail[df ? 1 : 0] : df ? h->gexec_df : h->gexec;
   hipGraph_t g = nullptr;
   if (const int rd = dbg_alloc()) return rd;
   NSGPU_HIP(hipStreamBeginCapture(h->s, h->M.dist ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal));
   int rc = NSGPU_OK;
   if (h->M.dist) rc = launch_windows_dist(h, h->s);
-  else launch_windows(h, h->s, df);
+  else launch_windows(h, h->s, df, tail ? NWIN_TAIL : NWIN);
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (rc != NSGPU_OK || e != hipSuccess) {
     if (g) (void)hipGraphDestroy(g);
@@ -3294,14 +3302,30 @@ static int drive(nsgpu_p2p *h, bool *paused) {
     const int rc = build_graph(h, true);
     if (rc) return rc;
   }
+  // The run's last windows in replays of NWIN_TAIL: a replay queued behind the final window is a no-op that still
+  // launches its kernels (~1.5 x NWIN of them trail the run).  The tail starts once the examined snapshots' pace
+  // (simulated ns a window) puts Simulator::Stop within the windows already queued plus one replay.  Speed only:
+  // the windows are the same whatever a replay holds.
+  const uint64_t stop_ts = h->C0.red[1].stopts;
+  bool tail = false;
+  uint64_t w_last = 0, t_last = 0;
+  int queued = 0;  // windows of the replay in flight behind the examined one
   for (;;) {
+    const int nw = tail ? NWIN_TAIL : NWIN;
     if (h->eager) {
-      const int rc = launch_windows(h, h->s, df);
+      const int rc = launch_windows(h, h->s, df, nw);
       if (rc) return rc;
       NSGPU_HIP(hipGetLastError());
     } else {
-      NSGPU_HIP(hipGraphLaunch(df ? h->gexec_df : h->gexec, h->s));
+      hipGraphExec_t gx = tail ? h->gtail[df ? 1 : 0] : df ? h->gexec_df : h->gexec;
+      if (tail && !gx) {
+        const int rc = build_graph(h, df, true);
+        if (rc) return rc;
+        gx = h->gtail[df ? 1 : 0];
+      }
+      NSGPU_HIP(hipGraphLaunch(gx, h->s));
     }
+    queued = nw;
     df_of[cur] = df;
     NSGPU_HIP(snapshot(h->M.C, &h->snap[cur], h->s));
     NSGPU_HIP(hipEventRecord(h->ev[cur], h->s));
@@ -3309,6 +3333,13 @@ static int drive(nsgpu_p2p *h, bool *paused) {
       NSGPU_HIP(hipEventSynchronize(h->ev[cur ^ 1]));
       const Ctl &c = h->snap[cur ^ 1];
       if (c.done >= 2) break;  // 2: the final window is appended
+      if (!tail && stop_ts != ~0ull && c.mode == MODE_NORMAL && c.windows > w_last && c.tmin > t_last &&
+          c.tmin != ~0ull && t_last != 0) {
+        const double pace = (double)(c.tmin - t_last) / (double)(c.windows - w_last);
+        const double left = stop_ts > c.tmin ? (double)(stop_ts - c.tmin) / pace : 0.0;
+        if (left < (double)(queued + NWIN)) tail = true;
+      }
+      if (c.mode == MODE_NORMAL && c.tmin != ~0ull) w_last = c.windows, t_last = c.tmin;
       if (c.mode >= MODE_SORT) {
         NSGPU_HIP(hipEventSynchronize(h->ev[cur]));
         if (df_of[cur ^ 1]) {  // (the pause came from the deferred pipeline: its last window is not accounted yet)
@@ -3592,6 +3623,11 @@ extern "C" int nsgpu_p2p_set_trace(nsgpu_p2p *h, uint64_t cap) {
     (void)hipGraphExecDestroy(h->gexec_df);
     h->gexec_df = nullptr;
   }
+  for (hipGraphExec_t &g : h->gtail)
+    if (g) {
+      (void)hipGraphExecDestroy(g);
+      g = nullptr;
+    }
   return NSGPU_OK;
 }
 
@@ -3600,7 +3636,7 @@ extern "C" int nsgpu_p2p_set_trace_kinds(nsgpu_p2p *h, uint32_t mask) {
   if (!h) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_trace_kinds: null");
   if (mask & ~0x7fu) return set_error(NSGPU_EINVAL, "nsgpu_p2p_set_trace_kinds: unknown kind bits 0x%x", mask);
   h->M.trace_kinds = mask;
-  for (hipGraphExec_t *g : {&h->gexec, &h->gexec_df})
+  for (hipGraphExec_t *g : {&h->gexec, &h->gexec_df, &h->gtail[0], &h->gtail[1]})
     if (*g) {
       (void)hipGraphExecDestroy(*g);
       *g = nullptr;
