@@ -51,7 +51,7 @@ constexpr int RTR = 1;           // window keys (rows) per thread of a rank tile
 constexpr int NRT = WCAP / (HB * RTR);  // rank tile rows
 constexpr int NRB = NRT * NJT;   // rank tile blocks (k2_handle)
 #ifndef GRID_POOL_N
-#define GRID_POOL_N 256
+#define GRID_POOL_N 128  // (r06, with 128-record slot blocks: 128 against 256 blocks, config 4 +1.4 %: ab/p2p_knobs2.log)
 #endif
 constexpr int GRID_POOL = GRID_POOL_N;   // blocks of the pool sweep (grid-stride; r06: 1,024 measured slower on
                                          // config 4 and on the dumbbell's 5 M-entry pool: per-block reductions)

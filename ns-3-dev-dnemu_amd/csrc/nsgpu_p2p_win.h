@@ -2466,6 +2466,9 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   const bool ranked = (go & 1u) != 0;
   __shared__ uint32_t pre[NLR + 1];
   __shared__ ulonglong2 cws[SUBS][RKC];
+  // the columns' rel ts alone (the gen-0-row and local-row x gen-0 tiles compare nothing else): 4 B a column, read
+  // 4 at a time — the tiles are bound by their per-column LDS reads and 64-bit compares
+  __shared__ __align__(16) uint32_t cwhs[SUBS][RKC];
   local_prefix<NT>((ranked && lim) ? lc : 0u, pre);
   const uint32_t Lt = pre[NLR], N = W + Lt;
   uint32_t *const wr = wrank_of(M, wn), *const lr = lrank_of(M, wn);
@@ -2497,6 +2500,7 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
   // SUBS tiles a block at once: sub-tile `sub` is RKT threads (whole waves) with its own column buffer
   const uint32_t sub = threadIdx.x / RKT, lt = threadIdx.x % RKT;
   ulonglong2 *const cw = cws[sub];
+  uint32_t *const cwh = cwhs[sub];
   // a block's sub-tiles are spread over the tile space (sub-tile `sub` of block b0 takes tile base + sub x nb +
   // b0), so each block gets a mix of the costly tiles (rows with local records) and the cheap ones
   for (uint32_t t0 = 0; t0 < ntile; t0 += nb * SUBS) {  // (uniform over the block)
@@ -2526,6 +2530,7 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
           }
         }
         cw[lt] = w;
+        cwh[lt] = (uint32_t)(w.x >> 32);  // (padding 0xffffffff: never below a row's rel ts)
       }
       if (ix < N) {
         rx = dense_rec(ix, W, pre);
@@ -2544,15 +2549,20 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
       ix = ti * RKT + lt;
       if (lt < (uint32_t)RKC) {
         const uint32_t cy = tj * RKC + lt;
-        cw[lt].x = cy < W ? M.wkey[cy] >> 32 : ~0ull;
+        cwh[lt] = cy < W ? (uint32_t)(M.wkey[cy] >> 32) : 0xffffffffu;  // (padding: counted out below)
       }
       if (ix < Lt) relx = M.wkey[dense_rec(W + ix, W, pre)] >> 32;
     }
     __syncthreads();
     TILE_MARK(50, c_win);
-    if (tA && g0rows) {  // a local column precedes a gen-0 row iff its rel ts is smaller: one compare
-#pragma unroll 16
-      for (uint32_t y = 0; y < (uint32_t)RKC; y++) c += cw[y].x < wx;
+    const uint4 *const cwh4 = reinterpret_cast<const uint4 *>(cwh);
+    if (tA && g0rows) {  // a local column precedes a gen-0 row iff its rel ts is smaller: one 32-bit compare
+      const uint32_t tx = (uint32_t)(wx >> 32);
+#pragma unroll 4
+      for (int y4 = 0; y4 < RKC / 4; y4++) {
+        const uint4 q = cwh4[y4];
+        c += (uint32_t)(q.x < tx) + (uint32_t)(q.y < tx) + (uint32_t)(q.z < tx) + (uint32_t)(q.w < tx);
+      }
       slot = rx;
     } else if (tA) {
       bool tie = false;
@@ -2580,8 +2590,14 @@ __global__ __launch_bounds__(DF ? RKT_DF : RKT) void k2_rank(const P2PDev M) {
       if (ix >= N) c = 0;
       slot = ix >= W ? ix - W + LBASE : rx;
     } else if (tB) {
-#pragma unroll 16
-      for (uint32_t y = 0; y < (uint32_t)RKC; y++) c += cw[y].x <= relx;
+      const uint32_t rx32 = (uint32_t)relx;  // (a rel ts: below 2^32)
+#pragma unroll 4
+      for (int y4 = 0; y4 < RKC / 4; y4++) {
+        const uint4 q = cwh4[y4];
+        c += (uint32_t)(q.x <= rx32) + (uint32_t)(q.y <= rx32) + (uint32_t)(q.z <= rx32) + (uint32_t)(q.w <= rx32);
+      }
+      const uint32_t nv = W - tj * RKC;  // (the last column tile's padding columns: 0xffffffff <= the row's rel ts
+      if (nv < (uint32_t)RKC && rx32 == 0xffffffffu) c -= (uint32_t)RKC - nv;  //  only at that rel ts)
       if (ix >= Lt) c = 0;
       slot = ix + LBASE;
     }
