@@ -53,6 +53,10 @@ constexpr int NRB = NRT * NJT;   // rank tile blocks (k2_handle)
 #ifndef GRID_POOL_N
 #define GRID_POOL_N 128  // (r06, with 128-record slot blocks: 128 against 256 blocks, config 4 +1.4 %: ab/p2p_knobs2.log)
 #endif
+#ifndef GRID_POOL_BIG_N
+#define GRID_POOL_BIG_N 256  // (config 5's 5 M-entry pool on one engine: 256 / 128 / 96 / 64 blocks 120.6 / 114.6 / 110.9 / 101.3 M
+#endif                       //  ev/s, ab/p2p_pool_blocks.log; config 4 flat from 64 to 128)
+constexpr int GRID_POOL_BIG = GRID_POOL_BIG_N;  // ... the single engine's, when the pool capacity is above 2^20 entries
 constexpr int GRID_POOL = GRID_POOL_N;   // blocks of the pool sweep (grid-stride; r06: 1,024 measured slower on
                                          // config 4 and on the dumbbell's 5 M-entry pool: per-block reductions)
 #ifndef PA_SLOT_LANES
@@ -2894,9 +2898,9 @@ bool launch_kernel(nsgpu_p2p *h, int k, hipStream_t s, bool df, hipEvent_t ev0 =
   const bool wide = h->M.wide != 0;
   switch (k) {
     case 0:
-      if (df) NSGPU_KLAUNCH((k2_pa<false, true, true>), dim3(pa_grid<true>()), dim3(TB), s, ev0, ev1, h->M);
-      else if (wide) NSGPU_KLAUNCH((k2_pa<false, true>), dim3(pa_grid<true>()), dim3(TB), s, ev0, ev1, h->M);
-      else NSGPU_KLAUNCH((k2_pa<false, false>), dim3(pa_grid<false>()), dim3(TB), s, ev0, ev1, h->M);
+      if (df) NSGPU_KLAUNCH((k2_pa<false, true, true>), dim3(pa_grid_rt<true>(h->M)), dim3(TB), s, ev0, ev1, h->M);
+      else if (wide) NSGPU_KLAUNCH((k2_pa<false, true>), dim3(pa_grid_rt<true>(h->M)), dim3(TB), s, ev0, ev1, h->M);
+      else NSGPU_KLAUNCH((k2_pa<false, false>), dim3(pa_grid_rt<false>(h->M)), dim3(TB), s, ev0, ev1, h->M);
       return true;
     case 1:
       if (wide) NSGPU_KLAUNCH(k2_handle<true>, dim3(K2_GRID), dim3(HB), s, ev0, ev1, h->M);

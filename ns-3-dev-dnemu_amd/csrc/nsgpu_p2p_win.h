@@ -450,6 +450,11 @@ constexpr int pa_grid() {
   constexpr int nsg = WIDE ? SLOTG : WCAP;
   return nsg / PA_SLOT_LANES + GRID_POOL - nsg / TB;
 }
+// ... at run time: a large pool (the default capacity is 2^20 entries; config 5's holds millions) sweeps with more blocks
+template <bool WIDE>
+inline int pa_grid_rt(const P2PDev &M) {
+  return pa_grid<WIDE>() + (M.pool_cap > (1ull << 20) ? GRID_POOL_BIG - GRID_POOL : 0);
+}
 // DF: the deferred pipeline's variant (single wide engine): when the last window is staged (C.pdf) its records
 // are written in rank order to the stage for k2_sdef and its children get provisional uids (no dispatch log
 // here); the pool's provisional uids of the window before it are resolved as the pool is read.
