@@ -28,7 +28,10 @@ enum : uint32_t { MODE_NORMAL = 0, MODE_RUN = 1, MODE_SORT = 2, MODE_COMPACT = 3
 constexpr uint64_t TOMB = ~0ull;        // ev_ts of a free pool slot
 constexpr uint32_t NOSRC = 0xffffffffu;
 constexpr int NHUB = 32;                // hub blocks of k2_handle
-constexpr int NMB = 128;                // maintenance blocks of k2_handle
+#ifndef NMB_N
+#define NMB_N 128
+#endif
+constexpr int NMB = NMB_N;              // maintenance blocks of k2_handle
 constexpr int MAXHUB = WCAP / (CH + 1) + 1;
 constexpr int K2_GRID_W = NHB + NHUB + NMB;  // holders, hub blocks, pool maintenance
 constexpr int K2_GRID = K2_GRID_W + NRB;       // + rank tiles (single engine; partitioned: k_gtile ranks)
