@@ -57,7 +57,11 @@ constexpr int NRB = NRT * NJT;   // rank tile blocks (k2_handle)
 #define GRID_POOL_BIG_N 256  // (config 5's 5 M-entry pool on one engine: 256 / 128 / 96 / 64 blocks 120.6 / 114.6 / 110.9 / 101.3 M
 #endif                       //  ev/s, ab/p2p_pool_blocks.log; config 4 flat from 64 to 128)
 constexpr int GRID_POOL_BIG = GRID_POOL_BIG_N;  // ... the single engine's, when the pool capacity is above 2^20 entries
-constexpr int GRID_POOL = GRID_POOL_N;   // blocks of the pool sweep (grid-stride; r06: 1,024 measured slower on
+constexpr int GRID_POOL = GRID_POOL_N;
+#ifndef GRID_POOL_DIST_N
+#define GRID_POOL_DIST_N GRID_POOL_N
+#endif
+constexpr int GRID_POOL_DIST = GRID_POOL_DIST_N;  // k2_pa<DIST>'s whole grid (slot, remote, chunk and pool blocks)   // blocks of the pool sweep (grid-stride; r06: 1,024 measured slower on
                                          // config 4 and on the dumbbell's 5 M-entry pool: per-block reductions)
 #ifndef PA_SLOT_LANES
 #define PA_SLOT_LANES 128        // k2_pa (single engine): last-window records per slot block (r06: 128 against 256,
@@ -2281,9 +2285,9 @@ static int plan_engine(const nsgpu_p2p_scenario *sc, const uint32_t *owner, int 
   }
   if (owner) {
     if (nranks < 1 || nranks > MAXR || rank < 0 || rank >= nranks ||
-        (uint64_t)nranks * CAPX_MAX + TB + 2 * WCAP >= (uint64_t)GRID_POOL * TB)  // (k2_pa: slot, remote, chunk blocks)
+        (uint64_t)nranks * CAPX_MAX + TB + 2 * WCAP >= (uint64_t)GRID_POOL_DIST * TB)  // (k2_pa: slot, remote, chunk blocks)
       return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: rank %d of %d (at most %d ranks)", rank, nranks,
-                       (int)(((uint64_t)GRID_POOL * TB - TB - 2 * WCAP - 1) / CAPX_MAX));
+                       (int)(((uint64_t)GRID_POOL_DIST * TB - TB - 2 * WCAP - 1) / CAPX_MAX));
     for (uint32_t n = 0; n < N; n++)
       if (owner[n] >= (uint32_t)nranks) return set_error(NSGPU_EINVAL, "nsgpu_p2p_create_dist: node %u: owner %u", n, owner[n]);
   }
@@ -3139,8 +3143,8 @@ static int x_alltoall(nsgpu_p2p *h, const void *send, void *recv, size_t bytes, 
 
 // The partitioned window's kernels (narrow, or wide: local records ranked across the ranks through X1Loc).
 static void dist_pa(const P2PDev &M, hipStream_t s) {
-  if (M.wide) hipLaunchKernelGGL((k2_pa<true, true>), dim3(GRID_POOL), dim3(TB), 0, s, M);
-  else hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL), dim3(TB), 0, s, M);
+  if (M.wide) hipLaunchKernelGGL((k2_pa<true, true>), dim3(GRID_POOL_DIST), dim3(TB), 0, s, M);
+  else hipLaunchKernelGGL((k2_pa<true, false>), dim3(GRID_POOL_DIST), dim3(TB), 0, s, M);
 }
 static void dist_handle(const P2PDev &M, hipStream_t s) {
   if (M.wide) {
